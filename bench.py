@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X two-tower training step (BASELINE.json metric).
+
+Workload (BASELINE cfg 2, the configuration the metric is quoted on): SASRec user tower
+(L=50, D=128, 4 heads, 2 layers, V=10,136 item vocabulary) + late-fusion item head on
+precomputed 512-d modality embeddings + symmetric in-batch InfoNCE, B=512 pairs per GPU,
+bf16 operands / fp32 accumulation, dropout 0.1 on (reference defaults), AdamW lr 1e-4.
+One step = forward + backward + AdamW over one synthetic batch already resident in HBM.
+
+Multi-GPU: one process per GPU (torchrun), per-GPU batch fixed (weak scaling), gradients
+averaged with RCCL all-reduce; value = pairs of all ranks / max-over-ranks time.
+
+Extra fields: "roofline" for the dominant kernel (timed live with HIP events on the launch
+stream) and "cpu_baseline" (the fp32 CPU oracle timed on this host, rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import importlib
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+pkg = importlib.import_module("music-recommendation-multimodal_amd")
+
+V, L, D, H = 10136, 50, 128, 4
+N_GENDERS, N_COUNTRIES, N_USERS = 3, 64, 840
+PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def synthetic_batches(n: int, B: int, seed: int, device):
+    """SURVEY §8(d) synthetic inputs, generated on the host then moved to HBM once."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        lengths = torch.randint(1, L + 1, (B,), generator=g)
+        mask = (torch.arange(L)[None] < lengths[:, None]).long()
+        ids = torch.randint(1, V, (B, L), generator=g) * mask
+        out.append({
+            "history_ids": ids.to(device), "history_mask": mask.to(device),
+            "user_gender": torch.randint(0, N_GENDERS, (B,), generator=g).to(device),
+            "user_country": torch.randint(0, N_COUNTRIES, (B,), generator=g).to(device),
+            "user_idx": torch.randint(0, N_USERS, (B,), generator=g).to(device),
+            "target_modal": torch.randn(B, 512, generator=g).to(device),
+        })
+    return out
+
+
+def step_flops(B: int) -> float:
+    """Algorithmic FLOPs of one train step (fwd + bwd ≈ 3x fwd GEMM/attention FLOPs)."""
+    M = B * L
+    layer = 2 * M * D * (3 * D + D + 4 * D + 4 * D) + 2 * 2 * B * H * L * L * (D // H)
+    user_head = 2 * B * (D + 48) * D + 2 * B * D * D
+    item_head = 2 * B * 512 * 512 + 2 * B * 512 * D
+    loss = 2 * B * B * D
+    return 3.0 * (2 * layer + user_head + item_head + loss)
+
+
+def probe_dominant(B: int, device, iters: int = 50):
+    """Time the dominant kernel (the FFN linear1 forward GEMM+bias+ReLU+dropout epilogue,
+    [B*L, 128] x [512, 128]^T) on the launch stream with HIP events."""
+    ops = pkg.ops
+    M, K, N = B * L, D, 4 * D
+    g = torch.Generator(device=device).manual_seed(0)
+    a = torch.randn(M, K, device=device, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, device=device, generator=g).to(torch.bfloat16)
+    bias = torch.randn(N, device=device, generator=g)
+    out = torch.empty(M, N, device=device, dtype=torch.bfloat16)
+    seed = torch.tensor([12345], dtype=torch.int64, device=device)
+    for _ in range(5):
+        ops.linear(a, w, bias, out, act=1, drop=(0.1, seed))
+    st = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        ops.linear(a, w, bias, out, act=1, drop=(0.1, seed))
+    e1.record(st)
+    torch.cuda.synchronize(device)
+    sec = e0.elapsed_time(e1) / 1e3 / iters
+    flops = 2.0 * M * N * K
+    tf = flops / sec / 1e12
+    return {"kernel": "gemm_kernel<bf16,128,128> (FFN linear1 fwd)", "bound": "mfma",
+            "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": read_traffic("gemm_kernel"),
+            "avg_us": round(sec * 1e6, 2), "flops_per_launch": flops}
+
+
+def read_traffic(name: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if present."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
+    if not files:
+        return None
+    try:
+        data = json.load(open(files[-1]))
+        return data.get(name, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(B: int, budget_s: float = 20.0):
+    """fp32 CPU oracle (oracle/two_tower_ref.py) train step on this host's cores."""
+    from oracle import two_tower_ref as ref
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(0)
+    params = ref.init_params(V, generator=g)
+    batch = ref.synthetic_batch(B, L, V, generator=g)
+    running = ref.init_running()
+    state = {}
+    drop = ref.TorchDropout()
+    ref.train_step(params, state, batch, p_drop=0.1, drop=drop, running=running)   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ref.train_step(params, state, batch, p_drop=0.1, drop=drop, running=running)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 30:
+            break
+    return {"value": round(n * B / el, 2), "unit": "user-item pairs/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} full cfg-2 steps (B={B}, L={L}, D={D}, V={V}, dropout 0.1) of the "
+                      f"fp32 torch-CPU oracle after 1 warm-up, {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    B = args.batch
+
+    torch.manual_seed(1234 + rank)
+    model = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=N_GENDERS,
+                              num_countries=N_COUNTRIES, max_seq_len=L, user_embedding_dim=D,
+                              item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
+                              compute_dtype=torch.bfloat16).to(device)
+    if world > 1:   # identical replicas, as DDP broadcasts from rank 0
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, 0)
+    step = pkg.TrainStep(model, lr=1e-4, use_graph=not args.no_graph, seed=rank + 1)
+    batches = synthetic_batches(4, B, seed=rank, device=device)
+
+    for i in range(args.warmup):
+        step.step(batches[i % len(batches)])
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    loss_sum = torch.zeros((), device=device)
+    for i in range(args.steps):
+        loss_sum += step.step(batches[i % len(batches)])
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    mean_loss = float(loss_sum) / max(args.steps, 1)
+
+    roof = probe_dominant(B, device) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        cpu = cpu_baseline(B, args.cpu_budget)
+
+    if rank == 0:
+        pairs = world * B * args.steps
+        value = pairs / el
+        ms = el / max(args.steps, 1) * 1e3
+        step_tf = step_flops(B) * args.steps / el / 1e12 * world
+        line = {
+            "metric": "user-item pairs/sec (train step) at batch=512 d=128; 1/2/4/8 MI355X scaling",
+            "value": round(value, 1), "unit": "user-item pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic (SURVEY §8d distributions), random-init weights",
+            "config": {"workload": "cfg2: SASRec L=50 D=128 H=4 x2 layers + late-fusion head on "
+                                   "precomputed 512-d modality embeddings + in-batch InfoNCE; "
+                                   "fwd+bwd+AdamW, dropout 0.1",
+                       "global_batch": world * B, "per_gpu_batch": B, "seq_len": L,
+                       "vocab": V, "parallelism": f"dp{world}",
+                       "graph": not args.no_graph},
+            "roofline": roof,
+            "step_mfma": {"achieved": round(step_tf, 3), "peak": PEAK_BF16_TFLOPS,
+                          "unit": "TFLOP/s", "frac": round(step_tf / PEAK_BF16_TFLOPS, 5),
+                          "flops_per_step_per_gpu": step_flops(B)},
+            "cpu_baseline": cpu,
+            "mean_loss": round(mean_loss, 5),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,210 @@
+/* ttmi.h — C ABI of libttmi.so, the MI355X (gfx950) two-tower training-step kernels.
+ *
+ * Drop-in boundary: the reference exposes no operator registry; its hot
+ * path is the PyTorch nn.Module API of src/models driven by src/train.py.  Each entry
+ * point below replaces the implicit PyTorch/cuBLAS/cuDNN work behind one reference call
+ * site, cited as reference-file:line.  The Python host (music-recommendation-multimodal_amd)
+ * binds these through ctypes and rebuilds the reference's constructors, forward(batch)
+ * contract and state_dict names on top (see INTEGRATION.md for the binding).
+ *
+ * Conventions
+ *  - Plain device pointers and sizes; all tensors row-major and contiguous unless an
+ *    explicit leading dimension (ld*) is given.  No allocation, no hidden mutable
+ *    state; every call is asynchronous on `stream` and safe to capture in a hipGraph.
+ *  - dtype arguments: TTMI_F32 or TTMI_BF16 (bf16 = uint16 bit pattern).  Reductions,
+ *    normalisation statistics, softmax/LSE and the loss are always fp32.
+ *  - Dropout: (p, seed) where `seed` points to a uint64 in DEVICE memory (read at kernel
+ *    entry, so a captured graph replays with whatever seed the step wrote there; may be
+ *    NULL when p == 0).  keep(i) = lowbias32(lowbias32(i + lo32(seed)) ^ hi32(seed))
+ *    >= p*2^32 over the flat element index i stated per call; kept values are scaled by
+ *    1/(1-p).  p = 0 is the identity (reference parity runs).
+ *  - Return 0 (TTMI_OK) on success; otherwise an error code, with a message available
+ *    from ttmi_last_error() (thread-local).  Invalid shapes are rejected before launch.
+ */
+#ifndef TTMI_H
+#define TTMI_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { TTMI_OK = 0, TTMI_ERR_ARG = 1, TTMI_ERR_LAUNCH = 2 };
+enum { TTMI_F32 = 0, TTMI_BF16 = 1 };
+
+/* Error message of the last failing call on this thread ("" if none). */
+const char* ttmi_last_error(void);
+/* ABI version (bumped on any signature change). */
+int ttmi_abi_version(void);
+
+/* ------------------------------------------------------------------------------------
+ * GEMM with fused epilogue — every nn.Linear on the path, forward and backward:
+ *   user_tower.py:37-45 (MHA in_proj/out_proj, linear1/linear2 of TransformerEncoderLayer),
+ *   user_tower.py:51-57 (user fusion MLP), item_tower.py:122-129 (item fusion head),
+ *   two_tower.py:106 (logits = û·îᵀ/τ) and the InfoNCE gradient products.
+ *
+ *   C[m,n] (=|+=) epi( alpha * Σ_k A(m,k)·B(n,k) )
+ *   A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m];  B(n,k) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n]
+ *   epi: v += bias[n]; v = act(v) (0 none, 1 relu); v = dropout(v, idx = m*ld_drop+n);
+ *        v = gate ? (gate[m*ld_gate+n] > 0 ? v*gate_scale : 0) : v;  colsum[n] += v;
+ *        v += residual[m*ld_res+n];  C = v (c_mode 0) or C += v atomically (c_mode 1, f32 C).
+ *   Operands A and B share `dtype`; C has `c_dtype`.  split_k > 1 partitions K over
+ *   workgroups and requires c_mode 1 and act 0 (bias/residual are added by split 0 only).
+ *   Alignment: rows of a k-major operand need K % 8 == 0 (bf16) / K % 4 == 0 (f32);
+ *   a non-k-major operand needs M (or N) % 8 == 0 (bf16) / % 4 == 0 (f32).
+ * ---------------------------------------------------------------------------------- */
+typedef struct {
+  int dtype;
+  int64_t M, N, K;
+  const void* A; int64_t lda; int a_kmajor;
+  const void* B; int64_t ldb; int b_kmajor;
+  void* C; int64_t ldc; int c_dtype; int c_mode;
+  float alpha;
+  const float* bias;
+  int act;
+  float drop_p; const uint64_t* drop_seed; int64_t ld_drop;
+  const void* gate; int gate_dtype; int64_t ld_gate; float gate_scale;
+  const float* residual; int64_t ld_res;
+  float* colsum;
+  int split_k;
+} ttmi_gemm_desc;
+int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0) — TransformerEncoderLayer
+ * norm1/norm2 (user_tower.py:37-45), user fusion LN (user_tower.py:54), item head final
+ * LN (item_tower.py:128).  Optional ReLU and dropout (idx = row*D + col) after the affine.
+ * Writes y (y_dtype, ldy) and per-row mean/rstd (fp32) for the backward.
+ * ---------------------------------------------------------------------------------- */
+int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const float* w,
+                       const float* b, float eps, int relu, float drop_p, const uint64_t* drop_seed,
+                       void* y, int y_dtype, int64_t ldy, float* mean, float* rstd,
+                       hipStream_t stream);
+/* Backward of the above.  dy (fp32) is the gradient w.r.t. y; if gate != NULL it is first
+ * multiplied by (gate > 0 ? gate_scale : 0) (gate = the stored y when ReLU/dropout followed
+ * the affine).  dx = res + LN'(dy) (res may alias dx or be NULL); dw/db are accumulated
+ * (atomic, fp32). */
+int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
+                       int64_t ldx, const float* mean, const float* rstd, const float* w,
+                       const void* gate, int gate_dtype, int64_t ldg, float gate_scale,
+                       const float* res, float* dx, int64_t lddx, float* dw, float* db,
+                       hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * SASRec input block (user_tower.py:83-93):
+ *   x[b,l,:] = dropout(LN(E[ids[b,l]] + P[l]))   (dropout idx = (b*L+l)*D + c)
+ * E [V,D], P [>=L,D] fp32 master tables; x [B*L,D] fp32 residual stream.
+ * ---------------------------------------------------------------------------------- */
+int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, int64_t V,
+                       const float* P, const float* w, const float* b, float eps,
+                       float drop_p, const uint64_t* drop_seed, float* x, float* mean, float* rstd,
+                       hipStream_t stream);
+/* Backward: dE[ids] += g (rows with ids == padding_idx skipped, nn.Embedding(padding_idx=0)
+ * user_tower.py:27), dP[l] += Σ_b g, dw/db += LN affine grads.  All accumulate (fp32). */
+int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const float* E,
+                       const float* P, const float* w, const float* mean, const float* rstd,
+                       float drop_p, const uint64_t* drop_seed, const float* dx, float* dE, float* dP,
+                       float* dw, float* db, int64_t padding_idx, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Multi-head self-attention core (SDPA inside nn.MultiheadAttention, user_tower.py:111-116):
+ *   per (b,h): S = Q·Kᵀ/√Dh, causal (key j <= query i) + key padding (key_valid[b,j] != 0;
+ *   pass history_mask, or history_ids when the mask is None), softmax, dropout on the
+ *   probabilities (idx = ((b*H+h)*L+i)*L+j), O = P·V.  Query rows with no valid key give 0.
+ * qkv [B*L, 3*H*Dh] (q|k|v, dtype), ctx [B*L, H*Dh] (dtype), lse [B*H*L] fp32 (+inf for
+ * fully masked rows).  L <= 64, Dh <= 64, Dh % 8 == 0.
+ * ---------------------------------------------------------------------------------- */
+int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                 const int64_t* key_valid, float drop_p, const uint64_t* drop_seed, void* ctx,
+                 float* lse, hipStream_t stream);
+int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                 const int64_t* key_valid, const float* lse, const void* dctx, float drop_p,
+                 const uint64_t* drop_seed, void* dqkv, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Last-valid gather + demographics concat (user_tower.py:118-139):
+ *   len_b = Σ_l (len_src[b,l] != 0) - 1 clamped >= 0; rows[b] = b*L + len_b;
+ *   comb[b] = [x[rows[b]], G[gender[b]], C[country[b]]]   ([B, D+dg+dc], dtype)
+ * ---------------------------------------------------------------------------------- */
+int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
+                         const int64_t* len_src, const int64_t* gender, const float* G, int dg,
+                         const int64_t* country, const float* C, int dc, void* comb,
+                         int32_t* rows, hipStream_t stream);
+/* Backward: dx[rows[b]] += dcomb[b,:D]; dG[gender[b]] += ...; dC[country[b]] += ... */
+int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
+                         const int64_t* gender, int dg, const int64_t* country, int dc,
+                         float* dx, float* dG, float* dC, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * BatchNorm1d + ReLU + dropout (item_tower.py:122-126 fusion head, item_tower.py:89-93
+ * tabular MLP).  training != 0: batch statistics (biased var) normalise, the running
+ * buffers get momentum updates with the unbiased var, num_batches_tracked += 1, and
+ * mean/rstd (may be NULL) receive the batch statistics.  training == 0: running statistics,
+ * no update.  z [B,C] fp32 -> y [B,C] (dtype); dropout idx = b*C + c.
+ * ---------------------------------------------------------------------------------- */
+int ttmi_batchnorm_fwd(int dtype, int B, int C, const float* z, const float* w, const float* b,
+                       float eps, float momentum, float* running_mean, float* running_var,
+                       int64_t* num_batches_tracked, int training, int relu, float drop_p,
+                       const uint64_t* drop_seed, void* y, float* mean, float* rstd,
+                       hipStream_t stream);
+/* dz = BN'(dy ⊙ (y > 0 ? gate_scale : 1 when relu/dropout)); dw/db accumulate. */
+int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, const float* z,
+                       const float* w, const float* mean, const float* rstd, const void* y,
+                       float gate_scale, int gated, float* dz, float* dw, float* db,
+                       hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Symmetric in-batch InfoNCE (two_tower.py:98-140), fp32 throughout:
+ *   û = u/max(|u|,1e-12), î likewise; S = û·îᵀ·inv_tau; S[i,j] = -1e4 where
+ *   user_idx[i] == user_idx[j] and i != j (user_idx may be NULL: no collision mask);
+ *   loss = ½(CE(S, arange) + CE(Sᵀ, arange)) with mean reduction.
+ * Outputs: û, î [B,D]; norms [2B]; logits [B,B] (masked, as the reference returns them);
+ * lse [2B] (row LSEs then column LSEs); loss [1].  ws: ttmi_infonce_workspace(B, D) bytes.
+ * ---------------------------------------------------------------------------------- */
+int64_t ttmi_infonce_workspace(int B, int D);
+int ttmi_infonce_fwd(int B, int D, const float* u, const float* it, const int64_t* user_idx,
+                     float inv_tau, float* u_hat, float* i_hat, float* norms, float* logits,
+                     float* lse, float* loss, void* ws, hipStream_t stream);
+/* Backward given dloss (device scalar; NULL means 1): writes du, di [B,D]. */
+int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat, const float* norms,
+                     const float* logits, const float* lse, const int64_t* user_idx,
+                     float inv_tau, const float* dloss, float* du, float* di, void* ws,
+                     hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Fused AdamW over flat fp32 buffers (torch.optim.AdamW defaults, train.py:302):
+ *   t = ++(*step); p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g²;
+ *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps).
+ * hyper (device, fp64) = {lr, beta1, beta2, eps, weight_decay}; step (device int32) holds
+ * t (the caller increments it with ttmi_step_inc before the update), so a captured graph
+ * replays with the live step count and learning rate.  p_bf16 (optional)
+ * receives the bf16 mirror used as GEMM operand by the next step.
+ * ---------------------------------------------------------------------------------- */
+int ttmi_adamw(int64_t n, float* p, const float* g, float* m, float* v, uint16_t* p_bf16,
+               const double* hyper, const int32_t* step, hipStream_t stream);
+int ttmi_step_inc(int32_t* step, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Elementwise helpers.
+ * ---------------------------------------------------------------------------------- */
+/* seeds[s] = splitmix64(splitmix64(base) ^ (*step * 64 + s)), s < n <= 256: per-site dropout
+ * seeds of the current step, derived on device from the live step counter. */
+int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int n,
+                       hipStream_t stream);
+/* dst = bf16(src) (parameter mirror for bf16 GEMM operands). */
+int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hipStream_t stream);
+/* Residual-branch dropout backward (TransformerEncoderLayer dropout1/dropout2):
+ * dy[m,n] = dx[m,n]·keep(m*ld_drop+n)/(1-p) cast to dtype; colsum[n] += dy[m,n] (bias grad). */
+int ttmi_dropout_bwd(int dtype, int64_t M, int N, const float* dx, int64_t ldx, float drop_p,
+                     const uint64_t* drop_seed, int64_t ld_drop, void* dy, int64_t ldy, float* colsum,
+                     hipStream_t stream);
+/* colsum[n] += Σ_m x[m*ldx+n]  (bias grads of GEMMs fed by attention backward). */
+int ttmi_colsum(int dtype, int64_t M, int N, const void* x, int64_t ldx, float* colsum,
+                hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TTMI_H */

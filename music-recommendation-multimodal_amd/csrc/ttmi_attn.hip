@@ -1,0 +1,357 @@
+// ttmi_attn.hip — SASRec causal self-attention core (SDPA inside nn.MultiheadAttention,
+// reference user_tower.py:111-116), forward and backward.
+//
+// One 64-lane wave owns one (sequence b, head h).  A whole sequence (L <= 64 keys) fits
+// in LDS, so there is no online softmax: S = Q·Kᵀ is built in MFMA accumulators (4x4 tiles
+// of 16x16; the six tiles above the diagonal are fully masked and skipped), softmax runs
+// in registers (row = 16 lanes x 4 column tiles -> group16 shuffles), P goes back to LDS
+// as the A operand of O = P·V.  The backward recomputes P from the forward's per-row LSE
+// and produces dQ, dK, dV with five MFMA products, overlaying the transposed P/dS images
+// on the row-major Q/K/V/dO images once they are consumed.
+//
+// Tiles are padded: keys/queries to 64 rows, the head dim to DHP (32 or 64) with zeros.
+#include "ttmi_common.h"
+
+namespace {
+
+constexpr int LP = 64;   // padded sequence length
+
+template <typename T, int DHP>
+struct AttnGeom {
+  static constexpr int ES = (int)sizeof(T);
+  static constexpr int E = 16 / ES;                 // elements per 16-byte chunk
+  static constexpr int RQ = DHP * ES + 16;          // row pitch of [64][DHP] images
+  static constexpr int RP = LP * ES + 16;           // row pitch of [*][64] images
+  static constexpr int CQ = DHP * ES / 64;          // 64-byte k-chunks along DHP
+  static constexpr int CP = LP * ES / 64;           // 64-byte k-chunks along 64 keys
+  static constexpr int TD = DHP / 16;               // 16-wide tiles along DHP
+  static constexpr int ROW_IMG = LP * RQ;           // bytes of one [64][DHP] image
+  static constexpr int SQ_IMG = LP * RP;            // bytes of one [64][64] image
+  static constexpr int T_IMG = DHP * RP;            // bytes of one [DHP][64] image
+};
+
+// Load a head slice [L][Dh] (row stride ld elements) into a row-major [64][DHP] image and/or
+// a transposed [DHP][64] image, zero-padded.
+template <typename T, int DHP>
+TTMI_DEV void load_head(const T* __restrict__ src, int64_t ld, int L, int Dh, char* rowimg,
+                        char* trimg, int lane) {
+  using G = AttnGeom<T, DHP>;
+  constexpr int CPR = DHP / G::E;                   // 16-byte chunks per row
+  for (int idx = lane; idx < LP * CPR; idx += 64) {
+    const int r = idx / CPR, ch = idx % CPR;
+    const int d0 = ch * G::E;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < L && d0 < Dh) v = *reinterpret_cast<const uint4*>(src + (int64_t)r * ld + d0);
+    if (rowimg) *reinterpret_cast<uint4*>(rowimg + r * G::RQ + ch * 16) = v;
+    if (trimg) {
+      const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+      for (int k = 0; k < G::E; ++k)
+        *reinterpret_cast<T*>(trimg + (d0 + k) * G::RP + r * G::ES) = e[k];
+    }
+  }
+}
+
+// acc[ti][tj] (tj <= ti) = Σ_k A[ti rows][k] · B[tj rows][k] over NCH 64-byte chunks.
+template <typename T, int NCH, int PITCH>
+TTMI_DEV void mma_lower(f32x4_t (&acc)[4][4], const char* A, const char* Bm, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int r = lane & 15, kq = (lane >> 4) * 16;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    uint4 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = lds16(A + (i * 16 + r) * PITCH + c * 64 + kq);
+      b[i] = lds16(Bm + (i * 16 + r) * PITCH + c * 64 + kq);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j <= i; ++j) Mma<T>::run(acc[i][j], a[i], b[j]);
+  }
+}
+
+// out[ti][td] = Σ_k A[ti rows][k] · B[td rows][k]; A pitch RP (k = 64 keys), B [DHP][64].
+template <typename T, int DHP>
+TTMI_DEV void mma_pv(f32x4_t (&acc)[4][DHP / 16], const char* A, const char* Bm, int lane) {
+  using G = AttnGeom<T, DHP>;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TD; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int r = lane & 15, kq = (lane >> 4) * 16;
+#pragma unroll
+  for (int c = 0; c < G::CP; ++c) {
+    uint4 a[4], b[G::TD];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = lds16(A + (i * 16 + r) * G::RP + c * 64 + kq);
+#pragma unroll
+    for (int j = 0; j < G::TD; ++j) b[j] = lds16(Bm + (j * 16 + r) * G::RP + c * 64 + kq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < G::TD; ++j) Mma<T>::run(acc[i][j], a[i], b[j]);
+  }
+}
+
+template <typename T, int DHP>
+TTMI_DEV void store_head(T* __restrict__ dst, int64_t ld, int L, int Dh,
+                         const f32x4_t (&acc)[4][DHP / 16], int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < DHP / 16; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = i * 16 + (lane >> 4) * 4 + e, d = j * 16 + (lane & 15);
+        if (r < L && d < Dh) stf<T>(dst, (int64_t)r * ld + d, acc[i][j][e]);
+      }
+}
+
+template <typename T, int DHP>
+__global__ __launch_bounds__(64) void mha_fwd_kernel(int B, int L, int H, int Dh,
+                                                     const T* __restrict__ qkv,
+                                                     const int64_t* __restrict__ kvalid,
+                                                     DropParams dp, T* __restrict__ ctx,
+                                                     float* __restrict__ lse, float scale) {
+  using G = AttnGeom<T, DHP>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::ROW_IMG + G::T_IMG + G::SQ_IMG];
+  char* sQ = smem;
+  char* sK = sQ + G::ROW_IMG;
+  char* sVt = sK + G::ROW_IMG;
+  char* sP = sVt + G::T_IMG;
+  const int lane = threadIdx.x;
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh % H;
+  const int D = H * Dh;
+  const int64_t ld = 3LL * D;
+  const T* base = qkv + (int64_t)b * L * ld + (int64_t)h * Dh;
+  load_head<T, DHP>(base, ld, L, Dh, sQ, nullptr, lane);
+  load_head<T, DHP>(base + D, ld, L, Dh, sK, nullptr, lane);
+  load_head<T, DHP>(base + 2 * D, ld, L, Dh, nullptr, sVt, lane);
+  bool kv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 16 + (lane & 15);
+    kv[j] = c < L && kvalid[(int64_t)b * L + c] != 0;
+  }
+  __syncthreads();
+
+  f32x4_t s[4][4];
+  mma_lower<T, G::CQ, G::RQ>(s, sQ, sK, lane);
+  const DropKeys dk = resolve_drop(dp);
+
+  const int q4 = (lane >> 4) * 4;
+  const int cl = lane & 15;
+  const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = i * 16 + q4 + e;
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j <= i; ++j) {
+        const int c = j * 16 + cl;
+        const bool ok = kv[j] && c <= r && r < L;
+        const float v = ok ? s[i][j][e] * scale : -INFINITY;
+        s[i][j][e] = v;
+        m = fmaxf(m, v);
+      }
+      m = group16_max(m);
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j <= i; ++j) {
+        const float p = m == -INFINITY ? 0.f : expf(s[i][j][e] - m);
+        s[i][j][e] = p;
+        sum += p;
+      }
+      sum = group16_sum(sum);
+      const float inv = sum > 0.f ? 1.f / sum : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = j * 16 + cl;
+        float p = 0.f;
+        if (j <= i) {
+          p = s[i][j][e] * inv;
+          if (dk.on && r < L && c < L) p = drop_apply(dk, pbase + (uint32_t)(r * L + c), p);
+        }
+        stf<T>(reinterpret_cast<T*>(sP + r * G::RP), c, p);
+      }
+      if (cl == 0 && r < L) lse[(int64_t)bh * L + r] = m == -INFINITY ? INFINITY : m + logf(sum);
+    }
+  }
+  __syncthreads();
+  f32x4_t o[4][G::TD];
+  mma_pv<T, DHP>(o, sP, sVt, lane);
+  store_head<T, DHP>(ctx + (int64_t)b * L * D + (int64_t)h * Dh, D, L, Dh, o, lane);
+}
+
+template <typename T, int DHP>
+__global__ __launch_bounds__(64) void mha_bwd_kernel(int B, int L, int H, int Dh,
+                                                     const T* __restrict__ qkv,
+                                                     const int64_t* __restrict__ kvalid,
+                                                     const float* __restrict__ lse,
+                                                     const T* __restrict__ dctx, DropParams dp,
+                                                     T* __restrict__ dqkv, float scale) {
+  using G = AttnGeom<T, DHP>;
+  constexpr int R1 = (4 * G::ROW_IMG > 3 * G::SQ_IMG) ? 4 * G::ROW_IMG : 3 * G::SQ_IMG;
+  __shared__ __attribute__((aligned(16))) char smem[R1 + 3 * G::T_IMG];
+  char* sQ = smem;                   // phase 1: row-major images
+  char* sK = sQ + G::ROW_IMG;
+  char* sV = sK + G::ROW_IMG;
+  char* sdO = sV + G::ROW_IMG;
+  char* sPt = smem;                  // phase 2: overlays region 1
+  char* sdS = sPt + G::SQ_IMG;
+  char* sdSt = sdS + G::SQ_IMG;
+  char* sQt = smem + R1;             // transposed images (both phases)
+  char* sKt = sQt + G::T_IMG;
+  char* sdOt = sKt + G::T_IMG;
+  const int lane = threadIdx.x;
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh % H;
+  const int D = H * Dh;
+  const int64_t ld = 3LL * D;
+  const T* base = qkv + (int64_t)b * L * ld + (int64_t)h * Dh;
+  const T* dob = dctx + (int64_t)b * L * D + (int64_t)h * Dh;
+  load_head<T, DHP>(base, ld, L, Dh, sQ, sQt, lane);
+  load_head<T, DHP>(base + D, ld, L, Dh, sK, sKt, lane);
+  load_head<T, DHP>(base + 2 * D, ld, L, Dh, sV, nullptr, lane);
+  load_head<T, DHP>(dob, D, L, Dh, sdO, sdOt, lane);
+  bool kv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 16 + (lane & 15);
+    kv[j] = c < L && kvalid[(int64_t)b * L + c] != 0;
+  }
+  __syncthreads();
+
+  f32x4_t s[4][4], dpd[4][4];
+  mma_lower<T, G::CQ, G::RQ>(s, sQ, sK, lane);      // S  = Q Kᵀ
+  mma_lower<T, G::CQ, G::RQ>(dpd, sdO, sV, lane);   // dPd = dO Vᵀ (grad of dropped probs)
+
+  const int q4 = (lane >> 4) * 4;
+  const int cl = lane & 15;
+  const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
+  const DropKeys dk = resolve_drop(dp);
+  __syncthreads();   // region 1 is rewritten below
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = i * 16 + q4 + e;
+      const float lr = r < L ? lse[(int64_t)bh * L + r] : INFINITY;
+      // pass A: p = softmax prob (pre-dropout), dP = dPd * keep/(1-p); row sum Σ p·dP
+      float dsum = 0.f;
+#pragma unroll
+      for (int j = 0; j <= i; ++j) {
+        const int c = j * 16 + cl;
+        const bool ok = kv[j] && c <= r && r < L;
+        const float p = ok ? expf(s[i][j][e] * scale - lr) : 0.f;
+        float dP = 0.f;
+        if (ok) {
+          dP = dpd[i][j][e];
+          if (dk.on) dP = drop_keep(dk, pbase + (uint32_t)(r * L + c)) ? dP * dk.scale : 0.f;
+        }
+        s[i][j][e] = p;
+        dpd[i][j][e] = dP;
+        dsum += p * dP;
+      }
+      dsum = group16_sum(dsum);
+      // pass B: dS = p (dP - Σ) · scale;  Pd = p·keep/(1-p); scatter to the LDS images
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = j * 16 + cl;
+        float pd = 0.f, ds = 0.f;
+        if (j <= i) {
+          const float p = s[i][j][e];
+          ds = p * (dpd[i][j][e] - dsum) * scale;
+          pd = p;
+          if (dk.on && p != 0.f) pd = drop_keep(dk, pbase + (uint32_t)(r * L + c)) ? p * dk.scale : 0.f;
+        }
+        stf<T>(reinterpret_cast<T*>(sPt + c * G::RP), r, pd);
+        stf<T>(reinterpret_cast<T*>(sdS + r * G::RP), c, ds);
+        stf<T>(reinterpret_cast<T*>(sdSt + c * G::RP), r, ds);
+      }
+    }
+  }
+  __syncthreads();
+
+  T* gq = dqkv + (int64_t)b * L * ld + (int64_t)h * Dh;
+  f32x4_t o[4][G::TD];
+  mma_pv<T, DHP>(o, sPt, sdOt, lane);                // dV = Pdᵀ dO
+  store_head<T, DHP>(gq + 2 * D, ld, L, Dh, o, lane);
+  mma_pv<T, DHP>(o, sdS, sKt, lane);                 // dQ = dS K
+  store_head<T, DHP>(gq, ld, L, Dh, o, lane);
+  mma_pv<T, DHP>(o, sdSt, sQt, lane);                // dK = dSᵀ Q
+  store_head<T, DHP>(gq + D, ld, L, Dh, o, lane);
+}
+
+template <typename T, int DHP>
+void launch_fwd(int B, int L, int H, int Dh, const void* qkv, const int64_t* kv, DropParams dp,
+                void* ctx, float* lse, hipStream_t s) {
+  hipLaunchKernelGGL((mha_fwd_kernel<T, DHP>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                     (const T*)qkv, kv, dp, (T*)ctx, lse, 1.f / sqrtf((float)Dh));
+}
+template <typename T, int DHP>
+void launch_bwd(int B, int L, int H, int Dh, const void* qkv, const int64_t* kv, const float* lse,
+                const void* dctx, DropParams dp, void* dqkv, hipStream_t s) {
+  hipLaunchKernelGGL((mha_bwd_kernel<T, DHP>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                     (const T*)qkv, kv, lse, (const T*)dctx, dp, (T*)dqkv, 1.f / sqrtf((float)Dh));
+}
+
+int check_mha(const char* fn, int dtype, int B, int L, int H, int Dh, const void* qkv,
+              const int64_t* kv) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "%s: bad dtype", fn);
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= LP && H > 0, "%s: need 0 < L <= %d (got L=%d)", fn, LP, L);
+  TTMI_REQUIRE(Dh > 0 && Dh <= 64 && Dh % 8 == 0, "%s: need Dh %% 8 == 0 and Dh <= 64 (got %d)", fn, Dh);
+  TTMI_REQUIRE(qkv && kv, "%s: null argument", fn);
+  TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "%s: qkv must be 16-byte aligned", fn);
+  TTMI_REQUIRE((int64_t)B * H * L * L < (1LL << 32), "%s: dropout index space exceeds 2^32", fn);
+  return TTMI_OK;
+}
+
+}  // namespace
+
+extern "C" int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                            const int64_t* key_valid, float drop_p, const uint64_t* drop_seed, void* ctx,
+                            float* lse, hipStream_t s) {
+  int rc = check_mha("ttmi_mha_fwd", dtype, B, L, H, Dh, qkv, key_valid);
+  if (rc) return rc;
+  TTMI_REQUIRE(ctx && lse, "ttmi_mha_fwd: null output");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_mha_fwd: drop_p out of [0,1)");
+  if (B == 0) return TTMI_OK;
+  DropParams dp = make_drop(drop_p, drop_seed);
+  if (dtype == TTMI_BF16) {
+    if (Dh <= 32) launch_fwd<bf16_t, 32>(B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
+    else launch_fwd<bf16_t, 64>(B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
+  } else {
+    if (Dh <= 32) launch_fwd<float, 32>(B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
+    else launch_fwd<float, 64>(B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
+  }
+  return ttmi_check_launch("ttmi_mha_fwd");
+}
+
+extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                            const int64_t* key_valid, const float* lse, const void* dctx,
+                            float drop_p, const uint64_t* drop_seed, void* dqkv, hipStream_t s) {
+  int rc = check_mha("ttmi_mha_bwd", dtype, B, L, H, Dh, qkv, key_valid);
+  if (rc) return rc;
+  TTMI_REQUIRE(lse && dctx && dqkv, "ttmi_mha_bwd: null argument");
+  TTMI_REQUIRE(((uintptr_t)dctx & 15) == 0, "ttmi_mha_bwd: dctx must be 16-byte aligned");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_mha_bwd: drop_p out of [0,1)");
+  if (B == 0) return TTMI_OK;
+  DropParams dp = make_drop(drop_p, drop_seed);
+  if (dtype == TTMI_BF16) {
+    if (Dh <= 32) launch_bwd<bf16_t, 32>(B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);
+    else launch_bwd<bf16_t, 64>(B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);
+  } else {
+    if (Dh <= 32) launch_bwd<float, 32>(B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);
+    else launch_bwd<float, 64>(B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);
+  }
+  return ttmi_check_launch("ttmi_mha_bwd");
+}

@@ -1,0 +1,145 @@
+// ttmi_common.h — shared device helpers for the MI355X (gfx950) two-tower kernels.
+//
+// * bf16 stored as uint16_t; f32->bf16 is round-to-nearest-even via the __bf16 cast
+//   (hipcc emits v_cvt_pk_bf16_f32, which keeps NaN a NaN).
+// * Dropout uses a stateless counter hash (restated in oracle/two_tower_ref.py:hash_keep)
+//   so forward and backward regenerate the same mask from (seed, flat index).
+// * MFMA operands: every kernel stages tiles in LDS as [row][k] with k contiguous and
+//   reads 16 bytes per lane at (row = lane&15, byte 16*(lane>>4)) of a 64-byte k-chunk.
+//   For bf16 that is exactly the v_mfma_f32_16x16x32_bf16 A/B fragment; for f32 the four
+//   floats feed four v_mfma_f32_16x16x4_f32 (k permuted identically on A and B, so the
+//   sum is unchanged).  C/D layout (both): col = lane&15, row = 4*(lane>>4) + reg.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <climits>
+
+#include "../../include/ttmi.h"
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+#define TTMI_DEV __device__ __forceinline__
+
+TTMI_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+TTMI_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static TTMI_DEV float ld(const float* p, int64_t i) { return p[i]; }
+  static TTMI_DEV void st(float* p, int64_t i, float v) { p[i] = v; }
+};
+template <> struct Elem<bf16_t> {
+  static TTMI_DEV float ld(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
+  static TTMI_DEV void st(bf16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
+};
+template <typename T> TTMI_DEV float ldf(const T* p, int64_t i) { return Elem<T>::ld(p, i); }
+template <typename T> TTMI_DEV void stf(T* p, int64_t i, float v) { Elem<T>::st(p, i, v); }
+TTMI_DEV float ld_dyn(const void* p, int64_t i, bool f32) {
+  return f32 ? ((const float*)p)[i] : bf2f(((const bf16_t*)p)[i]);
+}
+TTMI_DEV void st_dyn(void* p, int64_t i, float v, bool f32) {
+  if (f32) ((float*)p)[i] = v; else ((bf16_t*)p)[i] = f2bf(v);
+}
+
+// ---------------------------------------------------------------- dropout hash
+TTMI_DEV uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+// Host-built descriptor; the 64-bit seed lives in device memory so a captured hipGraph
+// replays with fresh masks (the train step rewrites its seed table every step).
+struct DropParams {
+  const uint64_t* seed;
+  uint32_t thresh;
+  float scale;   // 1/(1-p)
+  int on;        // p > 0
+};
+// Device-resolved keys (read the seed once at kernel entry).
+struct DropKeys {
+  uint32_t k0, k1, thresh;
+  float scale;
+  int on;
+};
+TTMI_DEV DropKeys resolve_drop(const DropParams& d) {
+  DropKeys k;
+  k.on = d.on;
+  k.thresh = d.thresh;
+  k.scale = d.scale;
+  const uint64_t s = d.on ? *d.seed : 0ull;
+  k.k0 = (uint32_t)(s & 0xFFFFFFFFull);
+  k.k1 = (uint32_t)(s >> 32);
+  return k;
+}
+TTMI_DEV bool drop_keep(const DropKeys& d, uint32_t idx) {
+  return lowbias32(lowbias32(idx + d.k0) ^ d.k1) >= d.thresh;
+}
+TTMI_DEV float drop_apply(const DropKeys& d, uint32_t idx, float v) {
+  if (!d.on) return v;
+  return drop_keep(d, idx) ? v * d.scale : 0.f;
+}
+static inline DropParams make_drop(float p, const uint64_t* seed) {
+  DropParams d;
+  d.seed = seed;
+  double t = (double)p * 4294967296.0;
+  d.thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  d.on = p > 0.f;
+  d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  return d;
+}
+
+// ---------------------------------------------------------------- wave reductions
+TTMI_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+TTMI_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reduce across the 16 lanes that share (lane >> 4) — one MFMA C-row group
+TTMI_DEV float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+TTMI_DEV float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- MFMA on 16-byte fragments
+// acc(16x16 f32) += A_frag · B_frag over one 64-byte k-chunk (32 bf16 or 16 f32).
+template <typename T> struct Mma;
+template <> struct Mma<bf16_t> {
+  static TTMI_DEV void run(f32x4_t& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                  __builtin_bit_cast(bf16x8_t, b), acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  static TTMI_DEV void run(f32x4_t& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+};
+TTMI_DEV uint4 lds16(const char* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// ---------------------------------------------------------------- host-side error plumbing
+void ttmi_set_error(const char* fmt, ...);
+#define TTMI_REQUIRE(cond, ...)                      \
+  do {                                               \
+    if (!(cond)) {                                   \
+      ttmi_set_error(__VA_ARGS__);                   \
+      return TTMI_ERR_ARG;                           \
+    }                                                \
+  } while (0)
+int ttmi_check_launch(const char* what);

@@ -1,0 +1,515 @@
+// ttmi_norm.hip — row/column normalisation kernels of the two-tower step:
+//   LayerNorm fwd/bwd (one wave per row, D <= 1024 held in registers, fp32 statistics),
+//   the SASRec input block (embedding gather + position add + LN + dropout) fwd/bwd,
+//   the last-valid-row gather + demographics concat fwd/bwd, BatchNorm1d train fwd/bwd.
+#include "ttmi_common.h"
+
+namespace {
+
+constexpr int MAXV = 16;   // D <= 64 * MAXV
+
+// ------------------------------------------------------------------------------ LayerNorm
+template <typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const float* __restrict__ x,
+                                                     int64_t ldx, const float* __restrict__ w,
+                                                     const float* __restrict__ b, float eps,
+                                                     int relu, DropParams dp, TY* __restrict__ y,
+                                                     int64_t ldy, float* __restrict__ mean,
+                                                     float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const float invD = 1.f / (float)D;
+  const DropKeys dk = resolve_drop(dp);
+  for (int64_t row = wid; row < M; row += nw) {
+    float v[MAXV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < D ? x[row * ldx + c] : 0.f;
+      s += v[i];
+    }
+    const float mu = wave_sum(s) * invD;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      const float dlt = c < D ? v[i] - mu : 0.f;
+      q += dlt * dlt;
+    }
+    const float rs = 1.f / sqrtf(wave_sum(q) * invD + eps);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        float o = (v[i] - mu) * rs * w[c] + b[c];
+        if (relu) o = fmaxf(o, 0.f);
+        if (dk.on) o = drop_apply(dk, (uint32_t)(row * D + c), o);
+        stf<TY>(y, row * ldy + c, o);
+      }
+    }
+    if (lane == 0) {
+      if (mean) mean[row] = mu;
+      if (rstd) rstd[row] = rs;
+    }
+  }
+}
+
+// Per-block reduction of per-lane column partials (4 waves) followed by one atomic per column.
+TTMI_DEV void block_col_atomic(float (&acc)[MAXV], int D, float* dst, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) red[wave * 64 * MAXV + c] = acc[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    const float t = red[c] + red[64 * MAXV + c] + red[2 * 64 * MAXV + c] + red[3 * 64 * MAXV + c];
+    atomicAdd(dst + c, t);
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    int64_t M, int D, const float* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
+    int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ w, const void* __restrict__ gate, int gate_f32, int64_t ldg,
+    float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ dw,
+    float* __restrict__ db) {
+  __shared__ float red[4 * 64 * MAXV];
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const float invD = 1.f / (float)D;
+  float aw[MAXV], ab[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) aw[i] = ab[i] = 0.f;
+  for (int64_t row = wid; row < M; row += nw) {
+    const float mu = mean[row], rs = rstd[row];
+    float g[MAXV], xh[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      g[i] = 0.f; xh[i] = 0.f;
+      if (c < D) {
+        float d = dy[row * lddy + c];
+        if (gate) d = ld_dyn(gate, row * ldg + c, gate_f32) > 0.f ? d * gate_scale : 0.f;
+        xh[i] = (x[row * ldx + c] - mu) * rs;
+        aw[i] += d * xh[i];
+        ab[i] += d;
+        g[i] = d * w[c];
+        s1 += g[i];
+        s2 += g[i] * xh[i];
+      }
+    }
+    const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        const float o = rs * (g[i] - c1 - xh[i] * c2);
+        dx[row * lddx + c] = (res ? res[row * lddx + c] : 0.f) + o;
+      }
+    }
+  }
+  if (dw) block_col_atomic(aw, D, dw, red);
+  if (db) block_col_atomic(ab, D, db, red);
+}
+
+// ------------------------------------------------------------------- SASRec input block
+// Forward: one wave per token row.
+__global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
+    int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E, int64_t V,
+    const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ b,
+    float eps, DropParams dp, float* __restrict__ x, float* __restrict__ mean,
+    float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t M = (int64_t)B * L;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const float invD = 1.f / (float)D;
+  const DropKeys dk = resolve_drop(dp);
+  for (int64_t row = wid; row < M; row += nw) {
+    const int l = (int)(row % L);
+    const int64_t id = ids[row];
+    const bool ok = id >= 0 && id < V;
+    float v[MAXV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < D ? (ok ? E[id * D + c] : 0.f) + P[(int64_t)l * D + c] : 0.f;
+      s += v[i];
+    }
+    const float mu = wave_sum(s) * invD;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      const float dlt = c < D ? v[i] - mu : 0.f;
+      q += dlt * dlt;
+    }
+    const float rs = 1.f / sqrtf(wave_sum(q) * invD + eps);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        float o = (v[i] - mu) * rs * w[c] + b[c];
+        if (dk.on) o = drop_apply(dk, (uint32_t)(row * D + c), o);
+        x[row * D + c] = o;
+      }
+    }
+    if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+  }
+}
+
+// Backward: block (l, b-chunk); each wave walks b = chunk*bpc + wave, +4, ... so the
+// position gradient dP[l] accumulates in registers (one atomic per column per block).
+__global__ __launch_bounds__(256) void seq_embed_bwd_kernel(
+    int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E,
+    const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ mean,
+    const float* __restrict__ rstd, DropParams dp, const float* __restrict__ dx,
+    float* __restrict__ dE, float* __restrict__ dP, float* __restrict__ dw, float* __restrict__ db,
+    int64_t padding_idx, int64_t V, int bpc) {
+  __shared__ float red[4 * 64 * MAXV];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l = blockIdx.x;
+  const int b0 = blockIdx.y * bpc;
+  const int b1 = min(B, b0 + bpc);
+  const float invD = 1.f / (float)D;
+  const DropKeys dk = resolve_drop(dp);
+  float ap[MAXV], aw[MAXV], ab[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) ap[i] = aw[i] = ab[i] = 0.f;
+  for (int bb = b0 + wave; bb < b1; bb += 4) {
+    const int64_t row = (int64_t)bb * L + l;
+    const int64_t id = ids[row];
+    const bool ok = id >= 0 && id < V;
+    const float mu = mean[row], rs = rstd[row];
+    float g[MAXV], xh[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      g[i] = 0.f; xh[i] = 0.f;
+      if (c < D) {
+        float d = dx[row * D + c];
+        if (dk.on) d = drop_keep(dk, (uint32_t)(row * D + c)) ? d * dk.scale : 0.f;
+        const float e = (ok ? E[id * D + c] : 0.f) + P[(int64_t)l * D + c];
+        xh[i] = (e - mu) * rs;
+        aw[i] += d * xh[i];
+        ab[i] += d;
+        g[i] = d * w[c];
+        s1 += g[i];
+        s2 += g[i] * xh[i];
+      }
+    }
+    const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
+    const bool emb = ok && id != padding_idx;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        const float o = rs * (g[i] - c1 - xh[i] * c2);
+        ap[i] += o;
+        if (emb) atomicAdd(dE + id * D + c, o);
+      }
+    }
+  }
+  block_col_atomic(ap, D, dP + (int64_t)l * D, red);
+  block_col_atomic(aw, D, dw, red);
+  block_col_atomic(ab, D, db, red);
+}
+
+// ------------------------------------------------------------ last-valid gather + concat
+template <typename T>
+__global__ void user_concat_fwd_kernel(int B, int L, int D, const float* __restrict__ x,
+                                       const int64_t* __restrict__ len_src,
+                                       const int64_t* __restrict__ gender,
+                                       const float* __restrict__ G, int dg,
+                                       const int64_t* __restrict__ country,
+                                       const float* __restrict__ C, int dc, T* __restrict__ comb,
+                                       int32_t* __restrict__ rows) {
+  const int lane = threadIdx.x & 63;
+  const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (b >= B) return;
+  float cnt = 0.f;
+  for (int l = lane; l < L; l += 64) cnt += len_src[(int64_t)b * L + l] != 0 ? 1.f : 0.f;
+  const int len = (int)(wave_sum(cnt) + 0.5f);
+  const int64_t row = (int64_t)b * L + max(len - 1, 0);
+  const int W = D + dg + dc;
+  const int64_t g = gender[b], c = country[b];
+  for (int k = lane; k < W; k += 64) {
+    float v;
+    if (k < D) v = x[row * D + k];
+    else if (k < D + dg) v = G[g * dg + (k - D)];
+    else v = C[c * dc + (k - D - dg)];
+    stf<T>(comb, (int64_t)b * W + k, v);
+  }
+  if (lane == 0) rows[b] = (int32_t)row;
+}
+
+__global__ void user_concat_bwd_kernel(int B, int D, const float* __restrict__ dcomb,
+                                       const int32_t* __restrict__ rows,
+                                       const int64_t* __restrict__ gender, int dg,
+                                       const int64_t* __restrict__ country, int dc,
+                                       float* __restrict__ dx, float* __restrict__ dG,
+                                       float* __restrict__ dC) {
+  const int lane = threadIdx.x & 63;
+  const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (b >= B) return;
+  const int W = D + dg + dc;
+  const int64_t row = rows[b];
+  const int64_t g = gender[b], c = country[b];
+  for (int k = lane; k < W; k += 64) {
+    const float v = dcomb[(int64_t)b * W + k];
+    if (k < D) atomicAdd(dx + row * D + k, v);
+    else if (k < D + dg) { if (dG) atomicAdd(dG + g * dg + (k - D), v); }
+    else if (dC) atomicAdd(dC + c * dc + (k - D - dg), v);
+  }
+}
+
+// ---------------------------------------------------------------------- BatchNorm1d
+// Block: 256 threads = 64 columns x 4 row groups.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_fwd_kernel(int B, int C, const float* __restrict__ z,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ b, float eps,
+                                                     float momentum, float* running_mean,
+                                                     float* running_var, int64_t* nbt,
+                                                     int training, int relu, DropParams dp,
+                                                     T* __restrict__ y, float* __restrict__ mean,
+                                                     float* __restrict__ rstd) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const bool ok = c < C;
+  float mu, var;
+  if (training) {
+    float s = 0.f;
+    if (ok) for (int r = rg; r < B; r += 4) s += z[(int64_t)r * C + c];
+    red[rg][cl] = s;
+    __syncthreads();
+    mu = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) / (float)B;
+    __syncthreads();
+    float q = 0.f;
+    if (ok) for (int r = rg; r < B; r += 4) { const float d = z[(int64_t)r * C + c] - mu; q += d * d; }
+    red[rg][cl] = q;
+    __syncthreads();
+    var = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) / (float)B;
+  } else {                                     // eval: running statistics, no update
+    mu = ok ? running_mean[c] : 0.f;
+    var = ok ? running_var[c] : 1.f;
+  }
+  const float rs = 1.f / sqrtf(var + eps);
+  const DropKeys dk = resolve_drop(dp);
+  if (ok) {
+    const float wc = w[c], bc = b[c];
+    for (int r = rg; r < B; r += 4) {
+      float o = (z[(int64_t)r * C + c] - mu) * rs * wc + bc;
+      if (relu) o = fmaxf(o, 0.f);
+      if (dk.on) o = drop_apply(dk, (uint32_t)((int64_t)r * C + c), o);
+      stf<T>(y, (int64_t)r * C + c, o);
+    }
+    if (rg == 0) {
+      if (mean) mean[c] = mu;
+      if (rstd) rstd[c] = rs;
+      if (training && running_mean)
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
+      if (training && running_var)
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * var * ((float)B / (float)(B - 1));
+    }
+  }
+  if (training && nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_kernel(int B, int C, const float* __restrict__ dy,
+                                                     const float* __restrict__ z,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     const T* __restrict__ y, float gate_scale,
+                                                     int gated, float* __restrict__ dz,
+                                                     float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[2][4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const bool ok = c < C;
+  const float mu = ok ? mean[c] : 0.f, rs = ok ? rstd[c] : 0.f, wc = ok ? w[c] : 0.f;
+  float s1 = 0.f, s2 = 0.f;   // Σ dy', Σ dy'·x̂
+  if (ok) {
+    for (int r = rg; r < B; r += 4) {
+      const int64_t o = (int64_t)r * C + c;
+      float d = dy[o];
+      if (gated) d = ldf<T>(y, o) > 0.f ? d * gate_scale : 0.f;
+      const float xh = (z[o] - mu) * rs;
+      s1 += d;
+      s2 += d * xh;
+    }
+  }
+  red[0][rg][cl] = s1;
+  red[1][rg][cl] = s2;
+  __syncthreads();
+  const float S1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  const float S2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  if (!ok) return;
+  const float invB = 1.f / (float)B;
+  for (int r = rg; r < B; r += 4) {
+    const int64_t o = (int64_t)r * C + c;
+    float d = dy[o];
+    if (gated) d = ldf<T>(y, o) > 0.f ? d * gate_scale : 0.f;
+    const float xh = (z[o] - mu) * rs;
+    dz[o] = wc * rs * (d - S1 * invB - xh * S2 * invB);
+  }
+  if (rg == 0) {
+    if (dw) atomicAdd(dw + c, S2);
+    if (db) atomicAdd(db + c, S1);
+  }
+}
+
+int rows_grid(int64_t rows) {   // 4 rows (waves) per 256-thread block, grid-stride beyond
+  return (int)std::min<int64_t>(std::max<int64_t>((rows + 3) / 4, 1), 2048);
+}
+
+}  // namespace
+
+extern "C" int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const float* w,
+                                  const float* b, float eps, int relu, float drop_p,
+                                  const uint64_t* drop_seed, void* y, int y_dtype, int64_t ldy,
+                                  float* mean, float* rstd, hipStream_t s) {
+  TTMI_REQUIRE(M >= 0 && D > 0 && D <= 64 * MAXV, "ttmi_layernorm_fwd: need 0 < D <= %d", 64 * MAXV);
+  TTMI_REQUIRE(x && w && b && y && ldx >= D && ldy >= D, "ttmi_layernorm_fwd: bad args");
+  TTMI_REQUIRE(y_dtype == TTMI_F32 || y_dtype == TTMI_BF16, "ttmi_layernorm_fwd: bad dtype");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_layernorm_fwd: drop_p out of [0,1)");
+  if (M == 0) return TTMI_OK;
+  DropParams dp = make_drop(drop_p, drop_seed);
+  if (y_dtype == TTMI_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(rows_grid(M)), dim3(256), 0, s, M, D, x, ldx, w, b,
+                       eps, relu, dp, (bf16_t*)y, ldy, mean, rstd);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(rows_grid(M)), dim3(256), 0, s, M, D, x, ldx, w, b,
+                       eps, relu, dp, (float*)y, ldy, mean, rstd);
+  return ttmi_check_launch("ttmi_layernorm_fwd");
+}
+
+extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
+                                  int64_t ldx, const float* mean, const float* rstd,
+                                  const float* w, const void* gate, int gate_dtype, int64_t ldg,
+                                  float gate_scale, const float* res, float* dx, int64_t lddx,
+                                  float* dw, float* db, hipStream_t s) {
+  TTMI_REQUIRE(M >= 0 && D > 0 && D <= 64 * MAXV, "ttmi_layernorm_bwd: need 0 < D <= %d", 64 * MAXV);
+  TTMI_REQUIRE(dy && x && mean && rstd && w && dx, "ttmi_layernorm_bwd: null argument");
+  TTMI_REQUIRE(lddy >= D && ldx >= D && lddx >= D && (!gate || ldg >= D), "ttmi_layernorm_bwd: bad ld");
+  if (M == 0) return TTMI_OK;
+  int grid = (int)std::min<int64_t>((M + 3) / 4, 512);
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w,
+                     gate, gate_dtype == TTMI_F32, ldg, gate_scale, res, dx, lddx, dw, db);
+  return ttmi_check_launch("ttmi_layernorm_bwd");
+}
+
+extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, int64_t V,
+                                  const float* P, const float* w, const float* b, float eps,
+                                  float drop_p, const uint64_t* drop_seed, float* x, float* mean,
+                                  float* rstd, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV, "ttmi_seq_embed_fwd: bad sizes");
+  TTMI_REQUIRE(ids && E && P && w && b && x && mean && rstd, "ttmi_seq_embed_fwd: null argument");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_seq_embed_fwd: drop_p out of [0,1)");
+  if (B == 0) return TTMI_OK;
+  hipLaunchKernelGGL(seq_embed_fwd_kernel, dim3(rows_grid((int64_t)B * L)), dim3(256), 0, s, B, L, D,
+                     ids, E, V, P, w, b, eps, make_drop(drop_p, drop_seed), x, mean, rstd);
+  return ttmi_check_launch("ttmi_seq_embed_fwd");
+}
+
+extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const float* E,
+                                  const float* P, const float* w, const float* mean,
+                                  const float* rstd, float drop_p, const uint64_t* drop_seed,
+                                  const float* dx, float* dE, float* dP, float* dw, float* db,
+                                  int64_t padding_idx, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV, "ttmi_seq_embed_bwd: bad sizes");
+  TTMI_REQUIRE(ids && E && P && w && mean && rstd && dx && dE && dP && dw && db,
+               "ttmi_seq_embed_bwd: null argument");
+  if (B == 0) return TTMI_OK;
+  // V is not needed for the math; rows with out-of-range ids were zero in the forward.
+  const int64_t V = INT64_MAX;
+  const int chunks = std::max(1, std::min((1024 + L - 1) / L, B));
+  const int bpc = (B + chunks - 1) / chunks;
+  dim3 grid(L, (B + bpc - 1) / bpc);
+  hipLaunchKernelGGL(seq_embed_bwd_kernel, grid, dim3(256), 0, s, B, L, D, ids, E, P, w, mean, rstd,
+                     make_drop(drop_p, drop_seed), dx, dE, dP, dw, db, padding_idx, V, bpc);
+  return ttmi_check_launch("ttmi_seq_embed_bwd");
+}
+
+extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
+                                    const int64_t* len_src, const int64_t* gender, const float* G,
+                                    int dg, const int64_t* country, const float* C, int dc,
+                                    void* comb, int32_t* rows, hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_user_concat_fwd: bad dtype");
+  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && dg >= 0 && dc >= 0, "ttmi_user_concat_fwd: bad sizes");
+  TTMI_REQUIRE(x && len_src && gender && country && comb && rows && (dg == 0 || G) && (dc == 0 || C),
+               "ttmi_user_concat_fwd: null argument");
+  if (B == 0) return TTMI_OK;
+  dim3 grid((B + 3) / 4);
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL(user_concat_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, L, D, x, len_src,
+                       gender, G, dg, country, C, dc, (bf16_t*)comb, rows);
+  else
+    hipLaunchKernelGGL(user_concat_fwd_kernel<float>, grid, dim3(256), 0, s, B, L, D, x, len_src,
+                       gender, G, dg, country, C, dc, (float*)comb, rows);
+  return ttmi_check_launch("ttmi_user_concat_fwd");
+}
+
+extern "C" int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
+                                    const int64_t* gender, int dg, const int64_t* country, int dc,
+                                    float* dx, float* dG, float* dC, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && D > 0 && dg >= 0 && dc >= 0, "ttmi_user_concat_bwd: bad sizes");
+  TTMI_REQUIRE(dcomb && rows && gender && country && dx, "ttmi_user_concat_bwd: null argument");
+  if (B == 0) return TTMI_OK;
+  hipLaunchKernelGGL(user_concat_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, B, D, dcomb, rows,
+                     gender, dg, country, dc, dx, dG, dC);
+  return ttmi_check_launch("ttmi_user_concat_bwd");
+}
+
+extern "C" int ttmi_batchnorm_fwd(int dtype, int B, int C, const float* z, const float* w,
+                                  const float* b, float eps, float momentum, float* running_mean,
+                                  float* running_var, int64_t* num_batches_tracked, int training,
+                                  int relu, float drop_p, const uint64_t* drop_seed, void* y,
+                                  float* mean, float* rstd, hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_batchnorm_fwd: bad dtype");
+  TTMI_REQUIRE(C > 0 && B >= 0, "ttmi_batchnorm_fwd: bad sizes");
+  TTMI_REQUIRE(!training || B > 1,
+               "ttmi_batchnorm_fwd: expected more than 1 value per channel when training");
+  TTMI_REQUIRE(training || (running_mean && running_var), "ttmi_batchnorm_fwd: eval needs running stats");
+  TTMI_REQUIRE(z && w && b && y, "ttmi_batchnorm_fwd: null argument");
+  if (B == 0) return TTMI_OK;
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_batchnorm_fwd: drop_p out of [0,1)");
+  DropParams dp = make_drop(drop_p, drop_seed);
+  dim3 grid((C + 63) / 64);
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL(bn_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, C, z, w, b, eps, momentum,
+                       running_mean, running_var, num_batches_tracked, training, relu, dp, (bf16_t*)y, mean, rstd);
+  else
+    hipLaunchKernelGGL(bn_fwd_kernel<float>, grid, dim3(256), 0, s, B, C, z, w, b, eps, momentum,
+                       running_mean, running_var, num_batches_tracked, training, relu, dp, (float*)y, mean, rstd);
+  return ttmi_check_launch("ttmi_batchnorm_fwd");
+}
+
+extern "C" int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, const float* z,
+                                  const float* w, const float* mean, const float* rstd,
+                                  const void* y, float gate_scale, int gated, float* dz, float* dw,
+                                  float* db, hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_batchnorm_bwd: bad dtype");
+  TTMI_REQUIRE(B > 1 && C > 0, "ttmi_batchnorm_bwd: bad sizes");
+  TTMI_REQUIRE(dy && z && w && mean && rstd && dz && (!gated || y), "ttmi_batchnorm_bwd: null argument");
+  dim3 grid((C + 63) / 64);
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL(bn_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, C, dy, z, w, mean, rstd,
+                       (const bf16_t*)y, gate_scale, gated, dz, dw, db);
+  else
+    hipLaunchKernelGGL(bn_bwd_kernel<float>, grid, dim3(256), 0, s, B, C, dy, z, w, mean, rstd,
+                       (const float*)y, gate_scale, gated, dz, dw, db);
+  return ttmi_check_launch("ttmi_batchnorm_bwd");
+}

@@ -1,0 +1,222 @@
+// ttmi_runtime.hip — error reporting, version, elementwise helpers and the fused AdamW.
+#include <cstdarg>
+#include <cstdio>
+
+#include "ttmi_common.h"
+
+namespace {
+thread_local char g_err[512] = "";
+}
+
+void ttmi_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int ttmi_check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    ttmi_set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return TTMI_ERR_LAUNCH;
+  }
+  return TTMI_OK;
+}
+
+extern "C" const char* ttmi_last_error(void) { return g_err; }
+extern "C" int ttmi_abi_version(void) { return 1; }
+
+namespace {
+
+__global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16_t* __restrict__ dst) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 4 <= n) {
+      float4 v = *reinterpret_cast<const float4*>(src + i);
+      ushort4 o;
+      o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
+      *reinterpret_cast<ushort4*>(dst + i) = o;
+    } else {
+      for (int64_t j = i; j < n; ++j) dst[j] = f2bf(src[j]);
+    }
+  }
+}
+
+// AdamW (torch.optim.AdamW, non-amsgrad, maximize=False) over flat fp32 buffers.
+__global__ void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v,
+                             bf16_t* __restrict__ pb, const double* __restrict__ hyper,
+                             const int32_t* __restrict__ step) {
+  // scalar terms in double, as torch computes them on the host (then used as f32 scalars)
+  const double lr = hyper[0], b1d = hyper[1], b2d = hyper[2], wd = hyper[4];
+  const double t = (double)step[0];
+  const float step_size = (float)(lr / (1.0 - pow(b1d, t)));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(b2d, t));
+  const float decay = (float)(1.0 - lr * wd);
+  const float b1c = (float)(1.0 - b1d), b2 = (float)b2d, b2c = (float)(1.0 - b2d);
+  const float eps = (float)hyper[3];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 4 <= n) {
+      float4 pp = *reinterpret_cast<float4*>(p + i);
+      const float4 gg = *reinterpret_cast<const float4*>(g + i);
+      float4 mm = *reinterpret_cast<float4*>(m + i);
+      float4 vv = *reinterpret_cast<float4*>(v + i);
+      float* P = &pp.x; const float* G = &gg.x; float* Mv = &mm.x; float* Vv = &vv.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        P[k] *= decay;
+        Mv[k] += b1c * (G[k] - Mv[k]);                  // exp_avg.lerp_(grad, 1-beta1)
+        Vv[k] = Vv[k] * b2 + b2c * (G[k] * G[k]);       // exp_avg_sq.mul_(b2).addcmul_(g,g,1-b2)
+        const float denom = sqrtf(Vv[k]) / bc2_sqrt + eps;
+        P[k] -= step_size * (Mv[k] / denom);
+      }
+      *reinterpret_cast<float4*>(p + i) = pp;
+      *reinterpret_cast<float4*>(m + i) = mm;
+      *reinterpret_cast<float4*>(v + i) = vv;
+      if (pb) {
+        ushort4 o;
+        o.x = f2bf(pp.x); o.y = f2bf(pp.y); o.z = f2bf(pp.z); o.w = f2bf(pp.w);
+        *reinterpret_cast<ushort4*>(pb + i) = o;
+      }
+    } else {
+      for (int64_t j = i; j < n; ++j) {
+        float pj = p[j] * decay;
+        const float gj = g[j];
+        m[j] += b1c * (gj - m[j]);
+        v[j] = v[j] * b2 + b2c * (gj * gj);
+        pj -= step_size * (m[j] / (sqrtf(v[j]) / bc2_sqrt + eps));
+        p[j] = pj;
+        if (pb) pb[j] = f2bf(pj);
+      }
+    }
+  }
+}
+
+__global__ void step_inc_kernel(int32_t* step) { step[0] += 1; }
+
+TTMI_DEV uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// seeds[s] = splitmix64(splitmix64(base) ^ (step*64 + s)) — functional.site_seeds restates it.
+__global__ void dropout_seeds_kernel(uint64_t base, const int32_t* step, uint64_t* seeds, int n) {
+  const int s = threadIdx.x;
+  if (s < n) seeds[s] = splitmix64(splitmix64(base) ^ ((uint64_t)(int64_t)step[0] * 64ull + (uint64_t)s));
+}
+
+// dy = dropout_bwd(dx) cast to T; colsum += Σ_rows dy.  Block: 256 threads = (N/...)...
+// Each thread owns one column n (looping over a chunk of rows): coalesced along n.
+template <typename T>
+__global__ void dropout_bwd_kernel(int64_t M, int N, const float* __restrict__ dx, int64_t ldx,
+                                   DropParams d, int64_t ld_drop, T* __restrict__ dy,
+                                   int64_t ldy, float* __restrict__ colsum, int rows_per_block) {
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  const DropKeys dk = resolve_drop(d);
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t m = r0; m < r1; ++m) {
+      float v = dx[m * ldx + n];
+      if (dk.on) v = drop_keep(dk, (uint32_t)(m * ld_drop + n)) ? v * dk.scale : 0.f;
+      stf<T>(dy, m * ldy + n, v);
+      s += v;
+    }
+    if (colsum) atomicAdd(colsum + n, s);
+  }
+}
+
+template <typename T>
+__global__ void colsum_kernel(int64_t M, int N, const T* __restrict__ x, int64_t ldx,
+                              float* __restrict__ colsum, int rows_per_block) {
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t m = r0; m < r1; ++m) s += ldf<T>(x, m * ldx + n);
+    atomicAdd(colsum + n, s);
+  }
+}
+
+int grid_for(int64_t n, int per_thread) {
+  int64_t b = (n + 256 * per_thread - 1) / (256 * per_thread);
+  return (int)std::min<int64_t>(std::max<int64_t>(b, 1), 4096);
+}
+
+}  // namespace
+
+extern "C" int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && (n == 0 || (src && dst)), "ttmi_cast_f32_bf16: bad args");
+  TTMI_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0,
+               "ttmi_cast_f32_bf16: src must be 16-B and dst 8-B aligned");
+  if (n == 0) return TTMI_OK;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, n, src, dst);
+  return ttmi_check_launch("ttmi_cast_f32_bf16");
+}
+
+extern "C" int ttmi_adamw(int64_t n, float* p, const float* g, float* m, float* v,
+                          uint16_t* p_bf16, const double* hyper, const int32_t* step,
+                          hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && p && g && m && v && hyper && step, "ttmi_adamw: null argument");
+  TTMI_REQUIRE(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 &&
+               ((uintptr_t)v & 15) == 0 && ((uintptr_t)p_bf16 & 7) == 0,
+               "ttmi_adamw: buffers must be 16-B aligned (bf16 mirror 8-B)");
+  if (n == 0) return TTMI_OK;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, n, p, g, m, v, p_bf16,
+                     hyper, step);
+  return ttmi_check_launch("ttmi_adamw");
+}
+
+extern "C" int ttmi_step_inc(int32_t* step, hipStream_t s) {
+  TTMI_REQUIRE(step, "ttmi_step_inc: null step");
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  return ttmi_check_launch("ttmi_step_inc");
+}
+
+extern "C" int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int n,
+                                  hipStream_t s) {
+  TTMI_REQUIRE(step && seeds && n > 0 && n <= 256, "ttmi_dropout_seeds: bad args");
+  hipLaunchKernelGGL(dropout_seeds_kernel, dim3(1), dim3(256), 0, s, base, step, seeds, n);
+  return ttmi_check_launch("ttmi_dropout_seeds");
+}
+
+extern "C" int ttmi_dropout_bwd(int dtype, int64_t M, int N, const float* dx, int64_t ldx,
+                                float drop_p, const uint64_t* drop_seed, int64_t ld_drop, void* dy,
+                                int64_t ldy, float* colsum, hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_dropout_bwd: bad dtype");
+  TTMI_REQUIRE(M >= 0 && N > 0 && dx && dy && ldx >= N && ldy >= N, "ttmi_dropout_bwd: bad args");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_dropout_bwd: drop_p out of [0,1)");
+  TTMI_REQUIRE(drop_p == 0.f || drop_seed, "ttmi_dropout_bwd: dropout needs a seed pointer");
+  if (M == 0) return TTMI_OK;
+  const int rpb = 64;
+  dim3 grid((N + 255) / 256, (unsigned)((M + rpb - 1) / rpb));
+  DropParams d = make_drop(drop_p, drop_seed);
+  if (ld_drop == 0) ld_drop = N;
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL(dropout_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, M, N, dx, ldx, d, ld_drop,
+                       (bf16_t*)dy, ldy, colsum, rpb);
+  else
+    hipLaunchKernelGGL(dropout_bwd_kernel<float>, grid, dim3(256), 0, s, M, N, dx, ldx, d, ld_drop,
+                       (float*)dy, ldy, colsum, rpb);
+  return ttmi_check_launch("ttmi_dropout_bwd");
+}
+
+extern "C" int ttmi_colsum(int dtype, int64_t M, int N, const void* x, int64_t ldx, float* colsum,
+                           hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_colsum: bad dtype");
+  TTMI_REQUIRE(M >= 0 && N > 0 && x && colsum && ldx >= N, "ttmi_colsum: bad args");
+  if (M == 0) return TTMI_OK;
+  const int rpb = 64;
+  dim3 grid((N + 255) / 256, (unsigned)((M + rpb - 1) / rpb));
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, M, N, (const bf16_t*)x, ldx,
+                       colsum, rpb);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)x, ldx,
+                       colsum, rpb);
+  return ttmi_check_launch("ttmi_colsum");
+}

@@ -1,0 +1,388 @@
+"""Explicit forward/backward schedules of the two-tower step on libttmi kernels.
+
+This is the functional core shared by the drop-in nn.Modules (``user_tower.py``,
+``item_tower.py``, ``two_tower.py`` wrap it in autograd Functions) and the graph-captured
+``train.TrainStep``.  Each ``*_fwd`` returns its output and a state object holding what the
+matching ``*_bwd`` needs; each ``*_bwd`` ACCUMULATES parameter gradients into the fp32
+tensors of a ``grads`` dict (so a flat gradient buffer can be zeroed once per step).
+
+Parameter dicts use the reference ``state_dict`` names (without the tower prefix):
+``P`` holds the fp32 master tensors, ``W`` the GEMM operands in the compute dtype (the bf16
+mirror, or ``P`` itself in fp32 mode).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+
+Tensor = torch.Tensor
+
+# Dropout site ids (restated by oracle/two_tower_ref.py: SITE_*).
+SITE_EMB = 0
+SITE_ITEM = 63
+
+
+def site_attn(i: int) -> int:
+    return 1 + 4 * i
+
+
+def site_drop1(i: int) -> int:
+    return 2 + 4 * i
+
+
+def site_ffn(i: int) -> int:
+    return 3 + 4 * i
+
+
+def site_drop2(i: int) -> int:
+    return 4 + 4 * i
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+N_SITES = 64
+
+
+def site_seeds(base: int, step: int) -> Dict[int, int]:
+    """Per-site dropout seeds of one step; restates ttmi_dropout_seeds (device) exactly:
+    seeds[s] = splitmix64(splitmix64(base) ^ (step*64 + s))."""
+    return {s: _splitmix64(_splitmix64(base) ^ ((step * 64 + s) & 0xFFFFFFFFFFFFFFFF))
+            for s in range(N_SITES)}
+
+
+def seed_table(seeds: Dict[int, int], device) -> Tensor:
+    """Upload a site->seed dict as the int64 [N_SITES] device table the kernels read."""
+    vals = [0] * N_SITES
+    for k, v in seeds.items():
+        vals[k] = v - (1 << 64) if v >= (1 << 63) else v
+    return torch.tensor(vals, dtype=torch.int64, device=device)
+
+
+@dataclass
+class TowerCfg:
+    D: int
+    H: int = 4
+    n_layers: int = 2
+    p_drop: float = 0.0
+    dtype: torch.dtype = torch.bfloat16
+    eps: float = 1e-5
+
+
+def _drop(cfg: TowerCfg, seeds: Optional[Tensor], site: int, p: Optional[float] = None):
+    """(p, device seed view) for one dropout site; ``seeds`` is the [N_SITES] table."""
+    p = cfg.p_drop if p is None else p
+    if p <= 0.0 or seeds is None:
+        return ops.NO_DROP
+    return (p, seeds[site:site + 1])
+
+
+def _scale(p: float) -> float:
+    return 1.0 / (1.0 - p) if p > 0 else 1.0
+
+
+# ===================================================================================== user
+@dataclass
+class LayerSaved:
+    x: Tensor          # layer input (fp32 residual)
+    a1: Tensor         # LN1(x)        (compute dtype)
+    m1: Tensor
+    r1: Tensor
+    qkv: Tensor        # (compute dtype)
+    ctx: Tensor        # attention output (compute dtype)
+    lse: Tensor
+    x1: Tensor         # after attention residual (fp32)
+    a2: Tensor         # LN2(x1)
+    m2: Tensor
+    r2: Tensor
+    h: Tensor          # dropout(relu(linear1)) (compute dtype)
+
+
+@dataclass
+class UserSaved:
+    ids: Tensor
+    key_valid: Tensor
+    gender: Tensor
+    country: Tensor
+    m0: Tensor
+    r0: Tensor
+    layers: List[LayerSaved] = field(default_factory=list)
+    comb: Optional[Tensor] = None
+    rows: Optional[Tensor] = None
+    z: Optional[Tensor] = None
+    mz: Optional[Tensor] = None
+    rz: Optional[Tensor] = None
+    az: Optional[Tensor] = None
+    seeds: Optional[Tensor] = None
+
+
+def _lp(i: int) -> str:
+    return f"transformer_encoder.layers.{i}."
+
+
+def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gender: Tensor,
+                   country: Tensor, mask: Optional[Tensor], cfg: TowerCfg,
+                   seeds: Optional[Tensor] = None):
+    """SequentialUserEncoder.forward (reference user_tower.py:73-144), train mode."""
+    dev = ids.device
+    B, L = ids.shape
+    D, H, dt = cfg.D, cfg.H, cfg.dtype
+    M = B * L
+    key_valid = ids if mask is None else mask
+    if key_valid.dtype != torch.int64:
+        key_valid = key_valid.to(torch.int64)
+    f32 = dict(device=dev, dtype=torch.float32)
+    x = torch.empty(M, D, **f32)
+    m0 = torch.empty(M, **f32)
+    r0 = torch.empty(M, **f32)
+    ops.seq_embed_fwd(ids, P["item_embedding.weight"], P["position_embedding.weight"],
+                      P["layer_norm.weight"], P["layer_norm.bias"], x, m0, r0, eps=cfg.eps,
+                      drop=_drop(cfg, seeds, SITE_EMB))
+    st = UserSaved(ids=ids, key_valid=key_valid, gender=gender, country=country, m0=m0, r0=r0,
+                   seeds=seeds)
+    for i in range(cfg.n_layers):
+        pre = _lp(i)
+        a1 = torch.empty(M, D, device=dev, dtype=dt)
+        m1 = torch.empty(M, **f32)
+        r1 = torch.empty(M, **f32)
+        ops.layernorm_fwd(x, P[pre + "norm1.weight"], P[pre + "norm1.bias"], a1, m1, r1, eps=cfg.eps)
+        qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
+        ops.linear(a1, W[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"], qkv)
+        ctx = torch.empty(M, D, device=dev, dtype=dt)
+        lse = torch.empty(B * H * L, **f32)
+        ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
+        x1 = torch.empty(M, D, **f32)
+        ops.linear(ctx, W[pre + "self_attn.out_proj.weight"], P[pre + "self_attn.out_proj.bias"],
+                   x1, drop=_drop(cfg, seeds, site_drop1(i)), residual=x)
+        a2 = torch.empty(M, D, device=dev, dtype=dt)
+        m2 = torch.empty(M, **f32)
+        r2 = torch.empty(M, **f32)
+        ops.layernorm_fwd(x1, P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2, eps=cfg.eps)
+        h = torch.empty(M, W[pre + "linear1.weight"].shape[0], device=dev, dtype=dt)
+        ops.linear(a2, W[pre + "linear1.weight"], P[pre + "linear1.bias"], h, act=1,
+                   drop=_drop(cfg, seeds, site_ffn(i)))
+        x2 = torch.empty(M, D, **f32)
+        ops.linear(h, W[pre + "linear2.weight"], P[pre + "linear2.bias"], x2,
+                   drop=_drop(cfg, seeds, site_drop2(i)), residual=x1)
+        st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, x1, a2, m2, r2, h))
+        x = x2
+    G = P["gender_embedding.weight"]
+    C = P["country_embedding.weight"]
+    comb = torch.empty(B, D + G.shape[1] + C.shape[1], device=dev, dtype=dt)
+    rows = torch.empty(B, device=dev, dtype=torch.int32)
+    ops.user_concat_fwd(x, key_valid, gender, G, country, C, comb, rows, B, L)
+    z = torch.empty(B, D, **f32)
+    ops.linear(comb, W["fusion_layer.0.weight"], P["fusion_layer.0.bias"], z)
+    az = torch.empty(B, D, device=dev, dtype=dt)
+    mz = torch.empty(B, **f32)
+    rz = torch.empty(B, **f32)
+    ops.layernorm_fwd(z, P["fusion_layer.1.weight"], P["fusion_layer.1.bias"], az, mz, rz,
+                      eps=cfg.eps, relu=True)
+    u = torch.empty(B, D, **f32)
+    ops.linear(az, W["fusion_layer.3.weight"], P["fusion_layer.3.bias"], u)
+    st.comb, st.rows, st.z, st.mz, st.rz, st.az = comb, rows, z, mz, rz, az
+    return u, st
+
+
+def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du: Tensor,
+                   grads: Dict[str, Tensor], cfg: TowerCfg) -> None:
+    """Backward of user_tower_fwd; accumulates into ``grads`` (fp32, reference names)."""
+    dev = du.device
+    B, L = st.ids.shape
+    D, H, dt = cfg.D, cfg.H, cfg.dtype
+    M = B * L
+    seeds = st.seeds
+    f32 = dict(device=dev, dtype=torch.float32)
+    # ---- user fusion MLP (user_tower.py:51-57, :142)
+    du_c = torch.empty(B, D, device=dev, dtype=dt)
+    ops.dropout_bwd(du, du_c, grads["fusion_layer.3.bias"])
+    ops.linear_dw(du_c, st.az, grads["fusion_layer.3.weight"])
+    daz = torch.empty(B, D, **f32)
+    ops.linear_dx(du_c, W["fusion_layer.3.weight"], daz)
+    dz = torch.empty(B, D, **f32)
+    ops.layernorm_bwd(daz, st.z, st.mz, st.rz, P["fusion_layer.1.weight"], dz,
+                      grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"], gate=st.az)
+    dz_c = torch.empty(B, D, device=dev, dtype=dt)
+    ops.dropout_bwd(dz, dz_c, grads["fusion_layer.0.bias"])
+    ops.linear_dw(dz_c, st.comb, grads["fusion_layer.0.weight"])
+    dcomb = torch.empty(B, st.comb.shape[1], **f32)
+    ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dcomb)
+    dx = torch.zeros(M, D, **f32)
+    G = P["gender_embedding.weight"]
+    C = P["country_embedding.weight"]
+    ops.user_concat_bwd(dcomb, st.rows, st.gender, G.shape[1], st.country, C.shape[1], dx,
+                        grads["gender_embedding.weight"], grads["country_embedding.weight"])
+    # ---- encoder layers, reversed (user_tower.py:37-45)
+    p = cfg.p_drop
+    for i in reversed(range(cfg.n_layers)):
+        pre = _lp(i)
+        s = st.layers[i]
+        F = W[pre + "linear1.weight"].shape[0]
+        dy2 = torch.empty(M, D, device=dev, dtype=dt)
+        ops.dropout_bwd(dx, dy2, grads[pre + "linear2.bias"], _drop(cfg, seeds, site_drop2(i)))
+        ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"])
+        dz1 = torch.empty(M, F, device=dev, dtype=dt)
+        ops.linear_dx(dy2, W[pre + "linear2.weight"], dz1, gate=s.h, gate_scale=_scale(p),
+                      colsum=grads[pre + "linear1.bias"])
+        ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"])
+        da2 = torch.empty(M, D, **f32)
+        ops.linear_dx(dz1, W[pre + "linear1.weight"], da2)
+        dx1 = torch.empty(M, D, **f32)
+        ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
+                          grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
+        dy1 = torch.empty(M, D, device=dev, dtype=dt)
+        ops.dropout_bwd(dx1, dy1, grads[pre + "self_attn.out_proj.bias"],
+                        _drop(cfg, seeds, site_drop1(i)))
+        ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"])
+        dctx = torch.empty(M, D, device=dev, dtype=dt)
+        ops.linear_dx(dy1, W[pre + "self_attn.out_proj.weight"], dctx)
+        dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
+        ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
+                    _drop(cfg, seeds, site_attn(i)))
+        ops.colsum(dqkv, grads[pre + "self_attn.in_proj_bias"])
+        ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"])
+        da1 = torch.empty(M, D, **f32)
+        ops.linear_dx(dqkv, W[pre + "self_attn.in_proj_weight"], da1)
+        dxn = torch.empty(M, D, **f32)
+        ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
+                          grads[pre + "norm1.weight"], grads[pre + "norm1.bias"], res=dx1)
+        dx = dxn
+    # ---- input block (user_tower.py:83-93)
+    ops.seq_embed_bwd(st.ids, P["item_embedding.weight"], P["position_embedding.weight"],
+                      P["layer_norm.weight"], st.m0, st.r0, dx, grads["item_embedding.weight"],
+                      grads["position_embedding.weight"], grads["layer_norm.weight"],
+                      grads["layer_norm.bias"], drop=_drop(cfg, seeds, SITE_EMB), padding_idx=0)
+
+
+# ===================================================================================== item
+@dataclass
+class ItemSaved:
+    modal: Tensor      # fusion input in compute dtype
+    z: Tensor
+    bn_mean: Tensor
+    bn_rstd: Tensor
+    y1: Tensor
+    y2: Tensor
+    m5: Tensor
+    r5: Tensor
+    seeds: Optional[Tensor] = None
+
+
+def item_fusion_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Tensor, cfg: TowerCfg,
+                    seeds: Optional[Tensor] = None,
+                    buffers: Optional[Dict[str, Tensor]] = None, p_drop: float = 0.1,
+                    training: bool = True):
+    """MultimodalItemEncoder fusion head (reference item_tower.py:122-129, :147-150) on the
+    concatenated [audio, visual, text, tabular] embeddings ``modal`` [B, 512] (fp32)."""
+    dev = modal.device
+    B = modal.shape[0]
+    dt = cfg.dtype
+    f32 = dict(device=dev, dtype=torch.float32)
+    if dt == torch.float32:
+        m_c = modal.contiguous()
+    else:
+        m_c = ops.cast_bf16(modal.contiguous(), torch.empty(modal.shape, device=dev, dtype=dt))
+    H1 = W["fusion_layer.0.weight"].shape[0]
+    z = torch.empty(B, H1, **f32)
+    ops.linear(m_c, W["fusion_layer.0.weight"], P["fusion_layer.0.bias"], z)
+    y1 = torch.empty(B, H1, device=dev, dtype=dt)
+    bn_mean = torch.empty(H1, **f32)
+    bn_rstd = torch.empty(H1, **f32)
+    bufs = buffers or {}
+    ops.batchnorm_fwd(z, P["fusion_layer.1.weight"], P["fusion_layer.1.bias"], y1, bn_mean, bn_rstd,
+                      bufs.get("fusion_layer.1.running_mean"), bufs.get("fusion_layer.1.running_var"),
+                      bufs.get("fusion_layer.1.num_batches_tracked"), relu=True,
+                      drop=_drop(cfg, seeds, SITE_ITEM, p_drop), training=training)
+    D = W["fusion_layer.4.weight"].shape[0]
+    y2 = torch.empty(B, D, **f32)
+    ops.linear(y1, W["fusion_layer.4.weight"], P["fusion_layer.4.bias"], y2)
+    out = torch.empty(B, D, **f32)
+    m5 = torch.empty(B, **f32)
+    r5 = torch.empty(B, **f32)
+    ops.layernorm_fwd(y2, P["fusion_layer.5.weight"], P["fusion_layer.5.bias"], out, m5, r5,
+                      eps=cfg.eps)
+    return out, ItemSaved(m_c, z, bn_mean, bn_rstd, y1, y2, m5, r5, seeds)
+
+
+def item_fusion_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, dout: Tensor,
+                    grads: Dict[str, Tensor], cfg: TowerCfg, p_drop: float = 0.1,
+                    dmodal: Optional[Tensor] = None) -> None:
+    dev = dout.device
+    B, D = dout.shape
+    dt = cfg.dtype
+    f32 = dict(device=dev, dtype=torch.float32)
+    dy2 = torch.empty(B, D, **f32)
+    ops.layernorm_bwd(dout, st.y2, st.m5, st.r5, P["fusion_layer.5.weight"], dy2,
+                      grads["fusion_layer.5.weight"], grads["fusion_layer.5.bias"])
+    dy2_c = torch.empty(B, D, device=dev, dtype=dt)
+    ops.dropout_bwd(dy2, dy2_c, grads["fusion_layer.4.bias"])
+    ops.linear_dw(dy2_c, st.y1, grads["fusion_layer.4.weight"])
+    H1 = st.z.shape[1]
+    dy1 = torch.empty(B, H1, **f32)
+    ops.linear_dx(dy2_c, W["fusion_layer.4.weight"], dy1)
+    pd = p_drop if st.seeds is not None else 0.0
+    dz = torch.empty(B, H1, **f32)
+    ops.batchnorm_bwd(dy1, st.z, P["fusion_layer.1.weight"], st.bn_mean, st.bn_rstd, st.y1, dz,
+                      grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"],
+                      gate_scale=_scale(pd), gated=True)
+    dz_c = torch.empty(B, H1, device=dev, dtype=dt)
+    ops.dropout_bwd(dz, dz_c, grads["fusion_layer.0.bias"])
+    ops.linear_dw(dz_c, st.modal, grads["fusion_layer.0.weight"])
+    if dmodal is not None:
+        ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dmodal)
+
+
+# ===================================================================================== loss
+@dataclass
+class LossSaved:
+    u_hat: Tensor
+    i_hat: Tensor
+    norms: Tensor
+    logits: Tensor
+    lse: Tensor
+    user_idx: Optional[Tensor]
+    ws: Tensor
+    inv_tau: float
+
+
+def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float = 0.07):
+    """TwoTowerModel.forward loss part (reference two_tower.py:98-140)."""
+    dev = u.device
+    B, D = u.shape
+    f32 = dict(device=dev, dtype=torch.float32)
+    u_hat = torch.empty(B, D, **f32)
+    i_hat = torch.empty(B, D, **f32)
+    norms = torch.empty(2 * B, **f32)
+    logits = torch.empty(B, B, **f32)
+    lse = torch.empty(2 * B, **f32)
+    loss = torch.empty((), **f32)
+    ws = torch.empty(ops.infonce_workspace(B, D), device=dev, dtype=torch.uint8)
+    if user_idx is not None and user_idx.dtype != torch.int64:
+        user_idx = user_idx.to(torch.int64)
+    inv_tau = 1.0 / temperature
+    ops.infonce_fwd(u.contiguous(), it.contiguous(), user_idx, inv_tau, u_hat, i_hat, norms, logits,
+                    lse, loss, ws)
+    return loss, logits, u_hat, i_hat, LossSaved(u_hat, i_hat, norms, logits, lse, user_idx, ws,
+                                                 inv_tau)
+
+
+def infonce_bwd(st: LossSaved, dloss: Optional[Tensor], du: Tensor, di: Tensor) -> None:
+    ops.infonce_bwd(st.u_hat, st.i_hat, st.norms, st.logits, st.lse, st.user_idx, st.inv_tau,
+                    dloss, du, di, st.ws)
+
+
+def count_flops_user(B: int, L: int, D: int, n_layers: int, ffn: int, extra: int = 48) -> float:
+    """Dense GEMM + attention FLOPs of one fwd+bwd of the user tower (for the roofline)."""
+    M = B * L
+    per_layer = 2 * M * D * (3 * D + D + 2 * ffn) + 4 * B * L * L * D
+    fwd = n_layers * per_layer + 2 * B * (D + extra) * D + 2 * B * D * D
+    return 3.0 * fwd
+

@@ -1,0 +1,112 @@
+"""ctypes binding of libttmi.so (include/ttmi.h).
+
+The library is built in-tree (``make`` at the repo root, or ``__graft_entry__.build()``)
+into ``lib/libttmi.so`` next to this file.  ``load()`` raises if it is missing: there is no
+CPU or eager-PyTorch fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
+
+F32, BF16 = 0, 1
+ABI_VERSION = 1
+
+c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
+                               ctypes.c_void_p)
+
+
+class GemmDesc(ctypes.Structure):
+    """ttmi_gemm_desc (include/ttmi.h)."""
+    _fields_ = [
+        ("dtype", c_i),
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("A", c_p), ("lda", c_i64), ("a_kmajor", c_i),
+        ("B", c_p), ("ldb", c_i64), ("b_kmajor", c_i),
+        ("C", c_p), ("ldc", c_i64), ("c_dtype", c_i), ("c_mode", c_i),
+        ("alpha", c_f),
+        ("bias", c_p),
+        ("act", c_i),
+        ("drop_p", c_f), ("drop_seed", c_p), ("ld_drop", c_i64),
+        ("gate", c_p), ("gate_dtype", c_i), ("ld_gate", c_i64), ("gate_scale", c_f),
+        ("residual", c_p), ("ld_res", c_i64),
+        ("colsum", c_p),
+        ("split_k", c_i),
+    ]
+
+
+# name -> (restype, argtypes); mirrors include/ttmi.h one-to-one.
+SIGNATURES = {
+    "ttmi_last_error": (ctypes.c_char_p, []),
+    "ttmi_abi_version": (c_i, []),
+    "ttmi_gemm": (c_i, [ctypes.POINTER(GemmDesc), c_p]),
+    "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
+                                 c_i64, c_p, c_p, c_p]),
+    "ttmi_layernorm_bwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i, c_i64,
+                                 c_f, c_p, c_p, c_i64, c_p, c_p, c_p]),
+    "ttmi_seq_embed_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_i64, c_p, c_p, c_p, c_f, c_f, c_p, c_p,
+                                 c_p, c_p, c_p]),
+    "ttmi_seq_embed_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p,
+                                 c_p, c_p, c_p, c_i64, c_p]),
+    "ttmi_mha_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
+    "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "ttmi_user_concat_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_p,
+                                   c_p, c_p]),
+    "ttmi_user_concat_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_batchnorm_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_i, c_i,
+                                 c_f, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_batchnorm_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_i, c_p, c_p, c_p,
+                                 c_p]),
+    "ttmi_infonce_workspace": (c_i64, [c_i, c_i]),
+    "ttmi_infonce_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_infonce_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_step_inc": (c_i, [c_p, c_p]),
+    "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_p]),
+    "ttmi_cast_f32_bf16": (c_i, [c_i64, c_p, c_p, c_p]),
+    "ttmi_dropout_bwd": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_f, c_p, c_i64, c_p, c_i64, c_p, c_p]),
+    "ttmi_colsum": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_p, c_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class TTMIError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libttmi.so and bind every entry point.  Raises if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise TTMIError(
+                f"libttmi.so not found at {path}: build it with `make` at the repo root "
+                "(or __graft_entry__.build()).  There is no fallback path.")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.ttmi_abi_version()
+        if v != ABI_VERSION:
+            raise TTMIError(f"libttmi.so ABI {v} != expected {ABI_VERSION}; rebuild")
+        _lib = lib
+        return lib
+
+
+def call(name: str, *args):
+    """Invoke an entry point; raise TTMIError with ttmi_last_error() on failure."""
+    lib = _lib if _lib is not None else load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.ttmi_last_error().decode(errors="replace")
+        raise TTMIError(f"{name} failed (rc={rc}): {msg}")
+    return rc

@@ -1,0 +1,247 @@
+"""Torch-tensor wrappers over the libttmi C ABI (include/ttmi.h).
+
+Every wrapper launches on ``torch.cuda.current_stream()`` and returns immediately; none
+allocates inside the library (outputs come from the torch caching allocator), so a whole
+step can be captured into a HIP graph.  Shapes are checked here and again in C.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import lib as _L
+from .lib import BF16, F32, GemmDesc, call
+
+Tensor = torch.Tensor
+# Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
+# seed bits (a view into a per-step seed table), or None when p == 0.
+Drop = Tuple[float, Optional[Tensor]]
+NO_DROP: Drop = (0.0, None)
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def code(dtype: torch.dtype) -> int:
+    try:
+        return _DT[dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {dtype} (float32 / bfloat16)") from None
+
+
+def _p(t: Optional[Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("libttmi ops need GPU tensors")
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a_kmajor: bool,
+         ldb: int, b_kmajor: bool, ldc: int, accumulate: bool = False, alpha: float = 1.0,
+         bias: Optional[Tensor] = None, act: int = 0, drop: Drop = NO_DROP, ld_drop: int = 0,
+         gate: Optional[Tensor] = None, ld_gate: int = 0, gate_scale: float = 1.0,
+         residual: Optional[Tensor] = None, ld_res: int = 0, colsum: Optional[Tensor] = None,
+         split_k: int = 1) -> Tensor:
+    _dev(A, B, C)
+    if A.dtype != B.dtype:
+        raise TypeError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
+    d = GemmDesc()
+    d.dtype = code(A.dtype)
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kmajor = _p(A), lda, int(a_kmajor)
+    d.B, d.ldb, d.b_kmajor = _p(B), ldb, int(b_kmajor)
+    d.C, d.ldc, d.c_dtype, d.c_mode = _p(C), ldc, code(C.dtype), int(accumulate)
+    d.alpha = alpha
+    d.bias = _p(bias)
+    d.act = act
+    d.drop_p, d.drop_seed, d.ld_drop = float(drop[0]), _p(drop[1]), ld_drop
+    d.gate, d.gate_dtype, d.ld_gate, d.gate_scale = (
+        _p(gate), code(gate.dtype) if gate is not None else 0, ld_gate, gate_scale)
+    d.residual, d.ld_res = _p(residual), ld_res
+    d.colsum = _p(colsum)
+    d.split_k = split_k
+    call("ttmi_gemm", ctypes.byref(d), _s())
+    return C
+
+
+def linear(x: Tensor, w: Tensor, bias: Optional[Tensor], out: Tensor, *, act: int = 0,
+           drop: Drop = NO_DROP, residual: Optional[Tensor] = None) -> Tensor:
+    """out[M,N] = epi(x[M,K] · w[N,K]ᵀ + bias)  (nn.Linear forward)."""
+    M, K = x.shape
+    N = w.shape[0]
+    return gemm(x, w, out, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True, ldc=N,
+                bias=bias, act=act, drop=drop, ld_drop=N, residual=residual, ld_res=N)
+
+
+def linear_dx(dy: Tensor, w: Tensor, out: Tensor, *, gate: Optional[Tensor] = None,
+              gate_scale: float = 1.0, colsum: Optional[Tensor] = None) -> Tensor:
+    """out[M,K] = (dy[M,N] · w[N,K]) ⊙ gate-mask  (nn.Linear input grad)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    return gemm(dy, w, out, M, K, N, lda=N, a_kmajor=True, ldb=K, b_kmajor=False, ldc=K,
+                gate=gate, ld_gate=K, gate_scale=gate_scale, colsum=colsum)
+
+
+def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, split_k: int = 0) -> Tensor:
+    """gw[N,K] += dy[M,N]ᵀ · x[M,K]  (nn.Linear weight grad, accumulated, split-K)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    return gemm(dy, x, gw, N, K, M, lda=N, a_kmajor=False, ldb=K, b_kmajor=False, ldc=K,
+                accumulate=True, split_k=split_k)
+
+
+# ----------------------------------------------------------------------------- norms
+def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor, *,
+                  eps: float = 1e-5, relu: bool = False, drop: Drop = NO_DROP) -> Tensor:
+    _dev(x, y)
+    M, D = x.shape
+    call("ttmi_layernorm_fwd", M, D, _p(x), D, _p(w), _p(b), eps, int(relu), float(drop[0]),
+         _p(drop[1]), _p(y), code(y.dtype), D, _p(mean), _p(rstd), _s())
+    return y
+
+
+def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, dx: Tensor,
+                  dw: Optional[Tensor], db: Optional[Tensor], *, gate: Optional[Tensor] = None,
+                  gate_scale: float = 1.0, res: Optional[Tensor] = None) -> Tensor:
+    M, D = x.shape
+    call("ttmi_layernorm_bwd", M, D, _p(dy), D, _p(x), D, _p(mean), _p(rstd), _p(w), _p(gate),
+         code(gate.dtype) if gate is not None else 0, D, gate_scale, _p(res), _p(dx), D, _p(dw),
+         _p(db), _s())
+    return dx
+
+
+def seq_embed_fwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, b: Tensor, x: Tensor,
+                  mean: Tensor, rstd: Tensor, *, eps: float = 1e-5, drop: Drop = NO_DROP):
+    B, L = ids.shape
+    V, D = E.shape
+    call("ttmi_seq_embed_fwd", B, L, D, _p(ids), _p(E), V, _p(P), _p(w), _p(b), eps,
+         float(drop[0]), _p(drop[1]), _p(x), _p(mean), _p(rstd), _s())
+    return x
+
+
+def seq_embed_bwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, mean: Tensor, rstd: Tensor,
+                  dx: Tensor, dE: Tensor, dP: Tensor, dw: Tensor, db: Tensor, *,
+                  drop: Drop = NO_DROP, padding_idx: int = 0):
+    B, L = ids.shape
+    D = E.shape[1]
+    call("ttmi_seq_embed_bwd", B, L, D, _p(ids), _p(E), _p(P), _p(w), _p(mean), _p(rstd),
+         float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), _p(dw), _p(db), padding_idx, _s())
+
+
+# ----------------------------------------------------------------------------- attention
+def mha_fwd(qkv: Tensor, key_valid: Tensor, B: int, L: int, H: int, ctx: Tensor, lse: Tensor,
+            drop: Drop = NO_DROP):
+    Dh = qkv.shape[1] // (3 * H)
+    call("ttmi_mha_fwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), float(drop[0]),
+         _p(drop[1]), _p(ctx), _p(lse), _s())
+    return ctx
+
+
+def mha_bwd(qkv: Tensor, key_valid: Tensor, lse: Tensor, dctx: Tensor, B: int, L: int, H: int,
+            dqkv: Tensor, drop: Drop = NO_DROP):
+    Dh = qkv.shape[1] // (3 * H)
+    call("ttmi_mha_bwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(lse), _p(dctx),
+         float(drop[0]), _p(drop[1]), _p(dqkv), _s())
+    return dqkv
+
+
+# ----------------------------------------------------------------------------- user head
+def user_concat_fwd(x: Tensor, len_src: Tensor, gender: Tensor, G: Tensor, country: Tensor,
+                    C: Tensor, comb: Tensor, rows: Tensor, B: int, L: int):
+    D = x.shape[1]
+    call("ttmi_user_concat_fwd", code(comb.dtype), B, L, D, _p(x), _p(len_src), _p(gender), _p(G),
+         G.shape[1], _p(country), _p(C), C.shape[1], _p(comb), _p(rows), _s())
+    return comb
+
+
+def user_concat_bwd(dcomb: Tensor, rows: Tensor, gender: Tensor, dg: int, country: Tensor,
+                    dc: int, dx: Tensor, dG: Optional[Tensor], dC: Optional[Tensor]):
+    B = dcomb.shape[0]
+    D = dcomb.shape[1] - dg - dc
+    call("ttmi_user_concat_bwd", B, D, _p(dcomb), _p(rows), _p(gender), dg, _p(country), dc,
+         _p(dx), _p(dG), _p(dC), _s())
+
+
+# ----------------------------------------------------------------------------- batchnorm
+def batchnorm_fwd(z: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor,
+                  running_mean: Optional[Tensor], running_var: Optional[Tensor],
+                  num_batches: Optional[Tensor], *, eps: float = 1e-5, momentum: float = 0.1,
+                  relu: bool = True, drop: Drop = NO_DROP, training: bool = True):
+    B, C = z.shape
+    call("ttmi_batchnorm_fwd", code(y.dtype), B, C, _p(z), _p(w), _p(b), eps, momentum,
+         _p(running_mean), _p(running_var), _p(num_batches), int(training), int(relu),
+         float(drop[0]),
+         _p(drop[1]), _p(y), _p(mean), _p(rstd), _s())
+    return y
+
+
+def batchnorm_bwd(dy: Tensor, z: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, y: Tensor,
+                  dz: Tensor, dw: Tensor, db: Tensor, *, gate_scale: float = 1.0,
+                  gated: bool = True):
+    B, C = z.shape
+    call("ttmi_batchnorm_bwd", code(y.dtype), B, C, _p(dy), _p(z), _p(w), _p(mean), _p(rstd),
+         _p(y), gate_scale, int(gated), _p(dz), _p(dw), _p(db), _s())
+    return dz
+
+
+# ----------------------------------------------------------------------------- InfoNCE
+def infonce_workspace(B: int, D: int) -> int:
+    _L.load()
+    return int(_L._lib.ttmi_infonce_workspace(B, D))
+
+
+def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], inv_tau: float, u_hat: Tensor,
+                i_hat: Tensor, norms: Tensor, logits: Tensor, lse: Tensor, loss: Tensor,
+                ws: Tensor):
+    B, D = u.shape
+    call("ttmi_infonce_fwd", B, D, _p(u), _p(it), _p(user_idx), inv_tau, _p(u_hat), _p(i_hat),
+         _p(norms), _p(logits), _p(lse), _p(loss), _p(ws), _s())
+
+
+def infonce_bwd(u_hat: Tensor, i_hat: Tensor, norms: Tensor, logits: Tensor, lse: Tensor,
+                user_idx: Optional[Tensor], inv_tau: float, dloss: Optional[Tensor], du: Tensor,
+                di: Tensor, ws: Tensor):
+    B, D = u_hat.shape
+    call("ttmi_infonce_bwd", B, D, _p(u_hat), _p(i_hat), _p(norms), _p(logits), _p(lse),
+         _p(user_idx), inv_tau, _p(dloss), _p(du), _p(di), _p(ws), _s())
+
+
+# ----------------------------------------------------------------------------- misc
+def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
+          step: Tensor):
+    call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step), _s())
+
+
+def step_inc(step: Tensor):
+    call("ttmi_step_inc", _p(step), _s())
+
+
+def dropout_seeds(base: int, step: Tensor, seeds: Tensor):
+    call("ttmi_dropout_seeds", base & (2**64 - 1), _p(step), _p(seeds), seeds.numel(), _s())
+
+
+def cast_bf16(src: Tensor, dst: Tensor) -> Tensor:
+    call("ttmi_cast_f32_bf16", src.numel(), _p(src), _p(dst), _s())
+    return dst
+
+
+def dropout_bwd(dx: Tensor, dy: Tensor, colsum: Optional[Tensor], drop: Drop = NO_DROP) -> Tensor:
+    M, N = dx.shape
+    call("ttmi_dropout_bwd", code(dy.dtype), M, N, _p(dx), N, float(drop[0]), _p(drop[1]), N,
+         _p(dy), N, _p(colsum), _s())
+    return dy
+
+
+def colsum(x: Tensor, out: Tensor) -> Tensor:
+    M, N = x.shape
+    call("ttmi_colsum", code(x.dtype), M, N, _p(x), N, _p(out), _s())
+    return out

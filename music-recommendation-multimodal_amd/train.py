@@ -1,0 +1,274 @@
+"""Training drivers — drop-in for the hot loop of reference src/train.py.
+
+* ``setup_ddp`` / ``cleanup_ddp`` / ``train_one_epoch``: the reference's functions
+  (train.py:29-76) with the same signatures; ``train_one_epoch`` runs unchanged against
+  ``TwoTowerModel`` + any torch optimizer (the module path goes through autograd).
+* ``TrainStep``: the MI355X-native step.  Parameters are re-homed into one flat fp32
+  buffer (views keep the module's ``state_dict`` working), gradients land in a flat buffer
+  written directly by the kernels, AdamW is one fused kernel that also refreshes the bf16
+  GEMM-operand mirror, and the whole forward + backward + update is captured once into a
+  HIP graph and replayed per step.  Dropout seeds and the Adam step count live in device
+  memory so replays draw fresh masks and correct bias corrections.  Under
+  ``torch.distributed`` (one process per GPU, RCCL) the flat gradient is averaged with one
+  all-reduce between the backward graph and the update graph (reference DDP semantics:
+  per-rank BatchNorm statistics, averaged gradients — train.py:300).
+"""
+from __future__ import annotations
+
+import logging
+import os
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import functional as F
+from . import ops
+from .two_tower import TwoTowerModel
+from .user_tower import _gemm_names
+from .item_tower import ITEM_GEMMS
+
+Tensor = torch.Tensor
+logger = logging.getLogger(__name__)
+
+
+# ------------------------------------------------------------------ reference-shaped API
+def setup_ddp() -> int:
+    """train.py:29-35: torchrun env -> process group (RCCL via the 'nccl' backend)."""
+    if "LOCAL_RANK" in os.environ:
+        local_rank = int(os.environ["LOCAL_RANK"])
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl")
+        return local_rank
+    return 0
+
+
+def cleanup_ddp() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def train_one_epoch(model, dataloader, optimizer, device, epoch, is_main_process=True,
+                    log_interval=50):
+    """train.py:41-76 with bf16 compute: no GradScaler is needed (no fp16 overflow range)."""
+    model.train()
+    total_loss = 0.0
+    num_batches = len(dataloader)
+    for i, batch in enumerate(dataloader):
+        for k, v in batch.items():
+            if isinstance(v, torch.Tensor):
+                batch[k] = v.to(device)
+        optimizer.zero_grad(set_to_none=True)
+        loss, _, _, _ = model(batch)
+        loss.backward()
+        optimizer.step()
+        loss_val = loss.item()
+        total_loss += loss_val
+        if is_main_process and (i + 1) % log_interval == 0:
+            logger.info(f"Epoch {epoch} [{i + 1}/{num_batches}] | Loss: {loss_val:.4f}")
+        del loss, batch
+    return total_loss / max(num_batches, 1)
+
+
+# ------------------------------------------------------------------ flat parameter store
+class FlatParams:
+    """All parameters of a module in one fp32 buffer (256-byte aligned slots).
+
+    ``param.data`` is re-pointed at its slot, so the module and its state_dict keep
+    working; ``grad``, ``exp_avg``, ``exp_avg_sq`` and (optionally) a bf16 ``mirror`` share
+    the same layout.  Device-agnostic (also used by the CPU/gloo tests)."""
+
+    ALIGN = 64  # elements (256 B)
+
+    def __init__(self, module: torch.nn.Module, mirror_dtype: Optional[torch.dtype] = None):
+        self.names, self.shapes, self.offsets = [], [], []
+        params = list(module.named_parameters())
+        dev = params[0][1].device
+        off = 0
+        for n, p in params:
+            self.names.append(n)
+            self.shapes.append(tuple(p.shape))
+            self.offsets.append(off)
+            off += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.numel = off
+        self.data = torch.zeros(off, device=dev, dtype=torch.float32)
+        for (n, p), o in zip(params, self.offsets):
+            self.data[o:o + p.numel()].copy_(p.detach().reshape(-1))
+            p.data = self.data[o:o + p.numel()].view(p.shape)
+        self.grad = torch.zeros_like(self.data)
+        self.exp_avg = torch.zeros_like(self.data)
+        self.exp_avg_sq = torch.zeros_like(self.data)
+        self.mirror = None
+        if mirror_dtype is not None and mirror_dtype != torch.float32:
+            self.mirror = torch.zeros(off, device=dev, dtype=mirror_dtype)
+
+    def views(self, buf: Tensor, prefix: str = "") -> Dict[str, Tensor]:
+        out = {}
+        for n, s, o in zip(self.names, self.shapes, self.offsets):
+            if n.startswith(prefix):
+                k = 1
+                for d in s:
+                    k *= d
+                out[n[len(prefix):]] = buf[o:o + k].view(s)
+        return out
+
+
+class GradSync:
+    """Data-parallel gradient averaging over the flat buffer (reference DDP, train.py:300).
+
+    Each rank pre-scales its loss gradient by 1/world (``loss_scale``) so one SUM
+    all-reduce of the flat buffer yields the average.  The buffer is reduced in
+    ``bucket_bytes`` slices (RCCL rings run per-link bound on xGMI; 32 MiB buckets keep every
+    call well above the latency knee)."""
+
+    def __init__(self, group=None, bucket_bytes: int = 32 << 20):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.bucket = max(1, bucket_bytes // 4)
+
+    @property
+    def loss_scale(self) -> float:
+        return 1.0 / self.world
+
+    def __call__(self, flat_grad: Tensor) -> None:
+        if self.world == 1:
+            return
+        n = flat_grad.numel()
+        for s in range(0, n, self.bucket):
+            dist.all_reduce(flat_grad[s:s + self.bucket], op=dist.ReduceOp.SUM, group=self.group)
+
+
+# ------------------------------------------------------------------ the fused step
+class TrainStep:
+    """Fused, graph-captured training step for ``TwoTowerModel`` (cfg-2 item inputs).
+
+    ``step(batch)`` stages the batch into static device buffers, replays the captured
+    forward+backward(+update) graph and returns the device loss tensor (no host sync)."""
+
+    INPUT_KEYS = ("history_ids", "history_mask", "user_gender", "user_country", "user_idx",
+                  "target_modal")
+
+    def __init__(self, model: TwoTowerModel, lr: float = 1e-4, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.01, use_graph: bool = True,
+                 seed: int = 0, group=None):
+        self.model = model
+        model.train()
+        dev = next(model.parameters()).device
+        self.device = dev
+        self.ucfg = model.user_tower.cfg()
+        self.icfg = model.item_tower.cfg()
+        self.p_item = model.item_tower.fusion_layer[3].p
+        self.dtype = self.ucfg.dtype
+        self.flat = FlatParams(model, self.dtype)
+        self.sync = GradSync(group)
+        self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay],
+                                  dtype=torch.float64, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.seeds = torch.zeros(F.N_SITES, dtype=torch.int64, device=dev)
+        self.base_seed = seed & ((1 << 63) - 1)
+        self.dloss = torch.full((1,), self.sync.loss_scale, dtype=torch.float32, device=dev)
+        self.Pu = self.flat.views(self.flat.data, "user_tower.")
+        self.Pi = self.flat.views(self.flat.data, "item_tower.")
+        self.Gu = self.flat.views(self.flat.grad, "user_tower.")
+        self.Gi = self.flat.views(self.flat.grad, "item_tower.")
+        if self.flat.mirror is not None:
+            Mu = self.flat.views(self.flat.mirror, "user_tower.")
+            Mi = self.flat.views(self.flat.mirror, "item_tower.")
+            self.Wu = dict(self.Pu)
+            self.Wu.update({n: Mu[n] for n in _gemm_names(list(self.Pu))})
+            self.Wi = dict(self.Pi)
+            self.Wi.update({n: Mi[n] for n in ITEM_GEMMS})
+        else:
+            self.Wu, self.Wi = self.Pu, self.Pi
+        self.bufs = {k[len("item_tower."):]: v for k, v in model.named_buffers()
+                     if k.startswith("item_tower.")}
+        self.sync_mirror()
+        self.use_graph = use_graph
+        self.static: Optional[Dict[str, Tensor]] = None
+        self.graph_fb = None      # forward + backward (+ update when world == 1)
+        self.graph_up = None      # update (world > 1)
+        self.loss: Optional[Tensor] = None
+        self.logits: Optional[Tensor] = None
+
+    # ---------------------------------------------------------------- pieces
+    def sync_mirror(self) -> None:
+        """Refresh the bf16 operand mirror from the fp32 masters (call after external
+        parameter edits, e.g. load_state_dict)."""
+        if self.flat.mirror is not None:
+            ops.cast_bf16(self.flat.data, self.flat.mirror)
+
+    def _fwd_bwd(self, b: Dict[str, Tensor]) -> None:
+        self.flat.grad.zero_()
+        ops.step_inc(self.step_t)
+        seeds = None
+        if self.ucfg.p_drop > 0 or self.p_item > 0:
+            ops.dropout_seeds(self.base_seed, self.step_t, self.seeds)
+            seeds = self.seeds
+        u, ust = F.user_tower_fwd(self.Pu, self.Wu, b["history_ids"], b["user_gender"],
+                                  b["user_country"], b.get("history_mask"), self.ucfg, seeds)
+        it, ist = F.item_fusion_fwd(self.Pi, self.Wi, b["target_modal"], self.icfg, seeds,
+                                    self.bufs, self.p_item)
+        loss, logits, _, _, lst = F.infonce_fwd(u, it, b.get("user_idx"),
+                                                self.model.temperature)
+        du = torch.empty_like(u)
+        di = torch.empty_like(it)
+        F.infonce_bwd(lst, self.dloss, du, di)
+        F.item_fusion_bwd(self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item)
+        F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg)
+        self.loss, self.logits = loss, logits
+
+    def _update(self) -> None:
+        f = self.flat
+        ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t)
+
+    def _body(self, b: Dict[str, Tensor]) -> None:
+        self._fwd_bwd(b)
+        if self.sync.world == 1:
+            self._update()
+
+    # ---------------------------------------------------------------- capture
+    def _stage(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        if self.static is None:
+            self.static = {k: torch.empty_like(batch[k], device=self.device)
+                           for k in self.INPUT_KEYS if k in batch}
+        for k, t in self.static.items():
+            t.copy_(batch[k], non_blocking=True)
+        return self.static
+
+    def _state(self):
+        return [self.flat.data, self.flat.exp_avg, self.flat.exp_avg_sq, self.step_t,
+                *self.bufs.values()] + ([self.flat.mirror] if self.flat.mirror is not None else [])
+
+    def _capture(self, b: Dict[str, Tensor]) -> None:
+        snap = [t.clone() for t in self._state()]
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):          # warm-up: load code objects, size the pool
+            self._fwd_bwd(b)
+            self._update()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        for t, s in zip(self._state(), snap):   # undo the warm-up's state changes
+            t.copy_(s)
+        torch.cuda.synchronize(self.device)
+        self.graph_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_fb):
+            self._body(b)
+        if self.sync.world > 1:
+            self.graph_up = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_up):
+                self._update()
+
+    def step(self, batch: Dict[str, Tensor]) -> Tensor:
+        b = self._stage(batch)
+        if not self.use_graph:
+            self._fwd_bwd(b)
+            self.sync(self.flat.grad)
+            self._update()
+            return self.loss
+        if self.graph_fb is None:
+            self._capture(b)
+        self.graph_fb.replay()
+        if self.sync.world > 1:
+            self.sync(self.flat.grad)
+            self.graph_up.replay()
+        return self.loss

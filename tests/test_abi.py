@@ -1,0 +1,77 @@
+"""CPU checks of the drop-in boundary: libttmi.so loads and exports every entry point that
+include/ttmi.h declares, the ctypes table matches the header, and argument validation
+rejects bad shapes before any launch (no GPU needed for these)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "ttmi.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ttmi_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    fns = header_functions()
+    assert "ttmi_gemm" in fns and "ttmi_mha_fwd" in fns and "ttmi_adamw" in fns
+    assert len(fns) >= 20
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = pkg.lib.load()
+    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_ctypes_table_covers_header(pkg):
+    assert sorted(pkg.lib.SIGNATURES) == header_functions()
+
+
+def test_abi_version_and_error_path(pkg):
+    lib = pkg.lib.load()
+    assert lib.ttmi_abi_version() == pkg.lib.ABI_VERSION
+    # invalid shapes are rejected before launch, with a message
+    with pytest.raises(pkg.lib.TTMIError, match="L <= 64"):
+        pkg.lib.call("ttmi_mha_fwd", 1, 2, 65, 4, 32, ctypes.c_void_p(16), ctypes.c_void_p(16),
+                     0.0, None, ctypes.c_void_p(16), ctypes.c_void_p(16), None)
+    with pytest.raises(pkg.lib.TTMIError, match="more than 1 value"):
+        pkg.lib.call("ttmi_batchnorm_fwd", 1, 1, 8, ctypes.c_void_p(16), ctypes.c_void_p(16),
+                     ctypes.c_void_p(16), 1e-5, 0.1, None, None, None, 1, 1, 0.0, None,
+                     ctypes.c_void_p(16), None, None, None)
+    d = pkg.lib.GemmDesc()
+    d.dtype, d.M, d.N, d.K = 1, 64, 64, 60          # k-major bf16 needs K % 8 == 0
+    d.A = d.B = d.C = 256
+    d.lda, d.ldb, d.ldc = 64, 64, 64
+    d.a_kmajor = d.b_kmajor = 1
+    d.split_k = 1
+    with pytest.raises(pkg.lib.TTMIError, match="K %"):
+        pkg.lib.call("ttmi_gemm", ctypes.byref(d), None)
+
+
+def test_missing_library_fails_loudly(pkg, tmp_path):
+    with pytest.raises(pkg.lib.TTMIError, match="not found"):
+        _load_fresh(pkg, str(tmp_path / "nope.so"))
+
+
+def _load_fresh(pkg, path):
+    saved = pkg.lib._lib
+    pkg.lib._lib = None
+    try:
+        return pkg.lib.load(path)
+    finally:
+        pkg.lib._lib = saved
+
+
+def test_seed_derivation_matches_device_formula(pkg):
+    F = pkg.functional
+    s = F.site_seeds(1234, 7)
+    assert len(s) == F.N_SITES and len(set(s.values())) == F.N_SITES
+    t = F.seed_table(s, "cpu")
+    assert t.dtype.is_floating_point is False and t.numel() == F.N_SITES

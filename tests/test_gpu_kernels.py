@@ -1,0 +1,306 @@
+"""Kernel-level parity of libttmi against fp32 PyTorch / the oracle (GPU only).
+
+Tolerances: fp32 paths 2e-5 relative to the tensor's max-abs (the f32 MFMA is an exact fma
+chain; only summation order differs); bf16 GEMMs are checked against an fp32 matmul of the
+SAME bf16-rounded operands, which they match to fp32 accumulation error.  Dropout masks are
+checked element-for-element against the oracle's restatement of the kernels' hash."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as TF
+
+from oracle import two_tower_ref as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def seed_dev(val):
+    v = val - (1 << 64) if val >= (1 << 63) else val
+    return torch.tensor([v], dtype=torch.int64, device=DEV)
+
+
+def keep_mask(seed, shape, p):
+    return torch.from_numpy(ref.hash_keep(seed, int(np.prod(shape)), p).reshape(shape))
+
+
+# ------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (104, 72, 176), (520, 136, 200),
+                                   (64, 64, 4096), (25600, 128, 128)])
+def test_gemm_layouts(gpu_pkg, dtype, ak, bk, M, N, K):
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g).to(dtype)
+    B = torch.randn(N, K, generator=g).to(dtype)
+    expect = A.float() @ B.float().t()
+    As = (A if ak else A.t().contiguous()).to(DEV)
+    Bs = (B if bk else B.t().contiguous()).to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(As, Bs, C, M, N, K, lda=K if ak else M, a_kmajor=ak, ldb=K if bk else N,
+             b_kmajor=bk, ldc=N)
+    assert rel(C, expect) < 2e-5 * max(1.0, math.sqrt(K / 256))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogue(gpu_pkg, dtype):
+    ops = gpu_pkg.ops
+    M, N, K = 300, 192, 96
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(M, K, generator=g).to(dtype)
+    W = torch.randn(N, K, generator=g).to(dtype)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    gate = torch.randn(M, N, generator=g).to(dtype)
+    p, seed = 0.25, 0xDEADBEEF12345
+    keep = keep_mask(seed, (M, N), p).float()
+    v = torch.relu(A.float() @ W.float().t() * 0.5 + bias) * keep / (1 - p)
+    v = torch.where(gate.float() > 0, v * 3.0, torch.zeros_like(v))
+    expect_cs = v.sum(0)
+    expect = v + res
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    cs = torch.zeros(N, device=DEV)
+    ops.gemm(A.to(DEV), W.to(DEV), C, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True,
+             ldc=N, alpha=0.5, bias=bias.to(DEV), act=1, drop=(p, seed_dev(seed)), ld_drop=N,
+             gate=gate.to(DEV), ld_gate=N, gate_scale=3.0, residual=res.to(DEV), ld_res=N,
+             colsum=cs)
+    assert rel(C, expect) < 2e-5
+    assert rel(cs, expect_cs) < 2e-5
+    # bf16 output rounding
+    Cb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(A.to(DEV), W.to(DEV), Cb, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True,
+             ldc=N, bias=bias.to(DEV))
+    assert rel(Cb.float(), A.float() @ W.float().t() + bias) < 8e-3
+
+
+@pytest.mark.parametrize("split", [0, 1, 7])
+def test_gemm_accumulate_split_k(gpu_pkg, split):
+    ops = gpu_pkg.ops
+    M, N, K = 384, 128, 25600                      # weight-gradient shape (dWin)
+    g = torch.Generator().manual_seed(5)
+    dy = torch.randn(K, M, generator=g).to(torch.bfloat16)   # [tokens, out]
+    x = torch.randn(K, N, generator=g).to(torch.bfloat16)    # [tokens, in]
+    gw = torch.ones(M, N, device=DEV)
+    ops.linear_dw(dy.to(DEV), x.to(DEV), gw, split_k=split)
+    expect = 1.0 + dy.float().t() @ x.float()
+    assert rel(gw, expect) < 5e-5
+
+
+# ------------------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("D", [32, 128, 176, 512])
+@pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
+def test_layernorm_fwd_bwd(gpu_pkg, D, ydt):
+    ops = gpu_pkg.ops
+    M = 333
+    g = torch.Generator().manual_seed(D)
+    x = torch.randn(M, D, generator=g) * 3 + 1
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    p, seed = 0.1, 42
+    keep = keep_mask(seed, (M, D), p).float()
+    xt = x.clone().requires_grad_(True)
+    wt = w.clone().requires_grad_(True)
+    bt = b.clone().requires_grad_(True)
+    y_ref = torch.relu(TF.layer_norm(xt, (D,), wt, bt, 1e-5)) * keep / (1 - p)
+    y = torch.empty(M, D, device=DEV, dtype=ydt)
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    xd = x.to(DEV)
+    ops.layernorm_fwd(xd, w.to(DEV), b.to(DEV), y, mean, rstd, relu=True, drop=(p, seed_dev(seed)))
+    assert rel(y.float(), y_ref) < (2e-5 if ydt == torch.float32 else 8e-3)
+    dy = torch.randn(M, D, generator=g)
+    res = torch.randn(M, D, generator=g)
+    y_ref.backward(dy)
+    dx = torch.empty(M, D, device=DEV)
+    dw = torch.zeros(D, device=DEV)
+    db = torch.zeros(D, device=DEV)
+    # gate with the fp32 output so the mask is exact in both dtypes
+    yg = torch.empty(M, D, device=DEV)
+    ops.layernorm_fwd(xd, w.to(DEV), b.to(DEV), yg, mean, rstd, relu=True, drop=(p, seed_dev(seed)))
+    ops.layernorm_bwd(dy.to(DEV), xd, mean, rstd, w.to(DEV), dx, dw, db, gate=yg,
+                      gate_scale=1 / (1 - p), res=res.to(DEV))
+    assert rel(dx, xt.grad + res) < 5e-5
+    assert rel(dw, wt.grad) < 5e-5
+    assert rel(db, bt.grad) < 5e-5
+
+
+# ------------------------------------------------------------------------------ attention
+def attn_ref(qkv, kv, B, L, H, p, seed):
+    D = qkv.shape[1] // 3
+    dh = D // H
+    q, k, v = qkv.float().reshape(B, L, 3, H, dh).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    allowed = torch.ones(L, L, dtype=torch.bool).tril()[None, None] & (kv != 0)[:, None, None, :]
+    row_any = allowed.any(-1, keepdim=True)
+    s = s.masked_fill(~allowed, float("-inf")).masked_fill(~row_any, 0.0)
+    lse = torch.logsumexp(s, -1).masked_fill(~row_any[..., 0], float("inf"))
+    prob = torch.softmax(s, -1) * row_any
+    if p > 0:
+        prob = prob * keep_mask(seed, (B, H, L, L), p).float() / (1 - p)
+    o = (prob @ v).transpose(1, 2).reshape(B * L, D)
+    return o, lse.reshape(-1)
+
+
+def masks(B, L, g):
+    lengths = torch.randint(1, L + 1, (B,), generator=g)
+    lengths[0] = L
+    lengths[1 % B] = 0
+    m = (torch.arange(L)[None] < lengths[:, None]).long()
+    if B > 2:
+        m[2] = m[2].flip(0)            # left-padded row
+    return m
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (3, 1, 4, 16)])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(B * L + Dh)
+    D = H * Dh
+    qkv = (torch.randn(B * L, 3 * D, generator=g) * 1.5).to(dtype)
+    kv = masks(B, L, g)
+    seed = 0x1234567890ABCDEF
+    qt = qkv.float().clone().requires_grad_(True)
+    o_ref, lse_ref = attn_ref(qt, kv, B, L, H, p, seed)
+    ctx = torch.empty(B * L, D, device=DEV, dtype=dtype)
+    lse = torch.empty(B * H * L, device=DEV)
+    sd = seed_dev(seed)
+    ops.mha_fwd(qkv.to(DEV), kv.to(DEV), B, L, H, ctx, lse, (p, sd))
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert rel(ctx.float(), o_ref) < tol
+    fin = torch.isfinite(lse_ref)
+    assert torch.equal(torch.isfinite(lse.cpu()), fin)
+    assert rel(lse.cpu()[fin], lse_ref[fin]) < (2e-6 if dtype == torch.float32 else 1e-2)
+    dctx = torch.randn(B * L, D, generator=g).to(dtype)
+    o_ref.backward(dctx.float())
+    dqkv = torch.empty(B * L, 3 * D, device=DEV, dtype=dtype)
+    ops.mha_bwd(qkv.to(DEV), kv.to(DEV), lse, dctx.to(DEV), B, L, H, dqkv, (p, sd))
+    assert rel(dqkv.float(), qt.grad) < (5e-5 if dtype == torch.float32 else 3e-2)
+
+
+# ------------------------------------------------------------------------------ embedding
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_seq_embed_fwd_bwd(gpu_pkg, p):
+    ops = gpu_pkg.ops
+    B, L, D, V = 37, 50, 128, 301
+    g = torch.Generator().manual_seed(9)
+    ids = torch.randint(0, V, (B, L), generator=g)
+    E = torch.randn(V, D, generator=g)
+    P = torch.randn(L, D, generator=g)
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    seed = 77
+    Et, Pt, wt, bt = (t.clone().requires_grad_(True) for t in (E, P, w, b))
+    x_ref = TF.layer_norm(TF.embedding(ids, Et, padding_idx=0) + Pt[None], (D,), wt, bt, 1e-5)
+    if p > 0:
+        x_ref = x_ref * keep_mask(seed, (B * L, D), p).float().reshape(B, L, D) / (1 - p)
+    x = torch.empty(B * L, D, device=DEV)
+    mean = torch.empty(B * L, device=DEV)
+    rstd = torch.empty(B * L, device=DEV)
+    Ed, Pd, wd, bd = (t.to(DEV) for t in (E, P, w, b))
+    sd = seed_dev(seed)
+    ops.seq_embed_fwd(ids.to(DEV), Ed, Pd, wd, bd, x, mean, rstd, drop=(p, sd))
+    assert rel(x, x_ref.reshape(B * L, D)) < 2e-5
+    dx = torch.randn(B * L, D, generator=g)
+    x_ref.reshape(B * L, D).backward(dx)
+    dE = torch.zeros(V, D, device=DEV)
+    dP = torch.zeros(L, D, device=DEV)
+    dw = torch.zeros(D, device=DEV)
+    db = torch.zeros(D, device=DEV)
+    ops.seq_embed_bwd(ids.to(DEV), Ed, Pd, wd, mean, rstd, dx.to(DEV), dE, dP, dw, db,
+                      drop=(p, sd), padding_idx=0)
+    assert rel(dE, Et.grad) < 5e-5
+    assert dE[0].abs().max().item() == 0.0
+    assert rel(dP, Pt.grad) < 5e-5
+    assert rel(dw, wt.grad) < 5e-5
+    assert rel(db, bt.grad) < 5e-5
+
+
+# ------------------------------------------------------------------------------ batchnorm
+@pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
+def test_batchnorm_train_eval(gpu_pkg, ydt):
+    ops = gpu_pkg.ops
+    B, C = 96, 200
+    g = torch.Generator().manual_seed(3)
+    z = torch.randn(B, C, generator=g) * 2 + 0.5
+    w = torch.randn(C, generator=g)
+    b = torch.randn(C, generator=g)
+    p, seed = 0.1, 99
+    bn = torch.nn.BatchNorm1d(C)
+    bn.weight.data.copy_(w)
+    bn.bias.data.copy_(b)
+    zt = z.clone().requires_grad_(True)
+    keep = keep_mask(seed, (B, C), p).float()
+    y_ref = torch.relu(bn(zt)) * keep / (1 - p)
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    y = torch.empty(B, C, device=DEV, dtype=ydt)
+    mean = torch.empty(C, device=DEV)
+    rstd = torch.empty(C, device=DEV)
+    zd = z.to(DEV)
+    ops.batchnorm_fwd(zd, w.to(DEV), b.to(DEV), y, mean, rstd, rm, rv, nbt, relu=True,
+                      drop=(p, seed_dev(seed)))
+    assert rel(y.float(), y_ref) < (2e-5 if ydt == torch.float32 else 8e-3)
+    assert rel(rm, bn.running_mean) < 2e-5 and rel(rv, bn.running_var) < 2e-5
+    assert int(nbt) == 1
+    dy = torch.randn(B, C, generator=g)
+    y_ref.backward(dy)
+    yf = torch.empty(B, C, device=DEV)
+    ops.batchnorm_fwd(zd, w.to(DEV), b.to(DEV), yf, mean, rstd, None, None, None, relu=True,
+                      drop=(p, seed_dev(seed)))
+    dz = torch.empty(B, C, device=DEV)
+    dw = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    ops.batchnorm_bwd(dy.to(DEV), zd, w.to(DEV), mean, rstd, yf, dz, dw, db, gate_scale=1 / (1 - p))
+    assert rel(dz, zt.grad) < 5e-5
+    assert rel(dw, bn.weight.grad) < 5e-5 and rel(db, bn.bias.grad) < 5e-5
+    # eval: running statistics
+    bn.eval()
+    ye = torch.empty(B, C, device=DEV)
+    ops.batchnorm_fwd(zd, w.to(DEV), b.to(DEV), ye, None, None, rm, rv, None, relu=False,
+                      training=False)
+    assert rel(ye, bn(z).detach()) < 2e-5
+
+
+# ------------------------------------------------------------------------------ AdamW
+def test_adamw_matches_torch_semantics(gpu_pkg):
+    ops = gpu_pkg.ops
+    n = 10007
+    g = torch.Generator().manual_seed(11)
+    p0 = torch.randn(n, generator=g)
+    params = {"w": p0.clone()}
+    state = {}
+    pd = p0.clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    mirror = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.01], dtype=torch.float64, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for _ in range(5):
+        gr = torch.randn(n, generator=g)
+        ref.adamw_(params, {"w": gr}, state, lr=1e-3)
+        ops.step_inc(step)
+        ops.adamw(pd, gr.to(DEV), m, v, mirror, hyper, step)
+    assert rel(pd, params["w"]) < 2e-6
+    assert torch.equal(mirror.cpu(), pd.cpu().to(torch.bfloat16))
+    assert int(step) == 5
+
+
+def test_dropout_seed_kernel_matches_host(gpu_pkg):
+    F = gpu_pkg.functional
+    step = torch.tensor([12], dtype=torch.int32, device=DEV)
+    seeds = torch.zeros(F.N_SITES, dtype=torch.int64, device=DEV)
+    gpu_pkg.ops.dropout_seeds(0xABCDEF, step, seeds)
+    host = F.seed_table(F.site_seeds(0xABCDEF, 12), "cpu")
+    assert torch.equal(seeds.cpu(), host)
