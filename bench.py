@@ -160,14 +160,17 @@ def main():
     step = pkg.TrainStep(model, lr=1e-4, use_graph=not args.no_graph, seed=rank + 1)
     batches = synthetic_batches(4, B, seed=rank, device=device)
 
-    for i in range(args.warmup):
-        step.step(batches[i % len(batches)])
+    # warm-up runs the exact timed-loop ops (incl. the loss accumulation: torch loads its
+    # kernels lazily, and a first-use load inside the timed region costs ~75 ms)
+    loss_sum = torch.zeros((), device=device)
+    for i in range(max(args.warmup, 1)):
+        loss_sum += step.step(batches[i % len(batches)])
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
+    loss_sum.zero_()
     t0 = time.perf_counter()
-    loss_sum = torch.zeros((), device=device)
     for i in range(args.steps):
         loss_sum += step.step(batches[i % len(batches)])
     torch.cuda.synchronize(device)

@@ -1,20 +1,31 @@
 // ttmi_gemm.hip — MFMA GEMM with fused epilogue for every nn.Linear on the hot path.
 //
-// C[m,n] = epi(alpha * Σ_k A(m,k) B(n,k)).  One 256-thread workgroup (4 waves, 2x2)
-// owns a BM x BN tile; each wave a (BM/2) x (BN/2) block of 16x16 MFMA tiles.  K is
-// walked in 128-byte tiles (64 bf16 / 32 f32) staged through LDS as [row][k] with a
-// 144-byte row pitch (16-byte pad: the 16 rows one ds_read_b128 lane-group touches land on
-// distinct 4-bank slots).  A k-major operand is copied 16 B per lane; a non-k-major one
-// (the weight-gradient operands dYᵀ and Xᵀ, or Wᵀ for dX = dY·W) is loaded 16 B along m/n
-// and transposed on the LDS write.  The next K-tile is prefetched into registers while
-// the current one feeds the MFMAs (register double-buffering, two barriers per K-tile).
+// C[m,n] = epi(alpha * Σ_k A(m,k) B(n,k)).  One 256-thread workgroup (4 waves, 2x2) owns
+// a BM x BN tile, each wave a (BM/2) x (BN/2) block of 16x16 MFMA tiles.  K is walked in
+// 128-byte tiles (64 bf16 / 32 f32), double-buffered in LDS with register prefetch (one
+// barrier per K-tile).
+//
+// Operand staging (bf16):
+//   k-major operand  -> LDS [row][k], 144-byte pitch, fragments by two ds_read_b64;
+//   row-major operand (the weight-gradient operands dYᵀ / Xᵀ and the Wᵀ of dX = dY·W)
+//                    -> LDS [k][row] exactly as it sits in HBM (16-byte copies, no
+//                       transpose), fragments by two ds_read_b64_tr_b16 (gfx950 transpose
+//                       read), pitch = rowbytes + 32 so the 8 k-rows a 32-lane half reads
+//                       land in disjoint 8-bank windows.
+//   Both read paths feed the 16x16x32 MFMA the same k-permutation (lane group g holds
+//   k = 4g..4g+3 and 16+4g..16+4g+3 of each 32-wide chunk), which is what makes both
+//   conflict-free.  fp32 operands use the 16x16x4 f32 MFMA; a row-major fp32 operand is
+//   transposed on its LDS write.
+// The MFMA is issued with the B tile as its row operand, so each lane ends up holding four
+// CONSECUTIVE output columns of one row: the epilogue reads bias/gate/residual and writes C
+// with 8-byte (bf16) / 16-byte (f32) vector accesses.
 //
 // Epilogue order (ttmi.h): bias -> act -> dropout -> gate -> colsum -> residual -> store.
 #include "ttmi_common.h"
 
 namespace {
 
-constexpr int ROWB = 144;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 
 struct GemmArgs {
   int64_t M, N, K;
@@ -28,13 +39,25 @@ struct GemmArgs {
   const float* residual; int64_t ld_res;
   float* colsum;
   int64_t k_split;   // K elements per split (multiple of the K tile)
+  int vec;           // 1: all row strides allow 4-wide vector epilogue accesses
 };
 
+TTMI_DEV uint2 lds8(const char* p) { return *reinterpret_cast<const uint2*>(p); }
+TTMI_DEV uint2 lds_tr8(const char* p) {
+  const s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4_t*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
+// One operand's K-tile: global -> registers -> LDS, and LDS -> MFMA fragments.
 template <typename T, int ROWS, bool KMAJ>
-struct TileLoader {
-  static constexpr int E = 16 / sizeof(T);
-  static constexpr int BKE = 128 / sizeof(T);
-  static constexpr int PER = ROWS / 32;           // 16-byte chunks per thread
+struct Operand {
+  static constexpr int E = 16 / sizeof(T);            // elements per 16-byte chunk
+  static constexpr int BKE = 128 / sizeof(T);         // k per tile
+  static constexpr bool TR = !KMAJ && sizeof(T) == 2; // natural [k][row] image + tr reads
+  static constexpr int PITCH = TR ? ROWS * 2 + 32 : 144;
+  static constexpr int BYTES = TR ? BKE * PITCH : ROWS * 144;
+  static constexpr int PER = ROWS / 32;               // 16-byte chunks per thread
   uint4 r[PER];
 
   TTMI_DEV void load(const char* base, int64_t ld, int64_t row0, int64_t nrows, int64_t k0,
@@ -47,7 +70,7 @@ struct TileLoader {
         row = row0 + (idx >> 3);
         k = k0 + (idx & 7) * E;
       } else {
-        constexpr int CPR = ROWS / E;               // chunks per k-row
+        constexpr int CPR = ROWS / E;
         k = k0 + idx / CPR;
         row = row0 + (idx % CPR) * E;
       }
@@ -65,28 +88,49 @@ struct TileLoader {
     for (int c = 0; c < PER; ++c) {
       const int idx = tid + c * 256;
       if constexpr (KMAJ) {
-        *reinterpret_cast<uint4*>(s + (idx >> 3) * ROWB + (idx & 7) * 16) = r[c];
-      } else {
+        *reinterpret_cast<uint4*>(s + (idx >> 3) * PITCH + (idx & 7) * 16) = r[c];
+      } else if constexpr (TR) {
+        constexpr int CPR = ROWS / E;
+        *reinterpret_cast<uint4*>(s + (idx / CPR) * PITCH + (idx % CPR) * 16) = r[c];
+      } else {                                         // f32 row-major: transpose on write
         constexpr int CPR = ROWS / E;
         const int kk = idx / CPR;
         const int rr = (idx % CPR) * E;
         const T* v = reinterpret_cast<const T*>(&r[c]);
 #pragma unroll
         for (int e = 0; e < E; ++e)
-          *reinterpret_cast<T*>(s + (rr + e) * ROWB + kk * (int)sizeof(T)) = v[e];
+          *reinterpret_cast<T*>(s + (rr + e) * PITCH + kk * (int)sizeof(T)) = v[e];
       }
+    }
+  }
+
+  // Fragment of the 16-row tile starting at `row0` for 64-byte k-chunk `c`.
+  TTMI_DEV uint4 frag(const char* s, int row0, int c, int lane) const {
+    const int i = lane & 15, g = lane >> 4;
+    if constexpr (sizeof(T) == 4) {
+      return lds16(s + (row0 + i) * PITCH + c * 64 + g * 16);
+    } else if constexpr (!TR) {
+      const char* p = s + (row0 + i) * PITCH + c * 64 + g * 8;
+      const uint2 lo = lds8(p), hi = lds8(p + 32);
+      return make_uint4(lo.x, lo.y, hi.x, hi.y);
+    } else {
+      const int q = i >> 2, pp = i & 3;
+      const char* p = s + (c * 32 + 4 * g + q) * PITCH + (row0 + 4 * pp) * 2;
+      const uint2 lo = lds_tr8(p), hi = lds_tr8(p + 16 * PITCH);
+      return make_uint4(lo.x, lo.y, hi.x, hi.y);
     }
   }
 };
 
 template <typename T, int BM, int BN, bool AK, bool BKM>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  using OA = Operand<T, BM, AK>;
+  using OB = Operand<T, BN, BKM>;
   constexpr int BKE = 128 / sizeof(T);
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  __shared__ __attribute__((aligned(16))) char smem[(BM + BN) * ROWB];
-  char* sA = smem;
-  char* sB = smem + BM * ROWB;
+  constexpr int STAGE = OA::BYTES + OB::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -104,75 +148,122 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  TileLoader<T, BM, AK> la;
-  TileLoader<T, BN, BKM> lb;
+  OA la;
+  OB lb;
   if (kbeg < kend) {
     la.load(g.A, g.lda, m0, g.M, kbeg, kend, tid);
     lb.load(g.B, g.ldb, n0, g.N, kbeg, kend, tid);
-    la.store(sA, tid);
-    lb.store(sB, tid);
+    la.store(smem, tid);
+    lb.store(smem + OA::BYTES, tid);
   }
   __syncthreads();
 
-  const int arow = wm * WTM + (lane & 15);
-  const int brow = wn * WTN + (lane & 15);
-  const int kq = (lane >> 4) * 16;
+  int buf = 0;
   for (int64_t k0 = kbeg; k0 < kend; k0 += BKE) {
     const bool more = k0 + BKE < kend;
     if (more) {
       la.load(g.A, g.lda, m0, g.M, k0 + BKE, kend, tid);
       lb.load(g.B, g.ldb, n0, g.N, k0 + BKE, kend, tid);
     }
+    const char* sA = smem + buf * STAGE;
+    const char* sB = sA + OA::BYTES;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       uint4 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = lds16(sA + (arow + i * 16) * ROWB + c * 64 + kq);
+      for (int i = 0; i < TM; ++i) af[i] = la.frag(sA, wm * WTM + i * 16, c, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = lds16(sB + (brow + j * 16) * ROWB + c * 64 + kq);
+      for (int j = 0; j < TN; ++j) bfr[j] = lb.frag(sB, wn * WTN + j * 16, c, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], af[i], bfr[j]);
+        for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], bfr[j], af[i]);   // Cᵀ tile
     }
-    __syncthreads();
     if (more) {
-      la.store(sA, tid);
-      lb.store(sB, tid);
+      char* nA = smem + (buf ^ 1) * STAGE;
+      la.store(nA, tid);
+      lb.store(nA + OA::BYTES, tid);
     }
     __syncthreads();
+    buf ^= 1;
   }
 
   // ------------------------------------------------------------------ epilogue
+  // lane holds C[m][n..n+3]: m = tile row + (lane&15), n = tile col + 4*(lane>>4)
   const bool first = blockIdx.z == 0;
-  const int rq = (lane >> 4) * 4;
+  const int li = lane & 15, lg = lane >> 4;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int64_t n = n0 + wn * WTN + j * 16 + (lane & 15);
-    const bool nok = n < g.N;
-    const float bias = (g.bias && first && nok) ? g.bias[n] : 0.f;
-    float csum = 0.f;
+    const int64_t n = n0 + wn * WTN + j * 16 + 4 * lg;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias && first) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias[e] = (n + e < g.N) ? g.bias[n + e] : 0.f;
+    }
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      const int64_t m = m0 + wm * WTM + i * 16 + li;
+      if (m >= g.M || n >= g.N) continue;
+      const bool full = g.vec && (n + 3 < g.N);
+      float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t m = m0 + wm * WTM + i * 16 + rq + e;
-        if (!(nok && m < g.M)) continue;
-        float v = g.alpha * acc[i][j][e] + bias;
-        if (g.act == 1) v = fmaxf(v, 0.f);
-        if (dk.on) v = drop_apply(dk, (uint32_t)(m * g.ld_drop + n), v);
-        if (g.gate) v = ld_dyn(g.gate, m * g.ld_gate + n, g.gate_f32) > 0.f ? v * g.gate_scale : 0.f;
-        csum += v;
-        if (g.residual && first) v += g.residual[m * g.ld_res + n];
-        const int64_t o = m * g.ldc + n;
-        if (g.c_mode == 1) atomicAdd(reinterpret_cast<float*>(g.C) + o, v);
-        else st_dyn(g.C, o, v, g.c_f32);
+        v[e] = g.alpha * acc[i][j][e] + bias[e];
+        if (g.act == 1) v[e] = fmaxf(v[e], 0.f);
+        if (dk.on) v[e] = drop_apply(dk, (uint32_t)(m * g.ld_drop + n + e), v[e]);
+      }
+      if (g.gate) {
+        const int64_t o = m * g.ld_gate + n;
+        float gv[4];
+        if (full && !g.gate_f32) {
+          const ushort4 q = *reinterpret_cast<const ushort4*>((const bf16_t*)g.gate + o);
+          gv[0] = bf2f(q.x); gv[1] = bf2f(q.y); gv[2] = bf2f(q.z); gv[3] = bf2f(q.w);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) gv[e] = (n + e < g.N) ? ld_dyn(g.gate, o + e, g.gate_f32) : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += (n + e < g.N) ? v[e] : 0.f;
+      if (g.residual && first) {
+        const float* rp = g.residual + m * g.ld_res + n;
+        if (full) {
+          const float4 rv = *reinterpret_cast<const float4*>(rp);
+          v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) if (n + e < g.N) v[e] += rp[e];
+        }
+      }
+      const int64_t o = m * g.ldc + n;
+      if (g.c_mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < g.N) atomicAdd(reinterpret_cast<float*>(g.C) + o + e, v[e]);
+      } else if (full && g.c_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + o) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if (full) {
+        ushort4 q;
+        q.x = f2bf(v[0]); q.y = f2bf(v[1]); q.z = f2bf(v[2]); q.w = f2bf(v[3]);
+        *reinterpret_cast<ushort4*>(reinterpret_cast<bf16_t*>(g.C) + o) = q;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) if (n + e < g.N) st_dyn(g.C, o + e, v[e], g.c_f32);
       }
     }
     if (g.colsum) {
-      csum += __shfl_xor(csum, 16, 64);
-      csum += __shfl_xor(csum, 32, 64);
-      if (lane < 16 && nok) atomicAdd(g.colsum + n, csum);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float s = cs[e];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        if (li == 0 && n + e < g.N) atomicAdd(g.colsum + n + e, s);
+      }
     }
   }
 }
@@ -187,7 +278,8 @@ void launch_layout(const GemmArgs& a, bool ak, bool bk, dim3 grid, hipStream_t s
 
 template <typename T>
 void launch_typed(const GemmArgs& a, bool ak, bool bk, int bm, int bn, dim3 grid, hipStream_t s) {
-  if (bm == 128) launch_layout<T, 128, 128>(a, ak, bk, grid, s);
+  if (bm == 128 && bn == 128) launch_layout<T, 128, 128>(a, ak, bk, grid, s);
+  else if (bm == 128) launch_layout<T, 128, 64>(a, ak, bk, grid, s);
   else if (bn == 128) launch_layout<T, 64, 128>(a, ak, bk, grid, s);
   else launch_layout<T, 64, 64>(a, ak, bk, grid, s);
 }
@@ -222,10 +314,10 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
 
   const int bke = 128 / es;
   int bm, bn;
-  const int64_t t128 = ((d->M + 127) / 128) * ((d->N + 127) / 128);
-  const int64_t t64x128 = ((d->M + 63) / 64) * ((d->N + 127) / 128);
-  if (d->N > 64 && t128 >= 256) { bm = 128; bn = 128; }
-  else if (d->N > 64 && t64x128 >= 128) { bm = 64; bn = 128; }
+  const int64_t tiles128 = ((d->M + 127) / 128) * ((d->N + 127) / 128);
+  const int64_t tiles64x128 = ((d->M + 63) / 64) * ((d->N + 127) / 128);
+  if (d->N > 64 && tiles128 >= 256) { bm = 128; bn = 128; }
+  else if (d->N > 64 && tiles64x128 >= 128) { bm = 64; bn = 128; }
   else { bm = 64; bn = 64; }
   const int64_t gx = (d->N + bn - 1) / bn, gy = (d->M + bm - 1) / bm;
   TTMI_REQUIRE(gy <= 65535 && gx <= 2147483647LL, "ttmi_gemm: grid too large");
@@ -259,6 +351,10 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   a.residual = d->residual; a.ld_res = d->ld_res;
   a.colsum = d->colsum;
   a.k_split = kspl;
+  const int cbytes = a.c_f32 ? 4 : 2;
+  a.vec = (d->ldc % 4 == 0) && ((uintptr_t)d->C % (4 * cbytes) == 0) &&
+          (!d->residual || (d->ld_res % 4 == 0 && (uintptr_t)d->residual % 16 == 0)) &&
+          (!d->gate || (d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 16 == 0));
 
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)split);
   if (d->dtype == TTMI_BF16) launch_typed<bf16_t>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);

@@ -39,8 +39,12 @@ TTMI_DEV bool collide(const int64_t* uid, int i, int j) {
   return uid && i != j && uid[i] == uid[j];
 }
 
-// blocks [0, nrb): rows (wave per row, masks the logits in place);
-// blocks [nrb, ...): columns (thread per column).
+// blocks [0, nrb): rows (wave per row; masks the logits in place);
+// blocks [nrb, ...): columns — 32 columns x 8 row groups per block, online max/sum-exp per
+// thread, partials merged through LDS (the mask is recomputed, so row and column blocks
+// need no ordering).
+constexpr int LC = 32, LRG = 8;
+
 __global__ __launch_bounds__(256) void lse_kernel(int B, float* __restrict__ S,
                                                   const int64_t* __restrict__ uid,
                                                   float* __restrict__ lse, float* __restrict__ ce,
@@ -68,19 +72,34 @@ __global__ __launch_bounds__(256) void lse_kernel(int B, float* __restrict__ S,
       lse[i] = l;
       ce[i] = l - row[i];
     }
-  } else {
-    const int j = (blockIdx.x - nrb) * blockDim.x + threadIdx.x;
-    if (j >= B) return;
-    float m = -INFINITY, s = 0.f, diag = 0.f;
-    for (int i = 0; i < B; ++i) {
+    return;
+  }
+  __shared__ float pm[LRG][LC], ps[LRG][LC], pd[LRG][LC];
+  const int cl = threadIdx.x % LC, rg = threadIdx.x / LC;
+  const int j = (blockIdx.x - nrb) * LC + cl;
+  float m = -INFINITY, s = 0.f, diag = 0.f;
+  if (j < B) {
+    for (int i = rg; i < B; i += LRG) {
       const float v = collide(uid, i, j) ? MASK_FILL : S[(int64_t)i * B + j];
       if (i == j) diag = v;
       if (v > m) { s = s * expf(m - v) + 1.f; m = v; }
       else s += expf(v - m);
     }
-    const float l = m + logf(s);
+  }
+  pm[rg][cl] = m;
+  ps[rg][cl] = s;
+  pd[rg][cl] = diag;
+  __syncthreads();
+  if (rg == 0 && j < B) {
+    float M = -INFINITY, D = 0.f;
+#pragma unroll
+    for (int k = 0; k < LRG; ++k) { M = fmaxf(M, pm[k][cl]); D += pd[k][cl]; }
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < LRG; ++k) tot += ps[k][cl] * expf(pm[k][cl] - M);
+    const float l = M + logf(tot);
     lse[B + j] = l;
-    ce[B + j] = l - diag;
+    ce[B + j] = l - D;
   }
 }
 
@@ -197,8 +216,8 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
   rc = ttmi_gemm(&g, s);
   if (rc) return rc;
   const int nrb = (B + 3) / 4;
-  hipLaunchKernelGGL(lse_kernel, dim3(nrb + (B + 255) / 256), dim3(256), 0, s, B, logits, user_idx, lse,
-                     w.ce, nrb);
+  hipLaunchKernelGGL(lse_kernel, dim3(nrb + (B + LC - 1) / LC), dim3(256), 0, s, B, logits, user_idx,
+                     lse, w.ce, nrb);
   rc = ttmi_check_launch("ttmi_infonce_fwd/lse");
   if (rc) return rc;
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, 2 * B, w.ce, 0.5f / (float)B, loss);

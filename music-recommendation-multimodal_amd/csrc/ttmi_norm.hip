@@ -8,8 +8,19 @@ namespace {
 
 constexpr int MAXV = 16;   // D <= 64 * MAXV
 
+// Instantiate a kernel template for the smallest NV (64-wide column chunks per row) that
+// covers D: NV in {1, 2, 4, 8, 16}.
+#define TTMI_NV_DISPATCH(D, ...)                 \
+  do {                                          \
+    if ((D) <= 64) { constexpr int NV = 1; __VA_ARGS__; }        \
+    else if ((D) <= 128) { constexpr int NV = 2; __VA_ARGS__; }  \
+    else if ((D) <= 256) { constexpr int NV = 4; __VA_ARGS__; }  \
+    else if ((D) <= 512) { constexpr int NV = 8; __VA_ARGS__; }  \
+    else { constexpr int NV = 16; __VA_ARGS__; }                 \
+  } while (0)
+
 // ------------------------------------------------------------------------------ LayerNorm
-template <typename TY>
+template <typename TY, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const float* __restrict__ x,
                                                      int64_t ldx, const float* __restrict__ w,
                                                      const float* __restrict__ b, float eps,
@@ -22,10 +33,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
   const float invD = 1.f / (float)D;
   const DropKeys dk = resolve_drop(dp);
   for (int64_t row = wid; row < M; row += nw) {
-    float v[MAXV];
+    float v[NV];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       v[i] = c < D ? x[row * ldx + c] : 0.f;
       s += v[i];
@@ -33,14 +44,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
     const float mu = wave_sum(s) * invD;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       const float dlt = c < D ? v[i] - mu : 0.f;
       q += dlt * dlt;
     }
     const float rs = 1.f / sqrtf(wave_sum(q) * invD + eps);
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       if (c < D) {
         float o = (v[i] - mu) * rs * w[c] + b[c];
@@ -57,41 +68,43 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
 }
 
 // Per-block reduction of per-lane column partials (4 waves) followed by one atomic per column.
-TTMI_DEV void block_col_atomic(float (&acc)[MAXV], int D, float* dst, float* red) {
+template <int NV>
+TTMI_DEV void block_col_atomic(float (&acc)[NV], int D, float* dst, float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
-    if (c < D) red[wave * 64 * MAXV + c] = acc[i];
+    if (c < D) red[wave * 64 * NV + c] = acc[i];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    const float t = red[c] + red[64 * MAXV + c] + red[2 * 64 * MAXV + c] + red[3 * 64 * MAXV + c];
+    const float t = red[c] + red[64 * NV + c] + red[2 * 64 * NV + c] + red[3 * 64 * NV + c];
     atomicAdd(dst + c, t);
   }
 }
 
+template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int64_t M, int D, const float* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
     int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ w, const void* __restrict__ gate, int gate_f32, int64_t ldg,
     float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ dw,
     float* __restrict__ db) {
-  __shared__ float red[4 * 64 * MAXV];
+  __shared__ float red[4 * 64 * NV];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const float invD = 1.f / (float)D;
-  float aw[MAXV], ab[MAXV];
+  float aw[NV], ab[NV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) aw[i] = ab[i] = 0.f;
+  for (int i = 0; i < NV; ++i) aw[i] = ab[i] = 0.f;
   for (int64_t row = wid; row < M; row += nw) {
     const float mu = mean[row], rs = rstd[row];
-    float g[MAXV], xh[MAXV];
+    float g[NV], xh[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       g[i] = 0.f; xh[i] = 0.f;
       if (c < D) {
@@ -107,7 +120,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     }
     const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       if (c < D) {
         const float o = rs * (g[i] - c1 - xh[i] * c2);
@@ -121,6 +134,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 
 // ------------------------------------------------------------------- SASRec input block
 // Forward: one wave per token row.
+template <int NV>
 __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
     int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E, int64_t V,
     const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ b,
@@ -136,10 +150,10 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
     const int l = (int)(row % L);
     const int64_t id = ids[row];
     const bool ok = id >= 0 && id < V;
-    float v[MAXV];
+    float v[NV];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       v[i] = c < D ? (ok ? E[id * D + c] : 0.f) + P[(int64_t)l * D + c] : 0.f;
       s += v[i];
@@ -147,14 +161,14 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
     const float mu = wave_sum(s) * invD;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       const float dlt = c < D ? v[i] - mu : 0.f;
       q += dlt * dlt;
     }
     const float rs = 1.f / sqrtf(wave_sum(q) * invD + eps);
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       if (c < D) {
         float o = (v[i] - mu) * rs * w[c] + b[c];
@@ -168,31 +182,32 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
 
 // Backward: block (l, b-chunk); each wave walks b = chunk*bpc + wave, +4, ... so the
 // position gradient dP[l] accumulates in registers (one atomic per column per block).
+template <int NV>
 __global__ __launch_bounds__(256) void seq_embed_bwd_kernel(
     int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E,
     const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ mean,
     const float* __restrict__ rstd, DropParams dp, const float* __restrict__ dx,
     float* __restrict__ dE, float* __restrict__ dP, float* __restrict__ dw, float* __restrict__ db,
     int64_t padding_idx, int64_t V, int bpc) {
-  __shared__ float red[4 * 64 * MAXV];
+  __shared__ float red[4 * 64 * NV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l = blockIdx.x;
   const int b0 = blockIdx.y * bpc;
   const int b1 = min(B, b0 + bpc);
   const float invD = 1.f / (float)D;
   const DropKeys dk = resolve_drop(dp);
-  float ap[MAXV], aw[MAXV], ab[MAXV];
+  float ap[NV], aw[NV], ab[NV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) ap[i] = aw[i] = ab[i] = 0.f;
+  for (int i = 0; i < NV; ++i) ap[i] = aw[i] = ab[i] = 0.f;
   for (int bb = b0 + wave; bb < b1; bb += 4) {
     const int64_t row = (int64_t)bb * L + l;
     const int64_t id = ids[row];
     const bool ok = id >= 0 && id < V;
     const float mu = mean[row], rs = rstd[row];
-    float g[MAXV], xh[MAXV];
+    float g[NV], xh[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       g[i] = 0.f; xh[i] = 0.f;
       if (c < D) {
@@ -210,7 +225,7 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_kernel(
     const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
     const bool emb = ok && id != padding_idx;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       if (c < D) {
         const float o = rs * (g[i] - c1 - xh[i] * c2);
@@ -273,7 +288,10 @@ __global__ void user_concat_bwd_kernel(int B, int D, const float* __restrict__ d
 }
 
 // ---------------------------------------------------------------------- BatchNorm1d
-// Block: 256 threads = 64 columns x 4 row groups.
+// Block: 256 threads = BN_COLS columns x BN_RG row groups; per-column statistics reduced
+// through LDS (no atomics: one block owns its columns).
+constexpr int BN_COLS = 16, BN_RG = 16;
+
 template <typename T>
 __global__ __launch_bounds__(256) void bn_fwd_kernel(int B, int C, const float* __restrict__ z,
                                                      const float* __restrict__ w,
@@ -283,23 +301,29 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(int B, int C, const float* 
                                                      int training, int relu, DropParams dp,
                                                      T* __restrict__ y, float* __restrict__ mean,
                                                      float* __restrict__ rstd) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float red[BN_RG][BN_COLS];
+  const int cl = threadIdx.x % BN_COLS, rg = threadIdx.x / BN_COLS;
+  const int c = blockIdx.x * BN_COLS + cl;
   const bool ok = c < C;
   float mu, var;
   if (training) {
     float s = 0.f;
-    if (ok) for (int r = rg; r < B; r += 4) s += z[(int64_t)r * C + c];
+    if (ok) for (int r = rg; r < B; r += BN_RG) s += z[(int64_t)r * C + c];
     red[rg][cl] = s;
     __syncthreads();
-    mu = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) / (float)B;
+    s = 0.f;
+#pragma unroll
+    for (int k = 0; k < BN_RG; ++k) s += red[k][cl];
+    mu = s / (float)B;
     __syncthreads();
     float q = 0.f;
-    if (ok) for (int r = rg; r < B; r += 4) { const float d = z[(int64_t)r * C + c] - mu; q += d * d; }
+    if (ok) for (int r = rg; r < B; r += BN_RG) { const float d = z[(int64_t)r * C + c] - mu; q += d * d; }
     red[rg][cl] = q;
     __syncthreads();
-    var = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) / (float)B;
+    q = 0.f;
+#pragma unroll
+    for (int k = 0; k < BN_RG; ++k) q += red[k][cl];
+    var = q / (float)B;
   } else {                                     // eval: running statistics, no update
     mu = ok ? running_mean[c] : 0.f;
     var = ok ? running_var[c] : 1.f;
@@ -308,7 +332,7 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(int B, int C, const float* 
   const DropKeys dk = resolve_drop(dp);
   if (ok) {
     const float wc = w[c], bc = b[c];
-    for (int r = rg; r < B; r += 4) {
+    for (int r = rg; r < B; r += BN_RG) {
       float o = (z[(int64_t)r * C + c] - mu) * rs * wc + bc;
       if (relu) o = fmaxf(o, 0.f);
       if (dk.on) o = drop_apply(dk, (uint32_t)((int64_t)r * C + c), o);
@@ -335,14 +359,14 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(int B, int C, const float* 
                                                      const T* __restrict__ y, float gate_scale,
                                                      int gated, float* __restrict__ dz,
                                                      float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[2][4][64];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float red[2][BN_RG][BN_COLS];
+  const int cl = threadIdx.x % BN_COLS, rg = threadIdx.x / BN_COLS;
+  const int c = blockIdx.x * BN_COLS + cl;
   const bool ok = c < C;
   const float mu = ok ? mean[c] : 0.f, rs = ok ? rstd[c] : 0.f, wc = ok ? w[c] : 0.f;
   float s1 = 0.f, s2 = 0.f;   // Σ dy', Σ dy'·x̂
   if (ok) {
-    for (int r = rg; r < B; r += 4) {
+    for (int r = rg; r < B; r += BN_RG) {
       const int64_t o = (int64_t)r * C + c;
       float d = dy[o];
       if (gated) d = ldf<T>(y, o) > 0.f ? d * gate_scale : 0.f;
@@ -354,11 +378,12 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(int B, int C, const float* 
   red[0][rg][cl] = s1;
   red[1][rg][cl] = s2;
   __syncthreads();
-  const float S1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-  const float S2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < BN_RG; ++k) { S1 += red[0][k][cl]; S2 += red[1][k][cl]; }
   if (!ok) return;
   const float invB = 1.f / (float)B;
-  for (int r = rg; r < B; r += 4) {
+  for (int r = rg; r < B; r += BN_RG) {
     const int64_t o = (int64_t)r * C + c;
     float d = dy[o];
     if (gated) d = ldf<T>(y, o) > 0.f ? d * gate_scale : 0.f;
@@ -387,12 +412,14 @@ extern "C" int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx,
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_layernorm_fwd: drop_p out of [0,1)");
   if (M == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
-  if (y_dtype == TTMI_BF16)
-    hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(rows_grid(M)), dim3(256), 0, s, M, D, x, ldx, w, b,
-                       eps, relu, dp, (bf16_t*)y, ldy, mean, rstd);
-  else
-    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(rows_grid(M)), dim3(256), 0, s, M, D, x, ldx, w, b,
-                       eps, relu, dp, (float*)y, ldy, mean, rstd);
+  TTMI_NV_DISPATCH(D, {
+    if (y_dtype == TTMI_BF16)
+      hipLaunchKernelGGL((ln_fwd_kernel<bf16_t, NV>), dim3(rows_grid(M)), dim3(256), 0, s, M, D, x, ldx,
+                         w, b, eps, relu, dp, (bf16_t*)y, ldy, mean, rstd);
+    else
+      hipLaunchKernelGGL((ln_fwd_kernel<float, NV>), dim3(rows_grid(M)), dim3(256), 0, s, M, D, x, ldx,
+                         w, b, eps, relu, dp, (float*)y, ldy, mean, rstd);
+  });
   return ttmi_check_launch("ttmi_layernorm_fwd");
 }
 
@@ -405,9 +432,10 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
   TTMI_REQUIRE(dy && x && mean && rstd && w && dx, "ttmi_layernorm_bwd: null argument");
   TTMI_REQUIRE(lddy >= D && ldx >= D && lddx >= D && (!gate || ldg >= D), "ttmi_layernorm_bwd: bad ld");
   if (M == 0) return TTMI_OK;
-  int grid = (int)std::min<int64_t>((M + 3) / 4, 512);
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w,
-                     gate, gate_dtype == TTMI_F32, ldg, gate_scale, res, dx, lddx, dw, db);
+  int grid = (int)std::min<int64_t>((M + 3) / 4, 1024);
+  TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(grid), dim3(256), 0, s, M, D, dy,
+                                         lddy, x, ldx, mean, rstd, w, gate, gate_dtype == TTMI_F32,
+                                         ldg, gate_scale, res, dx, lddx, dw, db));
   return ttmi_check_launch("ttmi_layernorm_bwd");
 }
 
@@ -419,8 +447,9 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
   TTMI_REQUIRE(ids && E && P && w && b && x && mean && rstd, "ttmi_seq_embed_fwd: null argument");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_seq_embed_fwd: drop_p out of [0,1)");
   if (B == 0) return TTMI_OK;
-  hipLaunchKernelGGL(seq_embed_fwd_kernel, dim3(rows_grid((int64_t)B * L)), dim3(256), 0, s, B, L, D,
-                     ids, E, V, P, w, b, eps, make_drop(drop_p, drop_seed), x, mean, rstd);
+  TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_fwd_kernel<NV>), dim3(rows_grid((int64_t)B * L)),
+                                         dim3(256), 0, s, B, L, D, ids, E, V, P, w, b, eps,
+                                         make_drop(drop_p, drop_seed), x, mean, rstd));
   return ttmi_check_launch("ttmi_seq_embed_fwd");
 }
 
@@ -438,8 +467,9 @@ extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const
   const int chunks = std::max(1, std::min((1024 + L - 1) / L, B));
   const int bpc = (B + chunks - 1) / chunks;
   dim3 grid(L, (B + bpc - 1) / bpc);
-  hipLaunchKernelGGL(seq_embed_bwd_kernel, grid, dim3(256), 0, s, B, L, D, ids, E, P, w, mean, rstd,
-                     make_drop(drop_p, drop_seed), dx, dE, dP, dw, db, padding_idx, V, bpc);
+  TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_bwd_kernel<NV>), grid, dim3(256), 0, s, B, L, D, ids,
+                                         E, P, w, mean, rstd, make_drop(drop_p, drop_seed), dx, dE,
+                                         dP, dw, db, padding_idx, V, bpc));
   return ttmi_check_launch("ttmi_seq_embed_bwd");
 }
 
@@ -487,7 +517,7 @@ extern "C" int ttmi_batchnorm_fwd(int dtype, int B, int C, const float* z, const
   if (B == 0) return TTMI_OK;
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_batchnorm_fwd: drop_p out of [0,1)");
   DropParams dp = make_drop(drop_p, drop_seed);
-  dim3 grid((C + 63) / 64);
+  dim3 grid((C + BN_COLS - 1) / BN_COLS);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(bn_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, C, z, w, b, eps, momentum,
                        running_mean, running_var, num_batches_tracked, training, relu, dp, (bf16_t*)y, mean, rstd);
@@ -504,7 +534,7 @@ extern "C" int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, cons
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_batchnorm_bwd: bad dtype");
   TTMI_REQUIRE(B > 1 && C > 0, "ttmi_batchnorm_bwd: bad sizes");
   TTMI_REQUIRE(dy && z && w && mean && rstd && dz && (!gated || y), "ttmi_batchnorm_bwd: null argument");
-  dim3 grid((C + 63) / 64);
+  dim3 grid((C + BN_COLS - 1) / BN_COLS);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(bn_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, C, dy, z, w, mean, rstd,
                        (const bf16_t*)y, gate_scale, gated, dz, dw, db);

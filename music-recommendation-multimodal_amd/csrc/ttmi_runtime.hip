@@ -109,8 +109,93 @@ __global__ void dropout_seeds_kernel(uint64_t base, const int32_t* step, uint64_
   if (s < n) seeds[s] = splitmix64(splitmix64(base) ^ ((uint64_t)(int64_t)step[0] * 64ull + (uint64_t)s));
 }
 
-// dy = dropout_bwd(dx) cast to T; colsum += Σ_rows dy.  Block: 256 threads = (N/...)...
-// Each thread owns one column n (looping over a chunk of rows): coalesced along n.
+// Column-reduction layout shared by dropout_bwd / colsum: each thread owns 4 consecutive
+// columns (16-byte loads), tpr = N/4 threads cover a row, 256/tpr rows per pass; a block
+// walks `rpb` rows, reduces its column sums through LDS and adds them with one atomic per
+// column.  Needs N % 4 == 0 and N <= 1024 (callers fall back to the scalar kernels).
+template <typename T>
+TTMI_DEV void store4(T* p, float a, float b, float c, float d);
+template <> TTMI_DEV void store4<float>(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+template <> TTMI_DEV void store4<bf16_t>(bf16_t* p, float a, float b, float c, float d) {
+  ushort4 q;
+  q.x = f2bf(a); q.y = f2bf(b); q.z = f2bf(c); q.w = f2bf(d);
+  *reinterpret_cast<ushort4*>(p) = q;
+}
+template <typename T>
+TTMI_DEV float4 load4(const T* p);
+template <> TTMI_DEV float4 load4<float>(const float* p) { return *reinterpret_cast<const float4*>(p); }
+template <> TTMI_DEV float4 load4<bf16_t>(const bf16_t* p) {
+  const ushort4 q = *reinterpret_cast<const ushort4*>(p);
+  return make_float4(bf2f(q.x), bf2f(q.y), bf2f(q.z), bf2f(q.w));
+}
+
+TTMI_DEV void colsum_block_reduce(float (&s)[4], int N, int tpr, int rpp, float* red,
+                                  float* colsum) {
+  const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
+  if (rg < rpp) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[rg * N + cg * 4 + e] = s[e];
+  }
+  __syncthreads();
+  for (int c = t; c < N; c += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < rpp; ++k) acc += red[k * N + c];
+    atomicAdd(colsum + c, acc);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_bwd_vec_kernel(int64_t M, int N,
+                                                              const float* __restrict__ dx,
+                                                              int64_t ldx, DropParams d,
+                                                              int64_t ld_drop, T* __restrict__ dy,
+                                                              int64_t ldy, float* __restrict__ colsum,
+                                                              int64_t rpb) {
+  __shared__ float red[1024];
+  const int tpr = N >> 2, rpp = 256 / tpr;
+  const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
+  const DropKeys dk = resolve_drop(d);
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rg < rpp) {
+    const int n = cg * 4;
+    for (int64_t m = r0 + rg; m < r1; m += rpp) {
+      float4 v = *reinterpret_cast<const float4*>(dx + m * ldx + n);
+      float* pv = &v.x;
+      if (dk.on) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          pv[e] = drop_keep(dk, (uint32_t)(m * ld_drop + n + e)) ? pv[e] * dk.scale : 0.f;
+      }
+      store4<T>(dy + m * ldy + n, v.x, v.y, v.z, v.w);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += pv[e];
+    }
+  }
+  if (colsum) colsum_block_reduce(s, N, tpr, rpp, red, colsum);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t M, int N, const T* __restrict__ x,
+                                                         int64_t ldx, float* __restrict__ colsum,
+                                                         int64_t rpb) {
+  __shared__ float red[1024];
+  const int tpr = N >> 2, rpp = 256 / tpr;
+  const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rg < rpp) {
+    for (int64_t m = r0 + rg; m < r1; m += rpp) {
+      const float4 v = load4<T>(x + m * ldx + cg * 4);
+      s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+    }
+  }
+  colsum_block_reduce(s, N, tpr, rpp, red, colsum);
+}
+
+// Scalar fallbacks (any N): each thread owns one column.
 template <typename T>
 __global__ void dropout_bwd_kernel(int64_t M, int N, const float* __restrict__ dx, int64_t ldx,
                                    DropParams d, int64_t ld_drop, T* __restrict__ dy,
@@ -140,6 +225,17 @@ __global__ void colsum_kernel(int64_t M, int N, const T* __restrict__ x, int64_t
     for (int64_t m = r0; m < r1; ++m) s += ldf<T>(x, m * ldx + n);
     atomicAdd(colsum + n, s);
   }
+}
+
+bool vec_ok(int N, int64_t ld, const void* a, const void* b) {
+  return N % 4 == 0 && N <= 1024 && ld % 4 == 0 && ((uintptr_t)a & 15) == 0 &&
+         ((uintptr_t)b & 7) == 0;
+}
+int64_t vec_rows_per_block(int64_t M, int N) {
+  const int rpp = 256 / (N / 4);
+  int64_t rpb = (M + 511) / 512;
+  rpb = (rpb + rpp - 1) / rpp * rpp;
+  return std::max<int64_t>(rpb, rpp);
 }
 
 int grid_for(int64_t n, int per_thread) {
@@ -192,10 +288,21 @@ extern "C" int ttmi_dropout_bwd(int dtype, int64_t M, int N, const float* dx, in
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_dropout_bwd: drop_p out of [0,1)");
   TTMI_REQUIRE(drop_p == 0.f || drop_seed, "ttmi_dropout_bwd: dropout needs a seed pointer");
   if (M == 0) return TTMI_OK;
-  const int rpb = 64;
-  dim3 grid((N + 255) / 256, (unsigned)((M + rpb - 1) / rpb));
   DropParams d = make_drop(drop_p, drop_seed);
   if (ld_drop == 0) ld_drop = N;
+  if (vec_ok(N, ldx, dx, dy) && ldy % 4 == 0) {
+    const int64_t rpb = vec_rows_per_block(M, N);
+    dim3 vg((unsigned)((M + rpb - 1) / rpb));
+    if (dtype == TTMI_BF16)
+      hipLaunchKernelGGL(dropout_bwd_vec_kernel<bf16_t>, vg, dim3(256), 0, s, M, N, dx, ldx, d,
+                         ld_drop, (bf16_t*)dy, ldy, colsum, rpb);
+    else
+      hipLaunchKernelGGL(dropout_bwd_vec_kernel<float>, vg, dim3(256), 0, s, M, N, dx, ldx, d,
+                         ld_drop, (float*)dy, ldy, colsum, rpb);
+    return ttmi_check_launch("ttmi_dropout_bwd");
+  }
+  const int rpb = 64;
+  dim3 grid((N + 255) / 256, (unsigned)((M + rpb - 1) / rpb));
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(dropout_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, M, N, dx, ldx, d, ld_drop,
                        (bf16_t*)dy, ldy, colsum, rpb);
@@ -210,6 +317,17 @@ extern "C" int ttmi_colsum(int dtype, int64_t M, int N, const void* x, int64_t l
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_colsum: bad dtype");
   TTMI_REQUIRE(M >= 0 && N > 0 && x && colsum && ldx >= N, "ttmi_colsum: bad args");
   if (M == 0) return TTMI_OK;
+  if (vec_ok(N, ldx, x, x)) {
+    const int64_t rpb = vec_rows_per_block(M, N);
+    dim3 vg((unsigned)((M + rpb - 1) / rpb));
+    if (dtype == TTMI_BF16)
+      hipLaunchKernelGGL(colsum_vec_kernel<bf16_t>, vg, dim3(256), 0, s, M, N, (const bf16_t*)x, ldx,
+                         colsum, rpb);
+    else
+      hipLaunchKernelGGL(colsum_vec_kernel<float>, vg, dim3(256), 0, s, M, N, (const float*)x, ldx,
+                         colsum, rpb);
+    return ttmi_check_launch("ttmi_colsum");
+  }
   const int rpb = 64;
   dim3 grid((N + 255) / 256, (unsigned)((M + rpb - 1) / rpb));
   if (dtype == TTMI_BF16)
