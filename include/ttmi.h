@@ -47,7 +47,8 @@ int ttmi_abi_version(void);
  *
  *   C[m,n] (=|+=) epi( alpha * Σ_k A(m,k)·B(n,k) )
  *   A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m];  B(n,k) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n]
- *   epi: v += bias[n]; v = act(v) (0 none, 1 relu); v = dropout(v, idx = m*ld_drop+n);
+ *   epi: v += bias[n]; v = act(v) (0 none, 1 relu);
+ *        v = dropout(v, idx = r(m)*ld_drop + n) with r(m) = drop_rows ? drop_rows[m] : m;
  *        v = gate ? (gate[m*ld_gate+n] > 0 ? v*gate_scale : 0) : v;  colsum[n] += v;
  *        v += residual[m*ld_res+n];  C = v (c_mode 0) or C += v atomically (c_mode 1, f32 C).
  *   Operands A and B share `dtype`; C has `c_dtype`.  split_k > 1 partitions K over
@@ -69,6 +70,7 @@ typedef struct {
   const float* residual; int64_t ld_res;
   float* colsum;
   int split_k;
+  const int32_t* drop_rows;
 } ttmi_gemm_desc;
 int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream);
 
@@ -125,7 +127,8 @@ int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
 
 /* ------------------------------------------------------------------------------------
  * Last-valid gather + demographics concat (user_tower.py:118-139):
- *   len_b = Σ_l (len_src[b,l] != 0) - 1 clamped >= 0; rows[b] = b*L + len_b;
+ *   len_b = Σ_l (len_src[b,l] != 0) - 1 clamped >= 0; rows[b] = b*L + len_b
+ *   (len_src == NULL: x is already gathered, rows[b] = b*L with L == 1);
  *   comb[b] = [x[rows[b]], G[gender[b]], C[country[b]]]   ([B, D+dg+dc], dtype)
  * ---------------------------------------------------------------------------------- */
 int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
@@ -196,13 +199,42 @@ int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int 
 /* dst = bf16(src) (parameter mirror for bf16 GEMM operands). */
 int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hipStream_t stream);
 /* Residual-branch dropout backward (TransformerEncoderLayer dropout1/dropout2):
- * dy[m,n] = dx[m,n]·keep(m*ld_drop+n)/(1-p) cast to dtype; colsum[n] += dy[m,n] (bias grad). */
+ * dy[m,n] = dx[m,n]·keep(r(m)*ld_drop+n)/(1-p) cast to dtype, r(m) = drop_rows ? drop_rows[m]
+ * : m; colsum[n] += dy[m,n] (bias grad, may be NULL). */
 int ttmi_dropout_bwd(int dtype, int64_t M, int N, const float* dx, int64_t ldx, float drop_p,
-                     const uint64_t* drop_seed, int64_t ld_drop, void* dy, int64_t ldy, float* colsum,
-                     hipStream_t stream);
+                     const uint64_t* drop_seed, int64_t ld_drop, const int32_t* drop_rows,
+                     void* dy, int64_t ldy, float* colsum, hipStream_t stream);
 /* colsum[n] += Σ_m x[m*ldx+n]  (bias grads of GEMMs fed by attention backward). */
 int ttmi_colsum(int dtype, int64_t M, int N, const void* x, int64_t ldx, float* colsum,
                 hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Last-layer pruning (SURVEY §8d F_min).  The last encoder layer's output is consumed only
+ * at the last valid position of each sequence (user_tower.py:118-132) and nothing after its
+ * attention mixes tokens, so it needs K/V for every token but Q, the attention output,
+ * out_proj, FFN and both residual adds only for B gathered rows.  Dropout indices stay the
+ * full-tensor ones (row-mapped), so results equal the unpruned layer's.
+ * ---------------------------------------------------------------------------------- */
+/* rows[b] = b*L + max(Σ_l (len_src[b,l] != 0) - 1, 0). */
+int ttmi_last_rows(int B, int L, const int64_t* len_src, int32_t* rows, hipStream_t stream);
+/* out[b,:] = x[rows[b],:] (fp32, row width D). */
+int ttmi_gather_rows(int B, int D, const float* x, const int32_t* rows, float* out,
+                     hipStream_t stream);
+/* dst[rows[b],:] += src[b,:] (rows distinct). */
+int ttmi_scatter_add_rows(int B, int D, const float* src, const int32_t* rows, float* dst,
+                          hipStream_t stream);
+/* Single-query causal attention for query row rows[b] of each sequence (position
+ * p = rows[b] - b*L): keys j <= p with key_valid[b,j] != 0; dropout idx as ttmi_mha_fwd
+ * with i = p.  qkv [B*L, 3HDh]; ctx [B, HDh]; lse [B*H]. */
+int ttmi_mha_q1_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                    const int64_t* key_valid, const int32_t* rows, float drop_p,
+                    const uint64_t* drop_seed, void* ctx, float* lse, hipStream_t stream);
+/* Backward: writes the full dqkv [B*L, 3HDh] (dQ only on the query rows, zero elsewhere;
+ * dK, dV on every row). */
+int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                    const int64_t* key_valid, const int32_t* rows, const float* lse,
+                    const void* dctx, float drop_p, const uint64_t* drop_seed, void* dqkv,
+                    hipStream_t stream);
 
 #ifdef __cplusplus
 }

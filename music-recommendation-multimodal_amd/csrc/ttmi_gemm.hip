@@ -34,7 +34,7 @@ struct GemmArgs {
   void* C; int64_t ldc; int c_f32; int c_mode;
   float alpha;
   const float* bias; int act;
-  DropParams drop; int64_t ld_drop;
+  DropParams drop; int64_t ld_drop; const int32_t* drop_rows;
   const void* gate; int gate_f32; int64_t ld_gate; float gate_scale;
   const float* residual; int64_t ld_res;
   float* colsum;
@@ -206,12 +206,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       const int64_t m = m0 + wm * WTM + i * 16 + li;
       if (m >= g.M || n >= g.N) continue;
       const bool full = g.vec && (n + 3 < g.N);
+      const int64_t drow = g.drop_rows ? (int64_t)g.drop_rows[m] : m;
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[e] = g.alpha * acc[i][j][e] + bias[e];
         if (g.act == 1) v[e] = fmaxf(v[e], 0.f);
-        if (dk.on) v[e] = drop_apply(dk, (uint32_t)(m * g.ld_drop + n + e), v[e]);
+        if (dk.on) v[e] = drop_apply(dk, (uint32_t)(drow * g.ld_drop + n + e), v[e]);
       }
       if (g.gate) {
         const int64_t o = m * g.ld_gate + n;
@@ -346,6 +347,7 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   a.alpha = d->alpha;
   a.bias = d->bias; a.act = d->act;
   a.drop = make_drop(d->drop_p, d->drop_seed); a.ld_drop = d->ld_drop ? d->ld_drop : d->N;
+  a.drop_rows = d->drop_rows;
   a.gate = d->gate; a.gate_f32 = d->gate_dtype == TTMI_F32; a.ld_gate = d->ld_gate;
   a.gate_scale = d->gate_scale;
   a.residual = d->residual; a.ld_res = d->ld_res;

@@ -252,8 +252,9 @@ __global__ void user_concat_fwd_kernel(int B, int L, int D, const float* __restr
   const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (b >= B) return;
   float cnt = 0.f;
-  for (int l = lane; l < L; l += 64) cnt += len_src[(int64_t)b * L + l] != 0 ? 1.f : 0.f;
-  const int len = (int)(wave_sum(cnt) + 0.5f);
+  if (len_src)
+    for (int l = lane; l < L; l += 64) cnt += len_src[(int64_t)b * L + l] != 0 ? 1.f : 0.f;
+  const int len = len_src ? (int)(wave_sum(cnt) + 0.5f) : 1;
   const int64_t row = (int64_t)b * L + max(len - 1, 0);
   const int W = D + dg + dc;
   const int64_t g = gender[b], c = country[b];
@@ -479,8 +480,9 @@ extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float*
                                     void* comb, int32_t* rows, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_user_concat_fwd: bad dtype");
   TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && dg >= 0 && dc >= 0, "ttmi_user_concat_fwd: bad sizes");
-  TTMI_REQUIRE(x && len_src && gender && country && comb && rows && (dg == 0 || G) && (dc == 0 || C),
+  TTMI_REQUIRE(x && gender && country && comb && rows && (dg == 0 || G) && (dc == 0 || C),
                "ttmi_user_concat_fwd: null argument");
+  TTMI_REQUIRE(len_src || L == 1, "ttmi_user_concat_fwd: len_src == NULL needs L == 1");
   if (B == 0) return TTMI_OK;
   dim3 grid((B + 3) / 4);
   if (dtype == TTMI_BF16)

@@ -1,0 +1,212 @@
+// ttmi_rows.hip — last-layer pruning primitives.
+//
+// The user tower consumes ONE token per sequence from the last encoder layer (the
+// last-valid gather, reference user_tower.py:118-132), and nothing after the last layer's
+// attention mixes tokens.  So the last layer only needs K/V for every token and everything
+// else (Q, attention output, out_proj, FFN, both residuals) for the gathered token:
+//   ttmi_last_rows      rows[b] = b*L + max(len_b - 1, 0)
+//   ttmi_gather_rows    out[b] = x[rows[b]]
+//   ttmi_scatter_add_rows dst[rows[b]] += src[b]
+//   ttmi_mha_q1_fwd/bwd single-query causal attention for the gathered row of each sequence
+// Dropout masks keep the full-tensor flat indices (row-mapped), so the pruned layer draws
+// exactly the masks the unpruned layer would: outputs and gradients are identical.
+#include "ttmi_common.h"
+
+namespace {
+
+__global__ void last_rows_kernel(int B, int L, const int64_t* __restrict__ len_src,
+                                 int32_t* __restrict__ rows) {
+  const int lane = threadIdx.x & 63;
+  const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (b >= B) return;
+  float cnt = 0.f;
+  for (int l = lane; l < L; l += 64) cnt += len_src[(int64_t)b * L + l] != 0 ? 1.f : 0.f;
+  const int len = (int)(wave_sum(cnt) + 0.5f);
+  if (lane == 0) rows[b] = (int32_t)((int64_t)b * L + max(len - 1, 0));
+}
+
+__global__ void gather_rows_kernel(int B, int D, const float* __restrict__ x,
+                                   const int32_t* __restrict__ rows, float* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int64_t r = rows[b];
+  for (int c = threadIdx.x; c < D; c += blockDim.x) out[(int64_t)b * D + c] = x[r * D + c];
+}
+
+__global__ void scatter_add_rows_kernel(int B, int D, const float* __restrict__ src,
+                                        const int32_t* __restrict__ rows, float* __restrict__ dst) {
+  const int b = blockIdx.x;
+  const int64_t r = rows[b];
+  for (int c = threadIdx.x; c < D; c += blockDim.x) dst[r * D + c] += src[(int64_t)b * D + c];
+}
+
+// One 64-lane wave per (b, h); lane j owns key j (L <= 64).
+template <typename T>
+__global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int Dh,
+                                                        const T* __restrict__ qkv,
+                                                        const int64_t* __restrict__ kvalid,
+                                                        const int32_t* __restrict__ rows,
+                                                        DropParams dp, T* __restrict__ ctx,
+                                                        float* __restrict__ lse, float scale) {
+  __shared__ float sq[64], sp[64];
+  const int j = threadIdx.x;
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * Dh;
+  const int64_t ld = 3LL * D;
+  const int64_t r = rows[b];
+  const int p = (int)(r - (int64_t)b * L);
+  const T* seq = qkv + (int64_t)b * L * ld + (int64_t)h * Dh;
+  if (j < Dh) sq[j] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + j);
+  __syncthreads();
+  const bool ok = j < L && j <= p && kvalid[(int64_t)b * L + j] != 0;
+  float s = -INFINITY;
+  if (ok) {
+    const T* kr = seq + (int64_t)j * ld + D;
+    float acc = 0.f;
+    for (int d = 0; d < Dh; ++d) acc += sq[d] * ldf<T>(kr, d);
+    s = acc * scale;
+  }
+  const float m = wave_max(s);
+  const float e = (ok && m != -INFINITY) ? expf(s - m) : 0.f;
+  const float sum = wave_sum(e);
+  float pj = sum > 0.f ? e / sum : 0.f;
+  const DropKeys dk = resolve_drop(dp);
+  if (dk.on && ok) pj = drop_apply(dk, (uint32_t)((((int64_t)bh * L) + p) * L + j), pj);
+  sp[j] = pj;
+  if (j == 0) lse[bh] = m == -INFINITY ? INFINITY : m + logf(sum);
+  __syncthreads();
+  if (j < Dh) {
+    float acc = 0.f;
+    const int last = min(p, L - 1);
+    for (int k = 0; k <= last; ++k) acc += sp[k] * ldf<T>(seq + (int64_t)k * ld + 2 * D, j);
+    stf<T>(ctx, (int64_t)b * D + (int64_t)h * Dh + j, acc);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void mha_q1_bwd_kernel(int B, int L, int H, int Dh,
+                                                        const T* __restrict__ qkv,
+                                                        const int64_t* __restrict__ kvalid,
+                                                        const int32_t* __restrict__ rows,
+                                                        const float* __restrict__ lse,
+                                                        const T* __restrict__ dctx, DropParams dp,
+                                                        T* __restrict__ dqkv, float scale) {
+  __shared__ float sq[64], sdo[64], sds[64];
+  const int j = threadIdx.x;
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * Dh;
+  const int64_t ld = 3LL * D;
+  const int64_t r = rows[b];
+  const int p = (int)(r - (int64_t)b * L);
+  const T* seq = qkv + (int64_t)b * L * ld + (int64_t)h * Dh;
+  T* dseq = dqkv + (int64_t)b * L * ld + (int64_t)h * Dh;
+  if (j < Dh) {
+    sq[j] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + j);
+    sdo[j] = ldf<T>(dctx, (int64_t)b * D + (int64_t)h * Dh + j);
+  }
+  __syncthreads();
+  const bool ok = j < L && j <= p && kvalid[(int64_t)b * L + j] != 0;
+  const float l = lse[bh];
+  const DropKeys dk = resolve_drop(dp);
+  float pj = 0.f, dP = 0.f, keep = 1.f;
+  if (ok) {
+    const T* kr = seq + (int64_t)j * ld + D;
+    const T* vr = seq + (int64_t)j * ld + 2 * D;
+    float sd = 0.f, dv = 0.f;
+    for (int d = 0; d < Dh; ++d) {
+      sd += sq[d] * ldf<T>(kr, d);
+      dv += sdo[d] * ldf<T>(vr, d);
+    }
+    pj = expf(sd * scale - l);
+    if (dk.on) keep = drop_keep(dk, (uint32_t)((((int64_t)bh * L) + p) * L + j)) ? dk.scale : 0.f;
+    dP = dv * keep;
+  }
+  const float Dsum = wave_sum(pj * dP);
+  const float ds = pj * (dP - Dsum) * scale;
+  const float pd = pj * keep;
+  sds[j] = ds;
+  if (j < L) {
+    T* row = dseq + (int64_t)j * ld;
+    for (int d = 0; d < Dh; ++d) {
+      if (j != p) stf<T>(row, d, 0.f);                    // Q slice of non-query rows
+      stf<T>(row + D, d, ds * sq[d]);                      // dK_j = dS_j q
+      stf<T>(row + 2 * D, d, pd * sdo[d]);                 // dV_j = Pd_j dO
+    }
+  }
+  __syncthreads();
+  if (j < Dh) {
+    float acc = 0.f;
+    const int last = min(p, L - 1);
+    for (int k = 0; k <= last; ++k) acc += sds[k] * ldf<T>(seq + (int64_t)k * ld + D, j);
+    stf<T>(dseq + (int64_t)p * ld, j, acc);               // dQ_p = Σ dS_j k_j
+  }
+}
+
+}  // namespace
+
+extern "C" int ttmi_last_rows(int B, int L, const int64_t* len_src, int32_t* rows, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && L > 0 && len_src && rows, "ttmi_last_rows: bad args");
+  if (B == 0) return TTMI_OK;
+  hipLaunchKernelGGL(last_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, s, B, L, len_src, rows);
+  return ttmi_check_launch("ttmi_last_rows");
+}
+
+extern "C" int ttmi_gather_rows(int B, int D, const float* x, const int32_t* rows, float* out,
+                                hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && D > 0 && x && rows && out, "ttmi_gather_rows: bad args");
+  if (B == 0) return TTMI_OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(B), dim3(128), 0, s, B, D, x, rows, out);
+  return ttmi_check_launch("ttmi_gather_rows");
+}
+
+extern "C" int ttmi_scatter_add_rows(int B, int D, const float* src, const int32_t* rows,
+                                     float* dst, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && D > 0 && src && rows && dst, "ttmi_scatter_add_rows: bad args");
+  if (B == 0) return TTMI_OK;
+  hipLaunchKernelGGL(scatter_add_rows_kernel, dim3(B), dim3(128), 0, s, B, D, src, rows, dst);
+  return ttmi_check_launch("ttmi_scatter_add_rows");
+}
+
+extern "C" int ttmi_mha_q1_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                               const int64_t* key_valid, const int32_t* rows, float drop_p,
+                               const uint64_t* drop_seed, void* ctx, float* lse, hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_fwd: bad dtype");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64,
+               "ttmi_mha_q1_fwd: need L <= 64, Dh <= 64");
+  TTMI_REQUIRE(qkv && key_valid && rows && ctx && lse, "ttmi_mha_q1_fwd: null argument");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
+               "ttmi_mha_q1_fwd: bad dropout");
+  if (B == 0) return TTMI_OK;
+  DropParams dp = make_drop(drop_p, drop_seed);
+  const float scale = 1.f / sqrtf((float)Dh);
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL(mha_q1_fwd_kernel<bf16_t>, dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const bf16_t*)qkv, key_valid, rows, dp, (bf16_t*)ctx, lse, scale);
+  else
+    hipLaunchKernelGGL(mha_q1_fwd_kernel<float>, dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const float*)qkv, key_valid, rows, dp, (float*)ctx, lse, scale);
+  return ttmi_check_launch("ttmi_mha_q1_fwd");
+}
+
+extern "C" int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                               const int64_t* key_valid, const int32_t* rows, const float* lse,
+                               const void* dctx, float drop_p, const uint64_t* drop_seed,
+                               void* dqkv, hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_bwd: bad dtype");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64,
+               "ttmi_mha_q1_bwd: need L <= 64, Dh <= 64");
+  TTMI_REQUIRE(qkv && key_valid && rows && lse && dctx && dqkv, "ttmi_mha_q1_bwd: null argument");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
+               "ttmi_mha_q1_bwd: bad dropout");
+  if (B == 0) return TTMI_OK;
+  DropParams dp = make_drop(drop_p, drop_seed);
+  const float scale = 1.f / sqrtf((float)Dh);
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL(mha_q1_bwd_kernel<bf16_t>, dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const bf16_t*)qkv, key_valid, rows, lse, (const bf16_t*)dctx, dp,
+                       (bf16_t*)dqkv, scale);
+  else
+    hipLaunchKernelGGL(mha_q1_bwd_kernel<float>, dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const float*)qkv, key_valid, rows, lse, (const float*)dctx, dp,
+                       (float*)dqkv, scale);
+  return ttmi_check_launch("ttmi_mha_q1_bwd");
+}

@@ -150,7 +150,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void dropout_bwd_vec_kernel(int64_t M, int N,
                                                               const float* __restrict__ dx,
                                                               int64_t ldx, DropParams d,
-                                                              int64_t ld_drop, T* __restrict__ dy,
+                                                              int64_t ld_drop,
+                                                              const int32_t* __restrict__ drows,
+                                                              T* __restrict__ dy,
                                                               int64_t ldy, float* __restrict__ colsum,
                                                               int64_t rpb) {
   __shared__ float red[1024];
@@ -165,9 +167,10 @@ __global__ __launch_bounds__(256) void dropout_bwd_vec_kernel(int64_t M, int N,
       float4 v = *reinterpret_cast<const float4*>(dx + m * ldx + n);
       float* pv = &v.x;
       if (dk.on) {
+        const int64_t dr = drows ? (int64_t)drows[m] : m;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          pv[e] = drop_keep(dk, (uint32_t)(m * ld_drop + n + e)) ? pv[e] * dk.scale : 0.f;
+          pv[e] = drop_keep(dk, (uint32_t)(dr * ld_drop + n + e)) ? pv[e] * dk.scale : 0.f;
       }
       store4<T>(dy + m * ldy + n, v.x, v.y, v.z, v.w);
 #pragma unroll
@@ -198,7 +201,8 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t M, int N, const
 // Scalar fallbacks (any N): each thread owns one column.
 template <typename T>
 __global__ void dropout_bwd_kernel(int64_t M, int N, const float* __restrict__ dx, int64_t ldx,
-                                   DropParams d, int64_t ld_drop, T* __restrict__ dy,
+                                   DropParams d, int64_t ld_drop,
+                                   const int32_t* __restrict__ drows, T* __restrict__ dy,
                                    int64_t ldy, float* __restrict__ colsum, int rows_per_block) {
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
@@ -207,7 +211,8 @@ __global__ void dropout_bwd_kernel(int64_t M, int N, const float* __restrict__ d
     float s = 0.f;
     for (int64_t m = r0; m < r1; ++m) {
       float v = dx[m * ldx + n];
-      if (dk.on) v = drop_keep(dk, (uint32_t)(m * ld_drop + n)) ? v * dk.scale : 0.f;
+      const int64_t dr = drows ? (int64_t)drows[m] : m;
+      if (dk.on) v = drop_keep(dk, (uint32_t)(dr * ld_drop + n)) ? v * dk.scale : 0.f;
       stf<T>(dy, m * ldy + n, v);
       s += v;
     }
@@ -281,8 +286,9 @@ extern "C" int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* 
 }
 
 extern "C" int ttmi_dropout_bwd(int dtype, int64_t M, int N, const float* dx, int64_t ldx,
-                                float drop_p, const uint64_t* drop_seed, int64_t ld_drop, void* dy,
-                                int64_t ldy, float* colsum, hipStream_t s) {
+                                float drop_p, const uint64_t* drop_seed, int64_t ld_drop,
+                                const int32_t* drop_rows, void* dy, int64_t ldy, float* colsum,
+                                hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_dropout_bwd: bad dtype");
   TTMI_REQUIRE(M >= 0 && N > 0 && dx && dy && ldx >= N && ldy >= N, "ttmi_dropout_bwd: bad args");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_dropout_bwd: drop_p out of [0,1)");
@@ -295,20 +301,20 @@ extern "C" int ttmi_dropout_bwd(int dtype, int64_t M, int N, const float* dx, in
     dim3 vg((unsigned)((M + rpb - 1) / rpb));
     if (dtype == TTMI_BF16)
       hipLaunchKernelGGL(dropout_bwd_vec_kernel<bf16_t>, vg, dim3(256), 0, s, M, N, dx, ldx, d,
-                         ld_drop, (bf16_t*)dy, ldy, colsum, rpb);
+                         ld_drop, drop_rows, (bf16_t*)dy, ldy, colsum, rpb);
     else
       hipLaunchKernelGGL(dropout_bwd_vec_kernel<float>, vg, dim3(256), 0, s, M, N, dx, ldx, d,
-                         ld_drop, (float*)dy, ldy, colsum, rpb);
+                         ld_drop, drop_rows, (float*)dy, ldy, colsum, rpb);
     return ttmi_check_launch("ttmi_dropout_bwd");
   }
   const int rpb = 64;
   dim3 grid((N + 255) / 256, (unsigned)((M + rpb - 1) / rpb));
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(dropout_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, M, N, dx, ldx, d, ld_drop,
-                       (bf16_t*)dy, ldy, colsum, rpb);
+                       drop_rows, (bf16_t*)dy, ldy, colsum, rpb);
   else
     hipLaunchKernelGGL(dropout_bwd_kernel<float>, grid, dim3(256), 0, s, M, N, dx, ldx, d, ld_drop,
-                       (float*)dy, ldy, colsum, rpb);
+                       drop_rows, (float*)dy, ldy, colsum, rpb);
   return ttmi_check_launch("ttmi_dropout_bwd");
 }
 

@@ -75,6 +75,10 @@ class TowerCfg:
     p_drop: float = 0.0
     dtype: torch.dtype = torch.bfloat16
     eps: float = 1e-5
+    # Run the last encoder layer only for the gathered last-valid row of each sequence
+    # (K/V still from every token).  Output- and gradient-identical (ttmi.h, "Last-layer
+    # pruning"); False runs the full layer.
+    prune_last: bool = True
 
 
 def _drop(cfg: TowerCfg, seeds: Optional[Tensor], site: int, p: Optional[float] = None):
@@ -104,6 +108,7 @@ class LayerSaved:
     m2: Tensor
     r2: Tensor
     h: Tensor          # dropout(relu(linear1)) (compute dtype)
+    rows: Optional[Tensor] = None   # pruned layer: int32 [B] gathered rows (x1/a2/h/ctx are [B,*])
 
 
 @dataclass
@@ -150,35 +155,51 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                    seeds=seeds)
     for i in range(cfg.n_layers):
         pre = _lp(i)
+        pruned = cfg.prune_last and i == cfg.n_layers - 1
         a1 = torch.empty(M, D, device=dev, dtype=dt)
         m1 = torch.empty(M, **f32)
         r1 = torch.empty(M, **f32)
         ops.layernorm_fwd(x, P[pre + "norm1.weight"], P[pre + "norm1.bias"], a1, m1, r1, eps=cfg.eps)
         qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         ops.linear(a1, W[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"], qkv)
-        ctx = torch.empty(M, D, device=dev, dtype=dt)
-        lse = torch.empty(B * H * L, **f32)
-        ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
-        x1 = torch.empty(M, D, **f32)
+        F_ = W[pre + "linear1.weight"].shape[0]
+        if pruned:
+            rows = torch.empty(B, device=dev, dtype=torch.int32)
+            ops.last_rows(key_valid, rows)
+            R, res_in, drows = B, torch.empty(B, D, **f32), rows
+            ops.gather_rows(x, rows, res_in)
+            ctx = torch.empty(B, D, device=dev, dtype=dt)
+            lse = torch.empty(B * H, **f32)
+            ops.mha_q1_fwd(qkv, key_valid, rows, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
+        else:
+            rows, R, res_in, drows = None, M, x, None
+            ctx = torch.empty(M, D, device=dev, dtype=dt)
+            lse = torch.empty(B * H * L, **f32)
+            ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
+        x1 = torch.empty(R, D, **f32)
         ops.linear(ctx, W[pre + "self_attn.out_proj.weight"], P[pre + "self_attn.out_proj.bias"],
-                   x1, drop=_drop(cfg, seeds, site_drop1(i)), residual=x)
-        a2 = torch.empty(M, D, device=dev, dtype=dt)
-        m2 = torch.empty(M, **f32)
-        r2 = torch.empty(M, **f32)
+                   x1, drop=_drop(cfg, seeds, site_drop1(i)), residual=res_in, drop_rows=drows)
+        a2 = torch.empty(R, D, device=dev, dtype=dt)
+        m2 = torch.empty(R, **f32)
+        r2 = torch.empty(R, **f32)
         ops.layernorm_fwd(x1, P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2, eps=cfg.eps)
-        h = torch.empty(M, W[pre + "linear1.weight"].shape[0], device=dev, dtype=dt)
+        h = torch.empty(R, F_, device=dev, dtype=dt)
         ops.linear(a2, W[pre + "linear1.weight"], P[pre + "linear1.bias"], h, act=1,
-                   drop=_drop(cfg, seeds, site_ffn(i)))
-        x2 = torch.empty(M, D, **f32)
+                   drop=_drop(cfg, seeds, site_ffn(i)), drop_rows=drows)
+        x2 = torch.empty(R, D, **f32)
         ops.linear(h, W[pre + "linear2.weight"], P[pre + "linear2.bias"], x2,
-                   drop=_drop(cfg, seeds, site_drop2(i)), residual=x1)
-        st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, x1, a2, m2, r2, h))
+                   drop=_drop(cfg, seeds, site_drop2(i)), residual=x1, drop_rows=drows)
+        st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, x1, a2, m2, r2, h, rows))
         x = x2
+    gathered = cfg.prune_last and cfg.n_layers > 0
     G = P["gender_embedding.weight"]
     C = P["country_embedding.weight"]
     comb = torch.empty(B, D + G.shape[1] + C.shape[1], device=dev, dtype=dt)
     rows = torch.empty(B, device=dev, dtype=torch.int32)
-    ops.user_concat_fwd(x, key_valid, gender, G, country, C, comb, rows, B, L)
+    if gathered:   # x is already [B, D] (the pruned last layer's gathered rows)
+        ops.user_concat_fwd(x, None, gender, G, country, C, comb, rows, B, 1)
+    else:
+        ops.user_concat_fwd(x, key_valid, gender, G, country, C, comb, rows, B, L)
     z = torch.empty(B, D, **f32)
     ops.linear(comb, W["fusion_layer.0.weight"], P["fusion_layer.0.bias"], z)
     az = torch.empty(B, D, device=dev, dtype=dt)
@@ -215,7 +236,8 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
     ops.linear_dw(dz_c, st.comb, grads["fusion_layer.0.weight"])
     dcomb = torch.empty(B, st.comb.shape[1], **f32)
     ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dcomb)
-    dx = torch.zeros(M, D, **f32)
+    gathered = cfg.prune_last and cfg.n_layers > 0
+    dx = torch.zeros(B if gathered else M, D, **f32)
     G = P["gender_embedding.weight"]
     C = P["country_embedding.weight"]
     ops.user_concat_bwd(dcomb, st.rows, st.gender, G.shape[1], st.country, C.shape[1], dx,
@@ -225,35 +247,47 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
     for i in reversed(range(cfg.n_layers)):
         pre = _lp(i)
         s = st.layers[i]
-        F = W[pre + "linear1.weight"].shape[0]
-        dy2 = torch.empty(M, D, device=dev, dtype=dt)
-        ops.dropout_bwd(dx, dy2, grads[pre + "linear2.bias"], _drop(cfg, seeds, site_drop2(i)))
+        R = s.x1.shape[0]                 # B for the pruned layer, M otherwise
+        drows = s.rows
+        F_ = W[pre + "linear1.weight"].shape[0]
+        dy2 = torch.empty(R, D, device=dev, dtype=dt)
+        ops.dropout_bwd(dx, dy2, grads[pre + "linear2.bias"], _drop(cfg, seeds, site_drop2(i)),
+                        drop_rows=drows)
         ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"])
-        dz1 = torch.empty(M, F, device=dev, dtype=dt)
+        dz1 = torch.empty(R, F_, device=dev, dtype=dt)
         ops.linear_dx(dy2, W[pre + "linear2.weight"], dz1, gate=s.h, gate_scale=_scale(p),
                       colsum=grads[pre + "linear1.bias"])
         ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"])
-        da2 = torch.empty(M, D, **f32)
+        da2 = torch.empty(R, D, **f32)
         ops.linear_dx(dz1, W[pre + "linear1.weight"], da2)
-        dx1 = torch.empty(M, D, **f32)
+        dx1 = torch.empty(R, D, **f32)
         ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
                           grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
-        dy1 = torch.empty(M, D, device=dev, dtype=dt)
+        dy1 = torch.empty(R, D, device=dev, dtype=dt)
         ops.dropout_bwd(dx1, dy1, grads[pre + "self_attn.out_proj.bias"],
-                        _drop(cfg, seeds, site_drop1(i)))
+                        _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
         ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"])
-        dctx = torch.empty(M, D, device=dev, dtype=dt)
+        dctx = torch.empty(R, D, device=dev, dtype=dt)
         ops.linear_dx(dy1, W[pre + "self_attn.out_proj.weight"], dctx)
         dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
-        ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
-                    _drop(cfg, seeds, site_attn(i)))
+        if drows is not None:
+            ops.mha_q1_bwd(s.qkv, st.key_valid, drows, s.lse, dctx, B, L, H, dqkv,
+                           _drop(cfg, seeds, site_attn(i)))
+        else:
+            ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
+                        _drop(cfg, seeds, site_attn(i)))
         ops.colsum(dqkv, grads[pre + "self_attn.in_proj_bias"])
         ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"])
         da1 = torch.empty(M, D, **f32)
         ops.linear_dx(dqkv, W[pre + "self_attn.in_proj_weight"], da1)
         dxn = torch.empty(M, D, **f32)
-        ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
-                          grads[pre + "norm1.weight"], grads[pre + "norm1.bias"], res=dx1)
+        if drows is not None:
+            ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
+                              grads[pre + "norm1.weight"], grads[pre + "norm1.bias"])
+            ops.scatter_add_rows(dx1, drows, dxn)      # residual path of the gathered rows
+        else:
+            ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
+                              grads[pre + "norm1.weight"], grads[pre + "norm1.bias"], res=dx1)
         dx = dxn
     # ---- input block (user_tower.py:83-93)
     ops.seq_embed_bwd(st.ids, P["item_embedding.weight"], P["position_embedding.weight"],

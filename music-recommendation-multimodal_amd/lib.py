@@ -36,6 +36,7 @@ class GemmDesc(ctypes.Structure):
         ("residual", c_p), ("ld_res", c_i64),
         ("colsum", c_p),
         ("split_k", c_i),
+        ("drop_rows", c_p),
     ]
 
 
@@ -68,7 +69,13 @@ SIGNATURES = {
     "ttmi_step_inc": (c_i, [c_p, c_p]),
     "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_p]),
     "ttmi_cast_f32_bf16": (c_i, [c_i64, c_p, c_p, c_p]),
-    "ttmi_dropout_bwd": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_f, c_p, c_i64, c_p, c_i64, c_p, c_p]),
+    "ttmi_dropout_bwd": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_f, c_p, c_i64, c_p, c_p, c_i64, c_p,
+                               c_p]),
+    "ttmi_last_rows": (c_i, [c_i, c_i, c_p, c_p, c_p]),
+    "ttmi_gather_rows": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_scatter_add_rows": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_mha_q1_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
+    "ttmi_mha_q1_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_colsum": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_p, c_p]),
 }
 

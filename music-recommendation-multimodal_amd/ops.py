@@ -50,7 +50,7 @@ def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a
          bias: Optional[Tensor] = None, act: int = 0, drop: Drop = NO_DROP, ld_drop: int = 0,
          gate: Optional[Tensor] = None, ld_gate: int = 0, gate_scale: float = 1.0,
          residual: Optional[Tensor] = None, ld_res: int = 0, colsum: Optional[Tensor] = None,
-         split_k: int = 1) -> Tensor:
+         split_k: int = 1, drop_rows: Optional[Tensor] = None) -> Tensor:
     _dev(A, B, C)
     if A.dtype != B.dtype:
         raise TypeError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
@@ -69,17 +69,21 @@ def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a
     d.residual, d.ld_res = _p(residual), ld_res
     d.colsum = _p(colsum)
     d.split_k = split_k
+    d.drop_rows = _p(drop_rows)
     call("ttmi_gemm", ctypes.byref(d), _s())
     return C
 
 
 def linear(x: Tensor, w: Tensor, bias: Optional[Tensor], out: Tensor, *, act: int = 0,
-           drop: Drop = NO_DROP, residual: Optional[Tensor] = None) -> Tensor:
-    """out[M,N] = epi(x[M,K] · w[N,K]ᵀ + bias)  (nn.Linear forward)."""
+           drop: Drop = NO_DROP, residual: Optional[Tensor] = None,
+           drop_rows: Optional[Tensor] = None) -> Tensor:
+    """out[M,N] = epi(x[M,K] · w[N,K]ᵀ + bias)  (nn.Linear forward); dropout indices use
+    drop_rows[m] (int32) as the row when given (pruned last layer)."""
     M, K = x.shape
     N = w.shape[0]
     return gemm(x, w, out, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True, ldc=N,
-                bias=bias, act=act, drop=drop, ld_drop=N, residual=residual, ld_res=N)
+                bias=bias, act=act, drop=drop, ld_drop=N, residual=residual, ld_res=N,
+                drop_rows=drop_rows)
 
 
 def linear_dx(dy: Tensor, w: Tensor, out: Tensor, *, gate: Optional[Tensor] = None,
@@ -155,8 +159,8 @@ def mha_bwd(qkv: Tensor, key_valid: Tensor, lse: Tensor, dctx: Tensor, B: int, L
 
 
 # ----------------------------------------------------------------------------- user head
-def user_concat_fwd(x: Tensor, len_src: Tensor, gender: Tensor, G: Tensor, country: Tensor,
-                    C: Tensor, comb: Tensor, rows: Tensor, B: int, L: int):
+def user_concat_fwd(x: Tensor, len_src: Optional[Tensor], gender: Tensor, G: Tensor,
+                    country: Tensor, C: Tensor, comb: Tensor, rows: Tensor, B: int, L: int):
     D = x.shape[1]
     call("ttmi_user_concat_fwd", code(comb.dtype), B, L, D, _p(x), _p(len_src), _p(gender), _p(G),
          G.shape[1], _p(country), _p(C), C.shape[1], _p(comb), _p(rows), _s())
@@ -234,11 +238,45 @@ def cast_bf16(src: Tensor, dst: Tensor) -> Tensor:
     return dst
 
 
-def dropout_bwd(dx: Tensor, dy: Tensor, colsum: Optional[Tensor], drop: Drop = NO_DROP) -> Tensor:
+def dropout_bwd(dx: Tensor, dy: Tensor, colsum: Optional[Tensor], drop: Drop = NO_DROP,
+                drop_rows: Optional[Tensor] = None) -> Tensor:
     M, N = dx.shape
     call("ttmi_dropout_bwd", code(dy.dtype), M, N, _p(dx), N, float(drop[0]), _p(drop[1]), N,
-         _p(dy), N, _p(colsum), _s())
+         _p(drop_rows), _p(dy), N, _p(colsum), _s())
     return dy
+
+
+# ----------------------------------------------------------------------------- pruning
+def last_rows(len_src: Tensor, rows: Tensor) -> Tensor:
+    B, L = len_src.shape
+    call("ttmi_last_rows", B, L, _p(len_src), _p(rows), _s())
+    return rows
+
+
+def gather_rows(x: Tensor, rows: Tensor, out: Tensor) -> Tensor:
+    call("ttmi_gather_rows", rows.numel(), x.shape[1], _p(x), _p(rows), _p(out), _s())
+    return out
+
+
+def scatter_add_rows(src: Tensor, rows: Tensor, dst: Tensor) -> Tensor:
+    call("ttmi_scatter_add_rows", rows.numel(), src.shape[1], _p(src), _p(rows), _p(dst), _s())
+    return dst
+
+
+def mha_q1_fwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, B: int, L: int, H: int,
+               ctx: Tensor, lse: Tensor, drop: Drop = NO_DROP):
+    Dh = qkv.shape[1] // (3 * H)
+    call("ttmi_mha_q1_fwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(rows),
+         float(drop[0]), _p(drop[1]), _p(ctx), _p(lse), _s())
+    return ctx
+
+
+def mha_q1_bwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, lse: Tensor, dctx: Tensor, B: int,
+               L: int, H: int, dqkv: Tensor, drop: Drop = NO_DROP):
+    Dh = qkv.shape[1] // (3 * H)
+    call("ttmi_mha_q1_bwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(rows),
+         _p(lse), _p(dctx), float(drop[0]), _p(drop[1]), _p(dqkv), _s())
+    return dqkv
 
 
 def colsum(x: Tensor, out: Tensor) -> Tensor:

@@ -101,7 +101,7 @@ class SequentialUserEncoder(nn.Module):
     def __init__(self, vocab_size: int, num_genders: int = 1, num_countries: int = 1,
                  embedding_dim: int = 256, max_seq_len: int = 50, num_heads: int = 4,
                  num_layers: int = 2, dropout: float = 0.1, *,
-                 compute_dtype: torch.dtype = torch.bfloat16):
+                 compute_dtype: torch.dtype = torch.bfloat16, prune_last: bool = True):
         super().__init__()
         if embedding_dim % num_heads:
             raise ValueError("embedding_dim must be divisible by num_heads")
@@ -110,6 +110,7 @@ class SequentialUserEncoder(nn.Module):
         self.num_heads = num_heads
         self.num_layers = num_layers
         self.compute_dtype = compute_dtype
+        self.prune_last = prune_last
         self.item_embedding = nn.Embedding(vocab_size, embedding_dim, padding_idx=0)
         self.gender_embedding = nn.Embedding(num_genders, 16)
         self.country_embedding = nn.Embedding(num_countries, 32)
@@ -144,7 +145,7 @@ class SequentialUserEncoder(nn.Module):
     def cfg(self) -> F.TowerCfg:
         return F.TowerCfg(D=self.embedding_dim, H=self.num_heads, n_layers=self.num_layers,
                           p_drop=self.dropout.p if self.training else 0.0,
-                          dtype=self.compute_dtype)
+                          dtype=self.compute_dtype, prune_last=self.prune_last)
 
     def forward(self, history_ids: Tensor, user_gender: Tensor, user_country: Tensor,
                 history_mask: Optional[Tensor] = None, seeds: Optional[Tensor] = None) -> Tensor:

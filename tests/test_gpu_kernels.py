@@ -188,6 +188,58 @@ def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
     assert rel(dqkv.float(), qt.grad) < (5e-5 if dtype == torch.float32 else 3e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64)])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_mha_single_query_matches_full_row(gpu_pkg, dtype, B, L, H, Dh, p):
+    """ttmi_mha_q1_* (pruned last layer) == the full attention restricted to each
+    sequence's last valid row, forward and backward, same dropout masks."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(B + L + Dh)
+    D = H * Dh
+    qkv = (torch.randn(B * L, 3 * D, generator=g) * 1.5).to(dtype)
+    kv = masks(B, L, g)
+    seed = 0xFEEDFACE0102
+    lengths = kv.sum(1)
+    rows = (torch.arange(B) * L + (lengths - 1).clamp(min=0)).to(torch.int32)
+    qt = qkv.float().clone().requires_grad_(True)
+    o_ref, lse_ref = attn_ref(qt, kv, B, L, H, p, seed)
+    o_sel = o_ref[rows.long()]
+    lse_sel = lse_ref.reshape(B, H, L)[torch.arange(B), :, (lengths - 1).clamp(min=0)]
+    sd = seed_dev(seed)
+    rows_d = torch.empty(B, dtype=torch.int32, device=DEV)
+    ops.last_rows(kv.to(DEV), rows_d)
+    assert torch.equal(rows_d.cpu(), rows)
+    ctx = torch.empty(B, D, device=DEV, dtype=dtype)
+    lse = torch.empty(B * H, device=DEV)
+    ops.mha_q1_fwd(qkv.to(DEV), kv.to(DEV), rows_d, B, L, H, ctx, lse, (p, sd))
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert rel(ctx.float(), o_sel) < tol
+    fin = torch.isfinite(lse_sel.reshape(-1))
+    assert torch.equal(torch.isfinite(lse.cpu()), fin)
+    assert rel(lse.cpu()[fin], lse_sel.reshape(-1)[fin]) < (2e-6 if dtype == torch.float32 else 1e-2)
+    dsel = torch.randn(B, D, generator=g).to(dtype)
+    o_sel.backward(dsel.float())
+    dqkv = torch.empty(B * L, 3 * D, device=DEV, dtype=dtype)
+    ops.mha_q1_bwd(qkv.to(DEV), kv.to(DEV), rows_d, lse, dsel.to(DEV), B, L, H, dqkv, (p, sd))
+    assert rel(dqkv.float(), qt.grad) < (5e-5 if dtype == torch.float32 else 3e-2)
+
+
+def test_gather_scatter_rows(gpu_pkg):
+    ops = gpu_pkg.ops
+    x = torch.randn(500, 96, device=DEV)
+    rows = torch.tensor([3, 499, 0, 250], dtype=torch.int32, device=DEV)
+    out = torch.empty(4, 96, device=DEV)
+    ops.gather_rows(x, rows, out)
+    assert torch.equal(out, x[rows.long()])
+    dst = torch.zeros(500, 96, device=DEV)
+    ops.scatter_add_rows(out, rows, dst)
+    ops.scatter_add_rows(out, rows, dst)
+    expect = torch.zeros(500, 96, device=DEV)
+    expect[rows.long()] = 2 * out
+    assert torch.equal(dst, expect)
+
+
 # ------------------------------------------------------------------------------ embedding
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_seq_embed_fwd_bwd(gpu_pkg, p):

@@ -266,6 +266,28 @@ def test_dropout_on_matches_oracle_hash(gpu_pkg):
         assert rel(mine[k].grad, params[k].grad) < 1e-4, k
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_pruned_last_layer_equals_full(gpu_pkg, p):
+    """Pruning the last encoder layer to the gathered rows (default) gives the same output
+    and parameter gradients as running it on every token (fp32, dropout on/off)."""
+    F = gpu_pkg.functional
+    outs, grads = [], []
+    for prune in (True, False):
+        m, batch = _cfg2(gpu_pkg, torch.float32, B=96, L=50, V=997, p=p, seed=5)
+        m.user_tower.prune_last = prune
+        seeds = F.seed_table(F.site_seeds(0xABC, 3), DEV)
+        bd = {k: v.to(DEV) for k, v in batch.items()}
+        loss, logits, _, _ = m(bd, seeds=seeds)
+        loss.backward()
+        outs.append(logits.detach().cpu())
+        grads.append({k: v.grad.detach().cpu() for k, v in m.named_parameters()})
+    assert rel(outs[0], outs[1]) < 1e-5
+    for k in grads[0]:
+        if k.endswith("in_proj_bias"):
+            continue
+        assert rel(grads[0][k], grads[1][k]) < 1e-4, k
+
+
 def test_train_step_graph_equals_eager_and_learns(gpu_pkg):
     """bf16, dropout on: graph replay == eager schedule step for step; loss decreases."""
     m1, batch = _cfg2(gpu_pkg, torch.bfloat16, B=256, p=0.1, seed=7)
