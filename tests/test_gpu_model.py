@@ -5,8 +5,10 @@ Tolerances (stated per test):
   * fp32 compute path: 1e-4 relative to the tensor's max-abs for outputs and gradients
     (two transformer layers of fp32-MFMA vs CPU summation order).
   * bf16 compute path (the product default): each output/gradient's deviation from the
-    fp32 reference must stay within 1.25x (+0.02) of the deviation that rounding the GEMM
-    operands to bf16 ALONE produces in the CPU oracle (``bf16_emulated``): ReLU gates that
+    fp32 reference must stay within 2x (+0.03) of the deviation that rounding every GEMM's
+    operands (forward and backward) and the bf16-stored QKV / FFN-hidden activations
+    produces in the CPU oracle (``bf16_emulated``; attention probabilities / dS / dctx, also
+    bf16 on the GPU, are not emulated): ReLU gates that
     flip under rounding make some gradients legitimately 40%+ off in max-abs terms, and this
     bound separates that from kernel bugs.  Plus the north-star bar
     |loss_bf16 - loss_fp32_oracle| <= 1e-3 at the full cfg-2 size (B=512, L=50, D=128,
@@ -31,16 +33,39 @@ def rel(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
 
 
+class _BfLinear(torch.autograd.Function):
+    """y = bf16(x)·bf16(w)ᵀ (+b); backward rounds the incoming gradient to bf16 before both
+    products, as the kernels do (dY is stored bf16 for the dX and dW GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        xb, wb = _bf(x), _bf(w)
+        ctx.save_for_backward(xb, wb)
+        return xb @ wb.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        dyb = _bf(dy)
+        return dyb @ wb, dyb.reshape(-1, dyb.shape[-1]).t() @ xb.reshape(-1, xb.shape[-1])
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
 @contextlib.contextmanager
 def bf16_linears():
-    """Run the CPU oracle with every GEMM operand rounded to bf16 (what the kernels feed the
-    MFMAs)."""
-    bf = lambda t: t.to(torch.bfloat16).to(torch.float32)    # noqa: E731
+    """Run the CPU oracle with every GEMM's operands rounded to bf16 (forward and backward)
+    and the QKV / FFN-hidden activations stored in bf16, as the kernels do."""
     orig = ref.linear
 
     def lin(x, w, b):
-        y = bf(x) @ bf(w).t()
-        return y + b if b is not None else y
+        y = _BfLinear.apply(x, w)
+        y = y + b if b is not None else y
+        if w.shape[0] in (3 * w.shape[1], 4 * w.shape[1]):
+            y = _bf(y)
+        return y
     ref.linear = lin
     try:
         yield
@@ -84,7 +109,7 @@ def test_user_tower_vs_reference(gpu_pkg, name, dtype):
         e_out, e_grads = bf16_emulated(z)
         emul = {k: rel(v, z["g/" + k]) for k, v in e_grads.items()}
         emul["out"] = rel(e_out, z["out"])
-        tol_of = lambda k: 1.25 * emul[k] + 0.02              # noqa: E731
+        tol_of = lambda k: 2.0 * emul[k] + 0.03               # noqa: E731
     assert rel(out, z["out"]) < tol_of("out")
     (out * torch.tensor(z["upstream"], device=DEV)).sum().backward()
     grads = dict(m.named_parameters())
@@ -139,7 +164,7 @@ def test_item_fusion_vs_reference(gpu_pkg, dtype):
             (eo * torch.tensor(z["upstream"])).sum().backward()
         emul = {k: rel(p.grad, z["g/" + k]) for k, p in params.items()}
         emul["out"] = rel(eo.detach(), z["out"])
-        tol_of = lambda k: 1.25 * emul[k] + 0.02              # noqa: E731
+        tol_of = lambda k: 2.0 * emul[k] + 0.03               # noqa: E731
     out = m.fuse(torch.tensor(z["modal"], device=DEV))
     assert rel(out, z["out"]) < tol_of("out")
     (out * torch.tensor(z["upstream"], device=DEV)).sum().backward()
