@@ -51,6 +51,8 @@ int ttmi_abi_version(void);
  *        v = dropout(v, idx = r(m)*ld_drop + n) with r(m) = drop_rows ? drop_rows[m] : m;
  *        v = gate ? (gate[m*ld_gate+n] > 0 ? v*gate_scale : 0) : v;  colsum[n] += v;
  *        v += residual[m*ld_res+n];  C = v (c_mode 0) or C += v atomically (c_mode 1, f32 C).
+ *   rowsum_a (may be NULL): rowsum_a[m] += Σ_k A(m,k) — with A = dYᵀ of a weight-gradient
+ *   GEMM this is the bias gradient, taken from the operand fragments already in registers.
  *   Operands A and B share `dtype`; C has `c_dtype`.  split_k > 1 partitions K over
  *   workgroups and requires c_mode 1 and act 0 (bias/residual are added by split 0 only).
  *   Alignment: rows of a k-major operand need K % 8 == 0 (bf16) / K % 4 == 0 (f32);
@@ -71,6 +73,7 @@ typedef struct {
   float* colsum;
   int split_k;
   const int32_t* drop_rows;
+  float* rowsum_a;
 } ttmi_gemm_desc;
 int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream);
 
@@ -182,11 +185,12 @@ int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat, const
  *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps).
  * hyper (device, fp64) = {lr, beta1, beta2, eps, weight_decay}; step (device int32) holds
  * t (the caller increments it with ttmi_step_inc before the update), so a captured graph
- * replays with the live step count and learning rate.  p_bf16 (optional)
+ * replays with the live step count and learning rate.  zero_grad != 0 also clears g after
+ * reading it (optimizer.zero_grad folded into the update).  p_bf16 (optional)
  * receives the bf16 mirror used as GEMM operand by the next step.
  * ---------------------------------------------------------------------------------- */
-int ttmi_adamw(int64_t n, float* p, const float* g, float* m, float* v, uint16_t* p_bf16,
-               const double* hyper, const int32_t* step, hipStream_t stream);
+int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
+               const double* hyper, const int32_t* step, int zero_grad, hipStream_t stream);
 int ttmi_step_inc(int32_t* step, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
@@ -196,6 +200,10 @@ int ttmi_step_inc(int32_t* step, hipStream_t stream);
  * seeds of the current step, derived on device from the live step counter. */
 int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int n,
                        hipStream_t stream);
+/* dst[i][0:nbytes[i]] = src[i][...] for i < n <= 16 device buffers, in one launch (stages a
+ * batch's tensors into a captured step's static inputs). */
+int ttmi_batch_copy(int n, void* const* dst, const void* const* src, const int64_t* nbytes,
+                    hipStream_t stream);
 /* dst = bf16(src) (parameter mirror for bf16 GEMM operands). */
 int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hipStream_t stream);
 /* Residual-branch dropout backward (TransformerEncoderLayer dropout1/dropout2):

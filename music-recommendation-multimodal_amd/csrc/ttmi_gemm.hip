@@ -40,7 +40,21 @@ struct GemmArgs {
   float* colsum;
   int64_t k_split;   // K elements per split (multiple of the K tile)
   int vec;           // 1: all row strides allow 4-wide vector epilogue accesses
+  float* rowsum_a;   // rowsum_a[m] += Σ_k A(m,k)  (bias grad of a weight-gradient GEMM)
 };
+
+// Sum of the 8 bf16 / 4 f32 operand values a lane holds in one fragment.
+template <typename T> TTMI_DEV float frag_sum(const uint4& f);
+template <> TTMI_DEV float frag_sum<bf16_t>(const uint4& f) {
+  const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s += __uint_as_float(w[i] << 16) + __uint_as_float(w[i] & 0xFFFF0000u);
+  return s;
+}
+template <> TTMI_DEV float frag_sum<float>(const uint4& f) {
+  return __uint_as_float(f.x) + __uint_as_float(f.y) + __uint_as_float(f.z) + __uint_as_float(f.w);
+}
 
 TTMI_DEV uint2 lds8(const char* p) { return *reinterpret_cast<const uint2*>(p); }
 TTMI_DEV uint2 lds_tr8(const char* p) {
@@ -147,6 +161,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float asum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) asum[i] = 0.f;
+  const bool do_asum = g.rowsum_a != nullptr && wn == 0;
 
   OA la;
   OB lb;
@@ -178,6 +196,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], bfr[j], af[i]);   // Cᵀ tile
+      if (do_asum) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asum[i] += frag_sum<T>(af[i]);
+      }
     }
     if (more) {
       char* nA = smem + (buf ^ 1) * STAGE;
@@ -192,6 +214,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   // lane holds C[m][n..n+3]: m = tile row + (lane&15), n = tile col + 4*(lane>>4)
   const bool first = blockIdx.z == 0;
   const int li = lane & 15, lg = lane >> 4;
+  if (do_asum) {                     // Σ over this split's k of A(m, k): reduce the 4 k-groups
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float v = asum[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int64_t m = m0 + wm * WTM + i * 16 + li;
+      if (lg == 0 && m < g.M) atomicAdd(g.rowsum_a + m, v);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int64_t n = n0 + wn * WTN + j * 16 + 4 * lg;
@@ -353,6 +385,7 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   a.residual = d->residual; a.ld_res = d->ld_res;
   a.colsum = d->colsum;
   a.k_split = kspl;
+  a.rowsum_a = d->rowsum_a;
   const int cbytes = a.c_f32 ? 4 : 2;
   a.vec = (d->ldc % 4 == 0) && ((uintptr_t)d->C % (4 * cbytes) == 0) &&
           (!d->residual || (d->ld_res % 4 == 0 && (uintptr_t)d->residual % 16 == 0)) &&

@@ -39,7 +39,23 @@ __global__ void scatter_add_rows_kernel(int B, int D, const float* __restrict__ 
   for (int c = threadIdx.x; c < D; c += blockDim.x) dst[r * D + c] += src[(int64_t)b * D + c];
 }
 
-// One 64-lane wave per (b, h); lane j owns key j (L <= 64).
+// Dot product of an LDS fp32 vector with a global row of Dh (multiple of 8 for bf16 / 4 for
+// f32) elements, loaded 16 bytes at a time.
+template <typename T>
+TTMI_DEV float dot_row(const float* __restrict__ v, const T* __restrict__ row, int Dh) {
+  constexpr int E = 16 / sizeof(T);
+  float acc = 0.f;
+  for (int d0 = 0; d0 < Dh; d0 += E) {
+    const uint4 q = *reinterpret_cast<const uint4*>(row + d0);
+    const T* e = reinterpret_cast<const T*>(&q);
+#pragma unroll
+    for (int k = 0; k < E; ++k) acc += v[d0 + k] * ldf<T>(e, k);
+  }
+  return acc;
+}
+
+// One 64-lane wave per (b, h); lane j owns key j (L <= 64) for the score/softmax phase;
+// lanes own head-dim elements for the P·V / dS·K reductions and the row stores.
 template <typename T>
 __global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int Dh,
                                                         const T* __restrict__ qkv,
@@ -58,13 +74,7 @@ __global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int
   if (j < Dh) sq[j] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + j);
   __syncthreads();
   const bool ok = j < L && j <= p && kvalid[(int64_t)b * L + j] != 0;
-  float s = -INFINITY;
-  if (ok) {
-    const T* kr = seq + (int64_t)j * ld + D;
-    float acc = 0.f;
-    for (int d = 0; d < Dh; ++d) acc += sq[d] * ldf<T>(kr, d);
-    s = acc * scale;
-  }
+  const float s = ok ? dot_row<T>(sq, seq + (int64_t)j * ld + D, Dh) * scale : -INFINITY;
   const float m = wave_max(s);
   const float e = (ok && m != -INFINITY) ? expf(s - m) : 0.f;
   const float sum = wave_sum(e);
@@ -90,8 +100,8 @@ __global__ __launch_bounds__(64) void mha_q1_bwd_kernel(int B, int L, int H, int
                                                         const float* __restrict__ lse,
                                                         const T* __restrict__ dctx, DropParams dp,
                                                         T* __restrict__ dqkv, float scale) {
-  __shared__ float sq[64], sdo[64], sds[64];
-  const int j = threadIdx.x;
+  __shared__ float sq[64], sdo[64], sds[64], spd[64];
+  const int t = threadIdx.x;
   const int bh = blockIdx.x, b = bh / H, h = bh % H;
   const int D = H * Dh;
   const int64_t ld = 3LL * D;
@@ -99,45 +109,45 @@ __global__ __launch_bounds__(64) void mha_q1_bwd_kernel(int B, int L, int H, int
   const int p = (int)(r - (int64_t)b * L);
   const T* seq = qkv + (int64_t)b * L * ld + (int64_t)h * Dh;
   T* dseq = dqkv + (int64_t)b * L * ld + (int64_t)h * Dh;
-  if (j < Dh) {
-    sq[j] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + j);
-    sdo[j] = ldf<T>(dctx, (int64_t)b * D + (int64_t)h * Dh + j);
+  if (t < Dh) {
+    sq[t] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + t);
+    sdo[t] = ldf<T>(dctx, (int64_t)b * D + (int64_t)h * Dh + t);
   }
   __syncthreads();
+  // ---- per key j = t: probabilities and gradients of the scores
+  const int j = t;
   const bool ok = j < L && j <= p && kvalid[(int64_t)b * L + j] != 0;
-  const float l = lse[bh];
   const DropKeys dk = resolve_drop(dp);
   float pj = 0.f, dP = 0.f, keep = 1.f;
   if (ok) {
-    const T* kr = seq + (int64_t)j * ld + D;
-    const T* vr = seq + (int64_t)j * ld + 2 * D;
-    float sd = 0.f, dv = 0.f;
-    for (int d = 0; d < Dh; ++d) {
-      sd += sq[d] * ldf<T>(kr, d);
-      dv += sdo[d] * ldf<T>(vr, d);
-    }
-    pj = expf(sd * scale - l);
+    const float sd = dot_row<T>(sq, seq + (int64_t)j * ld + D, Dh);
+    const float dv = dot_row<T>(sdo, seq + (int64_t)j * ld + 2 * D, Dh);
+    pj = expf(sd * scale - lse[bh]);
     if (dk.on) keep = drop_keep(dk, (uint32_t)((((int64_t)bh * L) + p) * L + j)) ? dk.scale : 0.f;
     dP = dv * keep;
   }
   const float Dsum = wave_sum(pj * dP);
-  const float ds = pj * (dP - Dsum) * scale;
-  const float pd = pj * keep;
-  sds[j] = ds;
-  if (j < L) {
-    T* row = dseq + (int64_t)j * ld;
-    for (int d = 0; d < Dh; ++d) {
-      if (j != p) stf<T>(row, d, 0.f);                    // Q slice of non-query rows
-      stf<T>(row + D, d, ds * sq[d]);                      // dK_j = dS_j q
-      stf<T>(row + 2 * D, d, pd * sdo[d]);                 // dV_j = Pd_j dO
+  sds[j] = pj * (dP - Dsum) * scale;
+  spd[j] = pj * keep;
+  __syncthreads();
+  // ---- row stores, lanes over the head dim (coalesced): dK_j = dS_j q, dV_j = Pd_j dO,
+  //      Q slice zero except the query row; dQ_p = Σ_j dS_j k_j
+  const int nl = 64 / Dh >= 2 ? 2 : 1;           // rows handled per pass (Dh <= 32: two)
+  const int sub = t / Dh, d = t % Dh;
+  if (sub < nl) {
+    const float qd = sq[d], od = sdo[d];
+    for (int jj = sub; jj < L; jj += nl) {
+      T* row = dseq + (int64_t)jj * ld;
+      if (jj != p) stf<T>(row, d, 0.f);
+      stf<T>(row + D, d, sds[jj] * qd);
+      stf<T>(row + 2 * D, d, spd[jj] * od);
     }
   }
-  __syncthreads();
-  if (j < Dh) {
+  if (t < Dh) {
     float acc = 0.f;
     const int last = min(p, L - 1);
-    for (int k = 0; k <= last; ++k) acc += sds[k] * ldf<T>(seq + (int64_t)k * ld + D, j);
-    stf<T>(dseq + (int64_t)p * ld, j, acc);               // dQ_p = Σ dS_j k_j
+    for (int k = 0; k <= last; ++k) acc += sds[k] * ldf<T>(seq + (int64_t)k * ld + D, t);
+    stf<T>(dseq + (int64_t)p * ld, t, acc);
   }
 }
 
@@ -170,8 +180,9 @@ extern "C" int ttmi_mha_q1_fwd(int dtype, int B, int L, int H, int Dh, const voi
                                const int64_t* key_valid, const int32_t* rows, float drop_p,
                                const uint64_t* drop_seed, void* ctx, float* lse, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_fwd: bad dtype");
-  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64,
-               "ttmi_mha_q1_fwd: need L <= 64, Dh <= 64");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0,
+               "ttmi_mha_q1_fwd: need L <= 64, Dh <= 64, Dh %% 8 == 0");
+  TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "ttmi_mha_q1_fwd: qkv must be 16-byte aligned");
   TTMI_REQUIRE(qkv && key_valid && rows && ctx && lse, "ttmi_mha_q1_fwd: null argument");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
                "ttmi_mha_q1_fwd: bad dropout");
@@ -192,8 +203,9 @@ extern "C" int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const voi
                                const void* dctx, float drop_p, const uint64_t* drop_seed,
                                void* dqkv, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_bwd: bad dtype");
-  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64,
-               "ttmi_mha_q1_bwd: need L <= 64, Dh <= 64");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0,
+               "ttmi_mha_q1_bwd: need L <= 64, Dh <= 64, Dh %% 8 == 0");
+  TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "ttmi_mha_q1_bwd: qkv must be 16-byte aligned");
   TTMI_REQUIRE(qkv && key_valid && rows && lse && dctx && dqkv, "ttmi_mha_q1_bwd: null argument");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
                "ttmi_mha_q1_bwd: bad dropout");

@@ -44,10 +44,10 @@ __global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16_t* __
 }
 
 // AdamW (torch.optim.AdamW, non-amsgrad, maximize=False) over flat fp32 buffers.
-__global__ void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+__global__ void adamw_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v,
                              bf16_t* __restrict__ pb, const double* __restrict__ hyper,
-                             const int32_t* __restrict__ step) {
+                             const int32_t* __restrict__ step, int zero_grad) {
   // scalar terms in double, as torch computes them on the host (then used as f32 scalars)
   const double lr = hyper[0], b1d = hyper[1], b2d = hyper[2], wd = hyper[4];
   const double t = (double)step[0];
@@ -75,6 +75,7 @@ __global__ void adamw_kernel(int64_t n, float* __restrict__ p, const float* __re
       *reinterpret_cast<float4*>(p + i) = pp;
       *reinterpret_cast<float4*>(m + i) = mm;
       *reinterpret_cast<float4*>(v + i) = vv;
+      if (zero_grad) *reinterpret_cast<float4*>(g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
       if (pb) {
         ushort4 o;
         o.x = f2bf(pp.x); o.y = f2bf(pp.y); o.z = f2bf(pp.z); o.w = f2bf(pp.w);
@@ -88,6 +89,7 @@ __global__ void adamw_kernel(int64_t n, float* __restrict__ p, const float* __re
         v[j] = v[j] * b2 + b2c * (gj * gj);
         pj -= step_size * (m[j] / (sqrtf(v[j]) / bc2_sqrt + eps));
         p[j] = pj;
+        if (zero_grad) g[j] = 0.f;
         if (pb) pb[j] = f2bf(pj);
       }
     }
@@ -243,6 +245,32 @@ int64_t vec_rows_per_block(int64_t M, int N) {
   return std::max<int64_t>(rpb, rpp);
 }
 
+constexpr int MAX_COPIES = 16;
+struct CopyList {
+  char* dst[MAX_COPIES];
+  const char* src[MAX_COPIES];
+  int64_t bytes[MAX_COPIES];
+  int n;
+};
+
+// blockIdx.y = tensor; 16-byte vectors when both ends are aligned, bytes otherwise.
+__global__ void batch_copy_kernel(CopyList cl) {
+  const int t = blockIdx.y;
+  char* dst = cl.dst[t];
+  const char* src = cl.src[t];
+  const int64_t nb = cl.bytes[t];
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+    const int64_t nv = nb / 16;
+    for (int64_t i = tid; i < nv; i += stride)
+      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (int64_t i = nv * 16 + tid; i < nb; i += stride) dst[i] = src[i];
+  } else {
+    for (int64_t i = tid; i < nb; i += stride) dst[i] = src[i];
+  }
+}
+
 int grid_for(int64_t n, int per_thread) {
   int64_t b = (n + 256 * per_thread - 1) / (256 * per_thread);
   return (int)std::min<int64_t>(std::max<int64_t>(b, 1), 4096);
@@ -259,17 +287,37 @@ extern "C" int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hi
   return ttmi_check_launch("ttmi_cast_f32_bf16");
 }
 
-extern "C" int ttmi_adamw(int64_t n, float* p, const float* g, float* m, float* v,
+extern "C" int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v,
                           uint16_t* p_bf16, const double* hyper, const int32_t* step,
-                          hipStream_t s) {
+                          int zero_grad, hipStream_t s) {
   TTMI_REQUIRE(n >= 0 && p && g && m && v && hyper && step, "ttmi_adamw: null argument");
   TTMI_REQUIRE(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 &&
                ((uintptr_t)v & 15) == 0 && ((uintptr_t)p_bf16 & 7) == 0,
                "ttmi_adamw: buffers must be 16-B aligned (bf16 mirror 8-B)");
   if (n == 0) return TTMI_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, n, p, g, m, v, p_bf16,
-                     hyper, step);
+                     hyper, step, zero_grad);
   return ttmi_check_launch("ttmi_adamw");
+}
+
+extern "C" int ttmi_batch_copy(int n, void* const* dst, const void* const* src,
+                               const int64_t* nbytes, hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && n <= MAX_COPIES, "ttmi_batch_copy: at most %d tensors", MAX_COPIES);
+  if (n == 0) return TTMI_OK;
+  TTMI_REQUIRE(dst && src && nbytes, "ttmi_batch_copy: null argument");
+  CopyList cl;
+  int64_t mx = 0;
+  for (int i = 0; i < n; ++i) {
+    TTMI_REQUIRE(nbytes[i] >= 0 && (nbytes[i] == 0 || (dst[i] && src[i])), "ttmi_batch_copy: bad entry %d", i);
+    cl.dst[i] = static_cast<char*>(dst[i]);
+    cl.src[i] = static_cast<const char*>(src[i]);
+    cl.bytes[i] = nbytes[i];
+    mx = std::max(mx, nbytes[i]);
+  }
+  cl.n = n;
+  const int gx = (int)std::min<int64_t>(std::max<int64_t>((mx / 16 + 255) / 256, 1), 256);
+  hipLaunchKernelGGL(batch_copy_kernel, dim3(gx, n), dim3(256), 0, s, cl);
+  return ttmi_check_launch("ttmi_batch_copy");
 }
 
 extern "C" int ttmi_step_inc(int32_t* step, hipStream_t s) {

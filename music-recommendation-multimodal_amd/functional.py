@@ -224,16 +224,16 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
     f32 = dict(device=dev, dtype=torch.float32)
     # ---- user fusion MLP (user_tower.py:51-57, :142)
     du_c = torch.empty(B, D, device=dev, dtype=dt)
-    ops.dropout_bwd(du, du_c, grads["fusion_layer.3.bias"])
-    ops.linear_dw(du_c, st.az, grads["fusion_layer.3.weight"])
+    ops.dropout_bwd(du, du_c, None)
+    ops.linear_dw(du_c, st.az, grads["fusion_layer.3.weight"], grads["fusion_layer.3.bias"])
     daz = torch.empty(B, D, **f32)
     ops.linear_dx(du_c, W["fusion_layer.3.weight"], daz)
     dz = torch.empty(B, D, **f32)
     ops.layernorm_bwd(daz, st.z, st.mz, st.rz, P["fusion_layer.1.weight"], dz,
                       grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"], gate=st.az)
     dz_c = torch.empty(B, D, device=dev, dtype=dt)
-    ops.dropout_bwd(dz, dz_c, grads["fusion_layer.0.bias"])
-    ops.linear_dw(dz_c, st.comb, grads["fusion_layer.0.weight"])
+    ops.dropout_bwd(dz, dz_c, None)
+    ops.linear_dw(dz_c, st.comb, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
     dcomb = torch.empty(B, st.comb.shape[1], **f32)
     ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dcomb)
     gathered = cfg.prune_last and cfg.n_layers > 0
@@ -251,22 +251,20 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         drows = s.rows
         F_ = W[pre + "linear1.weight"].shape[0]
         dy2 = torch.empty(R, D, device=dev, dtype=dt)
-        ops.dropout_bwd(dx, dy2, grads[pre + "linear2.bias"], _drop(cfg, seeds, site_drop2(i)),
-                        drop_rows=drows)
-        ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"])
+        ops.dropout_bwd(dx, dy2, None, _drop(cfg, seeds, site_drop2(i)), drop_rows=drows)
+        ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"], grads[pre + "linear2.bias"])
         dz1 = torch.empty(R, F_, device=dev, dtype=dt)
-        ops.linear_dx(dy2, W[pre + "linear2.weight"], dz1, gate=s.h, gate_scale=_scale(p),
-                      colsum=grads[pre + "linear1.bias"])
-        ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"])
+        ops.linear_dx(dy2, W[pre + "linear2.weight"], dz1, gate=s.h, gate_scale=_scale(p))
+        ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"], grads[pre + "linear1.bias"])
         da2 = torch.empty(R, D, **f32)
         ops.linear_dx(dz1, W[pre + "linear1.weight"], da2)
         dx1 = torch.empty(R, D, **f32)
         ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
                           grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
         dy1 = torch.empty(R, D, device=dev, dtype=dt)
-        ops.dropout_bwd(dx1, dy1, grads[pre + "self_attn.out_proj.bias"],
-                        _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
-        ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"])
+        ops.dropout_bwd(dx1, dy1, None, _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
+        ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"],
+                      grads[pre + "self_attn.out_proj.bias"])
         dctx = torch.empty(R, D, device=dev, dtype=dt)
         ops.linear_dx(dy1, W[pre + "self_attn.out_proj.weight"], dctx)
         dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
@@ -276,8 +274,8 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         else:
             ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
                         _drop(cfg, seeds, site_attn(i)))
-        ops.colsum(dqkv, grads[pre + "self_attn.in_proj_bias"])
-        ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"])
+        ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"],
+                      grads[pre + "self_attn.in_proj_bias"])
         da1 = torch.empty(M, D, **f32)
         ops.linear_dx(dqkv, W[pre + "self_attn.in_proj_weight"], da1)
         dxn = torch.empty(M, D, **f32)
@@ -357,8 +355,8 @@ def item_fusion_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, d
     ops.layernorm_bwd(dout, st.y2, st.m5, st.r5, P["fusion_layer.5.weight"], dy2,
                       grads["fusion_layer.5.weight"], grads["fusion_layer.5.bias"])
     dy2_c = torch.empty(B, D, device=dev, dtype=dt)
-    ops.dropout_bwd(dy2, dy2_c, grads["fusion_layer.4.bias"])
-    ops.linear_dw(dy2_c, st.y1, grads["fusion_layer.4.weight"])
+    ops.dropout_bwd(dy2, dy2_c, None)
+    ops.linear_dw(dy2_c, st.y1, grads["fusion_layer.4.weight"], grads["fusion_layer.4.bias"])
     H1 = st.z.shape[1]
     dy1 = torch.empty(B, H1, **f32)
     ops.linear_dx(dy2_c, W["fusion_layer.4.weight"], dy1)
@@ -368,8 +366,8 @@ def item_fusion_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, d
                       grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"],
                       gate_scale=_scale(pd), gated=True)
     dz_c = torch.empty(B, H1, device=dev, dtype=dt)
-    ops.dropout_bwd(dz, dz_c, grads["fusion_layer.0.bias"])
-    ops.linear_dw(dz_c, st.modal, grads["fusion_layer.0.weight"])
+    ops.dropout_bwd(dz, dz_c, None)
+    ops.linear_dw(dz_c, st.modal, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
     if dmodal is not None:
         ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dmodal)
 

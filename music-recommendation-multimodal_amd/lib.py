@@ -37,6 +37,7 @@ class GemmDesc(ctypes.Structure):
         ("colsum", c_p),
         ("split_k", c_i),
         ("drop_rows", c_p),
+        ("rowsum_a", c_p),
     ]
 
 
@@ -65,7 +66,8 @@ SIGNATURES = {
     "ttmi_infonce_workspace": (c_i64, [c_i, c_i]),
     "ttmi_infonce_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_infonce_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p]),
-    "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),
+    "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_step_inc": (c_i, [c_p, c_p]),
     "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_p]),
     "ttmi_cast_f32_bf16": (c_i, [c_i64, c_p, c_p, c_p]),

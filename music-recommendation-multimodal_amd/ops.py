@@ -50,7 +50,8 @@ def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a
          bias: Optional[Tensor] = None, act: int = 0, drop: Drop = NO_DROP, ld_drop: int = 0,
          gate: Optional[Tensor] = None, ld_gate: int = 0, gate_scale: float = 1.0,
          residual: Optional[Tensor] = None, ld_res: int = 0, colsum: Optional[Tensor] = None,
-         split_k: int = 1, drop_rows: Optional[Tensor] = None) -> Tensor:
+         split_k: int = 1, drop_rows: Optional[Tensor] = None,
+         rowsum_a: Optional[Tensor] = None) -> Tensor:
     _dev(A, B, C)
     if A.dtype != B.dtype:
         raise TypeError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
@@ -70,6 +71,7 @@ def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a
     d.colsum = _p(colsum)
     d.split_k = split_k
     d.drop_rows = _p(drop_rows)
+    d.rowsum_a = _p(rowsum_a)
     call("ttmi_gemm", ctypes.byref(d), _s())
     return C
 
@@ -95,12 +97,14 @@ def linear_dx(dy: Tensor, w: Tensor, out: Tensor, *, gate: Optional[Tensor] = No
                 gate=gate, ld_gate=K, gate_scale=gate_scale, colsum=colsum)
 
 
-def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, split_k: int = 0) -> Tensor:
-    """gw[N,K] += dy[M,N]ᵀ · x[M,K]  (nn.Linear weight grad, accumulated, split-K)."""
+def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
+              split_k: int = 0) -> Tensor:
+    """gw[N,K] += dy[M,N]ᵀ · x[M,K]; gb[N] += Σ_m dy[m,:] (nn.Linear weight and bias grads,
+    accumulated, split-K)."""
     M, N = dy.shape
     K = x.shape[1]
     return gemm(dy, x, gw, N, K, M, lda=N, a_kmajor=False, ldb=K, b_kmajor=False, ldc=K,
-                accumulate=True, split_k=split_k)
+                accumulate=True, split_k=split_k, rowsum_a=gb)
 
 
 # ----------------------------------------------------------------------------- norms
@@ -221,8 +225,21 @@ def infonce_bwd(u_hat: Tensor, i_hat: Tensor, norms: Tensor, logits: Tensor, lse
 
 # ----------------------------------------------------------------------------- misc
 def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
-          step: Tensor):
-    call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step), _s())
+          step: Tensor, zero_grad: bool = False):
+    call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
+         int(zero_grad), _s())
+
+
+def batch_copy(dsts, srcs):
+    """One launch copying each srcs[i] into dsts[i] (same byte sizes)."""
+    n = len(dsts)
+    D = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dsts])
+    S = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+    for d, s_ in zip(dsts, srcs):
+        if d.numel() * d.element_size() != s_.numel() * s_.element_size():
+            raise ValueError("batch_copy: size mismatch")
+    N = (ctypes.c_int64 * n)(*[t.numel() * t.element_size() for t in dsts])
+    call("ttmi_batch_copy", n, D, S, N, _s())
 
 
 def step_inc(step: Tensor):

@@ -198,7 +198,7 @@ class TrainStep:
             ops.cast_bf16(self.flat.data, self.flat.mirror)
 
     def _fwd_bwd(self, b: Dict[str, Tensor]) -> None:
-        self.flat.grad.zero_()
+        # the gradient buffer is zero here: it starts zeroed and the fused AdamW clears it
         ops.step_inc(self.step_t)
         seeds = None
         if self.ucfg.p_drop > 0 or self.p_item > 0:
@@ -219,7 +219,8 @@ class TrainStep:
 
     def _update(self) -> None:
         f = self.flat
-        ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t)
+        ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
+                  zero_grad=True)
 
     def _body(self, b: Dict[str, Tensor]) -> None:
         self._fwd_bwd(b)
@@ -231,8 +232,14 @@ class TrainStep:
         if self.static is None:
             self.static = {k: torch.empty_like(batch[k], device=self.device)
                            for k in self.INPUT_KEYS if k in batch}
-        for k, t in self.static.items():
-            t.copy_(batch[k], non_blocking=True)
+        keys = list(self.static)
+        srcs = [batch[k] for k in keys]
+        if all(t.is_cuda and t.is_contiguous() and t.dtype == self.static[k].dtype
+               for k, t in zip(keys, srcs)):
+            ops.batch_copy([self.static[k] for k in keys], srcs)   # one launch
+        else:
+            for k, t in zip(keys, srcs):
+                self.static[k].copy_(t, non_blocking=True)
         return self.static
 
     def _state(self):

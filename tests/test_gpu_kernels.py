@@ -90,9 +90,11 @@ def test_gemm_accumulate_split_k(gpu_pkg, split):
     dy = torch.randn(K, M, generator=g).to(torch.bfloat16)   # [tokens, out]
     x = torch.randn(K, N, generator=g).to(torch.bfloat16)    # [tokens, in]
     gw = torch.ones(M, N, device=DEV)
-    ops.linear_dw(dy.to(DEV), x.to(DEV), gw, split_k=split)
+    gb = torch.full((M,), 2.0, device=DEV)
+    ops.linear_dw(dy.to(DEV), x.to(DEV), gw, gb, split_k=split)
     expect = 1.0 + dy.float().t() @ x.float()
     assert rel(gw, expect) < 5e-5
+    assert rel(gb, 2.0 + dy.float().sum(0)) < 5e-5       # bias grad from the A row-sums
 
 
 # ------------------------------------------------------------------------------ LayerNorm
@@ -343,10 +345,21 @@ def test_adamw_matches_torch_semantics(gpu_pkg):
         gr = torch.randn(n, generator=g)
         ref.adamw_(params, {"w": gr}, state, lr=1e-3)
         ops.step_inc(step)
-        ops.adamw(pd, gr.to(DEV), m, v, mirror, hyper, step)
+        gd = gr.to(DEV)
+        ops.adamw(pd, gd, m, v, mirror, hyper, step, zero_grad=True)
+        assert gd.abs().max().item() == 0.0
     assert rel(pd, params["w"]) < 2e-6
     assert torch.equal(mirror.cpu(), pd.cpu().to(torch.bfloat16))
     assert int(step) == 5
+
+
+def test_batch_copy(gpu_pkg):
+    srcs = [torch.randint(0, 100, (513, 50), device=DEV), torch.randn(7, 3, device=DEV),
+            torch.randn(1000, 512, device=DEV)[:, 1:].contiguous()]
+    dsts = [torch.empty_like(t) for t in srcs]
+    gpu_pkg.ops.batch_copy(dsts, srcs)
+    for a, b in zip(dsts, srcs):
+        assert torch.equal(a, b)
 
 
 def test_dropout_seed_kernel_matches_host(gpu_pkg):
