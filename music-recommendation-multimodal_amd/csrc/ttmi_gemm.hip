@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   float asum[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) asum[i] = 0.f;
-  const bool do_asum = g.rowsum_a != nullptr && wn == 0;
+  const bool do_asum = g.rowsum_a != nullptr && wn == 0 && blockIdx.x == 0;   // one N-tile
 
   OA la;
   OB lb;
