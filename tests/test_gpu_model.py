@@ -201,7 +201,9 @@ def test_item_fusion_vs_reference(gpu_pkg, dtype):
     grads = dict(m.named_parameters())
     for k, gref in sub(z, "g/").items():
         if k.startswith("fusion_layer.0.bias"):      # exactly zero in math (BN follows)
-            assert grads[k].grad.abs().max().item() < 1e-3 * max(1.0, np.abs(gref).max())
+            # fp32: ~0; bf16: the row sum of a bf16-rounded dy (sums to 0 in exact math)
+            tol = 1e-3 if dtype == torch.float32 else 3e-2
+            assert grads[k].grad.abs().max().item() < tol * max(1.0, np.abs(gref).max())
             continue
         if dtype == torch.float32:
             assert rel(grads[k].grad, gref) < 1e-4, (k, rel(grads[k].grad, gref))
