@@ -23,6 +23,10 @@
 // Epilogue order (ttmi.h): bias -> act -> dropout -> gate -> colsum -> residual -> store.
 #include "ttmi_common.h"
 
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
@@ -301,6 +305,225 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   }
 }
 
+
+// ------------------------------------------------------------ weight-gradient GEMM (bf16)
+// C[m,n] += alpha * Σ_r A[r,m] B[r,n]: A = dY [R][lda], B = X [R][ldb], both row-major with
+// the reduction over rows (R = B*L tokens), C fp32.  This shape (output <= 512 x 512, R up
+// to 25,600) is latency-bound in the generic kernel: one 16 KB stage in flight per CU.  Here:
+//  * each workgroup owns a BM x BN tile and a contiguous row split; splits of one tile are
+//    combined with fp32 atomics, reshaped through LDS so every atomic wave-instruction adds
+//    256 contiguous bytes;
+//  * rows are staged by LDS-DMA (buffer_load ... lds, 16 B/lane) into an NS-deep ring of
+//    64-row stages, NS-1 stages in flight; the buffer descriptor's range is the split, so
+//    rows past it read as zero;
+//  * the LDS image is [64 k][W cols] unpadded with 32-byte chunks XOR-swizzled by k (the DMA
+//    destination is lane-linear, so the swizzle goes on the source address); the 8 k-rows a
+//    half-wave's ds_read_b64_tr_b16 touches land in 8 distinct bank windows;
+//  * splits of one row range are grouped on one XCD (blockIdx % 8) so the tiles that re-read
+//    the same rows share that XCD's L2.
+struct WgradArgs {
+  int64_t M, N, R;
+  const char* A; int64_t lda;
+  const char* B; int64_t ldb;
+  float* C; int64_t ldc;
+  float alpha;
+  float* rowsum_a;
+  int64_t rows_per_split;   // multiple of 64
+  int tiles_m, tiles_n, splits, xcd_remap;
+};
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+// Raw buffer descriptor over [base, base + bytes): loads past the end return zero.
+TTMI_DEV i32x4_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xFFFFu));
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+// One 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... lds): lane l's bytes land at
+// lds + 16*l.  Issued from asm so hipcc's waitcnt pass does not see an LDS write it would
+// drain with vmcnt(0) before every ds_read; callers count vmcnt themselves.
+TTMI_DEV void dma16(const i32x4_t& rs, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rs), "s"(__builtin_amdgcn_readfirstlane((int)lds))
+               : "memory");
+}
+
+TTMI_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p);
+}
+
+template <int W>
+struct WImg {
+  static constexpr int PB = W * 2;                       // k-row pitch, bytes
+  static constexpr int CPR = PB / 32;                    // 32-byte chunks per k-row
+  static constexpr int RPB = PB >= 256 ? 1 : 256 / PB;   // k-rows per 256-byte bank row
+  static constexpr int BYTES = 64 * PB;
+  static constexpr int INSTR = BYTES / 1024;             // DMA wave-instructions per stage
+  static TTMI_DEV int swz(int k) { return (k / RPB) % CPR; }
+
+  // Issue this wave's share of one 64-row stage: rows [r0, r0+64) of the descriptor's range,
+  // into the LDS image at byte address `img` (wave-uniform).
+  static TTMI_DEV void issue(const i32x4_t& rs, int64_t ld, int col0, int r0, uint32_t img,
+                             int wave, int lane) {
+    static_assert(INSTR % 4 == 0, "stage must split evenly over 4 waves");
+#pragma unroll
+    for (int t = 0; t < INSTR / 4; ++t) {
+      const int ii = wave + 4 * t;
+      const int o = ii * 1024 + lane * 16;
+      const int k = o / PB, pb = o % PB;
+      const int lc = (pb >> 5) ^ swz(k);
+      const uint32_t voff = (uint32_t)((int64_t)(r0 + k) * ld * 2 + col0 * 2 + lc * 32 + (pb & 16));
+      dma16(rs, voff, img + ii * 1024);
+    }
+  }
+
+  // MFMA fragment of the 16 columns at `row0` for 32-k chunk `c` (same k-permutation as
+  // Operand<bf16, *, false>::frag).
+  static TTMI_DEV uint4 frag(const char* img, int row0, int c, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    const int k = c * 32 + 4 * g + (i >> 2);
+    const char* p = img + k * PB + ((((row0 >> 4)) ^ swz(k)) << 5) + 8 * (i & 3);
+    const uint2 lo = lds_tr8(p), hi = lds_tr8(p + 16 * PB);
+    return make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+};
+
+template <int N_>
+TTMI_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
+// This wave's DMAs but the N_ youngest have landed and its LDS reads have returned; then
+// the workgroup barrier (one asm statement: no memory access moves across it).
+template <int N_>
+TTMI_DEV void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N_) : "memory");
+}
+
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
+  using IA = WImg<BM>;
+  using IB = WImg<BN>;
+  constexpr int STAGE = IA::BYTES + IB::BYTES;
+  constexpr int P = (IA::INSTR + IB::INSTR) / 4;          // DMA instructions per wave per stage
+  constexpr int TP = BN + 16;                              // epilogue fp32 tile pitch (floats)
+  static_assert(NS * STAGE >= BM * TP * 4, "epilogue tile must fit the ring");
+  static_assert((NS - 2) * P <= 63, "vmcnt range");
+  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+  __shared__ __attribute__((aligned(1024))) char ring[NS * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int T = g.tiles_m * g.tiles_n;
+  int tile, split;
+  if (g.xcd_remap) {          // splits % 8 == 0: one XCD per (split mod 8)
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    tile = j % T;
+    split = (j / T) * 8 + x;
+  } else {
+    tile = blockIdx.x % T;
+    split = blockIdx.x / T;
+  }
+  const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * g.rows_per_split;
+  if (kbeg >= g.R) return;
+  const int rows = (int)min(g.R - kbeg, g.rows_per_split);
+  const int nst = (rows + 63) >> 6;
+  const i32x4_t ra = make_rsrc(g.A + kbeg * g.lda * 2, (uint32_t)(rows * g.lda * 2));
+  const i32x4_t rb = make_rsrc(g.B + kbeg * g.ldb * 2, (uint32_t)(rows * g.ldb * 2));
+  const uint32_t ring_lds = lds_addr(ring);
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float asum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) asum[i] = 0.f;
+  const bool do_asum = g.rowsum_a != nullptr && wn == 0 && tn == 0;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) {
+    if (s < nst) {
+      IA::issue(ra, g.lda, (int)m0, s * 64, ring_lds + s * STAGE, wave, lane);
+      IB::issue(rb, g.ldb, (int)n0, s * 64, ring_lds + s * STAGE + IA::BYTES, wave, lane);
+    }
+  }
+  for (int t = 0; t < nst; ++t) {
+    // stage t landed for every wave; every wave is done reading slot (t-1) % NS
+    if (t + NS - 2 < nst) wait_vm_barrier<(NS - 2) * P>();
+    else wait_vm_barrier<0>();
+    const int tn_ = t + NS - 1;
+    if (tn_ < nst) {
+      const uint32_t dst = ring_lds + (tn_ % NS) * STAGE;
+      IA::issue(ra, g.lda, (int)m0, tn_ * 64, dst, wave, lane);
+      IB::issue(rb, g.ldb, (int)n0, tn_ * 64, dst + IA::BYTES, wave, lane);
+    }
+    const char* sA = ring + (t % NS) * STAGE;
+    const char* sB = sA + IA::BYTES;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = IA::frag(sA, wm * WTM + i * 16, c, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = IB::frag(sB, wn * WTN + j * 16, c, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Mma<bf16_t>::run(acc[i][j], bfr[j], af[i]);
+      if (do_asum) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asum[i] += frag_sum<bf16_t>(af[i]);
+      }
+    }
+  }
+
+  const int li = lane & 15, lg = lane >> 4;
+  if (do_asum) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float v = asum[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int64_t m = m0 + wm * WTM + i * 16 + li;
+      if (lg == 0 && m < g.M) atomicAdd(g.rowsum_a + m, v);
+    }
+  }
+  // reshape through LDS: every atomic wave-instruction then covers 64 consecutive columns
+  wait_vm<0>();
+  __syncthreads();
+  float* tl = reinterpret_cast<float*>(ring);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int m = wm * WTM + i * 16 + li, n = wn * WTN + j * 16 + 4 * lg;
+      *reinterpret_cast<float4*>(tl + m * TP + n) =
+          make_float4(g.alpha * acc[i][j][0], g.alpha * acc[i][j][1], g.alpha * acc[i][j][2],
+                      g.alpha * acc[i][j][3]);
+    }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = wave; r < BM; r += 4) {
+    const int64_t m = m0 + r;
+    if (m >= g.M) break;
+#pragma unroll
+    for (int c0 = 0; c0 < BN; c0 += 64) {
+      const int64_t n = n0 + c0 + lane;
+      if (n < g.N) atomicAdd(g.C + m * g.ldc + n, tl[r * TP + c0 + lane]);
+    }
+  }
+}
+
 template <typename T, int BM, int BN>
 void launch_layout(const GemmArgs& a, bool ak, bool bk, dim3 grid, hipStream_t s) {
   if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, true>), grid, dim3(256), 0, s, a);
@@ -315,6 +538,77 @@ void launch_typed(const GemmArgs& a, bool ak, bool bk, int bm, int bn, dim3 grid
   else if (bm == 128) launch_layout<T, 128, 64>(a, ak, bk, grid, s);
   else if (bn == 128) launch_layout<T, 64, 128>(a, ak, bk, grid, s);
   else launch_layout<T, 64, 64>(a, ak, bk, grid, s);
+}
+
+
+// Weight-gradient dispatch (bf16, both operands row-major over the reduction, accumulate into
+// an fp32 C, no epilogue extras).
+bool wgrad_applies(const ttmi_gemm_desc* d) {
+  return d->dtype == TTMI_BF16 && !d->a_kmajor && !d->b_kmajor && d->c_mode == 1 &&
+         d->c_dtype == TTMI_F32 && !d->bias && !d->act && d->drop_p == 0.f && !d->gate &&
+         !d->residual && !d->colsum && !d->drop_rows;
+}
+
+
+// Tile / ring-depth choice: 64x64 tiles, 4-deep ring (64 KB LDS: two workgroups per CU).
+// Measured on MI355X (tools/wgrad_sweep.sh, R = 25,600): a CU ingests ~33 GB/s from the
+// Infinity Cache whether staged by LDS-DMA or registers and whatever the ring depth, so the
+// time is ~ re-read input bytes / (#CUs x 33 GB/s) + atomic bytes / 1.3 TB/s; 64x64 tiles
+// with ~1.1 workgroups per CU minimise that sum (128x128 tiles halve the reads but
+// quadruple the atomic bytes per workgroup).  TTMI_WGRAD="BMxBNxNS[:noremap]" overrides the
+// tile for tuning runs.
+struct WgradCfg { int bm, bn, ns, remap; };
+
+WgradCfg wgrad_cfg() {
+  static const WgradCfg cfg = [] {
+    WgradCfg c{64, 64, 4, 1};
+    if (const char* e = getenv("TTMI_WGRAD")) {
+      int bm = 0, bn = 0, ns = 0;
+      if (sscanf(e, "%dx%dx%d", &bm, &bn, &ns) == 3) c = WgradCfg{bm, bn, ns, 1};
+      if (strstr(e, "noremap")) c.remap = 0;
+    }
+    return c;
+  }();
+  return cfg;
+}
+
+template <int BM, int BN, int NS>
+int launch_wgrad_t(const ttmi_gemm_desc* d, int remap, hipStream_t stream) {
+  const int tiles_m = (int)((d->M + BM - 1) / BM), tiles_n = (int)((d->N + BN - 1) / BN);
+  const int T = tiles_m * tiles_n;
+  const int64_t stages = (d->K + 63) / 64;
+  int S = d->split_k;
+  if (S <= 0) {                              // ~320 workgroups, splits a multiple of 8
+    S = (320 / T + 4) & ~7;
+    if (S < 8) S = std::max(1, 320 / T);
+  }
+  S = (int)std::max<int64_t>(1, std::min<int64_t>(S, stages));
+  int64_t sps = (stages + S - 1) / S;        // stages per split
+  const int64_t ldmax = std::max(d->lda, d->ldb);
+  while (sps > 1 && sps * 64 * ldmax * 2 >= (int64_t)1 << 31) sps = (sps + 1) / 2;
+  TTMI_REQUIRE(sps * 64 * ldmax * 2 < ((int64_t)1 << 31), "ttmi_gemm: split range exceeds 2 GiB");
+  S = (int)((stages + sps - 1) / sps);
+  WgradArgs a;
+  a.M = d->M; a.N = d->N; a.R = d->K;
+  a.A = static_cast<const char*>(d->A); a.lda = d->lda;
+  a.B = static_cast<const char*>(d->B); a.ldb = d->ldb;
+  a.C = static_cast<float*>(d->C); a.ldc = d->ldc;
+  a.alpha = d->alpha;
+  a.rowsum_a = d->rowsum_a;
+  a.rows_per_split = sps * 64;
+  a.tiles_m = tiles_m; a.tiles_n = tiles_n; a.splits = S;
+  a.xcd_remap = remap && (S % 8 == 0);
+  const int64_t nwg = (int64_t)T * S;
+  TTMI_REQUIRE(nwg <= 2147483647LL, "ttmi_gemm: grid too large");
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, NS>), dim3((unsigned)nwg), dim3(256), 0, stream, a);
+  return ttmi_check_launch("ttmi_gemm");
+}
+
+int launch_wgrad(const ttmi_gemm_desc* d, hipStream_t stream) {
+  const WgradCfg c = wgrad_cfg();
+  if (c.bm == 128 && c.bn == 128) return launch_wgrad_t<128, 128, 4>(d, c.remap, stream);
+  if (c.ns == 8) return launch_wgrad_t<64, 64, 8>(d, c.remap, stream);
+  return launch_wgrad_t<64, 64, 4>(d, c.remap, stream);
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -344,6 +638,8 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   TTMI_REQUIRE(d->drop_p == 0.f || d->drop_seed, "ttmi_gemm: dropout needs a seed pointer");
   TTMI_REQUIRE(!d->gate || d->ld_gate >= d->N, "ttmi_gemm: ld_gate < N");
   TTMI_REQUIRE(!d->residual || d->ld_res >= d->N, "ttmi_gemm: ld_res < N");
+
+  if (wgrad_applies(d)) return launch_wgrad(d, stream);
 
   const int bke = 128 / es;
   int bm, bn;

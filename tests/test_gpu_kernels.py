@@ -97,6 +97,29 @@ def test_gemm_accumulate_split_k(gpu_pkg, split):
     assert rel(gb, 2.0 + dy.float().sum(0)) < 5e-5       # bias grad from the A row-sums
 
 
+@pytest.mark.parametrize("M,N,R,split,pad", [
+    (384, 128, 25600, 0, 0), (128, 512, 25600, 0, 0), (128, 128, 25600, 0, 64),
+    (176, 128, 512, 0, 0), (72, 200, 1000, 0, 8), (512, 512, 512, 0, 0),
+    (64, 64, 100, 3, 0), (128, 64, 4096, 8, 0), (136, 72, 777, 16, 32), (8, 8, 1, 0, 0)])
+def test_gemm_weight_grad(gpu_pkg, M, N, R, split, pad):
+    """Weight-gradient GEMM (LDS-DMA ring kernel): gw[M,N] += alpha dyᵀ x over R rows, bias
+    row sums; partial tiles, row tails, strided operands, explicit splits."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(M * 7 + N + R)
+    dy_full = torch.randn(R, M + 2 * pad, generator=g).to(torch.bfloat16).to(DEV)
+    x_full = torch.randn(R, N + pad, generator=g).to(torch.bfloat16).to(DEV)
+    dy = dy_full[:, pad:pad + M]
+    x = x_full[:, :N]
+    gw = torch.full((M, N), 0.5, device=DEV)
+    gb = torch.full((M,), -1.0, device=DEV)
+    ops.gemm(dy, x, gw, M, N, R, lda=M + 2 * pad, a_kmajor=False, ldb=N + pad, b_kmajor=False,
+             ldc=N, accumulate=True, alpha=0.75, split_k=split, rowsum_a=gb)
+    torch.cuda.synchronize()
+    expect = 0.5 + 0.75 * (dy.float().t() @ x.float())
+    assert rel(gw, expect) < 5e-5, rel(gw, expect)
+    assert rel(gb, -1.0 + dy.float().sum(0)) < 5e-5
+
+
 # ------------------------------------------------------------------------------ LayerNorm
 @pytest.mark.parametrize("D", [32, 128, 176, 512])
 @pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
