@@ -15,8 +15,9 @@
  *    normalisation statistics, softmax/LSE and the loss are always fp32.
  *  - Dropout: (p, seed) where `seed` points to a uint64 in DEVICE memory (read at kernel
  *    entry, so a captured graph replays with whatever seed the step wrote there; may be
- *    NULL when p == 0).  keep(i) = lowbias32(lowbias32(i + lo32(seed)) ^ hi32(seed))
- *    >= p*2^32 over the flat element index i stated per call; kept values are scaled by
+ *    NULL when p == 0).  With h = lowbias32(((i >> 1) + lo32(seed)) ^ hi32(seed)),
+ *    keep(i) = (i odd ? h >> 16 : h & 0xFFFF) >= floor(p * 65536) over the flat element
+ *    index i stated per call (one hash per element pair); kept values are scaled by
  *    1/(1-p).  p = 0 is the identity (reference parity runs).
  *  - Return 0 (TTMI_OK) on success; otherwise an error code, with a message available
  *    from ttmi_last_error() (thread-local).  Invalid shapes are rejected before launch.
@@ -204,6 +205,12 @@ int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int 
  * batch's tensors into a captured step's static inputs). */
 int ttmi_batch_copy(int n, void* const* dst, const void* const* src, const int64_t* nbytes,
                     hipStream_t stream);
+/* dst[i] = transpose(src[i]) for i < n <= 16 row-major bf16 matrices of rows[i] x cols[i],
+ * in one launch (the transposed weight mirrors that make nn.Linear input-grad GEMMs
+ * k-major: dX = dY·W = dY·(Wᵀ)ᵀ; replaces the W-operand layout of user_tower.py's
+ * TransformerEncoderLayer backward, reference src/models/user_tower.py:37-45). */
+int ttmi_transpose_bf16_batch(int n, void* const* dst, const void* const* src,
+                              const int64_t* rows, const int64_t* cols, hipStream_t stream);
 /* dst = bf16(src) (parameter mirror for bf16 GEMM operands). */
 int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hipStream_t stream);
 /* Residual-branch dropout backward (TransformerEncoderLayer dropout1/dropout2):

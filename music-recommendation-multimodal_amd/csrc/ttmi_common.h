@@ -46,6 +46,11 @@ TTMI_DEV void st_dyn(void* p, int64_t i, float v, bool f32) {
 }
 
 // ---------------------------------------------------------------- dropout hash
+// keep(i) = u16(i) >= thresh16, where one 32-bit hash serves an element pair:
+//   h = lowbias32(((i >> 1) + k0) ^ k1),  u16(i) = (i & 1) ? h >> 16 : h & 0xFFFF,
+//   thresh16 = floor(p * 65536)  (p resolved to 1/65536).
+// Restated in oracle/two_tower_ref.py:hash_keep.  One mixer round per two elements keeps
+// the mask off the VALU critical path of the GEMM epilogues it is fused into.
 TTMI_DEV uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
   return x;
@@ -54,9 +59,9 @@ TTMI_DEV uint32_t lowbias32(uint32_t x) {
 // replays with fresh masks (the train step rewrites its seed table every step).
 struct DropParams {
   const uint64_t* seed;
-  uint32_t thresh;
-  float scale;   // 1/(1-p)
-  int on;        // p > 0
+  uint32_t thresh;   // 16-bit threshold
+  float scale;       // 1/(1-p)
+  int on;            // p > 0
 };
 // Device-resolved keys (read the seed once at kernel entry).
 struct DropKeys {
@@ -74,18 +79,38 @@ TTMI_DEV DropKeys resolve_drop(const DropParams& d) {
   k.k1 = (uint32_t)(s >> 32);
   return k;
 }
+TTMI_DEV uint32_t drop_hash(const DropKeys& d, uint32_t pair) {
+  return lowbias32((pair + d.k0) ^ d.k1);
+}
 TTMI_DEV bool drop_keep(const DropKeys& d, uint32_t idx) {
-  return lowbias32(lowbias32(idx + d.k0) ^ d.k1) >= d.thresh;
+  const uint32_t h = drop_hash(d, idx >> 1);
+  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= d.thresh;
 }
 TTMI_DEV float drop_apply(const DropKeys& d, uint32_t idx, float v) {
   if (!d.on) return v;
   return drop_keep(d, idx) ? v * d.scale : 0.f;
 }
+// v[0..NV) at consecutive indices idx0.. (one hash per aligned pair).
+template <int NV>
+TTMI_DEV void drop_apply_vec(const DropKeys& d, uint32_t idx0, float* v) {
+  if (!d.on) return;
+  if ((idx0 & 1) == 0) {
+#pragma unroll
+    for (int e = 0; e < NV; e += 2) {
+      const uint32_t h = drop_hash(d, (idx0 + e) >> 1);
+      v[e] = (h & 0xFFFFu) >= d.thresh ? v[e] * d.scale : 0.f;
+      if (e + 1 < NV) v[e + 1] = (h >> 16) >= d.thresh ? v[e + 1] * d.scale : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[e] = drop_apply(d, idx0 + e, v[e]);
+  }
+}
 static inline DropParams make_drop(float p, const uint64_t* seed) {
   DropParams d;
   d.seed = seed;
-  double t = (double)p * 4294967296.0;
-  d.thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  const double t = (double)p * 65536.0;
+  d.thresh = t >= 65535.0 ? 65535u : (uint32_t)t;
   d.on = p > 0.f;
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   return d;

@@ -248,8 +248,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       for (int e = 0; e < 4; ++e) {
         v[e] = g.alpha * acc[i][j][e] + bias[e];
         if (g.act == 1) v[e] = fmaxf(v[e], 0.f);
-        if (dk.on) v[e] = drop_apply(dk, (uint32_t)(drow * g.ld_drop + n + e), v[e]);
       }
+      drop_apply_vec<4>(dk, (uint32_t)(drow * g.ld_drop + n), v);
       if (g.gate) {
         const int64_t o = m * g.ld_gate + n;
         float gv[4];
@@ -305,6 +305,144 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   }
 }
 
+
+// ------------------------------------------------ row-panel GEMM (skinny K, whole N per WG)
+// C[m, :] = epi(alpha * A[m, :K] · Wᵀ) for M >> N with N in {128,..,512}, K <= 512, both
+// operands k-major (nn.Linear forward; input grads through a transposed weight mirror).
+// The generic tile kernel pays two serial K-tile load latencies per 128x128 tile here and
+// reaches ~1 TB/s.  Instead (measured on MI355X against hipBLASLt, tools/gemm_variants.py):
+//  * W is stationary in LDS (N x K, pitch 2K+16 so the 16 rows a ds_read_b128 lane group
+//    reads fall in distinct bank slots), loaded once per CU; the bias row sits beside it;
+//  * 8 waves per workgroup each own whole 16-row tiles across all N columns (column groups
+//    of 128 bound the live state); two waves per SIMD hide each other's latency and nothing
+//    synchronises after the W load;
+//  * k is permuted so every fragment is a contiguous 16-byte read: lane group g of chunk c
+//    holds k = g*K/4 + 8c .. +7 on both operands, so A fragments come straight from HBM
+//    into VGPRs (each A row read once), the first tile's under the W load;
+//  * W fragment columns are paired (tile 2p slot 4q+r <-> column 32p+8q+r, tile 2p+1 <->
+//    32p+8q+4+r), so each lane owns 8 consecutive output columns: 16-byte stores and
+//    16-byte bias / gate / residual loads; dropout hashes once per column pair.
+enum PanelEpi { PE_NONE = 0, PE_RES = 1, PE_GATE_BF16 = 2, PE_GATE_F32 = 3 };
+
+template <int NT, int KC, int EPI>
+__global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg) {
+  constexpr int K = KC * 32, N = NT * 16, WP = 2 * K + 16;
+  static_assert(NT % 8 == 0, "column groups of 128");
+  __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4];
+  float* sbias = reinterpret_cast<float*>(smem + N * WP);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
+  const int64_t tile_end = std::min<int64_t>((g.M + 15) / 16, tile_beg + tiles_per_wg);
+  const int64_t tile0 = tile_beg + wave;
+  uint4 a0[4];                       // this wave's first A fragments, in flight under the W load
+  {
+    const int64_t m = tile0 * 16 + li;
+    const char* ap = g.A + (m * g.lda + lg * (K / 4)) * 2;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      a0[c] = (tile0 < tile_end && m < g.M) ? *reinterpret_cast<const uint4*>(ap + 16 * c)
+                                            : make_uint4(0, 0, 0, 0);
+  }
+  {   // W -> LDS, coalesced 16-byte chunks
+    constexpr int CPR = K / 8;
+    for (int i = tid; i < N * CPR; i += 512) {
+      const int n = i / CPR, j = i % CPR;
+      *reinterpret_cast<uint4*>(smem + n * WP + j * 16) =
+          *reinterpret_cast<const uint4*>(g.B + ((int64_t)n * g.ldb + 8 * j) * 2);
+    }
+    for (int i = tid; i < N; i += 512) sbias[i] = g.bias ? g.bias[i] : 0.f;
+  }
+  const DropKeys dk = resolve_drop(g.drop);
+  __syncthreads();
+
+  // W fragment base for this lane (column-paired: tile 2p slot 4q+r <-> column 32p+8q+r)
+  const int wrow = 8 * (li >> 2) + (li & 3);
+  for (int64_t tile = tile_beg + wave; tile < tile_end; tile += 8) {
+    const int64_t m = tile * 16 + li;
+    const bool mok = m < g.M;
+    const char* ap = g.A + (m * g.lda + lg * (K / 4)) * 2;
+    // column groups of 128 (8 MFMA tiles) and k groups of 4 chunks keep the accumulator,
+    // A and W fragment state bounded (A re-reads per column group hit L1/L2)
+#pragma unroll 1
+    for (int cg = 0; cg < NT / 8; ++cg) {
+      f32x4_t acc[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const char* wb = smem + (cg * 128 + wrow) * WP + lg * (K / 2);
+#pragma unroll 1
+      for (int cq = 0; cq < KC / 4; ++cq) {
+        uint4 a[4];
+        if (tile == tile0 && cq == 0) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) a[c] = a0[c];
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            a[c] = mok ? *reinterpret_cast<const uint4*>(ap + 64 * cq + 16 * c) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const uint4 wf = lds16(wb + (32 * (t >> 1) + 4 * (t & 1)) * WP + 64 * cq + 16 * c);
+            Mma<bf16_t>::run(acc[t], wf, a[c]);
+          }
+        }
+      }
+      if (!mok) continue;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int n = cg * 128 + 32 * p + 8 * lg;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = g.alpha * acc[2 * p][e] + sbias[n + e];
+          v[4 + e] = g.alpha * acc[2 * p + 1][e] + sbias[n + 4 + e];
+        }
+        if (g.act == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + n), v);
+        if constexpr (EPI == PE_GATE_BF16) {
+          const uint4 q = *reinterpret_cast<const uint4*>((const bf16_t*)g.gate + m * g.ld_gate + n);
+          const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] = __uint_as_float(qw[e] << 16) > 0.f ? v[2 * e] * g.gate_scale : 0.f;
+            v[2 * e + 1] = __uint_as_float(qw[e] & 0xFFFF0000u) > 0.f ? v[2 * e + 1] * g.gate_scale : 0.f;
+          }
+        }
+        if constexpr (EPI == PE_GATE_F32) {
+          const float* gp = (const float*)g.gate + m * g.ld_gate + n;
+          const float4 q0 = *reinterpret_cast<const float4*>(gp), q1 = *reinterpret_cast<const float4*>(gp + 4);
+          const float gv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
+        }
+        if constexpr (EPI == PE_RES) {
+          const float* rp = g.residual + m * g.ld_res + n;
+          const float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
+          v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+          v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+        }
+        if (g.c_f32) {
+          float* cp = reinterpret_cast<float*>(g.C) + m * g.ldc + n;
+          *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+          uint4 q;
+          q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+          q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + m * g.ldc + n) = q;
+        }
+      }
+    }
+  }
+}
 
 // ------------------------------------------------------------ weight-gradient GEMM (bf16)
 // C[m,n] += alpha * Σ_r A[r,m] B[r,n]: A = dY [R][lda], B = X [R][ldb], both row-major with
@@ -611,6 +749,65 @@ int launch_wgrad(const ttmi_gemm_desc* d, hipStream_t stream) {
   return launch_wgrad_t<64, 64, 4>(d, c.remap, stream);
 }
 
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
+int panel_epi(const ttmi_gemm_desc* d) {
+  if (d->residual && d->gate) return -1;
+  if (d->residual) return PE_RES;
+  if (d->gate) return d->gate_dtype == TTMI_F32 ? PE_GATE_F32 : PE_GATE_BF16;
+  return PE_NONE;
+}
+
+// Row-panel dispatch: bf16, both operands k-major, plain store, N in {128,..,512} with the
+// W image in LDS, K % 128 == 0, many rows, 16-byte aligned epilogue operands.
+bool panel_applies(const ttmi_gemm_desc* d) {
+  if (getenv("TTMI_NO_PANEL")) return false;       // tuning runs only
+  if (d->dtype != TTMI_BF16 || !d->a_kmajor || !d->b_kmajor || d->c_mode != 0) return false;
+  if (d->colsum || d->split_k > 1 || d->drop_rows || d->M < 2048) return false;
+  if (d->N % 128 || d->N > 512 || d->K % 128 || d->K > 512) return false;
+  if (d->N * (2 * d->K + 16) + d->N * 4 > 150 * 1024 || panel_epi(d) < 0) return false;
+  if (d->ldc % 8 || !al16(d->C) || !al16(d->A) || !al16(d->B) || d->lda % 8 || d->ldb % 8) return false;
+  if (d->bias && !al16(d->bias)) return false;
+  const int64_t lim = (int64_t)INT_MAX;
+  if (d->M * d->lda * 2 >= lim) return false;
+  if (d->residual && (d->ld_res % 4 || !al16(d->residual) || d->M * d->ld_res * 4 >= lim)) return false;
+  if (d->gate && (d->ld_gate % 8 || !al16(d->gate) || d->M * d->ld_gate * 4 >= lim)) return false;
+  return true;
+}
+
+template <int NT, int KC, int EPI>
+void launch_panel_t(const GemmArgs& a, hipStream_t s) {
+  // contiguous row ranges, >= 8 tiles (one per wave) per workgroup, about one per CU
+  const int64_t tiles = (a.M + 15) / 16;
+  const int64_t tpw = std::max<int64_t>(8, (tiles + num_cus() - 1) / num_cus());
+  const int64_t grid = (tiles + tpw - 1) / tpw;
+  hipLaunchKernelGGL((panel_kernel<NT, KC, EPI>), dim3((unsigned)grid), dim3(512), 0, s, a, (int)tpw);
+}
+
+bool launch_panel(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
+  const int NT = (int)(a.N / 16), KC = (int)(a.K / 32), E = panel_epi(d);
+#define TTMI_PANEL(nt, kc, e) if (NT == nt && KC == kc && E == e) { launch_panel_t<nt, kc, e>(a, s); return true; }
+  TTMI_PANEL(8, 4, PE_NONE) TTMI_PANEL(8, 4, PE_RES) TTMI_PANEL(8, 4, PE_GATE_BF16)      // N=128
+  TTMI_PANEL(8, 12, PE_NONE) TTMI_PANEL(8, 16, PE_NONE) TTMI_PANEL(8, 16, PE_RES)
+  TTMI_PANEL(16, 4, PE_NONE) TTMI_PANEL(16, 8, PE_NONE)                                  // N=256
+  TTMI_PANEL(24, 4, PE_NONE)                                                             // N=384
+  TTMI_PANEL(32, 4, PE_NONE) TTMI_PANEL(32, 4, PE_GATE_BF16) TTMI_PANEL(32, 4, PE_GATE_F32)  // N=512
+#undef TTMI_PANEL
+  return false;
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
@@ -648,6 +845,12 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   if (d->N > 64 && tiles128 >= 256) { bm = 128; bn = 128; }
   else if (d->N > 64 && tiles64x128 >= 128) { bm = 64; bn = 128; }
   else { bm = 64; bn = 64; }
+  if (const char* e = getenv("TTMI_GEMM_TILE")) {     // tuning runs only
+    int tm = 0, tn = 0;
+    if (sscanf(e, "%dx%d", &tm, &tn) == 2 && (tm == 64 || tm == 128) && (tn == 64 || tn == 128)) {
+      bm = tm; bn = tn;
+    }
+  }
   const int64_t gx = (d->N + bn - 1) / bn, gy = (d->M + bm - 1) / bm;
   TTMI_REQUIRE(gy <= 65535 && gx <= 2147483647LL, "ttmi_gemm: grid too large");
 
@@ -687,6 +890,7 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
           (!d->residual || (d->ld_res % 4 == 0 && (uintptr_t)d->residual % 16 == 0)) &&
           (!d->gate || (d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 16 == 0));
 
+  if (panel_applies(d) && launch_panel(d, a, stream)) return ttmi_check_launch("ttmi_gemm");
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)split);
   if (d->dtype == TTMI_BF16) launch_typed<bf16_t>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
   else launch_typed<float>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);

@@ -170,9 +170,7 @@ __global__ __launch_bounds__(256) void dropout_bwd_vec_kernel(int64_t M, int N,
       float* pv = &v.x;
       if (dk.on) {
         const int64_t dr = drows ? (int64_t)drows[m] : m;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          pv[e] = drop_keep(dk, (uint32_t)(dr * ld_drop + n + e)) ? pv[e] * dk.scale : 0.f;
+        drop_apply_vec<4>(dk, (uint32_t)(dr * ld_drop + n), pv);
       }
       store4<T>(dy + m * ldy + n, v.x, v.y, v.z, v.w);
 #pragma unroll
@@ -318,6 +316,62 @@ extern "C" int ttmi_batch_copy(int n, void* const* dst, const void* const* src,
   const int gx = (int)std::min<int64_t>(std::max<int64_t>((mx / 16 + 255) / 256, 1), 256);
   hipLaunchKernelGGL(batch_copy_kernel, dim3(gx, n), dim3(256), 0, s, cl);
   return ttmi_check_launch("ttmi_batch_copy");
+}
+
+// ------------------------------------------------------------ batched bf16 transpose
+// dst_i[c][r] = src_i[r][c] for up to MAX_COPIES row-major matrices in one launch (the
+// transposed weight mirrors that make input-grad GEMMs k-major).  64x64 tiles through LDS
+// (pitch 65 elements); 16-bit loads/stores, each weight is at most a few hundred KB.
+struct TransposeList {
+  uint16_t* dst[MAX_COPIES];
+  const uint16_t* src[MAX_COPIES];
+  int rows[MAX_COPIES], cols[MAX_COPIES];
+  int tile0[MAX_COPIES + 1];        // prefix sums of 64x64 tile counts
+  int n;
+};
+
+__global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl) {
+  __shared__ uint16_t t[64][65];
+  int i = 0;
+  while (i + 1 < tl.n && (int)blockIdx.x >= tl.tile0[i + 1]) ++i;
+  const int local = blockIdx.x - tl.tile0[i];
+  const int R = tl.rows[i], C = tl.cols[i];
+  const int tcol = (C + 63) / 64;
+  const int r0 = (local / tcol) * 64, c0 = (local % tcol) * 64;
+  const uint16_t* src = tl.src[i];
+  uint16_t* dst = tl.dst[i];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4)
+    if (r0 + r < R && c0 + tx < C) t[r][tx] = src[(int64_t)(r0 + r) * C + c0 + tx];
+  __syncthreads();
+  for (int c = ty; c < 64; c += 4)
+    if (c0 + c < C && r0 + tx < R) dst[(int64_t)(c0 + c) * R + r0 + tx] = t[tx][c];
+}
+
+extern "C" int ttmi_transpose_bf16_batch(int n, void* const* dst, const void* const* src,
+                                         const int64_t* rows, const int64_t* cols,
+                                         hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && n <= MAX_COPIES, "ttmi_transpose_bf16_batch: at most %d matrices", MAX_COPIES);
+  if (n == 0) return TTMI_OK;
+  TTMI_REQUIRE(dst && src && rows && cols, "ttmi_transpose_bf16_batch: null argument");
+  TransposeList tl;
+  tl.n = n;
+  tl.tile0[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    TTMI_REQUIRE(rows[i] >= 0 && cols[i] >= 0 && rows[i] < (1 << 30) && cols[i] < (1 << 30),
+                 "ttmi_transpose_bf16_batch: bad shape %d", i);
+    TTMI_REQUIRE(rows[i] * cols[i] == 0 || (dst[i] && src[i]), "ttmi_transpose_bf16_batch: null entry %d", i);
+    tl.dst[i] = static_cast<uint16_t*>(dst[i]);
+    tl.src[i] = static_cast<const uint16_t*>(src[i]);
+    tl.rows[i] = (int)rows[i];
+    tl.cols[i] = (int)cols[i];
+    const int64_t tiles = ((rows[i] + 63) / 64) * ((cols[i] + 63) / 64);
+    TTMI_REQUIRE(tl.tile0[i] + tiles < (1 << 30), "ttmi_transpose_bf16_batch: too large");
+    tl.tile0[i + 1] = tl.tile0[i] + (int)tiles;
+  }
+  if (tl.tile0[n] == 0) return TTMI_OK;
+  hipLaunchKernelGGL(transpose_batch_kernel, dim3(tl.tile0[n]), dim3(256), 0, s, tl);
+  return ttmi_check_launch("ttmi_transpose_bf16_batch");
 }
 
 extern "C" int ttmi_step_inc(int32_t* step, hipStream_t s) {

@@ -129,6 +129,21 @@ class UserSaved:
     seeds: Optional[Tensor] = None
 
 
+def transposed_name(name: str) -> str:
+    """Key of the transposed bf16 weight mirror (k-major operand of the input-grad GEMM)."""
+    return name + ".T"
+
+
+def _dx(dy: Tensor, W: Dict[str, Tensor], name: str, out: Tensor, gate: Optional[Tensor] = None,
+        gate_scale: float = 1.0) -> Tensor:
+    """Input grad of an nn.Linear: dY · W.  Uses the transposed mirror when present (both
+    operands k-major: the row-panel kernel), else reads W in its natural layout."""
+    wt = W.get(transposed_name(name))
+    if wt is not None:
+        return ops.linear(dy, wt, None, out, gate=gate, gate_scale=gate_scale)
+    return ops.linear_dx(dy, W[name], out, gate=gate, gate_scale=gate_scale)
+
+
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
@@ -254,10 +269,10 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         ops.dropout_bwd(dx, dy2, None, _drop(cfg, seeds, site_drop2(i)), drop_rows=drows)
         ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"], grads[pre + "linear2.bias"])
         dz1 = torch.empty(R, F_, device=dev, dtype=dt)
-        ops.linear_dx(dy2, W[pre + "linear2.weight"], dz1, gate=s.h, gate_scale=_scale(p))
+        _dx(dy2, W, pre + "linear2.weight", dz1, gate=s.h, gate_scale=_scale(p))
         ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"], grads[pre + "linear1.bias"])
         da2 = torch.empty(R, D, **f32)
-        ops.linear_dx(dz1, W[pre + "linear1.weight"], da2)
+        _dx(dz1, W, pre + "linear1.weight", da2)
         dx1 = torch.empty(R, D, **f32)
         ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
                           grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
@@ -266,7 +281,7 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"],
                       grads[pre + "self_attn.out_proj.bias"])
         dctx = torch.empty(R, D, device=dev, dtype=dt)
-        ops.linear_dx(dy1, W[pre + "self_attn.out_proj.weight"], dctx)
+        _dx(dy1, W, pre + "self_attn.out_proj.weight", dctx)
         dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         if drows is not None:
             ops.mha_q1_bwd(s.qkv, st.key_valid, drows, s.lse, dctx, B, L, H, dqkv,
@@ -277,7 +292,7 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"],
                       grads[pre + "self_attn.in_proj_bias"])
         da1 = torch.empty(M, D, **f32)
-        ops.linear_dx(dqkv, W[pre + "self_attn.in_proj_weight"], da1)
+        _dx(dqkv, W, pre + "self_attn.in_proj_weight", da1)
         dxn = torch.empty(M, D, **f32)
         if drows is not None:
             ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,

@@ -68,6 +68,7 @@ SIGNATURES = {
     "ttmi_infonce_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_step_inc": (c_i, [c_p, c_p]),
     "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_p]),
     "ttmi_cast_f32_bf16": (c_i, [c_i64, c_p, c_p, c_p]),

@@ -78,14 +78,16 @@ def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a
 
 def linear(x: Tensor, w: Tensor, bias: Optional[Tensor], out: Tensor, *, act: int = 0,
            drop: Drop = NO_DROP, residual: Optional[Tensor] = None,
-           drop_rows: Optional[Tensor] = None) -> Tensor:
-    """out[M,N] = epi(x[M,K] · w[N,K]ᵀ + bias)  (nn.Linear forward); dropout indices use
-    drop_rows[m] (int32) as the row when given (pruned last layer)."""
+           drop_rows: Optional[Tensor] = None, gate: Optional[Tensor] = None,
+           gate_scale: float = 1.0) -> Tensor:
+    """out[M,N] = epi(x[M,K] · w[N,K]ᵀ + bias)  (nn.Linear forward; with w = Wᵀ mirror and a
+    gate, the input grad of a ReLU/dropout-gated Linear); dropout indices use drop_rows[m]
+    (int32) as the row when given (pruned last layer)."""
     M, K = x.shape
     N = w.shape[0]
     return gemm(x, w, out, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True, ldc=N,
                 bias=bias, act=act, drop=drop, ld_drop=N, residual=residual, ld_res=N,
-                drop_rows=drop_rows)
+                drop_rows=drop_rows, gate=gate, ld_gate=N, gate_scale=gate_scale)
 
 
 def linear_dx(dy: Tensor, w: Tensor, out: Tensor, *, gate: Optional[Tensor] = None,
@@ -240,6 +242,22 @@ def batch_copy(dsts, srcs):
             raise ValueError("batch_copy: size mismatch")
     N = (ctypes.c_int64 * n)(*[t.numel() * t.element_size() for t in dsts])
     call("ttmi_batch_copy", n, D, S, N, _s())
+
+
+def transpose_batch(dsts, srcs):
+    """One launch: dsts[i] = srcs[i].t() for 2-D bf16 matrices (dsts[i] is [cols, rows])."""
+    n = len(dsts)
+    if n == 0:
+        return
+    for d, s_ in zip(dsts, srcs):
+        if s_.dim() != 2 or d.shape != (s_.shape[1], s_.shape[0]) or not s_.is_contiguous() \
+                or not d.is_contiguous() or s_.dtype != torch.bfloat16 or d.dtype != torch.bfloat16:
+            raise ValueError("transpose_batch: need contiguous bf16 [R,C] -> [C,R]")
+    D = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dsts])
+    S = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+    R = (ctypes.c_int64 * n)(*[t.shape[0] for t in srcs])
+    C = (ctypes.c_int64 * n)(*[t.shape[1] for t in srcs])
+    call("ttmi_transpose_bf16_batch", n, D, S, R, C, _s())
 
 
 def step_inc(step: Tensor):

@@ -25,7 +25,7 @@ import torch.distributed as dist
 from . import functional as F
 from . import ops
 from .two_tower import TwoTowerModel
-from .user_tower import _gemm_names
+from .user_tower import _gemm_names, add_transposes, refresh_transposes
 from .item_tower import ITEM_GEMMS
 
 Tensor = torch.Tensor
@@ -176,6 +176,7 @@ class TrainStep:
             Mi = self.flat.views(self.flat.mirror, "item_tower.")
             self.Wu = dict(self.Pu)
             self.Wu.update({n: Mu[n] for n in _gemm_names(list(self.Pu))})
+            add_transposes(self.Wu, _gemm_names(list(self.Pu)))   # refreshed every step
             self.Wi = dict(self.Pi)
             self.Wi.update({n: Mi[n] for n in ITEM_GEMMS})
         else:
@@ -200,6 +201,8 @@ class TrainStep:
     def _fwd_bwd(self, b: Dict[str, Tensor]) -> None:
         # the gradient buffer is zero here: it starts zeroed and the fused AdamW clears it
         ops.step_inc(self.step_t)
+        if self.flat.mirror is not None:      # Wᵀ mirrors of the just-updated bf16 weights
+            refresh_transposes(self.Wu, _gemm_names(list(self.Pu)))
         seeds = None
         if self.ucfg.p_drop > 0 or self.p_item > 0:
             ops.dropout_seeds(self.base_seed, self.step_t, self.seeds)

@@ -58,14 +58,35 @@ class _EncoderParams(nn.Module):
 
 
 def make_operands(P: dict, dtype: torch.dtype, gemm_names) -> dict:
-    """GEMM operand view of the fp32 masters: bf16 copies (libttmi cast kernel) or P."""
+    """GEMM operand view of the fp32 masters: bf16 copies (libttmi cast kernel) plus the
+    transposed mirrors of the encoder weights, or P itself in fp32."""
     if dtype == torch.float32:
         return P
     W = dict(P)
     for n in gemm_names:
         src = P[n].contiguous()
         W[n] = ops.cast_bf16(src, torch.empty(src.shape, device=src.device, dtype=dtype))
+    add_transposes(W, gemm_names)
+    refresh_transposes(W, gemm_names)
     return W
+
+
+def encoder_weight_names(names) -> List[str]:
+    return [n for n in names if n.endswith(GEMM_WEIGHTS)]
+
+
+def add_transposes(W: dict, gemm_names) -> None:
+    """Allocate W[name + '.T'] ([in, out] bf16) for every encoder-layer weight."""
+    for n in encoder_weight_names(gemm_names):
+        w = W[n]
+        W[F.transposed_name(n)] = torch.empty(w.shape[1], w.shape[0], device=w.device,
+                                              dtype=w.dtype)
+
+
+def refresh_transposes(W: dict, gemm_names) -> None:
+    """W[name + '.T'] = W[name]ᵀ for all encoder-layer weights in one launch."""
+    names = [n for n in encoder_weight_names(gemm_names) if F.transposed_name(n) in W]
+    ops.transpose_batch([W[F.transposed_name(n)] for n in names], [W[n] for n in names])
 
 
 def _gemm_names(names: List[str]):

@@ -82,6 +82,57 @@ def test_gemm_epilogue(gpu_pkg, dtype):
     assert rel(Cb.float(), A.float() @ W.float().t() + bias) < 8e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(3000, 384, 128), (4100, 512, 128), (2100, 128, 512),
+                                   (2048, 128, 384), (2500, 256, 256), (2048, 128, 128)])
+@pytest.mark.parametrize("epi", ["res", "gate_bf16", "gate_f32", "none"])
+def test_gemm_row_panel(gpu_pkg, M, N, K, epi):
+    """Skinny-K row-panel kernel (persistent, W-stationary): each epilogue family, fp32 and
+    bf16 out, rows not a multiple of the tile; shapes without a panel instantiation take the
+    generic kernel and must agree just the same."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    gate = torch.randn(M, N, generator=g)
+    if epi == "gate_bf16":
+        gate = gate.to(torch.bfloat16)
+    p, seed = 0.2, 0x1234ABCD5678
+    keep = keep_mask(seed, (M, N), p).float()
+    base = A.float() @ W.float().t()
+    v = torch.relu(base * 0.5 + bias) * keep / (1 - p)
+    kw = {}
+    if epi == "res":
+        v = v + res
+        kw = dict(residual=res.to(DEV), ld_res=N)
+    elif epi.startswith("gate"):
+        v = torch.where(gate.float() > 0, v * 2.0, torch.zeros_like(v))
+        kw = dict(gate=gate.to(DEV), ld_gate=N, gate_scale=2.0)
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(A.to(DEV), W.to(DEV), C, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True,
+             ldc=N, alpha=0.5, bias=bias.to(DEV), act=1, drop=(p, seed_dev(seed)), ld_drop=N, **kw)
+    assert rel(C, v) < 2e-5 * max(1.0, math.sqrt(K / 256))
+    Cb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.linear(A.to(DEV), W.to(DEV), bias.to(DEV), Cb)
+    assert rel(Cb.float(), base + bias) < 8e-3
+
+
+def test_gemm_drop_rows(gpu_pkg):
+    """Dropout through a row map (the pruned last layer's gathered rows)."""
+    ops = gpu_pkg.ops
+    M, N, K = 512, 128, 128
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    p, seed = 0.2, 0x55AA
+    rows = torch.randperm(50 * M, generator=g)[:M].to(torch.int32)
+    keep = keep_mask(seed, (50 * M, N), p).float()[rows.long()]
+    C = torch.empty(M, N, device=DEV)
+    ops.linear(A.to(DEV), W.to(DEV), None, C, drop=(p, seed_dev(seed)), drop_rows=rows.to(DEV))
+    assert rel(C, (A.float() @ W.float().t()) * keep / (1 - p)) < 2e-5
+
+
 @pytest.mark.parametrize("split", [0, 1, 7])
 def test_gemm_accumulate_split_k(gpu_pkg, split):
     ops = gpu_pkg.ops
@@ -392,3 +443,16 @@ def test_dropout_seed_kernel_matches_host(gpu_pkg):
     gpu_pkg.ops.dropout_seeds(0xABCDEF, step, seeds)
     host = F.seed_table(F.site_seeds(0xABCDEF, 12), "cpu")
     assert torch.equal(seeds.cpu(), host)
+
+
+def test_transpose_batch(gpu_pkg):
+    """Batched bf16 transpose (the Wᵀ mirrors of the input-grad GEMMs): ragged shapes."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(11)
+    shapes = [(384, 128), (128, 128), (512, 128), (128, 512), (70, 33), (1, 200)]
+    srcs = [torch.randn(r, c, generator=g).to(torch.bfloat16).to(DEV) for r, c in shapes]
+    dsts = [torch.empty(c, r, device=DEV, dtype=torch.bfloat16) for r, c in shapes]
+    ops.transpose_batch(dsts, srcs)
+    torch.cuda.synchronize()
+    for s_, d in zip(srcs, dsts):
+        assert torch.equal(d.cpu(), s_.t().cpu())
