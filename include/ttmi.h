@@ -205,6 +205,28 @@ int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int 
  * batch's tensors into a captured step's static inputs). */
 int ttmi_batch_copy(int n, void* const* dst, const void* const* src, const int64_t* nbytes,
                     hipStream_t stream);
+/* Input grad of an nn.Linear fused with the LayerNorm backward (and dropout backward) that
+ * consume it — the reversed TransformerEncoderLayer (norm_first) sub-block
+ *   dY = dH · Wᵀᵀ  (dH [M,K] bf16, wt = Wᵀ [N,K] bf16 mirror, N = 128),
+ *   dx = LN'(dY; x, mean, rstd, ln_w) + res,  ln_dw += Σ dY·x̂,  ln_db += Σ dY,
+ *   next = bf16(dropout(dx)) with keep over (drop_rows ? drop_rows[m] : m)*ld_drop + n,
+ * replacing linear_dx + ttmi_layernorm_bwd + ttmi_dropout_bwd (reference
+ * src/models/user_tower.py:37-45 TransformerEncoderLayer(norm_first=True) backward).
+ * res / next / drop_rows / ln_dw / ln_db may be NULL.  K % 128 == 0, K <= 512. */
+typedef struct ttmi_linear_ln_bwd_desc {
+  int64_t M, N, K;
+  const void* dh; int64_t ld_dh;        /* bf16 [M, K] */
+  const void* wt; int64_t ld_wt;        /* bf16 [N, K] */
+  const float* x; int64_t ldx;          /* LayerNorm input [M, N] */
+  const float* mean; const float* rstd; /* [M] */
+  const float* ln_w;                    /* [N] */
+  const float* res; int64_t ld_res;     /* [M, N] or NULL */
+  float* dx; int64_t lddx;              /* [M, N] */
+  void* next; int64_t ld_next;          /* bf16 [M, N] or NULL */
+  float drop_p; const uint64_t* drop_seed; int64_t ld_drop; const int32_t* drop_rows;
+  float* ln_dw; float* ln_db;           /* [N], accumulated */
+} ttmi_linear_ln_bwd_desc;
+int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream);
 /* dst[i] = transpose(src[i]) for i < n <= 16 row-major bf16 matrices of rows[i] x cols[i],
  * in one launch (the transposed weight mirrors that make nn.Linear input-grad GEMMs
  * k-major: dX = dY·W = dY·(Wᵀ)ᵀ; replaces the W-operand layout of user_tower.py's

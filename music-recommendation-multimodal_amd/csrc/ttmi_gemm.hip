@@ -322,14 +322,125 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 //  * W fragment columns are paired (tile 2p slot 4q+r <-> column 32p+8q+r, tile 2p+1 <->
 //    32p+8q+4+r), so each lane owns 8 consecutive output columns: 16-byte stores and
 //    16-byte bias / gate / residual loads; dropout hashes once per column pair.
-enum PanelEpi { PE_NONE = 0, PE_RES = 1, PE_GATE_BF16 = 2, PE_GATE_F32 = 3 };
+enum PanelEpi { PE_NONE = 0, PE_RES = 1, PE_GATE_BF16 = 2, PE_GATE_F32 = 3, PE_LNBWD = 4 };
+
+// PE_LNBWD: the GEMM output dY (N = 128 = LayerNorm width, never stored) feeds the
+// LayerNorm backward of the rows it completes:
+//   xh = (x - mean) * rstd,  g = dY * w,  dx = rstd * (g - mean(g) - xh * mean(g * xh)) + res,
+//   dw += Σ_rows dY * xh,  db += Σ_rows dY,  next = bf16(dropout(dx))  (optional),
+// i.e. ttmi_layernorm_bwd + ttmi_dropout_bwd fused into the input-grad GEMM.
+struct LnBwdArgs {
+  const float* x; int64_t ldx;
+  const float* mean; const float* rstd; const float* w;
+  const float* res; int64_t ld_res;
+  float* dx; int64_t lddx;
+  bf16_t* next; int64_t ld_next;
+  DropParams drop; int64_t ld_drop; const int32_t* drop_rows;
+  float* dw; float* db;
+};
+
+// Sum over the 16 lanes of a DPP row (GFX9 quad_perm / row_half_mirror / row_mirror).
+template <int CTRL>
+TTMI_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+TTMI_DEV float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror
+  return v;
+}
+
+
+// LayerNorm-backward epilogue of one 16-row tile (N = 128): lane (li, lg) holds row li,
+// columns 32p + 8lg + e (p < 4, e < 8) of dY in acc (column-paired tiles 2p, 2p+1).
+TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, const f32x4_t (&acc)[8],
+                                    int64_t m, bool mok, int li, int lg, const float* sw,
+                                    float* sdw, float* sdb, const DropKeys& dk2) {
+  const float mu = mok ? ln.mean[m] : 0.f, rs = mok ? ln.rstd[m] : 0.f;
+  float dy[32], xh[32];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int n = 32 * p + 8 * lg;
+    float xr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (mok) {
+      const float4 x0 = *reinterpret_cast<const float4*>(ln.x + m * ln.ldx + n);
+      const float4 x1 = *reinterpret_cast<const float4*>(ln.x + m * ln.ldx + n + 4);
+      xr[0] = x0.x; xr[1] = x0.y; xr[2] = x0.z; xr[3] = x0.w;
+      xr[4] = x1.x; xr[5] = x1.y; xr[6] = x1.z; xr[7] = x1.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = mok ? g.alpha * (e < 4 ? acc[2 * p][e] : acc[2 * p + 1][e - 4]) : 0.f;
+      const float h = (xr[e] - mu) * rs;
+      const float gg = d * sw[n + e];
+      dy[8 * p + e] = d;
+      xh[8 * p + e] = h;
+      s1 += gg;
+      s2 += gg * h;
+    }
+  }
+  // the row's 128 columns live in the 4 lanes li, li+16, li+32, li+48
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  const float c1 = s1 * (1.f / 128.f), c2 = s2 * (1.f / 128.f);
+  if (mok) {
+    const int64_t drow = ln.drop_rows ? (int64_t)ln.drop_rows[m] : m;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = 32 * p + 8 * lg;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rs * (dy[8 * p + e] * sw[n + e] - c1 - xh[8 * p + e] * c2);
+      if (ln.res) {
+        const float4 r0 = *reinterpret_cast<const float4*>(ln.res + m * ln.ld_res + n);
+        const float4 r1 = *reinterpret_cast<const float4*>(ln.res + m * ln.ld_res + n + 4);
+        o[0] += r0.x; o[1] += r0.y; o[2] += r0.z; o[3] += r0.w;
+        o[4] += r1.x; o[5] += r1.y; o[6] += r1.z; o[7] += r1.w;
+      }
+      float* dp = ln.dx + m * ln.lddx + n;
+      *reinterpret_cast<float4*>(dp) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(dp + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      if (ln.next) {
+        drop_apply_vec<8>(dk2, (uint32_t)(drow * ln.ld_drop + n), o);
+        uint4 q;
+        q.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+        q.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        q.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+        q.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+        *reinterpret_cast<uint4*>(ln.next + m * ln.ld_next + n) = q;
+      }
+    }
+  }
+  // dw / db: sum the tile's 16 rows (one DPP row), one LDS add per column
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float a = row16_sum(dy[8 * p + e] * xh[8 * p + e]);
+      const float b = row16_sum(dy[8 * p + e]);
+      if (li == 0) {
+        atomicAdd(sdw + 32 * p + 8 * lg + e, a);
+        atomicAdd(sdb + 32 * p + 8 * lg + e, b);
+      }
+    }
+  }
+}
 
 template <int NT, int KC, int EPI>
-__global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg) {
+__global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg, LnBwdArgs ln) {
   constexpr int K = KC * 32, N = NT * 16, WP = 2 * K + 16;
+  constexpr bool LNB = EPI == PE_LNBWD;
   static_assert(NT % 8 == 0, "column groups of 128");
-  __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4];
-  float* sbias = reinterpret_cast<float*>(smem + N * WP);
+  static_assert(!LNB || NT == 8, "LayerNorm-backward epilogue needs N = 128");
+  __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4 + (LNB ? 2 * N * 4 : 0)];
+  float* sbias = reinterpret_cast<float*>(smem + N * WP);     // bias, or the LN weight
+  float* sdw = sbias + N;                                       // LNB: per-WG dw / db sums
+  float* sdb = sdw + N;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
@@ -351,9 +462,14 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
       *reinterpret_cast<uint4*>(smem + n * WP + j * 16) =
           *reinterpret_cast<const uint4*>(g.B + ((int64_t)n * g.ldb + 8 * j) * 2);
     }
-    for (int i = tid; i < N; i += 512) sbias[i] = g.bias ? g.bias[i] : 0.f;
+    if constexpr (LNB) {
+      for (int i = tid; i < N; i += 512) { sbias[i] = ln.w[i]; sdw[i] = 0.f; sdb[i] = 0.f; }
+    } else {
+      for (int i = tid; i < N; i += 512) sbias[i] = g.bias ? g.bias[i] : 0.f;
+    }
   }
   const DropKeys dk = resolve_drop(g.drop);
+  const DropKeys dk2 = resolve_drop(ln.drop);
   __syncthreads();
 
   // W fragment base for this lane (column-paired: tile 2p slot 4q+r <-> column 32p+8q+r)
@@ -389,6 +505,10 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
             Mma<bf16_t>::run(acc[t], wf, a[c]);
           }
         }
+      }
+      if constexpr (LNB) {
+        panel_ln_bwd_epilogue(g, ln, acc, m, mok, li, lg, sbias, sdw, sdb, dk2);
+        continue;
       }
       if (!mok) continue;
 #pragma unroll
@@ -440,6 +560,13 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + m * g.ldc + n) = q;
         }
       }
+    }
+  }
+  if constexpr (LNB) {
+    __syncthreads();
+    for (int i = tid; i < N; i += 512) {
+      if (ln.dw) atomicAdd(ln.dw + i, sdw[i]);
+      if (ln.db) atomicAdd(ln.db + i, sdb[i]);
     }
   }
 }
@@ -788,12 +915,12 @@ bool panel_applies(const ttmi_gemm_desc* d) {
 }
 
 template <int NT, int KC, int EPI>
-void launch_panel_t(const GemmArgs& a, hipStream_t s) {
+void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBwdArgs{}) {
   // contiguous row ranges, >= 8 tiles (one per wave) per workgroup, about one per CU
   const int64_t tiles = (a.M + 15) / 16;
   const int64_t tpw = std::max<int64_t>(8, (tiles + num_cus() - 1) / num_cus());
   const int64_t grid = (tiles + tpw - 1) / tpw;
-  hipLaunchKernelGGL((panel_kernel<NT, KC, EPI>), dim3((unsigned)grid), dim3(512), 0, s, a, (int)tpw);
+  hipLaunchKernelGGL((panel_kernel<NT, KC, EPI>), dim3((unsigned)grid), dim3(512), 0, s, a, (int)tpw, ln);
 }
 
 bool launch_panel(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
@@ -895,4 +1022,44 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   if (d->dtype == TTMI_BF16) launch_typed<bf16_t>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
   else launch_typed<float>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
   return ttmi_check_launch("ttmi_gemm");
+}
+
+extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream) {
+  TTMI_REQUIRE(d != nullptr, "ttmi_linear_ln_bwd: null descriptor");
+  TTMI_REQUIRE(d->M >= 0 && d->N == 128, "ttmi_linear_ln_bwd: N must be 128 (got %lld)", (long long)d->N);
+  TTMI_REQUIRE(d->K > 0 && d->K % 128 == 0 && d->K <= 512, "ttmi_linear_ln_bwd: K must be 128, 256, 384 or 512");
+  if (d->M == 0) return TTMI_OK;
+  TTMI_REQUIRE(d->dh && d->wt && d->x && d->mean && d->rstd && d->ln_w && d->dx,
+               "ttmi_linear_ln_bwd: null argument");
+  TTMI_REQUIRE(al16(d->dh) && al16(d->wt) && d->ld_dh % 8 == 0 && d->ld_wt % 8 == 0 &&
+               d->ld_dh >= d->K && d->ld_wt >= d->K, "ttmi_linear_ln_bwd: dh/wt need 16-byte rows");
+  TTMI_REQUIRE(al16(d->x) && d->ldx % 4 == 0 && d->ldx >= 128 && al16(d->dx) && d->lddx % 4 == 0 &&
+               d->lddx >= 128, "ttmi_linear_ln_bwd: x/dx need 16-byte rows");
+  TTMI_REQUIRE(!d->res || (al16(d->res) && d->ld_res % 4 == 0 && d->ld_res >= 128),
+               "ttmi_linear_ln_bwd: res needs 16-byte rows");
+  TTMI_REQUIRE(!d->next || (al16(d->next) && d->ld_next % 8 == 0 && d->ld_next >= 128),
+               "ttmi_linear_ln_bwd: next needs 16-byte rows");
+  TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f && (d->drop_p == 0.f || d->drop_seed),
+               "ttmi_linear_ln_bwd: bad dropout");
+  GemmArgs a{};
+  a.M = d->M; a.N = 128; a.K = d->K;
+  a.A = static_cast<const char*>(d->dh); a.lda = d->ld_dh;
+  a.B = static_cast<const char*>(d->wt); a.ldb = d->ld_wt;
+  a.alpha = 1.f;
+  a.drop = make_drop(0.f, nullptr);
+  LnBwdArgs ln{};
+  ln.x = d->x; ln.ldx = d->ldx; ln.mean = d->mean; ln.rstd = d->rstd; ln.w = d->ln_w;
+  ln.res = d->res; ln.ld_res = d->ld_res;
+  ln.dx = d->dx; ln.lddx = d->lddx;
+  ln.next = static_cast<bf16_t*>(d->next); ln.ld_next = d->ld_next;
+  ln.drop = make_drop(d->drop_p, d->drop_seed); ln.ld_drop = d->ld_drop ? d->ld_drop : 128;
+  ln.drop_rows = d->drop_rows;
+  ln.dw = d->ln_dw; ln.db = d->ln_db;
+  switch (d->K) {
+    case 128: launch_panel_t<8, 4, PE_LNBWD>(a, stream, ln); break;
+    case 256: launch_panel_t<8, 8, PE_LNBWD>(a, stream, ln); break;
+    case 384: launch_panel_t<8, 12, PE_LNBWD>(a, stream, ln); break;
+    default: launch_panel_t<8, 16, PE_LNBWD>(a, stream, ln); break;
+  }
+  return ttmi_check_launch("ttmi_linear_ln_bwd");
 }

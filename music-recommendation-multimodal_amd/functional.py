@@ -144,6 +144,15 @@ def _dx(dy: Tensor, W: Dict[str, Tensor], name: str, out: Tensor, gate: Optional
     return ops.linear_dx(dy, W[name], out, gate=gate, gate_scale=gate_scale)
 
 
+def _ln_fusable(W: Dict[str, Tensor], pre: str, D: int) -> bool:
+    """The layer's input-grad GEMMs can carry the LayerNorm backward in their epilogue:
+    bf16 with the transposed weight mirrors present and the LayerNorm width 128."""
+    wt1 = W.get(transposed_name(pre + "linear1.weight"))
+    wti = W.get(transposed_name(pre + "self_attn.in_proj_weight"))
+    return (D == 128 and wt1 is not None and wti is not None and wt1.shape[1] % 128 == 0
+            and wt1.shape[1] <= 512 and wti.shape[1] % 128 == 0 and wti.shape[1] <= 512)
+
+
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
@@ -259,25 +268,36 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
                         grads["gender_embedding.weight"], grads["country_embedding.weight"])
     # ---- encoder layers, reversed (user_tower.py:37-45)
     p = cfg.p_drop
+    dy2_next = None        # layer i's dy2, emitted by layer i+1's fused LN1 backward
     for i in reversed(range(cfg.n_layers)):
         pre = _lp(i)
         s = st.layers[i]
         R = s.x1.shape[0]                 # B for the pruned layer, M otherwise
         drows = s.rows
         F_ = W[pre + "linear1.weight"].shape[0]
-        dy2 = torch.empty(R, D, device=dev, dtype=dt)
-        ops.dropout_bwd(dx, dy2, None, _drop(cfg, seeds, site_drop2(i)), drop_rows=drows)
+        fuse = _ln_fusable(W, pre, D)
+        if dy2_next is not None:
+            dy2, dy2_next = dy2_next, None
+        else:
+            dy2 = torch.empty(R, D, device=dev, dtype=dt)
+            ops.dropout_bwd(dx, dy2, None, _drop(cfg, seeds, site_drop2(i)), drop_rows=drows)
         ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"], grads[pre + "linear2.bias"])
         dz1 = torch.empty(R, F_, device=dev, dtype=dt)
         _dx(dy2, W, pre + "linear2.weight", dz1, gate=s.h, gate_scale=_scale(p))
         ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"], grads[pre + "linear1.bias"])
-        da2 = torch.empty(R, D, **f32)
-        _dx(dz1, W, pre + "linear1.weight", da2)
         dx1 = torch.empty(R, D, **f32)
-        ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
-                          grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
         dy1 = torch.empty(R, D, device=dev, dtype=dt)
-        ops.dropout_bwd(dx1, dy1, None, _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
+        if fuse:     # linear1 input grad + LN2 backward + dropout1 backward, one kernel
+            ops.linear_ln_bwd(dz1, W[transposed_name(pre + "linear1.weight")], s.x1, s.m2, s.r2,
+                              P[pre + "norm2.weight"], dx1, grads[pre + "norm2.weight"],
+                              grads[pre + "norm2.bias"], res=dx, next_=dy1,
+                              drop=_drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
+        else:
+            da2 = torch.empty(R, D, **f32)
+            _dx(dz1, W, pre + "linear1.weight", da2)
+            ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
+                              grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
+            ops.dropout_bwd(dx1, dy1, None, _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
         ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"],
                       grads[pre + "self_attn.out_proj.bias"])
         dctx = torch.empty(R, D, device=dev, dtype=dt)
@@ -291,16 +311,28 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
                         _drop(cfg, seeds, site_attn(i)))
         ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"],
                       grads[pre + "self_attn.in_proj_bias"])
-        da1 = torch.empty(M, D, **f32)
-        _dx(dqkv, W, pre + "self_attn.in_proj_weight", da1)
         dxn = torch.empty(M, D, **f32)
-        if drows is not None:
-            ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
-                              grads[pre + "norm1.weight"], grads[pre + "norm1.bias"])
-            ops.scatter_add_rows(dx1, drows, dxn)      # residual path of the gathered rows
+        if fuse:     # in_proj input grad + LN1 backward (+ the layer below's dropout2 backward)
+            emit = drows is None and i > 0
+            nxt = torch.empty(M, D, device=dev, dtype=dt) if emit else None
+            ops.linear_ln_bwd(dqkv, W[transposed_name(pre + "self_attn.in_proj_weight")], s.x,
+                              s.m1, s.r1, P[pre + "norm1.weight"], dxn,
+                              grads[pre + "norm1.weight"], grads[pre + "norm1.bias"],
+                              res=dx1 if drows is None else None, next_=nxt,
+                              drop=_drop(cfg, seeds, site_drop2(i - 1)) if emit else ops.NO_DROP)
+            if drows is not None:
+                ops.scatter_add_rows(dx1, drows, dxn)      # residual path of the gathered rows
+            dy2_next = nxt
         else:
-            ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
-                              grads[pre + "norm1.weight"], grads[pre + "norm1.bias"], res=dx1)
+            da1 = torch.empty(M, D, **f32)
+            _dx(dqkv, W, pre + "self_attn.in_proj_weight", da1)
+            if drows is not None:
+                ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
+                                  grads[pre + "norm1.weight"], grads[pre + "norm1.bias"])
+                ops.scatter_add_rows(dx1, drows, dxn)      # residual path of the gathered rows
+            else:
+                ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
+                                  grads[pre + "norm1.weight"], grads[pre + "norm1.bias"], res=dx1)
         dx = dxn
     # ---- input block (user_tower.py:83-93)
     ops.seq_embed_bwd(st.ids, P["item_embedding.weight"], P["position_embedding.weight"],

@@ -41,6 +41,21 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class LnBwdDesc(ctypes.Structure):
+    """ttmi_linear_ln_bwd_desc (include/ttmi.h)."""
+    _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
+                ("dh", ctypes.c_void_p), ("ld_dh", ctypes.c_int64),
+                ("wt", ctypes.c_void_p), ("ld_wt", ctypes.c_int64),
+                ("x", ctypes.c_void_p), ("ldx", ctypes.c_int64),
+                ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p), ("ln_w", ctypes.c_void_p),
+                ("res", ctypes.c_void_p), ("ld_res", ctypes.c_int64),
+                ("dx", ctypes.c_void_p), ("lddx", ctypes.c_int64),
+                ("next", ctypes.c_void_p), ("ld_next", ctypes.c_int64),
+                ("drop_p", ctypes.c_float), ("drop_seed", ctypes.c_void_p),
+                ("ld_drop", ctypes.c_int64), ("drop_rows", ctypes.c_void_p),
+                ("ln_dw", ctypes.c_void_p), ("ln_db", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes); mirrors include/ttmi.h one-to-one.
 SIGNATURES = {
     "ttmi_last_error": (ctypes.c_char_p, []),
@@ -69,6 +84,7 @@ SIGNATURES = {
     "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
     "ttmi_step_inc": (c_i, [c_p, c_p]),
     "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_p]),
     "ttmi_cast_f32_bf16": (c_i, [c_i64, c_p, c_p, c_p]),

@@ -12,7 +12,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import lib as _L
-from .lib import BF16, F32, GemmDesc, call
+from .lib import BF16, F32, GemmDesc, LnBwdDesc, call
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -107,6 +107,31 @@ def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
     K = x.shape[1]
     return gemm(dy, x, gw, N, K, M, lda=N, a_kmajor=False, ldb=K, b_kmajor=False, ldc=K,
                 accumulate=True, split_k=split_k, rowsum_a=gb)
+
+
+def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, ln_w: Tensor,
+                  dx: Tensor, ln_dw: Optional[Tensor], ln_db: Optional[Tensor], *,
+                  res: Optional[Tensor] = None, next_: Optional[Tensor] = None,
+                  drop: Drop = NO_DROP, drop_rows: Optional[Tensor] = None) -> Tensor:
+    """dx = LN'(dh · wtᵀ) + res; ln_dw/ln_db += LN param grads; next_ = bf16(dropout(dx))
+    (one kernel: the Linear input grad, LayerNorm backward and dropout backward)."""
+    _dev(dh, wt, x, dx)
+    M, K = dh.shape
+    N = wt.shape[0]
+    d = LnBwdDesc()
+    d.M, d.N, d.K = M, N, K
+    d.dh, d.ld_dh = _p(dh), dh.stride(0)
+    d.wt, d.ld_wt = _p(wt), wt.stride(0)
+    d.x, d.ldx = _p(x), x.stride(0)
+    d.mean, d.rstd, d.ln_w = _p(mean), _p(rstd), _p(ln_w)
+    d.res, d.ld_res = _p(res), (res.stride(0) if res is not None else 0)
+    d.dx, d.lddx = _p(dx), dx.stride(0)
+    d.next, d.ld_next = _p(next_), (next_.stride(0) if next_ is not None else 0)
+    d.drop_p, d.drop_seed, d.ld_drop = float(drop[0]), _p(drop[1]), N
+    d.drop_rows = _p(drop_rows)
+    d.ln_dw, d.ln_db = _p(ln_dw), _p(ln_db)
+    call("ttmi_linear_ln_bwd", ctypes.byref(d), _s())
+    return dx
 
 
 # ----------------------------------------------------------------------------- norms

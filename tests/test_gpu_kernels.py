@@ -456,3 +456,44 @@ def test_transpose_batch(gpu_pkg):
     torch.cuda.synchronize()
     for s_, d in zip(srcs, dsts):
         assert torch.equal(d.cpu(), s_.t().cpu())
+
+
+@pytest.mark.parametrize("M,K", [(3000, 384), (2048, 512), (100, 128), (512, 256)])
+@pytest.mark.parametrize("with_res,with_next", [(True, True), (False, False), (True, False)])
+def test_linear_ln_bwd(gpu_pkg, M, K, with_res, with_next):
+    """Fused Linear input grad + LayerNorm backward (+ dropout backward) vs torch autograd
+    on the same bf16 operands (fp32 math): dx, LN dw/db, and the bf16 dropout output."""
+    ops = gpu_pkg.ops
+    D = 128
+    g = torch.Generator().manual_seed(M + K)
+    dh = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(D, K, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    x = torch.randn(M, D, generator=g) * 2 + 0.5
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    res = torch.randn(M, D, generator=g)
+    mean = x.mean(1)
+    rstd = 1.0 / torch.sqrt(x.var(1, unbiased=False) + 1e-5)
+    dY = dh.float() @ wt.float().t()
+    xt = x.clone().requires_grad_(True)
+    wt_ = w.clone().requires_grad_(True)
+    bt_ = b.clone().requires_grad_(True)
+    TF.layer_norm(xt, (D,), wt_, bt_, 1e-5).backward(dY)
+    dx_ref = xt.grad + (res if with_res else 0.0)
+    p, seed = 0.1, 0x77AA
+    rows = torch.randperm(3 * M, generator=g)[:M].to(torch.int32)
+    keep = keep_mask(seed, (3 * M, D), p).float()[rows.long()]
+    dx = torch.empty(M, D, device=DEV)
+    dw = torch.full((D,), 0.5, device=DEV)
+    db = torch.zeros(D, device=DEV)
+    nxt = torch.empty(M, D, device=DEV, dtype=torch.bfloat16) if with_next else None
+    ops.linear_ln_bwd(dh.to(DEV), wt.to(DEV), x.to(DEV), mean.to(DEV), rstd.to(DEV), w.to(DEV),
+                      dx, dw, db, res=res.to(DEV) if with_res else None, next_=nxt,
+                      drop=(p, seed_dev(seed)) if with_next else ops.NO_DROP,
+                      drop_rows=rows.to(DEV) if with_next else None)
+    torch.cuda.synchronize()
+    assert rel(dx, dx_ref) < 2e-5
+    assert rel(dw, 0.5 + wt_.grad) < 5e-5
+    assert rel(db, bt_.grad) < 5e-5
+    if with_next:
+        assert rel(nxt.float(), dx_ref * keep / (1 - p)) < 8e-3
