@@ -26,4 +26,11 @@ if [[ "$STEPS" == *prof* || "$STEPS" == all ]]; then
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 5 --skip-cpu) > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
   find gpurun_out/prof -name "*stats*" | head
 fi
+if [[ "$STEPS" == *traffic* ]]; then
+  run traffic
+  for c in FETCH_SIZE WRITE_SIZE; do
+    (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_$c -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --skip-cpu) > gpurun_out/pmc_$c.log 2>&1 || { tail -30 gpurun_out/pmc_$c.log; exit 1; }
+  done
+  find gpurun_out/pmc_* -name "*counter_collection*"
+fi
 echo DONE
