@@ -181,6 +181,35 @@ int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat, const
                      hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * Global in-batch negatives (BASELINE cfg 5; the reference InfoNCE two_tower.py:98-140
+ * applied to the concatenation of every rank's batch).  Per rank r with B local pairs and
+ * C = world·B gathered, L2-normalised rows:
+ *   loss_r = (Σ CE_rows(û_r·Îᵀ/τ) + Σ CE_rows(î_r·Ûᵀ/τ)) / 2B,  positives at column r·B + i,
+ *   collisions (same user_idx, different global index) masked to -1e4.
+ * The caller all-gathers Û, Î, user_idx and reduce-scatters the key grads; mean over ranks
+ * of loss_r is the global loss.  With world = 1 this is ttmi_infonce_fwd/bwd exactly.
+ * ---------------------------------------------------------------------------------- */
+/* y = x / max(||x||, 1e-12) per row; norms[n] = ||x|| (F.normalize). */
+int ttmi_l2norm_fwd(int n, int D, const float* x, float* y, float* norms, hipStream_t stream);
+/* dx = normalize backward of (dy + dy2) (dy2 may be NULL: the reduce-scattered key grads). */
+int ttmi_l2norm_bwd(int n, int D, const float* y, const float* norms, const float* dy,
+                    const float* dy2, float* dx, hipStream_t stream);
+/* logits[R,C] = q·kᵀ·inv_tau, masked in place; lse[R]; ce[R] = lse − logits[i, row0+i].
+ * uid_q/uid_k may both be NULL (no collision mask).  C % 4 == 0, row0 + R <= C. */
+int ttmi_rowce_fwd(int R, int C, int D, const float* q, const float* k, const int64_t* uid_q,
+                   const int64_t* uid_k, int64_t row0, float inv_tau, float* logits, float* lse,
+                   float* ce, hipStream_t stream);
+int64_t ttmi_rowce_workspace(int R, int C);
+/* dS = dloss·scale·(softmax − onehot(row0+i)) (0 where masked); dq = dS·k·inv_tau [R,D],
+ * dk = dSᵀ·q·inv_tau [C,D] (both written). */
+int ttmi_rowce_bwd(int R, int C, int D, const float* q, const float* k, const float* logits,
+                   const float* lse, const int64_t* uid_q, const int64_t* uid_k, int64_t row0,
+                   float inv_tau, const float* dloss, float scale, float* dq, float* dk, void* ws,
+                   hipStream_t stream);
+/* out[0] = scale · Σ x[0:n) (fixed order: deterministic). */
+int ttmi_sum_scaled(int n, const float* x, float scale, float* out, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * Fused AdamW over flat fp32 buffers (torch.optim.AdamW defaults, train.py:302):
  *   t = ++(*step); p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g²;
  *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps).

@@ -10,10 +10,10 @@ from . import ops
 from . import functional
 from .user_tower import SequentialUserEncoder
 from .item_tower import MultimodalItemEncoder
-from .two_tower import TwoTowerModel, infonce
+from .two_tower import TwoTowerModel, infonce, infonce_global
 from .train import (FlatParams, GradSync, TrainStep, cleanup_ddp, setup_ddp,
                     train_one_epoch)
 
 __all__ = ["lib", "ops", "functional", "SequentialUserEncoder", "MultimodalItemEncoder",
-           "TwoTowerModel", "infonce", "TrainStep", "FlatParams", "GradSync", "setup_ddp",
+           "TwoTowerModel", "infonce", "infonce_global", "TrainStep", "FlatParams", "GradSync", "setup_ddp",
            "cleanup_ddp", "train_one_epoch"]

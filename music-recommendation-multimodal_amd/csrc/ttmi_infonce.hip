@@ -164,6 +164,102 @@ __global__ __launch_bounds__(256) void l2norm_bwd_kernel(int B, int D, const flo
   }
 }
 
+// Single-tensor forms (wave per row) for the distributed InfoNCE pieces.
+__global__ __launch_bounds__(256) void rows_l2norm_kernel(int n, int D, const float* __restrict__ x,
+                                                          float* __restrict__ y,
+                                                          float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int r = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (r >= n) return;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += x[(int64_t)r * D + c] * x[(int64_t)r * D + c];
+  const float nrm = sqrtf(wave_sum(s));
+  const float inv = 1.f / fmaxf(nrm, NORM_EPS);
+  for (int c = lane; c < D; c += 64) y[(int64_t)r * D + c] = x[(int64_t)r * D + c] * inv;
+  if (lane == 0) norms[r] = nrm;
+}
+
+__global__ __launch_bounds__(256) void rows_l2norm_bwd_kernel(int n, int D, const float* __restrict__ y,
+                                                              const float* __restrict__ norms,
+                                                              const float* __restrict__ dy,
+                                                              const float* __restrict__ dy2,
+                                                              float* __restrict__ dx) {
+  const int lane = threadIdx.x & 63;
+  const int r = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (r >= n) return;
+  const float* yr = y + (int64_t)r * D;
+  const float* dyr = dy + (int64_t)r * D;
+  const float* dy2r = dy2 ? dy2 + (int64_t)r * D : nullptr;
+  float* dxr = dx + (int64_t)r * D;
+  const float nrm = norms[r];
+  auto g = [&](int c) { return dyr[c] + (dy2r ? dy2r[c] : 0.f); };
+  if (nrm > NORM_EPS) {
+    float s = 0.f;
+    for (int c = lane; c < D; c += 64) s += yr[c] * g(c);
+    s = wave_sum(s);
+    const float inv = 1.f / nrm;
+    for (int c = lane; c < D; c += 64) dxr[c] = (g(c) - yr[c] * s) * inv;
+  } else {
+    for (int c = lane; c < D; c += 64) dxr[c] = g(c) / NORM_EPS;
+  }
+}
+
+// ---------------------------------------------------------------- rectangular row CE
+// Global in-batch negatives (BASELINE cfg 5): each rank scores its R query rows against all
+// C = world·B gathered keys.  Row i's positive is column row0 + i; column j is masked to
+// MASK_FILL when uid_q[i] == uid_k[j] and j != row0 + i (two_tower.py:111-124 applied to the
+// concatenated global batch).  One wave per row: masked logits written back, LSE, CE.
+__global__ __launch_bounds__(256) void rowce_lse_kernel(int R, int C, int64_t row0,
+                                                        float* __restrict__ S,
+                                                        const int64_t* __restrict__ uq,
+                                                        const int64_t* __restrict__ uk,
+                                                        float* __restrict__ lse,
+                                                        float* __restrict__ ce) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= R) return;
+  float* row = S + (int64_t)i * C;
+  const int64_t tgt = row0 + i;
+  const bool mask = uq != nullptr && uk != nullptr;
+  const int64_t me = mask ? uq[i] : 0;
+  float m = -INFINITY;
+  for (int j = lane; j < C; j += 64) {
+    float v = row[j];
+    if (mask && j != tgt && uk[j] == me) { v = MASK_FILL; row[j] = v; }
+    m = fmaxf(m, v);
+  }
+  m = wave_max(m);
+  float sum = 0.f;
+  for (int j = lane; j < C; j += 64) sum += expf(row[j] - m);
+  sum = wave_sum(sum);
+  if (lane == 0) {
+    const float l = m + logf(sum);
+    lse[i] = l;
+    ce[i] = l - row[tgt];
+  }
+}
+
+// dS[i,j] = g·scale·(softmax_ij − [j == row0+i]), 0 at masked entries.
+__global__ __launch_bounds__(256) void rowce_dlogits_kernel(int R, int C, int64_t row0,
+                                                            const float* __restrict__ S,
+                                                            const float* __restrict__ lse,
+                                                            const int64_t* __restrict__ uq,
+                                                            const int64_t* __restrict__ uk,
+                                                            const float* __restrict__ dloss,
+                                                            float scale, float* __restrict__ dS) {
+  const int64_t n = (int64_t)R * C;
+  const float g = (dloss ? dloss[0] : 1.f) * scale;
+  const bool mask = uq != nullptr && uk != nullptr;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(k / C), j = (int)(k % C);
+    const bool pos = j == row0 + i;
+    float d = 0.f;
+    if (!(mask && !pos && uk[j] == uq[i])) d = g * (expf(S[k] - lse[i]) - (pos ? 1.f : 0.f));
+    dS[k] = d;
+  }
+}
+
 struct Ws {
   float* dS; float* ce; float* duh; float* dih;
 };
@@ -248,4 +344,69 @@ extern "C" int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i
   hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u_hat, i_hat,
                      norms, w.duh, w.dih, du, di);
   return ttmi_check_launch("ttmi_infonce_bwd/l2norm_bwd");
+}
+
+// ------------------------------------------------------------ building blocks (cfg 5)
+extern "C" int ttmi_l2norm_fwd(int n, int D, const float* x, float* y, float* norms,
+                               hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && D > 0, "ttmi_l2norm_fwd: bad sizes");
+  if (n == 0) return TTMI_OK;
+  TTMI_REQUIRE(x && y && norms, "ttmi_l2norm_fwd: null argument");
+  hipLaunchKernelGGL(rows_l2norm_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, D, x, y, norms);
+  return ttmi_check_launch("ttmi_l2norm_fwd");
+}
+
+extern "C" int ttmi_l2norm_bwd(int n, int D, const float* y, const float* norms, const float* dy,
+                               const float* dy2, float* dx, hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && D > 0, "ttmi_l2norm_bwd: bad sizes");
+  if (n == 0) return TTMI_OK;
+  TTMI_REQUIRE(y && norms && dy && dx, "ttmi_l2norm_bwd: null argument");
+  hipLaunchKernelGGL(rows_l2norm_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, D, y, norms, dy,
+                     dy2, dx);
+  return ttmi_check_launch("ttmi_l2norm_bwd");
+}
+
+extern "C" int ttmi_rowce_fwd(int R, int C, int D, const float* q, const float* k,
+                              const int64_t* uid_q, const int64_t* uid_k, int64_t row0,
+                              float inv_tau, float* logits, float* lse, float* ce, hipStream_t s) {
+  TTMI_REQUIRE(R > 0 && C > 0 && D > 0 && D % 4 == 0 && row0 >= 0 && row0 + R <= C,
+               "ttmi_rowce_fwd: need D %% 4 == 0 and 0 <= row0, row0 + R <= C");
+  TTMI_REQUIRE(q && k && logits && lse && ce, "ttmi_rowce_fwd: null argument");
+  TTMI_REQUIRE(C % 4 == 0, "ttmi_rowce_fwd: C must be a multiple of 4");
+  ttmi_gemm_desc g = f32_gemm(R, C, D, q, D, 1, k, D, 1, logits, C, inv_tau);
+  int rc = ttmi_gemm(&g, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rowce_lse_kernel, dim3((R + 3) / 4), dim3(256), 0, s, R, C, row0, logits, uid_q,
+                     uid_k, lse, ce);
+  return ttmi_check_launch("ttmi_rowce_fwd");
+}
+
+extern "C" int64_t ttmi_rowce_workspace(int R, int C) { return ((int64_t)R * C * 4 + 255) / 256 * 256; }
+
+extern "C" int ttmi_rowce_bwd(int R, int C, int D, const float* q, const float* k,
+                              const float* logits, const float* lse, const int64_t* uid_q,
+                              const int64_t* uid_k, int64_t row0, float inv_tau,
+                              const float* dloss, float scale, float* dq, float* dk, void* ws,
+                              hipStream_t s) {
+  TTMI_REQUIRE(R > 0 && C > 0 && D > 0 && D % 4 == 0 && C % 4 == 0 && row0 >= 0 && row0 + R <= C,
+               "ttmi_rowce_bwd: bad sizes");
+  TTMI_REQUIRE(q && k && logits && lse && dq && dk && ws, "ttmi_rowce_bwd: null argument");
+  float* dS = static_cast<float*>(ws);
+  const int64_t n = (int64_t)R * C;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(rowce_dlogits_kernel, dim3(grid), dim3(256), 0, s, R, C, row0, logits, lse,
+                     uid_q, uid_k, dloss, scale, dS);
+  int rc = ttmi_check_launch("ttmi_rowce_bwd/dlogits");
+  if (rc) return rc;
+  ttmi_gemm_desc g1 = f32_gemm(R, D, C, dS, C, 1, k, D, 0, dq, D, inv_tau);   // dq = dS·k
+  rc = ttmi_gemm(&g1, s);
+  if (rc) return rc;
+  ttmi_gemm_desc g2 = f32_gemm(C, D, R, dS, C, 0, q, D, 0, dk, D, inv_tau);   // dk = dSᵀ·q
+  return ttmi_gemm(&g2, s);
+}
+
+extern "C" int ttmi_sum_scaled(int n, const float* x, float scale, float* out, hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && x && out, "ttmi_sum_scaled: bad argument");
+  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, n, x, scale, out);
+  return ttmi_check_launch("ttmi_sum_scaled");
 }

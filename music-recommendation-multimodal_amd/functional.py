@@ -465,3 +465,89 @@ def count_flops_user(B: int, L: int, D: int, n_layers: int, ffn: int, extra: int
     fwd = n_layers * per_layer + 2 * B * (D + extra) * D + 2 * B * D * D
     return 3.0 * fwd
 
+
+
+# ============================================================ global negatives (cfg 5)
+@dataclass
+class GlobalLossSaved:
+    u_hat: Tensor
+    i_hat: Tensor
+    nu: Tensor
+    ni: Tensor
+    U: Tensor            # gathered û of every rank [W·B, D]
+    I: Tensor            # gathered î
+    uid: Optional[Tensor]
+    UID: Optional[Tensor]
+    row0: int
+    s_u2i: Tensor
+    lse_u2i: Tensor
+    s_i2u: Tensor
+    lse_i2u: Tensor
+    inv_tau: float
+
+
+def infonce_global_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float,
+                       group=None):
+    """InfoNCE over the concatenation of every rank's batch (BASELINE cfg 5; the reference
+    two_tower.py:98-140 applied to world·B rows).  Returns (loss_r, logits_u2i [B, W·B],
+    û_r, î_r, saved); the global loss is the mean of loss_r over ranks, which DDP's 1/world
+    gradient scaling realises.  All-gathers û, î and user_idx over `group` (RCCL)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    B, D = u.shape
+    dev = u.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    u_hat, i_hat = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+    nu, ni = torch.empty(B, **f32), torch.empty(B, **f32)
+    ops.l2norm_fwd(u.contiguous().float(), u_hat, nu)
+    ops.l2norm_fwd(it.contiguous().float(), i_hat, ni)
+    if world > 1:
+        U, I = torch.empty(world * B, D, **f32), torch.empty(world * B, D, **f32)
+        dist.all_gather_into_tensor(U, u_hat, group=group)
+        dist.all_gather_into_tensor(I, i_hat, group=group)
+        UID = None
+        if user_idx is not None:
+            UID = torch.empty(world * B, device=dev, dtype=torch.int64)
+            dist.all_gather_into_tensor(UID, user_idx.contiguous(), group=group)
+    else:
+        U, I, UID = u_hat, i_hat, user_idx
+    uid = user_idx.contiguous() if user_idx is not None else None
+    row0 = rank * B
+    inv_tau = 1.0 / temperature
+    C = world * B
+    s_u2i, s_i2u = torch.empty(B, C, **f32), torch.empty(B, C, **f32)
+    lse_u2i, lse_i2u = torch.empty(B, **f32), torch.empty(B, **f32)
+    ce = torch.empty(2 * B, **f32)
+    ops.rowce_fwd(u_hat, I, uid, UID, row0, inv_tau, s_u2i, lse_u2i, ce[:B])
+    ops.rowce_fwd(i_hat, U, uid, UID, row0, inv_tau, s_i2u, lse_i2u, ce[B:])
+    loss = torch.empty(1, **f32)
+    ops.sum_scaled(ce, 0.5 / B, loss)
+    saved = GlobalLossSaved(u_hat, i_hat, nu, ni, U, I, uid, UID, row0, s_u2i, lse_u2i, s_i2u,
+                            lse_i2u, inv_tau)
+    return loss.view(()), s_u2i, u_hat, i_hat, saved
+
+
+def infonce_global_bwd(st: GlobalLossSaved, dloss: Optional[Tensor], du: Tensor, di: Tensor,
+                       group=None) -> None:
+    """Backward of infonce_global_fwd for this rank's loss_r: local-row grads, key grads for
+    every rank's rows reduce-scattered (SUM) back to their owners, then normalize backward."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    B, D = st.u_hat.shape
+    f32 = dict(device=st.u_hat.device, dtype=torch.float32)
+    scale = 0.5 / B
+    duh, dih = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+    dI, dU = torch.empty(world * B, D, **f32), torch.empty(world * B, D, **f32)
+    ops.rowce_bwd(st.u_hat, st.I, st.s_u2i, st.lse_u2i, st.uid, st.UID, st.row0, st.inv_tau,
+                  dloss, scale, duh, dI)
+    ops.rowce_bwd(st.i_hat, st.U, st.s_i2u, st.lse_i2u, st.uid, st.UID, st.row0, st.inv_tau,
+                  dloss, scale, dih, dU)
+    if world > 1:
+        rs_u, rs_i = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+        dist.reduce_scatter_tensor(rs_u, dU, group=group)
+        dist.reduce_scatter_tensor(rs_i, dI, group=group)
+    else:
+        rs_u, rs_i = dU, dI
+    ops.l2norm_bwd(st.u_hat, st.nu, duh, du, dy2=rs_u)
+    ops.l2norm_bwd(st.i_hat, st.ni, dih, di, dy2=rs_i)

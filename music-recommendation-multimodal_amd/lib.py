@@ -85,6 +85,13 @@ SIGNATURES = {
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
+    "ttmi_l2norm_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_l2norm_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_rowce_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_p, c_p, c_p]),
+    "ttmi_rowce_workspace": (c_i64, [c_i, c_i]),
+    "ttmi_rowce_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_f,
+                             c_p, c_p, c_p, c_p]),
+    "ttmi_sum_scaled": (c_i, [c_i, c_p, c_f, c_p, c_p]),
     "ttmi_step_inc": (c_i, [c_p, c_p]),
     "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_p]),
     "ttmi_cast_f32_bf16": (c_i, [c_i64, c_p, c_p, c_p]),

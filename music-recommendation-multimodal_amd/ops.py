@@ -134,6 +134,49 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
     return dx
 
 
+# ----------------------------------------------------------------------------- cfg 5 pieces
+def l2norm_fwd(x: Tensor, y: Tensor, norms: Tensor) -> Tensor:
+    _dev(x, y, norms)
+    n, D = x.shape
+    call("ttmi_l2norm_fwd", n, D, _p(x), _p(y), _p(norms), _s())
+    return y
+
+
+def l2norm_bwd(y: Tensor, norms: Tensor, dy: Tensor, dx: Tensor,
+               dy2: Optional[Tensor] = None) -> Tensor:
+    n, D = y.shape
+    call("ttmi_l2norm_bwd", n, D, _p(y), _p(norms), _p(dy), _p(dy2), _p(dx), _s())
+    return dx
+
+
+def rowce_fwd(q: Tensor, k: Tensor, uid_q: Optional[Tensor], uid_k: Optional[Tensor], row0: int,
+              inv_tau: float, logits: Tensor, lse: Tensor, ce: Tensor) -> Tensor:
+    """logits = q·kᵀ·inv_tau (collision-masked), lse, ce per row; positives at row0 + i."""
+    _dev(q, k, logits)
+    R, D = q.shape
+    C = k.shape[0]
+    call("ttmi_rowce_fwd", R, C, D, _p(q), _p(k), _p(uid_q), _p(uid_k), row0, inv_tau,
+         _p(logits), _p(lse), _p(ce), _s())
+    return logits
+
+
+def rowce_bwd(q: Tensor, k: Tensor, logits: Tensor, lse: Tensor, uid_q: Optional[Tensor],
+              uid_k: Optional[Tensor], row0: int, inv_tau: float, dloss: Optional[Tensor],
+              scale: float, dq: Tensor, dk: Tensor) -> None:
+    R, D = q.shape
+    C = k.shape[0]
+    _L.load()
+    ws = torch.empty(int(_L._lib.ttmi_rowce_workspace(R, C)), device=q.device,
+                     dtype=torch.uint8)
+    call("ttmi_rowce_bwd", R, C, D, _p(q), _p(k), _p(logits), _p(lse), _p(uid_q), _p(uid_k),
+         row0, inv_tau, _p(dloss), scale, _p(dq), _p(dk), _p(ws), _s())
+
+
+def sum_scaled(x: Tensor, scale: float, out: Tensor) -> Tensor:
+    call("ttmi_sum_scaled", x.numel(), _p(x), scale, _p(out), _s())
+    return out
+
+
 # ----------------------------------------------------------------------------- norms
 def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor, *,
                   eps: float = 1e-5, relu: bool = False, drop: Drop = NO_DROP) -> Tensor:

@@ -53,6 +53,38 @@ def infonce(user_emb: Tensor, item_emb: Tensor, user_idx: Optional[Tensor],
     return loss, logits, uh, ih
 
 
+class _GlobalInfoNCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, temperature, user_idx, group, u, it):
+        loss, logits, u_hat, i_hat, st = F.infonce_global_fwd(u, it, user_idx, temperature, group)
+        ctx.st, ctx.group = st, group
+        ctx.mark_non_differentiable(logits, u_hat, i_hat)
+        return loss, logits, u_hat, i_hat
+
+    @staticmethod
+    def backward(ctx, dloss, _dlogits, _du_hat, _di_hat):
+        st, group = ctx.st, ctx.group
+        del ctx.st
+        du = torch.empty_like(st.u_hat)
+        di = torch.empty_like(st.i_hat)
+        F.infonce_global_bwd(st, dloss.reshape(1).float().contiguous(), du, di, group)
+        return None, None, None, du, di
+
+
+def infonce_global(user_emb: Tensor, item_emb: Tensor, user_idx: Optional[Tensor],
+                   temperature: float = 0.07, group=None):
+    """Global in-batch negatives (BASELINE cfg 5): this rank's share of the reference InfoNCE
+    over every rank's batch (RCCL all-gather of û, î, user_idx; reduce-scatter of the key
+    grads).  logits are this rank's u2i rows [B, world·B].  Averaging the per-rank losses (or
+    DDP's gradient average) gives the loss of the concatenated batch."""
+    u = user_emb.float().contiguous()
+    i = item_emb.float().contiguous()
+    if torch.is_grad_enabled() and (u.requires_grad or i.requires_grad):
+        return _GlobalInfoNCEFn.apply(temperature, user_idx, group, u, i)
+    loss, logits, uh, ih, _ = F.infonce_global_fwd(u, i, user_idx, temperature, group)
+    return loss, logits, uh, ih
+
+
 class TwoTowerModel(nn.Module):
     def __init__(self, vocab_size: int, tabular_input_dim: int, num_genders: int = 1,
                  num_countries: int = 1, max_seq_len: int = 50, user_embedding_dim: int = 256,
@@ -61,8 +93,11 @@ class TwoTowerModel(nn.Module):
                  text_model_name: str = "microsoft/mdeberta-v3-base", text_dim: int = 128,
                  tabular_dim: int = 128, use_lora: bool = True, temperature: float = 0.07, *,
                  compute_dtype: torch.dtype = torch.bfloat16,
-                 precomputed_modalities: bool = True):
+                 precomputed_modalities: bool = True, global_negatives: bool = False,
+                 process_group=None):
         super().__init__()
+        self.global_negatives = global_negatives   # cfg 5: negatives from every rank's batch
+        self.process_group = process_group
         assert user_embedding_dim == item_embedding_dim, \
             f"User dim ({user_embedding_dim}) must match Item dim ({item_embedding_dim})"
         self.temperature = temperature
@@ -89,6 +124,9 @@ class TwoTowerModel(nn.Module):
                                    user_country=batch["user_country"],
                                    history_mask=batch.get("history_mask"), seeds=seeds)
         item_emb = self._item(batch, seeds)
+        if self.global_negatives:
+            return infonce_global(user_emb, item_emb, batch.get("user_idx"), self.temperature,
+                                  self.process_group)
         return infonce(user_emb, item_emb, batch.get("user_idx"), self.temperature)
 
     def get_user_embedding(self, history_ids, history_mask=None, user_gender=None,

@@ -1,0 +1,115 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the data-parallel pieces.
+
+* GradSync: the 1/world loss scale + bucketed SUM all-reduce of the flat gradient buffer
+  equals DDP's average (reference train.py:300), over buckets smaller than the buffer.
+* Global negatives (BASELINE cfg 5): the per-rank decomposition the GPU path implements
+  (all-gather û, î, user_idx; rank r scores its rows against every rank's; key grads summed
+  back to their owners) reproduces the reference InfoNCE on the concatenated batch — loss and
+  embedding gradients.  The per-rank math is the oracle restatement (oracle.infonce_rank);
+  the collectives are real.  Gloo has no reduce_scatter, so the owner-sum is an all_reduce
+  followed by the owner's slice (same result as reduce_scatter_tensor on RCCL).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import two_tower_ref as ref
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(fn, *args):
+    port = _free_port()
+    mp.spawn(_entry, args=(fn, port, args), nprocs=WORLD, join=True)
+
+
+def _entry(rank, fn, port, args):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        torch.set_num_threads(1)
+        fn(rank, *args)
+    finally:
+        dist.destroy_process_group()
+
+
+def _grad_sync_worker(rank):
+    import importlib
+    pkg = importlib.import_module("music-recommendation-multimodal_amd")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(37, 19), torch.nn.Linear(19, 5))
+    flat = pkg.FlatParams(model)
+    # params are views into the flat buffer, in the same slots for grads
+    views = flat.views(flat.grad)
+    for n, p in model.named_parameters():
+        assert p.data.data_ptr() == flat.views(flat.data)[n].data_ptr()
+    g = torch.Generator().manual_seed(100 + rank)
+    local = torch.randn(flat.numel, generator=g)
+    sync = pkg.GradSync(bucket_bytes=64 * 4)                 # many buckets
+    assert sync.world == WORLD and abs(sync.loss_scale - 1.0 / WORLD) < 1e-12
+    flat.grad.copy_(local * sync.loss_scale)                 # the step pre-scales dloss
+    sync(flat.grad)
+    every = [torch.randn(flat.numel, generator=torch.Generator().manual_seed(100 + r))
+             for r in range(WORLD)]
+    expect = sum(every) / WORLD
+    assert torch.allclose(flat.grad, expect, atol=1e-6)
+    assert set(views) == {n for n, _ in model.named_parameters()}
+
+
+def test_grad_sync_averages_over_buckets():
+    _run(_grad_sync_worker)
+
+
+def _global_negatives_worker(rank, B, D, collide):
+    g = torch.Generator().manual_seed(7)
+    u_all = torch.randn(WORLD * B, D, generator=g, dtype=torch.float64)
+    i_all = torch.randn(WORLD * B, D, generator=g, dtype=torch.float64)
+    uid_all = torch.randint(0, 3 * B if collide else 10**6, (WORLD * B,), generator=g)
+    sl = slice(rank * B, (rank + 1) * B)
+    u = u_all[sl].clone().requires_grad_(True)
+    it = i_all[sl].clone().requires_grad_(True)
+    # --- the distributed algorithm (as functional.infonce_global_fwd/bwd run it)
+    uh = torch.nn.functional.normalize(u, dim=1)
+    ih = torch.nn.functional.normalize(it, dim=1)
+    U = [torch.empty_like(uh) for _ in range(WORLD)]
+    I = [torch.empty_like(ih) for _ in range(WORLD)]
+    UID = [torch.empty_like(uid_all[sl]) for _ in range(WORLD)]
+    dist.all_gather(U, uh.detach())
+    dist.all_gather(I, ih.detach())
+    dist.all_gather(UID, uid_all[sl].clone())
+    U = torch.cat(U).requires_grad_(True)
+    I = torch.cat(I).requires_grad_(True)
+    UID = torch.cat(UID)
+    loss_r = ref.infonce_rank(uh, ih, U, I, uid_all[sl], UID, rank * B)
+    # DDP's 1/world scaling of each rank's loss
+    duh, dih, dU, dI = torch.autograd.grad(loss_r / WORLD, [uh, ih, U, I])
+    dist.all_reduce(dU)                    # reduce-scatter: owner takes its slice of the sum
+    dist.all_reduce(dI)
+    torch.autograd.backward([uh, ih], [duh + dU[sl], dih + dI[sl]])
+    loss_mean = loss_r.detach().clone()
+    dist.all_reduce(loss_mean)
+    loss_mean /= WORLD
+    # --- the reference on the concatenated global batch
+    ua = u_all.clone().requires_grad_(True)
+    ia = i_all.clone().requires_grad_(True)
+    lref, _, _, _ = ref.infonce(ua, ia, uid_all)
+    lref.backward()
+    assert abs(float(loss_mean) - float(lref)) < 1e-12
+    assert torch.allclose(u.grad, ua.grad[sl], atol=1e-12)
+    assert torch.allclose(it.grad, ia.grad[sl], atol=1e-12)
+
+
+@pytest.mark.parametrize("collide", [False, True])
+def test_global_negatives_decomposition(collide):
+    _run(_global_negatives_worker, 16, 8, collide)

@@ -360,3 +360,77 @@ def test_train_step_graph_equals_eager_and_learns(gpu_pkg):
     assert abs(l1[0] - l2[0]) < 1e-5, (l1[0], l2[0])           # same params, same masks
     assert np.allclose(l1[1:3], l2[1:3], rtol=0, atol=5e-3), (l1[:3], l2[:3])
     assert l1[-1] < l1[0] - 0.3, l1
+
+
+@pytest.mark.parametrize("collide", [False, True])
+def test_global_negatives_kernels_simulated_world(gpu_pkg, collide):
+    """cfg-5 pieces (l2norm, rectangular row CE fwd/bwd, owner-summed key grads) for two
+    simulated ranks in one process vs the reference InfoNCE on the concatenated batch
+    (fp32 path: 1e-5 relative)."""
+    ops = gpu_pkg.ops
+    W, B, D, tau = 2, 64, 128, 0.07
+    g = torch.Generator().manual_seed(3)
+    u_all = torch.randn(W * B, D, generator=g)
+    i_all = torch.randn(W * B, D, generator=g)
+    uid = torch.randint(0, 40 if collide else 10**6, (W * B,), generator=g)
+    ua, ia = u_all.clone().requires_grad_(True), i_all.clone().requires_grad_(True)
+    lref, _, _, _ = ref.infonce(ua, ia, uid, tau)
+    lref.backward()
+    f32 = dict(device=DEV, dtype=torch.float32)
+    uh = [torch.empty(B, D, **f32) for _ in range(W)]
+    ih = [torch.empty(B, D, **f32) for _ in range(W)]
+    nu = [torch.empty(B, **f32) for _ in range(W)]
+    ni = [torch.empty(B, **f32) for _ in range(W)]
+    for r in range(W):
+        ops.l2norm_fwd(u_all[r * B:(r + 1) * B].to(DEV), uh[r], nu[r])
+        ops.l2norm_fwd(i_all[r * B:(r + 1) * B].to(DEV), ih[r], ni[r])
+    U, I, UID = torch.cat(uh), torch.cat(ih), uid.to(DEV)
+    losses, saved = [], []
+    for r in range(W):
+        s1, s2 = torch.empty(B, W * B, **f32), torch.empty(B, W * B, **f32)
+        l1, l2, ce = torch.empty(B, **f32), torch.empty(B, **f32), torch.empty(2 * B, **f32)
+        uq = UID[r * B:(r + 1) * B]
+        ops.rowce_fwd(uh[r], I, uq, UID, r * B, 1 / tau, s1, l1, ce[:B])
+        ops.rowce_fwd(ih[r], U, uq, UID, r * B, 1 / tau, s2, l2, ce[B:])
+        loss = torch.empty(1, **f32)
+        ops.sum_scaled(ce, 0.5 / B, loss)
+        losses.append(float(loss))
+        saved.append((s1, l1, s2, l2, uq))
+    assert abs(sum(losses) / W - float(lref)) < 1e-5 * max(1.0, abs(float(lref)))
+    dloss = torch.full((1,), 1.0 / W, **f32)
+    duh = [torch.empty(B, D, **f32) for _ in range(W)]
+    dih = [torch.empty(B, D, **f32) for _ in range(W)]
+    dU, dI = torch.zeros(W * B, D, **f32), torch.zeros(W * B, D, **f32)
+    for r in range(W):
+        s1, l1, s2, l2, uq = saved[r]
+        dIr, dUr = torch.empty(W * B, D, **f32), torch.empty(W * B, D, **f32)
+        ops.rowce_bwd(uh[r], I, s1, l1, uq, UID, r * B, 1 / tau, dloss, 0.5 / B, duh[r], dIr)
+        ops.rowce_bwd(ih[r], U, s2, l2, uq, UID, r * B, 1 / tau, dloss, 0.5 / B, dih[r], dUr)
+        dU += dUr          # the reduce-scatter's sum (test harness)
+        dI += dIr
+    for r in range(W):
+        sl = slice(r * B, (r + 1) * B)
+        du, di = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+        ops.l2norm_bwd(uh[r], nu[r], duh[r], du, dy2=dU[sl].contiguous())
+        ops.l2norm_bwd(ih[r], ni[r], dih[r], di, dy2=dI[sl].contiguous())
+        assert rel(du, ua.grad[sl]) < 1e-5
+        assert rel(di, ia.grad[sl]) < 1e-5
+
+
+def test_global_infonce_world1_equals_local(gpu_pkg):
+    """functional.infonce_global_fwd/bwd without a process group is the local InfoNCE."""
+    F = gpu_pkg.functional
+    B, D = 96, 128
+    g = torch.Generator().manual_seed(9)
+    u, it = torch.randn(B, D, generator=g), torch.randn(B, D, generator=g)
+    uid = torch.randint(0, 30, (B,), generator=g)
+    ua, ia = u.clone().requires_grad_(True), it.clone().requires_grad_(True)
+    lref, sref, _, _ = ref.infonce(ua, ia, uid)
+    lref.backward()
+    loss, logits, _, _, st = F.infonce_global_fwd(u.to(DEV), it.to(DEV), uid.to(DEV), 0.07)
+    assert abs(float(loss) - float(lref)) < 1e-5 * max(1.0, abs(float(lref)))
+    assert rel(logits, sref) < 1e-5
+    du, di = torch.empty(B, D, device=DEV), torch.empty(B, D, device=DEV)
+    F.infonce_global_bwd(st, None, du, di)
+    assert rel(du, ua.grad) < 1e-5
+    assert rel(di, ia.grad) < 1e-5
