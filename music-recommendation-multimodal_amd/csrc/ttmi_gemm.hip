@@ -447,13 +447,11 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   const int64_t tile_end = std::min<int64_t>((g.M + 15) / 16, tile_beg + tiles_per_wg);
   const int64_t tile0 = tile_beg + wave;
   uint4 a0[4];                       // this wave's first A fragments, in flight under the W load
-  {
-    const int64_t m = tile0 * 16 + li;
+  {                                  // (rows clamped into range: unconditional loads)
+    const int64_t m = std::min<int64_t>(tile0 * 16 + li, g.M - 1);
     const char* ap = g.A + (m * g.lda + lg * (K / 4)) * 2;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      a0[c] = (tile0 < tile_end && m < g.M) ? *reinterpret_cast<const uint4*>(ap + 16 * c)
-                                            : make_uint4(0, 0, 0, 0);
+    for (int c = 0; c < 4; ++c) a0[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
   }
   {   // W -> LDS, coalesced 16-byte chunks
     constexpr int CPR = K / 8;
@@ -477,7 +475,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   for (int64_t tile = tile_beg + wave; tile < tile_end; tile += 8) {
     const int64_t m = tile * 16 + li;
     const bool mok = m < g.M;
-    const char* ap = g.A + (m * g.lda + lg * (K / 4)) * 2;
+    const char* ap = g.A + (std::min<int64_t>(m, g.M - 1) * g.lda + lg * (K / 4)) * 2;
     // column groups of 128 (8 MFMA tiles) and k groups of 4 chunks keep the accumulator,
     // A and W fragment state bounded (A re-reads per column group hit L1/L2)
 #pragma unroll 1
@@ -494,8 +492,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
           for (int c = 0; c < 4; ++c) a[c] = a0[c];
         } else {
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            a[c] = mok ? *reinterpret_cast<const uint4*>(ap + 64 * cq + 16 * c) : make_uint4(0, 0, 0, 0);
+          for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const uint4*>(ap + 64 * cq + 16 * c);
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -802,6 +799,7 @@ void launch_typed(const GemmArgs& a, bool ak, bool bk, int bm, int bn, dim3 grid
   if (bm == 128 && bn == 128) launch_layout<T, 128, 128>(a, ak, bk, grid, s);
   else if (bm == 128) launch_layout<T, 128, 64>(a, ak, bk, grid, s);
   else if (bn == 128) launch_layout<T, 64, 128>(a, ak, bk, grid, s);
+  else if (bm == 32) launch_layout<T, 32, 32>(a, ak, bk, grid, s);
   else launch_layout<T, 64, 64>(a, ak, bk, grid, s);
 }
 
@@ -969,8 +967,10 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   int bm, bn;
   const int64_t tiles128 = ((d->M + 127) / 128) * ((d->N + 127) / 128);
   const int64_t tiles64x128 = ((d->M + 63) / 64) * ((d->N + 127) / 128);
+  const int64_t tiles64 = ((d->M + 63) / 64) * ((d->N + 63) / 64);
   if (d->N > 64 && tiles128 >= 256) { bm = 128; bn = 128; }
   else if (d->N > 64 && tiles64x128 >= 128) { bm = 64; bn = 128; }
+  else if (tiles64 < 128 && d->c_mode == 0) { bm = 32; bn = 32; }   // small GEMMs: fill the CUs
   else { bm = 64; bn = 64; }
   if (const char* e = getenv("TTMI_GEMM_TILE")) {     // tuning runs only
     int tm = 0, tn = 0;

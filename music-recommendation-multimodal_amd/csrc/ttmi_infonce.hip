@@ -260,6 +260,264 @@ __global__ __launch_bounds__(256) void rowce_dlogits_kernel(int R, int C, int64_
   }
 }
 
+// ------------------------------------------------------------ fused local InfoNCE
+// Both CE directions as rows: direction 0 scores û_i against every î_j (rows of S),
+// direction 1 scores î_j against every û_i (rows of Sᵀ = columns of S).  A workgroup owns 16
+// query rows of one direction and one of NSPLIT key ranges (2·(B/16)·NSPLIT workgroups);
+// f32 MFMA (16x16x4, exact fp32 products) gives the 16x16 logit tiles, each lane keeps an
+// online (max, sum-exp) over its keys; partials are merged by nce_combine_kernel.
+constexpr int NQ = 16, NSPLIT = 4;
+
+TTMI_DEV void online_add(float& m, float& s, float v) {
+  if (v == -INFINITY) return;
+  if (v > m) { s = s * expf(m - v) + 1.f; m = v; }
+  else s += expf(v - m);
+}
+TTMI_DEV void online_merge(float& m, float& s, float m2, float s2) {
+  if (m2 == -INFINITY) return;
+  if (m == -INFINITY) { m = m2; s = s2; return; }
+  const float M = fmaxf(m, m2);
+  s = s * expf(m - M) + s2 * expf(m2 - M);
+  m = M;
+}
+
+template <int DC>
+__global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __restrict__ uh,
+                                                      const float* __restrict__ ih,
+                                                      const int64_t* __restrict__ uid,
+                                                      float inv_tau, float* __restrict__ logits,
+                                                      float* __restrict__ part) {
+  constexpr int D = 16 * DC, QP = D * 4 + 16;
+  __shared__ __attribute__((aligned(16))) char sq[NQ * QP];
+  __shared__ float sm[4][NQ], ss[4][NQ], st[4][NQ];
+  const int nb = (B + NQ - 1) / NQ;
+  const int split = blockIdx.x % NSPLIT;
+  const int qb = blockIdx.x / NSPLIT;
+  const int dir = qb >= nb;
+  const int i0 = (qb - dir * nb) * NQ;
+  const float* Q = dir ? ih : uh;
+  const float* Kp = dir ? uh : ih;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
+  for (int idx = tid; idx < NQ * D / 4; idx += 256) {
+    const int r = idx / (D / 4), c4 = idx % (D / 4);
+    const int row = i0 + r;
+    const float4 v = row < B ? *reinterpret_cast<const float4*>(Q + (int64_t)row * D + 4 * c4)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(sq + r * QP + c4 * 16) = v;
+  }
+  __syncthreads();
+  const int i = i0 + li;
+  const bool iok = i < B;
+  const int64_t ui = (uid && iok) ? uid[i] : 0;
+  float m = -INFINITY, sum = 0.f, tgt = 0.f;
+  const int nkt = (B + 15) / 16;
+  const int kt0 = (int)((int64_t)nkt * split / NSPLIT), kt1 = (int)((int64_t)nkt * (split + 1) / NSPLIT);
+  for (int t = kt0 + wave; t < kt1; t += 4) {
+    f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int jrow = 16 * t + li;
+    const float* kp = Kp + (int64_t)min(jrow, B - 1) * D + 4 * lg;   // clamped; masked below
+    uint4 a[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c) a[c] = *reinterpret_cast<const uint4*>(kp + 16 * c);
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+      const uint4 b = lds16(sq + li * QP + (16 * c + 4 * lg) * 4);
+      Mma<float>::run(acc, a[c], b);
+    }
+    // this lane: query row li, keys 16t + 4lg + r
+    float o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * t + 4 * lg + r;
+      float v = acc[r] * inv_tau;
+      if (j >= B) v = -INFINITY;
+      else if (uid && j != i && uid[j] == ui) v = MASK_FILL;
+      if (j == i) tgt = v;
+      o[r] = v;
+      online_add(m, sum, v);
+    }
+    if (dir == 0 && iok && 16 * t + 4 * lg < B)
+      *reinterpret_cast<float4*>(logits + (int64_t)i * B + 16 * t + 4 * lg) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  // merge the 4 lane groups holding row li, then the 4 waves
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(sum, off, 64);
+    online_merge(m, sum, m2, s2);
+    tgt += __shfl_xor(tgt, off, 64);
+  }
+  if (lg == 0) { sm[wave][li] = m; ss[wave][li] = sum; st[wave][li] = tgt; }
+  __syncthreads();
+  if (tid < NQ && i0 + tid < B) {
+    float M = sm[0][tid], S_ = ss[0][tid], T = st[0][tid];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) { online_merge(M, S_, sm[w][tid], ss[w][tid]); T += st[w][tid]; }
+    const int64_t row = (int64_t)dir * B + i0 + tid;
+    part[(0 * NSPLIT + split) * 2 * (int64_t)B + row] = M;
+    part[(1 * NSPLIT + split) * 2 * (int64_t)B + row] = S_;
+    part[(2 * NSPLIT + split) * 2 * (int64_t)B + row] = T;
+  }
+}
+
+// lse[2B], loss = Σ CE / 2B (one block of 1024 threads, fixed order: deterministic).
+__global__ __launch_bounds__(1024) void nce_combine_kernel(int B, const float* __restrict__ part,
+                                                           float* __restrict__ lse,
+                                                           float* __restrict__ loss) {
+  __shared__ float red[1024];
+  const int64_t n = 2 * (int64_t)B;
+  float acc = 0.f;
+  for (int64_t r = threadIdx.x; r < n; r += 1024) {
+    float pm[NSPLIT], ps[NSPLIT], T = 0.f;
+#pragma unroll
+    for (int k = 0; k < NSPLIT; ++k) {
+      pm[k] = part[(0 * NSPLIT + k) * n + r];
+      ps[k] = part[(1 * NSPLIT + k) * n + r];
+      T += part[(2 * NSPLIT + k) * n + r];
+    }
+    float M = -INFINITY, S_ = 0.f;
+#pragma unroll
+    for (int k = 0; k < NSPLIT; ++k) online_merge(M, S_, pm[k], ps[k]);
+    const float l = M + logf(S_);
+    lse[r] = l;
+    acc += l - T;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] * (0.5f / (float)B);
+}
+
+// Backward.  G[i,j] = g/2B·(e^(S_ij − lse_i) + e^(S_ij − lse'_j) − 2δ_ij) (masked S = −1e4 gives
+// 0); dû_i = Σ_j G_ij î_j /τ (direction 0), dî_j = Σ_i G_ij û_i /τ (direction 1).  A
+// workgroup owns 16 output rows and one of NSPLIT k ranges; MFMA D[d][row] = Σ_k Vᵀ[d][k]
+// G'[k][row] with V streamed from L2 and G' recomputed per lane; partial rows go to part.
+template <int DC>
+__global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __restrict__ uh,
+                                                      const float* __restrict__ ih,
+                                                      const float* __restrict__ S,
+                                                      const float* __restrict__ lse,
+                                                      const float* __restrict__ dloss,
+                                                      float* __restrict__ part) {
+  constexpr int D = 16 * DC, TPW = DC / 4;
+  static_assert(DC % 4 == 0, "D % 64 == 0");
+  const int nb = (B + NQ - 1) / NQ;
+  const int split = blockIdx.x % NSPLIT;
+  const int qb = blockIdx.x / NSPLIT;
+  const int dir = qb >= nb;
+  const int r0 = (qb - dir * nb) * NQ;
+  const float* V = dir ? uh : ih;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
+  const float coef = (dloss ? dloss[0] : 1.f) * (0.5f / (float)B);
+  const int row = r0 + li;
+  const bool rok = row < B;
+  const float lrow = rok ? lse[(int64_t)dir * B + row] : 0.f;
+  f32x4_t acc[TPW];
+#pragma unroll
+  for (int q = 0; q < TPW; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int nkc = (B + 15) / 16;
+  const int k0 = (int)((int64_t)nkc * split / NSPLIT), k1 = (int)((int64_t)nkc * (split + 1) / NSPLIT);
+  // chunks in groups of KU: every load of a group is issued before any of its MFMAs
+  constexpr int KU = 4;
+  for (int kg = k0; kg < k1; kg += KU) {
+    float g[KU][4], x[KU][TPW][4];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int kb = 16 * (kg + u) + 4 * lg;   // this lane's 4 k values: kb .. kb+3
+      const bool cok = kg + u < k1;
+      // loads are unconditional (clamped addresses) and masked afterwards: a guarded load in
+      // an unrolled group makes hipcc branch and drain vmcnt per element
+      const int rowc = min(row, B - 1);
+      const int kbc = min(kb, B - 4);             // B % 4 == 0
+      if (dir == 0) {
+        const float4 sv = *reinterpret_cast<const float4*>(S + (int64_t)rowc * B + kbc);
+        const float4 l2 = *reinterpret_cast<const float4*>(lse + B + kbc);
+        const float svv[4] = {sv.x, sv.y, sv.z, sv.w}, l2v[4] = {l2.x, l2.y, l2.z, l2.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = coef * (expf(svv[e] - lrow) + expf(svv[e] - l2v[e]) - (kb + e == row ? 2.f : 0.f));
+          g[u][e] = (cok && rok && kb + e < B) ? gv : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = kbc + e;
+          const float sv = S[(int64_t)k * B + rowc];
+          const float gv = coef * (expf(sv - lse[k]) + expf(sv - lrow) - (k == row ? 2.f : 0.f));
+          g[u][e] = (cok && rok && kb + e < B) ? gv : 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) {
+        const int d = (wave + 4 * q) * 16 + li;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xv = V[(int64_t)(kbc + e) * D + d];
+          x[u][q][e] = (cok && kb + e < B) ? xv : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const uint4 gf = make_uint4(__float_as_uint(g[u][0]), __float_as_uint(g[u][1]),
+                                  __float_as_uint(g[u][2]), __float_as_uint(g[u][3]));
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) {
+        const uint4 xf = make_uint4(__float_as_uint(x[u][q][0]), __float_as_uint(x[u][q][1]),
+                                    __float_as_uint(x[u][q][2]), __float_as_uint(x[u][q][3]));
+        Mma<float>::run(acc[q], xf, gf);
+      }
+    }
+  }
+  // lane holds D[d = dtile*16 + 4lg + r][row = r0 + li]
+  if (rok) {
+    float* pr = part + ((int64_t)split * 2 * B + (int64_t)dir * B + row) * D;
+#pragma unroll
+    for (int q = 0; q < TPW; ++q)
+      *reinterpret_cast<float4*>(pr + (wave + 4 * q) * 16 + 4 * lg) =
+          make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+  }
+}
+
+// dx = normalize-backward(Σ_split part / τ); wave per row of the 2B rows.
+__global__ __launch_bounds__(256) void nce_bwd_finish_kernel(int B, int D, const float* __restrict__ uh,
+                                                             const float* __restrict__ ih,
+                                                             const float* __restrict__ norms,
+                                                             const float* __restrict__ part,
+                                                             float inv_tau, float* __restrict__ du,
+                                                             float* __restrict__ di) {
+  const int lane = threadIdx.x & 63;
+  const int row = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (row >= 2 * B) return;
+  const bool isu = row < B;
+  const int r = isu ? row : row - B;
+  const float* y = (isu ? uh : ih) + (int64_t)r * D;
+  float* dx = (isu ? du : di) + (int64_t)r * D;
+  const float nrm = norms[row];
+  float dy[4];
+  float sdot = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = lane + 64 * q;
+    float v = 0.f;
+    if (c < D) {
+#pragma unroll
+      for (int k = 0; k < NSPLIT; ++k) v += part[((int64_t)k * 2 * B + row) * D + c];
+      v *= inv_tau;
+      sdot += y[c] * v;
+    }
+    dy[q] = v;
+  }
+  sdot = wave_sum(sdot);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = lane + 64 * q;
+    if (c < D) dx[c] = nrm > NORM_EPS ? (dy[q] - y[c] * sdot) / nrm : dy[q] / NORM_EPS;
+  }
+}
+
 struct Ws {
   float* dS; float* ce; float* duh; float* dih;
 };
@@ -289,10 +547,14 @@ ttmi_gemm_desc f32_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t
 
 }  // namespace
 
+bool fused_ok(int B, int D) { return D % 64 == 0 && D <= 256; }
+
 extern "C" int64_t ttmi_infonce_workspace(int B, int D) {
+  auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+  if (fused_ok(B, D))   // fwd partials (3·NSPLIT·2B) + bwd partial rows (NSPLIT·2B·D)
+    return al((int64_t)3 * NSPLIT * 2 * B * 4) + al((int64_t)NSPLIT * 2 * B * D * 4);
   // dS [B,B] + ce [2B] + dû', dî' [B,D], each 256-B aligned
-  return ((int64_t)B * B * 4 + 255) / 256 * 256 + ((int64_t)2 * B * 4 + 255) / 256 * 256 +
-         2 * (((int64_t)B * D * 4 + 255) / 256 * 256);
+  return al((int64_t)B * B * 4) + al((int64_t)2 * B * 4) + 2 * al((int64_t)B * D * 4);
 }
 
 extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
@@ -303,11 +565,26 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
                "ttmi_infonce_fwd: need B %% 4 == 0, D %% 4 == 0, D <= 4096");
   TTMI_REQUIRE(u && it && u_hat && i_hat && norms && logits && lse && loss && ws,
                "ttmi_infonce_fwd: null argument");
-  Ws w = carve(ws, B, D);
   hipLaunchKernelGGL(l2norm_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u, it, u_hat, i_hat,
                      norms);
   int rc = ttmi_check_launch("ttmi_infonce_fwd/l2norm");
   if (rc) return rc;
+  if (fused_ok(B, D)) {
+    float* part = static_cast<float*>(ws);
+    const int nb = (B + NQ - 1) / NQ;
+    const dim3 grid(2 * nb * NSPLIT);
+    switch (D / 16) {
+      case 4: hipLaunchKernelGGL(nce_fwd_kernel<4>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
+      case 8: hipLaunchKernelGGL(nce_fwd_kernel<8>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
+      case 12: hipLaunchKernelGGL(nce_fwd_kernel<12>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
+      default: hipLaunchKernelGGL(nce_fwd_kernel<16>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
+    }
+    rc = ttmi_check_launch("ttmi_infonce_fwd/rows");
+    if (rc) return rc;
+    hipLaunchKernelGGL(nce_combine_kernel, dim3(1), dim3(1024), 0, s, B, part, lse, loss);
+    return ttmi_check_launch("ttmi_infonce_fwd/combine");
+  }
+  Ws w = carve(ws, B, D);
   ttmi_gemm_desc g = f32_gemm(B, B, D, u_hat, D, 1, i_hat, D, 1, logits, B, inv_tau);
   rc = ttmi_gemm(&g, s);
   if (rc) return rc;
@@ -328,6 +605,23 @@ extern "C" int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i
                "ttmi_infonce_bwd: need B %% 4 == 0, D %% 4 == 0, D <= 4096");
   TTMI_REQUIRE(u_hat && i_hat && norms && logits && lse && du && di && ws,
                "ttmi_infonce_bwd: null argument");
+  if (fused_ok(B, D)) {
+    float* part = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                           ((int64_t)3 * NSPLIT * 2 * B * 4 + 255) / 256 * 256);
+    const int nb = (B + NQ - 1) / NQ;
+    const dim3 grid(2 * nb * NSPLIT);
+    switch (D / 16) {
+      case 4: hipLaunchKernelGGL(nce_bwd_kernel<4>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
+      case 8: hipLaunchKernelGGL(nce_bwd_kernel<8>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
+      case 12: hipLaunchKernelGGL(nce_bwd_kernel<12>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
+      default: hipLaunchKernelGGL(nce_bwd_kernel<16>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
+    }
+    int rc = ttmi_check_launch("ttmi_infonce_bwd/rows");
+    if (rc) return rc;
+    hipLaunchKernelGGL(nce_bwd_finish_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u_hat, i_hat,
+                       norms, part, inv_tau, du, di);
+    return ttmi_check_launch("ttmi_infonce_bwd/finish");
+  }
   Ws w = carve(ws, B, D);
   const int64_t n = (int64_t)B * B;
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 2048);

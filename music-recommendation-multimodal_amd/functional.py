@@ -433,7 +433,9 @@ class LossSaved:
 
 
 def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float = 0.07):
-    """TwoTowerModel.forward loss part (reference two_tower.py:98-140)."""
+    """TwoTowerModel.forward loss part (reference two_tower.py:98-140): fused kernels — one
+    normalise launch, one f32-MFMA logits + masked row/column softmax-statistics launch, one
+    combine launch (ttmi_infonce_fwd)."""
     dev = u.device
     B, D = u.shape
     f32 = dict(device=dev, dtype=torch.float32)
@@ -487,14 +489,15 @@ class GlobalLossSaved:
 
 
 def infonce_global_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float,
-                       group=None):
+                       group=None, local: bool = False):
     """InfoNCE over the concatenation of every rank's batch (BASELINE cfg 5; the reference
     two_tower.py:98-140 applied to world·B rows).  Returns (loss_r, logits_u2i [B, W·B],
     û_r, î_r, saved); the global loss is the mean of loss_r over ranks, which DDP's 1/world
     gradient scaling realises.  All-gathers û, î and user_idx over `group` (RCCL)."""
     import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    distributed = dist.is_initialized() and not local
+    world = dist.get_world_size(group) if distributed else 1
+    rank = dist.get_rank(group) if distributed else 0
     B, D = u.shape
     dev = u.device
     f32 = dict(device=dev, dtype=torch.float32)
@@ -529,11 +532,11 @@ def infonce_global_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temper
 
 
 def infonce_global_bwd(st: GlobalLossSaved, dloss: Optional[Tensor], du: Tensor, di: Tensor,
-                       group=None) -> None:
+                       group=None, local: bool = False) -> None:
     """Backward of infonce_global_fwd for this rank's loss_r: local-row grads, key grads for
     every rank's rows reduce-scattered (SUM) back to their owners, then normalize backward."""
     import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    world = dist.get_world_size(group) if dist.is_initialized() and not local else 1
     B, D = st.u_hat.shape
     f32 = dict(device=st.u_hat.device, dtype=torch.float32)
     scale = 0.5 / B
