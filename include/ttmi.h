@@ -210,6 +210,37 @@ int ttmi_rowce_bwd(int R, int C, int D, const float* q, const float* k, const fl
 int ttmi_sum_scaled(int n, const float* x, float scale, float* out, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * 2-D convolution (ResNet-18 audio/visual encoders, reference item_tower.py:9-39 on
+ * torchvision resnet18): implicit GEMM over NHWC bf16 activations, C and Co multiples of 8
+ * (stems zero-padded with ttmi_nchw_to_nhwc), square stride/pad, no bias.
+ *   mode 0 FWD:   y[n,ho,wo,co] = Σ x[n, ho·s−p+kh, wo·s−p+kw, ci] W[co,ci,kh,kw]   (out bf16),
+ *                 colsum/colsumsq[co] += Σ y, Σ y² (fp32, may both be NULL; BatchNorm stats)
+ *   mode 1 DGRAD: dx[n,h,w,ci] = Σ dy[n,(h+p−kh)/s,(w+p−kw)/s,co] W[co,ci,kh,kw] (+ addend)
+ *                 over the stride lattice (out bf16; needs Cin == C)
+ *   mode 2 WGRAD: dW[co,ci,kh,kw] += Σ dy·x (out fp32, torch layout, ci < Cin)
+ * w is the bf16 mirror from ttmi_conv_weight_prep: Wf = [Co][KH][KW][C] for FWD,
+ * Wd = [Cin][KH][KW][Co] for DGRAD.
+ * ---------------------------------------------------------------------------------- */
+typedef struct ttmi_conv_desc {
+  int mode;
+  int N, H, W, C, Cin, Co, KH, KW, stride, pad;
+  const void* x;          /* bf16 NHWC [N,H,W,C] */
+  const void* dy;         /* bf16 NHWC [N,Ho,Wo,Co] */
+  const void* w;          /* bf16 mirror (FWD: Wf, DGRAD: Wd) */
+  void* out;
+  const void* addend;     /* DGRAD: bf16 [N,H,W,C] added before the store, or NULL */
+  float* colsum; float* colsumsq;
+} ttmi_conv_desc;
+int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream);
+/* wf[co][kh][kw][c] = bf16(w[co][ci][kh][kw]) zero for Cin <= c < Cp; wd[ci][kh][kw][co]
+ * likewise (wd may be NULL). w is torch's fp32 Conv2d.weight. */
+int ttmi_conv_weight_prep(int Co, int Cin, int Cp, int KH, int KW, const float* w, uint16_t* wf,
+                          uint16_t* wd, hipStream_t stream);
+/* y = bf16 NHWC [N,H,W,Cp] of x fp32 NCHW [N,Cin,H,W] (channels >= Cin zero). */
+int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const float* x, uint16_t* y,
+                      hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * Fused AdamW over flat fp32 buffers (torch.optim.AdamW defaults, train.py:302):
  *   t = ++(*step); p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g²;
  *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps).

@@ -41,6 +41,14 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class ConvDesc(ctypes.Structure):
+    """ttmi_conv_desc (include/ttmi.h)."""
+    _fields_ = [("mode", c_i), ("N", c_i), ("H", c_i), ("W", c_i), ("C", c_i), ("Cin", c_i),
+                ("Co", c_i), ("KH", c_i), ("KW", c_i), ("stride", c_i), ("pad", c_i),
+                ("x", c_p), ("dy", c_p), ("w", c_p), ("out", c_p), ("addend", c_p),
+                ("colsum", c_p), ("colsumsq", c_p)]
+
+
 class LnBwdDesc(ctypes.Structure):
     """ttmi_linear_ln_bwd_desc (include/ttmi.h)."""
     _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
@@ -85,6 +93,9 @@ SIGNATURES = {
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
+    "ttmi_conv2d": (c_i, [c_p, c_p]),
+    "ttmi_conv_weight_prep": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_nchw_to_nhwc": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
     "ttmi_l2norm_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_l2norm_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_rowce_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_p, c_p, c_p]),

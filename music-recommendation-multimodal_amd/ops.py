@@ -12,7 +12,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import lib as _L
-from .lib import BF16, F32, GemmDesc, LnBwdDesc, call
+from .lib import BF16, F32, ConvDesc, GemmDesc, LnBwdDesc, call
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -175,6 +175,42 @@ def rowce_bwd(q: Tensor, k: Tensor, logits: Tensor, lse: Tensor, uid_q: Optional
 def sum_scaled(x: Tensor, scale: float, out: Tensor) -> Tensor:
     call("ttmi_sum_scaled", x.numel(), _p(x), scale, _p(out), _s())
     return out
+
+
+# ----------------------------------------------------------------------------- convolution
+FWD, DGRAD, WGRAD = 0, 1, 2
+
+
+def conv_out_hw(H: int, W: int, k: int, stride: int, pad: int):
+    return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+
+
+def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int, stride: int,
+           pad: int, *, x: Optional[Tensor] = None, dy: Optional[Tensor] = None,
+           w: Optional[Tensor] = None, out: Tensor, addend: Optional[Tensor] = None,
+           colsum: Optional[Tensor] = None, colsumsq: Optional[Tensor] = None) -> Tensor:
+    """Implicit-GEMM conv (include/ttmi.h ttmi_conv2d): FWD y = conv(x), DGRAD dx, WGRAD dW."""
+    d = ConvDesc()
+    d.mode, d.N, d.H, d.W, d.C, d.Cin, d.Co = mode, N, H, W, C, Cin, Co
+    d.KH = d.KW = k
+    d.stride, d.pad = stride, pad
+    d.x, d.dy, d.w, d.out, d.addend = _p(x), _p(dy), _p(w), _p(out), _p(addend)
+    d.colsum, d.colsumsq = _p(colsum), _p(colsumsq)
+    call("ttmi_conv2d", ctypes.byref(d), _s())
+    return out
+
+
+def conv_weight_prep(w: Tensor, Cp: int, wf: Tensor, wd: Optional[Tensor] = None) -> None:
+    """bf16 GEMM mirrors of a torch Conv2d weight [Co, Cin, k, k]: wf [Co, k, k, Cp],
+    wd [Cin, k, k, Co]."""
+    Co, Cin, KH, KW = w.shape
+    call("ttmi_conv_weight_prep", Co, Cin, Cp, KH, KW, _p(w), _p(wf), _p(wd), _s())
+
+
+def nchw_to_nhwc(x: Tensor, Cp: int, y: Tensor) -> Tensor:
+    N, Cin, H, W = x.shape
+    call("ttmi_nchw_to_nhwc", N, Cin, H, W, Cp, _p(x), _p(y), _s())
+    return y
 
 
 # ----------------------------------------------------------------------------- norms

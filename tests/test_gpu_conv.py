@@ -1,0 +1,87 @@
+"""ResNet-18 building blocks (cfg 3) vs fp32 PyTorch on the same bf16-rounded operands.
+
+Convolutions: FWD output and BatchNorm column statistics, DGRAD (input grad, with the
+residual-branch addend) and WGRAD (weight grad in torch layout) against F.conv2d and its
+autograd, over the torchvision resnet18 conv shapes (7x7/2 stem with 1 and 3 channels padded
+to 8, 3x3/1, 3x3/2, 1x1/2 downsample).  bf16 outputs are compared at bf16 rounding (8e-3),
+fp32 reductions at 2e-5 relative (x sqrt(K/256) for long reductions)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+SHAPES = [  # N, Cin, H, W, Co, k, stride, pad
+    (2, 1, 30, 40, 64, 7, 2, 3),
+    (2, 3, 33, 29, 64, 7, 2, 3),
+    (2, 64, 14, 14, 64, 3, 1, 1),
+    (3, 64, 15, 13, 128, 3, 2, 1),
+    (3, 64, 15, 13, 128, 1, 2, 0),
+    (2, 128, 7, 9, 256, 3, 2, 1),
+    (2, 256, 5, 4, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Co,k,s,p", SHAPES)
+def test_conv_fwd_dgrad_wgrad(gpu_pkg, N, Cin, H, W, Co, k, s, p):
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(N * 1000 + Cin + Co + k)
+    Cp = (Cin + 7) // 8 * 8
+    x = torch.randn(N, Cin, H, W, generator=g).to(torch.bfloat16).float()
+    w = (torch.randn(Co, Cin, k, k, generator=g) / math.sqrt(Cin * k * k)).to(torch.bfloat16).float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y_ref = TF.conv2d(xr, wr, stride=s, padding=p)
+    Ho, Wo = ops.conv_out_hw(H, W, k, s, p)
+    assert y_ref.shape[2:] == (Ho, Wo)
+    dy = torch.randn(y_ref.shape, generator=g).to(torch.bfloat16).float()
+    y_ref.backward(dy)
+    # device operands
+    xd = torch.empty(N, H, W, Cp, device=DEV, dtype=torch.bfloat16)
+    ops.nchw_to_nhwc(x.to(DEV), Cp, xd)
+    assert torch.equal(xd[..., :Cin].float().cpu(), nhwc(x))
+    wf = torch.empty(Co, k, k, Cp, device=DEV, dtype=torch.bfloat16)
+    wd = torch.empty(Cin, k, k, Co, device=DEV, dtype=torch.bfloat16)
+    ops.conv_weight_prep(w.to(DEV), Cp, wf, wd)
+    y = torch.empty(N, Ho, Wo, Co, device=DEV, dtype=torch.bfloat16)
+    cs = torch.zeros(Co, device=DEV)
+    cq = torch.zeros(Co, device=DEV)
+    ops.conv2d(ops.FWD, N, H, W, Cp, Cin, Co, k, s, p, x=xd, w=wf, out=y, colsum=cs, colsumsq=cq)
+    torch.cuda.synchronize()
+    yr = y_ref.detach()
+    assert rel(nchw(y.float()), yr) < 8e-3
+    Kred = Cin * k * k
+    tol = 2e-5 * max(1.0, math.sqrt(Kred / 256))
+    assert rel(cs, yr.sum((0, 2, 3))) < 5e-3            # stats of the fp32 (pre-round) output
+    assert rel(cq, (yr ** 2).sum((0, 2, 3))) < 5e-3
+    dyd = nhwc(dy).to(torch.bfloat16).to(DEV)
+    dw = torch.full((Co, Cin, k, k), 0.25, device=DEV)
+    ops.conv2d(ops.WGRAD, N, H, W, Cp, Cin, Co, k, s, p, x=xd, dy=dyd, out=dw)
+    torch.cuda.synchronize()
+    Mred = N * Ho * Wo
+    assert rel(dw, 0.25 + wr.grad) < 2e-5 * max(1.0, math.sqrt(Mred / 256)) * 4
+    if Cp == Cin:
+        add = torch.randn(N, H, W, Cin, generator=g).to(torch.bfloat16)
+        dx = torch.empty(N, H, W, Cin, device=DEV, dtype=torch.bfloat16)
+        ops.conv2d(ops.DGRAD, N, H, W, Cin, Cin, Co, k, s, p, dy=dyd, w=wd, out=dx,
+                   addend=add.to(DEV))
+        torch.cuda.synchronize()
+        assert rel(nchw(dx.float()), xr.grad + nchw(add.float())) < 8e-3
