@@ -240,6 +240,33 @@ int ttmi_conv_weight_prep(int Co, int Cin, int Cp, int KH, int KW, const float* 
 int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const float* x, uint16_t* y,
                       hipStream_t stream);
 
+/* BatchNorm2d, train mode, over NHWC bf16 [M = N·H·W, C] (C % 8 == 0, C <= 512), batch
+ * statistics from the producing conv's colsum/colsumsq:  y = act(w·x̂ + b + residual)
+ * (act = ReLU if relu; residual bf16 or NULL); running stats updated with momentum and the
+ * unbiased variance, *num_batches_tracked += 1 (all three may be NULL: eval-free path);
+ * save_mean/save_rstd [C] for the backward (nn.BatchNorm2d + torchvision BasicBlock tail). */
+int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* colsum, const float* colsumsq,
+                  const float* w, const float* b, float eps, float momentum, float* running_mean,
+                  float* running_var, int64_t* num_batches_tracked, const uint16_t* residual,
+                  int relu, uint16_t* y, float* save_mean, float* save_rstd, hipStream_t stream);
+/* Backward: g = dy ⊙ (gate > 0) (gate = the ReLU output, or NULL); dx = w·rstd·(g − Σg/M −
+ * x̂·Σgx̂/M); dw += Σgx̂, db += Σg.  sums [2C] fp32 must be zero on entry (scratch);
+ * g_out (bf16, may be NULL) receives g for the residual branch. */
+int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate, const uint16_t* x,
+                  const float* mean, const float* rstd, const float* w, float* sums,
+                  uint16_t* g_out, uint16_t* dx, float* dw, float* db, hipStream_t stream);
+/* Max-pool k x k / stride, -inf padding (resnet18 maxpool 3/2/1), NHWC bf16; idx (uint8 per
+ * output element) = the window tap of the max, first on ties.  Backward gathers. */
+int ttmi_maxpool_fwd(int N, int H, int W, int C, int k, int stride, int pad, const uint16_t* x,
+                     uint16_t* y, uint8_t* idx, hipStream_t stream);
+int ttmi_maxpool_bwd(int N, int H, int W, int C, int k, int stride, int pad, const uint16_t* dy,
+                     const uint8_t* idx, uint16_t* dx, hipStream_t stream);
+/* Global average pool (AdaptiveAvgPool2d(1) + flatten): y[n,c] = mean_p x[n,p,c] (bf16);
+ * backward dx[n,p,c] = dy[n,c]/HW ⊙ (gate > 0 if gate != NULL). */
+int ttmi_avgpool_fwd(int N, int HW, int C, const uint16_t* x, uint16_t* y, hipStream_t stream);
+int ttmi_avgpool_bwd(int N, int HW, int C, const void* dy, int dy_dtype, const uint16_t* gate,
+                     uint16_t* dx, hipStream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * Fused AdamW over flat fp32 buffers (torch.optim.AdamW defaults, train.py:302):
  *   t = ++(*step); p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g²;

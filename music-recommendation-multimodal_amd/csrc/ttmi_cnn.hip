@@ -1,0 +1,383 @@
+// ttmi_cnn.hip — ResNet-18 non-GEMM layers over NHWC bf16 activations (torchvision
+// resnet18 as used by reference item_tower.py:9-39): BatchNorm2d in train mode (batch
+// statistics, running-stat update), residual add + ReLU, max-pool 3x3/2 and the global
+// average pool, with their backwards.
+//
+// BatchNorm2d forward takes the per-channel Σx and Σx² that the producing convolution
+// accumulated in its epilogue (ttmi_conv2d FWD), so it is one element-wise pass:
+//   y = act(w·(x − μ)·rstd + b + residual),  μ = Σx/M, var = Σx²/M − μ² (biased),
+//   running stats with momentum and the unbiased variance (nn.BatchNorm2d).
+// Its backward is a reduction pass (Σg, Σg·x̂ per channel, g = dy ⊙ ReLU gate, optionally
+// writing g for the residual branch) and an element-wise pass
+//   dx = w·rstd·(g − Σg/M − x̂·Σg x̂/M).
+// Element-wise passes move 8 channels (16 bytes) per thread.
+#include "ttmi_common.h"
+
+namespace {
+
+constexpr int MAXC = 512;
+
+TTMI_DEV void unpack8(const uint4& q, float* v) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+TTMI_DEV uint4 pack8(const float* v) {
+  uint4 q;
+  q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  return q;
+}
+
+int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096)); }
+
+// ---------------------------------------------------------------- BatchNorm2d forward
+__global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const bf16_t* __restrict__ x,
+                                                       const float* __restrict__ csum,
+                                                       const float* __restrict__ csq,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ b, float eps,
+                                                       float momentum, float* running_mean,
+                                                       float* running_var, int64_t* nbt,
+                                                       const bf16_t* __restrict__ res, int relu,
+                                                       bf16_t* __restrict__ y, float* save_mean,
+                                                       float* save_rstd) {
+  __shared__ float sa[MAXC], sb[MAXC];      // y = x·sa + sb
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float mu = csum[c] * invM;
+    const float var = fmaxf(csq[c] * invM - mu * mu, 0.f);
+    const float rs = 1.f / sqrtf(var + eps);
+    sa[c] = w[c] * rs;
+    sb[c] = b[c] - mu * w[c] * rs;
+    if (blockIdx.x == 0) {
+      save_mean[c] = mu;
+      save_rstd[c] = rs;
+      if (running_mean) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  __syncthreads();
+  const int cpr = C / 8;
+  const int64_t n = M * cpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpr) * 8;
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (res) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = v[e] * sa[c0 + e] + sb[c0 + e] + r[e];
+      if (relu) v[e] = fmaxf(v[e], 0.f);
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(v);
+  }
+}
+
+// ---------------------------------------------------------------- BatchNorm2d backward
+// Reduction: sums[c] += Σ g, sums[C + c] += Σ g·x̂ (g = dy ⊙ (gate > 0) when gate given);
+// g is written (bf16) when gout != NULL.  Block = 256 threads over row slabs; per thread 8
+// channels of strided rows, then an LDS reduction and one atomic per channel per block.
+__global__ __launch_bounds__(256) void bn2d_bwd_reduce_kernel(int64_t M, int C, const bf16_t* __restrict__ dy,
+                                                              const bf16_t* __restrict__ gate,
+                                                              const bf16_t* __restrict__ x,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd,
+                                                              bf16_t* __restrict__ gout,
+                                                              float* __restrict__ sums,
+                                                              int64_t rows_per_block) {
+  __shared__ float red[2][256][8];
+  const int cpr = C / 8;
+  const int tpr = 256 / cpr > 0 ? 256 / cpr : 1;     // row lanes per block (C <= 2048)
+  const int t = threadIdx.x;
+  const int cg = t % cpr, rl = t / cpr;
+  const int c0 = cg * 8;
+  float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mu[e] = cg < cpr ? mean[c0 + e] : 0.f; rs[e] = cg < cpr ? rstd[c0 + e] : 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (rl < tpr && cg < cpr) {
+    for (int64_t m = r0 + rl; m < r1; m += tpr) {
+      const int64_t i = m * cpr + cg;
+      float g[8], xv[8];
+      unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
+      if (gate) {
+        float gv[8];
+        unpack8(reinterpret_cast<const uint4*>(gate)[i], gv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = gv[e] > 0.f ? g[e] : 0.f;
+      }
+      if (gout) reinterpret_cast<uint4*>(gout)[i] = pack8(g);
+      unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += g[e];
+        s2[e] += g[e] * (xv[e] - mu[e]) * rs[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][t][e] = s1[e]; red[1][t][e] = s2[e]; }
+  __syncthreads();
+  if (t < cpr) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < tpr; ++r) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += red[0][r * cpr + t][e]; bb[e] += red[1][r * cpr + t][e]; }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(sums + t * 8 + e, a[e]);
+      atomicAdd(sums + C + t * 8 + e, bb[e]);
+    }
+  }
+}
+
+// dx = w·rstd·(g − Σg/M − x̂·Σgx̂/M) (+ addend); block 0 also adds the sums into dw/db.
+__global__ __launch_bounds__(256) void bn2d_bwd_apply_kernel(int64_t M, int C, const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ gate,
+                                                             const bf16_t* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ sums,
+                                                             bf16_t* __restrict__ dx,
+                                                             float* dw, float* db) {
+  __shared__ float sk[MAXC], sm1[MAXC], sm2[MAXC], smu[MAXC], srs[MAXC];
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    sk[c] = w[c] * rstd[c];
+    sm1[c] = sums[c] * invM;
+    sm2[c] = sums[C + c] * invM;
+    smu[c] = mean[c];
+    srs[c] = rstd[c];
+    if (blockIdx.x == 0) {
+      if (db) db[c] += sums[c];
+      if (dw) dw[c] += sums[C + c];
+    }
+  }
+  __syncthreads();
+  const int cpr = C / 8;
+  const int64_t n = M * cpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpr) * 8;
+    float g[8], xv[8], o[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
+    if (gate) {
+      float gv[8];
+      unpack8(reinterpret_cast<const uint4*>(gate)[i], gv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = gv[e] > 0.f ? g[e] : 0.f;
+    }
+    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const float xh = (xv[e] - smu[c]) * srs[c];
+      o[e] = sk[c] * (g[e] - sm1[c] - xh * sm2[c]);
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(o);
+  }
+}
+
+// ---------------------------------------------------------------- pools
+// max-pool k x k / s, padding p (-inf), NHWC; idx = window tap of the max (first on ties).
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, int k,
+                                                          int s, int p, const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ y, uint8_t* __restrict__ idx) {
+  const int cpr = C / 8;
+  const int64_t n = (int64_t)N * Ho * Wo * cpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % cpr);
+    int64_t t = i / cpr;
+    const int wo = (int)(t % Wo); t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int b = (int)(t / Ho);
+    float best[8];
+    uint8_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+    for (int kh = 0; kh < k; ++kh) {
+      const int h = ho * s - p + kh;
+      if (h < 0 || h >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int w = wo * s - p + kw;
+        if (w < 0 || w >= W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + (((int64_t)b * H + h) * W + w) * C + cg * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; arg[e] = (uint8_t)(kh * k + kw); }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+    a.y = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+    reinterpret_cast<uint2*>(idx)[i] = a;
+  }
+}
+
+// dx[h, w] = Σ over the windows that chose (h, w) of dy (gather form: deterministic).
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, int k,
+                                                          int s, int p, const bf16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ idx,
+                                                          bf16_t* __restrict__ dx) {
+  const int cpr = C / 8;
+  const int64_t n = (int64_t)N * H * W * cpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % cpr);
+    int64_t t = i / cpr;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int b = (int)(t / H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // windows (ho, wo) with ho*s - p <= h <= ho*s - p + k - 1
+    const int ho_lo = max(0, (h + p - k + s) / s), ho_hi = min(Ho - 1, (h + p) / s);
+    const int wo_lo = max(0, (w + p - k + s) / s), wo_hi = min(Wo - 1, (w + p) / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int kh = h - (ho * s - p);
+      if (kh < 0 || kh >= k) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int kw = w - (wo * s - p);
+        if (kw < 0 || kw >= k) continue;
+        const int64_t o = ((((int64_t)b * Ho + ho) * Wo + wo) * cpr + cg);
+        const uint2 a = reinterpret_cast<const uint2*>(idx)[o];
+        float g[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], g);
+        const uint8_t tap = (uint8_t)(kh * k + kw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t ae = (uint8_t)(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xFF);
+          if (ae == tap) acc[e] += g[e];
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
+  }
+}
+
+// y[n, c] = mean over H·W of x[n, :, :, c] (fp32 accumulate; out bf16).  Block per (n, 64-ch).
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(int N, int HW, int C, const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ y) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.x / ((C + 63) / 64), c = (blockIdx.x % ((C + 63) / 64)) * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < C)
+    for (int p = rl; p < HW; p += 4) s += bf2f(x[((int64_t)b * HW + p) * C + c]);
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    y[(int64_t)b * C + c] = f2bf(t / (float)HW);
+  }
+}
+
+// dx[n, p, c] = dy[n, c] / HW (dy fp32 or bf16), optionally gated by (gate > 0): the ReLU at
+// the end of the last block.
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(int N, int HW, int C, const void* __restrict__ dy,
+                                                          int dy_f32, const bf16_t* __restrict__ gate,
+                                                          bf16_t* __restrict__ dx) {
+  const int64_t n = (int64_t)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int b = (int)(i / ((int64_t)HW * C));
+    float g = ld_dyn(dy, (int64_t)b * C + c, dy_f32) * inv;
+    if (gate && bf2f(gate[i]) <= 0.f) g = 0.f;
+    dx[i] = f2bf(g);
+  }
+}
+
+}  // namespace
+
+extern "C" int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* colsum,
+                             const float* colsumsq, const float* w, const float* b, float eps,
+                             float momentum, float* running_mean, float* running_var,
+                             int64_t* num_batches_tracked, const uint16_t* residual, int relu,
+                             uint16_t* y, float* save_mean, float* save_rstd, hipStream_t s) {
+  TTMI_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= MAXC, "ttmi_bn2d_fwd: need 0 < C <= %d, C %% 8 == 0", MAXC);
+  TTMI_REQUIRE(x && colsum && colsumsq && w && b && y && save_mean && save_rstd, "ttmi_bn2d_fwd: null argument");
+  TTMI_REQUIRE(!running_mean == !running_var, "ttmi_bn2d_fwd: running_mean/var go together");
+  hipLaunchKernelGGL(bn2d_fwd_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, s, M, C, (const bf16_t*)x,
+                     colsum, colsumsq, w, b, eps, momentum, running_mean, running_var,
+                     num_batches_tracked, (const bf16_t*)residual, relu, (bf16_t*)y, save_mean, save_rstd);
+  return ttmi_check_launch("ttmi_bn2d_fwd");
+}
+
+extern "C" int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate,
+                             const uint16_t* x, const float* mean, const float* rstd,
+                             const float* w, float* sums, uint16_t* g_out, uint16_t* dx,
+                             float* dw, float* db, hipStream_t s) {
+  TTMI_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= MAXC, "ttmi_bn2d_bwd: need 0 < C <= %d, C %% 8 == 0", MAXC);
+  TTMI_REQUIRE(dy && x && mean && rstd && w && sums && dx, "ttmi_bn2d_bwd: null argument");
+  const int cpr = C / 8;
+  const int tpr = std::max(1, 256 / cpr);
+  int64_t blocks = std::min<int64_t>(1024, (M + tpr * 8 - 1) / (tpr * 8));
+  blocks = std::max<int64_t>(blocks, 1);
+  const int64_t rpb = (M + blocks - 1) / blocks;
+  hipLaunchKernelGGL(bn2d_bwd_reduce_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0, s, M, C,
+                     (const bf16_t*)dy, (const bf16_t*)gate, (const bf16_t*)x, mean, rstd, (bf16_t*)g_out,
+                     sums, rpb);
+  int rc = ttmi_check_launch("ttmi_bn2d_bwd/reduce");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn2d_bwd_apply_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, s, M, C,
+                     (const bf16_t*)dy, (const bf16_t*)gate, (const bf16_t*)x, mean, rstd, w, sums,
+                     (bf16_t*)dx, dw, db);
+  return ttmi_check_launch("ttmi_bn2d_bwd/apply");
+}
+
+extern "C" int ttmi_maxpool_fwd(int N, int H, int W, int C, int k, int stride, int pad,
+                                const uint16_t* x, uint16_t* y, uint8_t* idx, hipStream_t s) {
+  TTMI_REQUIRE(N >= 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0 && k > 0 && k * k <= 255 && stride > 0 &&
+                   pad >= 0 && pad < k, "ttmi_maxpool_fwd: bad shape");
+  TTMI_REQUIRE(x && y && idx, "ttmi_maxpool_fwd: null argument");
+  const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  if (N == 0) return TTMI_OK;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((int64_t)N * Ho * Wo * C / 8)), dim3(256), 0, s, N, H,
+                     W, C, Ho, Wo, k, stride, pad, (const bf16_t*)x, (bf16_t*)y, idx);
+  return ttmi_check_launch("ttmi_maxpool_fwd");
+}
+
+extern "C" int ttmi_maxpool_bwd(int N, int H, int W, int C, int k, int stride, int pad,
+                                const uint16_t* dy, const uint8_t* idx, uint16_t* dx, hipStream_t s) {
+  TTMI_REQUIRE(N >= 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0 && k > 0 && stride > 0 && pad >= 0,
+               "ttmi_maxpool_bwd: bad shape");
+  TTMI_REQUIRE(dy && idx && dx, "ttmi_maxpool_bwd: null argument");
+  const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  if (N == 0) return TTMI_OK;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((int64_t)N * H * W * C / 8)), dim3(256), 0, s, N, H, W,
+                     C, Ho, Wo, k, stride, pad, (const bf16_t*)dy, idx, (bf16_t*)dx);
+  return ttmi_check_launch("ttmi_maxpool_bwd");
+}
+
+extern "C" int ttmi_avgpool_fwd(int N, int HW, int C, const uint16_t* x, uint16_t* y, hipStream_t s) {
+  TTMI_REQUIRE(N >= 0 && HW > 0 && C > 0, "ttmi_avgpool_fwd: bad shape");
+  TTMI_REQUIRE(x && y, "ttmi_avgpool_fwd: null argument");
+  if (N == 0) return TTMI_OK;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(N * ((C + 63) / 64)), dim3(256), 0, s, N, HW, C, (const bf16_t*)x,
+                     (bf16_t*)y);
+  return ttmi_check_launch("ttmi_avgpool_fwd");
+}
+
+extern "C" int ttmi_avgpool_bwd(int N, int HW, int C, const void* dy, int dy_dtype, const uint16_t* gate,
+                                uint16_t* dx, hipStream_t s) {
+  TTMI_REQUIRE(N >= 0 && HW > 0 && C > 0, "ttmi_avgpool_bwd: bad shape");
+  TTMI_REQUIRE(dy && dx, "ttmi_avgpool_bwd: null argument");
+  if (N == 0) return TTMI_OK;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((int64_t)N * HW * C)), dim3(256), 0, s, N, HW, C, dy,
+                     dy_dtype == TTMI_F32, (const bf16_t*)gate, (bf16_t*)dx);
+  return ttmi_check_launch("ttmi_avgpool_bwd");
+}

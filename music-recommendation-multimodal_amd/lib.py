@@ -96,6 +96,13 @@ SIGNATURES = {
     "ttmi_conv2d": (c_i, [c_p, c_p]),
     "ttmi_conv_weight_prep": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_nchw_to_nhwc": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
+    "ttmi_bn2d_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_i,
+                            c_p, c_p, c_p, c_p]),
+    "ttmi_bn2d_bwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_maxpool_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_maxpool_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_avgpool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p]),
+    "ttmi_avgpool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_i, c_p, c_p, c_p]),
     "ttmi_l2norm_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_l2norm_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_rowce_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_p, c_p, c_p]),

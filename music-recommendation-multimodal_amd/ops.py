@@ -213,6 +213,53 @@ def nchw_to_nhwc(x: Tensor, Cp: int, y: Tensor) -> Tensor:
     return y
 
 
+def bn2d_fwd(x: Tensor, colsum: Tensor, colsumsq: Tensor, w: Tensor, b: Tensor, y: Tensor,
+             save_mean: Tensor, save_rstd: Tensor, *, running_mean: Optional[Tensor] = None,
+             running_var: Optional[Tensor] = None, num_batches: Optional[Tensor] = None,
+             residual: Optional[Tensor] = None, relu: bool = False, eps: float = 1e-5,
+             momentum: float = 0.1) -> Tensor:
+    C = x.shape[-1]
+    M = x.numel() // C
+    call("ttmi_bn2d_fwd", M, C, _p(x), _p(colsum), _p(colsumsq), _p(w), _p(b), eps, momentum,
+         _p(running_mean), _p(running_var), _p(num_batches), _p(residual), int(relu), _p(y),
+         _p(save_mean), _p(save_rstd), _s())
+    return y
+
+
+def bn2d_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, sums: Tensor,
+             dx: Tensor, dw: Optional[Tensor], db: Optional[Tensor], *,
+             gate: Optional[Tensor] = None, g_out: Optional[Tensor] = None) -> Tensor:
+    C = x.shape[-1]
+    M = x.numel() // C
+    call("ttmi_bn2d_bwd", M, C, _p(dy), _p(gate), _p(x), _p(mean), _p(rstd), _p(w), _p(sums),
+         _p(g_out), _p(dx), _p(dw), _p(db), _s())
+    return dx
+
+
+def maxpool_fwd(x: Tensor, k: int, stride: int, pad: int, y: Tensor, idx: Tensor) -> Tensor:
+    N, H, W, C = x.shape
+    call("ttmi_maxpool_fwd", N, H, W, C, k, stride, pad, _p(x), _p(y), _p(idx), _s())
+    return y
+
+
+def maxpool_bwd(dy: Tensor, idx: Tensor, k: int, stride: int, pad: int, dx: Tensor) -> Tensor:
+    N, H, W, C = dx.shape
+    call("ttmi_maxpool_bwd", N, H, W, C, k, stride, pad, _p(dy), _p(idx), _p(dx), _s())
+    return dx
+
+
+def avgpool_fwd(x: Tensor, y: Tensor) -> Tensor:
+    N, H, W, C = x.shape
+    call("ttmi_avgpool_fwd", N, H * W, C, _p(x), _p(y), _s())
+    return y
+
+
+def avgpool_bwd(dy: Tensor, dx: Tensor, gate: Optional[Tensor] = None) -> Tensor:
+    N, H, W, C = dx.shape
+    call("ttmi_avgpool_bwd", N, H * W, C, _p(dy), code(dy.dtype), _p(gate), _p(dx), _s())
+    return dx
+
+
 # ----------------------------------------------------------------------------- norms
 def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor, *,
                   eps: float = 1e-5, relu: bool = False, drop: Drop = NO_DROP) -> Tensor:

@@ -85,3 +85,79 @@ def test_conv_fwd_dgrad_wgrad(gpu_pkg, N, Cin, H, W, Co, k, s, p):
                    addend=add.to(DEV))
         torch.cuda.synchronize()
         assert rel(nchw(dx.float()), xr.grad + nchw(add.float())) < 8e-3
+
+
+@pytest.mark.parametrize("C,relu,res", [(64, True, False), (128, True, True), (512, False, False)])
+def test_bn2d_fwd_bwd(gpu_pkg, C, relu, res):
+    """BatchNorm2d (train) with stats from the conv epilogue's column sums, residual + ReLU,
+    running stats; backward through the ReLU gate with g written for the residual branch."""
+    ops = gpu_pkg.ops
+    N, H, W = 3, 9, 7
+    g = torch.Generator().manual_seed(C)
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 0.3).to(torch.bfloat16).float()
+    w = torch.randn(C, generator=g)
+    b = torch.randn(C, generator=g)
+    r = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).float()
+    rm, rv = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+    xt, wt, bt = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rm_ref, rv_ref = rm.clone(), rv.clone()
+    y_ref = TF.batch_norm(xt, rm_ref, rv_ref, wt, bt, training=True, momentum=0.1, eps=1e-5)
+    if res:
+        y_ref = y_ref + r
+    if relu:
+        y_ref = torch.relu(y_ref)
+    dy = torch.randn(y_ref.shape, generator=g).to(torch.bfloat16).float()
+    y_ref.backward(dy)
+    xd = nhwc(x).to(torch.bfloat16).to(DEV)
+    cs = nhwc(x).sum((0, 1, 2)).to(DEV)
+    cq = (nhwc(x) ** 2).sum((0, 1, 2)).to(DEV)
+    y = torch.empty_like(xd)
+    mean, rstd = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    rmd, rvd, nb = rm.to(DEV), rv.to(DEV), torch.zeros(1, device=DEV, dtype=torch.int64)
+    ops.bn2d_fwd(xd, cs, cq, w.to(DEV), b.to(DEV), y, mean, rstd, running_mean=rmd, running_var=rvd,
+                 num_batches=nb, residual=nhwc(r).to(torch.bfloat16).to(DEV) if res else None, relu=relu)
+    torch.cuda.synchronize()
+    assert rel(nchw(y.float()), y_ref.detach()) < 8e-3
+    assert rel(rmd, rm_ref) < 1e-5 and rel(rvd, rv_ref) < 1e-4 and int(nb) == 1
+    sums = torch.zeros(2 * C, device=DEV)
+    dx = torch.empty_like(xd)
+    dw, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    gout = torch.empty_like(xd)
+    ops.bn2d_bwd(nhwc(dy).to(torch.bfloat16).to(DEV), xd, mean, rstd, w.to(DEV), sums, dx, dw, db,
+                 gate=y if relu else None, g_out=gout)
+    torch.cuda.synchronize()
+    assert rel(nchw(dx.float()), xt.grad) < 1e-2
+    assert rel(dw, wt.grad) < 1e-3 and rel(db, bt.grad) < 1e-3
+    gexp = dy * (y_ref.detach() > 0).float() if relu else dy
+    assert rel(nchw(gout.float()), gexp) < 8e-3
+
+
+def test_pools(gpu_pkg):
+    ops = gpu_pkg.ops
+    N, C, H, W = 2, 64, 17, 12
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).float()
+    xt = x.clone().requires_grad_(True)
+    y_ref = TF.max_pool2d(xt, 3, 2, 1)
+    dy = torch.randn(y_ref.shape, generator=g).to(torch.bfloat16).float()
+    y_ref.backward(dy)
+    xd = nhwc(x).to(torch.bfloat16).to(DEV)
+    Ho, Wo = y_ref.shape[2:]
+    y = torch.empty(N, Ho, Wo, C, device=DEV, dtype=torch.bfloat16)
+    idx = torch.empty(N, Ho, Wo, C, device=DEV, dtype=torch.uint8)
+    ops.maxpool_fwd(xd, 3, 2, 1, y, idx)
+    dx = torch.empty_like(xd)
+    ops.maxpool_bwd(nhwc(dy).to(torch.bfloat16).to(DEV), idx, 3, 2, 1, dx)
+    torch.cuda.synchronize()
+    assert torch.equal(nchw(y.float()).cpu(), y_ref.detach())
+    assert rel(nchw(dx.float()), xt.grad) < 8e-3
+    # global average pool + its backward (gated by a ReLU output)
+    a = torch.empty(N, C, device=DEV, dtype=torch.bfloat16)
+    ops.avgpool_fwd(xd, a)
+    gy = torch.randn(N, C, generator=g)
+    da = torch.empty_like(xd)
+    ops.avgpool_bwd(gy.to(DEV), da, gate=xd)
+    torch.cuda.synchronize()
+    assert rel(a.float(), x.mean((2, 3))) < 8e-3
+    exp = (gy[:, :, None, None] / (H * W)).expand(N, C, H, W) * (x > 0).float()
+    assert rel(nchw(da.float()), exp) < 8e-3
