@@ -8,12 +8,13 @@ directory name is not a Python identifier).  Kernels live in ``lib/libttmi.so`` 
 from . import lib
 from . import ops
 from . import functional
+from . import cnn
 from .user_tower import SequentialUserEncoder
 from .item_tower import MultimodalItemEncoder
 from .two_tower import TwoTowerModel, infonce, infonce_global
 from .train import (FlatParams, GradSync, TrainStep, cleanup_ddp, setup_ddp,
                     train_one_epoch)
 
-__all__ = ["lib", "ops", "functional", "SequentialUserEncoder", "MultimodalItemEncoder",
+__all__ = ["lib", "ops", "functional", "cnn", "SequentialUserEncoder", "MultimodalItemEncoder",
            "TwoTowerModel", "infonce", "infonce_global", "TrainStep", "FlatParams", "GradSync", "setup_ddp",
            "cleanup_ddp", "train_one_epoch"]

@@ -1,0 +1,416 @@
+"""cfg-3 item encoders on libttmi kernels: ResNet-18 audio/visual backbones and the tabular
+MLP (reference src/models/item_tower.py:9-39, :85-98).
+
+ResNet-18 follows torchvision's resnet18 exactly (BasicBlock [2, 2, 2, 2], conv1 7x7/2 →
+BN → ReLU → maxpool 3/2/1, 1x1/2 conv + BN downsample at the first block of layers 2-4,
+global average pool, fc), with the reference's replacements (audio conv1 takes 1 channel;
+fc → Linear(512, embedding_dim)) and torchvision's parameter names, so checkpoints map
+one-to-one.  BatchNorm2d runs in train mode on batch statistics, as in the reference.
+
+Data layout: NHWC bf16 activations (the 1/3-channel input is zero-padded to 8 channels by
+ttmi_nchw_to_nhwc); conv weights are used through bf16 mirrors (ttmi_conv_weight_prep);
+every conv's forward epilogue accumulates the BatchNorm column sums, so a conv + BN + ReLU
+(+ residual) is two launches.  All parameters and grads stay fp32 (torch layouts).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import functional as F
+from . import ops
+
+Tensor = torch.Tensor
+
+LAYERS = (("layer1", 64, 64, 1), ("layer2", 64, 128, 2), ("layer3", 128, 256, 2),
+          ("layer4", 256, 512, 2))
+STEM_CP = 8          # the 1- or 3-channel stem input is padded to 8 channels
+
+
+@dataclass(frozen=True)
+class ConvSpec:
+    name: str          # parameter name of the weight ("conv1.weight", "layer2.0.downsample.0.weight")
+    bn: str            # its BatchNorm prefix ("bn1", "layer2.0.downsample.1")
+    cin: int
+    cout: int
+    k: int
+    stride: int
+    pad: int
+
+
+def resnet18_convs(in_ch: int) -> List[ConvSpec]:
+    specs = [ConvSpec("conv1.weight", "bn1", in_ch, 64, 7, 2, 3)]
+    for lname, cin, cout, s in LAYERS:
+        for bi in range(2):
+            ci = cin if bi == 0 else cout
+            st = s if bi == 0 else 1
+            b = f"{lname}.{bi}."
+            specs.append(ConvSpec(b + "conv1.weight", b + "bn1", ci, cout, 3, st, 1))
+            specs.append(ConvSpec(b + "conv2.weight", b + "bn2", cout, cout, 3, 1, 1))
+            if bi == 0 and (st != 1 or ci != cout):
+                specs.append(ConvSpec(b + "downsample.0.weight", b + "downsample.1", ci, cout, 1,
+                                      st, 0))
+    return specs
+
+
+# ---------------------------------------------------------------------------- state
+@dataclass
+class ConvAct:
+    x: Tensor              # conv input (bf16 NHWC)
+    H: int
+    W: int
+    y: Tensor              # conv output, pre-BN (bf16 NHWC)
+    mean: Tensor
+    rstd: Tensor
+    a: Tensor              # BN output (after residual/ReLU when fused)
+
+
+@dataclass
+class ResNetSaved:
+    N: int
+    acts: Dict[str, ConvAct] = field(default_factory=dict)
+    pool_idx: Optional[Tensor] = None
+    stem_out: Optional[Tensor] = None      # BN1+ReLU output (maxpool input)
+    feat: Optional[Tensor] = None          # pooled features bf16 [N, 512]
+    last: Optional[Tensor] = None          # last block output (avgpool input)
+    mirrors: Optional[Dict[str, Tuple[Tensor, Optional[Tensor]]]] = None
+    fc_w: Optional[Tensor] = None
+
+
+def weight_mirrors(P: Dict[str, Tensor], specs: List[ConvSpec]):
+    """bf16 GEMM mirrors (Wf for FWD, Wd for DGRAD) of every conv weight."""
+    out = {}
+    for sp in specs:
+        w = P[sp.name]
+        dev = w.device
+        cp = STEM_CP if sp.cin < 8 else sp.cin
+        wf = torch.empty(sp.cout, sp.k, sp.k, cp, device=dev, dtype=torch.bfloat16)
+        wd = None
+        if sp.cin >= 8:
+            wd = torch.empty(sp.cin, sp.k, sp.k, sp.cout, device=dev, dtype=torch.bfloat16)
+        ops.conv_weight_prep(w.contiguous(), cp, wf, wd)
+        out[sp.name] = (wf, wd)
+    return out
+
+
+def _conv_bn(P, bufs, sp: ConvSpec, x: Tensor, N: int, H: int, W: int, mirrors, stats: Tensor,
+             off: int, residual: Optional[Tensor], relu: bool, training: bool) -> ConvAct:
+    dev = x.device
+    C = x.shape[-1]
+    Ho, Wo = ops.conv_out_hw(H, W, sp.k, sp.stride, sp.pad)
+    y = torch.empty(N, Ho, Wo, sp.cout, device=dev, dtype=torch.bfloat16)
+    cs, cq = stats[off:off + sp.cout], stats[off + sp.cout:off + 2 * sp.cout]
+    ops.conv2d(ops.FWD, N, H, W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad, x=x,
+               w=mirrors[sp.name][0], out=y, colsum=cs, colsumsq=cq)
+    a = torch.empty_like(y)
+    mean = torch.empty(sp.cout, device=dev)
+    rstd = torch.empty(sp.cout, device=dev)
+    ops.bn2d_fwd(y, cs, cq, P[sp.bn + ".weight"], P[sp.bn + ".bias"], a, mean, rstd,
+                 running_mean=bufs.get(sp.bn + ".running_mean") if training else None,
+                 running_var=bufs.get(sp.bn + ".running_var") if training else None,
+                 num_batches=bufs.get(sp.bn + ".num_batches_tracked") if training else None,
+                 residual=residual, relu=relu)
+    return ConvAct(x, H, W, y, mean, rstd, a)
+
+
+def resnet18_fwd(P: Dict[str, Tensor], x: Tensor, in_ch: int, bufs: Dict[str, Tensor],
+                 training: bool = True, fc_dtype: torch.dtype = torch.bfloat16):
+    """torchvision resnet18.forward (train-mode BN) on x [N, in_ch, H, W] fp32 → [N, out] fp32."""
+    dev = x.device
+    N, _, H, W = x.shape
+    specs = resnet18_convs(in_ch)
+    mirrors = weight_mirrors(P, specs)
+    stats = torch.zeros(2 * sum(sp.cout for sp in specs), device=dev)
+    st = ResNetSaved(N, mirrors=mirrors)
+    x0 = torch.empty(N, H, W, STEM_CP, device=dev, dtype=torch.bfloat16)
+    ops.nchw_to_nhwc(x.contiguous().float(), STEM_CP, x0)
+    off = 0
+    sp = specs[0]
+    a = _conv_bn(P, bufs, sp, x0, N, H, W, mirrors, stats, off, None, True, training)
+    off += 2 * sp.cout
+    st.acts[sp.name] = a
+    st.stem_out = a.a
+    Hc, Wc = a.y.shape[1], a.y.shape[2]
+    Hp, Wp = ops.conv_out_hw(Hc, Wc, 3, 2, 1)
+    y = torch.empty(N, Hp, Wp, 64, device=dev, dtype=torch.bfloat16)
+    st.pool_idx = torch.empty(N, Hp, Wp, 64, device=dev, dtype=torch.uint8)
+    ops.maxpool_fwd(a.a, 3, 2, 1, y, st.pool_idx)
+    H, W = Hp, Wp
+    byname = {s.name: s for s in specs}
+    for lname, _, _, _ in LAYERS:
+        for bi in range(2):
+            b = f"{lname}.{bi}."
+            c1, c2 = byname[b + "conv1.weight"], byname[b + "conv2.weight"]
+            ds = byname.get(b + "downsample.0.weight")
+            idn = y
+            if ds is not None:
+                ad = _conv_bn(P, bufs, ds, y, N, H, W, mirrors, stats, off, None, False, training)
+                off += 2 * ds.cout
+                st.acts[ds.name] = ad
+                idn = ad.a
+            a1 = _conv_bn(P, bufs, c1, y, N, H, W, mirrors, stats, off, None, True, training)
+            off += 2 * c1.cout
+            st.acts[c1.name] = a1
+            H1, W1 = a1.y.shape[1], a1.y.shape[2]
+            a2 = _conv_bn(P, bufs, c2, a1.a, N, H1, W1, mirrors, stats, off, idn, True, training)
+            off += 2 * c2.cout
+            st.acts[c2.name] = a2
+            y, H, W = a2.a, H1, W1
+    st.last = y
+    feat = torch.empty(N, 512, device=dev, dtype=torch.bfloat16)
+    ops.avgpool_fwd(y, feat)
+    st.feat = feat
+    fc_w = P["fc.weight"]
+    st.fc_w = ops.cast_bf16(fc_w.contiguous(), torch.empty(fc_w.shape, device=dev, dtype=fc_dtype))
+    out = torch.empty(N, fc_w.shape[0], device=dev)
+    ops.linear(feat, st.fc_w, P["fc.bias"], out)
+    return out, st
+
+
+def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dict[str, Tensor],
+                 in_ch: int) -> None:
+    """Backward of resnet18_fwd: accumulates every parameter grad (torch layouts)."""
+    dev = dout.device
+    N = st.N
+    specs = resnet18_convs(in_ch)
+    byname = {s.name: s for s in specs}
+    sums = torch.zeros(2 * sum(sp.cout for sp in specs), device=dev)
+    soff = [0]
+
+    def bn_bwd(sp: ConvSpec, act: ConvAct, dy: Tensor, gate: Optional[Tensor],
+               g_out: Optional[Tensor] = None) -> Tensor:
+        s = sums[soff[0]:soff[0] + 2 * sp.cout]
+        soff[0] += 2 * sp.cout
+        dyc = torch.empty_like(act.y)
+        ops.bn2d_bwd(dy, act.y, act.mean, act.rstd, P[sp.bn + ".weight"], s, dyc,
+                     grads[sp.bn + ".weight"], grads[sp.bn + ".bias"], gate=gate, g_out=g_out)
+        return dyc
+
+    def conv_bwd(sp: ConvSpec, act: ConvAct, dyc: Tensor, need_dx: bool,
+                 addend: Optional[Tensor] = None) -> Optional[Tensor]:
+        C = act.x.shape[-1]
+        ops.conv2d(ops.WGRAD, N, act.H, act.W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad,
+                   x=act.x, dy=dyc, out=grads[sp.name])
+        if not need_dx:
+            return None
+        dx = torch.empty_like(act.x)
+        ops.conv2d(ops.DGRAD, N, act.H, act.W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad,
+                   dy=dyc, w=st.mirrors[sp.name][1], out=dx, addend=addend)
+        return dx
+
+    # fc + global average pool
+    dc = torch.empty(dout.shape, device=dev, dtype=st.feat.dtype)
+    ops.dropout_bwd(dout.contiguous().float(), dc, None)        # cast to the operand dtype
+    ops.linear_dw(dc, st.feat, grads["fc.weight"], grads["fc.bias"])
+    dfeat = torch.empty(N, 512, device=dev)
+    ops.linear_dx(dc, st.fc_w, dfeat)
+    dy = torch.empty_like(st.last)
+    ops.avgpool_bwd(dfeat, dy)
+    # residual stages, reversed
+    for lname, _, _, _ in reversed(LAYERS):
+        for bi in (1, 0):
+            b = f"{lname}.{bi}."
+            c1, c2 = byname[b + "conv1.weight"], byname[b + "conv2.weight"]
+            ds = byname.get(b + "downsample.0.weight")
+            a1, a2 = st.acts[c1.name], st.acts[c2.name]
+            g = torch.empty_like(a2.a)                # dy ⊙ ReLU gate: the identity branch's grad
+            d2 = bn_bwd(c2, a2, dy, a2.a, g_out=g)
+            dmid = conv_bwd(c2, a2, d2, True)
+            d1 = bn_bwd(c1, a1, dmid, a1.a)
+            if ds is not None:
+                ad = st.acts[ds.name]
+                dd = bn_bwd(ds, ad, g, None)
+                idn_dx = conv_bwd(ds, ad, dd, True)
+            else:
+                idn_dx = g
+            dy = conv_bwd(c1, a1, d1, True, addend=idn_dx)
+    # max-pool and stem (no input grad: the encoder input is data)
+    stem = specs[0]
+    act = st.acts[stem.name]
+    dpool = torch.empty_like(st.stem_out)
+    ops.maxpool_bwd(dy, st.pool_idx, 3, 2, 1, dpool)
+    d0 = bn_bwd(stem, act, dpool, st.stem_out)
+    conv_bwd(stem, act, d0, False)
+
+
+# ---------------------------------------------------------------------------- tabular
+@dataclass
+class TabSaved:
+    x: Tensor
+    z: Tensor
+    mean: Tensor
+    rstd: Tensor
+    y1: Tensor
+    w0: Tensor
+    w4: Tensor
+    p_drop: float
+
+
+def tabular_fwd(P: Dict[str, Tensor], x: Tensor, bufs: Dict[str, Tensor], seeds: Optional[Tensor],
+                p_drop: float, site: int, training: bool = True, dtype=torch.bfloat16):
+    """TabularEncoder (item_tower.py:85-98): Linear → BN1d → ReLU → Dropout → Linear."""
+    dev = x.device
+    B = x.shape[0]
+    xc = ops.cast_bf16(x.contiguous().float(), torch.empty(x.shape, device=dev, dtype=dtype))
+    w0 = ops.cast_bf16(P["mlp.0.weight"].contiguous(),
+                       torch.empty(P["mlp.0.weight"].shape, device=dev, dtype=dtype))
+    w4 = ops.cast_bf16(P["mlp.4.weight"].contiguous(),
+                       torch.empty(P["mlp.4.weight"].shape, device=dev, dtype=dtype))
+    H1 = w0.shape[0]
+    z = torch.empty(B, H1, device=dev)
+    ops.linear(xc, w0, P["mlp.0.bias"], z)
+    y1 = torch.empty(B, H1, device=dev, dtype=dtype)
+    mean, rstd = torch.empty(H1, device=dev), torch.empty(H1, device=dev)
+    drop = (p_drop, seeds[site:site + 1]) if (p_drop > 0 and seeds is not None) else ops.NO_DROP
+    ops.batchnorm_fwd(z, P["mlp.1.weight"], P["mlp.1.bias"], y1, mean, rstd,
+                      bufs.get("mlp.1.running_mean"), bufs.get("mlp.1.running_var"),
+                      bufs.get("mlp.1.num_batches_tracked"), relu=True, drop=drop,
+                      training=training)
+    out = torch.empty(B, w4.shape[0], device=dev)
+    ops.linear(y1, w4, P["mlp.4.bias"], out)
+    return out, TabSaved(xc, z, mean, rstd, y1, w0, w4, drop[0])
+
+
+def tabular_bwd(P: Dict[str, Tensor], st: TabSaved, dout: Tensor, grads: Dict[str, Tensor]) -> None:
+    dev = dout.device
+    dc = torch.empty(dout.shape, device=dev, dtype=st.y1.dtype)
+    ops.dropout_bwd(dout.contiguous().float(), dc, None)
+    ops.linear_dw(dc, st.y1, grads["mlp.4.weight"], grads["mlp.4.bias"])
+    dy1 = torch.empty(st.z.shape, device=dev)
+    ops.linear_dx(dc, st.w4, dy1)
+    dz = torch.empty_like(dy1)
+    scale = 1.0 / (1.0 - st.p_drop) if st.p_drop > 0 else 1.0
+    ops.batchnorm_bwd(dy1, st.z, P["mlp.1.weight"], st.mean, st.rstd, st.y1, dz,
+                      grads["mlp.1.weight"], grads["mlp.1.bias"], gate_scale=scale, gated=True)
+    dzc = torch.empty(dz.shape, device=dev, dtype=st.y1.dtype)
+    ops.dropout_bwd(dz, dzc, None)
+    ops.linear_dw(dzc, st.x, grads["mlp.0.weight"], grads["mlp.0.bias"])
+
+
+# ---------------------------------------------------------------------------- modules
+class BasicBlock(nn.Module):
+    """Parameter container with torchvision BasicBlock names (conv1, bn1, conv2, bn2,
+    downsample.{0,1}); the computation is resnet18_fwd/bwd."""
+
+    def __init__(self, cin: int, cout: int, stride: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
+                                            nn.BatchNorm2d(cout))
+
+
+class _ResNetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, in_ch, names, bufs, x, *params):
+        P = dict(zip(names, params))
+        out, st = resnet18_fwd(P, x, in_ch, bufs, training=True)
+        ctx.saved = (in_ch, names, P, st)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        in_ch, names, P, st = ctx.saved
+        del ctx.saved
+        grads = {n: torch.zeros_like(P[n]) for n in names}
+        resnet18_bwd(P, st, dout, grads, in_ch)
+        return (None, None, None, None) + tuple(grads[n] for n in names)
+
+
+class ResNet18(nn.Module):
+    """torchvision resnet18 with conv1 → Conv2d(in_ch, 64, 7, 2, 3) and fc → Linear(512, out_dim)
+    (AudioEncoder/VisualEncoder backbones, item_tower.py:15-22, :33-36)."""
+
+    def __init__(self, in_ch: int = 3, out_dim: int = 128):
+        super().__init__()
+        self.in_ch = in_ch
+        self.conv1 = nn.Conv2d(in_ch, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        for lname, cin, cout, s in LAYERS:
+            setattr(self, lname, nn.Sequential(BasicBlock(cin, cout, s), BasicBlock(cout, cout, 1)))
+        self.fc = nn.Linear(512, out_dim)
+        for m in self.modules():             # torchvision resnet init
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x: Tensor) -> Tensor:
+        names, params = zip(*self.named_parameters())
+        bufs = dict(self.named_buffers()) if self.training else {}
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _ResNetFn.apply(self.in_ch, list(names), bufs, x, *params)
+        out, _ = resnet18_fwd(dict(zip(names, [p.detach() for p in params])), x, self.in_ch,
+                              bufs, training=True)
+        return out
+
+
+class AudioEncoder(nn.Module):
+    """item_tower.py:9-25: ResNet-18 on 1-channel mel spectrograms, fc → embedding_dim."""
+
+    def __init__(self, embedding_dim: int = 128):
+        super().__init__()
+        self.backbone = ResNet18(1, embedding_dim)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.backbone(x)
+
+
+class VisualEncoder(nn.Module):
+    """item_tower.py:27-39: ResNet-18 on 3-channel covers (ImageNet weights are a download and
+    are not available offline: random init), fc → embedding_dim."""
+
+    def __init__(self, embedding_dim: int = 128, pretrained: bool = False):
+        super().__init__()
+        self.backbone = ResNet18(3, embedding_dim)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.backbone(x)
+
+
+class _TabularFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, names, bufs, p_drop, seeds, x, *params):
+        P = dict(zip(names, params))
+        out, st = tabular_fwd(P, x, bufs, seeds, p_drop, 0)
+        ctx.saved = (names, P, st)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        names, P, st = ctx.saved
+        del ctx.saved
+        grads = {n: torch.zeros_like(P[n]) for n in names}
+        tabular_bwd(P, st, dout, grads)
+        return (None, None, None, None, None) + tuple(grads[n] for n in names)
+
+
+class TabularEncoder(nn.Module):
+    """item_tower.py:85-98."""
+
+    def __init__(self, input_dim: int, embedding_dim: int = 128):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Linear(input_dim, 256), nn.BatchNorm1d(256), nn.ReLU(),
+                                 nn.Dropout(0.1), nn.Linear(256, embedding_dim))
+
+    def forward(self, x: Tensor, seeds: Optional[Tensor] = None) -> Tensor:
+        names, params = zip(*self.named_parameters())
+        bufs = dict(self.named_buffers()) if self.training else {}
+        p_drop = self.mlp[3].p if self.training else 0.0
+        if p_drop > 0 and seeds is None:
+            seeds = torch.randint(-(2 ** 62), 2 ** 62, (F.N_SITES,), device=x.device,
+                                  dtype=torch.int64)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _TabularFn.apply(list(names), bufs, p_drop, seeds, x, *params)
+        out, _ = tabular_fwd(dict(zip(names, [p.detach() for p in params])), x, bufs, seeds,
+                             p_drop, 0, training=self.training)
+        return out

@@ -1,0 +1,168 @@
+"""cfg-3 item encoders (ResNet-18 audio/visual backbones, tabular MLP) on the GPU vs the CPU
+oracle restatement (oracle/resnet_ref.py) with identical parameters.
+
+bf16 operands through 20 convolutions: the embedding is compared at 5e-2 relative to its
+max-abs (bf16 rounding compounds layer over layer, BatchNorm re-normalises it), every
+parameter gradient by direction (cosine >= 0.98) and norm (within 10 %), BN running stats at
+1e-2.  Parity against the reference itself is unpinned (torchvision is absent)."""
+import pytest
+import torch
+import torch.nn.functional as TF
+
+from oracle import resnet_ref as rref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def check_grad(name, g, gref):
+    g = g.detach().double().cpu().flatten()
+    gref = gref.detach().double().cpu().flatten()
+    nr = gref.norm().item()
+    if nr < 1e-8:
+        assert g.norm().item() < 1e-3, name
+        return
+    cos = torch.dot(g, gref).item() / (g.norm().item() * nr + 1e-30)
+    assert cos > 0.98, (name, cos)
+    assert abs(g.norm().item() / nr - 1) < 0.1, (name, g.norm().item() / nr)
+
+
+class _RB(torch.autograd.Function):
+    """bf16 rounding in forward and of the gradient in backward: the GPU path stores both
+    the activation and its gradient in bf16 at these points."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def rb(x):
+    return _RB.apply(x)
+
+
+def _emu_conv_bn(p, x, wname, bn, stride, pad, residual=None, relu=True):
+    """conv (bf16 operands, fp32 accumulate, bf16 store) -> BN with fp32 batch statistics of
+    the unrounded conv output applied to the stored bf16 values -> residual -> ReLU -> bf16."""
+    w = p[wname]
+    y32 = TF.conv2d(x, w.detach().to(torch.bfloat16).float() + (w - w.detach()), stride=stride, padding=pad)
+    mean = y32.mean((0, 2, 3), keepdim=True)
+    var = y32.var((0, 2, 3), unbiased=False, keepdim=True)
+    y = rb(y32)
+    out = (y - mean) / torch.sqrt(var + 1e-5) * p[bn + ".weight"][None, :, None, None] \
+        + p[bn + ".bias"][None, :, None, None]
+    if residual is not None:
+        out = out + residual
+    if relu:
+        out = torch.relu(out)
+    return rb(out)
+
+
+def resnet18_bf16_emulation(p, x):
+    y = _emu_conv_bn(p, rb(x), "conv1.weight", "bn1", 2, 3)
+    y = rb(TF.max_pool2d(y, 3, 2, 1))
+    for lname, cin, cout, s in rref.LAYERS:
+        for bi in range(2):
+            b = f"{lname}.{bi}."
+            st = s if bi == 0 else 1
+            idn = y
+            if b + "downsample.0.weight" in p:
+                idn = _emu_conv_bn(p, y, b + "downsample.0.weight", b + "downsample.1", st, 0,
+                                   relu=False)
+            h = _emu_conv_bn(p, y, b + "conv1.weight", b + "bn1", st, 1)
+            y = _emu_conv_bn(p, h, b + "conv2.weight", b + "bn2", 1, 1, residual=rb(idn))
+    feat = rb(TF.adaptive_avg_pool2d(y, 1).flatten(1))
+    w = p["fc.weight"]
+    return TF.linear(feat, w.detach().to(torch.bfloat16).float() + (w - w.detach()), p["fc.bias"])
+
+
+def _cos(a, b):
+    a = a.detach().double().cpu().flatten()
+    b = b.detach().double().cpu().flatten()
+    return torch.dot(a, b).item() / (a.norm().item() * b.norm().item() + 1e-30)
+
+
+@pytest.mark.parametrize("in_ch,H,W", [(1, 64, 96), (3, 64, 64)])
+def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W):
+    """GPU ResNet-18 vs the fp32 oracle (oracle/resnet_ref.py), with the bf16-emulating
+    restatement above as the yardstick for how close any bf16-storage implementation can get.
+
+    Measured on CPU: emulation vs fp32 gives gradient cosines of 0.93 at the stem rising to
+    0.98 at layer4 and 1.0 at fc, at 8x64x96 and at 32x128x128 alike — the train-mode BN
+    backward over 20 layers amplifies bf16 storage noise.  So per parameter the GPU gradient
+    must be as close to fp32 as the emulation is (cosine within 0.03 of it) with the norm
+    within 10 %; the output must agree to 5e-2 (fp32) / 2e-2 (emulation)."""
+    cnn = gpu_pkg.cnn
+    torch.manual_seed(in_ch)
+    net = cnn.ResNet18(in_ch, 128).to(DEV)
+    N = 8
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, in_ch, H, W, generator=g)
+    up = torch.randn(N, 128, generator=g)
+    sd0 = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+
+    def leaf():
+        return {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k
+                    else v.clone()) for k, v in sd0.items()}
+
+    Pe, Pr = leaf(), leaf()
+    out_emu = resnet18_bf16_emulation(Pe, x)
+    (out_emu * up).sum().backward()
+    out_ref = rref.resnet18_forward(Pr, x, update_running=True)
+    (out_ref * up).sum().backward()
+    out = net(x.to(DEV))
+    (out * up.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    report = [("out", rel(out, out_emu), rel(out, out_ref))]
+    for name, p in net.named_parameters():
+        ge, gr = Pe[name].grad, Pr[name].grad
+        report.append((name, _cos(p.grad, ge), p.grad.norm().item() / ge.norm().item(),
+                       _cos(p.grad, gr), p.grad.norm().item() / gr.norm().item()))
+    assert rel(out, out_emu) < 2e-2, report[0]
+    assert rel(out, out_ref) < 5e-2, report[0]
+    for name, _, _, cr, nr in report[1:]:
+        ce_ref = _cos(Pe[name].grad, Pr[name].grad)
+        assert cr > ce_ref - 0.03 and abs(nr - 1) < 0.1, (name, cr, ce_ref, nr)
+    sd = net.state_dict()
+    for k in sd:
+        if "running_mean" in k:
+            # mean error relative to the batch std (momentum 0.1 applied to both): channel
+            # means sit near zero next to their spread, so a plain relative norm is ill-posed
+            rv = Pr[k.replace("mean", "var")]
+            scale = 0.1 * ((rv - 0.9) / 0.1).clamp_min(0).sqrt()
+            assert (sd[k].cpu() - Pr[k]).norm() < 2e-2 * scale.norm(), k
+        if "running_var" in k:
+            assert rel(sd[k], Pr[k]) < 1e-2, k
+        if "num_batches_tracked" in k:
+            assert int(sd[k]) == 1, k
+
+
+def test_tabular_encoder_vs_oracle(gpu_pkg):
+    cnn = gpu_pkg.cnn
+    torch.manual_seed(0)
+    enc = cnn.TabularEncoder(128, 128).to(DEV)
+    enc.mlp[3].p = 0.0
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(64, 128, generator=g)
+    up = torch.randn(64, 128, generator=g)
+    Pr = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in enc.named_parameters()}
+    out_ref = rref.tabular_forward(Pr, x)
+    (out_ref * up).sum().backward()
+    out = enc(x.to(DEV))
+    (out * up.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel(out, out_ref) < 3e-2
+    for name, p in enc.named_parameters():
+        if name == "mlp.0.bias":       # exactly zero in math (BatchNorm follows)
+            assert p.grad.abs().max().item() < 3e-2 * max(1.0, Pr[name].grad.abs().max().item())
+            continue
+        check_grad(name, p.grad, Pr[name].grad)
