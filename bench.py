@@ -10,6 +10,9 @@ One step = forward + backward + AdamW over one synthetic batch already resident 
 Multi-GPU: one process per GPU (torchrun), per-GPU batch fixed (weak scaling), gradients
 averaged with RCCL all-reduce; value = pairs of all ranks / max-over-ranks time.
 
+``--config 3`` measures BASELINE configs[2] instead (full item tower on raw 128x256 mels,
+224x224 covers and tabular features, B=256; its roofline is the implicit-GEMM conv).
+
 Extra fields: "roofline" for the dominant kernel (timed live with HIP events on the launch
 stream) and "cpu_baseline" (the fp32 CPU oracle timed on this host, rank 0 at N=1).
 """
@@ -52,6 +55,24 @@ def synthetic_batches(n: int, B: int, seed: int, device):
             "target_modal": torch.randn(B, 512, generator=g).to(device),
         })
     return out
+
+
+MEL, COVER, TAB = (128, 256), (224, 224), 128
+# SURVEY §8 rows a7/a8 (FlopCounterMode on the torchvision topology): fwd+bwd FLOPs per sample
+RESNET_FLOPS_PER_SAMPLE = 6.75e9 + 10.65e9
+
+
+def add_raw_items(batches, seed: int, device):
+    """cfg 3 item inputs (BASELINE configs[2]): N(0,1) mels [B,1,128,256], covers
+    [B,3,224,224] and tabular features [B,128], replacing the precomputed embeddings."""
+    g = torch.Generator().manual_seed(seed + 7)
+    for b in batches:
+        B = b["history_ids"].shape[0]
+        del b["target_modal"]
+        b["target_audio"] = torch.randn(B, 1, *MEL, generator=g).to(device)
+        b["target_image"] = torch.randn(B, 3, *COVER, generator=g).to(device)
+        b["target_tabular"] = torch.randn(B, TAB, generator=g).to(device)
+    return batches
 
 
 def step_flops(B: int, pruned: bool = True) -> float:
@@ -118,6 +139,52 @@ def probe_dominant(step, batch, device, iters: int = 20):
             "mfma_tflops": round(fl / sec / 1e12, 1)}
 
 
+def probe_conv(step, batch, device, iters: int = 3):
+    """cfg 3 roofline of the dominant kernel, the implicit-GEMM conv (conv_gemm_kernel: FWD,
+    DGRAD and WGRAD launches of both ResNet-18s).  As probe_dominant: one eager forward +
+    backward records the step's conv launch mix, which is replayed between HIP events on
+    the launch stream.  Algorithmic FLOPs per launch: 2·N·Ho·Wo·Co·Cin·k² (the same for all
+    three modes; Cin is the real input width, not the padded stem width)."""
+    ops = pkg.ops
+    calls = []
+    orig = ops.conv2d
+
+    def rec(mode, N, H, W, C, Cin, Co, k, stride, pad, **kw):
+        calls.append(((mode, N, H, W, C, Cin, Co, k, stride, pad), dict(kw)))
+        return orig(mode, N, H, W, C, Cin, Co, k, stride, pad, **kw)
+
+    ops.conv2d = rec
+    try:
+        step._fwd_bwd(step._stage(batch))
+    finally:
+        ops.conv2d = orig
+    torch.cuda.synchronize(device)
+    for a, kw in calls:                                # warm
+        orig(*a, **kw)
+    st = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        for a, kw in calls:
+            orig(*a, **kw)
+    e1.record(st)
+    torch.cuda.synchronize(device)
+    n = max(len(calls), 1)
+    sec = e0.elapsed_time(e1) / 1e3 / (iters * n)
+    fl = 0.0
+    for (mode, N, H, W, C, Cin, Co, k, stride, pad), _ in calls:
+        Ho, Wo = ops.conv_out_hw(H, W, k, stride, pad)
+        fl += 2.0 * N * Ho * Wo * Co * Cin * k * k
+    fl /= n
+    tf = fl / sec / 1e12
+    return {"kernel": "conv_gemm_kernel (implicit-GEMM conv FWD/DGRAD/WGRAD, per-step launch "
+                      "mix of both ResNet-18s)",
+            "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "traffic": read_traffic("conv_gemm_kernel"), "avg_us": round(sec * 1e6, 2),
+            "launches_per_step": len(calls), "flops_per_launch": round(fl)}
+
+
 def read_traffic(name: str):
     """Per-launch HBM bytes of `name` from the committed rocprofv3 PMC summary
     (profiles/*traffic*.json, written by tools/traffic.py), or None."""
@@ -156,12 +223,55 @@ def cpu_baseline(B: int, budget_s: float = 20.0):
                       f"fp32 torch-CPU oracle after 1 warm-up, {el:.1f} s"}
 
 
+def cpu_baseline_cfg3(B: int, budget_s: float = 20.0):
+    """fp32 CPU oracle cfg-3 train step (two ResNet-18s + tabular + fusion + user tower)."""
+    from oracle import two_tower_ref as ref
+    from oracle import resnet_ref as rref
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(0)
+    params = ref.init_params(V, generator=g)
+    for k, v in rref.init_resnet18(1, 128, g, "item_tower.audio_encoder.backbone.").items():
+        params[k] = v
+    for k, v in rref.init_resnet18(3, 128, g, "item_tower.visual_encoder.backbone.").items():
+        params[k] = v
+    pt = "item_tower.tabular_encoder.mlp."
+    params.update({pt + "0.weight": torch.randn(256, TAB, generator=g) * 0.05,
+                   pt + "0.bias": torch.zeros(256), pt + "1.weight": torch.ones(256),
+                   pt + "1.bias": torch.zeros(256),
+                   pt + "4.weight": torch.randn(128, 256, generator=g) * 0.05,
+                   pt + "4.bias": torch.zeros(128)})
+    params = {k: v for k, v in params.items() if "running" not in k}
+    batch = ref.synthetic_batch(B, L, V, generator=g)
+    del batch["target_modal"]
+    batch.update(rref.synthetic_items(B, TAB, MEL, COVER, generator=g))
+    state = {}
+    drop = ref.TorchDropout()
+    t0 = time.perf_counter()
+    ref.train_step(params, state, batch, p_drop=0.1, drop=drop)                  # warm-up
+    warm = time.perf_counter() - t0
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ref.train_step(params, state, batch, p_drop=0.1, drop=drop)
+        n += 1
+        el = time.perf_counter() - t0
+        if el + el / n >= budget_s or n >= 30:
+            break
+    return {"value": round(n * B / el, 3), "unit": "user-item pairs/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} cfg-3 steps at B={B} (full 128x256 mels, 224x224 covers; "
+                      f"warm-up {warm:.1f} s) of the fp32 torch-CPU oracle, {el:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU pairs (default: 512 for cfg 2, 256 for cfg 3)")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+                    help="2 = BASELINE cfg 2 (the metric's configuration); 3 = full item "
+                         "tower on raw mels/covers/tabular (BASELINE configs[2])")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -174,18 +284,22 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     device = torch.device("cuda", local)
-    B = args.batch
+    cfg3 = args.config == 3
+    B = args.batch or (256 if cfg3 else 512)
 
     torch.manual_seed(1234 + rank)
     model = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=N_GENDERS,
                               num_countries=N_COUNTRIES, max_seq_len=L, user_embedding_dim=D,
                               item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
-                              compute_dtype=torch.bfloat16).to(device)
+                              compute_dtype=torch.bfloat16,
+                              precomputed_modalities=not cfg3).to(device)
     if world > 1:   # identical replicas, as DDP broadcasts from rank 0
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, 0)
     step = pkg.TrainStep(model, lr=1e-4, use_graph=not args.no_graph, seed=rank + 1)
-    batches = synthetic_batches(4, B, seed=rank, device=device)
+    batches = synthetic_batches(2 if cfg3 else 4, B, seed=rank, device=device)
+    if cfg3:
+        batches = add_raw_items(batches, rank, device)
 
     # warm-up runs the exact timed-loop ops (incl. the loss accumulation: torch loads its
     # kernels lazily, and a first-use load inside the timed region costs ~75 ms)
@@ -211,33 +325,45 @@ def main():
         el = float(t)
     mean_loss = float(loss_sum) / max(args.steps, 1)
 
-    roof = probe_dominant(step, batches[0], device) if rank == 0 else None
+    roof = None
+    if rank == 0:
+        roof = probe_conv(step, batches[0], device) if cfg3 else \
+            probe_dominant(step, batches[0], device)
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu:
-        cpu = cpu_baseline(B, args.cpu_budget)
+        cpu = cpu_baseline_cfg3(8, args.cpu_budget) if cfg3 else cpu_baseline(B, args.cpu_budget)
 
     if rank == 0:
         pairs = world * B * args.steps
         value = pairs / el
         ms = el / max(args.steps, 1) * 1e3
-        step_tf = step_flops(B) * args.steps / el / 1e12 * world
+        flops = step_flops(B) + (RESNET_FLOPS_PER_SAMPLE * B if cfg3 else 0.0)
+        step_tf = flops * args.steps / el / 1e12 * world
+        workload = ("cfg2: SASRec L=50 D=128 H=4 x2 layers + late-fusion head on "
+                    "precomputed 512-d modality embeddings + in-batch InfoNCE; "
+                    "fwd+bwd+AdamW, dropout 0.1")
+        if cfg3:
+            workload = ("cfg3: SASRec L=50 D=128 H=4 x2 layers + item tower on raw inputs "
+                        "(ResNet-18 on 1x128x256 mels, ResNet-18 on 3x224x224 covers, tabular "
+                        "MLP T=128, zero text slot) + late-fusion head + in-batch InfoNCE; "
+                        "fwd+bwd+AdamW, dropout 0.1, BN train mode")
         line = {
             "metric": "user-item pairs/sec (train step) at batch=512 d=128; 1/2/4/8 MI355X scaling",
             "value": round(value, 1), "unit": "user-item pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic (SURVEY §8d distributions), random-init weights",
-            "config": {"workload": "cfg2: SASRec L=50 D=128 H=4 x2 layers + late-fusion head on "
-                                   "precomputed 512-d modality embeddings + in-batch InfoNCE; "
-                                   "fwd+bwd+AdamW, dropout 0.1",
+            "config": {"workload": workload,
                        "global_batch": world * B, "per_gpu_batch": B, "seq_len": L,
                        "vocab": V, "parallelism": f"dp{world}",
                        "graph": not args.no_graph},
             "roofline": roof,
             "step_mfma": {"achieved": round(step_tf, 3), "peak": PEAK_BF16_TFLOPS,
                           "unit": "TFLOP/s", "frac": round(step_tf / PEAK_BF16_TFLOPS, 5),
-                          "flops_per_step_per_gpu": step_flops(B),
-                          "flops": "F_min (pruned last layer, SURVEY 8d)"},
+                          "flops_per_step_per_gpu": flops,
+                          "flops": "F_min (pruned last layer, SURVEY 8d)" +
+                                   (" + ResNet-18 fwd+bwd 17.4 GF/pair (SURVEY a7/a8)"
+                                    if cfg3 else "")},
             "cpu_baseline": cpu,
             "mean_loss": round(mean_loss, 5),
         }

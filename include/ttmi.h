@@ -244,7 +244,9 @@ int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const float* x, uint
  * statistics from the producing conv's colsum/colsumsq:  y = act(w·x̂ + b + residual)
  * (act = ReLU if relu; residual bf16 or NULL); running stats updated with momentum and the
  * unbiased variance, *num_batches_tracked += 1 (all three may be NULL: eval-free path);
- * save_mean/save_rstd [C] for the backward (nn.BatchNorm2d + torchvision BasicBlock tail). */
+ * save_mean/save_rstd [C] for the backward (nn.BatchNorm2d + torchvision BasicBlock tail).
+ * Eval mode (nn.BatchNorm2d.eval()): colsum = colsumsq = NULL normalises with
+ * running_mean/running_var and updates nothing. */
 int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* colsum, const float* colsumsq,
                   const float* w, const float* b, float eps, float momentum, float* running_mean,
                   float* running_var, int64_t* num_batches_tracked, const uint16_t* residual,

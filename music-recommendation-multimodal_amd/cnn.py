@@ -103,15 +103,17 @@ def _conv_bn(P, bufs, sp: ConvSpec, x: Tensor, N: int, H: int, W: int, mirrors, 
     C = x.shape[-1]
     Ho, Wo = ops.conv_out_hw(H, W, sp.k, sp.stride, sp.pad)
     y = torch.empty(N, Ho, Wo, sp.cout, device=dev, dtype=torch.bfloat16)
-    cs, cq = stats[off:off + sp.cout], stats[off + sp.cout:off + 2 * sp.cout]
+    cs = cq = None                       # eval: BN normalises with the running statistics
+    if training:
+        cs, cq = stats[off:off + sp.cout], stats[off + sp.cout:off + 2 * sp.cout]
     ops.conv2d(ops.FWD, N, H, W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad, x=x,
                w=mirrors[sp.name][0], out=y, colsum=cs, colsumsq=cq)
     a = torch.empty_like(y)
     mean = torch.empty(sp.cout, device=dev)
     rstd = torch.empty(sp.cout, device=dev)
     ops.bn2d_fwd(y, cs, cq, P[sp.bn + ".weight"], P[sp.bn + ".bias"], a, mean, rstd,
-                 running_mean=bufs.get(sp.bn + ".running_mean") if training else None,
-                 running_var=bufs.get(sp.bn + ".running_var") if training else None,
+                 running_mean=bufs.get(sp.bn + ".running_mean"),
+                 running_var=bufs.get(sp.bn + ".running_var"),
                  num_batches=bufs.get(sp.bn + ".num_batches_tracked") if training else None,
                  residual=residual, relu=relu)
     return ConvAct(x, H, W, y, mean, rstd, a)
@@ -119,12 +121,14 @@ def _conv_bn(P, bufs, sp: ConvSpec, x: Tensor, N: int, H: int, W: int, mirrors, 
 
 def resnet18_fwd(P: Dict[str, Tensor], x: Tensor, in_ch: int, bufs: Dict[str, Tensor],
                  training: bool = True, fc_dtype: torch.dtype = torch.bfloat16):
-    """torchvision resnet18.forward (train-mode BN) on x [N, in_ch, H, W] fp32 → [N, out] fp32."""
+    """torchvision resnet18.forward on x [N, in_ch, H, W] fp32 → [N, out] fp32.  training:
+    BN on batch statistics (running stats updated when ``bufs`` holds them); otherwise BN on
+    ``bufs``' running statistics."""
     dev = x.device
     N, _, H, W = x.shape
     specs = resnet18_convs(in_ch)
     mirrors = weight_mirrors(P, specs)
-    stats = torch.zeros(2 * sum(sp.cout for sp in specs), device=dev)
+    stats = torch.zeros(2 * sum(sp.cout for sp in specs), device=dev) if training else None
     st = ResNetSaved(N, mirrors=mirrors)
     x0 = torch.empty(N, H, W, STEM_CP, device=dev, dtype=torch.bfloat16)
     ops.nchw_to_nhwc(x.contiguous().float(), STEM_CP, x0)
@@ -251,7 +255,8 @@ class TabSaved:
 
 
 def tabular_fwd(P: Dict[str, Tensor], x: Tensor, bufs: Dict[str, Tensor], seeds: Optional[Tensor],
-                p_drop: float, site: int, training: bool = True, dtype=torch.bfloat16):
+                p_drop: float, site: int = F.SITE_TAB, training: bool = True,
+                dtype=torch.bfloat16):
     """TabularEncoder (item_tower.py:85-98): Linear → BN1d → ReLU → Dropout → Linear."""
     dev = x.device
     B = x.shape[0]
@@ -346,11 +351,11 @@ class ResNet18(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         names, params = zip(*self.named_parameters())
-        bufs = dict(self.named_buffers()) if self.training else {}
-        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        bufs = dict(self.named_buffers())
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
             return _ResNetFn.apply(self.in_ch, list(names), bufs, x, *params)
         out, _ = resnet18_fwd(dict(zip(names, [p.detach() for p in params])), x, self.in_ch,
-                              bufs, training=True)
+                              bufs, training=self.training)
         return out
 
 
@@ -381,7 +386,7 @@ class _TabularFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, names, bufs, p_drop, seeds, x, *params):
         P = dict(zip(names, params))
-        out, st = tabular_fwd(P, x, bufs, seeds, p_drop, 0)
+        out, st = tabular_fwd(P, x, bufs, seeds, p_drop)
         ctx.saved = (names, P, st)
         return out
 
@@ -404,13 +409,13 @@ class TabularEncoder(nn.Module):
 
     def forward(self, x: Tensor, seeds: Optional[Tensor] = None) -> Tensor:
         names, params = zip(*self.named_parameters())
-        bufs = dict(self.named_buffers()) if self.training else {}
+        bufs = dict(self.named_buffers())
         p_drop = self.mlp[3].p if self.training else 0.0
         if p_drop > 0 and seeds is None:
             seeds = torch.randint(-(2 ** 62), 2 ** 62, (F.N_SITES,), device=x.device,
                                   dtype=torch.int64)
-        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
             return _TabularFn.apply(list(names), bufs, p_drop, seeds, x, *params)
         out, _ = tabular_fwd(dict(zip(names, [p.detach() for p in params])), x, bufs, seeds,
-                             p_drop, 0, training=self.training)
+                             p_drop, training=self.training)
         return out

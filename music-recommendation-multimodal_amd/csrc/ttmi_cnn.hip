@@ -49,23 +49,24 @@ __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const b
                                                        float* save_rstd) {
   __shared__ float sa[MAXC], sb[MAXC];      // y = x·sa + sb
   const float invM = 1.f / (float)M;
+  const bool eval = csum == nullptr;        // eval mode: normalise with the running statistics
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float mu = csum[c] * invM;
-    const float var = fmaxf(csq[c] * invM - mu * mu, 0.f);
+    const float mu = eval ? running_mean[c] : csum[c] * invM;
+    const float var = eval ? running_var[c] : fmaxf(csq[c] * invM - mu * mu, 0.f);
     const float rs = 1.f / sqrtf(var + eps);
     sa[c] = w[c] * rs;
     sb[c] = b[c] - mu * w[c] * rs;
     if (blockIdx.x == 0) {
       save_mean[c] = mu;
       save_rstd[c] = rs;
-      if (running_mean) {
+      if (running_mean && !eval) {
         const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
         running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
         running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
       }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt && !eval) *nbt += 1;
   __syncthreads();
   const int cpr = C / 8;
   const int64_t n = M * cpr;
@@ -309,8 +310,10 @@ extern "C" int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* c
                              int64_t* num_batches_tracked, const uint16_t* residual, int relu,
                              uint16_t* y, float* save_mean, float* save_rstd, hipStream_t s) {
   TTMI_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= MAXC, "ttmi_bn2d_fwd: need 0 < C <= %d, C %% 8 == 0", MAXC);
-  TTMI_REQUIRE(x && colsum && colsumsq && w && b && y && save_mean && save_rstd, "ttmi_bn2d_fwd: null argument");
+  TTMI_REQUIRE(x && w && b && y && save_mean && save_rstd, "ttmi_bn2d_fwd: null argument");
   TTMI_REQUIRE(!running_mean == !running_var, "ttmi_bn2d_fwd: running_mean/var go together");
+  TTMI_REQUIRE(!colsum == !colsumsq, "ttmi_bn2d_fwd: colsum/colsumsq go together");
+  TTMI_REQUIRE(colsum || running_mean, "ttmi_bn2d_fwd: eval mode (no colsum) needs running stats");
   hipLaunchKernelGGL(bn2d_fwd_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, s, M, C, (const bf16_t*)x,
                      colsum, colsumsq, w, b, eps, momentum, running_mean, running_var,
                      num_batches_tracked, (const bf16_t*)residual, relu, (bf16_t*)y, save_mean, save_rstd);

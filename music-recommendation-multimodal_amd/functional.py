@@ -23,6 +23,7 @@ Tensor = torch.Tensor
 
 # Dropout site ids (restated by oracle/two_tower_ref.py: SITE_*).
 SITE_EMB = 0
+SITE_TAB = 62       # tabular encoder dropout (item_tower.py:94)
 SITE_ITEM = 63
 
 

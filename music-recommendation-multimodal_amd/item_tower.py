@@ -4,12 +4,18 @@ The late-fusion head (item_tower.py:122-129: Linear(512,512) -> BatchNorm1d -> R
 Dropout(0.1) -> Linear(512,D) -> LayerNorm(D)) runs on libttmi kernels with the reference's
 parameter/buffer names (``fusion_layer.{0,1,4,5}.*``, BatchNorm running stats included).
 
-BASELINE cfg 2 feeds the head *precomputed* 128-d modality embeddings; this module accepts
-them either concatenated (``fuse(modal[B, 512])``, order audio|visual|text|tabular as in
-item_tower.py:147) or through the reference ``forward(images, audio, input_ids,
-attention_mask, tabular)`` signature with each argument already a [B, 128] embedding.
-The raw-input encoders (ResNet-18 on mels/covers, mDeBERTa+LoRA) are the next rows of the
-build plan and are not constructed here yet.
+Two input modes:
+* ``precomputed_modalities=True`` (BASELINE cfg 2): the head takes precomputed 128-d modality
+  embeddings, either concatenated (``fuse(modal[B, 512])``, order audio|visual|text|tabular as
+  in item_tower.py:147) or through ``forward(images, audio, input_ids, attention_mask,
+  tabular)`` with each argument already a [B, 128] embedding.
+* ``precomputed_modalities=False`` (cfg 3): the raw-input encoders are built with the
+  reference's names — ``audio_encoder`` (ResNet-18 on [B,1,H,W] mels, item_tower.py:9-25),
+  ``visual_encoder`` (ResNet-18 on [B,3,224,224] covers, :27-39; random init, ImageNet
+  weights are a download), ``tabular_encoder`` (:85-98) — all on the libttmi conv/BN/pool
+  kernels (cnn.py).  The mDeBERTa-LoRA text encoder (:41-83, cfg 4) is not built: the text
+  slot of the concatenation is a zero 128-d vector, or ``input_ids`` itself when it is a
+  floating-point [B, text_dim] precomputed text embedding.
 """
 from __future__ import annotations
 
@@ -18,6 +24,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
+from . import cnn
 from . import functional as F
 from .user_tower import make_operands, new_dropout_seeds
 
@@ -55,11 +62,12 @@ class MultimodalItemEncoder(nn.Module):
                  precomputed_modalities: bool = True,
                  compute_dtype: torch.dtype = torch.bfloat16):
         super().__init__()
+        self.precomputed_modalities = precomputed_modalities
         if not precomputed_modalities:
-            raise NotImplementedError(
-                "raw-input modality encoders (ResNet-18 audio/visual, mDeBERTa+LoRA text, tabular "
-                "MLP) are not built yet (SURVEY §7 steps 6-7); pass precomputed modality "
-                "embeddings (BASELINE cfg 2)")
+            self.audio_encoder = cnn.AudioEncoder(embedding_dim=audio_dim)
+            self.visual_encoder = cnn.VisualEncoder(embedding_dim=visual_dim)
+            self.tabular_encoder = cnn.TabularEncoder(input_dim=tabular_input_dim,
+                                                      embedding_dim=tabular_dim)
         self.embedding_dim = embedding_dim
         self.modal_dims = (audio_dim, visual_dim, text_dim, tabular_dim)
         self.compute_dtype = compute_dtype
@@ -83,8 +91,8 @@ class MultimodalItemEncoder(nn.Module):
         p_drop = self.fusion_layer[3].p if self.training else 0.0
         if p_drop > 0 and seeds is None:
             seeds = new_dropout_seeds(modal.device)
-        names, params = zip(*self.named_parameters())
-        bufs = dict(self.named_buffers())
+        names, params = zip(*self.fusion_layer.named_parameters(prefix="fusion_layer"))
+        bufs = dict(self.fusion_layer.named_buffers(prefix="fusion_layer"))
         modal = modal.contiguous().float()
         if not self.training:
             P = dict(zip(names, [p.detach() for p in params]))
@@ -98,7 +106,26 @@ class MultimodalItemEncoder(nn.Module):
         out, _ = F.item_fusion_fwd(P, W, modal, cfg, seeds, bufs, p_drop)
         return out
 
-    def forward(self, images: Tensor, audio: Tensor, input_ids: Tensor,
-                attention_mask: Optional[Tensor], tabular: Tensor) -> Tensor:
-        """Reference signature (item_tower.py:131-152) with precomputed [B, 128] embeddings."""
-        return self.fuse(torch.cat([audio, images, input_ids, tabular], dim=1))
+    def text_slot(self, input_ids: Optional[Tensor], B: int, device) -> Tensor:
+        """cfg 3 text slot: a precomputed float [B, text_dim] embedding, else zeros."""
+        td = self.modal_dims[2]
+        if input_ids is not None and input_ids.is_floating_point() \
+                and tuple(input_ids.shape) == (B, td):
+            return input_ids.float()
+        return torch.zeros(B, td, device=device)
+
+    def forward(self, images: Tensor, audio: Tensor, input_ids: Optional[Tensor],
+                attention_mask: Optional[Tensor], tabular: Tensor,
+                seeds: Optional[Tensor] = None) -> Tensor:
+        """Reference signature (item_tower.py:131-152).  Precomputed mode: every argument is a
+        [B, 128] embedding.  Raw mode: audio [B,1,H,W], images [B,3,H,W], tabular [B,T]."""
+        if self.precomputed_modalities:
+            return self.fuse(torch.cat([audio, images, input_ids, tabular], dim=1), seeds)
+        if self.training and seeds is None:
+            seeds = new_dropout_seeds(audio.device)
+        audio_emb = self.audio_encoder(audio)
+        visual_emb = self.visual_encoder(images)
+        text_emb = self.text_slot(input_ids, audio.shape[0], audio.device)
+        tabular_emb = self.tabular_encoder(tabular, seeds)
+        combined = torch.cat([audio_emb, visual_emb, text_emb, tabular_emb], dim=1)
+        return self.fuse(combined, seeds)

@@ -213,7 +213,7 @@ def nchw_to_nhwc(x: Tensor, Cp: int, y: Tensor) -> Tensor:
     return y
 
 
-def bn2d_fwd(x: Tensor, colsum: Tensor, colsumsq: Tensor, w: Tensor, b: Tensor, y: Tensor,
+def bn2d_fwd(x: Tensor, colsum: Optional[Tensor], colsumsq: Optional[Tensor], w: Tensor, b: Tensor, y: Tensor,
              save_mean: Tensor, save_rstd: Tensor, *, running_mean: Optional[Tensor] = None,
              running_var: Optional[Tensor] = None, num_batches: Optional[Tensor] = None,
              residual: Optional[Tensor] = None, relu: bool = False, eps: float = 1e-5,

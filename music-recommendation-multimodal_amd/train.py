@@ -22,6 +22,7 @@ from typing import Dict, Optional
 import torch
 import torch.distributed as dist
 
+from . import cnn
 from . import functional as F
 from . import ops
 from .two_tower import TwoTowerModel
@@ -140,13 +141,15 @@ class GradSync:
 
 # ------------------------------------------------------------------ the fused step
 class TrainStep:
-    """Fused, graph-captured training step for ``TwoTowerModel`` (cfg-2 item inputs).
+    """Fused, graph-captured training step for ``TwoTowerModel`` (cfg-2 precomputed item
+    inputs, or cfg-3 raw mels / covers / tabular with ``precomputed_modalities=False``).
 
     ``step(batch)`` stages the batch into static device buffers, replays the captured
     forward+backward(+update) graph and returns the device loss tensor (no host sync)."""
 
     INPUT_KEYS = ("history_ids", "history_mask", "user_gender", "user_country", "user_idx",
-                  "target_modal")
+                  "target_modal", "target_audio", "target_image", "target_tabular")
+    RAW_ENCODERS = (("audio_encoder.backbone.", 1), ("visual_encoder.backbone.", 3))
 
     def __init__(self, model: TwoTowerModel, lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.01, use_graph: bool = True,
@@ -183,6 +186,18 @@ class TrainStep:
             self.Wu, self.Wi = self.Pu, self.Pi
         self.bufs = {k[len("item_tower."):]: v for k, v in model.named_buffers()
                      if k.startswith("item_tower.")}
+        self.raw_items = not model.item_tower.precomputed_modalities     # cfg 3
+        if self.raw_items:
+            it = model.item_tower
+            self.p_tab = it.tabular_encoder.mlp[3].p
+            self.text_dim = it.modal_dims[2]
+
+            def sub(d, pre):
+                return {k[len(pre):]: v for k, v in d.items() if k.startswith(pre)}
+            self.enc = [(sub(self.Pi, pre), sub(self.Gi, pre), sub(self.bufs, pre), c)
+                        for pre, c in self.RAW_ENCODERS]
+            pre = "tabular_encoder."
+            self.tab = (sub(self.Pi, pre), sub(self.Gi, pre), sub(self.bufs, pre))
         self.sync_mirror()
         self.use_graph = use_graph
         self.static: Optional[Dict[str, Tensor]] = None
@@ -204,21 +219,53 @@ class TrainStep:
         if self.flat.mirror is not None:      # Wᵀ mirrors of the just-updated bf16 weights
             refresh_transposes(self.Wu, _gemm_names(list(self.Pu)))
         seeds = None
-        if self.ucfg.p_drop > 0 or self.p_item > 0:
+        if self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0):
             ops.dropout_seeds(self.base_seed, self.step_t, self.seeds)
             seeds = self.seeds
         u, ust = F.user_tower_fwd(self.Pu, self.Wu, b["history_ids"], b["user_gender"],
                                   b["user_country"], b.get("history_mask"), self.ucfg, seeds)
-        it, ist = F.item_fusion_fwd(self.Pi, self.Wi, b["target_modal"], self.icfg, seeds,
+        if self.raw_items:
+            modal, rst = self._raw_items_fwd(b, seeds)
+        else:
+            modal = b["target_modal"]
+        it, ist = F.item_fusion_fwd(self.Pi, self.Wi, modal, self.icfg, seeds,
                                     self.bufs, self.p_item)
         loss, logits, _, _, lst = F.infonce_fwd(u, it, b.get("user_idx"),
                                                 self.model.temperature)
         du = torch.empty_like(u)
         di = torch.empty_like(it)
         F.infonce_bwd(lst, self.dloss, du, di)
-        F.item_fusion_bwd(self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item)
+        dmodal = torch.empty(modal.shape, device=modal.device) if self.raw_items else None
+        F.item_fusion_bwd(self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item, dmodal)
+        if self.raw_items:
+            self._raw_items_bwd(rst, dmodal)
         F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg)
         self.loss, self.logits = loss, logits
+
+    def _raw_items_fwd(self, b: Dict[str, Tensor], seeds: Optional[Tensor]):
+        """cfg 3 item encoders (item_tower.py:131-147): audio/visual ResNet-18, zero text slot,
+        tabular MLP, concatenated in the reference's order."""
+        outs, saved = [], []
+        for (P, _, bufs, c), key in zip(self.enc, ("target_audio", "target_image")):
+            o, st = cnn.resnet18_fwd(P, b[key], c, bufs)
+            outs.append(o)
+            saved.append(st)
+        B = outs[0].shape[0]
+        P, _, bufs = self.tab
+        t, tst = cnn.tabular_fwd(P, b["target_tabular"], bufs, seeds, self.p_tab)
+        text = torch.zeros(B, self.text_dim, device=t.device)
+        return torch.cat([outs[0], outs[1], text, t], dim=1), (saved, tst)
+
+    def _raw_items_bwd(self, rst, dmodal: Tensor) -> None:
+        saved, tst = rst
+        o = 0
+        for (P, G, _, c), st in zip(self.enc, saved):
+            n = G["fc.bias"].numel()
+            cnn.resnet18_bwd(P, st, dmodal[:, o:o + n], G, c)
+            o += n
+        o += self.text_dim
+        P, G, _ = self.tab
+        cnn.tabular_bwd(P, tst, dmodal[:, o:], G)
 
     def _update(self) -> None:
         f = self.flat

@@ -5,9 +5,11 @@ reference: symmetric in-batch InfoNCE over L2-normalised embeddings with τ = 0.
 same-user collision mask (-1e4) when ``batch['user_idx']`` is present.  The loss, logits
 and normalisation run in fp32 on libttmi kernels (``ttmi_infonce_fwd/bwd``).
 
-Item inputs (BASELINE cfg 2): ``batch['target_modal']`` [B, 512] precomputed modality
-embeddings (audio|visual|text|tabular), or the reference's item keys each carrying a
-precomputed [B, 128] embedding.
+Item inputs: cfg 2 — ``batch['target_modal']`` [B, 512] precomputed modality embeddings
+(audio|visual|text|tabular), or the reference's item keys each carrying a precomputed [B, 128]
+embedding; cfg 3 (``precomputed_modalities=False``) — the reference's raw item keys
+``target_audio`` [B,1,128,256], ``target_image`` [B,3,224,224], ``target_tabular`` [B,T]
+(two_tower.py:90-96).
 """
 from __future__ import annotations
 
@@ -114,6 +116,11 @@ class TwoTowerModel(nn.Module):
     def _item(self, batch: Dict[str, Tensor], seeds: Optional[Tensor] = None) -> Tensor:
         if "target_modal" in batch:
             return self.item_tower.fuse(batch["target_modal"], seeds)
+        if not self.item_tower.precomputed_modalities:        # cfg 3: raw mels/covers/tabular
+            return self.item_tower(images=batch["target_image"], audio=batch["target_audio"],
+                                   input_ids=batch.get("target_input_ids"),
+                                   attention_mask=batch.get("target_attention_mask"),
+                                   tabular=batch["target_tabular"], seeds=seeds)
         modal = torch.cat([batch["target_audio"], batch["target_image"],
                            batch["target_input_ids"], batch["target_tabular"]], dim=1)
         return self.item_tower.fuse(modal, seeds)

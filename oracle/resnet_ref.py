@@ -5,6 +5,7 @@ CPU fp32 restatement of the cfg-3 item encoders of reference src/models/item_tow
   conv1 replaced by Conv2d(in_ch, 64, 7, 2, 3, bias=False) for audio, fc replaced by
   Linear(512, embedding_dim).  BatchNorm2d runs in train mode on batch statistics.
 * TabularEncoder (:85-98): Linear(T, 256) → BatchNorm1d → ReLU → Dropout → Linear(256, 128).
+* MultimodalItemEncoder.forward (:131-152) for cfg 3 (zero text slot).
 
 torchvision (pinned 0.24.1 in the reference's uv.lock) is not installed here, so the
 ResNet-18 topology is restated from its published definition (BasicBlock [2, 2, 2, 2];
@@ -22,6 +23,8 @@ from typing import Dict, Optional
 
 import torch
 import torch.nn.functional as F
+
+from oracle import two_tower_ref as ttr
 
 Tensor = torch.Tensor
 
@@ -103,12 +106,39 @@ def resnet18_forward(p: Dict[str, Tensor], x: Tensor, prefix: str = "",
 
 
 def tabular_forward(p: Dict[str, Tensor], x: Tensor, prefix: str = "mlp.", p_drop: float = 0.0,
-                    drop=None) -> Tensor:
-    """TabularEncoder (item_tower.py:85-98) in train mode."""
+                    drop=None, update_running: bool = False) -> Tensor:
+    """TabularEncoder (item_tower.py:85-98) in train mode; dropout at site SITE_TAB."""
     z = F.linear(x, p[prefix + "0.weight"], p[prefix + "0.bias"])
-    z = F.batch_norm(z, None, None, p[prefix + "1.weight"], p[prefix + "1.bias"], training=True,
-                     momentum=0.1, eps=1e-5)
+    z = _bn(z, p, prefix + "1", update_running)
     z = F.relu(z)
     if p_drop > 0 and drop is not None:
-        z = drop(0, z, p_drop)
+        z = drop(ttr.SITE_TAB, z, p_drop)
     return F.linear(z, p[prefix + "4.weight"], p[prefix + "4.bias"])
+
+
+def item_tower_raw_forward(p: Dict[str, Tensor], batch: Dict[str, Tensor], p_drop: float = 0.0,
+                           drop=None, running: Optional[Dict[str, Tensor]] = None,
+                           text_dim: int = 128, update_running: bool = False) -> Tensor:
+    """MultimodalItemEncoder.forward (item_tower.py:131-152) for cfg 3: audio ResNet-18 on
+    ``target_audio``, visual ResNet-18 on ``target_image``, a zero text slot (the mDeBERTa
+    branch is cfg 4), the tabular MLP on ``target_tabular``; concatenated in the reference's
+    fixed order (:147) into the fusion head.  ``p`` holds item-tower names without the
+    ``item_tower.`` prefix."""
+    audio = resnet18_forward(p, batch["target_audio"], "audio_encoder.backbone.", update_running)
+    visual = resnet18_forward(p, batch["target_image"], "visual_encoder.backbone.",
+                              update_running)
+    text = torch.zeros(audio.shape[0], text_dim)
+    tab = tabular_forward(p, batch["target_tabular"], "tabular_encoder.mlp.", p_drop, drop,
+                          update_running)
+    modal = torch.cat([audio, visual, text, tab], dim=1)
+    return ttr.item_fusion_forward(p, modal, p_drop, drop, running)
+
+
+def synthetic_items(B: int, tabular_dim: int, mel=(128, 256), cover=(224, 224),
+                    generator: Optional[torch.Generator] = None) -> Dict[str, Tensor]:
+    """cfg-3 item inputs (BASELINE configs[2]): N(0,1) mel-spectrograms [B,1,128,256],
+    ImageNet-normalised-like covers N(0,1) [B,3,224,224], tabular features N(0,1) [B,T]."""
+    g = generator
+    return {"target_audio": torch.randn(B, 1, *mel, generator=g),
+            "target_image": torch.randn(B, 3, *cover, generator=g),
+            "target_tabular": torch.randn(B, tabular_dim, generator=g)}

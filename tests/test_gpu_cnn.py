@@ -2,14 +2,17 @@
 oracle restatement (oracle/resnet_ref.py) with identical parameters.
 
 bf16 operands through 20 convolutions: the embedding is compared at 5e-2 relative to its
-max-abs (bf16 rounding compounds layer over layer, BatchNorm re-normalises it), every
-parameter gradient by direction (cosine >= 0.98) and norm (within 10 %), BN running stats at
-1e-2.  Parity against the reference itself is unpinned (torchvision is absent)."""
+max-abs (bf16 rounding compounds layer over layer, BatchNorm re-normalises it); gradients by
+direction against the bf16-emulation yardstick (test_resnet18_vs_oracle's docstring); BN
+running stats at 1e-2.  Parity against the reference itself is unpinned (torchvision is
+absent).  The cfg-3 model tests run the whole two-tower forward/backward and
+the graph-captured TrainStep on raw mels / covers / tabular inputs."""
 import pytest
 import torch
 import torch.nn.functional as TF
 
 from oracle import resnet_ref as rref
+from oracle import two_tower_ref as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -166,3 +169,97 @@ def test_tabular_encoder_vs_oracle(gpu_pkg):
             assert p.grad.abs().max().item() < 3e-2 * max(1.0, Pr[name].grad.abs().max().item())
             continue
         check_grad(name, p.grad, Pr[name].grad)
+
+
+def test_resnet18_eval_mode_uses_running_stats(gpu_pkg):
+    """eval(): BatchNorm2d normalises with the running statistics (nn.BatchNorm2d.eval())."""
+    cnn = gpu_pkg.cnn
+    torch.manual_seed(4)
+    net = cnn.ResNet18(3, 128).to(DEV)
+    g = torch.Generator().manual_seed(5)
+    with torch.no_grad():
+        for _ in range(3):                     # populate the running statistics
+            net(torch.randn(8, 3, 64, 64, generator=g).to(DEV))
+    net.eval()
+    x = torch.randn(4, 3, 64, 64, generator=g)
+    with torch.no_grad():
+        out = net(x.to(DEV))
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    assert int(sd["bn1.num_batches_tracked"]) == 3
+    y = TF.conv2d(x, sd["conv1.weight"], stride=2, padding=3)
+
+    def bn(t, n):
+        return TF.batch_norm(t, sd[n + ".running_mean"], sd[n + ".running_var"],
+                             sd[n + ".weight"], sd[n + ".bias"], training=False)
+    y = TF.max_pool2d(torch.relu(bn(y, "bn1")), 3, 2, 1)
+    for lname, _, _, s in rref.LAYERS:
+        for bi in range(2):
+            b = f"{lname}.{bi}."
+            st = s if bi == 0 else 1
+            h = torch.relu(bn(TF.conv2d(y, sd[b + "conv1.weight"], stride=st, padding=1), b + "bn1"))
+            h = bn(TF.conv2d(h, sd[b + "conv2.weight"], padding=1), b + "bn2")
+            idn = y
+            if b + "downsample.0.weight" in sd:
+                idn = bn(TF.conv2d(y, sd[b + "downsample.0.weight"], stride=st), b + "downsample.1")
+            y = torch.relu(h + idn)
+    ref_out = TF.linear(TF.adaptive_avg_pool2d(y, 1).flatten(1), sd["fc.weight"], sd["fc.bias"])
+    assert rel(out, ref_out) < 5e-2, rel(out, ref_out)
+    assert int(net.state_dict()["bn1.num_batches_tracked"]) == 3     # eval updates nothing
+
+
+def _cfg3(pkg, B=8, L=12, V=211, T=32, mel=(64, 96), cover=(64, 64), seed=0, p=0.0):
+    torch.manual_seed(seed)
+    m = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=T, num_genders=3, num_countries=8,
+                          max_seq_len=L, user_embedding_dim=128, item_embedding_dim=128,
+                          user_dropout=p, precomputed_modalities=False).to(DEV)
+    m.item_tower.fusion_layer[3].p = p
+    m.item_tower.tabular_encoder.mlp[3].p = p
+    g = torch.Generator().manual_seed(seed + 1)
+    batch = ref.synthetic_batch(B, L, V, num_countries=8, generator=g)
+    del batch["target_modal"]
+    batch.update(rref.synthetic_items(B, T, mel, cover, generator=g))
+    return m, batch
+
+
+def test_cfg3_two_tower_vs_oracle(gpu_pkg):
+    """cfg 3 (raw mels / covers / tabular, zero text slot): loss and logits vs the fp32
+    oracle, item-tower gradients by direction.  bf16 through two ResNet-18s moves the
+    item embedding ~2 %, so the loss bound here is 1e-2 (the 1e-3 north-star bar is cfg 2's,
+    whose item inputs are precomputed)."""
+    m, batch = _cfg3(gpu_pkg)
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
+    lref, logits_ref, _, _ = ref.two_tower_loss(params, batch, running=None)
+    lref.backward()
+    bd = {k: v.to(DEV) for k, v in batch.items()}
+    loss, logits, _, _ = m(bd)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(lref)) < 1e-2, (float(loss), float(lref))
+    assert rel(logits, logits_ref) < 5e-2
+    mine = dict(m.named_parameters())
+    names = [k for k in mine if k.startswith("item_tower.") and "fusion_layer.0.bias" not in k
+             and "mlp.0.bias" not in k]
+    assert any("audio_encoder" in k for k in names) and any("visual_encoder" in k for k in names)
+    for k in names:
+        a = mine[k].grad.double().cpu().flatten()
+        b = params[k].grad.double().flatten()
+        cos = torch.dot(a, b).item() / (a.norm().item() * b.norm().item() + 1e-30)
+        assert cos > 0.85 and abs(a.norm().item() / b.norm().item() - 1) < 0.15, (k, cos)
+
+
+def test_cfg3_train_step_graph_equals_eager_and_learns(gpu_pkg):
+    """cfg-3 TrainStep: graph replay follows the eager schedule (atomics make the float
+    summation order differ, so not bit-exact) and the loss decreases."""
+    m1, batch = _cfg3(gpu_pkg, B=16, seed=7, p=0.1)
+    m2, _ = _cfg3(gpu_pkg, B=16, seed=7, p=0.1)
+    bd = {k: v.to(DEV) for k, v in batch.items()}
+    s1 = gpu_pkg.TrainStep(m1, lr=1e-3, use_graph=True, seed=11)
+    s2 = gpu_pkg.TrainStep(m2, lr=1e-3, use_graph=False, seed=11)
+    l1 = [float(s1.step(bd)) for _ in range(12)]
+    l2 = [float(s2.step(bd)) for _ in range(12)]
+    assert abs(l1[0] - l2[0]) < 1e-3, (l1[0], l2[0])
+    assert abs(l1[1] - l2[1]) < 2e-2, (l1[:3], l2[:3])
+    assert l1[-1] < l1[0] - 0.2, l1
+    bufs = dict(m1.named_buffers())
+    assert int(bufs["item_tower.audio_encoder.backbone.bn1.num_batches_tracked"]) == 12
+    assert int(bufs["item_tower.tabular_encoder.mlp.1.num_batches_tracked"]) == 12
