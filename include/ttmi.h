@@ -214,13 +214,18 @@ int ttmi_sum_scaled(int n, const float* x, float scale, float* out, hipStream_t 
  * torchvision resnet18): implicit GEMM over NHWC bf16 activations, C and Co multiples of 8
  * (stems zero-padded with ttmi_nchw_to_nhwc), square stride/pad, no bias.
  *   mode 0 FWD:   y[n,ho,wo,co] = Σ x[n, ho·s−p+kh, wo·s−p+kw, ci] W[co,ci,kh,kw]   (out bf16),
- *                 colsum/colsumsq[co] += Σ y, Σ y² (fp32, may both be NULL; BatchNorm stats)
+ *                 colsum/colsumsq [TTMI_CONV_STAT_REPS][Co] fp32 (zero on entry, may both be
+ *                 NULL): Σ_r colsum[r][co] = Σ y, Σ y² (BatchNorm stats, spread over replica
+ *                 rows so the workgroups' atomics do not serialise on one address)
  *   mode 1 DGRAD: dx[n,h,w,ci] = Σ dy[n,(h+p−kh)/s,(w+p−kw)/s,co] W[co,ci,kh,kw] (+ addend)
- *                 over the stride lattice (out bf16; needs Cin == C)
- *   mode 2 WGRAD: dW[co,ci,kh,kw] += Σ dy·x (out fp32, torch layout, ci < Cin)
+ *                 over the stride lattice (out bf16; needs Cin == C, Co % 64 == 0, stride <= 2)
+ *   mode 2 WGRAD: dW[co,ci,kh,kw] += Σ dy·x (out fp32, torch layout, ci < Cin); split-K
+ *                 partials go to `workspace` (ttmi_conv2d_workspace(d) bytes), then are
+ *                 summed in a fixed order (deterministic)
  * w is the bf16 mirror from ttmi_conv_weight_prep: Wf = [Co][KH][KW][C] for FWD,
- * Wd = [Cin][KH][KW][Co] for DGRAD.
+ * Wd = [Cin][KH][KW][Co] for DGRAD.  Every tensor must have < 2^31 elements.
  * ---------------------------------------------------------------------------------- */
+#define TTMI_CONV_STAT_REPS 16
 typedef struct ttmi_conv_desc {
   int mode;
   int N, H, W, C, Cin, Co, KH, KW, stride, pad;
@@ -230,8 +235,13 @@ typedef struct ttmi_conv_desc {
   void* out;
   const void* addend;     /* DGRAD: bf16 [N,H,W,C] added before the store, or NULL */
   float* colsum; float* colsumsq;
+  void* workspace;        /* WGRAD scratch (device), or NULL for FWD/DGRAD */
+  int64_t workspace_bytes;
 } ttmi_conv_desc;
 int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream);
+/* Bytes of WGRAD scratch ttmi_conv2d needs for this descriptor (0 for FWD/DGRAD; -1 on a bad
+ * descriptor). */
+int64_t ttmi_conv2d_workspace(const ttmi_conv_desc* d);
 /* wf[co][kh][kw][c] = bf16(w[co][ci][kh][kw]) zero for Cin <= c < Cp; wd[ci][kh][kw][co]
  * likewise (wd may be NULL). w is torch's fp32 Conv2d.weight. */
 int ttmi_conv_weight_prep(int Co, int Cin, int Cp, int KH, int KW, const float* w, uint16_t* wf,
@@ -241,7 +251,7 @@ int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const float* x, uint
                       hipStream_t stream);
 
 /* BatchNorm2d, train mode, over NHWC bf16 [M = N·H·W, C] (C % 8 == 0, C <= 512), batch
- * statistics from the producing conv's colsum/colsumsq:  y = act(w·x̂ + b + residual)
+ * statistics from the producing conv's colsum/colsumsq ([TTMI_CONV_STAT_REPS][C], summed):  y = act(w·x̂ + b + residual)
  * (act = ReLU if relu; residual bf16 or NULL); running stats updated with momentum and the
  * unbiased variance, *num_batches_tracked += 1 (all three may be NULL: eval-free path);
  * save_mean/save_rstd [C] for the backward (nn.BatchNorm2d + torchvision BasicBlock tail).

@@ -105,7 +105,8 @@ def _conv_bn(P, bufs, sp: ConvSpec, x: Tensor, N: int, H: int, W: int, mirrors, 
     y = torch.empty(N, Ho, Wo, sp.cout, device=dev, dtype=torch.bfloat16)
     cs = cq = None                       # eval: BN normalises with the running statistics
     if training:
-        cs, cq = stats[off:off + sp.cout], stats[off + sp.cout:off + 2 * sp.cout]
+        n = ops.CONV_STAT_REPS * sp.cout
+        cs, cq = stats[off:off + n], stats[off + n:off + 2 * n]
     ops.conv2d(ops.FWD, N, H, W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad, x=x,
                w=mirrors[sp.name][0], out=y, colsum=cs, colsumsq=cq)
     a = torch.empty_like(y)
@@ -128,14 +129,15 @@ def resnet18_fwd(P: Dict[str, Tensor], x: Tensor, in_ch: int, bufs: Dict[str, Te
     N, _, H, W = x.shape
     specs = resnet18_convs(in_ch)
     mirrors = weight_mirrors(P, specs)
-    stats = torch.zeros(2 * sum(sp.cout for sp in specs), device=dev) if training else None
+    stats = torch.zeros(2 * ops.CONV_STAT_REPS * sum(sp.cout for sp in specs), device=dev) \
+        if training else None
     st = ResNetSaved(N, mirrors=mirrors)
     x0 = torch.empty(N, H, W, STEM_CP, device=dev, dtype=torch.bfloat16)
     ops.nchw_to_nhwc(x.contiguous().float(), STEM_CP, x0)
     off = 0
     sp = specs[0]
     a = _conv_bn(P, bufs, sp, x0, N, H, W, mirrors, stats, off, None, True, training)
-    off += 2 * sp.cout
+    off += 2 * ops.CONV_STAT_REPS * sp.cout
     st.acts[sp.name] = a
     st.stem_out = a.a
     Hc, Wc = a.y.shape[1], a.y.shape[2]
@@ -153,15 +155,15 @@ def resnet18_fwd(P: Dict[str, Tensor], x: Tensor, in_ch: int, bufs: Dict[str, Te
             idn = y
             if ds is not None:
                 ad = _conv_bn(P, bufs, ds, y, N, H, W, mirrors, stats, off, None, False, training)
-                off += 2 * ds.cout
+                off += 2 * ops.CONV_STAT_REPS * ds.cout
                 st.acts[ds.name] = ad
                 idn = ad.a
             a1 = _conv_bn(P, bufs, c1, y, N, H, W, mirrors, stats, off, None, True, training)
-            off += 2 * c1.cout
+            off += 2 * ops.CONV_STAT_REPS * c1.cout
             st.acts[c1.name] = a1
             H1, W1 = a1.y.shape[1], a1.y.shape[2]
             a2 = _conv_bn(P, bufs, c2, a1.a, N, H1, W1, mirrors, stats, off, idn, True, training)
-            off += 2 * c2.cout
+            off += 2 * ops.CONV_STAT_REPS * c2.cout
             st.acts[c2.name] = a2
             y, H, W = a2.a, H1, W1
     st.last = y

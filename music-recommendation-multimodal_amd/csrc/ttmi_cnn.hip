@@ -51,8 +51,14 @@ __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const b
   const float invM = 1.f / (float)M;
   const bool eval = csum == nullptr;        // eval mode: normalise with the running statistics
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float mu = eval ? running_mean[c] : csum[c] * invM;
-    const float var = eval ? running_var[c] : fmaxf(csq[c] * invM - mu * mu, 0.f);
+    float s1 = 0.f, s2 = 0.f;
+    if (!eval)
+      for (int r = 0; r < TTMI_CONV_STAT_REPS; ++r) {   // replica rows of the conv epilogue
+        s1 += csum[r * C + c];
+        s2 += csq[r * C + c];
+      }
+    const float mu = eval ? running_mean[c] : s1 * invM;
+    const float var = eval ? running_var[c] : fmaxf(s2 * invM - mu * mu, 0.f);
     const float rs = 1.f / sqrtf(var + eps);
     sa[c] = w[c] * rs;
     sb[c] = b[c] - mu * w[c] * rs;

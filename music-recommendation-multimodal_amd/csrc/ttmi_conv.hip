@@ -3,17 +3,26 @@
 // resnet18: conv1 7x7/2, BasicBlock 3x3 convs, 1x1/2 downsample).
 //
 // Activations are NHWC bf16 with the channel count a multiple of 8 (the 1- and 3-channel
-// stems are zero-padded to 8).  Three modes share one tile kernel (64x64 output tile, four
-// waves 2x2, K walked in 64-element tiles, double-buffered LDS with register prefetch):
+// stems are zero-padded to 8).  One tile kernel, templated on the mode and the tile
+// (BM x BN of 64/128, four waves 2x2, each wave (BM/2)x(BN/2) of 16x16x32 MFMAs, K walked in
+// 64-element steps, double-buffered LDS with a register prefetch):
 //   FWD   y[m, co]  = Σ_k im2col(x)[m, k] · Wf[co, k]        m = (n, ho, wo), k = (kh, kw, ci)
-//   DGRAD dx[m, ci] = Σ_k taps(dy)[m, k] · Wd[ci, k]         m = (n, h, w),   k = (kh, kw, co)
-//   WGRAD dW[co, k] += Σ_m dy[m, co] · im2col(x)[m, k]       split over m, fp32 atomics
-// Wf = [Co][KH][KW][C] and Wd = [C][KH][KW][Co] are bf16 mirrors of torch's [Co][Ci][KH][KW]
-// (ttmi_conv_weight_prep); WGRAD scatters into torch's layout directly.  A 16-byte operand
-// chunk is 8 consecutive channels of one tap, so every gathered load is one uint4 (zero
-// outside the image / off the stride lattice).  FWD also accumulates the per-channel Σy and
-// Σy² of the fp32 output for the BatchNorm that follows.
+//         (+ BatchNorm Σy, Σy² per channel into TTMI_CONV_STAT_REPS replica rows)
+//   DGRAD dx[m, ci] = Σ_k taps(dy)[m, k] · Wd[ci, k]         per stride-parity class of m
+//   WGRAD dW[co, k] = Σ_m dy[m, co] · im2col(x)[m, k]        split over m, partials to a
+//                                                            workspace, reduced + permuted
+// Address generation: each thread's gathered rows are fixed for the whole K walk, so their
+// pixel coordinates are decoded once; the per-step (tap, channel) split uses 32-bit
+// magic-number division (all indices < 2^31).  Strided DGRAD runs one GEMM per output
+// parity class (h mod S, w mod S): only the taps on that class's lattice are walked, so no
+// MFMA work is spent on structural zeros.  WGRAD partials are plain 16-byte stores
+// (deterministic; no scattered fp32 atomics into torch's [Co][Cin][KH][KW] layout).
+// Wf = [Co][KH][KW][C] and Wd = [C][KH][KW][Co] are bf16 mirrors of torch's weight
+// (ttmi_conv_weight_prep).  FWD also accumulates Σy, Σy² per channel for the BatchNorm.
 #include "ttmi_common.h"
+
+#include <climits>
+#include <cstdlib>
 
 namespace {
 
@@ -26,61 +35,42 @@ TTMI_DEV uint2 c_lds_tr8(const char* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// q = n / d for n < 2^31 (Granlund–Montgomery round-up multiplier).
+struct FDiv {
+  uint32_t m, s;
+};
+FDiv fdiv_make(uint32_t d) {
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FDiv{(uint32_t)m, s};
+}
+TTMI_DEV int fq(int n, FDiv f) {
+  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.s);
+}
+
+constexpr int MAXCLS = 4;   // stride-parity classes (S <= 2)
+
 struct ConvArgs {
-  int mode;                 // 0 FWD, 1 DGRAD, 2 WGRAD
-  int N, H, W, C;           // input  (C padded, % 8)
-  int Ho, Wo, Co;           // output (Co % 8)
-  int KH, KW, S, P;
-  int Cin;                  // true input channels (WGRAD scatter; <= C)
+  int N, H, W, C, Ho, Wo, Co, KH, KW, S, P, Cin;
   const bf16_t* x;          // FWD/WGRAD: input NHWC
   const bf16_t* dy;         // DGRAD/WGRAD: output grad NHWC
   const bf16_t* w;          // FWD: Wf, DGRAD: Wd
-  void* out;                // FWD: y bf16 [M][Co]; DGRAD: dx bf16 [M][C]; WGRAD: dW f32 torch layout
-  const bf16_t* addend;     // DGRAD: added before the store (the other branch's grad), or NULL
+  void* out;                // FWD: y bf16 [M][Co]; DGRAD: dx bf16 [M][C]
+  const bf16_t* addend;     // DGRAD: added before the store, or NULL
   float* colsum;            // FWD: Σ y per channel (may be NULL)
-  float* colsumsq;          // FWD: Σ y² per channel
-  int64_t GM, GN, GK;       // GEMM sizes
-  int64_t k_split;          // WGRAD: pixels per split (multiple of 64)
+  float* colsumsq;
+  float* ws;                // WGRAD: partials [splits][GM][GN]
+  int GM, GN, GK;           // GEMM sizes (DGRAD: per class below)
+  int k_split;              // WGRAD: pixels per split (multiple of 64)
+  FDiv fC, fKW, fWo, fHo, fCo;
+  // DGRAD parity classes (ph, pw) = (cls / S, cls % S)
+  int cM[MAXCLS], cK[MAXCLS], cHc[MAXCLS], cWc[MAXCLS], ckh0[MAXCLS], ckw0[MAXCLS],
+      cnkw[MAXCLS], coffh[MAXCLS], coffw[MAXCLS];
+  FDiv cfW[MAXCLS], cfH[MAXCLS], cfnkw[MAXCLS];
 };
 
-constexpr int BM = 64, BN = 64, BKE = 64;
-constexpr int PK = 144;                     // k-major pitch: 64 bf16 + 16 B
-constexpr int PT = BM * 2 + 32;             // [k][row] pitch for transposed reads
-
-// Address of the 16-byte chunk of im2col(x) at output pixel m, column k (k % 8 == 0).
-TTMI_DEV const bf16_t* im2col_ptr(const ConvArgs& a, int64_t m, int64_t k) {
-  if (m >= (int64_t)a.N * a.Ho * a.Wo || k >= (int64_t)a.KH * a.KW * a.C) return nullptr;
-  const int wo = (int)(m % a.Wo);
-  const int64_t t = m / a.Wo;
-  const int ho = (int)(t % a.Ho);
-  const int n = (int)(t / a.Ho);
-  const int tap = (int)(k / a.C), ci = (int)(k % a.C);
-  const int kh = tap / a.KW, kw = tap % a.KW;
-  const int hi = ho * a.S - a.P + kh, wi = wo * a.S - a.P + kw;
-  if (hi < 0 || hi >= a.H || wi < 0 || wi >= a.W) return nullptr;
-  return a.x + (((int64_t)n * a.H + hi) * a.W + wi) * a.C + ci;
-}
-
-// Address of the chunk of the transposed-conv taps of dy at input pixel m, column k =
-// (kh, kw, co): dy[n, (h+P-kh)/S, (w+P-kw)/S, co] when on the stride lattice.
-TTMI_DEV const bf16_t* dgrad_ptr(const ConvArgs& a, int64_t m, int64_t k) {
-  if (m >= (int64_t)a.N * a.H * a.W || k >= (int64_t)a.KH * a.KW * a.Co) return nullptr;
-  const int w = (int)(m % a.W);
-  const int64_t t = m / a.W;
-  const int h = (int)(t % a.H);
-  const int n = (int)(t / a.H);
-  const int tap = (int)(k / a.Co), co = (int)(k % a.Co);
-  const int kh = tap / a.KW, kw = tap % a.KW;
-  const int th = h + a.P - kh, tw = w + a.P - kw;
-  if (th < 0 || tw < 0 || th % a.S || tw % a.S) return nullptr;
-  const int ho = th / a.S, wo = tw / a.S;
-  if (ho >= a.Ho || wo >= a.Wo) return nullptr;
-  return a.dy + (((int64_t)n * a.Ho + ho) * a.Wo + wo) * a.Co + co;
-}
-
-TTMI_DEV uint4 ld_or_zero(const bf16_t* p) {
-  return p ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-}
+constexpr int PK = 144;                     // k-major LDS pitch: 64 bf16 + 16 B
 
 // Fragment reads (same k-permutation on both operands: lane group g of each 32-wide k chunk
 // holds k = 4g..4g+3 and 16+4g..16+4g+3).
@@ -90,6 +80,7 @@ TTMI_DEV uint4 frag_k(const char* s, int row0, int c, int lane) {
   const uint2 lo = c_lds8(p), hi = c_lds8(p + 32);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
+template <int PT>
 TTMI_DEV uint4 frag_t(const char* s, int row0, int c, int lane) {
   const int i = lane & 15, g = lane >> 4;
   const int q = i >> 2, pp = i & 3;
@@ -98,65 +89,165 @@ TTMI_DEV uint4 frag_t(const char* s, int row0, int c, int lane) {
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
-  // FWD/DGRAD: A k-major gathered [BM][64 k], B k-major weight rows.
-  // WGRAD:     A = dy as [k=pixel][row=co] (transposed reads), B = im2col as [k=pixel][row=kcol].
-  constexpr int AKM = BM * PK, AT = BKE * PT;
-  constexpr int STAGE = (AKM > AT ? AKM : AT) + (BN * PK > AT ? BN * PK : AT);
+TTMI_DEV uint4 ldg16(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+}
+
+template <int MODE, int BM, int BN>
+__global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
+  constexpr bool WG = MODE == 2;
+  constexpr int CA = BM / 32, CB = BN / 32;             // 16-B chunks per thread per stage
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int PTA = BM * 2 + 32, PTB = BN * 2 + 32;   // [k][row] pitches (WGRAD)
+  constexpr int SA = WG ? 64 * PTA : BM * PK;
+  constexpr int SB = WG ? 64 * PTB : BN * PK;
+  constexpr int STAGE = SA + SB;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t n0 = (int64_t)blockIdx.x * BN, m0 = (int64_t)blockIdx.y * BM;
-  const bool wg = a.mode == 2;
-  const int64_t kbeg = wg ? (int64_t)blockIdx.z * a.k_split : 0;
-  const int64_t kend = wg ? std::min<int64_t>(a.GK, kbeg + a.k_split) : a.GK;
-  const int64_t Kw = (int64_t)a.KH * a.KW * a.C;        // weight row length (FWD)
 
-  // per-thread chunk coordinates: 2 chunks per operand per stage
-  uint4 ra[2], rb[2];
-  auto load = [&](int64_t k0) {
+  // tile coordinates: blockIdx.x enumerates (n-tile, m-tile), XCD-grouped so that the
+  // n-tiles of one m-row run on the same XCD (they share the gathered A rows in its L2)
+  const int gx = (a.GN + BN - 1) / BN;
+  int t = blockIdx.x;
+  if ((gridDim.x & 7) == 0) t = (t & 7) * (gridDim.x >> 3) + (t >> 3);
+  const int n0 = (t % gx) * BN, m0 = (t / gx) * BM;
+  const int cls = MODE == 1 ? (int)blockIdx.y : 0;
+  const int GM = MODE == 1 ? a.cM[cls] : a.GM;
+  const int GK = MODE == 1 ? a.cK[cls] : a.GK;
+  if (m0 >= GM) return;                                  // DGRAD: smaller parity class
+  const int kbeg = WG ? (int)blockIdx.y * a.k_split : 0;
+  const int kend = WG ? min(GK, kbeg + a.k_split) : GK;
+
+  // ---- per-thread gather state, decoded once
+  const int kk = (tid & 7) * 8;                          // FWD/DGRAD: k offset of my chunks
+  int rh[CA], rw[CA];                                    // row coordinates (see modes)
+  const bf16_t* rbase[CA];
+  int bkh[CB], bkw[CB], bci[CB];                         // WGRAD: tap/channel of my B chunks
+  bool bok[CB];
+  if constexpr (MODE == 0) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int idx = tid + c * 256;
-      if (!wg) {
-        const int r = idx >> 3, kk = (idx & 7) * 8;       // [row][k]: 8 chunks per row
-        const int64_t m = m0 + r, k = k0 + kk, n = n0 + r;
-        const bf16_t* pa = a.mode == 0 ? im2col_ptr(a, m, k) : dgrad_ptr(a, m, k);
-        ra[c] = ld_or_zero(pa);
-        const int64_t kw_len = a.mode == 0 ? Kw : (int64_t)a.KH * a.KW * a.Co;
-        const bf16_t* pb = (n < a.GN && k < kw_len) ? a.w + n * kw_len + k : nullptr;
-        rb[c] = ld_or_zero(pb);
-      } else {
-        const int kr = idx >> 3, rr = (idx & 7) * 8;      // [k][row]: 8 chunks per k row
-        const int64_t pix = k0 + kr;
-        const int64_t co = m0 + rr, kc = n0 + rr;
-        const bf16_t* pa = (pix < kend && co < a.Co) ? a.dy + pix * a.Co + co : nullptr;
-        ra[c] = ld_or_zero(pa);
-        rb[c] = pix < kend ? ld_or_zero(im2col_ptr(a, pix, kc)) : make_uint4(0, 0, 0, 0);
+    for (int c = 0; c < CA; ++c) {
+      const int m = m0 + (tid >> 3) + 32 * c;
+      rh[c] = INT_MIN / 2; rw[c] = 0; rbase[c] = a.x;
+      if (m < GM) {
+        const int q = fq(m, a.fWo), wo = m - q * a.Wo;
+        const int n = fq(q, a.fHo), ho = q - n * a.Ho;
+        rh[c] = ho * a.S - a.P;
+        rw[c] = wo * a.S - a.P;
+        rbase[c] = a.x + (int64_t)n * a.H * a.W * a.C;
+      }
+    }
+  } else if constexpr (MODE == 1) {
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      const int m = m0 + (tid >> 3) + 32 * c;
+      rh[c] = INT_MIN / 2; rw[c] = 0; rbase[c] = a.dy;
+      if (m < GM) {
+        const int q = fq(m, a.cfW[cls]), ww = m - q * a.cWc[cls];
+        const int n = fq(q, a.cfH[cls]), hh = q - n * a.cHc[cls];
+        rh[c] = hh + a.coffh[cls];
+        rw[c] = ww + a.coffw[cls];
+        rbase[c] = a.dy + (int64_t)n * a.Ho * a.Wo * a.Co;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int kc = n0 + ((tid + 256 * c) % (BN / 8)) * 8;
+      bok[c] = kc < a.GN;
+      const int tap = fq(kc, a.fC);
+      bci[c] = kc - tap * a.C;
+      bkh[c] = fq(tap, a.fKW);
+      bkw[c] = tap - bkh[c] * a.KW;
+    }
+  }
+
+  uint4 ra[CA], rb[CB];
+  auto load = [&](int k0) {
+    if constexpr (MODE == 0) {
+      const int k = k0 + kk;
+      const bool kin = k < GK;
+      const int tap = fq(k, a.fC), ci = k - tap * a.C;
+      const int kh = fq(tap, a.fKW), kw = tap - kh * a.KW;
+#pragma unroll
+      for (int c = 0; c < CA; ++c) {
+        const int hi = rh[c] + kh, wi = rw[c] + kw;
+        const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        ra[c] = ldg16(rbase[c] + ((int64_t)hi * a.W + wi) * a.C + ci, ok);
+      }
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        const int n = n0 + (tid >> 3) + 32 * c;
+        rb[c] = ldg16(a.w + (int64_t)n * GK + k, kin && n < a.GN);
+      }
+    } else if constexpr (MODE == 1) {
+      const int k = k0 + kk;
+      const bool kin = k < GK;
+      const int tt = fq(k, a.fCo), co = k - tt * a.Co;
+      const int i = fq(tt, a.cfnkw[cls]), j = tt - i * a.cnkw[cls];
+#pragma unroll
+      for (int c = 0; c < CA; ++c) {
+        const int ho = rh[c] - i, wo = rw[c] - j;
+        const bool ok = kin && (unsigned)ho < (unsigned)a.Ho && (unsigned)wo < (unsigned)a.Wo;
+        ra[c] = ldg16(rbase[c] + ((int64_t)ho * a.Wo + wo) * a.Co + co, ok);
+      }
+      const int kh = a.ckh0[cls] + a.S * i, kw = a.ckw0[cls] + a.S * j;
+      const int64_t wcol = (int64_t)(kh * a.KW + kw) * a.Co + co;
+      const int64_t wrow = (int64_t)a.KH * a.KW * a.Co;
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        const int n = n0 + (tid >> 3) + 32 * c;
+        rb[c] = ldg16(a.w + n * wrow + wcol, kin && n < a.GN);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < CA; ++c) {
+        const int idx = tid + 256 * c;
+        const int p = k0 + idx / (BM / 8), co = m0 + (idx % (BM / 8)) * 8;
+        ra[c] = ldg16(a.dy + (int64_t)p * a.Co + co, p < kend && co < a.GM);
+      }
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        const int p = k0 + (tid + 256 * c) / (BN / 8);
+        const int q = fq(p, a.fWo), wo = p - q * a.Wo;
+        const int n = fq(q, a.fHo), ho = q - n * a.Ho;
+        const int hi = ho * a.S - a.P + bkh[c], wi = wo * a.S - a.P + bkw[c];
+        const bool ok = p < kend && bok[c] && (unsigned)hi < (unsigned)a.H &&
+                        (unsigned)wi < (unsigned)a.W;
+        rb[c] = ldg16(a.x + (((int64_t)n * a.H + hi) * a.W + wi) * a.C + bci[c], ok);
       }
     }
   };
   auto store = [&](char* s) {
     char* sa = s;
-    char* sb = s + (AKM > AT ? AKM : AT);
+    char* sb = s + SA;
+    if constexpr (!WG) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int idx = tid + c * 256;
-      if (!wg) {
-        *reinterpret_cast<uint4*>(sa + (idx >> 3) * PK + (idx & 7) * 16) = ra[c];
-        *reinterpret_cast<uint4*>(sb + (idx >> 3) * PK + (idx & 7) * 16) = rb[c];
-      } else {
-        *reinterpret_cast<uint4*>(sa + (idx >> 3) * PT + (idx & 7) * 16) = ra[c];
-        *reinterpret_cast<uint4*>(sb + (idx >> 3) * PT + (idx & 7) * 16) = rb[c];
+      for (int c = 0; c < CA; ++c)
+        *reinterpret_cast<uint4*>(sa + ((tid >> 3) + 32 * c) * PK + (tid & 7) * 16) = ra[c];
+#pragma unroll
+      for (int c = 0; c < CB; ++c)
+        *reinterpret_cast<uint4*>(sb + ((tid >> 3) + 32 * c) * PK + (tid & 7) * 16) = rb[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < CA; ++c) {
+        const int idx = tid + 256 * c;
+        *reinterpret_cast<uint4*>(sa + (idx / (BM / 8)) * PTA + (idx % (BM / 8)) * 16) = ra[c];
+      }
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        const int idx = tid + 256 * c;
+        *reinterpret_cast<uint4*>(sb + (idx / (BN / 8)) * PTB + (idx % (BN / 8)) * 16) = rb[c];
       }
     }
   };
 
-  f32x4_t acc[2][2];
+  f32x4_t acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   if (kbeg < kend) {
     load(kbeg);
@@ -164,75 +255,144 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   }
   __syncthreads();
   int buf = 0;
-  for (int64_t k0 = kbeg; k0 < kend; k0 += BKE) {
-    const bool more = k0 + BKE < kend;
-    if (more) load(k0 + BKE);
+  for (int k0 = kbeg; k0 < kend; k0 += 64) {
+    const bool more = k0 + 64 < kend;
+    if (more) load(k0 + 64);
     const char* sa = smem + buf * STAGE;
-    const char* sb = sa + (AKM > AT ? AKM : AT);
+    const char* sb = sa + SA;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      uint4 af[2], bfr[2];
+      uint4 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = wg ? frag_t(sa, wm * 32 + i * 16, c, lane) : frag_k(sa, wm * 32 + i * 16, c, lane);
+      for (int i = 0; i < FM; ++i)
+        af[i] = WG ? frag_t<PTA>(sa, wm * WM + i * 16, c, lane) : frag_k(sa, wm * WM + i * 16, c, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = wg ? frag_t(sb, wn * 32 + j * 16, c, lane) : frag_k(sb, wn * 32 + j * 16, c, lane);
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = WG ? frag_t<PTB>(sb, wn * WN + j * 16, c, lane) : frag_k(sb, wn * WN + j * 16, c, lane);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) Mma<bf16_t>::run(acc[i][j], bfr[j], af[i]);
+        for (int j = 0; j < FN; ++j) Mma<bf16_t>::run(acc[i][j], bfr[j], af[i]);
     }
     if (more) store(smem + (buf ^ 1) * STAGE);
     __syncthreads();
     buf ^= 1;
   }
 
-  // epilogue: lane holds C[m][n..n+3], m = tile row + (lane & 15), n = tile col + 4*(lane >> 4)
+  // ---- epilogue: lane holds C[m][n..n+3], m = row + (lane & 15), n = col + 4*(lane >> 4)
   const int li = lane & 15, lg = lane >> 4;
+  if constexpr (MODE == 2) {
+    float* ws = a.ws + (int64_t)blockIdx.y * a.GM * a.GN;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t n = n0 + wn * 32 + j * 16 + 4 * lg;
-    float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + li;
+      if (m >= a.GM) continue;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t m = m0 + wm * 32 + i * 16 + li;
-      if (m >= a.GM || n >= a.GN) continue;
-      const float* v = reinterpret_cast<const float*>(&acc[i][j]);
-      if (a.mode == 2) {
-        // dW[co = m][kcol = n + e] -> torch [Co][Cin][KH][KW]
-        float* dw = static_cast<float*>(a.out);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t kc = n + e;
-          const int tap = (int)(kc / a.C), ci = (int)(kc % a.C);
-          if (ci < a.Cin) atomicAdd(dw + ((m * a.Cin + ci) * a.KH + tap / a.KW) * a.KW + tap % a.KW, v[e]);
-        }
-        continue;
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WN + j * 16 + 4 * lg;
+        if (n < a.GN) *reinterpret_cast<f32x4_t*>(ws + (int64_t)m * a.GN + n) = acc[i][j];
       }
+    }
+    return;
+  }
+  int64_t orow[FM];                                       // output pixel of each row
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * WM + i * 16 + li;
+    orow[i] = -1;
+    if (m < GM) {
+      if constexpr (MODE == 1) {
+        const int q = fq(m, a.cfW[cls]), ww = m - q * a.cWc[cls];
+        const int n = fq(q, a.cfH[cls]), hh = q - n * a.cHc[cls];
+        const int ph = cls / a.S, pw = cls - ph * a.S;
+        orow[i] = ((int64_t)n * a.H + hh * a.S + ph) * a.W + ww * a.S + pw;
+      } else {
+        orow[i] = m;
+      }
+    }
+  }
+  float cs[FN][4], cq[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + 4 * lg;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[j][e] = cq[j][e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (orow[i] < 0 || n >= a.GN) continue;
+      const float* v = reinterpret_cast<const float*>(&acc[i][j]);
       float o[4] = {v[0], v[1], v[2], v[3]};
-      if (a.mode == 1 && a.addend) {
-        const ushort4 q = *reinterpret_cast<const ushort4*>(a.addend + m * a.GN + n);
+      bf16_t* dst = static_cast<bf16_t*>(a.out) + orow[i] * a.GN + n;
+      if (MODE == 1 && a.addend) {
+        const ushort4 q = *reinterpret_cast<const ushort4*>(a.addend + orow[i] * a.GN + n);
         o[0] += bf2f(q.x); o[1] += bf2f(q.y); o[2] += bf2f(q.z); o[3] += bf2f(q.w);
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { cs[e] += o[e]; cq[e] += o[e] * o[e]; }
+      for (int e = 0; e < 4; ++e) { cs[j][e] += o[e]; cq[j][e] += o[e] * o[e]; }
       ushort4 q;
       q.x = f2bf(o[0]); q.y = f2bf(o[1]); q.z = f2bf(o[2]); q.w = f2bf(o[3]);
-      *reinterpret_cast<ushort4*>(static_cast<bf16_t*>(a.out) + m * a.GN + n) = q;
+      *reinterpret_cast<ushort4*>(dst) = q;
     }
-    if (a.mode == 0 && a.colsum && n < a.GN) {
+  }
+  if (MODE == 0 && a.colsum) {
+    // BatchNorm column statistics: reduce the tile's rows (registers, then the 16 row lanes,
+    // then the two row-waves through LDS) so each column gets one Σy and one Σy² atomic per
+    // workgroup, spread over TTMI_CONV_STAT_REPS replica rows (one hot address per channel
+    // would serialise every workgroup's atomics in a single L2 channel).
+    float* red = reinterpret_cast<float*>(smem);        // [2][BN]; the K loop has drained
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float s = cs[e], s2 = cq[e];
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
-          s += __shfl_xor(s, off, 64);
-          s2 += __shfl_xor(s2, off, 64);
+          cs[j][e] += __shfl_xor(cs[j][e], off, 64);
+          cq[j][e] += __shfl_xor(cq[j][e], off, 64);
         }
-        if (li == 0) {
-          atomicAdd(a.colsum + n + e, s);
-          atomicAdd(a.colsumsq + n + e, s2);
+    if (wm == 1 && li == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = wn * WN + j * 16 + 4 * lg + e;
+          red[col] = cs[j][e];
+          red[BN + col] = cq[j][e];
         }
-      }
+    }
+    __syncthreads();
+    if (wm == 0 && li == 0) {
+      const int rep = blockIdx.x % TTMI_CONV_STAT_REPS;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = wn * WN + j * 16 + 4 * lg + e;
+          const int n = n0 + col;
+          if (n < a.GN) {
+            atomicAdd(a.colsum + (int64_t)rep * a.GN + n, cs[j][e] + red[col]);
+            atomicAdd(a.colsumsq + (int64_t)rep * a.GN + n, cq[j][e] + red[BN + col]);
+          }
+        }
+    }
+  }
+}
+
+// dW (torch [Co][Cin][KH][KW]) += Σ_split ws[split][co][(kh·KW + kw)·C + ci], ci < Cin.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
+                                                           int GM, int GN, int C, int Cin, int KW,
+                                                           int KHKW, float* __restrict__ dw) {
+  const int64_t n4 = (int64_t)GM * GN / 4, plane = (int64_t)GM * GN;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4_t s = reinterpret_cast<const f32x4_t*>(ws)[i];
+    for (int sp = 1; sp < splits; ++sp) s += reinterpret_cast<const f32x4_t*>(ws + sp * plane)[i];
+    const int64_t e0 = i * 4;
+    const int co = (int)(e0 / GN), kc = (int)(e0 % GN);
+    const int tap = kc / C, ci0 = kc % C;
+    const float* v = reinterpret_cast<const float*>(&s);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ci = ci0 + e;
+      if (ci < Cin) dw[((int64_t)co * Cin + ci) * KHKW + tap] += v[e];
     }
   }
 }
@@ -296,7 +456,23 @@ extern "C" int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const flo
   return ttmi_check_launch("ttmi_nchw_to_nhwc");
 }
 
-extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
+namespace {
+
+// TTMI_CONV_BM=64|128 forces the FWD/DGRAD tile height (tests cover both tile shapes).
+int forced_bm() {
+  const char* e = getenv("TTMI_CONV_BM");
+  if (!e) return 0;
+  const int v = atoi(e);
+  return v == 64 || v == 128 ? v : 0;
+}
+
+struct ConvPlan {
+  ConvArgs a;
+  int bm, bn, splits;
+  int64_t ws_bytes;
+};
+
+int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
   TTMI_REQUIRE(d != nullptr, "ttmi_conv2d: null descriptor");
   TTMI_REQUIRE(d->mode >= 0 && d->mode <= 2, "ttmi_conv2d: bad mode");
   TTMI_REQUIRE(d->N >= 0 && d->H > 0 && d->W > 0 && d->C > 0 && d->C % 8 == 0 && d->Co > 0 &&
@@ -306,9 +482,11 @@ extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
   const int Ho = (d->H + 2 * d->pad - d->KH) / d->stride + 1;
   const int Wo = (d->W + 2 * d->pad - d->KW) / d->stride + 1;
   TTMI_REQUIRE(Ho > 0 && Wo > 0, "ttmi_conv2d: empty output");
-  if (d->N == 0) return TTMI_OK;
-  ConvArgs a{};
-  a.mode = d->mode;
+  const int64_t Mi = (int64_t)d->N * d->H * d->W, Mo = (int64_t)d->N * Ho * Wo;
+  TTMI_REQUIRE(Mi * std::max(d->C, d->Co) < (1ll << 31) && Mo * d->Co < (1ll << 31),
+               "ttmi_conv2d: tensors must have < 2^31 elements");
+  ConvArgs& a = pl->a;
+  a = ConvArgs{};
   a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C;
   a.Ho = Ho; a.Wo = Wo; a.Co = d->Co;
   a.KH = d->KH; a.KW = d->KW; a.S = d->stride; a.P = d->pad; a.Cin = d->Cin;
@@ -318,31 +496,105 @@ extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
   a.out = d->out;
   a.addend = static_cast<const bf16_t*>(d->addend);
   a.colsum = d->colsum; a.colsumsq = d->colsumsq;
-  const int64_t Mo = (int64_t)d->N * Ho * Wo, Mi = (int64_t)d->N * d->H * d->W;
-  int splits = 1;
+  a.fC = fdiv_make(d->C); a.fKW = fdiv_make(d->KW);
+  a.fWo = fdiv_make(Wo); a.fHo = fdiv_make(Ho); a.fCo = fdiv_make(d->Co);
+  pl->splits = 1;
+  pl->ws_bytes = 0;
+  if (d->mode == 0) {
+    a.GM = (int)Mo; a.GN = d->Co; a.GK = d->KH * d->KW * d->C;
+    pl->bn = d->Co % 128 == 0 ? 128 : 64;
+    pl->bm = 128;
+    if (((a.GM + 127) / 128) * (a.GN / pl->bn) < 512) pl->bm = 64;
+    if (forced_bm()) pl->bm = forced_bm();
+  } else if (d->mode == 1) {
+    TTMI_REQUIRE(d->Cin == d->C, "ttmi_conv2d: DGRAD needs unpadded channels (Cin == C)");
+    TTMI_REQUIRE(d->Co % 64 == 0, "ttmi_conv2d: DGRAD needs Co %% 64 == 0");
+    TTMI_REQUIRE(d->stride <= 2, "ttmi_conv2d: DGRAD supports stride 1 or 2");
+    const int S = d->stride;
+    a.GN = d->C; a.GM = 0; a.GK = 0;
+    for (int c = 0; c < S * S; ++c) {
+      const int ph = c / S, pw = c % S;
+      const int kh0 = (ph + d->pad) % S, kw0 = (pw + d->pad) % S;
+      const int nkh = kh0 < d->KH ? (d->KH - kh0 + S - 1) / S : 0;
+      const int nkw = kw0 < d->KW ? (d->KW - kw0 + S - 1) / S : 0;
+      const int Hc = (d->H - ph + S - 1) / S, Wc = (d->W - pw + S - 1) / S;
+      a.cHc[c] = Hc; a.cWc[c] = Wc;
+      a.cM[c] = Hc > 0 && Wc > 0 ? d->N * Hc * Wc : 0;
+      a.cK[c] = nkh * nkw * d->Co;
+      a.ckh0[c] = kh0; a.ckw0[c] = kw0; a.cnkw[c] = std::max(nkw, 1);
+      a.coffh[c] = (ph + d->pad - kh0) / S; a.coffw[c] = (pw + d->pad - kw0) / S;
+      a.cfW[c] = fdiv_make(std::max(Wc, 1)); a.cfH[c] = fdiv_make(std::max(Hc, 1));
+      a.cfnkw[c] = fdiv_make(std::max(nkw, 1));
+      a.GM = std::max(a.GM, a.cM[c]);
+    }
+    pl->bn = d->C % 128 == 0 ? 128 : 64;
+    pl->bm = 128;
+    if (((a.GM + 127) / 128) * (a.GN / pl->bn) * S * S < 512) pl->bm = 64;
+    if (forced_bm()) pl->bm = forced_bm();
+  } else {
+    a.GM = d->Co; a.GN = d->KH * d->KW * d->C; a.GK = (int)Mo;
+    pl->bm = d->Co % 128 == 0 ? 128 : 64;
+    pl->bn = 128;
+    const int64_t tiles = ((a.GM + pl->bm - 1) / pl->bm) * ((a.GN + 127) / 128);
+    const int64_t ksteps = (Mo + 63) / 64;
+    const int64_t want = std::max<int64_t>(1, (1024 + tiles - 1) / tiles);
+    const int64_t per = std::max<int64_t>(std::min<int64_t>(8, ksteps), (ksteps + want - 1) / want);
+    a.k_split = (int)(per * 64);
+    pl->splits = (int)((ksteps + per - 1) / per);
+    TTMI_REQUIRE(pl->splits <= 65535, "ttmi_conv2d: too many splits");
+    pl->ws_bytes = (int64_t)pl->splits * a.GM * a.GN * 4;
+  }
+  return TTMI_OK;
+}
+
+template <int MODE>
+void launch_conv(const ConvPlan& pl, hipStream_t s) {
+  const ConvArgs& a = pl.a;
+  const int64_t tiles = (int64_t)((a.GN + pl.bn - 1) / pl.bn) * ((a.GM + pl.bm - 1) / pl.bm);
+  const unsigned gy = MODE == 1 ? (unsigned)(a.S * a.S) : (unsigned)pl.splits;
+  const dim3 grid((unsigned)tiles, gy);
+  if (pl.bm == 128 && pl.bn == 128)
+    hipLaunchKernelGGL((conv_tile_kernel<MODE, 128, 128>), grid, dim3(256), 0, s, a);
+  else if (pl.bm == 128)
+    hipLaunchKernelGGL((conv_tile_kernel<MODE, 128, 64>), grid, dim3(256), 0, s, a);
+  else if (pl.bn == 128)
+    hipLaunchKernelGGL((conv_tile_kernel<MODE, 64, 128>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_tile_kernel<MODE, 64, 64>), grid, dim3(256), 0, s, a);
+}
+
+}  // namespace
+
+extern "C" int64_t ttmi_conv2d_workspace(const ttmi_conv_desc* d) {
+  ConvPlan pl;
+  if (conv_plan(d, &pl) != TTMI_OK) return -1;
+  return pl.ws_bytes;
+}
+
+extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
+  ConvPlan pl;
+  int rc = conv_plan(d, &pl);
+  if (rc) return rc;
+  if (d->N == 0) return TTMI_OK;
   if (d->mode == 0) {
     TTMI_REQUIRE(d->x && d->w && d->out, "ttmi_conv2d: FWD needs x, w, out");
     TTMI_REQUIRE(!d->colsum == !d->colsumsq, "ttmi_conv2d: colsum and colsumsq go together");
-    a.GM = Mo; a.GN = d->Co; a.GK = (int64_t)d->KH * d->KW * d->C;
+    launch_conv<0>(pl, stream);
   } else if (d->mode == 1) {
     TTMI_REQUIRE(d->dy && d->w && d->out, "ttmi_conv2d: DGRAD needs dy, w, out");
-    TTMI_REQUIRE(d->Cin == d->C, "ttmi_conv2d: DGRAD needs unpadded channels (Cin == C)");
-    a.GM = Mi; a.GN = d->C; a.GK = (int64_t)d->KH * d->KW * d->Co;
+    launch_conv<1>(pl, stream);
   } else {
     TTMI_REQUIRE(d->x && d->dy && d->out, "ttmi_conv2d: WGRAD needs x, dy, out");
-    a.GM = d->Co; a.GN = (int64_t)d->KH * d->KW * d->C; a.GK = Mo;
-    const int64_t tiles = ((a.GM + BM - 1) / BM) * ((a.GN + BN - 1) / BN);
-    const int64_t ktiles = (Mo + BKE - 1) / BKE;
-    int64_t want = std::max<int64_t>(1, (1024 + tiles - 1) / tiles);
-    want = std::min<int64_t>(want, ktiles);
-    const int64_t per = (ktiles + want - 1) / want;
-    a.k_split = per * BKE;
-    splits = (int)((Mo + a.k_split - 1) / a.k_split);
-    TTMI_REQUIRE(splits <= 65535, "ttmi_conv2d: too many splits");
+    TTMI_REQUIRE(d->workspace && d->workspace_bytes >= pl.ws_bytes,
+                 "ttmi_conv2d: WGRAD needs a workspace of ttmi_conv2d_workspace() bytes");
+    pl.a.ws = static_cast<float*>(d->workspace);
+    launch_conv<2>(pl, stream);
+    rc = ttmi_check_launch("ttmi_conv2d/wgrad");
+    if (rc) return rc;
+    const int64_t n4 = (int64_t)pl.a.GM * pl.a.GN / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>((n4 + 255) / 256, 4096)),
+                       dim3(256), 0, stream, static_cast<const float*>(pl.a.ws), pl.splits, pl.a.GM,
+                       pl.a.GN, d->C, d->Cin, d->KW, d->KH * d->KW, static_cast<float*>(d->out));
   }
-  const int64_t gx = (a.GN + BN - 1) / BN, gy = (a.GM + BM - 1) / BM;
-  TTMI_REQUIRE(gy <= 65535, "ttmi_conv2d: grid too large");
-  hipLaunchKernelGGL(conv_gemm_kernel, dim3((unsigned)gx, (unsigned)gy, (unsigned)splits), dim3(256), 0,
-                     stream, a);
   return ttmi_check_launch("ttmi_conv2d");
 }

@@ -46,7 +46,8 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [("mode", c_i), ("N", c_i), ("H", c_i), ("W", c_i), ("C", c_i), ("Cin", c_i),
                 ("Co", c_i), ("KH", c_i), ("KW", c_i), ("stride", c_i), ("pad", c_i),
                 ("x", c_p), ("dy", c_p), ("w", c_p), ("out", c_p), ("addend", c_p),
-                ("colsum", c_p), ("colsumsq", c_p)]
+                ("colsum", c_p), ("colsumsq", c_p), ("workspace", c_p),
+                ("workspace_bytes", ctypes.c_int64)]
 
 
 class LnBwdDesc(ctypes.Structure):
@@ -94,6 +95,7 @@ SIGNATURES = {
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
     "ttmi_conv2d": (c_i, [c_p, c_p]),
+    "ttmi_conv2d_workspace": (ctypes.c_int64, [c_p]),
     "ttmi_conv_weight_prep": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_nchw_to_nhwc": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
     "ttmi_bn2d_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_i,

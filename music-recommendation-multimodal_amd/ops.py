@@ -185,17 +185,40 @@ def conv_out_hw(H: int, W: int, k: int, stride: int, pad: int):
     return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
 
 
+CONV_STAT_REPS = 16    # TTMI_CONV_STAT_REPS: BatchNorm column stats are [16][C] replica rows
+
+
 def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int, stride: int,
            pad: int, *, x: Optional[Tensor] = None, dy: Optional[Tensor] = None,
            w: Optional[Tensor] = None, out: Tensor, addend: Optional[Tensor] = None,
            colsum: Optional[Tensor] = None, colsumsq: Optional[Tensor] = None) -> Tensor:
     """Implicit-GEMM conv (include/ttmi.h ttmi_conv2d): FWD y = conv(x), DGRAD dx, WGRAD dW."""
+    Ho, Wo = conv_out_hw(H, W, k, stride, pad)
+    need = {"x": (x, N * H * W * C), "dy": (dy, N * Ho * Wo * Co),
+            "colsum": (colsum, CONV_STAT_REPS * Co), "colsumsq": (colsumsq, CONV_STAT_REPS * Co)}
+    if mode == FWD:
+        need.update(w=(w, Co * k * k * C), out=(out, N * Ho * Wo * Co))
+    elif mode == DGRAD:
+        need.update(w=(w, C * k * k * Co), out=(out, N * H * W * C), addend=(addend, N * H * W * C))
+    else:
+        need.update(out=(out, Co * Cin * k * k))
+    for name, (t, n) in need.items():       # an undersized buffer would fault the GPU
+        if t is not None and t.numel() < n:
+            raise ValueError(f"conv2d: {name} has {t.numel()} elements, needs {n}")
     d = ConvDesc()
     d.mode, d.N, d.H, d.W, d.C, d.Cin, d.Co = mode, N, H, W, C, Cin, Co
     d.KH = d.KW = k
     d.stride, d.pad = stride, pad
     d.x, d.dy, d.w, d.out, d.addend = _p(x), _p(dy), _p(w), _p(out), _p(addend)
     d.colsum, d.colsumsq = _p(colsum), _p(colsumsq)
+    ws = None
+    if mode == WGRAD:
+        _L.load()
+        nb = int(_L._lib.ttmi_conv2d_workspace(ctypes.byref(d)))
+        if nb < 0:
+            raise _L.TTMIError(_L._lib.ttmi_last_error().decode())
+        ws = torch.empty(max(nb, 16), device=out.device, dtype=torch.uint8)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), nb
     call("ttmi_conv2d", ctypes.byref(d), _s())
     return out
 
@@ -220,6 +243,11 @@ def bn2d_fwd(x: Tensor, colsum: Optional[Tensor], colsumsq: Optional[Tensor], w:
              momentum: float = 0.1) -> Tensor:
     C = x.shape[-1]
     M = x.numel() // C
+    for name, t in (("colsum", colsum), ("colsumsq", colsumsq)):
+        if t is not None and t.numel() < CONV_STAT_REPS * C:
+            raise ValueError(f"bn2d_fwd: {name} needs [{CONV_STAT_REPS}][{C}] replica rows")
+    if y.numel() < x.numel() or (residual is not None and residual.numel() < x.numel()):
+        raise ValueError("bn2d_fwd: y / residual smaller than x")
     call("ttmi_bn2d_fwd", M, C, _p(x), _p(colsum), _p(colsumsq), _p(w), _p(b), eps, momentum,
          _p(running_mean), _p(running_var), _p(num_batches), _p(residual), int(relu), _p(y),
          _p(save_mean), _p(save_rstd), _s())

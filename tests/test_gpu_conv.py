@@ -37,11 +37,18 @@ SHAPES = [  # N, Cin, H, W, Co, k, stride, pad
     (3, 64, 15, 13, 128, 1, 2, 0),
     (2, 128, 7, 9, 256, 3, 2, 1),
     (2, 256, 5, 4, 512, 3, 1, 1),
+    (4, 128, 20, 18, 128, 3, 1, 1),
+    (2, 128, 9, 11, 256, 1, 2, 0),
 ]
 
 
+@pytest.mark.parametrize("bm", ["64", "128"])
 @pytest.mark.parametrize("N,Cin,H,W,Co,k,s,p", SHAPES)
-def test_conv_fwd_dgrad_wgrad(gpu_pkg, N, Cin, H, W, Co, k, s, p):
+def test_conv_fwd_dgrad_wgrad(gpu_pkg, monkeypatch, bm, N, Cin, H, W, Co, k, s, p):
+    """Both FWD/DGRAD tile heights (TTMI_CONV_BM) on every shape: partial tiles, stride-2
+    DGRAD parity classes (incl. the empty classes of a 1x1/2 conv: dx = addend), the 8-channel
+    padded stems, and WGRAD split-K with the fixed-order partial reduction."""
+    monkeypatch.setenv("TTMI_CONV_BM", bm)
     ops = gpu_pkg.ops
     g = torch.Generator().manual_seed(N * 1000 + Cin + Co + k)
     Cp = (Cin + 7) // 8 * 8
@@ -62,9 +69,12 @@ def test_conv_fwd_dgrad_wgrad(gpu_pkg, N, Cin, H, W, Co, k, s, p):
     wd = torch.empty(Cin, k, k, Co, device=DEV, dtype=torch.bfloat16)
     ops.conv_weight_prep(w.to(DEV), Cp, wf, wd)
     y = torch.empty(N, Ho, Wo, Co, device=DEV, dtype=torch.bfloat16)
-    cs = torch.zeros(Co, device=DEV)
-    cq = torch.zeros(Co, device=DEV)
-    ops.conv2d(ops.FWD, N, H, W, Cp, Cin, Co, k, s, p, x=xd, w=wf, out=y, colsum=cs, colsumsq=cq)
+    R = ops.CONV_STAT_REPS
+    csr = torch.zeros(R, Co, device=DEV)
+    cqr = torch.zeros(R, Co, device=DEV)
+    ops.conv2d(ops.FWD, N, H, W, Cp, Cin, Co, k, s, p, x=xd, w=wf, out=y, colsum=csr,
+               colsumsq=cqr)
+    cs, cq = csr.sum(0), cqr.sum(0)
     torch.cuda.synchronize()
     yr = y_ref.detach()
     assert rel(nchw(y.float()), yr) < 8e-3
@@ -109,8 +119,14 @@ def test_bn2d_fwd_bwd(gpu_pkg, C, relu, res):
     dy = torch.randn(y_ref.shape, generator=g).to(torch.bfloat16).float()
     y_ref.backward(dy)
     xd = nhwc(x).to(torch.bfloat16).to(DEV)
-    cs = nhwc(x).sum((0, 1, 2)).to(DEV)
-    cq = (nhwc(x) ** 2).sum((0, 1, 2)).to(DEV)
+    R = ops.CONV_STAT_REPS                    # replica rows: spread the sums over them
+    cs = torch.zeros(R, C)
+    cq = torch.zeros(R, C)
+    cs[0] = nhwc(x)[:1].sum((0, 1, 2))
+    cs[R - 1] = nhwc(x)[1:].sum((0, 1, 2))
+    cq[0] = (nhwc(x)[:1] ** 2).sum((0, 1, 2))
+    cq[R - 1] = (nhwc(x)[1:] ** 2).sum((0, 1, 2))
+    cs, cq = cs.to(DEV), cq.to(DEV)
     y = torch.empty_like(xd)
     mean, rstd = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
     rmd, rvd, nb = rm.to(DEV), rv.to(DEV), torch.zeros(1, device=DEV, dtype=torch.int64)
