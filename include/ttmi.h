@@ -262,7 +262,8 @@ int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* colsum, cons
                   float* running_var, int64_t* num_batches_tracked, const uint16_t* residual,
                   int relu, uint16_t* y, float* save_mean, float* save_rstd, hipStream_t stream);
 /* Backward: g = dy ⊙ (gate > 0) (gate = the ReLU output, or NULL); dx = w·rstd·(g − Σg/M −
- * x̂·Σgx̂/M); dw += Σgx̂, db += Σg.  sums [2C] fp32 must be zero on entry (scratch);
+ * x̂·Σgx̂/M); dw += Σgx̂, db += Σg.  sums [TTMI_CONV_STAT_REPS][2C] fp32 must be zero on
+ * entry (scratch);
  * g_out (bf16, may be NULL) receives g for the residual branch. */
 int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate, const uint16_t* x,
                   const float* mean, const float* rstd, const float* w, float* sums,

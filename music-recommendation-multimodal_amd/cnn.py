@@ -184,13 +184,14 @@ def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dic
     N = st.N
     specs = resnet18_convs(in_ch)
     byname = {s.name: s for s in specs}
-    sums = torch.zeros(2 * sum(sp.cout for sp in specs), device=dev)
+    R = ops.CONV_STAT_REPS
+    sums = torch.zeros(2 * R * sum(sp.cout for sp in specs), device=dev)
     soff = [0]
 
     def bn_bwd(sp: ConvSpec, act: ConvAct, dy: Tensor, gate: Optional[Tensor],
                g_out: Optional[Tensor] = None) -> Tensor:
-        s = sums[soff[0]:soff[0] + 2 * sp.cout]
-        soff[0] += 2 * sp.cout
+        s = sums[soff[0]:soff[0] + 2 * R * sp.cout]
+        soff[0] += 2 * R * sp.cout
         dyc = torch.empty_like(act.y)
         ops.bn2d_bwd(dy, act.y, act.mean, act.rstd, P[sp.bn + ".weight"], s, dyc,
                      grads[sp.bn + ".weight"], grads[sp.bn + ".bias"], gate=gate, g_out=g_out)

@@ -17,23 +17,6 @@ namespace {
 
 constexpr int MAXC = 512;
 
-TTMI_DEV void unpack8(const uint4& q, float* v) {
-  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
-  }
-}
-TTMI_DEV uint4 pack8(const float* v) {
-  uint4 q;
-  q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-  q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-  return q;
-}
-
 int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096)); }
 
 // ---------------------------------------------------------------- BatchNorm2d forward
@@ -92,9 +75,10 @@ __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const b
 }
 
 // ---------------------------------------------------------------- BatchNorm2d backward
-// Reduction: sums[c] += Σ g, sums[C + c] += Σ g·x̂ (g = dy ⊙ (gate > 0) when gate given);
-// g is written (bf16) when gout != NULL.  Block = 256 threads over row slabs; per thread 8
-// channels of strided rows, then an LDS reduction and one atomic per channel per block.
+// Reduction: sums[r][c] += Σ g, sums[r][C + c] += Σ g·x̂ (g = dy ⊙ (gate > 0) when gate
+// given) with r = block % TTMI_CONV_STAT_REPS; g is written (bf16) when gout != NULL.  Block =
+// 256 threads over row slabs; per thread 8 channels of strided rows, then an LDS reduction and
+// one atomic per channel per block into its replica row (spread: no single hot address).
 __global__ __launch_bounds__(256) void bn2d_bwd_reduce_kernel(int64_t M, int C, const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ gate,
                                                               const bf16_t* __restrict__ x,
@@ -143,10 +127,11 @@ __global__ __launch_bounds__(256) void bn2d_bwd_reduce_kernel(int64_t M, int C, 
 #pragma unroll
       for (int e = 0; e < 8; ++e) { a[e] += red[0][r * cpr + t][e]; bb[e] += red[1][r * cpr + t][e]; }
     }
+    float* rep = sums + (int64_t)(blockIdx.x % TTMI_CONV_STAT_REPS) * 2 * C;   // replica row
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      atomicAdd(sums + t * 8 + e, a[e]);
-      atomicAdd(sums + C + t * 8 + e, bb[e]);
+      atomicAdd(rep + t * 8 + e, a[e]);
+      atomicAdd(rep + C + t * 8 + e, bb[e]);
     }
   }
 }
@@ -164,14 +149,19 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_kernel(int64_t M, int C, c
   __shared__ float sk[MAXC], sm1[MAXC], sm2[MAXC], smu[MAXC], srs[MAXC];
   const float invM = 1.f / (float)M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int r = 0; r < TTMI_CONV_STAT_REPS; ++r) {
+      t1 += sums[(int64_t)r * 2 * C + c];
+      t2 += sums[(int64_t)r * 2 * C + C + c];
+    }
     sk[c] = w[c] * rstd[c];
-    sm1[c] = sums[c] * invM;
-    sm2[c] = sums[C + c] * invM;
+    sm1[c] = t1 * invM;
+    sm2[c] = t2 * invM;
     smu[c] = mean[c];
     srs[c] = rstd[c];
     if (blockIdx.x == 0) {
-      if (db) db[c] += sums[c];
-      if (dw) dw[c] += sums[C + c];
+      if (db) db[c] += t1;
+      if (dw) dw[c] += t2;
     }
   }
   __syncthreads();

@@ -168,3 +168,22 @@ void ttmi_set_error(const char* fmt, ...);
     }                                                \
   } while (0)
 int ttmi_check_launch(const char* what);
+
+// 8 bf16 <-> 8 floats (one 16-byte chunk)
+TTMI_DEV void unpack8(const uint4& q, float* v) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+TTMI_DEV uint4 pack8(const float* v) {
+  uint4 q;
+  q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  return q;
+}
+

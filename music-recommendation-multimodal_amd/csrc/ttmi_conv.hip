@@ -378,22 +378,31 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
 }
 
 // dW (torch [Co][Cin][KH][KW]) += Σ_split ws[split][co][(kh·KW + kw)·C + ci], ci < Cin.
+// 2-D grid: x over 4-column groups of the [GM][GN] plane, y over chunks of WR_SPLITS splits
+// (summed in a fixed order per chunk); each chunk adds its total with one atomic per element,
+// so an element sees ceil(splits / WR_SPLITS) atomics, not a serial walk over every split.
+constexpr int WR_SPLITS = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
                                                            int GM, int GN, int C, int Cin, int KW,
                                                            int KHKW, float* __restrict__ dw) {
   const int64_t n4 = (int64_t)GM * GN / 4, plane = (int64_t)GM * GN;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4_t s = reinterpret_cast<const f32x4_t*>(ws)[i];
-    for (int sp = 1; sp < splits; ++sp) s += reinterpret_cast<const f32x4_t*>(ws + sp * plane)[i];
-    const int64_t e0 = i * 4;
-    const int co = (int)(e0 / GN), kc = (int)(e0 % GN);
-    const int tap = kc / C, ci0 = kc % C;
-    const float* v = reinterpret_cast<const float*>(&s);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int s0 = blockIdx.y * WR_SPLITS, s1 = min(splits, s0 + WR_SPLITS);
+  f32x4_t s = reinterpret_cast<const f32x4_t*>(ws + s0 * plane)[i];
+  for (int sp = s0 + 1; sp < s1; ++sp) s += reinterpret_cast<const f32x4_t*>(ws + sp * plane)[i];
+  const int64_t e0 = i * 4;
+  const int co = (int)(e0 / GN), kc = (int)(e0 % GN);
+  const int tap = kc / C, ci0 = kc % C;
+  const float* v = reinterpret_cast<const float*>(&s);
+  const bool single = splits <= WR_SPLITS;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int ci = ci0 + e;
-      if (ci < Cin) dw[((int64_t)co * Cin + ci) * KHKW + tap] += v[e];
-    }
+  for (int e = 0; e < 4; ++e) {
+    const int ci = ci0 + e;
+    if (ci >= Cin) continue;
+    float* d = dw + ((int64_t)co * Cin + ci) * KHKW + tap;
+    if (single) *d += v[e];
+    else atomicAdd(d, v[e]);
   }
 }
 
@@ -416,19 +425,23 @@ __global__ __launch_bounds__(256) void conv_weight_prep_kernel(int Co, int Cin, 
   }
 }
 
-// x NCHW fp32 [N][Cin][H][W] -> NHWC bf16 [N][H][W][Cp] (channels zero-padded).
+// x NCHW fp32 [N][Cin][H][W] -> NHWC bf16 [N][H][W][Cp] (channels zero-padded).  One thread
+// per pixel: the Cin plane reads are coalesced across threads (consecutive w), the Cp-channel
+// row is written as whole 16-byte chunks.
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(int N, int Cin, int H, int W, int Cp,
                                                            const float* __restrict__ x,
                                                            bf16_t* __restrict__ y) {
-  const int64_t n = (int64_t)N * H * W * Cp;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % Cp);
-    const int64_t p = i / Cp;
-    const int w = (int)(p % W);
-    const int64_t t = p / W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
-    y[i] = c < Cin ? f2bf(x[(((int64_t)b * Cin + c) * H + h) * W + w]) : (bf16_t)0;
+  const int64_t HW = (int64_t)H * W, npix = (int64_t)N * HW;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = p / HW, hw = p - b * HW;
+    const float* src = x + b * Cin * HW + hw;
+    uint4* dst = reinterpret_cast<uint4*>(y + p * Cp);
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = c0 + e < Cin ? src[(int64_t)(c0 + e) * HW] : 0.f;
+      dst[c0 / 8] = pack8(v);
+    }
   }
 }
 
@@ -451,7 +464,7 @@ extern "C" int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const flo
   TTMI_REQUIRE(N >= 0 && Cin > 0 && Cp >= Cin && Cp % 8 == 0 && H > 0 && W > 0, "ttmi_nchw_to_nhwc: bad shape");
   TTMI_REQUIRE(x && y, "ttmi_nchw_to_nhwc: null argument");
   if (N == 0) return TTMI_OK;
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid1((int64_t)N * H * W * Cp)), dim3(256), 0, s, N, Cin, H,
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid1((int64_t)N * H * W)), dim3(256), 0, s, N, Cin, H,
                      W, Cp, x, y);
   return ttmi_check_launch("ttmi_nchw_to_nhwc");
 }
@@ -592,8 +605,8 @@ extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
     rc = ttmi_check_launch("ttmi_conv2d/wgrad");
     if (rc) return rc;
     const int64_t n4 = (int64_t)pl.a.GM * pl.a.GN / 4;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>((n4 + 255) / 256, 4096)),
-                       dim3(256), 0, stream, static_cast<const float*>(pl.a.ws), pl.splits, pl.a.GM,
+    const dim3 rg((unsigned)((n4 + 255) / 256), (unsigned)((pl.splits + WR_SPLITS - 1) / WR_SPLITS));
+    hipLaunchKernelGGL(wgrad_reduce_kernel, rg, dim3(256), 0, stream, static_cast<const float*>(pl.a.ws), pl.splits, pl.a.GM,
                        pl.a.GN, d->C, d->Cin, d->KW, d->KH * d->KW, static_cast<float*>(d->out));
   }
   return ttmi_check_launch("ttmi_conv2d");

@@ -259,6 +259,11 @@ def bn2d_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, sums:
              gate: Optional[Tensor] = None, g_out: Optional[Tensor] = None) -> Tensor:
     C = x.shape[-1]
     M = x.numel() // C
+    if sums.numel() < 2 * CONV_STAT_REPS * C:
+        raise ValueError(f"bn2d_bwd: sums needs [{CONV_STAT_REPS}][{2 * C}] replica rows")
+    for name, t in (("dy", dy), ("dx", dx), ("gate", gate), ("g_out", g_out)):
+        if t is not None and t.numel() < x.numel():
+            raise ValueError(f"bn2d_bwd: {name} smaller than x")
     call("ttmi_bn2d_bwd", M, C, _p(dy), _p(gate), _p(x), _p(mean), _p(rstd), _p(w), _p(sums),
          _p(g_out), _p(dx), _p(dw), _p(db), _s())
     return dx

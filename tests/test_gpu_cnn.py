@@ -227,7 +227,8 @@ def _cfg3(pkg, B=8, L=12, V=211, T=32, mel=(64, 96), cover=(64, 64), seed=0, p=0
 
 def test_cfg3_two_tower_vs_oracle(gpu_pkg):
     """cfg 3 (raw mels / covers / tabular, zero text slot): loss and logits vs the fp32
-    oracle, item-tower gradients by direction.  bf16 storage through two ResNet-18s moves the
+    oracle, item-tower gradients by direction and norm against the same emulation yardstick
+    (cosine within 0.05 of the emulation's).  bf16 storage through two ResNet-18s moves the
     item embedding ~2 %, which τ = 0.07 amplifies in the logits; the loss bound is 2x the
     deviation of the bf16-emulating oracle (same rounding points as the kernels) + 5e-3.
     (The 1e-3 north-star bar is cfg 2's, whose item inputs are precomputed.)"""
@@ -238,8 +239,10 @@ def test_cfg3_two_tower_vs_oracle(gpu_pkg):
     orig = rref.resnet18_forward
     rref.resnet18_forward = resnet18_bf16_emulation       # bf16-storage yardstick
     try:
-        pe = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
-        lemu = float(ref.two_tower_loss(pe, batch, running=None)[0])
+        pe = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
+        le = ref.two_tower_loss(pe, batch, running=None)[0]
+        le.backward()
+        lemu = float(le)
     finally:
         rref.resnet18_forward = orig
     bd = {k: v.to(DEV) for k, v in batch.items()}
@@ -260,11 +263,13 @@ def test_cfg3_two_tower_vs_oracle(gpu_pkg):
                 1.0, params[k].grad.abs().max().item()), k
     names = [k for k in mine if k.startswith("item_tower.") and not k.endswith(zero)]
     assert any("audio_encoder" in k for k in names) and any("visual_encoder" in k for k in names)
-    for k in names:
-        a = mine[k].grad.double().cpu().flatten()
-        b = params[k].grad.double().flatten()
-        cos = torch.dot(a, b).item() / (a.norm().item() * b.norm().item() + 1e-30)
-        assert cos > 0.85 and abs(a.norm().item() / b.norm().item() - 1) < 0.15, (k, cos)
+    for k in names:       # as close to fp32 as the bf16-storage emulation gets (see above)
+        g, gr, ge = mine[k].grad, params[k].grad, pe[k].grad
+        cos, cos_e = _cos(g, gr), _cos(ge, gr)
+        nr = g.norm().item() / gr.norm().item()
+        ne = ge.norm().item() / gr.norm().item()
+        assert cos > cos_e - 0.05, (k, cos, cos_e)
+        assert abs(nr - 1) < 2 * abs(ne - 1) + 0.15, (k, nr, ne)
 
 
 def test_cfg3_train_step_graph_equals_eager_and_learns(gpu_pkg):

@@ -135,7 +135,7 @@ def test_bn2d_fwd_bwd(gpu_pkg, C, relu, res):
     torch.cuda.synchronize()
     assert rel(nchw(y.float()), y_ref.detach()) < 8e-3
     assert rel(rmd, rm_ref) < 1e-5 and rel(rvd, rv_ref) < 1e-4 and int(nb) == 1
-    sums = torch.zeros(2 * C, device=DEV)
+    sums = torch.zeros(ops.CONV_STAT_REPS * 2 * C, device=DEV)
     dx = torch.empty_like(xd)
     dw, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
     gout = torch.empty_like(xd)
