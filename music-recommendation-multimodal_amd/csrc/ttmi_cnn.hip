@@ -194,13 +194,13 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(int N, int H, int W, i
                                                           int s, int p, const bf16_t* __restrict__ x,
                                                           bf16_t* __restrict__ y, uint8_t* __restrict__ idx) {
   const int cpr = C / 8;
-  const int64_t n = (int64_t)N * Ho * Wo * cpr;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % cpr);
-    int64_t t = i / cpr;
-    const int wo = (int)(t % Wo); t /= Wo;
-    const int ho = (int)(t % Ho);
-    const int b = (int)(t / Ho);
+  const int n = N * Ho * Wo * cpr;                    // < 2^31 (host-checked): 32-bit math
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int cg = i % cpr;
+    int t = i / cpr;
+    const int wo = t % Wo; t /= Wo;
+    const int ho = t % Ho;
+    const int b = t / Ho;
     float best[8];
     uint8_t arg[8];
 #pragma unroll
@@ -232,13 +232,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, i
                                                           const uint8_t* __restrict__ idx,
                                                           bf16_t* __restrict__ dx) {
   const int cpr = C / 8;
-  const int64_t n = (int64_t)N * H * W * cpr;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % cpr);
-    int64_t t = i / cpr;
-    const int w = (int)(t % W); t /= W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
+  const int n = N * H * W * cpr;                      // < 2^31 (host-checked): 32-bit math
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int cg = i % cpr;
+    int t = i / cpr;
+    const int w = t % W; t /= W;
+    const int h = t % H;
+    const int b = t / H;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // windows (ho, wo) with ho*s - p <= h <= ho*s - p + k - 1
     const int ho_lo = max(0, (h + p - k + s) / s), ho_hi = min(Ho - 1, (h + p) / s);
@@ -345,6 +345,7 @@ extern "C" int ttmi_maxpool_fwd(int N, int H, int W, int C, int k, int stride, i
   TTMI_REQUIRE(x && y && idx, "ttmi_maxpool_fwd: null argument");
   const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
   if (N == 0) return TTMI_OK;
+  TTMI_REQUIRE((int64_t)N * H * W * C < (1ll << 31), "ttmi_maxpool_fwd: tensor too large");
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((int64_t)N * Ho * Wo * C / 8)), dim3(256), 0, s, N, H,
                      W, C, Ho, Wo, k, stride, pad, (const bf16_t*)x, (bf16_t*)y, idx);
   return ttmi_check_launch("ttmi_maxpool_fwd");
@@ -357,6 +358,7 @@ extern "C" int ttmi_maxpool_bwd(int N, int H, int W, int C, int k, int stride, i
   TTMI_REQUIRE(dy && idx && dx, "ttmi_maxpool_bwd: null argument");
   const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
   if (N == 0) return TTMI_OK;
+  TTMI_REQUIRE((int64_t)N * H * W * C < (1ll << 31), "ttmi_maxpool_bwd: tensor too large");
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((int64_t)N * H * W * C / 8)), dim3(256), 0, s, N, H, W,
                      C, Ho, Wo, k, stride, pad, (const bf16_t*)dy, idx, (bf16_t*)dx);
   return ttmi_check_launch("ttmi_maxpool_bwd");

@@ -388,9 +388,15 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   const int64_t n4 = (int64_t)GM * GN / 4, plane = (int64_t)GM * GN;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  const int s0 = blockIdx.y * WR_SPLITS, s1 = min(splits, s0 + WR_SPLITS);
-  f32x4_t s = reinterpret_cast<const f32x4_t*>(ws + s0 * plane)[i];
-  for (int sp = s0 + 1; sp < s1; ++sp) s += reinterpret_cast<const f32x4_t*>(ws + sp * plane)[i];
+  const int s0 = blockIdx.y * WR_SPLITS, n = min(splits - s0, WR_SPLITS);
+  f32x4_t part[WR_SPLITS];
+#pragma unroll
+  for (int j = 0; j < WR_SPLITS; ++j)             // all loads in flight together
+    part[j] = j < n ? reinterpret_cast<const f32x4_t*>(ws + (s0 + j) * plane)[i]
+                    : f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t s = part[0];
+#pragma unroll
+  for (int j = 1; j < WR_SPLITS; ++j) s += part[j];
   const int64_t e0 = i * 4;
   const int co = (int)(e0 / GN), kc = (int)(e0 % GN);
   const int tap = kc / C, ci0 = kc % C;
