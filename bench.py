@@ -140,7 +140,7 @@ def probe_dominant(step, batch, device, iters: int = 20):
 
 
 def probe_conv(step, batch, device, iters: int = 3):
-    """cfg 3 roofline of the dominant kernel, the implicit-GEMM conv (conv_gemm_kernel: FWD,
+    """cfg 3 roofline of the dominant kernel, the implicit-GEMM conv (conv_tile_kernel: FWD,
     DGRAD and WGRAD launches of both ResNet-18s).  As probe_dominant: one eager forward +
     backward records the step's conv launch mix, which is replayed between HIP events on
     the launch stream.  Algorithmic FLOPs per launch: 2·N·Ho·Wo·Co·Cin·k² (the same for all
@@ -177,11 +177,11 @@ def probe_conv(step, batch, device, iters: int = 3):
         fl += 2.0 * N * Ho * Wo * Co * Cin * k * k
     fl /= n
     tf = fl / sec / 1e12
-    return {"kernel": "conv_gemm_kernel (implicit-GEMM conv FWD/DGRAD/WGRAD, per-step launch "
+    return {"kernel": "conv_tile_kernel (implicit-GEMM conv FWD/DGRAD/WGRAD, per-step launch "
                       "mix of both ResNet-18s)",
             "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4),
-            "traffic": read_traffic("conv_gemm_kernel"), "avg_us": round(sec * 1e6, 2),
+            "traffic": read_traffic("conv_tile_kernel"), "avg_us": round(sec * 1e6, 2),
             "launches_per_step": len(calls), "flops_per_launch": round(fl)}
 
 
