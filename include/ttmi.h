@@ -48,9 +48,11 @@ int ttmi_abi_version(void);
  *
  *   C[m,n] (=|+=) epi( alpha * Σ_k A(m,k)·B(n,k) )
  *   A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m];  B(n,k) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n]
- *   epi: v += bias[n]; v = act(v) (0 none, 1 relu);
+ *   epi: v += bias[n]; v = act(v) (0 none, 1 relu, 2 GELU (erf), 3 none: see gate);
  *        v = dropout(v, idx = r(m)*ld_drop + n) with r(m) = drop_rows ? drop_rows[m] : m;
  *        v = gate ? (gate[m*ld_gate+n] > 0 ? v*gate_scale : 0) : v;  colsum[n] += v;
+ *        act 3 instead multiplies by GELU'(gate[m*ld_gate+n]) (gate = the stored pre-activation:
+ *        the input gradient of a GELU-activated Linear, DeBERTa intermediate.dense).
  *        v += residual[m*ld_res+n];  C = v (c_mode 0) or C += v atomically (c_mode 1, f32 C).
  *   rowsum_a (may be NULL): rowsum_a[m] += Σ_k A(m,k) — with A = dYᵀ of a weight-gradient
  *   GEMM this is the bias gradient, taken from the operand fragments already in registers.
@@ -372,6 +374,59 @@ int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                     const int64_t* key_valid, const int32_t* rows, const float* lse,
                     const void* dctx, float drop_p, const uint64_t* drop_seed, void* dqkv,
                     hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * mDeBERTa-v3 text encoder (cfg 4; reference src/models/item_tower.py:41-83 = transformers
+ * DebertaV2Model + peft LoRA + masked mean-pool; modeling_deberta_v2.py).  d_head = 64.
+ * ---------------------------------------------------------------------------------- */
+/* DebertaV2Embeddings.forward: y = dropout(LN(table[ids]) · mask) per token row (H % 64 == 0);
+ * y32 (fp32 [M,H], may be NULL) and y16 (bf16, row stride ld16). table is the bf16 copy of
+ * word_embeddings.weight; mask may be NULL. */
+int ttmi_deb_embed_fwd(int64_t M, int H, const int64_t* ids, const uint16_t* table,
+                       const float* ln_w, const float* ln_b, float eps, const int64_t* mask,
+                       float drop_p, const uint64_t* drop_seed, float* y32, uint16_t* y16,
+                       int64_t ld16, hipStream_t stream);
+/* Post-LayerNorm (DebertaV2SelfOutput / DebertaV2Output LayerNorm(h + residual)): y = LN(z),
+ * z fp32 [M,H]; y32 (fp32, may be NULL) and y16 (bf16, stride ld16, may be NULL); mean/rstd. */
+int ttmi_deb_ln_fwd(int64_t M, int H, const float* z, const float* ln_w, const float* ln_b,
+                    float eps, float* y32, uint16_t* y16, int64_t ld16, float* mean,
+                    float* rstd, hipStream_t stream);
+/* Disentangled self-attention (DisentangledSelfAttention with share_att_key, c2p|p2c):
+ *   score[i,j] = (Q_i·K_j + Q_i·posK[δ(i-j)] + K_j·posQ[δ(i-j)]) · inv_scale, masked by
+ *   mask_i·mask_j (finfo.min), softmax, dropout(p), ·V.  δ = delta[i - j + S - 1] =
+ *   clamp(log-bucket(i - j) + span, 0, npos - 1) (make_log_bucket_position).  Q/K/V rows are
+ *   b·S + s with head h at column h·64 (ldqkv); posq/posk are [npos, ·] (ldpos) projections of
+ *   the LayerNorm'd relative table; ctx like Q; lse [B, nh, S] fp32 (saved for backward).
+ * Backward: dq/dk/dv (bf16, lddqkv) from dctx, recomputing the scores; posK gets no gradient
+ * (frozen).  With lora_u != NULL (the query_proj LoRA down-projection of the relative table,
+ * [npos, 8] fp32) it also writes the rank-8 contractions that carry the LoRA gradient through
+ * posQ = query_proj(rel): lora_hu [B·S, nh, 8] = Σ_i dS_ij·u[δ_ij] and lora_pb [B·nh, npos, 8]
+ * = Σ_ij dS_ij·(K_j·Bq_h)[δ_ij], with lora_bq = lora_B of query_proj [nh·64, 8] fp32 and dS the
+ * gradient of the unscaled score terms.  S <= 256. */
+typedef struct ttmi_dis_attn_desc {
+  int B, S, nh, d_head, npos;
+  const void* q; const void* k; const void* v; int64_t ldqkv;
+  const void* posq; const void* posk; int64_t ldpos;
+  const int64_t* mask;
+  const int16_t* delta;
+  float inv_scale;
+  float drop_p; const uint64_t* drop_seed;
+  void* ctx; int64_t ldctx;
+  float* lse;
+  const void* dctx; int64_t lddctx;
+  void* dq; void* dk; void* dv; int64_t lddqkv;
+  const float* lora_u; const float* lora_bq; float* lora_hu; float* lora_pb;
+} ttmi_dis_attn_desc;
+int ttmi_dis_attn_fwd(const ttmi_dis_attn_desc* d, hipStream_t stream);
+int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t stream);
+/* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
+int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
+/* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);
+ * backward dx[b,s] = m·dout[b] / max(Σ m, 1e-9).  x, dx fp32 [B·S, H]. */
+int ttmi_deb_pool_fwd(int B, int S, int H, const float* x, const int64_t* mask, float* out,
+                      hipStream_t stream);
+int ttmi_deb_pool_bwd(int B, int S, int H, const float* dout, const int64_t* mask, float* dx,
+                      hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,8 @@ from . import lib
 from . import ops
 from . import functional
 from . import cnn
+from . import text
+from .text import TextEncoder
 from .user_tower import SequentialUserEncoder
 from .item_tower import MultimodalItemEncoder
 from .two_tower import TwoTowerModel, infonce, infonce_global

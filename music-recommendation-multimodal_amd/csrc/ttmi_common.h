@@ -169,6 +169,12 @@ void ttmi_set_error(const char* fmt, ...);
   } while (0)
 int ttmi_check_launch(const char* what);
 
+// GELU, exact erf form (torch.nn.functional.gelu default; DeBERTa-v2 hidden_act "gelu")
+TTMI_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+TTMI_DEV float gelu_erf_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
 // 8 bf16 <-> 8 floats (one 16-byte chunk)
 TTMI_DEV void unpack8(const uint4& q, float* v) {
   const uint32_t w[4] = {q.x, q.y, q.z, q.w};

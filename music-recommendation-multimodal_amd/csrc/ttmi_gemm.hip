@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       for (int e = 0; e < 4; ++e) {
         v[e] = g.alpha * acc[i][j][e] + bias[e];
         if (g.act == 1) v[e] = fmaxf(v[e], 0.f);
+        if (g.act == 2) v[e] = gelu_erf(v[e]);
       }
       drop_apply_vec<4>(dk, (uint32_t)(drow * g.ld_drop + n), v);
       if (g.gate) {
@@ -260,8 +261,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) gv[e] = (n + e < g.N) ? ld_dyn(g.gate, o + e, g.gate_f32) : 0.f;
         }
+        if (g.act == 3) {                         // GELU backward: gate = pre-activation
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
+          for (int e = 0; e < 4; ++e) v[e] *= gelu_erf_grad(gv[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
+        }
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) cs[e] += (n + e < g.N) ? v[e] : 0.f;
@@ -900,7 +906,7 @@ int panel_epi(const ttmi_gemm_desc* d) {
 bool panel_applies(const ttmi_gemm_desc* d) {
   if (getenv("TTMI_NO_PANEL")) return false;       // tuning runs only
   if (d->dtype != TTMI_BF16 || !d->a_kmajor || !d->b_kmajor || d->c_mode != 0) return false;
-  if (d->colsum || d->split_k > 1 || d->drop_rows || d->M < 2048) return false;
+  if (d->colsum || d->split_k > 1 || d->drop_rows || d->M < 2048 || d->act >= 2) return false;
   if (d->N % 128 || d->N > 512 || d->K % 128 || d->K > 512) return false;
   if (d->N * (2 * d->K + 16) + d->N * 4 > 150 * 1024 || panel_epi(d) < 0) return false;
   if (d->ldc % 8 || !al16(d->C) || !al16(d->A) || !al16(d->B) || d->lda % 8 || d->ldb % 8) return false;
@@ -955,7 +961,8 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   TTMI_REQUIRE(d->ldc >= d->N, "ttmi_gemm: ldc < N");
   TTMI_REQUIRE(d->c_mode == 0 || d->c_mode == 1, "ttmi_gemm: bad c_mode");
   TTMI_REQUIRE(d->c_mode == 0 || d->c_dtype == TTMI_F32, "ttmi_gemm: accumulate needs an f32 C");
-  TTMI_REQUIRE(d->act == 0 || d->act == 1, "ttmi_gemm: bad act");
+  TTMI_REQUIRE(d->act >= 0 && d->act <= 3, "ttmi_gemm: bad act");
+  TTMI_REQUIRE(d->act != 3 || d->gate, "ttmi_gemm: act 3 (GELU backward) needs the pre-activation as gate");
   TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f, "ttmi_gemm: drop_p out of [0,1)");
   TTMI_REQUIRE(d->drop_p == 0.f || d->drop_seed, "ttmi_gemm: dropout needs a seed pointer");
   TTMI_REQUIRE(!d->gate || d->ld_gate >= d->N, "ttmi_gemm: ld_gate < N");

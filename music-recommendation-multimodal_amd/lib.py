@@ -50,6 +50,19 @@ class ConvDesc(ctypes.Structure):
                 ("workspace_bytes", ctypes.c_int64)]
 
 
+class DisAttnDesc(ctypes.Structure):
+    """ttmi_dis_attn_desc (include/ttmi.h)."""
+    _fields_ = [("B", c_i), ("S", c_i), ("nh", c_i), ("d_head", c_i), ("npos", c_i),
+                ("q", c_p), ("k", c_p), ("v", c_p), ("ldqkv", ctypes.c_int64),
+                ("posq", c_p), ("posk", c_p), ("ldpos", ctypes.c_int64),
+                ("mask", c_p), ("delta", c_p), ("inv_scale", ctypes.c_float),
+                ("drop_p", ctypes.c_float), ("drop_seed", c_p),
+                ("ctx", c_p), ("ldctx", ctypes.c_int64), ("lse", c_p),
+                ("dctx", c_p), ("lddctx", ctypes.c_int64),
+                ("dq", c_p), ("dk", c_p), ("dv", c_p), ("lddqkv", ctypes.c_int64),
+                ("lora_u", c_p), ("lora_bq", c_p), ("lora_hu", c_p), ("lora_pb", c_p)]
+
+
 class LnBwdDesc(ctypes.Structure):
     """ttmi_linear_ln_bwd_desc (include/ttmi.h)."""
     _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
@@ -94,6 +107,15 @@ SIGNATURES = {
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
+    "ttmi_deb_embed_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, ctypes.c_float, c_p,
+                                 ctypes.c_float, c_p, c_p, c_p, c_i64, c_p]),
+    "ttmi_deb_ln_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, ctypes.c_float, c_p, c_p, c_i64, c_p,
+                              c_p, c_p]),
+    "ttmi_deb_gelu": (c_i, [c_i64, c_p, c_p, c_p]),
+    "ttmi_dis_attn_fwd": (c_i, [c_p, c_p]),
+    "ttmi_dis_attn_bwd": (c_i, [c_p, c_p]),
+    "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_conv2d": (c_i, [c_p, c_p]),
     "ttmi_conv2d_workspace": (ctypes.c_int64, [c_p]),
     "ttmi_conv_weight_prep": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),

@@ -12,7 +12,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import lib as _L
-from .lib import BF16, F32, ConvDesc, GemmDesc, LnBwdDesc, call
+from .lib import BF16, F32, ConvDesc, DisAttnDesc, GemmDesc, LnBwdDesc, call
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -502,3 +502,96 @@ def colsum(x: Tensor, out: Tensor) -> Tensor:
     M, N = x.shape
     call("ttmi_colsum", code(x.dtype), M, N, _p(x), N, _p(out), _s())
     return out
+
+
+# ----------------------------------------------------------------------------- text encoder
+def deb_embed_fwd(ids: Tensor, table: Tensor, w: Tensor, b: Tensor, eps: float,
+                  mask: Optional[Tensor], y32: Optional[Tensor], y16: Tensor,
+                  drop: Drop = NO_DROP) -> Tensor:
+    """LN(table[ids]) · mask (· dropout) -> y32 fp32 [M,H] and y16 bf16 (row stride)."""
+    M = ids.numel()
+    H = table.shape[1]
+    if y16.shape[0] < M or y16.stride(0) < H or (y32 is not None and y32.numel() < M * H):
+        raise ValueError("deb_embed_fwd: output too small")
+    call("ttmi_deb_embed_fwd", M, H, _p(ids), _p(table), _p(w), _p(b), eps, _p(mask),
+         float(drop[0]), _p(drop[1]), _p(y32), _p(y16), y16.stride(0), _s())
+    return y16
+
+
+def deb_ln_fwd(z: Tensor, w: Tensor, b: Tensor, eps: float, y32: Optional[Tensor],
+               y16: Optional[Tensor], mean: Tensor, rstd: Tensor) -> None:
+    M, H = z.shape
+    call("ttmi_deb_ln_fwd", M, H, _p(z), _p(w), _p(b), eps, _p(y32), _p(y16),
+         y16.stride(0) if y16 is not None else 0, _p(mean), _p(rstd), _s())
+
+
+def deb_gelu(x: Tensor, y: Tensor) -> Tensor:
+    call("ttmi_deb_gelu", x.numel(), _p(x), _p(y), _s())
+    return y
+
+
+def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Tensor,
+             posk: Tensor, mask: Tensor, delta: Tensor, inv_scale: float, ctx: Tensor,
+             lse: Tensor, drop: Drop = NO_DROP, *, dctx: Optional[Tensor] = None,
+             dq: Optional[Tensor] = None, dk: Optional[Tensor] = None,
+             dv: Optional[Tensor] = None, lora_u: Optional[Tensor] = None,
+             lora_bq: Optional[Tensor] = None, lora_hu: Optional[Tensor] = None,
+             lora_pb: Optional[Tensor] = None) -> None:
+    """Disentangled self-attention forward (dctx None) or backward.  q/k/v/ctx/dq/dk/dv are
+    column views (head h at column h·64) sharing a row stride; posq/posk [npos, ·]."""
+    H = nh * 64
+    for name, t in (("q", q), ("k", k), ("v", v), ("ctx", ctx)):
+        if t.shape[0] != B * S or t.shape[1] < H:
+            raise ValueError(f"dis_attn: {name} must be [B·S, >= {H}]")
+    if posq.shape[0] != posk.shape[0] or posq.shape[1] < H or delta.numel() < 2 * S - 1:
+        raise ValueError("dis_attn: bad relative tables")
+    if mask.numel() < B * S or lse.numel() < B * nh * S:
+        raise ValueError("dis_attn: mask / lse too small")
+    d = DisAttnDesc()
+    d.B, d.S, d.nh, d.d_head, d.npos = B, S, nh, 64, posq.shape[0]
+    d.q, d.k, d.v, d.ldqkv = _p(q), _p(k), _p(v), q.stride(0)
+    if k.stride(0) != q.stride(0) or v.stride(0) != q.stride(0):
+        raise ValueError("dis_attn: q, k, v must share a row stride")
+    d.posq, d.posk, d.ldpos = _p(posq), _p(posk), posq.stride(0)
+    if posk.stride(0) != posq.stride(0):
+        raise ValueError("dis_attn: posq/posk must share a row stride")
+    d.mask, d.delta, d.inv_scale = _p(mask), _p(delta), inv_scale
+    d.drop_p, d.drop_seed = float(drop[0]), _p(drop[1])
+    d.ctx, d.ldctx, d.lse = _p(ctx), ctx.stride(0), _p(lse)
+    if dctx is None:
+        call("ttmi_dis_attn_fwd", ctypes.byref(d), _s())
+        return
+    for name, t in (("dq", dq), ("dk", dk), ("dv", dv), ("dctx", dctx)):
+        if t is None or t.shape[0] != B * S or t.shape[1] < H:
+            raise ValueError(f"dis_attn: {name} must be [B·S, >= {H}]")
+    if lora_u is not None:
+        if lora_u.numel() < d.npos * 8 or lora_hu.numel() < B * S * nh * 8 or \
+                lora_pb.numel() < B * nh * d.npos * 8 or lora_bq.numel() < H * 8:
+            raise ValueError("dis_attn: LoRA buffers too small")
+    d.dctx, d.lddctx = _p(dctx), dctx.stride(0)
+    d.dq, d.dk, d.dv, d.lddqkv = _p(dq), _p(dk), _p(dv), dq.stride(0)
+    d.lora_u, d.lora_bq, d.lora_hu, d.lora_pb = _p(lora_u), _p(lora_bq), _p(lora_hu), _p(lora_pb)
+    call("ttmi_dis_attn_bwd", ctypes.byref(d), _s())
+
+
+def deb_pool_fwd(x: Tensor, mask: Tensor, out: Tensor) -> Tensor:
+    B, H = out.shape
+    S = mask.shape[1]
+    call("ttmi_deb_pool_fwd", B, S, H, _p(x), _p(mask), _p(out), _s())
+    return out
+
+
+def deb_pool_bwd(dout: Tensor, mask: Tensor, dx: Tensor) -> Tensor:
+    B, H = dout.shape
+    S = mask.shape[1]
+    call("ttmi_deb_pool_bwd", B, S, H, _p(dout), _p(mask), _p(dx), _s())
+    return dx
+
+
+def dropout_to(x: Tensor, y: Tensor, drop: Drop = NO_DROP) -> Tensor:
+    """y = dropout(x) (fp32 x [M,N] contiguous -> y of any dtype with its own row stride; the
+    mask index is m·N + n, as in every other dropout site)."""
+    M, N = x.shape
+    call("ttmi_dropout_bwd", code(y.dtype), M, N, _p(x), N, float(drop[0]), _p(drop[1]), N,
+         None, _p(y), y.stride(0), None, _s())
+    return y

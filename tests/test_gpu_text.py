@@ -1,0 +1,169 @@
+"""cfg-4 text encoder on the GPU (mDeBERTa-v3 + LoRA, reference item_tower.py:41-83).
+
+* Kernel level: ttmi_dis_attn_fwd/bwd against torch fp32 math on the same bf16 inputs
+  (disentangled attention with log buckets, padding, partial blocks): ctx within 1e-2 of the
+  output's max-abs, dq/dk/dv within 2e-2 (bf16 operands of the backward products), and the
+  LoRA contractions HU / PB (built here from the explicit raw-score gradient) within 2e-2.
+* Module level: TextEncoder loaded with the transformers-generated fixture's parameters
+  (tests/golden/deberta_tiny.npz) — output within 3e-2 of the fixture (bf16 GEMMs through
+  two post-LN layers); LoRA and projection gradients against the fp32 oracle by direction
+  (cosine >= 0.99) and norm (within 5 %)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, sub
+from oracle import deberta_ref as dref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def _cos(a, b):
+    a = torch.as_tensor(a).detach().double().cpu().flatten()
+    b = torch.as_tensor(b).detach().double().cpu().flatten()
+    return torch.dot(a, b).item() / (a.norm().item() * b.norm().item() + 1e-30)
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("B,S,nh,lens", [(2, 64, 1, (64, 30)), (2, 160, 2, (160, 150)),
+                                         (1, 256, 2, (200,))])
+def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
+    ops = gpu_pkg.ops
+    text = gpu_pkg.text
+    cfg = text.TextCfg(hidden=64 * nh, heads=nh)
+    g = torch.Generator().manual_seed(S + nh)
+    H, npos = 64 * nh, cfg.npos
+    q, k, v = (_bf(torch.randn(B, S, H, generator=g)) for _ in range(3))
+    posq, posk = _bf(torch.randn(npos, H, generator=g)), _bf(torch.randn(npos, H, generator=g))
+    mask = torch.zeros(B, S, dtype=torch.int64)
+    for b, L in enumerate(lens):
+        mask[b, :L] = 1
+    dctx = _bf(torch.randn(B, S, H, generator=g))
+    u = torch.randn(npos, 8, generator=g)
+    bq = torch.randn(H, 8, generator=g) * 0.1
+    delta_t = text._Frozen().delta(S, cfg, "cpu").long()
+    dmat = torch.stack([delta_t[i - torch.arange(S) + S - 1] for i in range(S)])   # [S, S]
+    scale = 1.0 / math.sqrt(64 * 3)
+    # torch reference
+    qr, kr, vr = (t.clone().requires_grad_(True) for t in (q, k, v))
+
+    def heads(t):
+        return t.view(B, S, nh, 64).permute(0, 2, 1, 3)
+    Q, K, V = heads(qr), heads(kr), heads(vr)
+    pQ = posq.view(npos, nh, 64).permute(1, 0, 2)
+    pK = posk.view(npos, nh, 64).permute(1, 0, 2)
+    c2c = Q @ K.transpose(-1, -2)
+    c2p = torch.gather(Q @ pK.transpose(-1, -2), -1, dmat.expand(B, nh, S, S))
+    p2c = torch.gather(K @ pQ.transpose(-1, -2), -1, dmat.t().expand(B, nh, S, S)).transpose(-1, -2)
+    raw = c2c + c2p + p2c
+    raw.retain_grad()
+    m2 = (mask[:, None, :] * mask[:, :, None]).bool()[:, None]
+    sc = (raw * scale).masked_fill(~m2, torch.finfo(torch.float32).min)
+    ctx_ref = (torch.softmax(sc, -1) @ V).permute(0, 2, 1, 3).reshape(B, S, H)
+    (ctx_ref * dctx).sum().backward()
+    dS = raw.grad                                                       # [B, nh, S, S]
+    HU_ref = torch.einsum("bhij,ijc->bjhc", dS, u[dmat])
+    KB = torch.einsum("bhjd,hdc->bhjc", K.detach(), bq.view(nh, 64, 8))
+    PB_ref = torch.zeros(B, nh, npos, 8)
+    contrib = torch.einsum("bhij,bhjc->bhijc", dS, KB).reshape(B, nh, S * S, 8)
+    PB_ref.index_add_(2, dmat.reshape(-1), contrib)
+    # GPU
+    qkv = torch.cat([q, k, v], dim=2).reshape(B * S, 3 * H).to(torch.bfloat16).to(DEV)
+    pos = torch.cat([posq, posk], dim=1).to(torch.bfloat16).to(DEV)
+    md, dd = mask.to(DEV), delta_t.to(torch.int16).to(DEV)
+    ctx = torch.empty(B * S, H, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * nh * S, device=DEV)
+    ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:], md,
+                 dd, scale, ctx, lse)
+    torch.cuda.synchronize()
+    valid = mask.reshape(-1).bool()
+    cg = ctx.float().cpu().view(B * S, H)
+    cr = ctx_ref.detach().reshape(B * S, H)
+    assert rel(cg[valid], cr[valid]) < 1e-2, rel(cg[valid], cr[valid])
+    assert rel(cg, cr) < 1e-2                      # pad rows: uniform attention, as torch
+    dqkv = torch.zeros(B * S, 3 * H, device=DEV, dtype=torch.bfloat16)
+    hu = torch.zeros(B * S * nh * 8, device=DEV)
+    pb = torch.zeros(B * nh * npos * 8, device=DEV)
+    ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:], md,
+                 dd, scale, ctx, lse, dctx=dctx.reshape(B * S, H).to(torch.bfloat16).to(DEV),
+                 dq=dqkv[:, :H], dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:], lora_u=u.to(DEV),
+                 lora_bq=bq.to(DEV), lora_hu=hu, lora_pb=pb)
+    torch.cuda.synchronize()
+    dg = dqkv.float().cpu()
+    for name, got, want in (("dq", dg[:, :H], qr.grad), ("dk", dg[:, H:2 * H], kr.grad),
+                            ("dv", dg[:, 2 * H:], vr.grad)):
+        want = want.reshape(B * S, H)
+        assert rel(got, want) < 2e-2, (name, rel(got, want))
+    assert rel(hu.cpu().view(B, S, nh, 8), HU_ref) < 2e-2, rel(hu.cpu().view(B, S, nh, 8), HU_ref)
+    assert rel(pb.cpu().view(B, nh, npos, 8), PB_ref) < 2e-2
+
+
+def test_text_encoder_vs_transformers_fixture(gpu_pkg):
+    text = gpu_pkg.text
+    z = load_golden("deberta_tiny.npz")
+    H, NH, NL, I, V, R, ALPHA, B, S, OUT = z["cfg"].tolist()
+    cfg = text.TextCfg(vocab_size=V, hidden=H, layers=NL, heads=NH, intermediate=I, lora_r=R,
+                       lora_alpha=ALPHA, lora_dropout=0.0, hidden_dropout=0.0, attn_dropout=0.0)
+    enc = text.TextEncoder(embedding_dim=OUT, cfg=cfg).to(DEV)
+    enc.projection[2].p = 0.0
+    P = {k: torch.tensor(v) for k, v in sub(z, "p/").items()}
+    enc.load_state_dict(P)
+    enc.train()
+    ids, mask = torch.tensor(z["input_ids"]), torch.tensor(z["attention_mask"])
+    up = torch.tensor(z["upstream"])
+    out = enc(ids.to(DEV), mask.to(DEV))
+    (out * up.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel(out, z["out"]) < 3e-2, rel(out, z["out"])
+    # fp32 oracle gradients of the trainable tensors
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    dcfg = dref.DebertaCfg(vocab_size=V, hidden=H, layers=NL, heads=NH, intermediate=I, lora_r=R,
+                           lora_alpha=ALPHA)
+    ref_out = dref.text_encoder_forward(Pr, ids, mask, dcfg)
+    (ref_out * up).sum().backward()
+    n_checked = 0
+    for name, p in enc.named_parameters():
+        if not p.requires_grad:
+            assert p.grad is None, name
+            continue
+        gr = Pr[name].grad
+        assert _cos(p.grad, gr) > 0.99, (name, _cos(p.grad, gr))
+        assert abs(p.grad.norm().item() / gr.norm().item() - 1) < 0.05, name
+        n_checked += 1
+    assert n_checked == 4 * NL + 4
+
+
+def test_text_encoder_eval_and_shapes(gpu_pkg):
+    """Eval mode (no dropout, no autograd state) equals the train-mode forward with dropout off;
+    padded tokens do not influence the pooled output."""
+    text = gpu_pkg.text
+    cfg = text.TextCfg(vocab_size=300, hidden=128, layers=2, heads=2, intermediate=256,
+                       lora_dropout=0.0, hidden_dropout=0.0, attn_dropout=0.0)
+    torch.manual_seed(0)
+    enc = text.TextEncoder(embedding_dim=16, cfg=cfg).to(DEV)
+    enc.projection[2].p = 0.0
+    ids = torch.randint(1, 300, (3, 96), device=DEV)
+    mask = torch.ones(3, 96, dtype=torch.int64, device=DEV)
+    mask[1, 50:] = 0
+    enc.eval()
+    with torch.no_grad():
+        a = enc(ids, mask)
+        ids2 = ids.clone()
+        ids2[1, 50:] = 7                       # change only padded tokens of row 1
+        b = enc(ids2, mask)
+    enc.train()
+    c = enc(ids, mask)
+    assert torch.allclose(a, c, atol=1e-5)
+    assert torch.allclose(a[1], b[1], atol=1e-5)
