@@ -11,7 +11,9 @@ Multi-GPU: one process per GPU (torchrun), per-GPU batch fixed (weak scaling), g
 averaged with RCCL all-reduce; value = pairs of all ranks / max-over-ranks time.
 
 ``--config 3`` measures BASELINE configs[2] instead (full item tower on raw 128x256 mels,
-224x224 covers and tabular features, B=256; its roofline is the implicit-GEMM conv).
+224x224 covers and tabular features, B=256; its roofline is the implicit-GEMM conv);
+``--config 4`` adds the mDeBERTa-v3-base + LoRA lyrics encoder (configs[3], S=256; its
+roofline is the text encoder's token GEMMs).
 
 Extra fields: "roofline" for the dominant kernel (timed live with HIP events on the launch
 stream) and "cpu_baseline" (the fp32 CPU oracle timed on this host, rank 0 at N=1).
@@ -72,6 +74,25 @@ def add_raw_items(batches, seed: int, device):
         b["target_audio"] = torch.randn(B, 1, *MEL, generator=g).to(device)
         b["target_image"] = torch.randn(B, 3, *COVER, generator=g).to(device)
         b["target_tabular"] = torch.randn(B, TAB, generator=g).to(device)
+    return batches
+
+
+TEXT_S, TEXT_V = 256, 251000
+# mDeBERTa-v3-base fwd 50.7 GF + dX-only bwd 53.2 GF per sample, + 14.5 GF per
+# batch for the relative-table projections
+TEXT_FLOPS_PER_SAMPLE, TEXT_FLOPS_PER_BATCH = 103.9e9, 14.5e9
+
+
+def add_text(batches, seed: int, device):
+    """cfg 4 lyrics: tokens ~U[1, 251000), lengths ~U[16, 256], prefix mask."""
+    g = torch.Generator().manual_seed(seed + 11)
+    for b in batches:
+        B = b["history_ids"].shape[0]
+        lengths = torch.randint(16, TEXT_S + 1, (B,), generator=g)
+        mask = (torch.arange(TEXT_S)[None] < lengths[:, None]).long()
+        ids = torch.randint(1, TEXT_V, (B, TEXT_S), generator=g) * mask
+        b["target_input_ids"] = ids.to(device)
+        b["target_attention_mask"] = mask.to(device)
     return batches
 
 
@@ -185,6 +206,83 @@ def probe_conv(step, batch, device, iters: int = 3):
             "launches_per_step": len(calls), "flops_per_launch": round(fl)}
 
 
+def probe_text_gemm(step, batch, device, iters: int = 3):
+    """cfg 4 roofline of the dominant kernel family, the text encoder's GEMMs (gemm_kernel:
+    QKV / out-proj / FFN forward and their input-gradient GEMMs).  As probe_dominant: one eager
+    forward + backward records the bf16 GEMMs with M >= 4096 rows (the token-parallel ones),
+    which are replayed between HIP events on the launch stream.  Algorithmic FLOPs per launch:
+    2·M·N·K."""
+    ops = pkg.ops
+    calls = []
+    orig = ops.gemm
+
+    def rec(A, B_, C, M, N, K, **kw):
+        if A.dtype == torch.bfloat16 and M >= 4096 and N >= 512 and K >= 512:
+            calls.append((A, B_, C, M, N, K, dict(kw)))
+        return orig(A, B_, C, M, N, K, **kw)
+
+    ops.gemm = rec
+    try:
+        step._fwd_bwd(step._stage(batch))
+    finally:
+        ops.gemm = orig
+    torch.cuda.synchronize(device)
+    for c in calls:
+        orig(*c[:6], **c[6])
+    st = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        for c in calls:
+            orig(*c[:6], **c[6])
+    e1.record(st)
+    torch.cuda.synchronize(device)
+    n = max(len(calls), 1)
+    sec = e0.elapsed_time(e1) / 1e3 / (iters * n)
+    fl = sum(2.0 * M * N * K for (_, _, _, M, N, K, _) in calls) / n
+    tf = fl / sec / 1e12
+    return {"kernel": "gemm_kernel (text-encoder token GEMMs: QKV+LoRA, out-proj, FFN, and their "
+                      "input-gradient GEMMs; per-step launch mix)",
+            "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "traffic": read_traffic("gemm_kernel"), "avg_us": round(sec * 1e6, 2),
+            "launches_per_step": len(calls), "flops_per_launch": round(fl)}
+
+
+def cpu_baseline_cfg4(B: int, budget_s: float = 20.0):
+    """fp32 CPU oracle cfg-4 train step: cfg 3 + the mDeBERTa-v3-base + LoRA oracle."""
+    from oracle import two_tower_ref as ref
+    from oracle import resnet_ref as rref
+    from oracle import deberta_ref as dref
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(0)
+    dcfg = dref.DebertaCfg()
+    text = dref.init_text_params(dcfg, 128, g, lora_b_std=0.02)
+    params = {k: v for k, v in text.items() if "lora_" in k or k.startswith("projection.")}
+    frozen = {k: v for k, v in text.items() if k not in params}
+    ids, mask = dref.synthetic_text(B, TEXT_S, TEXT_V, generator=g)
+    x = {"ids": ids, "mask": mask}
+    out_w = torch.randn(128, generator=g)
+    t0 = time.perf_counter()
+    n = 0
+    while True:                            # text encoder fwd + dX/LoRA bwd dominates cfg 4
+        leaves = {k: v.detach().requires_grad_(True) for k, v in params.items()}
+        out = dref.text_encoder_forward({**frozen, **leaves}, x["ids"], x["mask"], dcfg)
+        (out * out_w).sum().backward()
+        n += 1
+        el = time.perf_counter() - t0
+        if el + el / n >= budget_s or n >= 10:
+            break
+    per_pair_text = el / (n * B)
+    c3 = cpu_baseline_cfg3(8, budget_s)
+    per_pair_c3 = 1.0 / c3["value"]
+    value = 1.0 / (per_pair_text + per_pair_c3)
+    return {"value": round(value, 4), "unit": "user-item pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} mDeBERTa-v3-base + LoRA fwd+bwd steps at B={B}, S={TEXT_S} "
+                      f"({el:.1f} s) combined with the cfg-3 oracle step rate "
+                      f"({c3['value']} pairs/s, {c3['sample']}); fp32 torch-CPU oracle"}
+
+
 def read_traffic(name: str):
     """Per-launch HBM bytes of `name` from the committed rocprofv3 PMC summary
     (profiles/*traffic*.json, written by tools/traffic.py), or None."""
@@ -269,9 +367,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU pairs (default: 512 for cfg 2, 256 for cfg 3)")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
                     help="2 = BASELINE cfg 2 (the metric's configuration); 3 = full item "
-                         "tower on raw mels/covers/tabular (BASELINE configs[2])")
+                         "tower on raw mels/covers/tabular (BASELINE configs[2]); 4 = cfg 3 + "
+                         "mDeBERTa-LoRA lyrics, S=256 (BASELINE configs[3])")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -284,7 +383,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     device = torch.device("cuda", local)
-    cfg3 = args.config == 3
+    cfg4 = args.config == 4
+    cfg3 = args.config == 3 or cfg4                      # cfg 4 = cfg 3 + text
     B = args.batch or (256 if cfg3 else 512)
 
     torch.manual_seed(1234 + rank)
@@ -292,7 +392,7 @@ def main():
                               num_countries=N_COUNTRIES, max_seq_len=L, user_embedding_dim=D,
                               item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
                               compute_dtype=torch.bfloat16,
-                              precomputed_modalities=not cfg3).to(device)
+                              precomputed_modalities=not cfg3, with_text=cfg4).to(device)
     if world > 1:   # identical replicas, as DDP broadcasts from rank 0
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, 0)
@@ -300,6 +400,8 @@ def main():
     batches = synthetic_batches(2 if cfg3 else 4, B, seed=rank, device=device)
     if cfg3:
         batches = add_raw_items(batches, rank, device)
+    if cfg4:
+        batches = add_text(batches, rank, device)
 
     # warm-up runs the exact timed-loop ops (incl. the loss accumulation: torch loads its
     # kernels lazily, and a first-use load inside the timed region costs ~75 ms)
@@ -327,22 +429,36 @@ def main():
 
     roof = None
     if rank == 0:
-        roof = probe_conv(step, batches[0], device) if cfg3 else \
-            probe_dominant(step, batches[0], device)
+        if cfg4:
+            roof = probe_text_gemm(step, batches[0], device)
+        elif cfg3:
+            roof = probe_conv(step, batches[0], device)
+        else:
+            roof = probe_dominant(step, batches[0], device)
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu:
-        cpu = cpu_baseline_cfg3(8, args.cpu_budget) if cfg3 else cpu_baseline(B, args.cpu_budget)
+        if cfg4:
+            cpu = cpu_baseline_cfg4(2, args.cpu_budget)
+        elif cfg3:
+            cpu = cpu_baseline_cfg3(8, args.cpu_budget)
+        else:
+            cpu = cpu_baseline(B, args.cpu_budget)
 
     if rank == 0:
         pairs = world * B * args.steps
         value = pairs / el
         ms = el / max(args.steps, 1) * 1e3
-        flops = step_flops(B) + (RESNET_FLOPS_PER_SAMPLE * B if cfg3 else 0.0)
+        flops = step_flops(B) + (RESNET_FLOPS_PER_SAMPLE * B if cfg3 else 0.0) + \
+            ((TEXT_FLOPS_PER_SAMPLE * B + TEXT_FLOPS_PER_BATCH) if cfg4 else 0.0)
         step_tf = flops * args.steps / el / 1e12 * world
         workload = ("cfg2: SASRec L=50 D=128 H=4 x2 layers + late-fusion head on "
                     "precomputed 512-d modality embeddings + in-batch InfoNCE; "
                     "fwd+bwd+AdamW, dropout 0.1")
-        if cfg3:
+        if cfg4:
+            workload = ("cfg4: cfg3 item tower + mDeBERTa-v3-base (12 layers, H=768, random init) "
+                        "with LoRA r=8 on query/value, lyrics S=256 (lengths U[16,256]); "
+                        "fwd+bwd+AdamW, dropout 0.1; 1 GPU (BASELINE quotes DDP x8)")
+        elif cfg3:
             workload = ("cfg3: SASRec L=50 D=128 H=4 x2 layers + item tower on raw inputs "
                         "(ResNet-18 on 1x128x256 mels, ResNet-18 on 3x224x224 covers, tabular "
                         "MLP T=128, zero text slot) + late-fusion head + in-batch InfoNCE; "
@@ -363,7 +479,9 @@ def main():
                           "flops_per_step_per_gpu": flops,
                           "flops": "F_min (pruned last layer, SURVEY 8d)" +
                                    (" + ResNet-18 fwd+bwd 17.4 GF/pair (SURVEY a7/a8)"
-                                    if cfg3 else "")},
+                                    if cfg3 else "") +
+                                   (" + mDeBERTa-LoRA 103.9 GF/pair + 14.5 GF/batch (SURVEY a9)"
+                                    if cfg4 else "")},
             "cpu_baseline": cpu,
             "mean_loss": round(mean_loss, 5),
         }

@@ -704,8 +704,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
   if (kbeg >= g.R) return;
   const int rows = (int)min(g.R - kbeg, g.rows_per_split);
   const int nst = (rows + 63) >> 6;
-  const i32x4_t ra = make_rsrc(g.A + kbeg * g.lda * 2, (uint32_t)(rows * g.lda * 2));
-  const i32x4_t rb = make_rsrc(g.B + kbeg * g.ldb * 2, (uint32_t)(rows * g.ldb * 2));
+  // the descriptor ends at the last valid element ((rows-1)·ld + extent): a column view of a
+  // wider buffer (ld > extent) must not read past its allocation in the last row
+  const i32x4_t ra = make_rsrc(g.A + kbeg * g.lda * 2, (uint32_t)(((int64_t)(rows - 1) * g.lda + g.M) * 2));
+  const i32x4_t rb = make_rsrc(g.B + kbeg * g.ldb * 2, (uint32_t)(((int64_t)(rows - 1) * g.ldb + g.N) * 2));
   const uint32_t ring_lds = lds_addr(ring);
 
   f32x4_t acc[TM][TN];

@@ -13,9 +13,10 @@ Two input modes:
   reference's names — ``audio_encoder`` (ResNet-18 on [B,1,H,W] mels, item_tower.py:9-25),
   ``visual_encoder`` (ResNet-18 on [B,3,224,224] covers, :27-39; random init, ImageNet
   weights are a download), ``tabular_encoder`` (:85-98) — all on the libttmi conv/BN/pool
-  kernels (cnn.py).  The mDeBERTa-LoRA text encoder (:41-83, cfg 4) is not built: the text
-  slot of the concatenation is a zero 128-d vector, or ``input_ids`` itself when it is a
-  floating-point [B, text_dim] precomputed text embedding.
+  kernels (cnn.py).  With ``with_text=True`` (cfg 4) it also builds ``text_encoder``, the
+  mDeBERTa-v3 + LoRA lyrics encoder (:41-83, text.py) fed ``input_ids``/``attention_mask``;
+  without it (cfg 3, no text branch) the text slot is a zero 128-d vector, or ``input_ids``
+  itself when it is a floating-point [B, text_dim] precomputed text embedding.
 """
 from __future__ import annotations
 
@@ -26,6 +27,7 @@ import torch.nn as nn
 
 from . import cnn
 from . import functional as F
+from .text import TextCfg, TextEncoder
 from .user_tower import make_operands, new_dropout_seeds
 
 Tensor = torch.Tensor
@@ -59,13 +61,19 @@ class MultimodalItemEncoder(nn.Module):
     def __init__(self, tabular_input_dim: int, embedding_dim: int = 256, audio_dim: int = 128,
                  visual_dim: int = 128, text_model_name: str = "microsoft/mdeberta-v3-base",
                  text_dim: int = 128, tabular_dim: int = 128, use_lora: bool = True, *,
-                 precomputed_modalities: bool = True,
+                 precomputed_modalities: bool = True, with_text: bool = False,
+                 text_cfg: Optional[TextCfg] = None,
                  compute_dtype: torch.dtype = torch.bfloat16):
         super().__init__()
         self.precomputed_modalities = precomputed_modalities
+        self.with_text = with_text and not precomputed_modalities
         if not precomputed_modalities:
             self.audio_encoder = cnn.AudioEncoder(embedding_dim=audio_dim)
             self.visual_encoder = cnn.VisualEncoder(embedding_dim=visual_dim)
+            if self.with_text:                                  # cfg 4
+                self.text_encoder = TextEncoder(model_name=text_model_name,
+                                                embedding_dim=text_dim, use_lora=use_lora,
+                                                cfg=text_cfg)
             self.tabular_encoder = cnn.TabularEncoder(input_dim=tabular_input_dim,
                                                       embedding_dim=tabular_dim)
         self.embedding_dim = embedding_dim
@@ -125,7 +133,10 @@ class MultimodalItemEncoder(nn.Module):
             seeds = new_dropout_seeds(audio.device)
         audio_emb = self.audio_encoder(audio)
         visual_emb = self.visual_encoder(images)
-        text_emb = self.text_slot(input_ids, audio.shape[0], audio.device)
+        if self.with_text:
+            text_emb = self.text_encoder(input_ids, attention_mask)
+        else:
+            text_emb = self.text_slot(input_ids, audio.shape[0], audio.device)
         tabular_emb = self.tabular_encoder(tabular, seeds)
         combined = torch.cat([audio_emb, visual_emb, text_emb, tabular_emb], dim=1)
         return self.fuse(combined, seeds)

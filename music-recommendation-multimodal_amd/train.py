@@ -24,6 +24,7 @@ import torch.distributed as dist
 
 from . import cnn
 from . import functional as F
+from . import text as T
 from . import ops
 from .two_tower import TwoTowerModel
 from .user_tower import _gemm_names, add_transposes, refresh_transposes
@@ -83,7 +84,9 @@ class FlatParams:
 
     def __init__(self, module: torch.nn.Module, mirror_dtype: Optional[torch.dtype] = None):
         self.names, self.shapes, self.offsets = [], [], []
-        params = list(module.named_parameters())
+        # trainable parameters only: frozen ones (the peft-frozen DeBERTa base) get neither
+        # gradients nor AdamW updates (torch's AdamW skips params whose grad is None)
+        params = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         dev = params[0][1].device
         off = 0
         for n, p in params:
@@ -148,7 +151,8 @@ class TrainStep:
     forward+backward(+update) graph and returns the device loss tensor (no host sync)."""
 
     INPUT_KEYS = ("history_ids", "history_mask", "user_gender", "user_country", "user_idx",
-                  "target_modal", "target_audio", "target_image", "target_tabular")
+                  "target_modal", "target_audio", "target_image", "target_tabular",
+                  "target_input_ids", "target_attention_mask")
     RAW_ENCODERS = (("audio_encoder.backbone.", 1), ("visual_encoder.backbone.", 3))
 
     def __init__(self, model: TwoTowerModel, lr: float = 1e-4, betas=(0.9, 0.999),
@@ -198,6 +202,11 @@ class TrainStep:
                         for pre, c in self.RAW_ENCODERS]
             pre = "tabular_encoder."
             self.tab = (sub(self.Pi, pre), sub(self.Gi, pre), sub(self.bufs, pre))
+            self.text = None
+            if it.with_text:                                   # cfg 4: LoRA + projection
+                pre = "text_encoder."
+                self.text = (it.text_encoder, sub(self.Pi, pre), sub(self.Gi, pre))
+                self.text_seeds = torch.zeros(T.N_TEXT_SITES, dtype=torch.int64, device=dev)
         self.sync_mirror()
         self.use_graph = use_graph
         self.static: Optional[Dict[str, Tensor]] = None
@@ -253,16 +262,29 @@ class TrainStep:
         B = outs[0].shape[0]
         P, _, bufs = self.tab
         t, tst = cnn.tabular_fwd(P, b["target_tabular"], bufs, seeds, self.p_tab)
-        text = torch.zeros(B, self.text_dim, device=t.device)
-        return torch.cat([outs[0], outs[1], text, t], dim=1), (saved, tst)
+        xst = ts = None
+        if self.text is not None:
+            enc, TP, _ = self.text
+            ts = None
+            if seeds is not None:
+                ops.dropout_seeds(self.base_seed ^ 0x7E47, self.step_t, self.text_seeds)
+                ts = self.text_seeds
+            text, xst = T.text_fwd(enc, TP, b["target_input_ids"], b["target_attention_mask"],
+                                   ts, True)
+        else:
+            text = torch.zeros(B, self.text_dim, device=t.device)
+        return torch.cat([outs[0], outs[1], text, t], dim=1), (saved, tst, xst, ts)
 
     def _raw_items_bwd(self, rst, dmodal: Tensor) -> None:
-        saved, tst = rst
+        saved, tst, xst, ts = rst
         o = 0
         for (P, G, _, c), st in zip(self.enc, saved):
             n = G["fc.bias"].numel()
             cnn.resnet18_bwd(P, st, dmodal[:, o:o + n], G, c)
             o += n
+        if xst is not None:
+            enc, TP, TG = self.text
+            T.text_bwd(enc, TP, xst, dmodal[:, o:o + self.text_dim], TG, ts)
         o += self.text_dim
         P, G, _ = self.tab
         cnn.tabular_bwd(P, tst, dmodal[:, o:], G)

@@ -95,8 +95,8 @@ class TwoTowerModel(nn.Module):
                  text_model_name: str = "microsoft/mdeberta-v3-base", text_dim: int = 128,
                  tabular_dim: int = 128, use_lora: bool = True, temperature: float = 0.07, *,
                  compute_dtype: torch.dtype = torch.bfloat16,
-                 precomputed_modalities: bool = True, global_negatives: bool = False,
-                 process_group=None):
+                 precomputed_modalities: bool = True, with_text: bool = False,
+                 text_cfg=None, global_negatives: bool = False, process_group=None):
         super().__init__()
         self.global_negatives = global_negatives   # cfg 5: negatives from every rank's batch
         self.process_group = process_group
@@ -111,7 +111,8 @@ class TwoTowerModel(nn.Module):
             tabular_input_dim=tabular_input_dim, embedding_dim=item_embedding_dim,
             audio_dim=audio_dim, visual_dim=visual_dim, text_model_name=text_model_name,
             text_dim=text_dim, tabular_dim=tabular_dim, use_lora=use_lora,
-            precomputed_modalities=precomputed_modalities, compute_dtype=compute_dtype)
+            precomputed_modalities=precomputed_modalities, with_text=with_text,
+            text_cfg=text_cfg, compute_dtype=compute_dtype)
 
     def _item(self, batch: Dict[str, Tensor], seeds: Optional[Tensor] = None) -> Tensor:
         if "target_modal" in batch:

@@ -167,3 +167,74 @@ def test_text_encoder_eval_and_shapes(gpu_pkg):
     c = enc(ids, mask)
     assert torch.allclose(a, c, atol=1e-5)
     assert torch.allclose(a[1], b[1], atol=1e-5)
+
+
+def _cfg4(pkg, B=8, S=96, seed=0, p=0.0):
+    from oracle import resnet_ref as rref
+    from oracle import two_tower_ref as ref
+    text = pkg.text
+    tcfg = text.TextCfg(vocab_size=400, hidden=128, layers=2, heads=2, intermediate=256,
+                        lora_dropout=p, hidden_dropout=p, attn_dropout=p)
+    torch.manual_seed(seed)
+    m = pkg.TwoTowerModel(vocab_size=211, tabular_input_dim=32, num_genders=3, num_countries=8,
+                          max_seq_len=12, user_embedding_dim=128, item_embedding_dim=128,
+                          user_dropout=p, precomputed_modalities=False, with_text=True,
+                          text_cfg=tcfg).to(DEV)
+    m.item_tower.fusion_layer[3].p = p
+    m.item_tower.tabular_encoder.mlp[3].p = p
+    m.item_tower.text_encoder.projection[2].p = p
+    with torch.no_grad():                         # non-zero LoRA B so every path is live
+        for n, prm in m.named_parameters():
+            if "lora_B" in n:
+                prm.normal_(0.0, 0.02)
+    g = torch.Generator().manual_seed(seed + 1)
+    batch = ref.synthetic_batch(B, 12, 211, num_countries=8, generator=g)
+    del batch["target_modal"]
+    batch.update(rref.synthetic_items(B, 32, (64, 96), (64, 64), generator=g))
+    ids, mask = dref.synthetic_text(B, S, 400, generator=g)
+    batch["target_input_ids"], batch["target_attention_mask"] = ids, mask
+    return m, {k: v.to(DEV) for k, v in batch.items()}
+
+
+def test_cfg4_train_step_graph_equals_eager_and_learns(gpu_pkg):
+    """cfg 4 (ResNet-18 x2 + mDeBERTa-LoRA + tabular): TrainStep graph replay follows the
+    eager schedule, the loss falls, and the frozen DeBERTa base never changes."""
+    m1, bd = _cfg4(gpu_pkg, seed=3, p=0.1)
+    m2, _ = _cfg4(gpu_pkg, seed=3, p=0.1)
+    frozen0 = {n: p.detach().clone() for n, p in m1.named_parameters() if not p.requires_grad}
+    lora0 = {n: p.detach().clone() for n, p in m1.named_parameters() if "lora_" in n}
+    assert frozen0 and all("text_encoder.transformer" in n and "lora_" not in n for n in frozen0)
+    s1 = gpu_pkg.TrainStep(m1, lr=1e-3, use_graph=True, seed=5)
+    s2 = gpu_pkg.TrainStep(m2, lr=1e-3, use_graph=False, seed=5)
+    l1 = [float(s1.step(bd)) for _ in range(10)]
+    l2 = [float(s2.step(bd)) for _ in range(10)]
+    assert abs(l1[0] - l2[0]) < 5e-3, (l1[0], l2[0])
+    assert abs(l1[1] - l2[1]) < 2e-2, (l1[:3], l2[:3])
+    assert l1[-1] < l1[0] - 0.2, l1
+    for n, p in m1.named_parameters():
+        if n in frozen0:
+            assert torch.equal(p.detach(), frozen0[n]), n
+    names = dict(m1.named_parameters())
+    assert len(lora0) == 4 * 2
+    for n, v0 in lora0.items():                  # the LoRA matrices train
+        assert not torch.equal(names[n].detach(), v0), n
+
+
+def test_cfg4_module_text_slot_is_text_encoder(gpu_pkg):
+    """The module path concatenates the TextEncoder output into the text slot (item_tower.py:147)."""
+    m, bd = _cfg4(gpu_pkg, seed=4)
+    it = m.item_tower
+    it.eval()
+    with torch.no_grad():
+        t = it.text_encoder(bd["target_input_ids"], bd["target_attention_mask"])
+        full = it(images=bd["target_image"], audio=bd["target_audio"],
+                  input_ids=bd["target_input_ids"], attention_mask=bd["target_attention_mask"],
+                  tabular=bd["target_tabular"])
+        zero_text = it.fuse(torch.cat([it.audio_encoder(bd["target_audio"]),
+                                       it.visual_encoder(bd["target_image"]),
+                                       torch.zeros_like(t), it.tabular_encoder(bd["target_tabular"])], 1))
+        with_text = it.fuse(torch.cat([it.audio_encoder(bd["target_audio"]),
+                                       it.visual_encoder(bd["target_image"]), t,
+                                       it.tabular_encoder(bd["target_tabular"])], 1))
+    assert torch.allclose(full, with_text, atol=1e-4)
+    assert not torch.allclose(full, zero_text, atol=1e-4)
