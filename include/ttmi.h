@@ -416,6 +416,7 @@ typedef struct ttmi_dis_attn_desc {
   const void* dctx; int64_t lddctx;
   void* dq; void* dk; void* dv; int64_t lddqkv;
   const float* lora_u; const float* lora_bq; float* lora_hu; float* lora_pb;
+  float* dq_scratch;      /* backward: fp32 [B·S, nh·64] workspace (dQ accumulation) */
 } ttmi_dis_attn_desc;
 int ttmi_dis_attn_fwd(const ttmi_dis_attn_desc* d, hipStream_t stream);
 int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t stream);

@@ -69,24 +69,32 @@ TTMI_DEV uint4 freg(const f32x4_t& lo, const f32x4_t& hi) {
   return make_uint4(pk2(lo[0], lo[1]), pk2(lo[2], lo[3]), pk2(hi[0], hi[1]), pk2(hi[2], hi[3]));
 }
 
-// rows [r0, r0 + 64) x 64 bf16 of src (row stride ld elements) -> LDS tile; rows >= nrows zero
-TTMI_DEV void load_tile(char* dst, const bf16_t* src, int64_t ld, int r0, int nrows, int tid) {
+// rows [r0, r0 + R) x 64 bf16 of src (row stride ld elements) -> LDS tile; rows >= nrows zero.
+// Loads are unconditional from a clamped row (then zeroed by a select): a guarded load would
+// compile to a branch + vmcnt(0) and serialise the whole group.
+template <int R>
+TTMI_DEV void load_rows(char* dst, const bf16_t* src, int64_t ld, int r0, int nrows, int tid) {
+  constexpr int C = R * 8 / 256;
+  uint4 v[C];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < C; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + r < nrows) v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + r) * ld + ch * 8);
-    *reinterpret_cast<uint4*>(dst + r * TP + ch * 16) = v;
+    const int rr = min(r0 + r, nrows - 1);
+    v[c] = *reinterpret_cast<const uint4*>(src + (int64_t)rr * ld + ch * 8);
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
+    const bool ok = r0 + r < nrows;
+    const uint4 z = make_uint4(ok ? v[c].x : 0u, ok ? v[c].y : 0u, ok ? v[c].z : 0u, ok ? v[c].w : 0u);
+    *reinterpret_cast<uint4*>(dst + r * TP + ch * 16) = z;
   }
 }
+TTMI_DEV void load_tile(char* dst, const bf16_t* src, int64_t ld, int r0, int nrows, int tid) {
+  load_rows<64>(dst, src, ld, r0, nrows, tid);
+}
 TTMI_DEV void load_win(char* dst, const bf16_t* src, int64_t ld, int r0, int nrows, int tid) {
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + r < nrows) v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + r) * ld + ch * 8);
-    *reinterpret_cast<uint4*>(dst + r * TP + ch * 16) = v;
-  }
+  load_rows<WIN>(dst, src, ld, r0, nrows, tid);
 }
 
 struct DisArgs {
@@ -106,6 +114,7 @@ struct DisArgs {
   const float* bq;                  // [nh·64, 8] LoRA B of query_proj
   float* hu;                        // [B·S, nh, 8]
   float* pb;                        // [B·nh, npos, 8]
+  float* dq32;                      // [B·S, nh·64] fp32 scratch (dQ accumulation)
 };
 
 // Scores of a 64x64 block pair for wave w's 16 query rows (fwd and bwd share this):
@@ -275,7 +284,6 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) float sKB[64 * 8];
   __shared__ float sHU[64 * 8];
   __shared__ __attribute__((aligned(16))) float sUw[WIN * 8];
-  __shared__ float sPB[512 * 8];
   const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
   const int S = a.S, nqb = (S + 63) / 64;
@@ -283,7 +291,9 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
   const DropKeys dk = resolve_drop(a.drop);
   const int64_t rowb = (int64_t)b * S;
   for (int r = tid; r < 2 * S - 1; r += 256) sDelta[r] = a.delta[r];
-  for (int r = tid; r < 512 * 8; r += 256) sPB[r] = 0.f;
+  float* pbw = lora ? a.pb + ((int64_t)b * a.nh + h) * a.npos * 8 : nullptr;   // owned slice
+  if (lora)
+    for (int r = tid; r < a.npos * 8; r += 256) pbw[r] = 0.f;
   // per-row D_i = dO_i · O_i, lse, mask
   for (int r = tid; r < S; r += 256) {
     const bf16_t* o = a.ctx + (rowb + r) * a.ldctx + h * DH;
@@ -301,11 +311,6 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
     sLse[r] = a.lse[((int64_t)b * a.nh + h) * S + r];
     sMq[r] = a.mask[rowb + r] != 0 ? 1.f : 0.f;
   }
-  f32x4_t dq[4][4];
-#pragma unroll
-  for (int qq = 0; qq < 4; ++qq)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) dq[qq][u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
   for (int j0 = 0; j0 < S; j0 += 64) {
@@ -333,9 +338,8 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
     f32x4_t dkacc[4], dvacc[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) dkacc[u] = dvacc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      if (qq >= nqb) break;
+#pragma unroll 1
+    for (int qq = 0; qq < nqb; ++qq) {
       const int i0 = qq * 64;
       const int dlo = block_dlo(sDelta, i0, j0, S);
       __syncthreads();
@@ -343,11 +347,19 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
       load_tile(sdO, a.dctx + rowb * a.lddctx + h * DH, a.lddctx, i0, S, tid);
       load_win(sPK, a.posk + h * DH, a.ldpos, dlo, a.npos, tid);
       load_win(sPQ, a.posq + h * DH, a.ldpos, dlo, a.npos, tid);
-      if (lora)
-        for (int r = tid; r < WIN * 8; r += 256) {
-          const int row = dlo + (r >> 3);
-          sUw[r] = row < a.npos ? a.u[(int64_t)row * 8 + (r & 7)] : 0.f;
+      if (lora) {
+        float uv[WIN * 8 / 256];
+#pragma unroll
+        for (int c = 0; c < WIN * 8 / 256; ++c) {
+          const int r = tid + 256 * c;
+          uv[c] = a.u[(int64_t)min(dlo + (r >> 3), a.npos - 1) * 8 + (r & 7)];
         }
+#pragma unroll
+        for (int c = 0; c < WIN * 8 / 256; ++c) {
+          const int r = tid + 256 * c;
+          sUw[r] = dlo + (r >> 3) < a.npos ? uv[c] : 0.f;
+        }
+      }
       __syncthreads();
       f32x4_t sc[4];
       block_scores(sQ, sK, sPK, sPQ, sW, sDelta, i0, j0, dlo, S, w, lane, sc);
@@ -381,12 +393,15 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
           const float ds = qv > 0.f ? p * (dp[t][e] * keep - Di) : 0.f;   // grad of the scaled score
           sc[t][e] = ds * a.inv_scale;                          // -> raw c2c / c2p / p2c terms
         }
-      // dQ += dS·K
+      // dQ (this block pair) = dS·K + G·posK_win, added to the fp32 scratch below
+      f32x4_t dqp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dqp[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const uint4 af = freg(sc[2 * c], sc[2 * c + 1]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dq[qq][u], ft<TP>(sK, 16 * u, c, lane), af);
+        for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dqp[u], ft<TP>(sK, 16 * u, c, lane), af);
       }
       // stash Pd and dS (bf16) for the key-side products; zero the window for G
 #pragma unroll
@@ -397,50 +412,64 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
         *reinterpret_cast<uint2*>(sP + (16 * w + li) * TP + (16 * t + 4 * lg) * 2) = pv;
         *reinterpret_cast<uint2*>(sdS + (16 * w + li) * TP + (16 * t + 4 * lg) * 2) = sv;
       }
-      for (int r = tid; r < 64 * GP; r += 256) sW[r] = 0.f;
-      __syncthreads();
-      // G[i][δ_ij - dlo] += dS_ij  ->  dQ_i += G·posK_win
+      // G[i][w] / H[j][w] = dS binned by w = δ(i - j) - dlo (fp32, LDS atomics: log buckets
+      // share w); then dQ += G·posK_win and dK += H·posQ_win
+      auto add_dq = [&]() {
+        if (irow) {           // each lane owns the same dQ elements in every block pair
+          float* d = a.dq32 + (rowb + i) * (int64_t)(a.nh * DH) + h * DH + 4 * lg;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rel = min(max(i - (j0 + 16 * t + 4 * lg + e), -(S - 1)), S - 1);
-          const int wi = min(max((int)sDelta[rel + S - 1] - dlo, 0), WIN - 1);
-          atomicAdd(&sW[(16 * w + li) * GP + wi], sc[t][e]);
+          for (int u = 0; u < 4; ++u) {
+            f32x4_t* pd4 = reinterpret_cast<f32x4_t*>(d + 16 * u);
+            *pd4 = j0 == 0 ? dqp[u] : *pd4 + dqp[u];
+          }
         }
-      __syncthreads();
+      };
+      {
+        for (int r = tid; r < 64 * GP; r += 256) sW[r] = 0.f;
+        __syncthreads();
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint4 af = fk32(sW, 16 * w, c, lane);
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dq[qq][u], ft<TP>(sPK, 16 * u, c, lane), af);
-      }
-      __syncthreads();
-      for (int r = tid; r < 64 * GP; r += 256) sW[r] = 0.f;
-      __syncthreads();
-      // H[j][δ_ij - dlo] += dS_ij  ->  dK_j += H·posQ_win (+ the LoRA rank-8 contractions)
+          for (int e = 0; e < 4; ++e) {
+            const int rel = min(max(i - (j0 + 16 * t + 4 * lg + e), -(S - 1)), S - 1);
+            const int wi = min(max((int)sDelta[rel + S - 1] - dlo, 0), WIN - 1);
+            atomicAdd(&sW[(16 * w + li) * GP + wi], sc[t][e]);
+          }
+        __syncthreads();
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int c = 0; c < 4; ++c) {
+          const uint4 af = fk32(sW, 16 * w, c, lane);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int jl = 16 * t + 4 * lg + e;
-          const int rel = min(max(i - (j0 + jl), -(S - 1)), S - 1);
-          const int wi = min(max((int)sDelta[rel + S - 1] - dlo, 0), WIN - 1);
-          atomicAdd(&sW[jl * GP + wi], sc[t][e]);
+          for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dqp[u], ft<TP>(sPK, 16 * u, c, lane), af);
         }
-      __syncthreads();
+        add_dq();
+        __syncthreads();
+        for (int r = tid; r < 64 * GP; r += 256) sW[r] = 0.f;
+        __syncthreads();
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint4 af = fk32(sW, 16 * w, c, lane);
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dkacc[u], ft<TP>(sPQ, 16 * u, c, lane), af);
+          for (int e = 0; e < 4; ++e) {
+            const int jl = 16 * t + 4 * lg + e;
+            const int rel = min(max(i - (j0 + jl), -(S - 1)), S - 1);
+            const int wi = min(max((int)sDelta[rel + S - 1] - dlo, 0), WIN - 1);
+            atomicAdd(&sW[jl * GP + wi], sc[t][e]);
+          }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint4 af = fk32(sW, 16 * w, c, lane);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dkacc[u], ft<TP>(sPQ, 16 * u, c, lane), af);
+        }
       }
       if (lora) {
+        auto hval = [&](int jl, int x) { return sW[jl * GP + x]; };
         // HU[j][c] += Σ_w H[j][w]·u[dlo + w][c]
         for (int r = tid; r < 64 * 8; r += 256) {
           const int jl = r >> 3, c = r & 7;
           float acc = 0.f;
-          for (int x = 0; x < WIN; ++x) acc += sW[jl * GP + x] * sUw[x * 8 + c];
+          for (int x = 0; x < WIN; ++x) acc += hval(jl, x) * sUw[x * 8 + c];
           sHU[r] += acc;
         }
         // PB[dlo + w][c] += Σ_j H[j][w]·KB[j][c]
@@ -448,14 +477,14 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
           const int x = tid >> 1, c0 = (tid & 1) * 4;
           float acc[4] = {0.f, 0.f, 0.f, 0.f};
           for (int jl = 0; jl < 64; ++jl) {
-            const float hv = sW[jl * GP + x];
+            const float hv = hval(jl, x);
             const float4 kb = *reinterpret_cast<const float4*>(sKB + jl * 8 + c0);
             acc[0] += hv * kb.x; acc[1] += hv * kb.y; acc[2] += hv * kb.z; acc[3] += hv * kb.w;
           }
           const int row = dlo + x;
-          if (row < a.npos && row < 512)
+          if (row < a.npos)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) sPB[row * 8 + c0 + e] += acc[e];
+            for (int e = 0; e < 4; ++e) pbw[row * 8 + c0 + e] += acc[e];
         }
       }
       // dK_j += dSᵀ·Q, dV_j += Pdᵀ·dO (rows j = 16w.. of this key block)
@@ -490,24 +519,20 @@ __global__ __launch_bounds__(256) void dis_attn_bwd_kernel(DisArgs a) {
         if (jj < S) a.hu[((rowb + jj) * a.nh + h) * 8 + (r & 7)] = sHU[r];
       }
   }
-  // dQ of every query block
-#pragma unroll
-  for (int qq = 0; qq < 4; ++qq) {
+  // dQ of every query block: fp32 scratch -> bf16 (same lane ownership as the accumulation)
+  for (int qq = 0; qq < nqb; ++qq) {
     const int i = qq * 64 + 16 * w + li;
-    if (qq < nqb && i < S) {
+    if (i < S) {
+      const float* d = a.dq32 + (rowb + i) * (int64_t)(a.nh * DH) + h * DH + 4 * lg;
       bf16_t* pq = a.dq + (rowb + i) * a.lddqkv + h * DH;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
+        const f32x4_t v4 = *reinterpret_cast<const f32x4_t*>(d + 16 * u);
         uint2 x;
-        x.x = pk2(dq[qq][u][0], dq[qq][u][1]); x.y = pk2(dq[qq][u][2], dq[qq][u][3]);
+        x.x = pk2(v4[0], v4[1]); x.y = pk2(v4[2], v4[3]);
         *reinterpret_cast<uint2*>(pq + 16 * u + 4 * lg) = x;
       }
     }
-  }
-  if (lora) {
-    __syncthreads();
-    float* dst = a.pb + ((int64_t)b * a.nh + h) * a.npos * 8;
-    for (int r = tid; r < a.npos * 8; r += 256) dst[r] = r < 512 * 8 ? sPB[r] : 0.f;
   }
 }
 
@@ -680,6 +705,7 @@ static DisArgs dis_args(const ttmi_dis_attn_desc* d) {
   a.dctx = (const bf16_t*)d->dctx; a.lddctx = d->lddctx;
   a.dq = (bf16_t*)d->dq; a.dk = (bf16_t*)d->dk; a.dv = (bf16_t*)d->dv; a.lddqkv = d->lddqkv;
   a.u = d->lora_u; a.bq = d->lora_bq; a.hu = d->lora_hu; a.pb = d->lora_pb;
+  a.dq32 = d->dq_scratch;
   return a;
 }
 
@@ -695,7 +721,8 @@ extern "C" int ttmi_dis_attn_fwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
 extern "C" int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
   int rc = dis_check(d);
   if (rc) return rc;
-  TTMI_REQUIRE(d->dctx && d->dq && d->dk && d->dv, "ttmi_dis_attn_bwd: null gradient argument");
+  TTMI_REQUIRE(d->dctx && d->dq && d->dk && d->dv && d->dq_scratch,
+               "ttmi_dis_attn_bwd: null gradient argument (dq_scratch: fp32 [B·S, nh·64])");
   TTMI_REQUIRE(d->lddctx % 8 == 0 && d->lddqkv % 4 == 0, "ttmi_dis_attn_bwd: bad leading dimension");
   TTMI_REQUIRE(!d->lora_u || (d->lora_bq && d->lora_hu && d->lora_pb),
                "ttmi_dis_attn_bwd: LoRA outputs need u, bq, hu and pb together");

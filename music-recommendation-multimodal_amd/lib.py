@@ -60,7 +60,8 @@ class DisAttnDesc(ctypes.Structure):
                 ("ctx", c_p), ("ldctx", ctypes.c_int64), ("lse", c_p),
                 ("dctx", c_p), ("lddctx", ctypes.c_int64),
                 ("dq", c_p), ("dk", c_p), ("dv", c_p), ("lddqkv", ctypes.c_int64),
-                ("lora_u", c_p), ("lora_bq", c_p), ("lora_hu", c_p), ("lora_pb", c_p)]
+                ("lora_u", c_p), ("lora_bq", c_p), ("lora_hu", c_p), ("lora_pb", c_p),
+                ("dq_scratch", c_p)]
 
 
 class LnBwdDesc(ctypes.Structure):

