@@ -429,6 +429,20 @@ int ttmi_deb_pool_fwd(int B, int S, int H, const float* x, const int64_t* mask, 
 int ttmi_deb_pool_bwd(int B, int S, int H, const float* dout, const int64_t* mask, float* dx,
                       hipStream_t stream);
 
+/* ------------------------------------------------------------------------------------
+ * Global retrieval (reference src/evaluate_metrics.py:107-192 calculate_metrics_global):
+ * scores = û·Îᵀ (ttmi_gemm) then per row the top-K item indices.
+ * ---------------------------------------------------------------------------------- */
+/* Per row r of scores [R, V] (fp32, row stride ld): the K largest values sorted descending
+ * (ties: lower index first) -> out_val [R, K], out_idx [R, K] (int64).  skip_first: column 0
+ * counts as -inf (the padding item, evaluate_metrics.py:157).  K <= 64, K <= V. */
+int ttmi_topk_rows(int R, int V, int K, const float* scores, int64_t ld, int skip_first,
+                   float* out_val, int64_t* out_idx, hipStream_t stream);
+/* rank[b] = first j with idx[b, j] == target[b], or K when absent (Recall@k: rank < k,
+ * NDCG@k: 1/log2(rank + 2) when rank < k). */
+int ttmi_rank_of(int B, int K, const int64_t* idx, const int64_t* target, int32_t* rank,
+                 hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,7 @@ from . import ops
 from . import functional
 from . import cnn
 from . import text
+from . import retrieval
 from .text import TextEncoder
 from .user_tower import SequentialUserEncoder
 from .item_tower import MultimodalItemEncoder

@@ -597,3 +597,25 @@ def dropout_to(x: Tensor, y: Tensor, drop: Drop = NO_DROP) -> Tensor:
     call("ttmi_dropout_bwd", code(y.dtype), M, N, _p(x), N, float(drop[0]), _p(drop[1]), N,
          None, _p(y), y.stride(0), None, _s())
     return y
+
+
+# ----------------------------------------------------------------------------- retrieval
+def topk_rows(scores: Tensor, K: int, out_val: Tensor, out_idx: Tensor,
+              skip_first: bool = False) -> None:
+    """Top-K per row of fp32 scores (descending, ties by lower index); column 0 excluded
+    (as -inf) when skip_first."""
+    R, V = scores.shape
+    if scores.dtype != torch.float32 or scores.stride(1) != 1:
+        raise ValueError("topk_rows: scores must be fp32 with unit column stride")
+    if out_val.numel() < R * K or out_idx.numel() < R * K or out_idx.dtype != torch.int64:
+        raise ValueError("topk_rows: outputs must be [R, K] (int64 indices)")
+    call("ttmi_topk_rows", R, V, K, _p(scores), scores.stride(0), int(skip_first), _p(out_val),
+         _p(out_idx), _s())
+
+
+def rank_of(idx: Tensor, target: Tensor, rank: Tensor) -> Tensor:
+    B, K = idx.shape
+    if target.numel() < B or rank.numel() < B:
+        raise ValueError("rank_of: target / rank too small")
+    call("ttmi_rank_of", B, K, _p(idx), _p(target), _p(rank), _s())
+    return rank

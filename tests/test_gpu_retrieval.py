@@ -1,0 +1,77 @@
+"""Global retrieval on the GPU: the radix-select top-K kernel against
+torch.topk (values exact, indices exact when scores are distinct; ties resolved to the lower
+index), the padding-column exclusion, and the full metrics path against the metrics the
+reference's calculate_metrics_global produced (tests/golden/retrieval.npz).  Ranks are
+integers: a fp32 summation-order difference may flip a near-tie, so the metrics are allowed
+one user's worth of difference."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("R,V,K", [(7, 100, 10), (33, 10136, 20), (5, 3001, 64), (3, 64, 64)])
+def test_topk_rows_vs_torch(gpu_pkg, R, V, K):
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(V + K)
+    s = torch.randn(R, V, generator=g)
+    val = torch.empty(R, K, device=DEV)
+    idx = torch.empty(R, K, device=DEV, dtype=torch.int64)
+    ops.topk_rows(s.to(DEV), K, val, idx)
+    rv, ri = torch.topk(s, K, dim=1)
+    assert torch.equal(val.cpu(), rv)
+    assert torch.equal(idx.cpu(), ri)
+    # padding column excluded
+    s2 = s.clone()
+    s2[:, 0] = 100.0
+    ops.topk_rows(s2.to(DEV), K, val, idx, skip_first=True)
+    s3 = s2.clone()
+    s3[:, 0] = -float("inf")
+    rv, ri = torch.topk(s3, K, dim=1)
+    assert torch.equal(idx.cpu(), ri) and torch.equal(val.cpu(), rv)
+
+
+def test_topk_rows_ties_lower_index_first(gpu_pkg):
+    ops = gpu_pkg.ops
+    s = torch.zeros(2, 500)
+    s[0, 10:20] = 1.0           # 10 tied best
+    s[1, ::7] = 2.0             # 72 tied best, K = 16
+    val = torch.empty(2, 16, device=DEV)
+    idx = torch.empty(2, 16, device=DEV, dtype=torch.int64)
+    ops.topk_rows(s.to(DEV), 16, val, idx)
+    assert idx[0, :10].cpu().tolist() == list(range(10, 20))
+    assert idx[0, 10:].cpu().tolist() == list(range(0, 6))          # then the zeros, in order
+    assert idx[1].cpu().tolist() == list(range(0, 7 * 16, 7))
+
+
+def test_retrieval_metrics_vs_reference_fixture(gpu_pkg):
+    retrieval = gpu_pkg.retrieval
+    z = load_golden("retrieval.npz")
+    users, items = torch.tensor(z["users"]).to(DEV), torch.tensor(z["items"]).to(DEV)
+    targets = torch.tensor(z["targets"]).to(DEV)
+    n = users.shape[0]
+
+    class Stub:
+        def __init__(self):
+            self.i = 0
+
+        def eval(self):
+            return self
+
+        def get_user_embedding(self, history_ids, history_mask, user_gender, user_country):
+            out = users[self.i:self.i + history_ids.shape[0]]
+            self.i += history_ids.shape[0]
+            return out
+    B = 48
+    loader = [{"history_ids": torch.ones(B, 5, dtype=torch.long),
+               "history_mask": torch.ones(B, 5, dtype=torch.long),
+               "user_gender": torch.zeros(B, dtype=torch.long),
+               "user_country": torch.zeros(B, dtype=torch.long),
+               "target_id": targets[b * B:(b + 1) * B].cpu()} for b in range(n // B)]
+    res = retrieval.calculate_metrics_global(Stub(), loader, items, DEV, k_list=[10, 20])
+    for k, v in res.items():
+        assert abs(v - float(z["metric/" + k])) <= 1.0 / n + 1e-6, (k, v, float(z["metric/" + k]))
