@@ -360,6 +360,113 @@ def cpu_baseline_cfg3(B: int, budget_s: float = 20.0):
                       f"warm-up {warm:.1f} s) of the fp32 torch-CPU oracle, {el:.1f} s"}
 
 
+def main_eval(args, world, rank, device):
+    """Global retrieval evaluation throughput (evaluate_metrics.py:107-192): per step one batch
+    of users -> user tower (eval) -> scores against the dense V=10,136 catalogue -> top-20 ->
+    target ranks (Recall/NDCG inputs).  Users/s over all ranks; roofline of the top-K kernel
+    (algorithmic bytes: the [B, V] fp32 score block read once)."""
+    B = args.batch or 512
+    K = 20
+    torch.manual_seed(1234 + rank)
+    model = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=N_GENDERS,
+                              num_countries=N_COUNTRIES, max_seq_len=L, user_embedding_dim=D,
+                              item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
+                              compute_dtype=torch.bfloat16).to(device).eval()
+    batches = synthetic_batches(4, B, seed=rank, device=device)
+    g = torch.Generator().manual_seed(rank + 3)
+    items = torch.nn.functional.normalize(torch.randn(V, D, generator=g), dim=1).to(device)
+    items[0] = 0.0
+    targets = [torch.randint(1, V, (B,), generator=g).to(device) for _ in batches]
+    rt = pkg.retrieval
+
+    def step(i):
+        b = batches[i % len(batches)]
+        u = model.get_user_embedding(b["history_ids"], b["history_mask"], b["user_gender"],
+                                     b["user_country"])
+        return rt.target_ranks(u, items, targets[i % len(targets)], K)
+
+    with torch.no_grad():
+        for i in range(max(args.warmup, 1)):
+            step(i)
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        roof = None
+        if rank == 0:                                    # top-K kernel, live, on its stream
+            u = model.get_user_embedding(batches[0]["history_ids"], batches[0]["history_mask"],
+                                         batches[0]["user_gender"], batches[0]["user_country"])
+            sc = rt.score_catalogue(u, items)
+            val = torch.empty(B, K, device=device)
+            idx = torch.empty(B, K, device=device, dtype=torch.int64)
+            st = torch.cuda.current_stream(device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            pkg.ops.topk_rows(sc, K, val, idx, skip_first=True)
+            e0.record(st)
+            for _ in range(20):
+                pkg.ops.topk_rows(sc, K, val, idx, skip_first=True)
+            e1.record(st)
+            torch.cuda.synchronize(device)
+            sec = e0.elapsed_time(e1) / 1e3 / 20
+            by = B * V * 4 + B * K * 12
+            gbs = by / sec / 1e9
+            roof = {"kernel": "topk_rows_kernel (radix-select top-20 over the [B, V] fp32 scores)",
+                    "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": read_traffic("topk_rows_kernel"),
+                    "avg_us": round(sec * 1e6, 2), "bytes_per_launch": by}
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        from oracle import two_tower_ref as ref
+        from oracle import retrieval_ref as rr
+        gc = torch.Generator().manual_seed(0)
+        params = ref.init_params(V, generator=gc)
+        up = {k[len("user_tower."):]: v for k, v in params.items() if k.startswith("user_tower.")}
+        cb = ref.synthetic_batch(B, L, V, generator=gc)
+        it_cpu, tg = items.cpu(), targets[0].cpu()
+        n, t0 = 0, time.perf_counter()
+        while True:
+            with torch.no_grad():
+                u = ref.user_tower_forward(up, cb["history_ids"], cb["user_gender"],
+                                           cb["user_country"], cb["history_mask"], H, 2)
+                rr.retrieval_metrics(torch.nn.functional.normalize(u, dim=1), it_cpu, tg, (10, 20))
+            n += 1
+            cel = time.perf_counter() - t0
+            if cel >= args.cpu_budget or n >= 30:
+                break
+        cpu = {"value": round(n * B / cel, 2), "unit": "users/s",
+               "cores": torch.get_num_threads(), "kind": "port",
+               "sample": f"{n} eval batches of {B} users (fp32 oracle user tower + torch.topk "
+                         f"over V={V}), {cel:.1f} s"}
+    if rank == 0:
+        line = {
+            "metric": "users/sec (global retrieval eval: user tower + catalogue scores + top-20 "
+                      "+ target rank), V=10136, batch=512",
+            "value": round(world * B * args.steps / el, 1), "unit": "users/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16+fp32",
+            "data": "synthetic histories and catalogue embeddings, random-init weights",
+            "config": {"workload": "eval: SURVEY 8(f) rank 2, evaluate_metrics.py:107-192",
+                       "global_batch": world * B, "catalogue": V, "k": K,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -367,10 +474,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU pairs (default: 512 for cfg 2, 256 for cfg 3)")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
+    ap.add_argument("--config", default="2", choices=("2", "3", "4", "eval"),
                     help="2 = BASELINE cfg 2 (the metric's configuration); 3 = full item "
                          "tower on raw mels/covers/tabular (BASELINE configs[2]); 4 = cfg 3 + "
-                         "mDeBERTa-LoRA lyrics, S=256 (BASELINE configs[3])")
+                         "mDeBERTa-LoRA lyrics, S=256 (BASELINE configs[3]); eval = global "
+                         "retrieval evaluation over the catalogue (SURVEY 8f rank 2)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -383,8 +491,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     device = torch.device("cuda", local)
-    cfg4 = args.config == 4
-    cfg3 = args.config == 3 or cfg4                      # cfg 4 = cfg 3 + text
+    if args.config == "eval":
+        return main_eval(args, world, rank, device)
+    cfg4 = args.config == "4"
+    cfg3 = args.config == "3" or cfg4                    # cfg 4 = cfg 3 + text
     B = args.batch or (256 if cfg3 else 512)
 
     torch.manual_seed(1234 + rank)
