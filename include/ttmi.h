@@ -438,6 +438,10 @@ int ttmi_deb_pool_bwd(int B, int S, int H, const float* dout, const int64_t* mas
  * counts as -inf (the padding item, evaluate_metrics.py:157).  K <= 64, K <= V. */
 int ttmi_topk_rows(int R, int V, int K, const float* scores, int64_t ld, int skip_first,
                    float* out_val, int64_t* out_idx, hipStream_t stream);
+/* scores[r, ids[r, j]] = -inf for j < Lh and 0 <= id < V (serving: exclude the user's history,
+ * reference src/inference.py:294-303). */
+int ttmi_mask_items(int R, int V, float* scores, int64_t ld, const int64_t* ids, int Lh,
+                    hipStream_t stream);
 /* rank[b] = first j with idx[b, j] == target[b], or K when absent (Recall@k: rank < k,
  * NDCG@k: 1/log2(rank + 2) when rank < k). */
 int ttmi_rank_of(int B, int K, const int64_t* idx, const int64_t* target, int32_t* rank,

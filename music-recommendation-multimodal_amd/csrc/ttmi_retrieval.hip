@@ -114,7 +114,27 @@ __global__ __launch_bounds__(256) void rank_kernel(int B, int K, const int64_t* 
   rank[b] = r;
 }
 
+// scores[r, ids[r, j]] = -inf for every listed item (the user's history, inference.py:294-303)
+__global__ __launch_bounds__(256) void mask_items_kernel(int R, int V, float* __restrict__ scores, int64_t ld,
+                                                         const int64_t* __restrict__ ids, int Lh) {
+  const int64_t n = (int64_t)R * Lh;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / Lh;
+    const int64_t id = ids[t];
+    if (id >= 0 && id < V) scores[r * ld + id] = -INFINITY;
+  }
+}
+
 }  // namespace
+
+extern "C" int ttmi_mask_items(int R, int V, float* scores, int64_t ld, const int64_t* ids, int Lh,
+                               hipStream_t s) {
+  TTMI_REQUIRE(R > 0 && V > 0 && Lh > 0 && ld >= V && scores && ids, "ttmi_mask_items: bad argument");
+  const int64_t n = (int64_t)R * Lh;
+  hipLaunchKernelGGL(mask_items_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s,
+                     R, V, scores, ld, ids, Lh);
+  return ttmi_check_launch("ttmi_mask_items");
+}
 
 extern "C" int ttmi_topk_rows(int R, int V, int K, const float* scores, int64_t ld, int skip_first,
                               float* out_val, int64_t* out_idx, hipStream_t s) {

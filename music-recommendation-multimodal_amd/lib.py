@@ -115,6 +115,7 @@ SIGNATURES = {
     "ttmi_deb_gelu": (c_i, [c_i64, c_p, c_p, c_p]),
     "ttmi_topk_rows": (c_i, [c_i, c_i, c_i, c_p, c_i64, c_i, c_p, c_p, c_p]),
     "ttmi_rank_of": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_mask_items": (c_i, [c_i, c_i, c_p, c_i64, c_p, c_i, c_p]),
     "ttmi_dis_attn_fwd": (c_i, [c_p, c_p]),
     "ttmi_dis_attn_bwd": (c_i, [c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),

@@ -619,3 +619,13 @@ def rank_of(idx: Tensor, target: Tensor, rank: Tensor) -> Tensor:
         raise ValueError("rank_of: target / rank too small")
     call("ttmi_rank_of", B, K, _p(idx), _p(target), _p(rank), _s())
     return rank
+
+
+def mask_items(scores: Tensor, ids: Tensor) -> Tensor:
+    """scores[r, ids[r, j]] = -inf (ids int64 [R, Lh]; out-of-range ids ignored)."""
+    R, V = scores.shape
+    ids = ids.to(torch.int64).contiguous()
+    if ids.shape[0] != R or scores.stride(1) != 1:
+        raise ValueError("mask_items: ids must be [R, Lh] and scores row-major")
+    call("ttmi_mask_items", R, V, _p(scores), scores.stride(0), _p(ids), ids.shape[1], _s())
+    return scores

@@ -1,6 +1,7 @@
-"""Global retrieval evaluation and top-K serving — SURVEY §8(f) rank 2, drop-in for reference
-src/evaluate_metrics.py:107-192 (``calculate_metrics_global``) and the scoring half of
-src/inference.py's ``recommend``.
+"""Global retrieval evaluation, top-K serving and checkpoint interchange — SURVEY §8(f)
+ranks 2-4: drop-ins for reference src/evaluate_metrics.py:107-192 (``calculate_metrics_global``),
+the scoring half of src/inference.py's ``recommend`` (:228-323) and the checkpoint loading of
+inference.py:97-107 / evaluate_metrics.py:300-305.
 
 Users are scored against the whole catalogue: ``scores = û·Îᵀ`` (fp32 MFMA GEMM, ttmi_gemm),
 column 0 (the padding item) excluded, top-K per user by radix select (``ttmi_topk_rows``),
@@ -90,3 +91,54 @@ def calculate_metrics_global(model, val_loader: Iterable, item_embeddings: Tenso
             for name, v in metrics_from_ranks(ranks, k_list).items():
                 per[name].append(v.cpu())
     return {name: torch.cat(v).mean().item() for name, v in per.items()}
+
+
+def recommend(model, history_ids: Tensor, item_embeddings: Tensor, k: int = 10,
+              user_gender: Optional[Tensor] = None, user_country: Optional[Tensor] = None,
+              max_len: int = 50) -> Tuple[Tensor, Tensor]:
+    """inference.py:254-310 for a batch of users: keep the last ``max_len`` history items,
+    user embedding (eval, L2-normalised with eps 1e-8), scores against the catalogue, padding
+    item and history items excluded, top-k -> (scores [B, k], item indices [B, k])."""
+    model.eval()
+    hist = history_ids[:, -max_len:].long()
+    with torch.no_grad():
+        u = model.get_user_embedding(history_ids=hist, user_gender=user_gender,
+                                     user_country=user_country)
+        u = TF.normalize(u, p=2, dim=1, eps=1e-8)
+        scores = score_catalogue(u, item_embeddings.to(u.device))
+        ops.mask_items(scores, hist)
+        B = scores.shape[0]
+        val = torch.empty(B, k, device=scores.device)
+        idx = torch.empty(B, k, device=scores.device, dtype=torch.int64)
+        ops.topk_rows(scores, k, val, idx, skip_first=True)
+    return val, idx
+
+
+def reference_state_dict(source) -> Dict[str, Tensor]:
+    """A reference checkpoint (path or dict) with DDP's ``module.`` prefix stripped
+    (inference.py:97-107).  Files are read with torch.load(weights_only=True): tensors only."""
+    sd = torch.load(source, map_location="cpu", weights_only=True) if isinstance(source, str) \
+        else dict(source)
+    if sd and next(iter(sd)).startswith("module."):
+        sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
+    return sd
+
+
+def model_from_reference_checkpoint(source, vocab_size: int, num_genders: int = 1, **kw):
+    """Build a TwoTowerModel whose dimensions come from the checkpoint (inference.py:109-128:
+    countries from user_tower.country_embedding, tabular width from the tabular encoder, the
+    embedding width from the item embedding) and load it (strict: every key must match)."""
+    from .two_tower import TwoTowerModel
+    sd = reference_state_dict(source)
+    D = sd["user_tower.item_embedding.weight"].shape[1]
+    kw.setdefault("num_countries", sd["user_tower.country_embedding.weight"].shape[0])
+    if "item_tower.tabular_encoder.mlp.0.weight" in sd:
+        kw.setdefault("tabular_input_dim", sd["item_tower.tabular_encoder.mlp.0.weight"].shape[1])
+        kw.setdefault("precomputed_modalities", False)
+        kw.setdefault("with_text", any(k.startswith("item_tower.text_encoder.") for k in sd))
+    else:
+        kw.setdefault("tabular_input_dim", 128)
+    model = TwoTowerModel(vocab_size=vocab_size, num_genders=num_genders, user_embedding_dim=D,
+                          item_embedding_dim=D, **kw)
+    model.load_state_dict(sd)
+    return model

@@ -75,3 +75,35 @@ def test_retrieval_metrics_vs_reference_fixture(gpu_pkg):
     res = retrieval.calculate_metrics_global(Stub(), loader, items, DEV, k_list=[10, 20])
     for k, v in res.items():
         assert abs(v - float(z["metric/" + k])) <= 1.0 / n + 1e-6, (k, v, float(z["metric/" + k]))
+
+
+def test_recommend_matches_oracle_inference(gpu_pkg):
+    """Serving (inference.py:254-310): last-50 history, normalised user embedding, padding and
+    history excluded, top-10 — fp32 model vs the oracle's user tower + torch ops."""
+    from oracle import two_tower_ref as ref
+    torch.manual_seed(0)
+    V, D, L = 997, 64, 60
+    m = gpu_pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=3, num_countries=8,
+                              max_seq_len=50, user_embedding_dim=D, item_embedding_dim=D,
+                              compute_dtype=torch.float32).to(DEV)
+    g = torch.Generator().manual_seed(1)
+    hist = torch.randint(1, V, (6, L), generator=g)
+    hist[2, :30] = 0                                         # left part padding
+    gender = torch.randint(0, 3, (6,), generator=g)
+    country = torch.randint(0, 8, (6,), generator=g)
+    items = torch.nn.functional.normalize(torch.randn(V, D, generator=g), dim=1)
+    val, idx = gpu_pkg.retrieval.recommend(m, hist.to(DEV), items.to(DEV), k=10,
+                                           user_gender=gender.to(DEV), user_country=country.to(DEV))
+    p = {k[len("user_tower."):]: v.detach().cpu() for k, v in m.named_parameters()
+         if k.startswith("user_tower.")}
+    h = hist[:, -50:]
+    u = ref.user_tower_forward(p, h, gender, country, None, 4, 2)
+    u = torch.nn.functional.normalize(torch.nn.functional.normalize(u, dim=1), p=2, dim=1, eps=1e-8)
+    s = u @ items.t()
+    s[:, 0] = -float("inf")
+    for r in range(6):
+        s[r, h[r]] = -float("inf")
+    rv, ri = torch.topk(s, 10, dim=1)
+    assert torch.equal(idx.cpu(), ri)
+    assert torch.allclose(val.cpu(), rv, atol=1e-4)
+    assert not any(int(i) in set(h[r].tolist()) for r in range(6) for i in idx[r].cpu())
