@@ -645,6 +645,108 @@ __global__ __launch_bounds__(256) void deb_gelu_kernel(int64_t n8, const bf16_t*
   }
 }
 
+// ---------------------------------------------------------------- rank-8 LoRA gradients
+// Skinny weight gradient (the LoRA A/B gradients of the cfg-4 text encoder, item_tower.py:
+// 51-59 under peft): C(m, c) += alpha · Σ_r W[r, m] · S[r, soff(m) + c] for m < Mw, c < 8,
+// r < R, where W (bf16, row stride ldw) is the wide operand (768 columns) and S (bf16 or
+// fp32, row stride lds) the rank-8 one; soff(m) = (m / group) · sgs selects a per-head slice
+// (group = 64, sgs = 8 for the relative-path Bq contraction; group = Mw for plain dB/dA).
+// C element (m, c) sits at m·ldc_m + c·ldc_c.  R is long (B·S = 65,536) and the output tiny
+// (768 x 8), so this is an HBM stream of W: each thread owns 8 consecutive W columns (16-byte
+// loads, 64 fp32 accumulators) over a strided row set; the block's row groups are summed in
+// LDS and every block adds its 6 KB partial with contiguous atomics.  The generic tile path
+// spent ~260 us per call here padding the rank-8 side to 64.
+template <typename TS>
+__global__ __launch_bounds__(256) void skinny_wgrad_kernel(int64_t R, int Mw, const bf16_t* __restrict__ W,
+                                                           int64_t ldw, const TS* __restrict__ S,
+                                                           int64_t lds, int group, int sgs, float alpha,
+                                                           float* __restrict__ C, int64_t ldc_m,
+                                                           int64_t ldc_c, int64_t rows_per_block) {
+  extern __shared__ float red[];                       // [RG][Mw·8]
+  const int ncol8 = Mw / 8, RG = 256 / ncol8;
+  const int t = threadIdx.x, rg = t / ncol8, c8 = t % ncol8;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(R, r0 + rows_per_block);
+  float acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[i][c] = 0.f;
+  if (rg < RG) {
+    const int soff = (c8 * 8 / group) * sgs;
+    for (int64_t r = r0 + rg; r < r1; r += RG) {
+      float w[8], s[8];
+      unpack8(*reinterpret_cast<const uint4*>(W + r * ldw + c8 * 8), w);
+      if constexpr (sizeof(TS) == 2) {
+        unpack8(*reinterpret_cast<const uint4*>(S + r * lds + soff), s);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(S + r * lds + soff);
+        const float4 b = *reinterpret_cast<const float4*>(S + r * lds + soff + 4);
+        s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[i][c] += w[i] * s[c];
+    }
+    float* dst = red + (int64_t)rg * Mw * 8 + c8 * 64;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int c = 0; c < 8; c += 4)
+        *reinterpret_cast<float4*>(dst + i * 8 + c) = make_float4(acc[i][c], acc[i][c + 1], acc[i][c + 2], acc[i][c + 3]);
+  }
+  __syncthreads();
+  // contiguous in C: walk (m fastest) when ldc_m == 1, else (c fastest)
+  const int n = Mw * 8;
+  for (int o = t; o < n; o += 256) {
+    int m, c;
+    if (ldc_m == 1) { c = o / Mw; m = o % Mw; } else { m = o / 8; c = o % 8; }
+    float v = 0.f;
+    for (int g = 0; g < RG; ++g) v += red[(int64_t)g * n + m * 8 + c];
+    atomicAdd(C + m * ldc_m + c * ldc_c, alpha * v);
+  }
+}
+
+// dx[m, n] += s · Σ_{p in {q, v}} drop_p(dL_p[m, :] · A_p[:, n])  (the LoRA input gradient of
+// query_proj / value_proj; drop_p regenerates the forward LoRA-dropout mask at m·ld_drop + n).
+// dL [M, 16] bf16 = [dL_q | dL_v], A_q/A_v [8, H] bf16.  One thread per 8 columns; HBM-bound on
+// the fp32 read-modify-write of dx (replaces two K=8 accumulate GEMMs with atomics).
+__global__ __launch_bounds__(256) void lora_dx_kernel(int64_t M, int H, const bf16_t* __restrict__ dL,
+                                                      int64_t ld_dl, const bf16_t* __restrict__ aq,
+                                                      const bf16_t* __restrict__ av, float s,
+                                                      DropParams dq, DropParams dv, int64_t ld_drop,
+                                                      float* __restrict__ dx, int64_t ld_dx) {
+  const int ncol8 = H / 8;
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= M * ncol8) return;
+  const int64_t m = id / ncol8;
+  const int n = (int)(id % ncol8) * 8;
+  const DropKeys kq = resolve_drop(dq), kv = resolve_drop(dv);
+  float lq[8], lv[8];
+  unpack8(*reinterpret_cast<const uint4*>(dL + m * ld_dl), lq);
+  unpack8(*reinterpret_cast<const uint4*>(dL + m * ld_dl + 8), lv);
+  float yq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, yv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    float a[8], b[8];
+    unpack8(*reinterpret_cast<const uint4*>(aq + r * H + n), a);
+    unpack8(*reinterpret_cast<const uint4*>(av + r * H + n), b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { yq[e] += lq[r] * a[e]; yv[e] += lv[r] * b[e]; }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { yq[e] *= s; yv[e] *= s; }
+  drop_apply_vec<8>(kq, (uint32_t)(m * ld_drop + n), yq);
+  drop_apply_vec<8>(kv, (uint32_t)(m * ld_drop + n), yv);
+  float* p = dx + m * ld_dx + n;
+  float4 x0 = *reinterpret_cast<float4*>(p), x1 = *reinterpret_cast<float4*>(p + 4);
+  x0.x += yq[0] + yv[0]; x0.y += yq[1] + yv[1]; x0.z += yq[2] + yv[2]; x0.w += yq[3] + yv[3];
+  x1.x += yq[4] + yv[4]; x1.y += yq[5] + yv[5]; x1.z += yq[6] + yv[6]; x1.w += yq[7] + yv[7];
+  *reinterpret_cast<float4*>(p) = x0;
+  *reinterpret_cast<float4*>(p + 4) = x1;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C ABI
@@ -744,4 +846,43 @@ extern "C" int ttmi_deb_pool_bwd(int B, int S, int H, const float* dout, const i
   hipLaunchKernelGGL(deb_pool_bwd_kernel, dim3((unsigned)((int64_t)B * S)), dim3(256), 0, s, S, H, dout,
                      mask, dx);
   return ttmi_check_launch("ttmi_deb_pool_bwd");
+}
+
+extern "C" int ttmi_skinny_wgrad(int64_t R, int Mw, const uint16_t* W, int64_t ldw, const void* S,
+                                 int s_f32, int64_t lds, int group, int sgs, float alpha, float* C,
+                                 int64_t ldc_m, int64_t ldc_c, hipStream_t s) {
+  TTMI_REQUIRE(R > 0 && Mw > 0 && Mw % 8 == 0 && Mw / 8 <= 256 && W && S && C,
+               "ttmi_skinny_wgrad: need Mw %% 8 == 0, Mw <= 2048");
+  TTMI_REQUIRE(group > 0 && group % 8 == 0 && ldw % 8 == 0 && (uintptr_t)W % 16 == 0 &&
+               (uintptr_t)S % 16 == 0 && lds % (s_f32 ? 4 : 8) == 0,
+               "ttmi_skinny_wgrad: W/S need 16-byte rows, group %% 8 == 0");
+  TTMI_REQUIRE((int64_t)((Mw - 1) / group) * sgs + 8 <= lds, "ttmi_skinny_wgrad: S slice past its row");
+  const int RG = 256 / (Mw / 8);
+  const size_t shm = (size_t)RG * Mw * 8 * sizeof(float);
+  TTMI_REQUIRE(shm <= 64 * 1024, "ttmi_skinny_wgrad: reduction tile exceeds 64 KB");
+  const int64_t blocks = std::min<int64_t>(256, std::max<int64_t>(1, R / (4 * RG)));
+  const int64_t rpb = (R + blocks - 1) / blocks;
+  if (s_f32)
+    hipLaunchKernelGGL(skinny_wgrad_kernel<float>, dim3((unsigned)blocks), dim3(256), shm, s, R, Mw,
+                       (const bf16_t*)W, ldw, (const float*)S, lds, group, sgs, alpha, C, ldc_m, ldc_c, rpb);
+  else
+    hipLaunchKernelGGL(skinny_wgrad_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), shm, s, R, Mw,
+                       (const bf16_t*)W, ldw, (const bf16_t*)S, lds, group, sgs, alpha, C, ldc_m, ldc_c, rpb);
+  return ttmi_check_launch("ttmi_skinny_wgrad");
+}
+
+extern "C" int ttmi_lora_dx(int64_t M, int H, const uint16_t* dL, int64_t ld_dl, const uint16_t* aq,
+                            const uint16_t* av, float scale, float drop_p, const uint64_t* seed_q,
+                            const uint64_t* seed_v, int64_t ld_drop, float* dx, int64_t ld_dx,
+                            hipStream_t s) {
+  TTMI_REQUIRE(M > 0 && H > 0 && H % 8 == 0 && dL && aq && av && dx, "ttmi_lora_dx: bad argument");
+  TTMI_REQUIRE(ld_dl % 8 == 0 && ld_dl >= 16 && ld_dx % 4 == 0 && (uintptr_t)dL % 16 == 0 &&
+               (uintptr_t)aq % 16 == 0 && (uintptr_t)av % 16 == 0 && (uintptr_t)dx % 16 == 0,
+               "ttmi_lora_dx: operands need 16-byte rows");
+  TTMI_REQUIRE(drop_p == 0.f || (seed_q && seed_v), "ttmi_lora_dx: dropout needs both seeds");
+  const int64_t n = M * (H / 8);
+  hipLaunchKernelGGL(lora_dx_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, H,
+                     (const bf16_t*)dL, ld_dl, (const bf16_t*)aq, (const bf16_t*)av, scale,
+                     make_drop(drop_p, seed_q), make_drop(drop_p, seed_v), ld_drop, dx, ld_dx);
+  return ttmi_check_launch("ttmi_lora_dx");
 }

@@ -885,6 +885,321 @@ int launch_wgrad(const ttmi_gemm_desc* d, hipStream_t stream) {
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// ------------------------------------------- large token GEMM: 256x256x64 tiles, 8 waves
+// C[M,N] = epi(alpha · A[M,K] · B[N,K]ᵀ) for the mDeBERTa token GEMMs (M = B·S = 65,536,
+// N, K in {768, 832, 2304, 3072}): bf16, both operands k-major, K % 64 == 0.
+//  * 8 waves as 2 (rows) x 4 (cols); a wave owns 128 x 64 outputs = 8 x 4 MFMA tiles (128
+//    accumulator registers).  Per 64-deep K-tile each wave runs 4 phases, one per 64 x 32
+//    quadrant of its block (16 v_mfma_f32_16x16x32_bf16 each).
+//  * Operands are staged by LDS-DMA (buffer_load_dwordx4 ... lds) into two 64 KB K-tile
+//    buffers, [row][128 B] images whose 16-byte chunks are XOR-swizzled per row on the SOURCE
+//    address (the DMA writes lane-linearly), so the 16 rows a ds_read_b128 lane group reads
+//    fall in 16 distinct bank slots.
+//  * The two wave groups (rows 0-127 / 128-255) run one barrier apart: while one group's
+//    waves issue their ds_reads and DMAs, the other group's waves, on the same SIMDs, run
+//    their MFMA cluster.  Every phase is {ds_read [+ DMA issue]; barrier; MFMA x16; barrier}.
+//  * DMA schedule of K-tile t+1 (buffer (t+1)&1, which held t-1): A/B rows 0-127 at phase 3
+//    of tile t-1 (after the last reads of those rows), rows 128-255 at phase 1 of tile t;
+//    all of t+1 is waited for (counted vmcnt, never in flight across the read) at phase 3
+//    of tile t, two barriers before any wave reads it.
+//  * B fragment rows are paired (tile 2p row 4q+r <-> column 32p+8q+r, tile 2p+1 <->
+//    32p+8q+4+r), so each lane owns 8 consecutive output columns: 16-byte epilogue accesses.
+//  * blockIdx is remapped so each XCD owns a contiguous run of tiles (row panels shared in
+//    its L2).
+namespace big {
+constexpr int BMN = 256;
+constexpr int HALF = 128 * 128;     // bytes: 128 rows x 64 bf16
+constexpr int IMG = 2 * HALF;       // one operand's K-tile image
+constexpr int STAGE = 2 * IMG;      // A + B
+TTMI_DEV int swz_a(int r) { return (r >> 1) & 7; }
+TTMI_DEV int swz_b(int r) { return ((r >> 1) & 1) | (((r >> 3) & 3) << 1); }
+TTMI_DEV void barrier() { asm volatile("s_barrier" ::: "memory"); }
+TTMI_DEV void wait_lgkm0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+}  // namespace big
+
+struct BigArgs {
+  GemmArgs g;
+  int tiles_n, tiles;
+};
+
+// One 128-row half of a K-tile image: this wave's 2 of its 16 DMA wave-instructions.
+template <bool ISB>
+TTMI_DEV void big_issue(const i32x4_t& rs, int64_t ld, int half, int k0, uint32_t img, int wave,
+                        int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int ii = wave + 8 * u;
+    const int r = half * 128 + ii * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ (ISB ? big::swz_b(r) : big::swz_a(r));
+    const uint32_t voff = (uint32_t)(((int64_t)r * ld + k0) * 2 + ch * 16);
+    dma16(rs, voff, img + half * big::HALF + ii * 1024);
+  }
+}
+
+TTMI_DEV uint4 big_frag_a(const char* img, int row, int c, int lane) {
+  const int ch = (4 * c + (lane >> 4)) ^ big::swz_a(row);
+  return lds16(img + row * 128 + ch * 16);
+}
+// B tile j of the wave's 64 columns (paired mapping), row-operand lane i = lane & 15
+TTMI_DEV int big_brow(int wc, int j, int lane) {
+  const int i = lane & 15;
+  return wc * 64 + 32 * (j >> 1) + 8 * (i >> 2) + 4 * (j & 1) + (i & 3);
+}
+TTMI_DEV uint4 big_frag_b(const char* img, int row, int c, int lane) {
+  const int ch = (4 * c + (lane >> 4)) ^ big::swz_b(row);
+  return lds16(img + row * 128 + ch * 16);
+}
+
+// Epilogue of 8 consecutive columns n..n+7 of row m (v holds alpha·acc).
+TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t n, float* v) {
+  const bool full = n + 7 < g.N;
+  if (g.bias) {
+    if (full) {
+      const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
+      const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += (n + e < g.N) ? g.bias[n + e] : 0.f;
+    }
+  }
+  if (g.act == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+  } else if (g.act == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+  }
+  drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + n), v);
+  if (g.gate) {
+    const int64_t o = m * g.ld_gate + n;
+    float gv[8];
+    if (full && !g.gate_f32) {
+      unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)g.gate + o), gv);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = (n + e < g.N) ? ld_dyn(g.gate, o + e, g.gate_f32) : 0.f;
+    }
+    if (g.act == 3) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad(gv[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
+    }
+  }
+  if (g.residual) {
+    const float* rp = g.residual + m * g.ld_res + n;
+    if (full) {
+      const float4 r0 = *reinterpret_cast<const float4*>(rp);
+      const float4 r1 = *reinterpret_cast<const float4*>(rp + 4);
+      v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+      v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) if (n + e < g.N) v[e] += rp[e];
+    }
+  }
+  const int64_t o = m * g.ldc + n;
+  if (g.c_mode == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (n + e < g.N) atomicAdd(reinterpret_cast<float*>(g.C) + o + e, v[e]);
+  } else if (full && g.c_f32) {
+    float* cp = reinterpret_cast<float*>(g.C) + o;
+    *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else if (full) {
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + o) = pack8(v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) if (n + e < g.N) st_dyn(g.C, o + e, v[e], g.c_f32);
+  }
+}
+
+__global__ __launch_bounds__(512) void gemm_big_kernel(BigArgs ba) {
+  using namespace big;
+  const GemmArgs& g = ba.g;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  // XCD-contiguous tile order (bijective for any tile count)
+  const int bid = blockIdx.x, nwg = ba.tiles;
+  const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+  const int64_t m0 = (int64_t)(tile / ba.tiles_n) * BMN, n0 = (int64_t)(tile % ba.tiles_n) * BMN;
+  const int nt = (int)(g.K / 64);
+  // descriptors start at the tile's first row; rows past M / N read as zero
+  const int64_t arows = min<int64_t>(g.M - m0, BMN), brows = min<int64_t>(g.N - n0, BMN);
+  const i32x4_t ra = make_rsrc(g.A + m0 * g.lda * 2, (uint32_t)(((arows - 1) * g.lda + g.K) * 2));
+  const i32x4_t rb = make_rsrc(g.B + n0 * g.ldb * 2, (uint32_t)(((brows - 1) * g.ldb + g.K) * 2));
+  const uint32_t sl = lds_addr(smem);
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: all of tile 0, rows 0-127 of tile 1
+  big_issue<false>(ra, g.lda, 0, 0, sl, wave, lane);
+  big_issue<false>(ra, g.lda, 1, 0, sl, wave, lane);
+  big_issue<true>(rb, g.ldb, 0, 0, sl + IMG, wave, lane);
+  big_issue<true>(rb, g.ldb, 1, 0, sl + IMG, wave, lane);
+  if (nt > 1) {
+    big_issue<false>(ra, g.lda, 0, 64, sl + STAGE, wave, lane);
+    big_issue<true>(rb, g.ldb, 0, 64, sl + STAGE + IMG, wave, lane);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+  if (wr == 1) barrier();          // the second wave group runs one barrier behind
+
+  const int arow0 = wr * 128 + (lane & 15);
+  uint4 a[4][2], b0[2][2], b1[2][2];
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const char* sA = smem + cur * STAGE;
+    const char* sB = sA + IMG;
+    const uint32_t nxt = sl + (cur ^ 1) * STAGE;
+    // phase 0: quadrant (rows 0-63, cols 0-31)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) a[i][c] = big_frag_a(sA, arow0 + 16 * i, c, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) b0[j][c] = big_frag_b(sB, big_brow(wc, j, lane), c, lane);
+    barrier();
+    wait_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) Mma<bf16_t>::run(acc[i][j], b0[j][c], a[i][c]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+    // phase 1: quadrant (rows 0-63, cols 32-63); DMA rows 128-255 of tile t+1
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) b1[j][c] = big_frag_b(sB, big_brow(wc, 2 + j, lane), c, lane);
+    if (t + 1 < nt) {
+      big_issue<false>(ra, g.lda, 1, 64 * (t + 1), nxt, wave, lane);
+      big_issue<true>(rb, g.ldb, 1, 64 * (t + 1), nxt + IMG, wave, lane);
+    }
+    barrier();
+    wait_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) Mma<bf16_t>::run(acc[i][2 + j], b1[j][c], a[i][c]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+    // phase 2: quadrant (rows 64-127, cols 32-63)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) a[i][c] = big_frag_a(sA, arow0 + 64 + 16 * i, c, lane);
+    barrier();
+    wait_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) Mma<bf16_t>::run(acc[4 + i][2 + j], b1[j][c], a[i][c]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+    // phase 3: quadrant (rows 64-127, cols 0-31) from registers; tile t+1 complete; DMA
+    // rows 0-127 of tile t+2 into this buffer (their last reads were phases 0-2)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t + 2 < nt) {
+      const uint32_t here = sl + cur * STAGE;
+      big_issue<false>(ra, g.lda, 0, 64 * (t + 2), here, wave, lane);
+      big_issue<true>(rb, g.ldb, 0, 64 * (t + 2), here + IMG, wave, lane);
+    }
+    barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) Mma<bf16_t>::run(acc[4 + i][j], b0[j][c], a[i][c]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+  }
+  if (wr == 0) barrier();          // balance the barrier count of the two groups
+
+  // epilogue: lane holds rows 16i + (lane&15), columns 32p + 8(lane>>4) .. +7
+  const DropKeys dk = resolve_drop(g.drop);
+  const int li = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t m = m0 + wr * 128 + 16 * i + li;
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int64_t n = n0 + wc * 64 + 32 * p + 8 * lg;
+      if (n >= g.N) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = g.alpha * acc[i][2 * p][e];
+        v[4 + e] = g.alpha * acc[i][2 * p + 1][e];
+      }
+      big_epi8(g, dk, m, n, v);
+    }
+  }
+}
+
+// Big-tile dispatch: bf16 k-major operands, K % 64 == 0, enough 256x256 tiles to fill the
+// chip, no split-K / colsum / row sums / row-mapped dropout, 16-byte epilogue rows.
+bool big_applies(const ttmi_gemm_desc* d) {
+  if (getenv("TTMI_NO_BIG")) return false;          // tuning runs only
+  if (d->dtype != TTMI_BF16 || !d->a_kmajor || !d->b_kmajor || d->K % 64 || d->K == 0) return false;
+  if (d->colsum || d->rowsum_a || d->drop_rows || d->split_k > 1) return false;
+  if (d->N < 256 || ((d->M + 255) / 256) * ((d->N + 255) / 256) < 256) return false;
+  if (!al16(d->A) || !al16(d->B) || d->lda % 8 || d->ldb % 8) return false;
+  const int cb = d->c_dtype == TTMI_F32 ? 4 : 2;
+  if (!al16(d->C) || (d->ldc * cb) % 16) return false;
+  if (d->bias && !al16(d->bias)) return false;
+  if (d->residual && (!al16(d->residual) || d->ld_res % 4)) return false;
+  if (d->gate && (!al16(d->gate) || d->ld_gate % 8 || d->gate_dtype == TTMI_F32)) return false;
+  // 32-bit buffer offsets within one 256-row panel
+  if ((int64_t)256 * std::max(d->lda, d->ldb) * 2 >= ((int64_t)1 << 31)) return false;
+  return true;
+}
+
+int launch_big(const GemmArgs& a, hipStream_t s) {
+  BigArgs ba;
+  ba.g = a;
+  ba.tiles_n = (int)((a.N + 255) / 256);
+  const int64_t tiles = ((a.M + 255) / 256) * (int64_t)ba.tiles_n;
+  TTMI_REQUIRE(tiles < (1ll << 31), "ttmi_gemm: grid too large");
+  ba.tiles = (int)tiles;
+  hipLaunchKernelGGL(gemm_big_kernel, dim3((unsigned)tiles), dim3(512), 0, s, ba);
+  return ttmi_check_launch("ttmi_gemm");
+}
+
 int num_cus() {
   static const int n = [] {
     int dev = 0, cus = 0;
@@ -1027,6 +1342,7 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
           (!d->gate || (d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 16 == 0));
 
   if (panel_applies(d) && launch_panel(d, a, stream)) return ttmi_check_launch("ttmi_gemm");
+  if (big_applies(d)) return launch_big(a, stream);
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)split);
   if (d->dtype == TTMI_BF16) launch_typed<bf16_t>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
   else launch_typed<float>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);

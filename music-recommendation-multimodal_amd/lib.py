@@ -120,6 +120,10 @@ SIGNATURES = {
     "ttmi_dis_attn_bwd": (c_i, [c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,
+                                c_i64, c_i64, c_p]),
+    "ttmi_lora_dx": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, ctypes.c_float, ctypes.c_float, c_p, c_p,
+                           c_i64, c_p, c_i64, c_p]),
     "ttmi_conv2d": (c_i, [c_p, c_p]),
     "ttmi_conv2d_workspace": (ctypes.c_int64, [c_p]),
     "ttmi_conv_weight_prep": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),

@@ -583,6 +583,32 @@ def deb_pool_fwd(x: Tensor, mask: Tensor, out: Tensor) -> Tensor:
     return out
 
 
+def skinny_wgrad(W: Tensor, S: Tensor, C: Tensor, Mw: int, *, ldc_m: int, ldc_c: int,
+                 alpha: float = 1.0, group: int = 0, sgs: int = 8) -> Tensor:
+    """C[m, c] += alpha · Σ_r W[r, m] · S[r, (m / group)·sgs + c] (rank-8 LoRA gradients);
+    W, S 2-D row-major views over the same R rows (column slices allowed)."""
+    _dev(W, S, C)
+    if W.dtype != torch.bfloat16 or S.dtype not in (torch.bfloat16, torch.float32) or C.dtype != torch.float32:
+        raise TypeError("skinny_wgrad: W bf16, S bf16/fp32, C fp32")
+    if W.shape[0] != S.shape[0] or W.shape[1] < Mw:
+        raise ValueError("skinny_wgrad: W and S must share R rows; W needs Mw columns")
+    call("ttmi_skinny_wgrad", W.shape[0], Mw, _p(W), W.stride(0), _p(S), int(S.dtype == torch.float32),
+         S.stride(0), group or Mw, sgs, alpha, _p(C), ldc_m, ldc_c, _s())
+    return C
+
+
+def lora_dx(dL: Tensor, aq: Tensor, av: Tensor, scale: float, drop_q: Drop, drop_v: Drop,
+            dx: Tensor, ld_drop: int) -> Tensor:
+    """dx += scale·(drop_q(dL[:, :8]·Aq) + drop_v(dL[:, 8:16]·Av)); the two dropouts share p."""
+    _dev(dL, aq, av, dx)
+    M, H = dx.shape
+    if float(drop_q[0]) != float(drop_v[0]):
+        raise ValueError("lora_dx: q and v LoRA dropout must share p")
+    call("ttmi_lora_dx", M, H, _p(dL), dL.stride(0), _p(aq), _p(av), scale, float(drop_q[0]),
+         _p(drop_q[1]), _p(drop_v[1]), ld_drop, _p(dx), dx.stride(0), _s())
+    return dx
+
+
 def deb_pool_bwd(dout: Tensor, mask: Tensor, dx: Tensor) -> Tensor:
     B, H = dout.shape
     S = mask.shape[1]

@@ -178,11 +178,17 @@ class _Frozen:
             bqkv = torch.cat([base[A + "query_proj.base_layer.bias"].detach(),
                               base[A + "key_proj.bias"].detach(),
                               base[A + "value_proj.base_layer.bias"].detach()]).contiguous()
-            self.layers.append(dict(
-                waug=waug, bqkv=bqkv,
-                wo=bf(base[L + "attention.output.dense.weight"]),
-                w1=bf(base[L + "intermediate.dense.weight"]),
-                w2=bf(base[L + "output.dense.weight"])))
+            wo = bf(base[L + "attention.output.dense.weight"])
+            w1 = bf(base[L + "intermediate.dense.weight"])
+            w2 = bf(base[L + "output.dense.weight"])
+            # k-major mirrors of the input-grad operands (dX = dY·W reads Wᵀ rows), so the
+            # backward token GEMMs take the 256x256 LDS-DMA tile kernel
+            wqkv = waug[:, :H].contiguous()
+            t = [torch.empty(m.shape[1], m.shape[0], device=dev, dtype=torch.bfloat16)
+                 for m in (wo, w1, w2, wqkv)]
+            ops.transpose_batch(t, [wo, w1, w2, wqkv])
+            self.layers.append(dict(waug=waug, bqkv=bqkv, wo=wo, w1=w1, w2=w2,
+                                    woT=t[0], w1T=t[1], w2T=t[2], wqkvT=t[3]))
         self.rel = torch.empty(c.npos, H, device=dev)
         m = torch.empty(c.npos, device=dev)
         ops.deb_ln_fwd(base["encoder.rel_embeddings.weight"].detach().contiguous(),
@@ -392,19 +398,21 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
         L = f"encoder.layer.{l}."
         lp = f"{PREFIX}encoder.layer.{l}.attention.self."
         r = st.aq16[l].shape[0]
+        if r != 8:
+            raise NotImplementedError("text backward kernels are built for LoRA rank 8 (the reference's r)")
         dz2 = torch.empty(M, H, device=dev)
         ops.layernorm_bwd(dx, sv.z2, sv.m2, sv.r2, Fz.base[L + "output.LayerNorm.weight"], dz2, None, None)
         g2 = ops.dropout_bwd(dz2, torch.empty(M, H, device=dev, dtype=bf), None, _drop(pd, seeds, tsite(l, 2)))
         dpre = torch.empty(M, I, device=dev, dtype=bf)
-        _mm(g2, W["w2"], dpre, M, I, H, lda=H, ldb=I, ldc=I, b_k=False, act=3, gate=sv.pre, ld_gate=I)
+        _mm(g2, W["w2T"], dpre, M, I, H, lda=H, ldb=H, ldc=I, act=3, gate=sv.pre, ld_gate=I)
         da = torch.empty(M, H, device=dev)
-        _mm(dpre, W["w1"], da, M, H, I, lda=I, ldb=H, ldc=H, b_k=False, residual=dz2, ld_res=H)
+        _mm(dpre, W["w1T"], da, M, H, I, lda=I, ldb=I, ldc=H, residual=dz2, ld_res=H)
         dz1 = torch.empty(M, H, device=dev)
         ops.layernorm_bwd(da, sv.z1, sv.m1, sv.r1, Fz.base[L + "attention.output.LayerNorm.weight"],
                           dz1, None, None)
         g1 = ops.dropout_bwd(dz1, torch.empty(M, H, device=dev, dtype=bf), None, _drop(pd, seeds, tsite(l, 1)))
         dctx = torch.empty(M, H, device=dev, dtype=bf)
-        _mm(g1, W["wo"], dctx, M, H, H, lda=H, ldb=H, ldc=H, b_k=False)
+        _mm(g1, W["woT"], dctx, M, H, H, lda=H, ldb=H, ldc=H)
         dqkv = torch.empty(M, 3 * H, device=dev, dtype=bf)
         bq32 = P[lp + "query_proj.lora_B.default.weight"].detach().contiguous()
         hu = torch.empty(M * nh * 8, device=dev)
@@ -416,32 +424,23 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
                      lora_hu=hu, lora_pb=pb)
         # input gradient through the QKV GEMM (+ residual) and the LoRA branch
         dxn = torch.empty(M, H, device=dev)
-        _mm(dqkv, W["waug"], dxn, M, H, 3 * H, lda=3 * H, ldb=Ha, ldc=H, b_k=False, residual=dz1, ld_res=H)
+        _mm(dqkv, W["wqkvT"], dxn, M, H, 3 * H, lda=3 * H, ldb=3 * H, ldc=H, residual=dz1, ld_res=H)
         dL = torch.empty(M, 2 * r, device=dev, dtype=bf)
         _mm(dqkv, W["waug"][:, H:], dL, M, 2 * r, 3 * H, lda=3 * H, ldb=Ha, ldc=2 * r, b_k=False)
         gAq, gBq = G[lp + "query_proj.lora_A.default.weight"], G[lp + "query_proj.lora_B.default.weight"]
         gAv, gBv = G[lp + "value_proj.lora_A.default.weight"], G[lp + "value_proj.lora_B.default.weight"]
-        # dB = dYᵀ·t (t = s·u lives in the augmented operand columns)
-        _mm(dqkv, sv.xaug[:, H:H + r], gBq, H, r, M, lda=3 * H, ldb=Ha, ldc=r, a_k=False, b_k=False,
-            accumulate=True)
-        _mm(dqkv[:, 2 * H:], sv.xaug[:, H + r:H + 2 * r], gBv, H, r, M, lda=3 * H, ldb=Ha, ldc=r,
-            a_k=False, b_k=False, accumulate=True)
-        # dA = s·dLᵀ·drop(x);  dx += s·drop'(dL·A)
-        _mm(dL, sv.xq, gAq, r, H, M, lda=2 * r, ldb=sv.xq.stride(0), ldc=H, a_k=False, b_k=False,
-            alpha=s, accumulate=True)
-        _mm(dL[:, r:], sv.xv, gAv, r, H, M, lda=2 * r, ldb=sv.xv.stride(0), ldc=H, a_k=False,
-            b_k=False, alpha=s, accumulate=True)
-        _mm(dL, st.aq16[l], dxn, M, H, r, lda=2 * r, ldb=H, ldc=H, b_k=False, alpha=s,
-            accumulate=True, drop=_drop(pl, seeds, tsite(l, 3)), ld_drop=H)
-        _mm(dL[:, r:], st.av16[l], dxn, M, H, r, lda=2 * r, ldb=H, ldc=H, b_k=False, alpha=s,
-            accumulate=True, drop=_drop(pl, seeds, tsite(l, 4)), ld_drop=H)
-        # relative path: posQ = query_proj(rel) carries the q LoRA too
-        hu16 = ops.cast_bf16(hu, torch.empty(M, nh * 8, device=dev, dtype=bf))
-        Z = torch.zeros(nh * 8, H, device=dev)
-        _mm(hu16, sv.qkv[:, H:2 * H], Z, nh * 8, H, M, lda=nh * 8, ldb=3 * H, ldc=H, a_k=False,
-            b_k=False, accumulate=True)
-        zd = torch.diagonal(Z.view(nh, 8, nh, 64), dim1=0, dim2=2)              # [8, 64, nh]
-        gBq += s * zd.permute(2, 1, 0).reshape(H, 8)
+        # dB = dYᵀ·t (t = s·u lives in the augmented operand columns): rank-8 HBM streams
+        ops.skinny_wgrad(dqkv[:, :H], sv.xaug[:, H:H + r], gBq, H, ldc_m=r, ldc_c=1)
+        ops.skinny_wgrad(dqkv[:, 2 * H:], sv.xaug[:, H + r:H + 2 * r], gBv, H, ldc_m=r, ldc_c=1)
+        # dA = s·dLᵀ·drop(x);  dx += s·drop'(dL·A) for q and v in one pass over dx
+        ops.skinny_wgrad(sv.xq, dL[:, :r], gAq, H, ldc_m=1, ldc_c=H, alpha=s)
+        ops.skinny_wgrad(sv.xv, dL[:, r:], gAv, H, ldc_m=1, ldc_c=H, alpha=s)
+        ops.lora_dx(dL, st.aq16[l], st.av16[l], s, _drop(pl, seeds, tsite(l, 3)),
+                    _drop(pl, seeds, tsite(l, 4)), dxn, H)
+        # relative path: posQ = query_proj(rel) carries the q LoRA too:
+        # dBq[h·64 + d, c] += s·Σ_m K[m, h·64 + d]·HU[m, h, c]  (per-head slices of HU)
+        ops.skinny_wgrad(sv.qkv[:, H:2 * H], hu.view(M, nh * 8), gBq, H, ldc_m=r, ldc_c=1, alpha=s,
+                         group=64, sgs=8)
         du = torch.zeros(c.npos * 8, device=dev)
         ops.colsum(pb.view(B * nh, c.npos * 8), du)
         _mm(du, sv.relq, gAq, r, H, c.npos, lda=r, ldb=H, ldc=H, a_k=False, b_k=False, alpha=s,

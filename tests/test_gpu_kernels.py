@@ -118,6 +118,90 @@ def test_gemm_row_panel(gpu_pkg, M, N, K, epi):
     assert rel(Cb.float(), base + bias) < 8e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 1024, 128), (16300, 1000, 192), (65536, 256, 64),
+                                   (8192, 2304, 832)])
+@pytest.mark.parametrize("epi", ["plain", "res_drop", "gelu_grad", "relu_gate", "acc"])
+def test_gemm_big_tile(gpu_pkg, M, N, K, epi):
+    """256x256 LDS-DMA tile kernel (the mDeBERTa token GEMMs): every epilogue family it
+    takes, rows/columns not a multiple of the tile, and against the generic kernel."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    W = torch.randn(N, K, generator=g).to(torch.bfloat16).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    base = A.float() @ W.float().t()
+    kw, out_dt = {}, torch.float32
+    if epi == "plain":
+        v, out_dt = base + bias, torch.bfloat16
+        kw = dict(bias=bias)
+    elif epi == "res_drop":
+        res = torch.randn(M, N, generator=g).to(DEV)
+        p, seed = 0.1, 0x5EED1234ABCD
+        keep = keep_mask(seed, (M, N), p).float().to(DEV)
+        v = (base * 0.5 + bias) * keep / (1 - p) + res
+        kw = dict(alpha=0.5, bias=bias, drop=(p, seed_dev(seed)), ld_drop=N, residual=res, ld_res=N)
+    elif epi == "gelu_grad":
+        pre = torch.randn(M, N, generator=g).to(torch.bfloat16).to(DEV)
+        x = pre.float()
+        gg = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+        v, out_dt = base * gg, torch.bfloat16
+        kw = dict(act=3, gate=pre, ld_gate=N)
+    elif epi == "relu_gate":
+        gate = torch.randn(M, N, generator=g).to(torch.bfloat16).to(DEV)
+        v = torch.where(gate.float() > 0, torch.relu(base + bias) * 2.0, torch.zeros_like(base))
+        kw = dict(bias=bias, act=1, gate=gate, ld_gate=N, gate_scale=2.0)
+    else:
+        C0 = torch.randn(M, N, generator=g).to(DEV)
+        v = C0 + base
+        kw = dict(accumulate=True)
+    C = C0.clone() if epi == "acc" else torch.empty(M, N, device=DEV, dtype=out_dt)
+    ops.gemm(A, W, C, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True, ldc=N, **kw)
+    tol = (2e-5 * max(1.0, math.sqrt(K / 256))) if out_dt == torch.float32 else 8e-3
+    assert rel(C.float(), v) < tol, epi
+    assert torch.isfinite(C.float()).all()
+
+
+@pytest.mark.parametrize("s_dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("R,Mw,group,trans", [(65536, 768, 768, False), (3000, 768, 64, False),
+                                              (4099, 256, 256, True), (777, 64, 64, True)])
+def test_skinny_wgrad(gpu_pkg, s_dt, R, Mw, group, trans):
+    """Rank-8 LoRA gradient stream: C += alpha·Wᵀ·S with per-group S slices, both C layouts."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(R + Mw)
+    ngr = Mw // group
+    W = torch.randn(R, Mw + 8, generator=g).to(torch.bfloat16).to(DEV)[:, :Mw]
+    S = torch.randn(R, ngr * 8 + 8, generator=g).to(s_dt).to(DEV)[:, :ngr * 8]
+    C0 = torch.randn(8, Mw, generator=g) if trans else torch.randn(Mw, 8, generator=g)
+    C = C0.clone().to(DEV)
+    ops.skinny_wgrad(W, S, C, Mw, ldc_m=1 if trans else 8, ldc_c=Mw if trans else 1, alpha=0.5,
+                     group=group, sgs=8)
+    Wf, Sf = W.float().cpu(), S.float().cpu()
+    full = torch.einsum("rm,rgc->mgc", Wf, Sf.view(R, ngr, 8))        # [Mw, ngr, 8]
+    sel = full[torch.arange(Mw), torch.arange(Mw) // group]            # [Mw, 8]
+    expect = C0 + 0.5 * (sel.t() if trans else sel)
+    assert rel(C, expect) < 1e-5
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_lora_dx(gpu_pkg, p):
+    ops = gpu_pkg.ops
+    M, H = 5000, 768
+    g = torch.Generator().manual_seed(3)
+    dL = torch.randn(M, 16, generator=g).to(torch.bfloat16)
+    aq = torch.randn(8, H, generator=g).to(torch.bfloat16)
+    av = torch.randn(8, H, generator=g).to(torch.bfloat16)
+    dx0 = torch.randn(M, H, generator=g)
+    sq, sv = 0x1111222233334444, 0x5555666677778888
+    yq = 4.0 * dL[:, :8].float() @ aq.float()
+    yv = 4.0 * dL[:, 8:].float() @ av.float()
+    if p > 0:
+        yq = yq * keep_mask(sq, (M, H), p).float() / (1 - p)
+        yv = yv * keep_mask(sv, (M, H), p).float() / (1 - p)
+    dx = dx0.clone().to(DEV)
+    ops.lora_dx(dL.to(DEV), aq.to(DEV), av.to(DEV), 4.0, (p, seed_dev(sq)), (p, seed_dev(sv)), dx, H)
+    assert rel(dx, dx0 + yq + yv) < 1e-5
+
+
 def test_gemm_drop_rows(gpu_pkg):
     """Dropout through a row map (the pruned last layer's gathered rows)."""
     ops = gpu_pkg.ops

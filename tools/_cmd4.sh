@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 200 python tools/attn_bench.py > gpurun_out/attn.log 2>&1 || { cat gpurun_out/attn.log; exit 1; }
+cat gpurun_out/attn.log
+(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof4 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --config 4 --steps 3 --warmup 1 --skip-cpu) > gpurun_out/prof4.log 2>&1 || { tail -30 gpurun_out/prof4.log; exit 1; }
+tail -1 gpurun_out/prof4.log

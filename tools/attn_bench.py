@@ -42,8 +42,12 @@ def main(B=256, S=256, nh=12, reps=5):
                      mask, delta, scale, ctx, lse, drop, dctx=dctx, dq=dqkv[:, :H],
                      dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:], lora_u=u, lora_bq=bq, lora_hu=hu,
                      lora_pb=pb)
+    def bwd_nolora():
+        ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:],
+                     mask, delta, scale, ctx, lse, drop, dctx=dctx, dq=dqkv[:, :H],
+                     dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:])
     pairs = B * nh * (S // 64) ** 2
-    for name, fn, units in (("fwd", fwd, 6), ("bwd", bwd, 13)):
+    for name, fn, units in (("fwd", fwd, 6), ("bwd", bwd, 13), ("bwd-nolora", bwd_nolora, 13)):
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
