@@ -416,10 +416,13 @@ typedef struct ttmi_dis_attn_desc {
   const void* dctx; int64_t lddctx;
   void* dq; void* dk; void* dv; int64_t lddqkv;
   const float* lora_u; const float* lora_bq; float* lora_hu; float* lora_pb;
-  float* dq_scratch;      /* backward: fp32 [B·S, nh·64] workspace (dQ accumulation) */
+  float* dq_scratch;      /* backward: fp32 workspace of >= B·nh·S floats (D_i = dO_i·O_i) */
+  float* lora_pbx;        /* backward with LoRA: fp32 workspace of ttmi_dis_attn_pbx_floats()
+                             (per block pair, PB over the pair's expanded window rows) */
 } ttmi_dis_attn_desc;
 int ttmi_dis_attn_fwd(const ttmi_dis_attn_desc* d, hipStream_t stream);
 int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t stream);
+int64_t ttmi_dis_attn_pbx_floats(int B, int S, int nh);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
 int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
 /* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);

@@ -61,7 +61,7 @@ class DisAttnDesc(ctypes.Structure):
                 ("dctx", c_p), ("lddctx", ctypes.c_int64),
                 ("dq", c_p), ("dk", c_p), ("dv", c_p), ("lddqkv", ctypes.c_int64),
                 ("lora_u", c_p), ("lora_bq", c_p), ("lora_hu", c_p), ("lora_pb", c_p),
-                ("dq_scratch", c_p)]
+                ("dq_scratch", c_p), ("lora_pbx", c_p)]
 
 
 class LnBwdDesc(ctypes.Structure):
@@ -118,6 +118,7 @@ SIGNATURES = {
     "ttmi_mask_items": (c_i, [c_i, c_i, c_p, c_i64, c_p, c_i, c_p]),
     "ttmi_dis_attn_fwd": (c_i, [c_p, c_p]),
     "ttmi_dis_attn_bwd": (c_i, [c_p, c_p]),
+    "ttmi_dis_attn_pbx_floats": (ctypes.c_int64, [c_i, c_i, c_i]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,

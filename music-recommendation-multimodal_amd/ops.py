@@ -571,8 +571,11 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
     d.dctx, d.lddctx = _p(dctx), dctx.stride(0)
     d.dq, d.dk, d.dv, d.lddqkv = _p(dq), _p(dk), _p(dv), dq.stride(0)
     d.lora_u, d.lora_bq, d.lora_hu, d.lora_pb = _p(lora_u), _p(lora_bq), _p(lora_hu), _p(lora_pb)
-    scratch = torch.empty(B * S, H, device=q.device)          # fp32 dQ accumulation
+    scratch = torch.empty(B * nh * S, device=q.device)        # D_i = dO_i·O_i
     d.dq_scratch = _p(scratch)
+    if lora_u is not None:
+        pbx = torch.empty(int(_L.load().ttmi_dis_attn_pbx_floats(B, S, nh)), device=q.device)
+        d.lora_pbx = _p(pbx)
     call("ttmi_dis_attn_bwd", ctypes.byref(d), _s())
 
 
