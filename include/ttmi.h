@@ -400,8 +400,8 @@ int ttmi_deb_ln_fwd(int64_t M, int H, const float* z, const float* ln_w, const f
  * Backward: dq/dk/dv (bf16, lddqkv) from dctx, recomputing the scores; posK gets no gradient
  * (frozen).  With lora_u != NULL (the query_proj LoRA down-projection of the relative table,
  * [npos, 8] fp32) it also writes the rank-8 contractions that carry the LoRA gradient through
- * posQ = query_proj(rel): lora_hu [B·S, nh, 8] = Σ_i dS_ij·u[δ_ij] and lora_pb [B·nh, npos, 8]
- * = Σ_ij dS_ij·(K_j·Bq_h)[δ_ij], with lora_bq = lora_B of query_proj [nh·64, 8] fp32 and dS the
+ * posQ = query_proj(rel): lora_hu [B·S, nh, 8] = Σ_i dS_ij·u[δ_ij] and lora_pb [npos, 8]
+ * = Σ_{b,h} Σ_ij dS_ij·(K_j·Bq_h)[δ_ij] (overwritten), with lora_bq = lora_B of query_proj [nh·64, 8] fp32 and dS the
  * gradient of the unscaled score terms.  S <= 256. */
 typedef struct ttmi_dis_attn_desc {
   int B, S, nh, d_head, npos;

@@ -147,20 +147,35 @@ __global__ __launch_bounds__(256) void skinny_wgrad_kernel(int64_t R, int Mw, co
     for (int c = 0; c < 8; ++c) acc[i][c] = 0.f;
   if (rg < RG) {
     const int soff = (c8 * 8 / group) * sgs;
-    for (int64_t r = r0 + rg; r < r1; r += RG) {
-      float w[8], s[8];
-      unpack8(*reinterpret_cast<const uint4*>(W + r * ldw + c8 * 8), w);
-      if constexpr (sizeof(TS) == 2) {
-        unpack8(*reinterpret_cast<const uint4*>(S + r * lds + soff), s);
-      } else {
-        const float4 a = *reinterpret_cast<const float4*>(S + r * lds + soff);
-        const float4 b = *reinterpret_cast<const float4*>(S + r * lds + soff + 4);
-        s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+    // 4 rows per step: all loads issued before the FMAs (the loop is load-latency bound)
+    constexpr int U = 4;
+    for (int64_t rb = r0 + rg; rb < r1; rb += U * RG) {
+      uint4 wq[U], sq[U], sq2[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int64_t r = min(rb + k * RG, r1 - 1);
+        wq[k] = *reinterpret_cast<const uint4*>(W + r * ldw + c8 * 8);
+        sq[k] = *reinterpret_cast<const uint4*>(S + r * lds + soff);
+        if constexpr (sizeof(TS) == 4) sq2[k] = *reinterpret_cast<const uint4*>(S + r * lds + soff + 4);
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int k = 0; k < U; ++k) {
+        if (rb + k * RG >= r1) break;
+        float w[8], s[8];
+        unpack8(wq[k], w);
+        if constexpr (sizeof(TS) == 2) {
+          unpack8(sq[k], s);
+        } else {
+          s[0] = __uint_as_float(sq[k].x); s[1] = __uint_as_float(sq[k].y);
+          s[2] = __uint_as_float(sq[k].z); s[3] = __uint_as_float(sq[k].w);
+          s[4] = __uint_as_float(sq2[k].x); s[5] = __uint_as_float(sq2[k].y);
+          s[6] = __uint_as_float(sq2[k].z); s[7] = __uint_as_float(sq2[k].w);
+        }
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc[i][c] += w[i] * s[c];
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) acc[i][c] += w[i] * s[c];
+      }
     }
     float* dst = red + (int64_t)rg * Mw * 8 + c8 * 64;
 #pragma unroll

@@ -20,7 +20,7 @@
 //   dis_fwd_kernel   per (query block, head, batch): online softmax over key blocks -> ctx, lse
 //   dis_dq_kernel    per (query block, head, batch): recomputes P, writes dQ and D = dO·O
 //   dis_dkv_kernel   per (key block, head, batch): recomputes Pᵀ, writes dK, dV, HU, PBexp
-//   dis_pb_kernel    per (batch, head): bins PBexp rows to δ rows -> PB [B·nh, npos, 8]
+//   dis_pb_kernel    sums PBexp over (batch, head) and bins its rows to δ -> PB [npos, 8]
 // Per block pair each kernel has three barriers: after staging, after the shared window
 // product (p2c for the query-side kernels, c2p for dis_dkv), and before the next staging.
 // The c2p (query side) / p2c (key side) window is private to each wave and lives in the
@@ -96,7 +96,7 @@ struct DisArgs {
   const float* bq;                  // [nh·64, 8] LoRA B of query_proj
   float* hu;                        // [B·S, nh, 8]
   float* pbx;                       // [B·nh, nqb, nqb, 128, 8]
-  float* pb;                        // [B·nh, npos, 8]
+  float* pb;                        // [npos, 8] (summed over batch and heads)
 };
 
 TTMI_DEV int win_row(const DisArgs& a, int rel) {
@@ -539,23 +539,20 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
     *reinterpret_cast<float4*>(a.hu + ((rowb + j) * a.nh + h) * 8 + 4 * lg) = make_float4(hua[0], hua[1], hua[2], hua[3]);
 }
 
-// PB[bh][δ][c] = Σ_pairs Σ_{r: δ(i0 - j0 - 63 + r) = δ} PBexp[bh][pair][r][c]
+// PB[δ][c] = Σ_{b,h} Σ_pairs Σ_{r: δ(i0 - j0 - 63 + r) = δ} PBexp[b,h][pair][r][c]: each thread
+// sums one PBexp column over a chunk of (b,h) rows (coalesced 1 KB rows), then adds it to its
+// δ row (the r -> δ map depends only on the pair).  PB is zeroed by the launcher.
+constexpr int PB_ROWS = 64;
 __global__ __launch_bounds__(256) void dis_pb_kernel(DisArgs a) {
-  __shared__ float acc[512 * 8];
-  const int64_t bh = blockIdx.x;
-  for (int r = threadIdx.x; r < a.npos * 8; r += 256) acc[r] = 0.f;
-  __syncthreads();
-  const int np = a.nqb * a.nqb;
-  for (int p = 0; p < np; ++p) {
-    const int qb = p / a.nqb, kb = p % a.nqb;
-    const float* src = a.pbx + (bh * np + p) * WIN * 8;
-    for (int x = threadIdx.x; x < WIN * 8; x += 256) {
-      const int r = x >> 3, rel = qb * 64 - kb * 64 - 63 + r;
-      if (rel > -a.S && rel < a.S) atomicAdd(&acc[win_row(a, rel) * 8 + (x & 7)], src[x]);
-    }
-  }
-  __syncthreads();
-  for (int r = threadIdx.x; r < a.npos * 8; r += 256) a.pb[bh * a.npos * 8 + r] = acc[r];
+  const int np = a.nqb * a.nqb, ncol = np * WIN * 8;
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= ncol) return;
+  const int64_t r0 = (int64_t)blockIdx.y * PB_ROWS, r1 = min((int64_t)a.B * a.nh, r0 + PB_ROWS);
+  float v = 0.f;
+  for (int64_t bh = r0; bh < r1; ++bh) v += a.pbx[bh * ncol + col];
+  const int p = col / (WIN * 8), r = (col / 8) % WIN, c = col % 8;
+  const int rel = (p / a.nqb) * 64 - (p % a.nqb) * 64 - 63 + r;
+  if (rel > -a.S && rel < a.S) atomicAdd(a.pb + win_row(a, rel) * 8 + c, v);
 }
 
 }  // namespace
@@ -615,7 +612,13 @@ extern "C" int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
   const dim3 grid((unsigned)a.nqb, (unsigned)d->nh, (unsigned)d->B);
   hipLaunchKernelGGL(dis_dq_kernel, grid, dim3(256), 0, s, a);
   hipLaunchKernelGGL(dis_dkv_kernel, grid, dim3(256), 0, s, a);
-  if (d->lora_u)
-    hipLaunchKernelGGL(dis_pb_kernel, dim3((unsigned)((int64_t)d->B * d->nh)), dim3(256), 0, s, a);
+  if (d->lora_u) {
+    if (hipMemsetAsync(d->lora_pb, 0, (size_t)d->npos * 8 * sizeof(float), s) != hipSuccess)
+      return ttmi_check_launch("ttmi_dis_attn_bwd (pb memset)");
+    const int ncol = a.nqb * a.nqb * WIN * 8;
+    const int64_t rows = (int64_t)d->B * d->nh;
+    hipLaunchKernelGGL(dis_pb_kernel, dim3((unsigned)((ncol + 255) / 256), (unsigned)((rows + PB_ROWS - 1) / PB_ROWS)),
+                       dim3(256), 0, s, a);
+  }
   return ttmi_check_launch("ttmi_dis_attn_bwd");
 }

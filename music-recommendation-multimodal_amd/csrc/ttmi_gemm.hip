@@ -953,10 +953,27 @@ TTMI_DEV uint4 big_frag_b(const char* img, int row, int c, int lane) {
   return lds16(img + row * 128 + ch * 16);
 }
 
-// Epilogue of 8 consecutive columns n..n+7 of row m (v holds alpha·acc).
+// Epilogue families, specialised at compile time (EPI >= 0) so each instantiation's
+// straight-line epilogue stays small; EPI_ANY reads every flag at run time.
+enum BigEpi {
+  BE_BIAS = 1, BE_RELU = 2, BE_GELU = 4, BE_DROP = 8, BE_GELU_GRAD = 16, BE_RELU_GATE = 32,
+  BE_RES = 64, BE_F32 = 128, BE_ACC = 256, BE_ANY = -1
+};
+
+template <int EPI>
 TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t n, float* v) {
+  constexpr bool RT = EPI < 0;
+  const bool bias = RT ? g.bias != nullptr : (EPI & BE_BIAS);
+  const bool relu = RT ? g.act == 1 : (EPI & BE_RELU);
+  const bool gelu = RT ? g.act == 2 : (EPI & BE_GELU);
+  const bool drop = RT ? true : (EPI & BE_DROP);
+  const bool gate = RT ? g.gate != nullptr : (EPI & (BE_GELU_GRAD | BE_RELU_GATE));
+  const bool ggrad = RT ? g.act == 3 : (EPI & BE_GELU_GRAD);
+  const bool res = RT ? g.residual != nullptr : (EPI & BE_RES);
+  const bool f32 = RT ? g.c_f32 != 0 : (EPI & BE_F32);
+  const bool accum = RT ? g.c_mode == 1 : (EPI & BE_ACC);
   const bool full = n + 7 < g.N;
-  if (g.bias) {
+  if (bias) {
     if (full) {
       const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
       const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
@@ -967,24 +984,24 @@ TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t
       for (int e = 0; e < 8; ++e) v[e] += (n + e < g.N) ? g.bias[n + e] : 0.f;
     }
   }
-  if (g.act == 1) {
+  if (relu) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-  } else if (g.act == 2) {
+  } else if (gelu) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
   }
-  drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + n), v);
-  if (g.gate) {
+  if (drop) drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + n), v);
+  if (gate) {
     const int64_t o = m * g.ld_gate + n;
     float gv[8];
-    if (full && !g.gate_f32) {
+    if (full) {
       unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)g.gate + o), gv);
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) gv[e] = (n + e < g.N) ? ld_dyn(g.gate, o + e, g.gate_f32) : 0.f;
+      for (int e = 0; e < 8; ++e) gv[e] = (n + e < g.N) ? bf2f(((const bf16_t*)g.gate)[o + e]) : 0.f;
     }
-    if (g.act == 3) {
+    if (ggrad) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad(gv[e]);
     } else {
@@ -992,7 +1009,7 @@ TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t
       for (int e = 0; e < 8; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
     }
   }
-  if (g.residual) {
+  if (res) {
     const float* rp = g.residual + m * g.ld_res + n;
     if (full) {
       const float4 r0 = *reinterpret_cast<const float4*>(rp);
@@ -1005,11 +1022,11 @@ TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t
     }
   }
   const int64_t o = m * g.ldc + n;
-  if (g.c_mode == 1) {
+  if (accum) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       if (n + e < g.N) atomicAdd(reinterpret_cast<float*>(g.C) + o + e, v[e]);
-  } else if (full && g.c_f32) {
+  } else if (full && f32) {
     float* cp = reinterpret_cast<float*>(g.C) + o;
     *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -1017,10 +1034,11 @@ TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t
     *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + o) = pack8(v);
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) if (n + e < g.N) st_dyn(g.C, o + e, v[e], g.c_f32);
+    for (int e = 0; e < 8; ++e) if (n + e < g.N) st_dyn(g.C, o + e, v[e], f32);
   }
 }
 
+template <int EPI>
 __global__ __launch_bounds__(512) void gemm_big_kernel(BigArgs ba) {
   using namespace big;
   const GemmArgs& g = ba.g;
@@ -1166,7 +1184,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigArgs ba) {
         v[e] = g.alpha * acc[i][2 * p][e];
         v[4 + e] = g.alpha * acc[i][2 * p + 1][e];
       }
-      big_epi8(g, dk, m, n, v);
+      big_epi8<EPI>(g, dk, m, n, v);
     }
   }
 }
@@ -1189,14 +1207,39 @@ bool big_applies(const ttmi_gemm_desc* d) {
   return true;
 }
 
-int launch_big(const GemmArgs& a, hipStream_t s) {
+int big_epi_code(const ttmi_gemm_desc* d) {
+  if (d->drop_p > 0.f && d->drop_rows) return BE_ANY;
+  int e = 0;
+  if (d->bias) e |= BE_BIAS;
+  if (d->act == 1 && !d->gate) e |= BE_RELU;
+  if (d->act == 2) e |= BE_GELU;
+  if (d->drop_p > 0.f) e |= BE_DROP;
+  if (d->gate) e |= d->act == 3 ? BE_GELU_GRAD : BE_RELU_GATE;
+  if (d->residual) e |= BE_RES;
+  if (d->c_dtype == TTMI_F32) e |= BE_F32;
+  if (d->c_mode == 1) e |= BE_ACC;
+  return e;
+}
+
+int launch_big(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
   BigArgs ba;
   ba.g = a;
   ba.tiles_n = (int)((a.N + 255) / 256);
   const int64_t tiles = ((a.M + 255) / 256) * (int64_t)ba.tiles_n;
   TTMI_REQUIRE(tiles < (1ll << 31), "ttmi_gemm: grid too large");
   ba.tiles = (int)tiles;
-  hipLaunchKernelGGL(gemm_big_kernel, dim3((unsigned)tiles), dim3(512), 0, s, ba);
+  const dim3 grid((unsigned)tiles), blk(512);
+  switch (big_epi_code(d)) {
+    case BE_BIAS: hipLaunchKernelGGL(gemm_big_kernel<BE_BIAS>, grid, blk, 0, s, ba); break;
+    case 0: hipLaunchKernelGGL(gemm_big_kernel<0>, grid, blk, 0, s, ba); break;
+    case BE_BIAS | BE_DROP | BE_RES | BE_F32:
+      hipLaunchKernelGGL((gemm_big_kernel<BE_BIAS | BE_DROP | BE_RES | BE_F32>), grid, blk, 0, s, ba); break;
+    case BE_RES | BE_F32: hipLaunchKernelGGL((gemm_big_kernel<BE_RES | BE_F32>), grid, blk, 0, s, ba); break;
+    case BE_BIAS | BE_RES | BE_F32:
+      hipLaunchKernelGGL((gemm_big_kernel<BE_BIAS | BE_RES | BE_F32>), grid, blk, 0, s, ba); break;
+    case BE_GELU_GRAD: hipLaunchKernelGGL(gemm_big_kernel<BE_GELU_GRAD>, grid, blk, 0, s, ba); break;
+    default: hipLaunchKernelGGL(gemm_big_kernel<BE_ANY>, grid, blk, 0, s, ba); break;
+  }
   return ttmi_check_launch("ttmi_gemm");
 }
 
@@ -1342,7 +1385,7 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
           (!d->gate || (d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 16 == 0));
 
   if (panel_applies(d) && launch_panel(d, a, stream)) return ttmi_check_launch("ttmi_gemm");
-  if (big_applies(d)) return launch_big(a, stream);
+  if (big_applies(d)) return launch_big(d, a, stream);
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)split);
   if (d->dtype == TTMI_BF16) launch_typed<bf16_t>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
   else launch_typed<float>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);

@@ -566,7 +566,7 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
             raise ValueError(f"dis_attn: {name} must be [B·S, >= {H}]")
     if lora_u is not None:
         if lora_u.numel() < d.npos * 8 or lora_hu.numel() < B * S * nh * 8 or \
-                lora_pb.numel() < B * nh * d.npos * 8 or lora_bq.numel() < H * 8:
+                lora_pb.numel() < d.npos * 8 or lora_bq.numel() < H * 8:
             raise ValueError("dis_attn: LoRA buffers too small")
     d.dctx, d.lddctx = _p(dctx), dctx.stride(0)
     d.dq, d.dk, d.dv, d.lddqkv = _p(dq), _p(dk), _p(dv), dq.stride(0)

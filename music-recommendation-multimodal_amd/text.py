@@ -416,7 +416,7 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
         dqkv = torch.empty(M, 3 * H, device=dev, dtype=bf)
         bq32 = P[lp + "query_proj.lora_B.default.weight"].detach().contiguous()
         hu = torch.empty(M * nh * 8, device=dev)
-        pb = torch.empty(B * nh * c.npos * 8, device=dev)
+        pb = torch.empty(c.npos * 8, device=dev)                  # Σ over batch and heads
         ops.dis_attn(B, S, nh, sv.qkv[:, :H], sv.qkv[:, H:2 * H], sv.qkv[:, 2 * H:],
                      sv.posqk[:, :H], sv.posqk[:, H:], st.mask, st.delta, 1.0 / math.sqrt(64 * 3),
                      sv.ctx, sv.lse, _drop(pa, seeds, tsite(l, 0)), dctx=dctx, dq=dqkv[:, :H],
@@ -441,8 +441,7 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
         # dBq[h·64 + d, c] += s·Σ_m K[m, h·64 + d]·HU[m, h, c]  (per-head slices of HU)
         ops.skinny_wgrad(sv.qkv[:, H:2 * H], hu.view(M, nh * 8), gBq, H, ldc_m=r, ldc_c=1, alpha=s,
                          group=64, sgs=8)
-        du = torch.zeros(c.npos * 8, device=dev)
-        ops.colsum(pb.view(B * nh, c.npos * 8), du)
+        du = pb
         _mm(du, sv.relq, gAq, r, H, c.npos, lda=r, ldb=H, ldc=H, a_k=False, b_k=False, alpha=s,
             accumulate=True)
         dx = dxn
