@@ -467,6 +467,97 @@ def main_eval(args, world, rank, device):
         dist.destroy_process_group()
 
 
+def main_prep(args, world, rank, device):
+    """Item-modality preprocessing throughput (dataset.tex:23,38): per step
+    one batch of B items -> mel spectrogram of a 65,024-sample 22.05 kHz clip (128 frames x 128
+    mels, dB, min-max) + 300x300 uint8 cover -> 224x224 ImageNet-normalised NCHW.  Items/s over
+    all ranks; roofline of the FFT/mel kernel (algorithmic bytes: waveform read + mel write)."""
+    B = args.batch or 256
+    N = 65024
+    prep = pkg.preprocess
+    mel = prep.MelSpectrogram(device=device)
+    cov = prep.CoverTransform(224)
+    g = torch.Generator(device=device).manual_seed(rank)
+    waves = [torch.randn(B, N, device=device, generator=g) * 0.1 for _ in range(2)]
+    covers = [torch.randint(0, 256, (B, 300, 300, 3), device=device, generator=g, dtype=torch.uint8)
+              for _ in range(2)]
+
+    def step(i):
+        mel(waves[i % 2])
+        cov(covers[i % 2])
+
+    for i in range(max(args.warmup, 1)):
+        step(i)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    roof = None
+    if rank == 0:                                        # mel_power kernel, live, on its stream
+        st = torch.cuda.current_stream(device)
+        out = torch.empty(B, 128, 1 + N // 512, device=device)
+        mel.power(waves[0], out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(10):
+            mel.power(waves[0], out)
+        e1.record(st)
+        torch.cuda.synchronize(device)
+        sec = e0.elapsed_time(e1) / 1e3 / 10
+        F = 1 + N // 512
+        by = B * (N * 4 + 128 * F * 4)
+        gbs = by / sec / 1e9
+        roof = {"kernel": "mel_power_kernel (per-frame 2048-point LDS FFT + sparse Slaney filterbank)",
+                "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": read_traffic("mel_power_kernel"),
+                "avg_us": round(sec * 1e6, 2), "bytes_per_launch": by,
+                "note": "frames overlap 4x (hop 512 of 2048): each sample is read by 4 workgroups"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        from oracle import prep_ref as pr
+        import numpy as np
+        w = waves[0][:8].cpu().numpy()
+        c = covers[0][:8].cpu().numpy()
+        n, t0c = 0, time.perf_counter()
+        while True:
+            pr.log_mel(w[n % 8])
+            pr.cover_transform(c[n % 8])
+            n += 1
+            cel = time.perf_counter() - t0c
+            if cel >= min(args.cpu_budget, 15.0) or n >= 64:
+                break
+        cpu = {"value": round(n / cel, 2), "unit": "items/s", "cores": 1, "kind": "port",
+               "sample": f"{n} items (float64 numpy oracle: 65,024-sample log-mel + 300->224 cover), "
+                         f"{cel:.1f} s"}
+    if rank == 0:
+        line = {
+            "metric": "items/sec (GPU item preprocessing: 22.05 kHz clip -> 128x128 log-mel in [0,1] "
+                      "+ 300x300 cover -> 224x224 ImageNet-normalised), batch=256",
+            "value": round(world * B * args.steps / el, 1), "unit": "items/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (u8 covers)",
+            "data": "synthetic waveforms and covers",
+            "config": {"workload": "prep: SURVEY 8(f) rank 1, dataset.tex:23,38", "global_batch": world * B,
+                       "samples_per_clip": N, "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -474,7 +565,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU pairs (default: 512 for cfg 2, 256 for cfg 3)")
-    ap.add_argument("--config", default="2", choices=("2", "3", "4", "eval"),
+    ap.add_argument("--config", default="2", choices=("2", "3", "4", "eval", "prep"),
                     help="2 = BASELINE cfg 2 (the metric's configuration); 3 = full item "
                          "tower on raw mels/covers/tabular (BASELINE configs[2]); 4 = cfg 3 + "
                          "mDeBERTa-LoRA lyrics, S=256 (BASELINE configs[3]); eval = global "
@@ -493,6 +584,8 @@ def main():
     device = torch.device("cuda", local)
     if args.config == "eval":
         return main_eval(args, world, rank, device)
+    if args.config == "prep":
+        return main_prep(args, world, rank, device)
     cfg4 = args.config == "4"
     cfg3 = args.config == "3" or cfg4                    # cfg 4 = cfg 3 + text
     B = args.batch or (256 if cfg3 else 512)

@@ -449,6 +449,29 @@ int ttmi_lora_dx(int64_t M, int H, const uint16_t* dL, int64_t ld_dl, const uint
                  hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * Item-modality preprocessing (the batch contract of the reference's missing
+ * src/data/dataset.py; transforms per report/chapters/dataset.tex:23 and :38).
+ * ---------------------------------------------------------------------------------- */
+/* Mel power spectrogram (librosa 0.11 melspectrogram: center=True, pad_mode='constant',
+ * n_fft = 2048, periodic Hann `window` [2048], power 2): x [B, ldx] fp32 waveforms of N
+ * samples -> out [B, n_mels, 1 + N/hop].  twiddle [1024][2] = exp(-2πi k/2048); the filterbank
+ * is given sparsely: band m has band_len[m] weights band_w[band_off[m]..] on rfft bins
+ * band_start[m].. */
+int ttmi_mel_power(int B, int64_t N, const float* x, int64_t ldx, int hop, int n_mels,
+                   const float* window, const float* twiddle, const int* band_start,
+                   const int* band_len, const int* band_off, const float* band_w, float* out,
+                   hipStream_t stream);
+/* In place, per clip of n values: power_to_db(ref = max, amin, top_db) then min-max to [0,1]
+ * (a clip with no dynamic range becomes all zeros). */
+int ttmi_mel_db_minmax(int B, int64_t n, float amin, float top_db, float* mel, hipStream_t stream);
+/* Album covers: img = B uint8 HWC images (stride ld_img bytes) -> antialiased bilinear resize to
+ * OH x OW (align_corners = False) -> (v/255 - mean[c]) / std[c] (mean, std: 3 host floats) ->
+ * out_nchw fp32 [B, 3, OH, OW] and/or out_nhwc8 bf16 [B, OH, OW, 8] (channels 3..7 zero). */
+int ttmi_cover_prep(int B, int H, int W, const uint8_t* img, int64_t ld_img, int OH, int OW,
+                    const float* mean, const float* std, float* out_nchw, uint16_t* out_nhwc8,
+                    hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * Global retrieval (reference src/evaluate_metrics.py:107-192 calculate_metrics_global):
  * scores = û·Îᵀ (ttmi_gemm) then per row the top-K item indices.
  * ---------------------------------------------------------------------------------- */

@@ -11,6 +11,9 @@ from . import functional
 from . import cnn
 from . import text
 from . import retrieval
+from . import preprocess
+from . import data
+from .data import MultimodalDataset, DeviceCollator, DevicePrefetcher
 from .text import TextEncoder
 from .user_tower import SequentialUserEncoder
 from .item_tower import MultimodalItemEncoder
@@ -20,4 +23,5 @@ from .train import (FlatParams, GradSync, TrainStep, cleanup_ddp, setup_ddp,
 
 __all__ = ["lib", "ops", "functional", "cnn", "SequentialUserEncoder", "MultimodalItemEncoder",
            "TwoTowerModel", "infonce", "infonce_global", "TrainStep", "FlatParams", "GradSync", "setup_ddp",
-           "cleanup_ddp", "train_one_epoch"]
+           "cleanup_ddp", "train_one_epoch", "preprocess", "data", "MultimodalDataset", "DeviceCollator",
+           "DevicePrefetcher"]

@@ -262,10 +262,20 @@ def tabular_fwd(P: Dict[str, Tensor], x: Tensor, bufs: Dict[str, Tensor], seeds:
                 dtype=torch.bfloat16):
     """TabularEncoder (item_tower.py:85-98): Linear → BN1d → ReLU → Dropout → Linear."""
     dev = x.device
-    B = x.shape[0]
-    xc = ops.cast_bf16(x.contiguous().float(), torch.empty(x.shape, device=dev, dtype=dtype))
-    w0 = ops.cast_bf16(P["mlp.0.weight"].contiguous(),
-                       torch.empty(P["mlp.0.weight"].shape, device=dev, dtype=dtype))
+    B, T = x.shape
+    if T % 8:
+        # the reference's T (14 numerics + one-hot genres) is arbitrary: the GEMM operands
+        # are zero-padded to a 16-byte row (the padding columns contribute nothing)
+        Tp = (T + 7) // 8 * 8
+        xc = ops.dropout_to(x.contiguous().float(), torch.zeros(B, Tp, device=dev, dtype=dtype)[:, :T])
+        xc = xc.as_strided((B, Tp), (Tp, 1))
+        w0 = ops.dropout_to(P["mlp.0.weight"].contiguous(),
+                            torch.zeros(P["mlp.0.weight"].shape[0], Tp, device=dev, dtype=dtype)[:, :T])
+        w0 = w0.as_strided((w0.shape[0], Tp), (Tp, 1))
+    else:
+        xc = ops.cast_bf16(x.contiguous().float(), torch.empty(x.shape, device=dev, dtype=dtype))
+        w0 = ops.cast_bf16(P["mlp.0.weight"].contiguous(),
+                           torch.empty(P["mlp.0.weight"].shape, device=dev, dtype=dtype))
     w4 = ops.cast_bf16(P["mlp.4.weight"].contiguous(),
                        torch.empty(P["mlp.4.weight"].shape, device=dev, dtype=dtype))
     H1 = w0.shape[0]
@@ -296,7 +306,13 @@ def tabular_bwd(P: Dict[str, Tensor], st: TabSaved, dout: Tensor, grads: Dict[st
                       grads["mlp.1.weight"], grads["mlp.1.bias"], gate_scale=scale, gated=True)
     dzc = torch.empty(dz.shape, device=dev, dtype=st.y1.dtype)
     ops.dropout_bwd(dz, dzc, None)
-    ops.linear_dw(dzc, st.x, grads["mlp.0.weight"], grads["mlp.0.bias"])
+    gw = grads["mlp.0.weight"]
+    if st.x.shape[1] != gw.shape[1]:                  # zero-padded T (see tabular_fwd)
+        pad = torch.zeros(gw.shape[0], st.x.shape[1], device=dev)
+        ops.linear_dw(dzc, st.x, pad, grads["mlp.0.bias"])
+        gw.add_(pad[:, :gw.shape[1]])
+    else:
+        ops.linear_dw(dzc, st.x, gw, grads["mlp.0.bias"])
 
 
 # ---------------------------------------------------------------------------- modules
