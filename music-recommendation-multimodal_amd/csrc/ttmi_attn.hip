@@ -12,6 +12,8 @@
 // Tiles are padded: keys/queries to 64 rows, the head dim to DHP (32 or 64) with zeros.
 #include "ttmi_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int LP = 64;   // padded sequence length
@@ -304,6 +306,323 @@ void launch_bwd(int B, int L, int H, int Dh, const void* qkv, const int64_t* kv,
                      (const T*)qkv, kv, lse, (const T*)dctx, dp, (T*)dqkv, 1.f / sqrtf((float)Dh));
 }
 
+// ============================================================================================
+// bf16 path v2 (the cfg-2 step): same math, one wave per (sequence, head), laid out so every
+// global access is a full 16-byte vector and no operand is transposed on its way into LDS:
+//   * Q/K/V/dO head slices are staged with unconditional (row-clamped) 16-byte loads, all
+//     issued before the first LDS write, into row-major [64][DH] images;
+//   * scores are built as Sᵀ-tiles (MFMA row operand = K), so a lane holds 4 consecutive keys
+//     of one query row: the softmax reduces over 4 lanes, P·V takes P straight from registers
+//     and V through the transposing LDS read (ds_read_b64_tr_b16), and the output lane holds
+//     4 consecutive head columns -> 8-byte stores;
+//   * the backward writes dS / Pd once as packed 8-byte rows and reads them transposed for
+//     dK = dSᵀ·Q and dV = Pdᵀ·dO.
+
+typedef __attribute__((ext_vector_type(4))) short s16x4a_t;
+TTMI_DEV uint2 a_lds8(const char* p) { return *reinterpret_cast<const uint2*>(p); }
+TTMI_DEV uint2 a_tr8(const char* p) {
+  const s16x4a_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4a_t*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+// fragment (16 rows x 32 k) of a [row][k] bf16 image; k-chunk c
+template <int P>
+TTMI_DEV uint4 a_fk(const char* s, int row0, int c, int lane) {
+  const char* p = s + (row0 + (lane & 15)) * P + c * 64 + (lane >> 4) * 8;
+  const uint2 lo = a_lds8(p), hi = a_lds8(p + 32);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+// fragment (16 rows x 32 k) of a [k][row] bf16 image (transposing read)
+template <int P>
+TTMI_DEV uint4 a_ft(const char* s, int row0, int c, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const char* p = s + (c * 32 + 4 * g + (i >> 2)) * P + (row0 + 4 * (i & 3)) * 2;
+  const uint2 lo = a_tr8(p), hi = a_tr8(p + 16 * P);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+TTMI_DEV uint32_t a_pk2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+TTMI_DEV uint4 a_freg(const f32x4_t& lo, const f32x4_t& hi) {
+  return make_uint4(a_pk2(lo[0], lo[1]), a_pk2(lo[2], lo[3]), a_pk2(hi[0], hi[1]), a_pk2(hi[2], hi[3]));
+}
+TTMI_DEV void a_st4(void* p, const f32x4_t& v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(a_pk2(v[0], v[1]), a_pk2(v[2], v[3]));
+}
+
+template <int DH>
+struct Img2 {
+  static constexpr int P = DH * 2 + 16;          // [64][DH] image pitch
+  static constexpr int BYTES = 64 * P;
+  static constexpr int SP = 64 * 2 + 16;         // [64][64] image pitch
+  static constexpr int CPR = DH / 8;             // 16-byte chunks per row
+  static constexpr int PER = 64 * CPR / 64;      // chunks per lane
+};
+
+// [L rows][DH] slice (row stride ld) -> [64][DH] image; rows >= L zero.
+template <int DH, int NOP>
+TTMI_DEV void stage_heads(char* const (&dst)[NOP], const bf16_t* const (&src)[NOP], int64_t ld,
+                          int L, int lane) {
+  using G = Img2<DH>;
+  uint4 v[NOP][G::PER];
+#pragma unroll
+  for (int o = 0; o < NOP; ++o)
+#pragma unroll
+    for (int c = 0; c < G::PER; ++c) {
+      const int idx = lane + 64 * c, r = idx / G::CPR, ch = idx % G::CPR;
+      v[o][c] = *reinterpret_cast<const uint4*>(src[o] + (int64_t)min(r, L - 1) * ld + ch * 8);
+    }
+#pragma unroll
+  for (int o = 0; o < NOP; ++o)
+#pragma unroll
+    for (int c = 0; c < G::PER; ++c) {
+      const int idx = lane + 64 * c, r = idx / G::CPR, ch = idx % G::CPR;
+      *reinterpret_cast<uint4*>(dst[o] + r * G::P + ch * 16) = r < L ? v[o][c] : make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+template <int DH>
+__global__ __launch_bounds__(64) void mha2_fwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
+                                                      const int64_t* __restrict__ kvalid, DropParams dp,
+                                                      bf16_t* __restrict__ ctx, float* __restrict__ lse,
+                                                      float scale) {
+  using G = Img2<DH>;
+  __shared__ __attribute__((aligned(16))) char smem[3 * G::BYTES];
+  char* sQ = smem;
+  char* sK = sQ + G::BYTES;
+  char* sV = sK + G::BYTES;
+  const int lane = threadIdx.x, li = lane & 15, lg = lane >> 4;
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3LL * D;
+  const bf16_t* base = qkv + (int64_t)b * L * ld + (int64_t)h * DH;
+  {
+    char* const dst[3] = {sQ, sK, sV};
+    const bf16_t* const src[3] = {base, base + D, base + 2 * D};
+    stage_heads<DH, 3>(dst, src, ld, L, lane);
+  }
+  // key validity of the 4 keys 16t + 4lg + e this lane holds, per key tile t
+  bool kv[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 16 * t + 4 * lg + e;
+      kv[t][e] = k < L && kvalid[(int64_t)b * L + min(k, L - 1)] != 0;
+    }
+  __syncthreads();
+  const DropKeys dk = resolve_drop(dp);
+  const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
+  constexpr int NC = DH / 32;                      // 32-wide k chunks of the head dim
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (16 * i >= L) break;
+    const int q = 16 * i + li;
+    uint4 qf[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) qf[c] = a_fk<G::P>(sQ, 16 * i, c, lane);
+    f32x4_t s[4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (t <= i) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) Mma<bf16_t>::run(s[t], a_fk<G::P>(sK, 16 * t, c, lane), qf[c]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 16 * t + 4 * lg + e;
+        const bool ok = t <= i && kv[t][e] && k <= q && q < L;
+        s[t][e] = ok ? s[t][e] * scale : -INFINITY;
+        m = fmaxf(m, s[t][e]);
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float p = m == -INFINITY ? 0.f : __expf(s[t][e] - m);
+        s[t][e] = p;
+        sum += p;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float p = s[t][e] * inv;
+        const int k = 16 * t + 4 * lg + e;
+        if (dk.on && q < L && k < L) p = drop_apply(dk, pbase + (uint32_t)(q * L + k), p);
+        s[t][e] = p;
+      }
+    f32x4_t o[DH / 16];
+#pragma unroll
+    for (int u = 0; u < DH / 16; ++u) o[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {                  // 32-key chunks
+      if (32 * c > 16 * i + 15) break;
+      const uint4 pf = a_freg(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+      for (int u = 0; u < DH / 16; ++u) Mma<bf16_t>::run(o[u], a_ft<G::P>(sV, 16 * u, c, lane), pf);
+    }
+    if (q < L) {
+      bf16_t* dst = ctx + ((int64_t)b * L + q) * D + (int64_t)h * DH + 4 * lg;
+#pragma unroll
+      for (int u = 0; u < DH / 16; ++u) a_st4(dst + 16 * u, o[u]);
+      if (lg == 0) lse[(int64_t)bh * L + q] = m == -INFINITY ? INFINITY : m + __logf(sum);
+    }
+  }
+}
+
+template <int DH>
+__global__ __launch_bounds__(64) void mha2_bwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
+                                                      const int64_t* __restrict__ kvalid,
+                                                      const float* __restrict__ lse,
+                                                      const bf16_t* __restrict__ dctx, DropParams dp,
+                                                      bf16_t* __restrict__ dqkv, float scale) {
+  using G = Img2<DH>;
+  __shared__ __attribute__((aligned(16))) char smem[4 * G::BYTES + 2 * 64 * G::SP];
+  char* sQ = smem;
+  char* sK = sQ + G::BYTES;
+  char* sV = sK + G::BYTES;
+  char* sdO = sV + G::BYTES;
+  char* sdS = sdO + G::BYTES;                      // [q][k] bf16 (raw-score gradient · scale)
+  char* sPd = sdS + 64 * G::SP;                    // [q][k] bf16 (dropped probabilities)
+  const int lane = threadIdx.x, li = lane & 15, lg = lane >> 4;
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3LL * D;
+  const bf16_t* base = qkv + (int64_t)b * L * ld + (int64_t)h * DH;
+  {
+    char* const dst[4] = {sQ, sK, sV, sdO};
+    const bf16_t* const src[4] = {base, base + D, base + 2 * D, dctx + (int64_t)b * L * D + (int64_t)h * DH};
+    // dctx rows have stride D, qkv rows 3D: stage in two calls
+    char* const d3[3] = {dst[0], dst[1], dst[2]};
+    const bf16_t* const s3[3] = {src[0], src[1], src[2]};
+    stage_heads<DH, 3>(d3, s3, ld, L, lane);
+    char* const d1[1] = {dst[3]};
+    const bf16_t* const s1[1] = {src[3]};
+    stage_heads<DH, 1>(d1, s1, D, L, lane);
+  }
+  bool kv[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 16 * t + 4 * lg + e;
+      kv[t][e] = k < L && kvalid[(int64_t)b * L + min(k, L - 1)] != 0;
+    }
+  __syncthreads();
+  const DropKeys dk = resolve_drop(dp);
+  const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
+  constexpr int NC = DH / 32;
+  bf16_t* gq = dqkv + (int64_t)b * L * ld + (int64_t)h * DH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = 16 * i + li;
+    uint4 qf[NC], of[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      qf[c] = a_fk<G::P>(sQ, 16 * i, c, lane);
+      of[c] = a_fk<G::P>(sdO, 16 * i, c, lane);
+    }
+    const float lr = q < L ? lse[(int64_t)bh * L + q] : INFINITY;
+    f32x4_t s[4], dpv[4];
+    float dsum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = dpv[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (t <= i) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          Mma<bf16_t>::run(s[t], a_fk<G::P>(sK, 16 * t, c, lane), qf[c]);
+          Mma<bf16_t>::run(dpv[t], a_fk<G::P>(sV, 16 * t, c, lane), of[c]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 16 * t + 4 * lg + e;
+        const bool ok = t <= i && kv[t][e] && k <= q && q < L;
+        const float p = ok ? __expf(s[t][e] * scale - lr) : 0.f;
+        float dP = 0.f;
+        if (ok) {
+          dP = dpv[t][e];
+          if (dk.on) dP = drop_keep(dk, pbase + (uint32_t)(q * L + k)) ? dP * dk.scale : 0.f;
+        }
+        s[t][e] = p;
+        dpv[t][e] = dP;
+        dsum += p * dP;
+      }
+    }
+    dsum += __shfl_xor(dsum, 16, 64);
+    dsum += __shfl_xor(dsum, 32, 64);
+    f32x4_t ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4_t pd;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 16 * t + 4 * lg + e;
+        const float p = s[t][e];
+        ds[t][e] = p * (dpv[t][e] - dsum) * scale;
+        float x = p;
+        if (dk.on && p != 0.f) x = drop_keep(dk, pbase + (uint32_t)(q * L + k)) ? p * dk.scale : 0.f;
+        pd[e] = x;
+      }
+      a_st4(sdS + q * G::SP + (16 * t + 4 * lg) * 2, ds[t]);
+      a_st4(sPd + q * G::SP + (16 * t + 4 * lg) * 2, pd);
+    }
+    // dQ rows of this tile = dS·K (K through the transposing read)
+    f32x4_t dq[DH / 16];
+#pragma unroll
+    for (int u = 0; u < DH / 16; ++u) dq[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (32 * c > 16 * i + 15) break;
+      const uint4 af = a_freg(ds[2 * c], ds[2 * c + 1]);
+#pragma unroll
+      for (int u = 0; u < DH / 16; ++u) Mma<bf16_t>::run(dq[u], a_ft<G::P>(sK, 16 * u, c, lane), af);
+    }
+    if (q < L) {
+      bf16_t* dst = gq + (int64_t)q * ld + 4 * lg;
+#pragma unroll
+      for (int u = 0; u < DH / 16; ++u) a_st4(dst + 16 * u, dq[u]);
+    }
+  }
+  __syncthreads();
+  // dK = dSᵀ·Q and dV = Pdᵀ·dO per key tile t (query rows >= 16t only: causal)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (16 * t >= L) break;
+    f32x4_t dkv[DH / 16], dvv[DH / 16];
+#pragma unroll
+    for (int u = 0; u < DH / 16; ++u) dkv[u] = dvv[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {                  // 32-query chunks
+      if (32 * c + 31 < 16 * t) continue;
+      const uint4 as = a_ft<G::SP>(sdS, 16 * t, c, lane), ap = a_ft<G::SP>(sPd, 16 * t, c, lane);
+#pragma unroll
+      for (int u = 0; u < DH / 16; ++u) {
+        Mma<bf16_t>::run(dkv[u], a_ft<G::P>(sQ, 16 * u, c, lane), as);
+        Mma<bf16_t>::run(dvv[u], a_ft<G::P>(sdO, 16 * u, c, lane), ap);
+      }
+    }
+    const int k = 16 * t + li;
+    if (k < L) {
+      bf16_t* dst = gq + (int64_t)k * ld + 4 * lg;
+#pragma unroll
+      for (int u = 0; u < DH / 16; ++u) {
+        a_st4(dst + D + 16 * u, dkv[u]);
+        a_st4(dst + 2 * D + 16 * u, dvv[u]);
+      }
+    }
+  }
+}
+
+
 int check_mha(const char* fn, int dtype, int B, int L, int H, int Dh, const void* qkv,
               const int64_t* kv) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "%s: bad dtype", fn);
@@ -326,7 +645,16 @@ extern "C" int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* 
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_mha_fwd: drop_p out of [0,1)");
   if (B == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
-  if (dtype == TTMI_BF16) {
+  if (dtype == TTMI_BF16 && (Dh == 32 || Dh == 64) && !getenv("TTMI_MHA_V1")) {
+    TTMI_REQUIRE(((uintptr_t)ctx & 7) == 0, "ttmi_mha_fwd: ctx must be 8-byte aligned");
+    const float sc = 1.f / sqrtf((float)Dh);
+    if (Dh == 32)
+      hipLaunchKernelGGL(mha2_fwd_kernel<32>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+                         key_valid, dp, (bf16_t*)ctx, lse, sc);
+    else
+      hipLaunchKernelGGL(mha2_fwd_kernel<64>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+                         key_valid, dp, (bf16_t*)ctx, lse, sc);
+  } else if (dtype == TTMI_BF16) {
     if (Dh <= 32) launch_fwd<bf16_t, 32>(B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
     else launch_fwd<bf16_t, 64>(B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
   } else {
@@ -346,7 +674,16 @@ extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* 
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_mha_bwd: drop_p out of [0,1)");
   if (B == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
-  if (dtype == TTMI_BF16) {
+  if (dtype == TTMI_BF16 && (Dh == 32 || Dh == 64) && !getenv("TTMI_MHA_V1")) {
+    TTMI_REQUIRE(((uintptr_t)dqkv & 7) == 0, "ttmi_mha_bwd: dqkv must be 8-byte aligned");
+    const float sc = 1.f / sqrtf((float)Dh);
+    if (Dh == 32)
+      hipLaunchKernelGGL(mha2_bwd_kernel<32>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+                         key_valid, lse, (const bf16_t*)dctx, dp, (bf16_t*)dqkv, sc);
+    else
+      hipLaunchKernelGGL(mha2_bwd_kernel<64>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+                         key_valid, lse, (const bf16_t*)dctx, dp, (bf16_t*)dqkv, sc);
+  } else if (dtype == TTMI_BF16) {
     if (Dh <= 32) launch_bwd<bf16_t, 32>(B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);
     else launch_bwd<bf16_t, 64>(B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);
   } else {
@@ -355,3 +692,4 @@ extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* 
   }
   return ttmi_check_launch("ttmi_mha_bwd");
 }
+
