@@ -110,11 +110,14 @@ int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, 
                        float drop_p, const uint64_t* drop_seed, float* x, float* mean, float* rstd,
                        hipStream_t stream);
 /* Backward: dE[ids] += g (rows with ids == padding_idx skipped, nn.Embedding(padding_idx=0)
- * user_tower.py:27), dP[l] += Σ_b g, dw/db += LN affine grads.  All accumulate (fp32). */
+ * user_tower.py:27), dP[l] += Σ_b g, dw/db += LN affine grads.  All accumulate (fp32).
+ * ws: ttmi_seq_embed_bwd_workspace(L, D) bytes, zero on entry and left zero on return (the
+ * per-position LN-grad partials; one buffer may serve every call on one stream). */
+int64_t ttmi_seq_embed_bwd_workspace(int L, int D);
 int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const float* E,
                        const float* P, const float* w, const float* mean, const float* rstd,
                        float drop_p, const uint64_t* drop_seed, const float* dx, float* dE, float* dP,
-                       float* dw, float* db, int64_t padding_idx, hipStream_t stream);
+                       float* dw, float* db, int64_t padding_idx, void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Multi-head self-attention core (SDPA inside nn.MultiheadAttention, user_tower.py:111-116):

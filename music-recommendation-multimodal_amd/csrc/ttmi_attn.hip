@@ -353,33 +353,35 @@ struct Img2 {
   static constexpr int BYTES = 64 * P;
   static constexpr int SP = 64 * 2 + 16;         // [64][64] image pitch
   static constexpr int CPR = DH / 8;             // 16-byte chunks per row
-  static constexpr int PER = 64 * CPR / 64;      // chunks per lane
 };
 
-// [L rows][DH] slice (row stride ld) -> [64][DH] image; rows >= L zero.
+// [L rows][DH] slice (row stride ld) -> [64][DH] image; rows >= L zero.  256 threads.
 template <int DH, int NOP>
 TTMI_DEV void stage_heads(char* const (&dst)[NOP], const bf16_t* const (&src)[NOP], int64_t ld,
                           int L, int lane) {
   using G = Img2<DH>;
-  uint4 v[NOP][G::PER];
+  constexpr int NT = 256;
+  static_assert((64 * G::CPR) % NT == 0, "head slice must split evenly over the workgroup");
+  constexpr int PER = 64 * G::CPR / NT;
+  uint4 v[NOP][PER];
 #pragma unroll
   for (int o = 0; o < NOP; ++o)
 #pragma unroll
-    for (int c = 0; c < G::PER; ++c) {
-      const int idx = lane + 64 * c, r = idx / G::CPR, ch = idx % G::CPR;
+    for (int c = 0; c < PER; ++c) {
+      const int idx = lane + NT * c, r = idx / G::CPR, ch = idx % G::CPR;
       v[o][c] = *reinterpret_cast<const uint4*>(src[o] + (int64_t)min(r, L - 1) * ld + ch * 8);
     }
 #pragma unroll
   for (int o = 0; o < NOP; ++o)
 #pragma unroll
-    for (int c = 0; c < G::PER; ++c) {
-      const int idx = lane + 64 * c, r = idx / G::CPR, ch = idx % G::CPR;
+    for (int c = 0; c < PER; ++c) {
+      const int idx = lane + NT * c, r = idx / G::CPR, ch = idx % G::CPR;
       *reinterpret_cast<uint4*>(dst[o] + r * G::P + ch * 16) = r < L ? v[o][c] : make_uint4(0u, 0u, 0u, 0u);
     }
 }
 
 template <int DH>
-__global__ __launch_bounds__(64) void mha2_fwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
                                                       const int64_t* __restrict__ kvalid, DropParams dp,
                                                       bf16_t* __restrict__ ctx, float* __restrict__ lse,
                                                       float scale) {
@@ -388,15 +390,16 @@ __global__ __launch_bounds__(64) void mha2_fwd_kernel(int L, int H, const bf16_t
   char* sQ = smem;
   char* sK = sQ + G::BYTES;
   char* sV = sK + G::BYTES;
-  const int lane = threadIdx.x, li = lane & 15, lg = lane >> 4;
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  // the H heads of one sequence read the same QKV rows: keep them on one XCD
+  const int bh = xcd_contiguous(blockIdx.x, gridDim.x), b = bh / H, h = bh % H;
   const int D = H * DH;
   const int64_t ld = 3LL * D;
   const bf16_t* base = qkv + (int64_t)b * L * ld + (int64_t)h * DH;
   {
     char* const dst[3] = {sQ, sK, sV};
     const bf16_t* const src[3] = {base, base + D, base + 2 * D};
-    stage_heads<DH, 3>(dst, src, ld, L, lane);
+    stage_heads<DH, 3>(dst, src, ld, L, threadIdx.x);
   }
   // key validity of the 4 keys 16t + 4lg + e this lane holds, per key tile t
   bool kv[4][4];
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(64) void mha2_fwd_kernel(int L, int H, const bf16_t
   const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
   constexpr int NC = DH / 32;                      // 32-wide k chunks of the head dim
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = wave; i < 4; i += 4) {      // wave w owns query tile w
     if (16 * i >= L) break;
     const int q = 16 * i + li;
     uint4 qf[NC];
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(64) void mha2_fwd_kernel(int L, int H, const bf16_t
 }
 
 template <int DH>
-__global__ __launch_bounds__(64) void mha2_bwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
                                                       const int64_t* __restrict__ kvalid,
                                                       const float* __restrict__ lse,
                                                       const bf16_t* __restrict__ dctx, DropParams dp,
@@ -491,8 +494,9 @@ __global__ __launch_bounds__(64) void mha2_bwd_kernel(int L, int H, const bf16_t
   char* sdO = sV + G::BYTES;
   char* sdS = sdO + G::BYTES;                      // [q][k] bf16 (raw-score gradient · scale)
   char* sPd = sdS + 64 * G::SP;                    // [q][k] bf16 (dropped probabilities)
-  const int lane = threadIdx.x, li = lane & 15, lg = lane >> 4;
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  // the H heads of one sequence read the same QKV rows: keep them on one XCD
+  const int bh = xcd_contiguous(blockIdx.x, gridDim.x), b = bh / H, h = bh % H;
   const int D = H * DH;
   const int64_t ld = 3LL * D;
   const bf16_t* base = qkv + (int64_t)b * L * ld + (int64_t)h * DH;
@@ -502,10 +506,10 @@ __global__ __launch_bounds__(64) void mha2_bwd_kernel(int L, int H, const bf16_t
     // dctx rows have stride D, qkv rows 3D: stage in two calls
     char* const d3[3] = {dst[0], dst[1], dst[2]};
     const bf16_t* const s3[3] = {src[0], src[1], src[2]};
-    stage_heads<DH, 3>(d3, s3, ld, L, lane);
+    stage_heads<DH, 3>(d3, s3, ld, L, threadIdx.x);
     char* const d1[1] = {dst[3]};
     const bf16_t* const s1[1] = {src[3]};
-    stage_heads<DH, 1>(d1, s1, D, L, lane);
+    stage_heads<DH, 1>(d1, s1, D, L, threadIdx.x);
   }
   bool kv[4][4];
 #pragma unroll
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(64) void mha2_bwd_kernel(int L, int H, const bf16_t
   constexpr int NC = DH / 32;
   bf16_t* gq = dqkv + (int64_t)b * L * ld + (int64_t)h * DH;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = wave; i < 4; i += 4) {      // wave w owns query tile w
     const int q = 16 * i + li;
     uint4 qf[NC], of[NC];
 #pragma unroll
@@ -595,7 +599,7 @@ __global__ __launch_bounds__(64) void mha2_bwd_kernel(int L, int H, const bf16_t
   __syncthreads();
   // dK = dSᵀ·Q and dV = Pdᵀ·dO per key tile t (query rows >= 16t only: causal)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = wave; t < 4; t += 4) {      // wave w owns key tile w
     if (16 * t >= L) break;
     f32x4_t dkv[DH / 16], dvv[DH / 16];
 #pragma unroll
@@ -649,10 +653,10 @@ extern "C" int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* 
     TTMI_REQUIRE(((uintptr_t)ctx & 7) == 0, "ttmi_mha_fwd: ctx must be 8-byte aligned");
     const float sc = 1.f / sqrtf((float)Dh);
     if (Dh == 32)
-      hipLaunchKernelGGL(mha2_fwd_kernel<32>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+      hipLaunchKernelGGL(mha2_fwd_kernel<32>, dim3(B * H), dim3(256), 0, s, L, H, (const bf16_t*)qkv,
                          key_valid, dp, (bf16_t*)ctx, lse, sc);
     else
-      hipLaunchKernelGGL(mha2_fwd_kernel<64>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+      hipLaunchKernelGGL(mha2_fwd_kernel<64>, dim3(B * H), dim3(256), 0, s, L, H, (const bf16_t*)qkv,
                          key_valid, dp, (bf16_t*)ctx, lse, sc);
   } else if (dtype == TTMI_BF16) {
     if (Dh <= 32) launch_fwd<bf16_t, 32>(B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
@@ -678,10 +682,10 @@ extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* 
     TTMI_REQUIRE(((uintptr_t)dqkv & 7) == 0, "ttmi_mha_bwd: dqkv must be 8-byte aligned");
     const float sc = 1.f / sqrtf((float)Dh);
     if (Dh == 32)
-      hipLaunchKernelGGL(mha2_bwd_kernel<32>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+      hipLaunchKernelGGL(mha2_bwd_kernel<32>, dim3(B * H), dim3(256), 0, s, L, H, (const bf16_t*)qkv,
                          key_valid, lse, (const bf16_t*)dctx, dp, (bf16_t*)dqkv, sc);
     else
-      hipLaunchKernelGGL(mha2_bwd_kernel<64>, dim3(B * H), dim3(64), 0, s, L, H, (const bf16_t*)qkv,
+      hipLaunchKernelGGL(mha2_bwd_kernel<64>, dim3(B * H), dim3(256), 0, s, L, H, (const bf16_t*)qkv,
                          key_valid, lse, (const bf16_t*)dctx, dp, (bf16_t*)dqkv, sc);
   } else if (dtype == TTMI_BF16) {
     if (Dh <= 32) launch_bwd<bf16_t, 32>(B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);

@@ -116,6 +116,15 @@ static inline DropParams make_drop(float p, const uint64_t* seed) {
   return d;
 }
 
+// ---------------------------------------------------------------- XCD-aware block order
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  This bijection of
+// [0, n) gives each XCD a contiguous run of logical ids, so neighbouring logical blocks that
+// read the same rows share one L2.
+TTMI_DEV int xcd_contiguous(int bid, int n) {
+  const int xcd = bid & 7, q = n >> 3, rem = n & 7;
+  return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+}
+
 // ---------------------------------------------------------------- wave reductions
 TTMI_DEV float wave_sum(float v) {
 #pragma unroll

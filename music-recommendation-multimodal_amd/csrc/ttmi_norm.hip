@@ -67,8 +67,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
   }
 }
 
-// Per-block reduction of per-lane column partials (4 waves) followed by one atomic per column.
-template <int NV>
+// Per-block reduction of per-lane column partials (W waves) followed by one atomic per column.
+template <int NV, int W = 4>
 TTMI_DEV void block_col_atomic(float (&acc)[NV], int D, float* dst, float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();
@@ -79,7 +79,9 @@ TTMI_DEV void block_col_atomic(float (&acc)[NV], int D, float* dst, float* red) 
   }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    const float t = red[c] + red[64 * NV + c] + red[2 * 64 * NV + c] + red[3 * 64 * NV + c];
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < W; ++k) t += red[k * 64 * NV + c];
     atomicAdd(dst + c, t);
   }
 }
@@ -180,16 +182,19 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
   }
 }
 
-// Backward: block (l, b-chunk); each wave walks b = chunk*bpc + wave, +4, ... so the
-// position gradient dP[l] accumulates in registers (one atomic per column per block).
+// Backward: block (l, b-chunk) of SEB_W waves; each wave walks b = chunk*bpc + wave,
+// + SEB_W, ... so the position gradient dP[l] accumulates in registers (one atomic per column
+// per block).  The chunk is sized so a wave makes ONE pass of U rows: the kernel is a
+// dependent-gather latency chain (ids -> E[id]), so waves, not rows per wave, hide it.
+constexpr int SEB_W = 8;
 template <int NV>
-__global__ __launch_bounds__(256) void seq_embed_bwd_kernel(
+__global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
     int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E,
     const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ mean,
     const float* __restrict__ rstd, DropParams dp, const float* __restrict__ dx,
-    float* __restrict__ dE, float* __restrict__ dP, float* __restrict__ dw, float* __restrict__ db,
-    int64_t padding_idx, int64_t V, int bpc) {
-  __shared__ float red[4 * 64 * NV];
+    float* __restrict__ dE, float* __restrict__ dP, float* __restrict__ ws, int64_t padding_idx,
+    int64_t V, int bpc) {
+  __shared__ float red[SEB_W * 64 * NV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l = blockIdx.x;
   const int b0 = blockIdx.y * bpc;
@@ -199,44 +204,107 @@ __global__ __launch_bounds__(256) void seq_embed_bwd_kernel(
   float ap[NV], aw[NV], ab[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) ap[i] = aw[i] = ab[i] = 0.f;
-  for (int bb = b0 + wave; bb < b1; bb += 4) {
-    const int64_t row = (int64_t)bb * L + l;
-    const int64_t id = ids[row];
-    const bool ok = id >= 0 && id < V;
-    const float mu = mean[row], rs = rstd[row];
-    float g[NV], xh[NV];
-    float s1 = 0.f, s2 = 0.f;
+  // two rows per wave per iteration, every load of both issued before any arithmetic (the
+  // loop is latency-bound: ids -> E[id] is a dependent gather)
+  constexpr int U = 2;
+  for (int bq = b0 + wave; bq < b1; bq += SEB_W * U) {
+    int64_t row[U], id[U];
+    bool ok[U], live[U];
+    float mu[U], rs[U], d[U][NV], e[U][NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
-      g[i] = 0.f; xh[i] = 0.f;
-      if (c < D) {
-        float d = dx[row * D + c];
-        if (dk.on) d = drop_keep(dk, (uint32_t)(row * D + c)) ? d * dk.scale : 0.f;
-        const float e = (ok ? E[id * D + c] : 0.f) + P[(int64_t)l * D + c];
-        xh[i] = (e - mu) * rs;
-        aw[i] += d * xh[i];
-        ab[i] += d;
-        g[i] = d * w[c];
-        s1 += g[i];
-        s2 += g[i] * xh[i];
+    for (int u = 0; u < U; ++u) {
+      live[u] = bq + SEB_W * u < b1;
+      row[u] = (int64_t)min(bq + SEB_W * u, b1 - 1) * L + l;
+      id[u] = ids[row[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ok[u] = id[u] >= 0 && id[u] < V;
+      const int64_t er = ok[u] ? id[u] : 0;
+      mu[u] = mean[row[u]];
+      rs[u] = rstd[row[u]];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = min(lane + 64 * i, D - 1);
+        d[u][i] = dx[row[u] * D + c];
+        e[u][i] = E[er * D + c];
       }
     }
-    const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
-    const bool emb = ok && id != padding_idx;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < D) {
-        const float o = rs * (g[i] - c1 - xh[i] * c2);
-        ap[i] += o;
-        if (emb) atomicAdd(dE + id * D + c, o);
+    for (int u = 0; u < U; ++u) {
+      if (!live[u]) continue;
+      float g[NV], xh[NV];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = lane + 64 * i;
+        g[i] = 0.f; xh[i] = 0.f;
+        if (c < D) {
+          float dd = d[u][i];
+          if (dk.on) dd = drop_keep(dk, (uint32_t)(row[u] * D + c)) ? dd * dk.scale : 0.f;
+          const float ev = (ok[u] ? e[u][i] : 0.f) + P[(int64_t)l * D + c];
+          xh[i] = (ev - mu[u]) * rs[u];
+          aw[i] += dd * xh[i];
+          ab[i] += dd;
+          g[i] = dd * w[c];
+          s1 += g[i];
+          s2 += g[i] * xh[i];
+        }
+      }
+      const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
+      const bool emb = ok[u] && id[u] != padding_idx;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = lane + 64 * i;
+        if (c < D) {
+          const float o = rs[u] * (g[i] - c1 - xh[i] * c2);
+          ap[i] += o;
+          if (emb) atomicAdd(dE + id[u] * D + c, o);
+        }
       }
     }
   }
-  block_col_atomic(ap, D, dP + (int64_t)l * D, red);
-  block_col_atomic(aw, D, dw, red);
-  block_col_atomic(ab, D, db, red);
+  block_col_atomic<NV, SEB_W>(ap, D, dP + (int64_t)l * D, red);
+  // LN weight / bias partials go to this position's slot of the workspace: adders per address
+  // = chunks, not every block of the grid (same-address float atomics serialise)
+  block_col_atomic<NV, SEB_W>(aw, D, ws + (int64_t)l * 2 * D, red);
+  block_col_atomic<NV, SEB_W>(ab, D, ws + (int64_t)l * 2 * D + D, red);
+}
+
+// dw += Σ_l ws[l][0], db += Σ_l ws[l][1]; leaves the workspace zero for the next call.
+// 1024 threads = 4 position groups x 256 columns; each thread loads its positions first
+// (independent loads), then zeroes them; the 4 partials meet in LDS.
+__global__ __launch_bounds__(1024) void seq_embed_red_kernel(int L, int D, float* __restrict__ ws,
+                                                             float* __restrict__ dw,
+                                                             float* __restrict__ db) {
+  __shared__ float red[4][256];
+  const int cl = threadIdx.x & 255, lg = threadIdx.x >> 8;
+  const int c = blockIdx.x * 256 + cl;
+  const bool ok = c < 2 * D;
+  float s = 0.f;
+  if (ok) {
+    constexpr int U = 8;
+    for (int l0 = lg; l0 < L; l0 += 4 * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int l = l0 + 4 * u;
+        v[u] = l < L ? ws[(int64_t)l * 2 * D + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int l = l0 + 4 * u;
+        s += v[u];
+        if (l < L) ws[(int64_t)l * 2 * D + c] = 0.f;
+      }
+    }
+  }
+  red[lg][cl] = s;
+  __syncthreads();
+  if (lg != 0 || !ok) return;
+  s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  if (c < D) dw[c] += s;
+  else db[c - D] += s;
 }
 
 // ------------------------------------------------------------ last-valid gather + concat
@@ -397,6 +465,123 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(int B, int C, const float* 
   }
 }
 
+// Register-resident BatchNorm1d for B <= BNR_RG * RPT (the fusion / tabular heads, B = 256-512):
+// 512 threads = BNR_COLS columns x BNR_RG row groups; every thread loads its RPT values of
+// one column ONCE (all loads issued before any arithmetic), so the statistics, the
+// normalisation and the backward's two sums cost one HBM latency instead of B / 16 serial
+// dependent loads per pass.  Numerics equal the looped kernels (two-pass mean / variance).
+constexpr int BNR_COLS = 16, BNR_RG = 32;
+
+TTMI_DEV float bnr_colsum(float v, float (*red)[BNR_COLS], int rg, int cl) {
+  __syncthreads();
+  red[rg][cl] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < BNR_RG; ++k) s += red[k][cl];
+  return s;
+}
+
+template <typename T, int RPT>
+__global__ __launch_bounds__(512) void bnr_fwd_kernel(int B, int C, const float* __restrict__ z,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ b, float eps,
+                                                      float momentum, float* running_mean,
+                                                      float* running_var, int64_t* nbt, int relu,
+                                                      DropParams dp, T* __restrict__ y,
+                                                      float* __restrict__ mean,
+                                                      float* __restrict__ rstd) {
+  __shared__ float red[BNR_RG][BNR_COLS];
+  const int cl = threadIdx.x % BNR_COLS, rg = threadIdx.x / BNR_COLS;
+  const int c = blockIdx.x * BNR_COLS + cl;
+  const int cc = min(c, C - 1);
+  float v[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) v[j] = z[(int64_t)min(rg + BNR_RG * j, B - 1) * C + cc];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) s += rg + BNR_RG * j < B ? v[j] : 0.f;
+  const float mu = bnr_colsum(s, red, rg, cl) / (float)B;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const float d = v[j] - mu;
+    q += rg + BNR_RG * j < B ? d * d : 0.f;
+  }
+  const float var = bnr_colsum(q, red, rg, cl) / (float)B;
+  const float rs = 1.f / sqrtf(var + eps);
+  if (c >= C) return;
+  const DropKeys dk = resolve_drop(dp);
+  const float wc = w[c], bc = b[c];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = rg + BNR_RG * j;
+    if (r < B) {
+      float o = (v[j] - mu) * rs * wc + bc;
+      if (relu) o = fmaxf(o, 0.f);
+      if (dk.on) o = drop_apply(dk, (uint32_t)((int64_t)r * C + c), o);
+      stf<T>(y, (int64_t)r * C + c, o);
+    }
+  }
+  if (rg == 0) {
+    if (mean) mean[c] = mu;
+    if (rstd) rstd[c] = rs;
+    if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
+    if (running_var)
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * var * ((float)B / (float)(B - 1));
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+}
+
+template <typename T, int RPT>
+__global__ __launch_bounds__(512) void bnr_bwd_kernel(int B, int C, const float* __restrict__ dy,
+                                                      const float* __restrict__ z,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd,
+                                                      const T* __restrict__ y, float gate_scale,
+                                                      int gated, float* __restrict__ dz,
+                                                      float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[BNR_RG][BNR_COLS];
+  const int cl = threadIdx.x % BNR_COLS, rg = threadIdx.x / BNR_COLS;
+  const int c = blockIdx.x * BNR_COLS + cl;
+  const int cc = min(c, C - 1);
+  float d[RPT], xh[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int64_t o = (int64_t)min(rg + BNR_RG * j, B - 1) * C + cc;
+    d[j] = dy[o];
+    xh[j] = z[o];
+    if (gated) d[j] = ldf<T>(y, o) > 0.f ? d[j] * gate_scale : 0.f;
+  }
+  const float mu = mean[cc], rs = rstd[cc], wc = w[cc];
+  float s1 = 0.f, s2 = 0.f;   // Σ dy', Σ dy'·x̂
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    xh[j] = (xh[j] - mu) * rs;
+    if (rg + BNR_RG * j < B) {
+      s1 += d[j];
+      s2 += d[j] * xh[j];
+    }
+  }
+  const float S1 = bnr_colsum(s1, red, rg, cl);
+  const float S2 = bnr_colsum(s2, red, rg, cl);
+  if (c >= C) return;
+  const float invB = 1.f / (float)B;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = rg + BNR_RG * j;
+    if (r < B) dz[(int64_t)r * C + c] = wc * rs * (d[j] - S1 * invB - xh[j] * S2 * invB);
+  }
+  if (rg == 0) {
+    if (dw) atomicAdd(dw + c, S2);
+    if (db) atomicAdd(db + c, S1);
+  }
+}
+
+// rows-per-thread class of the register kernels for batch B (0: use the looped kernels)
+int bnr_rpt(int B) { return B <= 4 * BNR_RG ? 4 : B <= 8 * BNR_RG ? 8 : B <= 16 * BNR_RG ? 16 : 0; }
+
 int rows_grid(int64_t rows) {   // 4 rows (waves) per 256-thread block, grid-stride beyond
   return (int)std::min<int64_t>(std::max<int64_t>((rows + 3) / 4, 1), 2048);
 }
@@ -454,24 +639,31 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
   return ttmi_check_launch("ttmi_seq_embed_fwd");
 }
 
+extern "C" int64_t ttmi_seq_embed_bwd_workspace(int L, int D) {
+  return (int64_t)L * 2 * D * (int64_t)sizeof(float);
+}
+
 extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const float* E,
                                   const float* P, const float* w, const float* mean,
                                   const float* rstd, float drop_p, const uint64_t* drop_seed,
                                   const float* dx, float* dE, float* dP, float* dw, float* db,
-                                  int64_t padding_idx, hipStream_t s) {
+                                  int64_t padding_idx, void* ws, hipStream_t s) {
   TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV, "ttmi_seq_embed_bwd: bad sizes");
-  TTMI_REQUIRE(ids && E && P && w && mean && rstd && dx && dE && dP && dw && db,
+  TTMI_REQUIRE(ids && E && P && w && mean && rstd && dx && dE && dP && dw && db && ws,
                "ttmi_seq_embed_bwd: null argument");
   if (B == 0) return TTMI_OK;
   // V is not needed for the math; rows with out-of-range ids were zero in the forward.
   const int64_t V = INT64_MAX;
-  const int chunks = std::max(1, std::min((1024 + L - 1) / L, B));
-  const int bpc = (B + chunks - 1) / chunks;
+  const int bpc = 2 * SEB_W;                   // one pass of two rows per wave
   dim3 grid(L, (B + bpc - 1) / bpc);
-  TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_bwd_kernel<NV>), grid, dim3(256), 0, s, B, L, D, ids,
+  TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_bwd_kernel<NV>), grid, dim3(64 * SEB_W), 0, s, B, L, D, ids,
                                          E, P, w, mean, rstd, make_drop(drop_p, drop_seed), dx, dE,
-                                         dP, dw, db, padding_idx, V, bpc));
-  return ttmi_check_launch("ttmi_seq_embed_bwd");
+                                         dP, (float*)ws, padding_idx, V, bpc));
+  const int rc = ttmi_check_launch("ttmi_seq_embed_bwd");
+  if (rc) return rc;
+  hipLaunchKernelGGL(seq_embed_red_kernel, dim3((2 * D + 255) / 256), dim3(1024), 0, s, L, D, (float*)ws,
+                     dw, db);
+  return ttmi_check_launch("ttmi_seq_embed_bwd/reduce");
 }
 
 extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
@@ -519,6 +711,20 @@ extern "C" int ttmi_batchnorm_fwd(int dtype, int B, int C, const float* z, const
   if (B == 0) return TTMI_OK;
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_batchnorm_fwd: drop_p out of [0,1)");
   DropParams dp = make_drop(drop_p, drop_seed);
+  const int rpt = training ? bnr_rpt(B) : 0;
+  if (rpt) {
+    const dim3 g((C + BNR_COLS - 1) / BNR_COLS);
+#define TTMI_BNR_FWD(T, R)                                                                          \
+  hipLaunchKernelGGL((bnr_fwd_kernel<T, R>), g, dim3(512), 0, s, B, C, z, w, b, eps, momentum,      \
+                     running_mean, running_var, num_batches_tracked, relu, dp, (T*)y, mean, rstd)
+    if (dtype == TTMI_BF16) {
+      if (rpt == 4) TTMI_BNR_FWD(bf16_t, 4); else if (rpt == 8) TTMI_BNR_FWD(bf16_t, 8); else TTMI_BNR_FWD(bf16_t, 16);
+    } else {
+      if (rpt == 4) TTMI_BNR_FWD(float, 4); else if (rpt == 8) TTMI_BNR_FWD(float, 8); else TTMI_BNR_FWD(float, 16);
+    }
+#undef TTMI_BNR_FWD
+    return ttmi_check_launch("ttmi_batchnorm_fwd");
+  }
   dim3 grid((C + BN_COLS - 1) / BN_COLS);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(bn_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, C, z, w, b, eps, momentum,
@@ -536,6 +742,19 @@ extern "C" int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, cons
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_batchnorm_bwd: bad dtype");
   TTMI_REQUIRE(B > 1 && C > 0, "ttmi_batchnorm_bwd: bad sizes");
   TTMI_REQUIRE(dy && z && w && mean && rstd && dz && (!gated || y), "ttmi_batchnorm_bwd: null argument");
+  if (const int rpt = bnr_rpt(B)) {
+    const dim3 g((C + BNR_COLS - 1) / BNR_COLS);
+#define TTMI_BNR_BWD(T, R)                                                                          \
+  hipLaunchKernelGGL((bnr_bwd_kernel<T, R>), g, dim3(512), 0, s, B, C, dy, z, w, mean, rstd,        \
+                     (const T*)y, gate_scale, gated, dz, dw, db)
+    if (dtype == TTMI_BF16) {
+      if (rpt == 4) TTMI_BNR_BWD(bf16_t, 4); else if (rpt == 8) TTMI_BNR_BWD(bf16_t, 8); else TTMI_BNR_BWD(bf16_t, 16);
+    } else {
+      if (rpt == 4) TTMI_BNR_BWD(float, 4); else if (rpt == 8) TTMI_BNR_BWD(float, 8); else TTMI_BNR_BWD(float, 16);
+    }
+#undef TTMI_BNR_BWD
+    return ttmi_check_launch("ttmi_batchnorm_bwd");
+  }
   dim3 grid((C + BN_COLS - 1) / BN_COLS);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(bn_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, C, dy, z, w, mean, rstd,

@@ -54,8 +54,63 @@ TTMI_DEV float dot_row(const float* __restrict__ v, const T* __restrict__ row, i
   return acc;
 }
 
-// One 64-lane wave per (b, h); lane j owns key j (L <= 64) for the score/softmax phase;
-// lanes own head-dim elements for the P·V / dS·K reductions and the row stores.
+// 16-byte vector of E = 16 / sizeof(T) elements from fp32 values.
+template <typename T>
+TTMI_DEV void st16(T* p, const float* v) {
+  constexpr int E = 16 / sizeof(T);
+  T tmp[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) stf<T>(tmp, i, v[i]);
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(tmp);
+}
+
+// Row-vector lane layout of one wave over [rows][Dh]: lane = (row group, 16-byte chunk).
+template <typename T>
+struct RowLanes {
+  static constexpr int E = 16 / sizeof(T);
+  int lpr, ngrp, grp, cv;
+  TTMI_DEV explicit RowLanes(int Dh) {
+    lpr = Dh / E;
+    ngrp = 64 / lpr;
+    grp = (int)threadIdx.x / lpr;
+    cv = (int)threadIdx.x % lpr;
+  }
+  TTMI_DEV bool active() const { return grp < ngrp; }
+};
+
+// out[t] = Σ_{k<n} coef[k]·rows[k][t] for lane t < Dh: lanes split over (row group, 16-byte
+// chunk) so each lane issues ceil(n / groups) independent 16-byte loads; partials meet in LDS
+// (red: 64·E floats).
+template <typename T>
+TTMI_DEV float rows_combine(const float* coef, const T* __restrict__ base, int64_t ld, int n,
+                            int Dh, float* red) {
+  constexpr int E = RowLanes<T>::E;
+  const RowLanes<T> rl(Dh);
+  float acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+  if (rl.active()) {
+    for (int k = rl.grp; k < n; k += rl.ngrp) {
+      const uint4 q = *reinterpret_cast<const uint4*>(base + (int64_t)k * ld + rl.cv * E);
+      const T* e = reinterpret_cast<const T*>(&q);
+      const float c = coef[k];
+#pragma unroll
+      for (int i = 0; i < E; ++i) acc[i] += c * ldf<T>(e, i);
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) red[rl.grp * Dh + rl.cv * E + i] = acc[i];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  float s = 0.f;
+  if (t < Dh)
+    for (int g = 0; g < rl.ngrp; ++g) s += red[g * Dh + t];
+  return s;
+}
+
+// One 64-lane wave per (b, h), XCD-contiguous so the H heads of a sequence share an L2;
+// lane j owns key j (L <= 64) for the score/softmax phase; lanes own (row group, 16-byte
+// chunk) pairs for the P·V / dS·K reductions and the row stores.
 template <typename T>
 __global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int Dh,
                                                         const T* __restrict__ qkv,
@@ -63,9 +118,9 @@ __global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int
                                                         const int32_t* __restrict__ rows,
                                                         DropParams dp, T* __restrict__ ctx,
                                                         float* __restrict__ lse, float scale) {
-  __shared__ float sq[64], sp[64];
+  __shared__ float sq[64], sp[64], red[64 * 8];
   const int j = threadIdx.x;
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int bh = xcd_contiguous(blockIdx.x, gridDim.x), b = bh / H, h = bh % H;
   const int D = H * Dh;
   const int64_t ld = 3LL * D;
   const int64_t r = rows[b];
@@ -84,12 +139,8 @@ __global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int
   sp[j] = pj;
   if (j == 0) lse[bh] = m == -INFINITY ? INFINITY : m + logf(sum);
   __syncthreads();
-  if (j < Dh) {
-    float acc = 0.f;
-    const int last = min(p, L - 1);
-    for (int k = 0; k <= last; ++k) acc += sp[k] * ldf<T>(seq + (int64_t)k * ld + 2 * D, j);
-    stf<T>(ctx, (int64_t)b * D + (int64_t)h * Dh + j, acc);
-  }
+  const float acc = rows_combine<T>(sp, seq + 2 * D, ld, min(p, L - 1) + 1, Dh, red);
+  if (j < Dh) stf<T>(ctx, (int64_t)b * D + (int64_t)h * Dh + j, acc);
 }
 
 template <typename T>
@@ -100,9 +151,10 @@ __global__ __launch_bounds__(64) void mha_q1_bwd_kernel(int B, int L, int H, int
                                                         const float* __restrict__ lse,
                                                         const T* __restrict__ dctx, DropParams dp,
                                                         T* __restrict__ dqkv, float scale) {
-  __shared__ float sq[64], sdo[64], sds[64], spd[64];
+  constexpr int E = RowLanes<T>::E;
+  __shared__ float sq[64], sdo[64], sds[64], spd[64], red[64 * 8];
   const int t = threadIdx.x;
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int bh = xcd_contiguous(blockIdx.x, gridDim.x), b = bh / H, h = bh % H;
   const int D = H * Dh;
   const int64_t ld = 3LL * D;
   const int64_t r = rows[b];
@@ -130,25 +182,31 @@ __global__ __launch_bounds__(64) void mha_q1_bwd_kernel(int B, int L, int H, int
   sds[j] = pj * (dP - Dsum) * scale;
   spd[j] = pj * keep;
   __syncthreads();
-  // ---- row stores, lanes over the head dim (coalesced): dK_j = dS_j q, dV_j = Pd_j dO,
-  //      Q slice zero except the query row; dQ_p = Σ_j dS_j k_j
-  const int nl = 64 / Dh >= 2 ? 2 : 1;           // rows handled per pass (Dh <= 32: two)
-  const int sub = t / Dh, d = t % Dh;
-  if (sub < nl) {
-    const float qd = sq[d], od = sdo[d];
-    for (int jj = sub; jj < L; jj += nl) {
-      T* row = dseq + (int64_t)jj * ld;
-      if (jj != p) stf<T>(row, d, 0.f);
-      stf<T>(row + D, d, sds[jj] * qd);
-      stf<T>(row + 2 * D, d, spd[jj] * od);
+  // ---- row stores as 16-byte vectors: dK_j = dS_j q, dV_j = Pd_j dO, Q slice zero except
+  //      the query row; dQ_p = Σ_j dS_j k_j
+  const RowLanes<T> rl(Dh);
+  if (rl.active()) {
+    float qv[E], ov[E], z[E], v[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      qv[i] = sq[rl.cv * E + i];
+      ov[i] = sdo[rl.cv * E + i];
+      z[i] = 0.f;
+    }
+    for (int jj = rl.grp; jj < L; jj += rl.ngrp) {
+      T* row = dseq + (int64_t)jj * ld + rl.cv * E;
+      if (jj != p) st16<T>(row, z);
+      const float a = sds[jj], c = spd[jj];
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] = a * qv[i];
+      st16<T>(row + D, v);
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] = c * ov[i];
+      st16<T>(row + 2 * D, v);
     }
   }
-  if (t < Dh) {
-    float acc = 0.f;
-    const int last = min(p, L - 1);
-    for (int k = 0; k <= last; ++k) acc += sds[k] * ldf<T>(seq + (int64_t)k * ld + D, t);
-    stf<T>(dseq + (int64_t)p * ld, t, acc);
-  }
+  const float acc = rows_combine<T>(sds, seq + D, ld, min(p, L - 1) + 1, Dh, red);
+  if (t < Dh) stf<T>(dseq + (int64_t)p * ld, t, acc);
 }
 
 }  // namespace
@@ -207,6 +265,7 @@ extern "C" int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const voi
                "ttmi_mha_q1_bwd: need L <= 64, Dh <= 64, Dh %% 8 == 0");
   TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "ttmi_mha_q1_bwd: qkv must be 16-byte aligned");
   TTMI_REQUIRE(qkv && key_valid && rows && lse && dctx && dqkv, "ttmi_mha_q1_bwd: null argument");
+  TTMI_REQUIRE(((uintptr_t)dqkv & 15) == 0, "ttmi_mha_q1_bwd: dqkv must be 16-byte aligned");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
                "ttmi_mha_q1_bwd: bad dropout");
   if (B == 0) return TTMI_OK;

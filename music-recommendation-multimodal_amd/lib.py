@@ -90,8 +90,9 @@ SIGNATURES = {
                                  c_f, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "ttmi_seq_embed_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_i64, c_p, c_p, c_p, c_f, c_f, c_p, c_p,
                                  c_p, c_p, c_p]),
+    "ttmi_seq_embed_bwd_workspace": (c_i64, [c_i, c_i]),
     "ttmi_seq_embed_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p,
-                                 c_p, c_p, c_p, c_i64, c_p]),
+                                 c_p, c_p, c_p, c_i64, c_p, c_p]),
     "ttmi_mha_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_user_concat_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_p,

@@ -7,7 +7,7 @@ step can be captured into a HIP graph.  Shapes are checked here and again in C.
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -322,13 +322,30 @@ def seq_embed_fwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, b: Tensor, x: Te
     return x
 
 
+_SEB_WS: Dict[tuple, Tensor] = {}
+
+
+def _seq_embed_ws(L: int, D: int, device) -> Tensor:
+    """Persistent per-(device, L, D) workspace of ttmi_seq_embed_bwd: zero on entry, left zero
+    by every call, so one buffer serves every call (and every graph replay) on a stream."""
+    key = (str(device), L, D)
+    ws = _SEB_WS.get(key)
+    if ws is None:
+        _L.load()
+        nb = int(_L._lib.ttmi_seq_embed_bwd_workspace(L, D))
+        ws = _SEB_WS[key] = torch.zeros(nb // 4, device=device, dtype=torch.float32)
+    return ws
+
+
 def seq_embed_bwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, mean: Tensor, rstd: Tensor,
                   dx: Tensor, dE: Tensor, dP: Tensor, dw: Tensor, db: Tensor, *,
                   drop: Drop = NO_DROP, padding_idx: int = 0):
     B, L = ids.shape
     D = E.shape[1]
+    ws = _seq_embed_ws(L, D, dx.device)
     call("ttmi_seq_embed_bwd", B, L, D, _p(ids), _p(E), _p(P), _p(w), _p(mean), _p(rstd),
-         float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), _p(dw), _p(db), padding_idx, _s())
+         float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), _p(dw), _p(db), padding_idx,
+         _p(ws), _s())
 
 
 # ----------------------------------------------------------------------------- attention

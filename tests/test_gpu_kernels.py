@@ -440,9 +440,10 @@ def test_seq_embed_fwd_bwd(gpu_pkg, p):
 
 # ------------------------------------------------------------------------------ batchnorm
 @pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
-def test_batchnorm_train_eval(gpu_pkg, ydt):
+@pytest.mark.parametrize("B", [96, 250, 512, 700])   # register kernels (<= 512) and the loop
+def test_batchnorm_train_eval(gpu_pkg, ydt, B):
     ops = gpu_pkg.ops
-    B, C = 96, 200
+    C = 200
     g = torch.Generator().manual_seed(3)
     z = torch.randn(B, C, generator=g) * 2 + 0.5
     w = torch.randn(C, generator=g)
