@@ -392,8 +392,12 @@ __global__ __launch_bounds__(1024) void nce_combine_kernel(int B, const float* _
 
 // Backward.  G[i,j] = g/2B·(e^(S_ij − lse_i) + e^(S_ij − lse'_j) − 2δ_ij) (masked S = −1e4 gives
 // 0); dû_i = Σ_j G_ij î_j /τ (direction 0), dî_j = Σ_i G_ij û_i /τ (direction 1).  A
-// workgroup owns 16 output rows and one of NSPLIT k ranges; MFMA D[d][row] = Σ_k Vᵀ[d][k]
-// G'[k][row] with V streamed from L2 and G' recomputed per lane; partial rows go to part.
+// workgroup owns 16 output rows of one direction and one of NSPLIT key ranges, walked in
+// blocks of 64 keys: the workgroup stages the key block of V (16-byte loads) and the 16 x 64
+// block of G (computed once per workgroup, not per wave) in LDS, then each wave runs its
+// d-tiles' MFMAs D[d][row] = Σ_k Vᵀ[d][k] G[row][k] from LDS; partial rows go to part.
+constexpr int NKB = 64;   // keys per staged block
+
 template <int DC>
 __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __restrict__ uh,
                                                       const float* __restrict__ ih,
@@ -403,6 +407,9 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
                                                       float* __restrict__ part) {
   constexpr int D = 16 * DC, TPW = DC / 4;
   static_assert(DC % 4 == 0, "D % 64 == 0");
+  constexpr int VP = D + 4, GP = NKB + 4;          // LDS pitches (floats)
+  __shared__ __attribute__((aligned(16))) float sV[NKB * VP];
+  __shared__ __attribute__((aligned(16))) float sG[NQ * GP];
   const int nb = (B + NQ - 1) / NQ;
   const int split = blockIdx.x % NSPLIT;
   const int qb = blockIdx.x / NSPLIT;
@@ -411,68 +418,80 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
   const float* V = dir ? uh : ih;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
   const float coef = (dloss ? dloss[0] : 1.f) * (0.5f / (float)B);
-  const int row = r0 + li;
-  const bool rok = row < B;
-  const float lrow = rok ? lse[(int64_t)dir * B + row] : 0.f;
+  const float* lse_q = lse + (int64_t)dir * B;     // the output rows' direction
+  const float* lse_k = lse + (int64_t)(1 - dir) * B;
   f32x4_t acc[TPW];
 #pragma unroll
   for (int q = 0; q < TPW; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int nkc = (B + 15) / 16;
-  const int k0 = (int)((int64_t)nkc * split / NSPLIT), k1 = (int)((int64_t)nkc * (split + 1) / NSPLIT);
-  // chunks in groups of KU: every load of a group is issued before any of its MFMAs
-  constexpr int KU = 4;
-  for (int kg = k0; kg < k1; kg += KU) {
-    float g[KU][4], x[KU][TPW][4];
+  const int kbeg = (int)((int64_t)B * split / NSPLIT) / 4 * 4;
+  const int kend = split == NSPLIT - 1 ? B : (int)((int64_t)B * (split + 1) / NSPLIT) / 4 * 4;
+  for (int k0 = kbeg; k0 < kend; k0 += NKB) {
+    // ---- stage V[k0 .. k0+64) (rows past kend zero) and G[16][64]
+    constexpr int VQ = NKB * D / 4 / 256;          // float4 per thread
+    float4 v[VQ];
 #pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const int kb = 16 * (kg + u) + 4 * lg;   // this lane's 4 k values: kb .. kb+3
-      const bool cok = kg + u < k1;
-      // loads are unconditional (clamped addresses) and masked afterwards: a guarded load in
-      // an unrolled group makes hipcc branch and drain vmcnt per element
-      const int rowc = min(row, B - 1);
-      const int kbc = min(kb, B - 4);             // B % 4 == 0
-      if (dir == 0) {
-        const float4 sv = *reinterpret_cast<const float4*>(S + (int64_t)rowc * B + kbc);
-        const float4 l2 = *reinterpret_cast<const float4*>(lse + B + kbc);
-        const float svv[4] = {sv.x, sv.y, sv.z, sv.w}, l2v[4] = {l2.x, l2.y, l2.z, l2.w};
+    for (int j = 0; j < VQ; ++j) {
+      const int idx = tid + 256 * j, kr = idx / (D / 4), c4 = idx % (D / 4);
+      v[j] = *reinterpret_cast<const float4*>(V + (int64_t)min(k0 + kr, B - 1) * D + 4 * c4);
+    }
+    float g[4];
+    int gr[4], gk[4];
+    if (dir == 0) {      // thread -> row tid/16, keys 4·(tid%16) .. +3 (one float4 of S's row)
+      const int r = tid >> 4, kq = (tid & 15) * 4;
+      const int row = r0 + r, k = k0 + kq;
+      const float4 sv = *reinterpret_cast<const float4*>(S + (int64_t)min(row, B - 1) * B + min(k, B - 4));
+      const float4 lk = *reinterpret_cast<const float4*>(lse_k + min(k, B - 4));
+      const float lq = lse_q[min(row, B - 1)];
+      const float svv[4] = {sv.x, sv.y, sv.z, sv.w}, lkv[4] = {lk.x, lk.y, lk.z, lk.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float gv = coef * (expf(svv[e] - lrow) + expf(svv[e] - l2v[e]) - (kb + e == row ? 2.f : 0.f));
-          g[u][e] = (cok && rok && kb + e < B) ? gv : 0.f;
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = kbc + e;
-          const float sv = S[(int64_t)k * B + rowc];
-          const float gv = coef * (expf(sv - lse[k]) + expf(sv - lrow) - (k == row ? 2.f : 0.f));
-          g[u][e] = (cok && rok && kb + e < B) ? gv : 0.f;
-        }
+      for (int e = 0; e < 4; ++e) {
+        gr[e] = r;
+        gk[e] = kq + e;
+        const bool ok = row < B && k + e < kend;
+        g[e] = ok ? coef * (__expf(svv[e] - lq) + __expf(svv[e] - lkv[e]) - (k + e == row ? 2.f : 0.f)) : 0.f;
       }
+    } else {             // thread -> key tid/4, rows 4·(tid%4) .. +3 (one float4 of S's row k)
+      const int kk = tid >> 2, rq = (tid & 3) * 4;
+      const int k = k0 + kk, row = r0 + rq;
+      const float4 sv = *reinterpret_cast<const float4*>(S + (int64_t)min(k, B - 1) * B + min(row, B - 4));
+      const float4 lq = *reinterpret_cast<const float4*>(lse_q + min(row, B - 4));
+      const float lk = lse_k[min(k, B - 1)];
+      const float svv[4] = {sv.x, sv.y, sv.z, sv.w}, lqv[4] = {lq.x, lq.y, lq.z, lq.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gr[e] = rq + e;
+        gk[e] = kk;
+        const bool ok = row + e < B && k < kend;
+        g[e] = ok ? coef * (__expf(svv[e] - lqv[e]) + __expf(svv[e] - lk) - (k == row + e ? 2.f : 0.f)) : 0.f;
+      }
+    }
+    __syncthreads();                               // previous block's MFMAs done with LDS
+#pragma unroll
+    for (int j = 0; j < VQ; ++j) {
+      const int idx = tid + 256 * j, kr = idx / (D / 4), c4 = idx % (D / 4);
+      *reinterpret_cast<float4*>(sV + kr * VP + 4 * c4) =
+          k0 + kr < kend ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sG[gr[e] * GP + gk[e]] = g[e];
+    __syncthreads();
+    // ---- MFMAs: A = Vᵀ fragment (lane li = d, k = 16c + 4lg + e), B = G fragment
+#pragma unroll
+    for (int c = 0; c < NKB / 16; ++c) {
+      const int kb = 16 * c + 4 * lg;
+      const uint4 gf = *reinterpret_cast<const uint4*>(sG + li * GP + kb);
 #pragma unroll
       for (int q = 0; q < TPW; ++q) {
         const int d = (wave + 4 * q) * 16 + li;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xv = V[(int64_t)(kbc + e) * D + d];
-          x[u][q][e] = (cok && kb + e < B) ? xv : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const uint4 gf = make_uint4(__float_as_uint(g[u][0]), __float_as_uint(g[u][1]),
-                                  __float_as_uint(g[u][2]), __float_as_uint(g[u][3]));
-#pragma unroll
-      for (int q = 0; q < TPW; ++q) {
-        const uint4 xf = make_uint4(__float_as_uint(x[u][q][0]), __float_as_uint(x[u][q][1]),
-                                    __float_as_uint(x[u][q][2]), __float_as_uint(x[u][q][3]));
+        const uint4 xf = make_uint4(__float_as_uint(sV[(kb + 0) * VP + d]), __float_as_uint(sV[(kb + 1) * VP + d]),
+                                    __float_as_uint(sV[(kb + 2) * VP + d]), __float_as_uint(sV[(kb + 3) * VP + d]));
         Mma<float>::run(acc[q], xf, gf);
       }
     }
   }
   // lane holds D[d = dtile*16 + 4lg + r][row = r0 + li]
-  if (rok) {
+  const int row = r0 + li;
+  if (row < B) {
     float* pr = part + ((int64_t)split * 2 * B + (int64_t)dir * B + row) * D;
 #pragma unroll
     for (int q = 0; q < TPW; ++q)
