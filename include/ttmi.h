@@ -93,22 +93,28 @@ int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const floa
 /* Backward of the above.  dy (fp32) is the gradient w.r.t. y; if gate != NULL it is first
  * multiplied by (gate > 0 ? gate_scale : 0) (gate = the stored y when ReLU/dropout followed
  * the affine).  dx = res + LN'(dy) (res may alias dx or be NULL); dw/db are accumulated
- * (atomic, fp32). */
+ * (fp32).  ws: ttmi_layernorm_bwd_workspace(D) bytes, zero on entry and left zero (replicated
+ * column sums folded once; may be NULL when dw and db are both NULL). */
+int64_t ttmi_layernorm_bwd_workspace(int D);
 int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
                        int64_t ldx, const float* mean, const float* rstd, const float* w,
                        const void* gate, int gate_dtype, int64_t ldg, float gate_scale,
                        const float* res, float* dx, int64_t lddx, float* dw, float* db,
-                       hipStream_t stream);
+                       void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * SASRec input block (user_tower.py:83-93):
  *   x[b,l,:] = dropout(LN(E[ids[b,l]] + P[l]))   (dropout idx = (b*L+l)*D + c)
  * E [V,D], P [>=L,D] fp32 master tables; x [B*L,D] fp32 residual stream.
+ * Optional (y1 != NULL): the first encoder layer's norm1 on the same rows,
+ *   y1 = bf16(LN(x) * w1 + b1), mean1 / rstd1 its row statistics (user_tower.py:111-116,
+ *   TransformerEncoderLayer(norm_first=True) layer 0), fused while the row is in registers.
  * ---------------------------------------------------------------------------------- */
 int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, int64_t V,
                        const float* P, const float* w, const float* b, float eps,
                        float drop_p, const uint64_t* drop_seed, float* x, float* mean, float* rstd,
-                       hipStream_t stream);
+                       const float* w1, const float* b1, float eps1, void* y1, float* mean1,
+                       float* rstd1, hipStream_t stream);
 /* Backward: dE[ids] += g (rows with ids == padding_idx skipped, nn.Embedding(padding_idx=0)
  * user_tower.py:27), dP[l] += Σ_b g, dw/db += LN affine grads.  All accumulate (fp32).
  * ws: ttmi_seq_embed_bwd_workspace(L, D) bytes, zero on entry and left zero on return (the
@@ -332,6 +338,26 @@ typedef struct ttmi_linear_ln_bwd_desc {
   float* ln_dw; float* ln_db;           /* [N], accumulated */
 } ttmi_linear_ln_bwd_desc;
 int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream);
+/* Fused residual sub-block end + the next LayerNorm (N = 128, K % 128 == 0, K <= 512):
+ *   out = residual + dropout(x · wᵀ + bias)   (fp32 [M, 128]; dropout keep index m*ld_drop + n)
+ *   y = bf16(LN(out) * ln_w + ln_b), mean / rstd = the row statistics
+ * i.e. TransformerEncoderLayer(norm_first=True)'s `x = x + dropout(out_proj(...))` followed by
+ * norm2(x) (or `x = x + dropout(linear2(...))` followed by the next layer's norm1(x)), the
+ * ttmi_gemm(residual) + ttmi_layernorm_fwd pair in one kernel (reference
+ * src/models/user_tower.py:37-45, torch TransformerEncoderLayer._sa_block/_ff_block). */
+typedef struct ttmi_linear_res_ln_desc {
+  int64_t M, N, K;
+  const void* x; int64_t ldx;           /* bf16 [M, K] */
+  const void* w; int64_t ldw;           /* bf16 [N, K] (nn.Linear weight) */
+  const float* bias;                    /* [N] or NULL */
+  float drop_p; const uint64_t* drop_seed; int64_t ld_drop;
+  const float* residual; int64_t ld_res;/* fp32 [M, N] */
+  float* out; int64_t ld_out;           /* fp32 [M, N] */
+  const float* ln_w; const float* ln_b; float eps;
+  void* y; int64_t ldy;                 /* bf16 [M, N] */
+  float* mean; float* rstd;             /* [M] */
+} ttmi_linear_res_ln_desc;
+int ttmi_linear_res_ln(const ttmi_linear_res_ln_desc* d, hipStream_t stream);
 /* dst[i] = transpose(src[i]) for i < n <= 16 row-major bf16 matrices of rows[i] x cols[i],
  * in one launch (the transposed weight mirrors that make nn.Linear input-grad GEMMs
  * k-major: dX = dY·W = dY·(Wᵀ)ᵀ; replaces the W-operand layout of user_tower.py's

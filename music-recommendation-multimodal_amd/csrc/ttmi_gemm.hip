@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 //  * W fragment columns are paired (tile 2p slot 4q+r <-> column 32p+8q+r, tile 2p+1 <->
 //    32p+8q+4+r), so each lane owns 8 consecutive output columns: 16-byte stores and
 //    16-byte bias / gate / residual loads; dropout hashes once per column pair.
-enum PanelEpi { PE_NONE = 0, PE_RES = 1, PE_GATE_BF16 = 2, PE_GATE_F32 = 3, PE_LNBWD = 4 };
+enum PanelEpi { PE_NONE = 0, PE_RES = 1, PE_GATE_BF16 = 2, PE_GATE_F32 = 3, PE_LNBWD = 4, PE_RESLN = 5 };
 
 // PE_LNBWD: the GEMM output dY (N = 128 = LayerNorm width, never stored) feeds the
 // LayerNorm backward of the rows it completes:
@@ -343,6 +343,8 @@ struct LnBwdArgs {
   bf16_t* next; int64_t ld_next;
   DropParams drop; int64_t ld_drop; const int32_t* drop_rows;
   float* dw; float* db;
+  // PE_RESLN (forward): y = LN(C row) * w + lnb -> bf16 y, per-row mean / rstd
+  const float* lnb; float eps; bf16_t* y; int64_t ldy; float* mean_out; float* rstd_out;
 };
 
 // Sum over the 16 lanes of a DPP row (GFX9 quad_perm / row_half_mirror / row_mirror).
@@ -440,13 +442,13 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
 template <int NT, int KC, int EPI>
 __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg, LnBwdArgs ln) {
   constexpr int K = KC * 32, N = NT * 16, WP = 2 * K + 16;
-  constexpr bool LNB = EPI == PE_LNBWD;
+  constexpr bool LNB = EPI == PE_LNBWD, LNF = EPI == PE_RESLN;
   static_assert(NT % 8 == 0, "column groups of 128");
-  static_assert(!LNB || NT == 8, "LayerNorm-backward epilogue needs N = 128");
-  __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4 + (LNB ? 2 * N * 4 : 0)];
+  static_assert(!(LNB || LNF) || NT == 8, "LayerNorm epilogues need N = 128");
+  __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4 + ((LNB || LNF) ? 2 * N * 4 : 0)];
   float* sbias = reinterpret_cast<float*>(smem + N * WP);     // bias, or the LN weight
   float* sdw = sbias + N;                                       // LNB: per-WG dw / db sums
-  float* sdb = sdw + N;
+  float* sdb = sdw + N;                                         // LNF: LN weight / bias
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
@@ -468,6 +470,12 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
     }
     if constexpr (LNB) {
       for (int i = tid; i < N; i += 512) { sbias[i] = ln.w[i]; sdw[i] = 0.f; sdb[i] = 0.f; }
+    } else if constexpr (LNF) {
+      for (int i = tid; i < N; i += 512) {
+        sbias[i] = g.bias ? g.bias[i] : 0.f;
+        sdw[i] = ln.w[i];
+        sdb[i] = ln.lnb[i];
+      }
     } else {
       for (int i = tid; i < N; i += 512) sbias[i] = g.bias ? g.bias[i] : 0.f;
     }
@@ -514,6 +522,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
         continue;
       }
       if (!mok) continue;
+      float vr[LNF ? 32 : 1];                     // LNF: the lane's 32 values of row m
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int n = cg * 128 + 32 * p + 8 * lg;
@@ -544,7 +553,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
         }
-        if constexpr (EPI == PE_RES) {
+        if constexpr (EPI == PE_RES || LNF) {
           const float* rp = g.residual + m * g.ld_res + n;
           const float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
           v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
@@ -561,6 +570,41 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
           q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
           q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + m * g.ldc + n) = q;
+        }
+        if constexpr (LNF) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vr[8 * p + e] = v[e];
+        }
+      }
+      if constexpr (LNF) {   // LayerNorm of the finished row: its 128 columns live in lanes
+        float s1 = 0.f;      // li, li+16, li+32, li+48 (two-pass mean / variance, as ln_fwd)
+#pragma unroll
+        for (int e = 0; e < 32; ++e) s1 += vr[e];
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        const float mu = s1 * (1.f / 128.f);
+        float s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 32; ++e) s2 += (vr[e] - mu) * (vr[e] - mu);
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        const float rs = 1.f / sqrtf(s2 * (1.f / 128.f) + ln.eps);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int n = 32 * p + 8 * lg;
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (vr[8 * p + e] - mu) * rs * sdw[n + e] + sdb[n + e];
+          uint4 q;
+          q.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+          q.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+          q.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+          q.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+          *reinterpret_cast<uint4*>(ln.y + m * ln.ldy + n) = q;
+        }
+        if (lg == 0) {
+          ln.mean_out[m] = mu;
+          ln.rstd_out[m] = rs;
         }
       }
     }
@@ -1390,6 +1434,42 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   if (d->dtype == TTMI_BF16) launch_typed<bf16_t>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
   else launch_typed<float>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
   return ttmi_check_launch("ttmi_gemm");
+}
+
+extern "C" int ttmi_linear_res_ln(const ttmi_linear_res_ln_desc* d, hipStream_t stream) {
+  TTMI_REQUIRE(d != nullptr, "ttmi_linear_res_ln: null descriptor");
+  TTMI_REQUIRE(d->M >= 0 && d->N == 128, "ttmi_linear_res_ln: N must be 128 (got %lld)", (long long)d->N);
+  TTMI_REQUIRE(d->K > 0 && d->K % 128 == 0 && d->K <= 512, "ttmi_linear_res_ln: K must be 128, 256, 384 or 512");
+  if (d->M == 0) return TTMI_OK;
+  TTMI_REQUIRE(d->x && d->w && d->residual && d->out && d->ln_w && d->ln_b && d->y && d->mean && d->rstd,
+               "ttmi_linear_res_ln: null argument");
+  TTMI_REQUIRE(al16(d->x) && al16(d->w) && d->ldx % 8 == 0 && d->ldw % 8 == 0 && d->ldx >= d->K &&
+               d->ldw >= d->K, "ttmi_linear_res_ln: x/w need 16-byte rows");
+  TTMI_REQUIRE(al16(d->residual) && d->ld_res % 4 == 0 && d->ld_res >= 128 && al16(d->out) &&
+               d->ld_out % 4 == 0 && d->ld_out >= 128, "ttmi_linear_res_ln: residual/out need 16-byte rows");
+  TTMI_REQUIRE(al16(d->y) && d->ldy % 8 == 0 && d->ldy >= 128, "ttmi_linear_res_ln: y needs 16-byte rows");
+  TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f && (d->drop_p == 0.f || d->drop_seed),
+               "ttmi_linear_res_ln: bad dropout");
+  GemmArgs a{};
+  a.M = d->M; a.N = 128; a.K = d->K;
+  a.A = static_cast<const char*>(d->x); a.lda = d->ldx;
+  a.B = static_cast<const char*>(d->w); a.ldb = d->ldw;
+  a.C = d->out; a.ldc = d->ld_out; a.c_f32 = 1;
+  a.alpha = 1.f;
+  a.bias = d->bias;
+  a.drop = make_drop(d->drop_p, d->drop_seed); a.ld_drop = d->ld_drop ? d->ld_drop : 128;
+  a.residual = d->residual; a.ld_res = d->ld_res;
+  LnBwdArgs ln{};
+  ln.w = d->ln_w; ln.lnb = d->ln_b; ln.eps = d->eps;
+  ln.y = static_cast<bf16_t*>(d->y); ln.ldy = d->ldy;
+  ln.mean_out = d->mean; ln.rstd_out = d->rstd;
+  switch (d->K) {
+    case 128: launch_panel_t<8, 4, PE_RESLN>(a, stream, ln); break;
+    case 256: launch_panel_t<8, 8, PE_RESLN>(a, stream, ln); break;
+    case 384: launch_panel_t<8, 12, PE_RESLN>(a, stream, ln); break;
+    default: launch_panel_t<8, 16, PE_RESLN>(a, stream, ln); break;
+  }
+  return ttmi_check_launch("ttmi_linear_res_ln");
 }
 
 extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream) {

@@ -7,6 +7,7 @@
 namespace {
 
 constexpr int MAXV = 16;   // D <= 64 * MAXV
+constexpr int LN_REPL = 32;   // replicas of the LayerNorm-backward weight/bias column sums
 
 // Instantiate a kernel template for the smallest NV (64-wide column chunks per row) that
 // covers D: NV in {1, 2, 4, 8, 16}.
@@ -91,8 +92,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int64_t M, int D, const float* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
     int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ w, const void* __restrict__ gate, int gate_f32, int64_t ldg,
-    float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ dw,
-    float* __restrict__ db) {
+    float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ ws) {
   __shared__ float red[4 * 64 * NV];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -130,18 +130,45 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     }
   }
-  if (dw) block_col_atomic(aw, D, dw, red);
-  if (db) block_col_atomic(ab, D, db, red);
+  if (ws) {   // this block's replica of the LN weight / bias partials (LNR adders per address)
+    float* rep = ws + (int64_t)(blockIdx.x % LN_REPL) * 2 * D;
+    block_col_atomic(aw, D, rep, red);
+    block_col_atomic(ab, D, rep + D, red);
+  }
+}
+
+// dst0[i] += Σ_r ws[r][i] (i < n0), dst1[i - n0] += ... (n0 <= i < n); zeroes the replicas.
+__global__ __launch_bounds__(256) void colsum_fold_kernel(int n, int n0, int R, float* __restrict__ ws,
+                                                          float* __restrict__ dst0,
+                                                          float* __restrict__ dst1) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  constexpr int U = 8;
+  for (int r0 = 0; r0 < R; r0 += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = r0 + u < R ? ws[(int64_t)(r0 + u) * n + i] : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s += v[u];
+      if (r0 + u < R) ws[(int64_t)(r0 + u) * n + i] = 0.f;
+    }
+  }
+  if (i < n0) { if (dst0) dst0[i] += s; }
+  else if (dst1) dst1[i - n0] += s;
 }
 
 // ------------------------------------------------------------------- SASRec input block
-// Forward: one wave per token row.
-template <int NV>
+// Forward: one wave per token row.  With LN2 the row also goes through the first encoder
+// layer's norm1 (norm_first) while it is in registers: y1 = bf16(LN1(x)), mean1 / rstd1.
+template <int NV, bool LN2>
 __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
     int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E, int64_t V,
     const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ b,
     float eps, DropParams dp, float* __restrict__ x, float* __restrict__ mean,
-    float* __restrict__ rstd) {
+    float* __restrict__ rstd, const float* __restrict__ w1, const float* __restrict__ b1,
+    float eps1, bf16_t* __restrict__ y1, float* __restrict__ mean1, float* __restrict__ rstd1) {
   const int lane = threadIdx.x & 63;
   const int64_t M = (int64_t)B * L;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -169,6 +196,7 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
       q += dlt * dlt;
     }
     const float rs = 1.f / sqrtf(wave_sum(q) * invD + eps);
+    float s1 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
@@ -176,9 +204,28 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
         float o = (v[i] - mu) * rs * w[c] + b[c];
         if (dk.on) o = drop_apply(dk, (uint32_t)(row * D + c), o);
         x[row * D + c] = o;
+        v[i] = o;
+        s1 += o;
       }
     }
     if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+    if constexpr (LN2) {
+      const float mu1 = wave_sum(s1) * invD;
+      float q1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = lane + 64 * i;
+        const float dlt = c < D ? v[i] - mu1 : 0.f;
+        q1 += dlt * dlt;
+      }
+      const float rs1 = 1.f / sqrtf(wave_sum(q1) * invD + eps1);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = lane + 64 * i;
+        if (c < D) stf<bf16_t>(y1, row * D + c, (v[i] - mu1) * rs1 * w1[c] + b1[c]);
+      }
+      if (lane == 0) { mean1[row] = mu1; rstd1[row] = rs1; }
+    }
   }
 }
 
@@ -609,33 +656,53 @@ extern "C" int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx,
   return ttmi_check_launch("ttmi_layernorm_fwd");
 }
 
+extern "C" int64_t ttmi_layernorm_bwd_workspace(int D) {
+  return (int64_t)LN_REPL * 2 * D * (int64_t)sizeof(float);
+}
+
 extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
                                   int64_t ldx, const float* mean, const float* rstd,
                                   const float* w, const void* gate, int gate_dtype, int64_t ldg,
                                   float gate_scale, const float* res, float* dx, int64_t lddx,
-                                  float* dw, float* db, hipStream_t s) {
+                                  float* dw, float* db, void* ws, hipStream_t s) {
   TTMI_REQUIRE(M >= 0 && D > 0 && D <= 64 * MAXV, "ttmi_layernorm_bwd: need 0 < D <= %d", 64 * MAXV);
   TTMI_REQUIRE(dy && x && mean && rstd && w && dx, "ttmi_layernorm_bwd: null argument");
   TTMI_REQUIRE(lddy >= D && ldx >= D && lddx >= D && (!gate || ldg >= D), "ttmi_layernorm_bwd: bad ld");
+  TTMI_REQUIRE(!(dw || db) || ws, "ttmi_layernorm_bwd: dw/db need the workspace");
   if (M == 0) return TTMI_OK;
+  const bool sums = dw || db;
   int grid = (int)std::min<int64_t>((M + 3) / 4, 1024);
   TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(grid), dim3(256), 0, s, M, D, dy,
                                          lddy, x, ldx, mean, rstd, w, gate, gate_dtype == TTMI_F32,
-                                         ldg, gate_scale, res, dx, lddx, dw, db));
-  return ttmi_check_launch("ttmi_layernorm_bwd");
+                                         ldg, gate_scale, res, dx, lddx, sums ? (float*)ws : nullptr));
+  int rc = ttmi_check_launch("ttmi_layernorm_bwd");
+  if (rc || !sums) return rc;
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, 2 * D, D,
+                     std::min(grid, LN_REPL), (float*)ws, dw, db);
+  return ttmi_check_launch("ttmi_layernorm_bwd/fold");
 }
 
 extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, int64_t V,
                                   const float* P, const float* w, const float* b, float eps,
                                   float drop_p, const uint64_t* drop_seed, float* x, float* mean,
-                                  float* rstd, hipStream_t s) {
+                                  float* rstd, const float* w1, const float* b1, float eps1, void* y1,
+                                  float* mean1, float* rstd1, hipStream_t s) {
   TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV, "ttmi_seq_embed_fwd: bad sizes");
   TTMI_REQUIRE(ids && E && P && w && b && x && mean && rstd, "ttmi_seq_embed_fwd: null argument");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_seq_embed_fwd: drop_p out of [0,1)");
+  const bool ln2 = y1 != nullptr;
+  TTMI_REQUIRE(!ln2 || (w1 && b1 && mean1 && rstd1), "ttmi_seq_embed_fwd: norm1 needs w1, b1, mean1, rstd1");
   if (B == 0) return TTMI_OK;
-  TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_fwd_kernel<NV>), dim3(rows_grid((int64_t)B * L)),
-                                         dim3(256), 0, s, B, L, D, ids, E, V, P, w, b, eps,
-                                         make_drop(drop_p, drop_seed), x, mean, rstd));
+  const DropParams dp = make_drop(drop_p, drop_seed);
+  const dim3 grid(rows_grid((int64_t)B * L));
+  TTMI_NV_DISPATCH(D, {
+    if (ln2)
+      hipLaunchKernelGGL((seq_embed_fwd_kernel<NV, true>), grid, dim3(256), 0, s, B, L, D, ids, E, V, P,
+                         w, b, eps, dp, x, mean, rstd, w1, b1, eps1, (bf16_t*)y1, mean1, rstd1);
+    else
+      hipLaunchKernelGGL((seq_embed_fwd_kernel<NV, false>), grid, dim3(256), 0, s, B, L, D, ids, E, V, P,
+                         w, b, eps, dp, x, mean, rstd, nullptr, nullptr, 0.f, nullptr, nullptr, nullptr);
+  });
   return ttmi_check_launch("ttmi_seq_embed_fwd");
 }
 

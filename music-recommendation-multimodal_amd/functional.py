@@ -158,6 +158,14 @@ def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
 
+def _resln_ok(W: Dict[str, Tensor], name: str, D: int) -> bool:
+    """The Linear `name` can end its residual sub-block with the following LayerNorm fused
+    (ttmi_linear_res_ln): bf16 weight [128, K], K % 128 == 0, K <= 512."""
+    w = W[name]
+    return (D == 128 and w.dtype == torch.bfloat16 and w.shape[0] == 128
+            and w.shape[1] % 128 == 0 and w.shape[1] <= 512)
+
+
 def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gender: Tensor,
                    country: Tensor, mask: Optional[Tensor], cfg: TowerCfg,
                    seeds: Optional[Tensor] = None):
@@ -173,18 +181,30 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
     x = torch.empty(M, D, **f32)
     m0 = torch.empty(M, **f32)
     r0 = torch.empty(M, **f32)
+
+    def ln_out(R: int):
+        return (torch.empty(R, D, device=dev, dtype=dt), torch.empty(R, **f32),
+                torch.empty(R, **f32))
+
+    # nxt: the next layer's norm1 output (a1, m1, r1) when a fused kernel already produced it
+    nxt = None
+    norm1 = None
+    if cfg.n_layers > 0 and dt == torch.bfloat16:
+        nxt = ln_out(M)
+        norm1 = (P[_lp(0) + "norm1.weight"], P[_lp(0) + "norm1.bias"], cfg.eps) + nxt
     ops.seq_embed_fwd(ids, P["item_embedding.weight"], P["position_embedding.weight"],
                       P["layer_norm.weight"], P["layer_norm.bias"], x, m0, r0, eps=cfg.eps,
-                      drop=_drop(cfg, seeds, SITE_EMB))
+                      drop=_drop(cfg, seeds, SITE_EMB), norm1=norm1)
     st = UserSaved(ids=ids, key_valid=key_valid, gender=gender, country=country, m0=m0, r0=r0,
                    seeds=seeds)
     for i in range(cfg.n_layers):
         pre = _lp(i)
         pruned = cfg.prune_last and i == cfg.n_layers - 1
-        a1 = torch.empty(M, D, device=dev, dtype=dt)
-        m1 = torch.empty(M, **f32)
-        r1 = torch.empty(M, **f32)
-        ops.layernorm_fwd(x, P[pre + "norm1.weight"], P[pre + "norm1.bias"], a1, m1, r1, eps=cfg.eps)
+        if nxt is not None:
+            (a1, m1, r1), nxt = nxt, None
+        else:
+            a1, m1, r1 = ln_out(M)
+            ops.layernorm_fwd(x, P[pre + "norm1.weight"], P[pre + "norm1.bias"], a1, m1, r1, eps=cfg.eps)
         qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         ops.linear(a1, W[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"], qkv)
         F_ = W[pre + "linear1.weight"].shape[0]
@@ -202,18 +222,31 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             lse = torch.empty(B * H * L, **f32)
             ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
         x1 = torch.empty(R, D, **f32)
-        ops.linear(ctx, W[pre + "self_attn.out_proj.weight"], P[pre + "self_attn.out_proj.bias"],
-                   x1, drop=_drop(cfg, seeds, site_drop1(i)), residual=res_in, drop_rows=drows)
-        a2 = torch.empty(R, D, device=dev, dtype=dt)
-        m2 = torch.empty(R, **f32)
-        r2 = torch.empty(R, **f32)
-        ops.layernorm_fwd(x1, P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2, eps=cfg.eps)
+        a2, m2, r2 = ln_out(R)
+        name = pre + "self_attn.out_proj.weight"
+        if not pruned and _resln_ok(W, name, D):       # out_proj + residual + norm2, one kernel
+            ops.linear_res_ln(ctx, W[name], P[pre + "self_attn.out_proj.bias"], res_in, x1,
+                              P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2,
+                              eps=cfg.eps, drop=_drop(cfg, seeds, site_drop1(i)))
+        else:
+            ops.linear(ctx, W[name], P[pre + "self_attn.out_proj.bias"], x1,
+                       drop=_drop(cfg, seeds, site_drop1(i)), residual=res_in, drop_rows=drows)
+            ops.layernorm_fwd(x1, P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2, eps=cfg.eps)
         h = torch.empty(R, F_, device=dev, dtype=dt)
         ops.linear(a2, W[pre + "linear1.weight"], P[pre + "linear1.bias"], h, act=1,
                    drop=_drop(cfg, seeds, site_ffn(i)), drop_rows=drows)
         x2 = torch.empty(R, D, **f32)
-        ops.linear(h, W[pre + "linear2.weight"], P[pre + "linear2.bias"], x2,
-                   drop=_drop(cfg, seeds, site_drop2(i)), residual=x1, drop_rows=drows)
+        name = pre + "linear2.weight"
+        if not pruned and i + 1 < cfg.n_layers and _resln_ok(W, name, D):
+            # linear2 + residual + the next layer's norm1, one kernel
+            nxt = ln_out(M)
+            nx = _lp(i + 1)
+            ops.linear_res_ln(h, W[name], P[pre + "linear2.bias"], x1, x2, P[nx + "norm1.weight"],
+                              P[nx + "norm1.bias"], *nxt, eps=cfg.eps,
+                              drop=_drop(cfg, seeds, site_drop2(i)))
+        else:
+            ops.linear(h, W[name], P[pre + "linear2.bias"], x2,
+                       drop=_drop(cfg, seeds, site_drop2(i)), residual=x1, drop_rows=drows)
         st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, x1, a2, m2, r2, h, rows))
         x = x2
     gathered = cfg.prune_last and cfg.n_layers > 0

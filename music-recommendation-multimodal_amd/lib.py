@@ -79,6 +79,20 @@ class LnBwdDesc(ctypes.Structure):
                 ("ln_dw", ctypes.c_void_p), ("ln_db", ctypes.c_void_p)]
 
 
+class ResLnDesc(ctypes.Structure):
+    """ttmi_linear_res_ln_desc (include/ttmi.h)."""
+    _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
+                ("x", ctypes.c_void_p), ("ldx", ctypes.c_int64),
+                ("w", ctypes.c_void_p), ("ldw", ctypes.c_int64),
+                ("bias", ctypes.c_void_p),
+                ("drop_p", ctypes.c_float), ("drop_seed", ctypes.c_void_p), ("ld_drop", ctypes.c_int64),
+                ("residual", ctypes.c_void_p), ("ld_res", ctypes.c_int64),
+                ("out", ctypes.c_void_p), ("ld_out", ctypes.c_int64),
+                ("ln_w", ctypes.c_void_p), ("ln_b", ctypes.c_void_p), ("eps", ctypes.c_float),
+                ("y", ctypes.c_void_p), ("ldy", ctypes.c_int64),
+                ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes); mirrors include/ttmi.h one-to-one.
 SIGNATURES = {
     "ttmi_last_error": (ctypes.c_char_p, []),
@@ -86,10 +100,11 @@ SIGNATURES = {
     "ttmi_gemm": (c_i, [ctypes.POINTER(GemmDesc), c_p]),
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
                                  c_i64, c_p, c_p, c_p]),
+    "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),
     "ttmi_layernorm_bwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i, c_i64,
-                                 c_f, c_p, c_p, c_i64, c_p, c_p, c_p]),
+                                 c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "ttmi_seq_embed_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_i64, c_p, c_p, c_p, c_f, c_f, c_p, c_p,
-                                 c_p, c_p, c_p]),
+                                 c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_seq_embed_bwd_workspace": (c_i64, [c_i, c_i]),
     "ttmi_seq_embed_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p,
                                  c_p, c_p, c_p, c_i64, c_p, c_p]),
@@ -109,6 +124,7 @@ SIGNATURES = {
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
+    "ttmi_linear_res_ln": (c_i, [c_p, c_p]),
     "ttmi_deb_embed_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, ctypes.c_float, c_p,
                                  ctypes.c_float, c_p, c_p, c_p, c_i64, c_p]),
     "ttmi_deb_ln_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, ctypes.c_float, c_p, c_p, c_i64, c_p,

@@ -134,6 +134,29 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
     return dx
 
 
+def linear_res_ln(x: Tensor, w: Tensor, bias: Optional[Tensor], residual: Tensor, out: Tensor,
+                  ln_w: Tensor, ln_b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor, *,
+                  eps: float = 1e-5, drop: Drop = NO_DROP) -> Tensor:
+    """out = residual + dropout(x·wᵀ + bias) (fp32), y = bf16(LN(out)·ln_w + ln_b), mean/rstd:
+    a residual sub-block's end and the following LayerNorm in one kernel (N = 128)."""
+    _dev(x, w, residual, out, y)
+    M, K = x.shape
+    N = w.shape[0]
+    d = _L.ResLnDesc()
+    d.M, d.N, d.K = M, N, K
+    d.x, d.ldx = _p(x), x.stride(0)
+    d.w, d.ldw = _p(w), w.stride(0)
+    d.bias = _p(bias)
+    d.drop_p, d.drop_seed, d.ld_drop = float(drop[0]), _p(drop[1]), N
+    d.residual, d.ld_res = _p(residual), residual.stride(0)
+    d.out, d.ld_out = _p(out), out.stride(0)
+    d.ln_w, d.ln_b, d.eps = _p(ln_w), _p(ln_b), float(eps)
+    d.y, d.ldy = _p(y), y.stride(0)
+    d.mean, d.rstd = _p(mean), _p(rstd)
+    call("ttmi_linear_res_ln", ctypes.byref(d), _s())
+    return out
+
+
 # ----------------------------------------------------------------------------- cfg 5 pieces
 def l2norm_fwd(x: Tensor, y: Tensor, norms: Tensor) -> Tensor:
     _dev(x, y, norms)
@@ -307,33 +330,44 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, 
                   dw: Optional[Tensor], db: Optional[Tensor], *, gate: Optional[Tensor] = None,
                   gate_scale: float = 1.0, res: Optional[Tensor] = None) -> Tensor:
     M, D = x.shape
+    ws = _zero_ws("ttmi_layernorm_bwd_workspace", (D,), x.device) \
+        if (dw is not None or db is not None) else None
     call("ttmi_layernorm_bwd", M, D, _p(dy), D, _p(x), D, _p(mean), _p(rstd), _p(w), _p(gate),
          code(gate.dtype) if gate is not None else 0, D, gate_scale, _p(res), _p(dx), D, _p(dw),
-         _p(db), _s())
+         _p(db), _p(ws), _s())
     return dx
 
 
 def seq_embed_fwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, b: Tensor, x: Tensor,
-                  mean: Tensor, rstd: Tensor, *, eps: float = 1e-5, drop: Drop = NO_DROP):
+                  mean: Tensor, rstd: Tensor, *, eps: float = 1e-5, drop: Drop = NO_DROP,
+                  norm1: Optional[Tuple[Tensor, Tensor, float, Tensor, Tensor, Tensor]] = None):
+    """x = dropout(LN(E[ids] + P)); with norm1 = (w1, b1, eps1, y1, mean1, rstd1) also
+    y1 = bf16(LN1(x)) (the first encoder layer's norm1, fused)."""
     B, L = ids.shape
     V, D = E.shape
+    w1, b1, eps1, y1, m1, r1 = norm1 if norm1 is not None else (None, None, 0.0, None, None, None)
+    if y1 is not None and y1.dtype != torch.bfloat16:
+        raise ValueError("seq_embed_fwd: norm1 output must be bf16")
     call("ttmi_seq_embed_fwd", B, L, D, _p(ids), _p(E), V, _p(P), _p(w), _p(b), eps,
-         float(drop[0]), _p(drop[1]), _p(x), _p(mean), _p(rstd), _s())
+         float(drop[0]), _p(drop[1]), _p(x), _p(mean), _p(rstd), _p(w1), _p(b1), float(eps1),
+         _p(y1), _p(m1), _p(r1), _s())
     return x
 
 
-_SEB_WS: Dict[tuple, Tensor] = {}
+_ZERO_WS: Dict[tuple, Tensor] = {}
 
 
-def _seq_embed_ws(L: int, D: int, device) -> Tensor:
-    """Persistent per-(device, L, D) workspace of ttmi_seq_embed_bwd: zero on entry, left zero
-    by every call, so one buffer serves every call (and every graph replay) on a stream."""
-    key = (str(device), L, D)
-    ws = _SEB_WS.get(key)
+def _zero_ws(sizer: str, args: tuple, device) -> Tensor:
+    """Persistent zero workspace of the kernels whose column sums go through replicas
+    (ttmi_seq_embed_bwd, ttmi_layernorm_bwd): zero on entry and left zero by every call, so
+    one buffer per (device, entry point, sizes) serves every call and every graph replay on a
+    stream.  Allocated on first use (the warm-up step, before any capture)."""
+    key = (str(device), sizer) + tuple(args)
+    ws = _ZERO_WS.get(key)
     if ws is None:
         _L.load()
-        nb = int(_L._lib.ttmi_seq_embed_bwd_workspace(L, D))
-        ws = _SEB_WS[key] = torch.zeros(nb // 4, device=device, dtype=torch.float32)
+        nb = int(getattr(_L._lib, sizer)(*args))
+        ws = _ZERO_WS[key] = torch.zeros(max(nb // 4, 1), device=device, dtype=torch.float32)
     return ws
 
 
@@ -342,7 +376,7 @@ def seq_embed_bwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, mean: Tensor, rs
                   drop: Drop = NO_DROP, padding_idx: int = 0):
     B, L = ids.shape
     D = E.shape[1]
-    ws = _seq_embed_ws(L, D, dx.device)
+    ws = _zero_ws("ttmi_seq_embed_bwd_workspace", (L, D), dx.device)
     call("ttmi_seq_embed_bwd", B, L, D, _p(ids), _p(E), _p(P), _p(w), _p(mean), _p(rstd),
          float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), _p(dw), _p(db), padding_idx,
          _p(ws), _s())

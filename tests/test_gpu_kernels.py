@@ -582,3 +582,60 @@ def test_linear_ln_bwd(gpu_pkg, M, K, with_res, with_next):
     assert rel(db, bt_.grad) < 5e-5
     if with_next:
         assert rel(nxt.float(), dx_ref * keep / (1 - p)) < 8e-3
+
+
+@pytest.mark.parametrize("M,K", [(300, 128), (4096, 512), (25600, 128)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_linear_res_ln(gpu_pkg, M, K, p):
+    """Fused out = res + dropout(x·wᵀ + b) and y = LN(out) (ttmi_linear_res_ln) vs fp32 torch
+    on the same bf16 operands: out to fp32 accumulation error, y to bf16 rounding, row stats."""
+    ops = gpu_pkg.ops
+    D = 128
+    g = torch.Generator().manual_seed(M + K + int(p * 10))
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(D, K, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(D, generator=g)
+    res = torch.randn(M, D, generator=g)
+    lw = torch.randn(D, generator=g)
+    lb = torch.randn(D, generator=g)
+    seed = 0x5EED
+    keep = keep_mask(seed, (M, D), p).float() if p > 0 else torch.ones(M, D)
+    out_ref = res + (x.float() @ w.float().t() + b) * keep / (1 - p)
+    y_ref = TF.layer_norm(out_ref, (D,), lw, lb, 1e-5)
+    out = torch.empty(M, D, device=DEV)
+    y = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    ops.linear_res_ln(x.to(DEV), w.to(DEV), b.to(DEV), res.to(DEV), out, lw.to(DEV), lb.to(DEV),
+                      y, mean, rstd, eps=1e-5, drop=(p, seed_dev(seed)) if p > 0 else ops.NO_DROP)
+    torch.cuda.synchronize()
+    assert rel(out, out_ref) < 2e-5
+    assert rel(y.float(), y_ref) < 8e-3
+    assert rel(mean, out_ref.mean(1)) < 1e-5
+    assert rel(rstd, 1.0 / torch.sqrt(out_ref.var(1, unbiased=False) + 1e-5)) < 1e-4
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_seq_embed_fwd_norm1(gpu_pkg, p):
+    """seq_embed_fwd with the first layer's norm1 fused: x unchanged, y1 = bf16(LN1(x))."""
+    ops = gpu_pkg.ops
+    B, L, D, V = 37, 50, 128, 301
+    g = torch.Generator().manual_seed(19)
+    ids = torch.randint(0, V, (B, L), generator=g).to(DEV)
+    E, P = torch.randn(V, D, generator=g).to(DEV), torch.randn(L, D, generator=g).to(DEV)
+    w, b = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    w1, b1 = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    sd = seed_dev(123)
+    M = B * L
+    x0, m0, r0 = torch.empty(M, D, device=DEV), torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.seq_embed_fwd(ids, E, P, w, b, x0, m0, r0, drop=(p, sd))
+    x = torch.empty(M, D, device=DEV)
+    m, r = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    y1 = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    m1, r1 = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.seq_embed_fwd(ids, E, P, w, b, x, m, r, drop=(p, sd), norm1=(w1, b1, 1e-5, y1, m1, r1))
+    torch.cuda.synchronize()
+    assert torch.equal(x, x0) and torch.equal(m, m0) and torch.equal(r, r0)
+    y_ref = TF.layer_norm(x.cpu(), (D,), w1.cpu(), b1.cpu(), 1e-5)
+    assert rel(y1.float(), y_ref) < 8e-3
+    assert rel(m1, x.cpu().mean(1)) < 1e-5
