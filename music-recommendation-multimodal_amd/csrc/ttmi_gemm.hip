@@ -498,16 +498,22 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       const char* wb = smem + (cg * 128 + wrow) * WP + lg * (K / 2);
+      // A fragments one k group ahead: group cq+1's loads are in flight under group cq's
+      // MFMAs (two memory latencies overlap instead of one per group)
+      uint4 a[4];
+      if (tile == tile0 && cg == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = a0[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
+      }
 #pragma unroll 1
       for (int cq = 0; cq < KC / 4; ++cq) {
-        uint4 a[4];
-        if (tile == tile0 && cq == 0) {
+        uint4 an[4];
+        const int cn = cq + 1 < KC / 4 ? cq + 1 : cq;      // last group: harmless re-load
 #pragma unroll
-          for (int c = 0; c < 4; ++c) a[c] = a0[c];
-        } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const uint4*>(ap + 64 * cq + 16 * c);
-        }
+        for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const uint4*>(ap + 64 * cn + 16 * c);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
 #pragma unroll
@@ -516,6 +522,8 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
             Mma<bf16_t>::run(acc[t], wf, a[c]);
           }
         }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = an[c];
       }
       if constexpr (LNB) {
         panel_ln_bwd_epilogue(g, ln, acc, m, mok, li, lg, sbias, sdw, sdb, dk2);
