@@ -431,7 +431,14 @@ int ttmi_deb_ln_fwd(int64_t M, int H, const float* z, const float* ln_w, const f
  * [npos, 8] fp32) it also writes the rank-8 contractions that carry the LoRA gradient through
  * posQ = query_proj(rel): lora_hu [B·S, nh, 8] = Σ_i dS_ij·u[δ_ij] and lora_pb [npos, 8]
  * = Σ_{b,h} Σ_ij dS_ij·(K_j·Bq_h)[δ_ij] (overwritten), with lora_bq = lora_B of query_proj [nh·64, 8] fp32 and dS the
- * gradient of the unscaled score terms.  S <= 256. */
+ * gradient of the unscaled score terms.  S <= 256.
+ * Padded tail: let end_b = 1 + the last position with mask != 0.  64-row blocks at or past
+ * end_b are skipped (as keys they are masked for every valid query; as queries they reach
+ * nothing the encoder returns): their ctx rows are written as 0 and lse as 0, and padded
+ * query rows inside a live block attend uniformly over the live blocks' keys instead of all S
+ * (a don't-care value: the masked mean-pool never reads it).  Backward requires dctx == 0 on
+ * padded rows (the mean-pool's gradient is 0 there); outputs on valid rows, and every
+ * gradient, are then those of the full computation (padded-block gradients are exactly 0). */
 typedef struct ttmi_dis_attn_desc {
   int B, S, nh, d_head, npos;
   const void* q; const void* k; const void* v; int64_t ldqkv;

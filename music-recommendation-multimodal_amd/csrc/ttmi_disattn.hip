@@ -104,6 +104,22 @@ TTMI_DEV int win_row(const DisArgs& a, int rel) {
   return a.delta[rel + a.S - 1];
 }
 
+// End of sequence b's attended range: 1 + the last position whose mask is set (0 if none).
+// Blocks of 64 rows at or past it hold only padded tokens: as keys they are masked for every
+// valid query (probability exactly 0), and as queries their outputs reach nothing the encoder
+// returns (the masked mean-pool) and their gradients are exactly 0.  The kernels skip those
+// blocks (block-uniform: every thread of the workgroup computes the same value).
+TTMI_DEV int seq_end(const DisArgs& a, int64_t rowb, int* red) {
+  if (threadIdx.x == 0) *red = 0;
+  __syncthreads();
+  int e = 0;
+  for (int t = threadIdx.x; t < a.S; t += blockDim.x)
+    if (a.mask[rowb + t] != 0) e = t + 1;
+  if (e) atomicMax(red, e);
+  __syncthreads();
+  return *red;
+}
+
 // rows [r0, r0 + R) x 64 bf16 of src -> LDS image (pitch TP); rows >= nrows are zero.  Loads
 // are unconditional from a clamped row (a guarded load compiles to a branch + vmcnt(0)).
 template <int R>
@@ -220,12 +236,22 @@ TTMI_DEV void qside_scores(QSide& L, const DisArgs& a, const uint4 (&qf)[2], boo
 
 __global__ __launch_bounds__(256, 2) void dis_fwd_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) QSide L;
+  __shared__ int s_end;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
   const int S = a.S, i0 = qb * 64, i = i0 + 16 * w + li;
   const int64_t rowb = (int64_t)b * S;
   const DropKeys dk = resolve_drop(a.drop);
   const bool irow = i < S;
+  const int send = seq_end(a, rowb, &s_end);
+  if (i0 >= send) {                      // padded query block: finite placeholder outputs
+    if (!irow) return;
+    bf16_t* dst = a.ctx + (rowb + i) * a.ldctx + h * DH;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), f32x4_t{0.f, 0.f, 0.f, 0.f});
+    if (lg == 0) a.lse[((int64_t)b * a.nh + h) * S + i] = 0.f;
+    return;
+  }
   const bool qvalid = irow && a.mask[rowb + i] != 0;
   const uint4 qf[2] = {fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 0, lane),
                        fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 1, lane)};
@@ -233,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void dis_fwd_kernel(DisArgs a) {
   f32x4_t o[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) o[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 0; j0 < S; j0 += 64) {
+  for (int j0 = 0; j0 < send; j0 += 64) {
     qside_stage(L, a, b, h, i0, j0, tid, w, lane);
     f32x4_t sc[4];
     qside_scores(L, a, qf, qvalid, w, lane, sc);
@@ -280,12 +306,22 @@ __global__ __launch_bounds__(256, 2) void dis_fwd_kernel(DisArgs a) {
 
 __global__ __launch_bounds__(256, 2) void dis_dq_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) QSide L;
+  __shared__ int s_end;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
   const int S = a.S, i0 = qb * 64, i = i0 + 16 * w + li;
   const int64_t rowb = (int64_t)b * S;
   const DropKeys dk = resolve_drop(a.drop);
   const bool irow = i < S;
+  const int send = seq_end(a, rowb, &s_end);
+  if (i0 >= send) {                      // padded query block: dS = 0, so dQ = 0 and D = 0
+    if (!irow) return;
+    bf16_t* dst = a.dq + (rowb + i) * a.lddqkv + h * DH;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), f32x4_t{0.f, 0.f, 0.f, 0.f});
+    if (lg == 0) a.dsum[((int64_t)b * a.nh + h) * S + i] = 0.f;
+    return;
+  }
   const bool qvalid = irow && a.mask[rowb + i] != 0;
   const uint4 qf[2] = {fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 0, lane),
                        fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 1, lane)};
@@ -315,7 +351,7 @@ __global__ __launch_bounds__(256, 2) void dis_dq_kernel(DisArgs a) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) dq[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   char* priv = L.sPQ + 16 * w * WP;
-  for (int j0 = 0; j0 < S; j0 += 64) {
+  for (int j0 = 0; j0 < send; j0 += 64) {
     qside_stage(L, a, b, h, i0, j0, tid, w, lane);
     f32x4_t sc[4], dp[4];
     qside_scores(L, a, qf, qvalid, w, lane, sc);
@@ -384,8 +420,16 @@ struct KSide {
 static_assert(4 * 16 * WP <= WIN * TP, "private images must fit the PKexp window");
 static_assert(sizeof(KSide) <= 80 * 1024, "two workgroups per CU");
 
+// PBexp of a skipped (query block, key block) pair: zero (dis_pb sums every pair).
+TTMI_DEV void zero_pbx(const DisArgs& a, int64_t bh, int qb, int kb) {
+  float* dst = a.pbx + ((bh * a.nqb + qb) * a.nqb + kb) * WIN * 8;
+  for (int t = threadIdx.x; t < WIN * 8 / 4; t += blockDim.x)
+    reinterpret_cast<float4*>(dst)[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) KSide L;
+  __shared__ int s_end;
   const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
   const int S = a.S, j0 = kb * 64, jl = 16 * w + li, j = j0 + jl;
@@ -394,6 +438,23 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
   const DropKeys dk = resolve_drop(a.drop);
   const bool lora = a.u != nullptr;
   const bool jrow = j < S;
+  const int send = seq_end(a, rowb, &s_end);
+  if (j0 >= send) {                      // padded key block: masked for every valid query
+    if (lora)
+      for (int qb = 0; qb < a.nqb; ++qb) zero_pbx(a, bh, qb, kb);
+    if (!jrow) return;
+    bf16_t* pk = a.dk + (rowb + j) * a.lddqkv + h * DH;
+    bf16_t* pv = a.dv + (rowb + j) * a.lddqkv + h * DH;
+    const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      st_bf4(reinterpret_cast<char*>(pk + 16 * u + 4 * lg), z);
+      st_bf4(reinterpret_cast<char*>(pv + 16 * u + 4 * lg), z);
+    }
+    if (lora && lg < 2)
+      *reinterpret_cast<float4*>(a.hu + ((rowb + j) * a.nh + h) * 8 + 4 * lg) = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   const bool kvalid = jrow && a.mask[rowb + j] != 0;
   const uint4 kf[2] = {fglob(a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 0, lane),
                        fglob(a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 1, lane)};
@@ -424,6 +485,10 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
   char* priv = L.sPK + 16 * w * WP;
   for (int qb = 0; qb < a.nqb; ++qb) {
     const int i0 = qb * 64, rel0 = i0 - j0 - 63;
+    if (i0 >= send) {                    // padded query block: dS = 0 and dO = 0
+      if (lora) zero_pbx(a, bh, qb, kb);
+      continue;
+    }
     stage_rows<64>(L.sQ, a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i0, S, tid);
     stage_rows<64>(L.sdO, a.dctx + rowb * a.lddctx + h * DH, a.lddctx, i0, S, tid);
     stage_win(L.sPK, a, a.posk + h * DH, rel0, tid);

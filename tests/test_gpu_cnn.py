@@ -282,8 +282,12 @@ def test_cfg3_train_step_graph_equals_eager_and_learns(gpu_pkg):
     s2 = gpu_pkg.TrainStep(m2, lr=1e-3, use_graph=False, seed=11)
     l1 = [float(s1.step(bd)) for _ in range(12)]
     l2 = [float(s2.step(bd)) for _ in range(12)]
-    assert abs(l1[0] - l2[0]) < 5e-3, (l1[0], l2[0])     # BN-stat atomics: bf16 flips
-    assert abs(l1[1] - l2[1]) < 2e-2, (l1[:3], l2[:3])
+    # Float atomics (BN statistics, split-K weight gradients) make every run's summation order
+    # differ, and bf16 storage through 20 train-mode BN layers amplifies it at B = 16: two
+    # identical EAGER runs measured 3.5e-3 apart at step 0 and 1.6e-2 at step 1
+    # (tools/diag_cfg3_det.py); the bounds are ~2.5x that spread.
+    assert abs(l1[0] - l2[0]) < 1e-2, (l1[0], l2[0])
+    assert abs(l1[1] - l2[1]) < 5e-2, (l1[:3], l2[:3])
     assert l1[-1] < l1[0] - 0.2, l1
     bufs = dict(m1.named_buffers())
     assert int(bufs["item_tower.audio_encoder.backbone.bn1.num_batches_tracked"]) == 12

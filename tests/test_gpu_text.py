@@ -39,7 +39,7 @@ def _bf(t):
 
 
 @pytest.mark.parametrize("B,S,nh,lens", [(2, 64, 1, (64, 30)), (2, 160, 2, (160, 150)),
-                                         (1, 256, 2, (200,))])
+                                         (1, 256, 2, (200,)), (3, 256, 2, (256, 70, 16))])
 def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
     ops = gpu_pkg.ops
     text = gpu_pkg.text
@@ -51,7 +51,9 @@ def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
     mask = torch.zeros(B, S, dtype=torch.int64)
     for b, L in enumerate(lens):
         mask[b, :L] = 1
-    dctx = _bf(torch.randn(B, S, H, generator=g))
+    # padded rows get zero upstream gradient in the encoder (masked mean-pool): the kernels'
+    # precondition for skipping padded blocks (include/ttmi.h, ttmi_dis_attn_desc)
+    dctx = _bf(torch.randn(B, S, H, generator=g)) * mask[:, :, None].to(torch.float32)
     u = torch.randn(npos, 8, generator=g)
     bq = torch.randn(H, 8, generator=g) * 0.1
     delta_t = text._Frozen().delta(S, cfg, "cpu").long()
@@ -93,7 +95,7 @@ def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
     cg = ctx.float().cpu().view(B * S, H)
     cr = ctx_ref.detach().reshape(B * S, H)
     assert rel(cg[valid], cr[valid]) < 1e-2, rel(cg[valid], cr[valid])
-    assert rel(cg, cr) < 1e-2                      # pad rows: uniform attention, as torch
+    assert torch.isfinite(cg).all()                # pad rows: don't-care, finite
     dqkv = torch.zeros(B * S, 3 * H, device=DEV, dtype=torch.bfloat16)
     hu = torch.zeros(B * S * nh * 8, device=DEV)
     pb = torch.full((npos * 8,), 7.0, device=DEV)         # overwritten
