@@ -577,10 +577,12 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; ranks beyond the visible GPU count share them (a multi-rank rehearsal
+    # on a 1-GPU box, with TTMI_DIST_BACKEND=gloo since RCCL wants distinct devices)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("TTMI_DIST_BACKEND", "nccl"))
     device = torch.device("cuda", local)
     if args.config == "eval":
         return main_eval(args, world, rank, device)

@@ -671,7 +671,10 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
   TTMI_REQUIRE(!(dw || db) || ws, "ttmi_layernorm_bwd: dw/db need the workspace");
   if (M == 0) return TTMI_OK;
   const bool sums = dw || db;
-  int grid = (int)std::min<int64_t>((M + 3) / 4, 1024);
+  // one row per wave when there are no column sums (the frozen text-encoder LayerNorms:
+  // a wave walking 16 rows serially ran the stream at ~2.9 TB/s); with sums, 1024 blocks
+  // bound the replicas' adders
+  int grid = (int)std::min<int64_t>((M + 3) / 4, sums ? 1024 : 16384);
   TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(grid), dim3(256), 0, s, M, D, dy,
                                          lddy, x, ldx, mean, rstd, w, gate, gate_dtype == TTMI_F32,
                                          ldg, gate_scale, res, dx, lddx, sums ? (float*)ws : nullptr));

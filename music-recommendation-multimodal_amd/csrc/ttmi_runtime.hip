@@ -180,6 +180,30 @@ __global__ __launch_bounds__(256) void dropout_bwd_vec_kernel(int64_t M, int N,
   if (colsum) colsum_block_reduce(s, N, tpr, rpp, red, colsum);
 }
 
+// Without a column sum the op is a pure stream: flat over (row, 4-column group), grid-stride,
+// enough workgroups to fill every CU (the column-reduction layout above launches ~512
+// workgroups with N/4 of 256 threads busy, ~2.9 TB/s on the text encoder's 65,536 x 768).
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_flat_kernel(int64_t M, int N, const float* __restrict__ dx,
+                                                           int64_t ldx, DropParams d, int64_t ld_drop,
+                                                           const int32_t* __restrict__ drows,
+                                                           T* __restrict__ dy, int64_t ldy) {
+  const int n4 = N >> 2;
+  const int64_t total = M * n4;
+  const DropKeys dk = resolve_drop(d);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / n4;
+    const int n = (int)(i - m * n4) * 4;
+    float4 v = *reinterpret_cast<const float4*>(dx + m * ldx + n);
+    if (dk.on) {
+      const int64_t dr = drows ? (int64_t)drows[m] : m;
+      drop_apply_vec<4>(dk, (uint32_t)(dr * ld_drop + n), &v.x);
+    }
+    store4<T>(dy + m * ldy + n, v.x, v.y, v.z, v.w);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t M, int N, const T* __restrict__ x,
                                                          int64_t ldx, float* __restrict__ colsum,
@@ -398,6 +422,18 @@ extern "C" int ttmi_dropout_bwd(int dtype, int64_t M, int N, const float* dx, in
   if (M == 0) return TTMI_OK;
   DropParams d = make_drop(drop_p, drop_seed);
   if (ld_drop == 0) ld_drop = N;
+  if (!colsum && N % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)dx & 15) == 0 &&
+      ((uintptr_t)dy & (dtype == TTMI_BF16 ? 7 : 15)) == 0) {
+    const int64_t total = M * (N / 4);
+    const dim3 fg((unsigned)std::min<int64_t>((total + 255) / 256, 16384));
+    if (dtype == TTMI_BF16)
+      hipLaunchKernelGGL(dropout_flat_kernel<bf16_t>, fg, dim3(256), 0, s, M, N, dx, ldx, d, ld_drop,
+                         drop_rows, (bf16_t*)dy, ldy);
+    else
+      hipLaunchKernelGGL(dropout_flat_kernel<float>, fg, dim3(256), 0, s, M, N, dx, ldx, d, ld_drop,
+                         drop_rows, (float*)dy, ldy);
+    return ttmi_check_launch("ttmi_dropout_bwd");
+  }
   if (vec_ok(N, ldx, dx, dy) && ldy % 4 == 0) {
     const int64_t rpb = vec_rows_per_block(M, N);
     dim3 vg((unsigned)((M + rpb - 1) / rpb));
