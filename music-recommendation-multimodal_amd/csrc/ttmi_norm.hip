@@ -137,6 +137,45 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
+// Wide rows (D % 256 == 0, no gate, no column sums: the frozen text-encoder LayerNorms,
+// D = 768): one wave per row, each lane 4 consecutive columns per 16-byte access (Q4 = D/256
+// float4 per lane) — the 4-byte-per-lane form streamed at ~3 TB/s.
+template <int Q4>
+__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int64_t M, int D, const float* __restrict__ dy,
+                                                         int64_t lddy, const float* __restrict__ x,
+                                                         int64_t ldx, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd,
+                                                         const float* __restrict__ w,
+                                                         const float* res, float* dx, int64_t lddx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= M) return;
+  const float invD = 1.f / (float)D;
+  const float mu = mean[row], rs = rstd[row];
+  float4 g[Q4], xh[Q4], r[Q4];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < Q4; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    const float4 d = *reinterpret_cast<const float4*>(dy + row * lddy + c);
+    const float4 xv = *reinterpret_cast<const float4*>(x + row * ldx + c);
+    const float4 wv = *reinterpret_cast<const float4*>(w + c);
+    r[i] = res ? *reinterpret_cast<const float4*>(res + row * lddx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+    g[i] = make_float4(d.x * wv.x, d.y * wv.y, d.z * wv.z, d.w * wv.w);
+    s1 += g[i].x + g[i].y + g[i].z + g[i].w;
+    s2 += g[i].x * xh[i].x + g[i].y * xh[i].y + g[i].z * xh[i].z + g[i].w * xh[i].w;
+  }
+  const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
+#pragma unroll
+  for (int i = 0; i < Q4; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    *reinterpret_cast<float4*>(dx + row * lddx + c) =
+        make_float4(r[i].x + rs * (g[i].x - c1 - xh[i].x * c2), r[i].y + rs * (g[i].y - c1 - xh[i].y * c2),
+                    r[i].z + rs * (g[i].z - c1 - xh[i].z * c2), r[i].w + rs * (g[i].w - c1 - xh[i].w * c2));
+  }
+}
+
 // dst0[i] += Σ_r ws[r][i] (i < n0), dst1[i - n0] += ... (n0 <= i < n); zeroes the replicas.
 __global__ __launch_bounds__(256) void colsum_fold_kernel(int n, int n0, int R, float* __restrict__ ws,
                                                           float* __restrict__ dst0,
@@ -671,6 +710,18 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
   TTMI_REQUIRE(!(dw || db) || ws, "ttmi_layernorm_bwd: dw/db need the workspace");
   if (M == 0) return TTMI_OK;
   const bool sums = dw || db;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!sums && !gate && D % 256 == 0 && D <= 1024 && lddy % 4 == 0 && ldx % 4 == 0 &&
+      lddx % 4 == 0 && al16(dy) && al16(x) && al16(w) && al16(dx) && (!res || al16(res))) {
+    const dim3 vg((unsigned)((M + 3) / 4));
+    switch (D / 256) {
+      case 1: hipLaunchKernelGGL(ln_bwd_vec_kernel<1>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
+      case 2: hipLaunchKernelGGL(ln_bwd_vec_kernel<2>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
+      case 3: hipLaunchKernelGGL(ln_bwd_vec_kernel<3>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
+      default: hipLaunchKernelGGL(ln_bwd_vec_kernel<4>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
+    }
+    return ttmi_check_launch("ttmi_layernorm_bwd");
+  }
   // one row per wave when there are no column sums (the frozen text-encoder LayerNorms:
   // a wave walking 16 rows serially ran the stream at ~2.9 TB/s); with sums, 1024 blocks
   // bound the replicas' adders

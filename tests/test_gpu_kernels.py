@@ -639,3 +639,47 @@ def test_seq_embed_fwd_norm1(gpu_pkg, p):
     y_ref = TF.layer_norm(x.cpu(), (D,), w1.cpu(), b1.cpu(), 1e-5)
     assert rel(y1.float(), y_ref) < 8e-3
     assert rel(m1, x.cpu().mean(1)) < 1e-5
+
+
+@pytest.mark.parametrize("D", [256, 768, 1024])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layernorm_bwd_wide_no_sums(gpu_pkg, D, with_res):
+    """The frozen-LayerNorm backward (no dw/db, no gate; the text encoder's post-LNs): the
+    16-byte-per-lane kernel vs torch autograd, with the residual added (and aliased)."""
+    ops = gpu_pkg.ops
+    M = 1000
+    g = torch.Generator().manual_seed(D + with_res)
+    x = torch.randn(M, D, generator=g) * 2 - 0.5
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    xt = x.clone().requires_grad_(True)
+    TF.layer_norm(xt, (D,), w, b, 1e-7).backward(dy := torch.randn(M, D, generator=g))
+    mean = x.mean(1)
+    rstd = 1.0 / torch.sqrt(x.var(1, unbiased=False) + 1e-7)
+    res = torch.randn(M, D, generator=g)
+    dx = res.clone().to(DEV) if with_res else torch.empty(M, D, device=DEV)
+    ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean.to(DEV), rstd.to(DEV), w.to(DEV), dx, None, None,
+                      res=dx if with_res else None)           # res aliases dx
+    torch.cuda.synchronize()
+    assert rel(dx, xt.grad + (res if with_res else 0.0)) < 5e-5
+
+
+@pytest.mark.parametrize("H", [192, 768])
+def test_deb_ln_fwd(gpu_pkg, H):
+    """DeBERTa post-LayerNorm (fp32 copy + bf16 operand with a wider row stride, row stats):
+    the scalar (H % 256 != 0) and the 16-byte-per-lane (H = 768) kernels vs torch."""
+    ops = gpu_pkg.ops
+    M, ld16 = 517, H + 64
+    g = torch.Generator().manual_seed(H)
+    z = torch.randn(M, H, generator=g) * 3 + 0.25
+    w, b = torch.randn(H, generator=g), torch.randn(H, generator=g)
+    ref = TF.layer_norm(z, (H,), w, b, 1e-7)
+    y32 = torch.empty(M, H, device=DEV)
+    y16 = torch.zeros(M, ld16, device=DEV, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.deb_ln_fwd(z.to(DEV), w.to(DEV), b.to(DEV), 1e-7, y32, y16[:, :H], mean, rstd)
+    torch.cuda.synchronize()
+    assert rel(y32, ref) < 2e-5
+    assert rel(y16[:, :H].float(), ref) < 8e-3
+    assert y16[:, H:].abs().max().item() == 0.0
+    assert rel(mean, z.mean(1)) < 1e-5
