@@ -226,8 +226,8 @@ __global__ __launch_bounds__(256) void skinny_wgrad_kernel(int64_t R, int Mw, co
     for (int c = 0; c < 8; ++c) acc[i][c] = 0.f;
   if (rg < RG) {
     const int soff = (c8 * 8 / group) * sgs;
-    // 4 rows per step: all loads issued before the FMAs (the loop is load-latency bound)
-    constexpr int U = 4;
+    // 8 rows per step: all loads issued before the FMAs (the loop is load-latency bound)
+    constexpr int U = 8;
     for (int64_t rb = r0 + rg; rb < r1; rb += U * RG) {
       uint4 wq[U], sq[U], sq2[U];
 #pragma unroll
@@ -279,6 +279,10 @@ __global__ __launch_bounds__(256) void skinny_wgrad_kernel(int64_t R, int Mw, co
 // query_proj / value_proj; drop_p regenerates the forward LoRA-dropout mask at m·ld_drop + n).
 // dL [M, 16] bf16 = [dL_q | dL_v], A_q/A_v [8, H] bf16.  One thread per 8 columns; HBM-bound on
 // the fp32 read-modify-write of dx (replaces two K=8 accumulate GEMMs with atomics).
+// A thread owns 8 columns of LDX_ROWS consecutive rows: the 16 A fragments (8 ranks x q/v) it
+// needs are loaded once per LDX_ROWS rows, and every row's dL / dx loads are issued before
+// the arithmetic.
+constexpr int LDX_ROWS = 4;
 __global__ __launch_bounds__(256) void lora_dx_kernel(int64_t M, int H, const bf16_t* __restrict__ dL,
                                                       int64_t ld_dl, const bf16_t* __restrict__ aq,
                                                       const bf16_t* __restrict__ av, float s,
@@ -286,32 +290,54 @@ __global__ __launch_bounds__(256) void lora_dx_kernel(int64_t M, int H, const bf
                                                       float* __restrict__ dx, int64_t ld_dx) {
   const int ncol8 = H / 8;
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= M * ncol8) return;
-  const int64_t m = id / ncol8;
+  const int64_t mblocks = (M + LDX_ROWS - 1) / LDX_ROWS;
+  if (id >= mblocks * ncol8) return;
+  const int64_t m0 = (id / ncol8) * LDX_ROWS;
   const int n = (int)(id % ncol8) * 8;
   const DropKeys kq = resolve_drop(dq), kv = resolve_drop(dv);
-  float lq[8], lv[8];
-  unpack8(*reinterpret_cast<const uint4*>(dL + m * ld_dl), lq);
-  unpack8(*reinterpret_cast<const uint4*>(dL + m * ld_dl + 8), lv);
-  float yq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, yv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  uint4 lqv[LDX_ROWS][2];
+  float4 xr[LDX_ROWS][2];
+#pragma unroll
+  for (int j = 0; j < LDX_ROWS; ++j) {
+    const int64_t m = min(m0 + j, M - 1);
+    lqv[j][0] = *reinterpret_cast<const uint4*>(dL + m * ld_dl);
+    lqv[j][1] = *reinterpret_cast<const uint4*>(dL + m * ld_dl + 8);
+    xr[j][0] = *reinterpret_cast<const float4*>(dx + m * ld_dx + n);
+    xr[j][1] = *reinterpret_cast<const float4*>(dx + m * ld_dx + n + 4);
+  }
+  uint4 ap[8], bp[8];                     // packed bf16, unpacked per use (register budget)
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    float a[8], b[8];
-    unpack8(*reinterpret_cast<const uint4*>(aq + r * H + n), a);
-    unpack8(*reinterpret_cast<const uint4*>(av + r * H + n), b);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { yq[e] += lq[r] * a[e]; yv[e] += lv[r] * b[e]; }
+    ap[r] = *reinterpret_cast<const uint4*>(aq + r * H + n);
+    bp[r] = *reinterpret_cast<const uint4*>(av + r * H + n);
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { yq[e] *= s; yv[e] *= s; }
-  drop_apply_vec<8>(kq, (uint32_t)(m * ld_drop + n), yq);
-  drop_apply_vec<8>(kv, (uint32_t)(m * ld_drop + n), yv);
-  float* p = dx + m * ld_dx + n;
-  float4 x0 = *reinterpret_cast<float4*>(p), x1 = *reinterpret_cast<float4*>(p + 4);
-  x0.x += yq[0] + yv[0]; x0.y += yq[1] + yv[1]; x0.z += yq[2] + yv[2]; x0.w += yq[3] + yv[3];
-  x1.x += yq[4] + yv[4]; x1.y += yq[5] + yv[5]; x1.z += yq[6] + yv[6]; x1.w += yq[7] + yv[7];
-  *reinterpret_cast<float4*>(p) = x0;
-  *reinterpret_cast<float4*>(p + 4) = x1;
+  for (int j = 0; j < LDX_ROWS; ++j) {
+    const int64_t m = m0 + j;
+    if (m >= M) break;
+    float lq[8], lv[8];
+    unpack8(lqv[j][0], lq);
+    unpack8(lqv[j][1], lv);
+    float yq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, yv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float a[8], b[8];
+      unpack8(ap[r], a);
+      unpack8(bp[r], b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { yq[e] += lq[r] * a[e]; yv[e] += lv[r] * b[e]; }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { yq[e] *= s; yv[e] *= s; }
+    drop_apply_vec<8>(kq, (uint32_t)(m * ld_drop + n), yq);
+    drop_apply_vec<8>(kv, (uint32_t)(m * ld_drop + n), yv);
+    float4 x0 = xr[j][0], x1 = xr[j][1];
+    x0.x += yq[0] + yv[0]; x0.y += yq[1] + yv[1]; x0.z += yq[2] + yv[2]; x0.w += yq[3] + yv[3];
+    x1.x += yq[4] + yv[4]; x1.y += yq[5] + yv[5]; x1.z += yq[6] + yv[6]; x1.w += yq[7] + yv[7];
+    float* p = dx + m * ld_dx + n;
+    *reinterpret_cast<float4*>(p) = x0;
+    *reinterpret_cast<float4*>(p + 4) = x1;
+  }
 }
 
 }  // namespace
@@ -415,7 +441,7 @@ extern "C" int ttmi_lora_dx(int64_t M, int H, const uint16_t* dL, int64_t ld_dl,
                (uintptr_t)aq % 16 == 0 && (uintptr_t)av % 16 == 0 && (uintptr_t)dx % 16 == 0,
                "ttmi_lora_dx: operands need 16-byte rows");
   TTMI_REQUIRE(drop_p == 0.f || (seed_q && seed_v), "ttmi_lora_dx: dropout needs both seeds");
-  const int64_t n = M * (H / 8);
+  const int64_t n = (M + LDX_ROWS - 1) / LDX_ROWS * (H / 8);
   hipLaunchKernelGGL(lora_dx_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, H,
                      (const bf16_t*)dL, ld_dl, (const bf16_t*)aq, (const bf16_t*)av, scale,
                      make_drop(drop_p, seed_q), make_drop(drop_p, seed_v), ld_drop, dx, ld_dx);

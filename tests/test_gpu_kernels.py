@@ -183,9 +183,10 @@ def test_skinny_wgrad(gpu_pkg, s_dt, R, Mw, group, trans):
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_lora_dx(gpu_pkg, p):
+@pytest.mark.parametrize("M", [5000, 5003])          # rows per thread: 4 (and a ragged tail)
+def test_lora_dx(gpu_pkg, p, M):
     ops = gpu_pkg.ops
-    M, H = 5000, 768
+    H = 768
     g = torch.Generator().manual_seed(3)
     dL = torch.randn(M, 16, generator=g).to(torch.bfloat16)
     aq = torch.randn(8, H, generator=g).to(torch.bfloat16)
