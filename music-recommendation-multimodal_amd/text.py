@@ -256,6 +256,18 @@ def _drop(p: float, seeds: Optional[Tensor], site: int):
     return ops.NO_DROP
 
 
+_SIDE: Dict[str, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(dev) -> "torch.cuda.Stream":
+    """One side stream per device for the backward's LoRA-gradient streams (created on first
+    use, i.e. in an eager step before any graph capture)."""
+    key = str(dev)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(dev)
+    return _SIDE[key]
+
+
 def _mm(A, B, C, M, N, K, *, lda, ldb, ldc, a_k=True, b_k=True, **kw):
     return ops.gemm(A, B, C, M, N, K, lda=lda, a_kmajor=a_k, ldb=ldb, b_kmajor=b_k, ldc=ldc, **kw)
 
@@ -392,6 +404,9 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
     dpooled = torch.empty(B, H, device=dev)
     ops.linear_dx(dy1, st.w0, dpooled)
     dx = ops.deb_pool_bwd(dpooled, st.mask, torch.empty(M, H, device=dev))
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    keep = []
     for l in reversed(range(c.layers)):
         sv = st.layers[l]
         W = Fz.layers[l]
@@ -422,29 +437,38 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
                      sv.ctx, sv.lse, _drop(pa, seeds, tsite(l, 0)), dctx=dctx, dq=dqkv[:, :H],
                      dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:], lora_u=sv.u, lora_bq=bq32,
                      lora_hu=hu, lora_pb=pb)
-        # input gradient through the QKV GEMM (+ residual) and the LoRA branch
-        dxn = torch.empty(M, H, device=dev)
-        _mm(dqkv, W["wqkvT"], dxn, M, H, 3 * H, lda=3 * H, ldb=3 * H, ldc=H, residual=dz1, ld_res=H)
-        dL = torch.empty(M, 2 * r, device=dev, dtype=bf)
-        _mm(dqkv, W["waug"][:, H:], dL, M, 2 * r, 3 * H, lda=3 * H, ldb=Ha, ldc=2 * r, b_k=False)
+        # input gradient through the QKV GEMM (+ residual) and the LoRA branch.  The rank-8
+        # LoRA weight gradients are HBM streams that no later op of this backward reads: they
+        # run on a side stream under the (MFMA-bound) dgrad GEMM.  dL goes first so the side
+        # stream can start on it; its inputs stay referenced in `keep` until the streams join.
         gAq, gBq = G[lp + "query_proj.lora_A.default.weight"], G[lp + "query_proj.lora_B.default.weight"]
         gAv, gBv = G[lp + "value_proj.lora_A.default.weight"], G[lp + "value_proj.lora_B.default.weight"]
-        # dB = dYᵀ·t (t = s·u lives in the augmented operand columns): rank-8 HBM streams
-        ops.skinny_wgrad(dqkv[:, :H], sv.xaug[:, H:H + r], gBq, H, ldc_m=r, ldc_c=1)
-        ops.skinny_wgrad(dqkv[:, 2 * H:], sv.xaug[:, H + r:H + 2 * r], gBv, H, ldc_m=r, ldc_c=1)
-        # dA = s·dLᵀ·drop(x);  dx += s·drop'(dL·A) for q and v in one pass over dx
-        ops.skinny_wgrad(sv.xq, dL[:, :r], gAq, H, ldc_m=1, ldc_c=H, alpha=s)
-        ops.skinny_wgrad(sv.xv, dL[:, r:], gAv, H, ldc_m=1, ldc_c=H, alpha=s)
+        dL = torch.empty(M, 2 * r, device=dev, dtype=bf)
+        _mm(dqkv, W["waug"][:, H:], dL, M, 2 * r, 3 * H, lda=3 * H, ldb=Ha, ldc=2 * r, b_k=False)
+        side.wait_stream(main)
+        keep.append((dqkv, dL, hu, pb))
+        with torch.cuda.stream(side):
+            # dB = dYᵀ·t (t = s·u lives in the augmented operand columns)
+            ops.skinny_wgrad(dqkv[:, :H], sv.xaug[:, H:H + r], gBq, H, ldc_m=r, ldc_c=1)
+            ops.skinny_wgrad(dqkv[:, 2 * H:], sv.xaug[:, H + r:H + 2 * r], gBv, H, ldc_m=r, ldc_c=1)
+            # dA = s·dLᵀ·drop(x)
+            ops.skinny_wgrad(sv.xq, dL[:, :r], gAq, H, ldc_m=1, ldc_c=H, alpha=s)
+            ops.skinny_wgrad(sv.xv, dL[:, r:], gAv, H, ldc_m=1, ldc_c=H, alpha=s)
+            # relative path: posQ = query_proj(rel) carries the q LoRA too:
+            # dBq[h·64 + d, c] += s·Σ_m K[m, h·64 + d]·HU[m, h, c]  (per-head slices of HU)
+            ops.skinny_wgrad(sv.qkv[:, H:2 * H], hu.view(M, nh * 8), gBq, H, ldc_m=r, ldc_c=1,
+                             alpha=s, group=64, sgs=8)
+            du = pb
+            _mm(du, sv.relq, gAq, r, H, c.npos, lda=r, ldb=H, ldc=H, a_k=False, b_k=False, alpha=s,
+                accumulate=True)
+        dxn = torch.empty(M, H, device=dev)
+        _mm(dqkv, W["wqkvT"], dxn, M, H, 3 * H, lda=3 * H, ldb=3 * H, ldc=H, residual=dz1, ld_res=H)
+        # dx += s·drop'(dL·A) for q and v in one pass over dx
         ops.lora_dx(dL, st.aq16[l], st.av16[l], s, _drop(pl, seeds, tsite(l, 3)),
                     _drop(pl, seeds, tsite(l, 4)), dxn, H)
-        # relative path: posQ = query_proj(rel) carries the q LoRA too:
-        # dBq[h·64 + d, c] += s·Σ_m K[m, h·64 + d]·HU[m, h, c]  (per-head slices of HU)
-        ops.skinny_wgrad(sv.qkv[:, H:2 * H], hu.view(M, nh * 8), gBq, H, ldc_m=r, ldc_c=1, alpha=s,
-                         group=64, sgs=8)
-        du = pb
-        _mm(du, sv.relq, gAq, r, H, c.npos, lda=r, ldb=H, ldc=H, a_k=False, b_k=False, alpha=s,
-            accumulate=True)
         dx = dxn
+    main.wait_stream(side)
+    del keep
     # the embeddings are frozen: the gradient stops here
 
 
