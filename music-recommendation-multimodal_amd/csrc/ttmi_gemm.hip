@@ -1332,9 +1332,11 @@ bool panel_applies(const ttmi_gemm_desc* d) {
 
 template <int NT, int KC, int EPI>
 void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBwdArgs{}) {
-  // contiguous row ranges, >= 8 tiles (one per wave) per workgroup, about one per CU
+  // contiguous row ranges, about one workgroup per CU; fewer than 8 tiles per workgroup
+  // leaves waves idle but puts a workgroup on more CUs (M = 25,600 -> 1,600 tiles -> 229
+  // workgroups of 7 instead of 200 of 8 on 256 CUs)
   const int64_t tiles = (a.M + 15) / 16;
-  const int64_t tpw = std::max<int64_t>(8, (tiles + num_cus() - 1) / num_cus());
+  const int64_t tpw = std::max<int64_t>(1, (tiles + num_cus() - 1) / num_cus());
   const int64_t grid = (tiles + tpw - 1) / tpw;
   hipLaunchKernelGGL((panel_kernel<NT, KC, EPI>), dim3((unsigned)grid), dim3(512), 0, s, a, (int)tpw, ln);
 }
