@@ -240,7 +240,7 @@ def test_cfg3_two_tower_vs_oracle(gpu_pkg):
     rref.resnet18_forward = resnet18_bf16_emulation       # bf16-storage yardstick
     try:
         pe = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
-        le = ref.two_tower_loss(pe, batch, running=None)[0]
+        le, logits_emu = ref.two_tower_loss(pe, batch, running=None)[:2]
         le.backward()
         lemu = float(le)
     finally:
@@ -251,7 +251,10 @@ def test_cfg3_two_tower_vs_oracle(gpu_pkg):
     torch.cuda.synchronize()
     bound = 2.0 * abs(lemu - float(lref)) + 5e-3
     assert abs(float(loss) - float(lref)) < bound, (float(loss), float(lref), lemu)
-    assert rel(logits, logits_ref) < 5e-2
+    # same yardstick as the loss: 2x the bf16-emulation's own logit deviation + 1e-2 (float
+    # atomics move the GPU value run to run by ~1e-2 here)
+    assert rel(logits, logits_ref) < 2.0 * rel(logits_emu, logits_ref) + 1e-2, \
+        (rel(logits, logits_ref), rel(logits_emu, logits_ref))
     mine = dict(m.named_parameters())
     # identically-zero true gradients (a bias feeding straight into a train-mode BatchNorm:
     # fusion_layer.0.bias, the tabular mlp.0.bias; and every encoder's last bias, whose output
