@@ -211,7 +211,9 @@ def test_cfg4_train_step_graph_equals_eager_and_learns(gpu_pkg):
     s2 = gpu_pkg.TrainStep(m2, lr=1e-3, use_graph=False, seed=5)
     l1 = [float(s1.step(bd)) for _ in range(10)]
     l2 = [float(s2.step(bd)) for _ in range(10)]
-    assert abs(l1[0] - l2[0]) < 5e-3, (l1[0], l2[0])
+    # step 0 is forward-only; float atomics (BN statistics in the two ResNet-18s) still move
+    # it run to run: two identical eager cfg-3 runs differ by ~3.5e-3 (tools/diag_cfg3_det.py)
+    assert abs(l1[0] - l2[0]) < 1e-2, (l1[0], l2[0])
     # Later steps are not compared value-for-value: AdamW's first update is ~lr·sign(g), and
     # cfg 4 has several exactly-zero true gradients (every bias feeding the fusion head's
     # BatchNorm: backbone.fc.bias x2, mlp.4.bias, projection.3.bias) whose sign is atomic-order
