@@ -402,15 +402,19 @@ __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_
     stage_heads<DH, 3>(dst, src, ld, L, threadIdx.x);
   }
   // key validity of the 4 keys 16t + 4lg + e this lane holds, per key tile t
+  // key validity as one 64-bit ballot of wave 0 (one 8-byte load per lane, not 16)
+  __shared__ uint64_t s_kv;
+  if (wave == 0) {
+    const uint64_t bal = __ballot(lane < L && kvalid[(int64_t)b * L + min(lane, L - 1)] != 0);
+    if (lane == 0) s_kv = bal;
+  }
+  __syncthreads();
+  const uint64_t kvm = s_kv;
   bool kv[4][4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = 16 * t + 4 * lg + e;
-      kv[t][e] = k < L && kvalid[(int64_t)b * L + min(k, L - 1)] != 0;
-    }
-  __syncthreads();
+    for (int e = 0; e < 4; ++e) kv[t][e] = (kvm >> (16 * t + 4 * lg + e)) & 1ull;
   const DropKeys dk = resolve_drop(dp);
   const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
   constexpr int NC = DH / 32;                      // 32-wide k chunks of the head dim
@@ -511,15 +515,19 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
     const bf16_t* const s1[1] = {src[3]};
     stage_heads<DH, 1>(d1, s1, D, L, threadIdx.x);
   }
+  // key validity as one 64-bit ballot of wave 0 (one 8-byte load per lane, not 16)
+  __shared__ uint64_t s_kv;
+  if (wave == 0) {
+    const uint64_t bal = __ballot(lane < L && kvalid[(int64_t)b * L + min(lane, L - 1)] != 0);
+    if (lane == 0) s_kv = bal;
+  }
+  __syncthreads();
+  const uint64_t kvm = s_kv;
   bool kv[4][4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = 16 * t + 4 * lg + e;
-      kv[t][e] = k < L && kvalid[(int64_t)b * L + min(k, L - 1)] != 0;
-    }
-  __syncthreads();
+    for (int e = 0; e < 4; ++e) kv[t][e] = (kvm >> (16 * t + 4 * lg + e)) & 1ull;
   const DropKeys dk = resolve_drop(dp);
   const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
   constexpr int NC = DH / 32;
