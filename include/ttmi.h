@@ -150,10 +150,11 @@ int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
                          const int64_t* len_src, const int64_t* gender, const float* G, int dg,
                          const int64_t* country, const float* C, int dc, void* comb,
                          int32_t* rows, hipStream_t stream);
-/* Backward: dx[rows[b]] += dcomb[b,:D]; dG[gender[b]] += ...; dC[country[b]] += ... */
+/* Backward: dx[rows[b]] += dcomb[b,:D] (accumulate != 0; = when 0, rows distinct);
+ * dG[gender[b]] += ...; dC[country[b]] += ... */
 int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
                          const int64_t* gender, int dg, const int64_t* country, int dc,
-                         float* dx, float* dG, float* dC, hipStream_t stream);
+                         float* dx, float* dG, float* dC, int accumulate, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * BatchNorm1d + ReLU + dropout (item_tower.py:122-126 fusion head, item_tower.py:89-93
@@ -309,8 +310,9 @@ int ttmi_step_inc(int32_t* step, hipStream_t stream);
  * Elementwise helpers.
  * ---------------------------------------------------------------------------------- */
 /* seeds[s] = splitmix64(splitmix64(base) ^ (*step * 64 + s)), s < n <= 256: per-site dropout
- * seeds of the current step, derived on device from the live step counter. */
-int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int n,
+ * seeds of the current step, derived on device from the live step counter.  inc_step != 0
+ * increments *step first (ttmi_step_inc in the same launch). */
+int ttmi_dropout_seeds(uint64_t base, int32_t* step, uint64_t* seeds, int n, int inc_step,
                        hipStream_t stream);
 /* dst[i][0:nbytes[i]] = src[i][...] for i < n <= 16 device buffers, in one launch (stages a
  * batch's tensors into a captured step's static inputs). */
@@ -385,6 +387,9 @@ int ttmi_colsum(int dtype, int64_t M, int N, const void* x, int64_t ldx, float* 
  * ---------------------------------------------------------------------------------- */
 /* rows[b] = b*L + max(Σ_l (len_src[b,l] != 0) - 1, 0). */
 int ttmi_last_rows(int B, int L, const int64_t* len_src, int32_t* rows, hipStream_t stream);
+/* ttmi_last_rows + ttmi_gather_rows in one launch. */
+int ttmi_last_rows_gather(int B, int L, int D, const int64_t* len_src, const float* x,
+                          int32_t* rows, float* out, hipStream_t stream);
 /* out[b,:] = x[rows[b],:] (fp32, row width D). */
 int ttmi_gather_rows(int B, int D, const float* x, const int32_t* rows, float* out,
                      hipStream_t stream);

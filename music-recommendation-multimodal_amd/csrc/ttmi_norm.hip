@@ -427,7 +427,7 @@ __global__ void user_concat_bwd_kernel(int B, int D, const float* __restrict__ d
                                        const int64_t* __restrict__ gender, int dg,
                                        const int64_t* __restrict__ country, int dc,
                                        float* __restrict__ dx, float* __restrict__ dG,
-                                       float* __restrict__ dC) {
+                                       float* __restrict__ dC, int accumulate) {
   const int lane = threadIdx.x & 63;
   const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (b >= B) return;
@@ -436,7 +436,10 @@ __global__ void user_concat_bwd_kernel(int B, int D, const float* __restrict__ d
   const int64_t g = gender[b], c = country[b];
   for (int k = lane; k < W; k += 64) {
     const float v = dcomb[(int64_t)b * W + k];
-    if (k < D) atomicAdd(dx + row * D + k, v);
+    if (k < D) {
+      if (accumulate) atomicAdd(dx + row * D + k, v);
+      else dx[row * D + k] = v;            // rows distinct: each dx row has one writer
+    }
     else if (k < D + dg) { if (dG) atomicAdd(dG + g * dg + (k - D), v); }
     else if (dC) atomicAdd(dC + c * dc + (k - D - dg), v);
   }
@@ -809,12 +812,12 @@ extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float*
 
 extern "C" int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
                                     const int64_t* gender, int dg, const int64_t* country, int dc,
-                                    float* dx, float* dG, float* dC, hipStream_t s) {
+                                    float* dx, float* dG, float* dC, int accumulate, hipStream_t s) {
   TTMI_REQUIRE(B >= 0 && D > 0 && dg >= 0 && dc >= 0, "ttmi_user_concat_bwd: bad sizes");
   TTMI_REQUIRE(dcomb && rows && gender && country && dx, "ttmi_user_concat_bwd: null argument");
   if (B == 0) return TTMI_OK;
   hipLaunchKernelGGL(user_concat_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, B, D, dcomb, rows,
-                     gender, dg, country, dc, dx, dG, dC);
+                     gender, dg, country, dc, dx, dG, dC, accumulate);
   return ttmi_check_launch("ttmi_user_concat_bwd");
 }
 

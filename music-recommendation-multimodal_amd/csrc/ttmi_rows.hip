@@ -25,6 +25,27 @@ __global__ void last_rows_kernel(int B, int L, const int64_t* __restrict__ len_s
   if (lane == 0) rows[b] = (int32_t)((int64_t)b * L + max(len - 1, 0));
 }
 
+// last_rows + gather_rows in one launch: wave per sequence counts its valid positions, then
+// copies that row (16-byte lanes when D % 4 == 0).
+__global__ void last_rows_gather_kernel(int B, int L, int D, const int64_t* __restrict__ len_src,
+                                        const float* __restrict__ x, int32_t* __restrict__ rows,
+                                        float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (b >= B) return;
+  float cnt = 0.f;
+  for (int l = lane; l < L; l += 64) cnt += len_src[(int64_t)b * L + l] != 0 ? 1.f : 0.f;
+  const int len = (int)(wave_sum(cnt) + 0.5f);
+  const int64_t r = (int64_t)b * L + max(len - 1, 0);
+  if (lane == 0) rows[b] = (int32_t)r;
+  if (D % 4 == 0) {
+    for (int c = lane * 4; c < D; c += 256)
+      *reinterpret_cast<float4*>(out + (int64_t)b * D + c) = *reinterpret_cast<const float4*>(x + r * D + c);
+  } else {
+    for (int c = lane; c < D; c += 64) out[(int64_t)b * D + c] = x[r * D + c];
+  }
+}
+
 __global__ void gather_rows_kernel(int B, int D, const float* __restrict__ x,
                                    const int32_t* __restrict__ rows, float* __restrict__ out) {
   const int b = blockIdx.x;
@@ -216,6 +237,17 @@ extern "C" int ttmi_last_rows(int B, int L, const int64_t* len_src, int32_t* row
   if (B == 0) return TTMI_OK;
   hipLaunchKernelGGL(last_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, s, B, L, len_src, rows);
   return ttmi_check_launch("ttmi_last_rows");
+}
+
+extern "C" int ttmi_last_rows_gather(int B, int L, int D, const int64_t* len_src, const float* x,
+                                     int32_t* rows, float* out, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && len_src && x && rows && out, "ttmi_last_rows_gather: bad args");
+  TTMI_REQUIRE(D % 4 != 0 || (((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0),
+               "ttmi_last_rows_gather: x/out need 16-byte alignment");
+  if (B == 0) return TTMI_OK;
+  hipLaunchKernelGGL(last_rows_gather_kernel, dim3((B + 3) / 4), dim3(256), 0, s, B, L, D, len_src, x,
+                     rows, out);
+  return ttmi_check_launch("ttmi_last_rows_gather");
 }
 
 extern "C" int ttmi_gather_rows(int B, int D, const float* x, const int32_t* rows, float* out,

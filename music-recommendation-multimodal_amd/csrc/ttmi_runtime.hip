@@ -25,7 +25,7 @@ int ttmi_check_launch(const char* what) {
 }
 
 extern "C" const char* ttmi_last_error(void) { return g_err; }
-extern "C" int ttmi_abi_version(void) { return 2; }
+extern "C" int ttmi_abi_version(void) { return 3; }
 
 namespace {
 
@@ -106,9 +106,13 @@ TTMI_DEV uint64_t splitmix64(uint64_t x) {
 }
 
 // seeds[s] = splitmix64(splitmix64(base) ^ (step*64 + s)) — functional.site_seeds restates it.
-__global__ void dropout_seeds_kernel(uint64_t base, const int32_t* step, uint64_t* seeds, int n) {
+// With inc, the step counter is incremented first (ttmi_step_inc folded in: one launch).
+__global__ void dropout_seeds_kernel(uint64_t base, int32_t* step, uint64_t* seeds, int n, int inc) {
   const int s = threadIdx.x;
-  if (s < n) seeds[s] = splitmix64(splitmix64(base) ^ ((uint64_t)(int64_t)step[0] * 64ull + (uint64_t)s));
+  const int32_t t = step[0] + (inc ? 1 : 0);
+  if (s < n) seeds[s] = splitmix64(splitmix64(base) ^ ((uint64_t)(int64_t)t * 64ull + (uint64_t)s));
+  __syncthreads();                        // every thread has read the old count
+  if (inc && s == 0) step[0] = t;
 }
 
 // Column-reduction layout shared by dropout_bwd / colsum: each thread owns 4 consecutive
@@ -404,10 +408,10 @@ extern "C" int ttmi_step_inc(int32_t* step, hipStream_t s) {
   return ttmi_check_launch("ttmi_step_inc");
 }
 
-extern "C" int ttmi_dropout_seeds(uint64_t base, const int32_t* step, uint64_t* seeds, int n,
+extern "C" int ttmi_dropout_seeds(uint64_t base, int32_t* step, uint64_t* seeds, int n, int inc_step,
                                   hipStream_t s) {
   TTMI_REQUIRE(step && seeds && n > 0 && n <= 256, "ttmi_dropout_seeds: bad args");
-  hipLaunchKernelGGL(dropout_seeds_kernel, dim3(1), dim3(256), 0, s, base, step, seeds, n);
+  hipLaunchKernelGGL(dropout_seeds_kernel, dim3(1), dim3(256), 0, s, base, step, seeds, n, inc_step);
   return ttmi_check_launch("ttmi_dropout_seeds");
 }
 

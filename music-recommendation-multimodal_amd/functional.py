@@ -210,9 +210,8 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
         F_ = W[pre + "linear1.weight"].shape[0]
         if pruned:
             rows = torch.empty(B, device=dev, dtype=torch.int32)
-            ops.last_rows(key_valid, rows)
             R, res_in, drows = B, torch.empty(B, D, **f32), rows
-            ops.gather_rows(x, rows, res_in)
+            ops.last_rows_gather(key_valid, x, rows, res_in)
             ctx = torch.empty(B, D, device=dev, dtype=dt)
             lse = torch.empty(B * H, **f32)
             ops.mha_q1_fwd(qkv, key_valid, rows, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
@@ -295,11 +294,13 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
     dcomb = torch.empty(B, st.comb.shape[1], **f32)
     ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dcomb)
     gathered = cfg.prune_last and cfg.n_layers > 0
-    dx = torch.zeros(B if gathered else M, D, **f32)
+    # gathered: every row of dx [B, D] is written once (no zero fill); else only B of M rows
+    dx = torch.empty(B, D, **f32) if gathered else torch.zeros(M, D, **f32)
     G = P["gender_embedding.weight"]
     C = P["country_embedding.weight"]
     ops.user_concat_bwd(dcomb, st.rows, st.gender, G.shape[1], st.country, C.shape[1], dx,
-                        grads["gender_embedding.weight"], grads["country_embedding.weight"])
+                        grads["gender_embedding.weight"], grads["country_embedding.weight"],
+                        accumulate=not gathered)
     # ---- encoder layers, reversed (user_tower.py:37-45)
     p = cfg.p_drop
     dy2_next = None        # layer i's dy2, emitted by layer i+1's fused LN1 backward

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -112,7 +112,7 @@ SIGNATURES = {
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_user_concat_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_p,
                                    c_p, c_p]),
-    "ttmi_user_concat_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_user_concat_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p, c_i, c_p]),
     "ttmi_batchnorm_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_i, c_i,
                                  c_f, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_batchnorm_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_i, c_p, c_p, c_p,
@@ -164,11 +164,12 @@ SIGNATURES = {
                              c_p, c_p, c_p, c_p]),
     "ttmi_sum_scaled": (c_i, [c_i, c_p, c_f, c_p, c_p]),
     "ttmi_step_inc": (c_i, [c_p, c_p]),
-    "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_p]),
+    "ttmi_dropout_seeds": (c_i, [c_u64, c_p, c_p, c_i, c_i, c_p]),
     "ttmi_cast_f32_bf16": (c_i, [c_i64, c_p, c_p, c_p]),
     "ttmi_dropout_bwd": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_f, c_p, c_i64, c_p, c_p, c_i64, c_p,
                                c_p]),
     "ttmi_last_rows": (c_i, [c_i, c_i, c_p, c_p, c_p]),
+    "ttmi_last_rows_gather": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_gather_rows": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_scatter_add_rows": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_mha_q1_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),

@@ -409,11 +409,12 @@ def user_concat_fwd(x: Tensor, len_src: Optional[Tensor], gender: Tensor, G: Ten
 
 
 def user_concat_bwd(dcomb: Tensor, rows: Tensor, gender: Tensor, dg: int, country: Tensor,
-                    dc: int, dx: Tensor, dG: Optional[Tensor], dC: Optional[Tensor]):
+                    dc: int, dx: Tensor, dG: Optional[Tensor], dC: Optional[Tensor],
+                    accumulate: bool = True):
     B = dcomb.shape[0]
     D = dcomb.shape[1] - dg - dc
     call("ttmi_user_concat_bwd", B, D, _p(dcomb), _p(rows), _p(gender), dg, _p(country), dc,
-         _p(dx), _p(dG), _p(dC), _s())
+         _p(dx), _p(dG), _p(dC), int(accumulate), _s())
 
 
 # ----------------------------------------------------------------------------- batchnorm
@@ -499,8 +500,11 @@ def step_inc(step: Tensor):
     call("ttmi_step_inc", _p(step), _s())
 
 
-def dropout_seeds(base: int, step: Tensor, seeds: Tensor):
-    call("ttmi_dropout_seeds", base & (2**64 - 1), _p(step), _p(seeds), seeds.numel(), _s())
+def dropout_seeds(base: int, step: Tensor, seeds: Tensor, inc_step: bool = False):
+    """Per-site dropout seeds of the live step (inc_step: increment the step first, in the
+    same launch)."""
+    call("ttmi_dropout_seeds", base & (2**64 - 1), _p(step), _p(seeds), seeds.numel(),
+         int(inc_step), _s())
 
 
 def cast_bf16(src: Tensor, dst: Tensor) -> Tensor:
@@ -521,6 +525,14 @@ def last_rows(len_src: Tensor, rows: Tensor) -> Tensor:
     B, L = len_src.shape
     call("ttmi_last_rows", B, L, _p(len_src), _p(rows), _s())
     return rows
+
+
+def last_rows_gather(len_src: Tensor, x: Tensor, rows: Tensor, out: Tensor) -> Tensor:
+    """rows[b] = the last valid row of sequence b; out[b] = x[rows[b]] (one launch)."""
+    B, L = len_src.shape
+    D = x.shape[1]
+    call("ttmi_last_rows_gather", B, L, D, _p(len_src), _p(x), _p(rows), _p(out), _s())
+    return out
 
 
 def gather_rows(x: Tensor, rows: Tensor, out: Tensor) -> Tensor:

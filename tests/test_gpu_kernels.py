@@ -386,6 +386,24 @@ def test_mha_single_query_matches_full_row(gpu_pkg, dtype, B, L, H, Dh, p):
     assert rel(dqkv.float(), qt.grad) < (5e-5 if dtype == torch.float32 else 3e-2)
 
 
+@pytest.mark.parametrize("D", [96, 130])
+def test_last_rows_gather(gpu_pkg, D):
+    """ttmi_last_rows_gather == ttmi_last_rows + ttmi_gather_rows (incl. empty histories)."""
+    ops = gpu_pkg.ops
+    B, L = 37, 50
+    g = torch.Generator().manual_seed(D)
+    lens = torch.randint(0, L + 1, (B,), generator=g)
+    kv = (torch.arange(L)[None] < lens[:, None]).long().to(DEV)
+    x = torch.randn(B * L, D, generator=g).to(DEV)
+    rows_a = torch.empty(B, dtype=torch.int32, device=DEV)
+    ops.last_rows(kv, rows_a)
+    rows_b = torch.empty(B, dtype=torch.int32, device=DEV)
+    out = torch.empty(B, D, device=DEV)
+    ops.last_rows_gather(kv, x, rows_b, out)
+    assert torch.equal(rows_a, rows_b)
+    assert torch.equal(out, x[rows_a.long()])
+
+
 def test_gather_scatter_rows(gpu_pkg):
     ops = gpu_pkg.ops
     x = torch.randn(500, 96, device=DEV)
@@ -529,6 +547,10 @@ def test_dropout_seed_kernel_matches_host(gpu_pkg):
     gpu_pkg.ops.dropout_seeds(0xABCDEF, step, seeds)
     host = F.seed_table(F.site_seeds(0xABCDEF, 12), "cpu")
     assert torch.equal(seeds.cpu(), host)
+    # with the step increment folded in: seeds of step 13, counter left at 13
+    gpu_pkg.ops.dropout_seeds(0xABCDEF, step, seeds, inc_step=True)
+    assert int(step) == 13
+    assert torch.equal(seeds.cpu(), F.seed_table(F.site_seeds(0xABCDEF, 13), "cpu"))
 
 
 def test_transpose_batch(gpu_pkg):
