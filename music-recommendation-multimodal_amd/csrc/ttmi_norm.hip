@@ -8,6 +8,7 @@ namespace {
 
 constexpr int MAXV = 16;   // D <= 64 * MAXV
 constexpr int LN_REPL = 32;   // replicas of the LayerNorm-backward weight/bias column sums
+constexpr int LN_DIRECT = 128;  // at most this many blocks add to dw/db directly
 
 // Instantiate a kernel template for the smallest NV (64-wide column chunks per row) that
 // covers D: NV in {1, 2, 4, 8, 16}.
@@ -92,7 +93,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int64_t M, int D, const float* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
     int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ w, const void* __restrict__ gate, int gate_f32, int64_t ldg,
-    float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ ws) {
+    float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ cw,
+    float* __restrict__ cb, int nrep, int64_t rstride) {
   __shared__ float red[4 * 64 * NV];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -130,10 +132,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     }
   }
-  if (ws) {   // this block's replica of the LN weight / bias partials (LNR adders per address)
-    float* rep = ws + (int64_t)(blockIdx.x % LN_REPL) * 2 * D;
-    block_col_atomic(aw, D, rep, red);
-    block_col_atomic(ab, D, rep + D, red);
+  if (cw) {   // LN weight / bias partials: this block's replica (or dw/db directly, nrep 1)
+    const int64_t o = (int64_t)(blockIdx.x % nrep) * rstride;
+    block_col_atomic(aw, D, cw + o, red);
+    block_col_atomic(ab, D, cb + o, red);
   }
 }
 
@@ -729,11 +731,24 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
   // a wave walking 16 rows serially ran the stream at ~2.9 TB/s); with sums, 1024 blocks
   // bound the replicas' adders
   int grid = (int)std::min<int64_t>((M + 3) / 4, sums ? 1024 : 16384);
+  // small grids (the B = 512 head LayerNorms: 128 blocks) add to dw/db directly: the
+  // contention of that few adders costs less than the fold launch
+  const bool direct = grid <= LN_DIRECT;
+  float* cw = !sums ? nullptr : direct ? dw : (float*)ws;
+  float* cb = !sums ? nullptr : direct ? db : (float*)ws + D;
+  if (direct && sums && (!dw || !db)) {     // one side only: route the other to the workspace
+    if (!dw) cw = (float*)ws;
+    if (!db) cb = (float*)ws + D;
+  }
+  const int nrep = direct ? 1 : LN_REPL;
+  const int64_t rstride = direct ? 0 : 2 * (int64_t)D;
   TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(grid), dim3(256), 0, s, M, D, dy,
                                          lddy, x, ldx, mean, rstd, w, gate, gate_dtype == TTMI_F32,
-                                         ldg, gate_scale, res, dx, lddx, sums ? (float*)ws : nullptr));
+                                         ldg, gate_scale, res, dx, lddx, cw, cb, nrep, rstride));
   int rc = ttmi_check_launch("ttmi_layernorm_bwd");
   if (rc || !sums) return rc;
+  if (direct && dw && db) return TTMI_OK;
+  // (direct with one side NULL: that side went to workspace replica 0; the fold clears it)
   hipLaunchKernelGGL(colsum_fold_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, 2 * D, D,
                      std::min(grid, LN_REPL), (float*)ws, dw, db);
   return ttmi_check_launch("ttmi_layernorm_bwd/fold");
