@@ -94,13 +94,14 @@ int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const floa
  * multiplied by (gate > 0 ? gate_scale : 0) (gate = the stored y when ReLU/dropout followed
  * the affine).  dx = res + LN'(dy) (res may alias dx or be NULL); dw/db are accumulated
  * (fp32).  ws: ttmi_layernorm_bwd_workspace(D) bytes, zero on entry and left zero (replicated
- * column sums folded once; may be NULL when dw and db are both NULL). */
+ * column sums folded once; may be NULL when dw and db are both NULL).  dx16 (optional, bf16,
+ * row stride ld16) also receives dx (the next GEMM's operand, saving a cast launch). */
 int64_t ttmi_layernorm_bwd_workspace(int D);
 int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
                        int64_t ldx, const float* mean, const float* rstd, const float* w,
                        const void* gate, int gate_dtype, int64_t ldg, float gate_scale,
                        const float* res, float* dx, int64_t lddx, float* dw, float* db,
-                       void* ws, hipStream_t stream);
+                       void* ws, void* dx16, int64_t ld16, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * SASRec input block (user_tower.py:83-93):
@@ -172,7 +173,7 @@ int ttmi_batchnorm_fwd(int dtype, int B, int C, const float* z, const float* w, 
 int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, const float* z,
                        const float* w, const float* mean, const float* rstd, const void* y,
                        float gate_scale, int gated, float* dz, float* dw, float* db,
-                       hipStream_t stream);
+                       void* dz16, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Symmetric in-batch InfoNCE (two_tower.py:98-140), fp32 throughout:

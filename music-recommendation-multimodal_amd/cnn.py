@@ -302,10 +302,13 @@ def tabular_bwd(P: Dict[str, Tensor], st: TabSaved, dout: Tensor, grads: Dict[st
     ops.linear_dx(dc, st.w4, dy1)
     dz = torch.empty_like(dy1)
     scale = 1.0 / (1.0 - st.p_drop) if st.p_drop > 0 else 1.0
-    ops.batchnorm_bwd(dy1, st.z, P["mlp.1.weight"], st.mean, st.rstd, st.y1, dz,
-                      grads["mlp.1.weight"], grads["mlp.1.bias"], gate_scale=scale, gated=True)
     dzc = torch.empty(dz.shape, device=dev, dtype=st.y1.dtype)
-    ops.dropout_bwd(dz, dzc, None)
+    fused16 = dzc.dtype == torch.bfloat16 and dz.shape[0] <= 512   # bf16 copy from the BN kernel
+    ops.batchnorm_bwd(dy1, st.z, P["mlp.1.weight"], st.mean, st.rstd, st.y1, dz,
+                      grads["mlp.1.weight"], grads["mlp.1.bias"], gate_scale=scale, gated=True,
+                      dz16=dzc if fused16 else None)
+    if not fused16:
+        ops.dropout_bwd(dz, dzc, None)
     gw = grads["mlp.0.weight"]
     if st.x.shape[1] != gw.shape[1]:                  # zero-padded T (see tabular_fwd)
         pad = torch.zeros(gw.shape[0], st.x.shape[1], device=dev)

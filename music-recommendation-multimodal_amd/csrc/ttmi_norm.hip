@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ w, const void* __restrict__ gate, int gate_f32, int64_t ldg,
     float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ cw,
-    float* __restrict__ cb, int nrep, int64_t rstride) {
+    float* __restrict__ cb, int nrep, int64_t rstride, bf16_t* __restrict__ dx16, int64_t ld16) {
   __shared__ float red[4 * 64 * NV];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -128,7 +128,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       const int c = lane + 64 * i;
       if (c < D) {
         const float o = rs * (g[i] - c1 - xh[i] * c2);
-        dx[row * lddx + c] = (res ? res[row * lddx + c] : 0.f) + o;
+        const float v = (res ? res[row * lddx + c] : 0.f) + o;
+        dx[row * lddx + c] = v;
+        if (dx16) dx16[row * ld16 + c] = f2bf(v);     // the next GEMM's bf16 operand
       }
     }
   }
@@ -632,7 +634,8 @@ __global__ __launch_bounds__(512) void bnr_bwd_kernel(int B, int C, const float*
                                                       const float* __restrict__ rstd,
                                                       const T* __restrict__ y, float gate_scale,
                                                       int gated, float* __restrict__ dz,
-                                                      float* __restrict__ dw, float* __restrict__ db) {
+                                                      float* __restrict__ dw, float* __restrict__ db,
+                                                      bf16_t* __restrict__ dz16) {
   __shared__ float red[BNR_RG][BNR_COLS];
   const int cl = threadIdx.x % BNR_COLS, rg = threadIdx.x / BNR_COLS;
   const int c = blockIdx.x * BNR_COLS + cl;
@@ -662,7 +665,11 @@ __global__ __launch_bounds__(512) void bnr_bwd_kernel(int B, int C, const float*
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
     const int r = rg + BNR_RG * j;
-    if (r < B) dz[(int64_t)r * C + c] = wc * rs * (d[j] - S1 * invB - xh[j] * S2 * invB);
+    if (r < B) {
+      const float v = wc * rs * (d[j] - S1 * invB - xh[j] * S2 * invB);
+      dz[(int64_t)r * C + c] = v;
+      if (dz16) dz16[(int64_t)r * C + c] = f2bf(v);   // the next GEMM's bf16 operand
+    }
   }
   if (rg == 0) {
     if (dw) atomicAdd(dw + c, S2);
@@ -708,15 +715,17 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
                                   int64_t ldx, const float* mean, const float* rstd,
                                   const float* w, const void* gate, int gate_dtype, int64_t ldg,
                                   float gate_scale, const float* res, float* dx, int64_t lddx,
-                                  float* dw, float* db, void* ws, hipStream_t s) {
+                                  float* dw, float* db, void* ws, void* dx16, int64_t ld16,
+                                  hipStream_t s) {
   TTMI_REQUIRE(M >= 0 && D > 0 && D <= 64 * MAXV, "ttmi_layernorm_bwd: need 0 < D <= %d", 64 * MAXV);
   TTMI_REQUIRE(dy && x && mean && rstd && w && dx, "ttmi_layernorm_bwd: null argument");
   TTMI_REQUIRE(lddy >= D && ldx >= D && lddx >= D && (!gate || ldg >= D), "ttmi_layernorm_bwd: bad ld");
   TTMI_REQUIRE(!(dw || db) || ws, "ttmi_layernorm_bwd: dw/db need the workspace");
+  TTMI_REQUIRE(!dx16 || ld16 >= D, "ttmi_layernorm_bwd: ld16 < D");
   if (M == 0) return TTMI_OK;
   const bool sums = dw || db;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (!sums && !gate && D % 256 == 0 && D <= 1024 && lddy % 4 == 0 && ldx % 4 == 0 &&
+  if (!sums && !gate && !dx16 && D % 256 == 0 && D <= 1024 && lddy % 4 == 0 && ldx % 4 == 0 &&
       lddx % 4 == 0 && al16(dy) && al16(x) && al16(w) && al16(dx) && (!res || al16(res))) {
     const dim3 vg((unsigned)((M + 3) / 4));
     switch (D / 256) {
@@ -744,7 +753,8 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
   const int64_t rstride = direct ? 0 : 2 * (int64_t)D;
   TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(grid), dim3(256), 0, s, M, D, dy,
                                          lddy, x, ldx, mean, rstd, w, gate, gate_dtype == TTMI_F32,
-                                         ldg, gate_scale, res, dx, lddx, cw, cb, nrep, rstride));
+                                         ldg, gate_scale, res, dx, lddx, cw, cb, nrep, rstride,
+                                         (bf16_t*)dx16, ld16));
   int rc = ttmi_check_launch("ttmi_layernorm_bwd");
   if (rc || !sums) return rc;
   if (direct && dw && db) return TTMI_OK;
@@ -877,15 +887,16 @@ extern "C" int ttmi_batchnorm_fwd(int dtype, int B, int C, const float* z, const
 extern "C" int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, const float* z,
                                   const float* w, const float* mean, const float* rstd,
                                   const void* y, float gate_scale, int gated, float* dz, float* dw,
-                                  float* db, hipStream_t s) {
+                                  float* db, void* dz16, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_batchnorm_bwd: bad dtype");
   TTMI_REQUIRE(B > 1 && C > 0, "ttmi_batchnorm_bwd: bad sizes");
   TTMI_REQUIRE(dy && z && w && mean && rstd && dz && (!gated || y), "ttmi_batchnorm_bwd: null argument");
+  TTMI_REQUIRE(!dz16 || bnr_rpt(B), "ttmi_batchnorm_bwd: the bf16 copy needs B <= %d", 16 * BNR_RG);
   if (const int rpt = bnr_rpt(B)) {
     const dim3 g((C + BNR_COLS - 1) / BNR_COLS);
 #define TTMI_BNR_BWD(T, R)                                                                          \
   hipLaunchKernelGGL((bnr_bwd_kernel<T, R>), g, dim3(512), 0, s, B, C, dy, z, w, mean, rstd,        \
-                     (const T*)y, gate_scale, gated, dz, dw, db)
+                     (const T*)y, gate_scale, gated, dz, dw, db, (bf16_t*)dz16)
     if (dtype == TTMI_BF16) {
       if (rpt == 4) TTMI_BNR_BWD(bf16_t, 4); else if (rpt == 8) TTMI_BNR_BWD(bf16_t, 8); else TTMI_BNR_BWD(bf16_t, 16);
     } else {

@@ -286,10 +286,12 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
     daz = torch.empty(B, D, **f32)
     ops.linear_dx(du_c, W["fusion_layer.3.weight"], daz)
     dz = torch.empty(B, D, **f32)
-    ops.layernorm_bwd(daz, st.z, st.mz, st.rz, P["fusion_layer.1.weight"], dz,
-                      grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"], gate=st.az)
     dz_c = torch.empty(B, D, device=dev, dtype=dt)
-    ops.dropout_bwd(dz, dz_c, None)
+    ops.layernorm_bwd(daz, st.z, st.mz, st.rz, P["fusion_layer.1.weight"], dz,
+                      grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"], gate=st.az,
+                      dx16=dz_c if dt == torch.bfloat16 else None)
+    if dt != torch.bfloat16:
+        ops.dropout_bwd(dz, dz_c, None)
     ops.linear_dw(dz_c, st.comb, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
     dcomb = torch.empty(B, st.comb.shape[1], **f32)
     ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dcomb)
@@ -434,21 +436,25 @@ def item_fusion_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, d
     dt = cfg.dtype
     f32 = dict(device=dev, dtype=torch.float32)
     dy2 = torch.empty(B, D, **f32)
-    ops.layernorm_bwd(dout, st.y2, st.m5, st.r5, P["fusion_layer.5.weight"], dy2,
-                      grads["fusion_layer.5.weight"], grads["fusion_layer.5.bias"])
     dy2_c = torch.empty(B, D, device=dev, dtype=dt)
-    ops.dropout_bwd(dy2, dy2_c, None)
+    ops.layernorm_bwd(dout, st.y2, st.m5, st.r5, P["fusion_layer.5.weight"], dy2,
+                      grads["fusion_layer.5.weight"], grads["fusion_layer.5.bias"],
+                      dx16=dy2_c if dt == torch.bfloat16 else None)
+    if dt != torch.bfloat16:
+        ops.dropout_bwd(dy2, dy2_c, None)
     ops.linear_dw(dy2_c, st.y1, grads["fusion_layer.4.weight"], grads["fusion_layer.4.bias"])
     H1 = st.z.shape[1]
     dy1 = torch.empty(B, H1, **f32)
     ops.linear_dx(dy2_c, W["fusion_layer.4.weight"], dy1)
     pd = p_drop if st.seeds is not None else 0.0
     dz = torch.empty(B, H1, **f32)
+    dz_c = torch.empty(B, H1, device=dev, dtype=dt)
+    fused16 = dt == torch.bfloat16 and B <= 512
     ops.batchnorm_bwd(dy1, st.z, P["fusion_layer.1.weight"], st.bn_mean, st.bn_rstd, st.y1, dz,
                       grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"],
-                      gate_scale=_scale(pd), gated=True)
-    dz_c = torch.empty(B, H1, device=dev, dtype=dt)
-    ops.dropout_bwd(dz, dz_c, None)
+                      gate_scale=_scale(pd), gated=True, dz16=dz_c if fused16 else None)
+    if not fused16:
+        ops.dropout_bwd(dz, dz_c, None)
     ops.linear_dw(dz_c, st.modal, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
     if dmodal is not None:
         ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dmodal)

@@ -328,13 +328,17 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd
 
 def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, dx: Tensor,
                   dw: Optional[Tensor], db: Optional[Tensor], *, gate: Optional[Tensor] = None,
-                  gate_scale: float = 1.0, res: Optional[Tensor] = None) -> Tensor:
+                  gate_scale: float = 1.0, res: Optional[Tensor] = None,
+                  dx16: Optional[Tensor] = None) -> Tensor:
+    """LayerNorm backward (+ gate, + residual); dx16 (bf16) optionally receives a copy of dx."""
     M, D = x.shape
     ws = _zero_ws("ttmi_layernorm_bwd_workspace", (D,), x.device) \
         if (dw is not None or db is not None) else None
+    if dx16 is not None and dx16.dtype != torch.bfloat16:
+        raise ValueError("layernorm_bwd: dx16 must be bf16")
     call("ttmi_layernorm_bwd", M, D, _p(dy), D, _p(x), D, _p(mean), _p(rstd), _p(w), _p(gate),
          code(gate.dtype) if gate is not None else 0, D, gate_scale, _p(res), _p(dx), D, _p(dw),
-         _p(db), _p(ws), _s())
+         _p(db), _p(ws), _p(dx16), dx16.stride(0) if dx16 is not None else 0, _s())
     return dx
 
 
@@ -432,10 +436,13 @@ def batchnorm_fwd(z: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd
 
 def batchnorm_bwd(dy: Tensor, z: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, y: Tensor,
                   dz: Tensor, dw: Tensor, db: Tensor, *, gate_scale: float = 1.0,
-                  gated: bool = True):
+                  gated: bool = True, dz16: Optional[Tensor] = None):
+    """BatchNorm1d backward; dz16 (bf16, contiguous) optionally receives a copy of dz."""
     B, C = z.shape
+    if dz16 is not None and dz16.dtype != torch.bfloat16:
+        raise ValueError("batchnorm_bwd: dz16 must be bf16")
     call("ttmi_batchnorm_bwd", code(y.dtype), B, C, _p(dy), _p(z), _p(w), _p(mean), _p(rstd),
-         _p(y), gate_scale, int(gated), _p(dz), _p(dw), _p(db), _s())
+         _p(y), gate_scale, int(gated), _p(dz), _p(dw), _p(db), _p(dz16), _s())
     return dz
 
 

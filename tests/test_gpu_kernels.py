@@ -706,3 +706,31 @@ def test_deb_ln_fwd(gpu_pkg, H):
     assert rel(y16[:, :H].float(), ref) < 8e-3
     assert y16[:, H:].abs().max().item() == 0.0
     assert rel(mean, z.mean(1)) < 1e-5
+
+
+def test_norm_backward_bf16_copies(gpu_pkg):
+    """The optional bf16 copies of LayerNorm / BatchNorm1d backward outputs (dx16 / dz16) equal
+    bf16(dx) / bf16(dz) exactly."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(5)
+    M, D = 512, 128
+    x = torch.randn(M, D, generator=g).to(DEV)
+    w, b = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    y = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.layernorm_fwd(x, w, b, y, mean, rstd, relu=True)
+    dy = torch.randn(M, D, generator=g).to(DEV)
+    dx, dx16 = torch.empty(M, D, device=DEV), torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    dw, db = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ops.layernorm_bwd(dy, x, mean, rstd, w, dx, dw, db, gate=y, dx16=dx16)
+    assert torch.equal(dx16, dx.to(torch.bfloat16))
+    B, C = 300, 96
+    z = torch.randn(B, C, generator=g).to(DEV)
+    yb = torch.empty(B, C, device=DEV, dtype=torch.bfloat16)
+    bm, br = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    ops.batchnorm_fwd(z, w[:C], b[:C], yb, bm, br, None, None, None, relu=True)
+    dyb = torch.randn(B, C, generator=g).to(DEV)
+    dz, dz16 = torch.empty(B, C, device=DEV), torch.empty(B, C, device=DEV, dtype=torch.bfloat16)
+    ops.batchnorm_bwd(dyb, z, w[:C], bm, br, yb, dz, torch.zeros(C, device=DEV),
+                      torch.zeros(C, device=DEV), dz16=dz16)
+    assert torch.equal(dz16, dz.to(torch.bfloat16))
