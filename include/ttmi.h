@@ -95,13 +95,15 @@ int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const floa
  * the affine).  dx = res + LN'(dy) (res may alias dx or be NULL); dw/db are accumulated
  * (fp32).  ws: ttmi_layernorm_bwd_workspace(D) bytes, zero on entry and left zero (replicated
  * column sums folded once; may be NULL when dw and db are both NULL).  dx16 (optional, bf16,
- * row stride ld16) also receives dx (the next GEMM's operand, saving a cast launch). */
+ * row stride ld16) receives bf16(dropout(dx)) with keep index m*D + n (drop_p may be 0): the
+ * next GEMM's operand, with the residual branch's dropout backward fused (saves a launch). */
 int64_t ttmi_layernorm_bwd_workspace(int D);
 int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
                        int64_t ldx, const float* mean, const float* rstd, const float* w,
                        const void* gate, int gate_dtype, int64_t ldg, float gate_scale,
                        const float* res, float* dx, int64_t lddx, float* dw, float* db,
-                       void* ws, void* dx16, int64_t ld16, hipStream_t stream);
+                       void* ws, void* dx16, int64_t ld16, float drop_p,
+                       const uint64_t* drop_seed, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * SASRec input block (user_tower.py:83-93):

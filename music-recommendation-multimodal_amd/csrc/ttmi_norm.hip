@@ -94,7 +94,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ w, const void* __restrict__ gate, int gate_f32, int64_t ldg,
     float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ cw,
-    float* __restrict__ cb, int nrep, int64_t rstride, bf16_t* __restrict__ dx16, int64_t ld16) {
+    float* __restrict__ cb, int nrep, int64_t rstride, bf16_t* __restrict__ dx16, int64_t ld16,
+    DropParams dp16) {
   __shared__ float red[4 * 64 * NV];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   float aw[NV], ab[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) aw[i] = ab[i] = 0.f;
+  const DropKeys dk16 = resolve_drop(dp16);
   for (int64_t row = wid; row < M; row += nw) {
     const float mu = mean[row], rs = rstd[row];
     float g[NV], xh[NV];
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         const float o = rs * (g[i] - c1 - xh[i] * c2);
         const float v = (res ? res[row * lddx + c] : 0.f) + o;
         dx[row * lddx + c] = v;
-        if (dx16) dx16[row * ld16 + c] = f2bf(v);     // the next GEMM's bf16 operand
+        if (dx16) dx16[row * ld16 + c] = f2bf(drop_apply(dk16, (uint32_t)(row * D + c), v));
       }
     }
   }
@@ -150,10 +152,13 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int64_t M, int D, const
                                                          int64_t ldx, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd,
                                                          const float* __restrict__ w,
-                                                         const float* res, float* dx, int64_t lddx) {
+                                                         const float* res, float* dx, int64_t lddx,
+                                                         bf16_t* __restrict__ dx16, int64_t ld16,
+                                                         DropParams dp16) {
   const int lane = threadIdx.x & 63;
   const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (row >= M) return;
+  const DropKeys dk16 = resolve_drop(dp16);
   const float invD = 1.f / (float)D;
   const float mu = mean[row], rs = rstd[row];
   float4 g[Q4], xh[Q4], r[Q4];
@@ -174,9 +179,15 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int64_t M, int D, const
 #pragma unroll
   for (int i = 0; i < Q4; ++i) {
     const int c = (lane + 64 * i) * 4;
-    *reinterpret_cast<float4*>(dx + row * lddx + c) =
-        make_float4(r[i].x + rs * (g[i].x - c1 - xh[i].x * c2), r[i].y + rs * (g[i].y - c1 - xh[i].y * c2),
-                    r[i].z + rs * (g[i].z - c1 - xh[i].z * c2), r[i].w + rs * (g[i].w - c1 - xh[i].w * c2));
+    float4 o = make_float4(r[i].x + rs * (g[i].x - c1 - xh[i].x * c2), r[i].y + rs * (g[i].y - c1 - xh[i].y * c2),
+                           r[i].z + rs * (g[i].z - c1 - xh[i].z * c2), r[i].w + rs * (g[i].w - c1 - xh[i].w * c2));
+    *reinterpret_cast<float4*>(dx + row * lddx + c) = o;
+    if (dx16) {          // bf16(dropout(dx)): the next GEMM's operand (dropout backward fused)
+      drop_apply_vec<4>(dk16, (uint32_t)(row * D + c), &o.x);
+      ushort4 h;
+      h.x = f2bf(o.x); h.y = f2bf(o.y); h.z = f2bf(o.z); h.w = f2bf(o.w);
+      *reinterpret_cast<ushort4*>(dx16 + row * ld16 + c) = h;
+    }
   }
 }
 
@@ -716,23 +727,27 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
                                   const float* w, const void* gate, int gate_dtype, int64_t ldg,
                                   float gate_scale, const float* res, float* dx, int64_t lddx,
                                   float* dw, float* db, void* ws, void* dx16, int64_t ld16,
-                                  hipStream_t s) {
+                                  float drop_p, const uint64_t* drop_seed, hipStream_t s) {
   TTMI_REQUIRE(M >= 0 && D > 0 && D <= 64 * MAXV, "ttmi_layernorm_bwd: need 0 < D <= %d", 64 * MAXV);
   TTMI_REQUIRE(dy && x && mean && rstd && w && dx, "ttmi_layernorm_bwd: null argument");
   TTMI_REQUIRE(lddy >= D && ldx >= D && lddx >= D && (!gate || ldg >= D), "ttmi_layernorm_bwd: bad ld");
   TTMI_REQUIRE(!(dw || db) || ws, "ttmi_layernorm_bwd: dw/db need the workspace");
   TTMI_REQUIRE(!dx16 || ld16 >= D, "ttmi_layernorm_bwd: ld16 < D");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || (dx16 && drop_seed)),
+               "ttmi_layernorm_bwd: dropout applies to dx16 and needs a seed");
+  const DropParams dp16 = make_drop(drop_p, drop_seed);
   if (M == 0) return TTMI_OK;
   const bool sums = dw || db;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (!sums && !gate && !dx16 && D % 256 == 0 && D <= 1024 && lddy % 4 == 0 && ldx % 4 == 0 &&
-      lddx % 4 == 0 && al16(dy) && al16(x) && al16(w) && al16(dx) && (!res || al16(res))) {
+  if (!sums && !gate && D % 256 == 0 && D <= 1024 && lddy % 4 == 0 && ldx % 4 == 0 &&
+      lddx % 4 == 0 && al16(dy) && al16(x) && al16(w) && al16(dx) && (!res || al16(res)) &&
+      (!dx16 || (((uintptr_t)dx16 & 7) == 0 && ld16 % 4 == 0))) {
     const dim3 vg((unsigned)((M + 3) / 4));
     switch (D / 256) {
-      case 1: hipLaunchKernelGGL(ln_bwd_vec_kernel<1>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
-      case 2: hipLaunchKernelGGL(ln_bwd_vec_kernel<2>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
-      case 3: hipLaunchKernelGGL(ln_bwd_vec_kernel<3>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
-      default: hipLaunchKernelGGL(ln_bwd_vec_kernel<4>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx); break;
+      case 1: hipLaunchKernelGGL(ln_bwd_vec_kernel<1>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx, (bf16_t*)dx16, ld16, dp16); break;
+      case 2: hipLaunchKernelGGL(ln_bwd_vec_kernel<2>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx, (bf16_t*)dx16, ld16, dp16); break;
+      case 3: hipLaunchKernelGGL(ln_bwd_vec_kernel<3>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx, (bf16_t*)dx16, ld16, dp16); break;
+      default: hipLaunchKernelGGL(ln_bwd_vec_kernel<4>, vg, dim3(256), 0, s, M, D, dy, lddy, x, ldx, mean, rstd, w, res, dx, lddx, (bf16_t*)dx16, ld16, dp16); break;
     }
     return ttmi_check_launch("ttmi_layernorm_bwd");
   }
@@ -754,7 +769,7 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
   TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(grid), dim3(256), 0, s, M, D, dy,
                                          lddy, x, ldx, mean, rstd, w, gate, gate_dtype == TTMI_F32,
                                          ldg, gate_scale, res, dx, lddx, cw, cb, nrep, rstride,
-                                         (bf16_t*)dx16, ld16));
+                                         (bf16_t*)dx16, ld16, dp16));
   int rc = ttmi_check_launch("ttmi_layernorm_bwd");
   if (rc || !sums) return rc;
   if (direct && dw && db) return TTMI_OK;

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -102,7 +102,7 @@ SIGNATURES = {
                                  c_i64, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),
     "ttmi_layernorm_bwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i, c_i64,
-                                 c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p]),
+                                 c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_p]),
     "ttmi_seq_embed_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_i64, c_p, c_p, c_p, c_f, c_f, c_p, c_p,
                                  c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_seq_embed_bwd_workspace": (c_i64, [c_i, c_i]),

@@ -329,8 +329,9 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd
 def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, dx: Tensor,
                   dw: Optional[Tensor], db: Optional[Tensor], *, gate: Optional[Tensor] = None,
                   gate_scale: float = 1.0, res: Optional[Tensor] = None,
-                  dx16: Optional[Tensor] = None) -> Tensor:
-    """LayerNorm backward (+ gate, + residual); dx16 (bf16) optionally receives a copy of dx."""
+                  dx16: Optional[Tensor] = None, drop: Drop = NO_DROP) -> Tensor:
+    """LayerNorm backward (+ gate, + residual); dx16 (bf16) optionally receives
+    bf16(dropout(dx)) (drop: the residual branch's dropout, keep index m*D + n)."""
     M, D = x.shape
     ws = _zero_ws("ttmi_layernorm_bwd_workspace", (D,), x.device) \
         if (dw is not None or db is not None) else None
@@ -338,7 +339,8 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, 
         raise ValueError("layernorm_bwd: dx16 must be bf16")
     call("ttmi_layernorm_bwd", M, D, _p(dy), D, _p(x), D, _p(mean), _p(rstd), _p(w), _p(gate),
          code(gate.dtype) if gate is not None else 0, D, gate_scale, _p(res), _p(dx), D, _p(dw),
-         _p(db), _p(ws), _p(dx16), dx16.stride(0) if dx16 is not None else 0, _s())
+         _p(db), _p(ws), _p(dx16), dx16.stride(0) if dx16 is not None else 0, float(drop[0]),
+         _p(drop[1]), _s())
     return dx
 
 

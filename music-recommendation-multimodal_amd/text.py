@@ -416,16 +416,17 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
         if r != 8:
             raise NotImplementedError("text backward kernels are built for LoRA rank 8 (the reference's r)")
         dz2 = torch.empty(M, H, device=dev)
-        ops.layernorm_bwd(dx, sv.z2, sv.m2, sv.r2, Fz.base[L + "output.LayerNorm.weight"], dz2, None, None)
-        g2 = ops.dropout_bwd(dz2, torch.empty(M, H, device=dev, dtype=bf), None, _drop(pd, seeds, tsite(l, 2)))
+        g2 = torch.empty(M, H, device=dev, dtype=bf)        # bf16(dropout'(dz2)), same kernel
+        ops.layernorm_bwd(dx, sv.z2, sv.m2, sv.r2, Fz.base[L + "output.LayerNorm.weight"], dz2, None,
+                          None, dx16=g2, drop=_drop(pd, seeds, tsite(l, 2)))
         dpre = torch.empty(M, I, device=dev, dtype=bf)
         _mm(g2, W["w2T"], dpre, M, I, H, lda=H, ldb=H, ldc=I, act=3, gate=sv.pre, ld_gate=I)
         da = torch.empty(M, H, device=dev)
         _mm(dpre, W["w1T"], da, M, H, I, lda=I, ldb=I, ldc=H, residual=dz2, ld_res=H)
         dz1 = torch.empty(M, H, device=dev)
+        g1 = torch.empty(M, H, device=dev, dtype=bf)
         ops.layernorm_bwd(da, sv.z1, sv.m1, sv.r1, Fz.base[L + "attention.output.LayerNorm.weight"],
-                          dz1, None, None)
-        g1 = ops.dropout_bwd(dz1, torch.empty(M, H, device=dev, dtype=bf), None, _drop(pd, seeds, tsite(l, 1)))
+                          dz1, None, None, dx16=g1, drop=_drop(pd, seeds, tsite(l, 1)))
         dctx = torch.empty(M, H, device=dev, dtype=bf)
         _mm(g1, W["woT"], dctx, M, H, H, lda=H, ldb=H, ldc=H)
         dqkv = torch.empty(M, 3 * H, device=dev, dtype=bf)

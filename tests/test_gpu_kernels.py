@@ -734,3 +734,23 @@ def test_norm_backward_bf16_copies(gpu_pkg):
     ops.batchnorm_bwd(dyb, z, w[:C], bm, br, yb, dz, torch.zeros(C, device=DEV),
                       torch.zeros(C, device=DEV), dz16=dz16)
     assert torch.equal(dz16, dz.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("D", [128, 768])            # generic and 16-byte-lane kernels
+def test_layernorm_bwd_dropout_copy(gpu_pkg, D):
+    """dx16 = bf16(dropout(dx)) with keep index m*D + n (the post-LN residual dropout
+    backward fused into the LayerNorm backward) vs the separate dropout kernel's mask."""
+    ops = gpu_pkg.ops
+    M, p, seed = 700, 0.1, 0x5151
+    g = torch.Generator().manual_seed(D)
+    x = torch.randn(M, D, generator=g).to(DEV)
+    w = torch.randn(D, generator=g).to(DEV)
+    mean, rstd = x.mean(1), 1.0 / torch.sqrt(x.var(1, unbiased=False) + 1e-7)
+    dy = torch.randn(M, D, generator=g).to(DEV)
+    dx = torch.empty(M, D, device=DEV)
+    dx16 = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    ops.layernorm_bwd(dy, x, mean, rstd, w, dx, None, None, dx16=dx16, drop=(p, seed_dev(seed)))
+    ref16 = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    ops.dropout_bwd(dx, ref16, None, (p, seed_dev(seed)))
+    torch.cuda.synchronize()
+    assert torch.equal(dx16, ref16)
