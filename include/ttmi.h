@@ -424,10 +424,13 @@ int ttmi_deb_embed_fwd(int64_t M, int H, const int64_t* ids, const uint16_t* tab
                        float drop_p, const uint64_t* drop_seed, float* y32, uint16_t* y16,
                        int64_t ld16, hipStream_t stream);
 /* Post-LayerNorm (DebertaV2SelfOutput / DebertaV2Output LayerNorm(h + residual)): y = LN(z),
- * z fp32 [M,H]; y32 (fp32, may be NULL) and y16 (bf16, stride ld16, may be NULL); mean/rstd. */
+ * z fp32 [M,H]; y32 (fp32, may be NULL) and y16 (bf16, stride ld16, may be NULL); mean/rstd.
+ * yq / yv (bf16 [M,H], may be NULL; H % 256 == 0): bf16(dropout(y)) with the next layer's
+ * peft lora_dropout masks of query_proj / value_proj (seed_q / seed_v, keep index m*H + n). */
 int ttmi_deb_ln_fwd(int64_t M, int H, const float* z, const float* ln_w, const float* ln_b,
                     float eps, float* y32, uint16_t* y16, int64_t ld16, float* mean,
-                    float* rstd, hipStream_t stream);
+                    float* rstd, uint16_t* yq, uint16_t* yv, float drop_p, const uint64_t* seed_q,
+                    const uint64_t* seed_v, hipStream_t stream);
 /* Disentangled self-attention (DisentangledSelfAttention with share_att_key, c2p|p2c):
  *   score[i,j] = (Q_i·K_j + Q_i·posK[δ(i-j)] + K_j·posQ[δ(i-j)]) · inv_scale, masked by
  *   mask_i·mask_j (finfo.min), softmax, dropout(p), ·V.  δ = delta[i - j + S - 1] =

@@ -82,10 +82,13 @@ __global__ __launch_bounds__(256) void deb_ln_vec_kernel(int64_t M, int H, const
                                                          const float* __restrict__ lb, float eps,
                                                          float* __restrict__ y32, bf16_t* __restrict__ y16,
                                                          int64_t ld16, float* __restrict__ mean,
-                                                         float* __restrict__ rstd) {
+                                                         float* __restrict__ rstd,
+                                                         bf16_t* __restrict__ yq, bf16_t* __restrict__ yv,
+                                                         DropParams dq, DropParams dv) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
+  const DropKeys kq = resolve_drop(dq), kv = resolve_drop(dv);
   float4 v[Q4];
   float s = 0.f;
 #pragma unroll
@@ -112,6 +115,22 @@ __global__ __launch_bounds__(256) void deb_ln_vec_kernel(int64_t M, int H, const
       ushort4 h;
       h.x = f2bf(o.x); h.y = f2bf(o.y); h.z = f2bf(o.z); h.w = f2bf(o.w);
       *reinterpret_cast<ushort4*>(y16 + row * ld16 + c) = h;
+    }
+    // the next layer's LoRA inputs bf16(drop_q(y)), bf16(drop_v(y)) (keep index row*H + c, as
+    // ttmi_dropout_bwd's): two more outputs of the row already in registers
+    if (yq) {
+      float4 a = o;
+      drop_apply_vec<4>(kq, (uint32_t)(row * H + c), &a.x);
+      ushort4 h;
+      h.x = f2bf(a.x); h.y = f2bf(a.y); h.z = f2bf(a.z); h.w = f2bf(a.w);
+      *reinterpret_cast<ushort4*>(yq + row * H + c) = h;
+    }
+    if (yv) {
+      float4 a = o;
+      drop_apply_vec<4>(kv, (uint32_t)(row * H + c), &a.x);
+      ushort4 h;
+      h.x = f2bf(a.x); h.y = f2bf(a.y); h.z = f2bf(a.z); h.w = f2bf(a.w);
+      *reinterpret_cast<ushort4*>(yv + row * H + c) = h;
     }
   }
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
@@ -366,20 +385,30 @@ extern "C" int ttmi_deb_embed_fwd(int64_t M, int H, const int64_t* ids, const ui
 
 extern "C" int ttmi_deb_ln_fwd(int64_t M, int H, const float* z, const float* ln_w, const float* ln_b,
                                float eps, float* y32, uint16_t* y16, int64_t ld16, float* mean,
-                               float* rstd, hipStream_t s) {
+                               float* rstd, uint16_t* yq, uint16_t* yv, float drop_p,
+                               const uint64_t* seed_q, const uint64_t* seed_v, hipStream_t s) {
   TTMI_REQUIRE(M > 0 && H % 64 == 0 && H <= 1024, "ttmi_deb_ln_fwd: need H %% 64 == 0, H <= 1024");
   TTMI_REQUIRE(z && ln_w && ln_b && mean && rstd && (y32 || y16), "ttmi_deb_ln_fwd: null argument");
   TTMI_REQUIRE(!y16 || ld16 >= H, "ttmi_deb_ln_fwd: ld16 < H");
   auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
-  if (H % 256 == 0 && al(z, 16) && al(ln_w, 16) && al(ln_b, 16) && (!y32 || al(y32, 16)) &&
-      (!y16 || (al(y16, 8) && ld16 % 4 == 0))) {
+  const bool vec = H % 256 == 0 && al(z, 16) && al(ln_w, 16) && al(ln_b, 16) && (!y32 || al(y32, 16)) &&
+                   (!y16 || (al(y16, 8) && ld16 % 4 == 0)) && (!yq || al(yq, 8)) && (!yv || al(yv, 8));
+  TTMI_REQUIRE(!(yq || yv) || vec, "ttmi_deb_ln_fwd: the LoRA-dropout outputs need H %% 256 == 0, aligned");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || (seed_q && seed_v)),
+               "ttmi_deb_ln_fwd: bad LoRA dropout");
+  if (vec) {
     const dim3 g((unsigned)((M + 3) / 4));
+    const DropParams dq = make_drop(drop_p, seed_q), dv = make_drop(drop_p, seed_v);
+#define TTMI_DEBLN(Q)                                                                                   \
+  hipLaunchKernelGGL(deb_ln_vec_kernel<Q>, g, dim3(256), 0, s, M, H, z, ln_w, ln_b, eps, y32,            \
+                     (bf16_t*)y16, ld16, mean, rstd, (bf16_t*)yq, (bf16_t*)yv, dq, dv)
     switch (H / 256) {
-      case 1: hipLaunchKernelGGL(deb_ln_vec_kernel<1>, g, dim3(256), 0, s, M, H, z, ln_w, ln_b, eps, y32, (bf16_t*)y16, ld16, mean, rstd); break;
-      case 2: hipLaunchKernelGGL(deb_ln_vec_kernel<2>, g, dim3(256), 0, s, M, H, z, ln_w, ln_b, eps, y32, (bf16_t*)y16, ld16, mean, rstd); break;
-      case 3: hipLaunchKernelGGL(deb_ln_vec_kernel<3>, g, dim3(256), 0, s, M, H, z, ln_w, ln_b, eps, y32, (bf16_t*)y16, ld16, mean, rstd); break;
-      default: hipLaunchKernelGGL(deb_ln_vec_kernel<4>, g, dim3(256), 0, s, M, H, z, ln_w, ln_b, eps, y32, (bf16_t*)y16, ld16, mean, rstd); break;
+      case 1: TTMI_DEBLN(1); break;
+      case 2: TTMI_DEBLN(2); break;
+      case 3: TTMI_DEBLN(3); break;
+      default: TTMI_DEBLN(4); break;
     }
+#undef TTMI_DEBLN
     return ttmi_check_launch("ttmi_deb_ln_fwd");
   }
   hipLaunchKernelGGL(deb_ln_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, M, H, z, ln_w, ln_b,

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -127,8 +127,8 @@ SIGNATURES = {
     "ttmi_linear_res_ln": (c_i, [c_p, c_p]),
     "ttmi_deb_embed_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, ctypes.c_float, c_p,
                                  ctypes.c_float, c_p, c_p, c_p, c_i64, c_p]),
-    "ttmi_deb_ln_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, ctypes.c_float, c_p, c_p, c_i64, c_p,
-                              c_p, c_p]),
+    "ttmi_deb_ln_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p,
+                               c_f, c_p, c_p, c_p]),
     "ttmi_deb_gelu": (c_i, [c_i64, c_p, c_p, c_p]),
     "ttmi_topk_rows": (c_i, [c_i, c_i, c_i, c_p, c_i64, c_i, c_p, c_p, c_p]),
     "ttmi_rank_of": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),

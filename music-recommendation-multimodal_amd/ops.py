@@ -591,10 +591,17 @@ def deb_embed_fwd(ids: Tensor, table: Tensor, w: Tensor, b: Tensor, eps: float,
 
 
 def deb_ln_fwd(z: Tensor, w: Tensor, b: Tensor, eps: float, y32: Optional[Tensor],
-               y16: Optional[Tensor], mean: Tensor, rstd: Tensor) -> None:
+               y16: Optional[Tensor], mean: Tensor, rstd: Tensor, *,
+               yq: Optional[Tensor] = None, yv: Optional[Tensor] = None,
+               drop_q: Drop = NO_DROP, drop_v: Drop = NO_DROP) -> None:
+    """Post-LayerNorm; yq / yv (bf16 [M, H]) optionally receive bf16(dropout(y)) with the
+    next layer's LoRA-dropout masks (drop_q / drop_v share p)."""
     M, H = z.shape
+    if float(drop_q[0]) != float(drop_v[0]):
+        raise ValueError("deb_ln_fwd: the q and v LoRA dropouts share p")
     call("ttmi_deb_ln_fwd", M, H, _p(z), _p(w), _p(b), eps, _p(y32), _p(y16),
-         y16.stride(0) if y16 is not None else 0, _p(mean), _p(rstd), _s())
+         y16.stride(0) if y16 is not None else 0, _p(mean), _p(rstd), _p(yq), _p(yv),
+         float(drop_q[0]), _p(drop_q[1]), _p(drop_v[1]), _s())
 
 
 def deb_gelu(x: Tensor, y: Tensor) -> Tensor:

@@ -296,6 +296,7 @@ def text_fwd(enc: "TextEncoder", P: Dict[str, Tensor], ids: Tensor, mask: Tensor
     ops.deb_embed_fwd(ids, Fz.table, Fz.base["embeddings.LayerNorm.weight"],
                       Fz.base["embeddings.LayerNorm.bias"], c.eps, mask, x32, xaug,
                       drop=_drop(pd, seeds, TSITE_EMB))
+    nxt_qv = None
     for l in range(c.layers):
         W = Fz.layers[l]
         lp = f"{PREFIX}encoder.layer.{l}.attention.self."
@@ -310,11 +311,14 @@ def text_fwd(enc: "TextEncoder", P: Dict[str, Tensor], ids: Tensor, mask: Tensor
         st.aq16.append(aq16)
         st.av16.append(av16)
         # x path: t_q = s·drop(x)·Aqᵀ, t_v = s·drop(x)·Avᵀ into the augmented columns
-        if pl > 0:
+        if pl > 0 and nxt_qv is not None:       # made by the previous layer's post-LN kernel
+            xq, xv = nxt_qv
+        elif pl > 0:
             xq = ops.dropout_to(x32, torch.empty(M, H, device=dev, dtype=bf), _drop(pl, seeds, tsite(l, 3)))
             xv = ops.dropout_to(x32, torch.empty(M, H, device=dev, dtype=bf), _drop(pl, seeds, tsite(l, 4)))
         else:
             xq = xv = xaug[:, :H]
+        nxt_qv = None
         _mm(xq, aq16, xaug[:, H:H + r], M, r, H, lda=xq.stride(0), ldb=H, ldc=Ha, alpha=s)
         _mm(xv, av16, xaug[:, H + r:H + 2 * r], M, r, H, lda=xv.stride(0), ldb=H, ldc=Ha, alpha=s)
         qkv = torch.empty(M, 3 * H, device=dev, dtype=bf)
@@ -359,8 +363,15 @@ def text_fwd(enc: "TextEncoder", P: Dict[str, Tensor], ids: Tensor, mask: Tensor
         x32n = torch.empty(M, H, device=dev)
         xaugn = torch.zeros(M, Ha, device=dev, dtype=bf)
         m2, r2 = torch.empty(M, device=dev), torch.empty(M, device=dev)
-        ops.deb_ln_fwd(z2, Fz.base[L + "output.LayerNorm.weight"],
-                       Fz.base[L + "output.LayerNorm.bias"], c.eps, x32n, xaugn, m2, r2)
+        if pl > 0 and l + 1 < c.layers and H % 256 == 0:   # next layer's LoRA inputs, fused
+            nxt_qv = (torch.empty(M, H, device=dev, dtype=bf), torch.empty(M, H, device=dev, dtype=bf))
+            ops.deb_ln_fwd(z2, Fz.base[L + "output.LayerNorm.weight"],
+                           Fz.base[L + "output.LayerNorm.bias"], c.eps, x32n, xaugn, m2, r2,
+                           yq=nxt_qv[0], yv=nxt_qv[1], drop_q=_drop(pl, seeds, tsite(l + 1, 3)),
+                           drop_v=_drop(pl, seeds, tsite(l + 1, 4)))
+        else:
+            ops.deb_ln_fwd(z2, Fz.base[L + "output.LayerNorm.weight"],
+                           Fz.base[L + "output.LayerNorm.bias"], c.eps, x32n, xaugn, m2, r2)
         st.layers.append(_LayerSaved(xaug, xq, xv, qkv, posqk, relq, u, ctx, lse, z1, m1, r1, pre,
                                      z2, m2, r2))
         x32, xaug = x32n, xaugn

@@ -754,3 +754,26 @@ def test_layernorm_bwd_dropout_copy(gpu_pkg, D):
     ops.dropout_bwd(dx, ref16, None, (p, seed_dev(seed)))
     torch.cuda.synchronize()
     assert torch.equal(dx16, ref16)
+
+
+def test_deb_ln_fwd_lora_dropout_outputs(gpu_pkg):
+    """The post-LN kernel's fused next-layer LoRA inputs equal ttmi_dropout_bwd applied to its
+    fp32 output with the same seeds (bit-exact: same values, same keep index)."""
+    ops = gpu_pkg.ops
+    M, H, p = 333, 768, 0.1
+    g = torch.Generator().manual_seed(7)
+    z = torch.randn(M, H, generator=g).to(DEV)
+    w, b = torch.randn(H, generator=g).to(DEV), torch.randn(H, generator=g).to(DEV)
+    y32 = torch.empty(M, H, device=DEV)
+    y16 = torch.empty(M, H + 64, device=DEV, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    yq = torch.empty(M, H, device=DEV, dtype=torch.bfloat16)
+    yv = torch.empty(M, H, device=DEV, dtype=torch.bfloat16)
+    sq, sv = seed_dev(0x1234), seed_dev(0x9876)
+    ops.deb_ln_fwd(z, w, b, 1e-7, y32, y16[:, :H], mean, rstd, yq=yq, yv=yv, drop_q=(p, sq),
+                   drop_v=(p, sv))
+    rq = ops.dropout_to(y32, torch.empty(M, H, device=DEV, dtype=torch.bfloat16), (p, sq))
+    rv = ops.dropout_to(y32, torch.empty(M, H, device=DEV, dtype=torch.bfloat16), (p, sv))
+    torch.cuda.synchronize()
+    assert torch.equal(yq, rq) and torch.equal(yv, rv)
+    assert not torch.equal(yq, yv)
