@@ -99,22 +99,38 @@ __global__ __launch_bounds__(256) void bn2d_bwd_reduce_kernel(int64_t M, int C, 
   for (int e = 0; e < 8; ++e) { mu[e] = cg < cpr ? mean[c0 + e] : 0.f; rs[e] = cg < cpr ? rstd[c0 + e] : 0.f; }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   if (rl < tpr && cg < cpr) {
-    for (int64_t m = r0 + rl; m < r1; m += tpr) {
-      const int64_t i = m * cpr + cg;
-      float g[8], xv[8];
-      unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
-      if (gate) {
-        float gv[8];
-        unpack8(reinterpret_cast<const uint4*>(gate)[i], gv);
+    // U rows per step, every load of the step issued before any arithmetic (a thread walks
+    // ~25 rows: one dependent memory latency per row made this a latency chain)
+    constexpr int U = 4;
+    for (int64_t mb = r0 + rl; mb < r1; mb += U * tpr) {
+      uint4 qd[U], qg[U], qx[U];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] = gv[e] > 0.f ? g[e] : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = min(mb + u * tpr, r1 - 1) * cpr + cg;
+        qd[u] = reinterpret_cast<const uint4*>(dy)[i];
+        qg[u] = gate ? reinterpret_cast<const uint4*>(gate)[i] : make_uint4(0u, 0u, 0u, 0u);
+        qx[u] = reinterpret_cast<const uint4*>(x)[i];
       }
-      if (gout) reinterpret_cast<uint4*>(gout)[i] = pack8(g);
-      unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] += g[e];
-        s2[e] += g[e] * (xv[e] - mu[e]) * rs[e];
+      for (int u = 0; u < U; ++u) {
+        const int64_t m = mb + u * tpr;
+        if (m >= r1) break;
+        const int64_t i = m * cpr + cg;
+        float g[8], xv[8];
+        unpack8(qd[u], g);
+        if (gate) {
+          float gv[8];
+          unpack8(qg[u], gv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] = gv[e] > 0.f ? g[e] : 0.f;
+        }
+        if (gout) reinterpret_cast<uint4*>(gout)[i] = pack8(g);
+        unpack8(qx[u], xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += g[e];
+          s2[e] += g[e] * (xv[e] - mu[e]) * rs[e];
+        }
       }
     }
   }

@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/c3_t.log 2>&1 || { tail -40 gpurun_out/c3_t.log; exit 1; }
+tail -2 gpurun_out/c3_t.log
+timeout -k 10 400 python bench.py --config 3 --steps 10 --warmup 3 --skip-cpu > gpurun_out/c3_b3.log 2>&1 || { tail -30 gpurun_out/c3_b3.log; exit 1; }
+grep '"metric"' gpurun_out/c3_b3.log | cut -c1-200
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/profc3 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --config 3 --steps 3 --warmup 1 --skip-cpu) > gpurun_out/profc3.log 2>&1 || { tail -30 gpurun_out/profc3.log; exit 1; }
+echo DONE
