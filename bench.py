@@ -378,12 +378,11 @@ def main_eval(args, world, rank, device):
     items[0] = 0.0
     targets = [torch.randint(1, V, (B,), generator=g).to(device) for _ in batches]
     rt = pkg.retrieval
+    ev = rt.GlobalEvaluator(model, items, K)            # one HIP graph replay per batch
+    ev_batches = [dict(b, target_id=t) for b, t in zip(batches, targets)]
 
     def step(i):
-        b = batches[i % len(batches)]
-        u = model.get_user_embedding(b["history_ids"], b["history_mask"], b["user_gender"],
-                                     b["user_country"])
-        return rt.target_ranks(u, items, targets[i % len(targets)], K)
+        return ev.ranks(ev_batches[i % len(ev_batches)])
 
     with torch.no_grad():
         for i in range(max(args.warmup, 1)):
@@ -460,7 +459,7 @@ def main_eval(args, world, rank, device):
             "data": "synthetic histories and catalogue embeddings, random-init weights",
             "config": {"workload": "eval: SURVEY 8(f) rank 2, evaluate_metrics.py:107-192",
                        "global_batch": world * B, "catalogue": V, "k": K,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "graph": True},
             "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:

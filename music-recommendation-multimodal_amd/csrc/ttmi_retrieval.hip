@@ -7,7 +7,8 @@
 //   topk_rows_kernel   one workgroup per row: exact K-th largest key by MSB-first radix select
 //                      (four 8-bit histogram passes over the row in LDS), then the keys above it
 //                      plus the lowest-index ties, sorted by (score desc, index asc) in one wave.
-//                      HBM-bound: the row is read 5 times (L2-resident for V <= ~100k).
+//                      Rows up to 16,384 scores are read from HBM once into LDS (as order keys);
+//                      longer rows are re-read per pass (L2-resident for V <= ~100k).
 //   rank_kernel        first position of target[b] in idx[b, :K] (K if absent).
 #include "ttmi_common.h"
 
@@ -24,43 +25,131 @@ TTMI_DEV float funkey(uint32_t k) {
   return __uint_as_float(u);
 }
 
-__global__ __launch_bounds__(256) void topk_rows_kernel(int V, int K, const float* __restrict__ scores,
-                                                        int64_t ld, int skip0, float* __restrict__ out_val,
-                                                        int64_t* __restrict__ out_idx) {
+constexpr int TK_LDS_MAX = 16384;      // rows up to this length are staged once in LDS (64 KB)
+constexpr int TK_NT = 512;              // threads per row (8 waves)
+
+// Block-wide exclusive prefix sum of one value per thread (TK_NT threads).
+TTMI_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* wtot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int w = 0; w < wave; ++w) base += wtot[w];
+  return base + inc - v;
+}
+
+// Histogram increment of `bin` for the lanes with `take`: the lanes sharing the first taking
+// lane's bin add once through that lane (in the first radix pass the scores of a row share
+// one or two exponents, so most of a wave lands in one bin and serialised LDS atomics on a
+// single address were the kernel's bound); the other lanes add individually.
+TTMI_DEV void hist_add(uint32_t* hist, bool take, uint32_t bin) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t act = __ballot(take);
+  if (!act) return;
+  const int leader = __ffsll((unsigned long long)act) - 1;
+  const uint32_t lb = __shfl(bin, leader, 64);
+  const uint64_t same = __ballot(take && bin == lb);
+  if (lane == leader) atomicAdd(&hist[lb], (uint32_t)__popcll(same));
+  if (take && bin != lb) atomicAdd(&hist[bin], 1u);
+}
+
+// One workgroup (8 waves) per row.  LDSROW: the row is read from HBM once (16-byte loads when
+// the row is 16-byte aligned) and kept in LDS as order keys, padded to a multiple of 4; the four
+// radix passes and the collection read it 4 keys per LDS instruction.  Otherwise every pass
+// re-reads the row from global memory (L2-resident for moderate V).
+template <bool LDSROW>
+__global__ __launch_bounds__(TK_NT) void topk_rows_kernel(int V, int K, const float* __restrict__ scores,
+                                                          int64_t ld, int skip0, float* __restrict__ out_val,
+                                                          int64_t* __restrict__ out_idx) {
+  extern __shared__ uint4 skeys4[];
+  uint32_t* skeys = reinterpret_cast<uint32_t*>(skeys4);
   __shared__ uint32_t hist[256];
   __shared__ uint32_t s_prefix, s_mask, s_rem;
-  __shared__ uint32_t s_cnt[256];
+  __shared__ uint32_t s_wtot[TK_NT / 64];
   __shared__ uint32_t s_ngt;
   __shared__ uint32_t ck[TK_MAX];
   __shared__ int32_t ci[TK_MAX];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   const float* row = scores + (int64_t)blockIdx.x * ld;
-  const int chunk = (V + 255) / 256;
+  const int chunk = (V + TK_NT - 1) / TK_NT;
   const int lo = min(V, tid * chunk), hi = min(V, lo + chunk);   // contiguous slice per thread
-  auto key_at = [&](int i) -> uint32_t {
+  const int V4 = (V + 3) >> 2;                                    // key quads (LDSROW)
+  auto gkey = [&](int i) -> uint32_t {
     return (skip0 && i == 0) ? fkey(-INFINITY) : fkey(row[i]);
   };
+  auto key_at = [&](int i) -> uint32_t {
+    if constexpr (LDSROW) return skeys[i];
+    else return gkey(i);
+  };
+  if constexpr (LDSROW) {
+    if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+      const int full = V >> 2;
+      for (int j = tid; j < full; j += TK_NT) {
+        const float4 f = reinterpret_cast<const float4*>(row)[j];
+        skeys4[j] = make_uint4(fkey(f.x), fkey(f.y), fkey(f.z), fkey(f.w));
+      }
+      for (int i = full * 4 + tid; i < V; i += TK_NT) skeys[i] = fkey(row[i]);
+    } else {
+      for (int i = tid; i < V; i += TK_NT) skeys[i] = fkey(row[i]);
+    }
+    if (tid == 0) {                        // same thread as the writes of key 0: no race
+      if (skip0) skeys[0] = fkey(-INFINITY);
+      for (int i = V; i < 4 * V4; ++i) skeys[i] = 0u;   // pad (never counted: i >= V)
+    }
+  }
   if (tid == 0) { s_prefix = 0; s_mask = 0; s_rem = (uint32_t)K; }
   // -- radix select of the K-th largest key
   for (int shift = 24; shift >= 0; shift -= 8) {
-    hist[tid] = 0;
+    if (tid < 256) hist[tid] = 0;
     __syncthreads();
     const uint32_t prefix = s_prefix, mask = s_mask;
-    for (int i = tid; i < V; i += 256) {                    // coalesced
-      const uint32_t u = key_at(i);
-      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+    if constexpr (LDSROW) {
+      for (int j = tid; j < V4; j += TK_NT) {
+        const uint4 q = skeys4[j];
+        const uint32_t k4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          hist_add(hist, 4 * j + e < V && (k4[e] & mask) == prefix, (k4[e] >> shift) & 255u);
+      }
+    } else {
+      for (int i = tid; i < V; i += TK_NT) {                // coalesced
+        const uint32_t u = gkey(i);
+        hist_add(hist, (u & mask) == prefix, (u >> shift) & 255u);
+      }
     }
     __syncthreads();
-    if (tid == 0) {
-      uint32_t rem = s_rem, above = 0;
-      int d = 255;
-      for (; d > 0; --d) {
-        if (above + hist[d] >= rem) break;
-        above += hist[d];
+    if (tid < 64) {
+      // the digit d: keys with a larger digit number < rem <= those with digit >= d.  Lane l
+      // holds digits 255-4l .. 252-4l; a wave prefix sum over lanes = descending digits.
+      uint32_t h[4], tot = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { h[j] = hist[255 - 4 * lane - j]; tot += h[j]; }
+      uint32_t inc = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
       }
-      s_rem = rem - above;                 // how many keys equal to the prefix we still need
-      s_prefix = prefix | ((uint32_t)d << shift);
-      s_mask = mask | (255u << shift);
+      const uint32_t rem = s_rem, excl = inc - tot;
+      if (excl < rem && rem <= inc) {                       // exactly one lane
+        uint32_t above = excl;
+        int d = 255 - 4 * lane;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (above + h[j] >= rem) break;
+          above += h[j];
+          --d;
+        }
+        s_rem = rem - above;               // how many keys equal to the prefix we still need
+        s_prefix = prefix | ((uint32_t)d << shift);
+        s_mask = mask | (255u << shift);
+      }
     }
     __syncthreads();
   }
@@ -69,17 +158,27 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(int V, int K, const floa
   // -- collect: keys > T anywhere, keys == T in index order
   uint32_t n_eq = 0;
   for (int i = lo; i < hi; ++i) n_eq += key_at(i) == T ? 1u : 0u;
-  s_cnt[tid] = n_eq;
   if (tid == 0) s_ngt = 0;
-  __syncthreads();
-  uint32_t before = 0;                     // exclusive scan of tie counts (contiguous slices)
-  for (int t = 0; t < tid; ++t) before += s_cnt[t];
+  uint32_t before = block_exclusive_scan(n_eq, s_wtot);   // tie counts of the slices before
   const uint32_t n_gt_total = (uint32_t)K - need_eq;
-  for (int i = tid; i < V; i += 256) {                      // keys above T: any order
-    const uint32_t u = key_at(i);
-    if (u > T) {
-      const uint32_t p = atomicAdd(&s_ngt, 1u);
-      ck[p] = u; ci[p] = i;
+  if constexpr (LDSROW) {
+    for (int j = tid; j < V4; j += TK_NT) {                 // keys above T: any order
+      const uint4 q = skeys4[j];
+      const uint32_t k4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (k4[e] > T && 4 * j + e < V) {
+          const uint32_t p = atomicAdd(&s_ngt, 1u);
+          ck[p] = k4[e]; ci[p] = 4 * j + e;
+        }
+    }
+  } else {
+    for (int i = tid; i < V; i += TK_NT) {
+      const uint32_t u = gkey(i);
+      if (u > T) {
+        const uint32_t p = atomicAdd(&s_ngt, 1u);
+        ck[p] = u; ci[p] = i;
+      }
     }
   }
   for (int i = lo; i < hi && before < need_eq; ++i) {       // ties at T: lowest indices first
@@ -141,8 +240,12 @@ extern "C" int ttmi_topk_rows(int R, int V, int K, const float* scores, int64_t 
   TTMI_REQUIRE(R > 0 && V > 0 && K > 0 && K <= TK_MAX && K <= V && ld >= V,
                "ttmi_topk_rows: need 0 < K <= min(V, %d), ld >= V", TK_MAX);
   TTMI_REQUIRE(scores && out_val && out_idx, "ttmi_topk_rows: null argument");
-  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)R), dim3(256), 0, s, V, K, scores, ld, skip_first,
-                     out_val, out_idx);
+  if (V <= TK_LDS_MAX)
+    hipLaunchKernelGGL(topk_rows_kernel<true>, dim3((unsigned)R), dim3(TK_NT), (size_t)((V + 3) / 4) * 16, s, V,
+                       K, scores, ld, skip_first, out_val, out_idx);
+  else
+    hipLaunchKernelGGL(topk_rows_kernel<false>, dim3((unsigned)R), dim3(TK_NT), 0, s, V, K, scores, ld,
+                       skip_first, out_val, out_idx);
   return ttmi_check_launch("ttmi_topk_rows");
 }
 

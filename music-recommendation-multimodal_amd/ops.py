@@ -471,8 +471,19 @@ def infonce_bwd(u_hat: Tensor, i_hat: Tensor, norms: Tensor, logits: Tensor, lse
 
 
 # ----------------------------------------------------------------------------- misc
+# Parameter writes through raw pointers (AdamW, TrainStep graph replays) do not
+# move torch's version counters; writers bump this epoch so caches of derived operands (the
+# eval-mode bf16 weight copies, user_tower.inference_operands) see the change.
+PARAM_EPOCH = [0]
+
+
+def bump_param_epoch() -> None:
+    PARAM_EPOCH[0] += 1
+
+
 def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
           step: Tensor, zero_grad: bool = False):
+    bump_param_epoch()
     call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
          int(zero_grad), _s())
 

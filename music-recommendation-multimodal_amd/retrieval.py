@@ -72,22 +72,75 @@ def metrics_from_ranks(ranks: Tensor, k_list: Sequence[int]) -> Dict[str, Tensor
     return out
 
 
+class GlobalEvaluator:
+    """The per-batch work of calculate_metrics_global (evaluate_metrics.py:139-161): user
+    embedding (eval) -> fp32 catalogue scores -> top-max_k -> target ranks, replayed from a HIP
+    graph captured once per batch signature (size, present keys, dtypes); the eval loop is then
+    one graph launch per batch instead of ~25 host-issued kernels.  Batches are staged into the
+    graph's static inputs; ``ranks`` returns the graph's static output (valid until the next
+    call).  The user tower's cached bf16 weights are re-checked before every replay, so a
+    model trained between evaluations is scored with its current weights."""
+
+    KEYS = ("history_ids", "history_mask", "user_gender", "user_country", "target_id")
+
+    def __init__(self, model, item_embeddings: Tensor, max_k: int, use_graph: bool = True):
+        self.model = model
+        self.items = item_embeddings.float().contiguous()
+        self.max_k = max_k
+        # graphs only for this package's model: a foreign model may keep host-side state
+        # (or run host syncs) per call, which a replay would not reproduce
+        self._tower = getattr(model, "user_tower", None)
+        if not hasattr(self._tower, "inference_operands"):
+            self._tower = None
+        self.use_graph = use_graph and self._tower is not None
+        self._graphs: Dict[tuple, tuple] = {}
+
+    def _run(self, b: Dict[str, Tensor]) -> Tensor:
+        u = self.model.get_user_embedding(history_ids=b["history_ids"],
+                                          history_mask=b.get("history_mask"),
+                                          user_gender=b.get("user_gender"),
+                                          user_country=b.get("user_country"))
+        return target_ranks(u, self.items, b["target_id"], self.max_k)
+
+    def ranks(self, batch: Dict[str, Tensor]) -> Tensor:
+        dev = self.items.device
+        b = {k: batch[k].to(dev, non_blocking=True) for k in self.KEYS if batch.get(k) is not None}
+        self.model.eval()
+        with torch.no_grad():
+            if self._tower is not None:
+                self._tower.inference_operands()             # refresh cached weights (host check)
+            if not self.use_graph:
+                return self._run(b)
+            sig = tuple((k, tuple(t.shape), t.dtype) for k, t in sorted(b.items()))
+            ent = self._graphs.get(sig)
+            if ent is None:
+                static = {k: t.clone() for k, t in b.items()}
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):              # warm-up: code objects, pool sizes
+                    self._run(static)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                torch.cuda.synchronize(dev)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    out = self._run(static)
+                ent = self._graphs[sig] = (static, out, graph)
+            static, out, graph = ent
+            ops.batch_copy([static[k] for k in static], [b[k].contiguous() for k in static])
+            graph.replay()
+            return out
+
+
 def calculate_metrics_global(model, val_loader: Iterable, item_embeddings: Tensor, device,
-                             k_list: List[int] = [10, 20]) -> Dict[str, float]:
+                             k_list: List[int] = [10, 20], use_graph: bool = True) -> Dict[str, float]:
     """evaluate_metrics.py:107-192 on libttmi kernels: same batch keys, same metrics."""
     model.eval()
-    item_embeddings = item_embeddings.to(device).float()
+    ev = GlobalEvaluator(model, item_embeddings.to(device), max(k_list), use_graph=use_graph)
     per: Dict[str, List[Tensor]] = {f"Recall@{k}": [] for k in k_list}
     per.update({f"NDCG@{k}": [] for k in k_list})
-    max_k = max(k_list)
     with torch.no_grad():
         for batch in val_loader:
-            user_emb = model.get_user_embedding(
-                history_ids=batch["history_ids"].to(device),
-                history_mask=batch["history_mask"].to(device),
-                user_gender=batch["user_gender"].to(device),
-                user_country=batch["user_country"].to(device))
-            ranks = target_ranks(user_emb, item_embeddings, batch["target_id"].to(device), max_k)
+            ranks = ev.ranks(batch)
             for name, v in metrics_from_ranks(ranks, k_list).items():
                 per[name].append(v.cpu())
     return {name: torch.cat(v).mean().item() for name, v in per.items()}

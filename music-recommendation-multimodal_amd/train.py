@@ -167,6 +167,7 @@ class TrainStep:
         self.p_item = model.item_tower.fusion_layer[3].p
         self.dtype = self.ucfg.dtype
         self.flat = FlatParams(model, self.dtype)
+        ops.bump_param_epoch()                 # parameters now live in (and move with) the flat buffer
         self.sync = GradSync(group)
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay],
                                   dtype=torch.float64, device=dev)
@@ -339,6 +340,7 @@ class TrainStep:
                 self._update()
 
     def step(self, batch: Dict[str, Tensor]) -> Tensor:
+        ops.bump_param_epoch()                 # the replay below rewrites the parameters
         b = self._stage(batch)
         if not self.use_graph:
             self._fwd_bwd(b)

@@ -71,6 +71,10 @@ def make_operands(P: dict, dtype: torch.dtype, gemm_names) -> dict:
     return W
 
 
+def cfg_dtype_bf16(dtype: torch.dtype) -> bool:
+    return dtype == torch.bfloat16
+
+
 def encoder_weight_names(names) -> List[str]:
     return [n for n in names if n.endswith(GEMM_WEIGHTS)]
 
@@ -179,8 +183,35 @@ class SequentialUserEncoder(nn.Module):
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             return _UserTowerFn.apply(cfg, list(names), seeds, ids, user_gender.contiguous(),
                                       user_country.contiguous(), mask, *params)
-        P = dict(zip(names, [p.detach() for p in params]))
-        W = make_operands(P, cfg.dtype, _gemm_names(list(names)))
+        P, W = self.inference_operands()
         u, _ = F.user_tower_fwd(P, W, ids, user_gender.contiguous(), user_country.contiguous(),
                                 mask, cfg, seeds)
         return u
+
+    def inference_operands(self):
+        """(P, W) for no-grad forwards.  The bf16 GEMM copies and transposed mirrors are cached
+        and rebuilt only when a parameter changed (storage or in-place version): an eval loop
+        over a fixed model casts its weights once, not once per batch.  A changed parameter at
+        the same storage is re-cast into the same buffers, so a captured graph that reads them
+        stays valid (GlobalEvaluator in retrieval.py re-checks before every replay).  Raw-pointer
+        parameter writers (TrainStep, ops.adamw) bump ops.PARAM_EPOCH, which is part of the key."""
+        names, params = zip(*self.named_parameters())
+        key = tuple((p.data_ptr(), p._version) for p in params) + (ops.PARAM_EPOCH[0], self.compute_dtype)
+        c = getattr(self, "_inf_cache", None)
+        if c is not None and c[0] == key:
+            return c[1], c[2]
+        P = dict(zip(names, [p.detach() for p in params]))
+        gn = _gemm_names(list(names))
+        if (c is not None and c[0][-1] == key[-1] and cfg_dtype_bf16(self.compute_dtype)
+                and all(a[0] == b[0] for a, b in zip(c[0][:-2], key[:-2]))):
+            W = c[2]                                    # same storages: refresh in place
+            for n in gn:
+                ops.cast_bf16(P[n].contiguous(), W[n])
+            refresh_transposes(W, gn)
+            for n in P:
+                if n not in gn:
+                    W[n] = P[n]
+        else:
+            W = make_operands(P, self.compute_dtype, gn)
+        self._inf_cache = (key, P, W)
+        return P, W

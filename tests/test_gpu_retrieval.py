@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("R,V,K", [(7, 100, 10), (33, 10136, 20), (5, 3001, 64), (3, 64, 64)])
+@pytest.mark.parametrize("R,V,K", [(7, 100, 10), (33, 10136, 20), (5, 3001, 64), (3, 64, 64), (4, 16384, 20),
+                                    (4, 16385, 20), (3, 40000, 50)])
 def test_topk_rows_vs_torch(gpu_pkg, R, V, K):
     ops = gpu_pkg.ops
     g = torch.Generator().manual_seed(V + K)
@@ -33,6 +34,21 @@ def test_topk_rows_vs_torch(gpu_pkg, R, V, K):
     s3[:, 0] = -float("inf")
     rv, ri = torch.topk(s3, K, dim=1)
     assert torch.equal(idx.cpu(), ri) and torch.equal(val.cpu(), rv)
+
+
+@pytest.mark.parametrize("V", [10136, 30000])
+def test_topk_rows_one_exponent(gpu_pkg, V):
+    """Scores in [1, 2): one exponent, so the first radix digit is the same for every key and
+    the histogram's wave aggregation carries the whole pass (LDS-staged and global rows)."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(V)
+    s = 1.0 + torch.rand(6, V, generator=g)
+    val = torch.empty(6, 20, device=DEV)
+    idx = torch.empty(6, 20, device=DEV, dtype=torch.int64)
+    ops.topk_rows(s.to(DEV), 20, val, idx, skip_first=True)
+    s[:, 0] = -float("inf")
+    nv, ri = torch.sort(-s, dim=1, stable=True)         # ties (a few here): lower index first
+    assert torch.equal(val.cpu(), -nv[:, :20]) and torch.equal(idx.cpu(), ri[:, :20])
 
 
 def test_topk_rows_ties_lower_index_first(gpu_pkg):
@@ -75,6 +91,49 @@ def test_retrieval_metrics_vs_reference_fixture(gpu_pkg):
     res = retrieval.calculate_metrics_global(Stub(), loader, items, DEV, k_list=[10, 20])
     for k, v in res.items():
         assert abs(v - float(z["metric/" + k])) <= 1.0 / n + 1e-6, (k, v, float(z["metric/" + k]))
+
+
+def test_global_evaluator_graph_matches_eager(gpu_pkg):
+    """GlobalEvaluator's graph replay vs the eager path: two batches of one size (one capture,
+    restaged inputs), a batch of another size (a second capture), and a replay after an in-place
+    weight update (the cached bf16 operands are refreshed into the captured buffers)."""
+    torch.manual_seed(0)
+    V, D = 2000, 128
+    m = gpu_pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=3, num_countries=8,
+                              max_seq_len=50, user_embedding_dim=D, item_embedding_dim=D,
+                              user_num_heads=4, compute_dtype=torch.bfloat16).to(DEV).eval()
+    g = torch.Generator().manual_seed(2)
+    items = torch.nn.functional.normalize(torch.randn(V, D, generator=g), dim=1).to(DEV)
+
+    def batch(B):
+        lens = torch.randint(1, 51, (B,), generator=g)
+        ids = torch.randint(1, V, (B, 50), generator=g)
+        ids[torch.arange(50)[None, :] >= lens[:, None]] = 0
+        return {"history_ids": ids, "history_mask": (ids != 0).long(),
+                "user_gender": torch.randint(0, 3, (B,), generator=g),
+                "user_country": torch.randint(0, 8, (B,), generator=g),
+                "target_id": torch.randint(1, V, (B,), generator=g)}
+    rt = gpu_pkg.retrieval
+    ev = rt.GlobalEvaluator(m, items, 20)
+    eager = rt.GlobalEvaluator(m, items, 20, use_graph=False)
+    assert ev.use_graph
+    for b in (batch(64), batch(64), batch(37)):
+        # targets taken from the eager top-20 so the ranks are informative
+        with torch.no_grad():
+            u = m.get_user_embedding(b["history_ids"].to(DEV), b["history_mask"].to(DEV),
+                                     b["user_gender"].to(DEV), b["user_country"].to(DEV))
+        top = rt.topk_items(u, items, 20)[1].cpu()
+        b["target_id"][::2] = top[::2, 5]
+        r_graph = ev.ranks(b).clone()
+        assert torch.equal(r_graph.cpu(), eager.ranks(b).cpu())
+        assert (r_graph[::2] < 20).float().mean() > 0.9
+    assert len(ev._graphs) == 2
+    with torch.no_grad():
+        m.user_tower.transformer_encoder.layers[0].linear1.weight.mul_(-1.0)
+        m.user_tower.fusion_layer[3].weight.mul_(0.5)
+    b = batch(64)
+    assert torch.equal(ev.ranks(b).cpu(), eager.ranks(b).cpu())
+    assert len(ev._graphs) == 2
 
 
 def test_recommend_matches_oracle_inference(gpu_pkg):
