@@ -369,6 +369,15 @@ int ttmi_linear_res_ln(const ttmi_linear_res_ln_desc* d, hipStream_t stream);
  * TransformerEncoderLayer backward, reference src/models/user_tower.py:37-45). */
 int ttmi_transpose_bf16_batch(int n, void* const* dst, const void* const* src,
                               const int64_t* rows, const int64_t* cols, hipStream_t stream);
+/* ttmi_transpose_bf16_batch plus, in one extra workgroup of the same launch, the step's
+ * dropout seeds exactly as ttmi_dropout_seeds(seed_base, step, seeds, n_seeds, inc_step)
+ * (0 < n_seeds <= 256; n_seeds = 0: transposes only; n = 0: seeds only).  The per-step
+ * prologue of the captured train step (mirror refresh after AdamW + dropout seeds of the
+ * reference's nn.Dropout draws) in one dispatch.  ABI 7. */
+int ttmi_transpose_bf16_batch_seeds(int n, void* const* dst, const void* const* src,
+                                    const int64_t* rows, const int64_t* cols, uint64_t seed_base,
+                                    int32_t* step, uint64_t* seeds, int n_seeds, int inc_step,
+                                    hipStream_t stream);
 /* dst = bf16(src) (parameter mirror for bf16 GEMM operands). */
 int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hipStream_t stream);
 /* Residual-branch dropout backward (TransformerEncoderLayer dropout1/dropout2):

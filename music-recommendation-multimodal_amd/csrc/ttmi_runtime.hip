@@ -25,7 +25,7 @@ int ttmi_check_launch(const char* what) {
 }
 
 extern "C" const char* ttmi_last_error(void) { return g_err; }
-extern "C" int ttmi_abi_version(void) { return 6; }
+extern "C" int ttmi_abi_version(void) { return 7; }
 
 namespace {
 
@@ -358,8 +358,26 @@ struct TransposeList {
   int n;
 };
 
-__global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl) {
+// Optional side job of the same launch: the step's dropout seeds (dropout_seeds_kernel's body
+// in one extra workgroup), so a step that refreshes its mirrors and draws its seeds pays one
+// launch for both.
+struct SeedJob {
+  uint64_t base;
+  int32_t* step;
+  uint64_t* seeds;
+  int n, inc;
+};
+
+__global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl, SeedJob sj) {
   __shared__ uint16_t t[64][65];
+  if ((int)blockIdx.x == tl.tile0[tl.n]) {         // the seed workgroup (launched when sj.n > 0)
+    const int s = threadIdx.x;
+    const int32_t st = sj.step[0] + (sj.inc ? 1 : 0);
+    if (s < sj.n) sj.seeds[s] = splitmix64(splitmix64(sj.base) ^ ((uint64_t)(int64_t)st * 64ull + (uint64_t)s));
+    __syncthreads();                               // every thread has read the old count
+    if (sj.inc && s == 0) sj.step[0] = st;
+    return;
+  }
   int i = 0;
   while (i + 1 < tl.n && (int)blockIdx.x >= tl.tile0[i + 1]) ++i;
   const int local = blockIdx.x - tl.tile0[i];
@@ -376,12 +394,16 @@ __global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl) 
     if (c0 + c < C && r0 + tx < R) dst[(int64_t)(c0 + c) * R + r0 + tx] = t[tx][c];
 }
 
-extern "C" int ttmi_transpose_bf16_batch(int n, void* const* dst, const void* const* src,
-                                         const int64_t* rows, const int64_t* cols,
-                                         hipStream_t s) {
+extern "C" int ttmi_transpose_bf16_batch_seeds(int n, void* const* dst, const void* const* src,
+                                               const int64_t* rows, const int64_t* cols,
+                                               uint64_t seed_base, int32_t* step, uint64_t* seeds,
+                                               int n_seeds, int inc_step, hipStream_t s) {
   TTMI_REQUIRE(n >= 0 && n <= MAX_COPIES, "ttmi_transpose_bf16_batch: at most %d matrices", MAX_COPIES);
-  if (n == 0) return TTMI_OK;
-  TTMI_REQUIRE(dst && src && rows && cols, "ttmi_transpose_bf16_batch: null argument");
+  TTMI_REQUIRE(n_seeds >= 0 && n_seeds <= 256 && (n_seeds == 0 || (step && seeds)),
+               "ttmi_transpose_bf16_batch_seeds: bad seed arguments");
+  SeedJob sj{seed_base, step, seeds, n_seeds, inc_step};
+  if (n == 0 && n_seeds == 0) return TTMI_OK;
+  TTMI_REQUIRE(n == 0 || (dst && src && rows && cols), "ttmi_transpose_bf16_batch: null argument");
   TransposeList tl;
   tl.n = n;
   tl.tile0[0] = 0;
@@ -397,9 +419,16 @@ extern "C" int ttmi_transpose_bf16_batch(int n, void* const* dst, const void* co
     TTMI_REQUIRE(tl.tile0[i] + tiles < (1 << 30), "ttmi_transpose_bf16_batch: too large");
     tl.tile0[i + 1] = tl.tile0[i] + (int)tiles;
   }
-  if (tl.tile0[n] == 0) return TTMI_OK;
-  hipLaunchKernelGGL(transpose_batch_kernel, dim3(tl.tile0[n]), dim3(256), 0, s, tl);
+  const int blocks = tl.tile0[n] + (n_seeds > 0 ? 1 : 0);
+  if (blocks == 0) return TTMI_OK;
+  hipLaunchKernelGGL(transpose_batch_kernel, dim3(blocks), dim3(256), 0, s, tl, sj);
   return ttmi_check_launch("ttmi_transpose_bf16_batch");
+}
+
+extern "C" int ttmi_transpose_bf16_batch(int n, void* const* dst, const void* const* src,
+                                         const int64_t* rows, const int64_t* cols,
+                                         hipStream_t s) {
+  return ttmi_transpose_bf16_batch_seeds(n, dst, src, rows, cols, 0, nullptr, nullptr, 0, 0, s);
 }
 
 extern "C" int ttmi_step_inc(int32_t* step, hipStream_t s) {

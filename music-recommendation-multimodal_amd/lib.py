@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -123,6 +123,7 @@ SIGNATURES = {
     "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_transpose_bf16_batch_seeds": (c_i, [c_i, c_p, c_p, c_p, c_p, c_u64, c_p, c_p, c_i, c_i, c_p]),
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
     "ttmi_linear_res_ln": (c_i, [c_p, c_p]),
     "ttmi_deb_embed_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, ctypes.c_float, c_p,

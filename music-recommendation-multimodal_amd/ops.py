@@ -500,10 +500,12 @@ def batch_copy(dsts, srcs):
     call("ttmi_batch_copy", n, D, S, N, _s())
 
 
-def transpose_batch(dsts, srcs):
-    """One launch: dsts[i] = srcs[i].t() for 2-D bf16 matrices (dsts[i] is [cols, rows])."""
+def transpose_batch(dsts, srcs, seeds=None):
+    """One launch: dsts[i] = srcs[i].t() for 2-D bf16 matrices (dsts[i] is [cols, rows]).
+    ``seeds=(base, step, seeds_tensor, inc_step)`` also draws the step's dropout seeds in the
+    same launch (``dropout_seeds``'s semantics, one extra workgroup)."""
     n = len(dsts)
-    if n == 0:
+    if n == 0 and seeds is None:
         return
     for d, s_ in zip(dsts, srcs):
         if s_.dim() != 2 or d.shape != (s_.shape[1], s_.shape[0]) or not s_.is_contiguous() \
@@ -513,7 +515,14 @@ def transpose_batch(dsts, srcs):
     S = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
     R = (ctypes.c_int64 * n)(*[t.shape[0] for t in srcs])
     C = (ctypes.c_int64 * n)(*[t.shape[1] for t in srcs])
-    call("ttmi_transpose_bf16_batch", n, D, S, R, C, _s())
+    if seeds is None:
+        call("ttmi_transpose_bf16_batch", n, D, S, R, C, _s())
+        return
+    base, step, sd, inc = seeds
+    if step.dtype != torch.int32 or sd.dtype != torch.int64 or not (0 < sd.numel() <= 256):
+        raise ValueError("transpose_batch: seeds need an int32 step and 1..256 int64 seeds")
+    call("ttmi_transpose_bf16_batch_seeds", n, D, S, R, C, base & (2**64 - 1), _p(step), _p(sd),
+         sd.numel(), int(inc), _s())
 
 
 def step_inc(step: Tensor):

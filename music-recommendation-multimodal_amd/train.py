@@ -226,13 +226,17 @@ class TrainStep:
     def _fwd_bwd(self, b: Dict[str, Tensor]) -> None:
         # the gradient buffer is zero here: it starts zeroed and the fused AdamW clears it
         seeds = None
-        if self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0):
-            ops.dropout_seeds(self.base_seed, self.step_t, self.seeds, inc_step=True)
+        draw = self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0)
+        if self.flat.mirror is not None:
+            # Wᵀ mirrors of the just-updated bf16 weights, and the step's seeds: one launch
+            refresh_transposes(self.Wu, _gemm_names(list(self.Pu)),
+                               (self.base_seed, self.step_t, self.seeds, True) if draw else None)
+        if draw:
+            if self.flat.mirror is None:
+                ops.dropout_seeds(self.base_seed, self.step_t, self.seeds, inc_step=True)
             seeds = self.seeds
         else:
             ops.step_inc(self.step_t)
-        if self.flat.mirror is not None:      # Wᵀ mirrors of the just-updated bf16 weights
-            refresh_transposes(self.Wu, _gemm_names(list(self.Pu)))
         u, ust = F.user_tower_fwd(self.Pu, self.Wu, b["history_ids"], b["user_gender"],
                                   b["user_country"], b.get("history_mask"), self.ucfg, seeds)
         if self.raw_items:

@@ -87,10 +87,11 @@ def add_transposes(W: dict, gemm_names) -> None:
                                               dtype=w.dtype)
 
 
-def refresh_transposes(W: dict, gemm_names) -> None:
-    """W[name + '.T'] = W[name]ᵀ for all encoder-layer weights in one launch."""
+def refresh_transposes(W: dict, gemm_names, seeds=None) -> None:
+    """W[name + '.T'] = W[name]ᵀ for all encoder-layer weights in one launch (plus the step's
+    dropout seeds when ``seeds`` = (base, step, table, inc_step) is given)."""
     names = [n for n in encoder_weight_names(gemm_names) if F.transposed_name(n) in W]
-    ops.transpose_batch([W[F.transposed_name(n)] for n in names], [W[n] for n in names])
+    ops.transpose_batch([W[F.transposed_name(n)] for n in names], [W[n] for n in names], seeds)
 
 
 def _gemm_names(names: List[str]):

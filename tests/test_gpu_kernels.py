@@ -553,6 +553,24 @@ def test_dropout_seed_kernel_matches_host(gpu_pkg):
     assert torch.equal(seeds.cpu(), F.seed_table(F.site_seeds(0xABCDEF, 13), "cpu"))
 
 
+def test_transpose_batch_with_seeds(gpu_pkg):
+    """The train step's prologue launch: mirror transposes plus the dropout seeds (same values
+    and step increment as dropout_seeds), and the seeds-only form (no matrices)."""
+    ops, F = gpu_pkg.ops, gpu_pkg.functional
+    srcs = [torch.randn(384, 128, device=DEV).bfloat16(), torch.randn(70, 130, device=DEV).bfloat16()]
+    dsts = [torch.empty(t.shape[1], t.shape[0], device=DEV, dtype=torch.bfloat16) for t in srcs]
+    step = torch.tensor([40], dtype=torch.int32, device=DEV)
+    seeds = torch.zeros(F.N_SITES, dtype=torch.int64, device=DEV)
+    ops.transpose_batch(dsts, srcs, (0x5EED, step, seeds, True))
+    for d, s_ in zip(dsts, srcs):
+        assert torch.equal(d, s_.t())
+    assert int(step) == 41
+    assert torch.equal(seeds.cpu(), F.seed_table(F.site_seeds(0x5EED, 41), "cpu"))
+    ops.transpose_batch([], [], (0x5EED, step, seeds, False))
+    assert int(step) == 41
+    assert torch.equal(seeds.cpu(), F.seed_table(F.site_seeds(0x5EED, 41), "cpu"))
+
+
 def test_transpose_batch(gpu_pkg):
     """Batched bf16 transpose (the Wᵀ mirrors of the input-grad GEMMs): ragged shapes."""
     ops = gpu_pkg.ops
