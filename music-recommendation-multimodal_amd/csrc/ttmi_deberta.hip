@@ -224,17 +224,19 @@ __global__ __launch_bounds__(256) void deb_gelu_kernel(int64_t n8, const bf16_t*
 // (group = 64, sgs = 8 for the relative-path Bq contraction; group = Mw for plain dB/dA).
 // C element (m, c) sits at m·ldc_m + c·ldc_c.  R is long (B·S = 65,536) and the output tiny
 // (768 x 8), so this is an HBM stream of W: each thread owns 8 consecutive W columns (16-byte
-// loads, 64 fp32 accumulators) over a strided row set; the block's row groups are summed in
-// LDS and every block adds its 6 KB partial with contiguous atomics.  The generic tile path
+// loads, 64 fp32 accumulators) over a strided row set; RG row groups of Mw/8 threads per block
+// (768 threads at Mw 768) are added in turn into one LDS tile and every block adds its 24 KB
+// partial with contiguous atomics.  One block per CU: the per-thread row walk is the latency
+// chain, the atomics (blocks x 24 KB at ~1.3 TB/s) the other cost.  The generic tile path
 // spent ~260 us per call here padding the rank-8 side to 64.
-template <typename TS>
-__global__ __launch_bounds__(256) void skinny_wgrad_kernel(int64_t R, int Mw, const bf16_t* __restrict__ W,
-                                                           int64_t ldw, const TS* __restrict__ S,
-                                                           int64_t lds, int group, int sgs, float alpha,
-                                                           float* __restrict__ C, int64_t ldc_m,
-                                                           int64_t ldc_c, int64_t rows_per_block) {
-  extern __shared__ float red[];                       // [RG][Mw·8]
-  const int ncol8 = Mw / 8, RG = 256 / ncol8;
+template <typename TS, int U>
+__global__ __launch_bounds__(1024) void skinny_wgrad_kernel(int64_t R, int Mw, const bf16_t* __restrict__ W,
+                                                            int64_t ldw, const TS* __restrict__ S,
+                                                            int64_t lds, int group, int sgs, float alpha,
+                                                            float* __restrict__ C, int64_t ldc_m,
+                                                            int64_t ldc_c, int64_t rows_per_block) {
+  extern __shared__ float red[];                       // [Mw·8], the row groups added in turn
+  const int ncol8 = Mw / 8, RG = blockDim.x / ncol8;   // blockDim.x = RG·ncol8
   const int t = threadIdx.x, rg = t / ncol8, c8 = t % ncol8;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(R, r0 + rows_per_block);
@@ -243,10 +245,9 @@ __global__ __launch_bounds__(256) void skinny_wgrad_kernel(int64_t R, int Mw, co
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int c = 0; c < 8; ++c) acc[i][c] = 0.f;
-  if (rg < RG) {
+  {
     const int soff = (c8 * 8 / group) * sgs;
-    // 8 rows per step: all loads issued before the FMAs (the loop is load-latency bound)
-    constexpr int U = 8;
+    // U rows per step: all loads issued before the FMAs (the loop is load-latency bound)
     for (int64_t rb = r0 + rg; rb < r1; rb += U * RG) {
       uint4 wq[U], sq[U], sq2[U];
 #pragma unroll
@@ -275,23 +276,45 @@ __global__ __launch_bounds__(256) void skinny_wgrad_kernel(int64_t R, int Mw, co
           for (int c = 0; c < 8; ++c) acc[i][c] += w[i] * s[c];
       }
     }
-    float* dst = red + (int64_t)rg * Mw * 8 + c8 * 64;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int c = 0; c < 8; c += 4)
-        *reinterpret_cast<float4*>(dst + i * 8 + c) = make_float4(acc[i][c], acc[i][c + 1], acc[i][c + 2], acc[i][c + 3]);
   }
-  __syncthreads();
+  float* dst = red + c8 * 64;
+  for (int g = 0; g < RG; ++g) {                       // fixed order: deterministic per block
+    if (rg == g) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int c = 0; c < 8; c += 4) {
+          float4* p = reinterpret_cast<float4*>(dst + i * 8 + c);
+          float4 v = make_float4(acc[i][c], acc[i][c + 1], acc[i][c + 2], acc[i][c + 3]);
+          if (g > 0) {
+            const float4 o = *p;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *p = v;
+        }
+    }
+    __syncthreads();
+  }
   // contiguous in C: walk (m fastest) when ldc_m == 1, else (c fastest)
   const int n = Mw * 8;
-  for (int o = t; o < n; o += 256) {
+  for (int o = t; o < n; o += blockDim.x) {
     int m, c;
     if (ldc_m == 1) { c = o / Mw; m = o % Mw; } else { m = o / 8; c = o % 8; }
-    float v = 0.f;
-    for (int g = 0; g < RG; ++g) v += red[(int64_t)g * n + m * 8 + c];
-    atomicAdd(C + m * ldc_m + c * ldc_c, alpha * v);
+    atomicAdd(C + m * ldc_m + c * ldc_c, alpha * red[m * 8 + c]);
   }
+}
+
+struct SkinnyCfg { int rg, u, blocks; };
+SkinnyCfg skinny_cfg() {                               // TTMI_SKINNY="RG,U,BLOCKS": tuning runs
+  static const SkinnyCfg cfg = [] {
+    SkinnyCfg c{8, 4, 256};   // tools/skinny_sweep.py (R 65,536, Mw 768): 69 -> 44 us vs {2, 8, 512}
+    if (const char* e = getenv("TTMI_SKINNY")) {
+      int rg = 0, u = 0, bl = 0;
+      if (sscanf(e, "%d,%d,%d", &rg, &u, &bl) == 3 && rg > 0 && (u == 4 || u == 8) && bl > 0) c = SkinnyCfg{rg, u, bl};
+    }
+    return c;
+  }();
+  return cfg;
 }
 
 // dx[m, n] += s · Σ_{p in {q, v}} drop_p(dL_p[m, :] · A_p[:, n])  (the LoRA input gradient of
@@ -445,19 +468,23 @@ extern "C" int ttmi_skinny_wgrad(int64_t R, int Mw, const uint16_t* W, int64_t l
                (uintptr_t)S % 16 == 0 && lds % (s_f32 ? 4 : 8) == 0,
                "ttmi_skinny_wgrad: W/S need 16-byte rows, group %% 8 == 0");
   TTMI_REQUIRE((int64_t)((Mw - 1) / group) * sgs + 8 <= lds, "ttmi_skinny_wgrad: S slice past its row");
-  const int RG = 256 / (Mw / 8);
-  const size_t shm = (size_t)RG * Mw * 8 * sizeof(float);
+  const SkinnyCfg cfg = skinny_cfg();
+  const int ncol8 = Mw / 8;
+  const int RG = std::max(1, std::min(cfg.rg, 1024 / ncol8));
+  const size_t shm = (size_t)Mw * 8 * sizeof(float);
   TTMI_REQUIRE(shm <= 64 * 1024, "ttmi_skinny_wgrad: reduction tile exceeds 64 KB");
-  // ~2 workgroups per CU: the stream needs the waves (one per CU ran at 1.2 TB/s); the 24 KB
-  // partial per workgroup keeps the atomic bytes ~1/8 of the streamed bytes
-  const int64_t blocks = std::min<int64_t>(512, std::max<int64_t>(1, R / (4 * RG)));
+  const int64_t blocks = std::min<int64_t>(cfg.blocks, std::max<int64_t>(1, R / (4 * RG)));
   const int64_t rpb = (R + blocks - 1) / blocks;
-  if (s_f32)
-    hipLaunchKernelGGL(skinny_wgrad_kernel<float>, dim3((unsigned)blocks), dim3(256), shm, s, R, Mw,
-                       (const bf16_t*)W, ldw, (const float*)S, lds, group, sgs, alpha, C, ldc_m, ldc_c, rpb);
-  else
-    hipLaunchKernelGGL(skinny_wgrad_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), shm, s, R, Mw,
-                       (const bf16_t*)W, ldw, (const bf16_t*)S, lds, group, sgs, alpha, C, ldc_m, ldc_c, rpb);
+  const dim3 grid((unsigned)blocks), blk((unsigned)(RG * ncol8));
+#define TTMI_SKINNY_LAUNCH(TS_, U_)                                                              \
+  hipLaunchKernelGGL((skinny_wgrad_kernel<TS_, U_>), grid, blk, shm, s, R, Mw, (const bf16_t*)W, ldw, \
+                     (const TS_*)S, lds, group, sgs, alpha, C, ldc_m, ldc_c, rpb)
+  if (s_f32) {
+    if (cfg.u == 4) TTMI_SKINNY_LAUNCH(float, 4); else TTMI_SKINNY_LAUNCH(float, 8);
+  } else {
+    if (cfg.u == 4) TTMI_SKINNY_LAUNCH(bf16_t, 4); else TTMI_SKINNY_LAUNCH(bf16_t, 8);
+  }
+#undef TTMI_SKINNY_LAUNCH
   return ttmi_check_launch("ttmi_skinny_wgrad");
 }
 
