@@ -77,6 +77,11 @@ typedef struct {
   int split_k;
   const int32_t* drop_rows;
   float* rowsum_a;
+  void* pre_out;      /* ABI 8; may be NULL.  With act 2 (GELU), bf16 C, c_mode 0 and no
+                         dropout / gate / residual / colsum / split: pre_out[m*ldc+n] = the
+                         pre-activation (after bias), bf16 — DebertaV2Intermediate's dense output
+                         kept for the GELU' of the backward, written by the same epilogue that
+                         writes C = GELU(pre) (item_tower.py:41-83, modeling_deberta_v2). */
 } ttmi_gemm_desc;
 int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream);
 

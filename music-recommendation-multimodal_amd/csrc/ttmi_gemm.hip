@@ -45,6 +45,7 @@ struct GemmArgs {
   int64_t k_split;   // K elements per split (multiple of the K tile)
   int vec;           // 1: all row strides allow 4-wide vector epilogue accesses
   float* rowsum_a;   // rowsum_a[m] += Σ_k A(m,k)  (bias grad of a weight-gradient GEMM)
+  bf16_t* pre_out;   // act 2: the pre-activation (after bias) is also stored here (row stride ldc)
 };
 
 // Sum of the 8 bf16 / 4 f32 operand values a lane holds in one fragment.
@@ -245,8 +246,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       const int64_t drow = g.drop_rows ? (int64_t)g.drop_rows[m] : m;
       float v[4];
 #pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][e] + bias[e];
+      if (g.pre_out) {
+        const int64_t o = m * g.ldc + n;
+        if (full) {
+          ushort4 q;
+          q.x = f2bf(v[0]); q.y = f2bf(v[1]); q.z = f2bf(v[2]); q.w = f2bf(v[3]);
+          *reinterpret_cast<ushort4*>(g.pre_out + o) = q;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) if (n + e < g.N) g.pre_out[o + e] = f2bf(v[e]);
+        }
+      }
+#pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = g.alpha * acc[i][j][e] + bias[e];
         if (g.act == 1) v[e] = fmaxf(v[e], 0.f);
         if (g.act == 2) v[e] = gelu_erf(v[e]);
       }
@@ -1009,7 +1022,7 @@ TTMI_DEV uint4 big_frag_b(const char* img, int row, int c, int lane) {
 // straight-line epilogue stays small; EPI_ANY reads every flag at run time.
 enum BigEpi {
   BE_BIAS = 1, BE_RELU = 2, BE_GELU = 4, BE_DROP = 8, BE_GELU_GRAD = 16, BE_RELU_GATE = 32,
-  BE_RES = 64, BE_F32 = 128, BE_ACC = 256, BE_ANY = -1
+  BE_RES = 64, BE_F32 = 128, BE_ACC = 256, BE_PRE = 512, BE_ANY = -1
 };
 
 template <int EPI>
@@ -1024,6 +1037,7 @@ TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t
   const bool res = RT ? g.residual != nullptr : (EPI & BE_RES);
   const bool f32 = RT ? g.c_f32 != 0 : (EPI & BE_F32);
   const bool accum = RT ? g.c_mode == 1 : (EPI & BE_ACC);
+  const bool pre = RT ? g.pre_out != nullptr : (EPI & BE_PRE);
   const bool full = n + 7 < g.N;
   if (bias) {
     if (full) {
@@ -1034,6 +1048,15 @@ TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += (n + e < g.N) ? g.bias[n + e] : 0.f;
+    }
+  }
+  if (pre) {                                   // pre-activation copy (bf16, C's row stride)
+    const int64_t o = m * g.ldc + n;
+    if (full) {
+      *reinterpret_cast<uint4*>(g.pre_out + o) = pack8(v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) if (n + e < g.N) g.pre_out[o + e] = f2bf(v[e]);
     }
   }
   if (relu) {
@@ -1270,6 +1293,7 @@ int big_epi_code(const ttmi_gemm_desc* d) {
   if (d->residual) e |= BE_RES;
   if (d->c_dtype == TTMI_F32) e |= BE_F32;
   if (d->c_mode == 1) e |= BE_ACC;
+  if (d->pre_out) e |= BE_PRE;
   return e;
 }
 
@@ -1290,6 +1314,8 @@ int launch_big(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
     case BE_BIAS | BE_RES | BE_F32:
       hipLaunchKernelGGL((gemm_big_kernel<BE_BIAS | BE_RES | BE_F32>), grid, blk, 0, s, ba); break;
     case BE_GELU_GRAD: hipLaunchKernelGGL(gemm_big_kernel<BE_GELU_GRAD>, grid, blk, 0, s, ba); break;
+    case BE_BIAS | BE_GELU | BE_PRE:
+      hipLaunchKernelGGL((gemm_big_kernel<BE_BIAS | BE_GELU | BE_PRE>), grid, blk, 0, s, ba); break;
     default: hipLaunchKernelGGL(gemm_big_kernel<BE_ANY>, grid, blk, 0, s, ba); break;
   }
   return ttmi_check_launch("ttmi_gemm");
@@ -1381,6 +1407,11 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   TTMI_REQUIRE(d->drop_p == 0.f || d->drop_seed, "ttmi_gemm: dropout needs a seed pointer");
   TTMI_REQUIRE(!d->gate || d->ld_gate >= d->N, "ttmi_gemm: ld_gate < N");
   TTMI_REQUIRE(!d->residual || d->ld_res >= d->N, "ttmi_gemm: ld_res < N");
+  TTMI_REQUIRE(!d->pre_out || (d->act == 2 && d->c_mode == 0 && d->c_dtype == TTMI_BF16 &&
+                               d->drop_p == 0.f && !d->gate && !d->residual && !d->colsum &&
+                               d->split_k <= 1 && ((uintptr_t)d->pre_out & 15) == 0),
+               "ttmi_gemm: pre_out needs act 2, a bf16 C written once, no dropout/gate/residual/"
+               "colsum/split, 16-byte alignment");
 
   if (wgrad_applies(d)) return launch_wgrad(d, stream);
 
@@ -1435,6 +1466,7 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   a.colsum = d->colsum;
   a.k_split = kspl;
   a.rowsum_a = d->rowsum_a;
+  a.pre_out = static_cast<bf16_t*>(d->pre_out);
   const int cbytes = a.c_f32 ? 4 : 2;
   a.vec = (d->ldc % 4 == 0) && ((uintptr_t)d->C % (4 * cbytes) == 0) &&
           (!d->residual || (d->ld_res % 4 == 0 && (uintptr_t)d->residual % 16 == 0)) &&

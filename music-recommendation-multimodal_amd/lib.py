@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -38,6 +38,7 @@ class GemmDesc(ctypes.Structure):
         ("split_k", c_i),
         ("drop_rows", c_p),
         ("rowsum_a", c_p),
+        ("pre_out", c_p),
     ]
 
 

@@ -51,8 +51,12 @@ def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a
          gate: Optional[Tensor] = None, ld_gate: int = 0, gate_scale: float = 1.0,
          residual: Optional[Tensor] = None, ld_res: int = 0, colsum: Optional[Tensor] = None,
          split_k: int = 1, drop_rows: Optional[Tensor] = None,
-         rowsum_a: Optional[Tensor] = None) -> Tensor:
+         rowsum_a: Optional[Tensor] = None, pre_out: Optional[Tensor] = None) -> Tensor:
+    """C = epi(alpha · A·Bᵀ) (include/ttmi.h ttmi_gemm).  pre_out (bf16, with act 2): also
+    store the pre-activation there, same row stride as C."""
     _dev(A, B, C)
+    if pre_out is not None and (pre_out.dtype != torch.bfloat16 or pre_out.device != C.device):
+        raise TypeError("gemm: pre_out must be a bf16 tensor on C's device")
     if A.dtype != B.dtype:
         raise TypeError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
     d = GemmDesc()
@@ -72,6 +76,7 @@ def gemm(A: Tensor, B: Tensor, C: Tensor, M: int, N: int, K: int, *, lda: int, a
     d.split_k = split_k
     d.drop_rows = _p(drop_rows)
     d.rowsum_a = _p(rowsum_a)
+    d.pre_out = _p(pre_out)
     call("ttmi_gemm", ctypes.byref(d), _s())
     return C
 

@@ -11,7 +11,7 @@ and Linear(768,512) -> ReLU -> Dropout(0.1) -> Linear(512, D), on libttmi kernel
 * relative positions: ``posQ|posK = [rel | s·drop(rel)·A_qᵀ | 0] · W_aug[q,k]ᵀ`` per layer
   (share_att_key: query_proj's LoRA applies to posQ too);
 * attention: ``ttmi_dis_attn_fwd/bwd`` (fused c2c + c2p + p2c, online softmax);
-* post-LayerNorms: ``ttmi_deb_ln_fwd`` / ``ttmi_layernorm_bwd``; GELU: ``ttmi_deb_gelu`` and the
+* post-LayerNorms: ``ttmi_deb_ln_fwd`` / ``ttmi_layernorm_bwd``; GELU: the intermediate GEMM's epilogue (``pre_out``) and the
   GEMM's GELU' epilogue; mean-pool: ``ttmi_deb_pool_fwd/bwd``.
 
 Parameter names are the peft-wrapped reference's (``transformer.base_model.model.encoder.
@@ -353,9 +353,11 @@ def text_fwd(enc: "TextEncoder", P: Dict[str, Tensor], ids: Tensor, mask: Tensor
         m1, r1 = torch.empty(M, device=dev), torch.empty(M, device=dev)
         ops.deb_ln_fwd(z1, Fz.base[L + "attention.output.LayerNorm.weight"],
                        Fz.base[L + "attention.output.LayerNorm.bias"], c.eps, a32, a16, m1, r1)
+        # intermediate.dense + GELU in one epilogue: hh = GELU(pre), pre kept for GELU'
         pre = torch.empty(M, I, device=dev, dtype=bf)
-        _mm(a16, W["w1"], pre, M, I, H, lda=H, ldb=H, ldc=I, bias=Fz.base[L + "intermediate.dense.bias"])
-        hh = ops.deb_gelu(pre, torch.empty_like(pre))
+        hh = torch.empty(M, I, device=dev, dtype=bf)
+        _mm(a16, W["w1"], hh, M, I, H, lda=H, ldb=H, ldc=I, bias=Fz.base[L + "intermediate.dense.bias"],
+            act=2, pre_out=pre)
         z2 = torch.empty(M, H, device=dev)
         _mm(hh, W["w2"], z2, M, H, I, lda=I, ldb=I, ldc=H, bias=Fz.base[L + "output.dense.bias"],
             drop=_drop(pd, seeds, tsite(l, 2)), ld_drop=H, residual=a32, ld_res=H)

@@ -161,6 +161,31 @@ def test_gemm_big_tile(gpu_pkg, M, N, K, epi):
     assert torch.isfinite(C.float()).all()
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 3072, 768), (8192, 1000, 192), (300, 200, 64)])
+def test_gemm_gelu_pre_out(gpu_pkg, M, N, K):
+    """act 2 with pre_out (DebertaV2Intermediate: dense + GELU, the pre-activation kept for the
+    backward): C = GELU(pre) and pre_out = pre, on the 256x256 tile kernel (first two shapes)
+    and the generic one (last); bf16 outputs against fp32 torch."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(torch.bfloat16).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    pre_ref = A.float() @ W.float().t() + bias
+    act_ref = torch.nn.functional.gelu(pre_ref)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(A, W, C, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True, ldc=N, bias=bias, act=2,
+             pre_out=pre)
+    assert rel(pre.float(), pre_ref) < 8e-3
+    assert rel(C.float(), act_ref) < 8e-3
+    # the stored pre-activation is what the epilogue activated
+    assert rel(C.float(), torch.nn.functional.gelu(pre.float())) < 8e-3
+    with pytest.raises(RuntimeError):
+        ops.gemm(A, W, C, M, N, K, lda=K, a_kmajor=True, ldb=K, b_kmajor=True, ldc=N, bias=bias,
+                 act=0, pre_out=pre)
+
+
 @pytest.mark.parametrize("s_dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("R,Mw,group,trans", [(65536, 768, 768, False), (3000, 768, 64, False),
                                               (4099, 256, 256, True), (777, 64, 64, True)])
