@@ -53,7 +53,7 @@ TTMI_DEV void hist_add(uint32_t* hist, bool take, uint32_t bin) {
   const uint64_t act = __ballot(take);
   if (!act) return;
   const int leader = __ffsll((unsigned long long)act) - 1;
-  const uint32_t lb = __shfl(bin, leader, 64);
+  const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)bin, leader);   // leader is uniform
   const uint64_t same = __ballot(take && bin == lb);
   if (lane == leader) atomicAdd(&hist[lb], (uint32_t)__popcll(same));
   if (take && bin != lb) atomicAdd(&hist[bin], 1u);
