@@ -915,8 +915,13 @@ int launch_wgrad_t(const ttmi_gemm_desc* d, int remap, hipStream_t stream) {
   const int64_t stages = (d->K + 63) / 64;
   int S = d->split_k;
   if (S <= 0) {                              // ~320 workgroups, splits a multiple of 8
-    S = (320 / T + 4) & ~7;
-    if (S < 8) S = std::max(1, 320 / T);
+    static const int target = [] {           // TTMI_WGRAD_WG: tuning runs only
+      const char* e = getenv("TTMI_WGRAD_WG");
+      const int v = e ? atoi(e) : 0;
+      return v > 0 ? v : 320;
+    }();
+    S = (target / T + 4) & ~7;
+    if (S < 8) S = std::max(1, target / T);
   }
   S = (int)std::max<int64_t>(1, std::min<int64_t>(S, stages));
   int64_t sps = (stages + S - 1) / S;        // stages per split
