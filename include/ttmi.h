@@ -199,6 +199,12 @@ int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat, const
                      const float* logits, const float* lse, const int64_t* user_idx,
                      float inv_tau, const float* dloss, float* du, float* di, void* ws,
                      hipStream_t stream);
+/* As ttmi_infonce_bwd, plus du16 (may be NULL): a bf16 copy of du [B,D] written by the same
+ * kernel (the user tower's fusion-MLP backward consumes du as a bf16 GEMM operand).  ABI 9. */
+int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float* i_hat, const float* norms,
+                       const float* logits, const float* lse, const int64_t* user_idx,
+                       float inv_tau, const float* dloss, float* du, float* di, uint16_t* du16,
+                       void* ws, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Global in-batch negatives (BASELINE cfg 5; the reference InfoNCE two_tower.py:98-140

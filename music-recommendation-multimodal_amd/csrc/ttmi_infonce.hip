@@ -506,7 +506,8 @@ __global__ __launch_bounds__(256) void nce_bwd_finish_kernel(int B, int D, const
                                                              const float* __restrict__ norms,
                                                              const float* __restrict__ part,
                                                              float inv_tau, float* __restrict__ du,
-                                                             float* __restrict__ di) {
+                                                             float* __restrict__ di,
+                                                             bf16_t* __restrict__ du16) {
   const int lane = threadIdx.x & 63;
   const int row = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (row >= 2 * B) return;
@@ -533,7 +534,11 @@ __global__ __launch_bounds__(256) void nce_bwd_finish_kernel(int B, int D, const
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = lane + 64 * q;
-    if (c < D) dx[c] = nrm > NORM_EPS ? (dy[q] - y[c] * sdot) / nrm : dy[q] / NORM_EPS;
+    if (c < D) {
+      const float g = nrm > NORM_EPS ? (dy[q] - y[c] * sdot) / nrm : dy[q] / NORM_EPS;
+      dx[c] = g;
+      if (isu && du16) du16[(int64_t)r * D + c] = f2bf(g);   // the user tower's bf16 operand
+    }
   }
 }
 
@@ -616,10 +621,23 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
   return ttmi_check_launch("ttmi_infonce_fwd/loss");
 }
 
+extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float* i_hat,
+                                  const float* norms, const float* logits, const float* lse,
+                                  const int64_t* user_idx, float inv_tau, const float* dloss,
+                                  float* du, float* di, uint16_t* du16, void* ws, hipStream_t s);
+
 extern "C" int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat,
                                 const float* norms, const float* logits, const float* lse,
                                 const int64_t* user_idx, float inv_tau, const float* dloss,
                                 float* du, float* di, void* ws, hipStream_t s) {
+  return ttmi_infonce_bwd16(B, D, u_hat, i_hat, norms, logits, lse, user_idx, inv_tau, dloss, du, di,
+                            nullptr, ws, s);
+}
+
+extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float* i_hat,
+                                  const float* norms, const float* logits, const float* lse,
+                                  const int64_t* user_idx, float inv_tau, const float* dloss,
+                                  float* du, float* di, uint16_t* du16, void* ws, hipStream_t s) {
   TTMI_REQUIRE(B > 0 && D > 0 && D <= 4096 && D % 4 == 0 && B % 4 == 0,
                "ttmi_infonce_bwd: need B %% 4 == 0, D %% 4 == 0, D <= 4096");
   TTMI_REQUIRE(u_hat && i_hat && norms && logits && lse && du && di && ws,
@@ -638,7 +656,7 @@ extern "C" int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i
     int rc = ttmi_check_launch("ttmi_infonce_bwd/rows");
     if (rc) return rc;
     hipLaunchKernelGGL(nce_bwd_finish_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u_hat, i_hat,
-                       norms, part, inv_tau, du, di);
+                       norms, part, inv_tau, du, di, (bf16_t*)du16);
     return ttmi_check_launch("ttmi_infonce_bwd/finish");
   }
   Ws w = carve(ws, B, D);
@@ -656,7 +674,9 @@ extern "C" int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i
   if (rc) return rc;
   hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u_hat, i_hat,
                      norms, w.duh, w.dih, du, di);
-  return ttmi_check_launch("ttmi_infonce_bwd/l2norm_bwd");
+  rc = ttmi_check_launch("ttmi_infonce_bwd/l2norm_bwd");
+  if (rc || !du16) return rc;
+  return ttmi_cast_f32_bf16((int64_t)B * D, du, du16, s);
 }
 
 // ------------------------------------------------------------ building blocks (cfg 5)

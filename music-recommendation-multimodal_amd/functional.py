@@ -271,8 +271,9 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
 
 
 def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du: Tensor,
-                   grads: Dict[str, Tensor], cfg: TowerCfg) -> None:
-    """Backward of user_tower_fwd; accumulates into ``grads`` (fp32, reference names)."""
+                   grads: Dict[str, Tensor], cfg: TowerCfg, du16: Optional[Tensor] = None) -> None:
+    """Backward of user_tower_fwd; accumulates into ``grads`` (fp32, reference names).  du16:
+    du already in the compute dtype (InfoNCE backward's bf16 copy), saving the cast launch."""
     dev = du.device
     B, L = st.ids.shape
     D, H, dt = cfg.D, cfg.H, cfg.dtype
@@ -280,8 +281,11 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
     seeds = st.seeds
     f32 = dict(device=dev, dtype=torch.float32)
     # ---- user fusion MLP (user_tower.py:51-57, :142)
-    du_c = torch.empty(B, D, device=dev, dtype=dt)
-    ops.dropout_bwd(du, du_c, None)
+    if du16 is not None and du16.dtype == dt:
+        du_c = du16
+    else:
+        du_c = torch.empty(B, D, device=dev, dtype=dt)
+        ops.dropout_bwd(du, du_c, None)
     ops.linear_dw(du_c, st.az, grads["fusion_layer.3.weight"], grads["fusion_layer.3.bias"])
     daz = torch.empty(B, D, **f32)
     ops.linear_dx(du_c, W["fusion_layer.3.weight"], daz)
@@ -496,9 +500,10 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: 
                                                  inv_tau)
 
 
-def infonce_bwd(st: LossSaved, dloss: Optional[Tensor], du: Tensor, di: Tensor) -> None:
+def infonce_bwd(st: LossSaved, dloss: Optional[Tensor], du: Tensor, di: Tensor,
+                du16: Optional[Tensor] = None) -> None:
     ops.infonce_bwd(st.u_hat, st.i_hat, st.norms, st.logits, st.lse, st.user_idx, st.inv_tau,
-                    dloss, du, di, st.ws)
+                    dloss, du, di, st.ws, du16)
 
 
 def count_flops_user(B: int, L: int, D: int, n_layers: int, ffn: int, extra: int = 48) -> float:

@@ -469,10 +469,13 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], inv_tau: floa
 
 def infonce_bwd(u_hat: Tensor, i_hat: Tensor, norms: Tensor, logits: Tensor, lse: Tensor,
                 user_idx: Optional[Tensor], inv_tau: float, dloss: Optional[Tensor], du: Tensor,
-                di: Tensor, ws: Tensor):
+                di: Tensor, ws: Tensor, du16: Optional[Tensor] = None):
+    """du16 (bf16 [B, D], optional): a bf16 copy of du from the same launch."""
     B, D = u_hat.shape
-    call("ttmi_infonce_bwd", B, D, _p(u_hat), _p(i_hat), _p(norms), _p(logits), _p(lse),
-         _p(user_idx), inv_tau, _p(dloss), _p(du), _p(di), _p(ws), _s())
+    if du16 is not None and (du16.dtype != torch.bfloat16 or du16.shape != du.shape):
+        raise ValueError("infonce_bwd: du16 must be bf16 shaped like du")
+    call("ttmi_infonce_bwd16", B, D, _p(u_hat), _p(i_hat), _p(norms), _p(logits), _p(lse),
+         _p(user_idx), inv_tau, _p(dloss), _p(du), _p(di), _p(du16), _p(ws), _s())
 
 
 # ----------------------------------------------------------------------------- misc

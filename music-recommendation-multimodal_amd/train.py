@@ -249,12 +249,14 @@ class TrainStep:
                                                 self.model.temperature)
         du = torch.empty_like(u)
         di = torch.empty_like(it)
-        F.infonce_bwd(lst, self.dloss, du, di)
+        du16 = torch.empty(u.shape, device=u.device, dtype=self.ucfg.dtype) \
+            if self.ucfg.dtype == torch.bfloat16 else None
+        F.infonce_bwd(lst, self.dloss, du, di, du16)
         dmodal = torch.empty(modal.shape, device=modal.device) if self.raw_items else None
         F.item_fusion_bwd(self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item, dmodal)
         if self.raw_items:
             self._raw_items_bwd(rst, dmodal)
-        F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg)
+        F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg, du16)
         self.loss, self.logits = loss, logits
 
     def _raw_items_fwd(self, b: Dict[str, Tensor], seeds: Optional[Tensor]):
