@@ -564,10 +564,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU pairs (default: 512 for cfg 2, 256 for cfg 3)")
-    ap.add_argument("--config", default="2", choices=("2", "3", "4", "eval", "prep"),
+    ap.add_argument("--config", default="2", choices=("2", "3", "4", "5", "eval", "prep"),
                     help="2 = BASELINE cfg 2 (the metric's configuration); 3 = full item "
                          "tower on raw mels/covers/tabular (BASELINE configs[2]); 4 = cfg 3 + "
-                         "mDeBERTa-LoRA lyrics, S=256 (BASELINE configs[3]); eval = global "
+                         "mDeBERTa-LoRA lyrics, S=256 (BASELINE configs[3]); 5 = cfg 2 with "
+                         "global in-batch negatives (all-gather of every rank's embeddings, "
+                         "BASELINE configs[4]); eval = global "
                          "retrieval evaluation over the catalogue (SURVEY 8f rank 2)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
@@ -588,6 +590,7 @@ def main():
     if args.config == "prep":
         return main_prep(args, world, rank, device)
     cfg4 = args.config == "4"
+    cfg5 = args.config == "5"
     cfg3 = args.config == "3" or cfg4                    # cfg 4 = cfg 3 + text
     B = args.batch or (256 if cfg3 else 512)
 
@@ -596,7 +599,8 @@ def main():
                               num_countries=N_COUNTRIES, max_seq_len=L, user_embedding_dim=D,
                               item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
                               compute_dtype=torch.bfloat16,
-                              precomputed_modalities=not cfg3, with_text=cfg4).to(device)
+                              precomputed_modalities=not cfg3, with_text=cfg4,
+                              global_negatives=cfg5).to(device)
     if world > 1:   # identical replicas, as DDP broadcasts from rank 0
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, 0)
@@ -653,11 +657,16 @@ def main():
         value = pairs / el
         ms = el / max(args.steps, 1) * 1e3
         flops = step_flops(B) + (RESNET_FLOPS_PER_SAMPLE * B if cfg3 else 0.0) + \
-            ((TEXT_FLOPS_PER_SAMPLE * B + TEXT_FLOPS_PER_BATCH) if cfg4 else 0.0)
+            ((TEXT_FLOPS_PER_SAMPLE * B + TEXT_FLOPS_PER_BATCH) if cfg4 else 0.0) + \
+            (2.0 * world * B * D * 3 * B if cfg5 else 0.0)     # +2·C·D·3 per pair
         step_tf = flops * args.steps / el / 1e12 * world
         workload = ("cfg2: SASRec L=50 D=128 H=4 x2 layers + late-fusion head on "
                     "precomputed 512-d modality embeddings + in-batch InfoNCE; "
                     "fwd+bwd+AdamW, dropout 0.1")
+        if cfg5:
+            workload = (f"cfg5: cfg2 with global in-batch negatives: all-gather of u_hat, i_hat, "
+                        f"user_idx over {world} rank(s), {world * B} negatives per row, "
+                        f"reduce-scatter of the key gradients; fwd+bwd+AdamW, dropout 0.1")
         if cfg4:
             workload = ("cfg4: cfg3 item tower + mDeBERTa-v3-base (12 layers, H=768, random init) "
                         "with LoRA r=8 on query/value, lyrics S=256 (lengths U[16,256]); "

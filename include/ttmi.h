@@ -189,6 +189,8 @@ int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, const float* z,
  *   loss = ½(CE(S, arange) + CE(Sᵀ, arange)) with mean reduction.
  * Outputs: û, î [B,D]; norms [2B]; logits [B,B] (masked, as the reference returns them);
  * lse [2B] (row LSEs then column LSEs); loss [1].  ws: ttmi_infonce_workspace(B, D) bytes.
+ * Any B >= 1 when D % 64 == 0 and D <= 256 (the fused kernels; a ragged last batch of the
+ * reference DataLoader, train.py:259-266, has no drop_last); otherwise B % 4 == 0.  ABI 10.
  * ---------------------------------------------------------------------------------- */
 int64_t ttmi_infonce_workspace(int B, int D);
 int ttmi_infonce_fwd(int B, int D, const float* u, const float* it, const int64_t* user_idx,

@@ -281,7 +281,7 @@ TTMI_DEV void online_merge(float& m, float& s, float m2, float s2) {
   m = M;
 }
 
-template <int DC>
+template <int DC, bool VEC>
 __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __restrict__ uh,
                                                       const float* __restrict__ ih,
                                                       const int64_t* __restrict__ uid,
@@ -336,8 +336,15 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
       o[r] = v;
       online_add(m, sum, v);
     }
-    if (dir == 0 && iok && 16 * t + 4 * lg < B)
-      *reinterpret_cast<float4*>(logits + (int64_t)i * B + 16 * t + 4 * lg) = make_float4(o[0], o[1], o[2], o[3]);
+    if (dir == 0 && iok && 16 * t + 4 * lg < B) {
+      if constexpr (VEC) {
+        *reinterpret_cast<float4*>(logits + (int64_t)i * B + 16 * t + 4 * lg) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {   // ragged B (row pitch not 16-byte aligned): element stores inside the row
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * t + 4 * lg + r < B) logits[(int64_t)i * B + 16 * t + 4 * lg + r] = o[r];
+      }
+    }
   }
   // merge the 4 lane groups holding row li, then the 4 waves
 #pragma unroll
@@ -398,7 +405,20 @@ __global__ __launch_bounds__(1024) void nce_combine_kernel(int B, const float* _
 // d-tiles' MFMAs D[d][row] = Σ_k Vᵀ[d][k] G[row][k] from LDS; partial rows go to part.
 constexpr int NKB = 64;   // keys per staged block
 
-template <int DC>
+// Four consecutive floats p[k .. k+3] of a row of n: one 16-byte load when the row pitch keeps
+// it aligned (VEC, n % 4 == 0, k clamped to n - 4), else element loads clamped to n - 1.
+template <bool VEC>
+TTMI_DEV void load4(const float* __restrict__ p, int k, int n, float (&v)[4]) {
+  if constexpr (VEC) {
+    const float4 q = *reinterpret_cast<const float4*>(p + min(k, n - 4));
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = p[min(k + e, n - 1)];
+  }
+}
+
+template <int DC, bool VEC>
 __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __restrict__ uh,
                                                       const float* __restrict__ ih,
                                                       const float* __restrict__ S,
@@ -439,10 +459,10 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
     if (dir == 0) {      // thread -> row tid/16, keys 4·(tid%16) .. +3 (one float4 of S's row)
       const int r = tid >> 4, kq = (tid & 15) * 4;
       const int row = r0 + r, k = k0 + kq;
-      const float4 sv = *reinterpret_cast<const float4*>(S + (int64_t)min(row, B - 1) * B + min(k, B - 4));
-      const float4 lk = *reinterpret_cast<const float4*>(lse_k + min(k, B - 4));
+      float svv[4], lkv[4];
+      load4<VEC>(S + (int64_t)min(row, B - 1) * B, k, B, svv);
+      load4<VEC>(lse_k, k, B, lkv);
       const float lq = lse_q[min(row, B - 1)];
-      const float svv[4] = {sv.x, sv.y, sv.z, sv.w}, lkv[4] = {lk.x, lk.y, lk.z, lk.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         gr[e] = r;
@@ -453,10 +473,10 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
     } else {             // thread -> key tid/4, rows 4·(tid%4) .. +3 (one float4 of S's row k)
       const int kk = tid >> 2, rq = (tid & 3) * 4;
       const int k = k0 + kk, row = r0 + rq;
-      const float4 sv = *reinterpret_cast<const float4*>(S + (int64_t)min(k, B - 1) * B + min(row, B - 4));
-      const float4 lq = *reinterpret_cast<const float4*>(lse_q + min(row, B - 4));
+      float svv[4], lqv[4];
+      load4<VEC>(S + (int64_t)min(k, B - 1) * B, row, B, svv);
+      load4<VEC>(lse_q, row, B, lqv);
       const float lk = lse_k[min(k, B - 1)];
-      const float svv[4] = {sv.x, sv.y, sv.z, sv.w}, lqv[4] = {lq.x, lq.y, lq.z, lq.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         gr[e] = rq + e;
@@ -585,8 +605,8 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
                                 const int64_t* user_idx, float inv_tau, float* u_hat,
                                 float* i_hat, float* norms, float* logits, float* lse, float* loss,
                                 void* ws, hipStream_t s) {
-  TTMI_REQUIRE(B > 0 && D > 0 && D <= 4096 && D % 4 == 0 && B % 4 == 0,
-               "ttmi_infonce_fwd: need B %% 4 == 0, D %% 4 == 0, D <= 4096");
+  TTMI_REQUIRE(B > 0 && D > 0 && D <= 4096 && D % 4 == 0 && (B % 4 == 0 || fused_ok(B, D)),
+               "ttmi_infonce_fwd: need D %% 4 == 0, D <= 4096, and B %% 4 == 0 unless D %% 64 == 0 and D <= 256");
   TTMI_REQUIRE(u && it && u_hat && i_hat && norms && logits && lse && loss && ws,
                "ttmi_infonce_fwd: null argument");
   hipLaunchKernelGGL(l2norm_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u, it, u_hat, i_hat,
@@ -597,12 +617,16 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
     float* part = static_cast<float*>(ws);
     const int nb = (B + NQ - 1) / NQ;
     const dim3 grid(2 * nb * NSPLIT);
+#define TTMI_NCE_FWD(DC, V) hipLaunchKernelGGL((nce_fwd_kernel<DC, V>), grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part)
+#define TTMI_NCE_FWD2(DC) do { if (B % 4 == 0) TTMI_NCE_FWD(DC, true); else TTMI_NCE_FWD(DC, false); } while (0)
     switch (D / 16) {
-      case 4: hipLaunchKernelGGL(nce_fwd_kernel<4>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
-      case 8: hipLaunchKernelGGL(nce_fwd_kernel<8>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
-      case 12: hipLaunchKernelGGL(nce_fwd_kernel<12>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
-      default: hipLaunchKernelGGL(nce_fwd_kernel<16>, grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part); break;
+      case 4: TTMI_NCE_FWD2(4); break;
+      case 8: TTMI_NCE_FWD2(8); break;
+      case 12: TTMI_NCE_FWD2(12); break;
+      default: TTMI_NCE_FWD2(16); break;
     }
+#undef TTMI_NCE_FWD2
+#undef TTMI_NCE_FWD
     rc = ttmi_check_launch("ttmi_infonce_fwd/rows");
     if (rc) return rc;
     hipLaunchKernelGGL(nce_combine_kernel, dim3(1), dim3(1024), 0, s, B, part, lse, loss);
@@ -638,8 +662,8 @@ extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float*
                                   const float* norms, const float* logits, const float* lse,
                                   const int64_t* user_idx, float inv_tau, const float* dloss,
                                   float* du, float* di, uint16_t* du16, void* ws, hipStream_t s) {
-  TTMI_REQUIRE(B > 0 && D > 0 && D <= 4096 && D % 4 == 0 && B % 4 == 0,
-               "ttmi_infonce_bwd: need B %% 4 == 0, D %% 4 == 0, D <= 4096");
+  TTMI_REQUIRE(B > 0 && D > 0 && D <= 4096 && D % 4 == 0 && (B % 4 == 0 || fused_ok(B, D)),
+               "ttmi_infonce_bwd: need D %% 4 == 0, D <= 4096, and B %% 4 == 0 unless D %% 64 == 0 and D <= 256");
   TTMI_REQUIRE(u_hat && i_hat && norms && logits && lse && du && di && ws,
                "ttmi_infonce_bwd: null argument");
   if (fused_ok(B, D)) {
@@ -647,12 +671,16 @@ extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float*
                                            ((int64_t)3 * NSPLIT * 2 * B * 4 + 255) / 256 * 256);
     const int nb = (B + NQ - 1) / NQ;
     const dim3 grid(2 * nb * NSPLIT);
+#define TTMI_NCE_BWD(DC, V) hipLaunchKernelGGL((nce_bwd_kernel<DC, V>), grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part)
+#define TTMI_NCE_BWD2(DC) do { if (B % 4 == 0) TTMI_NCE_BWD(DC, true); else TTMI_NCE_BWD(DC, false); } while (0)
     switch (D / 16) {
-      case 4: hipLaunchKernelGGL(nce_bwd_kernel<4>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
-      case 8: hipLaunchKernelGGL(nce_bwd_kernel<8>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
-      case 12: hipLaunchKernelGGL(nce_bwd_kernel<12>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
-      default: hipLaunchKernelGGL(nce_bwd_kernel<16>, grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part); break;
+      case 4: TTMI_NCE_BWD2(4); break;
+      case 8: TTMI_NCE_BWD2(8); break;
+      case 12: TTMI_NCE_BWD2(12); break;
+      default: TTMI_NCE_BWD2(16); break;
     }
+#undef TTMI_NCE_BWD2
+#undef TTMI_NCE_BWD
     int rc = ttmi_check_launch("ttmi_infonce_bwd/rows");
     if (rc) return rc;
     hipLaunchKernelGGL(nce_bwd_finish_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u_hat, i_hat,

@@ -13,11 +13,11 @@ mirror, or ``P`` itself in fp32 mode).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import torch
 
-from . import ops
+from . import comm, ops
 
 Tensor = torch.Tensor
 
@@ -271,9 +271,12 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
 
 
 def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du: Tensor,
-                   grads: Dict[str, Tensor], cfg: TowerCfg, du16: Optional[Tensor] = None) -> None:
+                   grads: Dict[str, Tensor], cfg: TowerCfg, du16: Optional[Tensor] = None,
+                   on_layer_done: Optional[Callable[[int], None]] = None) -> None:
     """Backward of user_tower_fwd; accumulates into ``grads`` (fp32, reference names).  du16:
-    du already in the compute dtype (InfoNCE backward's bf16 copy), saving the cast launch."""
+    du already in the compute dtype (InfoNCE backward's bf16 copy), saving the cast launch.
+    ``on_layer_done(i)`` is called once encoder layer i's parameter gradients are final (the
+    data-parallel step starts a bucket's all-reduce there)."""
     dev = du.device
     B, L = st.ids.shape
     D, H, dt = cfg.D, cfg.H, cfg.dtype
@@ -375,6 +378,8 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
                 ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
                                   grads[pre + "norm1.weight"], grads[pre + "norm1.bias"], res=dx1)
         dx = dxn
+        if on_layer_done is not None:
+            on_layer_done(i)
     # ---- input block (user_tower.py:83-93)
     ops.seq_embed_bwd(st.ids, P["item_embedding.weight"], P["position_embedding.weight"],
                       P["layer_norm.weight"], st.m0, st.r0, dx, grads["item_embedding.weight"],
@@ -527,11 +532,106 @@ class GlobalLossSaved:
     uid: Optional[Tensor]
     UID: Optional[Tensor]
     row0: int
-    s_u2i: Tensor
-    lse_u2i: Tensor
-    s_i2u: Tensor
-    lse_i2u: Tensor
+    world: int
     inv_tau: float
+    s_u2i: Optional[Tensor] = None
+    lse_u2i: Optional[Tensor] = None
+    s_i2u: Optional[Tensor] = None
+    lse_i2u: Optional[Tensor] = None
+    duh: Optional[Tensor] = None      # local-row grads [B, D]
+    dih: Optional[Tensor] = None
+    dU: Optional[Tensor] = None       # key grads for every rank's rows [W·B, D]
+    dI: Optional[Tensor] = None
+    rs_u: Optional[Tensor] = None     # this rank's share of the key grads (reduce-scattered)
+    rs_i: Optional[Tensor] = None
+
+
+def _world_rank(group, local: bool):
+    import torch.distributed as dist
+    if local or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def infonce_global_prep(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float,
+                        group=None, local: bool = False) -> GlobalLossSaved:
+    """Phase 1 of the cfg-5 loss: L2-normalise this rank's rows and size the gathered buffers
+    (no collective; TrainStep captures it in the forward graph)."""
+    world, rank = _world_rank(group, local)
+    B, D = u.shape
+    dev = u.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    u_hat, i_hat = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+    nu, ni = torch.empty(B, **f32), torch.empty(B, **f32)
+    ops.l2norm_fwd(u.contiguous().float(), u_hat, nu)
+    ops.l2norm_fwd(it.contiguous().float(), i_hat, ni)
+    uid = None
+    if user_idx is not None:
+        uid = user_idx if user_idx.dtype == torch.int64 else user_idx.to(torch.int64)
+        uid = uid.contiguous()
+    if world > 1:
+        U, I = torch.empty(world * B, D, **f32), torch.empty(world * B, D, **f32)
+        UID = torch.empty(world * B, device=dev, dtype=torch.int64) if uid is not None else None
+    else:
+        U, I, UID = u_hat, i_hat, uid
+    return GlobalLossSaved(u_hat, i_hat, nu, ni, U, I, uid, UID, rank * B, world,
+                           1.0 / temperature)
+
+
+def infonce_global_gather(st: GlobalLossSaved, group=None) -> None:
+    """Phase 2 (collective): all-gather û, î and user_idx over the group (RCCL)."""
+    if st.world == 1:
+        return
+    comm.all_gather_into(st.U, st.u_hat, group)
+    comm.all_gather_into(st.I, st.i_hat, group)
+    if st.UID is not None:
+        comm.all_gather_into(st.UID, st.uid, group)
+
+
+def infonce_global_loss(st: GlobalLossSaved) -> Tensor:
+    """Phase 3: this rank's u2i and i2u rows against every rank's keys; loss_r."""
+    B, D = st.u_hat.shape
+    C = st.world * B
+    f32 = dict(device=st.u_hat.device, dtype=torch.float32)
+    st.s_u2i, st.s_i2u = torch.empty(B, C, **f32), torch.empty(B, C, **f32)
+    st.lse_u2i, st.lse_i2u = torch.empty(B, **f32), torch.empty(B, **f32)
+    ce = torch.empty(2 * B, **f32)
+    ops.rowce_fwd(st.u_hat, st.I, st.uid, st.UID, st.row0, st.inv_tau, st.s_u2i, st.lse_u2i, ce[:B])
+    ops.rowce_fwd(st.i_hat, st.U, st.uid, st.UID, st.row0, st.inv_tau, st.s_i2u, st.lse_i2u, ce[B:])
+    loss = torch.empty(1, **f32)
+    ops.sum_scaled(ce, 0.5 / B, loss)
+    return loss.view(())
+
+
+def infonce_global_loss_bwd(st: GlobalLossSaved, dloss: Optional[Tensor]) -> None:
+    """Phase 4: local-row grads and key grads for every rank's rows."""
+    B, D = st.u_hat.shape
+    f32 = dict(device=st.u_hat.device, dtype=torch.float32)
+    scale = 0.5 / B
+    st.duh, st.dih = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+    st.dI, st.dU = torch.empty(st.world * B, D, **f32), torch.empty(st.world * B, D, **f32)
+    ops.rowce_bwd(st.u_hat, st.I, st.s_u2i, st.lse_u2i, st.uid, st.UID, st.row0, st.inv_tau,
+                  dloss, scale, st.duh, st.dI)
+    ops.rowce_bwd(st.i_hat, st.U, st.s_i2u, st.lse_i2u, st.uid, st.UID, st.row0, st.inv_tau,
+                  dloss, scale, st.dih, st.dU)
+    if st.world > 1:
+        st.rs_u, st.rs_i = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+    else:
+        st.rs_u, st.rs_i = st.dU, st.dI
+
+
+def infonce_global_scatter(st: GlobalLossSaved, group=None) -> None:
+    """Phase 5 (collective): reduce-scatter (SUM) of the key grads back to their owners."""
+    if st.world == 1:
+        return
+    comm.reduce_scatter_sum(st.rs_u, st.dU, group)
+    comm.reduce_scatter_sum(st.rs_i, st.dI, group)
+
+
+def infonce_global_norm_bwd(st: GlobalLossSaved, du: Tensor, di: Tensor) -> None:
+    """Phase 6: normalize backward of (local-row grad + owned key grad)."""
+    ops.l2norm_bwd(st.u_hat, st.nu, st.duh, du, dy2=st.rs_u)
+    ops.l2norm_bwd(st.i_hat, st.ni, st.dih, di, dy2=st.rs_i)
 
 
 def infonce_global_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float,
@@ -540,63 +640,16 @@ def infonce_global_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temper
     two_tower.py:98-140 applied to world·B rows).  Returns (loss_r, logits_u2i [B, W·B],
     û_r, î_r, saved); the global loss is the mean of loss_r over ranks, which DDP's 1/world
     gradient scaling realises.  All-gathers û, î and user_idx over `group` (RCCL)."""
-    import torch.distributed as dist
-    distributed = dist.is_initialized() and not local
-    world = dist.get_world_size(group) if distributed else 1
-    rank = dist.get_rank(group) if distributed else 0
-    B, D = u.shape
-    dev = u.device
-    f32 = dict(device=dev, dtype=torch.float32)
-    u_hat, i_hat = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
-    nu, ni = torch.empty(B, **f32), torch.empty(B, **f32)
-    ops.l2norm_fwd(u.contiguous().float(), u_hat, nu)
-    ops.l2norm_fwd(it.contiguous().float(), i_hat, ni)
-    if world > 1:
-        U, I = torch.empty(world * B, D, **f32), torch.empty(world * B, D, **f32)
-        dist.all_gather_into_tensor(U, u_hat, group=group)
-        dist.all_gather_into_tensor(I, i_hat, group=group)
-        UID = None
-        if user_idx is not None:
-            UID = torch.empty(world * B, device=dev, dtype=torch.int64)
-            dist.all_gather_into_tensor(UID, user_idx.contiguous(), group=group)
-    else:
-        U, I, UID = u_hat, i_hat, user_idx
-    uid = user_idx.contiguous() if user_idx is not None else None
-    row0 = rank * B
-    inv_tau = 1.0 / temperature
-    C = world * B
-    s_u2i, s_i2u = torch.empty(B, C, **f32), torch.empty(B, C, **f32)
-    lse_u2i, lse_i2u = torch.empty(B, **f32), torch.empty(B, **f32)
-    ce = torch.empty(2 * B, **f32)
-    ops.rowce_fwd(u_hat, I, uid, UID, row0, inv_tau, s_u2i, lse_u2i, ce[:B])
-    ops.rowce_fwd(i_hat, U, uid, UID, row0, inv_tau, s_i2u, lse_i2u, ce[B:])
-    loss = torch.empty(1, **f32)
-    ops.sum_scaled(ce, 0.5 / B, loss)
-    saved = GlobalLossSaved(u_hat, i_hat, nu, ni, U, I, uid, UID, row0, s_u2i, lse_u2i, s_i2u,
-                            lse_i2u, inv_tau)
-    return loss.view(()), s_u2i, u_hat, i_hat, saved
+    st = infonce_global_prep(u, it, user_idx, temperature, group, local)
+    infonce_global_gather(st, group)
+    loss = infonce_global_loss(st)
+    return loss, st.s_u2i, st.u_hat, st.i_hat, st
 
 
 def infonce_global_bwd(st: GlobalLossSaved, dloss: Optional[Tensor], du: Tensor, di: Tensor,
                        group=None, local: bool = False) -> None:
     """Backward of infonce_global_fwd for this rank's loss_r: local-row grads, key grads for
     every rank's rows reduce-scattered (SUM) back to their owners, then normalize backward."""
-    import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() and not local else 1
-    B, D = st.u_hat.shape
-    f32 = dict(device=st.u_hat.device, dtype=torch.float32)
-    scale = 0.5 / B
-    duh, dih = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
-    dI, dU = torch.empty(world * B, D, **f32), torch.empty(world * B, D, **f32)
-    ops.rowce_bwd(st.u_hat, st.I, st.s_u2i, st.lse_u2i, st.uid, st.UID, st.row0, st.inv_tau,
-                  dloss, scale, duh, dI)
-    ops.rowce_bwd(st.i_hat, st.U, st.s_i2u, st.lse_i2u, st.uid, st.UID, st.row0, st.inv_tau,
-                  dloss, scale, dih, dU)
-    if world > 1:
-        rs_u, rs_i = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
-        dist.reduce_scatter_tensor(rs_u, dU, group=group)
-        dist.reduce_scatter_tensor(rs_i, dI, group=group)
-    else:
-        rs_u, rs_i = dU, dI
-    ops.l2norm_bwd(st.u_hat, st.nu, duh, du, dy2=rs_u)
-    ops.l2norm_bwd(st.i_hat, st.ni, dih, di, dy2=rs_i)
+    infonce_global_loss_bwd(st, dloss)
+    infonce_global_scatter(st, group)
+    infonce_global_norm_bwd(st, du, di)

@@ -17,12 +17,13 @@ from __future__ import annotations
 
 import logging
 import os
-from typing import Dict, Optional
+from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
 from . import cnn
+from . import comm
 from . import functional as F
 from . import text as T
 from . import ops
@@ -78,23 +79,36 @@ class FlatParams:
 
     ``param.data`` is re-pointed at its slot, so the module and its state_dict keep
     working; ``grad``, ``exp_avg``, ``exp_avg_sq`` and (optionally) a bf16 ``mirror`` share
-    the same layout.  Device-agnostic (also used by the CPU/gloo tests)."""
+    the same layout.  ``tail`` lists name prefixes whose slots go last (in module order): the
+    parameters whose gradients the backward finishes last, so the all-reduce of everything
+    before ``tail_offset`` can start while they are still being computed.  Device-agnostic
+    (also used by the CPU/gloo tests)."""
 
     ALIGN = 64  # elements (256 B)
 
-    def __init__(self, module: torch.nn.Module, mirror_dtype: Optional[torch.dtype] = None):
+    def __init__(self, module: torch.nn.Module, mirror_dtype: Optional[torch.dtype] = None,
+                 tail: Sequence[str] = ()):
         self.names, self.shapes, self.offsets = [], [], []
         # trainable parameters only: frozen ones (the peft-frozen DeBERTa base) get neither
         # gradients nor AdamW updates (torch's AdamW skips params whose grad is None)
         params = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+        is_tail = [any(n.startswith(t) for t in tail) for n, _ in params]
+        params = [q for q, t in zip(params, is_tail) if not t] + \
+                 [q for q, t in zip(params, is_tail) if t]
+        n_head = len(params) - sum(is_tail)
         dev = params[0][1].device
         off = 0
-        for n, p in params:
+        self.tail_offset = None
+        for k, (n, p) in enumerate(params):
+            if k == n_head:
+                self.tail_offset = off
             self.names.append(n)
             self.shapes.append(tuple(p.shape))
             self.offsets.append(off)
             off += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         self.numel = off
+        if self.tail_offset is None:
+            self.tail_offset = off
         self.data = torch.zeros(off, device=dev, dtype=torch.float32)
         for (n, p), o in zip(params, self.offsets):
             self.data[o:o + p.numel()].copy_(p.detach().reshape(-1))
@@ -117,29 +131,125 @@ class FlatParams:
         return out
 
 
+class FlatBuffers:
+    """The module's floating-point buffers (BatchNorm running mean / var) re-homed into one
+    fp32 buffer, so DDP's ``broadcast_buffers`` (rank 0's buffers overwrite every rank's at
+    the start of each forward, reference train.py:300) is one collective.  Integer buffers
+    (``num_batches_tracked``) advance identically on every rank and are left in place."""
+
+    def __init__(self, module: torch.nn.Module):
+        bufs = [(n, b) for n, b in module.named_buffers() if b.is_floating_point()]
+        self.numel = sum(b.numel() for _, b in bufs)
+        self.data = None
+        if not bufs:
+            return
+        self.data = torch.empty(self.numel, device=bufs[0][1].device, dtype=torch.float32)
+        o = 0
+        for n, b in bufs:
+            k = b.numel()
+            self.data[o:o + k].copy_(b.detach().reshape(-1).float())
+            b.data = self.data[o:o + k].view(b.shape)
+            o += k
+
+
 class GradSync:
     """Data-parallel gradient averaging over the flat buffer (reference DDP, train.py:300).
 
     Each rank pre-scales its loss gradient by 1/world (``loss_scale``) so one SUM
     all-reduce of the flat buffer yields the average.  The buffer is reduced in
     ``bucket_bytes`` slices (RCCL rings run per-link bound on xGMI; 32 MiB buckets keep every
-    call well above the latency knee)."""
+    call well above the latency knee).  ``start`` launches a slice's reduction asynchronously
+    (RCCL runs it on its own stream, overlapping the rest of the backward)."""
 
     def __init__(self, group=None, bucket_bytes: int = 32 << 20):
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = comm.world_size(group)
         self.bucket = max(1, bucket_bytes // 4)
 
     @property
     def loss_scale(self) -> float:
         return 1.0 / self.world
 
-    def __call__(self, flat_grad: Tensor) -> None:
+    def start(self, flat_grad: Tensor) -> List:
         if self.world == 1:
-            return
+            return []
         n = flat_grad.numel()
-        for s in range(0, n, self.bucket):
-            dist.all_reduce(flat_grad[s:s + self.bucket], op=dist.ReduceOp.SUM, group=self.group)
+        return [comm.all_reduce_sum(flat_grad[s:s + self.bucket], self.group, async_op=True)
+                for s in range(0, n, self.bucket)]
+
+    def __call__(self, flat_grad: Tensor) -> None:
+        for w in self.start(flat_grad):
+            w.wait()
+
+
+class _Segments:
+    """A step recorded as HIP-graph segments separated by host actions (the collectives, which
+    run between graph replays on the same stream).  With no cut the step is one graph.  In
+    eager mode ``cut`` runs its action at once, so one code path serves both."""
+
+    def __init__(self, device, capture: bool, pool=None):
+        self.device = device
+        self.capture = capture
+        self.pool = pool
+        self.items: List = []           # ("graph", CUDAGraph) | ("host", fn)
+        self.cur = None
+        self.stream = None
+
+    def begin(self) -> None:
+        if self.capture:
+            self.stream = torch.cuda.Stream(self.device)
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            self._ctx = torch.cuda.stream(self.stream)
+            self._ctx.__enter__()
+            self._open()
+
+    def _open(self) -> None:
+        self.cur = torch.cuda.CUDAGraph()
+        self.cur.capture_begin(pool=self.pool)
+
+    def _close(self) -> None:
+        self.cur.capture_end()
+        self.items.append(("graph", self.cur))
+        self.cur = None
+
+    def cut(self, fn: Callable[[], None]) -> None:
+        if not self.capture:
+            fn()
+            return
+        self._close()
+        self.items.append(("host", fn))
+        self._open()
+
+    def end(self) -> None:
+        if self.capture:
+            self._close()
+            self._ctx.__exit__(None, None, None)
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def replay(self) -> None:
+        for kind, x in self.items:
+            if kind == "graph":
+                x.replay()
+            else:
+                x()
+
+    @property
+    def n_graphs(self) -> int:
+        return sum(1 for k, _ in self.items if k == "graph")
+
+
+def _no_cut(fn: Callable[[], None]) -> None:
+    fn()
+
+
+class _Entry:
+    """Per batch-signature state: static inputs, the recorded step and its outputs."""
+
+    def __init__(self, static: Dict[str, Tensor]):
+        self.static = static
+        self.seg: Optional[_Segments] = None
+        self.loss: Optional[Tensor] = None
+        self.logits: Optional[Tensor] = None
 
 
 # ------------------------------------------------------------------ the fused step
@@ -148,16 +258,31 @@ class TrainStep:
     inputs, or cfg-3 raw mels / covers / tabular with ``precomputed_modalities=False``).
 
     ``step(batch)`` stages the batch into static device buffers, replays the captured
-    forward+backward(+update) graph and returns the device loss tensor (no host sync)."""
+    forward+backward(+update) graph and returns the device loss tensor (no host sync).
+    A batch of a new shape (the reference DataLoader's ragged last batch, train.py:259-266)
+    gets its own static buffers and graph; later batches of a known shape reuse theirs.
+
+    Data-parallel (one process per GPU, RCCL): the gradient average is split in two buckets —
+    everything but the user tower's first encoder layer and input block is all-reduced
+    asynchronously while those are still being differentiated (DDP's bucketed overlap), the
+    rest after the backward; BatchNorm running buffers follow rank 0 at the start of every
+    step (DDP ``broadcast_buffers``).  With ``model.global_negatives`` (BASELINE cfg 5) the
+    loss all-gathers û, î, user_idx between the forward and loss graphs and reduce-scatters
+    the key gradients before the tower backward; ``loss`` is then this rank's share (the
+    mean over ranks is the loss of the concatenated batch)."""
 
     INPUT_KEYS = ("history_ids", "history_mask", "user_gender", "user_country", "user_idx",
                   "target_modal", "target_audio", "target_image", "target_tabular",
                   "target_input_ids", "target_attention_mask")
     RAW_ENCODERS = (("audio_encoder.backbone.", 1), ("visual_encoder.backbone.", 3))
+    # gradients finished last by the backward (user tower layer 0 + input block): bucket 2
+    LATE = ("user_tower.item_embedding.", "user_tower.position_embedding.",
+            "user_tower.layer_norm.", "user_tower.transformer_encoder.layers.0.")
 
     def __init__(self, model: TwoTowerModel, lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.01, use_graph: bool = True,
-                 seed: int = 0, group=None):
+                 seed: int = 0, group=None, broadcast_buffers: bool = True,
+                 overlap_grad_sync: bool = True):
         self.model = model
         model.train()
         dev = next(model.parameters()).device
@@ -166,9 +291,16 @@ class TrainStep:
         self.icfg = model.item_tower.cfg()
         self.p_item = model.item_tower.fusion_layer[3].p
         self.dtype = self.ucfg.dtype
-        self.flat = FlatParams(model, self.dtype)
+        self.group = group if group is not None else getattr(model, "process_group", None)
+        self.sync = GradSync(self.group)
+        self.world = self.sync.world
+        self.global_negatives = bool(getattr(model, "global_negatives", False))
+        self.overlap = overlap_grad_sync and self.world > 1 and self.ucfg.n_layers >= 2
+        self.flat = FlatParams(model, self.dtype, tail=self.LATE if self.overlap else ())
+        self.fbufs = FlatBuffers(model)
+        self.broadcast_buffers = broadcast_buffers and self.world > 1 and \
+            self.fbufs.data is not None
         ops.bump_param_epoch()                 # parameters now live in (and move with) the flat buffer
-        self.sync = GradSync(group)
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay],
                                   dtype=torch.float64, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -210,9 +342,9 @@ class TrainStep:
                 self.text_seeds = torch.zeros(T.N_TEXT_SITES, dtype=torch.int64, device=dev)
         self.sync_mirror()
         self.use_graph = use_graph
-        self.static: Optional[Dict[str, Tensor]] = None
-        self.graph_fb = None      # forward + backward (+ update when world == 1)
-        self.graph_up = None      # update (world > 1)
+        self._entries: Dict[tuple, _Entry] = {}
+        self._cur: Optional[_Entry] = None
+        self._pending: List = []               # in-flight async bucket reductions
         self.loss: Optional[Tensor] = None
         self.logits: Optional[Tensor] = None
 
@@ -223,7 +355,9 @@ class TrainStep:
         if self.flat.mirror is not None:
             ops.cast_bf16(self.flat.data, self.flat.mirror)
 
-    def _fwd_bwd(self, b: Dict[str, Tensor]) -> None:
+    def _fwd_bwd(self, b: Dict[str, Tensor], cut: Callable = _no_cut) -> None:
+        """Forward + backward into the flat gradient.  ``cut(fn)`` marks a point where a
+        collective ``fn`` runs between graph segments (see _Segments)."""
         # the gradient buffer is zero here: it starts zeroed and the fused AdamW clears it
         seeds = None
         draw = self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0)
@@ -245,19 +379,50 @@ class TrainStep:
             modal = b["target_modal"]
         it, ist = F.item_fusion_fwd(self.Pi, self.Wi, modal, self.icfg, seeds,
                                     self.bufs, self.p_item)
-        loss, logits, _, _, lst = F.infonce_fwd(u, it, b.get("user_idx"),
-                                                self.model.temperature)
         du = torch.empty_like(u)
         di = torch.empty_like(it)
-        du16 = torch.empty(u.shape, device=u.device, dtype=self.ucfg.dtype) \
-            if self.ucfg.dtype == torch.bfloat16 else None
-        F.infonce_bwd(lst, self.dloss, du, di, du16)
+        du16 = None
+        if self.global_negatives:         # cfg 5: negatives from every rank's batch
+            gst = F.infonce_global_prep(u, it, b.get("user_idx"), self.model.temperature,
+                                        self.group)
+            if gst.world > 1:
+                cut(lambda: F.infonce_global_gather(gst, self.group))
+            loss = F.infonce_global_loss(gst)
+            logits = gst.s_u2i
+            F.infonce_global_loss_bwd(gst, self.dloss)
+            if gst.world > 1:
+                cut(lambda: F.infonce_global_scatter(gst, self.group))
+            F.infonce_global_norm_bwd(gst, du, di)
+        else:
+            loss, logits, _, _, lst = F.infonce_fwd(u, it, b.get("user_idx"),
+                                                    self.model.temperature)
+            du16 = torch.empty(u.shape, device=u.device, dtype=self.ucfg.dtype) \
+                if self.ucfg.dtype == torch.bfloat16 else None
+            F.infonce_bwd(lst, self.dloss, du, di, du16)
         dmodal = torch.empty(modal.shape, device=modal.device) if self.raw_items else None
         F.item_fusion_bwd(self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item, dmodal)
         if self.raw_items:
             self._raw_items_bwd(rst, dmodal)
-        F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg, du16)
+        hook = None
+        if self.overlap:
+            def hook(i: int) -> None:
+                if i == 1:       # every gradient before the tail slots is final
+                    cut(self._sync_head)
+        F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg, du16, on_layer_done=hook)
         self.loss, self.logits = loss, logits
+
+    def _sync_head(self) -> None:
+        self._pending = self.sync.start(self.flat.grad[:self.flat.tail_offset])
+
+    def _sync_tail(self) -> None:
+        g = self.flat.grad[self.flat.tail_offset:] if self.overlap else self.flat.grad
+        works = self._pending + self.sync.start(g)
+        self._pending = []
+        for w in works:
+            w.wait()
+
+    def _broadcast_buffers(self) -> None:
+        comm.broadcast(self.fbufs.data, comm.group_src(0, self.group), self.group)
 
     def _raw_items_fwd(self, b: Dict[str, Tensor], seeds: Optional[Tensor]):
         """cfg 3 item encoders (item_tower.py:131-147): audio/visual ResNet-18, zero text slot,
@@ -302,61 +467,68 @@ class TrainStep:
         ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
                   zero_grad=True)
 
-    def _body(self, b: Dict[str, Tensor]) -> None:
-        self._fwd_bwd(b)
-        if self.sync.world == 1:
-            self._update()
+    def _body(self, b: Dict[str, Tensor], cut: Callable = _no_cut) -> None:
+        self._fwd_bwd(b, cut)
+        if self.world > 1:
+            cut(self._sync_tail)
+        self._update()
 
     # ---------------------------------------------------------------- capture
+    @staticmethod
+    def _signature(batch: Dict[str, Tensor]) -> tuple:
+        return tuple((k, tuple(batch[k].shape), batch[k].dtype)
+                     for k in TrainStep.INPUT_KEYS if k in batch)
+
     def _stage(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
-        if self.static is None:
-            self.static = {k: torch.empty_like(batch[k], device=self.device)
-                           for k in self.INPUT_KEYS if k in batch}
-        keys = list(self.static)
+        sig = self._signature(batch)
+        e = self._entries.get(sig)
+        if e is None:
+            e = _Entry({k: torch.empty(batch[k].shape, dtype=batch[k].dtype, device=self.device)
+                        for k in self.INPUT_KEYS if k in batch})
+            self._entries[sig] = e
+        self._cur = e
+        keys = list(e.static)
         srcs = [batch[k] for k in keys]
-        if all(t.is_cuda and t.is_contiguous() and t.dtype == self.static[k].dtype
+        if all(t.is_cuda and t.is_contiguous() and t.dtype == e.static[k].dtype
                for k, t in zip(keys, srcs)):
-            ops.batch_copy([self.static[k] for k in keys], srcs)   # one launch
+            ops.batch_copy([e.static[k] for k in keys], srcs)   # one launch
         else:
             for k, t in zip(keys, srcs):
-                self.static[k].copy_(t, non_blocking=True)
-        return self.static
+                e.static[k].copy_(t, non_blocking=True)
+        return e.static
 
     def _state(self):
         return [self.flat.data, self.flat.exp_avg, self.flat.exp_avg_sq, self.step_t,
                 *self.bufs.values()] + ([self.flat.mirror] if self.flat.mirror is not None else [])
 
-    def _capture(self, b: Dict[str, Tensor]) -> None:
+    def _capture(self, e: _Entry) -> None:
+        b = e.static
         snap = [t.clone() for t in self._state()]
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):          # warm-up: load code objects, size the pool
-            self._fwd_bwd(b)
-            self._update()
+            self._body(b)
         torch.cuda.current_stream(self.device).wait_stream(side)
         for t, s in zip(self._state(), snap):   # undo the warm-up's state changes
             t.copy_(s)
         torch.cuda.synchronize(self.device)
-        self.graph_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_fb):
-            self._body(b)
-        if self.sync.world > 1:
-            self.graph_up = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_up):
-                self._update()
+        seg = _Segments(self.device, capture=True, pool=torch.cuda.graph_pool_handle())
+        seg.begin()
+        self._body(b, seg.cut)
+        seg.end()
+        e.seg, e.loss, e.logits = seg, self.loss, self.logits
 
     def step(self, batch: Dict[str, Tensor]) -> Tensor:
         ops.bump_param_epoch()                 # the replay below rewrites the parameters
+        if self.broadcast_buffers:
+            self._broadcast_buffers()
         b = self._stage(batch)
+        e = self._cur
         if not self.use_graph:
-            self._fwd_bwd(b)
-            self.sync(self.flat.grad)
-            self._update()
+            self._body(b)
             return self.loss
-        if self.graph_fb is None:
-            self._capture(b)
-        self.graph_fb.replay()
-        if self.sync.world > 1:
-            self.sync(self.flat.grad)
-            self.graph_up.replay()
+        if e.seg is None:
+            self._capture(e)
+        e.seg.replay()
+        self.loss, self.logits = e.loss, e.logits
         return self.loss

@@ -131,6 +131,14 @@ class SequentialUserEncoder(nn.Module):
         super().__init__()
         if embedding_dim % num_heads:
             raise ValueError("embedding_dim must be divisible by num_heads")
+        # the attention kernels (ttmi_attn.hip) keep a whole sequence's K/V head slice in one
+        # workgroup's LDS: reject other shapes here, not mid-epoch at the first launch
+        d_h = embedding_dim // num_heads
+        if not 0 < max_seq_len <= 64:
+            raise ValueError(f"max_seq_len must be in [1, 64] (got {max_seq_len})")
+        if d_h > 64 or d_h % 8:
+            raise ValueError(f"head width embedding_dim / num_heads must be a multiple of 8 "
+                             f"and <= 64 (got {d_h})")
         self.embedding_dim = embedding_dim
         self.max_seq_len = max_seq_len
         self.num_heads = num_heads

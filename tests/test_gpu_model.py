@@ -434,3 +434,72 @@ def test_global_infonce_world1_equals_local(gpu_pkg):
     F.infonce_global_bwd(st, None, du, di)
     assert rel(du, ua.grad) < 1e-5
     assert rel(di, ia.grad) < 1e-5
+
+
+@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("B", [1, 2, 3, 5, 7, 13, 61])
+def test_infonce_ragged_batch(gpu_pkg, B, D):
+    """Any B >= 1 (the reference DataLoader keeps its ragged last batch, train.py:259-266):
+    the fused kernels' row pitch is then not 16-byte aligned (element loads/stores); fp32
+    path vs the reference InfoNCE restatement, with and without collisions."""
+    g = torch.Generator().manual_seed(B * 1000 + D)
+    u, it = torch.randn(B, D, generator=g), torch.randn(B, D, generator=g)
+    for uid in (None, torch.randint(0, max(1, B // 2), (B,), generator=g)):
+        ua, ia = u.clone().requires_grad_(True), it.clone().requires_grad_(True)
+        lref, sref, _, _ = ref.infonce(ua, ia, uid)
+        lref.backward()
+        ug, ig = u.to(DEV).requires_grad_(True), it.to(DEV).requires_grad_(True)
+        loss, logits, _, _ = gpu_pkg.infonce(ug, ig, None if uid is None else uid.to(DEV))
+        loss.backward()
+        assert abs(float(loss) - float(lref)) <= 1e-5 * max(1.0, abs(float(lref)))
+        assert rel(logits, sref) < 1e-5
+        if B > 1:
+            assert rel(ug.grad, ua.grad) < 1e-5
+            assert rel(ig.grad, ia.grad) < 1e-5
+        else:
+            assert float(ug.grad.abs().max()) < 1e-6
+
+
+@pytest.mark.parametrize("D,B", [(128, 64), (128, 7), (96, 64)])
+def test_infonce_du16_copy(gpu_pkg, D, B):
+    """ttmi_infonce_bwd16: du16 is du rounded to bf16, bit for bit, from the fused finish
+    kernel (D % 64 == 0) and from the unfused path's cast (D = 96); with/without collisions."""
+    F = gpu_pkg.functional
+    g = torch.Generator().manual_seed(D + B)
+    u = torch.randn(B, D, generator=g).to(DEV)
+    it = torch.randn(B, D, generator=g).to(DEV)
+    for uid in (None, torch.randint(0, 10, (B,), generator=g).to(DEV)):
+        _, _, _, _, st = F.infonce_fwd(u, it, uid)
+        du, di = torch.empty_like(u), torch.empty_like(it)
+        du16 = torch.full((B, D), float("nan"), device=DEV, dtype=torch.bfloat16)
+        F.infonce_bwd(st, None, du, di, du16)
+        assert torch.equal(du16.view(torch.int16), du.bfloat16().view(torch.int16))
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_trainstep_ragged_last_batch(gpu_pkg, use_graph):
+    """TrainStep over batches of 8, 8, 7 and 8 pairs (a new batch shape gets its own static
+    buffers and graph; a known one reuses its graph) vs the fp32 oracle's train step."""
+    V, D, L = 101, 64, 12
+    torch.manual_seed(0)
+    m = gpu_pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=3,
+                              num_countries=8, max_seq_len=L, user_embedding_dim=D,
+                              item_embedding_dim=D, user_dropout=0.0,
+                              compute_dtype=torch.float32, precomputed_modalities=True).to(DEV)
+    m.item_tower.fusion_layer[3].p = 0.0
+    params = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    opt, running = {}, ref.init_running()
+    step = gpu_pkg.TrainStep(m, lr=1e-3, use_graph=use_graph)
+    for s, B in enumerate((8, 8, 7, 8)):
+        b = ref.synthetic_batch(B, L, V, 3, 8, num_users=5,
+                                generator=torch.Generator().manual_seed(50 + s))
+        loss = float(step.step({k: v.to(DEV) for k, v in b.items()}))
+        want = ref.train_step(params, opt, b, lr=1e-3, running=running)
+        assert abs(loss - want) <= 2e-5 * max(1.0, abs(want)), (s, B, loss, want)
+    assert len(step._entries) == 2
+    got = {k: v.detach().cpu() for k, v in m.named_parameters()}
+    for k in params:
+        if any(d in k for d in DEGENERATE):      # exactly-zero gradients: AdamW ±lr noise
+            assert (got[k] - params[k]).abs().max().item() <= 1.01 * 1e-3 * 4, k
+        else:
+            assert rel(got[k], params[k]) < 2e-4, (k, rel(got[k], params[k]))
