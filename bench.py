@@ -368,7 +368,7 @@ def main_eval(args, world, rank, device):
     B = args.batch or 512
     K = 20
     torch.manual_seed(1234 + rank)
-    model = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=N_GENDERS,
+    model = pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128, num_genders=N_GENDERS,
                               num_countries=N_COUNTRIES, max_seq_len=L, user_embedding_dim=D,
                               item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
                               compute_dtype=torch.bfloat16).to(device).eval()

@@ -61,7 +61,7 @@ class MultimodalItemEncoder(nn.Module):
     def __init__(self, tabular_input_dim: int, embedding_dim: int = 256, audio_dim: int = 128,
                  visual_dim: int = 128, text_model_name: str = "microsoft/mdeberta-v3-base",
                  text_dim: int = 128, tabular_dim: int = 128, use_lora: bool = True, *,
-                 precomputed_modalities: bool = True, with_text: bool = False,
+                 precomputed_modalities: bool = False, with_text: bool = True,
                  text_cfg: Optional[TextCfg] = None,
                  compute_dtype: torch.dtype = torch.bfloat16):
         super().__init__()

@@ -177,20 +177,45 @@ def reference_state_dict(source) -> Dict[str, Tensor]:
     return sd
 
 
-def model_from_reference_checkpoint(source, vocab_size: int, num_genders: int = 1, **kw):
+def model_from_reference_checkpoint(source, vocab_size: Optional[int] = None,
+                                    num_genders: Optional[int] = None, **kw):
     """Build a TwoTowerModel whose dimensions come from the checkpoint (inference.py:109-128:
     countries from user_tower.country_embedding, tabular width from the tabular encoder, the
-    embedding width from the item embedding) and load it (strict: every key must match)."""
+    embedding width from the item embedding; here also the vocabulary, genders, history length,
+    encoder depth and the text encoder's shape) and load it (strict: every key must match).
+    Explicit keyword arguments override what the checkpoint implies; the head count is not
+    recorded in a state_dict (default 4, as train.py:289-297 builds it)."""
     from .two_tower import TwoTowerModel
+    from .text import TextCfg
     sd = reference_state_dict(source)
-    D = sd["user_tower.item_embedding.weight"].shape[1]
+    ue = sd["user_tower.item_embedding.weight"]
+    D = ue.shape[1]
+    if vocab_size is None:
+        vocab_size = ue.shape[0]
+    if num_genders is None:
+        num_genders = sd["user_tower.gender_embedding.weight"].shape[0]
     kw.setdefault("num_countries", sd["user_tower.country_embedding.weight"].shape[0])
+    kw.setdefault("max_seq_len", sd["user_tower.position_embedding.weight"].shape[0])
+    pre = "user_tower.transformer_encoder.layers."
+    kw.setdefault("user_num_layers", len({k[len(pre):].split(".")[0] for k in sd if k.startswith(pre)}))
     if "item_tower.tabular_encoder.mlp.0.weight" in sd:
         kw.setdefault("tabular_input_dim", sd["item_tower.tabular_encoder.mlp.0.weight"].shape[1])
         kw.setdefault("precomputed_modalities", False)
-        kw.setdefault("with_text", any(k.startswith("item_tower.text_encoder.") for k in sd))
+        tp = "item_tower.text_encoder.transformer.base_model.model."
+        with_text = any(k.startswith("item_tower.text_encoder.") for k in sd)
+        kw.setdefault("with_text", with_text)
+        if with_text and "text_cfg" not in kw:
+            lp = tp + "encoder.layer."
+            word = sd[tp + "embeddings.word_embeddings.weight"]
+            kw["text_cfg"] = TextCfg(
+                vocab_size=word.shape[0], hidden=word.shape[1],
+                layers=len({k[len(lp):].split(".")[0] for k in sd if k.startswith(lp)}),
+                intermediate=sd[lp + "0.intermediate.dense.weight"].shape[0],
+                heads=word.shape[1] // 64,
+                position_buckets=sd[tp + "encoder.rel_embeddings.weight"].shape[0] // 2)
     else:
         kw.setdefault("tabular_input_dim", 128)
+        kw.setdefault("precomputed_modalities", True)
     model = TwoTowerModel(vocab_size=vocab_size, num_genders=num_genders, user_embedding_dim=D,
                           item_embedding_dim=D, **kw)
     model.load_state_dict(sd)

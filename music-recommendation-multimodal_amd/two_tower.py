@@ -95,7 +95,7 @@ class TwoTowerModel(nn.Module):
                  text_model_name: str = "microsoft/mdeberta-v3-base", text_dim: int = 128,
                  tabular_dim: int = 128, use_lora: bool = True, temperature: float = 0.07, *,
                  compute_dtype: torch.dtype = torch.bfloat16,
-                 precomputed_modalities: bool = True, with_text: bool = False,
+                 precomputed_modalities: bool = False, with_text: bool = True,
                  text_cfg=None, global_negatives: bool = False, process_group=None):
         super().__init__()
         self.global_negatives = global_negatives   # cfg 5: negatives from every rank's batch

@@ -118,16 +118,23 @@ def tabular_forward(p: Dict[str, Tensor], x: Tensor, prefix: str = "mlp.", p_dro
 
 def item_tower_raw_forward(p: Dict[str, Tensor], batch: Dict[str, Tensor], p_drop: float = 0.0,
                            drop=None, running: Optional[Dict[str, Tensor]] = None,
-                           text_dim: int = 128, update_running: bool = False) -> Tensor:
+                           text_dim: int = 128, update_running: bool = False,
+                           text_cfg=None) -> Tensor:
     """MultimodalItemEncoder.forward (item_tower.py:131-152) for cfg 3: audio ResNet-18 on
-    ``target_audio``, visual ResNet-18 on ``target_image``, a zero text slot (the mDeBERTa
-    branch is cfg 4), the tabular MLP on ``target_tabular``; concatenated in the reference's
+    ``target_audio``, visual ResNet-18 on ``target_image``, a zero text slot (or, with
+    ``text_cfg``, the cfg-4 mDeBERTa-LoRA TextEncoder of deberta_ref), the tabular MLP on ``target_tabular``; concatenated in the reference's
     fixed order (:147) into the fusion head.  ``p`` holds item-tower names without the
     ``item_tower.`` prefix."""
     audio = resnet18_forward(p, batch["target_audio"], "audio_encoder.backbone.", update_running)
     visual = resnet18_forward(p, batch["target_image"], "visual_encoder.backbone.",
                               update_running)
-    text = torch.zeros(audio.shape[0], text_dim)
+    if text_cfg is not None:        # cfg 4: the mDeBERTa-LoRA branch (deberta_ref, dropout off)
+        from oracle import deberta_ref
+        text = deberta_ref.text_encoder_forward(
+            p, batch["target_input_ids"], batch["target_attention_mask"], text_cfg,
+            prefix="text_encoder.transformer.base_model.model.", proj_prefix="text_encoder.projection.")
+    else:
+        text = torch.zeros(audio.shape[0], text_dim)
     tab = tabular_forward(p, batch["target_tabular"], "tabular_encoder.mlp.", p_drop, drop,
                           update_running)
     modal = torch.cat([audio, visual, text, tab], dim=1)

@@ -213,7 +213,7 @@ def test_resnet18_eval_mode_uses_running_stats(gpu_pkg):
 
 def _cfg3(pkg, B=8, L=12, V=211, T=32, mel=(64, 96), cover=(64, 64), seed=0, p=0.0):
     torch.manual_seed(seed)
-    m = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=T, num_genders=3, num_countries=8,
+    m = pkg.TwoTowerModel(with_text=False, vocab_size=V, tabular_input_dim=T, num_genders=3, num_countries=8,
                           max_seq_len=L, user_embedding_dim=128, item_embedding_dim=128,
                           user_dropout=p, precomputed_modalities=False).to(DEV)
     m.item_tower.fusion_layer[3].p = p

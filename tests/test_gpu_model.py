@@ -178,7 +178,7 @@ def test_infonce_vs_reference(gpu_pkg, name, tag):
 def test_item_fusion_vs_reference(gpu_pkg, dtype):
     z = load_golden("item_fusion.npz")
     D = z["out"].shape[1]
-    m = gpu_pkg.MultimodalItemEncoder(tabular_input_dim=128, embedding_dim=D,
+    m = gpu_pkg.MultimodalItemEncoder(precomputed_modalities=True, tabular_input_dim=128, embedding_dim=D,
                                       compute_dtype=dtype).to(DEV)
     m.fusion_layer[3].p = 0.0
     m.load_state_dict({k: torch.tensor(v) for k, v in sub(z, "p/").items()})
@@ -218,7 +218,7 @@ def test_item_fusion_vs_reference(gpu_pkg, dtype):
 
 def _train_step_model(pkg, z, dtype):
     V, D, L, B, n_g, n_c, n_steps = z["cfg"].tolist()
-    m = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=n_g,
+    m = pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128, num_genders=n_g,
                           num_countries=n_c, max_seq_len=L, user_embedding_dim=D,
                           item_embedding_dim=D, user_dropout=0.0, use_lora=False,
                           compute_dtype=dtype).to(DEV)
@@ -271,7 +271,7 @@ def test_module_path_with_torch_adamw_vs_reference(gpu_pkg):
 
 def _cfg2(pkg, dtype, B=512, L=50, D=128, V=10136, p=0.0, seed=0):
     torch.manual_seed(seed)
-    m = pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=3,
+    m = pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128, num_genders=3,
                           num_countries=64, max_seq_len=L, user_embedding_dim=D,
                           item_embedding_dim=D, user_dropout=p, compute_dtype=dtype).to(DEV)
     m.item_tower.fusion_layer[3].p = p

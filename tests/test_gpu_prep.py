@@ -74,7 +74,7 @@ def test_device_collator_feeds_raw_item_tower(gpu_pkg, tmp_path):
     loader = torch.utils.data.DataLoader(ds, batch_size=16, shuffle=True, collate_fn=D.collate,
                                          generator=torch.Generator().manual_seed(0))
     coll = D.DeviceCollator(DEV)
-    m = gpu_pkg.TwoTowerModel(vocab_size=len(mapper) + 1, tabular_input_dim=ds.tabular_data.shape[1],
+    m = gpu_pkg.TwoTowerModel(with_text=False, vocab_size=len(mapper) + 1, tabular_input_dim=ds.tabular_data.shape[1],
                               num_genders=len(ds.encoders["gender_encoder"].classes_),
                               num_countries=len(ds.encoders["country_encoder"].classes_),
                               user_embedding_dim=128, item_embedding_dim=128,

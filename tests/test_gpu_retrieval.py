@@ -99,7 +99,7 @@ def test_global_evaluator_graph_matches_eager(gpu_pkg):
     weight update (the cached bf16 operands are refreshed into the captured buffers)."""
     torch.manual_seed(0)
     V, D = 2000, 128
-    m = gpu_pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=3, num_countries=8,
+    m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128, num_genders=3, num_countries=8,
                               max_seq_len=50, user_embedding_dim=D, item_embedding_dim=D,
                               user_num_heads=4, compute_dtype=torch.bfloat16).to(DEV).eval()
     g = torch.Generator().manual_seed(2)
@@ -142,7 +142,7 @@ def test_recommend_matches_oracle_inference(gpu_pkg):
     from oracle import two_tower_ref as ref
     torch.manual_seed(0)
     V, D, L = 997, 64, 60
-    m = gpu_pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=128, num_genders=3, num_countries=8,
+    m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128, num_genders=3, num_countries=8,
                               max_seq_len=50, user_embedding_dim=D, item_embedding_dim=D,
                               compute_dtype=torch.float32).to(DEV)
     g = torch.Generator().manual_seed(1)

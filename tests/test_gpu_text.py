@@ -246,3 +246,72 @@ def test_cfg4_module_text_slot_is_text_encoder(gpu_pkg):
                                        it.tabular_encoder(bd["target_tabular"])], 1))
     assert torch.allclose(full, with_text, atol=1e-4)
     assert not torch.allclose(full, zero_text, atol=1e-4)
+
+
+def _reference_loop(model, dataloader, optimizer, device):
+    """The reference's epoch loop body (train.py:41-76) call for call: batch dict moved to the
+    device in place, zero_grad(set_to_none), fp16 autocast forward, GradScaler
+    scale/backward/step/update, loss.item().  Returns the per-batch losses."""
+    model.train()
+    scaler = torch.amp.GradScaler("cuda")
+    losses = []
+    for batch in dataloader:
+        for k, v in batch.items():
+            if isinstance(v, torch.Tensor):
+                batch[k] = v.to(device)
+        optimizer.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss, _, _, _ = model(batch)
+        scaler.scale(loss).backward()
+        scaler.step(optimizer)
+        scaler.update()
+        losses.append(loss.item())
+        del loss, batch
+    return losses
+
+
+def test_reference_call_site_runs_unchanged(gpu_pkg):
+    """Drop-in at the reference call site (train.py:289-302 + train_one_epoch): the DEFAULT
+    constructor with the reference's arguments builds the full multimodal item tower (ResNet-18
+    audio + visual, mDeBERTa-LoRA text, tabular; tiny text dims here), the batches carry the
+    reference keys (plus the ignored target_id / user_id), the last batch is ragged (B = 7,
+    no drop_last), and the loop runs under fp16 autocast + GradScaler with torch.optim.AdamW.
+    The first batch's loss matches the fp32 oracle of the same model on the same inputs
+    (bf16 storage through two ResNet-18s and DeBERTa: 3e-2); every batch gives a finite loss
+    and every trainable parameter moves."""
+    from oracle import resnet_ref as rref
+    from oracle import two_tower_ref as ref
+    tcfg = gpu_pkg.text.TextCfg(vocab_size=400, hidden=128, layers=2, heads=2, intermediate=256,
+                                lora_dropout=0.0, hidden_dropout=0.0, attn_dropout=0.0)
+    dcfg = dref.DebertaCfg(vocab_size=400, hidden=128, layers=2, heads=2, intermediate=256)
+    torch.manual_seed(0)
+    model = gpu_pkg.TwoTowerModel(vocab_size=211, num_genders=3, num_countries=8,
+                                  tabular_input_dim=32, item_embedding_dim=256,
+                                  user_embedding_dim=256, use_lora=True, text_cfg=tcfg,
+                                  user_dropout=0.0).to(DEV)
+    it = model.item_tower
+    assert it.with_text and not it.precomputed_modalities
+    it.fusion_layer[3].p = 0.0
+    it.tabular_encoder.mlp[3].p = 0.0
+    it.text_encoder.projection[2].p = 0.0
+    loader = []
+    for s, B in enumerate((8, 8, 7)):
+        g = torch.Generator().manual_seed(40 + s)
+        b = ref.synthetic_batch(B, 50, 211, num_countries=8, generator=g)
+        del b["target_modal"]
+        b.update(rref.synthetic_items(B, 32, (64, 96), (64, 64), generator=g))
+        b["target_input_ids"], b["target_attention_mask"] = dref.synthetic_text(B, 64, 400,
+                                                                                 generator=g)
+        b["target_id"] = torch.arange(B)
+        b["user_id"] = b["user_idx"].clone()
+        loader.append(b)
+    params = {k: v.detach().cpu().clone() for k, v in model.named_parameters()}
+    lref = float(ref.two_tower_loss(params, loader[0], running=None, text_cfg=dcfg)[0])
+    before = {k: v.detach().clone() for k, v in model.named_parameters() if v.requires_grad}
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    losses = _reference_loop(model, loader, opt, DEV)
+    assert len(losses) == 3 and all(math.isfinite(x) for x in losses), losses
+    assert abs(losses[0] - lref) < 3e-2, (losses[0], lref)
+    moved = [k for k, v in model.named_parameters() if v.requires_grad
+             and not torch.equal(v.detach(), before[k])]
+    assert len(moved) >= 0.9 * len(before), (len(moved), len(before))

@@ -54,7 +54,7 @@ def main():
     only_wgrad = "--wgrad" in sys.argv
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = pkg.TwoTowerModel(vocab_size=bench.V, tabular_input_dim=128, num_genders=3,
+    model = pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=bench.V, tabular_input_dim=128, num_genders=3,
                               num_countries=64, max_seq_len=bench.L, user_embedding_dim=bench.D,
                               item_embedding_dim=bench.D, user_num_heads=bench.H,
                               user_dropout=0.1, compute_dtype=torch.bfloat16).to(dev)
