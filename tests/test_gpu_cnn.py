@@ -96,8 +96,9 @@ def _cos(a, b):
     return torch.dot(a, b).item() / (a.norm().item() * b.norm().item() + 1e-30)
 
 
-@pytest.mark.parametrize("in_ch,H,W", [(1, 64, 96), (3, 64, 64)])
-def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W):
+@pytest.mark.parametrize("in_ch,H,W,N", [(1, 64, 96, 8), (3, 64, 64, 8),
+                                          (1, 128, 256, 4), (3, 224, 224, 4)])
+def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W, N):
     """GPU ResNet-18 vs the fp32 oracle (oracle/resnet_ref.py), with the bf16-emulating
     restatement above as the yardstick for how close any bf16-storage implementation can get.
 
@@ -109,7 +110,6 @@ def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W):
     cnn = gpu_pkg.cnn
     torch.manual_seed(in_ch)
     net = cnn.ResNet18(in_ch, 128).to(DEV)
-    N = 8
     g = torch.Generator().manual_seed(11)
     x = torch.randn(N, in_ch, H, W, generator=g)
     up = torch.randn(N, 128, generator=g)
@@ -134,11 +134,19 @@ def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W):
                        _cos(p.grad, gr), p.grad.norm().item() / gr.norm().item()))
     assert rel(out, out_emu) < 2e-2, report[0]
     assert rel(out, out_ref) < 5e-2, report[0]
-    for name, _, _, cr, nr in report[1:]:
+    # full resolution: float-atomic BN statistics move single bias gradients by up to 0.04 in
+    # cosine run to run (measured 0.865 / 0.955 for layer1.0.bn1.bias on two runs, emulation
+    # 0.91-0.93); the small inputs keep the original 0.03
+    margin = 0.03 if H * W <= 64 * 96 else 0.06
+    bad = []
+    for name, ce_gpu, _, cr, nr in report[1:]:
         ce_ref = _cos(Pe[name].grad, Pr[name].grad)
         ne_ref = Pe[name].grad.norm().item() / Pr[name].grad.norm().item()
-        assert cr > ce_ref - 0.03, (name, cr, ce_ref)
-        assert abs(nr - 1) < 2 * abs(ne_ref - 1) + 0.1, (name, nr, ne_ref)
+        print("GRAD", name, f"gpu~fp32 {cr:.4f} emu~fp32 {ce_ref:.4f} gpu~emu {ce_gpu:.4f} "
+              f"norm gpu {nr:.4f} emu {ne_ref:.4f}")
+        if not (cr > ce_ref - margin and abs(nr - 1) < 2 * abs(ne_ref - 1) + 0.1):
+            bad.append((name, cr, ce_ref, nr, ne_ref))
+    assert not bad, bad
     sd = net.state_dict()
     for k in sd:
         if "running_mean" in k:
@@ -225,14 +233,16 @@ def _cfg3(pkg, B=8, L=12, V=211, T=32, mel=(64, 96), cover=(64, 64), seed=0, p=0
     return m, batch
 
 
-def test_cfg3_two_tower_vs_oracle(gpu_pkg):
+@pytest.mark.parametrize("B,mel,cover", [(8, (64, 96), (64, 64)), (4, (128, 256), (224, 224))])
+def test_cfg3_two_tower_vs_oracle(gpu_pkg, B, mel, cover):
     """cfg 3 (raw mels / covers / tabular, zero text slot): loss and logits vs the fp32
     oracle, item-tower gradients by direction and norm against the same emulation yardstick
     (cosine within 0.05 of the emulation's).  bf16 storage through two ResNet-18s moves the
     item embedding ~2 %, which τ = 0.07 amplifies in the logits; the loss bound is 2x the
     deviation of the bf16-emulating oracle (same rounding points as the kernels) + 5e-3.
-    (The 1e-3 north-star bar is cfg 2's, whose item inputs are precomputed.)"""
-    m, batch = _cfg3(gpu_pkg)
+    (The 1e-3 north-star bar is cfg 2's, whose item inputs are precomputed.)  Run at a small
+    size and at BASELINE configs[2]'s stated inputs (1x128x256 mels, 3x224x224 covers)."""
+    m, batch = _cfg3(gpu_pkg, B=B, mel=mel, cover=cover)
     params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
     lref, logits_ref, _, _ = ref.two_tower_loss(params, batch, running=None)
     lref.backward()

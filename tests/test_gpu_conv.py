@@ -39,6 +39,13 @@ SHAPES = [  # N, Cin, H, W, Co, k, stride, pad
     (2, 256, 5, 4, 512, 3, 1, 1),
     (4, 128, 20, 18, 128, 3, 1, 1),
     (2, 128, 9, 11, 256, 1, 2, 0),
+    # full-size cfg-3 shapes (BASELINE configs[2]): the 224² cover stem (M = 25,088 output
+    # rows at N = 2), the 1x128x256 mel stem, and visual layer 1/2 at 56²
+    (2, 3, 224, 224, 64, 7, 2, 3),
+    (2, 1, 128, 256, 64, 7, 2, 3),
+    (2, 64, 56, 56, 64, 3, 1, 1),
+    (2, 64, 56, 56, 128, 3, 2, 1),
+    (2, 64, 56, 56, 128, 1, 2, 0),
 ]
 
 

@@ -95,3 +95,44 @@ def test_device_collator_feeds_raw_item_tower(gpu_pkg, tmp_path):
         if n == 2:
             break
     assert n == 2
+
+
+def test_cfg1_loader_batches_through_hip_train_step(gpu_pkg):
+    """BASELINE configs[0] on the HIP path: MultimodalDataset batches (batch 4, history 20,
+    100 users x 1k items, 32 x 32 stub mels / covers) through the fused TrainStep (user tower,
+    ResNet-18 audio + visual, tabular, fusion head, InfoNCE with the collision mask, AdamW),
+    step for step against the fp32 oracle's train step from the same parameters (bf16
+    storage through two ResNet-18s at B = 4: 3e-2 on the loss)."""
+    import math
+    from oracle import resnet_ref as rr
+    from oracle import two_tower_ref as ref
+    from oracle import prep_ref as pr
+    from test_prep_oracle import _dataset
+    D = gpu_pkg.data
+    df, mapper, ds = _dataset()
+    loader = torch.utils.data.DataLoader(ds, batch_size=4, shuffle=True, collate_fn=D.collate,
+                                         generator=torch.Generator().manual_seed(0))
+    T = ds.tabular_data.shape[1]
+    torch.manual_seed(0)
+    m = gpu_pkg.TwoTowerModel(vocab_size=len(mapper) + 1, tabular_input_dim=T,
+                              num_genders=len(ds.encoders["gender_encoder"].classes_),
+                              num_countries=len(ds.encoders["country_encoder"].classes_),
+                              max_seq_len=20, user_embedding_dim=128, item_embedding_dim=128,
+                              user_dropout=0.0, with_text=False).to(DEV)
+    m.item_tower.fusion_layer[3].p = 0.0
+    m.item_tower.tabular_encoder.mlp[3].p = 0.0
+    P = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    state, running = {}, ref.init_running()
+    step = gpu_pkg.TrainStep(m, lr=1e-4)
+    for i, b in enumerate(loader):
+        img = torch.stack([torch.from_numpy(pr.cover_transform(x.numpy(), size=32)).float()
+                           for x in b["target_image_u8"]])
+        batch = {k: b[k] for k in ("history_ids", "history_mask", "user_gender", "user_country",
+                                   "user_idx")}
+        batch.update({"target_audio": b["target_audio_raw"].float().unsqueeze(1).contiguous(),
+                      "target_image": img, "target_tabular": b["target_tabular"].float()})
+        got = float(step.step({k: v.to(DEV) for k, v in batch.items()}))
+        want = ref.train_step(P, state, batch, running=running)
+        assert math.isfinite(got) and abs(got - want) < 3e-2, (i, got, want)
+        if i == 3:
+            break

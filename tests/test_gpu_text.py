@@ -315,3 +315,50 @@ def test_reference_call_site_runs_unchanged(gpu_pkg):
     moved = [k for k, v in model.named_parameters() if v.requires_grad
              and not torch.equal(v.detach(), before[k])]
     assert len(moved) >= 0.9 * len(before), (len(moved), len(before))
+
+
+def test_text_encoder_base_dims_vs_oracle(gpu_pkg):
+    """cfg 4 at mDeBERTa-v3-base dimensions (hidden 768, 12 heads, 12 layers, FFN 3072, 256
+    position buckets, vocab 251,000 — oracle DebertaCfg() defaults), S = 256, B = 2 with one
+    full and one 100-token sequence, LoRA B non-zero so every LoRA path is live: output vs the
+    fp32 oracle (bf16 storage through 12 layers: 5e-2), and every trainable gradient by
+    direction (cosine >= 0.98) and norm (±10 %)."""
+    text = gpu_pkg.text
+    dcfg = dref.DebertaCfg()
+    cfg = text.TextCfg(lora_dropout=0.0, hidden_dropout=0.0, attn_dropout=0.0)
+    assert (cfg.hidden, cfg.heads, cfg.layers, cfg.intermediate, cfg.vocab_size,
+            cfg.position_buckets) == (dcfg.hidden, dcfg.heads, dcfg.layers, dcfg.intermediate,
+                                      dcfg.vocab_size, dcfg.position_buckets)
+    g = torch.Generator().manual_seed(21)
+    P = dref.init_text_params(dcfg, 128, g, lora_b_std=0.02)
+    enc = text.TextEncoder(embedding_dim=128, cfg=cfg).to(DEV)
+    enc.projection[2].p = 0.0
+    enc.load_state_dict(P)
+    enc.train()
+    B, S = 2, 256
+    ids = torch.randint(1, dcfg.vocab_size, (B, S), generator=g)
+    mask = torch.ones(B, S, dtype=torch.int64)
+    mask[1, 100:] = 0
+    ids = ids * mask
+    up = torch.randn(B, 128, generator=g)
+    out = enc(ids.to(DEV), mask.to(DEV))
+    (out * up.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    train = {n for n, p in enc.named_parameters() if p.requires_grad}
+    Pr = {k: (v.clone().requires_grad_(True) if k in train else v) for k, v in P.items()}
+    ref_out = dref.text_encoder_forward(Pr, ids, mask, dcfg)
+    (ref_out * up).sum().backward()
+    assert rel(out, ref_out) < 5e-2, rel(out, ref_out)
+    rows = []
+    for name, p in enc.named_parameters():
+        if name in train:
+            gr = Pr[name].grad
+            rows.append((name, _cos(p.grad, gr), p.grad.norm().item() / gr.norm().item()))
+    for r in rows:
+        print("GRAD", *r)
+    assert len(rows) == 4 * dcfg.layers + 4
+    # measured (MI355X): cosines 0.991-1.000; LoRA-A norms spread ±6 % with one at -8 %
+    # (deterministic for this seed: bf16 rounding through 12 layers; the rank-8 contraction
+    # dL = dQ·B_q with B ~ N(0, 0.02) sums cancelling terms over every token)
+    bad = [r for r in rows if not (r[1] > 0.98 and abs(r[2] - 1) < 0.10)]
+    assert not bad, bad
