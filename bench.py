@@ -116,45 +116,66 @@ def _wgrad_call(kw) -> bool:
 
 
 def probe_dominant(step, batch, device, iters: int = 20):
-    """Roofline of the dominant kernel family, the weight-gradient GEMM (wgrad_kernel: 12
-    launches per step, five shapes, ~12 % of device time).  One eager forward+backward
-    records the exact launch mix of a step; the mix is then replayed `iters` times on the
-    current stream between HIP events, so avg_us is the per-launch mean over the same mix
-    the rocprofv3 summary averages.  Algorithmic bytes per launch: both bf16 operands once
-    (R x (M + N) x 2) plus the fp32 gradient tile (M x N x 4)."""
+    """Roofline of the dominant kernel family, the deterministic weight-gradient GEMM
+    (ttmi_wgrad: 12 launches per step — wgrad_kernel<64,64,4> on the five 25,600-row shapes,
+    wgrad_kernel<32,32,4> on the seven 512-row ones — plus the one wgrad_fold_kernel launch that
+    sums the split partials).  One eager forward+backward records the exact call mix of a
+    step; the mix (inside one deferred_wgrad block, as in the step: one fold) is captured into
+    a HIP graph and replayed `iters` times between HIP events on the launch stream, so avg_us =
+    device time of the family / 12 launches (the fold's time counted, shared out).
+    Algorithmic bytes per launch: both bf16 operands once (R x (M + N) x 2) plus the fp32
+    gradient tile (M x N x 4)."""
     ops = pkg.ops
     calls = []
-    orig = ops.gemm
+    orig = ops.linear_dw
 
-    def rec(A, B_, C, M, N, K, **kw):
-        if _wgrad_call(kw) and A.dtype == torch.bfloat16:
-            calls.append((A, B_, C, M, N, K, dict(kw)))
-        return orig(A, B_, C, M, N, K, **kw)
+    def rec(dy, x, gw, gb=None, split_k=0, defer=True):
+        if dy.dtype == torch.bfloat16:
+            calls.append((dy, x, gw, gb))
+        return orig(dy, x, gw, gb, split_k, defer)
 
-    ops.gemm = rec
+    ops.linear_dw = rec
     try:
         step._fwd_bwd(step._stage(batch))
     finally:
-        ops.gemm = orig
+        ops.linear_dw = orig
     torch.cuda.synchronize(device)
-    for c in calls:                                    # warm
-        orig(*c[:6], **c[6])
+
+    def mix():
+        with ops.deferred_wgrad():
+            for dy, x, gw, gb in calls:
+                orig(dy, x, gw, gb)
+
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        mix()                                          # warm
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            mix()
+    torch.cuda.current_stream(device).wait_stream(side)
+    torch.cuda.synchronize(device)
     st = torch.cuda.current_stream(device)
+    g.replay()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(iters):
-        for c in calls:
-            orig(*c[:6], **c[6])
+        g.replay()
     e1.record(st)
     torch.cuda.synchronize(device)
     n = max(len(calls), 1)
     sec = e0.elapsed_time(e1) / 1e3 / (iters * n)
-    by = sum(K * (M + N) * 2 + M * N * 4 for (_, _, _, M, N, K, _) in calls) / n
-    fl = sum(2.0 * M * N * K for (_, _, _, M, N, K, _) in calls) / n
+    shapes = [(dy.shape[0], dy.shape[1], x.shape[1]) for dy, x, _, _ in calls]
+    by = sum(R * (M + N) * 2 + M * N * 4 for R, M, N in shapes) / n
+    fl = sum(2.0 * M * N * R for R, M, N in shapes) / n
     gbs = by / sec / 1e9
-    return {"kernel": "wgrad_kernel<64,64,4> (weight-gradient GEMMs, per-step launch mix)",
+    tw, tfold = read_traffic("wgrad_kernel"), read_traffic("wgrad_fold_kernel")
+    traffic = round(tw + (tfold or 0) / n) if tw is not None else None   # the fold, shared out
+    return {"kernel": "ttmi_wgrad family: wgrad_kernel<64,64,4> x5 + wgrad_kernel<32,32,4> x7 + "
+                      "1 wgrad_fold_kernel (deterministic weight-gradient GEMMs, per-step mix, "
+                      "graph-replayed)",
             "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": read_traffic("wgrad_kernel"),
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
             "avg_us": round(sec * 1e6, 2), "launches_per_step": len(calls),
             "bytes_per_launch": round(by), "flops_per_launch": round(fl),
             "mfma_tflops": round(fl / sec / 1e12, 1)}
@@ -263,42 +284,68 @@ def cpu_baseline_cfg4(B: int, budget_s: float = 20.0):
     ids, mask = dref.synthetic_text(B, TEXT_S, TEXT_V, generator=g)
     x = {"ids": ids, "mask": mask}
     out_w = torch.randn(128, generator=g)
-    t0 = time.perf_counter()
-    n = 0
-    while True:                            # text encoder fwd + dX/LoRA bwd dominates cfg 4
+
+    def text_step():                       # text encoder fwd + dX/LoRA bwd dominates cfg 4
         leaves = {k: v.detach().requires_grad_(True) for k, v in params.items()}
         out = dref.text_encoder_forward({**frozen, **leaves}, x["ids"], x["mask"], dcfg)
         (out * out_w).sum().backward()
-        n += 1
-        el = time.perf_counter() - t0
-        if el + el / n >= budget_s or n >= 10:
-            break
-    per_pair_text = el / (n * B)
+    rate_t, med, tot = _cpu_protocol(text_step, B, warmup=1, timed=5)
     c3 = cpu_baseline_cfg3(8, budget_s)
-    per_pair_c3 = 1.0 / c3["value"]
-    value = 1.0 / (per_pair_text + per_pair_c3)
+    value = 1.0 / (1.0 / rate_t + 1.0 / c3["value"])
     return {"value": round(value, 4), "unit": "user-item pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} mDeBERTa-v3-base + LoRA fwd+bwd steps at B={B}, S={TEXT_S} "
-                      f"({el:.1f} s) combined with the cfg-3 oracle step rate "
-                      f"({c3['value']} pairs/s, {c3['sample']}); fp32 torch-CPU oracle"}
+            **_cpu_host(),
+            "sample": f"1 warm-up + 5 timed mDeBERTa-v3-base + LoRA fwd+bwd steps at B={B}, "
+                      f"S={TEXT_S} (median {med:.2f} s; fewer steps than BASELINE.md §2's 3 + 10 "
+                      f"to keep the sample near 20 s) combined per pair with the cfg-3 oracle "
+                      f"rate ({c3['value']} pairs/s: {c3['sample']}); fp32 torch-CPU oracle"}
 
 
 def read_traffic(name: str):
     """Per-launch HBM bytes of `name` from the committed rocprofv3 PMC summary
     (profiles/*traffic*.json, written by tools/traffic.py), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
-    if not files:
-        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+        try:                                   # newest round's file that measured `name`
+            with open(path) as f:
+                v = json.load(f).get(name, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            continue
+        if v is not None:
+            return v
+    return None
+
+
+def _cpu_host() -> dict:
+    """nproc and the CPU model name of this host (BASELINE.md §2 asks for both)."""
+    model = ""
     try:
-        with open(files[-1]) as f:
-            data = json.load(f)
-        return data.get(name, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
+def _cpu_protocol(step, B: int, warmup: int = 3, timed: int = 10):
+    """`warmup` untimed steps, then `timed` steps; pairs/s = B / median step
+    time.  Threads = torch's intra-op pool (the box exports OMP_NUM_THREADS = 16, its CPU
+    share beside one GPU; `nproc` reports the whole machine's CPUs, which this process is not
+    allotted), recorded as `cores`."""
+    for _ in range(warmup):
+        step()
+    times = []
+    for _ in range(timed):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return B / med, med, sum(times)
 
 
 def cpu_baseline(B: int, budget_s: float = 20.0):
-    """fp32 CPU oracle (oracle/two_tower_ref.py) train step on this host's cores."""
+    """fp32 CPU oracle (oracle/two_tower_ref.py) cfg-2 train step on this host's cores."""
     from oracle import two_tower_ref as ref
     threads = torch.get_num_threads()
     g = torch.Generator().manual_seed(0)
@@ -307,18 +354,13 @@ def cpu_baseline(B: int, budget_s: float = 20.0):
     running = ref.init_running()
     state = {}
     drop = ref.TorchDropout()
-    ref.train_step(params, state, batch, p_drop=0.1, drop=drop, running=running)   # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        ref.train_step(params, state, batch, p_drop=0.1, drop=drop, running=running)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 30:
-            break
-    return {"value": round(n * B / el, 2), "unit": "user-item pairs/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} full cfg-2 steps (B={B}, L={L}, D={D}, V={V}, dropout 0.1) of the "
-                      f"fp32 torch-CPU oracle after 1 warm-up, {el:.1f} s"}
+    rate, med, tot = _cpu_protocol(
+        lambda: ref.train_step(params, state, batch, p_drop=0.1, drop=drop, running=running), B)
+    return {"value": round(rate, 2), "unit": "user-item pairs/s", "cores": threads,
+            "kind": "port", **_cpu_host(),
+            "sample": f"3 warm-up + 10 timed full cfg-2 steps (B={B}, L={L}, D={D}, V={V}, "
+                      f"dropout 0.1) of the fp32 torch-CPU oracle; median step {med:.3f} s, "
+                      f"{tot:.1f} s timed"}
 
 
 def cpu_baseline_cfg3(B: int, budget_s: float = 20.0):
@@ -344,20 +386,13 @@ def cpu_baseline_cfg3(B: int, budget_s: float = 20.0):
     batch.update(rref.synthetic_items(B, TAB, MEL, COVER, generator=g))
     state = {}
     drop = ref.TorchDropout()
-    t0 = time.perf_counter()
-    ref.train_step(params, state, batch, p_drop=0.1, drop=drop)                  # warm-up
-    warm = time.perf_counter() - t0
-    n, t0 = 0, time.perf_counter()
-    while True:
-        ref.train_step(params, state, batch, p_drop=0.1, drop=drop)
-        n += 1
-        el = time.perf_counter() - t0
-        if el + el / n >= budget_s or n >= 30:
-            break
-    return {"value": round(n * B / el, 3), "unit": "user-item pairs/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} cfg-3 steps at B={B} (full 128x256 mels, 224x224 covers; "
-                      f"warm-up {warm:.1f} s) of the fp32 torch-CPU oracle, {el:.1f} s"}
+    rate, med, tot = _cpu_protocol(
+        lambda: ref.train_step(params, state, batch, p_drop=0.1, drop=drop), B)
+    return {"value": round(rate, 3), "unit": "user-item pairs/s", "cores": threads,
+            "kind": "port", **_cpu_host(),
+            "sample": f"3 warm-up + 10 timed cfg-3 steps at B={B} (full 128x256 mels, 224x224 "
+                      f"covers) of the fp32 torch-CPU oracle; median step {med:.3f} s, "
+                      f"{tot:.1f} s timed"}
 
 
 def main_eval(args, world, rank, device):

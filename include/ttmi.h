@@ -86,6 +86,32 @@ typedef struct {
 int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * Deterministic nn.Linear weight gradient (every Linear's backward on the path:
+ * user_tower.py:37-57, item_tower.py:85-129 — autograd's dW = dYᵀ·X, db = Σ_r dY):
+ *   dw[m, n] (+)= alpha · Σ_r dy[r, m] · x[r, n];   db[m] (+)= Σ_r dy[r, m]   (db may be NULL)
+ * dy bf16 [R][ld_dy], x bf16 [R][ld_x] (row-major over the reduction), dw fp32 [M][ld_dw].
+ * The reduction is split over workgroups; split partials go to `workspace`
+ * (ttmi_wgrad_workspace bytes; 0 when one split suffices) and are summed in split order, so
+ * the result is bit-reproducible (no float atomics).  defer = 1 leaves the partials in the
+ * workspace: a later ttmi_wgrad_fold over the same descriptors (several GEMMs per launch)
+ * completes dw / db.  M, N % 8 == 0; ld_dw % 4 == 0; operands 16-byte aligned.  ABI 10.
+ * ---------------------------------------------------------------------------------- */
+typedef struct {
+  int64_t R, M, N;
+  const void* dy; int64_t ld_dy;
+  const void* x; int64_t ld_x;
+  float* dw; int64_t ld_dw;
+  float* db;
+  float alpha;
+  int accumulate;
+  void* workspace; int64_t workspace_bytes;
+  int defer;
+} ttmi_wgrad_desc;
+int64_t ttmi_wgrad_workspace(int64_t R, int64_t M, int64_t N, int64_t ld_dy, int64_t ld_x);
+int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream);
+int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, hipStream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0) — TransformerEncoderLayer
  * norm1/norm2 (user_tower.py:37-45), user fusion LN (user_tower.py:54), item head final
  * LN (item_tower.py:128).  Optional ReLU and dropout (idx = row*D + col) after the affine.

@@ -312,7 +312,7 @@ def tabular_bwd(P: Dict[str, Tensor], st: TabSaved, dout: Tensor, grads: Dict[st
     gw = grads["mlp.0.weight"]
     if st.x.shape[1] != gw.shape[1]:                  # zero-padded T (see tabular_fwd)
         pad = torch.zeros(gw.shape[0], st.x.shape[1], device=dev)
-        ops.linear_dw(dzc, st.x, pad, grads["mlp.0.bias"])
+        ops.linear_dw(dzc, st.x, pad, grads["mlp.0.bias"], defer=False)   # read just below
         gw.add_(pad[:, :gw.shape[1]])
     else:
         ops.linear_dw(dzc, st.x, gw, grads["mlp.0.bias"])

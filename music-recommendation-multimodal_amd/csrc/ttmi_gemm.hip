@@ -663,7 +663,13 @@ struct WgradArgs {
   float* rowsum_a;
   int64_t rows_per_split;   // multiple of 64
   int tiles_m, tiles_n, splits, xcd_remap;
+  // epilogue: WG_ATOMIC adds into C (legacy ttmi_gemm path); WG_SLAB stores the split's
+  // partial tile to part[split][M][N] (and the row sums to part_rs[split][M]) with plain
+  // stores, folded in split order by wgrad_fold_kernel; WG_DIRECT (one split) writes C itself
+  int mode, accumulate;
+  float* part; float* part_rs;
 };
+enum { WG_ATOMIC = 0, WG_SLAB = 1, WG_DIRECT = 2 };
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
@@ -830,8 +836,37 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       const int64_t m = m0 + wm * WTM + i * 16 + li;
-      if (lg == 0 && m < g.M) atomicAdd(g.rowsum_a + m, v);
+      if (lg == 0 && m < g.M) {
+        if (g.mode == WG_ATOMIC) atomicAdd(g.rowsum_a + m, v);
+        else if (g.mode == WG_SLAB) g.part_rs[(int64_t)split * g.M + m] = v;
+        else g.rowsum_a[m] = g.accumulate ? g.rowsum_a[m] + v : v;
+      }
     }
+  }
+  if (g.mode != WG_ATOMIC) {
+    // deterministic epilogues: every (split, tile) element has exactly one writer; the lane
+    // holds 4 consecutive columns of one row per accumulator (16-byte stores, N % 4 == 0)
+    wait_vm<0>();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t m = m0 + wm * WTM + i * 16 + li, n = n0 + wn * WTN + j * 16 + 4 * lg;
+        if (m >= g.M || n >= g.N) continue;
+        float4 v = make_float4(g.alpha * acc[i][j][0], g.alpha * acc[i][j][1],
+                               g.alpha * acc[i][j][2], g.alpha * acc[i][j][3]);
+        if (g.mode == WG_SLAB) {
+          *reinterpret_cast<float4*>(g.part + ((int64_t)split * g.M + m) * g.N + n) = v;
+        } else {
+          float4* cp = reinterpret_cast<float4*>(g.C + m * g.ldc + n);
+          if (g.accumulate) {
+            const float4 c = *cp;
+            v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+          }
+          *cp = v;
+        }
+      }
+    return;
   }
   // reshape through LDS: every atomic wave-instruction then covers 64 consecutive columns
   wait_vm<0>();
@@ -939,6 +974,7 @@ int launch_wgrad_t(const ttmi_gemm_desc* d, int remap, hipStream_t stream) {
   a.rows_per_split = sps * 64;
   a.tiles_m = tiles_m; a.tiles_n = tiles_n; a.splits = S;
   a.xcd_remap = remap && (S % 8 == 0);
+  a.mode = WG_ATOMIC; a.accumulate = 1; a.part = nullptr; a.part_rs = nullptr;
   const int64_t nwg = (int64_t)T * S;
   TTMI_REQUIRE(nwg <= 2147483647LL, "ttmi_gemm: grid too large");
   hipLaunchKernelGGL((wgrad_kernel<BM, BN, NS>), dim3((unsigned)nwg), dim3(256), 0, stream, a);
@@ -954,6 +990,133 @@ int launch_wgrad(const ttmi_gemm_desc* d, hipStream_t stream) {
 
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// --------------------------------------------- deterministic weight gradient (ttmi_wgrad)
+// Same 64x64 tiles, ring and split geometry as the atomic path (about 320 workgroups, splits
+// a multiple of 8 so the tiles re-reading one row range share an XCD's L2), but the split
+// partials are plain 16-byte stores into a caller workspace, summed in split order by
+// wgrad_fold_kernel: bit-reproducible, and the partial bytes leave at store rate (~6 TB/s)
+// instead of the memory-side float-atomic rate (~1.3 TB/s, MI355X_MICROARCH §Global float
+// atomics).  One split (short R) writes C directly.  Folds of several GEMMs share one launch.
+struct WgradPlan { int tiles_m, tiles_n, S, tile; int64_t sps; };
+
+WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
+  WgradPlan p;
+  p.tile = 64;
+  p.tiles_m = (int)((M + 63) / 64);
+  p.tiles_n = (int)((N + 63) / 64);
+  const int T = p.tiles_m * p.tiles_n;
+  const int64_t stages = std::max<int64_t>(1, (R + 63) / 64);
+  static const int target = [] {
+    const char* e = getenv("TTMI_WGRAD_WG");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 320;
+  }();
+  int S = (target / T + 4) & ~7;
+  if (S < 8) S = std::max(1, target / T);
+  // at least MIN_STAGES 64-row stages per split: below that a split's partial tile costs more
+  // bytes (written, then folded) than the rows it reduces (R = 512 -> one split, direct)
+  static const int min_stages = [] {
+    const char* e = getenv("TTMI_WGRAD_MIN_STAGES");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 6;
+  }();
+  S = (int)std::max<int64_t>(1, std::min<int64_t>(S, stages / min_stages));
+  int64_t sps = (stages + S - 1) / S;
+  while (sps > 1 && sps * 64 * ldmax * 2 >= (int64_t)1 << 31) sps = (sps + 1) / 2;
+  p.S = (int)((stages + sps - 1) / sps);
+  p.sps = sps;
+  if (p.S == 1 && T < 128) {   // one split: 32x32 tiles put 4x the workgroups on the rows
+    p.tile = 32;
+    p.tiles_m = (int)((M + 31) / 32);
+    p.tiles_n = (int)((N + 31) / 32);
+  }
+  return p;
+}
+
+int64_t al256(int64_t b) { return (b + 255) / 256 * 256; }
+
+int64_t wgrad_ws_bytes(const WgradPlan& p, int64_t M, int64_t N) {
+  if (p.S <= 1) return 0;
+  return al256((int64_t)p.S * M * N * 4) + al256((int64_t)p.S * M * 4);
+}
+
+constexpr int FOLD_SEGS = 8;
+struct FoldSeg {
+  const float* part; const float* part_rs; float* C; float* rs;
+  int64_t M, N, ldc, units, base;
+  int S, acc;
+};
+struct FoldArgs { FoldSeg seg[FOLD_SEGS]; int n; int64_t total; };
+
+// The segment is read straight from the kernel-argument segment at the uniform offset
+// blockIdx.y (scalar loads); copying the argument array to a local and indexing it
+// dynamically would put it in scratch memory.
+typedef const __attribute__((address_space(4))) FoldArgs* KFoldArgs;
+
+__global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
+  (void)a;
+  const auto& sgk = ((KFoldArgs)__builtin_amdgcn_kernarg_segment_ptr())->seg[blockIdx.y];
+  FoldSeg sg;
+  sg.part = sgk.part; sg.part_rs = sgk.part_rs; sg.C = sgk.C; sg.rs = sgk.rs;
+  sg.M = sgk.M; sg.N = sgk.N; sg.ldc = sgk.ldc; sg.units = sgk.units; sg.base = 0;
+  sg.S = sgk.S; sg.acc = sgk.acc;
+  __shared__ float4 red[4][64];
+  const int ul = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t nq = sg.N / 4, nel = sg.M * nq;
+  const int64_t stride = sg.M * sg.N;
+  const int s_lo = (int)((int64_t)sg.S * q / 4), s_hi = (int)((int64_t)sg.S * (q + 1) / 4);
+  for (int64_t ub = (int64_t)blockIdx.x * 64; ub < sg.units; ub += (int64_t)gridDim.x * 64) {
+    const int64_t u = ub + ul;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (u < nel) {
+      const int64_t m = u / nq, n = (u % nq) * 4;
+      const float* p = sg.part + m * sg.N + n;
+      for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
+        float4 w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          w[j] = s0 + j < s_hi ? *reinterpret_cast<const float4*>(p + (s0 + j) * stride)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (s0 + j < s_hi) { v.x += w[j].x; v.y += w[j].y; v.z += w[j].z; v.w += w[j].w; }
+      }
+    } else if (u < sg.units) {
+      const int64_t m = u - nel;
+      for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
+        float w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = s0 + j < s_hi ? sg.part_rs[(s0 + j) * sg.M + m] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (s0 + j < s_hi) v.x += w[j];
+      }
+    }
+    red[q][ul] = v;
+    __syncthreads();
+    if (q == 0 && u < sg.units) {
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float4 w = red[k][ul];
+        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+      }
+      if (u < nel) {
+        const int64_t m = u / nq, n = (u % nq) * 4;
+        float4* cp = reinterpret_cast<float4*>(sg.C + m * sg.ldc + n);
+        if (sg.acc) {
+          const float4 c = *cp;
+          v.x = c.x + v.x; v.y = c.y + v.y; v.z = c.z + v.z; v.w = c.w + v.w;
+        }
+        *cp = v;
+      } else {
+        const int64_t m = u - nel;
+        sg.rs[m] = sg.acc ? sg.rs[m] + v.x : v.x;
+      }
+    }
+    __syncthreads();
+  }
+}
 
 // ------------------------------------------- large token GEMM: 256x256x64 tiles, 8 waves
 // C[M,N] = epi(alpha · A[M,K] · B[N,K]ᵀ) for the mDeBERTa token GEMMs (M = B·S = 65,536,
@@ -1559,4 +1722,116 @@ extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t 
     default: launch_panel_t<8, 16, PE_LNBWD>(a, stream, ln); break;
   }
   return ttmi_check_launch("ttmi_linear_ln_bwd");
+}
+
+namespace {
+int wgrad_check(const ttmi_wgrad_desc* d) {
+  TTMI_REQUIRE(d != nullptr, "ttmi_wgrad: null descriptor");
+  TTMI_REQUIRE(d->R >= 0 && d->M > 0 && d->N > 0, "ttmi_wgrad: bad sizes");
+  TTMI_REQUIRE(d->dy && d->x && d->dw, "ttmi_wgrad: null operand");
+  TTMI_REQUIRE(d->M % 8 == 0 && d->N % 8 == 0, "ttmi_wgrad: M and N must be multiples of 8");
+  TTMI_REQUIRE(d->ld_dy >= d->M && d->ld_x >= d->N && d->ld_dw >= d->N && d->ld_dw % 4 == 0,
+               "ttmi_wgrad: bad leading dimensions");
+  TTMI_REQUIRE(al16(d->dy) && al16(d->x) && al16(d->dw) && d->ld_dy % 8 == 0 && d->ld_x % 8 == 0,
+               "ttmi_wgrad: operands must be 16-byte aligned");
+  return TTMI_OK;
+}
+
+FoldSeg fold_seg(const ttmi_wgrad_desc* d, const WgradPlan& p) {
+  FoldSeg f;
+  f.part = static_cast<const float*>(d->workspace);
+  f.part_rs = reinterpret_cast<const float*>(static_cast<const char*>(d->workspace) +
+                                             al256((int64_t)p.S * d->M * d->N * 4));
+  f.C = d->dw; f.rs = d->db;
+  f.M = d->M; f.N = d->N; f.ldc = d->ld_dw;
+  f.units = d->M * (d->N / 4) + (d->db ? d->M : 0);
+  f.base = 0;
+  f.S = p.S; f.acc = d->accumulate;
+  return f;
+}
+
+int launch_fold(FoldArgs& a, hipStream_t s) {
+  if (a.n == 0 || a.total == 0) return TTMI_OK;
+  int64_t umax = 0;
+  for (int k = 0; k < a.n; ++k) umax = std::max(umax, a.seg[k].units);
+  const int64_t bx = std::min<int64_t>((umax + 63) / 64, 2048);
+  hipLaunchKernelGGL(wgrad_fold_kernel, dim3((unsigned)bx, (unsigned)a.n), dim3(256), 0, s, a);
+  return ttmi_check_launch("ttmi_wgrad_fold");
+}
+}  // namespace
+
+extern "C" int64_t ttmi_wgrad_workspace(int64_t R, int64_t M, int64_t N, int64_t ld_dy,
+                                        int64_t ld_x) {
+  if (R <= 0 || M <= 0 || N <= 0) return 0;
+  return wgrad_ws_bytes(wgrad_plan(R, M, N, std::max(ld_dy, ld_x)), M, N);
+}
+
+extern "C" int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream) {
+  int rc = wgrad_check(d);
+  if (rc) return rc;
+  const WgradPlan p = wgrad_plan(d->R, d->M, d->N, std::max(d->ld_dy, d->ld_x));
+  if (d->R == 0) {                          // empty reduction: dW (+)= 0
+    if (d->accumulate) return TTMI_OK;
+    if (hipMemset2DAsync(d->dw, (size_t)d->ld_dw * 4, 0, (size_t)d->N * 4, (size_t)d->M, stream) != hipSuccess ||
+        (d->db && hipMemsetAsync(d->db, 0, (size_t)d->M * 4, stream) != hipSuccess)) {
+      ttmi_set_error("ttmi_wgrad: memset failed");
+      return TTMI_ERR_LAUNCH;
+    }
+    return TTMI_OK;
+  }
+  const int64_t need = wgrad_ws_bytes(p, d->M, d->N);
+  TTMI_REQUIRE(need == 0 || (d->workspace && d->workspace_bytes >= need && al16(d->workspace)),
+               "ttmi_wgrad: workspace of %lld bytes required", (long long)need);
+  WgradArgs a;
+  a.M = d->M; a.N = d->N; a.R = d->R;
+  a.A = static_cast<const char*>(d->dy); a.lda = d->ld_dy;
+  a.B = static_cast<const char*>(d->x); a.ldb = d->ld_x;
+  a.C = d->dw; a.ldc = d->ld_dw;
+  a.alpha = d->alpha;
+  a.rowsum_a = d->db;
+  a.rows_per_split = p.sps * 64;
+  a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n; a.splits = p.S;
+  a.xcd_remap = p.S % 8 == 0;
+  a.accumulate = d->accumulate;
+  a.mode = p.S > 1 ? WG_SLAB : WG_DIRECT;
+  a.part = static_cast<float*>(d->workspace);
+  a.part_rs = p.S > 1 ? reinterpret_cast<float*>(static_cast<char*>(d->workspace) +
+                                                  al256((int64_t)p.S * d->M * d->N * 4)) : nullptr;
+  const int64_t nwg = (int64_t)p.tiles_m * p.tiles_n * p.S;
+  TTMI_REQUIRE(nwg <= 2147483647LL, "ttmi_wgrad: grid too large");
+  if (p.tile == 32) hipLaunchKernelGGL((wgrad_kernel<32, 32, 4>), dim3((unsigned)nwg), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((wgrad_kernel<64, 64, 4>), dim3((unsigned)nwg), dim3(256), 0, stream, a);
+  rc = ttmi_check_launch("ttmi_wgrad");
+  if (rc || p.S <= 1 || d->defer) return rc;
+  FoldArgs f;
+  f.seg[0] = fold_seg(d, p);
+  f.n = 1;
+  f.total = f.seg[0].units;
+  return launch_fold(f, stream);
+}
+
+extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, hipStream_t stream) {
+  TTMI_REQUIRE(n >= 0 && (n == 0 || descs), "ttmi_wgrad_fold: bad arguments");
+  FoldArgs f;
+  f.n = 0;
+  f.total = 0;
+  for (int i = 0; i < n; ++i) {
+    const ttmi_wgrad_desc* d = descs[i];
+    int rc = wgrad_check(d);
+    if (rc) return rc;
+    const WgradPlan p = wgrad_plan(d->R, d->M, d->N, std::max(d->ld_dy, d->ld_x));
+    if (p.S <= 1 || d->R == 0) continue;     // written directly by ttmi_wgrad
+    TTMI_REQUIRE(d->workspace, "ttmi_wgrad_fold: descriptor %d has no workspace", i);
+    if (f.n == FOLD_SEGS) {
+      rc = launch_fold(f, stream);
+      if (rc) return rc;
+      f.n = 0;
+      f.total = 0;
+    }
+    FoldSeg sg = fold_seg(d, p);
+    sg.base = f.total;
+    f.seg[f.n++] = sg;
+    f.total += sg.units;
+  }
+  return launch_fold(f, stream);
 }

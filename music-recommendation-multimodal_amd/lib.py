@@ -42,6 +42,19 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class WgradDesc(ctypes.Structure):
+    """ttmi_wgrad_desc (include/ttmi.h)."""
+    _fields_ = [("R", c_i64), ("M", c_i64), ("N", c_i64),
+                ("dy", c_p), ("ld_dy", c_i64),
+                ("x", c_p), ("ld_x", c_i64),
+                ("dw", c_p), ("ld_dw", c_i64),
+                ("db", c_p),
+                ("alpha", c_f),
+                ("accumulate", c_i),
+                ("workspace", c_p), ("workspace_bytes", c_i64),
+                ("defer", c_i)]
+
+
 class ConvDesc(ctypes.Structure):
     """ttmi_conv_desc (include/ttmi.h)."""
     _fields_ = [("mode", c_i), ("N", c_i), ("H", c_i), ("W", c_i), ("C", c_i), ("Cin", c_i),
@@ -99,6 +112,9 @@ SIGNATURES = {
     "ttmi_last_error": (ctypes.c_char_p, []),
     "ttmi_abi_version": (c_i, []),
     "ttmi_gemm": (c_i, [ctypes.POINTER(GemmDesc), c_p]),
+    "ttmi_wgrad_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "ttmi_wgrad": (c_i, [ctypes.POINTER(WgradDesc), c_p]),
+    "ttmi_wgrad_fold": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_p]),
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
                                  c_i64, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),

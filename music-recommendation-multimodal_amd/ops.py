@@ -6,13 +6,14 @@ step can be captured into a HIP graph.  Shapes are checked here and again in C.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
 from . import lib as _L
-from .lib import BF16, F32, ConvDesc, DisAttnDesc, GemmDesc, LnBwdDesc, call
+from .lib import BF16, F32, ConvDesc, DisAttnDesc, GemmDesc, LnBwdDesc, WgradDesc, call
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -104,14 +105,74 @@ def linear_dx(dy: Tensor, w: Tensor, out: Tensor, *, gate: Optional[Tensor] = No
                 gate=gate, ld_gate=K, gate_scale=gate_scale, colsum=colsum)
 
 
+class WgradPending:
+    """Weight-gradient GEMMs whose split partials still sit in their workspaces (ttmi_wgrad
+    with defer = 1).  ``flush()`` folds them all in one ttmi_wgrad_fold launch; the
+    descriptors and workspaces stay referenced until then."""
+
+    def __init__(self):
+        self.items = []
+
+    def flush(self) -> None:
+        if not self.items:
+            return
+        arr = (ctypes.POINTER(WgradDesc) * len(self.items))(
+            *[ctypes.pointer(d) for d, *_ in self.items])
+        call("ttmi_wgrad_fold", len(self.items), arr, _s())
+        self.items = []
+
+
+_PENDING: List[WgradPending] = []
+
+
+@contextlib.contextmanager
+def deferred_wgrad():
+    """Inside the block, bf16 ``linear_dw`` calls defer their split folds to the yielded
+    WgradPending (flushed, at the latest, on exit): one fold launch per step instead of one
+    per weight gradient."""
+    pend = WgradPending()
+    _PENDING.append(pend)
+    try:
+        yield pend
+    finally:
+        _PENDING.pop()
+        pend.flush()
+
+
 def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
-              split_k: int = 0) -> Tensor:
+              split_k: int = 0, defer: bool = True) -> Tensor:
     """gw[N,K] += dy[M,N]ᵀ · x[M,K]; gb[N] += Σ_m dy[m,:] (nn.Linear weight and bias grads,
-    accumulated, split-K)."""
+    accumulated).  bf16 operands: ttmi_wgrad (split partials summed in a fixed order: the
+    result is bit-reproducible); fp32 operands: the generic split-K GEMM.  Inside
+    ``deferred_wgrad()`` the fold waits for the block's flush unless ``defer=False`` (callers
+    that read gw right away)."""
     M, N = dy.shape
     K = x.shape[1]
-    return gemm(dy, x, gw, N, K, M, lda=N, a_kmajor=False, ldb=K, b_kmajor=False, ldc=K,
-                accumulate=True, split_k=split_k, rowsum_a=gb)
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+        return gemm(dy, x, gw, N, K, M, lda=dy.stride(0), a_kmajor=False, ldb=x.stride(0),
+                    b_kmajor=False, ldc=gw.stride(0), accumulate=True, split_k=split_k,
+                    rowsum_a=gb)
+    _dev(dy, x, gw)
+    if gw.dtype != torch.float32 or (gb is not None and gb.dtype != torch.float32):
+        raise TypeError("linear_dw: weight / bias gradients must be fp32")
+    _L.load()
+    d = WgradDesc()
+    d.R, d.M, d.N = M, N, K
+    d.dy, d.ld_dy = _p(dy), dy.stride(0)
+    d.x, d.ld_x = _p(x), x.stride(0)
+    d.dw, d.ld_dw = _p(gw), gw.stride(0)
+    d.db = _p(gb)
+    d.alpha = 1.0
+    d.accumulate = 1
+    nbytes = int(_L._lib.ttmi_wgrad_workspace(M, N, K, d.ld_dy, d.ld_x))
+    ws = torch.empty(nbytes, device=dy.device, dtype=torch.uint8) if nbytes else None
+    d.workspace, d.workspace_bytes = _p(ws), nbytes
+    pend = _PENDING[-1] if (_PENDING and defer) else None
+    d.defer = int(pend is not None)
+    call("ttmi_wgrad", ctypes.byref(d), _s())
+    if pend is not None and nbytes:
+        pend.items.append((d, ws, dy, x, gw, gb))
+    return gw
 
 
 def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, ln_w: Tensor,

@@ -379,6 +379,10 @@ class TrainStep:
             modal = b["target_modal"]
         it, ist = F.item_fusion_fwd(self.Pi, self.Wi, modal, self.icfg, seeds,
                                     self.bufs, self.p_item)
+        with ops.deferred_wgrad() as pend:     # one fold launch for the step's weight grads
+            self._bwd(b, u, it, modal, ust, ist, rst if self.raw_items else None, cut, pend)
+
+    def _bwd(self, b, u, it, modal, ust, ist, rst, cut, pend) -> None:
         du = torch.empty_like(u)
         di = torch.empty_like(it)
         du16 = None
@@ -407,6 +411,7 @@ class TrainStep:
         if self.overlap:
             def hook(i: int) -> None:
                 if i == 1:       # every gradient before the tail slots is final
+                    pend.flush()
                     cut(self._sync_head)
         F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg, du16, on_layer_done=hook)
         self.loss, self.logits = loss, logits

@@ -820,3 +820,75 @@ def test_deb_ln_fwd_lora_dropout_outputs(gpu_pkg):
     torch.cuda.synchronize()
     assert torch.equal(yq, rq) and torch.equal(yv, rv)
     assert not torch.equal(yq, yv)
+
+
+@pytest.mark.parametrize("M,N,R,pad", [
+    (384, 128, 25600, 0), (128, 512, 25600, 0), (128, 128, 25600, 64), (176, 128, 512, 0),
+    (72, 200, 1000, 8), (512, 512, 512, 0), (64, 64, 100, 0), (136, 72, 777, 32), (8, 8, 1, 0),
+    (128, 128, 7, 0)])
+def test_wgrad_deterministic(gpu_pkg, M, N, R, pad):
+    """ttmi_wgrad (the nn.Linear weight gradient of every bf16 Linear): dw += dyᵀx over R rows
+    and db += Σ dy, with strided operands, partial tiles, short and long R; split partials are
+    summed in split order, so two runs (and a graph replay) agree bit for bit."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(M * 7 + N + R)
+    dy_full = torch.randn(R, M + 2 * pad, generator=g).to(torch.bfloat16).to(DEV)
+    x_full = torch.randn(R, N + pad, generator=g).to(torch.bfloat16).to(DEV)
+    dy = dy_full[:, pad:pad + M]
+    x = x_full[:, :N]
+    expect = 0.5 + dy.float().t() @ x.float()
+    outs = []
+    for _ in range(2):
+        gw = torch.full((M, N), 0.5, device=DEV)
+        gb = torch.full((M,), -1.0, device=DEV)
+        ops.linear_dw(dy, x, gw, gb)
+        outs.append((gw, gb))
+    torch.cuda.synchronize()
+    gw, gb = outs[0]
+    assert rel(gw, expect) < 5e-5, rel(gw, expect)
+    assert rel(gb, -1.0 + dy.float().sum(0)) < 5e-5
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    # a captured replay equals the eager result bit for bit
+    gw2 = torch.full((M, N), 0.5, device=DEV)
+    gb2 = torch.full((M,), -1.0, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            ops.linear_dw(dy, x, gw2, gb2)
+    torch.cuda.current_stream().wait_stream(s)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(gw2, gw) and torch.equal(gb2, gb)
+
+
+def test_wgrad_deferred_fold_many(gpu_pkg):
+    """deferred_wgrad(): eleven weight gradients (more than one fold launch's 8 segments) leave
+    their partials in workspaces and are completed by the block's flush; equal, bit for bit,
+    to the immediate path; defer=False inside the block completes at once."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(5)
+    shapes = [(384, 128, 25600), (128, 128, 2048), (512, 128, 4096), (128, 512, 3000)] * 3
+    shapes = shapes[:11]
+    ins = [(torch.randn(R, M, generator=g).to(torch.bfloat16).to(DEV),
+            torch.randn(R, N, generator=g).to(torch.bfloat16).to(DEV)) for M, N, R in shapes]
+    ref_out = []
+    for dy, x in ins:
+        gw = torch.zeros(dy.shape[1], x.shape[1], device=DEV)
+        gb = torch.zeros(dy.shape[1], device=DEV)
+        ops.linear_dw(dy, x, gw, gb)
+        ref_out.append((gw, gb))
+    outs = []
+    with ops.deferred_wgrad() as pend:
+        for k, (dy, x) in enumerate(ins):
+            gw = torch.zeros(dy.shape[1], x.shape[1], device=DEV)
+            gb = torch.zeros(dy.shape[1], device=DEV)
+            ops.linear_dw(dy, x, gw, gb, defer=(k != 3))
+            outs.append((gw, gb))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[3][0], ref_out[3][0])          # defer=False: already complete
+        assert len(pend.items) >= 9
+    torch.cuda.synchronize()
+    for (a, b), (c, d) in zip(outs, ref_out):
+        assert torch.equal(a, c) and torch.equal(b, d)

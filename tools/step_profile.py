@@ -27,3 +27,10 @@ busy = sum(tot.values())
 print(f"step: {len(step)} dispatches, wall {wall:.1f} us, kernel busy {busy:.1f} us")
 for n, t in sorted(tot.items(), key=lambda x: -x[1])[:top]:
     print(f"{t:10.1f} us {100 * t / busy:5.1f}% {cnt[n]:5d}x {t / cnt[n]:9.2f} us  {n[:90]}")
+if len(sys.argv) > 4 and sys.argv[4] == "seq":          # the step's dispatches in order
+    t0 = int(step[0]["Start_Timestamp"])
+    for r in step:
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+        n = n.split("(")[0] if not n.startswith("void ") else n[5:].split("(")[0]
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.2f}  {n[:80]}")
