@@ -575,6 +575,12 @@ int ttmi_cover_prep(int B, int H, int W, const uint8_t* img, int64_t ld_img, int
  * counts as -inf (the padding item, evaluate_metrics.py:157).  K <= 64, K <= V. */
 int ttmi_topk_rows(int R, int V, int K, const float* scores, int64_t ld, int skip_first,
                    float* out_val, int64_t* out_idx, hipStream_t stream);
+/* Catalogue index rows (evaluate_metrics.py:58-104 compute_all_item_embeddings,
+ * inference.py:175-201 index_catalog): for each of n item-tower outputs x [n][ldx] (fp32),
+ * e = x / max(|x|, 1e-12) (get_item_embedding), NaN -> 0, e / max(|e|, 1e-8), written to row
+ * ids[r] of the dense [V][D] index (ids outside [0, V) skipped; other rows untouched).  ABI 10. */
+int ttmi_catalogue_rows(int n, int D, const float* x, int64_t ldx, const int64_t* ids, int64_t V,
+                        float* dense, hipStream_t stream);
 /* scores[r, ids[r, j]] = -inf for j < Lh and 0 <= id < V (serving: exclude the user's history,
  * reference src/inference.py:294-303). */
 int ttmi_mask_items(int R, int V, float* scores, int64_t ld, const int64_t* ids, int Lh,

@@ -226,6 +226,46 @@ __global__ __launch_bounds__(256) void mask_items_kernel(int R, int V, float* __
 
 }  // namespace
 
+// Catalogue index rows (evaluate_metrics.py:58-104, inference.py:175-201): per item row
+// e = get_item_embedding's F.normalize(x) (eps 1e-12); NaN -> 0 (nan_to_num, :76-78); e /
+// max(|e|, 1e-8) (:82); dense[ids[r]] = e.  One wave per row.
+__global__ __launch_bounds__(256) void catalogue_rows_kernel(int n, int D, const float* __restrict__ x,
+                                                             int64_t ldx, const int64_t* __restrict__ ids,
+                                                             int64_t V, float* __restrict__ dense) {
+  const int lane = threadIdx.x & 63;
+  const int r = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (r >= n) return;
+  const int64_t id = ids[r];
+  if (id < 0 || id >= V) return;
+  const float* xr = x + (int64_t)r * ldx;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += xr[c] * xr[c];
+  const float inv1 = 1.f / fmaxf(sqrtf(wave_sum(s)), 1e-12f);
+  float s2 = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    float e = xr[c] * inv1;
+    if (e != e) e = 0.f;
+    s2 += e * e;
+  }
+  const float inv2 = 1.f / fmaxf(sqrtf(wave_sum(s2)), 1e-8f);
+  float* dr = dense + id * (int64_t)D;
+  for (int c = lane; c < D; c += 64) {
+    float e = xr[c] * inv1;
+    if (e != e) e = 0.f;
+    dr[c] = e * inv2;
+  }
+}
+
+extern "C" int ttmi_catalogue_rows(int n, int D, const float* x, int64_t ldx, const int64_t* ids,
+                                   int64_t V, float* dense, hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && D > 0 && ldx >= D && V > 0, "ttmi_catalogue_rows: bad sizes");
+  if (n == 0) return TTMI_OK;
+  TTMI_REQUIRE(x && ids && dense, "ttmi_catalogue_rows: null argument");
+  hipLaunchKernelGGL(catalogue_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, D, x, ldx, ids,
+                     V, dense);
+  return ttmi_check_launch("ttmi_catalogue_rows");
+}
+
 extern "C" int ttmi_mask_items(int R, int V, float* scores, int64_t ld, const int64_t* ids, int Lh,
                                hipStream_t s) {
   TTMI_REQUIRE(R > 0 && V > 0 && Lh > 0 && ld >= V && scores && ids, "ttmi_mask_items: bad argument");

@@ -112,6 +112,7 @@ SIGNATURES = {
     "ttmi_last_error": (ctypes.c_char_p, []),
     "ttmi_abi_version": (c_i, []),
     "ttmi_gemm": (c_i, [ctypes.POINTER(GemmDesc), c_p]),
+    "ttmi_catalogue_rows": (c_i, [c_i, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "ttmi_wgrad_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64, c_i64]),
     "ttmi_wgrad": (c_i, [ctypes.POINTER(WgradDesc), c_p]),
     "ttmi_wgrad_fold": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_p]),

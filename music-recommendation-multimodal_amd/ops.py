@@ -818,6 +818,21 @@ def rank_of(idx: Tensor, target: Tensor, rank: Tensor) -> Tensor:
     return rank
 
 
+def catalogue_rows(x: Tensor, ids: Tensor, dense: Tensor) -> Tensor:
+    """dense[ids[r]] = normalize(nan_to_num(normalize(x[r], 1e-12)), 1e-8) (the indexers'
+    per-batch tail, evaluate_metrics.py:58-104)."""
+    _dev(x, ids, dense)
+    if x.dtype != torch.float32 or dense.dtype != torch.float32 or ids.dtype != torch.int64:
+        raise TypeError("catalogue_rows: fp32 rows and index, int64 ids")
+    if x.stride(1) != 1 or not dense.is_contiguous() or not ids.is_contiguous():
+        raise ValueError("catalogue_rows: rows must be unit-stride, index and ids contiguous")
+    n, D = x.shape
+    if dense.shape[1] != D or ids.shape[0] != n:
+        raise ValueError("catalogue_rows: shape mismatch")
+    call("ttmi_catalogue_rows", n, D, _p(x), x.stride(0), _p(ids), dense.shape[0], _p(dense), _s())
+    return dense
+
+
 def mask_items(scores: Tensor, ids: Tensor) -> Tensor:
     """scores[r, ids[r, j]] = -inf (ids int64 [R, Lh]; out-of-range ids ignored)."""
     R, V = scores.shape

@@ -107,8 +107,16 @@ class GlobalEvaluator:
         b = {k: batch[k].to(dev, non_blocking=True) for k in self.KEYS if batch.get(k) is not None}
         self.model.eval()
         with torch.no_grad():
+            opkey = None
             if self._tower is not None:
-                self._tower.inference_operands()             # refresh cached weights (host check)
+                P, W = self._tower.inference_operands()      # refresh cached weights (host check)
+                # a graph replays the buffers it was captured on: when the cache rebuilt them
+                # (new storages, e.g. TrainStep re-homed the parameters), every graph is stale
+                opkey = tuple(t.data_ptr() for t in P.values()) + \
+                    tuple(t.data_ptr() for t in W.values())
+                if opkey != getattr(self, "_opkey", None):
+                    self._graphs.clear()
+                    self._opkey = opkey
             if not self.use_graph:
                 return self._run(b)
             sig = tuple((k, tuple(t.shape), t.dtype) for k, t in sorted(b.items()))
@@ -129,6 +137,86 @@ class GlobalEvaluator:
             ops.batch_copy([static[k] for k in static], [b[k].contiguous() for k in static])
             graph.replay()
             return out
+
+
+class CatalogueIndexer:
+    """The catalogue index of compute_all_item_embeddings (evaluate_metrics.py:24-104) and
+    index_catalog (inference.py:137-209): every item's tower embedding (model.eval(): BatchNorm
+    on running statistics, no dropout), L2-normalised as get_item_embedding does, NaN -> 0,
+    normalised again with eps 1e-8, scattered into a dense [vocab_size, D] table whose row i is
+    item id i (row 0, padding, and items never seen stay 0).  The table stays on the device
+    (it feeds GlobalEvaluator / recommend directly).  Per batch: the item-tower forward and
+    the fused normalise-and-scatter kernel (ttmi_catalogue_rows), replayed from one HIP graph
+    per batch signature; the batch carries ``target_id`` and the item inputs under the
+    reference's keys (``target_image``, ``target_audio``, ``target_input_ids``,
+    ``target_attention_mask``, ``target_tabular``) or cfg 2's ``target_modal``."""
+
+    KEYS = ("target_id", "target_modal", "target_image", "target_audio", "target_input_ids",
+            "target_attention_mask", "target_tabular")
+
+    def __init__(self, model, vocab_size: int, device=None, use_graph: bool = True):
+        self.model = model
+        self.vocab_size = vocab_size
+        self.device = device if device is not None else next(model.parameters()).device
+        self.use_graph = use_graph
+        D = model.item_tower.embedding_dim
+        self.dense = torch.zeros(vocab_size, D, device=self.device)
+        self._graphs: Dict[tuple, tuple] = {}
+
+    def _item(self, b: Dict[str, Tensor]) -> Tensor:
+        it = self.model.item_tower
+        if "target_modal" in b:
+            return it.fuse(b["target_modal"])
+        return it(images=b.get("target_image"), audio=b.get("target_audio"),
+                  input_ids=b.get("target_input_ids"),
+                  attention_mask=b.get("target_attention_mask"), tabular=b["target_tabular"])
+
+    def _run(self, b: Dict[str, Tensor]) -> None:
+        emb = self._item(b).float()
+        ops.catalogue_rows(emb, b["target_id"].long().contiguous(), self.dense)
+
+    def add(self, batch: Dict[str, Tensor]) -> None:
+        """Index one batch of items."""
+        dev = self.device
+        b = {k: batch[k].to(dev, non_blocking=True) for k in self.KEYS if batch.get(k) is not None}
+        b["target_id"] = b["target_id"].long()
+        self.model.eval()
+        with torch.no_grad():
+            if not self.use_graph:
+                self._run(b)
+                return
+            sig = tuple((k, tuple(t.shape), t.dtype) for k, t in sorted(b.items()))
+            ent = self._graphs.get(sig)
+            if ent is None:
+                static = {k: t.clone() for k, t in b.items()}
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):              # warm-up: code objects, pool sizes
+                    self._run(static)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                torch.cuda.synchronize(dev)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    self._run(static)
+                ent = self._graphs[sig] = (static, graph)
+            static, graph = ent
+            ops.batch_copy([static[k] for k in static], [b[k].contiguous() for k in static])
+            graph.replay()
+
+    def index(self, loader: Iterable) -> Tensor:
+        """Zero the table, index every batch of ``loader``, return the dense [V, D] index."""
+        self.dense.zero_()
+        for batch in loader:
+            self.add(batch)
+        return self.dense
+
+
+def compute_all_item_embeddings(model, loader: Iterable, vocab_size: int, device=None,
+                                use_graph: bool = True) -> Tuple[Tensor, int]:
+    """evaluate_metrics.py:24-104's result, (dense [vocab_size, D], vocab_size), from a loader
+    over the unique catalogue items (the reference builds that loader from its dataset)."""
+    ix = CatalogueIndexer(model, vocab_size, device, use_graph=use_graph)
+    return ix.index(loader), vocab_size
 
 
 def calculate_metrics_global(model, val_loader: Iterable, item_embeddings: Tensor, device,

@@ -74,8 +74,13 @@ def init_resnet18(in_ch: int, out_dim: int, generator: torch.Generator,
     return p
 
 
-def _bn(x: Tensor, p: Dict[str, Tensor], name: str, update: bool) -> Tensor:
+def _bn(x: Tensor, p: Dict[str, Tensor], name: str, update) -> Tensor:
+    """Train-mode BatchNorm (batch statistics; running buffers updated when ``update``), or
+    eval mode (``update == "eval"``: the running statistics)."""
     rm, rv = p.get(name + ".running_mean"), p.get(name + ".running_var")
+    if update == "eval":
+        return F.batch_norm(x, rm, rv, p[name + ".weight"], p[name + ".bias"], training=False,
+                            eps=1e-5)
     if not update:
         rm = rv = None
     return F.batch_norm(x, rm, rv, p[name + ".weight"], p[name + ".bias"], training=True,
@@ -119,12 +124,15 @@ def tabular_forward(p: Dict[str, Tensor], x: Tensor, prefix: str = "mlp.", p_dro
 def item_tower_raw_forward(p: Dict[str, Tensor], batch: Dict[str, Tensor], p_drop: float = 0.0,
                            drop=None, running: Optional[Dict[str, Tensor]] = None,
                            text_dim: int = 128, update_running: bool = False,
-                           text_cfg=None) -> Tensor:
+                           text_cfg=None, eval_mode: bool = False) -> Tensor:
     """MultimodalItemEncoder.forward (item_tower.py:131-152) for cfg 3: audio ResNet-18 on
     ``target_audio``, visual ResNet-18 on ``target_image``, a zero text slot (or, with
     ``text_cfg``, the cfg-4 mDeBERTa-LoRA TextEncoder of deberta_ref), the tabular MLP on ``target_tabular``; concatenated in the reference's
     fixed order (:147) into the fusion head.  ``p`` holds item-tower names without the
-    ``item_tower.`` prefix."""
+    ``item_tower.`` prefix.  eval_mode: every BatchNorm on its running statistics (``p`` holds
+    them, ``running`` the fusion head's), dropout off — the indexers' model.eval()."""
+    if eval_mode:
+        update_running, p_drop = "eval", 0.0
     audio = resnet18_forward(p, batch["target_audio"], "audio_encoder.backbone.", update_running)
     visual = resnet18_forward(p, batch["target_image"], "visual_encoder.backbone.",
                               update_running)
@@ -138,7 +146,7 @@ def item_tower_raw_forward(p: Dict[str, Tensor], batch: Dict[str, Tensor], p_dro
     tab = tabular_forward(p, batch["target_tabular"], "tabular_encoder.mlp.", p_drop, drop,
                           update_running)
     modal = torch.cat([audio, visual, text, tab], dim=1)
-    return ttr.item_fusion_forward(p, modal, p_drop, drop, running)
+    return ttr.item_fusion_forward(p, modal, p_drop, drop, running, eval_mode=eval_mode)
 
 
 def synthetic_items(B: int, tabular_dim: int, mel=(128, 256), cover=(224, 224),

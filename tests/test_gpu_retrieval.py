@@ -166,3 +166,117 @@ def test_recommend_matches_oracle_inference(gpu_pkg):
     assert torch.equal(idx.cpu(), ri)
     assert torch.allclose(val.cpu(), rv, atol=1e-4)
     assert not any(int(i) in set(h[r].tolist()) for r in range(6) for i in idx[r].cpu())
+
+
+def test_global_evaluator_after_trainstep_rehomes_params(gpu_pkg):
+    """An evaluator built BEFORE TrainStep (which re-homes every parameter into its flat
+    buffer, new storages) and used again after training steps scores with the trained weights:
+    its graphs are keyed by the cached operand buffers and recaptured when they change."""
+    from oracle import two_tower_ref as ref
+    torch.manual_seed(0)
+    V, D = 500, 128
+    m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128,
+                              num_genders=3, num_countries=8, max_seq_len=50,
+                              user_embedding_dim=D, item_embedding_dim=D).to(DEV)
+    g = torch.Generator().manual_seed(4)
+    items = torch.nn.functional.normalize(torch.randn(V, D, generator=g), dim=1).to(DEV)
+    rt = gpu_pkg.retrieval
+    ev = rt.GlobalEvaluator(m, items, 20)
+    b = ref.synthetic_batch(64, 50, V, 3, 8, generator=g)
+    b["target_id"] = torch.randint(1, V, (64,), generator=g)
+    ev.ranks(b)
+    step = gpu_pkg.TrainStep(m, lr=1e-2)
+    m.train()
+    tb = {k: v.to(DEV) for k, v in ref.synthetic_batch(64, 50, V, 3, 8, generator=g).items()}
+    for _ in range(3):
+        step.step(tb)
+    torch.cuda.synchronize()
+    eager = rt.GlobalEvaluator(m, items, 20, use_graph=False)
+    with torch.no_grad():
+        u = m.get_user_embedding(b["history_ids"].to(DEV), b["history_mask"].to(DEV),
+                                 b["user_gender"].to(DEV), b["user_country"].to(DEV))
+    b["target_id"][::2] = rt.topk_items(u, items, 20)[1].cpu()[::2, 3]
+    got = ev.ranks(b).clone()
+    assert torch.equal(got.cpu(), eager.ranks(b).cpu())
+    assert (got[::2] < 20).float().mean() > 0.9
+
+
+def _oracle_index(item_out, ids, V):
+    e = torch.nn.functional.normalize(item_out, dim=1)                    # get_item_embedding
+    e = torch.nan_to_num(e, nan=0.0)
+    e = torch.nn.functional.normalize(e, p=2, dim=1, eps=1e-8)
+    dense = torch.zeros(V, e.shape[1])
+    dense[ids] = e
+    return dense
+
+
+def _randomise_bn(m, g):
+    with torch.no_grad():
+        for n, b in m.named_buffers():
+            if n.endswith("running_mean"):
+                b.copy_(torch.randn(b.shape, generator=g) * 0.1)
+            elif n.endswith("running_var"):
+                b.copy_(0.5 + torch.rand(b.shape, generator=g))
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_catalogue_indexer_precomputed_vs_oracle(gpu_pkg, use_graph):
+    """compute_all_item_embeddings / index_catalog (evaluate_metrics.py:24-104): fp32 fusion head
+    in eval mode (BatchNorm on running statistics), three batches (8, 8, 5 items; a ragged
+    last batch gets its own graph), 15 ids never indexed: rows match the oracle to 1e-5, row 0
+    and unseen rows are 0, and a second pass is bit-identical."""
+    from oracle import two_tower_ref as ref
+    torch.manual_seed(0)
+    V, D = 37, 64
+    m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128,
+                              user_embedding_dim=D, item_embedding_dim=D,
+                              compute_dtype=torch.float32).to(DEV)
+    g = torch.Generator().manual_seed(6)
+    _randomise_bn(m, g)
+    ids = torch.randperm(V - 1, generator=g)[:21] + 1
+    modal = torch.randn(21, 512, generator=g)
+    loader = [{"target_id": ids[s:s + 8], "target_modal": modal[s:s + 8]} for s in (0, 8, 16)]
+    ix = gpu_pkg.retrieval.CatalogueIndexer(m, V, use_graph=use_graph)
+    dense = ix.index(loader).clone()
+    p = {k[len("item_tower."):]: v.detach().cpu() for k, v in m.named_parameters()
+         if k.startswith("item_tower.")}
+    running = {k[len("item_tower.fusion_layer.1."):]: v.detach().cpu()
+               for k, v in m.named_buffers() if k.startswith("item_tower.fusion_layer.1.")}
+    out = ref.item_fusion_forward(p, modal, running=running, eval_mode=True)
+    want = _oracle_index(out, ids, V)
+    assert (dense[0] == 0).all()
+    seen = torch.zeros(V, dtype=torch.bool)
+    seen[ids] = True
+    assert (dense.cpu()[~seen] == 0).all()
+    assert (dense.cpu() - want).abs().max().item() < 1e-5
+    again = ix.index(loader)
+    assert torch.equal(again, dense)
+    if use_graph:
+        assert len(ix._graphs) == 2
+
+
+def test_catalogue_indexer_raw_items_vs_oracle(gpu_pkg):
+    """The index over raw item inputs (ResNet-18 audio + visual, tabular, zero text slot,
+    fusion head) in eval mode vs the oracle item tower in eval mode (bf16 storage: 3e-2 on the
+    unit rows)."""
+    from oracle import resnet_ref as rref
+    torch.manual_seed(0)
+    V, D, T = 29, 128, 32
+    m = gpu_pkg.TwoTowerModel(vocab_size=V, tabular_input_dim=T, user_embedding_dim=D,
+                              item_embedding_dim=D, with_text=False).to(DEV)
+    g = torch.Generator().manual_seed(8)
+    _randomise_bn(m, g)
+    ids = torch.arange(1, 17)
+    items = rref.synthetic_items(16, T, (32, 64), (32, 32), generator=g)
+    loader = [{"target_id": ids[s:s + 8], **{k: v[s:s + 8] for k, v in items.items()}}
+              for s in (0, 8)]
+    dense = gpu_pkg.retrieval.CatalogueIndexer(m, V).index(loader)
+    p = {k[len("item_tower."):]: v.detach().cpu() for k, v in m.state_dict().items()
+         if k.startswith("item_tower.")}
+    running = {k[len("fusion_layer.1."):]: v for k, v in p.items()
+               if k.startswith("fusion_layer.1.")}
+    out = rref.item_tower_raw_forward(p, items, running=running, eval_mode=True)
+    want = _oracle_index(out, ids, V)
+    err = (dense.cpu() - want).abs().max().item()
+    assert err < 3e-2, err
+    assert (dense[17:] == 0).all() and (dense[0] == 0).all()
