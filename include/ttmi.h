@@ -109,7 +109,16 @@ typedef struct {
 } ttmi_wgrad_desc;
 int64_t ttmi_wgrad_workspace(int64_t R, int64_t M, int64_t N, int64_t ld_dy, int64_t ld_x);
 int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream);
-int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, hipStream_t stream);
+/* Generic split fold: C[m*ldc + n] (+)= Σ_{s < S, in order} part[s*s_stride + m*N + n]. */
+typedef struct {
+  const float* part; int64_t S, s_stride, M, N;
+  float* C; int64_t ldc;
+  int accumulate;
+} ttmi_fold_desc;
+/* Completes the deferred ttmi_wgrad calls `descs` and the generic folds `folds` (one launch
+ * per 16 segments). */
+int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                    const ttmi_fold_desc* folds, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0) — TransformerEncoderLayer
@@ -380,7 +389,12 @@ typedef struct ttmi_linear_ln_bwd_desc {
   void* next; int64_t ld_next;          /* bf16 [M, N] or NULL */
   float drop_p; const uint64_t* drop_seed; int64_t ld_drop; const int32_t* drop_rows;
   float* ln_dw; float* ln_db;           /* [N], accumulated */
+  float* sum_ws;   /* ABI 10; NULL: ln_dw / ln_db take float atomics.  Else [G][2][N] fp32 with
+                      G = ttmi_linear_ln_bwd_sum_blocks(M): each workgroup's dw row and db row,
+                      plain stores; ln_dw / ln_db are then left to a fold (ttmi_wgrad_fold with
+                      {part = sum_ws (+ N for db), S = G, s_stride = 2N, M = 1}): deterministic. */
 } ttmi_linear_ln_bwd_desc;
+int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M);
 int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream);
 /* Fused residual sub-block end + the next LayerNorm (N = 128, K % 128 == 0, K <= 512):
  *   out = residual + dropout(x · wᵀ + bias)   (fp32 [M, 128]; dropout keep index m*ld_drop + n)

@@ -356,6 +356,7 @@ struct LnBwdArgs {
   bf16_t* next; int64_t ld_next;
   DropParams drop; int64_t ld_drop; const int32_t* drop_rows;
   float* dw; float* db;
+  float* sum_ws;   // non-NULL: per-workgroup dw / db sums to sum_ws[blockIdx][2][N] (no atomics)
   // PE_RESLN (forward): y = LN(C row) * w + lnb -> bf16 y, per-row mean / rstd
   const float* lnb; float eps; bf16_t* y; int64_t ldy; float* mean_out; float* rstd_out;
 };
@@ -374,12 +375,37 @@ TTMI_DEV float row16_sum(float v) {
 }
 
 
+// The LayerNorm-backward epilogue's row operands (x, residual, mean, rstd), loaded at the
+// start of the tile so their latency hides under the MFMAs (rows clamped: unconditional).
+struct LnBwdRow {
+  float4 x[8];
+  float4 r[8];
+  float mu, rs;
+};
+
+TTMI_DEV void panel_ln_bwd_load(const LnBwdArgs& ln, int64_t m, int64_t M, int lg, LnBwdRow& o) {
+  const int64_t mc = std::min<int64_t>(m, M - 1);
+  o.mu = ln.mean[mc];
+  o.rs = ln.rstd[mc];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int n = 32 * p + 8 * lg;
+    o.x[2 * p] = *reinterpret_cast<const float4*>(ln.x + mc * ln.ldx + n);
+    o.x[2 * p + 1] = *reinterpret_cast<const float4*>(ln.x + mc * ln.ldx + n + 4);
+    if (ln.res) {
+      o.r[2 * p] = *reinterpret_cast<const float4*>(ln.res + mc * ln.ld_res + n);
+      o.r[2 * p + 1] = *reinterpret_cast<const float4*>(ln.res + mc * ln.ld_res + n + 4);
+    }
+  }
+}
+
 // LayerNorm-backward epilogue of one 16-row tile (N = 128): lane (li, lg) holds row li,
 // columns 32p + 8lg + e (p < 4, e < 8) of dY in acc (column-paired tiles 2p, 2p+1).
 TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, const f32x4_t (&acc)[8],
                                     int64_t m, bool mok, int li, int lg, const float* sw,
-                                    float* sdw, float* sdb, const DropKeys& dk2) {
-  const float mu = mok ? ln.mean[m] : 0.f, rs = mok ? ln.rstd[m] : 0.f;
+                                    float* sdw, float* sdb, const DropKeys& dk2,
+                                    const LnBwdRow& pre) {
+  const float mu = mok ? pre.mu : 0.f, rs = mok ? pre.rs : 0.f;
   float dy[32], xh[32];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -387,8 +413,7 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
     const int n = 32 * p + 8 * lg;
     float xr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (mok) {
-      const float4 x0 = *reinterpret_cast<const float4*>(ln.x + m * ln.ldx + n);
-      const float4 x1 = *reinterpret_cast<const float4*>(ln.x + m * ln.ldx + n + 4);
+      const float4 x0 = pre.x[2 * p], x1 = pre.x[2 * p + 1];
       xr[0] = x0.x; xr[1] = x0.y; xr[2] = x0.z; xr[3] = x0.w;
       xr[4] = x1.x; xr[5] = x1.y; xr[6] = x1.z; xr[7] = x1.w;
     }
@@ -418,8 +443,7 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = rs * (dy[8 * p + e] * sw[n + e] - c1 - xh[8 * p + e] * c2);
       if (ln.res) {
-        const float4 r0 = *reinterpret_cast<const float4*>(ln.res + m * ln.ld_res + n);
-        const float4 r1 = *reinterpret_cast<const float4*>(ln.res + m * ln.ld_res + n + 4);
+        const float4 r0 = pre.r[2 * p], r1 = pre.r[2 * p + 1];
         o[0] += r0.x; o[1] += r0.y; o[2] += r0.z; o[3] += r0.w;
         o[4] += r1.x; o[5] += r1.y; o[6] += r1.z; o[7] += r1.w;
       }
@@ -474,12 +498,29 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
 #pragma unroll
     for (int c = 0; c < 4; ++c) a0[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
   }
-  {   // W -> LDS, coalesced 16-byte chunks
-    constexpr int CPR = K / 8;
-    for (int i = tid; i < N * CPR; i += 512) {
-      const int n = i / CPR, j = i % CPR;
-      *reinterpret_cast<uint4*>(smem + n * WP + j * 16) =
-          *reinterpret_cast<const uint4*>(g.B + ((int64_t)n * g.ldb + 8 * j) * 2);
+  {   // W -> LDS, coalesced 16-byte chunks, 8 loads in flight per thread before the LDS
+      // writes (a load -> wait -> write loop pays one memory round trip per chunk: 16 round
+      // trips for a 128 KB W image, which used to be most of the kernel's time)
+    constexpr int CPR = K / 8, TOT = N * CPR, PER = (TOT + 511) / 512, BATCH = 8;
+#pragma unroll
+    for (int j0 = 0; j0 < PER; j0 += BATCH) {
+      uint4 wv[BATCH];
+#pragma unroll
+      for (int j = 0; j < BATCH; ++j) {
+        const int i = tid + 512 * (j0 + j);
+        if (j0 + j < PER && i < TOT) {
+          const int n = i / CPR, c = i % CPR;
+          wv[j] = *reinterpret_cast<const uint4*>(g.B + ((int64_t)n * g.ldb + 8 * c) * 2);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < BATCH; ++j) {
+        const int i = tid + 512 * (j0 + j);
+        if (j0 + j < PER && i < TOT) {
+          const int n = i / CPR, c = i % CPR;
+          *reinterpret_cast<uint4*>(smem + n * WP + c * 16) = wv[j];
+        }
+      }
     }
     if constexpr (LNB) {
       for (int i = tid; i < N; i += 512) { sbias[i] = ln.w[i]; sdw[i] = 0.f; sdb[i] = 0.f; }
@@ -499,10 +540,18 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
 
   // W fragment base for this lane (column-paired: tile 2p slot 4q+r <-> column 32p+8q+r)
   const int wrow = 8 * (li >> 2) + (li & 3);
+  // A fragments run one k group ahead, across column groups and across tiles: group cq+1's
+  // loads (or the next column group's / next tile's first group) are in flight under group
+  // cq's MFMAs and the epilogue, so no tile starts with an exposed memory latency
+  uint4 a[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) a[c] = a0[c];
   for (int64_t tile = tile_beg + wave; tile < tile_end; tile += 8) {
     const int64_t m = tile * 16 + li;
     const bool mok = m < g.M;
     const char* ap = g.A + (std::min<int64_t>(m, g.M - 1) * g.lda + lg * (K / 4)) * 2;
+    // the next tile's rows (clamped: past the last tile the prefetch is a harmless re-load)
+    const char* ap_next = g.A + (std::min<int64_t>(m + 128, g.M - 1) * g.lda + lg * (K / 4)) * 2;
     // column groups of 128 (8 MFMA tiles) and k groups of 4 chunks keep the accumulator,
     // A and W fragment state bounded (A re-reads per column group hit L1/L2)
 #pragma unroll 1
@@ -511,22 +560,14 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       const char* wb = smem + (cg * 128 + wrow) * WP + lg * (K / 2);
-      // A fragments one k group ahead: group cq+1's loads are in flight under group cq's
-      // MFMAs (two memory latencies overlap instead of one per group)
-      uint4 a[4];
-      if (tile == tile0 && cg == 0) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) a[c] = a0[c];
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
-      }
+      LnBwdRow pre;
+      if constexpr (LNB) panel_ln_bwd_load(ln, m, g.M, lg, pre);
 #pragma unroll 1
       for (int cq = 0; cq < KC / 4; ++cq) {
         uint4 an[4];
-        const int cn = cq + 1 < KC / 4 ? cq + 1 : cq;      // last group: harmless re-load
+        const char* src = cq + 1 < KC / 4 ? ap + 64 * (cq + 1) : (cg + 1 < NT / 8 ? ap : ap_next);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const uint4*>(ap + 64 * cn + 16 * c);
+        for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const uint4*>(src + 16 * c);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
 #pragma unroll
@@ -539,7 +580,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
         for (int c = 0; c < 4; ++c) a[c] = an[c];
       }
       if constexpr (LNB) {
-        panel_ln_bwd_epilogue(g, ln, acc, m, mok, li, lg, sbias, sdw, sdb, dk2);
+        panel_ln_bwd_epilogue(g, ln, acc, m, mok, li, lg, sbias, sdw, sdb, dk2, pre);
         continue;
       }
       if (!mok) continue;
@@ -632,9 +673,14 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   }
   if constexpr (LNB) {
     __syncthreads();
-    for (int i = tid; i < N; i += 512) {
-      if (ln.dw) atomicAdd(ln.dw + i, sdw[i]);
-      if (ln.db) atomicAdd(ln.db + i, sdb[i]);
+    if (ln.sum_ws) {            // deterministic: folded later in workgroup order (ttmi_fold)
+      float* o = ln.sum_ws + (int64_t)blockIdx.x * 2 * N;
+      for (int i = tid; i < N; i += 512) { o[i] = sdw[i]; o[N + i] = sdb[i]; }
+    } else {
+      for (int i = tid; i < N; i += 512) {
+        if (ln.dw) atomicAdd(ln.dw + i, sdw[i]);
+        if (ln.db) atomicAdd(ln.db + i, sdb[i]);
+      }
     }
   }
 }
@@ -1041,10 +1087,10 @@ int64_t wgrad_ws_bytes(const WgradPlan& p, int64_t M, int64_t N) {
   return al256((int64_t)p.S * M * N * 4) + al256((int64_t)p.S * M * 4);
 }
 
-constexpr int FOLD_SEGS = 8;
+constexpr int FOLD_SEGS = 16;
 struct FoldSeg {
   const float* part; const float* part_rs; float* C; float* rs;
-  int64_t M, N, ldc, units, base;
+  int64_t M, N, ldc, units, base, s_stride;   // s_stride: elements between split slabs
   int S, acc;
 };
 struct FoldArgs { FoldSeg seg[FOLD_SEGS]; int n; int64_t total; };
@@ -1060,11 +1106,12 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   FoldSeg sg;
   sg.part = sgk.part; sg.part_rs = sgk.part_rs; sg.C = sgk.C; sg.rs = sgk.rs;
   sg.M = sgk.M; sg.N = sgk.N; sg.ldc = sgk.ldc; sg.units = sgk.units; sg.base = 0;
+  sg.s_stride = sgk.s_stride;
   sg.S = sgk.S; sg.acc = sgk.acc;
   __shared__ float4 red[4][64];
   const int ul = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int64_t nq = sg.N / 4, nel = sg.M * nq;
-  const int64_t stride = sg.M * sg.N;
+  const int64_t stride = sg.s_stride;
   const int s_lo = (int)((int64_t)sg.S * q / 4), s_hi = (int)((int64_t)sg.S * (q + 1) / 4);
   for (int64_t ub = (int64_t)blockIdx.x * 64; ub < sg.units; ub += (int64_t)gridDim.x * 64) {
     const int64_t u = ub + ul;
@@ -1715,6 +1762,7 @@ extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t 
   ln.drop = make_drop(d->drop_p, d->drop_seed); ln.ld_drop = d->ld_drop ? d->ld_drop : 128;
   ln.drop_rows = d->drop_rows;
   ln.dw = d->ln_dw; ln.db = d->ln_db;
+  ln.sum_ws = d->sum_ws;
   switch (d->K) {
     case 128: launch_panel_t<8, 4, PE_LNBWD>(a, stream, ln); break;
     case 256: launch_panel_t<8, 8, PE_LNBWD>(a, stream, ln); break;
@@ -1746,6 +1794,7 @@ FoldSeg fold_seg(const ttmi_wgrad_desc* d, const WgradPlan& p) {
   f.M = d->M; f.N = d->N; f.ldc = d->ld_dw;
   f.units = d->M * (d->N / 4) + (d->db ? d->M : 0);
   f.base = 0;
+  f.s_stride = d->M * d->N;
   f.S = p.S; f.acc = d->accumulate;
   return f;
 }
@@ -1810,11 +1859,39 @@ extern "C" int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream) {
   return launch_fold(f, stream);
 }
 
-extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, hipStream_t stream) {
-  TTMI_REQUIRE(n >= 0 && (n == 0 || descs), "ttmi_wgrad_fold: bad arguments");
+extern "C" int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M) {
+  if (M <= 0) return 0;
+  const int64_t tiles = (M + 15) / 16;
+  const int64_t tpw = std::max<int64_t>(1, (tiles + num_cus() - 1) / num_cus());
+  return (tiles + tpw - 1) / tpw;     // launch_panel_t's grid
+}
+
+extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                               const ttmi_fold_desc* folds, hipStream_t stream) {
+  TTMI_REQUIRE(n >= 0 && (n == 0 || descs) && nf >= 0 && (nf == 0 || folds),
+               "ttmi_wgrad_fold: bad arguments");
   FoldArgs f;
   f.n = 0;
   f.total = 0;
+  for (int i = 0; i < nf; ++i) {
+    const ttmi_fold_desc* d = folds + i;
+    TTMI_REQUIRE(d->part && d->C && d->S > 0 && d->M > 0 && d->N > 0 && d->N % 4 == 0 &&
+                 d->ldc % 4 == 0 && d->s_stride >= d->M * d->N && d->s_stride % 4 == 0 &&
+                 al16(d->part) && al16(d->C), "ttmi_wgrad_fold: bad fold descriptor %d", i);
+    if (f.n == FOLD_SEGS) {
+      int rc = launch_fold(f, stream);
+      if (rc) return rc;
+      f.n = 0;
+      f.total = 0;
+    }
+    FoldSeg sg;
+    sg.part = d->part; sg.part_rs = nullptr; sg.C = d->C; sg.rs = nullptr;
+    sg.M = d->M; sg.N = d->N; sg.ldc = d->ldc; sg.units = d->M * (d->N / 4);
+    sg.base = f.total; sg.s_stride = d->s_stride;
+    sg.S = (int)d->S; sg.acc = d->accumulate;
+    f.seg[f.n++] = sg;
+    f.total += sg.units;
+  }
   for (int i = 0; i < n; ++i) {
     const ttmi_wgrad_desc* d = descs[i];
     int rc = wgrad_check(d);

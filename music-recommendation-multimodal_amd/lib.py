@@ -90,7 +90,14 @@ class LnBwdDesc(ctypes.Structure):
                 ("next", ctypes.c_void_p), ("ld_next", ctypes.c_int64),
                 ("drop_p", ctypes.c_float), ("drop_seed", ctypes.c_void_p),
                 ("ld_drop", ctypes.c_int64), ("drop_rows", ctypes.c_void_p),
-                ("ln_dw", ctypes.c_void_p), ("ln_db", ctypes.c_void_p)]
+                ("ln_dw", ctypes.c_void_p), ("ln_db", ctypes.c_void_p),
+                ("sum_ws", ctypes.c_void_p)]
+
+
+class FoldDesc(ctypes.Structure):
+    """ttmi_fold_desc (include/ttmi.h)."""
+    _fields_ = [("part", c_p), ("S", c_i64), ("s_stride", c_i64), ("M", c_i64), ("N", c_i64),
+                ("C", c_p), ("ldc", c_i64), ("accumulate", c_i)]
 
 
 class ResLnDesc(ctypes.Structure):
@@ -115,7 +122,9 @@ SIGNATURES = {
     "ttmi_catalogue_rows": (c_i, [c_i, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "ttmi_wgrad_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64, c_i64]),
     "ttmi_wgrad": (c_i, [ctypes.POINTER(WgradDesc), c_p]),
-    "ttmi_wgrad_fold": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_p]),
+    "ttmi_wgrad_fold": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
+                              ctypes.POINTER(FoldDesc), c_p]),
+    "ttmi_linear_ln_bwd_sum_blocks": (c_i64, [c_i64]),
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
                                  c_i64, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),

@@ -13,7 +13,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from . import lib as _L
-from .lib import BF16, F32, ConvDesc, DisAttnDesc, GemmDesc, LnBwdDesc, WgradDesc, call
+from .lib import BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, WgradDesc, call
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -106,20 +106,24 @@ def linear_dx(dy: Tensor, w: Tensor, out: Tensor, *, gate: Optional[Tensor] = No
 
 
 class WgradPending:
-    """Weight-gradient GEMMs whose split partials still sit in their workspaces (ttmi_wgrad
-    with defer = 1).  ``flush()`` folds them all in one ttmi_wgrad_fold launch; the
-    descriptors and workspaces stay referenced until then."""
+    """Parameter gradients whose per-split / per-workgroup partials still sit in workspaces:
+    weight-gradient GEMMs (ttmi_wgrad with defer = 1) and LayerNorm weight/bias sums
+    (ttmi_linear_ln_bwd with sum_ws).  ``flush()`` folds them all, in a fixed order, in one
+    ttmi_wgrad_fold launch; descriptors and workspaces stay referenced until then."""
 
     def __init__(self):
         self.items = []
+        self.folds = []
 
     def flush(self) -> None:
-        if not self.items:
+        if not self.items and not self.folds:
             return
-        arr = (ctypes.POINTER(WgradDesc) * len(self.items))(
+        arr = (ctypes.POINTER(WgradDesc) * max(len(self.items), 1))(
             *[ctypes.pointer(d) for d, *_ in self.items])
-        call("ttmi_wgrad_fold", len(self.items), arr, _s())
+        farr = (FoldDesc * max(len(self.folds), 1))(*[f for f, *_ in self.folds])
+        call("ttmi_wgrad_fold", len(self.items), arr, len(self.folds), farr, _s())
         self.items = []
+        self.folds = []
 
 
 _PENDING: List[WgradPending] = []
@@ -196,6 +200,20 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
     d.drop_p, d.drop_seed, d.ld_drop = float(drop[0]), _p(drop[1]), N
     d.drop_rows = _p(drop_rows)
     d.ln_dw, d.ln_db = _p(ln_dw), _p(ln_db)
+    pend = _PENDING[-1] if _PENDING else None
+    ws = None
+    if pend is not None and (ln_dw is not None or ln_db is not None):
+        # per-workgroup sums, folded in workgroup order with the step's weight gradients
+        _L.load()
+        G = int(_L._lib.ttmi_linear_ln_bwd_sum_blocks(M))
+        ws = torch.empty(G * 2 * N, device=dx.device, dtype=torch.float32)
+        d.sum_ws = _p(ws)
+        for j, g in enumerate((ln_dw, ln_db)):
+            if g is not None:
+                f = FoldDesc()
+                f.part, f.S, f.s_stride, f.M, f.N = ws.data_ptr() + 4 * N * j, G, 2 * N, 1, N
+                f.C, f.ldc, f.accumulate = _p(g), N, 1
+                pend.folds.append((f, ws, g))
     call("ttmi_linear_ln_bwd", ctypes.byref(d), _s())
     return dx
 

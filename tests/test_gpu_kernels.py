@@ -648,6 +648,23 @@ def test_linear_ln_bwd(gpu_pkg, M, K, with_res, with_next):
     assert rel(db, bt_.grad) < 5e-5
     if with_next:
         assert rel(nxt.float(), dx_ref * keep / (1 - p)) < 8e-3
+    # inside deferred_wgrad the LN sums go to per-workgroup slabs folded in workgroup order:
+    # same values (to float reassociation), bit-identical run to run, dx untouched
+    outs = []
+    for _ in range(2):
+        dw2 = torch.full((D,), 0.5, device=DEV)
+        db2 = torch.zeros(D, device=DEV)
+        dx2 = torch.empty(M, D, device=DEV)
+        with ops.deferred_wgrad() as pend:
+            ops.linear_ln_bwd(dh.to(DEV), wt.to(DEV), x.to(DEV), mean.to(DEV), rstd.to(DEV),
+                              w.to(DEV), dx2, dw2, db2, res=res.to(DEV) if with_res else None)
+            assert len(pend.folds) == 2
+        outs.append((dw2, db2, dx2))
+    torch.cuda.synchronize()
+    assert rel(outs[0][0], 0.5 + wt_.grad) < 5e-5 and rel(outs[0][1], bt_.grad) < 5e-5
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    if not with_next:
+        assert torch.equal(outs[0][2], dx)
 
 
 @pytest.mark.parametrize("M,K", [(300, 128), (4096, 512), (25600, 128)])
@@ -864,13 +881,13 @@ def test_wgrad_deterministic(gpu_pkg, M, N, R, pad):
 
 
 def test_wgrad_deferred_fold_many(gpu_pkg):
-    """deferred_wgrad(): eleven weight gradients (more than one fold launch's 8 segments) leave
+    """deferred_wgrad(): eighteen weight gradients (more than one fold launch's 16 segments) leave
     their partials in workspaces and are completed by the block's flush; equal, bit for bit,
     to the immediate path; defer=False inside the block completes at once."""
     ops = gpu_pkg.ops
     g = torch.Generator().manual_seed(5)
-    shapes = [(384, 128, 25600), (128, 128, 2048), (512, 128, 4096), (128, 512, 3000)] * 3
-    shapes = shapes[:11]
+    shapes = [(384, 128, 25600), (128, 128, 2048), (512, 128, 4096), (128, 512, 3000)] * 5
+    shapes = shapes[:18]
     ins = [(torch.randn(R, M, generator=g).to(torch.bfloat16).to(DEV),
             torch.randn(R, N, generator=g).to(torch.bfloat16).to(DEV)) for M, N, R in shapes]
     ref_out = []
@@ -888,7 +905,7 @@ def test_wgrad_deferred_fold_many(gpu_pkg):
             outs.append((gw, gb))
         torch.cuda.synchronize()
         assert torch.equal(outs[3][0], ref_out[3][0])          # defer=False: already complete
-        assert len(pend.items) >= 9
+        assert len(pend.items) == 17
     torch.cuda.synchronize()
     for (a, b), (c, d) in zip(outs, ref_out):
         assert torch.equal(a, c) and torch.equal(b, d)
