@@ -116,13 +116,13 @@ def _wgrad_call(kw) -> bool:
 
 
 def probe_dominant(step, batch, device, iters: int = 20):
-    """Roofline of the dominant kernel family, the deterministic weight-gradient GEMM
-    (ttmi_wgrad: 12 launches per step — wgrad_kernel<64,64,4> on the five 25,600-row shapes,
-    wgrad_kernel<32,32,4> on the seven 512-row ones — plus the one wgrad_fold_kernel launch that
-    sums the split partials).  One eager forward+backward records the exact call mix of a
-    step; the mix (inside one deferred_wgrad block, as in the step: one fold) is captured into
-    a HIP graph and replayed `iters` times between HIP events on the launch stream, so avg_us =
-    device time of the family / 12 launches (the fold's time counted, shared out).
+    """Roofline of the dominant kernel family, the deterministic weight-gradient GEMMs: the
+    step's 12 nn.Linear weight gradients (five over 25,600 rows, seven over 512), computed as
+    one grouped launch (wgrad_group_kernel) plus one wgrad_fold_kernel that sums the split
+    partials (ttmi_wgrad_batch).  One eager forward+backward records the exact call mix of a
+    step; the mix (inside one deferred_wgrad block, as in the step) is captured into a HIP
+    graph and replayed `iters` times between HIP events on the launch stream, so avg_us =
+    device time of the two launches / 12 GEMMs.
     Algorithmic bytes per launch: both bf16 operands once (R x (M + N) x 2) plus the fp32
     gradient tile (M x N x 4)."""
     ops = pkg.ops
@@ -169,11 +169,13 @@ def probe_dominant(step, batch, device, iters: int = 20):
     by = sum(R * (M + N) * 2 + M * N * 4 for R, M, N in shapes) / n
     fl = sum(2.0 * M * N * R for R, M, N in shapes) / n
     gbs = by / sec / 1e9
-    tw, tfold = read_traffic("wgrad_kernel"), read_traffic("wgrad_fold_kernel")
-    traffic = round(tw + (tfold or 0) / n) if tw is not None else None   # the fold, shared out
-    return {"kernel": "ttmi_wgrad family: wgrad_kernel<64,64,4> x5 + wgrad_kernel<32,32,4> x7 + "
-                      "1 wgrad_fold_kernel (deterministic weight-gradient GEMMs, per-step mix, "
-                      "graph-replayed)",
+    # PMC bytes of the family's two launches per step (tools/traffic.py), shared out over the
+    # step's weight-gradient GEMMs like avg_us
+    tg, tfold = read_traffic("wgrad_group_kernel"), read_traffic("wgrad_fold_kernel")
+    traffic = round((tg + (tfold or 0)) / n) if tg is not None else None
+    return {"kernel": "ttmi_wgrad_batch: the step's 12 weight-gradient GEMMs as one "
+                      "wgrad_group_kernel launch + 1 wgrad_fold_kernel (deterministic split "
+                      "partials), graph-replayed; per-GEMM figures",
             "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
             "avg_us": round(sec * 1e6, 2), "launches_per_step": len(calls),

@@ -119,6 +119,12 @@ typedef struct {
  * per 16 segments). */
 int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int nf,
                     const ttmi_fold_desc* folds, hipStream_t stream);
+/* Computes the n weight gradients `descs` (their `defer` fields ignored) as one grouped
+ * launch (per 16 GEMMs), then folds their partials and the generic folds `folds`: a
+ * backward's weight gradients in two launches.  The operands must still hold their values
+ * when this runs (the caller keeps them alive and unmodified).  ABI 10. */
+int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                     const ttmi_fold_desc* folds, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0) — TransformerEncoderLayer

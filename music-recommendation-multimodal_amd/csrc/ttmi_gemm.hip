@@ -792,7 +792,7 @@ TTMI_DEV void wait_vm_barrier() {
 }
 
 template <int BM, int BN, int NS>
-__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
+TTMI_DEV void wgrad_body(const WgradArgs& g, const int bid) {
   using IA = WImg<BM>;
   using IB = WImg<BN>;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
@@ -808,12 +808,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
   const int T = g.tiles_m * g.tiles_n;
   int tile, split;
   if (g.xcd_remap) {          // splits % 8 == 0: one XCD per (split mod 8)
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int x = bid & 7, j = bid >> 3;
     tile = j % T;
     split = (j / T) * 8 + x;
   } else {
-    tile = blockIdx.x % T;
-    split = blockIdx.x / T;
+    tile = bid % T;
+    split = bid / T;
   }
   const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
@@ -940,6 +940,36 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
   }
 }
 
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs g) {
+  wgrad_body<BM, BN, NS>(g, blockIdx.x);
+}
+
+// Grouped weight gradients: several GEMMs' (tile, split) workgroups in one launch (the
+// step's deferred weight gradients: one launch instead of one per Linear, and the short
+// 512-row reductions fill the gaps the long ones leave).  Entry k owns workgroups
+// [wg_begin[k], wg_begin[k+1]); its arguments are read from the kernel-argument segment at a
+// uniform offset (no scratch copy of the table).
+constexpr int WG_GROUP = 16;
+struct WgradGroup { WgradArgs e[WG_GROUP]; int wg_begin[WG_GROUP + 1]; int n; };
+typedef const __attribute__((address_space(4))) WgradGroup* KWgradGroup;
+
+__global__ __launch_bounds__(256) void wgrad_group_kernel(WgradGroup grp) {
+  (void)grp;
+  KWgradGroup kg = (KWgradGroup)__builtin_amdgcn_kernarg_segment_ptr();
+  const int bid = blockIdx.x;
+  int k = 0;
+  while (k + 1 < kg->n && bid >= kg->wg_begin[k + 1]) ++k;
+  const auto& e = kg->e[k];
+  WgradArgs g;
+  g.M = e.M; g.N = e.N; g.R = e.R;
+  g.A = e.A; g.lda = e.lda; g.B = e.B; g.ldb = e.ldb; g.C = e.C; g.ldc = e.ldc;
+  g.alpha = e.alpha; g.rowsum_a = e.rowsum_a; g.rows_per_split = e.rows_per_split;
+  g.tiles_m = e.tiles_m; g.tiles_n = e.tiles_n; g.splits = e.splits; g.xcd_remap = e.xcd_remap;
+  g.mode = e.mode; g.accumulate = e.accumulate; g.part = e.part; g.part_rs = e.part_rs;
+  wgrad_body<64, 64, 4>(g, bid - kg->wg_begin[k]);
+}
+
 template <typename T, int BM, int BN>
 void launch_layout(const GemmArgs& a, bool ak, bool bk, dim3 grid, hipStream_t s) {
   if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, true>), grid, dim3(256), 0, s, a);
@@ -1046,7 +1076,7 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 // atomics).  One split (short R) writes C directly.  Folds of several GEMMs share one launch.
 struct WgradPlan { int tiles_m, tiles_n, S, tile; int64_t sps; };
 
-WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
+WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax, bool allow32 = true) {
   WgradPlan p;
   p.tile = 64;
   p.tiles_m = (int)((M + 63) / 64);
@@ -1072,7 +1102,7 @@ WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
   while (sps > 1 && sps * 64 * ldmax * 2 >= (int64_t)1 << 31) sps = (sps + 1) / 2;
   p.S = (int)((stages + sps - 1) / sps);
   p.sps = sps;
-  if (p.S == 1 && T < 128) {   // one split: 32x32 tiles put 4x the workgroups on the rows
+  if (allow32 && p.S == 1 && T < 128) {   // one split: 32x32 tiles, 4x the workgroups
     p.tile = 32;
     p.tiles_m = (int)((M + 31) / 32);
     p.tiles_n = (int)((N + 31) / 32);
@@ -1785,6 +1815,25 @@ int wgrad_check(const ttmi_wgrad_desc* d) {
   return TTMI_OK;
 }
 
+WgradArgs wgrad_args(const ttmi_wgrad_desc* d, const WgradPlan& p) {
+  WgradArgs a;
+  a.M = d->M; a.N = d->N; a.R = d->R;
+  a.A = static_cast<const char*>(d->dy); a.lda = d->ld_dy;
+  a.B = static_cast<const char*>(d->x); a.ldb = d->ld_x;
+  a.C = d->dw; a.ldc = d->ld_dw;
+  a.alpha = d->alpha;
+  a.rowsum_a = d->db;
+  a.rows_per_split = p.sps * 64;
+  a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n; a.splits = p.S;
+  a.xcd_remap = p.S % 8 == 0;
+  a.accumulate = d->accumulate;
+  a.mode = p.S > 1 ? WG_SLAB : WG_DIRECT;
+  a.part = static_cast<float*>(d->workspace);
+  a.part_rs = p.S > 1 ? reinterpret_cast<float*>(static_cast<char*>(d->workspace) +
+                                                  al256((int64_t)p.S * d->M * d->N * 4)) : nullptr;
+  return a;
+}
+
 FoldSeg fold_seg(const ttmi_wgrad_desc* d, const WgradPlan& p) {
   FoldSeg f;
   f.part = static_cast<const float*>(d->workspace);
@@ -1831,21 +1880,7 @@ extern "C" int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream) {
   const int64_t need = wgrad_ws_bytes(p, d->M, d->N);
   TTMI_REQUIRE(need == 0 || (d->workspace && d->workspace_bytes >= need && al16(d->workspace)),
                "ttmi_wgrad: workspace of %lld bytes required", (long long)need);
-  WgradArgs a;
-  a.M = d->M; a.N = d->N; a.R = d->R;
-  a.A = static_cast<const char*>(d->dy); a.lda = d->ld_dy;
-  a.B = static_cast<const char*>(d->x); a.ldb = d->ld_x;
-  a.C = d->dw; a.ldc = d->ld_dw;
-  a.alpha = d->alpha;
-  a.rowsum_a = d->db;
-  a.rows_per_split = p.sps * 64;
-  a.tiles_m = p.tiles_m; a.tiles_n = p.tiles_n; a.splits = p.S;
-  a.xcd_remap = p.S % 8 == 0;
-  a.accumulate = d->accumulate;
-  a.mode = p.S > 1 ? WG_SLAB : WG_DIRECT;
-  a.part = static_cast<float*>(d->workspace);
-  a.part_rs = p.S > 1 ? reinterpret_cast<float*>(static_cast<char*>(d->workspace) +
-                                                  al256((int64_t)p.S * d->M * d->N * 4)) : nullptr;
+  const WgradArgs a = wgrad_args(d, p);
   const int64_t nwg = (int64_t)p.tiles_m * p.tiles_n * p.S;
   TTMI_REQUIRE(nwg <= 2147483647LL, "ttmi_wgrad: grid too large");
   if (p.tile == 32) hipLaunchKernelGGL((wgrad_kernel<32, 32, 4>), dim3((unsigned)nwg), dim3(256), 0, stream, a);
@@ -1911,4 +1946,49 @@ extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int n
     f.total += sg.units;
   }
   return launch_fold(f, stream);
+}
+
+extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                                const ttmi_fold_desc* folds, hipStream_t stream) {
+  TTMI_REQUIRE(n >= 0 && (n == 0 || descs) && nf >= 0 && (nf == 0 || folds),
+               "ttmi_wgrad_batch: bad arguments");
+  WgradGroup grp;
+  grp.n = 0;
+  grp.wg_begin[0] = 0;
+  auto flush = [&]() -> int {
+    if (grp.n == 0) return TTMI_OK;
+    hipLaunchKernelGGL(wgrad_group_kernel, dim3((unsigned)grp.wg_begin[grp.n]), dim3(256), 0,
+                       stream, grp);
+    grp.n = 0;
+    grp.wg_begin[0] = 0;
+    return ttmi_check_launch("ttmi_wgrad_batch");
+  };
+  for (int i = 0; i < n; ++i) {
+    const ttmi_wgrad_desc* d = descs[i];
+    int rc = wgrad_check(d);
+    if (rc) return rc;
+    if (d->R == 0) {                                   // dW (+)= 0: no reduction to group
+      ttmi_wgrad_desc z = *d;
+      z.defer = 1;
+      rc = ttmi_wgrad(&z, stream);
+      if (rc) return rc;
+      continue;
+    }
+    const WgradPlan p = wgrad_plan(d->R, d->M, d->N, std::max(d->ld_dy, d->ld_x), false);
+    const int64_t need = wgrad_ws_bytes(p, d->M, d->N);
+    TTMI_REQUIRE(need == 0 || (d->workspace && d->workspace_bytes >= need && al16(d->workspace)),
+                 "ttmi_wgrad_batch: descriptor %d needs a workspace of %lld bytes", i,
+                 (long long)need);
+    const int64_t nwg = (int64_t)p.tiles_m * p.tiles_n * p.S;
+    if (grp.n == WG_GROUP || (int64_t)grp.wg_begin[grp.n] + nwg > 2147483647LL) {
+      rc = flush();
+      if (rc) return rc;
+    }
+    grp.e[grp.n] = wgrad_args(d, p);
+    grp.wg_begin[grp.n + 1] = grp.wg_begin[grp.n] + (int)nwg;
+    ++grp.n;
+  }
+  int rc = flush();
+  if (rc) return rc;
+  return ttmi_wgrad_fold(n, descs, nf, folds, stream);
 }

@@ -125,6 +125,8 @@ SIGNATURES = {
     "ttmi_wgrad_fold": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
                               ctypes.POINTER(FoldDesc), c_p]),
     "ttmi_linear_ln_bwd_sum_blocks": (c_i64, [c_i64]),
+    "ttmi_wgrad_batch": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
+                               ctypes.POINTER(FoldDesc), c_p]),
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
                                  c_i64, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),

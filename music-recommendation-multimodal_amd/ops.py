@@ -106,10 +106,11 @@ def linear_dx(dy: Tensor, w: Tensor, out: Tensor, *, gate: Optional[Tensor] = No
 
 
 class WgradPending:
-    """Parameter gradients whose per-split / per-workgroup partials still sit in workspaces:
-    weight-gradient GEMMs (ttmi_wgrad with defer = 1) and LayerNorm weight/bias sums
-    (ttmi_linear_ln_bwd with sum_ws).  ``flush()`` folds them all, in a fixed order, in one
-    ttmi_wgrad_fold launch; descriptors and workspaces stay referenced until then."""
+    """Parameter gradients still to be completed: weight-gradient GEMMs recorded but not yet
+    launched (their operands kept alive here) and LayerNorm weight/bias sums whose
+    per-workgroup partials sit in workspaces (ttmi_linear_ln_bwd with sum_ws).  ``flush()``
+    runs every recorded GEMM as one grouped launch and folds all partials in a fixed order
+    (ttmi_wgrad_batch: two launches per flush)."""
 
     def __init__(self):
         self.items = []
@@ -121,7 +122,7 @@ class WgradPending:
         arr = (ctypes.POINTER(WgradDesc) * max(len(self.items), 1))(
             *[ctypes.pointer(d) for d, *_ in self.items])
         farr = (FoldDesc * max(len(self.folds), 1))(*[f for f, *_ in self.folds])
-        call("ttmi_wgrad_fold", len(self.items), arr, len(self.folds), farr, _s())
+        call("ttmi_wgrad_batch", len(self.items), arr, len(self.folds), farr, _s())
         self.items = []
         self.folds = []
 
@@ -131,9 +132,9 @@ _PENDING: List[WgradPending] = []
 
 @contextlib.contextmanager
 def deferred_wgrad():
-    """Inside the block, bf16 ``linear_dw`` calls defer their split folds to the yielded
-    WgradPending (flushed, at the latest, on exit): one fold launch per step instead of one
-    per weight gradient."""
+    """Inside the block, bf16 ``linear_dw`` calls (and the fused LN-backward's weight sums)
+    are deferred to the yielded WgradPending (flushed, at the latest, on exit): a backward's
+    weight gradients become one grouped GEMM launch plus one fold launch."""
     pend = WgradPending()
     _PENDING.append(pend)
     try:
@@ -148,8 +149,8 @@ def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
     """gw[N,K] += dy[M,N]ᵀ · x[M,K]; gb[N] += Σ_m dy[m,:] (nn.Linear weight and bias grads,
     accumulated).  bf16 operands: ttmi_wgrad (split partials summed in a fixed order: the
     result is bit-reproducible); fp32 operands: the generic split-K GEMM.  Inside
-    ``deferred_wgrad()`` the fold waits for the block's flush unless ``defer=False`` (callers
-    that read gw right away)."""
+    ``deferred_wgrad()`` the GEMM runs at the block's flush (grouped with the others) unless
+    ``defer=False`` (callers that read gw right away); dy and x must not change before then."""
     M, N = dy.shape
     K = x.shape[1]
     if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
@@ -172,10 +173,11 @@ def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
     ws = torch.empty(nbytes, device=dy.device, dtype=torch.uint8) if nbytes else None
     d.workspace, d.workspace_bytes = _p(ws), nbytes
     pend = _PENDING[-1] if (_PENDING and defer) else None
-    d.defer = int(pend is not None)
-    call("ttmi_wgrad", ctypes.byref(d), _s())
-    if pend is not None and nbytes:
+    if pend is not None:                 # computed, with the block's others, at the flush
         pend.items.append((d, ws, dy, x, gw, gb))
+        return gw
+    d.defer = 0
+    call("ttmi_wgrad", ctypes.byref(d), _s())
     return gw
 
 

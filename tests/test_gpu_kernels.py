@@ -881,8 +881,8 @@ def test_wgrad_deterministic(gpu_pkg, M, N, R, pad):
 
 
 def test_wgrad_deferred_fold_many(gpu_pkg):
-    """deferred_wgrad(): eighteen weight gradients (more than one fold launch's 16 segments) leave
-    their partials in workspaces and are completed by the block's flush; equal, bit for bit,
+    """deferred_wgrad(): eighteen weight gradients (more than one grouped launch's / fold
+    launch's 16 entries) are recorded and computed at the block's flush; equal, bit for bit,
     to the immediate path; defer=False inside the block completes at once."""
     ops = gpu_pkg.ops
     g = torch.Generator().manual_seed(5)
