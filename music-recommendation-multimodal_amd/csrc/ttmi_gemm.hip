@@ -507,8 +507,8 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
       uint4 wv[BATCH];
 #pragma unroll
       for (int j = 0; j < BATCH; ++j) {
-        const int i = tid + 512 * (j0 + j);
-        if (j0 + j < PER && i < TOT) {
+        if (j0 + j < PER) {            // compile-time; the chunk index is clamped, not branched
+          const int i = min(tid + 512 * (j0 + j), TOT - 1);    // (a branch here spilled wv)
           const int n = i / CPR, c = i % CPR;
           wv[j] = *reinterpret_cast<const uint4*>(g.B + ((int64_t)n * g.ldb + 8 * c) * 2);
         }
