@@ -280,3 +280,43 @@ def test_catalogue_indexer_raw_items_vs_oracle(gpu_pkg):
     err = (dense.cpu() - want).abs().max().item()
     assert err < 3e-2, err
     assert (dense[17:] == 0).all() and (dense[0] == 0).all()
+
+
+def _serving_model(pkg):
+    from conftest import sub
+    z = load_golden("serving.npz")
+    V, D, L, n_g, n_c = z["cfg"].tolist()
+    m = pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128,
+                          num_genders=n_g, num_countries=n_c, max_seq_len=L,
+                          user_embedding_dim=D, item_embedding_dim=D,
+                          compute_dtype=torch.float32).to(DEV)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sub(z, "p/").items()})
+    return m.eval(), z
+
+
+def test_catalogue_index_vs_reference_index_catalog(gpu_pkg):
+    """The dense item index vs the REFERENCE's own index_catalog (inference.py:137-209, run by
+    tools/make_golden_serving.py on the reference model with the fusion head on precomputed
+    modality embeddings, eval-mode BatchNorm): every row to 1e-5, batches of 16 as there."""
+    m, z = _serving_model(gpu_pkg)
+    ids = torch.tensor(z["catalogue_ids"])
+    modal = torch.tensor(z["modal"])
+    loader = [{"target_id": ids[s:s + 16], "target_modal": modal[s:s + 16]}
+              for s in range(0, len(ids), 16)]
+    dense = gpu_pkg.retrieval.compute_all_item_embeddings(m, loader, m.user_tower.item_embedding.num_embeddings)[0]
+    want = torch.tensor(z["dense"])
+    assert dense.shape == want.shape
+    assert (dense.cpu() - want).abs().max().item() < 1e-5
+
+
+def test_recommend_vs_reference_recommend_for_user(gpu_pkg):
+    """Serving vs the REFERENCE's own recommend_for_user (inference.py:213-300): a user with
+    63 history items (the last 50 used and masked), the reference's dense index, top-10 ids
+    identical and scores to its printed 4 decimals."""
+    m, z = _serving_model(gpu_pkg)
+    hist = torch.tensor(z["history"])[None]
+    val, idx = gpu_pkg.retrieval.recommend(
+        m, hist.to(DEV), torch.tensor(z["dense"]).to(DEV), k=10,
+        user_gender=torch.tensor(z["gender"]).to(DEV), user_country=torch.tensor(z["country"]).to(DEV))
+    assert idx[0].cpu().tolist() == z["top_ids"].tolist()
+    assert np.abs(val[0].cpu().numpy() - z["top_scores"]).max() < 6e-5

@@ -107,3 +107,31 @@ def test_hash_dropout_rate_and_determinism():
     assert abs(keep.mean() - 0.9) < 3e-3
     assert np.array_equal(keep, ref.hash_keep(0x1234_5678_9ABC_DEF0, 1 << 20, 0.1))
     assert ref.hash_keep(7, 1000, 0.0).all()
+
+
+def test_serving_fixture_vs_oracle():
+    """tests/golden/serving.npz (the reference's index_catalog + recommend_for_user, run by
+    tools/make_golden_serving.py) restated by the oracle: eval-mode fusion head -> normalise
+    (1e-12) -> nan_to_num -> normalise (1e-8) -> dense rows; user tower (eval) on the last 50
+    history items -> normalise twice -> scores, padding + history masked -> top-10."""
+    import torch.nn.functional as TF
+    z = load_golden("serving.npz")
+    p = {k[2:]: torch.tensor(v) for k, v in z.items() if k.startswith("p/")}
+    ip = {k[len("item_tower."):]: v for k, v in p.items() if k.startswith("item_tower.")}
+    up = {k[len("user_tower."):]: v for k, v in p.items() if k.startswith("user_tower.")}
+    running = {k[len("fusion_layer.1."):]: v for k, v in ip.items() if k.startswith("fusion_layer.1.")}
+    out = ref.item_fusion_forward(ip, torch.tensor(z["modal"]), running=running, eval_mode=True)
+    e = TF.normalize(torch.nan_to_num(TF.normalize(out, dim=1), nan=0.0), p=2, dim=1, eps=1e-8)
+    dense = torch.zeros_like(torch.tensor(z["dense"]))
+    dense[torch.tensor(z["catalogue_ids"])] = e
+    assert (dense - torch.tensor(z["dense"])).abs().max().item() < 1e-5
+    hist = torch.tensor(z["history"])[-50:][None]
+    u = ref.user_tower_forward(up, hist, torch.tensor(z["gender"]), torch.tensor(z["country"]),
+                               None, 4, 2)
+    u = TF.normalize(TF.normalize(u, dim=1), p=2, dim=1, eps=1e-8)
+    s = (u @ torch.tensor(z["dense"]).t())[0]
+    s[0] = -float("inf")
+    s[hist[0]] = -float("inf")
+    v, i = torch.topk(s, 10)
+    assert i.tolist() == z["top_ids"].tolist()
+    assert np.abs(v.numpy() - z["top_scores"]).max() < 6e-5
