@@ -136,7 +136,7 @@ def probe_dominant(step, batch, device, iters: int = 20):
 
     ops.linear_dw = rec
     try:
-        step._fwd_bwd(step._stage(batch))
+        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
     finally:
         ops.linear_dw = orig
     torch.cuda.synchronize(device)
@@ -199,7 +199,7 @@ def probe_conv(step, batch, device, iters: int = 3):
 
     ops.conv2d = rec
     try:
-        step._fwd_bwd(step._stage(batch))
+        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
     finally:
         ops.conv2d = orig
     torch.cuda.synchronize(device)
@@ -246,7 +246,7 @@ def probe_text_gemm(step, batch, device, iters: int = 3):
 
     ops.gemm = rec
     try:
-        step._fwd_bwd(step._stage(batch))
+        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
     finally:
         ops.gemm = orig
     torch.cuda.synchronize(device)

@@ -87,7 +87,7 @@ class FlatParams:
     ALIGN = 64  # elements (256 B)
 
     def __init__(self, module: torch.nn.Module, mirror_dtype: Optional[torch.dtype] = None,
-                 tail: Sequence[str] = ()):
+                 tail: Sequence[str] = (), grad_extra: int = 0):
         self.names, self.shapes, self.offsets = [], [], []
         # trainable parameters only: frozen ones (the peft-frozen DeBERTa base) get neither
         # gradients nor AdamW updates (torch's AdamW skips params whose grad is None)
@@ -113,7 +113,10 @@ class FlatParams:
         for (n, p), o in zip(params, self.offsets):
             self.data[o:o + p.numel()].copy_(p.detach().reshape(-1))
             p.data = self.data[o:o + p.numel()].view(p.shape)
-        self.grad = torch.zeros_like(self.data)
+        # grad_extra: fp32 slots after the gradients that ride the same all-reduce (TrainStep
+        # carries rank 0's BatchNorm buffers there); AdamW only walks the first `numel`
+        self.grad = torch.zeros(off + grad_extra, device=dev, dtype=torch.float32)
+        self.grad_extra = self.grad[off:]
         self.exp_avg = torch.zeros_like(self.data)
         self.exp_avg_sq = torch.zeros_like(self.data)
         self.mirror = None
@@ -266,7 +269,7 @@ class TrainStep:
     everything but the user tower's first encoder layer and input block is all-reduced
     asynchronously while those are still being differentiated (DDP's bucketed overlap), the
     rest after the backward; BatchNorm running buffers follow rank 0 at the start of every
-    step (DDP ``broadcast_buffers``).  With ``model.global_negatives`` (BASELINE cfg 5) the
+    step (DDP ``broadcast_buffers``, carried by the previous step's gradient all-reduce).  With ``model.global_negatives`` (BASELINE cfg 5) the
     loss all-gathers û, î, user_idx between the forward and loss graphs and reduce-scatters
     the key gradients before the tower backward; ``loss`` is then this rank's share (the
     mean over ranks is the loss of the concatenated batch)."""
@@ -296,11 +299,25 @@ class TrainStep:
         self.world = self.sync.world
         self.global_negatives = bool(getattr(model, "global_negatives", False))
         self.overlap = overlap_grad_sync and self.world > 1 and self.ucfg.n_layers >= 2
-        self.flat = FlatParams(model, self.dtype, tail=self.LATE if self.overlap else ())
         self.fbufs = FlatBuffers(model)
         self.broadcast_buffers = broadcast_buffers and self.world > 1 and \
             self.fbufs.data is not None
+        self.flat = FlatParams(model, self.dtype, tail=self.LATE if self.overlap else (),
+                               grad_extra=self.fbufs.numel if self.broadcast_buffers else 0)
         ops.bump_param_epoch()                 # parameters now live in (and move with) the flat buffer
+        if self.world > 1:                     # DDP's constructor: rank 0's parameters and buffers
+            src = comm.group_src(0, self.group)
+            comm.broadcast(self.flat.data, src, self.group)
+            if self.fbufs.data is not None:
+                comm.broadcast(self.fbufs.data, src, self.group)
+        if self.broadcast_buffers:
+            # broadcast_buffers without a collective of its own: rank 0's buffers after step
+            # k's forward are exactly what DDP broadcasts at the start of step k + 1, so they
+            # ride step k's gradient all-reduce (rank 0 adds them, the others add zeros) into
+            # `bstage`, which the next step's first kernel copies over every rank's buffers
+            self.bstage = self.fbufs.data.clone()
+            self.bzero = torch.zeros_like(self.fbufs.data)
+            self.is_root = comm.rank(self.group) == 0
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay],
                                   dtype=torch.float64, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -371,6 +388,8 @@ class TrainStep:
             seeds = self.seeds
         else:
             ops.step_inc(self.step_t)
+        if self.broadcast_buffers:             # rank 0's buffers from the last all-reduce
+            ops.batch_copy([self.fbufs.data], [self.bstage])
         u, ust = F.user_tower_fwd(self.Pu, self.Wu, b["history_ids"], b["user_gender"],
                                   b["user_country"], b.get("history_mask"), self.ucfg, seeds)
         if self.raw_items:
@@ -426,9 +445,6 @@ class TrainStep:
         for w in works:
             w.wait()
 
-    def _broadcast_buffers(self) -> None:
-        comm.broadcast(self.fbufs.data, comm.group_src(0, self.group), self.group)
-
     def _raw_items_fwd(self, b: Dict[str, Tensor], seeds: Optional[Tensor]):
         """cfg 3 item encoders (item_tower.py:131-147): audio/visual ResNet-18, zero text slot,
         tabular MLP, concatenated in the reference's order."""
@@ -474,9 +490,13 @@ class TrainStep:
 
     def _body(self, b: Dict[str, Tensor], cut: Callable = _no_cut) -> None:
         self._fwd_bwd(b, cut)
+        if self.broadcast_buffers:             # rank 0 contributes its buffers, others zeros
+            ops.batch_copy([self.flat.grad_extra], [self.fbufs.data if self.is_root else self.bzero])
         if self.world > 1:
             cut(self._sync_tail)
         self._update()
+        if self.broadcast_buffers:
+            ops.batch_copy([self.bstage], [self.flat.grad_extra])
 
     # ---------------------------------------------------------------- capture
     @staticmethod
@@ -504,7 +524,8 @@ class TrainStep:
 
     def _state(self):
         return [self.flat.data, self.flat.exp_avg, self.flat.exp_avg_sq, self.step_t,
-                *self.bufs.values()] + ([self.flat.mirror] if self.flat.mirror is not None else [])
+                *self.bufs.values()] + ([self.flat.mirror] if self.flat.mirror is not None else []) + \
+            ([self.bstage] if self.broadcast_buffers else [])
 
     def _capture(self, e: _Entry) -> None:
         b = e.static
@@ -525,8 +546,6 @@ class TrainStep:
 
     def step(self, batch: Dict[str, Tensor]) -> Tensor:
         ops.bump_param_epoch()                 # the replay below rewrites the parameters
-        if self.broadcast_buffers:
-            self._broadcast_buffers()
         b = self._stage(batch)
         e = self._cur
         if not self.use_graph:
