@@ -17,6 +17,7 @@ import torch
 
 from conftest import load_golden, sub
 from oracle import deberta_ref as dref
+from oracle import two_tower_ref as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -38,9 +39,14 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
-@pytest.mark.parametrize("B,S,nh,lens", [(2, 64, 1, (64, 30)), (2, 160, 2, (160, 150)),
-                                         (1, 256, 2, (200,)), (3, 256, 2, (256, 70, 16))])
-def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
+@pytest.mark.parametrize("B,S,nh,lens,p", [(2, 64, 1, (64, 30), 0.0), (2, 160, 2, (160, 150), 0.0),
+                                           (1, 256, 2, (200,), 0.0), (3, 256, 2, (256, 70, 16), 0.0),
+                                           (2, 192, 2, (192, 77), 0.1), (2, 97, 1, (97, 41), 0.1),
+                                           (1, 131, 2, (120,), 0.1)])
+def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens, p):
+    """p > 0: attention-probability dropout with the kernels' counter-hash mask, regenerated
+    here by oracle.two_tower_ref.hash_keep at index ((b·nh + h)·S + i)·S + j (odd S puts the
+    hash pairs across rows)."""
     ops = gpu_pkg.ops
     text = gpu_pkg.text
     cfg = text.TextCfg(hidden=64 * nh, heads=nh)
@@ -74,7 +80,12 @@ def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
     raw.retain_grad()
     m2 = (mask[:, None, :] * mask[:, :, None]).bool()[:, None]
     sc = (raw * scale).masked_fill(~m2, torch.finfo(torch.float32).min)
-    ctx_ref = (torch.softmax(sc, -1) @ V).permute(0, 2, 1, 3).reshape(B, S, H)
+    probs = torch.softmax(sc, -1)
+    seed = 0x1234_5678_9ABC_DEF1
+    if p > 0:
+        keep = torch.from_numpy(ref.hash_keep(seed, B * nh * S * S, p)).view(B, nh, S, S)
+        probs = probs * keep.float() / (1.0 - p)
+    ctx_ref = (probs @ V).permute(0, 2, 1, 3).reshape(B, S, H)
     (ctx_ref * dctx).sum().backward()
     dS = raw.grad                                                       # [B, nh, S, S]
     HU_ref = torch.einsum("bhij,ijc->bjhc", dS, u[dmat])
@@ -88,8 +99,9 @@ def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
     md, dd = mask.to(DEV), delta_t.to(torch.int16).to(DEV)
     ctx = torch.empty(B * S, H, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B * nh * S, device=DEV)
+    drop = (p, torch.tensor([seed], dtype=torch.int64, device=DEV)) if p > 0 else ops.NO_DROP
     ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:], md,
-                 dd, scale, ctx, lse)
+                 dd, scale, ctx, lse, drop)
     torch.cuda.synchronize()
     valid = mask.reshape(-1).bool()
     cg = ctx.float().cpu().view(B * S, H)
@@ -100,7 +112,7 @@ def test_dis_attn_kernels_vs_torch(gpu_pkg, B, S, nh, lens):
     hu = torch.zeros(B * S * nh * 8, device=DEV)
     pb = torch.full((npos * 8,), 7.0, device=DEV)         # overwritten
     ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:], md,
-                 dd, scale, ctx, lse, dctx=dctx.reshape(B * S, H).to(torch.bfloat16).to(DEV),
+                 dd, scale, ctx, lse, drop, dctx=dctx.reshape(B * S, H).to(torch.bfloat16).to(DEV),
                  dq=dqkv[:, :H], dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:], lora_u=u.to(DEV),
                  lora_bq=bq.to(DEV), lora_hu=hu, lora_pb=pb)
     torch.cuda.synchronize()
