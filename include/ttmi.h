@@ -534,10 +534,18 @@ typedef struct ttmi_dis_attn_desc {
   float* dq_scratch;      /* backward: fp32 workspace of >= B·nh·S floats (D_i = dO_i·O_i) */
   float* lora_pbx;        /* backward with LoRA: fp32 workspace of ttmi_dis_attn_pbx_floats()
                              (per block pair, PB over the pair's expanded window rows) */
+  const int32_t* order;   /* ABI 11; NULL or ttmi_dis_attn_order()'s [B] batch order: one
+                             workgroup per (batch, head) runs every block pair of the sequence,
+                             longest sequences first (the longest-processing-time order keeps
+                             the last wave of workgroups short) */
 } ttmi_dis_attn_desc;
 int ttmi_dis_attn_fwd(const ttmi_dis_attn_desc* d, hipStream_t stream);
 int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t stream);
 int64_t ttmi_dis_attn_pbx_floats(int B, int S, int nh);
+/* order [B] int32: the batch indices sorted by live 64-row block count (1 + the last position
+ * with mask != 0, rounded up to 64) in descending order.  One launch per batch mask; every
+ * layer's ttmi_dis_attn_fwd/bwd of that batch reuses it. */
+int ttmi_dis_attn_order(const int64_t* mask, int B, int S, int32_t* order, hipStream_t stream);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
 int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
 /* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);

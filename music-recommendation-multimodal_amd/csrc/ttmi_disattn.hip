@@ -16,7 +16,7 @@
 //     the query_proj-LoRA contractions are HU = SkewK·Uexp (Uexp[r] = u[δ(...)]) and
 //     PBexp = SkewKᵀ·KB (binned to δ rows by a small reduction kernel).
 //
-// Kernels (4 waves, 16 rows per wave, < 80 KB LDS so two workgroups share a CU):
+// Kernels (4 waves, 16 rows per wave, <= 80 KB LDS so two workgroups share a CU):
 //   dis_fwd_kernel   per (query block, head, batch): online softmax over key blocks -> ctx, lse
 //   dis_dq_kernel    per (query block, head, batch): recomputes P, writes dQ and D = dO·O
 //   dis_dkv_kernel   per (key block, head, batch): recomputes Pᵀ, writes dK, dV, HU, PBexp
@@ -25,6 +25,18 @@
 // product (p2c for the query-side kernels, c2p for dis_dkv), and before the next staging.
 // The c2p (query side) / p2c (key side) window is private to each wave and lives in the
 // LDS of the window it no longer needs (PQexp / PKexp).
+//
+// Latency and VALU (round 2, from the SQ counters of round 1: waves parked on s_waitcnt for
+// half their lifetime, 4-5 vector instructions per MFMA):
+//   * software pipeline: the global loads of the NEXT block pair's rows and windows are
+//     issued into registers right after the staging barrier and written to LDS after the
+//     pair's last barrier, so their latency hides behind the pair's products;
+//   * δ lives in LDS (the window gather was two dependent global loads per row);
+//   * scores are kept in log2 units (inv_scale·log2 e folded into one fma with the key mask,
+//     exp2 on the VALU), lse is saved in log2 units;
+//   * the dropout hash serves an element pair: two hashes per four scores (fwd, dq), and in
+//     dis_dkv (pairs straddle two lanes) two hashes per four scores plus a DPP lane swap;
+//   * workgroups of one (batch, head) run on one XCD (shared K/V/Q/dO rows in its L2).
 #include "ttmi_common.h"
 
 namespace {
@@ -35,9 +47,13 @@ constexpr int WIN = 128;               // expanded window rows per block pair
 constexpr int WP = 272;                // LDS pitch (bytes) of a bf16 [rows][128] window product
 constexpr int UP = 32;                 // LDS pitch (bytes) of the bf16 [rows][16] LoRA images
 constexpr float FMIN = -3.4028234663852886e38f;   // torch.finfo(torch.float32).min
+constexpr float LOG2E = 1.4426950408889634f;
 constexpr int MAXS = 256;
 
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+// Staging registers are clang vectors, not HIP's uint4 struct: copies of the struct lower to
+// memcpy through a stack slot when they cross a loop's conditional blocks.
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
 TTMI_DEV uint2 lds8(const char* p) { return *reinterpret_cast<const uint2*>(p); }
 TTMI_DEV uint2 lds_tr8(const char* p) {
@@ -88,7 +104,7 @@ struct DisArgs {
   float inv_scale;
   DropParams drop;                  // probs dropout, index ((b·nh + h)·S + i)·S + j
   bf16_t* ctx; int64_t ldctx;
-  float* lse;                       // [B, nh, S]
+  float* lse;                       // [B, nh, S], log2 units: m + log2 Σ 2^(s - m)
   const bf16_t* dctx; int64_t lddctx;
   bf16_t* dq; bf16_t* dk; bf16_t* dv; int64_t lddqkv;
   float* dsum;                      // [B, nh, S]: D_i = dO_i·O_i (written by dis_dq)
@@ -97,6 +113,7 @@ struct DisArgs {
   float* hu;                        // [B·S, nh, 8]
   float* pbx;                       // [B·nh, nqb, nqb, 128, 8]
   float* pb;                        // [npos, 8] (summed over batch and heads)
+  const int32_t* order;             // [B] batch order (longest first) or null
 };
 
 TTMI_DEV int win_row(const DisArgs& a, int rel) {
@@ -104,11 +121,36 @@ TTMI_DEV int win_row(const DisArgs& a, int rel) {
   return a.delta[rel + a.S - 1];
 }
 
+// Workgroup -> (block, head, batch): the nqb workgroups of one (batch, head) are consecutive
+// logical ids, and xcd_contiguous keeps consecutive ids on one XCD (their rows share its L2).
+struct Tile { int blk, h, b; };
+TTMI_DEV Tile tile_of(const DisArgs& a) {
+  const int n = a.nqb * a.nh * a.B;
+  const int id = xcd_contiguous((int)blockIdx.x, n);
+  Tile t;
+  t.blk = id % a.nqb;
+  const int bh = id / a.nqb;
+  t.h = bh % a.nh;
+  t.b = bh / a.nh;
+  return t;
+}
+
+// Workgroup -> (batch, head) of the per-sequence kernels: longest sequences first.
+struct BH { int b, h; };
+TTMI_DEV BH bh_of(const DisArgs& a) {
+  const int k = (int)blockIdx.x, bi = k / a.nh;
+  BH r;
+  r.h = k - bi * a.nh;
+  r.b = a.order ? a.order[bi] : bi;
+  return r;
+}
+
 // End of sequence b's attended range: 1 + the last position whose mask is set (0 if none).
 // Blocks of 64 rows at or past it hold only padded tokens: as keys they are masked for every
 // valid query (probability exactly 0), and as queries their outputs reach nothing the encoder
 // returns (the masked mean-pool) and their gradients are exactly 0.  The kernels skip those
-// blocks (block-uniform: every thread of the workgroup computes the same value).
+// blocks (block-uniform: every thread of the workgroup computes the same value).  The
+// barriers also publish the δ table the caller copied to LDS before the call.
 TTMI_DEV int seq_end(const DisArgs& a, int64_t rowb, int* red) {
   if (threadIdx.x == 0) *red = 0;
   __syncthreads();
@@ -119,38 +161,74 @@ TTMI_DEV int seq_end(const DisArgs& a, int64_t rowb, int* red) {
   __syncthreads();
   return *red;
 }
+TTMI_DEV void load_delta(int16_t* sdel, const DisArgs& a) {
+  for (int t = threadIdx.x; t < 2 * a.S - 1; t += blockDim.x) sdel[t] = a.delta[t];
+}
 
-// rows [r0, r0 + R) x 64 bf16 of src -> LDS image (pitch TP); rows >= nrows are zero.  Loads
-// are unconditional from a clamped row (a guarded load compiles to a branch + vmcnt(0)).
-template <int R>
-TTMI_DEV void stage_rows(char* dst, const bf16_t* src, int64_t ld, int r0, int nrows, int tid) {
-  constexpr int C = R * 8 / 256;
-  uint4 v[C];
+// ------------------------------------------------------------------ register-staged loads
+// rows [r0, r0 + 64) x 64 bf16 of src: two 16-byte pieces per thread (clamped row: a guarded
+// load compiles to a branch + vmcnt(0)) ...
+TTMI_DEV void pf_rows(u32x4 (&v)[2], const bf16_t* src, int64_t ld, int r0, int nrows, int tid) {
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
+  for (int c = 0; c < 2; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    v[c] = *reinterpret_cast<const uint4*>(src + (int64_t)min(r0 + r, nrows - 1) * ld + ch * 8);
+    v[c] = *reinterpret_cast<const u32x4*>(src + (int64_t)min(r0 + r, nrows - 1) * ld + ch * 8);
   }
+}
+// ... written to an LDS image (pitch TP), rows >= nrows zero.
+TTMI_DEV void put_rows(char* dst, const u32x4 (&v)[2], int r0, int nrows, int tid) {
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
+  for (int c = 0; c < 2; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    const bool ok = r0 + r < nrows;
-    *reinterpret_cast<uint4*>(dst + r * TP + ch * 16) =
-        ok ? v[c] : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<u32x4*>(dst + r * TP + ch * 16) = r0 + r < nrows ? v[c] : u32x4{0u, 0u, 0u, 0u};
   }
 }
 // Expanded window: row r = table[δ(rel0 + r)] (head slice at column h·64), r < 128.
-TTMI_DEV void stage_win(char* dst, const DisArgs& a, const bf16_t* table, int rel0, int tid) {
-  uint4 v[4];
+TTMI_DEV void pf_win(u32x4 (&v)[4], const int16_t* sdel, const bf16_t* table, int64_t ld, int rel0,
+                     int S, int tid) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    v[c] = *reinterpret_cast<const uint4*>(table + (int64_t)win_row(a, rel0 + r) * a.ldpos + ch * 8);
+    const int rel = min(max(rel0 + r, -(S - 1)), S - 1);
+    v[c] = *reinterpret_cast<const u32x4*>(table + (int64_t)sdel[rel + S - 1] * ld + ch * 8);
   }
+}
+TTMI_DEV void put_win(char* dst, const u32x4 (&v)[4], int tid) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    *reinterpret_cast<uint4*>(dst + r * TP + ch * 16) = v[c];
+    *reinterpret_cast<u32x4*>(dst + r * TP + ch * 16) = v[c];
+  }
+}
+
+// Sliding window.  Consecutive block pairs of one workgroup shift the window by 64 rows, so
+// half of the next window is already staged: `keep_lo` (query side, j0 += 64: next rows
+// 64..127 = current rows 0..63) or !keep_lo (key side, i0 += 64: next rows 0..63 = current
+// rows 64..127).  Only the 64 new rows are loaded; each thread moves the old piece it owns and
+// then writes its new piece at the same place, so no other thread's piece is touched.
+TTMI_DEV void pf_win_half(u32x4 (&v)[2], const int16_t* sdel, const bf16_t* table, int64_t ld,
+                          int rel0, int S, int tid) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
+    const int rel = min(max(rel0 + r, -(S - 1)), S - 1);
+    v[c] = *reinterpret_cast<const u32x4*>(table + (int64_t)sdel[rel + S - 1] * ld + ch * 8);
+  }
+}
+template <bool NEW_LO>
+TTMI_DEV void put_win_slide(char* dst, const u32x4 (&v)[2], int tid) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
+    char* lo = dst + r * TP + ch * 16;
+    char* hi = lo + 64 * TP;
+    if (NEW_LO) {
+      *reinterpret_cast<u32x4*>(hi) = *reinterpret_cast<const u32x4*>(lo);
+      *reinterpret_cast<u32x4*>(lo) = v[c];
+    } else {
+      *reinterpret_cast<u32x4*>(lo) = *reinterpret_cast<const u32x4*>(hi);
+      *reinterpret_cast<u32x4*>(hi) = v[c];
+    }
   }
 }
 
@@ -177,42 +255,119 @@ TTMI_DEV void zero_rows16(char* img, int lane) {
   for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(p + 16 * k) = make_uint4(0u, 0u, 0u, 0u);
 }
 
-// ------------------------------------------------------------------ query-side staging
+// ------------------------------------------------------------------ dropout keep factors
+TTMI_DEV float keepf(const DropKeys& d, uint32_t u16) { return u16 >= d.thresh ? d.scale : 0.f; }
+// Keep factors (0 or 1/(1-p)) of the flat indices idx0 .. idx0 + 3, one hash per aligned
+// pair.  EVEN: idx0 is even (every lane, when S is even).
+template <bool EVEN>
+TTMI_DEV void keep4_row(const DropKeys& d, uint32_t idx0, float (&k)[4]) {
+  const uint32_t p0 = idx0 >> 1;
+  const uint32_t ha = drop_hash(d, p0), hb = drop_hash(d, p0 + 1);
+  if (EVEN) {
+    k[0] = keepf(d, ha & 0xFFFFu); k[1] = keepf(d, ha >> 16);
+    k[2] = keepf(d, hb & 0xFFFFu); k[3] = keepf(d, hb >> 16);
+  } else {
+    const uint32_t hc = drop_hash(d, p0 + 2);
+    const bool odd = idx0 & 1u;
+    k[0] = keepf(d, odd ? ha >> 16 : ha & 0xFFFFu);
+    k[1] = keepf(d, odd ? hb & 0xFFFFu : ha >> 16);
+    k[2] = keepf(d, odd ? hb >> 16 : hb & 0xFFFFu);
+    k[3] = keepf(d, odd ? hc & 0xFFFFu : hb >> 16);
+  }
+}
+// Swap with the neighbouring lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2].
+TTMI_DEV uint32_t swap_adj(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+// Keep factors of 4 scores of one key column j (lane) at query rows i0 .. i0 + 3, flat index
+// idx(e) = row(e)·S + j.  EVEN (S even): the pair of idx(e) is (j, j ^ 1) = this lane and its
+// neighbour, so each lane hashes two of the four pairs and the neighbour sends the others.
+template <bool EVEN>
+TTMI_DEV void keep4_col(const DropKeys& d, uint32_t idx0, uint32_t S, bool odd_lane, float (&k)[4]) {
+  if (EVEN) {
+    const uint32_t e0 = odd_lane ? 2u : 0u;
+    const uint32_t h0 = drop_hash(d, (idx0 + e0 * S) >> 1), h1 = drop_hash(d, (idx0 + (e0 + 1) * S) >> 1);
+    const uint32_t o0 = swap_adj(h0), o1 = swap_adj(h1);
+    const uint32_t g0 = odd_lane ? o0 : h0, g1 = odd_lane ? o1 : h1;   // pairs of e = 0, 1
+    const uint32_t g2 = odd_lane ? h0 : o0, g3 = odd_lane ? h1 : o1;   // pairs of e = 2, 3
+    k[0] = keepf(d, odd_lane ? g0 >> 16 : g0 & 0xFFFFu);
+    k[1] = keepf(d, odd_lane ? g1 >> 16 : g1 & 0xFFFFu);
+    k[2] = keepf(d, odd_lane ? g2 >> 16 : g2 & 0xFFFFu);
+    k[3] = keepf(d, odd_lane ? g3 >> 16 : g3 & 0xFFFFu);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) k[e] = drop_keep(d, idx0 + e * S) ? d.scale : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------ query side
 struct QSide {
   char sK[64 * TP];
   char sV[64 * TP];
   char sPK[WIN * TP];
   char sPQ[WIN * TP];     // PQexp, then the waves' private c2p / SkewQ images (4 x 16 x WP)
   char sX[64 * WP];       // shared p2c: [key jl][r]
-  float sMk[64];
+  float sCol[2][64][2];   // per key column {mul, add}: [0] valid query rows, [1] padded rows
+  int16_t sDel[2 * MAXS];
 };
 static_assert(4 * 16 * WP <= WIN * TP, "private images must fit the PQexp window");
 static_assert(sizeof(QSide) <= 80 * 1024, "two workgroups per CU");
 
-// Stage key block j0 and the expanded windows of the pair (i0, j0), then the shared p2c
-// product; returns after the barrier that publishes sX.  `priv` = this wave's image.
-TTMI_DEV void qside_stage(QSide& L, const DisArgs& a, int b, int h, int i0, int j0, int tid, int w,
-                          int lane) {
-  const int64_t rowb = (int64_t)b * a.S;
-  stage_rows<64>(L.sK, a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j0, a.S, tid);
-  stage_rows<64>(L.sV, a.v + rowb * a.ldqkv + h * DH, a.ldqkv, j0, a.S, tid);
-  stage_win(L.sPK, a, a.posk + h * DH, i0 - j0 - 63, tid);
-  stage_win(L.sPQ, a, a.posq + h * DH, i0 - j0 - 63, tid);
+// The next key block's staging, held in registers across a block pair: key rows, values,
+// the 64 new rows of the sliding PKexp and the whole PQexp (whose LDS holds the waves'
+// private images during a pair, so nothing of it carries over).
+struct QRows {
+  u32x4 k[2], v[2];
+  int64_t mk;             // mask of key j0 + tid (tid < 64)
+};
+TTMI_DEV void qrows_load(QRows& st, const DisArgs& a, int64_t rowb, int h, int j0, int tid) {
+  pf_rows(st.k, a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j0, a.S, tid);
+  pf_rows(st.v, a.v + rowb * a.ldqkv + h * DH, a.ldqkv, j0, a.S, tid);
+  // unconditional load from a clamped index: a guarded load is a branch + vmcnt(0), which
+  // would wait for the prefetch just issued
+  st.mk = a.mask[rowb + min(j0 + (tid & 63), a.S - 1)];
+}
+TTMI_DEV void qwins_load(u32x4 (&pk)[2], u32x4 (&pq)[4], const QSide& L, const DisArgs& a, int h,
+                         int i0, int j0, int tid) {
+  pf_win_half(pk, L.sDel, a.posk + h * DH, a.ldpos, i0 - j0 - 63, a.S, tid);
+  pf_win(pq, L.sDel, a.posq + h * DH, a.ldpos, i0 - j0 - 63, a.S, tid);
+}
+// Key column j = j0 + tid: s = raw·mul + add.  Valid query rows: valid key {c, 0}, masked
+// key {0, finfo.min} (masked_fill), key past S {0, -inf}.  Padded query rows (the reference
+// masks their whole row): every in-range key {0, finfo.min}, past S {0, -inf}.
+TTMI_DEV void qwins_store(const u32x4 (&pk)[2], const u32x4 (&pq)[4], QSide& L, int tid) {
+  put_win_slide<true>(L.sPK, pk, tid);
+  put_win(L.sPQ, pq, tid);
+}
+TTMI_DEV void qrows_store(const QRows& st, QSide& L, int S, int j0, float c, int tid) {
+  put_rows(L.sK, st.k, j0, S, tid);
+  put_rows(L.sV, st.v, j0, S, tid);
   if (tid < 64) {
-    const int j = j0 + tid;
-    L.sMk[tid] = j < a.S ? (a.mask[rowb + j] != 0 ? 1.f : 0.f) : -1.f;
+    const bool in = j0 + tid < S;
+    const float add = in ? FMIN : -INFINITY;
+    const bool valid = in && st.mk != 0;
+    L.sCol[0][tid][0] = valid ? c : 0.f;
+    L.sCol[0][tid][1] = valid ? 0.f : add;
+    L.sCol[1][tid][0] = 0.f;
+    L.sCol[1][tid][1] = add;
   }
-  __syncthreads();
-  // shared p2c: this wave's 16 keys against PQexp
-  win_product(L.sPQ, fk<TP>(L.sK, 16 * w, 0, lane), fk<TP>(L.sK, 16 * w, 1, lane),
-              L.sX + 16 * w * WP, lane);
-  __syncthreads();
 }
 
-// Masked, scaled scores of this wave's 16 query rows (i = i0 + 16w + li) against key block j0:
-// sc[t][e] for key jl = 16t + 4lg + e.  Writes the private c2p image first (PQexp is dead).
-TTMI_DEV void qside_scores(QSide& L, const DisArgs& a, const uint4 (&qf)[2], bool qvalid, int w,
-                           int lane, f32x4_t (&sc)[4]) {
+TTMI_DEV void qside_prologue(QSide& L, const DisArgs& a, int64_t rowb, int h, int i0, float c, int tid) {
+  QRows st;
+  qrows_load(st, a, rowb, h, 0, tid);
+  u32x4 pk[4], pq[4];
+  pf_win(pk, L.sDel, a.posk + h * DH, a.ldpos, i0 - 63, a.S, tid);
+  pf_win(pq, L.sDel, a.posq + h * DH, a.ldpos, i0 - 63, a.S, tid);
+  qrows_store(st, L, a.S, 0, c, tid);
+  put_win(L.sPK, pk, tid);
+  put_win(L.sPQ, pq, tid);
+}
+
+// Raw scores (c2c + c2p + p2c, unscaled) of this wave's 16 query rows (i = i0 + 16w + li)
+// against key block j0: sc[t][e] for key jl = 16t + 4lg + e.  Writes the private c2p image
+// first (PQexp is dead after the shared p2c product).
+TTMI_DEV void qside_raw(QSide& L, const uint4 (&qf)[2], int w, int lane, f32x4_t (&sc)[4]) {
   const int li = lane & 15, lg = lane >> 4;
   char* priv = L.sPQ + 16 * w * WP;
   win_product(L.sPK, qf[0], qf[1], priv, lane);
@@ -228,60 +383,109 @@ TTMI_DEV void qside_scores(QSide& L, const DisArgs& a, const uint4 (&qf)[2], boo
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int jl = 16 * t + 4 * lg + e, r = il - jl + 63;
-      const float raw = sc[t][e] + lds_bf(priv, li * (WP / 2) + r) + lds_bf(L.sX, jl * (WP / 2) + r);
-      const float mk = L.sMk[jl];
-      sc[t][e] = mk < 0.f ? -INFINITY : ((qvalid && mk > 0.f) ? raw * a.inv_scale : FMIN);
+      sc[t][e] += lds_bf(priv, li * (WP / 2) + r) + lds_bf(L.sX, jl * (WP / 2) + r);
     }
 }
+// s = raw·mul + add for this lane's 16 columns (log2 units).
+TTMI_DEV void apply_cols(const float (*col)[2], int lg, f32x4_t (&sc)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float4 c01 = *reinterpret_cast<const float4*>(&col[16 * t + 4 * lg][0]);
+    const float4 c23 = *reinterpret_cast<const float4*>(&col[16 * t + 4 * lg + 2][0]);
+    sc[t][0] = fmaf(sc[t][0], c01.x, c01.y);
+    sc[t][1] = fmaf(sc[t][1], c01.z, c01.w);
+    sc[t][2] = fmaf(sc[t][2], c23.x, c23.y);
+    sc[t][3] = fmaf(sc[t][3], c23.z, c23.w);
+  }
+}
 
-__global__ __launch_bounds__(256, 2) void dis_fwd_kernel(DisArgs a) {
+// One workgroup per (batch, head): every live block pair of the sequence runs in one software
+// pipeline (query blocks in order, key blocks inner), so the staging of a new query block
+// hides behind the previous pair, and the workgroup start (δ table, sequence end, first
+// staging) is paid once per head instead of once per query block.
+template <bool EVEN>
+__global__ __launch_bounds__(256, 2) void dis_fwd_bh_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) QSide L;
   __shared__ int s_end;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const BH id = bh_of(a);
+  const int h = id.h, b = id.b;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
-  const int S = a.S, i0 = qb * 64, i = i0 + 16 * w + li;
+  const int S = a.S;
   const int64_t rowb = (int64_t)b * S;
+  const int64_t bh = (int64_t)b * a.nh + h;
   const DropKeys dk = resolve_drop(a.drop);
-  const bool irow = i < S;
+  load_delta(L.sDel, a);
   const int send = seq_end(a, rowb, &s_end);
-  if (i0 >= send) {                      // padded query block: finite placeholder outputs
-    if (!irow) return;
+  const int nlive = (send + 63) / 64;
+  for (int qb = nlive; qb < a.nqb; ++qb) {   // padded query blocks: finite placeholder outputs
+    const int i = qb * 64 + 16 * w + li;
+    if (i >= S) break;
     bf16_t* dst = a.ctx + (rowb + i) * a.ldctx + h * DH;
 #pragma unroll
     for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), f32x4_t{0.f, 0.f, 0.f, 0.f});
-    if (lg == 0) a.lse[((int64_t)b * a.nh + h) * S + i] = 0.f;
-    return;
+    if (lg == 0) a.lse[bh * S + i] = 0.f;
   }
-  const bool qvalid = irow && a.mask[rowb + i] != 0;
-  const uint4 qf[2] = {fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 0, lane),
-                       fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 1, lane)};
+  if (nlive == 0) return;
+  const float c = a.inv_scale * LOG2E;
+  const bf16_t* qbase = a.q + rowb * a.ldqkv + h * DH;
+  // query block 0
+  int i = 16 * w + li;
+  bool qvalid = i < S && a.mask[rowb + min(i, S - 1)] != 0;
+  uint4 qf[2] = {fglob(qbase, a.ldqkv, i, S, 0, lane), fglob(qbase, a.ldqkv, i, S, 1, lane)};
+  qside_prologue(L, a, rowb, h, 0, c, tid);
   float m_run = -INFINITY, l_run = 0.f;
   f32x4_t o[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) o[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 0; j0 < send; j0 += 64) {
-    qside_stage(L, a, b, h, i0, j0, tid, w, lane);
+  int qb = 0, kb = 0;
+  const int npairs = nlive * nlive;
+  for (int p = 0; p < npairs; ++p) {
+    const int i0 = qb * 64, j0 = kb * 64;
+    const bool last_k = kb + 1 == nlive;
+    const int qbn = last_k ? qb + 1 : qb, kbn = last_k ? 0 : kb + 1;
+    const bool more = p + 1 < npairs;
+    __syncthreads();                      // staging of pair (i0, j0) is in LDS
+    // next pair's staging and the next query block's rows (all unconditional, clamped)
+    QRows nx;
+    u32x4 nwk[4], nwq[4];
+    qrows_load(nx, a, rowb, h, kbn * 64, tid);
+    pf_win(nwk, L.sDel, a.posk + h * DH, a.ldpos, qbn * 64 - kbn * 64 - 63, S, tid);
+    pf_win(nwq, L.sDel, a.posq + h * DH, a.ldpos, qbn * 64 - kbn * 64 - 63, S, tid);
+    const int in_ = qbn * 64 + 16 * w + li;
+    const uint4 nqf0 = fglob(qbase, a.ldqkv, in_, S, 0, lane), nqf1 = fglob(qbase, a.ldqkv, in_, S, 1, lane);
+    const int64_t nqm = a.mask[rowb + min(in_, S - 1)];
+    // shared p2c: this wave's 16 keys against PQexp
+    win_product(L.sPQ, fk<TP>(L.sK, 16 * w, 0, lane), fk<TP>(L.sK, 16 * w, 1, lane),
+                L.sX + 16 * w * WP, lane);
+    __syncthreads();
     f32x4_t sc[4];
-    qside_scores(L, a, qf, qvalid, w, lane, sc);
+    qside_raw(L, qf, w, lane, sc);
+    apply_cols(L.sCol[qvalid ? 0 : 1], lg, sc);
     float rmax = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) rmax = fmaxf(rmax, sc[t][e]);
+    for (int t = 0; t < 4; ++t) rmax = fmaxf(fmaxf(rmax, fmaxf(sc[t][0], sc[t][1])), fmaxf(sc[t][2], sc[t][3]));
     rmax = fmaxf(rmax, __shfl_xor(rmax, 16, 64));
     rmax = fmaxf(rmax, __shfl_xor(rmax, 32, 64));
     const float m_new = fmaxf(m_run, rmax);
-    const float corr = __expf(m_run - m_new);
+    const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
     float rsum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float p = __expf(sc[t][e] - m_new);
-        rsum += p;
-        const uint32_t idx = (uint32_t)((((int64_t)b * a.nh + h) * S + i) * S + j0 + 16 * t + 4 * lg + e);
-        sc[t][e] = dk.on ? (drop_keep(dk, idx) ? p * dk.scale : 0.f) : p;
+        sc[t][e] = __builtin_amdgcn_exp2f(sc[t][e] - m_new);
+        rsum += sc[t][e];
       }
+    if (dk.on) {
+      const uint32_t dbase = (uint32_t)((bh * S + i) * S) + 4 * lg + j0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float kp[4];
+        keep4_row<EVEN>(dk, dbase + (uint32_t)(16 * t), kp);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sc[t][e] *= kp[e];
+      }
+    }
     rsum += __shfl_xor(rsum, 16, 64);
     rsum += __shfl_xor(rsum, 32, 64);
     l_run = l_run * corr + rsum;
@@ -289,121 +493,192 @@ __global__ __launch_bounds__(256, 2) void dis_fwd_kernel(DisArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) o[u] *= corr;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const uint4 af = freg(sc[2 * c], sc[2 * c + 1]);
+    for (int cc = 0; cc < 2; ++cc) {
+      const uint4 af = freg(sc[2 * cc], sc[2 * cc + 1]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(o[u], ft<TP>(L.sV, 16 * u, c, lane), af);
+      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(o[u], ft<TP>(L.sV, 16 * u, cc, lane), af);
     }
-    __syncthreads();
-  }
-  if (!irow) return;
-  const float inv = 1.f / l_run;
-  bf16_t* dst = a.ctx + (rowb + i) * a.ldctx + h * DH;
+    if (last_k) {                         // query block done: write it, move to the next one
+      if (i < S) {
+        const float inv = 1.f / l_run;
+        bf16_t* dst = a.ctx + (rowb + i) * a.ldctx + h * DH;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), o[u] * inv);
-  if (lg == 0) a.lse[((int64_t)b * a.nh + h) * S + i] = m_run + __logf(l_run);
+        for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), o[u] * inv);
+        if (lg == 0) a.lse[bh * S + i] = m_run + __log2f(l_run);
+      }
+      m_run = -INFINITY;
+      l_run = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      i = in_;
+      qvalid = in_ < S && nqm != 0;
+      qf[0] = nqf0;
+      qf[1] = nqf1;
+    }
+    __syncthreads();                      // every wave is done with this pair's LDS
+    if (more) {
+      qrows_store(nx, L, S, kbn * 64, c, tid);
+      put_win(L.sPK, nwk, tid);
+      put_win(L.sPQ, nwq, tid);
+    }
+    qb = qbn;
+    kb = kbn;
+    (void)i0;
+  }
 }
 
+// Query-side backward, one workgroup per (batch, head) like dis_fwd_bh_kernel.  At the start
+// every thread computes D_i = dO_i·O_i of one row of the head (written to dsum for dis_dkv and
+// kept in LDS with the row's lse), so moving to the next query block needs only its Q / dO
+// fragments, which are prefetched with each pair's staging.
+struct QRowData {
+  float lse_s[MAXS];      // lse - log2 inv_scale (log2 units), +inf for padded rows
+  float d[MAXS];          // D_i
+};
+template <bool EVEN>
 __global__ __launch_bounds__(256, 2) void dis_dq_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) QSide L;
+  __shared__ QRowData R;
   __shared__ int s_end;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const BH id = bh_of(a);
+  const int h = id.h, b = id.b;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
-  const int S = a.S, i0 = qb * 64, i = i0 + 16 * w + li;
+  const int S = a.S;
   const int64_t rowb = (int64_t)b * S;
+  const int64_t bh = (int64_t)b * a.nh + h;
   const DropKeys dk = resolve_drop(a.drop);
-  const bool irow = i < S;
+  const float l2s = __log2f(a.inv_scale);
+  load_delta(L.sDel, a);
+  for (int r = tid; r < S; r += 256) {   // D and lse of every row of this head
+    const bf16_t* o = a.ctx + (rowb + r) * a.ldctx + h * DH;
+    const bf16_t* go = a.dctx + (rowb + r) * a.lddctx + h * DH;
+    float acc = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) {
+      float x[8], y[8];
+      unpack8(*reinterpret_cast<const uint4*>(o + 8 * cc), x);
+      unpack8(*reinterpret_cast<const uint4*>(go + 8 * cc), y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
+    }
+    const bool qv = a.mask[rowb + r] != 0;
+    a.dsum[bh * S + r] = acc;
+    R.d[r] = acc;
+    R.lse_s[r] = qv ? a.lse[bh * S + r] - l2s : INFINITY;
+  }
   const int send = seq_end(a, rowb, &s_end);
-  if (i0 >= send) {                      // padded query block: dS = 0, so dQ = 0 and D = 0
-    if (!irow) return;
+  const int nlive = (send + 63) / 64;
+  for (int qb = nlive; qb < a.nqb; ++qb) {   // padded query block: dS = 0, so dQ = 0
+    const int i = qb * 64 + 16 * w + li;
+    if (i >= S) break;
     bf16_t* dst = a.dq + (rowb + i) * a.lddqkv + h * DH;
 #pragma unroll
     for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), f32x4_t{0.f, 0.f, 0.f, 0.f});
-    if (lg == 0) a.dsum[((int64_t)b * a.nh + h) * S + i] = 0.f;
-    return;
   }
-  const bool qvalid = irow && a.mask[rowb + i] != 0;
-  const uint4 qf[2] = {fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 0, lane),
-                       fglob(a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i, S, 1, lane)};
-  const uint4 of[2] = {fglob(a.dctx + rowb * a.lddctx + h * DH, a.lddctx, i, S, 0, lane),
-                       fglob(a.dctx + rowb * a.lddctx + h * DH, a.lddctx, i, S, 1, lane)};
-  // D_i = dO_i · O_i (lanes li, li+16, li+32, li+48 split the row)
-  float Di = 0.f;
-  {
-    const int ic = min(i, S - 1);
-    const bf16_t* o = a.ctx + (rowb + ic) * a.ldctx + h * DH + 16 * lg;
-    const bf16_t* go = a.dctx + (rowb + ic) * a.lddctx + h * DH + 16 * lg;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      float x[8], y[8];
-      unpack8(*reinterpret_cast<const uint4*>(o + 8 * c), x);
-      unpack8(*reinterpret_cast<const uint4*>(go + 8 * c), y);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Di += x[e] * y[e];
-    }
-    Di += __shfl_xor(Di, 16, 64);
-    Di += __shfl_xor(Di, 32, 64);
-    if (!irow) Di = 0.f;
-    if (irow && lg == 0) a.dsum[((int64_t)b * a.nh + h) * S + i] = Di;
-  }
-  const float lse = irow ? a.lse[((int64_t)b * a.nh + h) * S + i] : 0.f;
+  if (nlive == 0) return;
+  const float c = a.inv_scale * LOG2E;
+  const bf16_t* qbase = a.q + rowb * a.ldqkv + h * DH;
+  const bf16_t* obase = a.dctx + rowb * a.lddctx + h * DH;
+  int i = 16 * w + li;
+  uint4 qf[2] = {fglob(qbase, a.ldqkv, i, S, 0, lane), fglob(qbase, a.ldqkv, i, S, 1, lane)};
+  uint4 of[2] = {fglob(obase, a.lddctx, i, S, 0, lane), fglob(obase, a.lddctx, i, S, 1, lane)};
+  qside_prologue(L, a, rowb, h, 0, c, tid);
   f32x4_t dq[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) dq[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   char* priv = L.sPQ + 16 * w * WP;
-  for (int j0 = 0; j0 < send; j0 += 64) {
-    qside_stage(L, a, b, h, i0, j0, tid, w, lane);
-    f32x4_t sc[4], dp[4];
-    qside_scores(L, a, qf, qvalid, w, lane, sc);
+  int qb = 0, kb = 0;
+  const int npairs = nlive * nlive;
+  for (int p = 0; p < npairs; ++p) {
+    const int j0 = kb * 64;
+    const bool last_k = kb + 1 == nlive;
+    const int qbn = last_k ? qb + 1 : qb, kbn = last_k ? 0 : kb + 1;
+    const bool more = p + 1 < npairs;
+    __syncthreads();                      // staging of the pair is in LDS (and R, at p = 0)
+    QRows nx;
+    qrows_load(nx, a, rowb, h, kbn * 64, tid);   // clamped: valid on the last pair too
+    const int in_ = qbn * 64 + 16 * w + li;
+    const uint4 nqf0 = fglob(qbase, a.ldqkv, in_, S, 0, lane), nqf1 = fglob(qbase, a.ldqkv, in_, S, 1, lane);
+    const uint4 nof0 = fglob(obase, a.lddctx, in_, S, 0, lane), nof1 = fglob(obase, a.lddctx, in_, S, 1, lane);
+    win_product(L.sPQ, fk<TP>(L.sK, 16 * w, 0, lane), fk<TP>(L.sK, 16 * w, 1, lane),
+                L.sX + 16 * w * WP, lane);
+    __syncthreads();
+    const int ic = min(i, S - 1);
+    const float lse_s = i < S ? R.lse_s[ic] : INFINITY;   // p·inv_scale = 2^(s - lse_s)
+    const float Di = i < S ? R.d[ic] : 0.f;
+    uint4 dsf[2];                         // dS as bf16 MFMA operands (16 scores per lane)
+    {
+      f32x4_t sc[4], dp[4];
+      qside_raw(L, qf, w, lane, sc);
+      apply_cols(L.sCol[0], lg, sc);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      dp[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      Mma<bf16_t>::run(dp[t], fk<TP>(L.sV, 16 * t, 0, lane), of[0]);
-      Mma<bf16_t>::run(dp[t], fk<TP>(L.sV, 16 * t, 1, lane), of[1]);
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int jl = 16 * t + 4 * lg + e;
-        const float mk = L.sMk[jl];
-        // a fully padded query row attends uniformly to the S keys (finfo.min everywhere);
-        // its masked_fill'ed scores are constants and receive no gradient
-        const float p = !irow ? 0.f : (qvalid ? __expf(sc[t][e] - lse) : (mk >= 0.f ? 1.f / (float)S : 0.f));
-        const uint32_t idx = (uint32_t)((((int64_t)b * a.nh + h) * S + i) * S + j0 + jl);
-        const float keep = dk.on ? (drop_keep(dk, idx) ? dk.scale : 0.f) : 1.f;
-        sc[t][e] = qvalid ? p * (dp[t][e] * keep - Di) * a.inv_scale : 0.f;   // d raw score
+      for (int t = 0; t < 4; ++t) {
+        dp[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        Mma<bf16_t>::run(dp[t], fk<TP>(L.sV, 16 * t, 0, lane), of[0]);
+        Mma<bf16_t>::run(dp[t], fk<TP>(L.sV, 16 * t, 1, lane), of[1]);
       }
+      const uint32_t dbase = (uint32_t)((bh * S + i) * S) + 4 * lg + j0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float kp[4] = {1.f, 1.f, 1.f, 1.f};
+        if (dk.on) keep4_row<EVEN>(dk, dbase + (uint32_t)(16 * t), kp);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)       // d raw score = p·(dP·keep - D)·inv_scale
+          sc[t][e] = __builtin_amdgcn_exp2f(sc[t][e] - lse_s) * fmaf(dp[t][e], kp[e], -Di);
+      }
+      dsf[0] = freg(sc[0], sc[1]);
+      dsf[1] = freg(sc[2], sc[3]);
+    }
     // dQ += dS·K
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const uint4 af = freg(sc[2 * c], sc[2 * c + 1]);
+    for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dq[u], ft<TP>(L.sK, 16 * u, c, lane), af);
-    }
+      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dq[u], ft<TP>(L.sK, 16 * u, cc, lane), dsf[cc]);
+    u32x4 nwk[4], nwq[4];                 // next pair's windows (clamped: valid on the last pair)
+    pf_win(nwk, L.sDel, a.posk + h * DH, a.ldpos, qbn * 64 - kbn * 64 - 63, S, tid);
+    pf_win(nwq, L.sDel, a.posq + h * DH, a.ldpos, qbn * 64 - kbn * 64 - 63, S, tid);
     // SkewQ[il][r] = dS[il][il - r + 63] (private image, after this wave's c2p reads)
     zero_rows16(priv, lane);
     {
       bf16_t* pr = reinterpret_cast<bf16_t*>(priv) + li * (WP / 2);
       const int il = 16 * w + li;
+      const uint32_t wv[8] = {dsf[0].x, dsf[0].y, dsf[0].z, dsf[0].w, dsf[1].x, dsf[1].y, dsf[1].z, dsf[1].w};
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pr[il - (16 * t + 4 * lg + e) + 63] = f2bf(sc[t][e]);
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t x = wv[2 * t + (e >> 1)];
+          pr[il - (16 * t + 4 * lg + e) + 63] = (bf16_t)((e & 1) ? x >> 16 : x & 0xFFFFu);
+        }
     }
     // dQ += SkewQ·PKexp
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint4 af = fk<WP>(priv, 0, c, lane);
+    for (int cc = 0; cc < 4; ++cc) {
+      const uint4 af = fk<WP>(priv, 0, cc, lane);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dq[u], ft<TP>(L.sPK, 16 * u, c, lane), af);
+      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dq[u], ft<TP>(L.sPK, 16 * u, cc, lane), af);
+    }
+    if (last_k) {                         // query block done: write dQ, move to the next one
+      if (i < S) {
+        bf16_t* dst = a.dq + (rowb + i) * a.lddqkv + h * DH;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), dq[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dq[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      i = in_;
+      qf[0] = nqf0; qf[1] = nqf1;
+      of[0] = nof0; of[1] = nof1;
     }
     __syncthreads();
+    if (more) {
+      qrows_store(nx, L, S, kbn * 64, c, tid);
+      put_win(L.sPK, nwk, tid);
+      put_win(L.sPQ, nwq, tid);
+    }
+    qb = qbn;
+    kb = kbn;
   }
-  if (!irow) return;
-  bf16_t* dst = a.dq + (rowb + i) * a.lddqkv + h * DH;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) st_bf4(reinterpret_cast<char*>(dst + 16 * u + 4 * lg), dq[u]);
 }
 
 // ------------------------------------------------------------------ key side
@@ -415,10 +690,80 @@ struct KSide {
   char sX[64 * WP];       // shared c2p [query il][r], then SkewK [key jl][r]
   char sU[WIN * UP];      // Uexp [r][16] (8 used)
   char sKB[64 * UP];      // KB [key jl][16] (8 used)
-  float sLse[64], sD[64], sQm[64];
+  float sRowA[64], sRowD[64];   // per query row: -lse (log2; -inf for padded rows), D
+  int16_t sDel[2 * MAXS];
 };
 static_assert(4 * 16 * WP <= WIN * TP, "private images must fit the PKexp window");
 static_assert(sizeof(KSide) <= 80 * 1024, "two workgroups per CU");
+
+// The next query block's staging, held in registers across a block pair: query rows, dO
+// rows and the per-row softmax data (loaded right after the staging barrier), then the whole
+// PKexp (its LDS holds the waves' private images during a pair), the 64 new rows of the
+// sliding PQexp and Uexp (loaded after the score phase, when fewer registers are live).
+struct KRows {
+  u32x4 q[2], o[2];
+  float lse, d;           // query row i0 + tid (tid < 64)
+  int64_t qm;
+};
+struct KWins {
+  u32x4 pk[4], pq[2];
+  float4 u;               // Uexp row tid >> 1, columns 4·(tid & 1) ..
+};
+TTMI_DEV void krows_load(KRows& st, const DisArgs& a, int64_t rowb, int64_t bh, int h, int i0, int tid) {
+  pf_rows(st.q, a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i0, a.S, tid);
+  pf_rows(st.o, a.dctx + rowb * a.lddctx + h * DH, a.lddctx, i0, a.S, tid);
+  const int ic = min(i0 + (tid & 63), a.S - 1);    // unconditional loads (see qrows_load)
+  st.lse = a.lse[bh * a.S + ic];
+  st.d = a.dsum[bh * a.S + ic];
+  st.qm = a.mask[rowb + ic];
+}
+TTMI_DEV void load_u(float4& u, const int16_t* sdel, const DisArgs& a, int rel0, int tid) {
+  const int rel = min(max(rel0 + (tid >> 1), -(a.S - 1)), a.S - 1);
+  u = *reinterpret_cast<const float4*>(a.u + (int64_t)sdel[rel + a.S - 1] * 8 + (tid & 1) * 4);
+}
+TTMI_DEV void kwins_load(KWins& st, const KSide& L, const DisArgs& a, int h, int i0, int j0, bool lora,
+                         int tid) {
+  const int rel0 = i0 - j0 - 63;
+  pf_win(st.pk, L.sDel, a.posk + h * DH, a.ldpos, rel0, a.S, tid);
+  pf_win_half(st.pq, L.sDel, a.posq + h * DH, a.ldpos, rel0 + 64, a.S, tid);
+  if (lora) load_u(st.u, L.sDel, a, rel0, tid);
+}
+TTMI_DEV void put_u(KSide& L, const float4& u, int tid) {
+  uint32_t* row = reinterpret_cast<uint32_t*>(L.sU + (tid >> 1) * UP) + (tid & 1) * 2;
+  row[0] = pk2(u.x, u.y);
+  row[1] = pk2(u.z, u.w);
+  row[4] = 0u;
+  row[5] = 0u;
+}
+TTMI_DEV void krows_store(const KRows& st, KSide& L, int S, int i0, int tid) {
+  put_rows(L.sQ, st.q, i0, S, tid);
+  put_rows(L.sdO, st.o, i0, S, tid);
+  if (tid < 64) {
+    // valid query row: p = 2^(s - lse); padded rows (dO = 0 there) and rows past S: p = 0
+    const bool ok = i0 + tid < S && st.qm != 0;
+    L.sRowA[tid] = ok ? -st.lse : -INFINITY;
+    L.sRowD[tid] = ok ? st.d : 0.f;
+  }
+}
+TTMI_DEV void kwins_store(const KWins& st, KSide& L, bool lora, int tid) {
+  put_win(L.sPK, st.pk, tid);
+  put_win_slide<false>(L.sPQ, st.pq, tid);
+  if (lora) put_u(L, st.u, tid);
+}
+TTMI_DEV void kside_prologue(KSide& L, const DisArgs& a, int64_t rowb, int64_t bh, int h, int j0,
+                             bool lora, int tid) {
+  KRows st;
+  krows_load(st, a, rowb, bh, h, 0, tid);
+  u32x4 pk[4], pq[4];
+  float4 u;
+  pf_win(pk, L.sDel, a.posk + h * DH, a.ldpos, -j0 - 63, a.S, tid);
+  pf_win(pq, L.sDel, a.posq + h * DH, a.ldpos, -j0 - 63, a.S, tid);
+  if (lora) load_u(u, L.sDel, a, -j0 - 63, tid);
+  krows_store(st, L, a.S, 0, tid);
+  put_win(L.sPK, pk, tid);
+  put_win(L.sPQ, pq, tid);
+  if (lora) put_u(L, u, tid);
+}
 
 // PBexp of a skipped (query block, key block) pair: zero (dis_pb sums every pair).
 TTMI_DEV void zero_pbx(const DisArgs& a, int64_t bh, int qb, int kb) {
@@ -427,10 +772,12 @@ TTMI_DEV void zero_pbx(const DisArgs& a, int64_t bh, int qb, int kb) {
     reinterpret_cast<float4*>(dst)[t] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+template <bool EVEN>
 __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) KSide L;
   __shared__ int s_end;
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const Tile tl = tile_of(a);
+  const int kb = tl.blk, h = tl.h, b = tl.b;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
   const int S = a.S, j0 = kb * 64, jl = 16 * w + li, j = j0 + jl;
   const int64_t rowb = (int64_t)b * S;
@@ -438,10 +785,14 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
   const DropKeys dk = resolve_drop(a.drop);
   const bool lora = a.u != nullptr;
   const bool jrow = j < S;
+  load_delta(L.sDel, a);
   const int send = seq_end(a, rowb, &s_end);
+  const int nlive = (send + 63) / 64;    // live query blocks: qb < nlive
+  if (lora)                              // padded query blocks: dS = 0 and dO = 0
+    for (int qb = nlive; qb < a.nqb; ++qb) zero_pbx(a, bh, qb, kb);
   if (j0 >= send) {                      // padded key block: masked for every valid query
     if (lora)
-      for (int qb = 0; qb < a.nqb; ++qb) zero_pbx(a, bh, qb, kb);
+      for (int qb = 0; qb < nlive; ++qb) zero_pbx(a, bh, qb, kb);
     if (!jrow) return;
     bf16_t* pk = a.dk + (rowb + j) * a.lddqkv + h * DH;
     bf16_t* pv = a.dv + (rowb + j) * a.lddqkv + h * DH;
@@ -455,7 +806,10 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
       *reinterpret_cast<float4*>(a.hu + ((rowb + j) * a.nh + h) * 8 + 4 * lg) = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
+  const float c = a.inv_scale * LOG2E;
   const bool kvalid = jrow && a.mask[rowb + j] != 0;
+  const float kbias = kvalid ? 0.f : -INFINITY;   // masked key / past S: p = 0
+  const float l2s = __log2f(a.inv_scale);
   const uint4 kf[2] = {fglob(a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 0, lane),
                        fglob(a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 1, lane)};
   const uint4 vf[2] = {fglob(a.v + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 0, lane),
@@ -478,102 +832,92 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
     row[c0 / 2] = pk2(s0, s1);
     row[4 + c0 / 2] = 0u;
   }
+  kside_prologue(L, a, rowb, bh, h, j0, lora, tid);
   f32x4_t dka[4], dva[4], hua;
 #pragma unroll
   for (int u = 0; u < 4; ++u) dka[u] = dva[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   hua = f32x4_t{0.f, 0.f, 0.f, 0.f};
   char* priv = L.sPK + 16 * w * WP;
-  for (int qb = 0; qb < a.nqb; ++qb) {
-    const int i0 = qb * 64, rel0 = i0 - j0 - 63;
-    if (i0 >= send) {                    // padded query block: dS = 0 and dO = 0
-      if (lora) zero_pbx(a, bh, qb, kb);
-      continue;
-    }
-    stage_rows<64>(L.sQ, a.q + rowb * a.ldqkv + h * DH, a.ldqkv, i0, S, tid);
-    stage_rows<64>(L.sdO, a.dctx + rowb * a.lddctx + h * DH, a.lddctx, i0, S, tid);
-    stage_win(L.sPK, a, a.posk + h * DH, rel0, tid);
-    stage_win(L.sPQ, a, a.posq + h * DH, rel0, tid);
-    if (tid < 64) {
-      const int i = i0 + tid;
-      const bool ok = i < S;
-      L.sLse[tid] = ok ? a.lse[bh * S + i] : 0.f;
-      L.sD[tid] = ok ? a.dsum[bh * S + i] : 0.f;
-      L.sQm[tid] = ok ? (a.mask[rowb + i] != 0 ? 1.f : 0.f) : -1.f;
-    }
-    if (lora) {
-      const int r = tid >> 1, c0 = (tid & 1) * 4;
-      const float* ur = a.u + (int64_t)win_row(a, rel0 + r) * 8 + c0;
-      uint32_t* row = reinterpret_cast<uint32_t*>(L.sU + r * UP);
-      row[c0 / 2] = pk2(ur[0], ur[1]);
-      row[c0 / 2 + 1] = pk2(ur[2], ur[3]);
-      row[4 + c0 / 2] = 0u;
-      row[5 + c0 / 2] = 0u;
-    }
-    __syncthreads();
+  const bool odd_lane = li & 1;
+  for (int qb = 0; qb < nlive; ++qb) {
+    const int i0 = qb * 64;
+    __syncthreads();                      // staging of pair (i0, j0) is in LDS
+    const bool more = qb + 1 < nlive;
+    KRows nx;
+    KWins nw;
+    krows_load(nx, a, rowb, bh, h, i0 + 64, tid);      // clamped: valid on the last pair too
     // shared c2p: this wave's 16 queries against PKexp
     win_product(L.sPK, fk<TP>(L.sQ, 16 * w, 0, lane), fk<TP>(L.sQ, 16 * w, 1, lane),
                 L.sX + 16 * w * WP, lane);
     __syncthreads();
     // private p2c: own 16 keys against PQexp (into the dead PKexp window)
     win_product(L.sPQ, kf[0], kf[1], priv, lane);
-    f32x4_t sc[4], dp[4];
+    uint4 pdf[2], dsf[2];                 // P·keep and dS as bf16 MFMA operands
+    {
+      f32x4_t sc[4], dp[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sc[t] = dp[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      Mma<bf16_t>::run(sc[t], fk<TP>(L.sQ, 16 * t, 0, lane), kf[0]);
-      Mma<bf16_t>::run(sc[t], fk<TP>(L.sQ, 16 * t, 1, lane), kf[1]);
-      Mma<bf16_t>::run(dp[t], fk<TP>(L.sdO, 16 * t, 0, lane), vf[0]);
-      Mma<bf16_t>::run(dp[t], fk<TP>(L.sdO, 16 * t, 1, lane), vf[1]);
-    }
-    f32x4_t pd[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float4 lse4 = *reinterpret_cast<const float4*>(L.sLse + 16 * t + 4 * lg);
-      const float4 d4 = *reinterpret_cast<const float4*>(L.sD + 16 * t + 4 * lg);
-      const float4 qm4 = *reinterpret_cast<const float4*>(L.sQm + 16 * t + 4 * lg);
-      const float lse_[4] = {lse4.x, lse4.y, lse4.z, lse4.w}, d_[4] = {d4.x, d4.y, d4.z, d4.w};
-      const float qm_[4] = {qm4.x, qm4.y, qm4.z, qm4.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int il = 16 * t + 4 * lg + e, r = il - jl + 63;
-        const float raw = sc[t][e] + lds_bf(L.sX, il * (WP / 2) + r) + lds_bf(priv, li * (WP / 2) + r);
-        const bool qv = qm_[e] > 0.f, irow = qm_[e] >= 0.f;
-        const float s = (qv && kvalid) ? raw * a.inv_scale : FMIN;
-        const float p = (!irow || !jrow) ? 0.f : (qv ? __expf(s - lse_[e]) : 1.f / (float)S);
-        const uint32_t idx = (uint32_t)((bh * S + i0 + il) * S + j);
-        const float keep = dk.on ? (drop_keep(dk, idx) ? dk.scale : 0.f) : 1.f;
-        pd[t][e] = p * keep;
-        sc[t][e] = qv ? p * (dp[t][e] * keep - d_[e]) * a.inv_scale : 0.f;      // d raw score
+      for (int t = 0; t < 4; ++t) {
+        sc[t] = dp[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        Mma<bf16_t>::run(sc[t], fk<TP>(L.sQ, 16 * t, 0, lane), kf[0]);
+        Mma<bf16_t>::run(sc[t], fk<TP>(L.sQ, 16 * t, 1, lane), kf[1]);
+        Mma<bf16_t>::run(dp[t], fk<TP>(L.sdO, 16 * t, 0, lane), vf[0]);
+        Mma<bf16_t>::run(dp[t], fk<TP>(L.sdO, 16 * t, 1, lane), vf[1]);
       }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 ra = *reinterpret_cast<const float4*>(L.sRowA + 16 * t + 4 * lg);
+        const float4 rd = *reinterpret_cast<const float4*>(L.sRowD + 16 * t + 4 * lg);
+        const float ra_[4] = {ra.x, ra.y, ra.z, ra.w}, rd_[4] = {rd.x, rd.y, rd.z, rd.w};
+        float kp[4] = {1.f, 1.f, 1.f, 1.f};
+        if (dk.on)
+          keep4_col<EVEN>(dk, (uint32_t)((bh * S + i0 + 16 * t + 4 * lg) * S + j), (uint32_t)S, odd_lane, kp);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int il = 16 * t + 4 * lg + e, r = il - jl + 63;
+          const float raw = sc[t][e] + lds_bf(L.sX, il * (WP / 2) + r) + lds_bf(priv, li * (WP / 2) + r);
+          const float arg = fmaf(raw, c, ra_[e] + kbias);
+          const float p = __builtin_amdgcn_exp2f(arg);
+          // d raw score = p·(dP·keep - D)·inv_scale
+          sc[t][e] = __builtin_amdgcn_exp2f(arg + l2s) * fmaf(dp[t][e], kp[e], -rd_[e]);
+          dp[t][e] = p * kp[e];
+        }
+      }
+      pdf[0] = freg(dp[0], dp[1]);
+      pdf[1] = freg(dp[2], dp[3]);
+      dsf[0] = freg(sc[0], sc[1]);
+      dsf[1] = freg(sc[2], sc[3]);
     }
     // dV += Pdᵀ·dO, dK += dSᵀ·Q
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const uint4 ap = freg(pd[2 * c], pd[2 * c + 1]), as = freg(sc[2 * c], sc[2 * c + 1]);
+    for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        Mma<bf16_t>::run(dva[u], ft<TP>(L.sdO, 16 * u, c, lane), ap);
-        Mma<bf16_t>::run(dka[u], ft<TP>(L.sQ, 16 * u, c, lane), as);
+        Mma<bf16_t>::run(dva[u], ft<TP>(L.sdO, 16 * u, cc, lane), pdf[cc]);
+        Mma<bf16_t>::run(dka[u], ft<TP>(L.sQ, 16 * u, cc, lane), dsf[cc]);
       }
-    }
+    kwins_load(nw, L, a, h, i0 + 64, j0, lora, tid);   // clamped: valid on the last pair too
     __syncthreads();                      // every wave is done reading the shared c2p image
     // SkewK[jl][r] = dS[jl + r - 63][jl] (own rows of sX)
     char* skew = L.sX + 16 * w * WP;
     zero_rows16(skew, lane);
     {
       bf16_t* pr = reinterpret_cast<bf16_t*>(skew) + li * (WP / 2);
+      const uint32_t wv[8] = {dsf[0].x, dsf[0].y, dsf[0].z, dsf[0].w, dsf[1].x, dsf[1].y, dsf[1].z, dsf[1].w};
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pr[16 * t + 4 * lg + e - jl + 63] = f2bf(sc[t][e]);
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t x = wv[2 * t + (e >> 1)];
+          pr[16 * t + 4 * lg + e - jl + 63] = (bf16_t)((e & 1) ? x >> 16 : x & 0xFFFFu);
+        }
     }
     // dK += SkewK·PQexp;  HU += SkewK·Uexp
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint4 af = fk<WP>(skew, 0, c, lane);
+    for (int cc = 0; cc < 4; ++cc) {
+      const uint4 af = fk<WP>(skew, 0, cc, lane);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dka[u], ft<TP>(L.sPQ, 16 * u, c, lane), af);
-      if (lora) Mma<bf16_t>::run(hua, ft<UP>(L.sU, 0, c, lane), af);
+      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(dka[u], ft<TP>(L.sPQ, 16 * u, cc, lane), af);
+      if (lora) Mma<bf16_t>::run(hua, ft<UP>(L.sU, 0, cc, lane), af);
     }
     if (lora) {
       __syncthreads();                    // all SkewK rows written
@@ -583,7 +927,7 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
         const int rt = 2 * w + q;
         f32x4_t pbv = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 2; ++c) Mma<bf16_t>::run(pbv, ft<UP>(L.sKB, 0, c, lane), ft<WP>(L.sX, 16 * rt, c, lane));
+        for (int cc = 0; cc < 2; ++cc) Mma<bf16_t>::run(pbv, ft<UP>(L.sKB, 0, cc, lane), ft<WP>(L.sX, 16 * rt, cc, lane));
         if (lg < 2) {
           float* dst = a.pbx + (((bh * a.nqb + qb) * a.nqb + kb) * WIN + 16 * rt + li) * 8 + 4 * lg;
           *reinterpret_cast<float4*>(dst) = make_float4(pbv[0], pbv[1], pbv[2], pbv[3]);
@@ -591,6 +935,10 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
       }
     }
     __syncthreads();
+    if (more) {
+      krows_store(nx, L, S, i0 + 64, tid);
+      kwins_store(nw, L, lora, tid);
+    }
   }
   if (!jrow) return;
   bf16_t* pk = a.dk + (rowb + j) * a.lddqkv + h * DH;
@@ -649,7 +997,46 @@ static DisArgs dis_args(const ttmi_dis_attn_desc* d) {
   a.dq = (bf16_t*)d->dq; a.dk = (bf16_t*)d->dk; a.dv = (bf16_t*)d->dv; a.lddqkv = d->lddqkv;
   a.dsum = d->dq_scratch;
   a.u = d->lora_u; a.bq = d->lora_bq; a.hu = d->lora_hu; a.pb = d->lora_pb; a.pbx = d->lora_pbx;
+  a.order = d->order;
   return a;
+}
+
+namespace {
+// Counting sort of the batch rows by live block count (descending); one workgroup.
+__global__ __launch_bounds__(1024) void dis_order_kernel(const int64_t* mask, int B, int S, int32_t* order) {
+  __shared__ int cnt[MAXS / 64 + 2], base[MAXS / 64 + 2];
+  const int nq = (S + 63) / 64;
+  if (threadIdx.x <= nq) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  // one wave per batch row: live blocks = ceil(end / 64), end = 1 + last set position
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int b = wv; b < B; b += nw) {
+    int e = 0;
+    for (int t = lane; t < S; t += 64)
+      if (mask[(int64_t)b * S + t] != 0) e = t + 1;
+    for (int o = 32; o > 0; o >>= 1) e = max(e, __shfl_xor(e, o, 64));
+    if (lane == 0) atomicAdd(&cnt[(e + 63) / 64], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {                // descending: the most live blocks first
+    int acc = 0;
+    for (int n = nq; n >= 0; --n) { base[n] = acc; acc += cnt[n]; }
+  }
+  __syncthreads();
+  for (int b = wv; b < B; b += nw) {
+    int e = 0;
+    for (int t = lane; t < S; t += 64)
+      if (mask[(int64_t)b * S + t] != 0) e = t + 1;
+    for (int o = 32; o > 0; o >>= 1) e = max(e, __shfl_xor(e, o, 64));
+    if (lane == 0) order[atomicAdd(&base[(e + 63) / 64], 1)] = b;
+  }
+}
+}  // namespace
+
+extern "C" int ttmi_dis_attn_order(const int64_t* mask, int B, int S, int32_t* order, hipStream_t s) {
+  TTMI_REQUIRE(mask && order && B > 0 && S > 0 && S <= MAXS, "ttmi_dis_attn_order: bad arguments (S <= %d)", MAXS);
+  hipLaunchKernelGGL(dis_order_kernel, dim3(1), dim3(1024), 0, s, mask, B, S, order);
+  return ttmi_check_launch("ttmi_dis_attn_order");
 }
 
 extern "C" int64_t ttmi_dis_attn_pbx_floats(int B, int S, int nh) {
@@ -661,7 +1048,9 @@ extern "C" int ttmi_dis_attn_fwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
   int rc = dis_check(d);
   if (rc) return rc;
   const DisArgs a = dis_args(d);
-  hipLaunchKernelGGL(dis_fwd_kernel, dim3((unsigned)a.nqb, (unsigned)d->nh, (unsigned)d->B), dim3(256), 0, s, a);
+  const dim3 grid((unsigned)(d->nh * d->B));
+  if (d->S % 2 == 0) hipLaunchKernelGGL(dis_fwd_bh_kernel<true>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dis_fwd_bh_kernel<false>, grid, dim3(256), 0, s, a);
   return ttmi_check_launch("ttmi_dis_attn_fwd");
 }
 
@@ -674,9 +1063,14 @@ extern "C" int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
   TTMI_REQUIRE(!d->lora_u || (d->lora_bq && d->lora_hu && d->lora_pb && d->lora_pbx),
                "ttmi_dis_attn_bwd: LoRA outputs need u, bq, hu, pb and the pbx workspace together");
   const DisArgs a = dis_args(d);
-  const dim3 grid((unsigned)a.nqb, (unsigned)d->nh, (unsigned)d->B);
-  hipLaunchKernelGGL(dis_dq_kernel, grid, dim3(256), 0, s, a);
-  hipLaunchKernelGGL(dis_dkv_kernel, grid, dim3(256), 0, s, a);
+  const dim3 grid((unsigned)(a.nqb * d->nh * d->B)), grid_bh((unsigned)(d->nh * d->B));
+  if (d->S % 2 == 0) {
+    hipLaunchKernelGGL(dis_dq_kernel<true>, grid_bh, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(dis_dkv_kernel<true>, grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(dis_dq_kernel<false>, grid_bh, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(dis_dkv_kernel<false>, grid, dim3(256), 0, s, a);
+  }
   if (d->lora_u) {
     if (hipMemsetAsync(d->lora_pb, 0, (size_t)d->npos * 8 * sizeof(float), s) != hipSuccess)
       return ttmi_check_launch("ttmi_dis_attn_bwd (pb memset)");

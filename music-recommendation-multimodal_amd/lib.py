@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -75,7 +75,7 @@ class DisAttnDesc(ctypes.Structure):
                 ("dctx", c_p), ("lddctx", ctypes.c_int64),
                 ("dq", c_p), ("dk", c_p), ("dv", c_p), ("lddqkv", ctypes.c_int64),
                 ("lora_u", c_p), ("lora_bq", c_p), ("lora_hu", c_p), ("lora_pb", c_p),
-                ("dq_scratch", c_p), ("lora_pbx", c_p)]
+                ("dq_scratch", c_p), ("lora_pbx", c_p), ("order", c_p)]
 
 
 class LnBwdDesc(ctypes.Structure):
@@ -167,6 +167,7 @@ SIGNATURES = {
     "ttmi_dis_attn_fwd": (c_i, [c_p, c_p]),
     "ttmi_dis_attn_bwd": (c_i, [c_p, c_p]),
     "ttmi_dis_attn_pbx_floats": (ctypes.c_int64, [c_i, c_i, c_i]),
+    "ttmi_dis_attn_order": (c_i, [c_p, c_i, c_i, c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,

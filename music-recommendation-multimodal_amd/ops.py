@@ -724,9 +724,10 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
              dq: Optional[Tensor] = None, dk: Optional[Tensor] = None,
              dv: Optional[Tensor] = None, lora_u: Optional[Tensor] = None,
              lora_bq: Optional[Tensor] = None, lora_hu: Optional[Tensor] = None,
-             lora_pb: Optional[Tensor] = None) -> None:
+             lora_pb: Optional[Tensor] = None, order: Optional[Tensor] = None) -> None:
     """Disentangled self-attention forward (dctx None) or backward.  q/k/v/ctx/dq/dk/dv are
-    column views (head h at column h·64) sharing a row stride; posq/posk [npos, ·]."""
+    column views (head h at column h·64) sharing a row stride; posq/posk [npos, ·].
+    order: dis_attn_order(mask) of this batch (optional; longest sequences first)."""
     H = nh * 64
     for name, t in (("q", q), ("k", k), ("v", v), ("ctx", ctx)):
         if t.shape[0] != B * S or t.shape[1] < H:
@@ -746,6 +747,10 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
     d.mask, d.delta, d.inv_scale = _p(mask), _p(delta), inv_scale
     d.drop_p, d.drop_seed = float(drop[0]), _p(drop[1])
     d.ctx, d.ldctx, d.lse = _p(ctx), ctx.stride(0), _p(lse)
+    if order is not None:
+        if order.dtype != torch.int32 or order.numel() < B:
+            raise ValueError("dis_attn: order must be int32 [B] (dis_attn_order)")
+        d.order = _p(order)
     if dctx is None:
         call("ttmi_dis_attn_fwd", ctypes.byref(d), _s())
         return
@@ -765,6 +770,15 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
         pbx = torch.empty(int(_L.load().ttmi_dis_attn_pbx_floats(B, S, nh)), device=q.device)
         d.lora_pbx = _p(pbx)
     call("ttmi_dis_attn_bwd", ctypes.byref(d), _s())
+
+
+def dis_attn_order(mask: Tensor, B: int, S: int) -> Tensor:
+    """[B] int32 batch order for dis_attn: sequences by live 64-row blocks, longest first."""
+    if mask.numel() < B * S or mask.dtype != torch.int64:
+        raise ValueError("dis_attn_order: mask must be int64 [B, S]")
+    order = torch.empty(B, device=mask.device, dtype=torch.int32)
+    call("ttmi_dis_attn_order", _p(mask), B, S, _p(order), _s())
+    return order
 
 
 def deb_pool_fwd(x: Tensor, mask: Tensor, out: Tensor) -> Tensor:

@@ -248,6 +248,7 @@ class TextSaved:
     aq16: List[Tensor] = field(default_factory=list)
     av16: List[Tensor] = field(default_factory=list)
     training: bool = True
+    order: Optional[Tensor] = None     # ops.dis_attn_order(mask): per-sequence kernel order
 
 
 def _drop(p: float, seeds: Optional[Tensor], site: int):
@@ -287,6 +288,7 @@ def text_fwd(enc: "TextEncoder", P: Dict[str, Tensor], ids: Tensor, mask: Tensor
     ids = ids.to(torch.int64).contiguous()
     delta = Fz.delta(S, c, dev)
     st = TextSaved(B, S, mask, delta, training=training)
+    st.order = ops.dis_attn_order(mask, B, S)         # shared by every layer's fwd and bwd
     pd = c.hidden_dropout if training else 0.0
     pa = c.attn_dropout if training else 0.0
     pl = c.lora_dropout if training else 0.0
@@ -341,7 +343,7 @@ def text_fwd(enc: "TextEncoder", P: Dict[str, Tensor], ids: Tensor, mask: Tensor
         lse = torch.empty(B * nh * S, device=dev)
         ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], posqk[:, :H],
                      posqk[:, H:], mask, delta, 1.0 / math.sqrt(64 * 3), ctx, lse,
-                     _drop(pa, seeds, tsite(l, 0)))
+                     _drop(pa, seeds, tsite(l, 0)), order=st.order)
         # output projection + residual + LN, FFN + residual + LN
         L = f"encoder.layer.{l}."
         z1 = torch.empty(M, H, device=dev)
@@ -450,7 +452,7 @@ def text_bwd(enc: "TextEncoder", P: Dict[str, Tensor], st: TextSaved, dout: Tens
                      sv.posqk[:, :H], sv.posqk[:, H:], st.mask, st.delta, 1.0 / math.sqrt(64 * 3),
                      sv.ctx, sv.lse, _drop(pa, seeds, tsite(l, 0)), dctx=dctx, dq=dqkv[:, :H],
                      dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:], lora_u=sv.u, lora_bq=bq32,
-                     lora_hu=hu, lora_pb=pb)
+                     lora_hu=hu, lora_pb=pb, order=st.order)
         # input gradient through the QKV GEMM (+ residual) and the LoRA branch.  The rank-8
         # LoRA weight gradients are HBM streams that no later op of this backward reads: they
         # run on a side stream under the (MFMA-bound) dgrad GEMM.  dL goes first so the side

@@ -11,6 +11,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 pkg = importlib.import_module("music-recommendation-multimodal_amd")
 ops, text = pkg.ops, pkg.text
+if os.environ.get("TTMI_LIB"):          # experiment builds (tools only; the product loads lib/)
+    pkg.lib.load(os.environ["TTMI_LIB"])
 
 
 def main(B=256, S=256, nh=12, reps=5):
@@ -32,22 +34,26 @@ def main(B=256, S=256, nh=12, reps=5):
     pb = torch.empty(B * nh * cfg.npos * 8, device=dev)
     scale = 1 / math.sqrt(192)
     drop = (0.1, torch.tensor([12345], dtype=torch.int64, device=dev))
+    order = ops.dis_attn_order(mask, B, S)
 
     def fwd():
         ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:],
-                     mask, delta, scale, ctx, lse, drop)
+                     mask, delta, scale, ctx, lse, drop, order=order)
 
     def bwd():
         ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:],
                      mask, delta, scale, ctx, lse, drop, dctx=dctx, dq=dqkv[:, :H],
                      dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:], lora_u=u, lora_bq=bq, lora_hu=hu,
-                     lora_pb=pb)
+                     lora_pb=pb, order=order)
     def bwd_nolora():
         ops.dis_attn(B, S, nh, qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], pos[:, :H], pos[:, H:],
                      mask, delta, scale, ctx, lse, drop, dctx=dctx, dq=dqkv[:, :H],
-                     dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:])
+                     dk=dqkv[:, H:2 * H], dv=dqkv[:, 2 * H:], order=order)
     pairs = B * nh * (S // 64) ** 2
-    for name, fn, units in (("fwd", fwd, 6), ("bwd", bwd, 13), ("bwd-nolora", bwd_nolora, 13)):
+    cases = (("fwd", fwd, 6), ("bwd", bwd, 13), ("bwd-nolora", bwd_nolora, 13))
+    if os.environ.get("ATTN_FWD_ONLY"):
+        cases = cases[:1]
+    for name, fn, units in cases:
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
