@@ -121,20 +121,6 @@ TTMI_DEV int win_row(const DisArgs& a, int rel) {
   return a.delta[rel + a.S - 1];
 }
 
-// Workgroup -> (block, head, batch): the nqb workgroups of one (batch, head) are consecutive
-// logical ids, and xcd_contiguous keeps consecutive ids on one XCD (their rows share its L2).
-struct Tile { int blk, h, b; };
-TTMI_DEV Tile tile_of(const DisArgs& a) {
-  const int n = a.nqb * a.nh * a.B;
-  const int id = xcd_contiguous((int)blockIdx.x, n);
-  Tile t;
-  t.blk = id % a.nqb;
-  const int bh = id / a.nqb;
-  t.h = bh % a.nh;
-  t.b = bh / a.nh;
-  return t;
-}
-
 // Workgroup -> (batch, head) of the per-sequence kernels: longest sequences first.
 struct BH { int b, h; };
 TTMI_DEV BH bh_of(const DisArgs& a) {
@@ -198,37 +184,6 @@ TTMI_DEV void put_win(char* dst, const u32x4 (&v)[4], int tid) {
   for (int c = 0; c < 4; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
     *reinterpret_cast<u32x4*>(dst + r * TP + ch * 16) = v[c];
-  }
-}
-
-// Sliding window.  Consecutive block pairs of one workgroup shift the window by 64 rows, so
-// half of the next window is already staged: `keep_lo` (query side, j0 += 64: next rows
-// 64..127 = current rows 0..63) or !keep_lo (key side, i0 += 64: next rows 0..63 = current
-// rows 64..127).  Only the 64 new rows are loaded; each thread moves the old piece it owns and
-// then writes its new piece at the same place, so no other thread's piece is touched.
-TTMI_DEV void pf_win_half(u32x4 (&v)[2], const int16_t* sdel, const bf16_t* table, int64_t ld,
-                          int rel0, int S, int tid) {
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    const int rel = min(max(rel0 + r, -(S - 1)), S - 1);
-    v[c] = *reinterpret_cast<const u32x4*>(table + (int64_t)sdel[rel + S - 1] * ld + ch * 8);
-  }
-}
-template <bool NEW_LO>
-TTMI_DEV void put_win_slide(char* dst, const u32x4 (&v)[2], int tid) {
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    char* lo = dst + r * TP + ch * 16;
-    char* hi = lo + 64 * TP;
-    if (NEW_LO) {
-      *reinterpret_cast<u32x4*>(hi) = *reinterpret_cast<const u32x4*>(lo);
-      *reinterpret_cast<u32x4*>(lo) = v[c];
-    } else {
-      *reinterpret_cast<u32x4*>(lo) = *reinterpret_cast<const u32x4*>(hi);
-      *reinterpret_cast<u32x4*>(hi) = v[c];
-    }
   }
 }
 
@@ -313,9 +268,8 @@ struct QSide {
 static_assert(4 * 16 * WP <= WIN * TP, "private images must fit the PQexp window");
 static_assert(sizeof(QSide) <= 80 * 1024, "two workgroups per CU");
 
-// The next key block's staging, held in registers across a block pair: key rows, values,
-// the 64 new rows of the sliding PKexp and the whole PQexp (whose LDS holds the waves'
-// private images during a pair, so nothing of it carries over).
+// The next pair's key rows, values and key mask, held in registers across a block pair (its
+// windows are prefetched separately, with pf_win, later in the pair).
 struct QRows {
   u32x4 k[2], v[2];
   int64_t mk;             // mask of key j0 + tid (tid < 64)
@@ -326,18 +280,6 @@ TTMI_DEV void qrows_load(QRows& st, const DisArgs& a, int64_t rowb, int h, int j
   // unconditional load from a clamped index: a guarded load is a branch + vmcnt(0), which
   // would wait for the prefetch just issued
   st.mk = a.mask[rowb + min(j0 + (tid & 63), a.S - 1)];
-}
-TTMI_DEV void qwins_load(u32x4 (&pk)[2], u32x4 (&pq)[4], const QSide& L, const DisArgs& a, int h,
-                         int i0, int j0, int tid) {
-  pf_win_half(pk, L.sDel, a.posk + h * DH, a.ldpos, i0 - j0 - 63, a.S, tid);
-  pf_win(pq, L.sDel, a.posq + h * DH, a.ldpos, i0 - j0 - 63, a.S, tid);
-}
-// Key column j = j0 + tid: s = raw·mul + add.  Valid query rows: valid key {c, 0}, masked
-// key {0, finfo.min} (masked_fill), key past S {0, -inf}.  Padded query rows (the reference
-// masks their whole row): every in-range key {0, finfo.min}, past S {0, -inf}.
-TTMI_DEV void qwins_store(const u32x4 (&pk)[2], const u32x4 (&pq)[4], QSide& L, int tid) {
-  put_win_slide<true>(L.sPK, pk, tid);
-  put_win(L.sPQ, pq, tid);
 }
 TTMI_DEV void qrows_store(const QRows& st, QSide& L, int S, int j0, float c, int tid) {
   put_rows(L.sK, st.k, j0, S, tid);
@@ -696,17 +638,16 @@ struct KSide {
 static_assert(4 * 16 * WP <= WIN * TP, "private images must fit the PKexp window");
 static_assert(sizeof(KSide) <= 80 * 1024, "two workgroups per CU");
 
-// The next query block's staging, held in registers across a block pair: query rows, dO
-// rows and the per-row softmax data (loaded right after the staging barrier), then the whole
-// PKexp (its LDS holds the waves' private images during a pair), the 64 new rows of the
-// sliding PQexp and Uexp (loaded after the score phase, when fewer registers are live).
+// The next pair's staging, held in registers across a block pair: query rows, dO rows and
+// the per-row softmax data (loaded right after the staging barrier), then both windows and
+// Uexp (loaded after the score phase, when fewer registers are live).
 struct KRows {
   u32x4 q[2], o[2];
   float lse, d;           // query row i0 + tid (tid < 64)
   int64_t qm;
 };
 struct KWins {
-  u32x4 pk[4], pq[2];
+  u32x4 pk[4], pq[4];
   float4 u;               // Uexp row tid >> 1, columns 4·(tid & 1) ..
 };
 TTMI_DEV void krows_load(KRows& st, const DisArgs& a, int64_t rowb, int64_t bh, int h, int i0, int tid) {
@@ -725,7 +666,7 @@ TTMI_DEV void kwins_load(KWins& st, const KSide& L, const DisArgs& a, int h, int
                          int tid) {
   const int rel0 = i0 - j0 - 63;
   pf_win(st.pk, L.sDel, a.posk + h * DH, a.ldpos, rel0, a.S, tid);
-  pf_win_half(st.pq, L.sDel, a.posq + h * DH, a.ldpos, rel0 + 64, a.S, tid);
+  pf_win(st.pq, L.sDel, a.posq + h * DH, a.ldpos, rel0, a.S, tid);
   if (lora) load_u(st.u, L.sDel, a, rel0, tid);
 }
 TTMI_DEV void put_u(KSide& L, const float4& u, int tid) {
@@ -747,7 +688,7 @@ TTMI_DEV void krows_store(const KRows& st, KSide& L, int S, int i0, int tid) {
 }
 TTMI_DEV void kwins_store(const KWins& st, KSide& L, bool lora, int tid) {
   put_win(L.sPK, st.pk, tid);
-  put_win_slide<false>(L.sPQ, st.pq, tid);
+  put_win(L.sPQ, st.pq, tid);
   if (lora) put_u(L, st.u, tid);
 }
 TTMI_DEV void kside_prologue(KSide& L, const DisArgs& a, int64_t rowb, int64_t bh, int h, int j0,
@@ -772,28 +713,32 @@ TTMI_DEV void zero_pbx(const DisArgs& a, int64_t bh, int qb, int kb) {
     reinterpret_cast<float4*>(dst)[t] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// Key-side backward, one workgroup per (batch, head): key blocks outer, query blocks inner,
+// one software pipeline over every live pair (the next pair's Q / dO rows, row data and
+// windows prefetched into registers).  A new key block loads its K / V fragments and, with
+// LoRA, forms KB = K·Bq_h with two MFMAs (Bq_h fragments are built once per workgroup).
 template <bool EVEN>
 __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
   __shared__ __attribute__((aligned(16))) KSide L;
   __shared__ int s_end;
-  const Tile tl = tile_of(a);
-  const int kb = tl.blk, h = tl.h, b = tl.b;
+  const BH id = bh_of(a);
+  const int h = id.h, b = id.b;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lg = lane >> 4;
-  const int S = a.S, j0 = kb * 64, jl = 16 * w + li, j = j0 + jl;
+  const int S = a.S, jl = 16 * w + li;
   const int64_t rowb = (int64_t)b * S;
   const int64_t bh = (int64_t)b * a.nh + h;
   const DropKeys dk = resolve_drop(a.drop);
   const bool lora = a.u != nullptr;
-  const bool jrow = j < S;
   load_delta(L.sDel, a);
   const int send = seq_end(a, rowb, &s_end);
-  const int nlive = (send + 63) / 64;    // live query blocks: qb < nlive
-  if (lora)                              // padded query blocks: dS = 0 and dO = 0
-    for (int qb = nlive; qb < a.nqb; ++qb) zero_pbx(a, bh, qb, kb);
-  if (j0 >= send) {                      // padded key block: masked for every valid query
-    if (lora)
-      for (int qb = 0; qb < nlive; ++qb) zero_pbx(a, bh, qb, kb);
-    if (!jrow) return;
+  const int nlive = (send + 63) / 64;    // live blocks (query and key): < nlive
+  if (lora)                              // pairs with a padded block: dS = 0
+    for (int kb = 0; kb < a.nqb; ++kb)
+      for (int qb = 0; qb < a.nqb; ++qb)
+        if (qb >= nlive || kb >= nlive) zero_pbx(a, bh, qb, kb);
+  for (int kb = nlive; kb < a.nqb; ++kb) {   // padded key blocks: masked for every valid query
+    const int j = kb * 64 + jl;
+    if (j >= S) break;
     bf16_t* pk = a.dk + (rowb + j) * a.lddqkv + h * DH;
     bf16_t* pv = a.dv + (rowb + j) * a.lddqkv + h * DH;
     const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -804,48 +749,60 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
     }
     if (lora && lg < 2)
       *reinterpret_cast<float4*>(a.hu + ((rowb + j) * a.nh + h) * 8 + 4 * lg) = make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
   }
+  if (nlive == 0) return;
   const float c = a.inv_scale * LOG2E;
-  const bool kvalid = jrow && a.mask[rowb + j] != 0;
-  const float kbias = kvalid ? 0.f : -INFINITY;   // masked key / past S: p = 0
   const float l2s = __log2f(a.inv_scale);
-  const uint4 kf[2] = {fglob(a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 0, lane),
-                       fglob(a.k + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 1, lane)};
-  const uint4 vf[2] = {fglob(a.v + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 0, lane),
-                       fglob(a.v + rowb * a.ldqkv + h * DH, a.ldqkv, j, S, 1, lane)};
-  if (lora) {                 // KB[jl][c] = K_j · Bq[h·64 + :, c] (bf16 image, columns 8-15 zero)
-    const int r = tid >> 2, c0 = (tid & 3) * 2;
-    const bf16_t* kr = a.k + (rowb + min(j0 + r, S - 1)) * a.ldqkv + h * DH;
-    float s0 = 0.f, s1 = 0.f;
-    for (int d = 0; d < DH; d += 8) {
-      float kv[8];
-      unpack8(*reinterpret_cast<const uint4*>(kr + d), kv);
+  const bf16_t* kbase = a.k + rowb * a.ldqkv + h * DH;
+  const bf16_t* vbase = a.v + rowb * a.ldqkv + h * DH;
+  // Bq_h as the MFMA B operand (column = lane & 15 < 8, k = d in the fk permutation), bf16
+  uint4 bqf[2] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
+  if (lora && li < 8) {
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        s0 += kv[e] * a.bq[(h * DH + d + e) * 8 + c0];
-        s1 += kv[e] * a.bq[(h * DH + d + e) * 8 + c0 + 1];
+        const int d = cc * 32 + (e >> 2) * 16 + 4 * lg + (e & 3);
+        v[e] = a.bq[(h * DH + d) * 8 + li];
       }
+      bqf[cc] = make_uint4(pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7]));
     }
-    if (j0 + r >= S) s0 = s1 = 0.f;
-    uint32_t* row = reinterpret_cast<uint32_t*>(L.sKB + r * UP);
-    row[c0 / 2] = pk2(s0, s1);
-    row[4 + c0 / 2] = 0u;
   }
-  kside_prologue(L, a, rowb, bh, h, j0, lora, tid);
+  kside_prologue(L, a, rowb, bh, h, 0, lora, tid);
   f32x4_t dka[4], dva[4], hua;
 #pragma unroll
   for (int u = 0; u < 4; ++u) dka[u] = dva[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   hua = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  uint4 kf[2], vf[2];
+  float kbias = 0.f;
   char* priv = L.sPK + 16 * w * WP;
   const bool odd_lane = li & 1;
-  for (int qb = 0; qb < nlive; ++qb) {
-    const int i0 = qb * 64;
+  int qb = 0, kb = 0;
+  const int npairs = nlive * nlive;
+  for (int p = 0; p < npairs; ++p) {
+    const int i0 = qb * 64, j0 = kb * 64, j = j0 + jl;
+    const bool last_q = qb + 1 == nlive;
+    const int qbn = last_q ? 0 : qb + 1, kbn = last_q ? kb + 1 : kb;
+    const bool more = p + 1 < npairs;
+    if (qb == 0) {                        // new key block: own key / value fragments, KB
+      kf[0] = fglob(kbase, a.ldqkv, j, S, 0, lane);
+      kf[1] = fglob(kbase, a.ldqkv, j, S, 1, lane);
+      vf[0] = fglob(vbase, a.ldqkv, j, S, 0, lane);
+      vf[1] = fglob(vbase, a.ldqkv, j, S, 1, lane);
+      kbias = (j < S && a.mask[rowb + min(j, S - 1)] != 0) ? 0.f : -INFINITY;   // masked key: p = 0
+      if (lora) {                         // KB[jl][c] = K_j · Bq[h·64 + :, c] (columns 8-15 zero)
+        f32x4_t kbv = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        Mma<bf16_t>::run(kbv, kf[0], bqf[0]);
+        Mma<bf16_t>::run(kbv, kf[1], bqf[1]);
+        bf16_t* dst = reinterpret_cast<bf16_t*>(L.sKB) + (16 * w + 4 * lg) * (UP / 2) + li;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dst[e * (UP / 2)] = f2bf(kbv[e]);
+      }
+    }
     __syncthreads();                      // staging of pair (i0, j0) is in LDS
-    const bool more = qb + 1 < nlive;
     KRows nx;
-    KWins nw;
-    krows_load(nx, a, rowb, bh, h, i0 + 64, tid);      // clamped: valid on the last pair too
+    krows_load(nx, a, rowb, bh, h, qbn * 64, tid);     // clamped: valid on the last pair too
     // shared c2p: this wave's 16 queries against PKexp
     win_product(L.sPK, fk<TP>(L.sQ, 16 * w, 0, lane), fk<TP>(L.sQ, 16 * w, 1, lane),
                 L.sX + 16 * w * WP, lane);
@@ -876,10 +833,10 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
           const int il = 16 * t + 4 * lg + e, r = il - jl + 63;
           const float raw = sc[t][e] + lds_bf(L.sX, il * (WP / 2) + r) + lds_bf(priv, li * (WP / 2) + r);
           const float arg = fmaf(raw, c, ra_[e] + kbias);
-          const float p = __builtin_amdgcn_exp2f(arg);
+          const float pr = __builtin_amdgcn_exp2f(arg);
           // d raw score = p·(dP·keep - D)·inv_scale
           sc[t][e] = __builtin_amdgcn_exp2f(arg + l2s) * fmaf(dp[t][e], kp[e], -rd_[e]);
-          dp[t][e] = p * kp[e];
+          dp[t][e] = pr * kp[e];
         }
       }
       pdf[0] = freg(dp[0], dp[1]);
@@ -895,7 +852,8 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
         Mma<bf16_t>::run(dva[u], ft<TP>(L.sdO, 16 * u, cc, lane), pdf[cc]);
         Mma<bf16_t>::run(dka[u], ft<TP>(L.sQ, 16 * u, cc, lane), dsf[cc]);
       }
-    kwins_load(nw, L, a, h, i0 + 64, j0, lora, tid);   // clamped: valid on the last pair too
+    KWins nw;
+    kwins_load(nw, L, a, h, qbn * 64, kbn * 64, lora, tid);   // clamped: valid on the last pair
     __syncthreads();                      // every wave is done reading the shared c2p image
     // SkewK[jl][r] = dS[jl + r - 63][jl] (own rows of sX)
     char* skew = L.sX + 16 * w * WP;
@@ -934,22 +892,30 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
         }
       }
     }
+    if (last_q) {                         // key block done: write dK, dV, HU
+      if (j < S) {
+        bf16_t* pk = a.dk + (rowb + j) * a.lddqkv + h * DH;
+        bf16_t* pv = a.dv + (rowb + j) * a.lddqkv + h * DH;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          st_bf4(reinterpret_cast<char*>(pk + 16 * u + 4 * lg), dka[u]);
+          st_bf4(reinterpret_cast<char*>(pv + 16 * u + 4 * lg), dva[u]);
+        }
+        if (lora && lg < 2)
+          *reinterpret_cast<float4*>(a.hu + ((rowb + j) * a.nh + h) * 8 + 4 * lg) = make_float4(hua[0], hua[1], hua[2], hua[3]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dka[u] = dva[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      hua = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
     __syncthreads();
     if (more) {
-      krows_store(nx, L, S, i0 + 64, tid);
+      krows_store(nx, L, S, qbn * 64, tid);
       kwins_store(nw, L, lora, tid);
     }
+    qb = qbn;
+    kb = kbn;
   }
-  if (!jrow) return;
-  bf16_t* pk = a.dk + (rowb + j) * a.lddqkv + h * DH;
-  bf16_t* pv = a.dv + (rowb + j) * a.lddqkv + h * DH;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    st_bf4(reinterpret_cast<char*>(pk + 16 * u + 4 * lg), dka[u]);
-    st_bf4(reinterpret_cast<char*>(pv + 16 * u + 4 * lg), dva[u]);
-  }
-  if (lora && lg < 2)
-    *reinterpret_cast<float4*>(a.hu + ((rowb + j) * a.nh + h) * 8 + 4 * lg) = make_float4(hua[0], hua[1], hua[2], hua[3]);
 }
 
 // PB[δ][c] = Σ_{b,h} Σ_pairs Σ_{r: δ(i0 - j0 - 63 + r) = δ} PBexp[b,h][pair][r][c]: each thread
@@ -1063,12 +1029,12 @@ extern "C" int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
   TTMI_REQUIRE(!d->lora_u || (d->lora_bq && d->lora_hu && d->lora_pb && d->lora_pbx),
                "ttmi_dis_attn_bwd: LoRA outputs need u, bq, hu, pb and the pbx workspace together");
   const DisArgs a = dis_args(d);
-  const dim3 grid((unsigned)(a.nqb * d->nh * d->B)), grid_bh((unsigned)(d->nh * d->B));
+  const dim3 grid((unsigned)(d->nh * d->B));
   if (d->S % 2 == 0) {
-    hipLaunchKernelGGL(dis_dq_kernel<true>, grid_bh, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(dis_dq_kernel<true>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(dis_dkv_kernel<true>, grid, dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(dis_dq_kernel<false>, grid_bh, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(dis_dq_kernel<false>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(dis_dkv_kernel<false>, grid, dim3(256), 0, s, a);
   }
   if (d->lora_u) {
