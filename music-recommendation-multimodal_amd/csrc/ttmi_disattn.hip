@@ -81,10 +81,14 @@ TTMI_DEV uint32_t pk2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)
 TTMI_DEV uint4 freg(const f32x4_t& lo, const f32x4_t& hi) {
   return make_uint4(pk2(lo[0], lo[1]), pk2(lo[2], lo[3]), pk2(hi[0], hi[1]), pk2(hi[2], hi[3]));
 }
+// Element offset of row r (< 2^9: a row of one sequence or of the relative table) at leading
+// dimension ld (< 2^23, checked by the launcher): one full-rate 24-bit multiply instead of the
+// 64-bit multiply-add sequence.
+TTMI_DEV uint32_t rowoff(int r, int64_t ld) { return __umul24((uint32_t)r, (uint32_t)ld); }
 // Fragment of 16 rows of a global bf16 [rows][ld] matrix, k chunk c (same permutation as fk).
 TTMI_DEV uint4 fglob(const bf16_t* base, int64_t ld, int row, int nrows, int c, int lane) {
   const int rr = min(row, nrows - 1);
-  const char* p = reinterpret_cast<const char*>(base + (int64_t)rr * ld) + c * 64 + (lane >> 4) * 8;
+  const char* p = reinterpret_cast<const char*>(base + rowoff(rr, ld)) + c * 64 + (lane >> 4) * 8;
   const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 32);
   return row < nrows ? make_uint4(lo.x, lo.y, hi.x, hi.y) : make_uint4(0u, 0u, 0u, 0u);
 }
@@ -158,7 +162,7 @@ TTMI_DEV void pf_rows(u32x4 (&v)[2], const bf16_t* src, int64_t ld, int r0, int 
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
-    v[c] = *reinterpret_cast<const u32x4*>(src + (int64_t)min(r0 + r, nrows - 1) * ld + ch * 8);
+    v[c] = *reinterpret_cast<const u32x4*>(src + rowoff(min(r0 + r, nrows - 1), ld) + ch * 8);
   }
 }
 // ... written to an LDS image (pitch TP), rows >= nrows zero.
@@ -176,7 +180,7 @@ TTMI_DEV void pf_win(u32x4 (&v)[4], const int16_t* sdel, const bf16_t* table, in
   for (int c = 0; c < 4; ++c) {
     const int idx = tid + 256 * c, r = idx >> 3, ch = idx & 7;
     const int rel = min(max(rel0 + r, -(S - 1)), S - 1);
-    v[c] = *reinterpret_cast<const u32x4*>(table + (int64_t)sdel[rel + S - 1] * ld + ch * 8);
+    v[c] = *reinterpret_cast<const u32x4*>(table + rowoff(sdel[rel + S - 1], ld) + ch * 8);
   }
 }
 TTMI_DEV void put_win(char* dst, const u32x4 (&v)[4], int tid) {
@@ -491,22 +495,30 @@ __global__ __launch_bounds__(256, 2) void dis_dq_kernel(DisArgs a) {
   const DropKeys dk = resolve_drop(a.drop);
   const float l2s = __log2f(a.inv_scale);
   load_delta(L.sDel, a);
-  for (int r = tid; r < S; r += 256) {   // D and lse of every row of this head
-    const bf16_t* o = a.ctx + (rowb + r) * a.ldctx + h * DH;
-    const bf16_t* go = a.dctx + (rowb + r) * a.lddctx + h * DH;
+  // D and lse of every row of this head: four lanes per row (16 columns each, coalesced
+  // 128-byte rows), reduced with two lane swaps
+  for (int r0 = 0; r0 < S; r0 += 64) {
+    const int r = r0 + (tid >> 2), q = tid & 3, rc = min(r, S - 1);
+    const bf16_t* o = a.ctx + (rowb + rc) * a.ldctx + h * DH + 16 * q;
+    const bf16_t* go = a.dctx + (rowb + rc) * a.lddctx + h * DH + 16 * q;
     float acc = 0.f;
 #pragma unroll
-    for (int cc = 0; cc < 8; ++cc) {
+    for (int cc = 0; cc < 2; ++cc) {
       float x[8], y[8];
       unpack8(*reinterpret_cast<const uint4*>(o + 8 * cc), x);
       unpack8(*reinterpret_cast<const uint4*>(go + 8 * cc), y);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
     }
-    const bool qv = a.mask[rowb + r] != 0;
-    a.dsum[bh * S + r] = acc;
-    R.d[r] = acc;
-    R.lse_s[r] = qv ? a.lse[bh * S + r] - l2s : INFINITY;
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    const bool qv = a.mask[rowb + rc] != 0;
+    const float lse = a.lse[bh * S + rc];
+    if (q == 0 && r < S) {
+      a.dsum[bh * S + r] = acc;
+      R.d[r] = acc;
+      R.lse_s[r] = qv ? lse - l2s : INFINITY;
+    }
   }
   const int send = seq_end(a, rowb, &s_end);
   const int nlive = (send + 63) / 64;
@@ -946,6 +958,8 @@ static int dis_check(const ttmi_dis_attn_desc* d) {
                "ttmi_dis_attn: null argument");
   TTMI_REQUIRE(d->ldqkv % 8 == 0 && d->ldpos % 8 == 0 && d->ldctx % 8 == 0,
                "ttmi_dis_attn: leading dimensions must be multiples of 8");
+  TTMI_REQUIRE(d->ldqkv < (1 << 23) && d->ldpos < (1 << 23) && d->ldctx < (1 << 23) &&
+               d->lddctx < (1 << 23), "ttmi_dis_attn: leading dimensions must be < 2^23");
   TTMI_REQUIRE(d->drop_p == 0.f || d->drop_seed, "ttmi_dis_attn: dropout needs a seed");
   TTMI_REQUIRE((int64_t)d->B * d->nh * d->S * d->S < (1ll << 32), "ttmi_dis_attn: dropout index overflow");
   return TTMI_OK;
