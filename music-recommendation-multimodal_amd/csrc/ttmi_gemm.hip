@@ -1358,6 +1358,74 @@ TTMI_DEV void big_epi8(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t
   }
 }
 
+// Epilogue operands of one 8-column item (bias, GELU gate, fp32 residual), loaded one item
+// ahead of its use: the loads of item k+1 issue before item k's math and stores, so their
+// latency hides behind them (a load right before its use waited vmcnt(0) 16 times per tile).
+// Addresses are clamped into the matrix; items off its edge fall back to big_epi8.
+struct EpiIn {
+  float4 b0, b1, r0, r1;
+  uint4 gate;
+};
+template <int EPI>
+TTMI_DEV void big_epi_load(const GemmArgs& g, int64_t m, int64_t n, EpiIn& in) {
+  const int64_t mc = min<int64_t>(m, g.M - 1), nc = min<int64_t>(n, g.N - 8);
+  if (EPI & BE_BIAS) {
+    in.b0 = *reinterpret_cast<const float4*>(g.bias + nc);
+    in.b1 = *reinterpret_cast<const float4*>(g.bias + nc + 4);
+  }
+  if (EPI & (BE_GELU_GRAD | BE_RELU_GATE))
+    in.gate = *reinterpret_cast<const uint4*>((const bf16_t*)g.gate + mc * g.ld_gate + nc);
+  if (EPI & BE_RES) {
+    const float* rp = g.residual + mc * g.ld_res + nc;
+    in.r0 = *reinterpret_cast<const float4*>(rp);
+    in.r1 = *reinterpret_cast<const float4*>(rp + 4);
+  }
+}
+// big_epi8 for a full item (n + 7 < N) with its operands already in registers.
+template <int EPI>
+TTMI_DEV void big_epi8_pre(const GemmArgs& g, const DropKeys& dk, int64_t m, int64_t n, float* v,
+                           const EpiIn& in) {
+  if (EPI & BE_BIAS) {
+    v[0] += in.b0.x; v[1] += in.b0.y; v[2] += in.b0.z; v[3] += in.b0.w;
+    v[4] += in.b1.x; v[5] += in.b1.y; v[6] += in.b1.z; v[7] += in.b1.w;
+  }
+  if (EPI & BE_PRE) *reinterpret_cast<uint4*>(g.pre_out + m * g.ldc + n) = pack8(v);
+  if (EPI & BE_RELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+  } else if (EPI & BE_GELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+  }
+  if (EPI & BE_DROP) drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + n), v);
+  if (EPI & (BE_GELU_GRAD | BE_RELU_GATE)) {
+    float gv[8];
+    unpack8(in.gate, gv);
+    if (EPI & BE_GELU_GRAD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad(gv[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
+    }
+  }
+  if (EPI & BE_RES) {
+    v[0] += in.r0.x; v[1] += in.r0.y; v[2] += in.r0.z; v[3] += in.r0.w;
+    v[4] += in.r1.x; v[5] += in.r1.y; v[6] += in.r1.z; v[7] += in.r1.w;
+  }
+  const int64_t o = m * g.ldc + n;
+  if (EPI & BE_ACC) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(reinterpret_cast<float*>(g.C) + o + e, v[e]);
+  } else if (EPI & BE_F32) {
+    float* cp = reinterpret_cast<float*>(g.C) + o;
+    *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + o) = pack8(v);
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_big_kernel(BigArgs ba) {
   using namespace big;
@@ -1490,21 +1558,47 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigArgs ba) {
   // epilogue: lane holds rows 16i + (lane&15), columns 32p + 8(lane>>4) .. +7
   const DropKeys dk = resolve_drop(g.drop);
   const int li = lane & 15, lg = lane >> 4;
+  if constexpr (EPI >= 0 && (EPI & (BE_BIAS | BE_GELU_GRAD | BE_RELU_GATE | BE_RES))) {
+    // 16 items (i, p), operands one item ahead
+    EpiIn cur, nxt;
+    big_epi_load<EPI>(g, m0 + wr * 128 + li, n0 + wc * 64 + 8 * lg, cur);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int64_t m = m0 + wr * 128 + 16 * i + li;
-    if (m >= g.M) continue;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
+    for (int it = 0; it < 16; ++it) {
+      const int i = it >> 1, p = it & 1;
+      if (it + 1 < 16)
+        big_epi_load<EPI>(g, m0 + wr * 128 + 16 * ((it + 1) >> 1) + li,
+                          n0 + wc * 64 + 32 * ((it + 1) & 1) + 8 * lg, nxt);
+      const int64_t m = m0 + wr * 128 + 16 * i + li;
       const int64_t n = n0 + wc * 64 + 32 * p + 8 * lg;
-      if (n >= g.N) continue;
-      float v[8];
+      if (m < g.M && n < g.N) {
+        float v[8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = g.alpha * acc[i][2 * p][e];
-        v[4 + e] = g.alpha * acc[i][2 * p + 1][e];
+        for (int e = 0; e < 4; ++e) {
+          v[e] = g.alpha * acc[i][2 * p][e];
+          v[4 + e] = g.alpha * acc[i][2 * p + 1][e];
+        }
+        if (n + 7 < g.N) big_epi8_pre<EPI>(g, dk, m, n, v, cur);
+        else big_epi8<EPI>(g, dk, m, n, v);
       }
-      big_epi8<EPI>(g, dk, m, n, v);
+      cur = nxt;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t m = m0 + wr * 128 + 16 * i + li;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int64_t n = n0 + wc * 64 + 32 * p + 8 * lg;
+        if (n >= g.N) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = g.alpha * acc[i][2 * p][e];
+          v[4 + e] = g.alpha * acc[i][2 * p + 1][e];
+        }
+        big_epi8<EPI>(g, dk, m, n, v);
+      }
     }
   }
 }
