@@ -264,11 +264,11 @@ def probe_text_gemm(step, batch, device, iters: int = 3):
     sec = e0.elapsed_time(e1) / 1e3 / (iters * n)
     fl = sum(2.0 * M * N * K for (_, _, _, M, N, K, _) in calls) / n
     tf = fl / sec / 1e12
-    return {"kernel": "gemm_kernel (text-encoder token GEMMs: QKV+LoRA, out-proj, FFN, and their "
-                      "input-gradient GEMMs; per-step launch mix)",
+    return {"kernel": "gemm_big_kernel (256x256 LDS-DMA tiles: the text-encoder token GEMMs, QKV+LoRA, "
+                      "out-proj, FFN, and their input-gradient GEMMs; per-step launch mix)",
             "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4),
-            "traffic": read_traffic("gemm_kernel"), "avg_us": round(sec * 1e6, 2),
+            "traffic": read_traffic("gemm_big_kernel"), "avg_us": round(sec * 1e6, 2),
             "launches_per_step": len(calls), "flops_per_launch": round(fl)}
 
 
