@@ -546,6 +546,31 @@ int64_t ttmi_dis_attn_pbx_floats(int B, int S, int nh);
  * with mask != 0, rounded up to 64) in descending order.  One launch per batch mask; every
  * layer's ttmi_dis_attn_fwd/bwd of that batch reuses it. */
 int ttmi_dis_attn_order(const int64_t* mask, int B, int S, int32_t* order, hipStream_t stream);
+
+/* User tower head, one launch (ABI 12; reference user_tower.py:37-57, :131-144) on the B
+ * gathered last-valid rows of the pruned last encoder layer (bf16 operands, fp32 math):
+ *   x1 = res + drop1(ctx·Woᵀ + bo); a2 = LN2(x1) (m2, r2); h = dropf(relu(a2·W1ᵀ + b1));
+ *   x2 = x1 + drop2(h·W2ᵀ + b2); comb = [x2, G[gender], C[country]] (rows[b] = b);
+ *   z = comb·Wf0ᵀ + bf0; az = relu(LN(z)) (mz, rz); u = az·Wf3ᵀ + bf3.
+ * Weights are k-major bf16 [out, in] (Wo, W1, W2, Wf3 with ld = in; Wf0 [D, D + dg + dc]);
+ * dropout indices drop_rows[b]·N + n with N the Linear's output width (the unfused
+ * ttmi_gemm's ld_drop).  D == 128, F % 256 == 0 and F <= 512, dg == 16, dc == 32. */
+typedef struct ttmi_user_head_desc {
+  int B, D, F, dg, dc;
+  float eps;
+  const void* ctx; const float* res; const int32_t* drop_rows;
+  const void* wo; const float* bo; const float* n2w; const float* n2b;
+  const void* w1; const float* b1; const void* w2; const float* b2;
+  const int64_t* gender; const float* G; const int64_t* country; const float* C;
+  const void* wf0; const float* bf0; const float* lnw; const float* lnb;
+  const void* wf3; const float* bf3;
+  float d1_p; const uint64_t* d1_seed;
+  float dff_p; const uint64_t* dff_seed;
+  float d2_p; const uint64_t* d2_seed;
+  float* x1; void* a2; float* m2; float* r2; void* h; void* comb; int32_t* rows;
+  float* z; void* az; float* mz; float* rz; float* u;
+} ttmi_user_head_desc;
+int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t stream);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
 int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
 /* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);

@@ -1,0 +1,378 @@
+// ttmi_head.hip — the user tower's head in one launch (reference user_tower.py:37-57 and
+// :131-144): on the gathered last-valid rows of the pruned last encoder layer,
+//   x1 = res + drop1(ctx·Woᵀ + bo);  a2 = LN2(x1);  h = dropf(relu(a2·W1ᵀ + b1));
+//   x2 = x1 + drop2(h·W2ᵀ + b2);  comb = [x2, G[gender], C[country]];
+//   z = comb·Wf0ᵀ + bf0;  az = relu(LN(z));  u = az·Wf3ᵀ + bf3.
+// These eight steps were eight launches of a few microseconds of work each on B = 512 rows;
+// in a captured step each launch costs ~4.8 us however small it is.  Here a workgroup takes
+// 16 rows through the whole chain with its activations in LDS (the row-local chain has no
+// cross-row dependency): four waves split each Linear's output columns, A fragments come from
+// LDS, weight fragments straight from L2, LayerNorm reduces across the waves through LDS.
+// Every value the backward reads is written out as the unfused ops did (x1, a2, m2, r2, h,
+// comb, rows, z, az, mz, rz) and the dropout masks are the same hash at the same indices
+// (drop_rows[m]·N + n).
+#include "ttmi_common.h"
+
+namespace {
+
+constexpr int HR = 16;                 // rows per workgroup (one MFMA row tile)
+constexpr int HD = 128;                // d_model
+constexpr int FMAX = 512;              // FFN width
+constexpr int WPAD = 192;              // concat width D + 16 + 32 = 176, padded to 32
+constexpr int PD = (HD + 8) * 2;       // LDS pitches (bytes) of the bf16 row images
+constexpr int PF = (FMAX + 8) * 2;
+constexpr int PW = (WPAD + 8) * 2;
+
+struct HeadArgs {
+  int B, F, dg, dc;
+  float eps;
+  const bf16_t* ctx; const float* res; const int32_t* drows;
+  const bf16_t* wo; const float* bo; const float* n2w; const float* n2b;
+  const bf16_t* w1; const float* b1; const bf16_t* w2; const float* b2;
+  const int64_t* gender; const float* G; const int64_t* country; const float* C;
+  const bf16_t* wf0; const float* bf0; const float* lnw; const float* lnb;
+  const bf16_t* wf3; const float* bf3;
+  DropParams d1, dff, d2;
+  float* x1; bf16_t* a2; float* m2; float* r2; bf16_t* h; bf16_t* comb; int32_t* rows;
+  float* z; bf16_t* az; float* mz; float* rz; float* u;
+};
+
+struct HeadLds {
+  char sA[HR * PD];        // ctx, then a2, then az
+  char sH[HR * PF];        // h
+  char sC[HR * PW];        // comb (zero-padded to WPAD)
+  float sX1[HR][HD + 4];   // x1 (fp32 residual of the FFN)
+  float red[4][HR];        // LayerNorm cross-wave partials
+};
+
+// MFMA k order.  Both operands of every product here use the same k permutation, so the sum
+// is the same: lane group g holds the 8 CONTIGUOUS k = 8g .. 8g+7 of a 32-wide chunk (one
+// 16-byte access per fragment, and each weight row segment is fetched once, by one lane).
+// A fragment (rows li, k chunk c) of an LDS row image.
+template <int P>
+TTMI_DEV uint4 afrag(const char* s, int c, int lane) {
+  return *reinterpret_cast<const uint4*>(s + (lane & 15) * P + c * 64 + (lane >> 4) * 16);
+}
+// Weight fragment: output column n (a row of the [N, K] k-major weight), k chunk c; k past
+// Kreal (Kreal % 8 == 0) reads as zero.  The load is unconditional from a clamped address (a
+// guarded load is a branch + vmcnt(0), which would serialise the stage's loads).
+TTMI_DEV uint4 wfrag(const bf16_t* W, int64_t ldw, int n, int c, int lane, int Kreal) {
+  const int k0 = c * 32 + (lane >> 4) * 8;
+  const uint4 q = *reinterpret_cast<const uint4*>(W + (int64_t)n * ldw + min(k0, Kreal - 8));
+  return k0 < Kreal ? q : make_uint4(0u, 0u, 0u, 0u);
+}
+// Weight fragments of one Linear stage for this wave (NT column tiles x K/32 chunks), all
+// loads issued at once: each stage is one L2 round trip, not K/32 of them.
+template <int NT, int K>
+struct WFrags {
+  uint4 f[K / 32][NT];
+  TTMI_DEV void load(const bf16_t* W, int64_t ldw, int n0, int lane, int Kreal) {
+#pragma unroll
+    for (int c = 0; c < K / 32; ++c)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) f[c][t] = wfrag(W, ldw, n0 + 16 * t + (lane & 15), c, lane, Kreal);
+  }
+};
+// acc[t] (lane: row li, columns n0 + 16t + 4g .. +3) = A[16 x K] · W[n0 + 16t .., :]ᵀ
+template <int NT, int K, int P>
+TTMI_DEV void head_gemm(const char* sA, const WFrags<NT, K>& wf, f32x4_t (&acc)[NT], int lane) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < K / 32; ++c) {
+    const uint4 a = afrag<P>(sA, c, lane);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) Mma<bf16_t>::run(acc[t], wf.f[c][t], a);
+  }
+}
+
+TTMI_DEV void st4_bf(char* p, const float* v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                            (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+}
+
+// Row sum over the 128 columns held as v[t][e] by the 4 lanes of row li in each of 4 waves.
+TTMI_DEV float row_sum(float s, HeadLds& L, int w, int lane) {
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  if (lane < 16) L.red[w][lane] = s;
+  __syncthreads();
+  const int li = lane & 15;
+  const float tot = L.red[0][li] + L.red[1][li] + L.red[2][li] + L.red[3][li];
+  __syncthreads();
+  return tot;
+}
+// LayerNorm of the row values v (2 tiles x 4 per lane); returns mean / rstd.
+TTMI_DEV void row_ln(f32x4_t (&v)[2], const float* w_, const float* b_, float eps, bool relu,
+                     int n0, HeadLds& L, int w, int lane, float& mu, float& rs) {
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[t][e];
+  mu = row_sum(s, L, w, lane) * (1.f / HD);
+  float q = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[t][e] - mu;
+      q += d * d;
+    }
+  rs = 1.f / sqrtf(row_sum(q, L, w, lane) * (1.f / HD) + eps);
+  const int g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + 16 * t + 4 * g + e;
+      float o = (v[t][e] - mu) * rs * w_[n] + b_[n];
+      v[t][e] = relu ? fmaxf(o, 0.f) : o;
+    }
+}
+
+// Per-column parameters staged in LDS once (bias / LayerNorm vectors: the epilogues read
+// them without a global round trip).
+struct HeadParams {
+  float bo[HD], n2w[HD], n2b[HD], b1[FMAX], b2[HD], bf0[HD], lnw[HD], lnb[HD], bf3[HD];
+};
+// Every thread loads (clamped index: no branch, so no vmcnt(0) that would serialise the
+// staging loads) and stores; duplicate stores write the same value.
+template <int N>
+TTMI_DEV float4 vec_ld(const float* src, int tid) {
+  return reinterpret_cast<const float4*>(src)[tid & (N / 4 - 1)];
+}
+template <int N>
+TTMI_DEV void vec_st(float* dst, const float4& v, int tid) {
+  reinterpret_cast<float4*>(dst)[tid & (N / 4 - 1)] = v;
+}
+
+#ifdef HEAD_STAMP
+#define STAMP(i) do { if (threadIdx.x == 0) stamp[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
+
+// Each stage's weight fragments are loaded one stage ahead.  (Loading every stage's weights
+// at the start, with the whole register file, measured slower: the ~360 KB of weights a
+// workgroup streams take ~25k cycles through one CU's vector memory path whatever the order,
+// and vmcnt retires in order, so the first stage then waited for all of them.)
+template <int F>
+__global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
+#ifdef HEAD_STAMP
+  uint64_t stamp[8];
+#endif
+  STAMP(0);
+  __shared__ __attribute__((aligned(16))) HeadLds L;
+  __shared__ __attribute__((aligned(16))) HeadParams Q;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * HR, m = r0 + li;
+  const bool mrow = m < a.B;
+  const int W = HD + a.dg + a.dc;
+  const int n0 = w * 32;                             // this wave's 32 of the 128 columns
+  const int nf0 = w * (F / 4);                       // ... and its F / 4 FFN columns
+  // every stage's weights are loaded one stage ahead (first: now, beside the staging below)
+  // Prologue: the first stage's weights first (the longest wait), then the row staging
+  WFrags<2, HD> wo;
+  wo.load(a.wo, HD, n0, lane, HD);
+  {                                                  // ctx: 16 rows x 16 chunks of 16 bytes
+    const int r = tid >> 4, ch = tid & 15;
+    *reinterpret_cast<uint4*>(L.sA + r * PD + ch * 16) =
+        *reinterpret_cast<const uint4*>(a.ctx + (int64_t)min(r0 + r, a.B - 1) * HD + ch * 8);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {                     // residual: 16 rows x 32 float4
+      const int idx = tid + 256 * q;
+      *reinterpret_cast<float4*>(&L.sX1[idx >> 5][(idx & 31) * 4]) =
+          *reinterpret_cast<const float4*>(a.res + (int64_t)min(r0 + (idx >> 5), a.B - 1) * HD + (idx & 31) * 4);
+    }
+  }
+  {
+    const float4 p0 = vec_ld<HD>(a.bo, tid), p1 = vec_ld<HD>(a.n2w, tid), p2 = vec_ld<HD>(a.n2b, tid);
+    const float4 p3 = vec_ld<F>(a.b1, tid), p4 = vec_ld<HD>(a.b2, tid), p5 = vec_ld<HD>(a.bf0, tid);
+    const float4 p6 = vec_ld<HD>(a.lnw, tid), p7 = vec_ld<HD>(a.lnb, tid), p8 = vec_ld<HD>(a.bf3, tid);
+    vec_st<HD>(Q.bo, p0, tid); vec_st<HD>(Q.n2w, p1, tid); vec_st<HD>(Q.n2b, p2, tid);
+    vec_st<F>(Q.b1, p3, tid); vec_st<HD>(Q.b2, p4, tid); vec_st<HD>(Q.bf0, p5, tid);
+    vec_st<HD>(Q.lnw, p6, tid); vec_st<HD>(Q.lnb, p7, tid); vec_st<HD>(Q.bf3, p8, tid);
+  }
+  {   // demographics: a thread owns 4 of a row's 64 trailing columns (one index load, then
+      // both tables read at clamped addresses and the value selected: no conditional load)
+    const int r = tid >> 4, k0 = HD + 4 * (tid & 15), rr = min(r0 + r, a.B - 1);
+    const int64_t gi = a.gender[rr], ci = a.country[rr];
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kk = k0 + e;
+      float gv = a.G[gi * a.dg + min(kk - HD, a.dg - 1)];
+      float cv = a.C[ci * a.dc + min(max(kk - HD - a.dg, 0), a.dc - 1)];
+      asm volatile("" : "+v"(gv), "+v"(cv));
+      v[e] = kk < HD + a.dg ? gv : (kk < W ? cv : 0.f);
+    }
+    st4_bf(L.sC + r * PW + k0 * 2, v);
+    if (k0 < W && r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.comb + (int64_t)(r0 + r) * W + k0), v);
+  }
+  if (tid < HR && r0 + tid < a.B) a.rows[r0 + tid] = r0 + tid;
+  const int drow = a.drows[min(m, a.B - 1)];
+  // the three sites' keys, read once (the launcher points an unused seed at valid memory)
+  const uint64_t s1 = *a.d1.seed, sf = *a.dff.seed, s2 = *a.d2.seed;
+  const DropKeys dk1{(uint32_t)s1, (uint32_t)(s1 >> 32), a.d1.thresh, a.d1.scale, a.d1.on};
+  const DropKeys dkf{(uint32_t)sf, (uint32_t)(sf >> 32), a.dff.thresh, a.dff.scale, a.dff.on};
+  const DropKeys dk2{(uint32_t)s2, (uint32_t)(s2 >> 32), a.d2.thresh, a.d2.scale, a.d2.on};
+  __syncthreads();
+  STAMP(1);
+  // ---- x1 = res + drop1(ctx·Woᵀ + bo); a2 = LN2(x1)
+  f32x4_t v[2];
+  head_gemm<2, HD, PD>(L.sA, wo, v, lane);
+  WFrags<4, HD> w1a;
+  w1a.load(a.w1, HD, nf0, lane, HD);
+  {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = v[t][e] + Q.bo[n + e];
+      drop_apply_vec<4>(dk1, (uint32_t)(drow * HD + n), x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] += L.sX1[li][n + e];
+        v[t][e] = x[e];
+      }
+      if (mrow) *reinterpret_cast<float4*>(a.x1 + (int64_t)m * HD + n) = make_float4(x[0], x[1], x[2], x[3]);
+    }
+    __syncthreads();                                 // every wave is done reading ctx and res
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) L.sX1[li][n0 + 16 * t + 4 * g + e] = v[t][e];
+    float mu, rs;
+    row_ln(v, Q.n2w, Q.n2b, a.eps, false, n0, L, w, lane, mu, rs);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+      st4_bf(L.sA + li * PD + n * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.a2 + (int64_t)m * HD + n), x);
+    }
+    if (mrow && lane < 16 && w == 0) { a.m2[m] = mu; a.r2[m] = rs; }
+  }
+  __syncthreads();
+  STAMP(2);
+  // ---- h = dropf(relu(a2·W1ᵀ + b1)), 64 columns of the wave's F / 4 at a time
+  WFrags<2, F> w2;
+  {
+    WFrags<4, HD> w1n;
+#pragma unroll
+    for (int nb = 0; nb < F / 4; nb += 64) {
+      f32x4_t hv[4];
+      head_gemm<4, HD, PD>(L.sA, nb == 0 ? w1a : w1n, hv, lane);
+      if (nb + 64 < F / 4) w1n.load(a.w1, HD, nf0 + nb + 64, lane, HD);
+      else w2.load(a.w2, F, n0, lane, F);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = nf0 + nb + 16 * t + 4 * g;
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = fmaxf(hv[t][e] + Q.b1[n + e], 0.f);
+        drop_apply_vec<4>(dkf, (uint32_t)(drow * F + n), x);
+        st4_bf(L.sH + li * PF + n * 2, x);
+        if (mrow) st4_bf(reinterpret_cast<char*>(a.h + (int64_t)m * F + n), x);
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(3);
+  // ---- x2 = x1 + drop2(h·W2ᵀ + b2) -> comb[:, :128]
+  head_gemm<2, F, PF>(L.sH, w2, v, lane);
+  WFrags<2, WPAD> wf0;
+  wf0.load(a.wf0, W, n0, lane, W);
+  {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = v[t][e] + Q.b2[n + e];
+      drop_apply_vec<4>(dk2, (uint32_t)(drow * HD + n), x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] += L.sX1[li][n + e];
+      st4_bf(L.sC + li * PW + n * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.comb + (int64_t)m * W + n), x);
+    }
+  }
+  __syncthreads();
+  STAMP(4);
+  // ---- z = comb·Wf0ᵀ + bf0; az = relu(LN(z))
+  head_gemm<2, WPAD, PW>(L.sC, wf0, v, lane);
+  WFrags<2, HD> wf3;
+  wf3.load(a.wf3, HD, n0, lane, HD);
+  {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[t][e] += Q.bf0[n + e];
+      if (mrow) *reinterpret_cast<float4*>(a.z + (int64_t)m * HD + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
+    }
+    float mu, rs;
+    row_ln(v, Q.lnw, Q.lnb, a.eps, true, n0, L, w, lane, mu, rs);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+      st4_bf(L.sA + li * PD + n * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.az + (int64_t)m * HD + n), x);
+    }
+    if (mrow && lane < 16 && w == 0) { a.mz[m] = mu; a.rz[m] = rs; }
+  }
+  __syncthreads();
+  STAMP(5);
+  // ---- u = az·Wf3ᵀ + bf3
+  head_gemm<2, HD, PD>(L.sA, wf3, v, lane);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    if (mrow)
+      *reinterpret_cast<float4*>(a.u + (int64_t)m * HD + n) =
+          make_float4(v[t][0] + Q.bf3[n], v[t][1] + Q.bf3[n + 1], v[t][2] + Q.bf3[n + 2], v[t][3] + Q.bf3[n + 3]);
+  }
+#ifdef HEAD_STAMP
+  __syncthreads();
+  STAMP(6);
+  if (threadIdx.x == 0 && blockIdx.x < 4)
+    for (int i = 1; i < 7; ++i) a.rz[blockIdx.x * 8 + i] = (float)(stamp[i] - stamp[0]);
+#endif
+}
+
+}  // namespace
+
+extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
+  TTMI_REQUIRE(d != nullptr, "ttmi_user_head_fwd: null descriptor");
+  TTMI_REQUIRE(d->B > 0 && d->D == HD, "ttmi_user_head_fwd: needs D == %d", HD);
+  TTMI_REQUIRE(d->F > 0 && d->F <= FMAX && d->F % 256 == 0, "ttmi_user_head_fwd: needs F %% 256 == 0, F <= %d", FMAX);
+  TTMI_REQUIRE(d->dg == 16 && d->dc == 32, "ttmi_user_head_fwd: demographic widths must be 16 and 32");
+  TTMI_REQUIRE(d->ctx && d->res && d->drop_rows && d->wo && d->bo && d->n2w && d->n2b && d->w1 && d->b1 && d->w2 &&
+               d->b2 && d->gender && d->G && d->country && d->C && d->wf0 && d->bf0 && d->lnw &&
+               d->lnb && d->wf3 && d->bf3 && d->x1 && d->a2 && d->m2 && d->r2 && d->h && d->comb &&
+               d->rows && d->z && d->az && d->mz && d->rz && d->u, "ttmi_user_head_fwd: null argument");
+  TTMI_REQUIRE((d->d1_p == 0.f || d->d1_seed) && (d->dff_p == 0.f || d->dff_seed) && (d->d2_p == 0.f || d->d2_seed),
+               "ttmi_user_head_fwd: dropout needs a seed");
+  HeadArgs a{};
+  a.B = d->B; a.F = d->F; a.dg = d->dg; a.dc = d->dc; a.eps = d->eps;
+  a.ctx = (const bf16_t*)d->ctx; a.res = d->res; a.drows = d->drop_rows;
+  a.wo = (const bf16_t*)d->wo; a.bo = d->bo; a.n2w = d->n2w; a.n2b = d->n2b;
+  a.w1 = (const bf16_t*)d->w1; a.b1 = d->b1; a.w2 = (const bf16_t*)d->w2; a.b2 = d->b2;
+  a.gender = d->gender; a.G = d->G; a.country = d->country; a.C = d->C;
+  a.wf0 = (const bf16_t*)d->wf0; a.bf0 = d->bf0; a.lnw = d->lnw; a.lnb = d->lnb;
+  a.wf3 = (const bf16_t*)d->wf3; a.bf3 = d->bf3;
+  const uint64_t* any = reinterpret_cast<const uint64_t*>(d->bo);   // read, never used when off
+  a.d1 = make_drop(d->d1_p, d->d1_seed ? d->d1_seed : any);
+  a.dff = make_drop(d->dff_p, d->dff_seed ? d->dff_seed : any);
+  a.d2 = make_drop(d->d2_p, d->d2_seed ? d->d2_seed : any);
+  a.x1 = d->x1; a.a2 = (bf16_t*)d->a2; a.m2 = d->m2; a.r2 = d->r2; a.h = (bf16_t*)d->h;
+  a.comb = (bf16_t*)d->comb; a.rows = d->rows; a.z = d->z; a.az = (bf16_t*)d->az;
+  a.mz = d->mz; a.rz = d->rz; a.u = d->u;
+  const dim3 grid((unsigned)((d->B + HR - 1) / HR));
+  if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_kernel<512>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(user_head_fwd_kernel<256>, grid, dim3(256), 0, s, a);
+  return ttmi_check_launch("ttmi_user_head_fwd");
+}

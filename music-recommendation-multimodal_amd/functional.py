@@ -215,6 +215,24 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             ctx = torch.empty(B, D, device=dev, dtype=dt)
             lse = torch.empty(B * H, **f32)
             ops.mha_q1_fwd(qkv, key_valid, rows, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
+            if ops.user_head_fusable(W, P, pre, D, dt):      # the rest of the tower: one launch
+                F_ = W[pre + "linear1.weight"].shape[0]
+                Wc = D + P["gender_embedding.weight"].shape[1] + P["country_embedding.weight"].shape[1]
+                o = dict(x1=torch.empty(B, D, **f32), a2=torch.empty(B, D, device=dev, dtype=dt),
+                         m2=torch.empty(B, **f32), r2=torch.empty(B, **f32),
+                         h=torch.empty(B, F_, device=dev, dtype=dt),
+                         comb=torch.empty(B, Wc, device=dev, dtype=dt),
+                         rows=torch.empty(B, device=dev, dtype=torch.int32),
+                         z=torch.empty(B, D, **f32), az=torch.empty(B, D, device=dev, dtype=dt),
+                         mz=torch.empty(B, **f32), rz=torch.empty(B, **f32), u=torch.empty(B, D, **f32))
+                ops.user_head_fwd(ctx, res_in, drows, W, P, pre, gender, country, cfg.eps,
+                                  (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_ffn(i)),
+                                   _drop(cfg, seeds, site_drop2(i))), o)
+                st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, o["x1"], o["a2"], o["m2"],
+                                            o["r2"], o["h"], rows))
+                st.comb, st.rows, st.z = o["comb"], o["rows"], o["z"]
+                st.mz, st.rz, st.az = o["mz"], o["rz"], o["az"]
+                return o["u"], st
         else:
             rows, R, res_in, drows = None, M, x, None
             ctx = torch.empty(M, D, device=dev, dtype=dt)

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -76,6 +76,23 @@ class DisAttnDesc(ctypes.Structure):
                 ("dq", c_p), ("dk", c_p), ("dv", c_p), ("lddqkv", ctypes.c_int64),
                 ("lora_u", c_p), ("lora_bq", c_p), ("lora_hu", c_p), ("lora_pb", c_p),
                 ("dq_scratch", c_p), ("lora_pbx", c_p), ("order", c_p)]
+
+
+class UserHeadDesc(ctypes.Structure):
+    """ttmi_user_head_desc (include/ttmi.h)."""
+    _fields_ = [("B", c_i), ("D", c_i), ("F", c_i), ("dg", c_i), ("dc", c_i),
+                ("eps", ctypes.c_float),
+                ("ctx", c_p), ("res", c_p), ("drop_rows", c_p),
+                ("wo", c_p), ("bo", c_p), ("n2w", c_p), ("n2b", c_p),
+                ("w1", c_p), ("b1", c_p), ("w2", c_p), ("b2", c_p),
+                ("gender", c_p), ("G", c_p), ("country", c_p), ("C", c_p),
+                ("wf0", c_p), ("bf0", c_p), ("lnw", c_p), ("lnb", c_p),
+                ("wf3", c_p), ("bf3", c_p),
+                ("d1_p", ctypes.c_float), ("d1_seed", c_p),
+                ("dff_p", ctypes.c_float), ("dff_seed", c_p),
+                ("d2_p", ctypes.c_float), ("d2_seed", c_p),
+                ("x1", c_p), ("a2", c_p), ("m2", c_p), ("r2", c_p), ("h", c_p), ("comb", c_p),
+                ("rows", c_p), ("z", c_p), ("az", c_p), ("mz", c_p), ("rz", c_p), ("u", c_p)]
 
 
 class LnBwdDesc(ctypes.Structure):
@@ -168,6 +185,7 @@ SIGNATURES = {
     "ttmi_dis_attn_bwd": (c_i, [c_p, c_p]),
     "ttmi_dis_attn_pbx_floats": (ctypes.c_int64, [c_i, c_i, c_i]),
     "ttmi_dis_attn_order": (c_i, [c_p, c_i, c_i, c_p, c_p]),
+    "ttmi_user_head_fwd": (c_i, [c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,

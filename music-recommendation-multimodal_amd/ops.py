@@ -13,7 +13,8 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from . import lib as _L
-from .lib import BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, WgradDesc, call
+from .lib import (BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, UserHeadDesc,
+                  WgradDesc, call)
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -770,6 +771,48 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
         pbx = torch.empty(int(_L.load().ttmi_dis_attn_pbx_floats(B, S, nh)), device=q.device)
         d.lora_pbx = _p(pbx)
     call("ttmi_dis_attn_bwd", ctypes.byref(d), _s())
+
+
+def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict[str, Tensor],
+                  P: Dict[str, Tensor], pre: str, gender: Tensor, country: Tensor, eps: float,
+                  drops: Tuple[Drop, Drop, Drop], out: Dict[str, Tensor]) -> None:
+    """The user tower head in one launch (ttmi_user_head_fwd): the pruned last layer's
+    out-proj + residual + norm2 + FFN on the gathered rows, the demographic concat and the
+    fusion MLP.  ``pre`` is the last layer's parameter prefix; ``out`` holds x1, a2, m2, r2, h,
+    comb, rows, z, az, mz, rz, u (allocated by the caller)."""
+    B, D = ctx.shape
+    d = UserHeadDesc()
+    d.B, d.D = B, D
+    d.F = W[pre + "linear1.weight"].shape[0]
+    d.dg, d.dc = P["gender_embedding.weight"].shape[1], P["country_embedding.weight"].shape[1]
+    d.eps = eps
+    d.ctx, d.res, d.drop_rows = _p(ctx), _p(res), _p(drop_rows)
+    d.wo, d.bo = _p(W[pre + "self_attn.out_proj.weight"]), _p(P[pre + "self_attn.out_proj.bias"])
+    d.n2w, d.n2b = _p(P[pre + "norm2.weight"]), _p(P[pre + "norm2.bias"])
+    d.w1, d.b1 = _p(W[pre + "linear1.weight"]), _p(P[pre + "linear1.bias"])
+    d.w2, d.b2 = _p(W[pre + "linear2.weight"]), _p(P[pre + "linear2.bias"])
+    d.gender, d.G = _p(gender), _p(P["gender_embedding.weight"])
+    d.country, d.C = _p(country), _p(P["country_embedding.weight"])
+    d.wf0, d.bf0 = _p(W["fusion_layer.0.weight"]), _p(P["fusion_layer.0.bias"])
+    d.lnw, d.lnb = _p(P["fusion_layer.1.weight"]), _p(P["fusion_layer.1.bias"])
+    d.wf3, d.bf3 = _p(W["fusion_layer.3.weight"]), _p(P["fusion_layer.3.bias"])
+    (d.d1_p, d1), (d.dff_p, dff), (d.d2_p, d2) = [(float(p), s) for p, s in drops]
+    d.d1_seed, d.dff_seed, d.d2_seed = _p(d1), _p(dff), _p(d2)
+    for k in ("x1", "a2", "m2", "r2", "h", "comb", "rows", "z", "az", "mz", "rz", "u"):
+        setattr(d, k, _p(out[k]))
+    call("ttmi_user_head_fwd", ctypes.byref(d), _s())
+
+
+def user_head_fusable(W: Dict[str, Tensor], P: Dict[str, Tensor], pre: str, D: int,
+                      dtype) -> bool:
+    """Shapes ttmi_user_head_fwd takes (include/ttmi.h)."""
+    F = W[pre + "linear1.weight"].shape[0]
+    return (dtype == torch.bfloat16 and D == 128 and F % 256 == 0 and F <= 512 and
+            P["gender_embedding.weight"].shape[1] == 16 and
+            P["country_embedding.weight"].shape[1] == 32 and
+            all(W[n].dtype == torch.bfloat16 for n in (
+                pre + "self_attn.out_proj.weight", pre + "linear1.weight", pre + "linear2.weight",
+                "fusion_layer.0.weight", "fusion_layer.3.weight")))
 
 
 def dis_attn_order(mask: Tensor, B: int, S: int) -> Tensor:

@@ -503,3 +503,76 @@ def test_trainstep_ragged_last_batch(gpu_pkg, use_graph):
             assert (got[k] - params[k]).abs().max().item() <= 1.01 * 1e-3 * 4, k
         else:
             assert rel(got[k], params[k]) < 2e-4, (k, rel(got[k], params[k]))
+
+
+@pytest.mark.parametrize("B,p", [(512, 0.1), (300, 0.0), (37, 0.1)])
+def test_user_head_fused_matches_ops(gpu_pkg, B, p):
+    """ttmi_user_head_fwd (the user tower head in one launch) against the unfused op sequence
+    it replaces (functional.user_tower_fwd's pruned-layer path): same dropout masks (same hash,
+    same drop_rows indices), fp32 values to 1e-4 of their scale, bf16 values to 1e-2."""
+    ops = gpu_pkg.ops
+    D, F, M = 128, 512, 7 * B
+    g = torch.Generator().manual_seed(B)
+
+    def bf(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+    def f32(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(DEV)
+    pre = "transformer_encoder.layers.1."
+    W = {pre + "self_attn.out_proj.weight": bf(D, D, scale=D ** -0.5),
+         pre + "linear1.weight": bf(F, D, scale=D ** -0.5),
+         pre + "linear2.weight": bf(D, F, scale=F ** -0.5),
+         "fusion_layer.0.weight": bf(D, D + 48, scale=(D + 48) ** -0.5),
+         "fusion_layer.3.weight": bf(D, D, scale=D ** -0.5)}
+    P = {pre + "self_attn.out_proj.bias": f32(D, scale=0.1), pre + "norm2.weight": 1 + f32(D, scale=0.1),
+         pre + "norm2.bias": f32(D, scale=0.1), pre + "linear1.bias": f32(F, scale=0.1),
+         pre + "linear2.bias": f32(D, scale=0.1), "gender_embedding.weight": f32(3, 16),
+         "country_embedding.weight": f32(11, 32), "fusion_layer.0.bias": f32(D, scale=0.1),
+         "fusion_layer.1.weight": 1 + f32(D, scale=0.1), "fusion_layer.1.bias": f32(D, scale=0.1),
+         "fusion_layer.3.bias": f32(D, scale=0.1)}
+    ctx, res = bf(B, D), f32(B, D)
+    drows = torch.randperm(M, generator=g)[:B].to(torch.int32).to(DEV)
+    gender = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    country = torch.randint(0, 11, (B,), generator=g).to(DEV)
+    seeds = torch.tensor([11, -22, 33], dtype=torch.int64, device=DEV)
+    drops = tuple((p, seeds[k:k + 1]) if p > 0 else ops.NO_DROP for k in range(3))
+    assert ops.user_head_fusable(W, P, pre, D, torch.bfloat16)
+    # unfused reference sequence
+    x1 = torch.empty(B, D, device=DEV)
+    ops.linear(ctx, W[pre + "self_attn.out_proj.weight"], P[pre + "self_attn.out_proj.bias"], x1,
+               drop=drops[0], residual=res, drop_rows=drows)
+    a2 = torch.empty(B, D, device=DEV, dtype=torch.bfloat16)
+    m2, r2 = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    ops.layernorm_fwd(x1, P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2, eps=1e-5)
+    h = torch.empty(B, F, device=DEV, dtype=torch.bfloat16)
+    ops.linear(a2, W[pre + "linear1.weight"], P[pre + "linear1.bias"], h, act=1, drop=drops[1],
+               drop_rows=drows)
+    x2 = torch.empty(B, D, device=DEV)
+    ops.linear(h, W[pre + "linear2.weight"], P[pre + "linear2.bias"], x2, drop=drops[2],
+               residual=x1, drop_rows=drows)
+    comb = torch.empty(B, D + 48, device=DEV, dtype=torch.bfloat16)
+    rows = torch.empty(B, device=DEV, dtype=torch.int32)
+    ops.user_concat_fwd(x2, None, gender, P["gender_embedding.weight"], country,
+                        P["country_embedding.weight"], comb, rows, B, 1)
+    z = torch.empty(B, D, device=DEV)
+    ops.linear(comb, W["fusion_layer.0.weight"], P["fusion_layer.0.bias"], z)
+    az = torch.empty(B, D, device=DEV, dtype=torch.bfloat16)
+    mz, rz = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    ops.layernorm_fwd(z, P["fusion_layer.1.weight"], P["fusion_layer.1.bias"], az, mz, rz,
+                      eps=1e-5, relu=True)
+    u = torch.empty(B, D, device=DEV)
+    ops.linear(az, W["fusion_layer.3.weight"], P["fusion_layer.3.bias"], u)
+    want = dict(x1=x1, a2=a2, m2=m2, r2=r2, h=h, comb=comb, rows=rows, z=z, az=az, mz=mz, rz=rz, u=u)
+    out = {k: torch.full_like(v, 7) for k, v in want.items()}
+    ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out["rows"], rows)
+    for k in ("x1", "m2", "r2", "z", "mz", "rz", "u"):
+        assert rel(out[k], want[k]) < 1e-4 if k in ("x1",) else rel(out[k], want[k]) < 2e-3, k
+    for k in ("a2", "h", "comb", "az"):
+        assert rel(out[k].float(), want[k].float()) < 1e-2, k
+        # masks: dropped (zero) positions agree except where the kept value rounds to zero
+        if p > 0 and k == "h":
+            zo, zw = out[k] == 0, want[k] == 0
+            assert (zo != zw).float().mean().item() < 1e-3
