@@ -571,6 +571,29 @@ typedef struct ttmi_user_head_desc {
   float* z; void* az; float* mz; float* rz; float* u;
 } ttmi_user_head_desc;
 int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t stream);
+/* Its backward, one launch (ABI 12), from du (bf16 [B, D]) and the forward's saved values:
+ *   daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0]); dcomb = dz·Wf0 (dG[gender] / dC[country] +=, atomics);
+ *   dy2 = drop2ᵀ(dcomb[:, :D]); dz1 = (dy2·W2) ⊙ [h > 0]·ffn_scale;
+ *   dx1 = LN2ᵀ(dz1·W1) + dcomb[:, :D]; dy1 = drop1ᵀ(dx1); dctx = dy1·Wo.
+ * The *t weights are the transposed k-major mirrors ([in, out]).  Outputs dz16, dy2, dz1, dy1
+ * (bf16: the weight-gradient GEMMs' dY operands), dx1 (fp32), dctx (bf16).  ws
+ * [ttmi_user_head_bwd_ws_floats(B)] receives per-16-row-block column sums of the four
+ * LayerNorm parameter gradients (dlnw, dlnb, dn2w, dn2b, [nblk][4][D]) to be folded. */
+typedef struct ttmi_user_head_bwd_desc {
+  int B, D, F, dg, dc;
+  float ffn_scale;
+  const void* du; const void* az; const float* z; const float* mz; const float* rz;
+  const void* h; const float* x1; const float* m2; const float* r2;
+  const int32_t* drop_rows; const int64_t* gender; const int64_t* country;
+  const void* wf3t; const void* wf0t; const void* w2t; const void* w1t; const void* wot;
+  const float* lnw; const float* n2w;
+  float d1_p; const uint64_t* d1_seed;
+  float d2_p; const uint64_t* d2_seed;
+  float* dG; float* dC;
+  void* dz16; void* dy2; void* dz1; float* dx1; void* dy1; void* dctx; float* ws;
+} ttmi_user_head_bwd_desc;
+int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t stream);
+int64_t ttmi_user_head_bwd_ws_floats(int B);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
 int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
 /* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);

@@ -343,6 +343,296 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
 #endif
 }
 
+// ------------------------------------------------------------------------------ backward
+// The head's backward, one launch (the unfused sequence: linear_dx of fusion_layer.3, the
+// ReLU-gated LayerNorm backward, linear_dx of fusion_layer.0, the concat backward, the
+// dropout-2 backward, the ReLU/dropout-gated linear2 input grad, linear1's input grad with
+// LN2's backward, the residual and the dropout-1 backward, and out_proj's input grad):
+//   daz = du·Wf3;  dz = LNᵀ(daz ⊙ [az > 0]);  dcomb = dz·Wf0;  dx2 = dcomb[:, :D] (dG, dC by
+//   atomics as before);  dy2 = drop2ᵀ(dx2);  dz1 = (dy2·W2) ⊙ [h > 0]·sf;
+//   dx1 = LN2ᵀ(dz1·W1) + dx2;  dy1 = drop1ᵀ(dx1);  dctx = dy1·Wo.
+// Weights are the transposed k-major mirrors.  The LayerNorm weight / bias gradients leave as
+// per-workgroup column sums (ws [nwg][4][D]: dlnw, dlnb, dn2w, dn2b), folded in workgroup order
+// with the step's weight gradients.
+struct HeadBwdArgs {
+  int B, F, dg, dc;
+  float sf;                                 // FFN dropout scale 1 / (1 - p)
+  const bf16_t* du; const bf16_t* az; const float* z; const float* mz; const float* rz;
+  const bf16_t* h; const float* x1; const float* m2; const float* r2;
+  const int32_t* drows; const int64_t* gender; const int64_t* country;
+  const bf16_t* wf3t; const bf16_t* wf0t; const bf16_t* w2t; const bf16_t* w1t; const bf16_t* wot;
+  const float* lnw; const float* n2w;
+  DropParams d1, d2;
+  float* dG; float* dC;
+  bf16_t* dz16; bf16_t* dy2; bf16_t* dz1; float* dx1; bf16_t* dy1; bf16_t* dctx; float* ws;
+};
+
+struct HeadBwdLds {
+  char sA[HR * PD];         // du, then dz, then dy2, then dy1
+  char sH[HR * PF];         // dz1
+  float sX[HR][HD + 4];     // dx2 (fp32 residual of dx1)
+  float sW[HR][HD + 4];     // LayerNorm weight-gradient terms dy·x̂ (column sums)
+  float sB[HR][HD + 4];     // ... and dy
+  float sDem[HR][48];       // dcomb's demographic columns (dG, dC rows), added at the end
+  int sGi[HR], sCi[HR];     // the rows' gender / country indices
+  float red[4][HR];
+};
+
+TTMI_DEV float bwd_row_sum(float s, HeadBwdLds& L, int w, int lane) {
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  if (lane < 16) L.red[w][lane] = s;
+  __syncthreads();
+  const int li = lane & 15;
+  const float tot = L.red[0][li] + L.red[1][li] + L.red[2][li] + L.red[3][li];
+  __syncthreads();
+  return tot;
+}
+// LayerNorm backward of the row values dy (2 tiles x 4 per lane, columns n0 + 16t + 4g + e);
+// xs / wv: the lane's LN-input values and LN weights, preloaded: dx = rs·(g − mean g − x̂·mean(g·x̂)), g = dy·w.
+// The weight / bias gradient terms are summed over the block's 16 rows through LDS and
+// written to ws (wsw / wsb rows).
+TTMI_DEV void ln_bwd16(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, float rs, const float (&wv)[2][4],
+                       int n0, bool mrow, HeadBwdLds& L, int w, int lane, float* wsw, float* wsb) {
+  const int g = lane >> 4, li = lane & 15;
+  float xh[2][4], gg[2][4];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = mrow ? dy[t][e] : 0.f;
+      xh[t][e] = (xs[t][e] - mu) * rs;
+      L.sW[li][n + e] = d * xh[t][e];
+      L.sB[li][n + e] = d;
+      gg[t][e] = d * wv[t][e];
+      s1 += gg[t][e];
+      s2 += gg[t][e] * xh[t][e];
+    }
+  }
+  const float c1 = bwd_row_sum(s1, L, w, lane) * (1.f / HD);   // (its barriers publish sW, sB)
+  const float c2 = bwd_row_sum(s2, L, w, lane) * (1.f / HD);
+  if (threadIdx.x < HD) {                            // one column per thread, rows in order
+    const int c = threadIdx.x;
+    float cw = 0.f, cb = 0.f;
+#pragma unroll
+    for (int r = 0; r < HR; ++r) { cw += L.sW[r][c]; cb += L.sB[r][c]; }
+    wsw[c] = cw;
+    wsb[c] = cb;
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dy[t][e] = rs * (gg[t][e] - c1 - xh[t][e] * c2);
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
+#ifdef HEAD_STAMP
+  uint64_t stamp[8];
+#endif
+  STAMP(0);
+  __shared__ __attribute__((aligned(16))) HeadBwdLds L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * HR, m = r0 + li, mc = min(m, a.B - 1);
+  const bool mrow = m < a.B;
+  const int W = HD + a.dg + a.dc;
+  const int n0 = w * 32, nf0 = w * (F / 4);
+  float* wsb = a.ws + (int64_t)blockIdx.x * 4 * HD;   // this workgroup's four sum rows
+  WFrags<2, HD> wf3;
+  wf3.load(a.wf3t, HD, n0, lane, HD);
+  {                                                  // du rows -> LDS
+    const int r = tid >> 4, ch = tid & 15;
+    *reinterpret_cast<uint4*>(L.sA + r * PD + ch * 16) =
+        *reinterpret_cast<const uint4*>(a.du + (int64_t)min(r0 + r, a.B - 1) * HD + ch * 8);
+  }
+  const int drow = a.drows[mc];
+  const float mzr = a.mz[mc], rzr = a.rz[mc], m2r = a.m2[mc], r2r = a.r2[mc];
+  const uint64_t s1 = *a.d1.seed, s2 = *a.d2.seed;
+  const DropKeys dk1{(uint32_t)s1, (uint32_t)(s1 >> 32), a.d1.thresh, a.d1.scale, a.d1.on};
+  const DropKeys dk2{(uint32_t)s2, (uint32_t)(s2 >> 32), a.d2.thresh, a.d2.scale, a.d2.on};
+  if (tid < HR) {
+    L.sGi[tid] = (int)a.gender[min(r0 + tid, a.B - 1)];
+    L.sCi[tid] = (int)a.country[min(r0 + tid, a.B - 1)];
+  }
+  // every per-row operand of the chain now, before any weight prefetch: vmcnt retires in
+  // order, so a late small load would also wait for the weights issued before it
+  uint2 azq[2];
+  float zs[2][4], x1s[2][4], lnw[2][4], n2w[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float4 lw = *reinterpret_cast<const float4*>(a.lnw + n);
+    const float4 nw = *reinterpret_cast<const float4*>(a.n2w + n);
+    lnw[t][0] = lw.x; lnw[t][1] = lw.y; lnw[t][2] = lw.z; lnw[t][3] = lw.w;
+    n2w[t][0] = nw.x; n2w[t][1] = nw.y; n2w[t][2] = nw.z; n2w[t][3] = nw.w;
+    azq[t] = *reinterpret_cast<const uint2*>(a.az + (int64_t)mc * HD + n);
+    const float4 zv = *reinterpret_cast<const float4*>(a.z + (int64_t)mc * HD + n);
+    const float4 xv = *reinterpret_cast<const float4*>(a.x1 + (int64_t)mc * HD + n);
+    zs[t][0] = zv.x; zs[t][1] = zv.y; zs[t][2] = zv.z; zs[t][3] = zv.w;
+    x1s[t][0] = xv.x; x1s[t][1] = xv.y; x1s[t][2] = xv.z; x1s[t][3] = xv.w;
+  }
+  uint2 hq[F / 64];                                  // the wave's F / 4 gate columns, 4 per lane
+#pragma unroll
+  for (int q = 0; q < F / 64; ++q)
+    hq[q] = *reinterpret_cast<const uint2*>(a.h + (int64_t)mc * F + nf0 + 16 * q + 4 * g);
+  __syncthreads();
+  STAMP(1);
+  // ---- daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0])
+  f32x4_t v[2];
+  head_gemm<2, HD, PD>(L.sA, wf3, v, lane);
+  WFrags<3, HD> wf0;                                 // dcomb's 11 column tiles: w, w+4, w+8
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int tj = min(w + 4 * j, W / 16 - 1);
+#pragma unroll
+    for (int c = 0; c < HD / 32; ++c) wf0.f[c][j] = wfrag(a.wf0t, HD, 16 * tj + li, c, lane, HD);
+  }
+  {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {                    // ReLU gate of the forward's az
+      const uint2 q = azq[t];
+      const float gz[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[t][e] = gz[e] > 0.f ? v[t][e] : 0.f;
+    }
+    __syncthreads();                                 // every wave is done reading du
+    ln_bwd16(v, zs, mzr, rzr, lnw, n0, mrow, L, w, lane, wsb, wsb + HD);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+      st4_bf(L.sA + li * PD + n * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.dz16 + (int64_t)m * HD + n), x);
+    }
+  }
+  __syncthreads();
+  STAMP(2);
+  // ---- dcomb = dz·Wf0: columns < D -> dx2 (LDS), the demographic ones -> dG / dC
+  WFrags<4, HD> w2a;
+  {
+    f32x4_t dc[3];
+    head_gemm<3, HD, PD>(L.sA, wf0, dc, lane);
+    w2a.load(a.w2t, HD, nf0, lane, HD);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int tj = w + 4 * j;
+      if (tj >= W / 16) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 16 * tj + 4 * g + e;
+        const float val = dc[j][e];
+        if (k < HD) L.sX[li][k] = mrow ? val : 0.f;
+        else L.sDem[li][k - HD] = val;
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(3);
+  // ---- dy2 = drop2ᵀ(dx2) -> LDS (A of the next product) and HBM
+  {
+    const int n = n0 + 4 * g;                        // two 16-column tiles per wave
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = L.sX[li][n + 16 * t + e];
+      drop_apply_vec<4>(dk2, (uint32_t)(drow * HD + n + 16 * t), x);
+      st4_bf(L.sA + li * PD + (n + 16 * t) * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.dy2 + (int64_t)m * HD + n + 16 * t), x);
+    }
+  }
+  __syncthreads();
+  STAMP(4);
+  // ---- dz1 = (dy2·W2) ⊙ [h > 0]·sf
+  WFrags<2, F> w1;
+  {
+    WFrags<4, HD> w2n;
+#pragma unroll
+    for (int nb = 0; nb < F / 4; nb += 64) {
+      f32x4_t hv[4];
+      head_gemm<4, HD, PD>(L.sA, nb == 0 ? w2a : w2n, hv, lane);
+      if (nb + 64 < F / 4) w2n.load(a.w2t, HD, nf0 + nb + 64, lane, HD);
+      else w1.load(a.w1t, F, n0, lane, F);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = nf0 + nb + 16 * t + 4 * g;
+        const uint2 q = hq[nb / 16 + t];
+        const float hg[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                             __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u)};
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = hg[e] > 0.f ? hv[t][e] * a.sf : 0.f;
+        st4_bf(L.sH + li * PF + n * 2, x);
+        if (mrow) st4_bf(reinterpret_cast<char*>(a.dz1 + (int64_t)m * F + n), x);
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(5);
+  // ---- dx1 = LN2ᵀ(dz1·W1) + dx2; dy1 = drop1ᵀ(dx1)
+  head_gemm<2, F, PF>(L.sH, w1, v, lane);
+  WFrags<2, HD> wo;
+  wo.load(a.wot, HD, n0, lane, HD);
+  ln_bwd16(v, x1s, m2r, r2r, n2w, n0, mrow, L, w, lane, wsb + 2 * HD, wsb + 3 * HD);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    float x[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = v[t][e] + L.sX[li][n + e];
+    if (mrow) *reinterpret_cast<float4*>(a.dx1 + (int64_t)m * HD + n) = make_float4(x[0], x[1], x[2], x[3]);
+    drop_apply_vec<4>(dk1, (uint32_t)(drow * HD + n), x);
+    st4_bf(L.sA + li * PD + n * 2, x);               // every wave is past its dy2 reads
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dy1 + (int64_t)m * HD + n), x);
+  }
+  __syncthreads();
+  STAMP(6);
+  // ---- dctx = dy1·Wo
+  head_gemm<2, HD, PD>(L.sA, wo, v, lane);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dctx + (int64_t)m * HD + n), x);
+  }
+  // ---- dG / dC last (nothing later waits on the atomics).  Rows sharing an index are summed
+  // here first: one atomic per (distinct index, column) per workgroup, a row's 48 columns in
+  // one coalesced instruction (lanes 0-15 gender, 16-47 country).
+  if (lane < 48) {
+    const bool isg = lane < 16;
+    const int k = isg ? lane : lane - 16;
+    const int nr = min(HR, a.B - r0);
+    int key[HR];
+    float val[HR];
+#pragma unroll
+    for (int j = 0; j < HR; ++j) {                   // all LDS reads at once, then registers
+      key[j] = isg ? L.sGi[j] : L.sCi[j];
+      val[j] = L.sDem[j][lane];
+    }
+#pragma unroll
+    for (int r = 0; r < HR; ++r) {                   // wave w issues rows r % 4 == w
+      if ((r & 3) != w || r >= nr) continue;
+      bool first = true;
+#pragma unroll
+      for (int j = 0; j < r; ++j) first &= key[j] != key[r];
+      if (!first) continue;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = r; j < HR; ++j) sum += (j < nr && key[j] == key[r]) ? val[j] : 0.f;
+      atomicAdd(isg ? a.dG + (int64_t)key[r] * a.dg + k : a.dC + (int64_t)key[r] * a.dc + k, sum);
+    }
+  }
+#ifdef HEAD_STAMP
+  __syncthreads();
+  STAMP(7);
+  if (threadIdx.x == 0 && blockIdx.x < 4)
+    for (int i = 1; i < 8; ++i) a.dx1[blockIdx.x * 8 + i] = (float)(stamp[i] - stamp[0]);
+#endif
+}
+
 }  // namespace
 
 extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
@@ -375,4 +665,33 @@ extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
   if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_kernel<512>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(user_head_fwd_kernel<256>, grid, dim3(256), 0, s, a);
   return ttmi_check_launch("ttmi_user_head_fwd");
+}
+
+extern "C" int64_t ttmi_user_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 4 * HD; }
+
+extern "C" int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t s) {
+  TTMI_REQUIRE(d != nullptr, "ttmi_user_head_bwd: null descriptor");
+  TTMI_REQUIRE(d->B > 0 && d->D == HD && (d->F == 256 || d->F == 512) && d->dg == 16 && d->dc == 32,
+               "ttmi_user_head_bwd: needs D == %d, F in {256, 512}, dg == 16, dc == 32", HD);
+  TTMI_REQUIRE(d->du && d->az && d->z && d->mz && d->rz && d->h && d->x1 && d->m2 && d->r2 &&
+               d->drop_rows && d->gender && d->country && d->wf3t && d->wf0t && d->w2t && d->w1t &&
+               d->wot && d->lnw && d->n2w && d->dG && d->dC && d->dz16 && d->dy2 && d->dz1 &&
+               d->dx1 && d->dy1 && d->dctx && d->ws, "ttmi_user_head_bwd: null argument");
+  HeadBwdArgs a{};
+  a.B = d->B; a.F = d->F; a.dg = d->dg; a.dc = d->dc; a.sf = d->ffn_scale;
+  a.du = (const bf16_t*)d->du; a.az = (const bf16_t*)d->az; a.z = d->z; a.mz = d->mz; a.rz = d->rz;
+  a.h = (const bf16_t*)d->h; a.x1 = d->x1; a.m2 = d->m2; a.r2 = d->r2;
+  a.drows = d->drop_rows; a.gender = d->gender; a.country = d->country;
+  a.wf3t = (const bf16_t*)d->wf3t; a.wf0t = (const bf16_t*)d->wf0t; a.w2t = (const bf16_t*)d->w2t;
+  a.w1t = (const bf16_t*)d->w1t; a.wot = (const bf16_t*)d->wot; a.lnw = d->lnw; a.n2w = d->n2w;
+  const uint64_t* any = reinterpret_cast<const uint64_t*>(d->lnw);   // read, never used when off
+  a.d1 = make_drop(d->d1_p, d->d1_seed ? d->d1_seed : any);
+  a.d2 = make_drop(d->d2_p, d->d2_seed ? d->d2_seed : any);
+  a.dG = d->dG; a.dC = d->dC;
+  a.dz16 = (bf16_t*)d->dz16; a.dy2 = (bf16_t*)d->dy2; a.dz1 = (bf16_t*)d->dz1; a.dx1 = d->dx1;
+  a.dy1 = (bf16_t*)d->dy1; a.dctx = (bf16_t*)d->dctx; a.ws = d->ws;
+  const dim3 grid((unsigned)((d->B + HR - 1) / HR));
+  if (d->F == 512) hipLaunchKernelGGL(user_head_bwd_kernel<512>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(user_head_bwd_kernel<256>, grid, dim3(256), 0, s, a);
+  return ttmi_check_launch("ttmi_user_head_bwd");
 }

@@ -301,33 +301,33 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
     M = B * L
     seeds = st.seeds
     f32 = dict(device=dev, dtype=torch.float32)
-    # ---- user fusion MLP (user_tower.py:51-57, :142)
-    if du16 is not None and du16.dtype == dt:
-        du_c = du16
-    else:
-        du_c = torch.empty(B, D, device=dev, dtype=dt)
-        ops.dropout_bwd(du, du_c, None)
-    ops.linear_dw(du_c, st.az, grads["fusion_layer.3.weight"], grads["fusion_layer.3.bias"])
-    daz = torch.empty(B, D, **f32)
-    ops.linear_dx(du_c, W["fusion_layer.3.weight"], daz)
-    dz = torch.empty(B, D, **f32)
-    dz_c = torch.empty(B, D, device=dev, dtype=dt)
-    ops.layernorm_bwd(daz, st.z, st.mz, st.rz, P["fusion_layer.1.weight"], dz,
-                      grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"], gate=st.az,
-                      dx16=dz_c if dt == torch.bfloat16 else None)
-    if dt != torch.bfloat16:
-        ops.dropout_bwd(dz, dz_c, None)
-    ops.linear_dw(dz_c, st.comb, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
-    dcomb = torch.empty(B, st.comb.shape[1], **f32)
-    ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dcomb)
     gathered = cfg.prune_last and cfg.n_layers > 0
-    # gathered: every row of dx [B, D] is written once (no zero fill); else only B of M rows
-    dx = torch.empty(B, D, **f32) if gathered else torch.zeros(M, D, **f32)
     G = P["gender_embedding.weight"]
     C = P["country_embedding.weight"]
-    ops.user_concat_bwd(dcomb, st.rows, st.gender, G.shape[1], st.country, C.shape[1], dx,
-                        grads["gender_embedding.weight"], grads["country_embedding.weight"],
-                        accumulate=not gathered)
+    head = None
+    last = _lp(cfg.n_layers - 1) if cfg.n_layers > 0 else ""
+    if gathered and du16 is not None and du16.dtype == torch.bfloat16 and \
+            ops.user_head_fusable(W, P, last, D, dt) and ops.user_head_bwd_fusable(W, last):
+        # the head's backward (fusion MLP, concat, the pruned layer's FFN / LN2 / out_proj input
+        # grads) in one launch; its weight gradients are the same deferred GEMMs
+        i = cfg.n_layers - 1
+        s = st.layers[i]
+        saved = dict(az=st.az, z=st.z, mz=st.mz, rz=st.rz, h=s.h, x1=s.x1, m2=s.m2, r2=s.r2)
+        head = ops.user_head_bwd(
+            du16, saved, s.rows, W, P, last, st.gender, st.country, _scale(cfg.p_drop),
+            (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_drop2(i))),
+            grads["gender_embedding.weight"], grads["country_embedding.weight"],
+            (grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"],
+             grads[last + "norm2.weight"], grads[last + "norm2.bias"]))
+        ops.linear_dw(du16, st.az, grads["fusion_layer.3.weight"], grads["fusion_layer.3.bias"])
+        ops.linear_dw(head["dz16"], st.comb, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
+        ops.linear_dw(head["dy2"], s.h, grads[last + "linear2.weight"], grads[last + "linear2.bias"])
+        ops.linear_dw(head["dz1"], s.a2, grads[last + "linear1.weight"], grads[last + "linear1.bias"])
+        ops.linear_dw(head["dy1"], s.ctx, grads[last + "self_attn.out_proj.weight"],
+                      grads[last + "self_attn.out_proj.bias"])
+        dx = None
+    else:
+        dx = _head_bwd_unfused(P, W, st, du, grads, cfg, du16, gathered)
     # ---- encoder layers, reversed (user_tower.py:37-45)
     p = cfg.p_drop
     dy2_next = None        # layer i's dy2, emitted by layer i+1's fused LN1 backward
@@ -338,32 +338,11 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         drows = s.rows
         F_ = W[pre + "linear1.weight"].shape[0]
         fuse = _ln_fusable(W, pre, D)
-        if dy2_next is not None:
-            dy2, dy2_next = dy2_next, None
+        if head is not None and i == cfg.n_layers - 1:
+            dctx, dx1 = head["dctx"], head["dx1"]
         else:
-            dy2 = torch.empty(R, D, device=dev, dtype=dt)
-            ops.dropout_bwd(dx, dy2, None, _drop(cfg, seeds, site_drop2(i)), drop_rows=drows)
-        ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"], grads[pre + "linear2.bias"])
-        dz1 = torch.empty(R, F_, device=dev, dtype=dt)
-        _dx(dy2, W, pre + "linear2.weight", dz1, gate=s.h, gate_scale=_scale(p))
-        ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"], grads[pre + "linear1.bias"])
-        dx1 = torch.empty(R, D, **f32)
-        dy1 = torch.empty(R, D, device=dev, dtype=dt)
-        if fuse:     # linear1 input grad + LN2 backward + dropout1 backward, one kernel
-            ops.linear_ln_bwd(dz1, W[transposed_name(pre + "linear1.weight")], s.x1, s.m2, s.r2,
-                              P[pre + "norm2.weight"], dx1, grads[pre + "norm2.weight"],
-                              grads[pre + "norm2.bias"], res=dx, next_=dy1,
-                              drop=_drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
-        else:
-            da2 = torch.empty(R, D, **f32)
-            _dx(dz1, W, pre + "linear1.weight", da2)
-            ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
-                              grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
-            ops.dropout_bwd(dx1, dy1, None, _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
-        ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"],
-                      grads[pre + "self_attn.out_proj.bias"])
-        dctx = torch.empty(R, D, device=dev, dtype=dt)
-        _dx(dy1, W, pre + "self_attn.out_proj.weight", dctx)
+            dx1, dctx, dy2_next = _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre,
+                                                  R, drows, F_, fuse, D, dt, p)
         dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         if drows is not None:
             ops.mha_q1_bwd(s.qkv, st.key_valid, drows, s.lse, dctx, B, L, H, dqkv,
@@ -403,6 +382,79 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
                       P["layer_norm.weight"], st.m0, st.r0, dx, grads["item_embedding.weight"],
                       grads["position_embedding.weight"], grads["layer_norm.weight"],
                       grads["layer_norm.bias"], drop=_drop(cfg, seeds, SITE_EMB), padding_idx=0)
+
+
+def _head_bwd_unfused(P, W, st, du, grads, cfg, du16, gathered):
+    """The user fusion MLP and concat backward as separate launches; returns dx (the grad of
+    the last encoder layer's output rows)."""
+    dev = du.device
+    B, L = st.ids.shape
+    D, dt = cfg.D, cfg.dtype
+    M = B * L
+    f32 = dict(device=dev, dtype=torch.float32)
+    # ---- user fusion MLP (user_tower.py:51-57, :142)
+    if du16 is not None and du16.dtype == dt:
+        du_c = du16
+    else:
+        du_c = torch.empty(B, D, device=dev, dtype=dt)
+        ops.dropout_bwd(du, du_c, None)
+    ops.linear_dw(du_c, st.az, grads["fusion_layer.3.weight"], grads["fusion_layer.3.bias"])
+    daz = torch.empty(B, D, **f32)
+    ops.linear_dx(du_c, W["fusion_layer.3.weight"], daz)
+    dz = torch.empty(B, D, **f32)
+    dz_c = torch.empty(B, D, device=dev, dtype=dt)
+    ops.layernorm_bwd(daz, st.z, st.mz, st.rz, P["fusion_layer.1.weight"], dz,
+                      grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"], gate=st.az,
+                      dx16=dz_c if dt == torch.bfloat16 else None)
+    if dt != torch.bfloat16:
+        ops.dropout_bwd(dz, dz_c, None)
+    ops.linear_dw(dz_c, st.comb, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
+    dcomb = torch.empty(B, st.comb.shape[1], **f32)
+    ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dcomb)
+    gathered = cfg.prune_last and cfg.n_layers > 0
+    # gathered: every row of dx [B, D] is written once (no zero fill); else only B of M rows
+    dx = torch.empty(B, D, **f32) if gathered else torch.zeros(M, D, **f32)
+    G = P["gender_embedding.weight"]
+    C = P["country_embedding.weight"]
+    ops.user_concat_bwd(dcomb, st.rows, st.gender, G.shape[1], st.country, C.shape[1], dx,
+                        grads["gender_embedding.weight"], grads["country_embedding.weight"],
+                        accumulate=not gathered)
+    return dx
+
+
+def _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre, R, drows, F_, fuse, D, dt, p):
+    """One encoder layer's backward from its output grad dx down to dctx (FFN, LN2, residual,
+    out_proj input grad).  Returns dx1 (the grad of the attention residual), dctx and the
+    pending dy2 (None)."""
+    dev = dx.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    if dy2_next is not None:
+        dy2 = dy2_next
+    else:
+        dy2 = torch.empty(R, D, device=dev, dtype=dt)
+        ops.dropout_bwd(dx, dy2, None, _drop(cfg, seeds, site_drop2(i)), drop_rows=drows)
+    ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"], grads[pre + "linear2.bias"])
+    dz1 = torch.empty(R, F_, device=dev, dtype=dt)
+    _dx(dy2, W, pre + "linear2.weight", dz1, gate=s.h, gate_scale=_scale(p))
+    ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"], grads[pre + "linear1.bias"])
+    dx1 = torch.empty(R, D, **f32)
+    dy1 = torch.empty(R, D, device=dev, dtype=dt)
+    if fuse:     # linear1 input grad + LN2 backward + dropout1 backward, one kernel
+        ops.linear_ln_bwd(dz1, W[transposed_name(pre + "linear1.weight")], s.x1, s.m2, s.r2,
+                          P[pre + "norm2.weight"], dx1, grads[pre + "norm2.weight"],
+                          grads[pre + "norm2.bias"], res=dx, next_=dy1,
+                          drop=_drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
+    else:
+        da2 = torch.empty(R, D, **f32)
+        _dx(dz1, W, pre + "linear1.weight", da2)
+        ops.layernorm_bwd(da2, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx1,
+                          grads[pre + "norm2.weight"], grads[pre + "norm2.bias"], res=dx)
+        ops.dropout_bwd(dx1, dy1, None, _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
+    ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"],
+                  grads[pre + "self_attn.out_proj.bias"])
+    dctx = torch.empty(R, D, device=dev, dtype=dt)
+    _dx(dy1, W, pre + "self_attn.out_proj.weight", dctx)
+    return dx1, dctx, None
 
 
 # ===================================================================================== item

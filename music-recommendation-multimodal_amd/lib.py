@@ -95,6 +95,22 @@ class UserHeadDesc(ctypes.Structure):
                 ("rows", c_p), ("z", c_p), ("az", c_p), ("mz", c_p), ("rz", c_p), ("u", c_p)]
 
 
+class UserHeadBwdDesc(ctypes.Structure):
+    """ttmi_user_head_bwd_desc (include/ttmi.h)."""
+    _fields_ = [("B", c_i), ("D", c_i), ("F", c_i), ("dg", c_i), ("dc", c_i),
+                ("ffn_scale", ctypes.c_float),
+                ("du", c_p), ("az", c_p), ("z", c_p), ("mz", c_p), ("rz", c_p),
+                ("h", c_p), ("x1", c_p), ("m2", c_p), ("r2", c_p),
+                ("drop_rows", c_p), ("gender", c_p), ("country", c_p),
+                ("wf3t", c_p), ("wf0t", c_p), ("w2t", c_p), ("w1t", c_p), ("wot", c_p),
+                ("lnw", c_p), ("n2w", c_p),
+                ("d1_p", ctypes.c_float), ("d1_seed", c_p),
+                ("d2_p", ctypes.c_float), ("d2_seed", c_p),
+                ("dG", c_p), ("dC", c_p),
+                ("dz16", c_p), ("dy2", c_p), ("dz1", c_p), ("dx1", c_p), ("dy1", c_p),
+                ("dctx", c_p), ("ws", c_p)]
+
+
 class LnBwdDesc(ctypes.Structure):
     """ttmi_linear_ln_bwd_desc (include/ttmi.h)."""
     _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
@@ -186,6 +202,8 @@ SIGNATURES = {
     "ttmi_dis_attn_pbx_floats": (ctypes.c_int64, [c_i, c_i, c_i]),
     "ttmi_dis_attn_order": (c_i, [c_p, c_i, c_i, c_p, c_p]),
     "ttmi_user_head_fwd": (c_i, [c_p, c_p]),
+    "ttmi_user_head_bwd": (c_i, [c_p, c_p]),
+    "ttmi_user_head_bwd_ws_floats": (ctypes.c_int64, [c_i]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,

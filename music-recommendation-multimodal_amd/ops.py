@@ -13,8 +13,8 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from . import lib as _L
-from .lib import (BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, UserHeadDesc,
-                  WgradDesc, call)
+from .lib import (BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, UserHeadBwdDesc,
+                  UserHeadDesc, WgradDesc, call)
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -801,6 +801,68 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
     for k in ("x1", "a2", "m2", "r2", "h", "comb", "rows", "z", "az", "mz", "rz", "u"):
         setattr(d, k, _p(out[k]))
     call("ttmi_user_head_fwd", ctypes.byref(d), _s())
+
+
+def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: Dict[str, Tensor],
+                  P: Dict[str, Tensor], pre: str, gender: Tensor, country: Tensor, ffn_scale: float,
+                  drops: Tuple[Drop, Drop], dG: Tensor, dC: Tensor,
+                  ln_grads: Tuple[Tensor, Tensor, Tensor, Tensor]) -> Dict[str, Tensor]:
+    """Backward of user_head_fwd in one launch (ttmi_user_head_bwd).  ``saved``: az, z, mz, rz,
+    h, x1, m2, r2 of the forward; ``drops`` = (drop1, drop2).  Returns dz16, dy2, dz1, dx1, dy1,
+    dctx; the four LayerNorm parameter gradients (``ln_grads``: fusion LN weight, bias, norm2
+    weight, bias) are folded from per-block sums (deferred with the step's weight gradients
+    inside ``deferred_wgrad``)."""
+    B, D = du16.shape
+    F = W[pre + "linear1.weight"].shape[0]
+    dev = du16.device
+    bf = torch.bfloat16
+    o = dict(dz16=torch.empty(B, D, device=dev, dtype=bf), dy2=torch.empty(B, D, device=dev, dtype=bf),
+             dz1=torch.empty(B, F, device=dev, dtype=bf), dx1=torch.empty(B, D, device=dev),
+             dy1=torch.empty(B, D, device=dev, dtype=bf), dctx=torch.empty(B, D, device=dev, dtype=bf))
+    _L.load()
+    nws = int(_L._lib.ttmi_user_head_bwd_ws_floats(B))
+    ws = torch.empty(nws, device=dev)
+    d = UserHeadBwdDesc()
+    d.B, d.D, d.F = B, D, F
+    d.dg, d.dc = P["gender_embedding.weight"].shape[1], P["country_embedding.weight"].shape[1]
+    d.ffn_scale = ffn_scale
+    d.du = _p(du16)
+    for k in ("az", "z", "mz", "rz", "h", "x1", "m2", "r2"):
+        setattr(d, k, _p(saved[k]))
+    d.drop_rows, d.gender, d.country = _p(drop_rows), _p(gender), _p(country)
+    T = ".T"
+    d.wf3t, d.wf0t = _p(W["fusion_layer.3.weight" + T]), _p(W["fusion_layer.0.weight" + T])
+    d.w2t, d.w1t = _p(W[pre + "linear2.weight" + T]), _p(W[pre + "linear1.weight" + T])
+    d.wot = _p(W[pre + "self_attn.out_proj.weight" + T])
+    d.lnw, d.n2w = _p(P["fusion_layer.1.weight"]), _p(P[pre + "norm2.weight"])
+    (d.d1_p, s1), (d.d2_p, s2) = [(float(p), sd) for p, sd in drops]
+    d.d1_seed, d.d2_seed = _p(s1), _p(s2)
+    d.dG, d.dC = _p(dG), _p(dC)
+    for k in ("dz16", "dy2", "dz1", "dx1", "dy1", "dctx"):
+        setattr(d, k, _p(o[k]))
+    d.ws = _p(ws)
+    call("ttmi_user_head_bwd", ctypes.byref(d), _s())
+    nblk = nws // (4 * D)
+    folds = []
+    for j, g in enumerate(ln_grads):
+        f = FoldDesc()
+        f.part, f.S, f.s_stride, f.M, f.N = ws.data_ptr() + 4 * D * j, nblk, 4 * D, 1, D
+        f.C, f.ldc, f.accumulate = _p(g), D, 1
+        folds.append((f, ws, g))
+    pend = _PENDING[-1] if _PENDING else None
+    if pend is not None:
+        pend.folds.extend(folds)
+    else:
+        farr = (FoldDesc * len(folds))(*[f for f, *_ in folds])
+        call("ttmi_wgrad_batch", 0, (ctypes.POINTER(WgradDesc) * 1)(), len(folds), farr, _s())
+    return o
+
+
+def user_head_bwd_fusable(W: Dict[str, Tensor], pre: str) -> bool:
+    """The transposed weight mirrors ttmi_user_head_bwd reads are present."""
+    return all(n + ".T" in W for n in ("fusion_layer.3.weight", "fusion_layer.0.weight",
+                                       pre + "linear2.weight", pre + "linear1.weight",
+                                       pre + "self_attn.out_proj.weight"))
 
 
 def user_head_fusable(W: Dict[str, Tensor], P: Dict[str, Tensor], pre: str, D: int,

@@ -76,11 +76,14 @@ def cfg_dtype_bf16(dtype: torch.dtype) -> bool:
 
 
 def encoder_weight_names(names) -> List[str]:
-    return [n for n in names if n.endswith(GEMM_WEIGHTS)]
+    """Weights with a transposed mirror: every encoder-layer GEMM weight and the fusion MLP's
+    two (the fused head backward, ttmi_user_head_bwd, reads all of them k-major)."""
+    return [n for n in names if n.endswith(GEMM_WEIGHTS) or n.endswith(("fusion_layer.0.weight",
+                                                                        "fusion_layer.3.weight"))]
 
 
 def add_transposes(W: dict, gemm_names) -> None:
-    """Allocate W[name + '.T'] ([in, out] bf16) for every encoder-layer weight."""
+    """Allocate W[name + '.T'] ([in, out] bf16) for every weight encoder_weight_names lists."""
     for n in encoder_weight_names(gemm_names):
         w = W[n]
         W[F.transposed_name(n)] = torch.empty(w.shape[1], w.shape[0], device=w.device,

@@ -576,3 +576,88 @@ def test_user_head_fused_matches_ops(gpu_pkg, B, p):
         if p > 0 and k == "h":
             zo, zw = out[k] == 0, want[k] == 0
             assert (zo != zw).float().mean().item() < 1e-3
+
+
+@pytest.mark.parametrize("B,p", [(512, 0.1), (37, 0.0)])
+def test_user_head_bwd_fused_matches_ops(gpu_pkg, B, p):
+    """ttmi_user_head_bwd against the unfused backward ops it replaces (functional's
+    _head_bwd_unfused + _layer_tail_bwd for the pruned layer): dctx, dx1, the bf16 dY operands
+    of the deferred weight gradients, the LayerNorm parameter gradients (folded per-block sums)
+    and the demographic embedding gradients."""
+    ops, F_ = gpu_pkg.ops, gpu_pkg.functional
+    D, F, M = 128, 512, 9 * B
+    g = torch.Generator().manual_seed(B + 1)
+
+    def bf(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+    def f32(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(DEV)
+    pre = "transformer_encoder.layers.1."
+    names = {pre + "self_attn.out_proj.weight": (D, D), pre + "linear1.weight": (F, D),
+             pre + "linear2.weight": (D, F), "fusion_layer.0.weight": (D, D + 48),
+             "fusion_layer.3.weight": (D, D)}
+    W = {}
+    for n, (o, i) in names.items():
+        W[n] = bf(o, i, scale=i ** -0.5)
+        W[n + ".T"] = W[n].t().contiguous()
+    P = {pre + "norm2.weight": 1 + f32(D, scale=0.1), "fusion_layer.1.weight": 1 + f32(D, scale=0.1),
+         "gender_embedding.weight": f32(3, 16), "country_embedding.weight": f32(11, 32)}
+    for n in ("self_attn.out_proj.bias", "norm2.bias", "linear1.bias", "linear2.bias"):
+        P[pre + n] = f32(F if n == "linear1.bias" else D, scale=0.1)
+    for n in ("fusion_layer.0.bias", "fusion_layer.1.bias", "fusion_layer.3.bias"):
+        P[n] = f32(D, scale=0.1)
+    # a forward to get consistent saved values
+    ctx, res = bf(B, D), f32(B, D)
+    drows = torch.randperm(M, generator=g)[:B].to(torch.int32).to(DEV)
+    gender = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    country = torch.randint(0, 11, (B,), generator=g).to(DEV)
+    seeds = torch.tensor([5, -6, 7], dtype=torch.int64, device=DEV)
+    drops = tuple((p, seeds[k:k + 1]) if p > 0 else ops.NO_DROP for k in range(3))
+    o = dict(x1=f32(B, D), a2=bf(B, D), m2=f32(B), r2=f32(B), h=bf(B, F), comb=bf(B, D + 48),
+             rows=torch.empty(B, dtype=torch.int32, device=DEV), z=f32(B, D), az=bf(B, D),
+             mz=f32(B), rz=f32(B), u=f32(B, D))
+    ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, o)
+    du16 = bf(B, D)
+    cfg = F_.TowerCfg(D=D, n_layers=2, p_drop=p)
+
+    def grads0():
+        return {k: torch.zeros(P[k].shape if k in P else (D, D), device=DEV) for k in (
+            "fusion_layer.1.weight", "fusion_layer.1.bias", pre + "norm2.weight", pre + "norm2.bias",
+            "gender_embedding.weight", "country_embedding.weight")}
+    # unfused: head MLP + concat, then the layer tail
+    Gu = grads0()
+    for k in ("fusion_layer.3.weight", "fusion_layer.0.weight", pre + "linear2.weight",
+              pre + "linear1.weight", pre + "self_attn.out_proj.weight"):
+        Gu[k] = torch.zeros(names[k], device=DEV)
+        Gu[k.replace("weight", "bias")] = torch.zeros(names[k][0], device=DEV)
+
+    class St:
+        pass
+    st = St()
+    st.ids = torch.zeros(B, 1, dtype=torch.int64, device=DEV)
+    st.az, st.z, st.mz, st.rz, st.comb, st.rows = o["az"], o["z"], o["mz"], o["rz"], o["comb"], o["rows"]
+    st.gender, st.country = gender, country
+    dx = F_._head_bwd_unfused(P, W, st, du16.float(), Gu, cfg, du16, True)
+    s = F_.LayerSaved(None, None, None, None, None, ctx, None, o["x1"], o["a2"], o["m2"], o["r2"],
+                      o["h"], drows)
+    sd = torch.arange(1, 65, dtype=torch.int64, device=DEV) * 7919      # a full site table
+    cfg_seeds = sd
+    dx1_u, dctx_u, _ = F_._layer_tail_bwd(P, W, s, dx, None, Gu, cfg, cfg_seeds, 1, pre, B, drows,
+                                          F, True, D, torch.bfloat16, p)
+    # fused
+    Gf = grads0()
+    site = (F_.site_drop1(1), F_.site_drop2(1))
+    dr = tuple((p, sd[k:k + 1]) if p > 0 else ops.NO_DROP for k in site)
+    head = ops.user_head_bwd(du16, dict(az=o["az"], z=o["z"], mz=o["mz"], rz=o["rz"], h=o["h"],
+                                        x1=o["x1"], m2=o["m2"], r2=o["r2"]),
+                             drows, W, P, pre, gender, country, F_._scale(p), dr,
+                             Gf["gender_embedding.weight"], Gf["country_embedding.weight"],
+                             (Gf["fusion_layer.1.weight"], Gf["fusion_layer.1.bias"],
+                              Gf[pre + "norm2.weight"], Gf[pre + "norm2.bias"]))
+    torch.cuda.synchronize()
+    assert rel(head["dx1"], dx1_u) < 2e-3
+    assert rel(head["dctx"].float(), dctx_u.float()) < 2e-2
+    for k in ("fusion_layer.1.weight", "fusion_layer.1.bias", pre + "norm2.weight", pre + "norm2.bias",
+              "gender_embedding.weight", "country_embedding.weight"):
+        assert rel(Gf[k], Gu[k]) < 2e-3, k

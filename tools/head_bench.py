@@ -58,6 +58,32 @@ def main(B=512, D=128, F=512):
         print("stamps (cycles since start; prologue, S1+LN2, FFN1, FFN2, fusion0+LN, end):")
         print(st)
 
+    # backward (fused ttmi_user_head_bwd) on the forward's saved values
+    W2 = dict(W)
+    for n in list(W):
+        W2[n + ".T"] = W[n].t().contiguous()
+    du16 = bf(B, D)
+    dG, dC = torch.zeros(3, 16, device=dev), torch.zeros(11, 32, device=dev)
+    lg = tuple(torch.zeros(D, device=dev) for _ in range(4))
+
+    def fb():
+        return ops.user_head_bwd(du16, o, drows, W2, P, pre, gender, country, 1 / 0.9,
+                                 (drops[0], drops[2]), dG, dC, lg)
+    fb()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(100):
+        fb()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"user_head_bwd: {e0.elapsed_time(e1) * 10:.2f} us per launch + fold (back-to-back)")
+    if os.environ.get("TTMI_LIB"):
+        r = fb()
+        torch.cuda.synchronize()
+        st = r["dx1"][0, :32].view(4, 8)[:, 1:8].cpu()
+        print("bwd stamps (prologue, dz, dcomb, dy2, dz1, dx1, end):")
+        print(st)
+
 
 if __name__ == "__main__":
     main()
