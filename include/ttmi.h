@@ -399,6 +399,9 @@ typedef struct ttmi_linear_ln_bwd_desc {
                       G = ttmi_linear_ln_bwd_sum_blocks(M): each workgroup's dw row and db row,
                       plain stores; ln_dw / ln_db are then left to a fold (ttmi_wgrad_fold with
                       {part = sum_ws (+ N for db), S = G, s_stride = 2N, M = 1}): deterministic. */
+  const int32_t* res_rows; int64_t res_L;  /* ABI 13; non-NULL: res is [M / res_L, N] and its row
+                      b is added only to row res_rows[b] (b = m / res_L), other rows get none —
+                      the pruned last layer's gathered residual (replaces ttmi_scatter_add_rows) */
 } ttmi_linear_ln_bwd_desc;
 int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M);
 int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream);
@@ -473,6 +476,15 @@ int ttmi_scatter_add_rows(int B, int D, const float* src, const int32_t* rows, f
 int ttmi_mha_q1_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                     const int64_t* key_valid, const int32_t* rows, float drop_p,
                     const uint64_t* drop_seed, void* ctx, float* lse, hipStream_t stream);
+/* ttmi_mha_q1_fwd with the last-valid rows found in the same launch (ABI 13): rows[b] =
+ * b·L + max(len_b - 1, 0), len_b = the count of non-zero key_valid[b, :] (the reference's
+ * right-padding gather, user_tower.py:131-136), x_rows[b, :] = x[rows[b], :] (fp32 [M, H·Dh]),
+ * then the one-query attention of ttmi_mha_q1_fwd.  Replaces ttmi_last_rows_gather +
+ * ttmi_mha_q1_fwd. */
+int ttmi_mha_q1_gather_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                           const int64_t* key_valid, const float* x, int32_t* rows, float* x_rows,
+                           float drop_p, const uint64_t* drop_seed, void* ctx, float* lse,
+                           hipStream_t stream);
 /* Backward: writes the full dqkv [B*L, 3HDh] (dQ only on the query rows, zero elsewhere;
  * dK, dV on every row). */
 int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,

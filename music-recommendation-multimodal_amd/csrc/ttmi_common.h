@@ -178,19 +178,29 @@ void ttmi_set_error(const char* fmt, ...);
   } while (0)
 int ttmi_check_launch(const char* what);
 
-// GELU, exact erf form (torch.nn.functional.gelu default; DeBERTa-v2 hidden_act "gelu")
-TTMI_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-// GELU'(x) = Phi(x) + x·phi(x).  erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7), whose
-// exp(-z²) (z = x/√2) is the same exponential phi needs: one exp + one rcp per element (the
-// erff call was ~3x the VALU of this in the GELU-backward GEMM epilogue).
-TTMI_DEV float gelu_erf_grad(float x) {
+// GELU, erf form (torch.nn.functional.gelu default; DeBERTa-v2 hidden_act "gelu"), and its
+// derivative GELU'(x) = Phi(x) + x·phi(x).  Phi through erf by Abramowitz-Stegun 7.1.26
+// (|error| <= 1.5e-7): erfc(z) = poly(t)·exp(-z²), t = 1 / (1 + p·z), z = |x|/√2, and exp(-z²)
+// is also the exponential phi needs — one exp and one rcp per element (libm erff was ~3x the
+// VALU in the GEMM epilogues).  Phi = 1 - erfc/2 for x >= 0 and erfc/2 below, so the negative
+// tail keeps its relative precision (no 1 - (1 - small)).
+TTMI_DEV float gelu_phi_e(float x, float& e) {
   const float z = fabsf(x) * 0.70710678118654752f;
   const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * z);
-  const float e = __expf(-0.5f * x * x);
+  e = __expf(-0.5f * x * x);
   const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f +
                      t * (-1.453152027f + t * 1.061405429f))));
-  const float erf_abs = 1.f - poly * e;
-  return 0.5f * (1.f + copysignf(erf_abs, x)) + x * 0.39894228040143268f * e;
+  const float half_erfc = 0.5f * poly * e;
+  return x >= 0.f ? 1.f - half_erfc : half_erfc;
+}
+TTMI_DEV float gelu_erf(float x) {
+  float e;
+  return x * gelu_phi_e(x, e);
+}
+TTMI_DEV float gelu_erf_grad(float x) {
+  float e;
+  const float phi_cdf = gelu_phi_e(x, e);
+  return phi_cdf + x * 0.39894228040143268f * e;
 }
 
 // 8 bf16 <-> 8 floats (one 16-byte chunk)

@@ -352,6 +352,7 @@ struct LnBwdArgs {
   const float* x; int64_t ldx;
   const float* mean; const float* rstd; const float* w;
   const float* res; int64_t ld_res;
+  const int32_t* res_rows; int64_t res_L;   // res row b feeds row res_rows[b] (b = m / res_L) only
   float* dx; int64_t lddx;
   bf16_t* next; int64_t ld_next;
   DropParams drop; int64_t ld_drop; const int32_t* drop_rows;
@@ -387,15 +388,27 @@ TTMI_DEV void panel_ln_bwd_load(const LnBwdArgs& ln, int64_t m, int64_t M, int l
   const int64_t mc = std::min<int64_t>(m, M - 1);
   o.mu = ln.mean[mc];
   o.rs = ln.rstd[mc];
+  // gathered residual: row b = m / res_L of res, added only at row res_rows[b] (the pruned
+  // layer's last-valid rows); the select follows the unconditional clamped load
+  int64_t rr = mc;
+  bool rhit = true;
+  if (ln.res_rows) {
+    rr = mc / ln.res_L;
+    rhit = (int64_t)ln.res_rows[rr] == mc;
+  }
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int n = 32 * p + 8 * lg;
     o.x[2 * p] = *reinterpret_cast<const float4*>(ln.x + mc * ln.ldx + n);
     o.x[2 * p + 1] = *reinterpret_cast<const float4*>(ln.x + mc * ln.ldx + n + 4);
     if (ln.res) {
-      o.r[2 * p] = *reinterpret_cast<const float4*>(ln.res + mc * ln.ld_res + n);
-      o.r[2 * p + 1] = *reinterpret_cast<const float4*>(ln.res + mc * ln.ld_res + n + 4);
+      o.r[2 * p] = *reinterpret_cast<const float4*>(ln.res + rr * ln.ld_res + n);
+      o.r[2 * p + 1] = *reinterpret_cast<const float4*>(ln.res + rr * ln.ld_res + n + 4);
     }
+  }
+  if (ln.res && !rhit) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o.r[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -1559,15 +1572,20 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigArgs ba) {
   const DropKeys dk = resolve_drop(g.drop);
   const int li = lane & 15, lg = lane >> 4;
   if constexpr (EPI >= 0 && (EPI & (BE_BIAS | BE_GELU_GRAD | BE_RELU_GATE | BE_RES))) {
-    // 16 items (i, p), operands one item ahead
-    EpiIn cur, nxt;
-    big_epi_load<EPI>(g, m0 + wr * 128 + li, n0 + wc * 64 + 8 * lg, cur);
+    // 16 items (i, p), operands DEPTH items ahead (a ring of registers once the loop is
+    // unrolled).  One item ahead left each item waiting out most of an HBM round trip: with
+    // one workgroup per CU the epilogue is not hidden behind another tile's main loop.
+    constexpr int DEPTH = (EPI & BE_RES) ? 4 : 8;
+    EpiIn buf[16];
+#pragma unroll
+    for (int it = 0; it < DEPTH; ++it)
+      big_epi_load<EPI>(g, m0 + wr * 128 + 16 * (it >> 1) + li, n0 + wc * 64 + 32 * (it & 1) + 8 * lg, buf[it]);
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int i = it >> 1, p = it & 1;
-      if (it + 1 < 16)
-        big_epi_load<EPI>(g, m0 + wr * 128 + 16 * ((it + 1) >> 1) + li,
-                          n0 + wc * 64 + 32 * ((it + 1) & 1) + 8 * lg, nxt);
+      if (it + DEPTH < 16)
+        big_epi_load<EPI>(g, m0 + wr * 128 + 16 * ((it + DEPTH) >> 1) + li,
+                          n0 + wc * 64 + 32 * ((it + DEPTH) & 1) + 8 * lg, buf[it + DEPTH]);
       const int64_t m = m0 + wr * 128 + 16 * i + li;
       const int64_t n = n0 + wc * 64 + 32 * p + 8 * lg;
       if (m < g.M && n < g.N) {
@@ -1577,10 +1595,9 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigArgs ba) {
           v[e] = g.alpha * acc[i][2 * p][e];
           v[4 + e] = g.alpha * acc[i][2 * p + 1][e];
         }
-        if (n + 7 < g.N) big_epi8_pre<EPI>(g, dk, m, n, v, cur);
+        if (n + 7 < g.N) big_epi8_pre<EPI>(g, dk, m, n, v, buf[it]);
         else big_epi8<EPI>(g, dk, m, n, v);
       }
-      cur = nxt;
     }
   } else {
 #pragma unroll
@@ -1868,6 +1885,7 @@ extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t 
                d->lddx >= 128, "ttmi_linear_ln_bwd: x/dx need 16-byte rows");
   TTMI_REQUIRE(!d->res || (al16(d->res) && d->ld_res % 4 == 0 && d->ld_res >= 128),
                "ttmi_linear_ln_bwd: res needs 16-byte rows");
+  TTMI_REQUIRE(!d->res_rows || (d->res && d->res_L > 0), "ttmi_linear_ln_bwd: res_rows needs res and res_L > 0");
   TTMI_REQUIRE(!d->next || (al16(d->next) && d->ld_next % 8 == 0 && d->ld_next >= 128),
                "ttmi_linear_ln_bwd: next needs 16-byte rows");
   TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f && (d->drop_p == 0.f || d->drop_seed),
@@ -1881,6 +1899,7 @@ extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t 
   LnBwdArgs ln{};
   ln.x = d->x; ln.ldx = d->ldx; ln.mean = d->mean; ln.rstd = d->rstd; ln.w = d->ln_w;
   ln.res = d->res; ln.ld_res = d->ld_res;
+  ln.res_rows = d->res_rows; ln.res_L = d->res_L;
   ln.dx = d->dx; ln.lddx = d->lddx;
   ln.next = static_cast<bf16_t*>(d->next); ln.ld_next = d->ld_next;
   ln.drop = make_drop(d->drop_p, d->drop_seed); ln.ld_drop = d->ld_drop ? d->ld_drop : 128;

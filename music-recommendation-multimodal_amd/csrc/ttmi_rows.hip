@@ -132,11 +132,17 @@ TTMI_DEV float rows_combine(const float* coef, const T* __restrict__ base, int64
 // One 64-lane wave per (b, h), XCD-contiguous so the H heads of a sequence share an L2;
 // lane j owns key j (L <= 64) for the score/softmax phase; lanes own (row group, 16-byte
 // chunk) pairs for the P·V / dS·K reductions and the row stores.
-template <typename T>
+// GATHER: the wave also finds the sequence's last valid row itself (rows[b] = b·L +
+// max(len - 1, 0), len = the count of non-zero key_valid entries: the right-padding convention
+// of last_rows_gather_kernel) and the head-0 wave writes rows[b] and x_rows[b] = x[rows[b]]
+// (the pruned layer's residual rows), so no separate gather launch precedes it.
+template <typename T, bool GATHER>
 __global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int Dh,
                                                         const T* __restrict__ qkv,
                                                         const int64_t* __restrict__ kvalid,
-                                                        const int32_t* __restrict__ rows,
+                                                        int32_t* __restrict__ rows,
+                                                        const float* __restrict__ x,
+                                                        float* __restrict__ x_rows,
                                                         DropParams dp, T* __restrict__ ctx,
                                                         float* __restrict__ lse, float scale) {
   __shared__ float sq[64], sp[64], red[64 * 8];
@@ -144,7 +150,18 @@ __global__ __launch_bounds__(64) void mha_q1_fwd_kernel(int B, int L, int H, int
   const int bh = xcd_contiguous(blockIdx.x, gridDim.x), b = bh / H, h = bh % H;
   const int D = H * Dh;
   const int64_t ld = 3LL * D;
-  const int64_t r = rows[b];
+  int64_t r;
+  if constexpr (GATHER) {
+    const float cnt = (j < L && kvalid[(int64_t)b * L + j] != 0) ? 1.f : 0.f;
+    const int len = (int)(wave_sum(cnt) + 0.5f);
+    r = (int64_t)b * L + max(len - 1, 0);
+    if (h == 0) {
+      if (j == 0) rows[b] = (int32_t)r;
+      for (int c = j; c < D; c += 64) x_rows[(int64_t)b * D + c] = x[r * D + c];
+    }
+  } else {
+    r = rows[b];
+  }
   const int p = (int)(r - (int64_t)b * L);
   const T* seq = qkv + (int64_t)b * L * ld + (int64_t)h * Dh;
   if (j < Dh) sq[j] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + j);
@@ -279,13 +296,37 @@ extern "C" int ttmi_mha_q1_fwd(int dtype, int B, int L, int H, int Dh, const voi
   if (B == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
   const float scale = 1.f / sqrtf((float)Dh);
+  int32_t* rw = const_cast<int32_t*>(rows);          // read only (GATHER = false)
   if (dtype == TTMI_BF16)
-    hipLaunchKernelGGL(mha_q1_fwd_kernel<bf16_t>, dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
-                       (const bf16_t*)qkv, key_valid, rows, dp, (bf16_t*)ctx, lse, scale);
+    hipLaunchKernelGGL((mha_q1_fwd_kernel<bf16_t, false>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const bf16_t*)qkv, key_valid, rw, nullptr, nullptr, dp, (bf16_t*)ctx, lse, scale);
   else
-    hipLaunchKernelGGL(mha_q1_fwd_kernel<float>, dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
-                       (const float*)qkv, key_valid, rows, dp, (float*)ctx, lse, scale);
+    hipLaunchKernelGGL((mha_q1_fwd_kernel<float, false>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const float*)qkv, key_valid, rw, nullptr, nullptr, dp, (float*)ctx, lse, scale);
   return ttmi_check_launch("ttmi_mha_q1_fwd");
+}
+
+extern "C" int ttmi_mha_q1_gather_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                                      const int64_t* key_valid, const float* x, int32_t* rows,
+                                      float* x_rows, float drop_p, const uint64_t* drop_seed,
+                                      void* ctx, float* lse, hipStream_t s) {
+  TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_gather_fwd: bad dtype");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0,
+               "ttmi_mha_q1_gather_fwd: need L <= 64, Dh <= 64, Dh %% 8 == 0");
+  TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "ttmi_mha_q1_gather_fwd: qkv must be 16-byte aligned");
+  TTMI_REQUIRE(qkv && key_valid && x && rows && x_rows && ctx && lse, "ttmi_mha_q1_gather_fwd: null argument");
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
+               "ttmi_mha_q1_gather_fwd: bad dropout");
+  if (B == 0) return TTMI_OK;
+  DropParams dp = make_drop(drop_p, drop_seed);
+  const float scale = 1.f / sqrtf((float)Dh);
+  if (dtype == TTMI_BF16)
+    hipLaunchKernelGGL((mha_q1_fwd_kernel<bf16_t, true>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const bf16_t*)qkv, key_valid, rows, x, x_rows, dp, (bf16_t*)ctx, lse, scale);
+  else
+    hipLaunchKernelGGL((mha_q1_fwd_kernel<float, true>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
+                       (const float*)qkv, key_valid, rows, x, x_rows, dp, (float*)ctx, lse, scale);
+  return ttmi_check_launch("ttmi_mha_q1_gather_fwd");
 }
 
 extern "C" int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,

@@ -211,10 +211,11 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
         if pruned:
             rows = torch.empty(B, device=dev, dtype=torch.int32)
             R, res_in, drows = B, torch.empty(B, D, **f32), rows
-            ops.last_rows_gather(key_valid, x, rows, res_in)
             ctx = torch.empty(B, D, device=dev, dtype=dt)
             lse = torch.empty(B * H, **f32)
-            ops.mha_q1_fwd(qkv, key_valid, rows, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
+            # the last-valid rows, their residual rows and the one-query attention: one launch
+            ops.mha_q1_gather_fwd(qkv, key_valid, x, rows, res_in, B, L, H, ctx, lse,
+                                  _drop(cfg, seeds, site_attn(i)))
             if ops.user_head_fusable(W, P, pre, D, dt):      # the rest of the tower: one launch
                 F_ = W[pre + "linear1.weight"].shape[0]
                 Wc = D + P["gender_embedding.weight"].shape[1] + P["country_embedding.weight"].shape[1]
@@ -353,16 +354,16 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"],
                       grads[pre + "self_attn.in_proj_bias"])
         dxn = torch.empty(M, D, **f32)
-        if fuse:     # in_proj input grad + LN1 backward (+ the layer below's dropout2 backward)
-            emit = drows is None and i > 0
+        if fuse:     # in_proj input grad + LN1 backward (+ the layer below's dropout2 backward);
+            # the pruned layer's residual grad dx1 [B, D] lands on its gathered rows in-kernel
+            emit = i > 0
             nxt = torch.empty(M, D, device=dev, dtype=dt) if emit else None
             ops.linear_ln_bwd(dqkv, W[transposed_name(pre + "self_attn.in_proj_weight")], s.x,
                               s.m1, s.r1, P[pre + "norm1.weight"], dxn,
                               grads[pre + "norm1.weight"], grads[pre + "norm1.bias"],
-                              res=dx1 if drows is None else None, next_=nxt,
+                              res=dx1, res_rows=drows, res_L=L if drows is not None else 0,
+                              next_=nxt,
                               drop=_drop(cfg, seeds, site_drop2(i - 1)) if emit else ops.NO_DROP)
-            if drows is not None:
-                ops.scatter_add_rows(dx1, drows, dxn)      # residual path of the gathered rows
             dy2_next = nxt
         else:
             da1 = torch.empty(M, D, **f32)

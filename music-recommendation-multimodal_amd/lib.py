@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -124,7 +124,8 @@ class LnBwdDesc(ctypes.Structure):
                 ("drop_p", ctypes.c_float), ("drop_seed", ctypes.c_void_p),
                 ("ld_drop", ctypes.c_int64), ("drop_rows", ctypes.c_void_p),
                 ("ln_dw", ctypes.c_void_p), ("ln_db", ctypes.c_void_p),
-                ("sum_ws", ctypes.c_void_p)]
+                ("sum_ws", ctypes.c_void_p),
+                ("res_rows", ctypes.c_void_p), ("res_L", ctypes.c_int64)]
 
 
 class FoldDesc(ctypes.Structure):
@@ -241,6 +242,8 @@ SIGNATURES = {
     "ttmi_gather_rows": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_scatter_add_rows": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_mha_q1_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
+    "ttmi_mha_q1_gather_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p,
+                                     c_p, c_p]),
     "ttmi_mha_q1_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_colsum": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_p, c_p]),
 }

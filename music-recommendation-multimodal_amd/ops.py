@@ -185,9 +185,13 @@ def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
 def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, ln_w: Tensor,
                   dx: Tensor, ln_dw: Optional[Tensor], ln_db: Optional[Tensor], *,
                   res: Optional[Tensor] = None, next_: Optional[Tensor] = None,
-                  drop: Drop = NO_DROP, drop_rows: Optional[Tensor] = None) -> Tensor:
+                  drop: Drop = NO_DROP, drop_rows: Optional[Tensor] = None,
+                  res_rows: Optional[Tensor] = None, res_L: int = 0) -> Tensor:
     """dx = LN'(dh · wtᵀ) + res; ln_dw/ln_db += LN param grads; next_ = bf16(dropout(dx))
-    (one kernel: the Linear input grad, LayerNorm backward and dropout backward)."""
+    (one kernel: the Linear input grad, LayerNorm backward and dropout backward).  res_rows:
+    res is [M / res_L, N] and its row b is added only to row res_rows[b] (b = m / res_L)."""
+    if res_rows is not None and (res is None or res_L <= 0 or res.shape[0] * res_L != dh.shape[0]):
+        raise ValueError("linear_ln_bwd: res_rows needs res [M / res_L, N]")
     _dev(dh, wt, x, dx)
     M, K = dh.shape
     N = wt.shape[0]
@@ -202,6 +206,7 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
     d.next, d.ld_next = _p(next_), (next_.stride(0) if next_ is not None else 0)
     d.drop_p, d.drop_seed, d.ld_drop = float(drop[0]), _p(drop[1]), N
     d.drop_rows = _p(drop_rows)
+    d.res_rows, d.res_L = _p(res_rows), int(res_L)
     d.ln_dw, d.ln_db = _p(ln_dw), _p(ln_db)
     pend = _PENDING[-1] if _PENDING else None
     ws = None
@@ -669,6 +674,19 @@ def mha_q1_fwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, B: int, L: int, H: 
     Dh = qkv.shape[1] // (3 * H)
     call("ttmi_mha_q1_fwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(rows),
          float(drop[0]), _p(drop[1]), _p(ctx), _p(lse), _s())
+    return ctx
+
+
+def mha_q1_gather_fwd(qkv: Tensor, key_valid: Tensor, x: Tensor, rows: Tensor, x_rows: Tensor,
+                      B: int, L: int, H: int, ctx: Tensor, lse: Tensor, drop: Drop = NO_DROP) -> Tensor:
+    """last_rows_gather + mha_q1_fwd in one launch: rows[b] = the last valid row of sequence b
+    (right padding), x_rows[b] = x[rows[b]], ctx[b] = its one-query attention."""
+    _dev(qkv, key_valid, x, rows, x_rows, ctx, lse)
+    D = qkv.shape[1] // 3
+    if x.dtype != torch.float32 or x.shape[1] != D or x_rows.shape != (B, D) or rows.dtype != torch.int32:
+        raise TypeError("mha_q1_gather_fwd: x / x_rows fp32 [*, D], rows int32 [B]")
+    call("ttmi_mha_q1_gather_fwd", code(qkv.dtype), B, L, H, D // H, _p(qkv), _p(key_valid), _p(x),
+         _p(rows), _p(x_rows), float(drop[0]), _p(drop[1]), _p(ctx), _p(lse), _s())
     return ctx
 
 

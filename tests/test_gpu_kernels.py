@@ -429,6 +429,38 @@ def test_last_rows_gather(gpu_pkg, D):
     assert torch.equal(out, x[rows_a.long()])
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,L,H,Dh,p", [(37, 50, 4, 32, 0.1), (8, 64, 2, 64, 0.0), (5, 7, 2, 8, 0.2)])
+def test_mha_q1_gather_fwd(gpu_pkg, dtype, B, L, H, Dh, p):
+    """ttmi_mha_q1_gather_fwd == ttmi_last_rows_gather + ttmi_mha_q1_fwd bit for bit (rows,
+    gathered residual rows, ctx, lse), incl. empty and full histories."""
+    ops = gpu_pkg.ops
+    D = H * Dh
+    g = torch.Generator().manual_seed(B * L + Dh)
+    lens = torch.randint(0, L + 1, (B,), generator=g)
+    lens[0], lens[-1] = 0, L
+    kv = (torch.arange(L)[None] < lens[:, None]).long().to(DEV)
+    qkv = torch.randn(B * L, 3 * D, generator=g).to(dtype).to(DEV)
+    x = torch.randn(B * L, D, generator=g).to(DEV)
+    sd = seed_dev(0xABCD1234)
+    rows_a = torch.empty(B, dtype=torch.int32, device=DEV)
+    xr_a = torch.empty(B, D, device=DEV)
+    ops.last_rows_gather(kv, x, rows_a, xr_a)
+    ctx_a = torch.empty(B, D, device=DEV, dtype=dtype)
+    lse_a = torch.empty(B * H, device=DEV)
+    ops.mha_q1_fwd(qkv, kv, rows_a, B, L, H, ctx_a, lse_a, (p, sd))
+    rows_b = torch.full((B,), -1, dtype=torch.int32, device=DEV)
+    xr_b = torch.empty(B, D, device=DEV)
+    ctx_b = torch.empty(B, D, device=DEV, dtype=dtype)
+    lse_b = torch.empty(B * H, device=DEV)
+    ops.mha_q1_gather_fwd(qkv, kv, x, rows_b, xr_b, B, L, H, ctx_b, lse_b, (p, sd))
+    torch.cuda.synchronize()
+    assert torch.equal(rows_a, rows_b)
+    assert torch.equal(xr_a, xr_b)
+    assert torch.equal(ctx_a, ctx_b)
+    assert torch.equal(lse_a, lse_b)
+
+
 def test_gather_scatter_rows(gpu_pkg):
     ops = gpu_pkg.ops
     x = torch.randn(500, 96, device=DEV)
@@ -909,3 +941,37 @@ def test_wgrad_deferred_fold_many(gpu_pkg):
     torch.cuda.synchronize()
     for (a, b), (c, d) in zip(outs, ref_out):
         assert torch.equal(a, c) and torch.equal(b, d)
+
+
+@pytest.mark.parametrize("B,L,K", [(64, 50, 384), (7, 20, 512)])
+def test_linear_ln_bwd_gathered_residual(gpu_pkg, B, L, K):
+    """res_rows (the pruned layer): res [B, D] row b lands only on row res_rows[b] == the
+    un-gathered residual followed by ttmi_scatter_add_rows; the emitted dropout output
+    (next) is dropout(dx) of the full rows."""
+    ops = gpu_pkg.ops
+    D, M = 128, B * L
+    g = torch.Generator().manual_seed(B + K)
+    dh = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    wt = (torch.randn(D, K, generator=g) / math.sqrt(K)).to(torch.bfloat16).to(DEV)
+    x = (torch.randn(M, D, generator=g) * 2 + 0.5).to(DEV)
+    w = torch.randn(D, generator=g).to(DEV)
+    mean, rstd = x.mean(1), 1.0 / torch.sqrt(x.var(1, unbiased=False) + 1e-5)
+    lens = torch.randint(0, L + 1, (B,), generator=g)
+    rows = (torch.arange(B) * L + (lens - 1).clamp(min=0)).to(torch.int32).to(DEV)
+    res = torch.randn(B, D, generator=g).to(DEV)
+    p, sd = 0.1, seed_dev(0x5151)
+    dx_a = torch.empty(M, D, device=DEV)
+    dw_a, db_a = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ops.linear_ln_bwd(dh, wt, x, mean, rstd, w, dx_a, dw_a, db_a)
+    ops.scatter_add_rows(res, rows, dx_a)
+    nx_a = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    ops.dropout_bwd(dx_a, nx_a, None, (p, sd))
+    dx_b = torch.empty(M, D, device=DEV)
+    dw_b, db_b = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    nx_b = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    ops.linear_ln_bwd(dh, wt, x, mean, rstd, w, dx_b, dw_b, db_b, res=res, res_rows=rows, res_L=L,
+                      next_=nx_b, drop=(p, sd))
+    torch.cuda.synchronize()
+    assert torch.allclose(dx_a, dx_b, rtol=0, atol=1e-6)
+    assert rel(dw_a, dw_b) < 1e-5 and rel(db_a, db_b) < 1e-5   # float atomics (no fold here)
+    assert (nx_a.float() - nx_b.float()).abs().max().item() <= 1e-2 * nx_a.float().abs().max().item()

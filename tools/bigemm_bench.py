@@ -29,7 +29,8 @@ def main():
     M = 65536
     g = torch.Generator(device=dev).manual_seed(0)
     for name, N, K, epi in (("qkv", 2304, 832, "bias"), ("out", 768, 768, "res"),
-                            ("ffn1", 3072, 768, "bias"), ("ffn2", 768, 3072, "res"),
+                            ("ffn1", 3072, 768, "bias"), ("ffn1g", 3072, 768, "gelu"),
+                            ("ffn2", 768, 3072, "res"),
                             ("dpre", 3072, 768, "gelu'"), ("dxn", 768, 2304, "res")):
         A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
@@ -37,6 +38,8 @@ def main():
         kw, C = {}, torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         if epi == "bias":
             kw = dict(bias=bias)
+        elif epi == "gelu":
+            kw = dict(bias=bias, act=2, pre_out=torch.empty(M, N, device=dev, dtype=torch.bfloat16))
         elif epi == "res":
             C = torch.empty(M, N, device=dev)
             kw = dict(bias=bias, residual=torch.randn(M, N, device=dev, generator=g), ld_res=N)
