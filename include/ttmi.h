@@ -559,6 +559,26 @@ int64_t ttmi_dis_attn_pbx_floats(int B, int S, int nh);
  * layer's ttmi_dis_attn_fwd/bwd of that batch reuses it. */
 int ttmi_dis_attn_order(const int64_t* mask, int B, int S, int32_t* order, hipStream_t stream);
 
+/* The item tower's late-fusion MLP forward in training mode (reference item_tower.py:122-129:
+ * Linear(512, 512) -> BatchNorm1d(512) -> ReLU -> Dropout -> Linear(512, D) -> LayerNorm(D),
+ * D = 128) in three launches instead of five (ABI 14): modal16 = bf16(modal) and
+ * z = modal16·W0ᵀ + b0 in one; the BatchNorm + ReLU + dropout of ttmi_batchnorm_fwd (batch
+ * statistics, running stats with momentum, keep index m·512 + n; running_* / num_batches_tracked
+ * may be NULL) into y1 (bf16), bn_mean, bn_rstd; y2 = y1·W4ᵀ + b4 (fp32) and out = LN(y2) with
+ * m5 / r5 in one.  W0 [512, 512], W4 [128, 512] bf16 row-major; ws unused (may be NULL). */
+typedef struct ttmi_item_head_desc {
+  int B, K, N1, D;
+  const float* modal; const void* w0; const float* b0;
+  const float* bn_w; const float* bn_b; float bn_eps; float momentum;
+  float* running_mean; float* running_var; int64_t* num_batches_tracked;
+  float drop_p; const uint64_t* drop_seed;
+  const void* w4; const float* b4; const float* ln_w; const float* ln_b; float ln_eps;
+  void* modal16; float* z; float* bn_mean; float* bn_rstd; void* y1; float* y2;
+  float* out; float* m5; float* r5;
+  float* ws;
+} ttmi_item_head_desc;
+int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t stream);
+
 /* User tower head, one launch (ABI 12; reference user_tower.py:37-57, :131-144) on the B
  * gathered last-valid rows of the pruned last encoder layer (bf16 operands, fp32 math):
  *   x1 = res + drop1(ctx·Woᵀ + bo); a2 = LN2(x1) (m2, r2); h = dropf(relu(a2·W1ᵀ + b1));

@@ -92,7 +92,8 @@ TTMI_DEV void st4_bf(char* p, const float* v) {
 }
 
 // Row sum over the 128 columns held as v[t][e] by the 4 lanes of row li in each of 4 waves.
-TTMI_DEV float row_sum(float s, HeadLds& L, int w, int lane) {
+template <class LDS>
+TTMI_DEV float row_sum(float s, LDS& L, int w, int lane) {
   s += __shfl_xor(s, 16, 64);
   s += __shfl_xor(s, 32, 64);
   if (lane < 16) L.red[w][lane] = s;
@@ -103,8 +104,9 @@ TTMI_DEV float row_sum(float s, HeadLds& L, int w, int lane) {
   return tot;
 }
 // LayerNorm of the row values v (2 tiles x 4 per lane); returns mean / rstd.
+template <class LDS>
 TTMI_DEV void row_ln(f32x4_t (&v)[2], const float* w_, const float* b_, float eps, bool relu,
-                     int n0, HeadLds& L, int w, int lane, float& mu, float& rs) {
+                     int n0, LDS& L, int w, int lane, float& mu, float& rs) {
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -633,7 +635,152 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
 #endif
 }
 
+// ------------------------------------------------------------------------------ item head
+// The item tower's late-fusion MLP (reference item_tower.py:122-129) in three launches instead
+// of five (cast, Linear, BatchNorm+ReLU+dropout, Linear, LayerNorm):
+//   A: m = bf16(modal); z = m·W0ᵀ + b0 (16 rows x 64 columns per workgroup);
+//   BatchNorm + ReLU + dropout: bnr_fwd_kernel (ttmi_norm.hip), unchanged — the batch
+//      statistics are a reduction over all rows, column-blocked;
+//   C: y2 = y1·W4ᵀ + b4; out = LN(y2) (16 rows per workgroup, y1 rows in LDS).
+// Saved for the backward exactly as the unfused ops wrote them: m, z, BN mean / rstd, y1, y2,
+// the LayerNorm mean / rstd.
+constexpr int IK = 512;                // modal width (4 x 128) = Linear 0 fan-in
+constexpr int IN1 = 512;               // Linear 0 width (BatchNorm channels)
+constexpr int PI = (IK + 8) * 2;       // LDS pitch of a bf16 row of 512
+
+struct ItemArgs {
+  int B;
+  const float* modal; const bf16_t* w0; const float* b0;
+  const bf16_t* y1; const bf16_t* w4; const float* b4; const float* lnw; const float* lnb; float ln_eps;
+  bf16_t* m16; float* z; float* y2; float* out; float* m5; float* r5;
+};
+
+struct ItemLdsA {
+  char sA[HR * PI];
+};
+
+__global__ __launch_bounds__(256) void item_head_a_kernel(ItemArgs a) {
+  __shared__ __attribute__((aligned(16))) ItemLdsA L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * HR, q = blockIdx.y;
+  const int n0 = 64 * q + 16 * w;                    // this wave's 16 of the 512 columns
+  WFrags<1, IK> wf;
+  wf.load(a.w0, IK, n0, lane, IK);
+  const float4 bias = *reinterpret_cast<const float4*>(a.b0 + n0 + 4 * g);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {                      // 16 rows x 128 float4 of modal -> bf16
+    const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+    const int rr = min(r0 + r, a.B - 1);
+    const float4 v = *reinterpret_cast<const float4*>(a.modal + (int64_t)rr * IK + 4 * c4);
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    st4_bf(L.sA + r * PI + c4 * 8, x);
+    if (q == 0 && r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.m16 + (int64_t)(r0 + r) * IK + 4 * c4), x);
+  }
+  __syncthreads();
+  f32x4_t v[1];
+  head_gemm<1, IK, PI>(L.sA, wf, v, lane);
+  const int m = r0 + li;
+  if (m < a.B)
+    *reinterpret_cast<float4*>(a.z + (int64_t)m * IN1 + n0 + 4 * g) =
+        make_float4(v[0][0] + bias.x, v[0][1] + bias.y, v[0][2] + bias.z, v[0][3] + bias.w);
+}
+
+struct ItemLdsC {
+  char sY[HR * PI];
+  float red[4][HR];
+};
+
+__global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
+  __shared__ __attribute__((aligned(16))) ItemLdsC L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * HR;
+  const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
+  {                                                  // y1 rows: 16 x 64 chunks of 16 bytes
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = tid + 256 * k, r = idx >> 6, ch = idx & 63;
+      *reinterpret_cast<uint4*>(L.sY + r * PI + ch * 16) =
+          *reinterpret_cast<const uint4*>(a.y1 + (int64_t)min(r0 + r, a.B - 1) * IN1 + ch * 8);
+    }
+  }
+  WFrags<2, IN1> wf;
+  wf.load(a.w4, IN1, n0, lane, IN1);
+  float b4[2][4], lw[2][4], lb[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float4 b = *reinterpret_cast<const float4*>(a.b4 + n);
+    const float4 x = *reinterpret_cast<const float4*>(a.lnw + n);
+    const float4 y = *reinterpret_cast<const float4*>(a.lnb + n);
+    b4[t][0] = b.x; b4[t][1] = b.y; b4[t][2] = b.z; b4[t][3] = b.w;
+    lw[t][0] = x.x; lw[t][1] = x.y; lw[t][2] = x.z; lw[t][3] = x.w;
+    lb[t][0] = y.x; lb[t][1] = y.y; lb[t][2] = y.z; lb[t][3] = y.w;
+  }
+  __syncthreads();
+  f32x4_t v[2];
+  head_gemm<2, IN1, PI>(L.sY, wf, v, lane);
+  const int m = r0 + li;
+  const bool mrow = m < a.B;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[t][e] += b4[t][e];
+    if (mrow) *reinterpret_cast<float4*>(a.y2 + (int64_t)m * HD + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
+  }
+  // LayerNorm over the 128 columns (the 4 waves' 32 each), two-pass like ttmi_layernorm_fwd
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[t][e];
+  const float mu = row_sum(s, L, w, lane) * (1.f / HD);
+  float qv = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[t][e] - mu;
+      qv += d * d;
+    }
+  const float rs = 1.f / sqrtf(row_sum(qv, L, w, lane) * (1.f / HD) + a.ln_eps);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[t][e] - mu) * rs * lw[t][e] + lb[t][e];
+    if (mrow) *reinterpret_cast<float4*>(a.out + (int64_t)m * HD + n) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  if (mrow && lane < 16 && w == 0) { a.m5[m] = mu; a.r5[m] = rs; }
+}
+
 }  // namespace
+
+extern "C" int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t s) {
+  TTMI_REQUIRE(d != nullptr, "ttmi_item_head_fwd: null descriptor");
+  TTMI_REQUIRE(d->B > 1 && d->K == IK && d->N1 == IN1 && d->D == HD,
+               "ttmi_item_head_fwd: needs B > 1 (training BatchNorm), K == N1 == %d, D == %d", IK, HD);
+  TTMI_REQUIRE(d->modal && d->w0 && d->b0 && d->bn_w && d->bn_b && d->w4 && d->b4 && d->ln_w && d->ln_b &&
+               d->modal16 && d->z && d->bn_mean && d->bn_rstd && d->y1 && d->y2 && d->out && d->m5 &&
+               d->r5, "ttmi_item_head_fwd: null argument");
+  ItemArgs a{};
+  a.B = d->B;
+  a.modal = d->modal; a.w0 = (const bf16_t*)d->w0; a.b0 = d->b0;
+  a.y1 = (const bf16_t*)d->y1; a.w4 = (const bf16_t*)d->w4; a.b4 = d->b4;
+  a.lnw = d->ln_w; a.lnb = d->ln_b; a.ln_eps = d->ln_eps;
+  a.m16 = (bf16_t*)d->modal16; a.z = d->z; a.y2 = d->y2; a.out = d->out; a.m5 = d->m5; a.r5 = d->r5;
+  const unsigned nblk = (unsigned)((d->B + HR - 1) / HR);
+  hipLaunchKernelGGL(item_head_a_kernel, dim3(nblk, IN1 / 64), dim3(256), 0, s, a);
+  int rc = ttmi_check_launch("ttmi_item_head_fwd");
+  if (rc != TTMI_OK) return rc;
+  rc = ttmi_batchnorm_fwd(TTMI_BF16, d->B, IN1, d->z, d->bn_w, d->bn_b, d->bn_eps, d->momentum,
+                          d->running_mean, d->running_var, d->num_batches_tracked, 1, 1, d->drop_p,
+                          d->drop_seed, d->y1, d->bn_mean, d->bn_rstd, s);
+  if (rc != TTMI_OK) return rc;
+  hipLaunchKernelGGL(item_head_c_kernel, dim3(nblk), dim3(256), 0, s, a);
+  return ttmi_check_launch("ttmi_item_head_fwd");
+}
 
 extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_fwd: null descriptor");

@@ -482,6 +482,18 @@ def item_fusion_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Tensor, c
     B = modal.shape[0]
     dt = cfg.dtype
     f32 = dict(device=dev, dtype=torch.float32)
+    bufs = buffers or {}
+    if training and ops.item_head_fusable(W, modal, dt):
+        # the whole MLP in three launches (cast + Linear; BatchNorm + ReLU + dropout; Linear +
+        # LayerNorm), saving what the unfused ops below save
+        H1, D = W["fusion_layer.0.weight"].shape[0], W["fusion_layer.4.weight"].shape[0]
+        o = dict(m16=torch.empty(modal.shape, device=dev, dtype=dt), z=torch.empty(B, H1, **f32),
+                 bn_mean=torch.empty(H1, **f32), bn_rstd=torch.empty(H1, **f32),
+                 y1=torch.empty(B, H1, device=dev, dtype=dt), y2=torch.empty(B, D, **f32),
+                 out=torch.empty(B, D, **f32), m5=torch.empty(B, **f32), r5=torch.empty(B, **f32))
+        ops.item_head_fwd(modal.contiguous(), W, P, bufs, _drop(cfg, seeds, SITE_ITEM, p_drop), cfg.eps, o)
+        return o["out"], ItemSaved(o["m16"], o["z"], o["bn_mean"], o["bn_rstd"], o["y1"], o["y2"],
+                                   o["m5"], o["r5"], seeds)
     if dt == torch.float32:
         m_c = modal.contiguous()
     else:
@@ -492,7 +504,6 @@ def item_fusion_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Tensor, c
     y1 = torch.empty(B, H1, device=dev, dtype=dt)
     bn_mean = torch.empty(H1, **f32)
     bn_rstd = torch.empty(H1, **f32)
-    bufs = buffers or {}
     ops.batchnorm_fwd(z, P["fusion_layer.1.weight"], P["fusion_layer.1.bias"], y1, bn_mean, bn_rstd,
                       bufs.get("fusion_layer.1.running_mean"), bufs.get("fusion_layer.1.running_var"),
                       bufs.get("fusion_layer.1.num_batches_tracked"), relu=True,

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -76,6 +76,18 @@ class DisAttnDesc(ctypes.Structure):
                 ("dq", c_p), ("dk", c_p), ("dv", c_p), ("lddqkv", ctypes.c_int64),
                 ("lora_u", c_p), ("lora_bq", c_p), ("lora_hu", c_p), ("lora_pb", c_p),
                 ("dq_scratch", c_p), ("lora_pbx", c_p), ("order", c_p)]
+
+
+class ItemHeadDesc(ctypes.Structure):
+    """ttmi_item_head_desc (include/ttmi.h, ABI 14)."""
+    _fields_ = [("B", c_i), ("K", c_i), ("N1", c_i), ("D", c_i),
+                ("modal", c_p), ("w0", c_p), ("b0", c_p),
+                ("bn_w", c_p), ("bn_b", c_p), ("bn_eps", ctypes.c_float), ("momentum", ctypes.c_float),
+                ("running_mean", c_p), ("running_var", c_p), ("num_batches_tracked", c_p),
+                ("drop_p", ctypes.c_float), ("drop_seed", c_p),
+                ("w4", c_p), ("b4", c_p), ("ln_w", c_p), ("ln_b", c_p), ("ln_eps", ctypes.c_float),
+                ("modal16", c_p), ("z", c_p), ("bn_mean", c_p), ("bn_rstd", c_p), ("y1", c_p), ("y2", c_p),
+                ("out", c_p), ("m5", c_p), ("r5", c_p), ("ws", c_p)]
 
 
 class UserHeadDesc(ctypes.Structure):
@@ -205,6 +217,7 @@ SIGNATURES = {
     "ttmi_user_head_fwd": (c_i, [c_p, c_p]),
     "ttmi_user_head_bwd": (c_i, [c_p, c_p]),
     "ttmi_user_head_bwd_ws_floats": (ctypes.c_int64, [c_i]),
+    "ttmi_item_head_fwd": (c_i, [c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,

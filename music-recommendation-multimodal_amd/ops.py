@@ -14,7 +14,7 @@ import torch
 
 from . import lib as _L
 from .lib import (BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, UserHeadBwdDesc,
-                  UserHeadDesc, WgradDesc, call)
+                  UserHeadDesc, ItemHeadDesc, WgradDesc, call)
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -526,6 +526,40 @@ def batchnorm_fwd(z: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd
          float(drop[0]),
          _p(drop[1]), _p(y), _p(mean), _p(rstd), _s())
     return y
+
+
+def item_head_fwd(modal: Tensor, W: Dict[str, Tensor], P: Dict[str, Tensor],
+                  bufs: Dict[str, Optional[Tensor]], drop: Drop, eps: float, out: Dict[str, Tensor],
+                  momentum: float = 0.1) -> Dict[str, Tensor]:
+    """The item late-fusion MLP forward in training mode in three launches (ttmi_item_head_fwd):
+    fills out's m16, z, bn_mean, bn_rstd, y1, y2, out, m5, r5 exactly as cast_bf16 + linear +
+    batchnorm_fwd(relu, dropout) + linear + layernorm_fwd write them."""
+    B = modal.shape[0]
+    _dev(modal, *out.values())
+    d = ItemHeadDesc()
+    d.B, d.K, d.N1, d.D = B, modal.shape[1], W["fusion_layer.0.weight"].shape[0], W["fusion_layer.4.weight"].shape[0]
+    d.modal, d.w0, d.b0 = _p(modal), _p(W["fusion_layer.0.weight"]), _p(P["fusion_layer.0.bias"])
+    d.bn_w, d.bn_b = _p(P["fusion_layer.1.weight"]), _p(P["fusion_layer.1.bias"])
+    d.bn_eps, d.momentum = 1e-5, momentum
+    d.running_mean = _p(bufs.get("fusion_layer.1.running_mean"))
+    d.running_var = _p(bufs.get("fusion_layer.1.running_var"))
+    d.num_batches_tracked = _p(bufs.get("fusion_layer.1.num_batches_tracked"))
+    d.drop_p, d.drop_seed = float(drop[0]), _p(drop[1])
+    d.w4, d.b4 = _p(W["fusion_layer.4.weight"]), _p(P["fusion_layer.4.bias"])
+    d.ln_w, d.ln_b, d.ln_eps = _p(P["fusion_layer.5.weight"]), _p(P["fusion_layer.5.bias"]), eps
+    d.modal16, d.z, d.bn_mean, d.bn_rstd = _p(out["m16"]), _p(out["z"]), _p(out["bn_mean"]), _p(out["bn_rstd"])
+    d.y1, d.y2, d.out, d.m5, d.r5 = _p(out["y1"]), _p(out["y2"]), _p(out["out"]), _p(out["m5"]), _p(out["r5"])
+    d.ws = None
+    call("ttmi_item_head_fwd", ctypes.byref(d), _s())
+    return out
+
+
+def item_head_fusable(W: Dict[str, Tensor], modal: Tensor, dtype) -> bool:
+    """Shapes ttmi_item_head_fwd takes (include/ttmi.h): bf16, 512 -> 512 -> BN -> 128."""
+    w0, w4 = W["fusion_layer.0.weight"], W["fusion_layer.4.weight"]
+    return (dtype == torch.bfloat16 and modal.dim() == 2 and modal.shape[0] > 1 and
+            modal.shape[1] == 512 and modal.dtype == torch.float32 and tuple(w0.shape) == (512, 512) and
+            tuple(w4.shape) == (128, 512) and w0.dtype == torch.bfloat16 and w4.dtype == torch.bfloat16)
 
 
 def batchnorm_bwd(dy: Tensor, z: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, y: Tensor,

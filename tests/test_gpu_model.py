@@ -578,6 +578,64 @@ def test_user_head_fused_matches_ops(gpu_pkg, B, p):
             assert (zo != zw).float().mean().item() < 1e-3
 
 
+@pytest.mark.parametrize("B,p", [(512, 0.1), (300, 0.0), (37, 0.1), (2, 0.0)])
+def test_item_head_fused_matches_ops(gpu_pkg, B, p):
+    """ttmi_item_head_fwd (the item late-fusion MLP in three launches) against the unfused op
+    sequence of functional.item_fusion_fwd (cast, Linear, BatchNorm+ReLU+dropout, Linear,
+    LayerNorm): every saved tensor, the BatchNorm batch statistics and the running buffers."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(B + 5)
+
+    def bf(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+    def f32(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(DEV)
+    W = {"fusion_layer.0.weight": bf(512, 512, scale=512 ** -0.5),
+         "fusion_layer.4.weight": bf(128, 512, scale=512 ** -0.5)}
+    P = {"fusion_layer.0.bias": f32(512, scale=0.1), "fusion_layer.1.weight": 1 + f32(512, scale=0.1),
+         "fusion_layer.1.bias": f32(512, scale=0.1), "fusion_layer.4.bias": f32(128, scale=0.1),
+         "fusion_layer.5.weight": 1 + f32(128, scale=0.1), "fusion_layer.5.bias": f32(128, scale=0.1)}
+    modal = f32(B, 512) * 2 + 0.3
+    seeds = torch.tensor([0x1234567], dtype=torch.int64, device=DEV)
+    drop = (p, seeds[0:1]) if p > 0 else ops.NO_DROP
+
+    def bufs():
+        return {"fusion_layer.1.running_mean": torch.full((512,), 0.2, device=DEV),
+                "fusion_layer.1.running_var": torch.full((512,), 1.5, device=DEV),
+                "fusion_layer.1.num_batches_tracked": torch.full((), 3, dtype=torch.int64, device=DEV)}
+    assert ops.item_head_fusable(W, modal, torch.bfloat16)
+    # unfused reference sequence
+    bw = bufs()
+    m16 = ops.cast_bf16(modal, torch.empty(B, 512, device=DEV, dtype=torch.bfloat16))
+    z = torch.empty(B, 512, device=DEV)
+    ops.linear(m16, W["fusion_layer.0.weight"], P["fusion_layer.0.bias"], z)
+    y1 = torch.empty(B, 512, device=DEV, dtype=torch.bfloat16)
+    bm, br = torch.empty(512, device=DEV), torch.empty(512, device=DEV)
+    ops.batchnorm_fwd(z, P["fusion_layer.1.weight"], P["fusion_layer.1.bias"], y1, bm, br,
+                      bw["fusion_layer.1.running_mean"], bw["fusion_layer.1.running_var"],
+                      bw["fusion_layer.1.num_batches_tracked"], relu=True, drop=drop, training=True)
+    y2 = torch.empty(B, 128, device=DEV)
+    ops.linear(y1, W["fusion_layer.4.weight"], P["fusion_layer.4.bias"], y2)
+    out = torch.empty(B, 128, device=DEV)
+    m5, r5 = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    ops.layernorm_fwd(y2, P["fusion_layer.5.weight"], P["fusion_layer.5.bias"], out, m5, r5, eps=1e-5)
+    want = dict(m16=m16, z=z, bn_mean=bm, bn_rstd=br, y1=y1, y2=y2, out=out, m5=m5, r5=r5)
+    got = {k: torch.full_like(v, 7) for k, v in want.items()}
+    bf_ = bufs()
+    ops.item_head_fwd(modal, W, P, bf_, drop, 1e-5, got)
+    torch.cuda.synchronize()
+    assert torch.equal(got["m16"], want["m16"])
+    for k in ("z", "bn_mean", "bn_rstd", "y2", "out", "m5", "r5"):
+        assert rel(got[k], want[k]) < (1e-5 if k == "z" else 1e-4 if k in ("bn_mean", "bn_rstd") else 2e-3), k
+    assert rel(got["y1"].float(), want["y1"].float()) < 1e-2
+    if p > 0:     # same dropout mask (zeros agree except where a kept value rounds to zero)
+        assert ((got["y1"] == 0) != (want["y1"] == 0)).float().mean().item() < 1e-3
+    for k in ("fusion_layer.1.running_mean", "fusion_layer.1.running_var"):
+        assert rel(bf_[k], bw[k]) < 1e-5, k
+    assert int(bf_["fusion_layer.1.num_batches_tracked"]) == 4
+
+
 @pytest.mark.parametrize("B,p", [(512, 0.1), (37, 0.0)])
 def test_user_head_bwd_fused_matches_ops(gpu_pkg, B, p):
     """ttmi_user_head_bwd against the unfused backward ops it replaces (functional's
