@@ -403,8 +403,14 @@ __global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl, 
   const uint16_t* src = tl.src[i];
   uint16_t* dst = tl.dst[i];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < 64; r += 4)
-    if (r0 + r < R && c0 + tx < C) t[r][tx] = src[(int64_t)(r0 + r) * C + c0 + tx];
+  // all 16 loads first, from clamped addresses (a guarded load is a branch + vmcnt(0) each:
+  // 16 round trips in a row); elements past the edge are never stored
+  uint16_t v[16];
+  const int cc = min(c0 + tx, C - 1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = src[(int64_t)min(r0 + ty + 4 * k, R - 1) * C + cc];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t[ty + 4 * k][tx] = v[k];
   __syncthreads();
   for (int c = ty; c < 64; c += 4)
     if (c0 + c < C && r0 + tx < R) dst[(int64_t)(c0 + c) * R + r0 + tx] = t[tx][c];
