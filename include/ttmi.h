@@ -109,7 +109,9 @@ typedef struct {
 } ttmi_wgrad_desc;
 int64_t ttmi_wgrad_workspace(int64_t R, int64_t M, int64_t N, int64_t ld_dy, int64_t ld_x);
 int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream);
-/* Generic split fold: C[m*ldc + n] (+)= Σ_{s < S, in order} part[s*s_stride + m*N + n]. */
+/* Generic split fold: C[m*ldc + n] (+)= Σ_{s < S, in order} part[s*s_stride + m*N + n].
+ * accumulate: bit 0 = add to C (else overwrite); bit 1 (ABI 15) = zero the partials read
+ * (a workspace that must be zero on the next use, e.g. ttmi_seq_embed_bwd's). */
 typedef struct {
   const float* part; int64_t S, s_stride, M, N;
   float* C; int64_t ldc;
@@ -167,7 +169,10 @@ int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, 
 /* Backward: dE[ids] += g (rows with ids == padding_idx skipped, nn.Embedding(padding_idx=0)
  * user_tower.py:27), dP[l] += Σ_b g, dw/db += LN affine grads.  All accumulate (fp32).
  * ws: ttmi_seq_embed_bwd_workspace(L, D) bytes, zero on entry and left zero on return (the
- * per-position LN-grad partials; one buffer may serve every call on one stream). */
+ * per-position LN-grad partials; one buffer may serve every call on one stream).  With
+ * dw = db = NULL (ABI 15) the per-position partials ws[l][0..D) (weight) and ws[l][D..2D)
+ * (bias) stay in ws for the caller to fold (ttmi_fold_desc, S = L, s_stride = 2D,
+ * accumulate = 3: added, and ws left zero) with its deferred weight gradients. */
 int64_t ttmi_seq_embed_bwd_workspace(int L, int D);
 int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const float* E,
                        const float* P, const float* w, const float* mean, const float* rstd,
@@ -626,6 +631,35 @@ typedef struct ttmi_user_head_bwd_desc {
 } ttmi_user_head_bwd_desc;
 int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t stream);
 int64_t ttmi_user_head_bwd_ws_floats(int B);
+
+/* Co-launched heads (ABI 15).  The user head kernels occupy one workgroup per 16 rows (32 of
+ * 256 CUs at B = 512); the item tower's row-local head work is independent of them, so it
+ * rides in the same launch on the idle CUs (workgroups past the user head's):
+ *  - ttmi_item_head_fwd_stages: ttmi_item_head_fwd split by stage mask 1 = A (cast +
+ *    Linear 0), 2 = BatchNorm + ReLU + dropout, 4 = C (Linear 4 + LayerNorm), in that order;
+ *    ttmi_item_head_fwd == stages 7.
+ *  - ttmi_user_item_head_fwd: ttmi_user_head_fwd plus item stage A of `it` (NULL: user head
+ *    only).  Stages 2 | 4 must follow.
+ *  - ttmi_item_head_bwd_c: the item head backward's row-local part (replaces the
+ *    ttmi_layernorm_bwd + Linear-4 input-grad launches of item_tower.py:122-129 under
+ *    autograd): dy2 = LayerNorm(fusion_layer.5) backward of dout (bf16 [B, D] out), dy1 =
+ *    dy2·W4 (fp32 [B, N1]; w4t = W4ᵀ [N1, D] bf16); ws [ttmi_item_head_bwd_ws_floats(B)]
+ *    receives per-16-row-block column sums of the LN weight / bias gradients ([nblk][2][D]).
+ *  - ttmi_user_item_head_bwd: ttmi_user_head_bwd plus ttmi_item_head_bwd_c of `it` (NULL:
+ *    user head only).  D == 128, N1 == 512. */
+typedef struct ttmi_item_head_bwd_desc {
+  int B, D, N1;
+  const float* dout; const float* y2; const float* m5; const float* r5; const float* ln_w;
+  const void* w4t;
+  void* dy2; float* dy1; float* ws;
+} ttmi_item_head_bwd_desc;
+int ttmi_item_head_fwd_stages(const ttmi_item_head_desc* d, int stages, hipStream_t stream);
+int ttmi_user_item_head_fwd(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
+                            hipStream_t stream);
+int ttmi_item_head_bwd_c(const ttmi_item_head_bwd_desc* d, hipStream_t stream);
+int64_t ttmi_item_head_bwd_ws_floats(int B);
+int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const ttmi_item_head_bwd_desc* it,
+                            hipStream_t stream);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
 int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
 /* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);

@@ -1130,7 +1130,7 @@ int64_t wgrad_ws_bytes(const WgradPlan& p, int64_t M, int64_t N) {
   return al256((int64_t)p.S * M * N * 4) + al256((int64_t)p.S * M * 4);
 }
 
-constexpr int FOLD_SEGS = 16;
+constexpr int FOLD_SEGS = 32;   // kernarg: 32 x 88 B (a cfg-2 step folds ~20 segments)
 struct FoldSeg {
   const float* part; const float* part_rs; float* C; float* rs;
   int64_t M, N, ldc, units, base, s_stride;   // s_stride: elements between split slabs
@@ -1168,6 +1168,12 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
         for (int j = 0; j < 16; ++j)
           w[j] = s0 + j < s_hi ? *reinterpret_cast<const float4*>(p + (s0 + j) * stride)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (sg.acc & 2) {                            // consume: leave the partials zero
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (s0 + j < s_hi)
+              *reinterpret_cast<float4*>(const_cast<float*>(p) + (s0 + j) * stride) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
 #pragma unroll
         for (int j = 0; j < 16; ++j)
           if (s0 + j < s_hi) { v.x += w[j].x; v.y += w[j].y; v.z += w[j].z; v.w += w[j].w; }
@@ -1194,14 +1200,14 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
       if (u < nel) {
         const int64_t m = u / nq, n = (u % nq) * 4;
         float4* cp = reinterpret_cast<float4*>(sg.C + m * sg.ldc + n);
-        if (sg.acc) {
+        if (sg.acc & 1) {
           const float4 c = *cp;
           v.x = c.x + v.x; v.y = c.y + v.y; v.z = c.z + v.z; v.w = c.w + v.w;
         }
         *cp = v;
       } else {
         const int64_t m = u - nel;
-        sg.rs[m] = sg.acc ? sg.rs[m] + v.x : v.x;
+        sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v.x : v.x;
       }
     }
     __syncthreads();

@@ -23,6 +23,30 @@ constexpr int PD = (HD + 8) * 2;       // LDS pitches (bytes) of the bf16 row im
 constexpr int PF = (FMAX + 8) * 2;
 constexpr int PW = (WPAD + 8) * 2;
 
+constexpr int IK = 512;                // modal width (4 x 128) = Linear 0 fan-in
+constexpr int IN1 = 512;               // Linear 0 width (BatchNorm channels)
+constexpr int PI = (IK + 8) * 2;       // LDS pitch of a bf16 row of 512
+
+struct ItemArgs {
+  int B;
+  const float* modal; const bf16_t* w0; const float* b0;
+  const bf16_t* y1; const bf16_t* w4; const float* b4; const float* lnw; const float* lnb; float ln_eps;
+  bf16_t* m16; float* z; float* y2; float* out; float* m5; float* r5;
+};
+
+struct ItemLdsA {
+  char sA[HR * PI];
+};
+
+// Item head backward's row-local part (ttmi_item_head_bwd_c): the LayerNorm backward of
+// fusion_layer.5 and the input gradient of fusion_layer.4 on 16 rows per workgroup.
+struct ItemBwdArgs {
+  int B;
+  const float* dout; const float* y2; const float* m5; const float* r5; const float* lnw;
+  const bf16_t* w4t;
+  bf16_t* dy2; float* dy1; float* ws;
+};
+
 struct HeadArgs {
   int B, F, dg, dc;
   float eps;
@@ -35,6 +59,9 @@ struct HeadArgs {
   DropParams d1, dff, d2;
   float* x1; bf16_t* a2; float* m2; float* r2; bf16_t* h; bf16_t* comb; int32_t* rows;
   float* z; bf16_t* az; float* mz; float* rz; float* u;
+  // co-launched item head stage A (ttmi_user_item_head_fwd): workgroups >= nbu run
+  // item_a_body on row block (l % it_nblk), column quarter (l / it_nblk)
+  ItemArgs it; int nbu, it_nblk;
 };
 
 struct HeadLds {
@@ -149,6 +176,33 @@ TTMI_DEV void vec_st(float* dst, const float4& v, int tid) {
   reinterpret_cast<float4*>(dst)[tid & (N / 4 - 1)] = v;
 }
 
+// Item head stage A on row block bx, column quarter q (item_head_a_kernel, or the workgroups
+// of ttmi_user_item_head_fwd past the user head's).
+TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = bx * HR;
+  const int n0 = 64 * q + 16 * w;                    // this wave's 16 of the 512 columns
+  WFrags<1, IK> wf;
+  wf.load(a.w0, IK, n0, lane, IK);
+  const float4 bias = *reinterpret_cast<const float4*>(a.b0 + n0 + 4 * g);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {                      // 16 rows x 128 float4 of modal -> bf16
+    const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+    const int rr = min(r0 + r, a.B - 1);
+    const float4 v = *reinterpret_cast<const float4*>(a.modal + (int64_t)rr * IK + 4 * c4);
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    st4_bf(L.sA + r * PI + c4 * 8, x);
+    if (q == 0 && r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.m16 + (int64_t)(r0 + r) * IK + 4 * c4), x);
+  }
+  __syncthreads();
+  f32x4_t v[1];
+  head_gemm<1, IK, PI>(L.sA, wf, v, lane);
+  const int m = r0 + li;
+  if (m < a.B)
+    *reinterpret_cast<float4*>(a.z + (int64_t)m * IN1 + n0 + 4 * g) =
+        make_float4(v[0][0] + bias.x, v[0][1] + bias.y, v[0][2] + bias.z, v[0][3] + bias.w);
+}
+
 #ifdef HEAD_STAMP
 #define STAMP(i) do { if (threadIdx.x == 0) stamp[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
@@ -167,6 +221,12 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
   STAMP(0);
   __shared__ __attribute__((aligned(16))) HeadLds L;
   __shared__ __attribute__((aligned(16))) HeadParams Q;
+  static_assert(sizeof(HeadLds) >= sizeof(ItemLdsA), "item stage A reuses the head's LDS");
+  if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head stage A
+    const int l = (int)blockIdx.x - a.nbu;
+    item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = blockIdx.x * HR, m = r0 + li;
   const bool mrow = m < a.B;
@@ -367,6 +427,7 @@ struct HeadBwdArgs {
   DropParams d1, d2;
   float* dG; float* dC;
   bf16_t* dz16; bf16_t* dy2; bf16_t* dz1; float* dx1; bf16_t* dy1; bf16_t* dctx; float* ws;
+  ItemBwdArgs it; int nbu;     // co-launched item head backward: workgroups >= nbu
 };
 
 struct HeadBwdLds {
@@ -429,6 +490,57 @@ TTMI_DEV void ln_bwd16(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, floa
     for (int e = 0; e < 4; ++e) dy[t][e] = rs * (gg[t][e] - c1 - xh[t][e] * c2);
 }
 
+// Item head backward, row-local part (ABI 15; reference item_tower.py:122-129 under autograd),
+// on 16 rows: dy2 = backward of LayerNorm fusion_layer.5 (stored mean / rstd), written bf16
+// (the fusion_layer.4 weight-gradient operand) and kept in LDS; dy1 = dy2·W4 (fp32, the
+// BatchNorm backward's input) from W4ᵀ fragments.  The LN weight / bias gradient terms leave
+// as this block's column sums (ws rows 2·bx, 2·bx + 1), folded later in block order.
+TTMI_DEV void item_c_bwd_body(const ItemBwdArgs& a, int bx, HeadBwdLds& L) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = bx * HR, m = r0 + li, mc = min(m, a.B - 1);
+  const bool mrow = m < a.B;
+  const int n0 = 32 * w;                             // LN: this wave's 32 of the 128 columns
+  const int nn0 = 128 * w;                           // dy1: this wave's 128 of the 512 columns
+  float xs[2][4], wv[2][4];
+  f32x4_t dy[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float4 d = *reinterpret_cast<const float4*>(a.dout + (int64_t)mc * HD + n);
+    const float4 x = *reinterpret_cast<const float4*>(a.y2 + (int64_t)mc * HD + n);
+    const float4 v = *reinterpret_cast<const float4*>(a.lnw + n);
+    dy[t] = f32x4_t{d.x, d.y, d.z, d.w};
+    xs[t][0] = x.x; xs[t][1] = x.y; xs[t][2] = x.z; xs[t][3] = x.w;
+    wv[t][0] = v.x; wv[t][1] = v.y; wv[t][2] = v.z; wv[t][3] = v.w;
+  }
+  const float mu = a.m5[mc], rs = a.r5[mc];
+  WFrags<8, HD> wf;                                  // W4ᵀ [512, 128]: the wave's 8 column tiles
+  wf.load(a.w4t, HD, nn0, lane, HD);
+  float* wsr = a.ws + (int64_t)bx * 2 * HD;
+  ln_bwd16(dy, xs, mu, rs, wv, n0, mrow, L, w, lane, wsr, wsr + HD);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float o[4] = {dy[t][0], dy[t][1], dy[t][2], dy[t][3]};
+    st4_bf(L.sA + li * PD + n * 2, o);
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dy2 + (int64_t)m * HD + n), o);
+  }
+  __syncthreads();
+  f32x4_t acc[8];
+  head_gemm<8, HD, PD>(L.sA, wf, acc, lane);
+  if (mrow) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      *reinterpret_cast<float4*>(a.dy1 + (int64_t)m * IN1 + nn0 + 16 * t + 4 * g) =
+          make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void item_head_bwd_c_kernel(ItemBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) HeadBwdLds L;
+  item_c_bwd_body(a, blockIdx.x, L);
+}
+
 template <int F>
 __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
 #ifdef HEAD_STAMP
@@ -436,6 +548,10 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
 #endif
   STAMP(0);
   __shared__ __attribute__((aligned(16))) HeadBwdLds L;
+  if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head backward (rows)
+    item_c_bwd_body(a.it, (int)blockIdx.x - a.nbu, L);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = blockIdx.x * HR, m = r0 + li, mc = min(m, a.B - 1);
   const bool mrow = m < a.B;
@@ -644,45 +760,9 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
 //   C: y2 = y1·W4ᵀ + b4; out = LN(y2) (16 rows per workgroup, y1 rows in LDS).
 // Saved for the backward exactly as the unfused ops wrote them: m, z, BN mean / rstd, y1, y2,
 // the LayerNorm mean / rstd.
-constexpr int IK = 512;                // modal width (4 x 128) = Linear 0 fan-in
-constexpr int IN1 = 512;               // Linear 0 width (BatchNorm channels)
-constexpr int PI = (IK + 8) * 2;       // LDS pitch of a bf16 row of 512
-
-struct ItemArgs {
-  int B;
-  const float* modal; const bf16_t* w0; const float* b0;
-  const bf16_t* y1; const bf16_t* w4; const float* b4; const float* lnw; const float* lnb; float ln_eps;
-  bf16_t* m16; float* z; float* y2; float* out; float* m5; float* r5;
-};
-
-struct ItemLdsA {
-  char sA[HR * PI];
-};
-
 __global__ __launch_bounds__(256) void item_head_a_kernel(ItemArgs a) {
   __shared__ __attribute__((aligned(16))) ItemLdsA L;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
-  const int r0 = blockIdx.x * HR, q = blockIdx.y;
-  const int n0 = 64 * q + 16 * w;                    // this wave's 16 of the 512 columns
-  WFrags<1, IK> wf;
-  wf.load(a.w0, IK, n0, lane, IK);
-  const float4 bias = *reinterpret_cast<const float4*>(a.b0 + n0 + 4 * g);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {                      // 16 rows x 128 float4 of modal -> bf16
-    const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-    const int rr = min(r0 + r, a.B - 1);
-    const float4 v = *reinterpret_cast<const float4*>(a.modal + (int64_t)rr * IK + 4 * c4);
-    const float x[4] = {v.x, v.y, v.z, v.w};
-    st4_bf(L.sA + r * PI + c4 * 8, x);
-    if (q == 0 && r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.m16 + (int64_t)(r0 + r) * IK + 4 * c4), x);
-  }
-  __syncthreads();
-  f32x4_t v[1];
-  head_gemm<1, IK, PI>(L.sA, wf, v, lane);
-  const int m = r0 + li;
-  if (m < a.B)
-    *reinterpret_cast<float4*>(a.z + (int64_t)m * IN1 + n0 + 4 * g) =
-        make_float4(v[0][0] + bias.x, v[0][1] + bias.y, v[0][2] + bias.z, v[0][3] + bias.w);
+  item_a_body(a, blockIdx.x, blockIdx.y, L);
 }
 
 struct ItemLdsC {
@@ -757,32 +837,83 @@ __global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
 
 }  // namespace
 
-extern "C" int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t s) {
+namespace {
+int item_fwd_check(const ttmi_item_head_desc* d) {
   TTMI_REQUIRE(d != nullptr, "ttmi_item_head_fwd: null descriptor");
   TTMI_REQUIRE(d->B > 1 && d->K == IK && d->N1 == IN1 && d->D == HD,
                "ttmi_item_head_fwd: needs B > 1 (training BatchNorm), K == N1 == %d, D == %d", IK, HD);
   TTMI_REQUIRE(d->modal && d->w0 && d->b0 && d->bn_w && d->bn_b && d->w4 && d->b4 && d->ln_w && d->ln_b &&
                d->modal16 && d->z && d->bn_mean && d->bn_rstd && d->y1 && d->y2 && d->out && d->m5 &&
                d->r5, "ttmi_item_head_fwd: null argument");
+  return TTMI_OK;
+}
+ItemArgs item_args(const ttmi_item_head_desc* d) {
   ItemArgs a{};
   a.B = d->B;
   a.modal = d->modal; a.w0 = (const bf16_t*)d->w0; a.b0 = d->b0;
   a.y1 = (const bf16_t*)d->y1; a.w4 = (const bf16_t*)d->w4; a.b4 = d->b4;
   a.lnw = d->ln_w; a.lnb = d->ln_b; a.ln_eps = d->ln_eps;
   a.m16 = (bf16_t*)d->modal16; a.z = d->z; a.y2 = d->y2; a.out = d->out; a.m5 = d->m5; a.r5 = d->r5;
+  return a;
+}
+int item_bwd_check(const ttmi_item_head_bwd_desc* d) {
+  TTMI_REQUIRE(d != nullptr, "ttmi_item_head_bwd_c: null descriptor");
+  TTMI_REQUIRE(d->B > 0 && d->D == HD && d->N1 == IN1, "ttmi_item_head_bwd_c: needs D == %d, N1 == %d", HD, IN1);
+  TTMI_REQUIRE(d->dout && d->y2 && d->m5 && d->r5 && d->ln_w && d->w4t && d->dy2 && d->dy1 && d->ws,
+               "ttmi_item_head_bwd_c: null argument");
+  TTMI_REQUIRE(((uintptr_t)d->dout & 15) == 0 && ((uintptr_t)d->y2 & 15) == 0 && ((uintptr_t)d->dy1 & 15) == 0 &&
+               ((uintptr_t)d->w4t & 15) == 0 && ((uintptr_t)d->dy2 & 7) == 0,
+               "ttmi_item_head_bwd_c: dout / y2 / dy1 / w4t need 16-byte, dy2 8-byte alignment");
+  return TTMI_OK;
+}
+ItemBwdArgs item_bwd_args(const ttmi_item_head_bwd_desc* d) {
+  ItemBwdArgs a{};
+  a.B = d->B; a.dout = d->dout; a.y2 = d->y2; a.m5 = d->m5; a.r5 = d->r5; a.lnw = d->ln_w;
+  a.w4t = (const bf16_t*)d->w4t; a.dy2 = (bf16_t*)d->dy2; a.dy1 = d->dy1; a.ws = d->ws;
+  return a;
+}
+}  // namespace
+
+extern "C" int ttmi_item_head_fwd_stages(const ttmi_item_head_desc* d, int stages, hipStream_t s) {
+  int rc = item_fwd_check(d);
+  if (rc != TTMI_OK) return rc;
+  TTMI_REQUIRE(stages > 0 && stages < 8, "ttmi_item_head_fwd_stages: stages is a mask of 1 (A), 2 (BN), 4 (C)");
+  const ItemArgs a = item_args(d);
   const unsigned nblk = (unsigned)((d->B + HR - 1) / HR);
-  hipLaunchKernelGGL(item_head_a_kernel, dim3(nblk, IN1 / 64), dim3(256), 0, s, a);
-  int rc = ttmi_check_launch("ttmi_item_head_fwd");
-  if (rc != TTMI_OK) return rc;
-  rc = ttmi_batchnorm_fwd(TTMI_BF16, d->B, IN1, d->z, d->bn_w, d->bn_b, d->bn_eps, d->momentum,
-                          d->running_mean, d->running_var, d->num_batches_tracked, 1, 1, d->drop_p,
-                          d->drop_seed, d->y1, d->bn_mean, d->bn_rstd, s);
-  if (rc != TTMI_OK) return rc;
-  hipLaunchKernelGGL(item_head_c_kernel, dim3(nblk), dim3(256), 0, s, a);
-  return ttmi_check_launch("ttmi_item_head_fwd");
+  if (stages & 1) {
+    hipLaunchKernelGGL(item_head_a_kernel, dim3(nblk, IN1 / 64), dim3(256), 0, s, a);
+    rc = ttmi_check_launch("ttmi_item_head_fwd");
+    if (rc != TTMI_OK) return rc;
+  }
+  if (stages & 2) {
+    rc = ttmi_batchnorm_fwd(TTMI_BF16, d->B, IN1, d->z, d->bn_w, d->bn_b, d->bn_eps, d->momentum,
+                            d->running_mean, d->running_var, d->num_batches_tracked, 1, 1, d->drop_p,
+                            d->drop_seed, d->y1, d->bn_mean, d->bn_rstd, s);
+    if (rc != TTMI_OK) return rc;
+  }
+  if (stages & 4) {
+    hipLaunchKernelGGL(item_head_c_kernel, dim3(nblk), dim3(256), 0, s, a);
+    return ttmi_check_launch("ttmi_item_head_fwd");
+  }
+  return TTMI_OK;
 }
 
-extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
+extern "C" int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t s) {
+  return ttmi_item_head_fwd_stages(d, 7, s);
+}
+
+extern "C" int64_t ttmi_item_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 2 * HD; }
+
+extern "C" int ttmi_item_head_bwd_c(const ttmi_item_head_bwd_desc* d, hipStream_t s) {
+  const int rc = item_bwd_check(d);
+  if (rc != TTMI_OK) return rc;
+  hipLaunchKernelGGL(item_head_bwd_c_kernel, dim3((unsigned)((d->B + HR - 1) / HR)), dim3(256), 0, s,
+                     item_bwd_args(d));
+  return ttmi_check_launch("ttmi_item_head_bwd_c");
+}
+
+extern "C" int ttmi_user_item_head_fwd(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
+                                       hipStream_t s) {
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_fwd: null descriptor");
   TTMI_REQUIRE(d->B > 0 && d->D == HD, "ttmi_user_head_fwd: needs D == %d", HD);
   TTMI_REQUIRE(d->F > 0 && d->F <= FMAX && d->F % 256 == 0, "ttmi_user_head_fwd: needs F %% 256 == 0, F <= %d", FMAX);
@@ -808,15 +939,30 @@ extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
   a.x1 = d->x1; a.a2 = (bf16_t*)d->a2; a.m2 = d->m2; a.r2 = d->r2; a.h = (bf16_t*)d->h;
   a.comb = (bf16_t*)d->comb; a.rows = d->rows; a.z = d->z; a.az = (bf16_t*)d->az;
   a.mz = d->mz; a.rz = d->rz; a.u = d->u;
-  const dim3 grid((unsigned)((d->B + HR - 1) / HR));
+  a.nbu = (d->B + HR - 1) / HR;
+  a.it_nblk = 1;
+  int extra = 0;
+  if (it) {                                          // item stage A on the idle CUs
+    const int rc = item_fwd_check(it);
+    if (rc != TTMI_OK) return rc;
+    a.it = item_args(it);
+    a.it_nblk = (it->B + HR - 1) / HR;
+    extra = a.it_nblk * (IN1 / 64);
+  }
+  const dim3 grid((unsigned)(a.nbu + extra));
   if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_kernel<512>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(user_head_fwd_kernel<256>, grid, dim3(256), 0, s, a);
   return ttmi_check_launch("ttmi_user_head_fwd");
 }
 
+extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
+  return ttmi_user_item_head_fwd(d, nullptr, s);
+}
+
 extern "C" int64_t ttmi_user_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 4 * HD; }
 
-extern "C" int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t s) {
+extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const ttmi_item_head_bwd_desc* it,
+                                       hipStream_t s) {
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_bwd: null descriptor");
   TTMI_REQUIRE(d->B > 0 && d->D == HD && (d->F == 256 || d->F == 512) && d->dg == 16 && d->dc == 32,
                "ttmi_user_head_bwd: needs D == %d, F in {256, 512}, dg == 16, dc == 32", HD);
@@ -837,8 +983,20 @@ extern "C" int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t 
   a.dG = d->dG; a.dC = d->dC;
   a.dz16 = (bf16_t*)d->dz16; a.dy2 = (bf16_t*)d->dy2; a.dz1 = (bf16_t*)d->dz1; a.dx1 = d->dx1;
   a.dy1 = (bf16_t*)d->dy1; a.dctx = (bf16_t*)d->dctx; a.ws = d->ws;
-  const dim3 grid((unsigned)((d->B + HR - 1) / HR));
+  a.nbu = (d->B + HR - 1) / HR;
+  int extra = 0;
+  if (it) {                                          // item head rows on the idle CUs
+    const int rc = item_bwd_check(it);
+    if (rc != TTMI_OK) return rc;
+    a.it = item_bwd_args(it);
+    extra = (it->B + HR - 1) / HR;
+  }
+  const dim3 grid((unsigned)(a.nbu + extra));
   if (d->F == 512) hipLaunchKernelGGL(user_head_bwd_kernel<512>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(user_head_bwd_kernel<256>, grid, dim3(256), 0, s, a);
   return ttmi_check_launch("ttmi_user_head_bwd");
+}
+
+extern "C" int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t s) {
+  return ttmi_user_item_head_bwd(d, nullptr, s);
 }

@@ -813,7 +813,7 @@ extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const
                                   const float* dx, float* dE, float* dP, float* dw, float* db,
                                   int64_t padding_idx, void* ws, hipStream_t s) {
   TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV, "ttmi_seq_embed_bwd: bad sizes");
-  TTMI_REQUIRE(ids && E && P && w && mean && rstd && dx && dE && dP && dw && db && ws,
+  TTMI_REQUIRE(ids && E && P && w && mean && rstd && dx && dE && dP && ws && (dw == nullptr) == (db == nullptr),
                "ttmi_seq_embed_bwd: null argument");
   if (B == 0) return TTMI_OK;
   // V is not needed for the math; rows with out-of-range ids were zero in the forward.
@@ -824,7 +824,7 @@ extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const
                                          E, P, w, mean, rstd, make_drop(drop_p, drop_seed), dx, dE,
                                          dP, (float*)ws, padding_idx, V, bpc));
   const int rc = ttmi_check_launch("ttmi_seq_embed_bwd");
-  if (rc) return rc;
+  if (rc || dw == nullptr) return rc;       // dw = db = NULL: the caller folds ws (ABI 15)
   hipLaunchKernelGGL(seq_embed_red_kernel, dim3((2 * D + 255) / 256), dim3(1024), 0, s, L, D, (float*)ws,
                      dw, db);
   return ttmi_check_launch("ttmi_seq_embed_bwd/reduce");

@@ -168,8 +168,10 @@ def _resln_ok(W: Dict[str, Tensor], name: str, D: int) -> bool:
 
 def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gender: Tensor,
                    country: Tensor, mask: Optional[Tensor], cfg: TowerCfg,
-                   seeds: Optional[Tensor] = None):
-    """SequentialUserEncoder.forward (reference user_tower.py:73-144), train mode."""
+                   seeds: Optional[Tensor] = None, co_item: Optional["ItemHeadPending"] = None):
+    """SequentialUserEncoder.forward (reference user_tower.py:73-144), train mode.  ``co_item``
+    (item_fusion_fwd_begin): the item head's first stage rides in the fused user head launch
+    when that path runs (``co_item.a_done`` tells item_fusion_fwd_end)."""
     dev = ids.device
     B, L = ids.shape
     D, H, dt = cfg.D, cfg.H, cfg.dtype
@@ -228,7 +230,10 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                          mz=torch.empty(B, **f32), rz=torch.empty(B, **f32), u=torch.empty(B, D, **f32))
                 ops.user_head_fwd(ctx, res_in, drows, W, P, pre, gender, country, cfg.eps,
                                   (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_ffn(i)),
-                                   _drop(cfg, seeds, site_drop2(i))), o)
+                                   _drop(cfg, seeds, site_drop2(i))), o,
+                                  co_item=co_item.desc if co_item is not None else None)
+                if co_item is not None:
+                    co_item.a_done = True
                 st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, o["x1"], o["a2"], o["m2"],
                                             o["r2"], o["h"], rows))
                 st.comb, st.rows, st.z = o["comb"], o["rows"], o["z"]
@@ -291,11 +296,15 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
 
 def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du: Tensor,
                    grads: Dict[str, Tensor], cfg: TowerCfg, du16: Optional[Tensor] = None,
-                   on_layer_done: Optional[Callable[[int], None]] = None) -> None:
+                   on_layer_done: Optional[Callable[[int], None]] = None,
+                   co_item: Optional["ItemBwdPending"] = None) -> None:
     """Backward of user_tower_fwd; accumulates into ``grads`` (fp32, reference names).  du16:
     du already in the compute dtype (InfoNCE backward's bf16 copy), saving the cast launch.
     ``on_layer_done(i)`` is called once encoder layer i's parameter gradients are final (the
-    data-parallel step starts a bucket's all-reduce there)."""
+    data-parallel step starts a bucket's all-reduce there).  ``co_item``
+    (item_fusion_bwd_begin): the item head's row-local backward rides in the fused user head
+    launch when that path runs; item_fusion_bwd_end(co_item) runs right after the head, before
+    any encoder layer, so the item gradients are final by the first ``on_layer_done``."""
     dev = du.device
     B, L = st.ids.shape
     D, H, dt = cfg.D, cfg.H, cfg.dtype
@@ -319,7 +328,10 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
             (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_drop2(i))),
             grads["gender_embedding.weight"], grads["country_embedding.weight"],
             (grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"],
-             grads[last + "norm2.weight"], grads[last + "norm2.bias"]))
+             grads[last + "norm2.weight"], grads[last + "norm2.bias"]),
+            co_item=co_item.desc if co_item is not None else None)
+        if co_item is not None:
+            co_item.done = True
         ops.linear_dw(du16, st.az, grads["fusion_layer.3.weight"], grads["fusion_layer.3.bias"])
         ops.linear_dw(head["dz16"], st.comb, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
         ops.linear_dw(head["dy2"], s.h, grads[last + "linear2.weight"], grads[last + "linear2.bias"])
@@ -329,6 +341,8 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         dx = None
     else:
         dx = _head_bwd_unfused(P, W, st, du, grads, cfg, du16, gathered)
+    if co_item is not None:
+        item_fusion_bwd_end(co_item)
     # ---- encoder layers, reversed (user_tower.py:37-45)
     p = cfg.p_drop
     dy2_next = None        # layer i's dy2, emitted by layer i+1's fused LN1 backward
@@ -519,6 +533,91 @@ def item_fusion_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Tensor, c
     return out, ItemSaved(m_c, z, bn_mean, bn_rstd, y1, y2, m5, r5, seeds)
 
 
+@dataclass
+class ItemHeadPending:
+    """A training forward of the item fusion head split around the user head launch (ABI 15):
+    item_fusion_fwd_begin builds the descriptor, user_tower_fwd(co_item=...) issues stage A
+    inside the fused user head launch, item_fusion_fwd_end issues the rest."""
+    desc: object
+    o: Dict[str, Tensor]
+    modal: Tensor
+    seeds: Optional[Tensor]
+    a_done: bool = False
+
+
+def item_fusion_fwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Tensor, cfg: TowerCfg,
+                          seeds: Optional[Tensor] = None,
+                          buffers: Optional[Dict[str, Tensor]] = None,
+                          p_drop: float = 0.1) -> Optional[ItemHeadPending]:
+    """item_fusion_fwd (training) as a pending co-launch, or None when the fused head does not
+    take these shapes (then call item_fusion_fwd)."""
+    if not ops.item_head_fusable(W, modal, cfg.dtype):
+        return None
+    dev = modal.device
+    B = modal.shape[0]
+    f32 = dict(device=dev, dtype=torch.float32)
+    H1, D = W["fusion_layer.0.weight"].shape[0], W["fusion_layer.4.weight"].shape[0]
+    o = dict(m16=torch.empty(modal.shape, device=dev, dtype=cfg.dtype), z=torch.empty(B, H1, **f32),
+             bn_mean=torch.empty(H1, **f32), bn_rstd=torch.empty(H1, **f32),
+             y1=torch.empty(B, H1, device=dev, dtype=cfg.dtype), y2=torch.empty(B, D, **f32),
+             out=torch.empty(B, D, **f32), m5=torch.empty(B, **f32), r5=torch.empty(B, **f32))
+    m = modal.contiguous()
+    d = ops.item_head_desc(m, W, P, buffers or {}, _drop(cfg, seeds, SITE_ITEM, p_drop), cfg.eps, o)
+    return ItemHeadPending(d, o, m, seeds)
+
+
+def item_fusion_fwd_end(pend: ItemHeadPending):
+    """The pending forward's remaining stages; returns (out, ItemSaved) as item_fusion_fwd."""
+    ops.item_head_fwd_stages(pend.desc, 6 if pend.a_done else 7)
+    o = pend.o
+    return o["out"], ItemSaved(o["m16"], o["z"], o["bn_mean"], o["bn_rstd"], o["y1"], o["y2"],
+                               o["m5"], o["r5"], pend.seeds)
+
+
+@dataclass
+class ItemBwdPending:
+    """item_fusion_bwd split around the user head backward launch (ABI 15)."""
+    desc: object
+    keep: tuple
+    dy2: Tensor
+    dy1: Tensor
+    ws: Tensor
+    args: tuple
+    done: bool = False
+
+
+def item_fusion_bwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, dout: Tensor,
+                          grads: Dict[str, Tensor], cfg: TowerCfg, p_drop: float = 0.1,
+                          dmodal: Optional[Tensor] = None) -> Optional[ItemBwdPending]:
+    """item_fusion_bwd as a pending co-launch (its LayerNorm backward and Linear-4 input grad
+    in the user head backward launch), or None when the shapes or the W4ᵀ mirror are missing."""
+    w4t = W.get(transposed_name("fusion_layer.4.weight"))
+    B, D = dout.shape
+    if cfg.dtype != torch.bfloat16 or w4t is None or D != 128 or tuple(w4t.shape) != (512, 128) \
+            or st.y2.dtype != torch.float32:
+        return None
+    dev = dout.device
+    dy2 = torch.empty(B, D, device=dev, dtype=cfg.dtype)
+    dy1 = torch.empty(B, w4t.shape[0], device=dev, dtype=torch.float32)
+    ws = ops.item_head_bwd_ws(B, dev)
+    dc = dout.contiguous()
+    d = ops.item_head_bwd_desc(dc, st.y2, st.m5, st.r5, P["fusion_layer.5.weight"], w4t, dy2, dy1, ws)
+    return ItemBwdPending(d, (dc, w4t), dy2, dy1, ws, (P, W, st, grads, cfg, p_drop, dmodal))
+
+
+def item_fusion_bwd_end(pend: ItemBwdPending) -> None:
+    """The rest of item_fusion_bwd: the row-local launch if the user head did not carry it,
+    the LayerNorm parameter sums, the weight gradients and the BatchNorm backward."""
+    P, W, st, grads, cfg, p_drop, dmodal = pend.args
+    if not pend.done:
+        ops.item_head_bwd_c(pend.desc)
+        pend.done = True
+    D = pend.dy2.shape[1]
+    ops.ln_sum_folds(pend.ws, (grads["fusion_layer.5.weight"], grads["fusion_layer.5.bias"]), 2, D)
+    ops.linear_dw(pend.dy2, st.y1, grads["fusion_layer.4.weight"], grads["fusion_layer.4.bias"])
+    _item_bwd_tail(P, W, st, pend.dy1, grads, cfg, p_drop, dmodal)
+
+
 def item_fusion_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, dout: Tensor,
                     grads: Dict[str, Tensor], cfg: TowerCfg, p_drop: float = 0.1,
                     dmodal: Optional[Tensor] = None) -> None:
@@ -537,6 +636,16 @@ def item_fusion_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, d
     H1 = st.z.shape[1]
     dy1 = torch.empty(B, H1, **f32)
     ops.linear_dx(dy2_c, W["fusion_layer.4.weight"], dy1)
+    _item_bwd_tail(P, W, st, dy1, grads, cfg, p_drop, dmodal)
+
+
+def _item_bwd_tail(P, W, st: ItemSaved, dy1: Tensor, grads, cfg: TowerCfg, p_drop: float,
+                   dmodal: Optional[Tensor]) -> None:
+    """BatchNorm1d + ReLU + dropout backward and Linear 0 of the item fusion head."""
+    dev = dy1.device
+    B, H1 = dy1.shape
+    dt = cfg.dtype
+    f32 = dict(device=dev, dtype=torch.float32)
     pd = p_drop if st.seeds is not None else 0.0
     dz = torch.empty(B, H1, **f32)
     dz_c = torch.empty(B, H1, device=dev, dtype=dt)

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -79,7 +79,7 @@ class DisAttnDesc(ctypes.Structure):
 
 
 class ItemHeadDesc(ctypes.Structure):
-    """ttmi_item_head_desc (include/ttmi.h, ABI 14)."""
+    """ttmi_item_head_desc (include/ttmi.h, ABI 14; stages ABI 15)."""
     _fields_ = [("B", c_i), ("K", c_i), ("N1", c_i), ("D", c_i),
                 ("modal", c_p), ("w0", c_p), ("b0", c_p),
                 ("bn_w", c_p), ("bn_b", c_p), ("bn_eps", ctypes.c_float), ("momentum", ctypes.c_float),
@@ -88,6 +88,13 @@ class ItemHeadDesc(ctypes.Structure):
                 ("w4", c_p), ("b4", c_p), ("ln_w", c_p), ("ln_b", c_p), ("ln_eps", ctypes.c_float),
                 ("modal16", c_p), ("z", c_p), ("bn_mean", c_p), ("bn_rstd", c_p), ("y1", c_p), ("y2", c_p),
                 ("out", c_p), ("m5", c_p), ("r5", c_p), ("ws", c_p)]
+
+
+class ItemHeadBwdDesc(ctypes.Structure):
+    """ttmi_item_head_bwd_desc (include/ttmi.h, ABI 15)."""
+    _fields_ = [("B", c_i), ("D", c_i), ("N1", c_i),
+                ("dout", c_p), ("y2", c_p), ("m5", c_p), ("r5", c_p), ("ln_w", c_p),
+                ("w4t", c_p), ("dy2", c_p), ("dy1", c_p), ("ws", c_p)]
 
 
 class UserHeadDesc(ctypes.Structure):
@@ -218,6 +225,11 @@ SIGNATURES = {
     "ttmi_user_head_bwd": (c_i, [c_p, c_p]),
     "ttmi_user_head_bwd_ws_floats": (ctypes.c_int64, [c_i]),
     "ttmi_item_head_fwd": (c_i, [c_p, c_p]),
+    "ttmi_item_head_fwd_stages": (c_i, [c_p, c_i, c_p]),
+    "ttmi_user_item_head_fwd": (c_i, [c_p, c_p, c_p]),
+    "ttmi_item_head_bwd_c": (c_i, [c_p, c_p]),
+    "ttmi_item_head_bwd_ws_floats": (ctypes.c_int64, [c_i]),
+    "ttmi_user_item_head_bwd": (c_i, [c_p, c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,

@@ -8,13 +8,13 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
 from . import lib as _L
 from .lib import (BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, UserHeadBwdDesc,
-                  UserHeadDesc, ItemHeadDesc, WgradDesc, call)
+                  UserHeadDesc, ItemHeadBwdDesc, ItemHeadDesc, WgradDesc, call)
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -475,9 +475,12 @@ def seq_embed_bwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, mean: Tensor, rs
     B, L = ids.shape
     D = E.shape[1]
     ws = _zero_ws("ttmi_seq_embed_bwd_workspace", (L, D), dx.device)
+    defer = bool(_PENDING) and D % 4 == 0
     call("ttmi_seq_embed_bwd", B, L, D, _p(ids), _p(E), _p(P), _p(w), _p(mean), _p(rstd),
-         float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), _p(dw), _p(db), padding_idx,
-         _p(ws), _s())
+         float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), None if defer else _p(dw),
+         None if defer else _p(db), padding_idx, _p(ws), _s())
+    if defer:       # the LN partials fold with the deferred weight gradients (ws left zero)
+        ln_sum_folds(ws, (dw, db), 2, D, S=L, consume=True)
 
 
 # ----------------------------------------------------------------------------- attention
@@ -528,12 +531,11 @@ def batchnorm_fwd(z: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd
     return y
 
 
-def item_head_fwd(modal: Tensor, W: Dict[str, Tensor], P: Dict[str, Tensor],
-                  bufs: Dict[str, Optional[Tensor]], drop: Drop, eps: float, out: Dict[str, Tensor],
-                  momentum: float = 0.1) -> Dict[str, Tensor]:
-    """The item late-fusion MLP forward in training mode in three launches (ttmi_item_head_fwd):
-    fills out's m16, z, bn_mean, bn_rstd, y1, y2, out, m5, r5 exactly as cast_bf16 + linear +
-    batchnorm_fwd(relu, dropout) + linear + layernorm_fwd write them."""
+def item_head_desc(modal: Tensor, W: Dict[str, Tensor], P: Dict[str, Tensor],
+                   bufs: Dict[str, Optional[Tensor]], drop: Drop, eps: float, out: Dict[str, Tensor],
+                   momentum: float = 0.1) -> ItemHeadDesc:
+    """The ttmi_item_head_desc of one training forward of the item late-fusion MLP (the
+    caller keeps modal, the weights and ``out`` alive until its launches are issued)."""
     B = modal.shape[0]
     _dev(modal, *out.values())
     d = ItemHeadDesc()
@@ -550,8 +552,68 @@ def item_head_fwd(modal: Tensor, W: Dict[str, Tensor], P: Dict[str, Tensor],
     d.modal16, d.z, d.bn_mean, d.bn_rstd = _p(out["m16"]), _p(out["z"]), _p(out["bn_mean"]), _p(out["bn_rstd"])
     d.y1, d.y2, d.out, d.m5, d.r5 = _p(out["y1"]), _p(out["y2"]), _p(out["out"]), _p(out["m5"]), _p(out["r5"])
     d.ws = None
+    return d
+
+
+def item_head_fwd(modal: Tensor, W: Dict[str, Tensor], P: Dict[str, Tensor],
+                  bufs: Dict[str, Optional[Tensor]], drop: Drop, eps: float, out: Dict[str, Tensor],
+                  momentum: float = 0.1) -> Dict[str, Tensor]:
+    """The item late-fusion MLP forward in training mode in three launches (ttmi_item_head_fwd):
+    fills out's m16, z, bn_mean, bn_rstd, y1, y2, out, m5, r5 exactly as cast_bf16 + linear +
+    batchnorm_fwd(relu, dropout) + linear + layernorm_fwd write them."""
+    d = item_head_desc(modal, W, P, bufs, drop, eps, out, momentum)
     call("ttmi_item_head_fwd", ctypes.byref(d), _s())
     return out
+
+
+def item_head_fwd_stages(d: ItemHeadDesc, stages: int) -> None:
+    """ttmi_item_head_fwd_stages: stage mask 1 = cast + Linear 0, 2 = BatchNorm + ReLU +
+    dropout, 4 = Linear 4 + LayerNorm."""
+    call("ttmi_item_head_fwd_stages", ctypes.byref(d), stages, _s())
+
+
+def item_head_bwd_desc(dout: Tensor, y2: Tensor, m5: Tensor, r5: Tensor, ln_w: Tensor, w4t: Tensor,
+                       dy2: Tensor, dy1: Tensor, ws: Tensor) -> ItemHeadBwdDesc:
+    """ttmi_item_head_bwd_desc: LN(fusion_layer.5) backward + fusion_layer.4 input gradient."""
+    _dev(dout, y2, m5, r5, ln_w, w4t, dy2, dy1, ws)
+    B, D = dout.shape
+    if w4t.dtype != torch.bfloat16 or dy2.dtype != torch.bfloat16 or not all(
+            t.is_contiguous() for t in (dout, y2, w4t, dy2, dy1)):
+        raise ValueError("item_head_bwd: contiguous operands, bf16 w4t / dy2")
+    d = ItemHeadBwdDesc()
+    d.B, d.D, d.N1 = B, D, w4t.shape[0]
+    d.dout, d.y2, d.m5, d.r5, d.ln_w = _p(dout), _p(y2), _p(m5), _p(r5), _p(ln_w)
+    d.w4t, d.dy2, d.dy1, d.ws = _p(w4t), _p(dy2), _p(dy1), _p(ws)
+    return d
+
+
+def item_head_bwd_ws(B: int, device) -> Tensor:
+    _L.load()
+    return torch.empty(int(_L._lib.ttmi_item_head_bwd_ws_floats(B)), device=device)
+
+
+def item_head_bwd_c(d: ItemHeadBwdDesc) -> None:
+    call("ttmi_item_head_bwd_c", ctypes.byref(d), _s())
+
+
+def ln_sum_folds(ws: Tensor, grads: Sequence[Tensor], rows: int, D: int, S: Optional[int] = None,
+                 consume: bool = False) -> None:
+    """Fold per-block column sums ws [S][rows][D] (row j -> grads[j], accumulated, in block
+    order; S defaults to all of ws) with the deferred weight gradients, or now outside
+    ``deferred_wgrad``.  ``consume``: the fold leaves the partials zero."""
+    nblk = ws.numel() // (rows * D) if S is None else S
+    folds = []
+    for j, g in enumerate(grads):
+        f = FoldDesc()
+        f.part, f.S, f.s_stride, f.M, f.N = ws.data_ptr() + 4 * D * j, nblk, rows * D, 1, D
+        f.C, f.ldc, f.accumulate = _p(g), D, 3 if consume else 1
+        folds.append((f, ws, g))
+    pend = _PENDING[-1] if _PENDING else None
+    if pend is not None:
+        pend.folds.extend(folds)
+    else:
+        farr = (FoldDesc * len(folds))(*[f for f, *_ in folds])
+        call("ttmi_wgrad_batch", 0, (ctypes.POINTER(WgradDesc) * 1)(), len(folds), farr, _s())
 
 
 def item_head_fusable(W: Dict[str, Tensor], modal: Tensor, dtype) -> bool:
@@ -827,7 +889,8 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
 
 def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict[str, Tensor],
                   P: Dict[str, Tensor], pre: str, gender: Tensor, country: Tensor, eps: float,
-                  drops: Tuple[Drop, Drop, Drop], out: Dict[str, Tensor]) -> None:
+                  drops: Tuple[Drop, Drop, Drop], out: Dict[str, Tensor],
+                  co_item: Optional[ItemHeadDesc] = None) -> None:
     """The user tower head in one launch (ttmi_user_head_fwd): the pruned last layer's
     out-proj + residual + norm2 + FFN on the gathered rows, the demographic concat and the
     fusion MLP.  ``pre`` is the last layer's parameter prefix; ``out`` holds x1, a2, m2, r2, h,
@@ -852,13 +915,17 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
     d.d1_seed, d.dff_seed, d.d2_seed = _p(d1), _p(dff), _p(d2)
     for k in ("x1", "a2", "m2", "r2", "h", "comb", "rows", "z", "az", "mz", "rz", "u"):
         setattr(d, k, _p(out[k]))
-    call("ttmi_user_head_fwd", ctypes.byref(d), _s())
+    if co_item is None:
+        call("ttmi_user_head_fwd", ctypes.byref(d), _s())
+    else:      # item head stage A on the CUs the 16-row user blocks leave idle (ABI 15)
+        call("ttmi_user_item_head_fwd", ctypes.byref(d), ctypes.byref(co_item), _s())
 
 
 def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: Dict[str, Tensor],
                   P: Dict[str, Tensor], pre: str, gender: Tensor, country: Tensor, ffn_scale: float,
                   drops: Tuple[Drop, Drop], dG: Tensor, dC: Tensor,
-                  ln_grads: Tuple[Tensor, Tensor, Tensor, Tensor]) -> Dict[str, Tensor]:
+                  ln_grads: Tuple[Tensor, Tensor, Tensor, Tensor],
+                  co_item: Optional[ItemHeadBwdDesc] = None) -> Dict[str, Tensor]:
     """Backward of user_head_fwd in one launch (ttmi_user_head_bwd).  ``saved``: az, z, mz, rz,
     h, x1, m2, r2 of the forward; ``drops`` = (drop1, drop2).  Returns dz16, dy2, dz1, dx1, dy1,
     dctx; the four LayerNorm parameter gradients (``ln_grads``: fusion LN weight, bias, norm2
@@ -893,20 +960,11 @@ def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: 
     for k in ("dz16", "dy2", "dz1", "dx1", "dy1", "dctx"):
         setattr(d, k, _p(o[k]))
     d.ws = _p(ws)
-    call("ttmi_user_head_bwd", ctypes.byref(d), _s())
-    nblk = nws // (4 * D)
-    folds = []
-    for j, g in enumerate(ln_grads):
-        f = FoldDesc()
-        f.part, f.S, f.s_stride, f.M, f.N = ws.data_ptr() + 4 * D * j, nblk, 4 * D, 1, D
-        f.C, f.ldc, f.accumulate = _p(g), D, 1
-        folds.append((f, ws, g))
-    pend = _PENDING[-1] if _PENDING else None
-    if pend is not None:
-        pend.folds.extend(folds)
-    else:
-        farr = (FoldDesc * len(folds))(*[f for f, *_ in folds])
-        call("ttmi_wgrad_batch", 0, (ctypes.POINTER(WgradDesc) * 1)(), len(folds), farr, _s())
+    if co_item is None:
+        call("ttmi_user_head_bwd", ctypes.byref(d), _s())
+    else:      # the item head's row-local backward on the idle CUs (ABI 15)
+        call("ttmi_user_item_head_bwd", ctypes.byref(d), ctypes.byref(co_item), _s())
+    ln_sum_folds(ws, ln_grads, 4, D)
     return o
 
 

@@ -28,7 +28,7 @@ from . import functional as F
 from . import text as T
 from . import ops
 from .two_tower import TwoTowerModel
-from .user_tower import _gemm_names, add_transposes, refresh_transposes
+from .user_tower import _gemm_names, add_transposes, encoder_weight_names
 from .item_tower import ITEM_GEMMS
 
 Tensor = torch.Tensor
@@ -336,6 +336,10 @@ class TrainStep:
             add_transposes(self.Wu, _gemm_names(list(self.Pu)))   # refreshed every step
             self.Wi = dict(self.Pi)
             self.Wi.update({n: Mi[n] for n in ITEM_GEMMS})
+            w4 = self.Wi.get("fusion_layer.4.weight")
+            if w4 is not None and w4.dim() == 2:   # W4ᵀ: the item head backward's k-major operand
+                self.Wi[F.transposed_name("fusion_layer.4.weight")] = torch.empty(
+                    w4.shape[1], w4.shape[0], device=w4.device, dtype=w4.dtype)
         else:
             self.Wu, self.Wi = self.Pu, self.Pi
         self.bufs = {k[len("item_tower."):]: v for k, v in model.named_buffers()
@@ -380,8 +384,7 @@ class TrainStep:
         draw = self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0)
         if self.flat.mirror is not None:
             # Wᵀ mirrors of the just-updated bf16 weights, and the step's seeds: one launch
-            refresh_transposes(self.Wu, _gemm_names(list(self.Pu)),
-                               (self.base_seed, self.step_t, self.seeds, True) if draw else None)
+            self._refresh_mirrors((self.base_seed, self.step_t, self.seeds, True) if draw else None)
         if draw:
             if self.flat.mirror is None:
                 ops.dropout_seeds(self.base_seed, self.step_t, self.seeds, inc_step=True)
@@ -390,14 +393,21 @@ class TrainStep:
             ops.step_inc(self.step_t)
         if self.broadcast_buffers:             # rank 0's buffers from the last all-reduce
             ops.batch_copy([self.fbufs.data], [self.bstage])
+        # cfg 2: the item head's first stage rides in the user head launch (idle CUs)
+        co = None if self.raw_items else F.item_fusion_fwd_begin(
+            self.Pi, self.Wi, b["target_modal"], self.icfg, seeds, self.bufs, self.p_item)
         u, ust = F.user_tower_fwd(self.Pu, self.Wu, b["history_ids"], b["user_gender"],
-                                  b["user_country"], b.get("history_mask"), self.ucfg, seeds)
+                                  b["user_country"], b.get("history_mask"), self.ucfg, seeds,
+                                  co_item=co)
         if self.raw_items:
             modal, rst = self._raw_items_fwd(b, seeds)
         else:
             modal = b["target_modal"]
-        it, ist = F.item_fusion_fwd(self.Pi, self.Wi, modal, self.icfg, seeds,
-                                    self.bufs, self.p_item)
+        if co is not None:
+            it, ist = F.item_fusion_fwd_end(co)
+        else:
+            it, ist = F.item_fusion_fwd(self.Pi, self.Wi, modal, self.icfg, seeds,
+                                        self.bufs, self.p_item)
         with ops.deferred_wgrad() as pend:     # one fold launch for the step's weight grads
             self._bwd(b, u, it, modal, ust, ist, rst if self.raw_items else None, cut, pend)
 
@@ -422,18 +432,36 @@ class TrainStep:
             du16 = torch.empty(u.shape, device=u.device, dtype=self.ucfg.dtype) \
                 if self.ucfg.dtype == torch.bfloat16 else None
             F.infonce_bwd(lst, self.dloss, du, di, du16)
-        dmodal = torch.empty(modal.shape, device=modal.device) if self.raw_items else None
-        F.item_fusion_bwd(self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item, dmodal)
-        if self.raw_items:
-            self._raw_items_bwd(rst, dmodal)
+        # cfg 2: the item head's row-local backward rides in the user head backward launch
+        ib = None if self.raw_items else F.item_fusion_bwd_begin(
+            self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item)
+        if ib is None:
+            dmodal = torch.empty(modal.shape, device=modal.device) if self.raw_items else None
+            F.item_fusion_bwd(self.Pi, self.Wi, ist, di, self.Gi, self.icfg, self.p_item, dmodal)
+            if self.raw_items:
+                self._raw_items_bwd(rst, dmodal)
         hook = None
         if self.overlap:
             def hook(i: int) -> None:
                 if i == 1:       # every gradient before the tail slots is final
                     pend.flush()
                     cut(self._sync_head)
-        F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg, du16, on_layer_done=hook)
+        F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg, du16, on_layer_done=hook,
+                         co_item=ib)
         self.loss, self.logits = loss, logits
+
+    def _refresh_mirrors(self, seeds) -> None:
+        """Every Wᵀ mirror of the just-updated bf16 weights (user tower encoder + fusion MLP,
+        item W4) and the step's dropout seeds: one launch."""
+        T = F.transposed_name
+        names = [n for n in encoder_weight_names(_gemm_names(list(self.Pu))) if T(n) in self.Wu]
+        dsts = [self.Wu[T(n)] for n in names]
+        srcs = [self.Wu[n] for n in names]
+        t4 = T("fusion_layer.4.weight")
+        if t4 in self.Wi:
+            dsts.append(self.Wi[t4])
+            srcs.append(self.Wi["fusion_layer.4.weight"])
+        ops.transpose_batch(dsts, srcs, seeds)
 
     def _sync_head(self) -> None:
         self._pending = self.sync.start(self.flat.grad[:self.flat.tail_offset])

@@ -477,8 +477,11 @@ def test_gather_scatter_rows(gpu_pkg):
 
 
 # ------------------------------------------------------------------------------ embedding
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_seq_embed_fwd_bwd(gpu_pkg, p):
+@pytest.mark.parametrize("p,deferred", [(0.0, False), (0.1, False), (0.1, True)])
+def test_seq_embed_fwd_bwd(gpu_pkg, p, deferred):
+    """seq_embed_fwd/bwd vs torch autograd.  deferred (ABI 15): inside deferred_wgrad the LN
+    partials are folded by the weight-gradient fold (accumulate bit 2 leaves the workspace
+    zero), so two deferred calls in a row must each give the same gradients."""
     ops = gpu_pkg.ops
     B, L, D, V = 37, 50, 128, 301
     g = torch.Generator().manual_seed(9)
@@ -505,8 +508,19 @@ def test_seq_embed_fwd_bwd(gpu_pkg, p):
     dP = torch.zeros(L, D, device=DEV)
     dw = torch.zeros(D, device=DEV)
     db = torch.zeros(D, device=DEV)
-    ops.seq_embed_bwd(ids.to(DEV), Ed, Pd, wd, mean, rstd, dx.to(DEV), dE, dP, dw, db,
-                      drop=(p, sd), padding_idx=0)
+    if deferred:
+        for k in range(2):
+            dw.zero_()
+            db.zero_()
+            with ops.deferred_wgrad():
+                ops.seq_embed_bwd(ids.to(DEV), Ed, Pd, wd, mean, rstd, dx.to(DEV), dE, dP, dw, db,
+                                  drop=(p, sd), padding_idx=0)
+            assert rel(dw, wt.grad) < 5e-5 and rel(db, bt.grad) < 5e-5, k
+        dE /= 2
+        dP /= 2
+    else:
+        ops.seq_embed_bwd(ids.to(DEV), Ed, Pd, wd, mean, rstd, dx.to(DEV), dE, dP, dw, db,
+                          drop=(p, sd), padding_idx=0)
     assert rel(dE, Et.grad) < 5e-5
     assert dE[0].abs().max().item() == 0.0
     assert rel(dP, Pt.grad) < 5e-5

@@ -505,8 +505,41 @@ def test_trainstep_ragged_last_batch(gpu_pkg, use_graph):
             assert rel(got[k], params[k]) < 2e-4, (k, rel(got[k], params[k]))
 
 
-@pytest.mark.parametrize("B,p", [(512, 0.1), (300, 0.0), (37, 0.1)])
-def test_user_head_fused_matches_ops(gpu_pkg, B, p):
+def _item_head_inputs(ops, B, g, p):
+    """Random item fusion-head weights / input / buffers (bf16 operands) for the fused tests."""
+    def bf(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+    def f32(*s, scale=1.0):
+        return (torch.randn(*s, generator=g) * scale).to(DEV)
+    W = {"fusion_layer.0.weight": bf(512, 512, scale=512 ** -0.5),
+         "fusion_layer.4.weight": bf(128, 512, scale=512 ** -0.5)}
+    W["fusion_layer.4.weight.T"] = W["fusion_layer.4.weight"].t().contiguous()
+    P = {"fusion_layer.0.bias": f32(512, scale=0.1), "fusion_layer.1.weight": 1 + f32(512, scale=0.1),
+         "fusion_layer.1.bias": f32(512, scale=0.1), "fusion_layer.4.bias": f32(128, scale=0.1),
+         "fusion_layer.5.weight": 1 + f32(128, scale=0.1), "fusion_layer.5.bias": f32(128, scale=0.1)}
+    modal = f32(B, 512) * 2 + 0.3
+    seeds = torch.tensor([0x7654321], dtype=torch.int64, device=DEV)
+    drop = (p, seeds[0:1]) if p > 0 else ops.NO_DROP
+
+    def bufs():
+        return {"fusion_layer.1.running_mean": torch.full((512,), 0.2, device=DEV),
+                "fusion_layer.1.running_var": torch.full((512,), 1.5, device=DEV),
+                "fusion_layer.1.num_batches_tracked": torch.full((), 3, dtype=torch.int64, device=DEV)}
+    return W, P, modal, drop, bufs
+
+
+def _item_head_outs(B):
+    f = dict(device=DEV)
+    return dict(m16=torch.full((B, 512), 7, dtype=torch.bfloat16, **f), z=torch.full((B, 512), 7., **f),
+                bn_mean=torch.full((512,), 7., **f), bn_rstd=torch.full((512,), 7., **f),
+                y1=torch.full((B, 512), 7, dtype=torch.bfloat16, **f), y2=torch.full((B, 128), 7., **f),
+                out=torch.full((B, 128), 7., **f), m5=torch.full((B,), 7., **f), r5=torch.full((B,), 7., **f))
+
+
+@pytest.mark.parametrize("B,p,co", [(512, 0.1, False), (300, 0.0, False), (37, 0.1, False),
+                                    (512, 0.1, True), (37, 0.1, True)])
+def test_user_head_fused_matches_ops(gpu_pkg, B, p, co):
     """ttmi_user_head_fwd (the user tower head in one launch) against the unfused op sequence
     it replaces (functional.user_tower_fwd's pruned-layer path): same dropout masks (same hash,
     same drop_rows indices), fp32 values to 1e-4 of their scale, bf16 values to 1e-2."""
@@ -565,7 +598,24 @@ def test_user_head_fused_matches_ops(gpu_pkg, B, p):
     ops.linear(az, W["fusion_layer.3.weight"], P["fusion_layer.3.bias"], u)
     want = dict(x1=x1, a2=a2, m2=m2, r2=r2, h=h, comb=comb, rows=rows, z=z, az=az, mz=mz, rz=rz, u=u)
     out = {k: torch.full_like(v, 7) for k, v in want.items()}
-    ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, out)
+    if co:      # ABI 15: the item head's stage A rides in the same launch (idle CUs)
+        Wi, Pi, modal, drop_i, bufs = _item_head_inputs(ops, B, g, p)
+        iw, ig = _item_head_outs(B), _item_head_outs(B)
+        ops.item_head_fwd(modal, Wi, Pi, bufs(), drop_i, 1e-5, iw)
+        d = ops.item_head_desc(modal, Wi, Pi, bufs(), drop_i, 1e-5, ig)
+        ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, out, co_item=d)
+        ops.item_head_fwd_stages(d, 6)
+        solo = {k: torch.full_like(v, 7) for k, v in want.items()}
+        ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, solo)
+        torch.cuda.synchronize()
+        for k in solo:                       # the user blocks run the same code either way
+            assert torch.equal(out[k], solo[k]), k
+        for k in ("m16", "z", "y1"):         # stage A (and BN) are the same kernels' arithmetic
+            assert torch.equal(ig[k], iw[k]), k
+        for k in ("bn_mean", "bn_rstd", "y2", "out", "m5", "r5"):
+            assert rel(ig[k], iw[k]) < 1e-6, k
+    else:
+        ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, out)
     torch.cuda.synchronize()
     assert torch.equal(out["rows"], rows)
     for k in ("x1", "m2", "r2", "z", "mz", "rz", "u"):
@@ -636,8 +686,52 @@ def test_item_head_fused_matches_ops(gpu_pkg, B, p):
     assert int(bf_["fusion_layer.1.num_batches_tracked"]) == 4
 
 
-@pytest.mark.parametrize("B,p", [(512, 0.1), (37, 0.0)])
-def test_user_head_bwd_fused_matches_ops(gpu_pkg, B, p):
+def _item_bwd_case(ops, B, g):
+    """LayerNorm(fusion_layer.5)-backward + Linear-4 input-grad inputs and the unfused ops'
+    results (ttmi_layernorm_bwd with its bf16 copy, then the dgrad GEMM)."""
+    W, P, _, _, _ = _item_head_inputs(ops, B, g, 0.0)
+    y2 = (torch.randn(B, 128, generator=g) * 1.5 + 0.2).to(DEV)
+    out, m5, r5 = torch.empty(B, 128, device=DEV), torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    ops.layernorm_fwd(y2, P["fusion_layer.5.weight"], P["fusion_layer.5.bias"], out, m5, r5, eps=1e-5)
+    dout = torch.randn(B, 128, generator=g).to(DEV)
+    dy2, dy2c = torch.empty(B, 128, device=DEV), torch.empty(B, 128, device=DEV, dtype=torch.bfloat16)
+    gw, gb = torch.zeros(128, device=DEV), torch.zeros(128, device=DEV)
+    ops.layernorm_bwd(dout, y2, m5, r5, P["fusion_layer.5.weight"], dy2, gw, gb, dx16=dy2c)
+    dy1 = torch.empty(B, 512, device=DEV)
+    ops.linear_dx(dy2c, W["fusion_layer.4.weight"], dy1)
+    return dict(W=W, P=P, y2=y2, m5=m5, r5=r5, dout=dout, dy2c=dy2c, dy1=dy1, gw=gw, gb=gb)
+
+
+def _item_bwd_check(ops, c, dy2, dy1, gw, gb):
+    assert rel(dy2.float(), c["dy2c"].float()) < 1e-2
+    assert ((dy2.float() - c["dy2c"].float()).abs() >
+            2 ** -7 * c["dy2c"].float().abs() + 1e-6).float().mean().item() < 1e-2   # ≤ 1 bf16 ulp
+    assert rel(dy1, c["dy1"]) < 5e-3
+    assert rel(gw, c["gw"]) < 1e-4 and rel(gb, c["gb"]) < 1e-4
+
+
+@pytest.mark.parametrize("B", [512, 300, 37, 2])
+def test_item_head_bwd_c_matches_ops(gpu_pkg, B):
+    """ttmi_item_head_bwd_c (ABI 15) against the ops it replaces in item_fusion_bwd:
+    ttmi_layernorm_bwd (dy2, its bf16 copy, the LN weight / bias gradients) and the Linear-4
+    input-gradient GEMM (dy1 = dy2·W4)."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(B + 77)
+    c = _item_bwd_case(ops, B, g)
+    dy2 = torch.full((B, 128), 7, device=DEV, dtype=torch.bfloat16)
+    dy1 = torch.full((B, 512), 7., device=DEV)
+    ws = ops.item_head_bwd_ws(B, DEV)
+    gw, gb = torch.zeros(128, device=DEV), torch.zeros(128, device=DEV)
+    d = ops.item_head_bwd_desc(c["dout"], c["y2"], c["m5"], c["r5"], c["P"]["fusion_layer.5.weight"],
+                               c["W"]["fusion_layer.4.weight.T"], dy2, dy1, ws)
+    ops.item_head_bwd_c(d)
+    ops.ln_sum_folds(ws, (gw, gb), 2, 128)
+    torch.cuda.synchronize()
+    _item_bwd_check(ops, c, dy2, dy1, gw, gb)
+
+
+@pytest.mark.parametrize("B,p,co", [(512, 0.1, False), (37, 0.0, False), (512, 0.1, True)])
+def test_user_head_bwd_fused_matches_ops(gpu_pkg, B, p, co):
     """ttmi_user_head_bwd against the unfused backward ops it replaces (functional's
     _head_bwd_unfused + _layer_tail_bwd for the pruned layer): dctx, dx1, the bf16 dY operands
     of the deferred weight gradients, the LayerNorm parameter gradients (folded per-block sums)
@@ -707,13 +801,26 @@ def test_user_head_bwd_fused_matches_ops(gpu_pkg, B, p):
     Gf = grads0()
     site = (F_.site_drop1(1), F_.site_drop2(1))
     dr = tuple((p, sd[k:k + 1]) if p > 0 else ops.NO_DROP for k in site)
+    co_d = None
+    if co:      # ABI 15: the item head's row-local backward rides in the same launch
+        c = _item_bwd_case(ops, B, g)
+        idy2 = torch.full((B, 128), 7, device=DEV, dtype=torch.bfloat16)
+        idy1 = torch.full((B, 512), 7., device=DEV)
+        iws = ops.item_head_bwd_ws(B, DEV)
+        co_d = ops.item_head_bwd_desc(c["dout"], c["y2"], c["m5"], c["r5"], c["P"]["fusion_layer.5.weight"],
+                                      c["W"]["fusion_layer.4.weight.T"], idy2, idy1, iws)
     head = ops.user_head_bwd(du16, dict(az=o["az"], z=o["z"], mz=o["mz"], rz=o["rz"], h=o["h"],
                                         x1=o["x1"], m2=o["m2"], r2=o["r2"]),
                              drows, W, P, pre, gender, country, F_._scale(p), dr,
                              Gf["gender_embedding.weight"], Gf["country_embedding.weight"],
                              (Gf["fusion_layer.1.weight"], Gf["fusion_layer.1.bias"],
-                              Gf[pre + "norm2.weight"], Gf[pre + "norm2.bias"]))
+                              Gf[pre + "norm2.weight"], Gf[pre + "norm2.bias"]), co_item=co_d)
     torch.cuda.synchronize()
+    if co:
+        igw, igb = torch.zeros(128, device=DEV), torch.zeros(128, device=DEV)
+        ops.ln_sum_folds(iws, (igw, igb), 2, 128)
+        torch.cuda.synchronize()
+        _item_bwd_check(ops, c, idy2, idy1, igw, igb)
     assert rel(head["dx1"], dx1_u) < 2e-3
     assert rel(head["dctx"].float(), dctx_u.float()) < 2e-2
     for k in ("fusion_layer.1.weight", "fusion_layer.1.bias", pre + "norm2.weight", pre + "norm2.bias",
