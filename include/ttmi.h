@@ -242,6 +242,16 @@ int64_t ttmi_infonce_workspace(int B, int D);
 int ttmi_infonce_fwd(int B, int D, const float* u, const float* it, const int64_t* user_idx,
                      float inv_tau, float* u_hat, float* i_hat, float* norms, float* logits,
                      float* lse, float* loss, void* ws, hipStream_t stream);
+/* ttmi_infonce_fwd on rows the producers already normalised (ABI 15): u_hat, i_hat [B, D] and
+ * norms [2B] (u norms, then i norms) as the l2norm launch would write them (the fused user /
+ * item heads' u_hat / out_hat outputs); logits, lse, loss, ws as ttmi_infonce_fwd.  counters
+ * (optional, ttmi_infonce_counter_bytes(B) bytes, zero on entry and left zero): the lse / loss
+ * combine runs inside the logits launch (last-arriving workgroups; deterministic order)
+ * instead of a launch of its own.  The backward (ttmi_infonce_bwd / _bwd16) is unchanged. */
+int ttmi_infonce_fwd_pre(int B, int D, const int64_t* user_idx, float inv_tau, const float* u_hat,
+                         const float* i_hat, const float* norms, float* logits, float* lse,
+                         float* loss, void* ws, int32_t* counters, hipStream_t stream);
+int64_t ttmi_infonce_counter_bytes(int B);
 /* Backward given dloss (device scalar; NULL means 1): writes du, di [B,D]. */
 int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat, const float* norms,
                      const float* logits, const float* lse, const int64_t* user_idx,
@@ -581,6 +591,7 @@ typedef struct ttmi_item_head_desc {
   void* modal16; float* z; float* bn_mean; float* bn_rstd; void* y1; float* y2;
   float* out; float* m5; float* r5;
   float* ws;
+  float* out_hat; float* out_norm;   /* ABI 15, optional (NULL): F.normalize(out) and ||out|| */
 } ttmi_item_head_desc;
 int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t stream);
 
@@ -606,6 +617,7 @@ typedef struct ttmi_user_head_desc {
   float d2_p; const uint64_t* d2_seed;
   float* x1; void* a2; float* m2; float* r2; void* h; void* comb; int32_t* rows;
   float* z; void* az; float* mz; float* rz; float* u;
+  float* u_hat; float* u_norm;       /* ABI 15, optional (NULL): F.normalize(u) and ||u|| */
 } ttmi_user_head_desc;
 int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t stream);
 /* Its backward, one launch (ABI 12), from du (bf16 [B, D]) and the forward's saved values:

@@ -32,6 +32,7 @@ struct ItemArgs {
   const float* modal; const bf16_t* w0; const float* b0;
   const bf16_t* y1; const bf16_t* w4; const float* b4; const float* lnw; const float* lnb; float ln_eps;
   bf16_t* m16; float* z; float* y2; float* out; float* m5; float* r5;
+  float* ohat; float* onrm;    // optional: out / max(||out||, eps) and ||out|| (InfoNCE's l2norm)
 };
 
 struct ItemLdsA {
@@ -59,6 +60,7 @@ struct HeadArgs {
   DropParams d1, dff, d2;
   float* x1; bf16_t* a2; float* m2; float* r2; bf16_t* h; bf16_t* comb; int32_t* rows;
   float* z; bf16_t* az; float* mz; float* rz; float* u;
+  float* uhat; float* unrm;    // optional: u / max(||u||, eps) and ||u|| (InfoNCE's l2norm)
   // co-launched item head stage A (ttmi_user_item_head_fwd): workgroups >= nbu run
   // item_a_body on row block (l % it_nblk), column quarter (l / it_nblk)
   ItemArgs it; int nbu, it_nblk;
@@ -130,6 +132,30 @@ TTMI_DEV float row_sum(float s, LDS& L, int w, int lane) {
   __syncthreads();
   return tot;
 }
+// F.normalize of the row values x (2 tiles x 4 per lane, columns n0 + 16t + 4g + e) as
+// ttmi_infonce_fwd's l2norm writes it (eps 1e-12): xhat rows and the norms.  Every thread
+// calls it (row_sum barriers); no-op outputs when xhat is NULL.
+template <class LDS>
+TTMI_DEV void row_l2norm(const float (&x)[2][4], float* xhat, float* nrm, int m, bool mrow, int n0,
+                         LDS& L, int w, int lane) {
+  if (xhat == nullptr) return;                     // uniform: a kernel argument
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += x[t][e] * x[t][e];
+  const float nr = sqrtf(row_sum(s, L, w, lane));
+  const float inv = 1.f / fmaxf(nr, 1e-12f);
+  const int g = lane >> 4;
+  if (mrow) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      *reinterpret_cast<float4*>(xhat + (int64_t)m * HD + n0 + 16 * t + 4 * g) =
+          make_float4(x[t][0] * inv, x[t][1] * inv, x[t][2] * inv, x[t][3] * inv);
+    if (lane < 16 && w == 0) nrm[m] = nr;
+  }
+}
+
 // LayerNorm of the row values v (2 tiles x 4 per lane); returns mean / rstd.
 template <class LDS>
 TTMI_DEV void row_ln(f32x4_t (&v)[2], const float* w_, const float* b_, float eps, bool relu,
@@ -390,13 +416,16 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
   STAMP(5);
   // ---- u = az·Wf3ᵀ + bf3
   head_gemm<2, HD, PD>(L.sA, wf3, v, lane);
+  float uo[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) uo[t][e] = v[t][e] + Q.bf3[n + e];
     if (mrow)
-      *reinterpret_cast<float4*>(a.u + (int64_t)m * HD + n) =
-          make_float4(v[t][0] + Q.bf3[n], v[t][1] + Q.bf3[n + 1], v[t][2] + Q.bf3[n + 2], v[t][3] + Q.bf3[n + 3]);
+      *reinterpret_cast<float4*>(a.u + (int64_t)m * HD + n) = make_float4(uo[t][0], uo[t][1], uo[t][2], uo[t][3]);
   }
+  row_l2norm(uo, a.uhat, a.unrm, m, mrow, n0, L, w, lane);
 #ifdef HEAD_STAMP
   __syncthreads();
   STAMP(6);
@@ -824,15 +853,17 @@ __global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
       qv += d * d;
     }
   const float rs = 1.f / sqrtf(row_sum(qv, L, w, lane) * (1.f / HD) + a.ln_eps);
+  float oo[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n = n0 + 16 * t + 4 * g;
-    float o[4];
+    float* o = oo[t];
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[t][e] - mu) * rs * lw[t][e] + lb[t][e];
     if (mrow) *reinterpret_cast<float4*>(a.out + (int64_t)m * HD + n) = make_float4(o[0], o[1], o[2], o[3]);
   }
   if (mrow && lane < 16 && w == 0) { a.m5[m] = mu; a.r5[m] = rs; }
+  row_l2norm(oo, a.ohat, a.onrm, m, mrow, n0, L, w, lane);
 }
 
 }  // namespace
@@ -844,7 +875,7 @@ int item_fwd_check(const ttmi_item_head_desc* d) {
                "ttmi_item_head_fwd: needs B > 1 (training BatchNorm), K == N1 == %d, D == %d", IK, HD);
   TTMI_REQUIRE(d->modal && d->w0 && d->b0 && d->bn_w && d->bn_b && d->w4 && d->b4 && d->ln_w && d->ln_b &&
                d->modal16 && d->z && d->bn_mean && d->bn_rstd && d->y1 && d->y2 && d->out && d->m5 &&
-               d->r5, "ttmi_item_head_fwd: null argument");
+               d->r5 && (!d->out_hat || d->out_norm), "ttmi_item_head_fwd: null argument");
   return TTMI_OK;
 }
 ItemArgs item_args(const ttmi_item_head_desc* d) {
@@ -854,6 +885,7 @@ ItemArgs item_args(const ttmi_item_head_desc* d) {
   a.y1 = (const bf16_t*)d->y1; a.w4 = (const bf16_t*)d->w4; a.b4 = d->b4;
   a.lnw = d->ln_w; a.lnb = d->ln_b; a.ln_eps = d->ln_eps;
   a.m16 = (bf16_t*)d->modal16; a.z = d->z; a.y2 = d->y2; a.out = d->out; a.m5 = d->m5; a.r5 = d->r5;
+  a.ohat = d->out_hat; a.onrm = d->out_hat ? d->out_norm : nullptr;
   return a;
 }
 int item_bwd_check(const ttmi_item_head_bwd_desc* d) {
@@ -939,6 +971,8 @@ extern "C" int ttmi_user_item_head_fwd(const ttmi_user_head_desc* d, const ttmi_
   a.x1 = d->x1; a.a2 = (bf16_t*)d->a2; a.m2 = d->m2; a.r2 = d->r2; a.h = (bf16_t*)d->h;
   a.comb = (bf16_t*)d->comb; a.rows = d->rows; a.z = d->z; a.az = (bf16_t*)d->az;
   a.mz = d->mz; a.rz = d->rz; a.u = d->u;
+  a.uhat = d->u_hat; a.unrm = d->u_hat ? d->u_norm : nullptr;
+  TTMI_REQUIRE(!d->u_hat || d->u_norm, "ttmi_user_head_fwd: u_hat needs u_norm");
   a.nbu = (d->B + HR - 1) / HR;
   a.it_nblk = 1;
   int extra = 0;

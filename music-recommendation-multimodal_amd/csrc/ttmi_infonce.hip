@@ -281,12 +281,23 @@ TTMI_DEV void online_merge(float& m, float& s, float m2, float s2) {
   m = M;
 }
 
+// Agent-scope relaxed atomic store / load of a float (visible to every XCD without a cache
+// writeback fence).
+TTMI_DEV void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+TTMI_DEV float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int DC, bool VEC>
 __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __restrict__ uh,
                                                       const float* __restrict__ ih,
                                                       const int64_t* __restrict__ uid,
                                                       float inv_tau, float* __restrict__ logits,
-                                                      float* __restrict__ part) {
+                                                      float* __restrict__ part, int* __restrict__ cnt,
+                                                      float* __restrict__ qsum, float* __restrict__ lse,
+                                                      float* __restrict__ loss) {
   constexpr int D = 16 * DC, QP = D * 4 + 16;
   __shared__ __attribute__((aligned(16))) char sq[NQ * QP];
   __shared__ float sm[4][NQ], ss[4][NQ], st[4][NQ];
@@ -360,9 +371,72 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
 #pragma unroll
     for (int w = 1; w < 4; ++w) { online_merge(M, S_, sm[w][tid], ss[w][tid]); T += st[w][tid]; }
     const int64_t row = (int64_t)dir * B + i0 + tid;
-    part[(0 * NSPLIT + split) * 2 * (int64_t)B + row] = M;
-    part[(1 * NSPLIT + split) * 2 * (int64_t)B + row] = S_;
-    part[(2 * NSPLIT + split) * 2 * (int64_t)B + row] = T;
+    if (cnt == nullptr) {
+      part[(0 * NSPLIT + split) * 2 * (int64_t)B + row] = M;
+      part[(1 * NSPLIT + split) * 2 * (int64_t)B + row] = S_;
+      part[(2 * NSPLIT + split) * 2 * (int64_t)B + row] = T;
+    } else {                                         // read by another XCD's workgroup
+      st_agent(part + (0 * NSPLIT + split) * 2 * (int64_t)B + row, M);
+      st_agent(part + (1 * NSPLIT + split) * 2 * (int64_t)B + row, S_);
+      st_agent(part + (2 * NSPLIT + split) * 2 * (int64_t)B + row, T);
+    }
+  }
+  if (cnt == nullptr) return;                        // nce_combine_kernel follows
+  // ---- the combine in the same launch (ABI 15): the last of a query block's NSPLIT
+  // workgroups (arrival count) merges its 16 rows into lse and their CE sum; the last query
+  // block adds the per-block sums in block order (deterministic).  Each last arriver resets
+  // its counter.  Cross-XCD visibility without fences: the exchanged values are agent-scope
+  // relaxed atomic stores / loads (coherent at the memory side, sc1), the stores are retired
+  // (vmcnt(0)) before the arrival increment.  (A __threadfence pair instead wrote back the
+  // whole L2 per workgroup: 8.7 -> 43 us.)
+  __shared__ int s_last;
+  const int nqb = 2 * nb;
+  __builtin_amdgcn_s_waitcnt(0);                     // every counter at zero: stores retired
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(cnt + qb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NSPLIT - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (tid < 64) {
+    float c = 0.f;
+    if (tid < NQ && i0 + tid < B) {
+      const int64_t n2 = 2 * (int64_t)B, row = (int64_t)dir * B + i0 + tid;
+      float pm[NSPLIT], ps[NSPLIT], T = 0.f;
+#pragma unroll
+      for (int k = 0; k < NSPLIT; ++k) {
+        pm[k] = ld_agent(part + (0 * NSPLIT + k) * n2 + row);
+        ps[k] = ld_agent(part + (1 * NSPLIT + k) * n2 + row);
+        T += ld_agent(part + (2 * NSPLIT + k) * n2 + row);
+      }
+      float M = -INFINITY, S_ = 0.f;
+#pragma unroll
+      for (int k = 0; k < NSPLIT; ++k) online_merge(M, S_, pm[k], ps[k]);
+      const float l = M + logf(S_);
+      lse[row] = l;
+      c = l - T;
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (tid == 0) {
+      st_agent(qsum + qb, c);
+      __hip_atomic_store(cnt + qb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(cnt + nqb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nqb - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (tid < 64) {
+    float c = 0.f;
+    for (int q = tid; q < nqb; q += 64) c += ld_agent(qsum + q);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (tid == 0) {
+      loss[0] = c * (0.5f / (float)B);
+      __hip_atomic_store(cnt + nqb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -601,23 +675,29 @@ extern "C" int64_t ttmi_infonce_workspace(int B, int D) {
   return al((int64_t)B * B * 4) + al((int64_t)2 * B * 4) + 2 * al((int64_t)B * D * 4);
 }
 
-extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
-                                const int64_t* user_idx, float inv_tau, float* u_hat,
-                                float* i_hat, float* norms, float* logits, float* lse, float* loss,
-                                void* ws, hipStream_t s) {
+namespace {
+int infonce_fwd_impl(int B, int D, const float* u, const float* it, const int64_t* user_idx,
+                     float inv_tau, float* u_hat, float* i_hat, float* norms, float* logits,
+                     float* lse, float* loss, void* ws, bool normalise, int32_t* counters,
+                     hipStream_t s) {
   TTMI_REQUIRE(B > 0 && D > 0 && D <= 4096 && D % 4 == 0 && (B % 4 == 0 || fused_ok(B, D)),
                "ttmi_infonce_fwd: need D %% 4 == 0, D <= 4096, and B %% 4 == 0 unless D %% 64 == 0 and D <= 256");
-  TTMI_REQUIRE(u && it && u_hat && i_hat && norms && logits && lse && loss && ws,
+  TTMI_REQUIRE((!normalise || (u && it)) && u_hat && i_hat && norms && logits && lse && loss && ws,
                "ttmi_infonce_fwd: null argument");
-  hipLaunchKernelGGL(l2norm_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u, it, u_hat, i_hat,
-                     norms);
-  int rc = ttmi_check_launch("ttmi_infonce_fwd/l2norm");
-  if (rc) return rc;
+  int rc = TTMI_OK;
+  if (normalise) {
+    hipLaunchKernelGGL(l2norm_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, s, B, D, u, it, u_hat, i_hat,
+                       norms);
+    rc = ttmi_check_launch("ttmi_infonce_fwd/l2norm");
+    if (rc) return rc;
+  }
   if (fused_ok(B, D)) {
     float* part = static_cast<float*>(ws);
     const int nb = (B + NQ - 1) / NQ;
     const dim3 grid(2 * nb * NSPLIT);
-#define TTMI_NCE_FWD(DC, V) hipLaunchKernelGGL((nce_fwd_kernel<DC, V>), grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part)
+    // per-query-block CE sums of the fused combine: scratch in the backward's partial region
+    float* qsum = reinterpret_cast<float*>(static_cast<char*>(ws) + (((int64_t)3 * NSPLIT * 2 * B * 4 + 255) / 256 * 256));
+#define TTMI_NCE_FWD(DC, V) hipLaunchKernelGGL((nce_fwd_kernel<DC, V>), grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part, counters, qsum, lse, loss)
 #define TTMI_NCE_FWD2(DC) do { if (B % 4 == 0) TTMI_NCE_FWD(DC, true); else TTMI_NCE_FWD(DC, false); } while (0)
     switch (D / 16) {
       case 4: TTMI_NCE_FWD2(4); break;
@@ -628,7 +708,7 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
 #undef TTMI_NCE_FWD2
 #undef TTMI_NCE_FWD
     rc = ttmi_check_launch("ttmi_infonce_fwd/rows");
-    if (rc) return rc;
+    if (rc || counters) return rc;
     hipLaunchKernelGGL(nce_combine_kernel, dim3(1), dim3(1024), 0, s, B, part, lse, loss);
     return ttmi_check_launch("ttmi_infonce_fwd/combine");
   }
@@ -643,6 +723,29 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
   if (rc) return rc;
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, 2 * B, w.ce, 0.5f / (float)B, loss);
   return ttmi_check_launch("ttmi_infonce_fwd/loss");
+}
+}  // namespace
+
+extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
+                                const int64_t* user_idx, float inv_tau, float* u_hat,
+                                float* i_hat, float* norms, float* logits, float* lse, float* loss,
+                                void* ws, hipStream_t s) {
+  return infonce_fwd_impl(B, D, u, it, user_idx, inv_tau, u_hat, i_hat, norms, logits, lse, loss,
+                          ws, true, nullptr, s);
+}
+
+extern "C" int64_t ttmi_infonce_counter_bytes(int B) {
+  return B > 0 ? (int64_t)(2 * ((B + NQ - 1) / NQ) + 1) * 4 : 0;
+}
+
+extern "C" int ttmi_infonce_fwd_pre(int B, int D, const int64_t* user_idx, float inv_tau,
+                                    const float* u_hat, const float* i_hat, const float* norms,
+                                    float* logits, float* lse, float* loss, void* ws,
+                                    int32_t* counters, hipStream_t s) {
+  TTMI_REQUIRE(((uintptr_t)counters & 3) == 0, "ttmi_infonce_fwd_pre: counters need 4-byte alignment");
+  return infonce_fwd_impl(B, D, nullptr, nullptr, user_idx, inv_tau, const_cast<float*>(u_hat),
+                          const_cast<float*>(i_hat), const_cast<float*>(norms), logits, lse, loss,
+                          ws, false, counters, s);
 }
 
 extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float* i_hat,

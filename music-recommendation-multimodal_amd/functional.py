@@ -13,7 +13,7 @@ mirror, or ``P`` itself in fp32 mode).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 
@@ -128,6 +128,7 @@ class UserSaved:
     rz: Optional[Tensor] = None
     az: Optional[Tensor] = None
     seeds: Optional[Tensor] = None
+    normed: bool = False          # the fused head also wrote InfoNCE's l2norm of u
 
 
 def transposed_name(name: str) -> str:
@@ -168,10 +169,12 @@ def _resln_ok(W: Dict[str, Tensor], name: str, D: int) -> bool:
 
 def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gender: Tensor,
                    country: Tensor, mask: Optional[Tensor], cfg: TowerCfg,
-                   seeds: Optional[Tensor] = None, co_item: Optional["ItemHeadPending"] = None):
+                   seeds: Optional[Tensor] = None, co_item: Optional["ItemHeadPending"] = None,
+                   normed: Optional[Tuple[Tensor, Tensor]] = None):
     """SequentialUserEncoder.forward (reference user_tower.py:73-144), train mode.  ``co_item``
     (item_fusion_fwd_begin): the item head's first stage rides in the fused user head launch
-    when that path runs (``co_item.a_done`` tells item_fusion_fwd_end)."""
+    when that path runs (``co_item.a_done`` tells item_fusion_fwd_end).  ``normed`` = (u_hat,
+    norms[:B]): that launch also writes InfoNCE's l2norm of u (``st.normed`` says so)."""
     dev = ids.device
     B, L = ids.shape
     D, H, dt = cfg.D, cfg.H, cfg.dtype
@@ -231,9 +234,11 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                 ops.user_head_fwd(ctx, res_in, drows, W, P, pre, gender, country, cfg.eps,
                                   (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_ffn(i)),
                                    _drop(cfg, seeds, site_drop2(i))), o,
-                                  co_item=co_item.desc if co_item is not None else None)
+                                  co_item=co_item.desc if co_item is not None else None,
+                                  normed=normed)
                 if co_item is not None:
                     co_item.a_done = True
+                st.normed = normed is not None
                 st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, o["x1"], o["a2"], o["m2"],
                                             o["r2"], o["h"], rows))
                 st.comb, st.rows, st.z = o["comb"], o["rows"], o["z"]
@@ -548,9 +553,11 @@ class ItemHeadPending:
 def item_fusion_fwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Tensor, cfg: TowerCfg,
                           seeds: Optional[Tensor] = None,
                           buffers: Optional[Dict[str, Tensor]] = None,
-                          p_drop: float = 0.1) -> Optional[ItemHeadPending]:
+                          p_drop: float = 0.1,
+                          normed: Optional[Tuple[Tensor, Tensor]] = None) -> Optional[ItemHeadPending]:
     """item_fusion_fwd (training) as a pending co-launch, or None when the fused head does not
-    take these shapes (then call item_fusion_fwd)."""
+    take these shapes (then call item_fusion_fwd).  ``normed`` = (i_hat, norms[B:]): stage C
+    also writes InfoNCE's l2norm of the item embedding."""
     if not ops.item_head_fusable(W, modal, cfg.dtype):
         return None
     dev = modal.device
@@ -561,6 +568,8 @@ def item_fusion_fwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Ten
              bn_mean=torch.empty(H1, **f32), bn_rstd=torch.empty(H1, **f32),
              y1=torch.empty(B, H1, device=dev, dtype=cfg.dtype), y2=torch.empty(B, D, **f32),
              out=torch.empty(B, D, **f32), m5=torch.empty(B, **f32), r5=torch.empty(B, **f32))
+    if normed is not None:
+        o["out_hat"], o["out_norm"] = normed
     m = modal.contiguous()
     d = ops.item_head_desc(m, W, P, buffers or {}, _drop(cfg, seeds, SITE_ITEM, p_drop), cfg.eps, o)
     return ItemHeadPending(d, o, m, seeds)
@@ -673,16 +682,21 @@ class LossSaved:
     inv_tau: float
 
 
-def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float = 0.07):
+def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float = 0.07,
+                normed: Optional[Tuple[Tensor, Tensor, Tensor]] = None):
     """TwoTowerModel.forward loss part (reference two_tower.py:98-140): fused kernels — one
     normalise launch, one f32-MFMA logits + masked row/column softmax-statistics launch, one
-    combine launch (ttmi_infonce_fwd)."""
+    combine launch (ttmi_infonce_fwd).  ``normed`` = (u_hat, i_hat, norms) already written by
+    the fused heads: the normalise launch is skipped (ttmi_infonce_fwd_pre)."""
     dev = u.device
     B, D = u.shape
     f32 = dict(device=dev, dtype=torch.float32)
-    u_hat = torch.empty(B, D, **f32)
-    i_hat = torch.empty(B, D, **f32)
-    norms = torch.empty(2 * B, **f32)
+    if normed is not None:
+        u_hat, i_hat, norms = normed
+    else:
+        u_hat = torch.empty(B, D, **f32)
+        i_hat = torch.empty(B, D, **f32)
+        norms = torch.empty(2 * B, **f32)
     logits = torch.empty(B, B, **f32)
     lse = torch.empty(2 * B, **f32)
     loss = torch.empty((), **f32)
@@ -690,8 +704,11 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: 
     if user_idx is not None and user_idx.dtype != torch.int64:
         user_idx = user_idx.to(torch.int64)
     inv_tau = 1.0 / temperature
-    ops.infonce_fwd(u.contiguous(), it.contiguous(), user_idx, inv_tau, u_hat, i_hat, norms, logits,
-                    lse, loss, ws)
+    if normed is not None:
+        ops.infonce_fwd_pre(user_idx, inv_tau, u_hat, i_hat, norms, logits, lse, loss, ws)
+    else:
+        ops.infonce_fwd(u.contiguous(), it.contiguous(), user_idx, inv_tau, u_hat, i_hat, norms,
+                        logits, lse, loss, ws)
     return loss, logits, u_hat, i_hat, LossSaved(u_hat, i_hat, norms, logits, lse, user_idx, ws,
                                                  inv_tau)
 

@@ -87,7 +87,8 @@ class ItemHeadDesc(ctypes.Structure):
                 ("drop_p", ctypes.c_float), ("drop_seed", c_p),
                 ("w4", c_p), ("b4", c_p), ("ln_w", c_p), ("ln_b", c_p), ("ln_eps", ctypes.c_float),
                 ("modal16", c_p), ("z", c_p), ("bn_mean", c_p), ("bn_rstd", c_p), ("y1", c_p), ("y2", c_p),
-                ("out", c_p), ("m5", c_p), ("r5", c_p), ("ws", c_p)]
+                ("out", c_p), ("m5", c_p), ("r5", c_p), ("ws", c_p),
+                ("out_hat", c_p), ("out_norm", c_p)]
 
 
 class ItemHeadBwdDesc(ctypes.Structure):
@@ -111,7 +112,8 @@ class UserHeadDesc(ctypes.Structure):
                 ("dff_p", ctypes.c_float), ("dff_seed", c_p),
                 ("d2_p", ctypes.c_float), ("d2_seed", c_p),
                 ("x1", c_p), ("a2", c_p), ("m2", c_p), ("r2", c_p), ("h", c_p), ("comb", c_p),
-                ("rows", c_p), ("z", c_p), ("az", c_p), ("mz", c_p), ("rz", c_p), ("u", c_p)]
+                ("rows", c_p), ("z", c_p), ("az", c_p), ("mz", c_p), ("rz", c_p), ("u", c_p),
+                ("u_hat", c_p), ("u_norm", c_p)]
 
 
 class UserHeadBwdDesc(ctypes.Structure):
@@ -201,6 +203,8 @@ SIGNATURES = {
                                  c_p, c_p]),
     "ttmi_infonce_workspace": (c_i64, [c_i, c_i]),
     "ttmi_infonce_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_infonce_fwd_pre": (c_i, [c_i, c_i, c_p, ctypes.c_float, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_infonce_counter_bytes": (ctypes.c_int64, [c_i]),
     "ttmi_infonce_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_infonce_bwd16": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),

@@ -552,6 +552,8 @@ def item_head_desc(modal: Tensor, W: Dict[str, Tensor], P: Dict[str, Tensor],
     d.modal16, d.z, d.bn_mean, d.bn_rstd = _p(out["m16"]), _p(out["z"]), _p(out["bn_mean"]), _p(out["bn_rstd"])
     d.y1, d.y2, d.out, d.m5, d.r5 = _p(out["y1"]), _p(out["y2"]), _p(out["out"]), _p(out["m5"]), _p(out["r5"])
     d.ws = None
+    if "out_hat" in out:       # InfoNCE's l2norm of the item embedding, in stage C (ABI 15)
+        d.out_hat, d.out_norm = _p(out["out_hat"]), _p(out["out_norm"])
     return d
 
 
@@ -648,6 +650,18 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], inv_tau: floa
     B, D = u.shape
     call("ttmi_infonce_fwd", B, D, _p(u), _p(it), _p(user_idx), inv_tau, _p(u_hat), _p(i_hat),
          _p(norms), _p(logits), _p(lse), _p(loss), _p(ws), _s())
+
+
+def infonce_fwd_pre(user_idx: Optional[Tensor], inv_tau: float, u_hat: Tensor, i_hat: Tensor,
+                    norms: Tensor, logits: Tensor, lse: Tensor, loss: Tensor, ws: Tensor,
+                    fused_combine: bool = True):
+    """infonce_fwd on rows already normalised by their producers (ttmi_infonce_fwd_pre); with
+    ``fused_combine`` the lse / loss combine runs inside the logits launch (persistent zero
+    arrival counters)."""
+    B, D = u_hat.shape
+    cnt = _zero_ws("ttmi_infonce_counter_bytes", (B,), u_hat.device) if fused_combine else None
+    call("ttmi_infonce_fwd_pre", B, D, _p(user_idx), inv_tau, _p(u_hat), _p(i_hat), _p(norms),
+         _p(logits), _p(lse), _p(loss), _p(ws), _p(cnt), _s())
 
 
 def infonce_bwd(u_hat: Tensor, i_hat: Tensor, norms: Tensor, logits: Tensor, lse: Tensor,
@@ -890,7 +904,8 @@ def dis_attn(B: int, S: int, nh: int, q: Tensor, k: Tensor, v: Tensor, posq: Ten
 def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict[str, Tensor],
                   P: Dict[str, Tensor], pre: str, gender: Tensor, country: Tensor, eps: float,
                   drops: Tuple[Drop, Drop, Drop], out: Dict[str, Tensor],
-                  co_item: Optional[ItemHeadDesc] = None) -> None:
+                  co_item: Optional[ItemHeadDesc] = None,
+                  normed: Optional[Tuple[Tensor, Tensor]] = None) -> None:
     """The user tower head in one launch (ttmi_user_head_fwd): the pruned last layer's
     out-proj + residual + norm2 + FFN on the gathered rows, the demographic concat and the
     fusion MLP.  ``pre`` is the last layer's parameter prefix; ``out`` holds x1, a2, m2, r2, h,
@@ -915,6 +930,8 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
     d.d1_seed, d.dff_seed, d.d2_seed = _p(d1), _p(dff), _p(d2)
     for k in ("x1", "a2", "m2", "r2", "h", "comb", "rows", "z", "az", "mz", "rz", "u"):
         setattr(d, k, _p(out[k]))
+    if normed is not None:     # (u_hat [B, D], norms [B]): InfoNCE's l2norm of u, same launch
+        d.u_hat, d.u_norm = _p(normed[0]), _p(normed[1])
     if co_item is None:
         call("ttmi_user_head_fwd", ctypes.byref(d), _s())
     else:      # item head stage A on the CUs the 16-row user blocks leave idle (ABI 15)

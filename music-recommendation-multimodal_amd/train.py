@@ -394,11 +394,20 @@ class TrainStep:
         if self.broadcast_buffers:             # rank 0's buffers from the last all-reduce
             ops.batch_copy([self.fbufs.data], [self.bstage])
         # cfg 2: the item head's first stage rides in the user head launch (idle CUs)
+        # and both heads also write InfoNCE's l2norm of their rows (no normalise launch)
+        normed = None
+        if not self.raw_items and not self.global_negatives:
+            B, D = b["history_ids"].shape[0], self.ucfg.D
+            normed = (torch.empty(B, D, device=self.device), torch.empty(B, D, device=self.device),
+                      torch.empty(2 * B, device=self.device))
         co = None if self.raw_items else F.item_fusion_fwd_begin(
-            self.Pi, self.Wi, b["target_modal"], self.icfg, seeds, self.bufs, self.p_item)
+            self.Pi, self.Wi, b["target_modal"], self.icfg, seeds, self.bufs, self.p_item,
+            normed=(normed[1], normed[2][B:]) if normed is not None else None)
         u, ust = F.user_tower_fwd(self.Pu, self.Wu, b["history_ids"], b["user_gender"],
                                   b["user_country"], b.get("history_mask"), self.ucfg, seeds,
-                                  co_item=co)
+                                  co_item=co, normed=(normed[0], normed[2][:B]) if co is not None and
+                                  normed is not None else None)
+        self._normed = normed if co is not None and ust.normed else None
         if self.raw_items:
             modal, rst = self._raw_items_fwd(b, seeds)
         else:
@@ -428,7 +437,7 @@ class TrainStep:
             F.infonce_global_norm_bwd(gst, du, di)
         else:
             loss, logits, _, _, lst = F.infonce_fwd(u, it, b.get("user_idx"),
-                                                    self.model.temperature)
+                                                    self.model.temperature, normed=self._normed)
             du16 = torch.empty(u.shape, device=u.device, dtype=self.ucfg.dtype) \
                 if self.ucfg.dtype == torch.bfloat16 else None
             F.infonce_bwd(lst, self.dloss, du, di, du16)

@@ -602,8 +602,12 @@ def test_user_head_fused_matches_ops(gpu_pkg, B, p, co):
         Wi, Pi, modal, drop_i, bufs = _item_head_inputs(ops, B, g, p)
         iw, ig = _item_head_outs(B), _item_head_outs(B)
         ops.item_head_fwd(modal, Wi, Pi, bufs(), drop_i, 1e-5, iw)
+        norms = torch.full((2 * B,), 7., device=DEV)
+        uh, ih = torch.full((B, D), 7., device=DEV), torch.full((B, D), 7., device=DEV)
+        ig["out_hat"], ig["out_norm"] = ih, norms[B:]          # InfoNCE's l2norm in stage C
         d = ops.item_head_desc(modal, Wi, Pi, bufs(), drop_i, 1e-5, ig)
-        ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, out, co_item=d)
+        ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, out, co_item=d,
+                          normed=(uh, norms[:B]))
         ops.item_head_fwd_stages(d, 6)
         solo = {k: torch.full_like(v, 7) for k, v in want.items()}
         ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, solo)
@@ -614,6 +618,20 @@ def test_user_head_fused_matches_ops(gpu_pkg, B, p, co):
             assert torch.equal(ig[k], iw[k]), k
         for k in ("bn_mean", "bn_rstd", "y2", "out", "m5", "r5"):
             assert rel(ig[k], iw[k]) < 1e-6, k
+        # the heads' l2norm outputs = F.normalize (eps 1e-12) and the row norms
+        for x, xh, nr in ((out["u"], uh, norms[:B]), (ig["out"], ih, norms[B:])):
+            assert rel(xh, torch.nn.functional.normalize(x, dim=1)) < 1e-6
+            assert rel(nr, x.norm(dim=1)) < 1e-6
+        # ttmi_infonce_fwd_pre on them = ttmi_infonce_fwd from the raw rows
+        F_ = gpu_pkg.functional
+        # (its lse / loss combine runs in the logits launch: arrival counters, reset by the last
+        # arrivers, so a second call must agree too)
+        l0, lg0, _, _, s0 = F_.infonce_fwd(out["u"], ig["out"], None, 0.07)
+        for _ in range(2):
+            l1, lg1, _, _, s1 = F_.infonce_fwd(out["u"], ig["out"], None, 0.07, normed=(uh, ih, norms))
+            torch.cuda.synchronize()
+            assert abs(float(l1) - float(l0)) <= 1e-6 * max(1.0, abs(float(l0)))
+            assert rel(lg1, lg0) < 1e-6 and rel(s1.lse, s0.lse) < 1e-6
     else:
         ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, out)
     torch.cuda.synchronize()
