@@ -592,7 +592,13 @@ typedef struct ttmi_item_head_desc {
   float* out; float* m5; float* r5;
   float* ws;
   float* out_hat; float* out_norm;   /* ABI 15, optional (NULL): F.normalize(out) and ||out|| */
+  /* ABI 15, optional (NULL: a separate BatchNorm launch): with B <= 512 the BatchNorm batch
+   * statistics are merged inside stage A (bn_part [ttmi_item_head_bn_part_floats(B)] scratch,
+   * bn_cnt [ttmi_item_head_bn_counter_bytes] zero on entry and left zero) and applied in C. */
+  float* bn_part; int32_t* bn_cnt;
 } ttmi_item_head_desc;
+int64_t ttmi_item_head_bn_part_floats(int B);
+int64_t ttmi_item_head_bn_counter_bytes(int B);
 int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t stream);
 
 /* User tower head, one launch (ABI 12; reference user_tower.py:37-57, :131-144) on the B

@@ -33,10 +33,18 @@ struct ItemArgs {
   const bf16_t* y1; const bf16_t* w4; const float* b4; const float* lnw; const float* lnb; float ln_eps;
   bf16_t* m16; float* z; float* y2; float* out; float* m5; float* r5;
   float* ohat; float* onrm;    // optional: out / max(||out||, eps) and ||out|| (InfoNCE's l2norm)
+  // fused BatchNorm (ABI 15; bncnt NULL: the separate bnr_fwd launch): stage A leaves per-block
+  // column (mean, M2) in bnpart, the last row block of a column quarter merges them into the
+  // batch statistics; stage C applies BN + ReLU + dropout while staging z rows
+  const float* bnw; const float* bnb; float bn_eps, bn_mom;
+  float* rmean; float* rvar; int64_t* nbt; float* bmean; float* brstd; bf16_t* y1w;
+  DropParams bd;
+  float* bnpart; int* bncnt;
 };
 
 struct ItemLdsA {
   char sA[HR * PI];
+  int s_last;
 };
 
 // Item head backward's row-local part (ttmi_item_head_bwd_c): the LayerNorm backward of
@@ -202,6 +210,14 @@ TTMI_DEV void vec_st(float* dst, const float4& v, int tid) {
   reinterpret_cast<float4*>(dst)[tid & (N / 4 - 1)] = v;
 }
 
+constexpr int BN_MAXBLK = 32;          // fused BatchNorm statistics: B <= 512
+TTMI_DEV void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+TTMI_DEV float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Item head stage A on row block bx, column quarter q (item_head_a_kernel, or the workgroups
 // of ttmi_user_item_head_fwd past the user head's).
 TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
@@ -227,6 +243,66 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   if (m < a.B)
     *reinterpret_cast<float4*>(a.z + (int64_t)m * IN1 + n0 + 4 * g) =
         make_float4(v[0][0] + bias.x, v[0][1] + bias.y, v[0][2] + bias.z, v[0][3] + bias.w);
+  if (a.bncnt == nullptr) return;
+  // ---- fused BatchNorm statistics: this block's (mean, M2) of its 4 x 16 columns over its
+  // valid rows (the 16 lanes of a lane group share the columns), exchanged through agent-scope
+  // relaxed atomics (cross-XCD, no cache-writeback fence); the last of the column quarter's
+  // row blocks merges them in block order (Chan et al.'s pairwise update: deterministic).
+  const int nv = min(HR, a.B - r0);
+  const float bv[4] = {bias.x, bias.y, bias.z, bias.w};
+  float bm[4], b2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = m < a.B ? v[0][e] + bv[e] : 0.f;
+    float s = x;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
+    bm[e] = s / (float)nv;
+    const float d = m < a.B ? x - bm[e] : 0.f;
+    float q2 = d * d;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) q2 += __shfl_xor(q2, off, 64);
+    b2[e] = q2;
+  }
+  if (li == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      st_agent(a.bnpart + (int64_t)(2 * bx) * IN1 + n0 + 4 * g + e, bm[e]);
+      st_agent(a.bnpart + (int64_t)(2 * bx + 1) * IN1 + n0 + 4 * g + e, b2[e]);
+    }
+  }
+  const int nblk = (a.B + HR - 1) / HR;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0)
+    L.s_last = __hip_atomic_fetch_add(a.bncnt + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+  __syncthreads();
+  if (!L.s_last || tid >= 64) return;
+  const int c = 64 * q + tid;
+  float pm[BN_MAXBLK], p2[BN_MAXBLK];                // every load in flight first
+#pragma unroll
+  for (int b = 0; b < BN_MAXBLK; ++b) {
+    const int bb = min(b, nblk - 1);
+    pm[b] = ld_agent(a.bnpart + (int64_t)(2 * bb) * IN1 + c);
+    p2[b] = ld_agent(a.bnpart + (int64_t)(2 * bb + 1) * IN1 + c);
+  }
+  float n = 0.f, mean = 0.f, M2 = 0.f;
+#pragma unroll
+  for (int b = 0; b < BN_MAXBLK; ++b) {
+    if (b < nblk) {
+      const float nb = (float)min(HR, a.B - HR * b), tot = n + nb, delta = pm[b] - mean;
+      mean += delta * (nb / tot);
+      M2 += p2[b] + delta * delta * (n * nb / tot);
+      n = tot;
+    }
+  }
+  const float var = M2 / (float)a.B;
+  a.bmean[c] = mean;
+  a.brstd[c] = 1.f / sqrtf(var + a.bn_eps);
+  if (a.rmean) a.rmean[c] = (1.f - a.bn_mom) * a.rmean[c] + a.bn_mom * mean;
+  if (a.rvar) a.rvar[c] = (1.f - a.bn_mom) * a.rvar[c] + a.bn_mom * var * ((float)a.B / (float)(a.B - 1));
+  if (q == 0 && tid == 0 && a.nbt) a.nbt[0] += 1;
+  if (tid == 0) __hip_atomic_store(a.bncnt + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 #ifdef HEAD_STAMP
@@ -804,7 +880,28 @@ __global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = blockIdx.x * HR;
   const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
-  {                                                  // y1 rows: 16 x 64 chunks of 16 bytes
+  if (a.bncnt != nullptr) {      // fused BatchNorm: y1 = drop(relu(BN(z))) staged from z rows
+    float4 zv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+      zv[k] = *reinterpret_cast<const float4*>(a.z + (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4);
+    }
+    const DropKeys dk = resolve_drop(a.bd);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+      const float4 mu = *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
+      const float4 rs = *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
+      const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
+      const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
+      float x[4] = {fmaxf((zv[k].x - mu.x) * rs.x * ww.x + bb.x, 0.f), fmaxf((zv[k].y - mu.y) * rs.y * ww.y + bb.y, 0.f),
+                    fmaxf((zv[k].z - mu.z) * rs.z * ww.z + bb.z, 0.f), fmaxf((zv[k].w - mu.w) * rs.w * ww.w + bb.w, 0.f)};
+      drop_apply_vec<4>(dk, (uint32_t)((int64_t)(r0 + r) * IN1 + 4 * c4), x);
+      st4_bf(L.sY + r * PI + c4 * 8, x);
+      if (r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.y1w + (int64_t)(r0 + r) * IN1 + 4 * c4), x);
+    }
+  } else {                                           // y1 rows: 16 x 64 chunks of 16 bytes
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = tid + 256 * k, r = idx >> 6, ch = idx & 63;
@@ -886,6 +983,13 @@ ItemArgs item_args(const ttmi_item_head_desc* d) {
   a.lnw = d->ln_w; a.lnb = d->ln_b; a.ln_eps = d->ln_eps;
   a.m16 = (bf16_t*)d->modal16; a.z = d->z; a.y2 = d->y2; a.out = d->out; a.m5 = d->m5; a.r5 = d->r5;
   a.ohat = d->out_hat; a.onrm = d->out_hat ? d->out_norm : nullptr;
+  a.bnw = d->bn_w; a.bnb = d->bn_b; a.bn_eps = d->bn_eps; a.bn_mom = d->momentum;
+  a.rmean = d->running_mean; a.rvar = d->running_var; a.nbt = d->num_batches_tracked;
+  a.bmean = d->bn_mean; a.brstd = d->bn_rstd; a.y1w = (bf16_t*)d->y1;
+  a.bd = make_drop(d->drop_p, d->drop_seed ? d->drop_seed : reinterpret_cast<const uint64_t*>(d->b0));
+  const bool fuse = d->bn_part && d->bn_cnt && d->B <= BN_MAXBLK * HR;
+  a.bnpart = fuse ? d->bn_part : nullptr;
+  a.bncnt = fuse ? d->bn_cnt : nullptr;
   return a;
 }
 int item_bwd_check(const ttmi_item_head_bwd_desc* d) {
@@ -917,7 +1021,7 @@ extern "C" int ttmi_item_head_fwd_stages(const ttmi_item_head_desc* d, int stage
     rc = ttmi_check_launch("ttmi_item_head_fwd");
     if (rc != TTMI_OK) return rc;
   }
-  if (stages & 2) {
+  if ((stages & 2) && a.bncnt == nullptr) {          // fused: statistics in A, applied in C
     rc = ttmi_batchnorm_fwd(TTMI_BF16, d->B, IN1, d->z, d->bn_w, d->bn_b, d->bn_eps, d->momentum,
                             d->running_mean, d->running_var, d->num_batches_tracked, 1, 1, d->drop_p,
                             d->drop_seed, d->y1, d->bn_mean, d->bn_rstd, s);
@@ -933,6 +1037,9 @@ extern "C" int ttmi_item_head_fwd_stages(const ttmi_item_head_desc* d, int stage
 extern "C" int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t s) {
   return ttmi_item_head_fwd_stages(d, 7, s);
 }
+
+extern "C" int64_t ttmi_item_head_bn_part_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 2 * IN1; }
+extern "C" int64_t ttmi_item_head_bn_counter_bytes(int B) { (void)B; return (IN1 / 64) * 4; }
 
 extern "C" int64_t ttmi_item_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 2 * HD; }
 

@@ -88,7 +88,7 @@ class ItemHeadDesc(ctypes.Structure):
                 ("w4", c_p), ("b4", c_p), ("ln_w", c_p), ("ln_b", c_p), ("ln_eps", ctypes.c_float),
                 ("modal16", c_p), ("z", c_p), ("bn_mean", c_p), ("bn_rstd", c_p), ("y1", c_p), ("y2", c_p),
                 ("out", c_p), ("m5", c_p), ("r5", c_p), ("ws", c_p),
-                ("out_hat", c_p), ("out_norm", c_p)]
+                ("out_hat", c_p), ("out_norm", c_p), ("bn_part", c_p), ("bn_cnt", c_p)]
 
 
 class ItemHeadBwdDesc(ctypes.Structure):
@@ -232,6 +232,8 @@ SIGNATURES = {
     "ttmi_item_head_fwd_stages": (c_i, [c_p, c_i, c_p]),
     "ttmi_user_item_head_fwd": (c_i, [c_p, c_p, c_p]),
     "ttmi_item_head_bwd_c": (c_i, [c_p, c_p]),
+    "ttmi_item_head_bn_part_floats": (ctypes.c_int64, [c_i]),
+    "ttmi_item_head_bn_counter_bytes": (ctypes.c_int64, [c_i]),
     "ttmi_item_head_bwd_ws_floats": (ctypes.c_int64, [c_i]),
     "ttmi_user_item_head_bwd": (c_i, [c_p, c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),

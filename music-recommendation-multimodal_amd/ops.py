@@ -554,6 +554,12 @@ def item_head_desc(modal: Tensor, W: Dict[str, Tensor], P: Dict[str, Tensor],
     d.ws = None
     if "out_hat" in out:       # InfoNCE's l2norm of the item embedding, in stage C (ABI 15)
         d.out_hat, d.out_norm = _p(out["out_hat"]), _p(out["out_norm"])
+    if B <= 512:               # BatchNorm statistics in stage A, applied in C (no BN launch)
+        _L.load()
+        part = torch.empty(int(_L._lib.ttmi_item_head_bn_part_floats(B)), device=modal.device)
+        out["_bn_part"] = part            # kept alive with the outputs
+        d.bn_part = _p(part)
+        d.bn_cnt = _p(_zero_ws("ttmi_item_head_bn_counter_bytes", (0,), modal.device))
     return d
 
 
