@@ -648,19 +648,20 @@ def main():
     if cfg4:
         batches = add_text(batches, rank, device)
 
-    # warm-up runs the exact timed-loop ops (incl. the loss accumulation: torch loads its
-    # kernels lazily, and a first-use load inside the timed region costs ~75 ms)
-    loss_sum = torch.zeros((), device=device)
+    # warm-up runs the exact timed-loop ops.  The step losses are summed on the device by the
+    # step itself (TrainStep.loss_sum: inside the InfoNCE logits launch on cfg 2, an add in
+    # the captured graph otherwise), read once after the timed region.
     for i in range(max(args.warmup, 1)):
-        loss_sum += step.step(batches[i % len(batches)])
+        step.step(batches[i % len(batches)])
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
-    loss_sum.zero_()
+    step.loss_sum.zero_()
+    torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss_sum += step.step(batches[i % len(batches)])
+        step.step(batches[i % len(batches)])
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -670,7 +671,7 @@ def main():
         t = torch.tensor([el], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
-    mean_loss = float(loss_sum) / max(args.steps, 1)
+    mean_loss = float(step.loss_sum) / max(args.steps, 1)
 
     roof = None
     if rank == 0:

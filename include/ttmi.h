@@ -247,10 +247,13 @@ int ttmi_infonce_fwd(int B, int D, const float* u, const float* it, const int64_
  * item heads' u_hat / out_hat outputs); logits, lse, loss, ws as ttmi_infonce_fwd.  counters
  * (optional, ttmi_infonce_counter_bytes(B) bytes, zero on entry and left zero): the lse / loss
  * combine runs inside the logits launch (last-arriving workgroups; deterministic order)
- * instead of a launch of its own.  The backward (ttmi_infonce_bwd / _bwd16) is unchanged. */
+ * instead of a launch of its own; then loss_acc (optional, device float) += loss in the same
+ * launch (a training loop's running loss sum, src/train.py:68's total_loss, without a host
+ * sync or an add launch per step).  The backward (ttmi_infonce_bwd / _bwd16) is unchanged. */
 int ttmi_infonce_fwd_pre(int B, int D, const int64_t* user_idx, float inv_tau, const float* u_hat,
                          const float* i_hat, const float* norms, float* logits, float* lse,
-                         float* loss, void* ws, int32_t* counters, hipStream_t stream);
+                         float* loss, void* ws, int32_t* counters, float* loss_acc,
+                         hipStream_t stream);
 int64_t ttmi_infonce_counter_bytes(int B);
 /* Backward given dloss (device scalar; NULL means 1): writes du, di [B,D]. */
 int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat, const float* norms,

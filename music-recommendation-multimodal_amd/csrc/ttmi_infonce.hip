@@ -297,7 +297,8 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
                                                       float inv_tau, float* __restrict__ logits,
                                                       float* __restrict__ part, int* __restrict__ cnt,
                                                       float* __restrict__ qsum, float* __restrict__ lse,
-                                                      float* __restrict__ loss) {
+                                                      float* __restrict__ loss,
+                                                      float* __restrict__ loss_acc) {
   constexpr int D = 16 * DC, QP = D * 4 + 16;
   __shared__ __attribute__((aligned(16))) char sq[NQ * QP];
   __shared__ float sm[4][NQ], ss[4][NQ], st[4][NQ];
@@ -434,7 +435,9 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
     if (tid == 0) {
-      loss[0] = c * (0.5f / (float)B);
+      const float lv = c * (0.5f / (float)B);
+      loss[0] = lv;
+      if (loss_acc) loss_acc[0] += lv;               // the caller's running sum (epoch mean)
       __hip_atomic_store(cnt + nqb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -679,7 +682,7 @@ namespace {
 int infonce_fwd_impl(int B, int D, const float* u, const float* it, const int64_t* user_idx,
                      float inv_tau, float* u_hat, float* i_hat, float* norms, float* logits,
                      float* lse, float* loss, void* ws, bool normalise, int32_t* counters,
-                     hipStream_t s) {
+                     float* loss_acc, hipStream_t s) {
   TTMI_REQUIRE(B > 0 && D > 0 && D <= 4096 && D % 4 == 0 && (B % 4 == 0 || fused_ok(B, D)),
                "ttmi_infonce_fwd: need D %% 4 == 0, D <= 4096, and B %% 4 == 0 unless D %% 64 == 0 and D <= 256");
   TTMI_REQUIRE((!normalise || (u && it)) && u_hat && i_hat && norms && logits && lse && loss && ws,
@@ -697,7 +700,7 @@ int infonce_fwd_impl(int B, int D, const float* u, const float* it, const int64_
     const dim3 grid(2 * nb * NSPLIT);
     // per-query-block CE sums of the fused combine: scratch in the backward's partial region
     float* qsum = reinterpret_cast<float*>(static_cast<char*>(ws) + (((int64_t)3 * NSPLIT * 2 * B * 4 + 255) / 256 * 256));
-#define TTMI_NCE_FWD(DC, V) hipLaunchKernelGGL((nce_fwd_kernel<DC, V>), grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part, counters, qsum, lse, loss)
+#define TTMI_NCE_FWD(DC, V) hipLaunchKernelGGL((nce_fwd_kernel<DC, V>), grid, dim3(256), 0, s, B, u_hat, i_hat, user_idx, inv_tau, logits, part, counters, qsum, lse, loss, loss_acc)
 #define TTMI_NCE_FWD2(DC) do { if (B % 4 == 0) TTMI_NCE_FWD(DC, true); else TTMI_NCE_FWD(DC, false); } while (0)
     switch (D / 16) {
       case 4: TTMI_NCE_FWD2(4); break;
@@ -731,7 +734,7 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
                                 float* i_hat, float* norms, float* logits, float* lse, float* loss,
                                 void* ws, hipStream_t s) {
   return infonce_fwd_impl(B, D, u, it, user_idx, inv_tau, u_hat, i_hat, norms, logits, lse, loss,
-                          ws, true, nullptr, s);
+                          ws, true, nullptr, nullptr, s);
 }
 
 extern "C" int64_t ttmi_infonce_counter_bytes(int B) {
@@ -741,11 +744,12 @@ extern "C" int64_t ttmi_infonce_counter_bytes(int B) {
 extern "C" int ttmi_infonce_fwd_pre(int B, int D, const int64_t* user_idx, float inv_tau,
                                     const float* u_hat, const float* i_hat, const float* norms,
                                     float* logits, float* lse, float* loss, void* ws,
-                                    int32_t* counters, hipStream_t s) {
+                                    int32_t* counters, float* loss_acc, hipStream_t s) {
   TTMI_REQUIRE(((uintptr_t)counters & 3) == 0, "ttmi_infonce_fwd_pre: counters need 4-byte alignment");
+  TTMI_REQUIRE(!loss_acc || (counters && fused_ok(B, D)), "ttmi_infonce_fwd_pre: loss_acc needs the fused combine");
   return infonce_fwd_impl(B, D, nullptr, nullptr, user_idx, inv_tau, const_cast<float*>(u_hat),
                           const_cast<float*>(i_hat), const_cast<float*>(norms), logits, lse, loss,
-                          ws, false, counters, s);
+                          ws, false, counters, loss_acc, s);
 }
 
 extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float* i_hat,

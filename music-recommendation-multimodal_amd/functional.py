@@ -683,11 +683,13 @@ class LossSaved:
 
 
 def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: float = 0.07,
-                normed: Optional[Tuple[Tensor, Tensor, Tensor]] = None):
+                normed: Optional[Tuple[Tensor, Tensor, Tensor]] = None,
+                loss_acc: Optional[Tensor] = None):
     """TwoTowerModel.forward loss part (reference two_tower.py:98-140): fused kernels — one
     normalise launch, one f32-MFMA logits + masked row/column softmax-statistics launch, one
     combine launch (ttmi_infonce_fwd).  ``normed`` = (u_hat, i_hat, norms) already written by
-    the fused heads: the normalise launch is skipped (ttmi_infonce_fwd_pre)."""
+    the fused heads: the normalise launch is skipped (ttmi_infonce_fwd_pre).  ``loss_acc``
+    (fp32 device scalar): += loss (inside the logits launch on the pre-normalised path)."""
     dev = u.device
     B, D = u.shape
     f32 = dict(device=dev, dtype=torch.float32)
@@ -705,10 +707,13 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: 
         user_idx = user_idx.to(torch.int64)
     inv_tau = 1.0 / temperature
     if normed is not None:
-        ops.infonce_fwd_pre(user_idx, inv_tau, u_hat, i_hat, norms, logits, lse, loss, ws)
+        ops.infonce_fwd_pre(user_idx, inv_tau, u_hat, i_hat, norms, logits, lse, loss, ws,
+                            loss_acc=loss_acc)
     else:
         ops.infonce_fwd(u.contiguous(), it.contiguous(), user_idx, inv_tau, u_hat, i_hat, norms,
                         logits, lse, loss, ws)
+        if loss_acc is not None:
+            loss_acc.add_(loss.view(loss_acc.shape))
     return loss, logits, u_hat, i_hat, LossSaved(u_hat, i_hat, norms, logits, lse, user_idx, ws,
                                                  inv_tau)
 

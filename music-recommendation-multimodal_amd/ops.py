@@ -660,14 +660,16 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], inv_tau: floa
 
 def infonce_fwd_pre(user_idx: Optional[Tensor], inv_tau: float, u_hat: Tensor, i_hat: Tensor,
                     norms: Tensor, logits: Tensor, lse: Tensor, loss: Tensor, ws: Tensor,
-                    fused_combine: bool = True):
+                    fused_combine: bool = True, loss_acc: Optional[Tensor] = None):
     """infonce_fwd on rows already normalised by their producers (ttmi_infonce_fwd_pre); with
     ``fused_combine`` the lse / loss combine runs inside the logits launch (persistent zero
-    arrival counters)."""
+    arrival counters); ``loss_acc`` (fp32 device scalar, needs the fused combine) += loss."""
     B, D = u_hat.shape
+    if loss_acc is not None and (not fused_combine or loss_acc.dtype != torch.float32):
+        raise ValueError("infonce_fwd_pre: loss_acc needs fused_combine and fp32")
     cnt = _zero_ws("ttmi_infonce_counter_bytes", (B,), u_hat.device) if fused_combine else None
     call("ttmi_infonce_fwd_pre", B, D, _p(user_idx), inv_tau, _p(u_hat), _p(i_hat), _p(norms),
-         _p(logits), _p(lse), _p(loss), _p(ws), _p(cnt), _s())
+         _p(logits), _p(lse), _p(loss), _p(ws), _p(cnt), _p(loss_acc), _s())
 
 
 def infonce_bwd(u_hat: Tensor, i_hat: Tensor, norms: Tensor, logits: Tensor, lse: Tensor,

@@ -324,6 +324,9 @@ class TrainStep:
         self.seeds = torch.zeros(F.N_SITES, dtype=torch.int64, device=dev)
         self.base_seed = seed & ((1 << 63) - 1)
         self.dloss = torch.full((1,), self.sync.loss_scale, dtype=torch.float32, device=dev)
+        # running sum of the step losses on the device (the reference loop's total_loss,
+        # src/train.py:68, without a host sync per step): read / reset via loss_sum
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
         self.Pu = self.flat.views(self.flat.data, "user_tower.")
         self.Pi = self.flat.views(self.flat.data, "item_tower.")
         self.Gu = self.flat.views(self.flat.grad, "user_tower.")
@@ -430,6 +433,7 @@ class TrainStep:
             if gst.world > 1:
                 cut(lambda: F.infonce_global_gather(gst, self.group))
             loss = F.infonce_global_loss(gst)
+            self.loss_sum.add_(loss.view(1))
             logits = gst.s_u2i
             F.infonce_global_loss_bwd(gst, self.dloss)
             if gst.world > 1:
@@ -437,7 +441,8 @@ class TrainStep:
             F.infonce_global_norm_bwd(gst, du, di)
         else:
             loss, logits, _, _, lst = F.infonce_fwd(u, it, b.get("user_idx"),
-                                                    self.model.temperature, normed=self._normed)
+                                                    self.model.temperature, normed=self._normed,
+                                                    loss_acc=self.loss_sum)
             du16 = torch.empty(u.shape, device=u.device, dtype=self.ucfg.dtype) \
                 if self.ucfg.dtype == torch.bfloat16 else None
             F.infonce_bwd(lst, self.dloss, du, di, du16)
@@ -560,7 +565,7 @@ class TrainStep:
         return e.static
 
     def _state(self):
-        return [self.flat.data, self.flat.exp_avg, self.flat.exp_avg_sq, self.step_t,
+        return [self.flat.data, self.flat.exp_avg, self.flat.exp_avg_sq, self.step_t, self.loss_sum,
                 *self.bufs.values()] + ([self.flat.mirror] if self.flat.mirror is not None else []) + \
             ([self.bstage] if self.broadcast_buffers else [])
 

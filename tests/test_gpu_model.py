@@ -844,3 +844,21 @@ def test_user_head_bwd_fused_matches_ops(gpu_pkg, B, p, co):
     for k in ("fusion_layer.1.weight", "fusion_layer.1.bias", pre + "norm2.weight", pre + "norm2.bias",
               "gender_embedding.weight", "country_embedding.weight"):
         assert rel(Gf[k], Gu[k]) < 2e-3, k
+
+
+@pytest.mark.parametrize("use_graph,glob", [(True, False), (False, False), (True, True)])
+def test_trainstep_loss_sum(gpu_pkg, use_graph, glob):
+    """TrainStep.loss_sum (the reference loop's total_loss, src/train.py:68) is the running sum
+    of the returned step losses: added inside the InfoNCE logits launch on the cfg-2 path, by
+    an add in the step on the global-negatives path; the capture's warm-up step is undone."""
+    torch.manual_seed(3)
+    m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=1001, tabular_input_dim=128,
+                              num_genders=3, num_countries=64, max_seq_len=50, user_embedding_dim=128,
+                              item_embedding_dim=128, global_negatives=glob).to(DEV)
+    step = gpu_pkg.TrainStep(m, lr=1e-4, use_graph=use_graph)
+    total = 0.0
+    for s in range(3):
+        b = ref.synthetic_batch(64, 50, 1001, generator=torch.Generator().manual_seed(70 + s))
+        total += float(step.step({k: v.to(DEV) for k, v in b.items()}))
+    torch.cuda.synchronize()
+    assert abs(float(step.loss_sum) - total) <= 1e-5 * max(1.0, abs(total)), (float(step.loss_sum), total)
