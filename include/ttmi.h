@@ -111,11 +111,14 @@ int64_t ttmi_wgrad_workspace(int64_t R, int64_t M, int64_t N, int64_t ld_dy, int
 int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream);
 /* Generic split fold: C[m*ldc + n] (+)= Σ_{s < S, in order} part[s*s_stride + m*N + n].
  * accumulate: bit 0 = add to C (else overwrite); bit 1 (ABI 15) = zero the partials read
- * (a workspace that must be zero on the next use, e.g. ttmi_seq_embed_bwd's). */
+ * (a workspace that must be zero on the next use, e.g. ttmi_seq_embed_bwd's).
+ * fx_shift (ABI 16): 0 = fp32 partials; > 0 = int64 fixed-point partials (value = q·2^-fx_shift,
+ * the order-independent accumulators of ttmi_seq_embed_bwd / ttmi_user_head_bwd / ...). */
 typedef struct {
-  const float* part; int64_t S, s_stride, M, N;
+  const void* part; int64_t S, s_stride, M, N;
   float* C; int64_t ldc;
   int accumulate;
+  int fx_shift;
 } ttmi_fold_desc;
 /* Completes the deferred ttmi_wgrad calls `descs` and the generic folds `folds` (one launch
  * per 16 segments). */
@@ -141,17 +144,21 @@ int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const floa
 /* Backward of the above.  dy (fp32) is the gradient w.r.t. y; if gate != NULL it is first
  * multiplied by (gate > 0 ? gate_scale : 0) (gate = the stored y when ReLU/dropout followed
  * the affine).  dx = res + LN'(dy) (res may alias dx or be NULL); dw/db are accumulated
- * (fp32).  ws: ttmi_layernorm_bwd_workspace(D) bytes, zero on entry and left zero (replicated
- * column sums folded once; may be NULL when dw and db are both NULL).  dx16 (optional, bf16,
- * row stride ld16) receives bf16(dropout(dx)) with keep index m*D + n (drop_p may be 0): the
- * next GEMM's operand, with the residual branch's dropout backward fused (saves a launch). */
+ * (fp32).  ws: ttmi_layernorm_bwd_workspace(D) bytes, zero on entry and left zero: int64
+ * fixed-point replica rows of the column sums (ABI 16: order-independent, so dw / db are
+ * bit-reproducible), folded once (may be NULL when dw and db are both NULL).  defer != 0
+ * (ABI 16) leaves the fold to the caller: ttmi_layernorm_bwd_folds writes its
+ * ttmi_fold_desc, one per non-NULL dw, db (in that order).  dx16 (optional, bf16, row stride ld16) receives
+ * bf16(dropout(dx)) with keep index m*D + n (drop_p may be 0): the next GEMM's operand, with
+ * the residual branch's dropout backward fused (saves a launch). */
 int64_t ttmi_layernorm_bwd_workspace(int D);
+int ttmi_layernorm_bwd_folds(int D, void* ws, float* dw, float* db, ttmi_fold_desc* out);
 int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
                        int64_t ldx, const float* mean, const float* rstd, const float* w,
                        const void* gate, int gate_dtype, int64_t ldg, float gate_scale,
                        const float* res, float* dx, int64_t lddx, float* dw, float* db,
                        void* ws, void* dx16, int64_t ld16, float drop_p,
-                       const uint64_t* drop_seed, hipStream_t stream);
+                       const uint64_t* drop_seed, int defer, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * SASRec input block (user_tower.py:83-93):
@@ -167,17 +174,22 @@ int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, 
                        const float* w1, const float* b1, float eps1, void* y1, float* mean1,
                        float* rstd1, hipStream_t stream);
 /* Backward: dE[ids] += g (rows with ids == padding_idx skipped, nn.Embedding(padding_idx=0)
- * user_tower.py:27), dP[l] += Σ_b g, dw/db += LN affine grads.  All accumulate (fp32).
- * ws: ttmi_seq_embed_bwd_workspace(L, D) bytes, zero on entry and left zero on return (the
- * per-position LN-grad partials; one buffer may serve every call on one stream).  With
- * dw = db = NULL (ABI 15) the per-position partials ws[l][0..D) (weight) and ws[l][D..2D)
- * (bias) stay in ws for the caller to fold (ttmi_fold_desc, S = L, s_stride = 2D,
- * accumulate = 3: added, and ws left zero) with its deferred weight gradients. */
-int64_t ttmi_seq_embed_bwd_workspace(int L, int D);
-int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const float* E,
+ * user_tower.py:27; ids outside [0, V) contribute nothing), dP[l] += Σ_b g, dw/db += LN affine
+ * grads.  All accumulate (fp32).  ABI 16: the cross-row sums go to int64 fixed-point
+ * accumulators in ws (ttmi_seq_embed_bwd_workspace(V, L, D) bytes, 16-byte aligned, zero on
+ * entry and left zero by the fold; one buffer may serve every call on one stream), so the
+ * gradients are bit-reproducible whatever order the token rows land in.  defer = 0 folds
+ * them into dE / dP / dw / db before returning; defer != 0 leaves the 4 folds to the caller
+ * (ttmi_seq_embed_bwd_folds writes the 4 ttmi_fold_desc, to run with its deferred weight
+ * gradients).  D % 4 == 0. */
+int64_t ttmi_seq_embed_bwd_workspace(int64_t V, int L, int D);
+int ttmi_seq_embed_bwd_folds(int64_t V, int L, int D, void* ws, float* dE, float* dP, float* dw,
+                             float* db, ttmi_fold_desc* out);
+int ttmi_seq_embed_bwd(int B, int L, int D, int64_t V, const int64_t* ids, const float* E,
                        const float* P, const float* w, const float* mean, const float* rstd,
                        float drop_p, const uint64_t* drop_seed, const float* dx, float* dE, float* dP,
-                       float* dw, float* db, int64_t padding_idx, void* ws, hipStream_t stream);
+                       float* dw, float* db, int64_t padding_idx, void* ws, int defer,
+                       hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Multi-head self-attention core (SDPA inside nn.MultiheadAttention, user_tower.py:111-116):
@@ -204,11 +216,13 @@ int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
                          const int64_t* len_src, const int64_t* gender, const float* G, int dg,
                          const int64_t* country, const float* C, int dc, void* comb,
                          int32_t* rows, hipStream_t stream);
-/* Backward: dx[rows[b]] += dcomb[b,:D] (accumulate != 0; = when 0, rows distinct);
- * dG[gender[b]] += ...; dC[country[b]] += ... */
+/* Backward: dx[rows[b]] += dcomb[b,:D] (accumulate != 0; = when 0; rows distinct);
+ * dG[gender[b]] += ...; dC[country[b]] += ... into int64 fixed-point accumulators (ABI 16,
+ * scale 2^36 = TTMI_FX_GRAD_SHIFT, zero on entry; the caller folds them with a
+ * ttmi_fold_desc of fx_shift 36; may be NULL). */
 int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
                          const int64_t* gender, int dg, const int64_t* country, int dc,
-                         float* dx, float* dG, float* dC, int accumulate, hipStream_t stream);
+                         float* dx, int64_t* dG, int64_t* dC, int accumulate, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * BatchNorm1d + ReLU + dropout (item_tower.py:122-126 fusion head, item_tower.py:89-93
@@ -301,9 +315,11 @@ int ttmi_sum_scaled(int n, const float* x, float scale, float* out, hipStream_t 
  * torchvision resnet18): implicit GEMM over NHWC bf16 activations, C and Co multiples of 8
  * (stems zero-padded with ttmi_nchw_to_nhwc), square stride/pad, no bias.
  *   mode 0 FWD:   y[n,ho,wo,co] = Σ x[n, ho·s−p+kh, wo·s−p+kw, ci] W[co,ci,kh,kw]   (out bf16),
- *                 colsum/colsumsq [TTMI_CONV_STAT_REPS][Co] fp32 (zero on entry, may both be
- *                 NULL): Σ_r colsum[r][co] = Σ y, Σ y² (BatchNorm stats, spread over replica
- *                 rows so the workgroups' atomics do not serialise on one address)
+ *                 colsum/colsumsq [TTMI_CONV_STAT_REPS][Co] int64 fixed point, scale 2^24
+ *                 (TTMI_FX_STAT_SHIFT; ABI 16; zero on entry, may both be NULL):
+ *                 Σ_r colsum[r][co]·2^-24 = Σ y, Σ y² (BatchNorm stats, spread over replica
+ *                 rows so the workgroups' atomics do not serialise on one address; integer
+ *                 adds, so the statistics do not depend on the workgroups' order)
  *   mode 1 DGRAD: dx[n,h,w,ci] = Σ dy[n,(h+p−kh)/s,(w+p−kw)/s,co] W[co,ci,kh,kw] (+ addend)
  *                 over the stride lattice (out bf16; needs Cin == C, Co % 64 == 0, stride <= 2)
  *   mode 2 WGRAD: dW[co,ci,kh,kw] += Σ dy·x (out fp32, torch layout, ci < Cin); split-K
@@ -321,7 +337,7 @@ typedef struct ttmi_conv_desc {
   const void* w;          /* bf16 mirror (FWD: Wf, DGRAD: Wd) */
   void* out;
   const void* addend;     /* DGRAD: bf16 [N,H,W,C] added before the store, or NULL */
-  float* colsum; float* colsumsq;
+  int64_t* colsum; int64_t* colsumsq;
   void* workspace;        /* WGRAD scratch (device), or NULL for FWD/DGRAD */
   int64_t workspace_bytes;
 } ttmi_conv_desc;
@@ -338,22 +354,23 @@ int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const float* x, uint
                       hipStream_t stream);
 
 /* BatchNorm2d, train mode, over NHWC bf16 [M = N·H·W, C] (C % 8 == 0, C <= 512), batch
- * statistics from the producing conv's colsum/colsumsq ([TTMI_CONV_STAT_REPS][C], summed):  y = act(w·x̂ + b + residual)
+ * statistics from the producing conv's colsum/colsumsq ([TTMI_CONV_STAT_REPS][C] int64 fixed
+ * point, summed exactly; mean / variance in double):  y = act(w·x̂ + b + residual)
  * (act = ReLU if relu; residual bf16 or NULL); running stats updated with momentum and the
  * unbiased variance, *num_batches_tracked += 1 (all three may be NULL: eval-free path);
  * save_mean/save_rstd [C] for the backward (nn.BatchNorm2d + torchvision BasicBlock tail).
  * Eval mode (nn.BatchNorm2d.eval()): colsum = colsumsq = NULL normalises with
  * running_mean/running_var and updates nothing. */
-int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* colsum, const float* colsumsq,
+int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const int64_t* colsum, const int64_t* colsumsq,
                   const float* w, const float* b, float eps, float momentum, float* running_mean,
                   float* running_var, int64_t* num_batches_tracked, const uint16_t* residual,
                   int relu, uint16_t* y, float* save_mean, float* save_rstd, hipStream_t stream);
 /* Backward: g = dy ⊙ (gate > 0) (gate = the ReLU output, or NULL); dx = w·rstd·(g − Σg/M −
- * x̂·Σgx̂/M); dw += Σgx̂, db += Σg.  sums [TTMI_CONV_STAT_REPS][2C] fp32 must be zero on
- * entry (scratch);
+ * x̂·Σgx̂/M); dw += Σgx̂, db += Σg.  sums [TTMI_CONV_STAT_REPS][2C] int64 fixed point (scale
+ * 2^36, TTMI_FX_GRAD_SHIFT; ABI 16: order-independent) must be zero on entry (scratch);
  * g_out (bf16, may be NULL) receives g for the residual branch. */
 int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate, const uint16_t* x,
-                  const float* mean, const float* rstd, const float* w, float* sums,
+                  const float* mean, const float* rstd, const float* w, int64_t* sums,
                   uint16_t* g_out, uint16_t* dx, float* dw, float* db, hipStream_t stream);
 /* Max-pool k x k / stride, -inf padding (resnet18 maxpool 3/2/1), NHWC bf16; idx (uint8 per
  * output element) = the window tap of the max, first on ties.  Backward gathers. */
@@ -630,13 +647,19 @@ typedef struct ttmi_user_head_desc {
 } ttmi_user_head_desc;
 int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t stream);
 /* Its backward, one launch (ABI 12), from du (bf16 [B, D]) and the forward's saved values:
- *   daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0]); dcomb = dz·Wf0 (dG[gender] / dC[country] +=, atomics);
+ *   daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0]); dcomb = dz·Wf0 (dG[gender] / dC[country] +=);
  *   dy2 = drop2ᵀ(dcomb[:, :D]); dz1 = (dy2·W2) ⊙ [h > 0]·ffn_scale;
  *   dx1 = LN2ᵀ(dz1·W1) + dcomb[:, :D]; dy1 = drop1ᵀ(dx1); dctx = dy1·Wo.
  * The *t weights are the transposed k-major mirrors ([in, out]).  Outputs dz16, dy2, dz1, dy1
  * (bf16: the weight-gradient GEMMs' dY operands), dx1 (fp32), dctx (bf16).  ws
  * [ttmi_user_head_bwd_ws_floats(B)] receives per-16-row-block column sums of the four
- * LayerNorm parameter gradients (dlnw, dlnb, dn2w, dn2b, [nblk][4][D]) to be folded. */
+ * LayerNorm parameter gradients (dlnw, dlnb, dn2w, dn2b, [nblk][4][D]) to be folded.
+ * ABI 16: dG / dC are int64 fixed-point accumulators ([n_genders][dg], [n_countries][dc],
+ * scale 2^36, TTMI_FX_GRAD_SHIFT; zero on entry): adds in any order give the same bits.  The
+ * caller converts them into the fp32 gradients with a ttmi_fold_desc (fx_shift = 36, S = 1,
+ * accumulate = 3). */
+#define TTMI_FX_GRAD_SHIFT 36
+#define TTMI_FX_STAT_SHIFT 24
 typedef struct ttmi_user_head_bwd_desc {
   int B, D, F, dg, dc;
   float ffn_scale;
@@ -647,7 +670,7 @@ typedef struct ttmi_user_head_bwd_desc {
   const float* lnw; const float* n2w;
   float d1_p; const uint64_t* d1_seed;
   float d2_p; const uint64_t* d2_seed;
-  float* dG; float* dC;
+  int64_t* dG; int64_t* dC;
   void* dz16; void* dy2; void* dz1; float* dx1; void* dy1; void* dctx; float* ws;
 } ttmi_user_head_bwd_desc;
 int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t stream);

@@ -9,8 +9,8 @@ one-to-one.  BatchNorm2d runs in train mode on batch statistics, as in the refer
 
 Data layout: NHWC bf16 activations (the 1/3-channel input is zero-padded to 8 channels by
 ttmi_nchw_to_nhwc); conv weights are used through bf16 mirrors (ttmi_conv_weight_prep);
-every conv's forward epilogue accumulates the BatchNorm column sums, so a conv + BN + ReLU
-(+ residual) is two launches.  All parameters and grads stay fp32 (torch layouts).
+every conv's forward epilogue accumulates the BatchNorm column sums (int64 fixed point, so the
+statistics are bit-reproducible), so a conv + BN + ReLU (+ residual) is two launches.  All parameters and grads stay fp32 (torch layouts).
 """
 from __future__ import annotations
 
@@ -129,8 +129,9 @@ def resnet18_fwd(P: Dict[str, Tensor], x: Tensor, in_ch: int, bufs: Dict[str, Te
     N, _, H, W = x.shape
     specs = resnet18_convs(in_ch)
     mirrors = weight_mirrors(P, specs)
-    stats = torch.zeros(2 * ops.CONV_STAT_REPS * sum(sp.cout for sp in specs), device=dev) \
-        if training else None
+    # BatchNorm Σy, Σy² replica rows: int64 fixed point (order-independent, include/ttmi.h)
+    stats = torch.zeros(2 * ops.CONV_STAT_REPS * sum(sp.cout for sp in specs), device=dev,
+                        dtype=torch.int64) if training else None
     st = ResNetSaved(N, mirrors=mirrors)
     x0 = torch.empty(N, H, W, STEM_CP, device=dev, dtype=torch.bfloat16)
     ops.nchw_to_nhwc(x.contiguous().float(), STEM_CP, x0)
@@ -185,7 +186,7 @@ def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dic
     specs = resnet18_convs(in_ch)
     byname = {s.name: s for s in specs}
     R = ops.CONV_STAT_REPS
-    sums = torch.zeros(2 * R * sum(sp.cout for sp in specs), device=dev)
+    sums = torch.zeros(2 * R * sum(sp.cout for sp in specs), device=dev, dtype=torch.int64)
     soff = [0]
 
     def bn_bwd(sp: ConvSpec, act: ConvAct, dy: Tensor, gate: Optional[Tensor],

@@ -4,7 +4,8 @@
 // average pool, with their backwards.
 //
 // BatchNorm2d forward takes the per-channel Σx and Σx² that the producing convolution
-// accumulated in its epilogue (ttmi_conv2d FWD), so it is one element-wise pass:
+// accumulated in its epilogue (ttmi_conv2d FWD; int64 fixed point, so order-independent), so
+// it is one element-wise pass:
 //   y = act(w·(x − μ)·rstd + b + residual),  μ = Σx/M, var = Σx²/M − μ² (biased),
 //   running stats with momentum and the unbiased variance (nn.BatchNorm2d).
 // Its backward is a reduction pass (Σg, Σg·x̂ per channel, g = dy ⊙ ReLU gate, optionally
@@ -21,8 +22,8 @@ int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n 
 
 // ---------------------------------------------------------------- BatchNorm2d forward
 __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const bf16_t* __restrict__ x,
-                                                       const float* __restrict__ csum,
-                                                       const float* __restrict__ csq,
+                                                       const int64_t* __restrict__ csum,
+                                                       const int64_t* __restrict__ csq,
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ b, float eps,
                                                        float momentum, float* running_mean,
@@ -31,17 +32,19 @@ __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const b
                                                        bf16_t* __restrict__ y, float* save_mean,
                                                        float* save_rstd) {
   __shared__ float sa[MAXC], sb[MAXC];      // y = x·sa + sb
-  const float invM = 1.f / (float)M;
   const bool eval = csum == nullptr;        // eval mode: normalise with the running statistics
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s1 = 0.f, s2 = 0.f;
+    long long q1 = 0, q2 = 0;
     if (!eval)
       for (int r = 0; r < TTMI_CONV_STAT_REPS; ++r) {   // replica rows of the conv epilogue
-        s1 += csum[r * C + c];
-        s2 += csq[r * C + c];
+        q1 += csum[r * C + c];
+        q2 += csq[r * C + c];
       }
-    const float mu = eval ? running_mean[c] : s1 * invM;
-    const float var = eval ? running_var[c] : fmaxf(s2 * invM - mu * mu, 0.f);
+    // fixed-point sums -> double moments (E[x²] − E[x]² without fp32 cancellation)
+    const double dmu = fx_to_d(q1, TTMI_FX_STAT) / (double)M;
+    const double dvar = fx_to_d(q2, TTMI_FX_STAT) / (double)M - dmu * dmu;
+    const float mu = eval ? running_mean[c] : (float)dmu;
+    const float var = eval ? running_var[c] : (float)fmax(dvar, 0.0);
     const float rs = 1.f / sqrtf(var + eps);
     sa[c] = w[c] * rs;
     sb[c] = b[c] - mu * w[c] * rs;
@@ -77,15 +80,16 @@ __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const b
 // ---------------------------------------------------------------- BatchNorm2d backward
 // Reduction: sums[r][c] += Σ g, sums[r][C + c] += Σ g·x̂ (g = dy ⊙ (gate > 0) when gate
 // given) with r = block % TTMI_CONV_STAT_REPS; g is written (bf16) when gout != NULL.  Block =
-// 256 threads over row slabs; per thread 8 channels of strided rows, then an LDS reduction and
-// one atomic per channel per block into its replica row (spread: no single hot address).
+// 256 threads over row slabs; per thread 8 channels of strided rows, then an LDS reduction (a
+// fixed order) and one int64 fixed-point add (TTMI_FX_GRAD) per channel per block into its
+// replica row (spread: no single hot address; order-independent: deterministic).
 __global__ __launch_bounds__(256) void bn2d_bwd_reduce_kernel(int64_t M, int C, const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ gate,
                                                               const bf16_t* __restrict__ x,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ rstd,
                                                               bf16_t* __restrict__ gout,
-                                                              float* __restrict__ sums,
+                                                              int64_t* __restrict__ sums,
                                                               int64_t rows_per_block) {
   __shared__ float red[2][256][8];
   const int cpr = C / 8;
@@ -143,11 +147,11 @@ __global__ __launch_bounds__(256) void bn2d_bwd_reduce_kernel(int64_t M, int C, 
 #pragma unroll
       for (int e = 0; e < 8; ++e) { a[e] += red[0][r * cpr + t][e]; bb[e] += red[1][r * cpr + t][e]; }
     }
-    float* rep = sums + (int64_t)(blockIdx.x % TTMI_CONV_STAT_REPS) * 2 * C;   // replica row
+    int64_t* rep = sums + (int64_t)(blockIdx.x % TTMI_CONV_STAT_REPS) * 2 * C;   // replica row
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      atomicAdd(rep + t * 8 + e, a[e]);
-      atomicAdd(rep + C + t * 8 + e, bb[e]);
+      fx_add(rep + t * 8 + e, a[e], TTMI_FX_GRAD);
+      fx_add(rep + C + t * 8 + e, bb[e], TTMI_FX_GRAD);
     }
   }
 }
@@ -159,17 +163,18 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_kernel(int64_t M, int C, c
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ rstd,
                                                              const float* __restrict__ w,
-                                                             const float* __restrict__ sums,
+                                                             const int64_t* __restrict__ sums,
                                                              bf16_t* __restrict__ dx,
                                                              float* dw, float* db) {
   __shared__ float sk[MAXC], sm1[MAXC], sm2[MAXC], smu[MAXC], srs[MAXC];
   const float invM = 1.f / (float)M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float t1 = 0.f, t2 = 0.f;
+    long long q1 = 0, q2 = 0;
     for (int r = 0; r < TTMI_CONV_STAT_REPS; ++r) {
-      t1 += sums[(int64_t)r * 2 * C + c];
-      t2 += sums[(int64_t)r * 2 * C + C + c];
+      q1 += sums[(int64_t)r * 2 * C + c];
+      q2 += sums[(int64_t)r * 2 * C + C + c];
     }
+    const float t1 = fx_to_f(q1, TTMI_FX_GRAD), t2 = fx_to_f(q2, TTMI_FX_GRAD);
     sk[c] = w[c] * rstd[c];
     sm1[c] = t1 * invM;
     sm2[c] = t2 * invM;
@@ -316,8 +321,8 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(int N, int HW, int C, 
 
 }  // namespace
 
-extern "C" int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* colsum,
-                             const float* colsumsq, const float* w, const float* b, float eps,
+extern "C" int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const int64_t* colsum,
+                             const int64_t* colsumsq, const float* w, const float* b, float eps,
                              float momentum, float* running_mean, float* running_var,
                              int64_t* num_batches_tracked, const uint16_t* residual, int relu,
                              uint16_t* y, float* save_mean, float* save_rstd, hipStream_t s) {
@@ -334,7 +339,7 @@ extern "C" int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const float* c
 
 extern "C" int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate,
                              const uint16_t* x, const float* mean, const float* rstd,
-                             const float* w, float* sums, uint16_t* g_out, uint16_t* dx,
+                             const float* w, int64_t* sums, uint16_t* g_out, uint16_t* dx,
                              float* dw, float* db, hipStream_t s) {
   TTMI_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= MAXC, "ttmi_bn2d_bwd: need 0 < C <= %d, C %% 8 == 0", MAXC);
   TTMI_REQUIRE(dy && x && mean && rstd && w && sums && dx, "ttmi_bn2d_bwd: null argument");

@@ -116,6 +116,26 @@ static inline DropParams make_drop(float p, const uint64_t* seed) {
   return d;
 }
 
+// ---------------------------------------------------------------- deterministic scatter-add
+// Sums whose adders arrive in no fixed order (embedding-row scatters, column statistics over
+// many workgroups) accumulate in int64 fixed point: integer addition is associative, so the
+// total is the same bit pattern whatever the arrival order, and graph replays equal eager
+// runs bit for bit.  v is rounded to the nearest multiple of 2^-shift once per adder:
+//   TTMI_FX_GRAD (gradient scatters)        2^-36 ≈ 1.5e-11 resolution, |sum| < 2^27 ≈ 1.3e8
+//   TTMI_FX_STAT (BatchNorm Σy, Σy²)        2^-24 ≈ 6.0e-8  resolution, |sum| < 2^39 ≈ 5.5e11
+// Consumers convert with fx_to_f (through double; exact for |sum| < 2^53 units).
+constexpr int TTMI_FX_GRAD = TTMI_FX_GRAD_SHIFT;   // 36 (include/ttmi.h)
+constexpr int TTMI_FX_STAT = TTMI_FX_STAT_SHIFT;   // 24
+TTMI_DEV long long fx_of(float v, int shift) {
+  const float s = __builtin_ldexpf(v, shift);
+  return __builtin_llrintf(fminf(fmaxf(s, -9.0e18f), 9.0e18f));
+}
+TTMI_DEV void fx_add(int64_t* p, float v, int shift) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)fx_of(v, shift));
+}
+TTMI_DEV double fx_to_d(int64_t q, int shift) { return __builtin_ldexp((double)q, -shift); }
+TTMI_DEV float fx_to_f(int64_t q, int shift) { return (float)fx_to_d(q, shift); }
+
 // ---------------------------------------------------------------- XCD-aware block order
 // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  This bijection of
 // [0, n) gives each XCD a contiguous run of logical ids, so neighbouring logical blocks that

@@ -58,8 +58,8 @@ struct ConvArgs {
   const bf16_t* w;          // FWD: Wf, DGRAD: Wd
   void* out;                // FWD: y bf16 [M][Co]; DGRAD: dx bf16 [M][C]
   const bf16_t* addend;     // DGRAD: added before the store, or NULL
-  float* colsum;            // FWD: Σ y per channel (may be NULL)
-  float* colsumsq;
+  int64_t* colsum;          // FWD: Σ y per channel, int64 fixed point 2^-24 (may be NULL)
+  int64_t* colsumsq;
   float* ws;                // WGRAD: partials [splits][GM][GN]
   int GM, GN, GK;           // GEMM sizes (DGRAD: per class below)
   int k_split;              // WGRAD: pixels per split (multiple of 64)
@@ -336,9 +336,11 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
   }
   if (MODE == 0 && a.colsum) {
     // BatchNorm column statistics: reduce the tile's rows (registers, then the 16 row lanes,
-    // then the two row-waves through LDS) so each column gets one Σy and one Σy² atomic per
-    // workgroup, spread over TTMI_CONV_STAT_REPS replica rows (one hot address per channel
-    // would serialise every workgroup's atomics in a single L2 channel).
+    // then the two row-waves through LDS, a fixed order) so each column gets one Σy and one
+    // Σy² add per workgroup, spread over TTMI_CONV_STAT_REPS replica rows (one hot address
+    // per channel would serialise every workgroup's atomics in a single L2 channel).  The
+    // adds are int64 fixed point (TTMI_FX_STAT): the statistics do not depend on the order
+    // the workgroups finish in, so the whole step is bit-reproducible.
     float* red = reinterpret_cast<float*>(smem);        // [2][BN]; the K loop has drained
 #pragma unroll
     for (int j = 0; j < FN; ++j)
@@ -369,46 +371,53 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
           const int col = wn * WN + j * 16 + 4 * lg + e;
           const int n = n0 + col;
           if (n < a.GN) {
-            atomicAdd(a.colsum + (int64_t)rep * a.GN + n, cs[j][e] + red[col]);
-            atomicAdd(a.colsumsq + (int64_t)rep * a.GN + n, cq[j][e] + red[BN + col]);
+            fx_add(a.colsum + (int64_t)rep * a.GN + n, cs[j][e] + red[col], TTMI_FX_STAT);
+            fx_add(a.colsumsq + (int64_t)rep * a.GN + n, cq[j][e] + red[BN + col], TTMI_FX_STAT);
           }
         }
     }
   }
 }
 
-// dW (torch [Co][Cin][KH][KW]) += Σ_split ws[split][co][(kh·KW + kw)·C + ci], ci < Cin.
-// 2-D grid: x over 4-column groups of the [GM][GN] plane, y over chunks of WR_SPLITS splits
-// (summed in a fixed order per chunk); each chunk adds its total with one atomic per element,
-// so an element sees ceil(splits / WR_SPLITS) atomics, not a serial walk over every split.
+// dW (torch [Co][Cin][KH][KW]) += Σ_split ws[split][co][(kh·KW + kw)·C + ci], ci < Cin, in
+// split order (deterministic).  Up to WR_SPLITS splits: one pass (x over 4-column groups of
+// the [GM][GN] plane; a thread's WR_SPLITS loads in flight together).  More: a first pass
+// (y over chunks of WR_SPLITS splits) sums each chunk into the chunk's first slab in place,
+// then the final pass sums the chunk slabs in chunk order — fixed order, no atomics.
 constexpr int WR_SPLITS = 16;
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
-                                                           int GM, int GN, int C, int Cin, int KW,
-                                                           int KHKW, float* __restrict__ dw) {
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(float* __restrict__ ws, int splits,
+                                                           int step, int GM, int GN, int C, int Cin,
+                                                           int KW, int KHKW, int final_pass,
+                                                           float* __restrict__ dw) {
   const int64_t n4 = (int64_t)GM * GN / 4, plane = (int64_t)GM * GN;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  const int s0 = blockIdx.y * WR_SPLITS, n = min(splits - s0, WR_SPLITS);
-  f32x4_t part[WR_SPLITS];
+  // this thread's slabs: s = first + j*step for j < count
+  const int first = final_pass ? 0 : blockIdx.y * WR_SPLITS * step;
+  const int count = final_pass ? (splits + step - 1) / step : min(WR_SPLITS, (splits - first + step - 1) / step);
+  f32x4_t s = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < count; j0 += WR_SPLITS) {
+    f32x4_t part[WR_SPLITS];
 #pragma unroll
-  for (int j = 0; j < WR_SPLITS; ++j)             // all loads in flight together
-    part[j] = j < n ? reinterpret_cast<const f32x4_t*>(ws + (s0 + j) * plane)[i]
-                    : f32x4_t{0.f, 0.f, 0.f, 0.f};
-  f32x4_t s = part[0];
+    for (int j = 0; j < WR_SPLITS; ++j)           // all loads in flight together
+      part[j] = j0 + j < count ? reinterpret_cast<const f32x4_t*>(ws + (int64_t)(first + (j0 + j) * step) * plane)[i]
+                               : f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 1; j < WR_SPLITS; ++j) s += part[j];
+    for (int j = 0; j < WR_SPLITS; ++j) s += part[j];
+  }
+  if (!final_pass) {                               // chunk total into the chunk's first slab
+    reinterpret_cast<f32x4_t*>(ws + (int64_t)first * plane)[i] = s;
+    return;
+  }
   const int64_t e0 = i * 4;
   const int co = (int)(e0 / GN), kc = (int)(e0 % GN);
   const int tap = kc / C, ci0 = kc % C;
   const float* v = reinterpret_cast<const float*>(&s);
-  const bool single = splits <= WR_SPLITS;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int ci = ci0 + e;
     if (ci >= Cin) continue;
-    float* d = dw + ((int64_t)co * Cin + ci) * KHKW + tap;
-    if (single) *d += v[e];
-    else atomicAdd(d, v[e]);
+    dw[((int64_t)co * Cin + ci) * KHKW + tap] += v[e];
   }
 }
 
@@ -611,9 +620,18 @@ extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
     rc = ttmi_check_launch("ttmi_conv2d/wgrad");
     if (rc) return rc;
     const int64_t n4 = (int64_t)pl.a.GM * pl.a.GN / 4;
-    const dim3 rg((unsigned)((n4 + 255) / 256), (unsigned)((pl.splits + WR_SPLITS - 1) / WR_SPLITS));
-    hipLaunchKernelGGL(wgrad_reduce_kernel, rg, dim3(256), 0, stream, static_cast<const float*>(pl.a.ws), pl.splits, pl.a.GM,
-                       pl.a.GN, d->C, d->Cin, d->KW, d->KH * d->KW, static_cast<float*>(d->out));
+    const unsigned gx = (unsigned)((n4 + 255) / 256);
+    int step = 1;
+    if (pl.splits > WR_SPLITS) {         // chunk totals first (in place), then the chunk slabs
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx, (unsigned)((pl.splits + WR_SPLITS - 1) / WR_SPLITS)),
+                         dim3(256), 0, stream, pl.a.ws, pl.splits, 1, pl.a.GM, pl.a.GN, d->C, d->Cin, d->KW,
+                         d->KH * d->KW, 0, static_cast<float*>(d->out));
+      rc = ttmi_check_launch("ttmi_conv2d/wgrad_chunks");
+      if (rc) return rc;
+      step = WR_SPLITS;
+    }
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx), dim3(256), 0, stream, pl.a.ws, pl.splits, step, pl.a.GM,
+                       pl.a.GN, d->C, d->Cin, d->KW, d->KH * d->KW, 1, static_cast<float*>(d->out));
   }
   return ttmi_check_launch("ttmi_conv2d");
 }

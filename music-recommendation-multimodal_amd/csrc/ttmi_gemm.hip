@@ -474,7 +474,9 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
       }
     }
   }
-  // dw / db: sum the tile's 16 rows (one DPP row), one LDS add per column
+  // dw / db: sum the tile's 16 rows (one DPP row) into this wave's own LDS row (sdw / sdb
+  // point at it): one writer per column, tiles in the wave's program order (deterministic;
+  // the waves' rows are summed in wave order at the end)
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
 #pragma unroll
@@ -482,8 +484,8 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
       const float a = row16_sum(dy[8 * p + e] * xh[8 * p + e]);
       const float b = row16_sum(dy[8 * p + e]);
       if (li == 0) {
-        atomicAdd(sdw + 32 * p + 8 * lg + e, a);
-        atomicAdd(sdb + 32 * p + 8 * lg + e, b);
+        sdw[32 * p + 8 * lg + e] += a;
+        sdb[32 * p + 8 * lg + e] += b;
       }
     }
   }
@@ -495,10 +497,11 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   constexpr bool LNB = EPI == PE_LNBWD, LNF = EPI == PE_RESLN;
   static_assert(NT % 8 == 0, "column groups of 128");
   static_assert(!(LNB || LNF) || NT == 8, "LayerNorm epilogues need N = 128");
-  __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4 + ((LNB || LNF) ? 2 * N * 4 : 0)];
+  constexpr int SROWS = LNB ? 8 : 1;                            // LNB: one row per wave
+  __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4 + ((LNB || LNF) ? 2 * SROWS * N * 4 : 0)];
   float* sbias = reinterpret_cast<float*>(smem + N * WP);     // bias, or the LN weight
-  float* sdw = sbias + N;                                       // LNB: per-WG dw / db sums
-  float* sdb = sdw + N;                                         // LNF: LN weight / bias
+  float* sdw = sbias + N;                                       // LNB: per-wave dw / db sums
+  float* sdb = sdw + SROWS * N;                                 // LNF: LN weight / bias
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
@@ -536,7 +539,8 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
       }
     }
     if constexpr (LNB) {
-      for (int i = tid; i < N; i += 512) { sbias[i] = ln.w[i]; sdw[i] = 0.f; sdb[i] = 0.f; }
+      for (int i = tid; i < N; i += 512) sbias[i] = ln.w[i];
+      for (int i = tid; i < SROWS * N; i += 512) { sdw[i] = 0.f; sdb[i] = 0.f; }
     } else if constexpr (LNF) {
       for (int i = tid; i < N; i += 512) {
         sbias[i] = g.bias ? g.bias[i] : 0.f;
@@ -593,7 +597,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
         for (int c = 0; c < 4; ++c) a[c] = an[c];
       }
       if constexpr (LNB) {
-        panel_ln_bwd_epilogue(g, ln, acc, m, mok, li, lg, sbias, sdw, sdb, dk2, pre);
+        panel_ln_bwd_epilogue(g, ln, acc, m, mok, li, lg, sbias, sdw + wave * N, sdb + wave * N, dk2, pre);
         continue;
       }
       if (!mok) continue;
@@ -686,13 +690,17 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   }
   if constexpr (LNB) {
     __syncthreads();
-    if (ln.sum_ws) {            // deterministic: folded later in workgroup order (ttmi_fold)
-      float* o = ln.sum_ws + (int64_t)blockIdx.x * 2 * N;
-      for (int i = tid; i < N; i += 512) { o[i] = sdw[i]; o[N + i] = sdb[i]; }
-    } else {
-      for (int i = tid; i < N; i += 512) {
-        if (ln.dw) atomicAdd(ln.dw + i, sdw[i]);
-        if (ln.db) atomicAdd(ln.db + i, sdb[i]);
+    for (int i = tid; i < N; i += 512) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < SROWS; ++w) { a += sdw[w * N + i]; b += sdb[w * N + i]; }
+      if (ln.sum_ws) {          // deterministic: folded later in workgroup order (ttmi_fold)
+        float* o = ln.sum_ws + (int64_t)blockIdx.x * 2 * N;
+        o[i] = a;
+        o[N + i] = b;
+      } else {                  // legacy ABI callers without a workspace: float atomics
+        if (ln.dw) atomicAdd(ln.dw + i, a);
+        if (ln.db) atomicAdd(ln.db + i, b);
       }
     }
   }
@@ -967,6 +975,7 @@ constexpr int WG_GROUP = 16;
 struct WgradGroup { WgradArgs e[WG_GROUP]; int wg_begin[WG_GROUP + 1]; int n; };
 typedef const __attribute__((address_space(4))) WgradGroup* KWgradGroup;
 
+template <int BM, int BN, int NS>
 __global__ __launch_bounds__(256) void wgrad_group_kernel(WgradGroup grp) {
   (void)grp;
   KWgradGroup kg = (KWgradGroup)__builtin_amdgcn_kernarg_segment_ptr();
@@ -980,7 +989,7 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(WgradGroup grp) {
   g.alpha = e.alpha; g.rowsum_a = e.rowsum_a; g.rows_per_split = e.rows_per_split;
   g.tiles_m = e.tiles_m; g.tiles_n = e.tiles_n; g.splits = e.splits; g.xcd_remap = e.xcd_remap;
   g.mode = e.mode; g.accumulate = e.accumulate; g.part = e.part; g.part_rs = e.part_rs;
-  wgrad_body<64, 64, 4>(g, bid - kg->wg_begin[k]);
+  wgrad_body<BM, BN, NS>(g, bid - kg->wg_begin[k]);
 }
 
 template <typename T, int BM, int BN>
@@ -1123,6 +1132,43 @@ WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax, bool allow3
   return p;
 }
 
+// Grouped launches (ttmi_wgrad_batch) may use larger tiles: a 128 x 128 tile reads each
+// operand row slice once for twice the outputs of a 64 x 64 one, halving what the CUs ingest
+// (the family is bound by per-CU ingest from L2 / Infinity Cache), at one workgroup per CU
+// (128 KB ring).  TTMI_WGRAD_GROUP="T:S" (T = 64 or 128, S = splits per long-GEMM tile, 0 =
+// the 64-tile default sizing) selects it; the default is the measured best.
+struct WgradGroupCfg { int tile, splits; };
+
+WgradGroupCfg wgrad_group_cfg() {
+  static const WgradGroupCfg cfg = [] {
+    WgradGroupCfg c{64, 0};
+    if (const char* e = getenv("TTMI_WGRAD_GROUP")) {
+      int t = 0, sp = 0;
+      if (sscanf(e, "%d:%d", &t, &sp) >= 1 && (t == 64 || t == 128)) c = WgradGroupCfg{t, std::max(sp, 0)};
+    }
+    return c;
+  }();
+  return cfg;
+}
+
+WgradPlan wgrad_group_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
+  const WgradGroupCfg c = wgrad_group_cfg();
+  if (c.tile == 64) return wgrad_plan(R, M, N, ldmax, false);
+  WgradPlan p;
+  p.tile = c.tile;
+  p.tiles_m = (int)((M + c.tile - 1) / c.tile);
+  p.tiles_n = (int)((N + c.tile - 1) / c.tile);
+  const int T = p.tiles_m * p.tiles_n;
+  const int64_t stages = std::max<int64_t>(1, (R + 63) / 64);
+  int S = c.splits > 0 ? c.splits : std::max(1, 256 / T);
+  S = (int)std::max<int64_t>(1, std::min<int64_t>(S, stages / 6));
+  int64_t sps = (stages + S - 1) / S;
+  while (sps > 1 && sps * 64 * ldmax * 2 >= (int64_t)1 << 31) sps = (sps + 1) / 2;
+  p.S = (int)((stages + sps - 1) / sps);
+  p.sps = sps;
+  return p;
+}
+
 int64_t al256(int64_t b) { return (b + 255) / 256 * 256; }
 
 int64_t wgrad_ws_bytes(const WgradPlan& p, int64_t M, int64_t N) {
@@ -1130,11 +1176,11 @@ int64_t wgrad_ws_bytes(const WgradPlan& p, int64_t M, int64_t N) {
   return al256((int64_t)p.S * M * N * 4) + al256((int64_t)p.S * M * 4);
 }
 
-constexpr int FOLD_SEGS = 32;   // kernarg: 32 x 88 B (a cfg-2 step folds ~20 segments)
+constexpr int FOLD_SEGS = 32;   // kernarg: 32 x 96 B (a cfg-2 step folds ~24 segments)
 struct FoldSeg {
-  const float* part; const float* part_rs; float* C; float* rs;
+  const void* part; const float* part_rs; float* C; float* rs;
   int64_t M, N, ldc, units, base, s_stride;   // s_stride: elements between split slabs
-  int S, acc;
+  int S, acc, fx;                             // fx > 0: int64 fixed-point partials, 2^-fx
 };
 struct FoldArgs { FoldSeg seg[FOLD_SEGS]; int n; int64_t total; };
 
@@ -1143,6 +1189,65 @@ struct FoldArgs { FoldSeg seg[FOLD_SEGS]; int n; int64_t total; };
 // dynamically would put it in scratch memory.
 typedef const __attribute__((address_space(4))) FoldArgs* KFoldArgs;
 
+// The S partials of one 4-column unit, summed in split order: fp32 partials in float, int64
+// fixed-point partials exactly (integer adds) and converted once.  `consume` zeroes them.
+TTMI_DEV float4 fold_unit(const FoldSeg& sg, int64_t off, int s_lo, int s_hi, bool consume) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sg.fx) {
+    const int64_t* p = static_cast<const int64_t*>(sg.part) + off;
+    long long q[4] = {0, 0, 0, 0};
+    for (int s0 = s_lo; s0 < s_hi; s0 += 8) {
+      longlong2 w[8][2];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s = min(s0 + j, s_hi - 1);     // clamped: unconditional loads
+        w[j][0] = *reinterpret_cast<const longlong2*>(p + s * sg.s_stride);
+        w[j][1] = *reinterpret_cast<const longlong2*>(p + s * sg.s_stride + 2);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (s0 + j < s_hi) {
+          q[0] += w[j][0].x; q[1] += w[j][0].y; q[2] += w[j][1].x; q[3] += w[j][1].y;
+          if (consume) {
+            int64_t* z = const_cast<int64_t*>(p) + (s0 + j) * sg.s_stride;
+            *reinterpret_cast<longlong2*>(z) = make_longlong2(0, 0);
+            *reinterpret_cast<longlong2*>(z + 2) = make_longlong2(0, 0);
+          }
+        }
+    }
+    v = make_float4(fx_to_f(q[0], sg.fx), fx_to_f(q[1], sg.fx), fx_to_f(q[2], sg.fx), fx_to_f(q[3], sg.fx));
+    return v;
+  }
+  const float* p = static_cast<const float*>(sg.part) + off;
+  for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
+    float4 w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      w[j] = s0 + j < s_hi ? *reinterpret_cast<const float4*>(p + (s0 + j) * sg.s_stride)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (consume) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (s0 + j < s_hi)
+          *reinterpret_cast<float4*>(const_cast<float*>(p) + (s0 + j) * sg.s_stride) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (s0 + j < s_hi) { v.x += w[j].x; v.y += w[j].y; v.z += w[j].z; v.w += w[j].w; }
+  }
+  return v;
+}
+
+TTMI_DEV void fold_store(const FoldSeg& sg, int64_t u, int64_t nq, float4 v) {
+  const int64_t m = u / nq, n = (u % nq) * 4;
+  float4* cp = reinterpret_cast<float4*>(sg.C + m * sg.ldc + n);
+  if (sg.acc & 1) {
+    const float4 c = *cp;
+    v.x = c.x + v.x; v.y = c.y + v.y; v.z = c.z + v.z; v.w = c.w + v.w;
+  }
+  *cp = v;
+}
+
 __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   (void)a;
   const auto& sgk = ((KFoldArgs)__builtin_amdgcn_kernarg_segment_ptr())->seg[blockIdx.y];
@@ -1150,34 +1255,25 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   sg.part = sgk.part; sg.part_rs = sgk.part_rs; sg.C = sgk.C; sg.rs = sgk.rs;
   sg.M = sgk.M; sg.N = sgk.N; sg.ldc = sgk.ldc; sg.units = sgk.units; sg.base = 0;
   sg.s_stride = sgk.s_stride;
-  sg.S = sgk.S; sg.acc = sgk.acc;
+  sg.S = sgk.S; sg.acc = sgk.acc; sg.fx = sgk.fx;
+  const int64_t nq = sg.N / 4, nel = sg.M * nq;
+  const bool consume = (sg.acc & 2) != 0;
+  if (sg.S <= 2) {            // few partials (a fixed-point accumulator): one unit per thread
+    for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < nel; u += (int64_t)gridDim.x * 256) {
+      const int64_t m = u / nq, n = (u % nq) * 4;
+      fold_store(sg, u, nq, fold_unit(sg, m * sg.N + n, 0, sg.S, consume));
+    }
+    return;
+  }
   __shared__ float4 red[4][64];
   const int ul = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int64_t nq = sg.N / 4, nel = sg.M * nq;
-  const int64_t stride = sg.s_stride;
   const int s_lo = (int)((int64_t)sg.S * q / 4), s_hi = (int)((int64_t)sg.S * (q + 1) / 4);
   for (int64_t ub = (int64_t)blockIdx.x * 64; ub < sg.units; ub += (int64_t)gridDim.x * 64) {
     const int64_t u = ub + ul;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (u < nel) {
       const int64_t m = u / nq, n = (u % nq) * 4;
-      const float* p = sg.part + m * sg.N + n;
-      for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
-        float4 w[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          w[j] = s0 + j < s_hi ? *reinterpret_cast<const float4*>(p + (s0 + j) * stride)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (sg.acc & 2) {                            // consume: leave the partials zero
-#pragma unroll
-          for (int j = 0; j < 16; ++j)
-            if (s0 + j < s_hi)
-              *reinterpret_cast<float4*>(const_cast<float*>(p) + (s0 + j) * stride) = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (s0 + j < s_hi) { v.x += w[j].x; v.y += w[j].y; v.z += w[j].z; v.w += w[j].w; }
-      }
+      v = fold_unit(sg, m * sg.N + n, s_lo, s_hi, consume);
     } else if (u < sg.units) {
       const int64_t m = u - nel;
       for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
@@ -1198,13 +1294,7 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
         v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
       }
       if (u < nel) {
-        const int64_t m = u / nq, n = (u % nq) * 4;
-        float4* cp = reinterpret_cast<float4*>(sg.C + m * sg.ldc + n);
-        if (sg.acc & 1) {
-          const float4 c = *cp;
-          v.x = c.x + v.x; v.y = c.y + v.y; v.z = c.z + v.z; v.w = c.w + v.w;
-        }
-        *cp = v;
+        fold_store(sg, u, nq, v);
       } else {
         const int64_t m = u - nel;
         sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v.x : v.x;
@@ -1963,7 +2053,7 @@ FoldSeg fold_seg(const ttmi_wgrad_desc* d, const WgradPlan& p) {
   f.units = d->M * (d->N / 4) + (d->db ? d->M : 0);
   f.base = 0;
   f.s_stride = d->M * d->N;
-  f.S = p.S; f.acc = d->accumulate;
+  f.S = p.S; f.acc = d->accumulate; f.fx = 0;
   return f;
 }
 
@@ -1980,7 +2070,9 @@ int launch_fold(FoldArgs& a, hipStream_t s) {
 extern "C" int64_t ttmi_wgrad_workspace(int64_t R, int64_t M, int64_t N, int64_t ld_dy,
                                         int64_t ld_x) {
   if (R <= 0 || M <= 0 || N <= 0) return 0;
-  return wgrad_ws_bytes(wgrad_plan(R, M, N, std::max(ld_dy, ld_x)), M, N);
+  const int64_t ldmax = std::max(ld_dy, ld_x);
+  return std::max(wgrad_ws_bytes(wgrad_plan(R, M, N, ldmax), M, N),
+                  wgrad_ws_bytes(wgrad_group_plan(R, M, N, ldmax), M, N));
 }
 
 extern "C" int ttmi_wgrad(const ttmi_wgrad_desc* d, hipStream_t stream) {
@@ -2020,8 +2112,9 @@ extern "C" int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M) {
   return (tiles + tpw - 1) / tpw;     // launch_panel_t's grid
 }
 
-extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int nf,
-                               const ttmi_fold_desc* folds, hipStream_t stream) {
+namespace {
+int wgrad_fold_impl(int n, const ttmi_wgrad_desc* const* descs, int nf, const ttmi_fold_desc* folds,
+                    hipStream_t stream, bool grouped) {
   TTMI_REQUIRE(n >= 0 && (n == 0 || descs) && nf >= 0 && (nf == 0 || folds),
                "ttmi_wgrad_fold: bad arguments");
   FoldArgs f;
@@ -2031,7 +2124,8 @@ extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int n
     const ttmi_fold_desc* d = folds + i;
     TTMI_REQUIRE(d->part && d->C && d->S > 0 && d->M > 0 && d->N > 0 && d->N % 4 == 0 &&
                  d->ldc % 4 == 0 && d->s_stride >= d->M * d->N && d->s_stride % 4 == 0 &&
-                 al16(d->part) && al16(d->C), "ttmi_wgrad_fold: bad fold descriptor %d", i);
+                 al16(d->part) && al16(d->C) && d->fx_shift >= 0 && d->fx_shift < 63,
+                 "ttmi_wgrad_fold: bad fold descriptor %d", i);
     if (f.n == FOLD_SEGS) {
       int rc = launch_fold(f, stream);
       if (rc) return rc;
@@ -2042,7 +2136,7 @@ extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int n
     sg.part = d->part; sg.part_rs = nullptr; sg.C = d->C; sg.rs = nullptr;
     sg.M = d->M; sg.N = d->N; sg.ldc = d->ldc; sg.units = d->M * (d->N / 4);
     sg.base = f.total; sg.s_stride = d->s_stride;
-    sg.S = (int)d->S; sg.acc = d->accumulate;
+    sg.S = (int)d->S; sg.acc = d->accumulate; sg.fx = d->fx_shift;
     f.seg[f.n++] = sg;
     f.total += sg.units;
   }
@@ -2050,7 +2144,9 @@ extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int n
     const ttmi_wgrad_desc* d = descs[i];
     int rc = wgrad_check(d);
     if (rc) return rc;
-    const WgradPlan p = wgrad_plan(d->R, d->M, d->N, std::max(d->ld_dy, d->ld_x));
+    const int64_t ldmax = std::max(d->ld_dy, d->ld_x);
+    const WgradPlan p = grouped ? wgrad_group_plan(d->R, d->M, d->N, ldmax)
+                                : wgrad_plan(d->R, d->M, d->N, ldmax);
     if (p.S <= 1 || d->R == 0) continue;     // written directly by ttmi_wgrad
     TTMI_REQUIRE(d->workspace, "ttmi_wgrad_fold: descriptor %d has no workspace", i);
     if (f.n == FOLD_SEGS) {
@@ -2066,6 +2162,12 @@ extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int n
   }
   return launch_fold(f, stream);
 }
+}  // namespace
+
+extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                               const ttmi_fold_desc* folds, hipStream_t stream) {
+  return wgrad_fold_impl(n, descs, nf, folds, stream, false);
+}
 
 extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int nf,
                                 const ttmi_fold_desc* folds, hipStream_t stream) {
@@ -2074,10 +2176,15 @@ extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int 
   WgradGroup grp;
   grp.n = 0;
   grp.wg_begin[0] = 0;
+  const int tile = wgrad_group_cfg().tile;
   auto flush = [&]() -> int {
     if (grp.n == 0) return TTMI_OK;
-    hipLaunchKernelGGL(wgrad_group_kernel, dim3((unsigned)grp.wg_begin[grp.n]), dim3(256), 0,
-                       stream, grp);
+    if (tile == 128)
+      hipLaunchKernelGGL((wgrad_group_kernel<128, 128, 4>), dim3((unsigned)grp.wg_begin[grp.n]), dim3(256), 0,
+                         stream, grp);
+    else
+      hipLaunchKernelGGL((wgrad_group_kernel<64, 64, 4>), dim3((unsigned)grp.wg_begin[grp.n]), dim3(256), 0,
+                         stream, grp);
     grp.n = 0;
     grp.wg_begin[0] = 0;
     return ttmi_check_launch("ttmi_wgrad_batch");
@@ -2093,7 +2200,7 @@ extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int 
       if (rc) return rc;
       continue;
     }
-    const WgradPlan p = wgrad_plan(d->R, d->M, d->N, std::max(d->ld_dy, d->ld_x), false);
+    const WgradPlan p = wgrad_group_plan(d->R, d->M, d->N, std::max(d->ld_dy, d->ld_x));
     const int64_t need = wgrad_ws_bytes(p, d->M, d->N);
     TTMI_REQUIRE(need == 0 || (d->workspace && d->workspace_bytes >= need && al16(d->workspace)),
                  "ttmi_wgrad_batch: descriptor %d needs a workspace of %lld bytes", i,
@@ -2109,5 +2216,5 @@ extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int 
   }
   int rc = flush();
   if (rc) return rc;
-  return ttmi_wgrad_fold(n, descs, nf, folds, stream);
+  return wgrad_fold_impl(n, descs, nf, folds, stream, true);
 }

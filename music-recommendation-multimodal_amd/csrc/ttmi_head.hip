@@ -516,7 +516,7 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
 // dropout-2 backward, the ReLU/dropout-gated linear2 input grad, linear1's input grad with
 // LN2's backward, the residual and the dropout-1 backward, and out_proj's input grad):
 //   daz = du·Wf3;  dz = LNᵀ(daz ⊙ [az > 0]);  dcomb = dz·Wf0;  dx2 = dcomb[:, :D] (dG, dC by
-//   atomics as before);  dy2 = drop2ᵀ(dx2);  dz1 = (dy2·W2) ⊙ [h > 0]·sf;
+//   fixed-point int64 atomics: order-independent, folded into the fp32 grads by the caller);  dy2 = drop2ᵀ(dx2);  dz1 = (dy2·W2) ⊙ [h > 0]·sf;
 //   dx1 = LN2ᵀ(dz1·W1) + dx2;  dy1 = drop1ᵀ(dx1);  dctx = dy1·Wo.
 // Weights are the transposed k-major mirrors.  The LayerNorm weight / bias gradients leave as
 // per-workgroup column sums (ws [nwg][4][D]: dlnw, dlnb, dn2w, dn2b), folded in workgroup order
@@ -530,7 +530,7 @@ struct HeadBwdArgs {
   const bf16_t* wf3t; const bf16_t* wf0t; const bf16_t* w2t; const bf16_t* w1t; const bf16_t* wot;
   const float* lnw; const float* n2w;
   DropParams d1, d2;
-  float* dG; float* dC;
+  int64_t* dG; int64_t* dC;          // TTMI_FX_GRAD fixed-point accumulators
   bf16_t* dz16; bf16_t* dy2; bf16_t* dz1; float* dx1; bf16_t* dy1; bf16_t* dctx; float* ws;
   ItemBwdArgs it; int nbu;     // co-launched item head backward: workgroups >= nbu
 };
@@ -822,8 +822,9 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
     if (mrow) st4_bf(reinterpret_cast<char*>(a.dctx + (int64_t)m * HD + n), x);
   }
   // ---- dG / dC last (nothing later waits on the atomics).  Rows sharing an index are summed
-  // here first: one atomic per (distinct index, column) per workgroup, a row's 48 columns in
-  // one coalesced instruction (lanes 0-15 gender, 16-47 country).
+  // here first (in row order): one fixed-point atomic per (distinct index, column) per
+  // workgroup, a row's 48 columns in one coalesced instruction (lanes 0-15 gender, 16-47
+  // country).  Integer adds: the accumulated bits do not depend on the workgroups' order.
   if (lane < 48) {
     const bool isg = lane < 16;
     const int k = isg ? lane : lane - 16;
@@ -845,7 +846,7 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
       float sum = 0.f;
 #pragma unroll
       for (int j = r; j < HR; ++j) sum += (j < nr && key[j] == key[r]) ? val[j] : 0.f;
-      atomicAdd(isg ? a.dG + (int64_t)key[r] * a.dg + k : a.dC + (int64_t)key[r] * a.dc + k, sum);
+      fx_add(isg ? a.dG + (int64_t)key[r] * a.dg + k : a.dC + (int64_t)key[r] * a.dc + k, sum, TTMI_FX_GRAD);
     }
   }
 #ifdef HEAD_STAMP

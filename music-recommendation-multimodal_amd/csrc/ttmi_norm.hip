@@ -8,7 +8,6 @@ namespace {
 
 constexpr int MAXV = 16;   // D <= 64 * MAXV
 constexpr int LN_REPL = 32;   // replicas of the LayerNorm-backward weight/bias column sums
-constexpr int LN_DIRECT = 128;  // at most this many blocks add to dw/db directly
 
 // Instantiate a kernel template for the smallest NV (64-wide column chunks per row) that
 // covers D: NV in {1, 2, 4, 8, 16}.
@@ -69,9 +68,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
   }
 }
 
-// Per-block reduction of per-lane column partials (W waves) followed by one atomic per column.
-template <int NV, int W = 4>
-TTMI_DEV void block_col_atomic(float (&acc)[NV], int D, float* dst, float* red) {
+// Per-block reduction of per-lane column partials (W waves, in wave order) followed by one
+// fixed-point atomic per column (order-independent: the sum's bits do not depend on which
+// block adds first).
+template <int NV, int W>
+TTMI_DEV void block_col_fx(float (&acc)[NV], int D, int64_t* dst, float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();
 #pragma unroll
@@ -84,7 +85,7 @@ TTMI_DEV void block_col_atomic(float (&acc)[NV], int D, float* dst, float* red) 
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < W; ++k) t += red[k * 64 * NV + c];
-    atomicAdd(dst + c, t);
+    fx_add(dst + c, t, TTMI_FX_GRAD);
   }
 }
 
@@ -93,8 +94,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int64_t M, int D, const float* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
     int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ w, const void* __restrict__ gate, int gate_f32, int64_t ldg,
-    float gate_scale, const float* res, float* dx, int64_t lddx, float* __restrict__ cw,
-    float* __restrict__ cb, int nrep, int64_t rstride, bf16_t* __restrict__ dx16, int64_t ld16,
+    float gate_scale, const float* res, float* dx, int64_t lddx, int64_t* __restrict__ cw,
+    int64_t* __restrict__ cb, int nrep, int64_t rstride, bf16_t* __restrict__ dx16, int64_t ld16,
     DropParams dp16) {
   __shared__ float red[4 * 64 * NV];
   const int lane = threadIdx.x & 63;
@@ -136,10 +137,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     }
   }
-  if (cw) {   // LN weight / bias partials: this block's replica (or dw/db directly, nrep 1)
+  if (cw) {   // LN weight / bias partials: fixed-point adds into this block's replica row
     const int64_t o = (int64_t)(blockIdx.x % nrep) * rstride;
-    block_col_atomic(aw, D, cw + o, red);
-    block_col_atomic(ab, D, cb + o, red);
+    block_col_fx<NV, 4>(aw, D, cw + o, red);
+    block_col_fx<NV, 4>(ab, D, cb + o, red);
   }
 }
 
@@ -191,26 +192,28 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int64_t M, int D, const
   }
 }
 
-// dst0[i] += Σ_r ws[r][i] (i < n0), dst1[i - n0] += ... (n0 <= i < n); zeroes the replicas.
-__global__ __launch_bounds__(256) void colsum_fold_kernel(int n, int n0, int R, float* __restrict__ ws,
+// dst0[i] += Σ_r ws[r][i] (i < n0), dst1[i - n0] += ... (n0 <= i < n) over int64 fixed-point
+// replicas (exact integer sum, converted once); zeroes the replicas.
+__global__ __launch_bounds__(256) void colsum_fold_kernel(int n, int n0, int R, int64_t* __restrict__ ws,
                                                           float* __restrict__ dst0,
                                                           float* __restrict__ dst1) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  float s = 0.f;
+  long long s = 0;
   constexpr int U = 8;
   for (int r0 = 0; r0 < R; r0 += U) {
-    float v[U];
+    long long v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = r0 + u < R ? ws[(int64_t)(r0 + u) * n + i] : 0.f;
+    for (int u = 0; u < U; ++u) v[u] = r0 + u < R ? ws[(int64_t)(r0 + u) * n + i] : 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       s += v[u];
-      if (r0 + u < R) ws[(int64_t)(r0 + u) * n + i] = 0.f;
+      if (r0 + u < R) ws[(int64_t)(r0 + u) * n + i] = 0;
     }
   }
-  if (i < n0) { if (dst0) dst0[i] += s; }
-  else if (dst1) dst1[i - n0] += s;
+  const float f = fx_to_f(s, TTMI_FX_GRAD);
+  if (i < n0) { if (dst0) dst0[i] += f; }
+  else if (dst1) dst1[i - n0] += f;
 }
 
 // ------------------------------------------------------------------- SASRec input block
@@ -284,17 +287,21 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
 }
 
 // Backward: block (l, b-chunk) of SEB_W waves; each wave walks b = chunk*bpc + wave,
-// + SEB_W, ... so the position gradient dP[l] accumulates in registers (one atomic per column
+// + SEB_W, ... so the position gradient dP[l] accumulates in registers (one add per column
 // per block).  The chunk is sized so a wave makes ONE pass of U rows: the kernel is a
 // dependent-gather latency chain (ids -> E[id]), so waves, not rows per wave, hide it.
+// Every cross-block sum goes to int64 fixed-point accumulators (ABI 16): the item-embedding
+// rows accE[V][D] (one add per token and column) and accL[3][L][D] (dP, and the LayerNorm
+// weight / bias partials per position), converted into the fp32 gradients by the fold
+// (ttmi_seq_embed_bwd_folds): the gradient is bit-identical run to run (the fp32 atomics it
+// replaces summed in arrival order).
 constexpr int SEB_W = 8;
 template <int NV>
 __global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
     int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E,
     const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ mean,
     const float* __restrict__ rstd, DropParams dp, const float* __restrict__ dx,
-    float* __restrict__ dE, float* __restrict__ dP, float* __restrict__ ws, int64_t padding_idx,
-    int64_t V, int bpc) {
+    int64_t* __restrict__ accE, int64_t* __restrict__ accL, int64_t padding_idx, int64_t V, int bpc) {
   __shared__ float red[SEB_W * 64 * NV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l = blockIdx.x;
@@ -360,52 +367,15 @@ __global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
         if (c < D) {
           const float o = rs[u] * (g[i] - c1 - xh[i] * c2);
           ap[i] += o;
-          if (emb) atomicAdd(dE + id[u] * D + c, o);
+          if (emb) fx_add(accE + id[u] * D + c, o, TTMI_FX_GRAD);
         }
       }
     }
   }
-  block_col_atomic<NV, SEB_W>(ap, D, dP + (int64_t)l * D, red);
-  // LN weight / bias partials go to this position's slot of the workspace: adders per address
-  // = chunks, not every block of the grid (same-address float atomics serialise)
-  block_col_atomic<NV, SEB_W>(aw, D, ws + (int64_t)l * 2 * D, red);
-  block_col_atomic<NV, SEB_W>(ab, D, ws + (int64_t)l * 2 * D + D, red);
-}
-
-// dw += Σ_l ws[l][0], db += Σ_l ws[l][1]; leaves the workspace zero for the next call.
-// 1024 threads = 4 position groups x 256 columns; each thread loads its positions first
-// (independent loads), then zeroes them; the 4 partials meet in LDS.
-__global__ __launch_bounds__(1024) void seq_embed_red_kernel(int L, int D, float* __restrict__ ws,
-                                                             float* __restrict__ dw,
-                                                             float* __restrict__ db) {
-  __shared__ float red[4][256];
-  const int cl = threadIdx.x & 255, lg = threadIdx.x >> 8;
-  const int c = blockIdx.x * 256 + cl;
-  const bool ok = c < 2 * D;
-  float s = 0.f;
-  if (ok) {
-    constexpr int U = 8;
-    for (int l0 = lg; l0 < L; l0 += 4 * U) {
-      float v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int l = l0 + 4 * u;
-        v[u] = l < L ? ws[(int64_t)l * 2 * D + c] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int l = l0 + 4 * u;
-        s += v[u];
-        if (l < L) ws[(int64_t)l * 2 * D + c] = 0.f;
-      }
-    }
-  }
-  red[lg][cl] = s;
-  __syncthreads();
-  if (lg != 0 || !ok) return;
-  s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
-  if (c < D) dw[c] += s;
-  else db[c - D] += s;
+  const int64_t LD = (int64_t)L * D;
+  block_col_fx<NV, SEB_W>(ap, D, accL + (int64_t)l * D, red);
+  block_col_fx<NV, SEB_W>(aw, D, accL + LD + (int64_t)l * D, red);
+  block_col_fx<NV, SEB_W>(ab, D, accL + 2 * LD + (int64_t)l * D, red);
 }
 
 // ------------------------------------------------------------ last-valid gather + concat
@@ -441,8 +411,8 @@ __global__ void user_concat_bwd_kernel(int B, int D, const float* __restrict__ d
                                        const int32_t* __restrict__ rows,
                                        const int64_t* __restrict__ gender, int dg,
                                        const int64_t* __restrict__ country, int dc,
-                                       float* __restrict__ dx, float* __restrict__ dG,
-                                       float* __restrict__ dC, int accumulate) {
+                                       float* __restrict__ dx, int64_t* __restrict__ dG,
+                                       int64_t* __restrict__ dC, int accumulate) {
   const int lane = threadIdx.x & 63;
   const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (b >= B) return;
@@ -452,11 +422,11 @@ __global__ void user_concat_bwd_kernel(int B, int D, const float* __restrict__ d
   for (int k = lane; k < W; k += 64) {
     const float v = dcomb[(int64_t)b * W + k];
     if (k < D) {
-      if (accumulate) atomicAdd(dx + row * D + k, v);
-      else dx[row * D + k] = v;            // rows distinct: each dx row has one writer
-    }
-    else if (k < D + dg) { if (dG) atomicAdd(dG + g * dg + (k - D), v); }
-    else if (dC) atomicAdd(dC + c * dc + (k - D - dg), v);
+      if (accumulate) dx[row * D + k] += v;   // rows distinct: each dx row has one writer
+      else dx[row * D + k] = v;
+    }   // demographic rows shared by users: fixed-point adds (order-independent)
+    else if (k < D + dg) { if (dG) fx_add(dG + g * dg + (k - D), v, TTMI_FX_GRAD); }
+    else if (dC) fx_add(dC + c * dc + (k - D - dg), v, TTMI_FX_GRAD);
   }
 }
 
@@ -719,7 +689,21 @@ extern "C" int ttmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx,
 }
 
 extern "C" int64_t ttmi_layernorm_bwd_workspace(int D) {
-  return (int64_t)LN_REPL * 2 * D * (int64_t)sizeof(float);
+  return (int64_t)LN_REPL * 2 * D * (int64_t)sizeof(int64_t);
+}
+
+extern "C" int ttmi_layernorm_bwd_folds(int D, void* ws, float* dw, float* db, ttmi_fold_desc* out) {
+  TTMI_REQUIRE(D > 0 && D % 4 == 0 && ws && out, "ttmi_layernorm_bwd_folds: bad arguments");
+  int n = 0;
+  float* dst[2] = {dw, db};
+  for (int j = 0; j < 2; ++j) {
+    if (!dst[j]) continue;
+    ttmi_fold_desc& f = out[n++];
+    f.part = static_cast<int64_t*>(ws) + (int64_t)j * D;
+    f.S = LN_REPL; f.s_stride = 2 * (int64_t)D; f.M = 1; f.N = D;
+    f.C = dst[j]; f.ldc = D; f.accumulate = 3; f.fx_shift = TTMI_FX_GRAD;
+  }
+  return TTMI_OK;
 }
 
 extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const float* x,
@@ -727,7 +711,7 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
                                   const float* w, const void* gate, int gate_dtype, int64_t ldg,
                                   float gate_scale, const float* res, float* dx, int64_t lddx,
                                   float* dw, float* db, void* ws, void* dx16, int64_t ld16,
-                                  float drop_p, const uint64_t* drop_seed, hipStream_t s) {
+                                  float drop_p, const uint64_t* drop_seed, int defer, hipStream_t s) {
   TTMI_REQUIRE(M >= 0 && D > 0 && D <= 64 * MAXV, "ttmi_layernorm_bwd: need 0 < D <= %d", 64 * MAXV);
   TTMI_REQUIRE(dy && x && mean && rstd && w && dx, "ttmi_layernorm_bwd: null argument");
   TTMI_REQUIRE(lddy >= D && ldx >= D && lddx >= D && (!gate || ldg >= D), "ttmi_layernorm_bwd: bad ld");
@@ -753,29 +737,19 @@ extern "C" int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t ldd
   }
   // one row per wave when there are no column sums (the frozen text-encoder LayerNorms:
   // a wave walking 16 rows serially ran the stream at ~2.9 TB/s); with sums, 1024 blocks
-  // bound the replicas' adders
+  // bound the replicas' adders.  The column sums go to LN_REPL int64 fixed-point replica
+  // rows (ws [LN_REPL][2][D]; order-independent) folded once: deterministic.
   int grid = (int)std::min<int64_t>((M + 3) / 4, sums ? 1024 : 16384);
-  // small grids (the B = 512 head LayerNorms: 128 blocks) add to dw/db directly: the
-  // contention of that few adders costs less than the fold launch
-  const bool direct = grid <= LN_DIRECT;
-  float* cw = !sums ? nullptr : direct ? dw : (float*)ws;
-  float* cb = !sums ? nullptr : direct ? db : (float*)ws + D;
-  if (direct && sums && (!dw || !db)) {     // one side only: route the other to the workspace
-    if (!dw) cw = (float*)ws;
-    if (!db) cb = (float*)ws + D;
-  }
-  const int nrep = direct ? 1 : LN_REPL;
-  const int64_t rstride = direct ? 0 : 2 * (int64_t)D;
+  int64_t* cw = sums ? static_cast<int64_t*>(ws) : nullptr;
+  int64_t* cb = sums ? static_cast<int64_t*>(ws) + D : nullptr;
   TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(grid), dim3(256), 0, s, M, D, dy,
                                          lddy, x, ldx, mean, rstd, w, gate, gate_dtype == TTMI_F32,
-                                         ldg, gate_scale, res, dx, lddx, cw, cb, nrep, rstride,
+                                         ldg, gate_scale, res, dx, lddx, cw, cb, LN_REPL, 2 * (int64_t)D,
                                          (bf16_t*)dx16, ld16, dp16));
   int rc = ttmi_check_launch("ttmi_layernorm_bwd");
-  if (rc || !sums) return rc;
-  if (direct && dw && db) return TTMI_OK;
-  // (direct with one side NULL: that side went to workspace replica 0; the fold clears it)
+  if (rc || !sums || defer) return rc;      // defer: the caller folds (ttmi_layernorm_bwd_folds)
   hipLaunchKernelGGL(colsum_fold_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, 2 * D, D,
-                     std::min(grid, LN_REPL), (float*)ws, dw, db);
+                     LN_REPL, static_cast<int64_t*>(ws), dw, db);
   return ttmi_check_launch("ttmi_layernorm_bwd/fold");
 }
 
@@ -803,31 +777,54 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
   return ttmi_check_launch("ttmi_seq_embed_fwd");
 }
 
-extern "C" int64_t ttmi_seq_embed_bwd_workspace(int L, int D) {
-  return (int64_t)L * 2 * D * (int64_t)sizeof(float);
+extern "C" int64_t ttmi_seq_embed_bwd_workspace(int64_t V, int L, int D) {
+  if (V <= 0 || L <= 0 || D <= 0) return 0;
+  return ((int64_t)V * D + 3 * (int64_t)L * D) * (int64_t)sizeof(int64_t);
 }
 
-extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, const int64_t* ids, const float* E,
+extern "C" int ttmi_seq_embed_bwd_folds(int64_t V, int L, int D, void* ws, float* dE, float* dP,
+                                        float* dw, float* db, ttmi_fold_desc* out) {
+  TTMI_REQUIRE(V > 0 && L > 0 && D > 0 && D % 4 == 0 && ws && dE && dP && dw && db && out,
+               "ttmi_seq_embed_bwd_folds: bad arguments (D %% 4 == 0)");
+  int64_t* accE = static_cast<int64_t*>(ws);
+  int64_t* accL = accE + V * D;
+  const int64_t LD = (int64_t)L * D;
+  auto set = [&](ttmi_fold_desc& f, const int64_t* part, int64_t S, int64_t ss, int64_t M, float* C) {
+    f.part = part; f.S = S; f.s_stride = ss; f.M = M; f.N = D; f.C = C; f.ldc = D;
+    f.accumulate = 3; f.fx_shift = TTMI_FX_GRAD;      // add, and leave the accumulators zero
+  };
+  set(out[0], accE, 1, V * D, V, dE);
+  set(out[1], accL, 1, LD, L, dP);
+  set(out[2], accL + LD, L, D, 1, dw);
+  set(out[3], accL + 2 * LD, L, D, 1, db);
+  return TTMI_OK;
+}
+
+extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, int64_t V, const int64_t* ids, const float* E,
                                   const float* P, const float* w, const float* mean,
                                   const float* rstd, float drop_p, const uint64_t* drop_seed,
                                   const float* dx, float* dE, float* dP, float* dw, float* db,
-                                  int64_t padding_idx, void* ws, hipStream_t s) {
-  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV, "ttmi_seq_embed_bwd: bad sizes");
-  TTMI_REQUIRE(ids && E && P && w && mean && rstd && dx && dE && dP && ws && (dw == nullptr) == (db == nullptr),
+                                  int64_t padding_idx, void* ws, int defer, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV && D % 4 == 0 && V > 0,
+               "ttmi_seq_embed_bwd: bad sizes (D %% 4 == 0)");
+  TTMI_REQUIRE(ids && E && P && w && mean && rstd && dx && dE && dP && dw && db && ws,
                "ttmi_seq_embed_bwd: null argument");
-  if (B == 0) return TTMI_OK;
-  // V is not needed for the math; rows with out-of-range ids were zero in the forward.
-  const int64_t V = INT64_MAX;
-  const int bpc = 2 * SEB_W;                   // one pass of two rows per wave
-  dim3 grid(L, (B + bpc - 1) / bpc);
-  TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_bwd_kernel<NV>), grid, dim3(64 * SEB_W), 0, s, B, L, D, ids,
-                                         E, P, w, mean, rstd, make_drop(drop_p, drop_seed), dx, dE,
-                                         dP, (float*)ws, padding_idx, V, bpc));
-  const int rc = ttmi_check_launch("ttmi_seq_embed_bwd");
-  if (rc || dw == nullptr) return rc;       // dw = db = NULL: the caller folds ws (ABI 15)
-  hipLaunchKernelGGL(seq_embed_red_kernel, dim3((2 * D + 255) / 256), dim3(1024), 0, s, L, D, (float*)ws,
-                     dw, db);
-  return ttmi_check_launch("ttmi_seq_embed_bwd/reduce");
+  TTMI_REQUIRE(((uintptr_t)ws & 15) == 0, "ttmi_seq_embed_bwd: ws must be 16-byte aligned");
+  if (B > 0) {
+    const int bpc = 2 * SEB_W;                   // one pass of two rows per wave
+    dim3 grid(L, (B + bpc - 1) / bpc);
+    int64_t* accE = static_cast<int64_t*>(ws);
+    TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_bwd_kernel<NV>), grid, dim3(64 * SEB_W), 0, s, B, L, D, ids,
+                                           E, P, w, mean, rstd, make_drop(drop_p, drop_seed), dx, accE,
+                                           accE + V * D, padding_idx, V, bpc));
+    const int rc = ttmi_check_launch("ttmi_seq_embed_bwd");
+    if (rc) return rc;
+  }
+  if (defer) return TTMI_OK;            // the caller folds (ttmi_seq_embed_bwd_folds)
+  ttmi_fold_desc f[4];
+  int rc = ttmi_seq_embed_bwd_folds(V, L, D, ws, dE, dP, dw, db, f);
+  if (rc) return rc;
+  return ttmi_wgrad_fold(0, nullptr, 4, f, s);
 }
 
 extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
@@ -852,7 +849,7 @@ extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float*
 
 extern "C" int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
                                     const int64_t* gender, int dg, const int64_t* country, int dc,
-                                    float* dx, float* dG, float* dC, int accumulate, hipStream_t s) {
+                                    float* dx, int64_t* dG, int64_t* dC, int accumulate, hipStream_t s) {
   TTMI_REQUIRE(B >= 0 && D > 0 && dg >= 0 && dc >= 0, "ttmi_user_concat_bwd: bad sizes");
   TTMI_REQUIRE(dcomb && rows && gender && country && dx, "ttmi_user_concat_bwd: null argument");
   if (B == 0) return TTMI_OK;

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -152,7 +152,7 @@ class LnBwdDesc(ctypes.Structure):
 class FoldDesc(ctypes.Structure):
     """ttmi_fold_desc (include/ttmi.h)."""
     _fields_ = [("part", c_p), ("S", c_i64), ("s_stride", c_i64), ("M", c_i64), ("N", c_i64),
-                ("C", c_p), ("ldc", c_i64), ("accumulate", c_i)]
+                ("C", c_p), ("ldc", c_i64), ("accumulate", c_i), ("fx_shift", c_i)]
 
 
 class ResLnDesc(ctypes.Structure):
@@ -185,13 +185,15 @@ SIGNATURES = {
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
                                  c_i64, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),
+    "ttmi_layernorm_bwd_folds": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i, c_i64,
-                                 c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_p]),
+                                 c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_i, c_p]),
     "ttmi_seq_embed_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_i64, c_p, c_p, c_p, c_f, c_f, c_p, c_p,
                                  c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
-    "ttmi_seq_embed_bwd_workspace": (c_i64, [c_i, c_i]),
-    "ttmi_seq_embed_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p,
-                                 c_p, c_p, c_p, c_i64, c_p, c_p]),
+    "ttmi_seq_embed_bwd_workspace": (c_i64, [c_i64, c_i, c_i]),
+    "ttmi_seq_embed_bwd_folds": (c_i, [c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_seq_embed_bwd": (c_i, [c_i, c_i, c_i, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p,
+                                 c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_p]),
     "ttmi_mha_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_user_concat_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_p,

@@ -208,10 +208,10 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
     d.drop_rows = _p(drop_rows)
     d.res_rows, d.res_L = _p(res_rows), int(res_L)
     d.ln_dw, d.ln_db = _p(ln_dw), _p(ln_db)
-    pend = _PENDING[-1] if _PENDING else None
-    ws = None
-    if pend is not None and (ln_dw is not None or ln_db is not None):
-        # per-workgroup sums, folded in workgroup order with the step's weight gradients
+    folds = []
+    if ln_dw is not None or ln_db is not None:
+        # per-workgroup sums, folded in workgroup order (with the step's weight gradients
+        # inside deferred_wgrad, else right after the launch): bit-reproducible
         _L.load()
         G = int(_L._lib.ttmi_linear_ln_bwd_sum_blocks(M))
         ws = torch.empty(G * 2 * N, device=dx.device, dtype=torch.float32)
@@ -220,9 +220,10 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
             if g is not None:
                 f = FoldDesc()
                 f.part, f.S, f.s_stride, f.M, f.N = ws.data_ptr() + 4 * N * j, G, 2 * N, 1, N
-                f.C, f.ldc, f.accumulate = _p(g), N, 1
-                pend.folds.append((f, ws, g))
+                f.C, f.ldc, f.accumulate, f.fx_shift = _p(g), N, 1, 0
+                folds.append((f, ws, g))
     call("ttmi_linear_ln_bwd", ctypes.byref(d), _s())
+    _run_folds(folds)
     return dx
 
 
@@ -300,7 +301,7 @@ def conv_out_hw(H: int, W: int, k: int, stride: int, pad: int):
     return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
 
 
-CONV_STAT_REPS = 16    # TTMI_CONV_STAT_REPS: BatchNorm column stats are [16][C] replica rows
+CONV_STAT_REPS = 16    # TTMI_CONV_STAT_REPS: BatchNorm column stats are [16][C] int64 replica rows
 
 
 def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int, stride: int,
@@ -320,6 +321,9 @@ def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int,
     for name, (t, n) in need.items():       # an undersized buffer would fault the GPU
         if t is not None and t.numel() < n:
             raise ValueError(f"conv2d: {name} has {t.numel()} elements, needs {n}")
+    for t in (colsum, colsumsq):
+        if t is not None and t.dtype != torch.int64:
+            raise TypeError("conv2d: colsum / colsumsq are int64 fixed-point replica rows")
     d = ConvDesc()
     d.mode, d.N, d.H, d.W, d.C, d.Cin, d.Co = mode, N, H, W, C, Cin, Co
     d.KH = d.KW = k
@@ -359,8 +363,8 @@ def bn2d_fwd(x: Tensor, colsum: Optional[Tensor], colsumsq: Optional[Tensor], w:
     C = x.shape[-1]
     M = x.numel() // C
     for name, t in (("colsum", colsum), ("colsumsq", colsumsq)):
-        if t is not None and t.numel() < CONV_STAT_REPS * C:
-            raise ValueError(f"bn2d_fwd: {name} needs [{CONV_STAT_REPS}][{C}] replica rows")
+        if t is not None and (t.numel() < CONV_STAT_REPS * C or t.dtype != torch.int64):
+            raise ValueError(f"bn2d_fwd: {name} needs [{CONV_STAT_REPS}][{C}] int64 replica rows")
     if y.numel() < x.numel() or (residual is not None and residual.numel() < x.numel()):
         raise ValueError("bn2d_fwd: y / residual smaller than x")
     call("ttmi_bn2d_fwd", M, C, _p(x), _p(colsum), _p(colsumsq), _p(w), _p(b), eps, momentum,
@@ -374,8 +378,8 @@ def bn2d_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, sums:
              gate: Optional[Tensor] = None, g_out: Optional[Tensor] = None) -> Tensor:
     C = x.shape[-1]
     M = x.numel() // C
-    if sums.numel() < 2 * CONV_STAT_REPS * C:
-        raise ValueError(f"bn2d_bwd: sums needs [{CONV_STAT_REPS}][{2 * C}] replica rows")
+    if sums.numel() < 2 * CONV_STAT_REPS * C or sums.dtype != torch.int64:
+        raise ValueError(f"bn2d_bwd: sums needs [{CONV_STAT_REPS}][{2 * C}] int64 replica rows")
     for name, t in (("dy", dy), ("dx", dx), ("gate", gate), ("g_out", g_out)):
         if t is not None and t.numel() < x.numel():
             raise ValueError(f"bn2d_bwd: {name} smaller than x")
@@ -423,16 +427,24 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, 
                   gate_scale: float = 1.0, res: Optional[Tensor] = None,
                   dx16: Optional[Tensor] = None, drop: Drop = NO_DROP) -> Tensor:
     """LayerNorm backward (+ gate, + residual); dx16 (bf16) optionally receives
-    bf16(dropout(dx)) (drop: the residual branch's dropout, keep index m*D + n)."""
+    bf16(dropout(dx)) (drop: the residual branch's dropout, keep index m*D + n).  The weight /
+    bias sums go through int64 fixed-point replicas (bit-reproducible), folded with the
+    deferred weight gradients inside ``deferred_wgrad`` (else right away)."""
     M, D = x.shape
-    ws = _zero_ws("ttmi_layernorm_bwd_workspace", (D,), x.device) \
-        if (dw is not None or db is not None) else None
+    sums = dw is not None or db is not None
+    ws = _zero_ws("ttmi_layernorm_bwd_workspace", (D,), x.device) if sums else None
     if dx16 is not None and dx16.dtype != torch.bfloat16:
         raise ValueError("layernorm_bwd: dx16 must be bf16")
+    defer = bool(_PENDING) and sums
     call("ttmi_layernorm_bwd", M, D, _p(dy), D, _p(x), D, _p(mean), _p(rstd), _p(w), _p(gate),
          code(gate.dtype) if gate is not None else 0, D, gate_scale, _p(res), _p(dx), D, _p(dw),
          _p(db), _p(ws), _p(dx16), dx16.stride(0) if dx16 is not None else 0, float(drop[0]),
-         _p(drop[1]), _s())
+         _p(drop[1]), int(defer), _s())
+    if defer:
+        out = (FoldDesc * 2)()
+        call("ttmi_layernorm_bwd_folds", D, _p(ws), _p(dw), _p(db), out)
+        n = (dw is not None) + (db is not None)
+        _PENDING[-1].folds.extend((out[j], ws, dw, db) for j in range(n))
     return dx
 
 
@@ -469,18 +481,66 @@ def _zero_ws(sizer: str, args: tuple, device) -> Tensor:
     return ws
 
 
+_FX_ZERO: Dict[tuple, Tensor] = {}
+FX_GRAD_SHIFT = 36      # TTMI_FX_GRAD_SHIFT (include/ttmi.h)
+
+
+def _fx_zero(name: str, numel: int, device) -> Tensor:
+    """Persistent zero int64 fixed-point accumulator (one per (device, name, size)); the fold
+    that converts it (fx_folds) leaves it zero again, so graph replays reuse it."""
+    key = (str(device), name, int(numel))
+    t = _FX_ZERO.get(key)
+    if t is None:
+        t = _FX_ZERO[key] = torch.zeros(max(int(numel), 2), device=device, dtype=torch.int64)
+    return t
+
+
+def _run_folds(folds) -> None:
+    """(FoldDesc, keep-alive...) tuples: deferred to the open ``deferred_wgrad`` block's flush,
+    else launched now."""
+    if not folds:
+        return
+    pend = _PENDING[-1] if _PENDING else None
+    if pend is not None:
+        pend.folds.extend(folds)
+        return
+    farr = (FoldDesc * len(folds))(*[f for f, *_ in folds])
+    call("ttmi_wgrad_batch", 0, (ctypes.POINTER(WgradDesc) * 1)(), len(folds), farr, _s())
+
+
+def fx_folds(pairs) -> None:
+    """Convert int64 fixed-point accumulators into fp32 gradients (added; accumulators left
+    zero): pairs of (acc, grad) with acc shaped like grad (None pairs skipped)."""
+    folds = []
+    for acc, g in pairs:
+        if acc is None or g is None:
+            continue
+        N = g.shape[-1]
+        M = g.numel() // N
+        f = FoldDesc()
+        f.part, f.S, f.s_stride, f.M, f.N = acc.data_ptr(), 1, M * N, M, N
+        f.C, f.ldc, f.accumulate, f.fx_shift = _p(g), N, 3, FX_GRAD_SHIFT
+        folds.append((f, acc, g))
+    _run_folds(folds)
+
+
 def seq_embed_bwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, mean: Tensor, rstd: Tensor,
                   dx: Tensor, dE: Tensor, dP: Tensor, dw: Tensor, db: Tensor, *,
                   drop: Drop = NO_DROP, padding_idx: int = 0):
+    """SASRec input-block backward (ttmi_seq_embed_bwd): the embedding-row scatter and the
+    position / LayerNorm sums accumulate in int64 fixed point (bit-reproducible), converted
+    by folds that run with the deferred weight gradients (else right away)."""
     B, L = ids.shape
-    D = E.shape[1]
-    ws = _zero_ws("ttmi_seq_embed_bwd_workspace", (L, D), dx.device)
-    defer = bool(_PENDING) and D % 4 == 0
-    call("ttmi_seq_embed_bwd", B, L, D, _p(ids), _p(E), _p(P), _p(w), _p(mean), _p(rstd),
-         float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), None if defer else _p(dw),
-         None if defer else _p(db), padding_idx, _p(ws), _s())
-    if defer:       # the LN partials fold with the deferred weight gradients (ws left zero)
-        ln_sum_folds(ws, (dw, db), 2, D, S=L, consume=True)
+    V, D = E.shape
+    ws = _zero_ws("ttmi_seq_embed_bwd_workspace", (V, L, D), dx.device)
+    defer = bool(_PENDING)
+    call("ttmi_seq_embed_bwd", B, L, D, V, _p(ids), _p(E), _p(P), _p(w), _p(mean), _p(rstd),
+         float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), _p(dw), _p(db), padding_idx,
+         _p(ws), int(defer), _s())
+    if defer:       # the four conversions fold with the deferred weight gradients (ws left zero)
+        out = (FoldDesc * 4)()
+        call("ttmi_seq_embed_bwd_folds", V, L, D, _p(ws), _p(dE), _p(dP), _p(dw), _p(db), out)
+        _PENDING[-1].folds.extend((out[j], ws, dE, dP, dw, db) for j in range(4))
 
 
 # ----------------------------------------------------------------------------- attention
@@ -512,10 +572,15 @@ def user_concat_fwd(x: Tensor, len_src: Optional[Tensor], gender: Tensor, G: Ten
 def user_concat_bwd(dcomb: Tensor, rows: Tensor, gender: Tensor, dg: int, country: Tensor,
                     dc: int, dx: Tensor, dG: Optional[Tensor], dC: Optional[Tensor],
                     accumulate: bool = True):
+    """Concat backward: dx rows (one writer each) and the demographic embedding gradients,
+    whose rows users share, through int64 fixed-point accumulators folded into dG / dC."""
     B = dcomb.shape[0]
     D = dcomb.shape[1] - dg - dc
+    aG = _fx_zero("concat.dG", dG.numel(), dG.device) if dG is not None else None
+    aC = _fx_zero("concat.dC", dC.numel(), dC.device) if dC is not None else None
     call("ttmi_user_concat_bwd", B, D, _p(dcomb), _p(rows), _p(gender), dg, _p(country), dc,
-         _p(dx), _p(dG), _p(dC), int(accumulate), _s())
+         _p(dx), _p(aG), _p(aC), int(accumulate), _s())
+    fx_folds([(aG, dG), (aC, dC)])
 
 
 # ----------------------------------------------------------------------------- batchnorm
@@ -614,14 +679,9 @@ def ln_sum_folds(ws: Tensor, grads: Sequence[Tensor], rows: int, D: int, S: Opti
     for j, g in enumerate(grads):
         f = FoldDesc()
         f.part, f.S, f.s_stride, f.M, f.N = ws.data_ptr() + 4 * D * j, nblk, rows * D, 1, D
-        f.C, f.ldc, f.accumulate = _p(g), D, 3 if consume else 1
+        f.C, f.ldc, f.accumulate, f.fx_shift = _p(g), D, 3 if consume else 1, 0
         folds.append((f, ws, g))
-    pend = _PENDING[-1] if _PENDING else None
-    if pend is not None:
-        pend.folds.extend(folds)
-    else:
-        farr = (FoldDesc * len(folds))(*[f for f, *_ in folds])
-        call("ttmi_wgrad_batch", 0, (ctypes.POINTER(WgradDesc) * 1)(), len(folds), farr, _s())
+    _run_folds(folds)
 
 
 def item_head_fusable(W: Dict[str, Tensor], modal: Tensor, dtype) -> bool:
@@ -981,7 +1041,9 @@ def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: 
     d.lnw, d.n2w = _p(P["fusion_layer.1.weight"]), _p(P[pre + "norm2.weight"])
     (d.d1_p, s1), (d.d2_p, s2) = [(float(p), sd) for p, sd in drops]
     d.d1_seed, d.d2_seed = _p(s1), _p(s2)
-    d.dG, d.dC = _p(dG), _p(dC)
+    aG = _fx_zero("head.dG", dG.numel(), dev)      # int64 fixed point (ABI 16), folded below
+    aC = _fx_zero("head.dC", dC.numel(), dev)
+    d.dG, d.dC = _p(aG), _p(aC)
     for k in ("dz16", "dy2", "dz1", "dx1", "dy1", "dctx"):
         setattr(d, k, _p(o[k]))
     d.ws = _p(ws)
@@ -990,6 +1052,7 @@ def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: 
     else:      # the item head's row-local backward on the idle CUs (ABI 15)
         call("ttmi_user_item_head_bwd", ctypes.byref(d), ctypes.byref(co_item), _s())
     ln_sum_folds(ws, ln_grads, 4, D)
+    fx_folds([(aG, dG), (aC, dC)])
     return o
 
 

@@ -77,11 +77,11 @@ def test_conv_fwd_dgrad_wgrad(gpu_pkg, monkeypatch, bm, N, Cin, H, W, Co, k, s, 
     ops.conv_weight_prep(w.to(DEV), Cp, wf, wd)
     y = torch.empty(N, Ho, Wo, Co, device=DEV, dtype=torch.bfloat16)
     R = ops.CONV_STAT_REPS
-    csr = torch.zeros(R, Co, device=DEV)
-    cqr = torch.zeros(R, Co, device=DEV)
+    csr = torch.zeros(R, Co, device=DEV, dtype=torch.int64)     # int64 fixed point, 2^-24
+    cqr = torch.zeros(R, Co, device=DEV, dtype=torch.int64)
     ops.conv2d(ops.FWD, N, H, W, Cp, Cin, Co, k, s, p, x=xd, w=wf, out=y, colsum=csr,
                colsumsq=cqr)
-    cs, cq = csr.sum(0), cqr.sum(0)
+    cs, cq = csr.sum(0).double() * 2.0 ** -24, cqr.sum(0).double() * 2.0 ** -24
     torch.cuda.synchronize()
     yr = y_ref.detach()
     assert rel(nchw(y.float()), yr) < 8e-3
@@ -127,13 +127,15 @@ def test_bn2d_fwd_bwd(gpu_pkg, C, relu, res):
     y_ref.backward(dy)
     xd = nhwc(x).to(torch.bfloat16).to(DEV)
     R = ops.CONV_STAT_REPS                    # replica rows: spread the sums over them
-    cs = torch.zeros(R, C)
-    cq = torch.zeros(R, C)
-    cs[0] = nhwc(x)[:1].sum((0, 1, 2))
-    cs[R - 1] = nhwc(x)[1:].sum((0, 1, 2))
-    cq[0] = (nhwc(x)[:1] ** 2).sum((0, 1, 2))
-    cq[R - 1] = (nhwc(x)[1:] ** 2).sum((0, 1, 2))
-    cs, cq = cs.to(DEV), cq.to(DEV)
+    cs = torch.zeros(R, C, dtype=torch.float64)
+    cq = torch.zeros(R, C, dtype=torch.float64)
+    cs[0] = nhwc(x)[:1].double().sum((0, 1, 2))
+    cs[R - 1] = nhwc(x)[1:].double().sum((0, 1, 2))
+    cq[0] = (nhwc(x)[:1].double() ** 2).sum((0, 1, 2))
+    cq[R - 1] = (nhwc(x)[1:].double() ** 2).sum((0, 1, 2))
+    # int64 fixed point, scale 2^24 (TTMI_FX_STAT_SHIFT), as the conv epilogue writes them
+    cs = torch.round(cs * 2.0 ** 24).to(torch.int64).to(DEV)
+    cq = torch.round(cq * 2.0 ** 24).to(torch.int64).to(DEV)
     y = torch.empty_like(xd)
     mean, rstd = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
     rmd, rvd, nb = rm.to(DEV), rv.to(DEV), torch.zeros(1, device=DEV, dtype=torch.int64)
@@ -142,7 +144,7 @@ def test_bn2d_fwd_bwd(gpu_pkg, C, relu, res):
     torch.cuda.synchronize()
     assert rel(nchw(y.float()), y_ref.detach()) < 8e-3
     assert rel(rmd, rm_ref) < 1e-5 and rel(rvd, rv_ref) < 1e-4 and int(nb) == 1
-    sums = torch.zeros(ops.CONV_STAT_REPS * 2 * C, device=DEV)
+    sums = torch.zeros(ops.CONV_STAT_REPS * 2 * C, device=DEV, dtype=torch.int64)
     dx = torch.empty_like(xd)
     dw, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
     gout = torch.empty_like(xd)

@@ -12,6 +12,14 @@ stages device tensors through the host under gloo — the arithmetic is the same
   rank 0's at the step start updated with rank r's batch.  Both local negatives and
   ``global_negatives=True`` (oracle: the reference InfoNCE over both ranks' embeddings,
   differentiated through both ranks' towers).  fp32 compute: params 2e-4 relative.
+* The bf16 product step at D = 128 (every fused head on its fused path: co-launched user /
+  item heads, ``infonce_fwd_pre`` with the loss accumulator, the fused item BatchNorm, the
+  overlap hook that flushes the deferred weight gradients at the layer-1 cut) with dropout
+  on, local and global negatives: run with ``overlap_grad_sync`` on and off, the flat
+  parameters, AdamW moments and BatchNorm buffers are bit-identical (the step is
+  deterministic, so any flush-placement or bucket-split error shows as a bit difference),
+  identical on both ranks, and the losses stay within the bf16 emulation's distance of the
+  fp32 DDP oracle.
 """
 import importlib
 import os
@@ -23,6 +31,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from bf16emu import bf16_linears
 from conftest import GOLDEN, PKG_NAME, ROOT
 from oracle import two_tower_ref as ref
 
@@ -111,9 +120,10 @@ def _batch(rank, step):
     return ref.synthetic_batch(B, L, V, NG, NC, num_users=6, generator=g)
 
 
-def _oracle_ddp(params, global_negatives):
+def _oracle_ddp(params, global_negatives, batch=None, p_drop=0.0, seeds=None):
     """fp32 CPU oracle of STEPS DDP steps at WORLD ranks; returns (params, running per rank,
-    mean losses)."""
+    mean losses).  ``seeds(rank, step)``: the rank's hash-dropout site seeds (p_drop > 0)."""
+    batch = batch or _batch
     params = {k: v.clone() for k, v in params.items()}
     opt = {}
     running = [ref.init_running() for _ in range(WORLD)]
@@ -126,10 +136,12 @@ def _oracle_ddp(params, global_negatives):
         ip = {k[len("item_tower."):]: v for k, v in leaves.items() if k.startswith("item_tower.")}
         us, its, uids = [], [], []
         for r in range(WORLD):
-            b = _batch(r, s)
+            b = batch(r, s)
+            drop = ref.HashDropout(seeds(r, s)) if p_drop > 0 else None
             us.append(ref.user_tower_forward(up, b["history_ids"], b["user_gender"],
-                                             b["user_country"], b["history_mask"], 4, 2, 0.0))
-            its.append(ref.item_fusion_forward(ip, b["target_modal"], 0.0, None, running[r]))
+                                             b["user_country"], b["history_mask"], 4, 2, p_drop,
+                                             drop))
+            its.append(ref.item_fusion_forward(ip, b["target_modal"], p_drop, drop, running[r]))
             uids.append(b["user_idx"])
         if global_negatives:
             loss = ref.infonce(torch.cat(us), torch.cat(its), torch.cat(uids))[0]
@@ -205,4 +217,63 @@ def _trainstep_worker(rank, global_negatives, use_graph, out):
 def test_trainstep_world2_vs_ddp_oracle(tmp_path, global_negatives, use_graph):
     out = str(tmp_path / "r0.pt")
     _run(_trainstep_worker, global_negatives, use_graph, out)
+    assert os.path.exists(out)
+
+
+# ------------------------------------------------------------------ bf16 product step at N = 2
+V16, D16, L16, B16, P16 = 997, 128, 20, 64, 0.1
+
+
+def _batch16(rank, step):
+    g = torch.Generator().manual_seed(2000 + 10 * step + rank)
+    return ref.synthetic_batch(B16, L16, V16, NG, NC, num_users=20, generator=g)
+
+
+def _trainstep_bf16_worker(rank, global_negatives, out):
+    pkg = importlib.import_module(PKG_NAME)
+    F = pkg.functional
+    states = []
+    for overlap in (True, False):
+        torch.manual_seed(0)
+        m = pkg.TwoTowerModel(vocab_size=V16, tabular_input_dim=128, num_genders=NG,
+                              num_countries=NC, max_seq_len=L16, user_embedding_dim=D16,
+                              item_embedding_dim=D16, user_dropout=P16,
+                              compute_dtype=torch.bfloat16, precomputed_modalities=True,
+                              global_negatives=global_negatives).cuda()
+        m.item_tower.fusion_layer[3].p = P16
+        p0 = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+        step = pkg.TrainStep(m, lr=LR, use_graph=True, seed=rank + 1, overlap_grad_sync=overlap)
+        assert step.world == WORLD and step.overlap == overlap and step.broadcast_buffers
+        losses = []
+        for s in range(STEPS):
+            b = {k: v.cuda() for k, v in _batch16(rank, s).items()}
+            loss = step.step(b).detach().reshape(1).clone()
+            dist.all_reduce(loss)
+            losses.append(float(loss) / WORLD)
+        torch.cuda.synchronize()
+        st = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        st["__m"], st["__v"] = step.flat.exp_avg.cpu().clone(), step.flat.exp_avg_sq.cpu().clone()
+        flat = step.flat.data.detach().clone()
+        other = flat.clone()
+        dist.broadcast(other, 0)
+        assert torch.equal(flat, other)              # both ranks hold the same parameters
+        states.append((st, losses))
+    (sa, la), (sb, lb) = states
+    bad = [k for k in sa if not torch.equal(sa[k], sb[k])]
+    assert not bad, ("overlap on/off differ", bad[:8])
+    assert la == lb
+    seeds = (lambda r, s: F.site_seeds(r + 1, s + 1))
+    _, _, wl = _oracle_ddp(p0, global_negatives, _batch16, P16, seeds)
+    with bf16_linears():
+        _, _, el = _oracle_ddp(p0, global_negatives, _batch16, P16, seeds)
+    for s in range(STEPS):
+        assert abs(la[s] - wl[s]) <= 2 * abs(el[s] - wl[s]) + 2e-3, (s, la[s], wl[s], el[s])
+    if rank == 0:
+        torch.save({"losses": la}, out)
+
+
+@pytest.mark.parametrize("global_negatives", [False, True])
+def test_trainstep_world2_bf16_fused_overlap_bitexact(tmp_path, global_negatives):
+    out = str(tmp_path / "r0.pt")
+    _run(_trainstep_bf16_worker, global_negatives, out)
     assert os.path.exists(out)

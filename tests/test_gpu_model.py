@@ -19,57 +19,12 @@ import numpy as np
 import pytest
 import torch
 
+from bf16emu import bf16_linears, check_bf16_grad, cosine, frob, rel
 from conftest import load_golden, sub
 from oracle import two_tower_ref as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-
-
-def rel(a, b):
-    a = torch.as_tensor(a).detach().double().cpu()
-    b = torch.as_tensor(b).detach().double().cpu()
-    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
-
-
-class _BfLinear(torch.autograd.Function):
-    """y = bf16(x)·bf16(w)ᵀ (+b); backward rounds the incoming gradient to bf16 before both
-    products, as the kernels do (dY is stored bf16 for the dX and dW GEMMs)."""
-
-    @staticmethod
-    def forward(ctx, x, w):
-        xb, wb = _bf(x), _bf(w)
-        ctx.save_for_backward(xb, wb)
-        return xb @ wb.t()
-
-    @staticmethod
-    def backward(ctx, dy):
-        xb, wb = ctx.saved_tensors
-        dyb = _bf(dy)
-        return dyb @ wb, dyb.reshape(-1, dyb.shape[-1]).t() @ xb.reshape(-1, xb.shape[-1])
-
-
-def _bf(t):
-    return t.to(torch.bfloat16).to(torch.float32)
-
-
-@contextlib.contextmanager
-def bf16_linears():
-    """Run the CPU oracle with every GEMM's operands rounded to bf16 (forward and backward)
-    and the QKV / FFN-hidden activations stored in bf16, as the kernels do."""
-    orig = ref.linear
-
-    def lin(x, w, b):
-        y = _BfLinear.apply(x, w)
-        y = y + b if b is not None else y
-        if w.shape[0] in (3 * w.shape[1], 4 * w.shape[1]):
-            y = _bf(y)
-        return y
-    ref.linear = lin
-    try:
-        yield
-    finally:
-        ref.linear = orig
 
 
 def bf16_emulated(z):
@@ -348,18 +303,117 @@ def test_pruned_last_layer_equals_full(gpu_pkg, p):
         assert rel(grads[0][k], grads[1][k]) < 1e-4, k
 
 
-def test_train_step_graph_equals_eager_and_learns(gpu_pkg):
-    """bf16, dropout on: graph replay == eager schedule step for step; loss decreases."""
-    m1, batch = _cfg2(gpu_pkg, torch.bfloat16, B=256, p=0.1, seed=7)
-    m2, _ = _cfg2(gpu_pkg, torch.bfloat16, B=256, p=0.1, seed=7)
+def _state_bits(m, step):
+    """Every parameter, buffer and AdamW moment of a TrainStep, for bit comparisons."""
+    out = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    out["__exp_avg"] = step.flat.exp_avg.detach().clone()
+    out["__exp_avg_sq"] = step.flat.exp_avg_sq.detach().clone()
+    return out
+
+
+def assert_bit_equal(a, b):
+    assert a.keys() == b.keys()
+    bad = [k for k in a if not torch.equal(a[k], b[k])]
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_cfg2_graph_equals_eager_bitexact(gpu_pkg, p):
+    """The benchmarked step (cfg 2: B 512, L 50, D 128, V 10,136, bf16) is deterministic: the
+    HIP-graph replay and the eager schedule give bit-identical losses, parameters, BatchNorm
+    buffers and AdamW moments for 3 steps (every cross-workgroup sum is fixed-order or int64
+    fixed point: the embedding scatter, the LN / BN column sums, the split weight gradients)."""
+    m1, batch = _cfg2(gpu_pkg, torch.bfloat16, p=p, seed=7)
+    m2, _ = _cfg2(gpu_pkg, torch.bfloat16, p=p, seed=7)
     bd = {k: v.to(DEV) for k, v in batch.items()}
     s1 = gpu_pkg.TrainStep(m1, lr=1e-3, use_graph=True, seed=11)
     s2 = gpu_pkg.TrainStep(m2, lr=1e-3, use_graph=False, seed=11)
+    for i in range(3):
+        l1, l2 = float(s1.step(bd)), float(s2.step(bd))
+        assert l1 == l2, (i, l1, l2)
+    torch.cuda.synchronize()
+    assert_bit_equal(_state_bits(m1, s1), _state_bits(m2, s2))
+
+
+def test_train_step_graph_learns(gpu_pkg):
+    """bf16, dropout on: 30 graph replays on one batch drive the loss down."""
+    m1, batch = _cfg2(gpu_pkg, torch.bfloat16, B=256, p=0.1, seed=7)
+    bd = {k: v.to(DEV) for k, v in batch.items()}
+    s1 = gpu_pkg.TrainStep(m1, lr=1e-3, use_graph=True, seed=11)
     l1 = [float(s1.step(bd)) for _ in range(30)]
-    l2 = [float(s2.step(bd)) for _ in range(30)]
-    assert abs(l1[0] - l2[0]) < 1e-5, (l1[0], l2[0])           # same params, same masks
-    assert np.allclose(l1[1:3], l2[1:3], rtol=0, atol=5e-3), (l1[:3], l2[:3])
     assert l1[-1] < l1[0] - 0.3, l1
+
+
+def _grad_from_moments(step, prev_m):
+    """The step's fp32 gradient, recovered from AdamW's first moment (m_t = β1 m_{t-1} +
+    (1 - β1) g_t; the fused AdamW clears the gradient buffer itself)."""
+    m = step.flat.exp_avg.detach().double()
+    g = (m - 0.9 * prev_m) / 0.1
+    return g, m
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_cfg2_bf16_trainstep_vs_oracle_full_size(gpu_pkg, p):
+    """The exact benchmarked step — bf16 TrainStep (fused user / item heads, co-launched
+    item head, fused InfoNCE with the in-launch combine and loss accumulator, grouped
+    weight gradients, fused AdamW) at BASELINE cfg 2 (B 512, L 50, D 128, V 10,136) — against
+    the fp32 oracle's train_step (reference src/train.py:41-76 loop body, two_tower.py:68-142)
+    for 2 steps, dropout off and on (the oracle restates the kernels' hash dropout):
+      * loss per step within 1e-3 of the fp32 oracle (the north-star bar);
+      * step-1 gradients (recovered from AdamW's first moment) by direction and norm against
+        the bf16-emulated oracle (check_bf16_grad);
+      * the 2-step parameter update by direction: cosine(Δ_gpu, Δ_fp32) at least the bf16
+        emulation's cosine − 0.05, norm ratio within 2x the emulation's deviation + 0.05.
+    Exactly-zero true gradients (in_proj bias's key third, the bias ahead of BatchNorm) are
+    AdamW-amplified noise in every implementation and are skipped."""
+    F = gpu_pkg.functional
+    base = 11
+    m, batch = _cfg2(gpu_pkg, torch.bfloat16, p=p, seed=21)
+    b2 = ref.synthetic_batch(512, 50, 10136, generator=torch.Generator().manual_seed(99))
+    batches = [batch, b2]
+    p0 = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    step = gpu_pkg.TrainStep(m, lr=1e-3, use_graph=True, seed=base)
+    losses, grads1 = [], None
+    prev_m = torch.zeros_like(step.flat.exp_avg, dtype=torch.float64)
+    for i, b in enumerate(batches):
+        losses.append(float(step.step({k: v.to(DEV) for k, v in b.items()})))
+        g, prev_m = _grad_from_moments(step, prev_m)
+        if i == 0:
+            grads1 = {k: v.detach().double().cpu().clone() for k, v in step.flat.views(g).items()}
+    got = {k: v.detach().cpu().double() for k, v in m.named_parameters()}
+
+    def oracle(emulate):
+        params = {k: v.clone() for k, v in p0.items()}
+        opt, running, ls, g1 = {}, ref.init_running(), [], None
+        for i, b in enumerate(batches):
+            drop = ref.HashDropout(F.site_seeds(base, i + 1)) if p > 0 else None
+            leaves = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+            ctx = bf16_linears() if emulate else contextlib.nullcontext()
+            with ctx:
+                loss, _, _, _ = ref.two_tower_loss(leaves, b, p_drop=p, drop=drop, running=running)
+                loss.backward()
+            ls.append(float(loss))
+            gr = {k: v.grad for k, v in leaves.items()}
+            if i == 0:
+                g1 = {k: v.detach().double().clone() for k, v in gr.items()}
+            with torch.no_grad():
+                ref.adamw_(params, gr, opt, lr=1e-3)
+        return ls, g1, {k: v.double() for k, v in params.items()}
+
+    l_ref, g_ref, p_ref = oracle(False)
+    l_emu, g_emu, p_emu = oracle(True)
+    for i in range(2):
+        assert abs(losses[i] - l_ref[i]) <= 1e-3, (i, losses[i], l_ref[i], l_emu[i])
+    skip = ("in_proj_bias", "item_tower.fusion_layer.0.bias")
+    for k in g_ref:
+        if any(s in k for s in skip):
+            continue
+        check_bf16_grad(k, grads1[k], g_ref[k], g_emu[k])
+        d_gpu, d_ref, d_emu = got[k] - p0[k].double(), p_ref[k] - p0[k].double(), p_emu[k] - p0[k].double()
+        c_gpu, c_emu = cosine(d_gpu, d_ref), cosine(d_emu, d_ref)
+        assert c_gpu >= c_emu - 0.05, (k, c_gpu, c_emu)
+        n_gpu, n_emu = d_gpu.norm() / d_ref.norm(), d_emu.norm() / d_ref.norm()
+        assert abs(n_gpu - 1) <= 2 * abs(n_emu - 1) + 0.05, (k, float(n_gpu), float(n_emu))
 
 
 @pytest.mark.parametrize("collide", [False, True])
