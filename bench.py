@@ -351,7 +351,7 @@ def cpu_baseline(B: int, budget_s: float = 20.0):
     from oracle import two_tower_ref as ref
     threads = torch.get_num_threads()
     g = torch.Generator().manual_seed(0)
-    params = ref.init_params(V, generator=g)
+    params = ref.init_params(V, D=D, generator=g)
     batch = ref.synthetic_batch(B, L, V, generator=g)
     running = ref.init_running()
     state = {}
@@ -608,10 +608,15 @@ def main():
                          "global in-batch negatives (all-gather of every rank's embeddings, "
                          "BASELINE configs[4]); eval = global "
                          "retrieval evaluation over the catalogue (SURVEY 8f rank 2)")
+    ap.add_argument("--dim", type=int, default=128,
+                    help="d_model of both towers (128 = BASELINE cfg 2; 256 = the reference's "
+                         "own default, src/train.py:289-297)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
+    global D
+    D = args.dim
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -698,7 +703,7 @@ def main():
             ((TEXT_FLOPS_PER_SAMPLE * B + TEXT_FLOPS_PER_BATCH) if cfg4 else 0.0) + \
             (2.0 * world * B * D * 3 * B if cfg5 else 0.0)     # +2·C·D·3 per pair
         step_tf = flops * args.steps / el / 1e12 * world
-        workload = ("cfg2: SASRec L=50 D=128 H=4 x2 layers + late-fusion head on "
+        workload = (f"cfg2: SASRec L=50 D={D} H=4 x2 layers + late-fusion head on "
                     "precomputed 512-d modality embeddings + in-batch InfoNCE; "
                     "fwd+bwd+AdamW, dropout 0.1")
         if cfg5:
@@ -722,7 +727,7 @@ def main():
             "dtype": "bf16", "data": "synthetic (SURVEY §8d distributions), random-init weights",
             "config": {"workload": workload,
                        "global_batch": world * B, "per_gpu_batch": B, "seq_len": L,
-                       "vocab": V, "parallelism": f"dp{world}",
+                       "vocab": V, "d_model": D, "parallelism": f"dp{world}",
                        "graph": not args.no_graph},
             "roofline": roof,
             "step_mfma": {"achieved": round(step_tf, 3), "peak": PEAK_BF16_TFLOPS,

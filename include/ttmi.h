@@ -396,6 +396,14 @@ int ttmi_avgpool_bwd(int N, int HW, int C, const void* dy, int dy_dtype, const u
  * ---------------------------------------------------------------------------------- */
 int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                const double* hyper, const int32_t* step, int zero_grad, hipStream_t stream);
+/* ttmi_adamw where the gradient of elements [fx_off, fx_off + fx_len) is read from an int64
+ * fixed-point accumulator fx (value = fx[i - fx_off]·2^-fx_shift; ttmi_seq_embed_bwd's
+ * item-embedding rows, ABI 16) instead of g, and fx (not g) is cleared there: the train step
+ * then skips the fold that would convert it into g.  fx_off, fx_len multiples of 4, fx 16-B
+ * aligned; fx = NULL is ttmi_adamw. */
+int ttmi_adamw_fx(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
+                  const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
+                  int64_t fx_off, int64_t fx_len, int fx_shift, hipStream_t stream);
 int ttmi_step_inc(int32_t* step, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------

@@ -475,7 +475,7 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
     }
   }
   // dw / db: sum the tile's 16 rows (one DPP row) into this wave's own LDS row (sdw / sdb
-  // point at it): one writer per column, tiles in the wave's program order (deterministic;
+  // point at it): one adder per column, tiles in the wave's program order (deterministic;
   // the waves' rows are summed in wave order at the end)
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -483,9 +483,9 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
     for (int e = 0; e < 8; ++e) {
       const float a = row16_sum(dy[8 * p + e] * xh[8 * p + e]);
       const float b = row16_sum(dy[8 * p + e]);
-      if (li == 0) {
-        sdw[32 * p + 8 * lg + e] += a;
-        sdb[32 * p + 8 * lg + e] += b;
+      if (li == 0) {          // ds_add on the wave's own row: program order, no read stall
+        atomicAdd(sdw + 32 * p + 8 * lg + e, a);
+        atomicAdd(sdb + 32 * p + 8 * lg + e, b);
       }
     }
   }
@@ -1136,12 +1136,14 @@ WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax, bool allow3
 // operand row slice once for twice the outputs of a 64 x 64 one, halving what the CUs ingest
 // (the family is bound by per-CU ingest from L2 / Infinity Cache), at one workgroup per CU
 // (128 KB ring).  TTMI_WGRAD_GROUP="T:S" (T = 64 or 128, S = splits per long-GEMM tile, 0 =
-// the 64-tile default sizing) selects it; the default is the measured best.
+// the 64-tile default sizing) selects it.  Default 128:12, the measured best (cfg-2 step on
+// MI355X, tools/wgrad_group_sweep.sh: per GEMM 64:0 4.73 µs, 128:8 5.11, 128:12 4.28,
+// 128:16 5.02, 128:24 4.83, 128:32 5.01).
 struct WgradGroupCfg { int tile, splits; };
 
 WgradGroupCfg wgrad_group_cfg() {
   static const WgradGroupCfg cfg = [] {
-    WgradGroupCfg c{64, 0};
+    WgradGroupCfg c{128, 12};
     if (const char* e = getenv("TTMI_WGRAD_GROUP")) {
       int t = 0, sp = 0;
       if (sscanf(e, "%d:%d", &t, &sp) >= 1 && (t == 64 || t == 128)) c = WgradGroupCfg{t, std::max(sp, 0)};
@@ -1176,13 +1178,13 @@ int64_t wgrad_ws_bytes(const WgradPlan& p, int64_t M, int64_t N) {
   return al256((int64_t)p.S * M * N * 4) + al256((int64_t)p.S * M * 4);
 }
 
-constexpr int FOLD_SEGS = 32;   // kernarg: 32 x 96 B (a cfg-2 step folds ~24 segments)
+constexpr int FOLD_SEGS = 32;   // kernarg: 32 x 100 B (a cfg-2 step folds ~24 segments)
 struct FoldSeg {
   const void* part; const float* part_rs; float* C; float* rs;
   int64_t M, N, ldc, units, base, s_stride;   // s_stride: elements between split slabs
   int S, acc, fx;                             // fx > 0: int64 fixed-point partials, 2^-fx
 };
-struct FoldArgs { FoldSeg seg[FOLD_SEGS]; int n; int64_t total; };
+struct FoldArgs { FoldSeg seg[FOLD_SEGS]; int blk_begin[FOLD_SEGS + 1]; int n; int64_t total; };
 
 // The segment is read straight from the kernel-argument segment at the uniform offset
 // blockIdx.y (scalar loads); copying the argument array to a local and indexing it
@@ -1250,7 +1252,14 @@ TTMI_DEV void fold_store(const FoldSeg& sg, int64_t u, int64_t nq, float4 v) {
 
 __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   (void)a;
-  const auto& sgk = ((KFoldArgs)__builtin_amdgcn_kernarg_segment_ptr())->seg[blockIdx.y];
+  // segment k owns blocks [blk_begin[k], blk_begin[k+1]) of the flat grid (each sized to its
+  // units: launching the largest segment's block count for every segment dispatched tens of
+  // thousands of empty blocks)
+  const KFoldArgs ka = (KFoldArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  int k = 0;
+  while (k + 1 < ka->n && (int)blockIdx.x >= ka->blk_begin[k + 1]) ++k;
+  const int bx = (int)blockIdx.x - ka->blk_begin[k], nbx = ka->blk_begin[k + 1] - ka->blk_begin[k];
+  const auto& sgk = ka->seg[k];
   FoldSeg sg;
   sg.part = sgk.part; sg.part_rs = sgk.part_rs; sg.C = sgk.C; sg.rs = sgk.rs;
   sg.M = sgk.M; sg.N = sgk.N; sg.ldc = sgk.ldc; sg.units = sgk.units; sg.base = 0;
@@ -1259,16 +1268,23 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   const int64_t nq = sg.N / 4, nel = sg.M * nq;
   const bool consume = (sg.acc & 2) != 0;
   if (sg.S <= 2) {            // few partials (a fixed-point accumulator): one unit per thread
-    for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < nel; u += (int64_t)gridDim.x * 256) {
-      const int64_t m = u / nq, n = (u % nq) * 4;
-      fold_store(sg, u, nq, fold_unit(sg, m * sg.N + n, 0, sg.S, consume));
+    for (int64_t u = (int64_t)bx * 256 + threadIdx.x; u < sg.units; u += (int64_t)nbx * 256) {
+      if (u < nel) {
+        const int64_t m = u / nq, n = (u % nq) * 4;
+        fold_store(sg, u, nq, fold_unit(sg, m * sg.N + n, 0, sg.S, consume));
+      } else {                // a weight gradient's bias: the split row sums
+        const int64_t m = u - nel;
+        float v = 0.f;
+        for (int s = 0; s < sg.S; ++s) v += sg.part_rs[(int64_t)s * sg.M + m];
+        sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v : v;
+      }
     }
     return;
   }
   __shared__ float4 red[4][64];
   const int ul = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int s_lo = (int)((int64_t)sg.S * q / 4), s_hi = (int)((int64_t)sg.S * (q + 1) / 4);
-  for (int64_t ub = (int64_t)blockIdx.x * 64; ub < sg.units; ub += (int64_t)gridDim.x * 64) {
+  for (int64_t ub = (int64_t)bx * 64; ub < sg.units; ub += (int64_t)nbx * 64) {
     const int64_t u = ub + ul;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (u < nel) {
@@ -2059,10 +2075,13 @@ FoldSeg fold_seg(const ttmi_wgrad_desc* d, const WgradPlan& p) {
 
 int launch_fold(FoldArgs& a, hipStream_t s) {
   if (a.n == 0 || a.total == 0) return TTMI_OK;
-  int64_t umax = 0;
-  for (int k = 0; k < a.n; ++k) umax = std::max(umax, a.seg[k].units);
-  const int64_t bx = std::min<int64_t>((umax + 63) / 64, 2048);
-  hipLaunchKernelGGL(wgrad_fold_kernel, dim3((unsigned)bx, (unsigned)a.n), dim3(256), 0, s, a);
+  a.blk_begin[0] = 0;
+  for (int k = 0; k < a.n; ++k) {
+    const int per = a.seg[k].S <= 2 ? 256 : 64;           // units per block pass
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((a.seg[k].units + per - 1) / per, 1024));
+    a.blk_begin[k + 1] = a.blk_begin[k] + (int)nb;
+  }
+  hipLaunchKernelGGL(wgrad_fold_kernel, dim3((unsigned)a.blk_begin[a.n]), dim3(256), 0, s, a);
   return ttmi_check_launch("ttmi_wgrad_fold");
 }
 }  // namespace

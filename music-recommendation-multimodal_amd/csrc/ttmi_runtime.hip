@@ -48,10 +48,16 @@ __global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16_t* __
 // and issues all their p / g / m / v loads before any arithmetic: 4·ADAM_U independent
 // 16-byte loads in flight per thread instead of 4.
 constexpr int ADAM_U = 2;
+// fx (optional): the gradient of the float4 range [fx_lo, fx_hi) is not in g but in an int64
+// fixed-point accumulator (2^-fx_shift; the item-embedding rows of ttmi_seq_embed_bwd): it is
+// read from there, converted, and the accumulator cleared instead of g (the fold that would
+// otherwise convert it into g is skipped: ~31 MB of traffic per cfg-2 step).
 __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     bf16_t* __restrict__ pb, const double* __restrict__ hyper,
-                                                    const int32_t* __restrict__ step, int zero_grad) {
+                                                    const int32_t* __restrict__ step, int zero_grad,
+                                                    int64_t* __restrict__ fx, int64_t fx_lo, int64_t fx_hi,
+                                                    int fx_shift) {
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n4 = n / 4;
@@ -61,7 +67,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
     const int64_t q = min(t0 + u * T, max<int64_t>(n4 - 1, 0));   // clamped: loads unconditional
     if (n4 > 0) {
       pp[u] = reinterpret_cast<const float4*>(p)[q];
-      gg[u] = reinterpret_cast<const float4*>(g)[q];
+      if (fx != nullptr && q >= fx_lo && q < fx_hi) {
+        const longlong2 a = reinterpret_cast<const longlong2*>(fx)[2 * (q - fx_lo)];
+        const longlong2 b = reinterpret_cast<const longlong2*>(fx)[2 * (q - fx_lo) + 1];
+        gg[u] = make_float4(fx_to_f(a.x, fx_shift), fx_to_f(a.y, fx_shift), fx_to_f(b.x, fx_shift),
+                            fx_to_f(b.y, fx_shift));
+      } else {
+        gg[u] = reinterpret_cast<const float4*>(g)[q];
+      }
       mm[u] = reinterpret_cast<const float4*>(m)[q];
       vv[u] = reinterpret_cast<const float4*>(v)[q];
     }
@@ -92,7 +105,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
     reinterpret_cast<float4*>(p)[q] = pp[u];
     reinterpret_cast<float4*>(m)[q] = mm[u];
     reinterpret_cast<float4*>(v)[q] = vv[u];
-    if (zero_grad) reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (fx != nullptr && q >= fx_lo && q < fx_hi) {
+      reinterpret_cast<longlong2*>(fx)[2 * (q - fx_lo)] = make_longlong2(0, 0);
+      reinterpret_cast<longlong2*>(fx)[2 * (q - fx_lo) + 1] = make_longlong2(0, 0);
+    } else if (zero_grad) {
+      reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (pb) {
       ushort4 o;
       o.x = f2bf(pp[u].x); o.y = f2bf(pp[u].y); o.z = f2bf(pp[u].z); o.w = f2bf(pp[u].w);
@@ -327,19 +345,31 @@ extern "C" int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hi
   return ttmi_check_launch("ttmi_cast_f32_bf16");
 }
 
-extern "C" int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v,
-                          uint16_t* p_bf16, const double* hyper, const int32_t* step,
-                          int zero_grad, hipStream_t s) {
+extern "C" int ttmi_adamw_fx(int64_t n, float* p, float* g, float* m, float* v,
+                             uint16_t* p_bf16, const double* hyper, const int32_t* step,
+                             int zero_grad, int64_t* fx, int64_t fx_off, int64_t fx_len,
+                             int fx_shift, hipStream_t s) {
   TTMI_REQUIRE(n >= 0 && p && g && m && v && hyper && step, "ttmi_adamw: null argument");
   TTMI_REQUIRE(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 &&
                ((uintptr_t)v & 15) == 0 && ((uintptr_t)p_bf16 & 7) == 0,
                "ttmi_adamw: buffers must be 16-B aligned (bf16 mirror 8-B)");
+  TTMI_REQUIRE(!fx || (fx_off >= 0 && fx_len >= 0 && fx_off % 4 == 0 && fx_len % 4 == 0 &&
+                       fx_off + fx_len <= n - n % 4 && ((uintptr_t)fx & 15) == 0 &&
+                       fx_shift > 0 && fx_shift < 63),
+               "ttmi_adamw_fx: the fixed-point range must be float4-aligned, inside [0, n)");
   if (n == 0) return TTMI_OK;
   const int64_t groups = std::max<int64_t>(n / 4, 1);
   const int blocks = (int)std::max<int64_t>((groups + 256 * ADAM_U - 1) / (256 * ADAM_U), 1);
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, n, p, g, m, v, (bf16_t*)p_bf16,
-                     hyper, step, zero_grad);
+                     hyper, step, zero_grad, fx, fx ? fx_off / 4 : 0, fx ? (fx_off + fx_len) / 4 : 0,
+                     fx_shift);
   return ttmi_check_launch("ttmi_adamw");
+}
+
+extern "C" int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v,
+                          uint16_t* p_bf16, const double* hyper, const int32_t* step,
+                          int zero_grad, hipStream_t s) {
+  return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, nullptr, 0, 0, 0, s);
 }
 
 extern "C" int ttmi_batch_copy(int n, void* const* dst, const void* const* src,

@@ -211,6 +211,8 @@ SIGNATURES = {
     "ttmi_infonce_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_infonce_bwd16": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),
+    "ttmi_adamw_fx": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
+                            c_p]),
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch_seeds": (c_i, [c_i, c_p, c_p, c_p, c_p, c_u64, c_p, c_p, c_i, c_i, c_p]),

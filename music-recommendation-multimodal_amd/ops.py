@@ -116,6 +116,15 @@ class WgradPending:
     def __init__(self):
         self.items = []
         self.folds = []
+        self.slots: Dict[str, int] = {}
+
+    def slot(self, key: str) -> int:
+        """Index of the next persistent zero workspace for ``key`` within this block: calls
+        whose partials wait for the same flush must not share one (the k-th call of a step
+        always gets slot k, so graph replays reuse the same buffers)."""
+        k = self.slots.get(key, 0)
+        self.slots[key] = k + 1
+        return k
 
     def flush(self) -> None:
         if not self.items and not self.folds:
@@ -126,6 +135,7 @@ class WgradPending:
         call("ttmi_wgrad_batch", len(self.items), arr, len(self.folds), farr, _s())
         self.items = []
         self.folds = []
+        self.slots = {}
 
 
 _PENDING: List[WgradPending] = []
@@ -432,10 +442,11 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, 
     deferred weight gradients inside ``deferred_wgrad`` (else right away)."""
     M, D = x.shape
     sums = dw is not None or db is not None
-    ws = _zero_ws("ttmi_layernorm_bwd_workspace", (D,), x.device) if sums else None
+    defer = bool(_PENDING) and sums
+    slot = _PENDING[-1].slot(f"ln{D}") if defer else 0
+    ws = _zero_ws("ttmi_layernorm_bwd_workspace", (D,), x.device, slot) if sums else None
     if dx16 is not None and dx16.dtype != torch.bfloat16:
         raise ValueError("layernorm_bwd: dx16 must be bf16")
-    defer = bool(_PENDING) and sums
     call("ttmi_layernorm_bwd", M, D, _p(dy), D, _p(x), D, _p(mean), _p(rstd), _p(w), _p(gate),
          code(gate.dtype) if gate is not None else 0, D, gate_scale, _p(res), _p(dx), D, _p(dw),
          _p(db), _p(ws), _p(dx16), dx16.stride(0) if dx16 is not None else 0, float(drop[0]),
@@ -467,12 +478,12 @@ def seq_embed_fwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, b: Tensor, x: Te
 _ZERO_WS: Dict[tuple, Tensor] = {}
 
 
-def _zero_ws(sizer: str, args: tuple, device) -> Tensor:
+def _zero_ws(sizer: str, args: tuple, device, slot: int = 0) -> Tensor:
     """Persistent zero workspace of the kernels whose column sums go through replicas
     (ttmi_seq_embed_bwd, ttmi_layernorm_bwd): zero on entry and left zero by every call, so
     one buffer per (device, entry point, sizes) serves every call and every graph replay on a
     stream.  Allocated on first use (the warm-up step, before any capture)."""
-    key = (str(device), sizer) + tuple(args)
+    key = (str(device), sizer, slot) + tuple(args)
     ws = _ZERO_WS.get(key)
     if ws is None:
         _L.load()
@@ -486,9 +497,11 @@ FX_GRAD_SHIFT = 36      # TTMI_FX_GRAD_SHIFT (include/ttmi.h)
 
 
 def _fx_zero(name: str, numel: int, device) -> Tensor:
-    """Persistent zero int64 fixed-point accumulator (one per (device, name, size)); the fold
-    that converts it (fx_folds) leaves it zero again, so graph replays reuse it."""
-    key = (str(device), name, int(numel))
+    """Persistent zero int64 fixed-point accumulator (one per (device, name, size) and, inside
+    ``deferred_wgrad``, per call of the block); the fold that converts it (fx_folds) leaves it
+    zero again, so graph replays reuse it."""
+    slot = _PENDING[-1].slot("fx:" + name) if _PENDING else 0
+    key = (str(device), name, int(numel), slot)
     t = _FX_ZERO.get(key)
     if t is None:
         t = _FX_ZERO[key] = torch.zeros(max(int(numel), 2), device=device, dtype=torch.int64)
@@ -532,15 +545,20 @@ def seq_embed_bwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, mean: Tensor, rs
     by folds that run with the deferred weight gradients (else right away)."""
     B, L = ids.shape
     V, D = E.shape
-    ws = _zero_ws("ttmi_seq_embed_bwd_workspace", (V, L, D), dx.device)
     defer = bool(_PENDING)
+    slot = _PENDING[-1].slot("seq_embed") if defer else 0
+    ws = _zero_ws("ttmi_seq_embed_bwd_workspace", (V, L, D), dx.device, slot)
     call("ttmi_seq_embed_bwd", B, L, D, V, _p(ids), _p(E), _p(P), _p(w), _p(mean), _p(rstd),
          float(drop[0]), _p(drop[1]), _p(dx), _p(dE), _p(dP), _p(dw), _p(db), padding_idx,
          _p(ws), int(defer), _s())
     if defer:       # the four conversions fold with the deferred weight gradients (ws left zero)
         out = (FoldDesc * 4)()
         call("ttmi_seq_embed_bwd_folds", V, L, D, _p(ws), _p(dE), _p(dP), _p(dw), _p(db), out)
-        _PENDING[-1].folds.extend((out[j], ws, dE, dP, dw, db) for j in range(4))
+        first = 0
+        if _FX_SINK and not _FX_SINK[-1]:     # dE stays fixed point: AdamW converts it
+            _FX_SINK[-1].append((ws.view(torch.int64)[:V * D], dE))
+            first = 1
+        _PENDING[-1].folds.extend((out[j], ws, dE, dP, dw, db) for j in range(first, 4))
 
 
 # ----------------------------------------------------------------------------- attention
@@ -755,10 +773,37 @@ def bump_param_epoch() -> None:
 
 
 def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
-          step: Tensor, zero_grad: bool = False):
+          step: Tensor, zero_grad: bool = False,
+          fx: Optional[Tuple[Tensor, Tensor]] = None):
+    """Fused AdamW over flat buffers.  ``fx`` = (acc, grad_view): the gradient of the slot
+    ``grad_view`` (a view into ``g``) is still in the int64 fixed-point accumulator ``acc``
+    (fx_grad_sink): read from there and ``acc`` cleared (ttmi_adamw_fx)."""
     bump_param_epoch()
-    call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
-         int(zero_grad), _s())
+    if fx is None:
+        call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
+             int(zero_grad), _s())
+        return
+    acc, view = fx
+    off = (view.data_ptr() - g.data_ptr()) // g.element_size()
+    call("ttmi_adamw_fx", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
+         int(zero_grad), _p(acc), off, view.numel(), FX_GRAD_SHIFT, _s())
+
+
+_FX_SINK: List[list] = []
+
+
+@contextlib.contextmanager
+def fx_grad_sink():
+    """Inside the block, ``seq_embed_bwd`` leaves the item-embedding gradient in its int64
+    fixed-point accumulator and appends (acc, grad) to the yielded list instead of folding it
+    into ``grad``: the caller's AdamW reads it from there (``adamw(fx=...)``).  Only for a
+    single-process step whose gradient is not all-reduced."""
+    sink: list = []
+    _FX_SINK.append(sink)
+    try:
+        yield sink
+    finally:
+        _FX_SINK.pop()
 
 
 def batch_copy(dsts, srcs):

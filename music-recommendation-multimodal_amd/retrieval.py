@@ -185,6 +185,15 @@ class CatalogueIndexer:
             if not self.use_graph:
                 self._run(b)
                 return
+            # a graph replays the storages it was captured on: when the item tower's parameters
+            # or buffers were re-homed (TrainStep's flat buffers, load_state_dict into new
+            # tensors), every captured graph is stale
+            it = self.model.item_tower
+            opkey = tuple(t.data_ptr() for t in it.parameters()) + \
+                tuple(t.data_ptr() for t in it.buffers())
+            if opkey != getattr(self, "_opkey", None):
+                self._graphs.clear()
+                self._opkey = opkey
             sig = tuple((k, tuple(t.shape), t.dtype) for k, t in sorted(b.items()))
             ent = self._graphs.get(sig)
             if ent is None:

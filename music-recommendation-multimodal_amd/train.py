@@ -15,6 +15,7 @@
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 from typing import Callable, Dict, List, Optional, Sequence
@@ -379,9 +380,10 @@ class TrainStep:
         if self.flat.mirror is not None:
             ops.cast_bf16(self.flat.data, self.flat.mirror)
 
-    def _fwd_bwd(self, b: Dict[str, Tensor], cut: Callable = _no_cut) -> None:
+    def _fwd_bwd(self, b: Dict[str, Tensor], cut: Callable = _no_cut, fx_sink: bool = False) -> None:
         """Forward + backward into the flat gradient.  ``cut(fn)`` marks a point where a
-        collective ``fn`` runs between graph segments (see _Segments)."""
+        collective ``fn`` runs between graph segments (see _Segments).  ``fx_sink``: leave the
+        item-embedding gradient in its fixed-point accumulator for the update (self._fx)."""
         # the gradient buffer is zero here: it starts zeroed and the fused AdamW clears it
         seeds = None
         draw = self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0)
@@ -420,8 +422,18 @@ class TrainStep:
         else:
             it, ist = F.item_fusion_fwd(self.Pi, self.Wi, modal, self.icfg, seeds,
                                         self.bufs, self.p_item)
-        with ops.deferred_wgrad() as pend:     # one fold launch for the step's weight grads
+        self._fx = None
+        with ops.deferred_wgrad() as pend, \
+                (ops.fx_grad_sink() if fx_sink else contextlib.nullcontext([])) as sink:
+            # one fold launch for the step's weight grads
             self._bwd(b, u, it, modal, ust, ist, rst if self.raw_items else None, cut, pend)
+        if sink:
+            acc, view = sink[0]
+            if view.data_ptr() >= self.flat.grad.data_ptr() and \
+                    view.data_ptr() + 4 * view.numel() <= self.flat.grad.data_ptr() + 4 * self.flat.numel:
+                self._fx = (acc, view)
+            else:                              # not a slot of the flat gradient: fold it now
+                ops.fx_folds([(acc, view)])
 
     def _bwd(self, b, u, it, modal, ust, ist, rst, cut, pend) -> None:
         du = torch.empty_like(u)
@@ -528,10 +540,14 @@ class TrainStep:
     def _update(self) -> None:
         f = self.flat
         ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
-                  zero_grad=True)
+                  zero_grad=True, fx=self._fx)
+        self._fx = None
 
     def _body(self, b: Dict[str, Tensor], cut: Callable = _no_cut) -> None:
-        self._fwd_bwd(b, cut)
+        # one process: the item-embedding gradient goes from its fixed-point accumulator
+        # straight into AdamW (no fold pass over the [V, D] table); with DDP it is folded
+        # into the flat gradient for the all-reduce
+        self._fwd_bwd(b, cut, fx_sink=self.world == 1)
         if self.broadcast_buffers:             # rank 0 contributes its buffers, others zeros
             ops.batch_copy([self.flat.grad_extra], [self.fbufs.data if self.is_root else self.bzero])
         if self.world > 1:

@@ -7,6 +7,7 @@ direction against the bf16-emulation yardstick (test_resnet18_vs_oracle's docstr
 running stats at 1e-2.  Parity against the reference itself is unpinned (torchvision is
 absent).  The cfg-3 model tests run the whole two-tower forward/backward and
 the graph-captured TrainStep on raw mels / covers / tabular inputs."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as TF
@@ -53,16 +54,51 @@ def rb(x):
     return _RB.apply(x)
 
 
+class _BnKernel(torch.autograd.Function):
+    """Train-mode BatchNorm2d exactly as ttmi_bn2d_fwd / ttmi_bn2d_bwd compute it: batch
+    statistics of the UNROUNDED conv output y32 (the conv epilogue's column sums), applied to
+    the bf16-stored y; backward from the (bf16) gated gradient g:
+    dy32 = bf16(w·rstd·(g − Σg/M − x̂·Σg x̂/M)) with x̂ from the bf16 y (the value the kernel
+    reads back), dw = Σg x̂, db = Σg."""
+
+    @staticmethod
+    def forward(ctx, y32, w, b):
+        mean = y32.mean((0, 2, 3), keepdim=True)
+        var = y32.var((0, 2, 3), unbiased=False, keepdim=True)
+        rstd = 1.0 / torch.sqrt(var + 1e-5)
+        xh = (y32.to(torch.bfloat16).float() - mean) * rstd
+        ctx.save_for_backward(xh, rstd, w)
+        return xh * w[None, :, None, None] + b[None, :, None, None]
+
+    @staticmethod
+    def backward(ctx, g):
+        xh, rstd, w = ctx.saved_tensors
+        M = g.numel() // g.shape[1]
+        s1 = g.sum((0, 2, 3), keepdim=True)
+        s2 = (g * xh).sum((0, 2, 3), keepdim=True)
+        dx = w[None, :, None, None] * rstd * (g - s1 / M - xh * s2 / M)
+        return dx.to(torch.bfloat16).float(), s2.flatten(), s1.flatten()
+
+
+class _GradRound(torch.autograd.Function):
+    """Identity forward; rounds the gradient to bf16 (a branch whose input grad the kernels
+    store in bf16 before it is added to another branch's: the downsample conv's DGRAD)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
 def _emu_conv_bn(p, x, wname, bn, stride, pad, residual=None, relu=True):
-    """conv (bf16 operands, fp32 accumulate, bf16 store) -> BN with fp32 batch statistics of
-    the unrounded conv output applied to the stored bf16 values -> residual -> ReLU -> bf16."""
+    """conv (bf16 operands, fp32 accumulate) -> BN as the kernels compute it (_BnKernel) ->
+    residual -> ReLU -> bf16."""
     w = p[wname]
     y32 = TF.conv2d(x, w.detach().to(torch.bfloat16).float() + (w - w.detach()), stride=stride, padding=pad)
-    mean = y32.mean((0, 2, 3), keepdim=True)
-    var = y32.var((0, 2, 3), unbiased=False, keepdim=True)
-    y = rb(y32)
-    out = (y - mean) / torch.sqrt(var + 1e-5) * p[bn + ".weight"][None, :, None, None] \
-        + p[bn + ".bias"][None, :, None, None]
+    out = _BnKernel.apply(y32, p[bn + ".weight"], p[bn + ".bias"])
     if residual is not None:
         out = out + residual
     if relu:
@@ -81,13 +117,15 @@ def resnet18_bf16_emulation(p, x, prefix="", update_running=False):
             st = s if bi == 0 else 1
             idn = y
             if b + "downsample.0.weight" in p:
-                idn = _emu_conv_bn(p, y, b + "downsample.0.weight", b + "downsample.1", st, 0,
-                                   relu=False)
+                idn = _emu_conv_bn(p, _GradRound.apply(y), b + "downsample.0.weight",
+                                   b + "downsample.1", st, 0, relu=False)
             h = _emu_conv_bn(p, y, b + "conv1.weight", b + "bn1", st, 1)
             y = _emu_conv_bn(p, h, b + "conv2.weight", b + "bn2", 1, 1, residual=rb(idn))
     feat = rb(TF.adaptive_avg_pool2d(y, 1).flatten(1))
     w = p["fc.weight"]
-    return TF.linear(feat, w.detach().to(torch.bfloat16).float() + (w - w.detach()), p["fc.bias"])
+    # the kernels take the fc's upstream gradient as a bf16 GEMM operand
+    return _GradRound.apply(TF.linear(feat, w.detach().to(torch.bfloat16).float() + (w - w.detach()),
+                                      p["fc.bias"]))
 
 
 def _cos(a, b):
@@ -178,6 +216,38 @@ def test_tabular_encoder_vs_oracle(gpu_pkg):
             assert p.grad.abs().max().item() < 3e-2 * max(1.0, Pr[name].grad.abs().max().item())
             continue
         check_grad(name, p.grad, Pr[name].grad)
+
+
+@pytest.mark.parametrize("name", ["tabular_t128.npz", "tabular_t37.npz"])
+def test_tabular_encoder_vs_reference_fixture(gpu_pkg, name):
+    """TabularEncoder (the reference's own class ran to make the fixture: item_tower.py:85-98,
+    train mode, dropout off; T = 37 exercises the zero-padded operand path) vs the fixture:
+    bf16 output within 3e-2, gradients by direction / norm, BN running stats to 1e-2 (the
+    running mean is 0.1 x the batch mean of a bf16-operand Linear's output: ~2e-3 of its
+    near-zero values)."""
+    from conftest import load_golden, sub
+    cnn = gpu_pkg.cnn
+    z = load_golden(name)
+    T, B = z["cfg"].tolist()
+    enc = cnn.TabularEncoder(T, 128).to(DEV)
+    enc.mlp[3].p = 0.0
+    enc.load_state_dict({k: torch.tensor(v) for k, v in sub(z, "p/").items()})
+    out = enc(torch.tensor(z["x"]).to(DEV))
+    (out * torch.tensor(z["upstream"]).to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel(out, torch.tensor(z["out"])) < 3e-2
+    ref_g = sub(z, "g/")
+    for name_, p in enc.named_parameters():
+        if name_ == "mlp.0.bias":       # exactly zero in math (BatchNorm follows)
+            assert p.grad.abs().max().item() < 3e-2 * max(1.0, np.abs(ref_g[name_]).max())
+            continue
+        check_grad(name_, p.grad, torch.tensor(ref_g[name_]))
+    sd = enc.state_dict()
+    for k, v in sub(z, "after/").items():
+        if "running" in k:
+            assert rel(sd[k], torch.tensor(v)) < 1e-2, k
+        if "num_batches_tracked" in k:
+            assert int(sd[k]) == int(v), k
 
 
 def test_resnet18_eval_mode_uses_running_stats(gpu_pkg):

@@ -252,7 +252,10 @@ def _trainstep_bf16_worker(rank, global_negatives, out):
             losses.append(float(loss) / WORLD)
         torch.cuda.synchronize()
         st = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-        st["__m"], st["__v"] = step.flat.exp_avg.cpu().clone(), step.flat.exp_avg_sq.cpu().clone()
+        # AdamW moments per parameter (the flat layout differs: overlap puts the late
+        # parameters last)
+        st.update({"m/" + k: v.cpu().clone() for k, v in step.flat.views(step.flat.exp_avg).items()})
+        st.update({"v/" + k: v.cpu().clone() for k, v in step.flat.views(step.flat.exp_avg_sq).items()})
         flat = step.flat.data.detach().clone()
         other = flat.clone()
         dist.broadcast(other, 0)

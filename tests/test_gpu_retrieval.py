@@ -255,6 +255,34 @@ def test_catalogue_indexer_precomputed_vs_oracle(gpu_pkg, use_graph):
         assert len(ix._graphs) == 2
 
 
+def test_catalogue_indexer_follows_rehomed_parameters(gpu_pkg):
+    """Graphs captured before a TrainStep re-homes the item tower's parameters and buffers into
+    its flat storage (and trains them) must not replay the freed old storage: the index after
+    training equals a fresh indexer's (key the graph cache on the operand
+    storages)."""
+    torch.manual_seed(1)
+    V, D = 37, 64
+    m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128,
+                              user_embedding_dim=D, item_embedding_dim=D,
+                              compute_dtype=torch.float32).to(DEV)
+    g = torch.Generator().manual_seed(8)
+    ids = torch.randperm(V - 1, generator=g)[:16] + 1
+    modal = torch.randn(16, 512, generator=g)
+    loader = [{"target_id": ids[s:s + 8], "target_modal": modal[s:s + 8]} for s in (0, 8)]
+    ix = gpu_pkg.retrieval.CatalogueIndexer(m, V)
+    before = ix.index(loader).clone()
+    from oracle import two_tower_ref as ref
+    step = gpu_pkg.TrainStep(m, lr=1e-2, use_graph=False)
+    b = ref.synthetic_batch(8, 12, V, generator=torch.Generator().manual_seed(9))
+    for _ in range(3):
+        step.step({k: v.to(DEV) for k, v in b.items()})
+    torch.cuda.synchronize()
+    after = ix.index(loader).clone()
+    fresh = gpu_pkg.retrieval.CatalogueIndexer(m, V).index(loader)
+    assert torch.equal(after, fresh)
+    assert not torch.equal(after, before)
+
+
 def test_catalogue_indexer_raw_items_vs_oracle(gpu_pkg):
     """The index over raw item inputs (ResNet-18 audio + visual, tabular, zero text slot,
     fusion head) in eval mode vs the oracle item tower in eval mode (bf16 storage: 3e-2 on the

@@ -135,3 +135,23 @@ def test_serving_fixture_vs_oracle():
     v, i = torch.topk(s, 10)
     assert i.tolist() == z["top_ids"].tolist()
     assert np.abs(v.numpy() - z["top_scores"]).max() < 6e-5
+
+
+@pytest.mark.parametrize("name", ["tabular_t128.npz", "tabular_t37.npz"])
+def test_tabular_encoder_matches_reference(name):
+    """oracle/resnet_ref.tabular_forward vs the reference's own TabularEncoder
+    (item_tower.py:85-98, train mode, dropout off): output, gradients, BN running stats."""
+    from oracle import resnet_ref as rref
+    z = load_golden(name)
+    p0 = sub(z, "p/")
+    params = {k: torch.tensor(v, requires_grad=("running" not in k and "num_batches" not in k
+                                                and v.dtype.kind == "f"))
+              for k, v in p0.items()}
+    out = rref.tabular_forward(params, torch.tensor(z["x"]), update_running=True)
+    close(out.detach(), z["out"])
+    (out * torch.tensor(z["upstream"])).sum().backward()
+    for k, g in sub(z, "g/").items():
+        close(params[k].grad, g)
+    for k, v in sub(z, "after/").items():
+        if "running" in k:
+            close(params[k], v)

@@ -56,7 +56,12 @@ def _import_reference():
     import src.models.two_tower as tt
     import src.models.user_tower as ut
     import src.train as tr
+    global REAL_TABULAR
+    REAL_TABULAR = it.TabularEncoder      # kept before _stub_item_encoders replaces it
     return ut, it, tt, tr
+
+
+REAL_TABULAR = None
 
 
 class _Identity(nn.Module):
@@ -169,6 +174,31 @@ def item_fusion_case(it, name, B, D, seed):
     _save(name, **arrays)
 
 
+def tabular_case(name, T, B, seed):
+    """The reference's own TabularEncoder (item_tower.py:85-98: Linear -> BatchNorm1d -> ReLU ->
+    Dropout -> Linear) in train mode with dropout off: output, parameter gradients under a
+    random upstream, and the BatchNorm running statistics after the step."""
+    torch.manual_seed(seed)
+    m = REAL_TABULAR(input_dim=T, embedding_dim=128)
+    m.mlp[3].p = 0.0
+    m.train()
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.randn(B, T, generator=g)
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    out = m(x)
+    G = torch.randn(out.shape, generator=g)
+    (out * G).sum().backward()
+    arrays = {"x": _np(x), "out": _np(out), "upstream": _np(G),
+              "cfg": np.array([T, B], dtype=np.int64)}
+    for k, v in sd0.items():
+        arrays["p/" + k] = _np(v)
+    for k, v in m.state_dict().items():
+        arrays["after/" + k] = _np(v)
+    for k, v in m.named_parameters():
+        arrays["g/" + k] = _np(v.grad)
+    _save(name, **arrays)
+
+
 def train_step_case(it, tt, tr, name, V, D, L, B, n_g, n_c, n_steps, seed):
     _stub_item_encoders(it)
     torch.manual_seed(seed)
@@ -233,10 +263,17 @@ def main():
                         n_c=64, lengths=[50, 17, 1, 33, 0, 49, 2, 25], seed=30)
         infonce_case(tt, "infonce_b8.npz", B=8, D=32, n_users=4, seed=40)
         infonce_case(tt, "infonce_b64.npz", B=64, D=128, n_users=24, seed=41)
+        tabular_case("tabular_t128.npz", T=128, B=16, seed=70)
+        tabular_case("tabular_t37.npz", T=37, B=16, seed=71)
         item_fusion_case(it, "item_fusion.npz", B=8, D=32, seed=50)
         train_step_case(it, tt, tr, "train_step.npz", V=101, D=32, L=8, B=8, n_g=3, n_c=5,
                         n_steps=2, seed=60)
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["tabular"]:     # only the TabularEncoder fixtures
+        _import_reference()
+        tabular_case("tabular_t128.npz", T=128, B=16, seed=70)
+        tabular_case("tabular_t37.npz", T=37, B=16, seed=71)
+    else:
+        main()

@@ -1,5 +1,5 @@
 # PMC HBM traffic of one bench config: FETCH_SIZE and WRITE_SIZE in separate passes
-# (MI355X_MICROARCH.md §HBM), then tools/traffic.py.  Usage: bash tools/_cmd_pmc2.sh TAG CONFIG
+# (MI355X_MICROARCH.md §HBM), then tools/traffic.py.  Usage: bash tools/pmc_traffic.sh TAG CONFIG
 set -o pipefail
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
