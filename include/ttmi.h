@@ -725,10 +725,13 @@ int ttmi_deb_pool_bwd(int B, int S, int H, const float* dout, const int64_t* mas
  * C[m·ldc_m + c·ldc_c] += alpha · Σ_r W[r·ldw + m] · S[r·lds + (m / group)·sgs + c] for
  * m < Mw (Mw % 8 == 0), c < 8, r < R.  W bf16; S bf16 (s_f32 = 0) or fp32 (s_f32 = 1).
  * dB = dYᵀ·t (group = Mw), dA = dLᵀ·drop(x) (ldc_m = 1), and the relative-path
- * Σ_j K_jᵀ·HU_j per head (group = 64, sgs = 8). */
+ * Σ_j K_jᵀ·HU_j per head (group = 64, sgs = 8).  acc (ABI 16): int64 scratch in C's layout
+ * (element (m, c) at m·ldc_m + c·ldc_c), zero on entry and left zero: the per-workgroup
+ * partials are summed there in fixed point (order-independent, so C is bit-reproducible),
+ * then added into C by a second launch. */
 int ttmi_skinny_wgrad(int64_t R, int Mw, const uint16_t* W, int64_t ldw, const void* S, int s_f32,
                       int64_t lds, int group, int sgs, float alpha, float* C, int64_t ldc_m,
-                      int64_t ldc_c, hipStream_t stream);
+                      int64_t ldc_c, int64_t* acc, hipStream_t stream);
 /* LoRA input gradient of query_proj + value_proj: dx[m, n] += scale · (drop_q(dL[m, 0:8]·Aq[:, n])
  * + drop_v(dL[m, 8:16]·Av[:, n])), masks regenerated from the forward's LoRA-dropout seeds at
  * index m·ld_drop + n.  dL bf16 [M, ld_dl >= 16]; Aq, Av bf16 [8, H]; dx fp32. */

@@ -226,14 +226,15 @@ __global__ __launch_bounds__(256) void deb_gelu_kernel(int64_t n8, const bf16_t*
 // (768 x 8), so this is an HBM stream of W: each thread owns 8 consecutive W columns (16-byte
 // loads, 64 fp32 accumulators) over a strided row set; RG row groups of Mw/8 threads per block
 // (768 threads at Mw 768) are added in turn into one LDS tile and every block adds its 24 KB
-// partial with contiguous atomics.  One block per CU: the per-thread row walk is the latency
-// chain, the atomics (blocks x 24 KB at ~1.3 TB/s) the other cost.  The generic tile path
+// partial with contiguous int64 fixed-point atomics (deterministic), converted into C by a
+// second tiny launch.  One block per CU: the per-thread row walk is the latency chain, the
+// atomics (blocks x 48 KB at ~1.3 TB/s) the other cost.  The generic tile path
 // spent ~260 us per call here padding the rank-8 side to 64.
 template <typename TS, int U>
 __global__ __launch_bounds__(1024) void skinny_wgrad_kernel(int64_t R, int Mw, const bf16_t* __restrict__ W,
                                                             int64_t ldw, const TS* __restrict__ S,
                                                             int64_t lds, int group, int sgs, float alpha,
-                                                            float* __restrict__ C, int64_t ldc_m,
+                                                            int64_t* __restrict__ cacc, int64_t ldc_m,
                                                             int64_t ldc_c, int64_t rows_per_block) {
   extern __shared__ float red[];                       // [Mw·8], the row groups added in turn
   const int ncol8 = Mw / 8, RG = blockDim.x / ncol8;   // blockDim.x = RG·ncol8
@@ -295,13 +296,27 @@ __global__ __launch_bounds__(1024) void skinny_wgrad_kernel(int64_t R, int Mw, c
     }
     __syncthreads();
   }
-  // contiguous in C: walk (m fastest) when ldc_m == 1, else (c fastest)
+  // contiguous in C's layout: walk (m fastest) when ldc_m == 1, else (c fastest); int64
+  // fixed-point adds (ABI 16): the blocks' partials sum to the same bits in any order
   const int n = Mw * 8;
   for (int o = t; o < n; o += blockDim.x) {
     int m, c;
     if (ldc_m == 1) { c = o / Mw; m = o % Mw; } else { m = o / 8; c = o % 8; }
-    atomicAdd(C + m * ldc_m + c * ldc_c, alpha * red[m * 8 + c]);
+    fx_add(cacc + m * ldc_m + c * ldc_c, alpha * red[m * 8 + c], TTMI_FX_GRAD);
   }
+}
+
+// C(m, c) += acc(m, c) converted; acc cleared (the skinny gradient's accumulator, C's layout).
+__global__ __launch_bounds__(256) void skinny_fx_out_kernel(int Mw, int64_t* __restrict__ acc,
+                                                            float* __restrict__ C, int64_t ldc_m,
+                                                            int64_t ldc_c) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= Mw * 8) return;
+  int m, c;
+  if (ldc_m == 1) { c = o / Mw; m = o % Mw; } else { m = o / 8; c = o % 8; }
+  const int64_t i = m * ldc_m + c * ldc_c;
+  C[i] += fx_to_f(acc[i], TTMI_FX_GRAD);
+  acc[i] = 0;
 }
 
 struct SkinnyCfg { int rg, u, blocks; };
@@ -461,9 +476,9 @@ extern "C" int ttmi_deb_pool_bwd(int B, int S, int H, const float* dout, const i
 
 extern "C" int ttmi_skinny_wgrad(int64_t R, int Mw, const uint16_t* W, int64_t ldw, const void* S,
                                  int s_f32, int64_t lds, int group, int sgs, float alpha, float* C,
-                                 int64_t ldc_m, int64_t ldc_c, hipStream_t s) {
-  TTMI_REQUIRE(R > 0 && Mw > 0 && Mw % 8 == 0 && Mw / 8 <= 256 && W && S && C,
-               "ttmi_skinny_wgrad: need Mw %% 8 == 0, Mw <= 2048");
+                                 int64_t ldc_m, int64_t ldc_c, int64_t* acc, hipStream_t s) {
+  TTMI_REQUIRE(R > 0 && Mw > 0 && Mw % 8 == 0 && Mw / 8 <= 256 && W && S && C && acc,
+               "ttmi_skinny_wgrad: need Mw %% 8 == 0, Mw <= 2048, and the accumulator");
   TTMI_REQUIRE(group > 0 && group % 8 == 0 && ldw % 8 == 0 && (uintptr_t)W % 16 == 0 &&
                (uintptr_t)S % 16 == 0 && lds % (s_f32 ? 4 : 8) == 0,
                "ttmi_skinny_wgrad: W/S need 16-byte rows, group %% 8 == 0");
@@ -478,14 +493,18 @@ extern "C" int ttmi_skinny_wgrad(int64_t R, int Mw, const uint16_t* W, int64_t l
   const dim3 grid((unsigned)blocks), blk((unsigned)(RG * ncol8));
 #define TTMI_SKINNY_LAUNCH(TS_, U_)                                                              \
   hipLaunchKernelGGL((skinny_wgrad_kernel<TS_, U_>), grid, blk, shm, s, R, Mw, (const bf16_t*)W, ldw, \
-                     (const TS_*)S, lds, group, sgs, alpha, C, ldc_m, ldc_c, rpb)
+                     (const TS_*)S, lds, group, sgs, alpha, acc, ldc_m, ldc_c, rpb)
   if (s_f32) {
     if (cfg.u == 4) TTMI_SKINNY_LAUNCH(float, 4); else TTMI_SKINNY_LAUNCH(float, 8);
   } else {
     if (cfg.u == 4) TTMI_SKINNY_LAUNCH(bf16_t, 4); else TTMI_SKINNY_LAUNCH(bf16_t, 8);
   }
 #undef TTMI_SKINNY_LAUNCH
-  return ttmi_check_launch("ttmi_skinny_wgrad");
+  const int rc = ttmi_check_launch("ttmi_skinny_wgrad");
+  if (rc) return rc;
+  hipLaunchKernelGGL(skinny_fx_out_kernel, dim3((unsigned)((Mw * 8 + 255) / 256)), dim3(256), 0, s, Mw, acc,
+                     C, ldc_m, ldc_c);
+  return ttmi_check_launch("ttmi_skinny_wgrad/out");
 }
 
 extern "C" int ttmi_lora_dx(int64_t M, int H, const uint16_t* dL, int64_t ld_dl, const uint16_t* aq,

@@ -117,6 +117,7 @@ struct DisArgs {
   float* hu;                        // [B·S, nh, 8]
   float* pbx;                       // [B·nh, nqb, nqb, 128, 8]
   float* pb;                        // [npos, 8] (summed over batch and heads)
+  int64_t* pbacc;                   // its int64 fixed-point accumulator (in the pbx workspace)
   const int32_t* order;             // [B] batch order (longest first) or null
 };
 
@@ -932,7 +933,9 @@ __global__ __launch_bounds__(256, 2) void dis_dkv_kernel(DisArgs a) {
 
 // PB[δ][c] = Σ_{b,h} Σ_pairs Σ_{r: δ(i0 - j0 - 63 + r) = δ} PBexp[b,h][pair][r][c]: each thread
 // sums one PBexp column over a chunk of (b,h) rows (coalesced 1 KB rows), then adds it to its
-// δ row (the r -> δ map depends only on the pair).  PB is zeroed by the launcher.
+// δ row (the r -> δ map depends only on the pair) with an int64 fixed-point add (several
+// chunks and several r land on one δ row: integer adds make the sum order-independent);
+// the launcher zeroes the accumulator and converts it into PB.
 constexpr int PB_ROWS = 64;
 __global__ __launch_bounds__(256) void dis_pb_kernel(DisArgs a) {
   const int np = a.nqb * a.nqb, ncol = np * WIN * 8;
@@ -943,10 +946,21 @@ __global__ __launch_bounds__(256) void dis_pb_kernel(DisArgs a) {
   for (int64_t bh = r0; bh < r1; ++bh) v += a.pbx[bh * ncol + col];
   const int p = col / (WIN * 8), r = (col / 8) % WIN, c = col % 8;
   const int rel = (p / a.nqb) * 64 - (p % a.nqb) * 64 - 63 + r;
-  if (rel > -a.S && rel < a.S) atomicAdd(a.pb + win_row(a, rel) * 8 + c, v);
+  if (rel > -a.S && rel < a.S) fx_add(a.pbacc + win_row(a, rel) * 8 + c, v, TTMI_FX_GRAD);
+}
+
+__global__ __launch_bounds__(256) void dis_pb_out_kernel(int n, const int64_t* __restrict__ acc,
+                                                         float* __restrict__ pb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) pb[i] = fx_to_f(acc[i], TTMI_FX_GRAD);
 }
 
 }  // namespace
+
+static int64_t pbx_base_floats(int B, int S, int nh) {
+  const int64_t nb = (S + 63) / 64;
+  return (int64_t)B * nh * nb * nb * WIN * 8;
+}
 
 // ---------------------------------------------------------------- C ABI
 static int dis_check(const ttmi_dis_attn_desc* d) {
@@ -977,6 +991,7 @@ static DisArgs dis_args(const ttmi_dis_attn_desc* d) {
   a.dq = (bf16_t*)d->dq; a.dk = (bf16_t*)d->dk; a.dv = (bf16_t*)d->dv; a.lddqkv = d->lddqkv;
   a.dsum = d->dq_scratch;
   a.u = d->lora_u; a.bq = d->lora_bq; a.hu = d->lora_hu; a.pb = d->lora_pb; a.pbx = d->lora_pbx;
+  a.pbacc = d->lora_pbx ? reinterpret_cast<int64_t*>(d->lora_pbx + pbx_base_floats(d->B, d->S, d->nh)) : nullptr;
   a.order = d->order;
   return a;
 }
@@ -1020,8 +1035,7 @@ extern "C" int ttmi_dis_attn_order(const int64_t* mask, int B, int S, int32_t* o
 }
 
 extern "C" int64_t ttmi_dis_attn_pbx_floats(int B, int S, int nh) {
-  const int64_t nb = (S + 63) / 64;
-  return (int64_t)B * nh * nb * nb * WIN * 8;
+  return pbx_base_floats(B, S, nh) + 2 * 512 * 8;    // + the int64 PB accumulator (npos <= 512)
 }
 
 extern "C" int ttmi_dis_attn_fwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
@@ -1052,12 +1066,14 @@ extern "C" int ttmi_dis_attn_bwd(const ttmi_dis_attn_desc* d, hipStream_t s) {
     hipLaunchKernelGGL(dis_dkv_kernel<false>, grid, dim3(256), 0, s, a);
   }
   if (d->lora_u) {
-    if (hipMemsetAsync(d->lora_pb, 0, (size_t)d->npos * 8 * sizeof(float), s) != hipSuccess)
+    if (hipMemsetAsync(a.pbacc, 0, (size_t)d->npos * 8 * sizeof(int64_t), s) != hipSuccess)
       return ttmi_check_launch("ttmi_dis_attn_bwd (pb memset)");
     const int ncol = a.nqb * a.nqb * WIN * 8;
     const int64_t rows = (int64_t)d->B * d->nh;
     hipLaunchKernelGGL(dis_pb_kernel, dim3((unsigned)((ncol + 255) / 256), (unsigned)((rows + PB_ROWS - 1) / PB_ROWS)),
                        dim3(256), 0, s, a);
+    hipLaunchKernelGGL(dis_pb_out_kernel, dim3((unsigned)((d->npos * 8 + 255) / 256)), dim3(256), 0, s,
+                       d->npos * 8, a.pbacc, d->lora_pb);
   }
   return ttmi_check_launch("ttmi_dis_attn_bwd");
 }

@@ -517,7 +517,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   {   // W -> LDS, coalesced 16-byte chunks, 8 loads in flight per thread before the LDS
       // writes (a load -> wait -> write loop pays one memory round trip per chunk: 16 round
       // trips for a 128 KB W image, which used to be most of the kernel's time)
-    constexpr int CPR = K / 8, TOT = N * CPR, PER = (TOT + 511) / 512, BATCH = 8;
+    constexpr int CPR = K / 8, TOT = N * CPR, PER = (TOT + 511) / 512, BATCH = PER <= 16 ? PER : 8;
 #pragma unroll
     for (int j0 = 0; j0 < PER; j0 += BATCH) {
       uint4 wv[BATCH];
@@ -1098,7 +1098,7 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 // atomics).  One split (short R) writes C directly.  Folds of several GEMMs share one launch.
 struct WgradPlan { int tiles_m, tiles_n, S, tile; int64_t sps; };
 
-WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax, bool allow32 = true) {
+WgradPlan wgrad_plan64(int64_t R, int64_t M, int64_t N, int64_t ldmax, bool allow32) {
   WgradPlan p;
   p.tile = 64;
   p.tiles_m = (int)((M + 63) / 64);
@@ -1155,7 +1155,7 @@ WgradGroupCfg wgrad_group_cfg() {
 
 WgradPlan wgrad_group_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
   const WgradGroupCfg c = wgrad_group_cfg();
-  if (c.tile == 64) return wgrad_plan(R, M, N, ldmax, false);
+  if (c.tile == 64) return wgrad_plan64(R, M, N, ldmax, false);
   WgradPlan p;
   p.tile = c.tile;
   p.tiles_m = (int)((M + c.tile - 1) / c.tile);
@@ -1168,6 +1168,23 @@ WgradPlan wgrad_group_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
   while (sps > 1 && sps * 64 * ldmax * 2 >= (int64_t)1 << 31) sps = (sps + 1) / 2;
   p.S = (int)((stages + sps - 1) / sps);
   p.sps = sps;
+  return p;
+}
+
+// The standalone ttmi_wgrad uses the grouped launch's split boundaries (so a deferred,
+// grouped weight gradient and an immediate one are bit-identical: the result depends on the
+// splits, not on the tile shape that computes them), executed with 64 x 64 tiles (32 x 32 for
+// a single split of a small output: 4x the workgroups).
+WgradPlan wgrad_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax, bool allow32 = true) {
+  WgradPlan p = wgrad_group_plan(R, M, N, ldmax);
+  p.tile = 64;
+  p.tiles_m = (int)((M + 63) / 64);
+  p.tiles_n = (int)((N + 63) / 64);
+  if (allow32 && p.S == 1 && p.tiles_m * p.tiles_n < 128) {
+    p.tile = 32;
+    p.tiles_m = (int)((M + 31) / 32);
+    p.tiles_n = (int)((N + 31) / 32);
+  }
   return p;
 }
 

@@ -244,7 +244,7 @@ SIGNATURES = {
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_deb_pool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_skinny_wgrad": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i, c_i64, c_i, c_i, ctypes.c_float, c_p,
-                                c_i64, c_i64, c_p]),
+                                c_i64, c_i64, c_p, c_p]),
     "ttmi_mel_power": (c_i, [c_i, c_i64, c_p, c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_mel_db_minmax": (c_i, [c_i, c_i64, ctypes.c_float, ctypes.c_float, c_p, c_p]),
     "ttmi_cover_prep": (c_i, [c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_p]),

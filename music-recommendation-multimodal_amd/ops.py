@@ -1145,8 +1145,12 @@ def skinny_wgrad(W: Tensor, S: Tensor, C: Tensor, Mw: int, *, ldc_m: int, ldc_c:
         raise TypeError("skinny_wgrad: W bf16, S bf16/fp32, C fp32")
     if W.shape[0] != S.shape[0] or W.shape[1] < Mw:
         raise ValueError("skinny_wgrad: W and S must share R rows; W needs Mw columns")
+    # int64 fixed-point scratch in C's layout (left zero by the call): one per stream, since
+    # calls on one stream are ordered (the step runs these on a side stream)
+    span = (Mw - 1) * ldc_m + 7 * ldc_c + 1
+    acc = _fx_zero(f"skinny@{_s()}", span, C.device)
     call("ttmi_skinny_wgrad", W.shape[0], Mw, _p(W), W.stride(0), _p(S), int(S.dtype == torch.float32),
-         S.stride(0), group or Mw, sgs, alpha, _p(C), ldc_m, ldc_c, _s())
+         S.stride(0), group or Mw, sgs, alpha, _p(C), ldc_m, ldc_c, _p(acc), _s())
     return C
 
 

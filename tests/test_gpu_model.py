@@ -352,8 +352,8 @@ def _grad_from_moments(step, prev_m):
     return g, m
 
 
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_cfg2_bf16_trainstep_vs_oracle_full_size(gpu_pkg, p):
+@pytest.mark.parametrize("D,p", [(128, 0.0), (128, 0.1), (256, 0.1)])
+def test_cfg2_bf16_trainstep_vs_oracle_full_size(gpu_pkg, D, p):
     """The exact benchmarked step — bf16 TrainStep (fused user / item heads, co-launched
     item head, fused InfoNCE with the in-launch combine and loss accumulator, grouped
     weight gradients, fused AdamW) at BASELINE cfg 2 (B 512, L 50, D 128, V 10,136) — against
@@ -366,10 +366,11 @@ def test_cfg2_bf16_trainstep_vs_oracle_full_size(gpu_pkg, p):
       * the 2-step parameter update by direction: cosine(Δ_gpu, Δ_fp32) at least the bf16
         emulation's cosine − 0.05, norm ratio within 2x the emulation's deviation + 0.05.
     Exactly-zero true gradients (in_proj bias's key third, the bias ahead of BatchNorm) are
-    AdamW-amplified noise in every implementation and are skipped."""
+    AdamW-amplified noise in every implementation and are skipped.  D = 256 is the reference's
+    own default width (src/train.py:289-297, two_tower.py:18,23)."""
     F = gpu_pkg.functional
     base = 11
-    m, batch = _cfg2(gpu_pkg, torch.bfloat16, p=p, seed=21)
+    m, batch = _cfg2(gpu_pkg, torch.bfloat16, D=D, p=p, seed=21)
     b2 = ref.synthetic_batch(512, 50, 10136, generator=torch.Generator().manual_seed(99))
     batches = [batch, b2]
     p0 = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
