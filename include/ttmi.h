@@ -325,6 +325,13 @@ int ttmi_sum_scaled(int n, const float* x, float scale, float* out, hipStream_t 
  *   mode 2 WGRAD: dW[co,ci,kh,kw] += Σ dy·x (out fp32, torch layout, ci < Cin); split-K
  *                 partials go to `workspace` (ttmi_conv2d_workspace(d) bytes), then are
  *                 summed in a fixed order (deterministic)
+ *   mode 3 / 4:   FWD / WGRAD of the 7x7/2/3 stem (resnet18 conv1; ABI 17) over the
+ *                 space-to-depth input of ttmi_stem_s2d: the descriptor states the stem on
+ *                 the image (H, W even; Cin image channels; C = the s2d channel count >= 4 Cin;
+ *                 KH = KW = 7, stride 2, pad 3; Co % 64 == 0), w is ttmi_stem_weight_prep's
+ *                 [Co][4][4][C] mirror, and the conv runs as the equivalent 4x4/1 conv with
+ *                 K = 16·C (128 / 256 for 1 / 3 channels instead of 49·8 = 392 padded taps).
+ *                 WGRAD writes torch's [Co][Cin][7][7] layout like mode 2.
  * w is the bf16 mirror from ttmi_conv_weight_prep: Wf = [Co][KH][KW][C] for FWD,
  * Wd = [Cin][KH][KW][Co] for DGRAD.  Every tensor must have < 2^31 elements.
  * ---------------------------------------------------------------------------------- */
@@ -352,6 +359,15 @@ int ttmi_conv_weight_prep(int Co, int Cin, int Cp, int KH, int KW, const float* 
 /* y = bf16 NHWC [N,H,W,Cp] of x fp32 NCHW [N,Cin,H,W] (channels >= Cin zero). */
 int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const float* x, uint16_t* y,
                       hipStream_t stream);
+/* Space-to-depth stem input (ABI 17): y = bf16 [N][H/2][W/2][Cp] of x fp32 NCHW [N,Cin,H,W]
+ * (H, W even), channel (ph·2 + pw)·Cin + ci = x[n][ci][2h+ph][2w+pw], channels >= 4·Cin zero
+ * (Cp % 8 == 0).  Replaces the stem's ttmi_nchw_to_nhwc for conv modes 3 / 4. */
+int ttmi_stem_s2d(int N, int Cin, int H, int W, int Cp, const float* x, uint16_t* y,
+                  hipStream_t stream);
+/* wf[co][a][b][(ph·2+pw)·Cin + ci] = bf16(w[co][ci][2a+ph−1][2b+pw−1]), zero off the 7x7
+ * window and for channels >= 4·Cin: the stem weight (torch fp32 [Co][Cin][7][7]) as the 4x4
+ * kernel over ttmi_stem_s2d's input (ABI 17). */
+int ttmi_stem_weight_prep(int Co, int Cin, int Cp, const float* w, uint16_t* wf, hipStream_t stream);
 
 /* BatchNorm2d, train mode, over NHWC bf16 [M = N·H·W, C] (C % 8 == 0, C <= 512), batch
  * statistics from the producing conv's colsum/colsumsq ([TTMI_CONV_STAT_REPS][C] int64 fixed
@@ -372,6 +388,22 @@ int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const int64_t* colsum, co
 int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate, const uint16_t* x,
                   const float* mean, const float* rstd, const float* w, int64_t* sums,
                   uint16_t* g_out, uint16_t* dx, float* dw, float* db, hipStream_t stream);
+/* resnet18 stem tail (ABI 17): bn1 (train statistics from the conv's colsum/colsumsq, or eval
+ * with colsum = colsumsq = NULL, as ttmi_bn2d_fwd) → ReLU → max-pool 3/2/1 over the conv output
+ * x [N,H,W,C] bf16 without storing the BN output: y [N,Ho,Wo,C] bf16 pooled, idx the window tap
+ * (uint8, first on ties) — bit-identical to ttmi_bn2d_fwd(relu) + ttmi_maxpool_fwd. */
+int ttmi_stem_pool_fwd(int N, int H, int W, int C, const uint16_t* x, const int64_t* colsum,
+                       const int64_t* colsumsq, const float* w, const float* b, float eps, float momentum,
+                       float* running_mean, float* running_var, int64_t* num_batches_tracked, uint16_t* y,
+                       uint8_t* idx, float* save_mean, float* save_rstd, hipStream_t stream);
+/* Its backward: the pooled gradient dy is gathered onto the conv output (as ttmi_maxpool_bwd),
+ * gated by the recomputed BN+ReLU output, and run through the BatchNorm backward (as
+ * ttmi_bn2d_bwd: sums [TTMI_CONV_STAT_REPS][2C] int64 zero on entry; dw, db accumulate):
+ * dx [N,H,W,C] bf16 = the gradient at the conv output.  b is bn1.bias (for the gate). */
+int ttmi_stem_pool_bwd(int N, int H, int W, int C, const uint16_t* dy, const uint8_t* idx,
+                       const uint16_t* x, const float* mean, const float* rstd, const float* w,
+                       const float* b, int64_t* sums, uint16_t* dx, float* dw, float* db,
+                       hipStream_t stream);
 /* Max-pool k x k / stride, -inf padding (resnet18 maxpool 3/2/1), NHWC bf16; idx (uint8 per
  * output element) = the window tap of the max, first on ties.  Backward gathers. */
 int ttmi_maxpool_fwd(int N, int H, int W, int C, int k, int stride, int pad, const uint16_t* x,

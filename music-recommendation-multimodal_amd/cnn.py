@@ -7,10 +7,13 @@ global average pool, fc), with the reference's replacements (audio conv1 takes 1
 fc → Linear(512, embedding_dim)) and torchvision's parameter names, so checkpoints map
 one-to-one.  BatchNorm2d runs in train mode on batch statistics, as in the reference.
 
-Data layout: NHWC bf16 activations (the 1/3-channel input is zero-padded to 8 channels by
-ttmi_nchw_to_nhwc); conv weights are used through bf16 mirrors (ttmi_conv_weight_prep);
+Data layout: NHWC bf16 activations; the 1/3-channel image goes to a space-to-depth layout
+(ttmi_stem_s2d: [N][H/2][W/2][8 or 16]) so the 7x7/2 stem runs as a 4x4/1 conv (K = 128 / 256
+instead of 392 padded taps); conv weights are used through bf16 mirrors (ttmi_conv_weight_prep);
 every conv's forward epilogue accumulates the BatchNorm column sums (int64 fixed point, so the
-statistics are bit-reproducible), so a conv + BN + ReLU (+ residual) is two launches.  All parameters and grads stay fp32 (torch layouts).
+statistics are bit-reproducible), so a conv + BN + ReLU (+ residual) is two launches; the stem's
+bn1 + ReLU + maxpool is one (ttmi_stem_pool_fwd, the 112x112 BN output never stored).  All
+parameters and grads stay fp32 (torch layouts).
 """
 from __future__ import annotations
 
@@ -28,7 +31,17 @@ Tensor = torch.Tensor
 
 LAYERS = (("layer1", 64, 64, 1), ("layer2", 64, 128, 2), ("layer3", 128, 256, 2),
           ("layer4", 256, 512, 2))
-STEM_CP = 8          # the 1- or 3-channel stem input is padded to 8 channels
+STEM_CP = 8          # odd-sized images: the 1- or 3-channel stem input padded to 8 channels
+STEM_S2D = True      # even-sized images: the 7x7/2 stem on the space-to-depth input
+
+
+def stem_s2d_cp(cin: int) -> int:
+    """Channels of the space-to-depth stem input (4·cin rounded up to 8: 8 / 16 for 1 / 3)."""
+    return (4 * cin + 7) // 8 * 8
+
+
+def _is_stem(sp: "ConvSpec") -> bool:
+    return sp.cin < 8 and sp.k == 7 and sp.stride == 2 and sp.pad == 3
 
 
 @dataclass(frozen=True)
@@ -66,7 +79,7 @@ class ConvAct:
     y: Tensor              # conv output, pre-BN (bf16 NHWC)
     mean: Tensor
     rstd: Tensor
-    a: Tensor              # BN output (after residual/ReLU when fused)
+    a: Optional[Tensor]    # BN output (after residual/ReLU when fused); None for the stem
 
 
 @dataclass
@@ -74,19 +87,25 @@ class ResNetSaved:
     N: int
     acts: Dict[str, ConvAct] = field(default_factory=dict)
     pool_idx: Optional[Tensor] = None
-    stem_out: Optional[Tensor] = None      # BN1+ReLU output (maxpool input)
     feat: Optional[Tensor] = None          # pooled features bf16 [N, 512]
     last: Optional[Tensor] = None          # last block output (avgpool input)
     mirrors: Optional[Dict[str, Tuple[Tensor, Optional[Tensor]]]] = None
     fc_w: Optional[Tensor] = None
 
 
-def weight_mirrors(P: Dict[str, Tensor], specs: List[ConvSpec]):
-    """bf16 GEMM mirrors (Wf for FWD, Wd for DGRAD) of every conv weight."""
+def weight_mirrors(P: Dict[str, Tensor], specs: List[ConvSpec], s2d: bool = True):
+    """bf16 GEMM mirrors (Wf for FWD, Wd for DGRAD) of every conv weight; the stem's as the
+    4x4 kernel over the space-to-depth input when ``s2d`` (ttmi_stem_weight_prep)."""
     out = {}
     for sp in specs:
         w = P[sp.name]
         dev = w.device
+        if s2d and _is_stem(sp):
+            cp = stem_s2d_cp(sp.cin)
+            wf = torch.empty(sp.cout, 4, 4, cp, device=dev, dtype=torch.bfloat16)
+            ops.stem_weight_prep(w.contiguous(), cp, wf)
+            out[sp.name] = (wf, None)
+            continue
         cp = STEM_CP if sp.cin < 8 else sp.cin
         wf = torch.empty(sp.cout, sp.k, sp.k, cp, device=dev, dtype=torch.bfloat16)
         wd = None
@@ -98,7 +117,8 @@ def weight_mirrors(P: Dict[str, Tensor], specs: List[ConvSpec]):
 
 
 def _conv_bn(P, bufs, sp: ConvSpec, x: Tensor, N: int, H: int, W: int, mirrors, stats: Tensor,
-             off: int, residual: Optional[Tensor], relu: bool, training: bool) -> ConvAct:
+             off: int, residual: Optional[Tensor], relu: bool, training: bool,
+             mode: int = ops.FWD) -> ConvAct:
     dev = x.device
     C = x.shape[-1]
     Ho, Wo = ops.conv_out_hw(H, W, sp.k, sp.stride, sp.pad)
@@ -107,7 +127,7 @@ def _conv_bn(P, bufs, sp: ConvSpec, x: Tensor, N: int, H: int, W: int, mirrors, 
     if training:
         n = ops.CONV_STAT_REPS * sp.cout
         cs, cq = stats[off:off + n], stats[off + n:off + 2 * n]
-    ops.conv2d(ops.FWD, N, H, W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad, x=x,
+    ops.conv2d(mode, N, H, W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad, x=x,
                w=mirrors[sp.name][0], out=y, colsum=cs, colsumsq=cq)
     a = torch.empty_like(y)
     mean = torch.empty(sp.cout, device=dev)
@@ -128,24 +148,40 @@ def resnet18_fwd(P: Dict[str, Tensor], x: Tensor, in_ch: int, bufs: Dict[str, Te
     dev = x.device
     N, _, H, W = x.shape
     specs = resnet18_convs(in_ch)
-    mirrors = weight_mirrors(P, specs)
+    s2d = STEM_S2D and H % 2 == 0 and W % 2 == 0   # the 7x7/2 stem as a 4x4/1 conv (ttmi_stem_s2d)
+    mirrors = weight_mirrors(P, specs, s2d)
     # BatchNorm Σy, Σy² replica rows: int64 fixed point (order-independent, include/ttmi.h)
     stats = torch.zeros(2 * ops.CONV_STAT_REPS * sum(sp.cout for sp in specs), device=dev,
                         dtype=torch.int64) if training else None
     st = ResNetSaved(N, mirrors=mirrors)
-    x0 = torch.empty(N, H, W, STEM_CP, device=dev, dtype=torch.bfloat16)
-    ops.nchw_to_nhwc(x.contiguous().float(), STEM_CP, x0)
-    off = 0
     sp = specs[0]
-    a = _conv_bn(P, bufs, sp, x0, N, H, W, mirrors, stats, off, None, True, training)
-    off += 2 * ops.CONV_STAT_REPS * sp.cout
-    st.acts[sp.name] = a
-    st.stem_out = a.a
-    Hc, Wc = a.y.shape[1], a.y.shape[2]
+    if s2d:
+        x0 = torch.empty(N, H // 2, W // 2, stem_s2d_cp(in_ch), device=dev, dtype=torch.bfloat16)
+        ops.stem_s2d(x.contiguous().float(), x0.shape[-1], x0)
+    else:
+        x0 = torch.empty(N, H, W, STEM_CP, device=dev, dtype=torch.bfloat16)
+        ops.nchw_to_nhwc(x.contiguous().float(), STEM_CP, x0)
+    # stem: conv1 (+ BN column sums) -> fused bn1 + ReLU + maxpool (ttmi_stem_pool_fwd: the
+    # full-resolution BN output is never stored; the backward re-derives its ReLU gate)
+    Hc, Wc = ops.conv_out_hw(H, W, sp.k, sp.stride, sp.pad)
+    yc = torch.empty(N, Hc, Wc, sp.cout, device=dev, dtype=torch.bfloat16)
+    cs = cq = None
+    if training:
+        n = ops.CONV_STAT_REPS * sp.cout
+        cs, cq = stats[:n], stats[n:2 * n]
+    ops.conv2d(ops.STEM_FWD if s2d else ops.FWD, N, H, W, x0.shape[-1], sp.cin, sp.cout, sp.k,
+               sp.stride, sp.pad, x=x0, w=mirrors[sp.name][0], out=yc, colsum=cs, colsumsq=cq)
+    mean = torch.empty(sp.cout, device=dev)
+    rstd = torch.empty(sp.cout, device=dev)
     Hp, Wp = ops.conv_out_hw(Hc, Wc, 3, 2, 1)
-    y = torch.empty(N, Hp, Wp, 64, device=dev, dtype=torch.bfloat16)
-    st.pool_idx = torch.empty(N, Hp, Wp, 64, device=dev, dtype=torch.uint8)
-    ops.maxpool_fwd(a.a, 3, 2, 1, y, st.pool_idx)
+    y = torch.empty(N, Hp, Wp, sp.cout, device=dev, dtype=torch.bfloat16)
+    st.pool_idx = torch.empty(N, Hp, Wp, sp.cout, device=dev, dtype=torch.uint8)
+    ops.stem_pool_fwd(yc, cs, cq, P[sp.bn + ".weight"], P[sp.bn + ".bias"], y, st.pool_idx, mean, rstd,
+                      running_mean=bufs.get(sp.bn + ".running_mean"),
+                      running_var=bufs.get(sp.bn + ".running_var"),
+                      num_batches=bufs.get(sp.bn + ".num_batches_tracked") if training else None)
+    st.acts[sp.name] = ConvAct(x0, H, W, yc, mean, rstd, None)
+    off = 2 * ops.CONV_STAT_REPS * sp.cout
     H, W = Hp, Wp
     byname = {s.name: s for s in specs}
     for lname, _, _, _ in LAYERS:
@@ -201,8 +237,9 @@ def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dic
     def conv_bwd(sp: ConvSpec, act: ConvAct, dyc: Tensor, need_dx: bool,
                  addend: Optional[Tensor] = None) -> Optional[Tensor]:
         C = act.x.shape[-1]
-        ops.conv2d(ops.WGRAD, N, act.H, act.W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad,
-                   x=act.x, dy=dyc, out=grads[sp.name])
+        s2d = _is_stem(sp) and act.x.shape[1] * 2 == act.H     # space-to-depth stem input
+        ops.conv2d(ops.STEM_WGRAD if s2d else ops.WGRAD, N, act.H, act.W, C, sp.cin, sp.cout,
+                   sp.k, sp.stride, sp.pad, x=act.x, dy=dyc, out=grads[sp.name])
         if not need_dx:
             return None
         dx = torch.empty_like(act.x)
@@ -239,9 +276,10 @@ def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dic
     # max-pool and stem (no input grad: the encoder input is data)
     stem = specs[0]
     act = st.acts[stem.name]
-    dpool = torch.empty_like(st.stem_out)
-    ops.maxpool_bwd(dy, st.pool_idx, 3, 2, 1, dpool)
-    d0 = bn_bwd(stem, act, dpool, st.stem_out)
+    s = sums[soff[0]:soff[0] + 2 * R * stem.cout]
+    d0 = torch.empty_like(act.y)
+    ops.stem_pool_bwd(dy, st.pool_idx, act.y, act.mean, act.rstd, P[stem.bn + ".weight"],
+                      P[stem.bn + ".bias"], s, d0, grads[stem.bn + ".weight"], grads[stem.bn + ".bias"])
     conv_bwd(stem, act, d0, False)
 
 

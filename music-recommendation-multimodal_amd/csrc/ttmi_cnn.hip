@@ -319,6 +319,258 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(int N, int HW, int C, 
   }
 }
 
+// ---------------------------------------------------------------- stem: BN + ReLU + max-pool
+// resnet18's conv1 → bn1 → relu → maxpool(3, 2, 1) with the BN output never stored: the
+// forward normalises each window element on the fly (a = bf16(relu(x·sa + sb)), the exact
+// value bn2d_fwd would store, so the window max and its first-on-ties tap are the unfused
+// ones) and writes only the pooled map + taps; the backward gathers the pooled gradient onto
+// each conv output (as maxpool_bwd), re-derives the ReLU gate from x, and runs the BN
+// backward's two passes on it.  Saves the 4x-larger pre-pool map's write and its re-reads.
+struct StemBn {
+  float sa[MAXC], sb[MAXC];
+};
+// sa/sb from the batch statistics (train) or the running ones (eval), as bn2d_fwd_kernel
+TTMI_DEV void stem_bn_coeffs(StemBn& s, int64_t M, int C, const int64_t* csum, const int64_t* csq,
+                             const float* w, const float* b, float eps, float momentum,
+                             float* running_mean, float* running_var, int64_t* nbt, float* save_mean,
+                             float* save_rstd) {
+  const bool eval = csum == nullptr;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    long long q1 = 0, q2 = 0;
+    if (!eval)
+      for (int r = 0; r < TTMI_CONV_STAT_REPS; ++r) {
+        q1 += csum[r * C + c];
+        q2 += csq[r * C + c];
+      }
+    const double dmu = fx_to_d(q1, TTMI_FX_STAT) / (double)M;
+    const double dvar = fx_to_d(q2, TTMI_FX_STAT) / (double)M - dmu * dmu;
+    const float mu = eval ? running_mean[c] : (float)dmu;
+    const float var = eval ? running_var[c] : (float)fmax(dvar, 0.0);
+    const float rs = 1.f / sqrtf(var + eps);
+    s.sa[c] = w[c] * rs;
+    s.sb[c] = b[c] - mu * w[c] * rs;
+    if (blockIdx.x == 0) {
+      save_mean[c] = mu;
+      save_rstd[c] = rs;
+      if (running_mean && !eval) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt && !eval) *nbt += 1;
+}
+// the stored-BN value of 8 channels (bf16-rounded, as bn2d_fwd writes it)
+TTMI_DEV void stem_act8(const StemBn& s, int c0, const uint4& q, float* a) {
+  float v[8];
+  unpack8(q, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = bf2f(f2bf(fmaxf(v[e] * s.sa[c0 + e] + s.sb[c0 + e], 0.f)));
+}
+
+__global__ __launch_bounds__(256) void stem_pool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo,
+                                                            const bf16_t* __restrict__ x,
+                                                            const int64_t* __restrict__ csum,
+                                                            const int64_t* __restrict__ csq,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ b, float eps,
+                                                            float momentum, float* running_mean,
+                                                            float* running_var, int64_t* nbt,
+                                                            bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                                                            float* save_mean, float* save_rstd) {
+  __shared__ StemBn s;
+  stem_bn_coeffs(s, (int64_t)N * H * W, C, csum, csq, w, b, eps, momentum, running_mean, running_var, nbt,
+                 save_mean, save_rstd);
+  __syncthreads();
+  const int cpr = C / 8;
+  const int n = N * Ho * Wo * cpr;                    // < 2^31 (host-checked)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int cg = i % cpr;
+    int t = i / cpr;
+    const int wo = t % Wo; t /= Wo;
+    const int ho = t % Ho;
+    const int bb = t / Ho;
+    float best[8];
+    uint8_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = ho * 2 - 1 + kh;
+      if (h < 0 || h >= H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ww = wo * 2 - 1 + kw;
+        if (ww < 0 || ww >= W) continue;
+        float v[8];
+        stem_act8(s, cg * 8, *reinterpret_cast<const uint4*>(x + (((int64_t)bb * H + h) * W + ww) * C + cg * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; arg[e] = (uint8_t)(kh * 3 + kw); }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+    a.y = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+    reinterpret_cast<uint2*>(idx)[i] = a;
+  }
+}
+
+// g (8 channels at conv-output element i) = Σ over the pool windows that chose it of dy,
+// zeroed where the recomputed BN+ReLU output is 0; xv = the conv output there.
+TTMI_DEV void stem_grad8(const StemBn& s, int64_t i, int cpr, int H, int W, int Ho, int Wo,
+                         const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                         const bf16_t* __restrict__ x, float* g, float* xv) {
+  const int cg = (int)(i % cpr);
+  int64_t t = i / cpr;
+  const int w = (int)(t % W); t /= W;
+  const int h = (int)(t % H);
+  const int bb = (int)(t / H);
+  const uint4 qx = reinterpret_cast<const uint4*>(x)[i];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = 0.f;
+  const int ho_lo = max(0, (h + 1 - 3 + 2) / 2), ho_hi = min(Ho - 1, (h + 1) / 2);
+  const int wo_lo = max(0, (w + 1 - 3 + 2) / 2), wo_hi = min(Wo - 1, (w + 1) / 2);
+  for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+    const int kh = h - (ho * 2 - 1);
+    if (kh < 0 || kh >= 3) continue;
+    for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+      const int kw = w - (wo * 2 - 1);
+      if (kw < 0 || kw >= 3) continue;
+      const int64_t o = (((int64_t)bb * Ho + ho) * Wo + wo) * cpr + cg;
+      const uint2 a = reinterpret_cast<const uint2*>(idx)[o];
+      float d[8];
+      unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
+      const uint8_t tap = (uint8_t)(kh * 3 + kw);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint8_t ae = (uint8_t)(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xFF);
+        if (ae == tap) g[e] += d[e];
+      }
+    }
+  }
+  float av[8];
+  stem_act8(s, cg * 8, qx, av);
+  unpack8(qx, xv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    g[e] = bf2f(f2bf(g[e]));                          // maxpool_bwd stores dpool in bf16
+    if (!(av[e] > 0.f)) g[e] = 0.f;
+  }
+}
+
+TTMI_DEV void stem_coeffs_bwd(StemBn& s, int C, const float* mean, const float* rstd, const float* w,
+                              const float* b) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float mu = mean[c], rs = rstd[c];
+    s.sa[c] = w[c] * rs;
+    s.sb[c] = b[c] - mu * w[c] * rs;
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(int N, int H, int W, int C, int Ho, int Wo,
+                                                                   const bf16_t* __restrict__ dy,
+                                                                   const uint8_t* __restrict__ idx,
+                                                                   const bf16_t* __restrict__ x,
+                                                                   const float* __restrict__ mean,
+                                                                   const float* __restrict__ rstd,
+                                                                   const float* __restrict__ w,
+                                                                   const float* __restrict__ b,
+                                                                   int64_t* __restrict__ sums,
+                                                                   int64_t rows_per_block) {
+  __shared__ StemBn s;
+  __shared__ float red[2][256][8];
+  stem_coeffs_bwd(s, C, mean, rstd, w, b);
+  __syncthreads();
+  const int64_t M = (int64_t)N * H * W;
+  const int cpr = C / 8;
+  const int tpr = 256 / cpr > 0 ? 256 / cpr : 1;
+  const int t = threadIdx.x;
+  const int cg = t % cpr, rl = t / cpr;
+  const int c0 = cg * 8;
+  float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mu[e] = cg < cpr ? mean[c0 + e] : 0.f; rs[e] = cg < cpr ? rstd[c0 + e] : 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (rl < tpr && cg < cpr) {
+    for (int64_t m = r0 + rl; m < r1; m += tpr) {
+      float g[8], xv[8];
+      stem_grad8(s, m * cpr + cg, cpr, H, W, Ho, Wo, dy, idx, x, g, xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += g[e];
+        s2[e] += g[e] * (xv[e] - mu[e]) * rs[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][t][e] = s1[e]; red[1][t][e] = s2[e]; }
+  __syncthreads();
+  if (t < cpr) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < tpr; ++r) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += red[0][r * cpr + t][e]; bb[e] += red[1][r * cpr + t][e]; }
+    }
+    int64_t* rep = sums + (int64_t)(blockIdx.x % TTMI_CONV_STAT_REPS) * 2 * C;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      fx_add(rep + t * 8 + e, a[e], TTMI_FX_GRAD);
+      fx_add(rep + C + t * 8 + e, bb[e], TTMI_FX_GRAD);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_pool_bwd_apply_kernel(int N, int H, int W, int C, int Ho, int Wo,
+                                                                  const bf16_t* __restrict__ dy,
+                                                                  const uint8_t* __restrict__ idx,
+                                                                  const bf16_t* __restrict__ x,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ rstd,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ b,
+                                                                  const int64_t* __restrict__ sums,
+                                                                  bf16_t* __restrict__ dx, float* dw, float* db) {
+  __shared__ StemBn s;
+  __shared__ float sk[MAXC], sm1[MAXC], sm2[MAXC], smu[MAXC], srs[MAXC];
+  const int64_t M = (int64_t)N * H * W;
+  const float invM = 1.f / (float)M;
+  stem_coeffs_bwd(s, C, mean, rstd, w, b);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    long long q1 = 0, q2 = 0;
+    for (int r = 0; r < TTMI_CONV_STAT_REPS; ++r) {
+      q1 += sums[(int64_t)r * 2 * C + c];
+      q2 += sums[(int64_t)r * 2 * C + C + c];
+    }
+    const float t1 = fx_to_f(q1, TTMI_FX_GRAD), t2 = fx_to_f(q2, TTMI_FX_GRAD);
+    sk[c] = w[c] * rstd[c];
+    sm1[c] = t1 * invM;
+    sm2[c] = t2 * invM;
+    smu[c] = mean[c];
+    srs[c] = rstd[c];
+    if (blockIdx.x == 0) {
+      if (db) db[c] += t1;
+      if (dw) dw[c] += t2;
+    }
+  }
+  __syncthreads();
+  const int cpr = C / 8;
+  const int64_t n = M * cpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpr) * 8;
+    float g[8], xv[8], o[8];
+    stem_grad8(s, i, cpr, H, W, Ho, Wo, dy, idx, x, g, xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const float xh = (xv[e] - smu[c]) * srs[c];
+      o[e] = sk[c] * (g[e] - sm1[c] - xh * sm2[c]);
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(o);
+  }
+}
+
 }  // namespace
 
 extern "C" int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const int64_t* colsum,
@@ -402,4 +654,47 @@ extern "C" int ttmi_avgpool_bwd(int N, int HW, int C, const void* dy, int dy_dty
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((int64_t)N * HW * C)), dim3(256), 0, s, N, HW, C, dy,
                      dy_dtype == TTMI_F32, (const bf16_t*)gate, (bf16_t*)dx);
   return ttmi_check_launch("ttmi_avgpool_bwd");
+}
+
+extern "C" int ttmi_stem_pool_fwd(int N, int H, int W, int C, const uint16_t* x, const int64_t* colsum,
+                                  const int64_t* colsumsq, const float* w, const float* b, float eps,
+                                  float momentum, float* running_mean, float* running_var,
+                                  int64_t* num_batches_tracked, uint16_t* y, uint8_t* idx, float* save_mean,
+                                  float* save_rstd, hipStream_t s) {
+  TTMI_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0 && C <= MAXC,
+               "ttmi_stem_pool_fwd: need 0 < C <= %d, C %% 8 == 0", MAXC);
+  TTMI_REQUIRE(x && w && b && y && idx && save_mean && save_rstd, "ttmi_stem_pool_fwd: null argument");
+  TTMI_REQUIRE(!running_mean == !running_var, "ttmi_stem_pool_fwd: running_mean/var go together");
+  TTMI_REQUIRE(!colsum == !colsumsq, "ttmi_stem_pool_fwd: colsum/colsumsq go together");
+  TTMI_REQUIRE(colsum || running_mean, "ttmi_stem_pool_fwd: eval mode (no colsum) needs running stats");
+  TTMI_REQUIRE((int64_t)N * H * W * C < (1ll << 31), "ttmi_stem_pool_fwd: tensor too large");
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(stem_pool_fwd_kernel, dim3(grid_for((int64_t)N * Ho * Wo * C / 8)), dim3(256), 0, s, N, H,
+                     W, C, Ho, Wo, (const bf16_t*)x, colsum, colsumsq, w, b, eps, momentum, running_mean,
+                     running_var, num_batches_tracked, (bf16_t*)y, idx, save_mean, save_rstd);
+  return ttmi_check_launch("ttmi_stem_pool_fwd");
+}
+
+extern "C" int ttmi_stem_pool_bwd(int N, int H, int W, int C, const uint16_t* dy, const uint8_t* idx,
+                                  const uint16_t* x, const float* mean, const float* rstd, const float* w,
+                                  const float* b, int64_t* sums, uint16_t* dx, float* dw, float* db,
+                                  hipStream_t s) {
+  TTMI_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0 && C <= MAXC,
+               "ttmi_stem_pool_bwd: need 0 < C <= %d, C %% 8 == 0", MAXC);
+  TTMI_REQUIRE(dy && idx && x && mean && rstd && w && b && sums && dx, "ttmi_stem_pool_bwd: null argument");
+  TTMI_REQUIRE((int64_t)N * H * W * C < (1ll << 31), "ttmi_stem_pool_bwd: tensor too large");
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const int64_t M = (int64_t)N * H * W;
+  const int cpr = C / 8;
+  const int tpr = std::max(1, 256 / cpr);
+  int64_t blocks = std::min<int64_t>(2048, (M + tpr * 8 - 1) / (tpr * 8));
+  blocks = std::max<int64_t>(blocks, 1);
+  const int64_t rpb = (M + blocks - 1) / blocks;
+  hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0, s, N, H, W,
+                     C, Ho, Wo, (const bf16_t*)dy, idx, (const bf16_t*)x, mean, rstd, w, b, sums, rpb);
+  int rc = ttmi_check_launch("ttmi_stem_pool_bwd/reduce");
+  if (rc) return rc;
+  hipLaunchKernelGGL(stem_pool_bwd_apply_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, s, N, H, W, C, Ho, Wo,
+                     (const bf16_t*)dy, idx, (const bf16_t*)x, mean, rstd, w, b, sums, (bf16_t*)dx, dw, db);
+  return ttmi_check_launch("ttmi_stem_pool_bwd/apply");
 }

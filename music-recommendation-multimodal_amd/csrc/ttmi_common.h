@@ -187,6 +187,37 @@ template <> struct Mma<float> {
 };
 TTMI_DEV uint4 lds16(const char* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// ---------------------------------------------------------------- LDS-DMA (buffer_load ... lds)
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+// Raw buffer descriptor over [base, base + bytes): loads past the end return zero.
+TTMI_DEV i32x4_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xFFFFu));
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+// One 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... lds): lane l's bytes land at
+// lds + 16*l.  Issued from asm so hipcc's waitcnt pass does not see an LDS write it would
+// drain with vmcnt(0) before every ds_read; callers count vmcnt themselves.
+TTMI_DEV void dma16(const i32x4_t& rs, uint32_t voff, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rs), "s"(__builtin_amdgcn_readfirstlane((int)lds))
+               : "memory");
+}
+
+TTMI_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p);
+}
+
+
 // ---------------------------------------------------------------- host-side error plumbing
 void ttmi_set_error(const char* fmt, ...);
 #define TTMI_REQUIRE(cond, ...)                      \

@@ -22,6 +22,7 @@
 #include "ttmi_common.h"
 
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 
 namespace {
@@ -379,6 +380,408 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- LDS-DMA tile (FWD / DGRAD)
+// The large layers: 256 x BN output tiles (BN = 64 or 128 channels), 8 waves as 4 (rows) x 2
+// (cols), a wave owning 64 x BN/2 outputs (4 x BN/32 MFMA tiles of 16x16x32).  Two waves per
+// SIMD: one's fragment reads and DMA issue hide under the other's MFMAs (measured: 4 waves of
+// 64 x 64 on the BN = 64 tile read less LDS but ran 1.2-1.3x longer).
+// Both operands go global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds, no register
+// staging) into a 3-deep ring of k-step images, [row][128 B] = 64 bf16 of k per row, with
+// the 16-byte chunks XOR-swizzled per row on the SOURCE side (the DMA writes lane-linearly)
+// so the 16 rows one ds_read_b128 lane group reads fall in 16 distinct bank slots.  A wave
+// instruction fills 8 rows x 128 B; a lane's rows are fixed for the whole K walk, so their
+// pixel bases are decoded once.  Padding taps, rows past M and k past K get an offset past
+// the buffer descriptor's range: the DMA writes zeros, nothing is branched around.  Two
+// k-steps are in flight while the third is multiplied (counted vmcnt, one barrier a step).
+namespace cdma {
+constexpr uint32_t OOB = 0xFFFFFFF0u;
+TTMI_DEV int swz(int r) { return (r >> 1) & 7; }
+TTMI_DEV uint4 frag(const char* img, int row, int c, int lane) {
+  return lds16(img + row * 128 + (((4 * c + (lane >> 4)) ^ swz(row)) << 4));
+}
+template <int N_>
+TTMI_DEV void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N_) : "memory");
+}
+}  // namespace cdma
+
+template <int MODE, int BM, int BN, int NS>
+__global__ __launch_bounds__(512) void conv_dma_kernel(ConvArgs a) {
+  using namespace cdma;
+  constexpr int NW = 8;                                    // waves: 4 (rows) x 2 (cols)
+  constexpr int SA = BM * 128, SB = BN * 128, STAGE = SA + SB;
+  constexpr int IA = SA / 1024 / NW, IB = SB / 1024 / NW;  // DMA wave-instructions per wave per stage
+  constexpr int P = IA + IB;
+  static_assert(IA * NW * 1024 == SA && IB * NW * 1024 == SB, "stage must split over the waves");
+  static_assert((NS - 2) * P <= 63, "vmcnt range");
+  constexpr int WM = BM / 4, WN = BN / 2, FM = WM / 16, FN = WN / 16;   // a wave owns WM x WN
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+
+  // XCD-contiguous tile order (bijective for any count): neighbouring m-tiles share input
+  // rows through their taps, the n-tiles of an m-tile share all of them
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rem = nwg & 7;
+  const int tile = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (bid >> 3);
+  const int gx = a.GN / BN;
+  const int n0 = (tile % gx) * BN, m0 = (tile / gx) * BM;
+  const int cls = MODE == 1 ? (int)blockIdx.y : 0;
+  const int GM = MODE == 1 ? a.cM[cls] : a.GM;
+  const int GK = MODE == 1 ? a.cK[cls] : a.GK;
+  if (m0 >= GM) return;                                   // DGRAD: smaller parity class
+  const int nt = (GK + 63) / 64;
+
+  const i32x4_t rsa = MODE == 0 ? make_rsrc(a.x, (uint32_t)((int64_t)a.N * a.H * a.W * a.C * 2))
+                                : make_rsrc(a.dy, (uint32_t)((int64_t)a.N * a.Ho * a.Wo * a.Co * 2));
+  const i32x4_t rsb = MODE == 0 ? make_rsrc(a.w, (uint32_t)((int64_t)a.GN * GK * 2))
+                                : make_rsrc(a.w, (uint32_t)((int64_t)a.C * a.KH * a.KW * a.Co * 2));
+
+  // ---- this lane's DMA rows: A rows (wave + NW·u) * 8 + lane / 8, its 16-byte chunk slot
+  // lane % 8 holding global chunk slot ^ swz(row)
+  int apix[IA], ah[IA], aw[IA], ach[IA];
+#pragma unroll
+  for (int u = 0; u < IA; ++u) {
+    const int r = (wave + NW * u) * 8 + (lane >> 3);
+    ach[u] = (lane & 7) ^ swz(r);
+    const int m = m0 + r;
+    ah[u] = INT_MIN / 2; aw[u] = 0; apix[u] = 0;
+    if (m < GM) {
+      if constexpr (MODE == 0) {
+        const int q = fq(m, a.fWo), wo = m - q * a.Wo;
+        const int n = fq(q, a.fHo), ho = q - n * a.Ho;
+        ah[u] = ho * a.S - a.P;
+        aw[u] = wo * a.S - a.P;
+        apix[u] = n * a.H * a.W;
+      } else {
+        const int q = fq(m, a.cfW[cls]), ww = m - q * a.cWc[cls];
+        const int n = fq(q, a.cfH[cls]), hh = q - n * a.cHc[cls];
+        ah[u] = hh + a.coffh[cls];
+        aw[u] = ww + a.coffw[cls];
+        apix[u] = n * a.Ho * a.Wo;
+      }
+    }
+  }
+  int bch[IB];
+  uint32_t brow[IB];
+#pragma unroll
+  for (int v = 0; v < IB; ++v) {
+    const int r = (wave + NW * v) * 8 + (lane >> 3);
+    bch[v] = (lane & 7) ^ swz(r);
+    brow[v] = MODE == 0 ? (uint32_t)(n0 + r) * (uint32_t)GK * 2u
+                        : (uint32_t)(n0 + r) * (uint32_t)(a.KH * a.KW * a.Co) * 2u;
+  }
+  const uint32_t sl = lds_addr(smem);
+
+  auto issue = [&](int t, int slot) {
+    const uint32_t img = sl + slot * STAGE;
+    const int k0 = t * 64;
+    if constexpr (MODE == 0) {
+      const bool uni = a.C % 64 == 0;                      // the whole k-step is one tap
+      const int tap0 = fq(k0, a.fC), ci0 = k0 - tap0 * a.C;
+      const int kh0 = fq(tap0, a.fKW), kw0 = tap0 - kh0 * a.KW;
+#pragma unroll
+      for (int u = 0; u < IA; ++u) {
+        const int k = k0 + ach[u] * 8;
+        int kh = kh0, kw = kw0, ci = ci0 + ach[u] * 8;
+        if (!uni) {
+          const int tap = fq(k, a.fC);
+          ci = k - tap * a.C;
+          kh = fq(tap, a.fKW);
+          kw = tap - kh * a.KW;
+        }
+        const int hi = ah[u] + kh, wi = aw[u] + kw;
+        const bool ok = k < GK && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const uint32_t off = ((uint32_t)(apix[u] + hi * a.W + wi) * (uint32_t)a.C + (uint32_t)ci) * 2u;
+        dma16(rsa, ok ? off : OOB, img + (wave + NW * u) * 1024);
+      }
+#pragma unroll
+      for (int v = 0; v < IB; ++v) {
+        const int k = k0 + bch[v] * 8;
+        dma16(rsb, k < GK ? brow[v] + (uint32_t)k * 2u : OOB, img + SA + (wave + NW * v) * 1024);
+      }
+    } else {
+      // k = (i, j, co) on this class's tap lattice; Co % 64 == 0: one tap per k-step
+      const int tt = fq(k0, a.fCo), co0 = k0 - tt * a.Co;
+      const int i = fq(tt, a.cfnkw[cls]), j = tt - i * a.cnkw[cls];
+#pragma unroll
+      for (int u = 0; u < IA; ++u) {
+        const int ho = ah[u] - i, wo = aw[u] - j;
+        const bool ok = (unsigned)ho < (unsigned)a.Ho && (unsigned)wo < (unsigned)a.Wo;
+        const uint32_t off =
+            ((uint32_t)(apix[u] + ho * a.Wo + wo) * (uint32_t)a.Co + (uint32_t)(co0 + ach[u] * 8)) * 2u;
+        dma16(rsa, ok ? off : OOB, img + (wave + NW * u) * 1024);
+      }
+      const int kh = a.ckh0[cls] + a.S * i, kw = a.ckw0[cls] + a.S * j;
+      const uint32_t wcol = (uint32_t)((kh * a.KW + kw) * a.Co + co0) * 2u;
+#pragma unroll
+      for (int v = 0; v < IB; ++v) dma16(rsb, brow[v] + wcol + bch[v] * 16u, img + SA + (wave + NW * v) * 1024);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nt) issue(s, s);
+  const int ar = wm * WM + (lane & 15), br = wn * WN + (lane & 15);
+  for (int t = 0; t < nt; ++t) {
+    // step t landed for every wave (later steps may fly); slot (t-1) % NS is free
+    if (t + NS - 2 < nt) wait_vm_barrier<(NS - 2) * P>();
+    else if (t + 1 < nt) wait_vm_barrier<P>();
+    else wait_vm_barrier<0>();
+    if (t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
+    const char* sA = smem + (t % NS) * STAGE;
+    const char* sB = sA + SA;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = frag(sA, ar + 16 * i, c, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = frag(sB, br + 16 * j, c, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) Mma<bf16_t>::run(acc[i][j], bfr[j], af[i]);
+    }
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3], m = row + (lane & 15), n = col + 4*(lane >> 4)
+  const int li = lane & 15, lg = lane >> 4;
+  int64_t orow[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * WM + i * 16 + li;
+    orow[i] = -1;
+    if (m < GM) {
+      if constexpr (MODE == 1) {
+        const int q = fq(m, a.cfW[cls]), ww = m - q * a.cWc[cls];
+        const int n = fq(q, a.cfH[cls]), hh = q - n * a.cHc[cls];
+        const int ph = cls / a.S, pw = cls - ph * a.S;
+        orow[i] = ((int64_t)n * a.H + hh * a.S + ph) * a.W + ww * a.S + pw;
+      } else {
+        orow[i] = m;
+      }
+    }
+  }
+  float cs[FN][4], cq[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + 4 * lg;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[j][e] = cq[j][e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (orow[i] < 0) continue;
+      const float* v = reinterpret_cast<const float*>(&acc[i][j]);
+      float o[4] = {v[0], v[1], v[2], v[3]};
+      bf16_t* dst = static_cast<bf16_t*>(a.out) + orow[i] * a.GN + n;
+      if (MODE == 1 && a.addend) {
+        const ushort4 q = *reinterpret_cast<const ushort4*>(a.addend + orow[i] * a.GN + n);
+        o[0] += bf2f(q.x); o[1] += bf2f(q.y); o[2] += bf2f(q.z); o[3] += bf2f(q.w);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { cs[j][e] += o[e]; cq[j][e] += o[e] * o[e]; }
+      ushort4 q;
+      q.x = f2bf(o[0]); q.y = f2bf(o[1]); q.z = f2bf(o[2]); q.w = f2bf(o[3]);
+      *reinterpret_cast<ushort4*>(dst) = q;
+    }
+  }
+  if (MODE == 0 && a.colsum) {
+    // BatchNorm column statistics (as conv_tile_kernel): rows reduced in registers, over the
+    // 16 row lanes, then over the four row-waves through LDS in a fixed order; one int64
+    // fixed-point add per column per workgroup into replica row blockIdx.x % REPS.
+    float* red = reinterpret_cast<float*>(smem);          // [4][2][BN]
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          cs[j][e] += __shfl_xor(cs[j][e], off, 64);
+          cq[j][e] += __shfl_xor(cq[j][e], off, 64);
+        }
+    __syncthreads();                                      // every wave is past the ring
+    if (li == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = wn * WN + j * 16 + 4 * lg + e;
+          red[(wm * 2) * BN + col] = cs[j][e];
+          red[(wm * 2 + 1) * BN + col] = cq[j][e];
+        }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) { s += red[(w * 2) * BN + tid]; s2 += red[(w * 2 + 1) * BN + tid]; }
+      const int rep = blockIdx.x % TTMI_CONV_STAT_REPS;
+      fx_add(a.colsum + (int64_t)rep * a.GN + n0 + tid, s, TTMI_FX_STAT);
+      fx_add(a.colsumsq + (int64_t)rep * a.GN + n0 + tid, s2, TTMI_FX_STAT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- LDS-DMA tile (WGRAD)
+// dW[co, kc] over one split's pixel range: BM x 128 tiles (BM = 64 or 128 output channels),
+// 4 waves 2 x 2, K = pixels walked in 64-pixel stages through a 4-deep LDS-DMA ring.  Both
+// operands are pixel-major: the A image holds dy[p][co0 .. co0+BM), the B image the im2col
+// row x[pix(p, tap)][ci ..] of each 16-byte column chunk — a lane's column chunk (so its tap
+// and channel) is fixed for the whole walk, only the pixel of its k-row moves.  Images are
+// [k][W·2 B] with 32-byte chunks XOR-swizzled per k-row on the source side and read as MFMA
+// fragments by ds_read_b64_tr_b16 (the k-major transpose in the LDS read).  Partials go to
+// the split's slab as 16-byte stores (deterministic; reduced by wgrad_reduce_kernel).
+namespace cdma {
+template <int W>
+struct KImg {                                              // [64 k-rows][W bf16] image
+  static constexpr int PB = W * 2;
+  static constexpr int CPR = PB / 32;                      // 32-byte chunks per k-row
+  static constexpr int RPB = PB >= 256 ? 1 : 256 / PB;     // k-rows per 256-byte bank row
+  static constexpr int BYTES = 64 * PB;
+  static constexpr int INSTR = BYTES / 1024;
+  static TTMI_DEV int swz(int k) { return (k / RPB) % CPR; }
+  // k-row and source byte (within the row's W-column window) of this lane's bytes in
+  // wave-instruction ii
+  static TTMI_DEV void slot(int ii, int lane, int& k, int& col_b) {
+    const int o = ii * 1024 + lane * 16;
+    k = o / PB;
+    const int pb = o % PB;
+    col_b = (((pb >> 5) ^ swz(k)) << 5) + (pb & 16);
+  }
+  static TTMI_DEV uint4 frag(const char* img, int row0, int c, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    const int k = c * 32 + 4 * g + (i >> 2);
+    const char* p = img + k * PB + (((row0 >> 4) ^ swz(k)) << 5) + 8 * (i & 3);
+    const uint2 lo = c_lds_tr8(p), hi = c_lds_tr8(p + 16 * PB);
+    return make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+};
+}  // namespace cdma
+
+template <int BM, int NW, int NS>
+__global__ __launch_bounds__(NW * 64) void conv_wgrad_dma_kernel(ConvArgs a, int tiles_n, int tiles) {
+  using namespace cdma;
+  constexpr int BN = 128;
+  using IA = KImg<BM>;
+  using IB = KImg<BN>;
+  constexpr int STAGE = IA::BYTES + IB::BYTES;
+  constexpr int JA = IA::INSTR / NW, JB = IB::INSTR / NW;  // per wave per stage
+  constexpr int P = JA + JB;
+  static_assert(JA * NW == IA::INSTR && JB * NW == IB::INSTR, "stage must split over the waves");
+  static_assert((NS - 2) * P <= 63, "vmcnt range");
+  constexpr int WCOL = NW / 2;                             // waves: 2 (rows) x NW/2 (cols)
+  constexpr int WTM = BM / 2, WTN = BN / WCOL, TM = WTM / 16, TN = WTN / 16;
+  __shared__ __attribute__((aligned(1024))) char ring[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WCOL, wn = wave % WCOL;
+
+  // (split, tile) in XCD-contiguous order: the tiles of one split (same pixel rows) share an
+  // XCD's L2
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rem = nwg & 7;
+  const int L = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (bid >> 3);
+  const int tile = L % tiles, split = L / tiles;
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int kbeg = split * a.k_split;
+  const int kend = min(a.GK, kbeg + a.k_split);
+  if (kbeg >= kend) return;
+  const int nst = (kend - kbeg + 63) >> 6;
+
+  const i32x4_t rsa = make_rsrc(a.dy, (uint32_t)((int64_t)a.GK * a.Co * 2));
+  const i32x4_t rsx = make_rsrc(a.x, (uint32_t)((int64_t)a.N * a.H * a.W * a.C * 2));
+  // this lane's fixed A column byte and B column chunk (tap, channel) per wave-instruction
+  int ak[JA], acol[JA], bk[JB], bkh[JB], bkw[JB], bci[JB];
+  bool bok[JB];
+#pragma unroll
+  for (int j = 0; j < JA; ++j) {
+    IA::slot(wave + NW * j, lane, ak[j], acol[j]);
+    acol[j] += m0 * 2;
+  }
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    int cb;
+    IB::slot(wave + NW * j, lane, bk[j], cb);
+    const int kc = n0 + cb / 2;
+    bok[j] = kc < a.GN;
+    const int tap = fq(kc, a.fC);
+    bci[j] = kc - tap * a.C;
+    bkh[j] = fq(tap, a.fKW);
+    bkw[j] = tap - bkh[j] * a.KW;
+    bkh[j] -= a.P;
+    bkw[j] -= a.P;
+  }
+  const uint32_t sl = lds_addr(ring);
+  auto issue = [&](int t, int slot) {
+    const uint32_t img = sl + slot * STAGE;
+    const int p0 = kbeg + t * 64;
+#pragma unroll
+    for (int j = 0; j < JA; ++j) {
+      const int p = p0 + ak[j];
+      const uint32_t off = (uint32_t)p * (uint32_t)(a.Co * 2) + (uint32_t)acol[j];
+      dma16(rsa, p < kend ? off : OOB, img + (wave + NW * j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int p = p0 + bk[j];
+      const int q = fq(p, a.fWo), wo = p - q * a.Wo;
+      const int n = fq(q, a.fHo), ho = q - n * a.Ho;
+      const int hi = ho * a.S + bkh[j], wi = wo * a.S + bkw[j];
+      const bool ok = p < kend && bok[j] && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      const uint32_t off = ((uint32_t)((n * a.H + hi) * a.W + wi) * (uint32_t)a.C + (uint32_t)bci[j]) * 2u;
+      dma16(rsx, ok ? off : OOB, img + IA::BYTES + (wave + NW * j) * 1024);
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nst) issue(s, s);
+  for (int t = 0; t < nst; ++t) {
+    // stage t landed for every wave (later stages may fly); slot (t-1) % NS is free
+    if (t + NS - 2 < nst) wait_vm_barrier<(NS - 2) * P>();
+    else if (t + 1 < nst) wait_vm_barrier<P>();
+    else wait_vm_barrier<0>();
+    if (t + NS - 1 < nst) issue(t + NS - 1, (t + NS - 1) % NS);
+    const char* sA = ring + (t % NS) * STAGE;
+    const char* sB = sA + IA::BYTES;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = IA::frag(sA, wm * WTM + i * 16, c, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = IB::frag(sB, wn * WTN + j * 16, c, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Mma<bf16_t>::run(acc[i][j], bfr[j], af[i]);
+    }
+  }
+  const int li = lane & 15, lg = lane >> 4;
+  float* ws = a.ws + (int64_t)split * a.GM * a.GN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WTM + i * 16 + li;
+    if (m >= a.GM) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WTN + j * 16 + 4 * lg;
+      if (n < a.GN) *reinterpret_cast<f32x4_t*>(ws + (int64_t)m * a.GN + n) = acc[i][j];
+    }
+  }
+}
+
 // dW (torch [Co][Cin][KH][KW]) += Σ_split ws[split][co][(kh·KW + kw)·C + ci], ci < Cin, in
 // split order (deterministic).  Up to WR_SPLITS splits: one pass (x over 4-column groups of
 // the [GM][GN] plane; a thread's WR_SPLITS loads in flight together).  More: a first pass
@@ -388,7 +791,7 @@ constexpr int WR_SPLITS = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(float* __restrict__ ws, int splits,
                                                            int step, int GM, int GN, int C, int Cin,
                                                            int KW, int KHKW, int final_pass,
-                                                           float* __restrict__ dw) {
+                                                           float* __restrict__ dw, int s2d) {
   const int64_t n4 = (int64_t)GM * GN / 4, plane = (int64_t)GM * GN;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
@@ -413,6 +816,19 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(float* __restrict__ w
   const int co = (int)(e0 / GN), kc = (int)(e0 % GN);
   const int tap = kc / C, ci0 = kc % C;
   const float* v = reinterpret_cast<const float*>(&s);
+  if (s2d) {
+    // space-to-depth stem (ttmi_stem_s2d): tap (a, b) of the 4x4 kernel, channel
+    // (ph·2 + pw)·Cin + ci  ->  torch tap (kh, kw) = (2a + ph − 1, 2b + pw − 1) of the 7x7
+    const int ta = tap >> 2, tb = tap & 3;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = (ci0 + e) / Cin, ci = (ci0 + e) - q * Cin;
+      const int kh = 2 * ta + (q >> 1) - 1, kw = 2 * tb + (q & 1) - 1;
+      if (q >= 4 || kh < 0 || kh >= 7 || kw < 0 || kw >= 7) continue;
+      dw[(((int64_t)co * Cin + ci) * 7 + kh) * 7 + kw] += v[e];
+    }
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int ci = ci0 + e;
@@ -460,6 +876,46 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(int N, int Cin, int H
   }
 }
 
+// 7x7/2 stem as a 4x4/1 conv on a space-to-depth input (ttmi_stem_s2d): x' [N][H/2][W/2][Cp],
+// channel (ph·2 + pw)·Cin + ci = x[n][ci][2h'+ph][2w'+pw] (zero for channels >= 4·Cin), and
+// W'[co][a][b][(ph, pw, ci)] = W[co][ci][2a+ph−1][2b+pw−1] (zero off the 7x7 window): with
+// pad 2 top/left, y[ho][wo] = Σ_{a,b} x'[ho−2+a][wo−2+b] · W'[a][b] is exactly the 7x7/2/3
+// conv, at K = 16·Cp (128 / 256 for 1 / 3 channels) instead of 49·8 = 392 padded taps.
+__global__ __launch_bounds__(256) void stem_s2d_kernel(int N, int Cin, int H, int W, int Cp,
+                                                       const float* __restrict__ x,
+                                                       bf16_t* __restrict__ y) {
+  const int Hh = H / 2, Wh = W / 2;
+  const int64_t HW = (int64_t)H * W, npix = (int64_t)N * Hh * Wh;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = p / ((int64_t)Hh * Wh);
+    const int r = (int)(p - b * Hh * Wh), h = r / Wh, w = r - h * Wh;
+    const float* src = x + b * Cin * HW + (int64_t)(2 * h) * W + 2 * w;
+    uint4* dst = reinterpret_cast<uint4*>(y + p * Cp);
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int q = (c0 + e) / Cin, ci = (c0 + e) - q * Cin;
+        v[e] = q < 4 ? src[(int64_t)ci * HW + (q >> 1) * W + (q & 1)] : 0.f;
+      }
+      dst[c0 / 8] = pack8(v);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void stem_weight_prep_kernel(int Co, int Cin, int Cp,
+                                                               const float* __restrict__ w,
+                                                               bf16_t* __restrict__ wf) {
+  const int64_t n = (int64_t)Co * 16 * Cp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const int tap = (int)((i / Cp) % 16), co = (int)(i / (16 * Cp));
+    const int q = c / Cin, ci = c - q * Cin;
+    const int kh = 2 * (tap >> 2) + (q >> 1) - 1, kw = 2 * (tap & 3) + (q & 1) - 1;
+    const bool ok = q < 4 && kh >= 0 && kh < 7 && kw >= 0 && kw < 7;
+    wf[i] = f2bf(ok ? w[(((int64_t)co * Cin + ci) * 7 + kh) * 7 + kw] : 0.f);
+  }
+}
+
 int grid1(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 8192); }
 
 }  // namespace
@@ -484,6 +940,25 @@ extern "C" int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const flo
   return ttmi_check_launch("ttmi_nchw_to_nhwc");
 }
 
+extern "C" int ttmi_stem_s2d(int N, int Cin, int H, int W, int Cp, const float* x, uint16_t* y,
+                             hipStream_t s) {
+  TTMI_REQUIRE(N >= 0 && Cin > 0 && H > 0 && W > 0 && H % 2 == 0 && W % 2 == 0 && Cp >= 4 * Cin &&
+                   Cp % 8 == 0, "ttmi_stem_s2d: bad shape (H, W even, Cp >= 4 Cin, Cp % 8 == 0)");
+  TTMI_REQUIRE(x && y, "ttmi_stem_s2d: null argument");
+  if (N == 0) return TTMI_OK;
+  hipLaunchKernelGGL(stem_s2d_kernel, dim3(grid1((int64_t)N * (H / 2) * (W / 2))), dim3(256), 0, s, N, Cin,
+                     H, W, Cp, x, reinterpret_cast<bf16_t*>(y));
+  return ttmi_check_launch("ttmi_stem_s2d");
+}
+
+extern "C" int ttmi_stem_weight_prep(int Co, int Cin, int Cp, const float* w, uint16_t* wf, hipStream_t s) {
+  TTMI_REQUIRE(Co > 0 && Cin > 0 && Cp >= 4 * Cin && Cp % 8 == 0, "ttmi_stem_weight_prep: bad shape");
+  TTMI_REQUIRE(w && wf, "ttmi_stem_weight_prep: null argument");
+  hipLaunchKernelGGL(stem_weight_prep_kernel, dim3(grid1((int64_t)Co * 16 * Cp)), dim3(256), 0, s, Co, Cin, Cp,
+                     w, reinterpret_cast<bf16_t*>(wf));
+  return ttmi_check_launch("ttmi_stem_weight_prep");
+}
+
 namespace {
 
 // TTMI_CONV_BM=64|128 forces the FWD/DGRAD tile height (tests cover both tile shapes).
@@ -494,15 +969,84 @@ int forced_bm() {
   return v == 64 || v == 128 ? v : 0;
 }
 
+// TTMI_CONV_DMA=0|1 forces the FWD/DGRAD kernel family; by default the LDS-DMA tile runs
+// whenever its 256-row tiles still give every CU a workgroup (N % 64 == 0 channels).
+// TTMI_CONV_FT=<rows>:<stages> picks the FWD/DGRAD LDS-DMA tile (default 256:3; the grid
+// must then be recomputed, so the host plans with the same value).
+struct FtCfg {
+  int bm, ns;
+};
+FtCfg ft_cfg() {
+  FtCfg f{256, 3};
+  const char* e = getenv("TTMI_CONV_FT");
+  int a = 0, b = 0;
+  if (e && sscanf(e, "%d:%d", &a, &b) == 2 && (a == 128 || a == 256) && b >= 2 && b <= 4) f = FtCfg{a, b};
+  return f;
+}
+// TTMI_CONV_WG=<waves>:<stages> picks the WGRAD LDS-DMA variant (default 8:2: two 64 KB
+// workgroups per CU beat deeper rings, measured over every cfg-3 layer).
+struct WgCfg {
+  int nw, ns;
+};
+WgCfg wg_cfg() {
+  WgCfg w{8, 2};
+  const char* e = getenv("TTMI_CONV_WG");
+  int a = 0, b = 0;
+  if (e && sscanf(e, "%d:%d", &a, &b) == 2) w = WgCfg{a, b};
+  return w;
+}
+int forced_dma() {
+  const char* e = getenv("TTMI_CONV_DMA");
+  return e ? (atoi(e) ? 1 : 0) : -1;
+}
+bool use_dma(int64_t tiles, int n) {
+  if (n % 64 != 0) return false;
+  const int f = forced_dma();
+  return f >= 0 ? f == 1 : tiles >= 256;
+}
+
 struct ConvPlan {
   ConvArgs a;
   int bm, bn, splits;
+  bool dma;                 // on the LDS-DMA kernels (conv_dma_kernel / conv_wgrad_dma_kernel)
+  int s2d;                  // space-to-depth stem (modes 3 / 4)
   int64_t ws_bytes;
 };
 
 int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
   TTMI_REQUIRE(d != nullptr, "ttmi_conv2d: null descriptor");
-  TTMI_REQUIRE(d->mode >= 0 && d->mode <= 2, "ttmi_conv2d: bad mode");
+  TTMI_REQUIRE(d->mode >= 0 && d->mode <= 4, "ttmi_conv2d: bad mode");
+  if (d->mode >= 3) {
+    // space-to-depth stem: the descriptor states the 7x7/2/3 conv on the image; run the
+    // equivalent 4x4/1 conv (pad 2 top/left) over ttmi_stem_s2d's [N][H/2][W/2][C] input
+    TTMI_REQUIRE(d->KH == 7 && d->KW == 7 && d->stride == 2 && d->pad == 3 && d->H % 2 == 0 &&
+                     d->W % 2 == 0 && d->C >= 4 * d->Cin && d->C % 8 == 0 && d->Co % 64 == 0,
+                 "ttmi_conv2d: stem modes need a 7x7/2/3 conv, even H, W, C >= 4 Cin, Co %% 64 == 0");
+    ttmi_conv_desc e = *d;
+    e.mode = d->mode == 3 ? 0 : 2;
+    e.H = d->H / 2; e.W = d->W / 2; e.KH = e.KW = 4; e.stride = 1; e.pad = 2; e.Cin = d->C;
+    const int rc = conv_plan(&e, pl);
+    if (rc) return rc;
+    ConvArgs& a = pl->a;                                  // output grid of the 7x7/2 conv
+    a.Ho = d->H / 2; a.Wo = d->W / 2;
+    a.fWo = fdiv_make(a.Wo); a.fHo = fdiv_make(a.Ho);
+    a.Cin = d->Cin;
+    if (e.mode == 0) {
+      a.GM = d->N * a.Ho * a.Wo;
+      pl->dma = use_dma(((int64_t)a.GM + 255) / 256 * (a.GN / pl->bn), d->Co);
+    } else {
+      a.GK = d->N * a.Ho * a.Wo;
+      const int64_t tiles = ((a.GM + pl->bm - 1) / pl->bm) * ((a.GN + 127) / 128);
+      const int64_t ksteps = ((int64_t)a.GK + 63) / 64;
+      const int64_t want = std::max<int64_t>(1, (1024 + tiles - 1) / tiles);
+      const int64_t per = std::max<int64_t>(std::min<int64_t>(8, ksteps), (ksteps + want - 1) / want);
+      a.k_split = (int)(per * 64);
+      pl->splits = (int)((ksteps + per - 1) / per);
+      pl->ws_bytes = (int64_t)pl->splits * a.GM * a.GN * 4;
+    }
+    pl->s2d = 1;
+    return TTMI_OK;
+  }
   TTMI_REQUIRE(d->N >= 0 && d->H > 0 && d->W > 0 && d->C > 0 && d->C % 8 == 0 && d->Co > 0 &&
                    d->Co % 8 == 0 && d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0,
                "ttmi_conv2d: bad geometry (C, Co must be multiples of 8)");
@@ -528,12 +1072,15 @@ int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
   a.fWo = fdiv_make(Wo); a.fHo = fdiv_make(Ho); a.fCo = fdiv_make(d->Co);
   pl->splits = 1;
   pl->ws_bytes = 0;
+  pl->dma = false;
+  pl->s2d = 0;
   if (d->mode == 0) {
     a.GM = (int)Mo; a.GN = d->Co; a.GK = d->KH * d->KW * d->C;
     pl->bn = d->Co % 128 == 0 ? 128 : 64;
     pl->bm = 128;
     if (((a.GM + 127) / 128) * (a.GN / pl->bn) < 512) pl->bm = 64;
     if (forced_bm()) pl->bm = forced_bm();
+    pl->dma = use_dma(((int64_t)a.GM + 255) / 256 * (a.GN / pl->bn), d->Co);
   } else if (d->mode == 1) {
     TTMI_REQUIRE(d->Cin == d->C, "ttmi_conv2d: DGRAD needs unpadded channels (Cin == C)");
     TTMI_REQUIRE(d->Co % 64 == 0, "ttmi_conv2d: DGRAD needs Co %% 64 == 0");
@@ -559,6 +1106,9 @@ int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
     pl->bm = 128;
     if (((a.GM + 127) / 128) * (a.GN / pl->bn) * S * S < 512) pl->bm = 64;
     if (forced_bm()) pl->bm = forced_bm();
+    int64_t dt = 0;
+    for (int c = 0; c < S * S; ++c) dt += ((int64_t)a.cM[c] + 255) / 256 * (a.GN / pl->bn);
+    pl->dma = use_dma(dt, d->C) && (d->KH * d->KW > 1 || forced_dma() == 1);   // 1x1/2: reg tile
   } else {
     a.GM = d->Co; a.GN = d->KH * d->KW * d->C; a.GK = (int)Mo;
     pl->bm = d->Co % 128 == 0 ? 128 : 64;
@@ -570,6 +1120,7 @@ int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
     a.k_split = (int)(per * 64);
     pl->splits = (int)((ksteps + per - 1) / per);
     TTMI_REQUIRE(pl->splits <= 65535, "ttmi_conv2d: too many splits");
+    pl->dma = d->Co % 64 == 0 && forced_dma() != 0;
     pl->ws_bytes = (int64_t)pl->splits * a.GM * a.GN * 4;
   }
   return TTMI_OK;
@@ -578,6 +1129,39 @@ int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
 template <int MODE>
 void launch_conv(const ConvPlan& pl, hipStream_t s) {
   const ConvArgs& a = pl.a;
+  if constexpr (MODE == 2) if (pl.dma) {
+    const int tn = (a.GN + 127) / 128, tiles = ((a.GM + pl.bm - 1) / pl.bm) * tn;
+    const dim3 grid((unsigned)((int64_t)tiles * pl.splits));
+    const WgCfg w = wg_cfg();
+#define TTMI_WG(BM_, NW_, NS_)                                                                    \
+  if (pl.bm == BM_ && w.nw == NW_ && w.ns == NS_) {                                             \
+    hipLaunchKernelGGL((conv_wgrad_dma_kernel<BM_, NW_, NS_>), grid, dim3(NW_ * 64), 0, s, a, tn, tiles); \
+    return;                                                                                      \
+  }
+    TTMI_WG(128, 4, 4) TTMI_WG(128, 8, 4) TTMI_WG(128, 8, 3) TTMI_WG(128, 4, 2) TTMI_WG(128, 8, 2)
+    TTMI_WG(64, 4, 4) TTMI_WG(64, 8, 4) TTMI_WG(64, 8, 3) TTMI_WG(64, 4, 2) TTMI_WG(64, 8, 2)
+    TTMI_WG(64, 8, 6)
+#undef TTMI_WG
+    if (pl.bm == 128) hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 8, 2>), grid, dim3(512), 0, s, a, tn, tiles);
+    else hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 8, 2>), grid, dim3(512), 0, s, a, tn, tiles);
+    return;
+  }
+  if constexpr (MODE != 2) if (pl.dma) {
+    const FtCfg f = ft_cfg();
+    const unsigned gy = MODE == 1 ? (unsigned)(a.S * a.S) : 1u;
+    const dim3 grid((unsigned)(((int64_t)a.GM + f.bm - 1) / f.bm * (a.GN / pl.bn)), gy);
+#define TTMI_FT(BM_, BN_, NS_)                                                                    \
+  if (f.bm == BM_ && pl.bn == BN_ && f.ns == NS_) {                                             \
+    hipLaunchKernelGGL((conv_dma_kernel<MODE, BM_, BN_, NS_>), grid, dim3(512), 0, s, a);        \
+    return;                                                                                      \
+  }
+    TTMI_FT(256, 128, 3) TTMI_FT(256, 128, 2) TTMI_FT(128, 128, 2) TTMI_FT(128, 128, 3) TTMI_FT(128, 128, 4)
+    TTMI_FT(256, 64, 3) TTMI_FT(256, 64, 2) TTMI_FT(128, 64, 2) TTMI_FT(128, 64, 3) TTMI_FT(128, 64, 4)
+#undef TTMI_FT
+    if (pl.bn == 128) hipLaunchKernelGGL((conv_dma_kernel<MODE, 256, 128, 3>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((conv_dma_kernel<MODE, 256, 64, 3>), grid, dim3(512), 0, s, a);
+    return;
+  }
   const int64_t tiles = (int64_t)((a.GN + pl.bn - 1) / pl.bn) * ((a.GM + pl.bm - 1) / pl.bm);
   const unsigned gy = MODE == 1 ? (unsigned)(a.S * a.S) : (unsigned)pl.splits;
   const dim3 grid((unsigned)tiles, gy);
@@ -604,11 +1188,12 @@ extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
   int rc = conv_plan(d, &pl);
   if (rc) return rc;
   if (d->N == 0) return TTMI_OK;
-  if (d->mode == 0) {
+  const int mode = d->mode == 3 ? 0 : d->mode == 4 ? 2 : d->mode;
+  if (mode == 0) {
     TTMI_REQUIRE(d->x && d->w && d->out, "ttmi_conv2d: FWD needs x, w, out");
     TTMI_REQUIRE(!d->colsum == !d->colsumsq, "ttmi_conv2d: colsum and colsumsq go together");
     launch_conv<0>(pl, stream);
-  } else if (d->mode == 1) {
+  } else if (mode == 1) {
     TTMI_REQUIRE(d->dy && d->w && d->out, "ttmi_conv2d: DGRAD needs dy, w, out");
     launch_conv<1>(pl, stream);
   } else {
@@ -621,17 +1206,18 @@ extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
     if (rc) return rc;
     const int64_t n4 = (int64_t)pl.a.GM * pl.a.GN / 4;
     const unsigned gx = (unsigned)((n4 + 255) / 256);
+    const int KW = pl.a.KW, KHKW = pl.a.KH * pl.a.KW;
     int step = 1;
     if (pl.splits > WR_SPLITS) {         // chunk totals first (in place), then the chunk slabs
       hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx, (unsigned)((pl.splits + WR_SPLITS - 1) / WR_SPLITS)),
-                         dim3(256), 0, stream, pl.a.ws, pl.splits, 1, pl.a.GM, pl.a.GN, d->C, d->Cin, d->KW,
-                         d->KH * d->KW, 0, static_cast<float*>(d->out));
+                         dim3(256), 0, stream, pl.a.ws, pl.splits, 1, pl.a.GM, pl.a.GN, d->C, d->Cin, KW, KHKW,
+                         0, static_cast<float*>(d->out), pl.s2d);
       rc = ttmi_check_launch("ttmi_conv2d/wgrad_chunks");
       if (rc) return rc;
       step = WR_SPLITS;
     }
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx), dim3(256), 0, stream, pl.a.ws, pl.splits, step, pl.a.GM,
-                       pl.a.GN, d->C, d->Cin, d->KW, d->KH * d->KW, 1, static_cast<float*>(d->out));
+                       pl.a.GN, d->C, d->Cin, KW, KHKW, 1, static_cast<float*>(d->out), pl.s2d);
   }
   return ttmi_check_launch("ttmi_conv2d");
 }

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -254,11 +254,17 @@ SIGNATURES = {
     "ttmi_conv2d_workspace": (ctypes.c_int64, [c_p]),
     "ttmi_conv_weight_prep": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_nchw_to_nhwc": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
+    "ttmi_stem_s2d": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
+    "ttmi_stem_weight_prep": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p]),
     "ttmi_bn2d_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_i,
                             c_p, c_p, c_p, c_p]),
     "ttmi_bn2d_bwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_maxpool_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_maxpool_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
+    "ttmi_stem_pool_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p,
+                                 c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_stem_pool_bwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                 c_p, c_p, c_p]),
     "ttmi_avgpool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p]),
     "ttmi_avgpool_bwd": (c_i, [c_i, c_i, c_i, c_p, c_i, c_p, c_p, c_p]),
     "ttmi_l2norm_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p]),

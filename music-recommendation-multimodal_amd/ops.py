@@ -320,9 +320,12 @@ def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int,
            colsum: Optional[Tensor] = None, colsumsq: Optional[Tensor] = None) -> Tensor:
     """Implicit-GEMM conv (include/ttmi.h ttmi_conv2d): FWD y = conv(x), DGRAD dx, WGRAD dW."""
     Ho, Wo = conv_out_hw(H, W, k, stride, pad)
-    need = {"x": (x, N * H * W * C), "dy": (dy, N * Ho * Wo * Co),
+    xn = N * (H // 2) * (W // 2) * C if mode in (STEM_FWD, STEM_WGRAD) else N * H * W * C
+    need = {"x": (x, xn), "dy": (dy, N * Ho * Wo * Co),
             "colsum": (colsum, CONV_STAT_REPS * Co), "colsumsq": (colsumsq, CONV_STAT_REPS * Co)}
-    if mode == FWD:
+    if mode == STEM_FWD:
+        need.update(w=(w, Co * 16 * C), out=(out, N * Ho * Wo * Co))
+    elif mode == FWD:
         need.update(w=(w, Co * k * k * C), out=(out, N * Ho * Wo * Co))
     elif mode == DGRAD:
         need.update(w=(w, C * k * k * Co), out=(out, N * H * W * C), addend=(addend, N * H * W * C))
@@ -341,7 +344,7 @@ def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int,
     d.x, d.dy, d.w, d.out, d.addend = _p(x), _p(dy), _p(w), _p(out), _p(addend)
     d.colsum, d.colsumsq = _p(colsum), _p(colsumsq)
     ws = None
-    if mode == WGRAD:
+    if mode in (WGRAD, STEM_WGRAD):
         _L.load()
         nb = int(_L._lib.ttmi_conv2d_workspace(ctypes.byref(d)))
         if nb < 0:
@@ -363,6 +366,28 @@ def nchw_to_nhwc(x: Tensor, Cp: int, y: Tensor) -> Tensor:
     N, Cin, H, W = x.shape
     call("ttmi_nchw_to_nhwc", N, Cin, H, W, Cp, _p(x), _p(y), _s())
     return y
+
+
+STEM_FWD, STEM_WGRAD = 3, 4     # ttmi_conv2d modes of the 7x7/2 stem on a space-to-depth input
+
+
+def stem_s2d(x: Tensor, Cp: int, y: Tensor) -> Tensor:
+    """Space-to-depth stem input (include/ttmi.h ttmi_stem_s2d): x fp32 NCHW [N, Cin, H, W]
+    -> y bf16 [N, H/2, W/2, Cp], channel (ph*2 + pw)*Cin + ci."""
+    N, Cin, H, W = x.shape
+    if y.numel() < N * (H // 2) * (W // 2) * Cp:
+        raise ValueError("stem_s2d: y too small")
+    call("ttmi_stem_s2d", N, Cin, H, W, Cp, _p(x), _p(y), _s())
+    return y
+
+
+def stem_weight_prep(w: Tensor, Cp: int, wf: Tensor) -> None:
+    """The 7x7 stem weight [Co, Cin, 7, 7] fp32 as the 4x4 kernel over stem_s2d's input:
+    wf bf16 [Co, 4, 4, Cp]."""
+    Co, Cin, KH, KW = w.shape
+    if (KH, KW) != (7, 7) or wf.numel() < Co * 16 * Cp:
+        raise ValueError("stem_weight_prep: needs a 7x7 weight and a [Co, 4, 4, Cp] mirror")
+    call("ttmi_stem_weight_prep", Co, Cin, Cp, _p(w), _p(wf), _s())
 
 
 def bn2d_fwd(x: Tensor, colsum: Optional[Tensor], colsumsq: Optional[Tensor], w: Tensor, b: Tensor, y: Tensor,
@@ -395,6 +420,38 @@ def bn2d_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, sums:
             raise ValueError(f"bn2d_bwd: {name} smaller than x")
     call("ttmi_bn2d_bwd", M, C, _p(dy), _p(gate), _p(x), _p(mean), _p(rstd), _p(w), _p(sums),
          _p(g_out), _p(dx), _p(dw), _p(db), _s())
+    return dx
+
+
+def stem_pool_fwd(x: Tensor, colsum: Optional[Tensor], colsumsq: Optional[Tensor], w: Tensor, b: Tensor,
+                  y: Tensor, idx: Tensor, save_mean: Tensor, save_rstd: Tensor, *,
+                  running_mean: Optional[Tensor] = None, running_var: Optional[Tensor] = None,
+                  num_batches: Optional[Tensor] = None, eps: float = 1e-5, momentum: float = 0.1) -> Tensor:
+    """resnet18 stem tail bn1 → ReLU → maxpool(3, 2, 1) without storing the BN output
+    (include/ttmi.h ttmi_stem_pool_fwd): x [N, H, W, C] conv output -> y [N, Ho, Wo, C] + idx."""
+    N, H, W, C = x.shape
+    Ho, Wo = conv_out_hw(H, W, 3, 2, 1)
+    for name, t in (("colsum", colsum), ("colsumsq", colsumsq)):
+        if t is not None and (t.numel() < CONV_STAT_REPS * C or t.dtype != torch.int64):
+            raise ValueError(f"stem_pool_fwd: {name} needs [{CONV_STAT_REPS}][{C}] int64 replica rows")
+    if y.numel() < N * Ho * Wo * C or idx.numel() < N * Ho * Wo * C:
+        raise ValueError("stem_pool_fwd: y / idx too small")
+    call("ttmi_stem_pool_fwd", N, H, W, C, _p(x), _p(colsum), _p(colsumsq), _p(w), _p(b), eps, momentum,
+         _p(running_mean), _p(running_var), _p(num_batches), _p(y), _p(idx), _p(save_mean), _p(save_rstd), _s())
+    return y
+
+
+def stem_pool_bwd(dy: Tensor, idx: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, b: Tensor,
+                  sums: Tensor, dx: Tensor, dw: Optional[Tensor], db: Optional[Tensor]) -> Tensor:
+    """Backward of stem_pool_fwd (include/ttmi.h ttmi_stem_pool_bwd): dx at the conv output."""
+    N, H, W, C = x.shape
+    Ho, Wo = conv_out_hw(H, W, 3, 2, 1)
+    if sums.numel() < 2 * CONV_STAT_REPS * C or sums.dtype != torch.int64:
+        raise ValueError(f"stem_pool_bwd: sums needs [{CONV_STAT_REPS}][{2 * C}] int64 replica rows")
+    if dy.numel() < N * Ho * Wo * C or idx.numel() < N * Ho * Wo * C or dx.numel() < x.numel():
+        raise ValueError("stem_pool_bwd: dy / idx / dx too small")
+    call("ttmi_stem_pool_bwd", N, H, W, C, _p(dy), _p(idx), _p(x), _p(mean), _p(rstd), _p(w), _p(b),
+         _p(sums), _p(dx), _p(dw), _p(db), _s())
     return dx
 
 

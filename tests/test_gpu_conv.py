@@ -49,13 +49,19 @@ SHAPES = [  # N, Cin, H, W, Co, k, stride, pad
 ]
 
 
-@pytest.mark.parametrize("bm", ["64", "128"])
+@pytest.mark.parametrize("bm", ["64", "128", "dma"])
 @pytest.mark.parametrize("N,Cin,H,W,Co,k,s,p", SHAPES)
 def test_conv_fwd_dgrad_wgrad(gpu_pkg, monkeypatch, bm, N, Cin, H, W, Co, k, s, p):
-    """Both FWD/DGRAD tile heights (TTMI_CONV_BM) on every shape: partial tiles, stride-2
-    DGRAD parity classes (incl. the empty classes of a 1x1/2 conv: dx = addend), the 8-channel
-    padded stems, and WGRAD split-K with the fixed-order partial reduction."""
-    monkeypatch.setenv("TTMI_CONV_BM", bm)
+    """Every FWD/DGRAD kernel on every shape: the register-staged tile at both heights
+    (TTMI_CONV_BM, TTMI_CONV_DMA=0) and the 256-row LDS-DMA tile (TTMI_CONV_DMA=1, forced even
+    where the grid is small): partial tiles, stride-2 DGRAD parity classes (incl. the empty
+    classes of a 1x1/2 conv: dx = addend), the 8-channel padded stems (per-lane taps, k past
+    K zero-filled), and WGRAD split-K with the fixed-order partial reduction."""
+    if bm == "dma":
+        monkeypatch.setenv("TTMI_CONV_DMA", "1")
+    else:
+        monkeypatch.setenv("TTMI_CONV_DMA", "0")
+        monkeypatch.setenv("TTMI_CONV_BM", bm)
     ops = gpu_pkg.ops
     g = torch.Generator().manual_seed(N * 1000 + Cin + Co + k)
     Cp = (Cin + 7) // 8 * 8
@@ -102,6 +108,114 @@ def test_conv_fwd_dgrad_wgrad(gpu_pkg, monkeypatch, bm, N, Cin, H, W, Co, k, s, 
                    addend=add.to(DEV))
         torch.cuda.synchronize()
         assert rel(nchw(dx.float()), xr.grad + nchw(add.float())) < 8e-3
+
+
+@pytest.mark.parametrize("variant", ["reg", "dma"])
+@pytest.mark.parametrize("N,Cin,H,W", [(2, 3, 224, 224), (2, 1, 128, 256), (3, 3, 30, 34),
+                                       (2, 1, 16, 18)])
+def test_stem_s2d(gpu_pkg, monkeypatch, variant, N, Cin, H, W):
+    """The 7x7/2/3 stem as a 4x4/1 conv over the space-to-depth input (ttmi_stem_s2d, conv
+    modes 3 / 4): FWD output + BatchNorm column sums and WGRAD in torch's [Co][Cin][7][7]
+    layout against F.conv2d and its autograd, on both kernel families."""
+    monkeypatch.setenv("TTMI_CONV_DMA", "1" if variant == "dma" else "0")
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(N * 100 + Cin + H)
+    Co = 64
+    x = torch.randn(N, Cin, H, W, generator=g).to(torch.bfloat16).float()
+    w = (torch.randn(Co, Cin, 7, 7, generator=g) / math.sqrt(Cin * 49)).to(torch.bfloat16).float()
+    wr = w.clone().requires_grad_(True)
+    y_ref = TF.conv2d(x, wr, stride=2, padding=3)
+    dy = torch.randn(y_ref.shape, generator=g).to(torch.bfloat16).float()
+    y_ref.backward(dy)
+    Cp = gpu_pkg.cnn.stem_s2d_cp(Cin)
+    xd = torch.empty(N, H // 2, W // 2, Cp, device=DEV, dtype=torch.bfloat16)
+    ops.stem_s2d(x.to(DEV), Cp, xd)
+    xs = x.reshape(N, Cin, H // 2, 2, W // 2, 2).permute(0, 2, 4, 3, 5, 1).reshape(N, H // 2, W // 2, 4 * Cin)
+    assert torch.equal(xd[..., :4 * Cin].float().cpu(), xs)
+    assert not xd[..., 4 * Cin:].any()
+    wf = torch.empty(Co, 4, 4, Cp, device=DEV, dtype=torch.bfloat16)
+    ops.stem_weight_prep(w.to(DEV), Cp, wf)
+    Ho, Wo = H // 2, W // 2
+    y = torch.empty(N, Ho, Wo, Co, device=DEV, dtype=torch.bfloat16)
+    R = ops.CONV_STAT_REPS
+    csr = torch.zeros(R, Co, device=DEV, dtype=torch.int64)
+    cqr = torch.zeros(R, Co, device=DEV, dtype=torch.int64)
+    ops.conv2d(ops.STEM_FWD, N, H, W, Cp, Cin, Co, 7, 2, 3, x=xd, w=wf, out=y, colsum=csr, colsumsq=cqr)
+    torch.cuda.synchronize()
+    yr = y_ref.detach()
+    assert rel(nchw(y.float()), yr) < 8e-3
+    cs, cq = csr.sum(0).double() * 2.0 ** -24, cqr.sum(0).double() * 2.0 ** -24
+    assert rel(cs, yr.sum((0, 2, 3))) < 5e-3
+    assert rel(cq, (yr ** 2).sum((0, 2, 3))) < 5e-3
+    dyd = nhwc(dy).to(torch.bfloat16).to(DEV)
+    dw = torch.full((Co, Cin, 7, 7), 0.25, device=DEV)
+    ops.conv2d(ops.STEM_WGRAD, N, H, W, Cp, Cin, Co, 7, 2, 3, x=xd, dy=dyd, out=dw)
+    torch.cuda.synchronize()
+    assert rel(dw, 0.25 + wr.grad) < 2e-5 * max(1.0, math.sqrt(N * Ho * Wo / 256)) * 4
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 112, 112), (3, 13, 10)])
+def test_stem_pool_fused(gpu_pkg, N, H, W):
+    """ttmi_stem_pool_fwd / _bwd (bn1 + ReLU + maxpool with the BN output never stored) against
+    the unfused bn2d_fwd + maxpool_fwd and maxpool_bwd + bn2d_bwd: forward bit-identical
+    (pooled map, taps, saved stats, running stats), backward dx / dw / db to fp32 reduction
+    order (the fused reduce walks other row slabs), eval mode bit-identical."""
+    ops = gpu_pkg.ops
+    C = 64
+    g = torch.Generator().manual_seed(H * 10 + N)
+    x = (torch.randn(N, H, W, C, generator=g) * 2 + 0.3).to(torch.bfloat16).to(DEV)
+    R = ops.CONV_STAT_REPS
+    xf = x.float()
+    cs = torch.zeros(R, C, dtype=torch.int64, device=DEV)
+    cq = torch.zeros(R, C, dtype=torch.int64, device=DEV)
+    cs[0] = torch.round(xf.sum((0, 1, 2)).double() * 2 ** 24).long()
+    cq[0] = torch.round((xf ** 2).sum((0, 1, 2)).double() * 2 ** 24).long()
+    w = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    w[::7] *= -1                                      # negative scales flip the window order
+    b = (torch.randn(C, generator=g) * 0.5).to(DEV)
+    Ho, Wo = ops.conv_out_hw(H, W, 3, 2, 1)
+    rm1, rv1 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1 = torch.zeros(1, dtype=torch.int64, device=DEV)
+    nb2 = nb1.clone()
+    # unfused reference
+    a = torch.empty_like(x)
+    m1, r1 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    ops.bn2d_fwd(x, cs, cq, w, b, a, m1, r1, running_mean=rm1, running_var=rv1, num_batches=nb1, relu=True)
+    y1 = torch.empty(N, Ho, Wo, C, device=DEV, dtype=torch.bfloat16)
+    i1 = torch.empty(N, Ho, Wo, C, device=DEV, dtype=torch.uint8)
+    ops.maxpool_fwd(a, 3, 2, 1, y1, i1)
+    # fused
+    y2, i2 = torch.empty_like(y1), torch.empty_like(i1)
+    m2, r2 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    ops.stem_pool_fwd(x, cs, cq, w, b, y2, i2, m2, r2, running_mean=rm2, running_var=rv2, num_batches=nb2)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2) and torch.equal(i1, i2)
+    assert torch.equal(m1, m2) and torch.equal(r1, r2) and torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
+    assert nb2.item() == 1
+    # eval mode (running statistics)
+    y3, i3 = torch.empty_like(y1), torch.empty_like(i1)
+    ops.bn2d_fwd(x, None, None, w, b, a, m1, r1, running_mean=rm1, running_var=rv1, relu=True)
+    ops.maxpool_fwd(a, 3, 2, 1, y1, i1)
+    ops.stem_pool_fwd(x, None, None, w, b, y3, i3, m2, r2, running_mean=rm2, running_var=rv2)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y3) and torch.equal(i1, i3)
+    # backward
+    ops.bn2d_fwd(x, cs, cq, w, b, a, m1, r1, relu=True)
+    dy = torch.randn(N, Ho, Wo, C, generator=g).to(torch.bfloat16).to(DEV)
+    dpool = torch.empty_like(x)
+    ops.maxpool_bwd(dy, i2, 3, 2, 1, dpool)
+    sums1 = torch.zeros(2 * R * C, dtype=torch.int64, device=DEV)
+    dx1 = torch.empty_like(x)
+    dw1, db1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ops.bn2d_bwd(dpool, x, m1, r1, w, sums1, dx1, dw1, db1, gate=a)
+    sums2 = torch.zeros_like(sums1)
+    dx2 = torch.empty_like(x)
+    dw2, db2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ops.stem_pool_bwd(dy, i2, x, m1, r1, w, b, sums2, dx2, dw2, db2)
+    torch.cuda.synchronize()
+    assert rel(dw2, dw1) < 1e-5 and rel(db2, db1) < 1e-5
+    assert rel(dx2.float(), dx1.float()) < 8e-3
 
 
 @pytest.mark.parametrize("C,relu,res", [(64, True, False), (128, True, True), (512, False, False)])
