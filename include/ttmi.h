@@ -347,6 +347,14 @@ typedef struct ttmi_conv_desc {
   int64_t* colsum; int64_t* colsumsq;
   void* workspace;        /* WGRAD scratch (device), or NULL for FWD/DGRAD */
   int64_t workspace_bytes;
+  /* DGRAD only (ABI 17): the backward reduction of the BatchNorm(+ReLU) that produced this
+   * conv's input x, fused into the epilogue (bn_sums NULL: off).  Then out receives
+   * g = bf16(dx) ⊙ (bn_gate > 0) instead of dx (bn_gate = that BN's output, bf16 [N,H,W,C];
+   * NULL: no ReLU) and bn_sums [TTMI_CONV_STAT_REPS][2C] (int64 fixed point 2^36, zero on
+   * entry) += Σ g, Σ g·(bn_x − mean)·rstd per channel (bn_x = that BN's input) — exactly
+   * ttmi_bn2d_bwd_reduce's, so ttmi_bn2d_bwd_apply(g, ...) completes the BatchNorm backward. */
+  const void* bn_gate; const void* bn_x; const float* bn_mean; const float* bn_rstd;
+  int64_t* bn_sums;
 } ttmi_conv_desc;
 int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream);
 /* Bytes of WGRAD scratch ttmi_conv2d needs for this descriptor (0 for FWD/DGRAD; -1 on a bad
@@ -356,6 +364,17 @@ int64_t ttmi_conv2d_workspace(const ttmi_conv_desc* d);
  * likewise (wd may be NULL). w is torch's fp32 Conv2d.weight. */
 int ttmi_conv_weight_prep(int Co, int Cin, int Cp, int KH, int KW, const float* w, uint16_t* wf,
                           uint16_t* wd, hipStream_t stream);
+/* Every conv's mirrors in one launch (ABI 17): items[i] as ttmi_conv_weight_prep's arguments,
+ * or (s2d = 1, KH = KW = 7) ttmi_stem_weight_prep's [Co][4][4][Cp] mirror (wd unused).  At
+ * most TTMI_WPREP_MAX items per launch (more are split over launches). */
+#define TTMI_WPREP_MAX 24
+typedef struct ttmi_conv_wprep {
+  int Co, Cin, Cp, KH, KW, s2d;
+  const float* w;
+  uint16_t* wf;
+  uint16_t* wd;           /* may be NULL */
+} ttmi_conv_wprep;
+int ttmi_conv_weight_prep_batch(int n, const ttmi_conv_wprep* items, hipStream_t stream);
 /* y = bf16 NHWC [N,H,W,Cp] of x fp32 NCHW [N,Cin,H,W] (channels >= Cin zero). */
 int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const float* x, uint16_t* y,
                       hipStream_t stream);
@@ -404,6 +423,16 @@ int ttmi_stem_pool_bwd(int N, int H, int W, int C, const uint16_t* dy, const uin
                        const uint16_t* x, const float* mean, const float* rstd, const float* w,
                        const float* b, int64_t* sums, uint16_t* dx, float* dw, float* db,
                        hipStream_t stream);
+/* The two passes of ttmi_bn2d_bwd as separate calls (ABI 17), for a reduction fused elsewhere
+ * (ttmi_conv_desc.bn_sums): _reduce accumulates sums (and writes g_out = dy ⊙ (gate > 0) when
+ * g_out != NULL; g_out may alias dy); _apply computes dx from g (gate NULL: dy is already g)
+ * and adds the sums into dw, db. */
+int ttmi_bn2d_bwd_reduce(int64_t M, int C, const uint16_t* dy, const uint16_t* gate, const uint16_t* x,
+                         const float* mean, const float* rstd, int64_t* sums, uint16_t* g_out,
+                         hipStream_t stream);
+int ttmi_bn2d_bwd_apply(int64_t M, int C, const uint16_t* dy, const uint16_t* gate, const uint16_t* x,
+                        const float* mean, const float* rstd, const float* w, const int64_t* sums,
+                        uint16_t* dx, float* dw, float* db, hipStream_t stream);
 /* Max-pool k x k / stride, -inf padding (resnet18 maxpool 3/2/1), NHWC bf16; idx (uint8 per
  * output element) = the window tap of the max, first on ties.  Backward gathers. */
 int ttmi_maxpool_fwd(int N, int H, int W, int C, int k, int stride, int pad, const uint16_t* x,

@@ -96,14 +96,14 @@ class ResNetSaved:
 def weight_mirrors(P: Dict[str, Tensor], specs: List[ConvSpec], s2d: bool = True):
     """bf16 GEMM mirrors (Wf for FWD, Wd for DGRAD) of every conv weight; the stem's as the
     4x4 kernel over the space-to-depth input when ``s2d`` (ttmi_stem_weight_prep)."""
-    out = {}
+    out, items = {}, []
     for sp in specs:
-        w = P[sp.name]
+        w = P[sp.name].contiguous()
         dev = w.device
         if s2d and _is_stem(sp):
             cp = stem_s2d_cp(sp.cin)
             wf = torch.empty(sp.cout, 4, 4, cp, device=dev, dtype=torch.bfloat16)
-            ops.stem_weight_prep(w.contiguous(), cp, wf)
+            items.append((w, cp, wf, None, True))
             out[sp.name] = (wf, None)
             continue
         cp = STEM_CP if sp.cin < 8 else sp.cin
@@ -111,8 +111,9 @@ def weight_mirrors(P: Dict[str, Tensor], specs: List[ConvSpec], s2d: bool = True
         wd = None
         if sp.cin >= 8:
             wd = torch.empty(sp.cin, sp.k, sp.k, sp.cout, device=dev, dtype=torch.bfloat16)
-        ops.conv_weight_prep(w.contiguous(), cp, wf, wd)
+        items.append((w, cp, wf, wd, False))
         out[sp.name] = (wf, wd)
+    ops.conv_weight_prep_batch(items)          # one launch for the whole network
     return out
 
 
@@ -223,19 +224,29 @@ def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dic
     byname = {s.name: s for s in specs}
     R = ops.CONV_STAT_REPS
     sums = torch.zeros(2 * R * sum(sp.cout for sp in specs), device=dev, dtype=torch.int64)
-    soff = [0]
+    sl, o = {}, 0                       # each BatchNorm's [R][2C] fixed-point sums
+    for sp in specs:
+        sl[sp.name] = sums[o:o + 2 * R * sp.cout]
+        o += 2 * R * sp.cout
 
     def bn_bwd(sp: ConvSpec, act: ConvAct, dy: Tensor, gate: Optional[Tensor],
                g_out: Optional[Tensor] = None) -> Tensor:
-        s = sums[soff[0]:soff[0] + 2 * R * sp.cout]
-        soff[0] += 2 * R * sp.cout
         dyc = torch.empty_like(act.y)
-        ops.bn2d_bwd(dy, act.y, act.mean, act.rstd, P[sp.bn + ".weight"], s, dyc,
+        ops.bn2d_bwd(dy, act.y, act.mean, act.rstd, P[sp.bn + ".weight"], sl[sp.name], dyc,
                      grads[sp.bn + ".weight"], grads[sp.bn + ".bias"], gate=gate, g_out=g_out)
         return dyc
 
+    def bn_apply(sp: ConvSpec, act: ConvAct, g: Tensor) -> Tensor:
+        """BN backward whose reduction a DGRAD epilogue already did (g gated, sums filled)."""
+        dyc = torch.empty_like(act.y)
+        ops.bn2d_bwd_apply(g, act.y, act.mean, act.rstd, P[sp.bn + ".weight"], sl[sp.name], dyc,
+                           grads[sp.bn + ".weight"], grads[sp.bn + ".bias"])
+        return dyc
+
     def conv_bwd(sp: ConvSpec, act: ConvAct, dyc: Tensor, need_dx: bool,
-                 addend: Optional[Tensor] = None) -> Optional[Tensor]:
+                 addend: Optional[Tensor] = None, bn_of: Optional[Tuple[ConvSpec, ConvAct]] = None):
+        """WGRAD (+ DGRAD).  bn_of = (spec, act) of the BatchNorm+ReLU that produced this conv's
+        input: its backward reduction rides in the DGRAD epilogue, which then returns g."""
         C = act.x.shape[-1]
         s2d = _is_stem(sp) and act.x.shape[1] * 2 == act.H     # space-to-depth stem input
         ops.conv2d(ops.STEM_WGRAD if s2d else ops.WGRAD, N, act.H, act.W, C, sp.cin, sp.cout,
@@ -243,8 +254,12 @@ def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dic
         if not need_dx:
             return None
         dx = torch.empty_like(act.x)
+        bn = None
+        if bn_of is not None:
+            bsp, bact = bn_of
+            bn = (bact.a, bact.y, bact.mean, bact.rstd, sl[bsp.name])
         ops.conv2d(ops.DGRAD, N, act.H, act.W, C, sp.cin, sp.cout, sp.k, sp.stride, sp.pad,
-                   dy=dyc, w=st.mirrors[sp.name][1], out=dx, addend=addend)
+                   dy=dyc, w=st.mirrors[sp.name][1], out=dx, addend=addend, bn=bn)
         return dx
 
     # fc + global average pool
@@ -255,31 +270,43 @@ def resnet18_bwd(P: Dict[str, Tensor], st: ResNetSaved, dout: Tensor, grads: Dic
     ops.linear_dx(dc, st.fc_w, dfeat)
     dy = torch.empty_like(st.last)
     ops.avgpool_bwd(dfeat, dy)
-    # residual stages, reversed
-    for lname, _, _, _ in reversed(LAYERS):
-        for bi in (1, 0):
-            b = f"{lname}.{bi}."
-            c1, c2 = byname[b + "conv1.weight"], byname[b + "conv2.weight"]
-            ds = byname.get(b + "downsample.0.weight")
-            a1, a2 = st.acts[c1.name], st.acts[c2.name]
-            g = torch.empty_like(a2.a)                # dy ⊙ ReLU gate: the identity branch's grad
+    # residual stages, reversed.  Every BatchNorm whose input gradient comes out of a DGRAD
+    # (bn1 from conv2's, the previous block's bn2 from conv1's) has its backward reduction
+    # fused into that DGRAD's epilogue (ttmi_conv_desc.bn_sums) and only its apply pass here.
+    fwd_blocks = [f"{lname}.{bi}." for lname, _, _, _ in LAYERS for bi in range(2)]
+    gated = False                        # dy is already the gated g of this block's bn2
+    for j in reversed(range(len(fwd_blocks))):
+        b = fwd_blocks[j]
+        c1, c2 = byname[b + "conv1.weight"], byname[b + "conv2.weight"]
+        ds = byname.get(b + "downsample.0.weight")
+        a1, a2 = st.acts[c1.name], st.acts[c2.name]
+        if gated:
+            g = dy                                    # dy ⊙ ReLU gate: the identity branch's grad
+            d2 = bn_apply(c2, a2, g)
+        else:
+            g = torch.empty_like(a2.a)
             d2 = bn_bwd(c2, a2, dy, a2.a, g_out=g)
-            dmid = conv_bwd(c2, a2, d2, True)
-            d1 = bn_bwd(c1, a1, dmid, a1.a)
-            if ds is not None:
-                ad = st.acts[ds.name]
-                dd = bn_bwd(ds, ad, g, None)
-                idn_dx = conv_bwd(ds, ad, dd, True)
-            else:
-                idn_dx = g
-            dy = conv_bwd(c1, a1, d1, True, addend=idn_dx)
+        g1 = conv_bwd(c2, a2, d2, True, bn_of=(c1, a1))
+        d1 = bn_apply(c1, a1, g1)
+        if ds is not None:
+            ad = st.acts[ds.name]
+            dd = bn_bwd(ds, ad, g, None)
+            idn_dx = conv_bwd(ds, ad, dd, True)
+        else:
+            idn_dx = g
+        prev = None
+        if j > 0:                                     # the previous block's bn2 + ReLU output
+            pc2 = byname[fwd_blocks[j - 1] + "conv2.weight"]
+            prev = (pc2, st.acts[pc2.name])
+        dy = conv_bwd(c1, a1, d1, True, addend=idn_dx, bn_of=prev)
+        gated = prev is not None
     # max-pool and stem (no input grad: the encoder input is data)
     stem = specs[0]
     act = st.acts[stem.name]
-    s = sums[soff[0]:soff[0] + 2 * R * stem.cout]
     d0 = torch.empty_like(act.y)
     ops.stem_pool_bwd(dy, st.pool_idx, act.y, act.mean, act.rstd, P[stem.bn + ".weight"],
-                      P[stem.bn + ".bias"], s, d0, grads[stem.bn + ".weight"], grads[stem.bn + ".bias"])
+                      P[stem.bn + ".bias"], sl[stem.name], d0, grads[stem.bn + ".weight"],
+                      grads[stem.bn + ".bias"])
     conv_bwd(stem, act, d0, False)
 
 

@@ -19,6 +19,8 @@ namespace {
 constexpr int MAXC = 512;
 
 int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096)); }
+constexpr int EW_U = 4;     // 16-byte items per thread per trip in the element-wise BN passes
+int grid_ew(int64_t n) { return grid_for((n + EW_U - 1) / EW_U); }
 
 // ---------------------------------------------------------------- BatchNorm2d forward
 __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const bf16_t* __restrict__ x,
@@ -62,18 +64,32 @@ __global__ __launch_bounds__(256) void bn2d_fwd_kernel(int64_t M, int C, const b
   __syncthreads();
   const int cpr = C / 8;
   const int64_t n = M * cpr;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cpr) * 8;
-    float v[8];
-    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
-    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (res) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+  // EW_U 16-byte items per thread per trip, every load issued before any math (one load per
+  // trip left the pass latency-bound at ~half the HBM rate)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * EW_U;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * EW_U + threadIdx.x; i0 < n; i0 += stride) {
+    uint4 qx[EW_U], qr[EW_U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      v[e] = v[e] * sa[c0 + e] + sb[c0 + e] + r[e];
-      if (relu) v[e] = fmaxf(v[e], 0.f);
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t i = min(i0 + (int64_t)u * blockDim.x, n - 1);
+      qx[u] = reinterpret_cast<const uint4*>(x)[i];
+      qr[u] = res ? reinterpret_cast<const uint4*>(res)[i] : make_uint4(0u, 0u, 0u, 0u);
     }
-    reinterpret_cast<uint4*>(y)[i] = pack8(v);
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i >= n) break;
+      const int c0 = (int)(i % cpr) * 8;
+      float v[8], r[8];
+      unpack8(qx[u], v);
+      unpack8(qr[u], r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = v[e] * sa[c0 + e] + sb[c0 + e] + r[e];
+        if (relu) v[e] = fmaxf(v[e], 0.f);
+      }
+      reinterpret_cast<uint4*>(y)[i] = pack8(v);
+    }
   }
 }
 
@@ -188,24 +204,38 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_kernel(int64_t M, int C, c
   __syncthreads();
   const int cpr = C / 8;
   const int64_t n = M * cpr;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cpr) * 8;
-    float g[8], xv[8], o[8];
-    unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
-    if (gate) {
-      float gv[8];
-      unpack8(reinterpret_cast<const uint4*>(gate)[i], gv);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * EW_U;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * EW_U + threadIdx.x; i0 < n; i0 += stride) {
+    uint4 qd[EW_U], qg[EW_U], qx[EW_U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = gv[e] > 0.f ? g[e] : 0.f;
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t i = min(i0 + (int64_t)u * blockDim.x, n - 1);
+      qd[u] = reinterpret_cast<const uint4*>(dy)[i];
+      qg[u] = gate ? reinterpret_cast<const uint4*>(gate)[i] : make_uint4(0u, 0u, 0u, 0u);
+      qx[u] = reinterpret_cast<const uint4*>(x)[i];
     }
-    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
-      const float xh = (xv[e] - smu[c]) * srs[c];
-      o[e] = sk[c] * (g[e] - sm1[c] - xh * sm2[c]);
+    for (int u = 0; u < EW_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i >= n) break;
+      const int c0 = (int)(i % cpr) * 8;
+      float g[8], xv[8], o[8];
+      unpack8(qd[u], g);
+      if (gate) {
+        float gv[8];
+        unpack8(qg[u], gv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = gv[e] > 0.f ? g[e] : 0.f;
+      }
+      unpack8(qx[u], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        const float xh = (xv[e] - smu[c]) * srs[c];
+        o[e] = sk[c] * (g[e] - sm1[c] - xh * sm2[c]);
+      }
+      reinterpret_cast<uint4*>(dx)[i] = pack8(o);
     }
-    reinterpret_cast<uint4*>(dx)[i] = pack8(o);
   }
 }
 
@@ -417,7 +447,10 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(int N, int H, int W,
 }
 
 // g (8 channels at conv-output element i) = Σ over the pool windows that chose it of dy,
-// zeroed where the recomputed BN+ReLU output is 0; xv = the conv output there.
+// zeroed where the recomputed BN+ReLU output is 0; xv = the conv output there.  For the 3/2/1
+// pool, input row h lies in window ho = (h+1)/2 (tap kh = h+1−2ho) and, for odd h, also in
+// ho − 1: the 2 x 2 candidate windows are loaded unconditionally (clamped, then masked), so a
+// row's five loads are independent and in flight together.
 TTMI_DEV void stem_grad8(const StemBn& s, int64_t i, int cpr, int H, int W, int Ho, int Wo,
                          const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
                          const bf16_t* __restrict__ x, float* g, float* xv) {
@@ -427,28 +460,40 @@ TTMI_DEV void stem_grad8(const StemBn& s, int64_t i, int cpr, int H, int W, int 
   const int h = (int)(t % H);
   const int bb = (int)(t / H);
   const uint4 qx = reinterpret_cast<const uint4*>(x)[i];
+  const int hh = (h + 1) >> 1, wh = (w + 1) >> 1;
+  uint4 qd[2][2];
+  uint2 qa[2][2];
+  int tap[2][2];
+  bool ok[2][2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int ho = hh - dh, wo = wh - dw;
+      const int kh = h + 1 - 2 * ho, kw = w + 1 - 2 * wo;
+      ok[dh][dw] = ho >= 0 && ho < Ho && wo >= 0 && wo < Wo && kh < 3 && kw < 3;
+      const int64_t o = (((int64_t)bb * Ho + min(max(ho, 0), Ho - 1)) * Wo + min(max(wo, 0), Wo - 1)) * cpr + cg;
+      qd[dh][dw] = reinterpret_cast<const uint4*>(dy)[o];
+      qa[dh][dw] = reinterpret_cast<const uint2*>(idx)[o];
+      tap[dh][dw] = kh * 3 + kw;
+    }
 #pragma unroll
   for (int e = 0; e < 8; ++e) g[e] = 0.f;
-  const int ho_lo = max(0, (h + 1 - 3 + 2) / 2), ho_hi = min(Ho - 1, (h + 1) / 2);
-  const int wo_lo = max(0, (w + 1 - 3 + 2) / 2), wo_hi = min(Wo - 1, (w + 1) / 2);
-  for (int ho = ho_lo; ho <= ho_hi; ++ho) {
-    const int kh = h - (ho * 2 - 1);
-    if (kh < 0 || kh >= 3) continue;
-    for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-      const int kw = w - (wo * 2 - 1);
-      if (kw < 0 || kw >= 3) continue;
-      const int64_t o = (((int64_t)bb * Ho + ho) * Wo + wo) * cpr + cg;
-      const uint2 a = reinterpret_cast<const uint2*>(idx)[o];
+  // windows in (ho, wo) ascending order, as maxpool_bwd adds them
+#pragma unroll
+  for (int dh = 1; dh >= 0; --dh)
+#pragma unroll
+    for (int dw = 1; dw >= 0; --dw) {
+      if (!ok[dh][dw]) continue;
       float d[8];
-      unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
-      const uint8_t tap = (uint8_t)(kh * 3 + kw);
+      unpack8(qd[dh][dw], d);
+      const uint2 a = qa[dh][dw];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const uint8_t ae = (uint8_t)(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xFF);
-        if (ae == tap) g[e] += d[e];
+        const int ae = (int)(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xFF);
+        if (ae == tap[dh][dw]) g[e] += d[e];
       }
     }
-  }
   float av[8];
   stem_act8(s, cg * 8, qx, av);
   unpack8(qx, xv);
@@ -494,6 +539,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(int N, int H,
   for (int e = 0; e < 8; ++e) { mu[e] = cg < cpr ? mean[c0 + e] : 0.f; rs[e] = cg < cpr ? rstd[c0 + e] : 0.f; }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   if (rl < tpr && cg < cpr) {
+#pragma unroll 2
     for (int64_t m = r0 + rl; m < r1; m += tpr) {
       float g[8], xv[8];
       stem_grad8(s, m * cpr + cg, cpr, H, W, Ho, Wo, dy, idx, x, g, xv);
@@ -583,18 +629,18 @@ extern "C" int ttmi_bn2d_fwd(int64_t M, int C, const uint16_t* x, const int64_t*
   TTMI_REQUIRE(!running_mean == !running_var, "ttmi_bn2d_fwd: running_mean/var go together");
   TTMI_REQUIRE(!colsum == !colsumsq, "ttmi_bn2d_fwd: colsum/colsumsq go together");
   TTMI_REQUIRE(colsum || running_mean, "ttmi_bn2d_fwd: eval mode (no colsum) needs running stats");
-  hipLaunchKernelGGL(bn2d_fwd_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, s, M, C, (const bf16_t*)x,
+  hipLaunchKernelGGL(bn2d_fwd_kernel, dim3(grid_ew(M * C / 8)), dim3(256), 0, s, M, C, (const bf16_t*)x,
                      colsum, colsumsq, w, b, eps, momentum, running_mean, running_var,
                      num_batches_tracked, (const bf16_t*)residual, relu, (bf16_t*)y, save_mean, save_rstd);
   return ttmi_check_launch("ttmi_bn2d_fwd");
 }
 
-extern "C" int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate,
-                             const uint16_t* x, const float* mean, const float* rstd,
-                             const float* w, int64_t* sums, uint16_t* g_out, uint16_t* dx,
-                             float* dw, float* db, hipStream_t s) {
-  TTMI_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= MAXC, "ttmi_bn2d_bwd: need 0 < C <= %d, C %% 8 == 0", MAXC);
-  TTMI_REQUIRE(dy && x && mean && rstd && w && sums && dx, "ttmi_bn2d_bwd: null argument");
+extern "C" int ttmi_bn2d_bwd_reduce(int64_t M, int C, const uint16_t* dy, const uint16_t* gate,
+                                    const uint16_t* x, const float* mean, const float* rstd, int64_t* sums,
+                                    uint16_t* g_out, hipStream_t s) {
+  TTMI_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= MAXC, "ttmi_bn2d_bwd_reduce: need 0 < C <= %d, C %% 8 == 0",
+               MAXC);
+  TTMI_REQUIRE(dy && x && mean && rstd && sums, "ttmi_bn2d_bwd_reduce: null argument");
   const int cpr = C / 8;
   const int tpr = std::max(1, 256 / cpr);
   int64_t blocks = std::min<int64_t>(1024, (M + tpr * 8 - 1) / (tpr * 8));
@@ -603,12 +649,29 @@ extern "C" int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_
   hipLaunchKernelGGL(bn2d_bwd_reduce_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0, s, M, C,
                      (const bf16_t*)dy, (const bf16_t*)gate, (const bf16_t*)x, mean, rstd, (bf16_t*)g_out,
                      sums, rpb);
-  int rc = ttmi_check_launch("ttmi_bn2d_bwd/reduce");
-  if (rc) return rc;
-  hipLaunchKernelGGL(bn2d_bwd_apply_kernel, dim3(grid_for(M * C / 8)), dim3(256), 0, s, M, C,
+  return ttmi_check_launch("ttmi_bn2d_bwd_reduce");
+}
+
+extern "C" int ttmi_bn2d_bwd_apply(int64_t M, int C, const uint16_t* dy, const uint16_t* gate,
+                                   const uint16_t* x, const float* mean, const float* rstd, const float* w,
+                                   const int64_t* sums, uint16_t* dx, float* dw, float* db, hipStream_t s) {
+  TTMI_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= MAXC, "ttmi_bn2d_bwd_apply: need 0 < C <= %d, C %% 8 == 0",
+               MAXC);
+  TTMI_REQUIRE(dy && x && mean && rstd && w && sums && dx, "ttmi_bn2d_bwd_apply: null argument");
+  hipLaunchKernelGGL(bn2d_bwd_apply_kernel, dim3(grid_ew(M * C / 8)), dim3(256), 0, s, M, C,
                      (const bf16_t*)dy, (const bf16_t*)gate, (const bf16_t*)x, mean, rstd, w, sums,
                      (bf16_t*)dx, dw, db);
-  return ttmi_check_launch("ttmi_bn2d_bwd/apply");
+  return ttmi_check_launch("ttmi_bn2d_bwd_apply");
+}
+
+extern "C" int ttmi_bn2d_bwd(int64_t M, int C, const uint16_t* dy, const uint16_t* gate,
+                             const uint16_t* x, const float* mean, const float* rstd,
+                             const float* w, int64_t* sums, uint16_t* g_out, uint16_t* dx,
+                             float* dw, float* db, hipStream_t s) {
+  TTMI_REQUIRE(dy && x && mean && rstd && w && sums && dx, "ttmi_bn2d_bwd: null argument");
+  int rc = ttmi_bn2d_bwd_reduce(M, C, dy, gate, x, mean, rstd, sums, g_out, s);
+  if (rc) return rc;
+  return ttmi_bn2d_bwd_apply(M, C, dy, gate, x, mean, rstd, w, sums, dx, dw, db, s);
 }
 
 extern "C" int ttmi_maxpool_fwd(int N, int H, int W, int C, int k, int stride, int pad,
@@ -687,7 +750,7 @@ extern "C" int ttmi_stem_pool_bwd(int N, int H, int W, int C, const uint16_t* dy
   const int64_t M = (int64_t)N * H * W;
   const int cpr = C / 8;
   const int tpr = std::max(1, 256 / cpr);
-  int64_t blocks = std::min<int64_t>(2048, (M + tpr * 8 - 1) / (tpr * 8));
+  int64_t blocks = std::min<int64_t>(8192, (M + tpr * 4 - 1) / (tpr * 4));
   blocks = std::max<int64_t>(blocks, 1);
   const int64_t rpb = (M + blocks - 1) / blocks;
   hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0, s, N, H, W,

@@ -62,6 +62,12 @@ struct ConvArgs {
   int64_t* colsum;          // FWD: Σ y per channel, int64 fixed point 2^-24 (may be NULL)
   int64_t* colsumsq;
   float* ws;                // WGRAD: partials [splits][GM][GN]
+  // DGRAD: fused BatchNorm-backward reduction of the layer that produced x (bn_sums != NULL)
+  const bf16_t* bn_gate;    // that BN's (ReLU) output, or NULL
+  const bf16_t* bn_x;       // that BN's input
+  const float* bn_mean;
+  const float* bn_rstd;
+  int64_t* bn_sums;         // [REPS][2][GN] int64 fixed point 2^36
   int GM, GN, GK;           // GEMM sizes (DGRAD: per class below)
   int k_split;              // WGRAD: pixels per split (multiple of 64)
   FDiv fC, fKW, fWo, fHo, fCo;
@@ -570,11 +576,19 @@ __global__ __launch_bounds__(512) void conv_dma_kernel(ConvArgs a) {
     }
   }
   float cs[FN][4], cq[FN][4];
+  // DGRAD + fused BN-backward reduction: g = bf16(dx) gated by the BN's ReLU output is stored,
+  // and (cs, cq) collect Σg, Σg·x̂ (the FWD statistics path reuses them for Σy, Σy²)
+  const bool bnf = MODE == 1 && a.bn_sums != nullptr;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * WN + j * 16 + 4 * lg;
+    float mu[4], rs[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) cs[j][e] = cq[j][e] = 0.f;
+    for (int e = 0; e < 4; ++e) {
+      cs[j][e] = cq[j][e] = 0.f;
+      mu[e] = bnf ? a.bn_mean[n + e] : 0.f;
+      rs[e] = bnf ? a.bn_rstd[n + e] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       if (orow[i] < 0) continue;
@@ -585,14 +599,29 @@ __global__ __launch_bounds__(512) void conv_dma_kernel(ConvArgs a) {
         const ushort4 q = *reinterpret_cast<const ushort4*>(a.addend + orow[i] * a.GN + n);
         o[0] += bf2f(q.x); o[1] += bf2f(q.y); o[2] += bf2f(q.z); o[3] += bf2f(q.w);
       }
+      if (bnf) {
+        const ushort4 qx = *reinterpret_cast<const ushort4*>(a.bn_x + orow[i] * a.GN + n);
+        ushort4 qg = make_ushort4(0x3F80, 0x3F80, 0x3F80, 0x3F80);          // 1.0: no gate
+        if (a.bn_gate) qg = *reinterpret_cast<const ushort4*>(a.bn_gate + orow[i] * a.GN + n);
+        const float xv[4] = {bf2f(qx.x), bf2f(qx.y), bf2f(qx.z), bf2f(qx.w)};
+        const float gv[4] = {bf2f(qg.x), bf2f(qg.y), bf2f(qg.z), bf2f(qg.w)};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { cs[j][e] += o[e]; cq[j][e] += o[e] * o[e]; }
+        for (int e = 0; e < 4; ++e) {
+          const float gr = gv[e] > 0.f ? bf2f(f2bf(o[e])) : 0.f;
+          o[e] = gr;
+          cs[j][e] += gr;
+          cq[j][e] += gr * (xv[e] - mu[e]) * rs[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { cs[j][e] += o[e]; cq[j][e] += o[e] * o[e]; }
+      }
       ushort4 q;
       q.x = f2bf(o[0]); q.y = f2bf(o[1]); q.z = f2bf(o[2]); q.w = f2bf(o[3]);
       *reinterpret_cast<ushort4*>(dst) = q;
     }
   }
-  if (MODE == 0 && a.colsum) {
+  if ((MODE == 0 && a.colsum) || bnf) {
     // BatchNorm column statistics (as conv_tile_kernel): rows reduced in registers, over the
     // 16 row lanes, then over the four row-waves through LDS in a fixed order; one int64
     // fixed-point add per column per workgroup into replica row blockIdx.x % REPS.
@@ -622,9 +651,15 @@ __global__ __launch_bounds__(512) void conv_dma_kernel(ConvArgs a) {
       float s = 0.f, s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) { s += red[(w * 2) * BN + tid]; s2 += red[(w * 2 + 1) * BN + tid]; }
-      const int rep = blockIdx.x % TTMI_CONV_STAT_REPS;
-      fx_add(a.colsum + (int64_t)rep * a.GN + n0 + tid, s, TTMI_FX_STAT);
-      fx_add(a.colsumsq + (int64_t)rep * a.GN + n0 + tid, s2, TTMI_FX_STAT);
+      const int rep = (blockIdx.x + blockIdx.y) % TTMI_CONV_STAT_REPS;
+      if (bnf) {
+        int64_t* r = a.bn_sums + (int64_t)rep * 2 * a.GN + n0 + tid;
+        fx_add(r, s, TTMI_FX_GRAD);
+        fx_add(r + a.GN, s2, TTMI_FX_GRAD);
+      } else {
+        fx_add(a.colsum + (int64_t)rep * a.GN + n0 + tid, s, TTMI_FX_STAT);
+        fx_add(a.colsumsq + (int64_t)rep * a.GN + n0 + tid, s2, TTMI_FX_STAT);
+      }
     }
   }
 }
@@ -916,6 +951,67 @@ __global__ __launch_bounds__(256) void stem_weight_prep_kernel(int Co, int Cin, 
   }
 }
 
+// All convs' weight mirrors in one launch.  A workgroup owns a 32 (co) x TC (c) tile of one
+// item: it reads w[co][c0 .. c0+TC)[KH][KW] — contiguous per co — into LDS, then writes Wf
+// [co][kh][kw][c] with c fastest and Wd [c][kh][kw][co] with co fastest, both as contiguous
+// runs (the per-element kernel wrote Wd 2 bytes at a stride of KH·KW·Co: one transaction per
+// element).  Space-to-depth stem items (small) go element-wise.  Items are found by a scan of
+// <= TTMI_WPREP_MAX prefix offsets over workgroups.
+struct WPrepBatch {
+  int n;
+  int blk[TTMI_WPREP_MAX + 1];            // first workgroup of each item
+  ttmi_conv_wprep it[TTMI_WPREP_MAX];
+};
+constexpr int WP_CO = 32;
+TTMI_DEV int wp_tc(const ttmi_conv_wprep& t) { return t.KH * t.KW <= 9 ? 32 : 4; }
+__global__ __launch_bounds__(256) void conv_weight_prep_batch_kernel(WPrepBatch b) {
+  __shared__ float tile[WP_CO * (32 * 9 + 1)];
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.blk[k + 1]) ++k;
+  const ttmi_conv_wprep& t = b.it[k];
+  const int j = blockIdx.x - b.blk[k];
+  bf16_t* wf = reinterpret_cast<bf16_t*>(t.wf);
+  if (t.s2d) {                                          // 1024 elements per workgroup
+    const int64_t n = (int64_t)t.Co * 16 * t.Cp;
+    for (int64_t i = (int64_t)j * 1024 + threadIdx.x; i < min(n, (int64_t)(j + 1) * 1024); i += blockDim.x) {
+      const int cc = (int)(i % t.Cp);
+      const int tap = (int)((i / t.Cp) % 16), co = (int)(i / (16 * t.Cp));
+      const int q = cc / t.Cin, ci = cc - q * t.Cin;
+      const int kh = 2 * (tap >> 2) + (q >> 1) - 1, kw = 2 * (tap & 3) + (q & 1) - 1;
+      const bool ok = q < 4 && kh >= 0 && kh < 7 && kw >= 0 && kw < 7;
+      wf[i] = f2bf(ok ? t.w[(((int64_t)co * t.Cin + ci) * 7 + kh) * 7 + kw] : 0.f);
+    }
+    return;
+  }
+  const int T = t.KH * t.KW, TC = wp_tc(t), P = TC * T + 1;   // LDS pitch per co (odd: no conflicts)
+  const int ntc = (t.Cp + TC - 1) / TC;
+  const int co0 = (j / ntc) * WP_CO, c0 = (j % ntc) * TC;
+  // load: w[co0 + r][c0 + cl][tap], cl * T + tap fastest (one contiguous run per co)
+  for (int f = threadIdx.x; f < WP_CO * TC * T; f += blockDim.x) {
+    const int r = f / (TC * T), q = f - r * (TC * T);
+    const int cl = q / T, tap = q - cl * T;
+    const int co = co0 + r, cc = c0 + cl;
+    tile[r * P + q] = (co < t.Co && cc < t.Cin) ? t.w[((int64_t)co * t.Cin + cc) * T + tap] : 0.f;
+  }
+  __syncthreads();
+  // Wf[co][tap][c]: c fastest
+  for (int f = threadIdx.x; f < WP_CO * T * TC; f += blockDim.x) {
+    const int cl = f % TC, q = f / TC;
+    const int tap = q % T, r = q / T;
+    const int co = co0 + r, cc = c0 + cl;
+    if (co < t.Co && cc < t.Cp) wf[((int64_t)co * T + tap) * t.Cp + cc] = f2bf(tile[r * P + cl * T + tap]);
+  }
+  if (t.wd) {                                           // Wd[c][tap][co]: co fastest
+    bf16_t* wd = reinterpret_cast<bf16_t*>(t.wd);
+    for (int f = threadIdx.x; f < TC * T * WP_CO; f += blockDim.x) {
+      const int r = f % WP_CO, q = f / WP_CO;
+      const int tap = q % T, cl = q / T;
+      const int co = co0 + r, cc = c0 + cl;
+      if (co < t.Co && cc < t.Cin) wd[((int64_t)cc * T + tap) * t.Co + co] = f2bf(tile[r * P + cl * T + tap]);
+    }
+  }
+}
+
 int grid1(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 8192); }
 
 }  // namespace
@@ -938,6 +1034,33 @@ extern "C" int ttmi_nchw_to_nhwc(int N, int Cin, int H, int W, int Cp, const flo
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid1((int64_t)N * H * W)), dim3(256), 0, s, N, Cin, H,
                      W, Cp, x, y);
   return ttmi_check_launch("ttmi_nchw_to_nhwc");
+}
+
+extern "C" int ttmi_conv_weight_prep_batch(int n, const ttmi_conv_wprep* items, hipStream_t s) {
+  TTMI_REQUIRE(n >= 0 && (n == 0 || items), "ttmi_conv_weight_prep_batch: bad item list");
+  for (int base = 0; base < n; base += TTMI_WPREP_MAX) {
+    WPrepBatch b{};
+    b.n = std::min(TTMI_WPREP_MAX, n - base);
+    b.blk[0] = 0;
+    for (int k = 0; k < b.n; ++k) {
+      const ttmi_conv_wprep& t = items[base + k];
+      TTMI_REQUIRE(t.Co > 0 && t.Cin > 0 && t.Cp % 8 == 0 && t.w && t.wf, "ttmi_conv_weight_prep_batch: item %d",
+                   base + k);
+      TTMI_REQUIRE(t.s2d ? (t.KH == 7 && t.KW == 7 && t.Cp >= 4 * t.Cin)
+                         : (t.Cp >= t.Cin && t.KH > 0 && t.KW > 0 && t.KH * t.KW <= 49),
+                   "ttmi_conv_weight_prep_batch: item %d shape", base + k);
+      b.it[k] = t;
+      const int tc = t.KH * t.KW <= 9 ? 32 : 4;
+      const int64_t nb = t.s2d ? ((int64_t)t.Co * 16 * t.Cp + 1023) / 1024
+                               : (int64_t)((t.Co + WP_CO - 1) / WP_CO) * ((t.Cp + tc - 1) / tc);
+      TTMI_REQUIRE(b.blk[k] + nb < (1ll << 30), "ttmi_conv_weight_prep_batch: too many tiles");
+      b.blk[k + 1] = b.blk[k] + (int)nb;
+    }
+    hipLaunchKernelGGL(conv_weight_prep_batch_kernel, dim3((unsigned)b.blk[b.n]), dim3(256), 0, s, b);
+    const int rc = ttmi_check_launch("ttmi_conv_weight_prep_batch");
+    if (rc) return rc;
+  }
+  return TTMI_OK;
 }
 
 extern "C" int ttmi_stem_s2d(int N, int Cin, int H, int W, int Cp, const float* x, uint16_t* y,
@@ -969,15 +1092,18 @@ int forced_bm() {
   return v == 64 || v == 128 ? v : 0;
 }
 
-// TTMI_CONV_DMA=0|1 forces the FWD/DGRAD kernel family; by default the LDS-DMA tile runs
-// whenever its 256-row tiles still give every CU a workgroup (N % 64 == 0 channels).
-// TTMI_CONV_FT=<rows>:<stages> picks the FWD/DGRAD LDS-DMA tile (default 256:3; the grid
-// must then be recomputed, so the host plans with the same value).
+// TTMI_CONV_DMA=0|1 forces the kernel family; by default the LDS-DMA kernels run whenever
+// the GEMM's N (output channels) is a multiple of 64: they beat the register-staged tile on
+// every cfg-3 layer, the 7x7 / 4x4 stems and the 1x1 downsamples included.
+// TTMI_CONV_FT=<rows>:<stages> picks the FWD/DGRAD LDS-DMA tile.  Default (measured over
+// every cfg-3 layer, tools/conv_bench.py): two-stage rings, so two workgroups share a CU —
+// 256 x 64 tiles for 64-channel outputs, 128 x 128 otherwise (3- and 4-stage rings, one
+// workgroup per CU, ran 1.2-1.9x longer).
 struct FtCfg {
   int bm, ns;
 };
-FtCfg ft_cfg() {
-  FtCfg f{256, 3};
+FtCfg ft_cfg(int bn) {
+  FtCfg f{bn == 64 ? 256 : 128, 2};
   const char* e = getenv("TTMI_CONV_FT");
   int a = 0, b = 0;
   if (e && sscanf(e, "%d:%d", &a, &b) == 2 && (a == 128 || a == 256) && b >= 2 && b <= 4) f = FtCfg{a, b};
@@ -999,10 +1125,10 @@ int forced_dma() {
   const char* e = getenv("TTMI_CONV_DMA");
   return e ? (atoi(e) ? 1 : 0) : -1;
 }
-bool use_dma(int64_t tiles, int n) {
+bool use_dma(int64_t, int n) {
   if (n % 64 != 0) return false;
   const int f = forced_dma();
-  return f >= 0 ? f == 1 : tiles >= 256;
+  return f >= 0 ? f == 1 : true;
 }
 
 struct ConvPlan {
@@ -1068,6 +1194,12 @@ int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
   a.out = d->out;
   a.addend = static_cast<const bf16_t*>(d->addend);
   a.colsum = d->colsum; a.colsumsq = d->colsumsq;
+  if (d->mode == 1 && d->bn_sums) {
+    TTMI_REQUIRE(d->bn_x && d->bn_mean && d->bn_rstd, "ttmi_conv2d: bn_sums needs bn_x, bn_mean, bn_rstd");
+    a.bn_gate = static_cast<const bf16_t*>(d->bn_gate);
+    a.bn_x = static_cast<const bf16_t*>(d->bn_x);
+    a.bn_mean = d->bn_mean; a.bn_rstd = d->bn_rstd; a.bn_sums = d->bn_sums;
+  }
   a.fC = fdiv_make(d->C); a.fKW = fdiv_make(d->KW);
   a.fWo = fdiv_make(Wo); a.fHo = fdiv_make(Ho); a.fCo = fdiv_make(d->Co);
   pl->splits = 1;
@@ -1108,7 +1240,7 @@ int conv_plan(const ttmi_conv_desc* d, ConvPlan* pl) {
     if (forced_bm()) pl->bm = forced_bm();
     int64_t dt = 0;
     for (int c = 0; c < S * S; ++c) dt += ((int64_t)a.cM[c] + 255) / 256 * (a.GN / pl->bn);
-    pl->dma = use_dma(dt, d->C) && (d->KH * d->KW > 1 || forced_dma() == 1);   // 1x1/2: reg tile
+    pl->dma = use_dma(dt, d->C);
   } else {
     a.GM = d->Co; a.GN = d->KH * d->KW * d->C; a.GK = (int)Mo;
     pl->bm = d->Co % 128 == 0 ? 128 : 64;
@@ -1147,7 +1279,7 @@ void launch_conv(const ConvPlan& pl, hipStream_t s) {
     return;
   }
   if constexpr (MODE != 2) if (pl.dma) {
-    const FtCfg f = ft_cfg();
+    const FtCfg f = ft_cfg(pl.bn);
     const unsigned gy = MODE == 1 ? (unsigned)(a.S * a.S) : 1u;
     const dim3 grid((unsigned)(((int64_t)a.GM + f.bm - 1) / f.bm * (a.GN / pl.bn)), gy);
 #define TTMI_FT(BM_, BN_, NS_)                                                                    \
@@ -1195,7 +1327,17 @@ extern "C" int ttmi_conv2d(const ttmi_conv_desc* d, hipStream_t stream) {
     launch_conv<0>(pl, stream);
   } else if (mode == 1) {
     TTMI_REQUIRE(d->dy && d->w && d->out, "ttmi_conv2d: DGRAD needs dy, w, out");
-    launch_conv<1>(pl, stream);
+    ConvPlan pr = pl;
+    if (!pl.dma) pr.a.bn_sums = nullptr;       // register tile: the reduction runs as its own pass
+    launch_conv<1>(pr, stream);
+    if (d->bn_sums && !pl.dma) {
+      rc = ttmi_check_launch("ttmi_conv2d/dgrad");
+      if (rc) return rc;
+      const uint16_t* o = static_cast<const uint16_t*>(d->out);
+      return ttmi_bn2d_bwd_reduce((int64_t)d->N * d->H * d->W, d->C, o, static_cast<const uint16_t*>(d->bn_gate),
+                                  static_cast<const uint16_t*>(d->bn_x), d->bn_mean, d->bn_rstd, d->bn_sums,
+                                  static_cast<uint16_t*>(d->out), stream);
+    }
   } else {
     TTMI_REQUIRE(d->x && d->dy && d->out, "ttmi_conv2d: WGRAD needs x, dy, out");
     TTMI_REQUIRE(d->workspace && d->workspace_bytes >= pl.ws_bytes,

@@ -61,7 +61,15 @@ class ConvDesc(ctypes.Structure):
                 ("Co", c_i), ("KH", c_i), ("KW", c_i), ("stride", c_i), ("pad", c_i),
                 ("x", c_p), ("dy", c_p), ("w", c_p), ("out", c_p), ("addend", c_p),
                 ("colsum", c_p), ("colsumsq", c_p), ("workspace", c_p),
-                ("workspace_bytes", ctypes.c_int64)]
+                ("workspace_bytes", ctypes.c_int64),
+                ("bn_gate", c_p), ("bn_x", c_p), ("bn_mean", c_p), ("bn_rstd", c_p),
+                ("bn_sums", c_p)]
+
+
+class ConvWPrep(ctypes.Structure):
+    """ttmi_conv_wprep (include/ttmi.h)."""
+    _fields_ = [("Co", c_i), ("Cin", c_i), ("Cp", c_i), ("KH", c_i), ("KW", c_i), ("s2d", c_i),
+                ("w", c_p), ("wf", c_p), ("wd", c_p)]
 
 
 class DisAttnDesc(ctypes.Structure):
@@ -254,11 +262,14 @@ SIGNATURES = {
     "ttmi_conv2d_workspace": (ctypes.c_int64, [c_p]),
     "ttmi_conv_weight_prep": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_nchw_to_nhwc": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
+    "ttmi_conv_weight_prep_batch": (c_i, [c_i, c_p, c_p]),
     "ttmi_stem_s2d": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
     "ttmi_stem_weight_prep": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p]),
     "ttmi_bn2d_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_i,
                             c_p, c_p, c_p, c_p]),
     "ttmi_bn2d_bwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_bn2d_bwd_reduce": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_bn2d_bwd_apply": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_maxpool_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_maxpool_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "ttmi_stem_pool_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p,

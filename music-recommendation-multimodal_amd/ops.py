@@ -317,8 +317,11 @@ CONV_STAT_REPS = 16    # TTMI_CONV_STAT_REPS: BatchNorm column stats are [16][C]
 def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int, stride: int,
            pad: int, *, x: Optional[Tensor] = None, dy: Optional[Tensor] = None,
            w: Optional[Tensor] = None, out: Tensor, addend: Optional[Tensor] = None,
-           colsum: Optional[Tensor] = None, colsumsq: Optional[Tensor] = None) -> Tensor:
-    """Implicit-GEMM conv (include/ttmi.h ttmi_conv2d): FWD y = conv(x), DGRAD dx, WGRAD dW."""
+           colsum: Optional[Tensor] = None, colsumsq: Optional[Tensor] = None,
+           bn: Optional[Tuple[Optional[Tensor], Tensor, Tensor, Tensor, Tensor]] = None) -> Tensor:
+    """Implicit-GEMM conv (include/ttmi.h ttmi_conv2d): FWD y = conv(x), DGRAD dx, WGRAD dW.
+    DGRAD ``bn`` = (gate, x, mean, rstd, sums): the backward reduction of the BatchNorm(+ReLU)
+    that produced the conv input, fused into the epilogue (out then holds the gated g)."""
     Ho, Wo = conv_out_hw(H, W, k, stride, pad)
     xn = N * (H // 2) * (W // 2) * C if mode in (STEM_FWD, STEM_WGRAD) else N * H * W * C
     need = {"x": (x, xn), "dy": (dy, N * Ho * Wo * Co),
@@ -343,6 +346,16 @@ def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int,
     d.stride, d.pad = stride, pad
     d.x, d.dy, d.w, d.out, d.addend = _p(x), _p(dy), _p(w), _p(out), _p(addend)
     d.colsum, d.colsumsq = _p(colsum), _p(colsumsq)
+    if bn is not None:
+        if mode != DGRAD:
+            raise ValueError("conv2d: bn (fused BatchNorm-backward reduction) is a DGRAD option")
+        gate, bx, bmean, brstd, bsums = bn
+        n_in = N * H * W * C
+        if bx.numel() < n_in or (gate is not None and gate.numel() < n_in):
+            raise ValueError("conv2d: bn gate / x smaller than the DGRAD output")
+        if bsums.numel() < 2 * CONV_STAT_REPS * C or bsums.dtype != torch.int64:
+            raise ValueError(f"conv2d: bn sums needs [{CONV_STAT_REPS}][{2 * C}] int64 replica rows")
+        d.bn_gate, d.bn_x, d.bn_mean, d.bn_rstd, d.bn_sums = _p(gate), _p(bx), _p(bmean), _p(brstd), _p(bsums)
     ws = None
     if mode in (WGRAD, STEM_WGRAD):
         _L.load()
@@ -360,6 +373,19 @@ def conv_weight_prep(w: Tensor, Cp: int, wf: Tensor, wd: Optional[Tensor] = None
     wd [Cin, k, k, Co]."""
     Co, Cin, KH, KW = w.shape
     call("ttmi_conv_weight_prep", Co, Cin, Cp, KH, KW, _p(w), _p(wf), _p(wd), _s())
+
+
+def conv_weight_prep_batch(items) -> None:
+    """All mirrors in one launch (ttmi_conv_weight_prep_batch): items = [(w, Cp, wf, wd, s2d)]
+    with w torch's fp32 [Co, Cin, k, k]; s2d: the stem's 4x4 space-to-depth mirror."""
+    arr = (_L.ConvWPrep * max(1, len(items)))()
+    for i, (w, Cp, wf, wd, s2d) in enumerate(items):
+        Co, Cin, KH, KW = w.shape
+        n = Co * (16 if s2d else KH * KW) * Cp
+        if wf.numel() < n or (wd is not None and wd.numel() < Co * Cin * KH * KW) or not w.is_contiguous():
+            raise ValueError(f"conv_weight_prep_batch: item {i} buffers / layout")
+        arr[i] = _L.ConvWPrep(Co, Cin, Cp, KH, KW, int(s2d), w.data_ptr(), wf.data_ptr(), _p(wd) or 0)
+    call("ttmi_conv_weight_prep_batch", len(items), ctypes.addressof(arr), _s())
 
 
 def nchw_to_nhwc(x: Tensor, Cp: int, y: Tensor) -> Tensor:
@@ -452,6 +478,21 @@ def stem_pool_bwd(dy: Tensor, idx: Tensor, x: Tensor, mean: Tensor, rstd: Tensor
         raise ValueError("stem_pool_bwd: dy / idx / dx too small")
     call("ttmi_stem_pool_bwd", N, H, W, C, _p(dy), _p(idx), _p(x), _p(mean), _p(rstd), _p(w), _p(b),
          _p(sums), _p(dx), _p(dw), _p(db), _s())
+    return dx
+
+
+def bn2d_bwd_apply(g: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor, sums: Tensor,
+                   dx: Tensor, dw: Optional[Tensor], db: Optional[Tensor]) -> Tensor:
+    """Second pass of bn2d_bwd on an already-gated g whose sums were accumulated elsewhere
+    (conv2d(..., bn=...)): dx = w·rstd·(g − Σg/M − x̂·Σgx̂/M); dw, db += the sums."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    if sums.numel() < 2 * CONV_STAT_REPS * C or sums.dtype != torch.int64:
+        raise ValueError(f"bn2d_bwd_apply: sums needs [{CONV_STAT_REPS}][{2 * C}] int64 replica rows")
+    if g.numel() < x.numel() or dx.numel() < x.numel():
+        raise ValueError("bn2d_bwd_apply: g / dx smaller than x")
+    call("ttmi_bn2d_bwd_apply", M, C, _p(g), None, _p(x), _p(mean), _p(rstd), _p(w), _p(sums), _p(dx),
+         _p(dw), _p(db), _s())
     return dx
 
 

@@ -218,6 +218,80 @@ def test_stem_pool_fused(gpu_pkg, N, H, W):
     assert rel(dx2.float(), dx1.float()) < 8e-3
 
 
+@pytest.mark.parametrize("variant", ["reg", "dma"])
+@pytest.mark.parametrize("N,C,H,W,Co,s,gate,add", [(2, 64, 14, 14, 64, 1, True, False),
+                                                  (3, 64, 15, 13, 128, 2, True, True),
+                                                  (2, 128, 9, 11, 128, 1, False, True)])
+def test_dgrad_fused_bn_reduce(gpu_pkg, monkeypatch, variant, N, C, H, W, Co, s, gate, add):
+    """DGRAD with the producing BatchNorm's backward reduction in its epilogue
+    (ttmi_conv_desc.bn_sums) against DGRAD + ttmi_bn2d_bwd_reduce: the gated g bit-identical,
+    the fixed-point sums to fp32 partial-sum order; then bn2d_bwd_apply(g) = bn2d_bwd."""
+    monkeypatch.setenv("TTMI_CONV_DMA", "1" if variant == "dma" else "0")
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(N * 7 + C + Co)
+    R = ops.CONV_STAT_REPS
+    Ho, Wo = ops.conv_out_hw(H, W, 3, s, 1)
+    dy = torch.randn(N, Ho, Wo, Co, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(C, 3, 3, Co, generator=g) / math.sqrt(9 * Co)).to(torch.bfloat16).to(DEV)
+    bx = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).to(DEV)
+    bgate = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).to(DEV) if gate else None
+    addend = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).to(DEV) if add else None
+    mean = torch.randn(C, generator=g).to(DEV) * 0.1
+    rstd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    # unfused
+    dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    ops.conv2d(ops.DGRAD, N, H, W, C, C, Co, 3, s, 1, dy=dy, w=w, out=dx, addend=addend)
+    s1 = torch.zeros(2 * R * C, dtype=torch.int64, device=DEV)
+    g1 = torch.empty_like(dx)
+    wbn = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    dxa = torch.empty_like(dx)
+    dw1, db1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ops.bn2d_bwd(dx, bx, mean, rstd, wbn, s1, dxa, dw1, db1, gate=bgate, g_out=g1)
+    # fused
+    g2 = torch.empty_like(dx)
+    s2 = torch.zeros_like(s1)
+    ops.conv2d(ops.DGRAD, N, H, W, C, C, Co, 3, s, 1, dy=dy, w=w, out=g2, addend=addend,
+               bn=(bgate, bx, mean, rstd, s2))
+    dxb = torch.empty_like(dx)
+    dw2, db2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ops.bn2d_bwd_apply(g2, bx, mean, rstd, wbn, s2, dxb, dw2, db2)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g2)
+    t1 = s1.view(R, 2 * C).sum(0).double()
+    t2 = s2.view(R, 2 * C).sum(0).double()
+    assert rel(t2, t1) < 1e-5
+    assert rel(dw2, dw1) < 1e-5 and rel(db2, db1) < 1e-5
+    assert rel(dxb.float(), dxa.float()) < 8e-3
+
+
+def test_conv_weight_prep_batch(gpu_pkg):
+    """ttmi_conv_weight_prep_batch (one launch for every mirror of a network, split into
+    launches of TTMI_WPREP_MAX items) = the per-conv conv_weight_prep / stem_weight_prep."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(3)
+    shapes = [(64, 3, 7, 16, True), (64, 1, 7, 8, False)] + [(64 * (1 + i % 3), 64 * (1 + i % 2), 3 if i % 4 else 1,
+                                                              64 * (1 + i % 2), False) for i in range(27)]
+    items, ref = [], []
+    for Co, Cin, k, Cp, s2d in shapes:
+        w = torch.randn(Co, Cin, k, k, generator=g).to(DEV)
+        kk = 4 if s2d else k
+        wf = torch.full((Co, kk, kk, Cp), 7.0, device=DEV, dtype=torch.bfloat16)
+        wd = None if (s2d or Cin < 8) else torch.full((Cin, k, k, Co), 7.0, device=DEV, dtype=torch.bfloat16)
+        items.append((w, Cp, wf, wd, s2d))
+        rf = torch.empty_like(wf)
+        rd = None if wd is None else torch.empty_like(wd)
+        if s2d:
+            ops.stem_weight_prep(w, Cp, rf)
+        else:
+            ops.conv_weight_prep(w, Cp, rf, rd)
+        ref.append((rf, rd))
+    ops.conv_weight_prep_batch(items)
+    torch.cuda.synchronize()
+    for (w, Cp, wf, wd, s2d), (rf, rd) in zip(items, ref):
+        assert torch.equal(wf, rf)
+        assert (wd is None) or torch.equal(wd, rd)
+
+
 @pytest.mark.parametrize("C,relu,res", [(64, True, False), (128, True, True), (512, False, False)])
 def test_bn2d_fwd_bwd(gpu_pkg, C, relu, res):
     """BatchNorm2d (train) with stats from the conv epilogue's column sums, residual + ReLU,
