@@ -197,8 +197,11 @@ int ttmi_seq_embed_bwd(int B, int L, int D, int64_t V, const int64_t* ids, const
  *   pass history_mask, or history_ids when the mask is None), softmax, dropout on the
  *   probabilities (idx = ((b*H+h)*L+i)*L+j), O = P·V.  Query rows with no valid key give 0.
  * qkv [B*L, 3*H*Dh] (q|k|v, dtype), ctx [B*L, H*Dh] (dtype), lse [B*H*L] fp32 (+inf for
- * fully masked rows).  L <= 64, Dh <= 64, Dh % 8 == 0.
+ * fully masked rows).  L <= TTMI_ATTN_LMAX, Dh <= 64, Dh % 8 == 0; L <= 64 runs whole sequences
+ * in one LDS image (MFMA), 64 < L <= TTMI_ATTN_LMAX (ABI 17) the tiled long-sequence kernels
+ * (online softmax over 64-key blocks).  The one-query ttmi_mha_q1_* calls take the same range.
  * ---------------------------------------------------------------------------------- */
+#define TTMI_ATTN_LMAX 512
 int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                  const int64_t* key_valid, float drop_p, const uint64_t* drop_seed, void* ctx,
                  float* lse, hipStream_t stream);

@@ -638,7 +638,8 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
 int check_mha(const char* fn, int dtype, int B, int L, int H, int Dh, const void* qkv,
               const int64_t* kv) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "%s: bad dtype", fn);
-  TTMI_REQUIRE(B >= 0 && L > 0 && L <= LP && H > 0, "%s: need 0 < L <= %d (got L=%d)", fn, LP, L);
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= TTMI_ATTN_LMAX && H > 0, "%s: need 0 < L <= %d (got L=%d)", fn,
+               TTMI_ATTN_LMAX, L);
   TTMI_REQUIRE(Dh > 0 && Dh <= 64 && Dh % 8 == 0, "%s: need Dh %% 8 == 0 and Dh <= 64 (got %d)", fn, Dh);
   TTMI_REQUIRE(qkv && kv, "%s: null argument", fn);
   TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "%s: qkv must be 16-byte aligned", fn);
@@ -657,6 +658,7 @@ extern "C" int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* 
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_mha_fwd: drop_p out of [0,1)");
   if (B == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
+  if (L > LP) return attn_long_fwd(dtype, B, L, H, Dh, qkv, key_valid, dp, ctx, lse, s);
   if (dtype == TTMI_BF16 && (Dh == 32 || Dh == 64) && !getenv("TTMI_MHA_V1")) {
     TTMI_REQUIRE(((uintptr_t)ctx & 7) == 0, "ttmi_mha_fwd: ctx must be 8-byte aligned");
     const float sc = 1.f / sqrtf((float)Dh);
@@ -686,6 +688,7 @@ extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* 
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_mha_bwd: drop_p out of [0,1)");
   if (B == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
+  if (L > LP) return attn_long_bwd(dtype, B, L, H, Dh, qkv, key_valid, lse, dctx, dp, dqkv, s);
   if (dtype == TTMI_BF16 && (Dh == 32 || Dh == 64) && !getenv("TTMI_MHA_V1")) {
     TTMI_REQUIRE(((uintptr_t)dqkv & 7) == 0, "ttmi_mha_bwd: dqkv must be 8-byte aligned");
     const float sc = 1.f / sqrtf((float)Dh);

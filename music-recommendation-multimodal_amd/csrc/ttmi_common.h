@@ -116,6 +116,19 @@ static inline DropParams make_drop(float p, const uint64_t* seed) {
   return d;
 }
 
+// ---------------------------------------------------------------- long-sequence attention
+// ttmi_attn_long.hip: the attention entry points' path for 64 < L <= TTMI_ATTN_LMAX.
+int attn_long_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv, const int64_t* kv, DropParams dp,
+                  void* ctx, float* lse, hipStream_t s);
+int attn_long_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv, const int64_t* kv, const float* lse,
+                  const void* dctx, DropParams dp, void* dqkv, hipStream_t s);
+int attn_long_q1_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv, const int64_t* kv, int32_t* rows,
+                     const float* x, float* x_rows, bool gather, DropParams dp, void* ctx, float* lse,
+                     hipStream_t s);
+int attn_long_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv, const int64_t* kv,
+                     const int32_t* rows, const float* lse, const void* dctx, DropParams dp, void* dqkv,
+                     hipStream_t s);
+
 // ---------------------------------------------------------------- deterministic scatter-add
 // Sums whose adders arrive in no fixed order (embedding-row scatters, column statistics over
 // many workgroups) accumulate in int64 fixed point: integer addition is associative, so the

@@ -287,8 +287,9 @@ extern "C" int ttmi_mha_q1_fwd(int dtype, int B, int L, int H, int Dh, const voi
                                const int64_t* key_valid, const int32_t* rows, float drop_p,
                                const uint64_t* drop_seed, void* ctx, float* lse, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_fwd: bad dtype");
-  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0,
-               "ttmi_mha_q1_fwd: need L <= 64, Dh <= 64, Dh %% 8 == 0");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= TTMI_ATTN_LMAX && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0 &&
+                   (int64_t)B * H * L * L < (1LL << 32),
+               "ttmi_mha_q1_fwd: need L <= %d, Dh <= 64, Dh %% 8 == 0", TTMI_ATTN_LMAX);
   TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "ttmi_mha_q1_fwd: qkv must be 16-byte aligned");
   TTMI_REQUIRE(qkv && key_valid && rows && ctx && lse, "ttmi_mha_q1_fwd: null argument");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
@@ -297,6 +298,7 @@ extern "C" int ttmi_mha_q1_fwd(int dtype, int B, int L, int H, int Dh, const voi
   DropParams dp = make_drop(drop_p, drop_seed);
   const float scale = 1.f / sqrtf((float)Dh);
   int32_t* rw = const_cast<int32_t*>(rows);          // read only (GATHER = false)
+  if (L > 64) return attn_long_q1_fwd(dtype, B, L, H, Dh, qkv, key_valid, rw, nullptr, nullptr, false, dp, ctx, lse, s);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL((mha_q1_fwd_kernel<bf16_t, false>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
                        (const bf16_t*)qkv, key_valid, rw, nullptr, nullptr, dp, (bf16_t*)ctx, lse, scale);
@@ -311,8 +313,9 @@ extern "C" int ttmi_mha_q1_gather_fwd(int dtype, int B, int L, int H, int Dh, co
                                       float* x_rows, float drop_p, const uint64_t* drop_seed,
                                       void* ctx, float* lse, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_gather_fwd: bad dtype");
-  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0,
-               "ttmi_mha_q1_gather_fwd: need L <= 64, Dh <= 64, Dh %% 8 == 0");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= TTMI_ATTN_LMAX && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0 &&
+                   (int64_t)B * H * L * L < (1LL << 32),
+               "ttmi_mha_q1_gather_fwd: need L <= %d, Dh <= 64, Dh %% 8 == 0", TTMI_ATTN_LMAX);
   TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "ttmi_mha_q1_gather_fwd: qkv must be 16-byte aligned");
   TTMI_REQUIRE(qkv && key_valid && x && rows && x_rows && ctx && lse, "ttmi_mha_q1_gather_fwd: null argument");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || drop_seed),
@@ -320,6 +323,7 @@ extern "C" int ttmi_mha_q1_gather_fwd(int dtype, int B, int L, int H, int Dh, co
   if (B == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
   const float scale = 1.f / sqrtf((float)Dh);
+  if (L > 64) return attn_long_q1_fwd(dtype, B, L, H, Dh, qkv, key_valid, rows, x, x_rows, true, dp, ctx, lse, s);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL((mha_q1_fwd_kernel<bf16_t, true>), dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
                        (const bf16_t*)qkv, key_valid, rows, x, x_rows, dp, (bf16_t*)ctx, lse, scale);
@@ -334,8 +338,9 @@ extern "C" int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const voi
                                const void* dctx, float drop_p, const uint64_t* drop_seed,
                                void* dqkv, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_mha_q1_bwd: bad dtype");
-  TTMI_REQUIRE(B >= 0 && L > 0 && L <= 64 && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0,
-               "ttmi_mha_q1_bwd: need L <= 64, Dh <= 64, Dh %% 8 == 0");
+  TTMI_REQUIRE(B >= 0 && L > 0 && L <= TTMI_ATTN_LMAX && H > 0 && Dh > 0 && Dh <= 64 && Dh % 8 == 0 &&
+                   (int64_t)B * H * L * L < (1LL << 32),
+               "ttmi_mha_q1_bwd: need L <= %d, Dh <= 64, Dh %% 8 == 0", TTMI_ATTN_LMAX);
   TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "ttmi_mha_q1_bwd: qkv must be 16-byte aligned");
   TTMI_REQUIRE(qkv && key_valid && rows && lse && dctx && dqkv, "ttmi_mha_q1_bwd: null argument");
   TTMI_REQUIRE(((uintptr_t)dqkv & 15) == 0, "ttmi_mha_q1_bwd: dqkv must be 16-byte aligned");
@@ -344,6 +349,7 @@ extern "C" int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const voi
   if (B == 0) return TTMI_OK;
   DropParams dp = make_drop(drop_p, drop_seed);
   const float scale = 1.f / sqrtf((float)Dh);
+  if (L > 64) return attn_long_q1_bwd(dtype, B, L, H, Dh, qkv, key_valid, rows, lse, dctx, dp, dqkv, s);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(mha_q1_bwd_kernel<bf16_t>, dim3(B * H), dim3(64), 0, s, B, L, H, Dh,
                        (const bf16_t*)qkv, key_valid, rows, lse, (const bf16_t*)dctx, dp,

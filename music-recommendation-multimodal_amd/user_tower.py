@@ -22,6 +22,7 @@ import torch.nn as nn
 
 from . import functional as F
 from . import ops
+from .ops import ATTN_LMAX
 
 Tensor = torch.Tensor
 
@@ -135,10 +136,11 @@ class SequentialUserEncoder(nn.Module):
         if embedding_dim % num_heads:
             raise ValueError("embedding_dim must be divisible by num_heads")
         # the attention kernels (ttmi_attn.hip) keep a whole sequence's K/V head slice in one
-        # workgroup's LDS: reject other shapes here, not mid-epoch at the first launch
+        # workgroup's LDS up to 64 positions and tile longer ones over 64-key blocks
+        # (ttmi_attn_long.hip) up to TTMI_ATTN_LMAX: reject other shapes here, not mid-epoch
         d_h = embedding_dim // num_heads
-        if not 0 < max_seq_len <= 64:
-            raise ValueError(f"max_seq_len must be in [1, 64] (got {max_seq_len})")
+        if not 0 < max_seq_len <= ATTN_LMAX:
+            raise ValueError(f"max_seq_len must be in [1, {ATTN_LMAX}] (got {max_seq_len})")
         if d_h > 64 or d_h % 8:
             raise ValueError(f"head width embedding_dim / num_heads must be a multiple of 8 "
                              f"and <= 64 (got {d_h})")

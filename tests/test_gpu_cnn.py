@@ -144,10 +144,12 @@ def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W, N):
     0.98 at layer4 and 1.0 at fc, at 8x64x96 and at 32x128x128 alike — the train-mode BN
     backward over 20 layers amplifies bf16 storage noise.  So per parameter the GPU gradient
     must be as close to fp32 as the emulation is (cosine within 0.03 of it — 0.05 for the
-    BatchNorm2d weights and biases, which carry that amplified noise: at 1x128x256, N = 4 the
-    summation order alone moves layer1.1.bn1.weight's cosine from 0.91 (register-staged conv
-    tiles) to 0.877 (LDS-DMA tiles) against the emulation's 0.908; norm deviation within 2x the
-    emulation's + 10 %); the output must agree to 5e-2 (fp32) / 2e-2 (emulation)."""
+    BatchNorm2d weights and biases, which carry that amplified noise: the summation order alone
+    moves the worst BatchNorm parameter from 0.016 (register-staged conv tiles) to 0.031
+    (LDS-DMA tiles) below the emulation's cosine at 1x128x256, N = 4, and from 0.028 to 0.041 at
+    3x224², while every conv and fc weight stays inside 0.03 — tools/diag_resnet_margin.py;
+    norm deviation within 2x the emulation's + 10 %); the output must agree to 5e-2 (fp32) /
+    2e-2 (emulation)."""
     cnn = gpu_pkg.cnn
     torch.manual_seed(in_ch)
     net = cnn.ResNet18(in_ch, 128).to(DEV)

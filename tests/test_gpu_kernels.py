@@ -347,7 +347,8 @@ def masks(B, L, g):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (3, 1, 4, 16)])
+@pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (3, 1, 4, 16),
+                                      (4, 65, 2, 32), (3, 200, 4, 32), (2, 130, 2, 64), (2, 512, 1, 8)])
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
     ops = gpu_pkg.ops
@@ -375,7 +376,8 @@ def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64)])
+@pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (5, 150, 4, 32),
+                                      (3, 300, 2, 64)])
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_mha_single_query_matches_full_row(gpu_pkg, dtype, B, L, H, Dh, p):
     """ttmi_mha_q1_* (pruned last layer) == the full attention restricted to each
@@ -430,7 +432,8 @@ def test_last_rows_gather(gpu_pkg, D):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,L,H,Dh,p", [(37, 50, 4, 32, 0.1), (8, 64, 2, 64, 0.0), (5, 7, 2, 8, 0.2)])
+@pytest.mark.parametrize("B,L,H,Dh,p", [(37, 50, 4, 32, 0.1), (8, 64, 2, 64, 0.0), (5, 7, 2, 8, 0.2),
+                                        (9, 100, 4, 32, 0.1)])
 def test_mha_q1_gather_fwd(gpu_pkg, dtype, B, L, H, Dh, p):
     """ttmi_mha_q1_gather_fwd == ttmi_last_rows_gather + ttmi_mha_q1_fwd bit for bit (rows,
     gathered residual rows, ctx, lse), incl. empty and full histories."""

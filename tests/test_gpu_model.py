@@ -255,10 +255,13 @@ def test_cfg2_loss_parity_full_size(gpu_pkg, dtype, tol):
     assert rel(logits, logits_ref) < (3e-2 if dtype == torch.bfloat16 else 1e-4)
 
 
-def test_dropout_on_matches_oracle_hash(gpu_pkg):
-    """Dropout ON (p=0.1 at every site) — kernels' masks vs the oracle's restatement."""
+@pytest.mark.parametrize("L", [20, 150])
+def test_dropout_on_matches_oracle_hash(gpu_pkg, L):
+    """Dropout ON (p=0.1 at every site) — kernels' masks vs the oracle's restatement.  L = 150
+    runs the long-sequence attention (ttmi_attn_long.hip: tiled full attention in layer 0, the
+    one-query kernel in the pruned layer 1)."""
     F = gpu_pkg.functional
-    m, batch = _cfg2(gpu_pkg, torch.float32, B=64, L=20, V=997, p=0.1, seed=3)
+    m, batch = _cfg2(gpu_pkg, torch.float32, B=64, L=L, V=997, p=0.1, seed=3)
     seeds = F.site_seeds(0x5EED, 1)
     table = F.seed_table(seeds, DEV)
     lref, _ = _oracle_loss(m, batch, drop=ref.HashDropout(seeds), p=0.1)
