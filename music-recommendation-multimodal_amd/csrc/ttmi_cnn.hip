@@ -504,6 +504,76 @@ TTMI_DEV void stem_grad8(const StemBn& s, int64_t i, int cpr, int H, int W, int 
   }
 }
 
+// Even H, W: a thread owns a 2x2 quad of conv-output pixels (2t+dh, 2u+dw) x 8 channels.
+// The quad's pixels lie in the pool windows (t or t+1) x (u or u+1) only — row 2t in window
+// t (tap 1), row 2t+1 in t (tap 2) and t+1 (tap 0) — so 4 window loads serve 4 pixels (the
+// per-pixel gather issued 9 for the same quad).  Sums run in (ho, wo) order as maxpool_bwd's.
+template <typename F>
+TTMI_DEV void stem_quad_grad(const StemBn& s, int64_t q, int cpr, int H, int W, int Ho, int Wo,
+                             const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                             const bf16_t* __restrict__ x, F&& use) {   // use(pix, g[8], xv[8])
+  const int cg = (int)(q % cpr);
+  int64_t t = q / cpr;
+  const int W2 = W >> 1, H2 = H >> 1;
+  const int u = (int)(t % W2); t /= W2;
+  const int tq = (int)(t % H2);
+  const int bb = (int)(t / H2);
+  uint4 qx[4], qd[2][2];
+  uint2 qa[2][2];
+  int64_t pix[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int h = 2 * tq + (p >> 1), w = 2 * u + (p & 1);
+    pix[p] = (((int64_t)bb * H + h) * W + w) * cpr + cg;
+    qx[p] = reinterpret_cast<const uint4*>(x)[pix[p]];
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2) {
+      const int ho = min(tq + a, Ho - 1), wo = min(u + b2, Wo - 1);
+      const int64_t o = (((int64_t)bb * Ho + ho) * Wo + wo) * cpr + cg;
+      qd[a][b2] = reinterpret_cast<const uint4*>(dy)[o];
+      qa[a][b2] = reinterpret_cast<const uint2*>(idx)[o];
+    }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int dh = p >> 1, dw = p & 1;
+    float g[8], xv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = 0.f;
+    // windows of this pixel, ascending: row a = 0 (tap 1 + dh) and, for dh = 1, a = 1 (tap 0)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a == 1 && (dh == 0 || tq + 1 >= Ho)) continue;
+      const int kh = a == 0 ? 1 + dh : 0;
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2) {
+        if (b2 == 1 && (dw == 0 || u + 1 >= Wo)) continue;
+        const int kw = b2 == 0 ? 1 + dw : 0;
+        const uint8_t tap = (uint8_t)(kh * 3 + kw);
+        float d[8];
+        unpack8(qd[a][b2], d);
+        const uint2 aa = qa[a][b2];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t ae = (uint8_t)(((e < 4 ? aa.x : aa.y) >> (8 * (e & 3))) & 0xFF);
+          if (ae == tap) g[e] += d[e];
+        }
+      }
+    }
+    float av[8];
+    stem_act8(s, cg * 8, qx[p], av);
+    unpack8(qx[p], xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      g[e] = bf2f(f2bf(g[e]));                        // maxpool_bwd stores dpool in bf16
+      if (!(av[e] > 0.f)) g[e] = 0.f;
+    }
+    use(pix[p], g, xv);
+  }
+}
+
 TTMI_DEV void stem_coeffs_bwd(StemBn& s, int C, const float* mean, const float* rstd, const float* w,
                               const float* b) {
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -614,6 +684,111 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_apply_kernel(int N, int H, 
       o[e] = sk[c] * (g[e] - sm1[c] - xh * sm2[c]);
     }
     reinterpret_cast<uint4*>(dx)[i] = pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_quad_bwd_reduce_kernel(int N, int H, int W, int C, int Ho, int Wo,
+                                                                   const bf16_t* __restrict__ dy,
+                                                                   const uint8_t* __restrict__ idx,
+                                                                   const bf16_t* __restrict__ x,
+                                                                   const float* __restrict__ mean,
+                                                                   const float* __restrict__ rstd,
+                                                                   const float* __restrict__ w,
+                                                                   const float* __restrict__ b,
+                                                                   int64_t* __restrict__ sums,
+                                                                   int64_t quads_per_block) {
+  __shared__ StemBn s;
+  __shared__ float red[2][256][8];
+  stem_coeffs_bwd(s, C, mean, rstd, w, b);
+  __syncthreads();
+  const int64_t NQ = (int64_t)N * (H / 2) * (W / 2);
+  const int cpr = C / 8;
+  const int tpr = 256 / cpr > 0 ? 256 / cpr : 1;
+  const int t = threadIdx.x;
+  const int cg = t % cpr, rl = t / cpr;
+  const int c0 = cg * 8;
+  float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mu[e] = cg < cpr ? mean[c0 + e] : 0.f; rs[e] = cg < cpr ? rstd[c0 + e] : 0.f; }
+  const int64_t q0 = (int64_t)blockIdx.x * quads_per_block, q1 = min(NQ, q0 + quads_per_block);
+  if (rl < tpr && cg < cpr) {
+    for (int64_t qq = q0 + rl; qq < q1; qq += tpr) {
+      stem_quad_grad(s, qq * cpr + cg, cpr, H, W, Ho, Wo, dy, idx, x,
+                     [&](int64_t, const float* g, const float* xv) {
+#pragma unroll
+                       for (int e = 0; e < 8; ++e) {
+                         s1[e] += g[e];
+                         s2[e] += g[e] * (xv[e] - mu[e]) * rs[e];
+                       }
+                     });
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][t][e] = s1[e]; red[1][t][e] = s2[e]; }
+  __syncthreads();
+  if (t < cpr) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < tpr; ++r) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a[e] += red[0][r * cpr + t][e]; bb[e] += red[1][r * cpr + t][e]; }
+    }
+    int64_t* rep = sums + (int64_t)(blockIdx.x % TTMI_CONV_STAT_REPS) * 2 * C;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      fx_add(rep + t * 8 + e, a[e], TTMI_FX_GRAD);
+      fx_add(rep + C + t * 8 + e, bb[e], TTMI_FX_GRAD);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_quad_bwd_apply_kernel(int N, int H, int W, int C, int Ho, int Wo,
+                                                                  const bf16_t* __restrict__ dy,
+                                                                  const uint8_t* __restrict__ idx,
+                                                                  const bf16_t* __restrict__ x,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ rstd,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ b,
+                                                                  const int64_t* __restrict__ sums,
+                                                                  bf16_t* __restrict__ dx, float* dw, float* db) {
+  __shared__ StemBn s;
+  __shared__ float sk[MAXC], sm1[MAXC], sm2[MAXC], smu[MAXC], srs[MAXC];
+  const int64_t M = (int64_t)N * H * W;
+  const float invM = 1.f / (float)M;
+  stem_coeffs_bwd(s, C, mean, rstd, w, b);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    long long q1 = 0, q2 = 0;
+    for (int r = 0; r < TTMI_CONV_STAT_REPS; ++r) {
+      q1 += sums[(int64_t)r * 2 * C + c];
+      q2 += sums[(int64_t)r * 2 * C + C + c];
+    }
+    const float t1 = fx_to_f(q1, TTMI_FX_GRAD), t2 = fx_to_f(q2, TTMI_FX_GRAD);
+    sk[c] = w[c] * rstd[c];
+    sm1[c] = t1 * invM;
+    sm2[c] = t2 * invM;
+    smu[c] = mean[c];
+    srs[c] = rstd[c];
+    if (blockIdx.x == 0) {
+      if (db) db[c] += t1;
+      if (dw) dw[c] += t2;
+    }
+  }
+  __syncthreads();
+  const int cpr = C / 8;
+  const int64_t n = (int64_t)N * (H / 2) * (W / 2) * cpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpr) * 8;
+    stem_quad_grad(s, i, cpr, H, W, Ho, Wo, dy, idx, x, [&](int64_t pix, const float* g, const float* xv) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        const float xh = (xv[e] - smu[c]) * srs[c];
+        o[e] = sk[c] * (g[e] - sm1[c] - xh * sm2[c]);
+      }
+      reinterpret_cast<uint4*>(dx)[pix] = pack8(o);
+    });
   }
 }
 
@@ -750,6 +925,19 @@ extern "C" int ttmi_stem_pool_bwd(int N, int H, int W, int C, const uint16_t* dy
   const int64_t M = (int64_t)N * H * W;
   const int cpr = C / 8;
   const int tpr = std::max(1, 256 / cpr);
+  if (H % 2 == 0 && W % 2 == 0) {                   // 2x2 quads per thread
+    const int64_t NQ = M / 4;
+    int64_t qb = std::min<int64_t>(8192, (NQ + tpr - 1) / tpr);
+    qb = std::max<int64_t>(qb, 1);
+    const int64_t qpb = (NQ + qb - 1) / qb;
+    hipLaunchKernelGGL(stem_quad_bwd_reduce_kernel, dim3((unsigned)((NQ + qpb - 1) / qpb)), dim3(256), 0, s, N, H,
+                       W, C, Ho, Wo, (const bf16_t*)dy, idx, (const bf16_t*)x, mean, rstd, w, b, sums, qpb);
+    int rc = ttmi_check_launch("ttmi_stem_pool_bwd/reduce");
+    if (rc) return rc;
+    hipLaunchKernelGGL(stem_quad_bwd_apply_kernel, dim3(grid_for(NQ * C / 8)), dim3(256), 0, s, N, H, W, C, Ho,
+                       Wo, (const bf16_t*)dy, idx, (const bf16_t*)x, mean, rstd, w, b, sums, (bf16_t*)dx, dw, db);
+    return ttmi_check_launch("ttmi_stem_pool_bwd/apply");
+  }
   int64_t blocks = std::min<int64_t>(8192, (M + tpr * 4 - 1) / (tpr * 4));
   blocks = std::max<int64_t>(blocks, 1);
   const int64_t rpb = (M + blocks - 1) / blocks;

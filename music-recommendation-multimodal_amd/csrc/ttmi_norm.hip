@@ -544,7 +544,7 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(int B, int C, const float* 
 // one column ONCE (all loads issued before any arithmetic), so the statistics, the
 // normalisation and the backward's two sums cost one HBM latency instead of B / 16 serial
 // dependent loads per pass.  Numerics equal the looped kernels (two-pass mean / variance).
-constexpr int BNR_COLS = 16, BNR_RG = 32;
+constexpr int BNR_COLS = 8, BNR_RG = 64;     // 8 columns: twice the workgroups of 16 (C = 512: 64 CUs)
 
 TTMI_DEV float bnr_colsum(float v, float (*red)[BNR_COLS], int rg, int cl) {
   __syncthreads();
