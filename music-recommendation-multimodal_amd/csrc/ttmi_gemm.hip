@@ -46,6 +46,7 @@ struct GemmArgs {
   int vec;           // 1: all row strides allow 4-wide vector epilogue accesses
   float* rowsum_a;   // rowsum_a[m] += Σ_k A(m,k)  (bias grad of a weight-gradient GEMM)
   bf16_t* pre_out;   // act 2: the pre-activation (after bias) is also stored here (row stride ldc)
+  int wdma;          // panel kernel: stage W by LDS-DMA (set by launch_panel_t)
 };
 
 // Sum of the 8 bf16 / 4 f32 operand values a lane holds in one fragment.
@@ -325,6 +326,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 }
 
 
+template <int N_>
+TTMI_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
+
 // ------------------------------------------------ row-panel GEMM (skinny K, whole N per WG)
 // C[m, :] = epi(alpha * A[m, :K] · Wᵀ) for M >> N with N in {128,..,512}, K <= 512, both
 // operands k-major (nn.Linear forward; input grads through a transposed weight mirror).
@@ -514,7 +518,24 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
 #pragma unroll
     for (int c = 0; c < 4; ++c) a0[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
   }
-  {   // W -> LDS, coalesced 16-byte chunks, 8 loads in flight per thread before the LDS
+  if (g.wdma) {
+    // W -> LDS by LDS-DMA, every chunk in flight at once (no VGPR round trip): the image is
+    // a run of 16-byte chunks, K/8 + 1 per row (the last one is the row pad, filled with the
+    // buffer's out-of-range zeros); wave-instruction ii writes chunks [64 ii, 64 ii + 64)
+    constexpr int CPRP = K / 8 + 1, INSTR = N * CPRP / 64;
+    static_assert((N * CPRP) % 64 == 0, "whole DMA instructions");
+    const uint32_t wbytes = (uint32_t)(((int64_t)(N - 1) * g.ldb + K) * 2);
+    const i32x4_t rw = make_rsrc(g.B, wbytes);
+    const uint32_t base = lds_addr(smem);
+#pragma unroll
+    for (int t = 0; t < (INSTR + 7) / 8; ++t) {
+      const int ii = wave + 8 * t;
+      if (ii >= INSTR) break;                   // wave-uniform
+      const int q = ii * 64 + lane, n = q / CPRP, c = q % CPRP;
+      const uint32_t voff = c == K / 8 ? wbytes : (uint32_t)(((int64_t)n * g.ldb + 8 * c) * 2);
+      dma16(rw, voff, base + ii * 1024);
+    }
+  } else {   // W -> LDS, coalesced 16-byte chunks, 8 loads in flight per thread before the LDS
       // writes (a load -> wait -> write loop pays one memory round trip per chunk: 16 round
       // trips for a 128 KB W image, which used to be most of the kernel's time)
     constexpr int CPR = K / 8, TOT = N * CPR, PER = (TOT + 511) / 512, BATCH = PER <= 16 ? PER : 8;
@@ -538,6 +559,8 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
         }
       }
     }
+  }
+  {
     if constexpr (LNB) {
       for (int i = tid; i < N; i += 512) sbias[i] = ln.w[i];
       for (int i = tid; i < SROWS * N; i += 512) { sdw[i] = 0.f; sdb[i] = 0.f; }
@@ -553,6 +576,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   }
   const DropKeys dk = resolve_drop(g.drop);
   const DropKeys dk2 = resolve_drop(ln.drop);
+  if (g.wdma) wait_vm<0>();          // this wave's W DMAs landed (the barrier covers the rest)
   __syncthreads();
 
   // W fragment base for this lane (column-paired: tile 2p slot 4q+r <-> column 32p+8q+r)
@@ -774,8 +798,6 @@ struct WImg {
   }
 };
 
-template <int N_>
-TTMI_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
 // This wave's DMAs but the N_ youngest have landed and its LDS reads have returned; then
 // the workgroup barrier (one asm statement: no memory access moves across it).
 template <int N_>
@@ -1238,6 +1260,54 @@ TTMI_DEV void fold_store(const FoldSeg& sg, int64_t u, int64_t nq, float4 v) {
   *cp = v;
 }
 
+// P partitions of the S partials x 256/P units per block pass: partition q sums its splits in
+// split order, the P partition sums are added in partition order through LDS (deterministic
+// for a given S).  P = 4 for a weight gradient's ~12 splits; P = 16 for the many-partial
+// slabs (a LayerNorm's per-workgroup column sums, S ~ 229, 32-64 units), where 4 partitions
+// meant ~57 dependent loads per thread in 4 serial batches.
+constexpr int FOLD_WIDE_S = 32;
+template <int P>
+TTMI_DEV void fold_parts(const FoldSeg& sg, int bx, int nbx, bool consume, int64_t nel, int64_t nq) {
+  constexpr int U = 256 / P;
+  __shared__ float4 red[256];
+  const int ul = threadIdx.x % U, q = threadIdx.x / U;
+  const int s_lo = (int)((int64_t)sg.S * q / P), s_hi = (int)((int64_t)sg.S * (q + 1) / P);
+  for (int64_t ub = (int64_t)bx * U; ub < sg.units; ub += (int64_t)nbx * U) {
+    const int64_t u = ub + ul;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (u < nel) {
+      const int64_t m = u / nq, n = (u % nq) * 4;
+      v = fold_unit(sg, m * sg.N + n, s_lo, s_hi, consume);
+    } else if (u < sg.units) {
+      const int64_t m = u - nel;
+      for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
+        float w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = s0 + j < s_hi ? sg.part_rs[(s0 + j) * sg.M + m] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (s0 + j < s_hi) v.x += w[j];
+      }
+    }
+    red[q * U + ul] = v;
+    __syncthreads();
+    if (q == 0 && u < sg.units) {
+#pragma unroll
+      for (int k = 1; k < P; ++k) {
+        const float4 w = red[k * U + ul];
+        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+      }
+      if (u < nel) {
+        fold_store(sg, u, nq, v);
+      } else {
+        const int64_t m = u - nel;
+        sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v.x : v.x;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   (void)a;
   // segment k owns blocks [blk_begin[k], blk_begin[k+1]) of the flat grid (each sized to its
@@ -1269,43 +1339,8 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
     }
     return;
   }
-  __shared__ float4 red[4][64];
-  const int ul = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int s_lo = (int)((int64_t)sg.S * q / 4), s_hi = (int)((int64_t)sg.S * (q + 1) / 4);
-  for (int64_t ub = (int64_t)bx * 64; ub < sg.units; ub += (int64_t)nbx * 64) {
-    const int64_t u = ub + ul;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (u < nel) {
-      const int64_t m = u / nq, n = (u % nq) * 4;
-      v = fold_unit(sg, m * sg.N + n, s_lo, s_hi, consume);
-    } else if (u < sg.units) {
-      const int64_t m = u - nel;
-      for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
-        float w[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = s0 + j < s_hi ? sg.part_rs[(s0 + j) * sg.M + m] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (s0 + j < s_hi) v.x += w[j];
-      }
-    }
-    red[q][ul] = v;
-    __syncthreads();
-    if (q == 0 && u < sg.units) {
-#pragma unroll
-      for (int k = 1; k < 4; ++k) {
-        const float4 w = red[k][ul];
-        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-      }
-      if (u < nel) {
-        fold_store(sg, u, nq, v);
-      } else {
-        const int64_t m = u - nel;
-        sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v.x : v.x;
-      }
-    }
-    __syncthreads();
-  }
+  if (sg.S > FOLD_WIDE_S) fold_parts<16>(sg, bx, nbx, consume, nel, nq);
+  else fold_parts<4>(sg, bx, nbx, consume, nel, nq);
 }
 
 // ------------------------------------------- large token GEMM: 256x256x64 tiles, 8 waves
@@ -1820,7 +1855,13 @@ void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBw
   const int64_t tiles = (a.M + 15) / 16;
   const int64_t tpw = std::max<int64_t>(1, (tiles + num_cus() - 1) / num_cus());
   const int64_t grid = (tiles + tpw - 1) / tpw;
-  hipLaunchKernelGGL((panel_kernel<NT, KC, EPI>), dim3((unsigned)grid), dim3(512), 0, s, a, (int)tpw, ln);
+  static const int wdma = [] {            // TTMI_PANEL_WDMA=0: VGPR staging (A/B runs only)
+    const char* e = getenv("TTMI_PANEL_WDMA");
+    return e ? atoi(e) : 1;
+  }();
+  GemmArgs b = a;
+  b.wdma = wdma && a.ldb * 2 * a.N < ((int64_t)1 << 31);
+  hipLaunchKernelGGL((panel_kernel<NT, KC, EPI>), dim3((unsigned)grid), dim3(512), 0, s, b, (int)tpw, ln);
 }
 
 bool launch_panel(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
@@ -2065,7 +2106,7 @@ int launch_fold(FoldArgs& a, hipStream_t s) {
   if (a.n == 0 || a.total == 0) return TTMI_OK;
   a.blk_begin[0] = 0;
   for (int k = 0; k < a.n; ++k) {
-    const int per = a.seg[k].S <= 2 ? 256 : 64;           // units per block pass
+    const int per = a.seg[k].S <= 2 ? 256 : a.seg[k].S > FOLD_WIDE_S ? 16 : 64;   // units per block pass
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((a.seg[k].units + per - 1) / per, 1024));
     a.blk_begin[k + 1] = a.blk_begin[k] + (int)nb;
   }
@@ -2186,7 +2227,14 @@ extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int 
   const int tile = wgrad_group_cfg().tile;
   auto flush = [&]() -> int {
     if (grp.n == 0) return TTMI_OK;
-    if (tile == 128)
+    static const int ns = [] {               // TTMI_WGRAD_NS=5: 5-deep ring (tuning runs)
+      const char* e = getenv("TTMI_WGRAD_NS");
+      return e ? atoi(e) : 4;
+    }();
+    if (tile == 128 && ns == 5)
+      hipLaunchKernelGGL((wgrad_group_kernel<128, 128, 5>), dim3((unsigned)grp.wg_begin[grp.n]), dim3(256), 0,
+                         stream, grp);
+    else if (tile == 128)
       hipLaunchKernelGGL((wgrad_group_kernel<128, 128, 4>), dim3((unsigned)grp.wg_begin[grp.n]), dim3(256), 0,
                          stream, grp);
     else
