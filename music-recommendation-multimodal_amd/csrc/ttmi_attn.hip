@@ -457,14 +457,17 @@ __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_
     sum += __shfl_xor(sum, 32, 64);
     const float inv = sum > 0.f ? 1.f / sum : 0.f;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      // masked scores are 0 already, so the mask applies without a range check (the pair
+      // hash when L is even; identical to drop_keep per index)
+      bool kp[4] = {true, true, true, true};
+      if (dk.on) drop_keep4(dk, pbase + (uint32_t)(q * L + 16 * t + 4 * lg), kp);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float p = s[t][e] * inv;
-        const int k = 16 * t + 4 * lg + e;
-        if (dk.on && q < L && k < L) p = drop_apply(dk, pbase + (uint32_t)(q * L + k), p);
-        s[t][e] = p;
+        const float p = s[t][e] * inv;
+        s[t][e] = kp[e] ? (dk.on ? p * dk.scale : p) : 0.f;
       }
+    }
     f32x4_t o[DH / 16];
 #pragma unroll
     for (int u = 0; u < DH / 16; ++u) o[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -543,6 +546,7 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
     }
     const float lr = q < L ? lse[(int64_t)bh * L + q] : INFINITY;
     f32x4_t s[4], dpv[4];
+    uint32_t keep[4];                              // dropout keep bits, one hash pass
     float dsum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -554,6 +558,9 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
           Mma<bf16_t>::run(dpv[t], a_fk<G::P>(sV, 16 * t, c, lane), of[c]);
         }
       }
+      bool kp[4] = {true, true, true, true};
+      if (dk.on) drop_keep4(dk, pbase + (uint32_t)(q * L + 16 * t + 4 * lg), kp);
+      keep[t] = (kp[0] ? 1u : 0u) | (kp[1] ? 2u : 0u) | (kp[2] ? 4u : 0u) | (kp[3] ? 8u : 0u);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = 16 * t + 4 * lg + e;
@@ -562,7 +569,7 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
         float dP = 0.f;
         if (ok) {
           dP = dpv[t][e];
-          if (dk.on) dP = drop_keep(dk, pbase + (uint32_t)(q * L + k)) ? dP * dk.scale : 0.f;
+          if (dk.on) dP = kp[e] ? dP * dk.scale : 0.f;
         }
         s[t][e] = p;
         dpv[t][e] = dP;
@@ -577,12 +584,9 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
       f32x4_t pd;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = 16 * t + 4 * lg + e;
         const float p = s[t][e];
         ds[t][e] = p * (dpv[t][e] - dsum) * scale;
-        float x = p;
-        if (dk.on && p != 0.f) x = drop_keep(dk, pbase + (uint32_t)(q * L + k)) ? p * dk.scale : 0.f;
-        pd[e] = x;
+        pd[e] = dk.on ? (((keep[t] >> e) & 1u) ? p * dk.scale : 0.f) : p;
       }
       a_st4(sdS + q * G::SP + (16 * t + 4 * lg) * 2, ds[t]);
       a_st4(sPd + q * G::SP + (16 * t + 4 * lg) * 2, pd);

@@ -90,6 +90,20 @@ TTMI_DEV float drop_apply(const DropKeys& d, uint32_t idx, float v) {
   if (!d.on) return v;
   return drop_keep(d, idx) ? v * d.scale : 0.f;
 }
+// keep bits of the 4 consecutive indices idx0 .. idx0+3: two pair hashes when idx0 is even
+// (identical to drop_keep per index), else one hash per index.
+TTMI_DEV void drop_keep4(const DropKeys& d, uint32_t idx0, bool (&kp)[4]) {
+  if ((idx0 & 1) == 0) {
+    const uint32_t h0 = drop_hash(d, idx0 >> 1), h1 = drop_hash(d, (idx0 >> 1) + 1);
+    kp[0] = (h0 & 0xFFFFu) >= d.thresh;
+    kp[1] = (h0 >> 16) >= d.thresh;
+    kp[2] = (h1 & 0xFFFFu) >= d.thresh;
+    kp[3] = (h1 >> 16) >= d.thresh;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kp[e] = drop_keep(d, idx0 + e);
+  }
+}
 // v[0..NV) at consecutive indices idx0.. (one hash per aligned pair).
 template <int NV>
 TTMI_DEV void drop_apply_vec(const DropKeys& d, uint32_t idx0, float* v) {

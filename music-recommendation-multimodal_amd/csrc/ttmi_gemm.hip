@@ -1208,16 +1208,16 @@ TTMI_DEV float4 fold_unit(const FoldSeg& sg, int64_t off, int s_lo, int s_hi, bo
   if (sg.fx) {
     const int64_t* p = static_cast<const int64_t*>(sg.part) + off;
     long long q[4] = {0, 0, 0, 0};
-    for (int s0 = s_lo; s0 < s_hi; s0 += 8) {
-      longlong2 w[8][2];
+    for (int s0 = s_lo; s0 < s_hi; s0 += 4) {
+      longlong2 w[4][2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 4; ++j) {
         const int s = min(s0 + j, s_hi - 1);     // clamped: unconditional loads
         w[j][0] = *reinterpret_cast<const longlong2*>(p + s * sg.s_stride);
         w[j][1] = *reinterpret_cast<const longlong2*>(p + s * sg.s_stride + 2);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < 4; ++j)
         if (s0 + j < s_hi) {
           q[0] += w[j][0].x; q[1] += w[j][0].y; q[2] += w[j][1].x; q[3] += w[j][1].y;
           if (consume) {
@@ -1231,20 +1231,22 @@ TTMI_DEV float4 fold_unit(const FoldSeg& sg, int64_t off, int s_lo, int s_hi, bo
     return v;
   }
   const float* p = static_cast<const float*>(sg.part) + off;
-  for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
-    float4 w[16];
+  if (s_hi <= s_lo) return v;
+  for (int s0 = s_lo; s0 < s_hi; s0 += 8) {
+    float4 w[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      w[j] = s0 + j < s_hi ? *reinterpret_cast<const float4*>(p + (s0 + j) * sg.s_stride)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < 8; ++j) {          // clamped: unconditional loads, all in flight
+      const int s = min(s0 + j, s_hi - 1);
+      w[j] = *reinterpret_cast<const float4*>(p + s * sg.s_stride);
+    }
     if (consume) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < 8; ++j)
         if (s0 + j < s_hi)
           *reinterpret_cast<float4*>(const_cast<float*>(p) + (s0 + j) * sg.s_stride) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
+    for (int j = 0; j < 8; ++j)
       if (s0 + j < s_hi) { v.x += w[j].x; v.y += w[j].y; v.z += w[j].z; v.w += w[j].w; }
   }
   return v;
@@ -1280,12 +1282,12 @@ TTMI_DEV void fold_parts(const FoldSeg& sg, int bx, int nbx, bool consume, int64
       v = fold_unit(sg, m * sg.N + n, s_lo, s_hi, consume);
     } else if (u < sg.units) {
       const int64_t m = u - nel;
-      for (int s0 = s_lo; s0 < s_hi; s0 += 16) {
-        float w[16];
+      for (int s0 = s_lo; s0 < s_hi; s0 += 8) {
+        float w[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = s0 + j < s_hi ? sg.part_rs[(s0 + j) * sg.M + m] : 0.f;
+        for (int j = 0; j < 8; ++j) w[j] = sg.part_rs[min(s0 + j, s_hi - 1) * sg.M + m];
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+        for (int j = 0; j < 8; ++j)
           if (s0 + j < s_hi) v.x += w[j];
       }
     }

@@ -30,17 +30,28 @@ def flush(self):
 ops.WgradPending.flush = flush
 
 
-def timeit(fn, reps=50):
-    for _ in range(3):
-        fn()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+def timeit(fn, reps=20, replays=10):
+    """Device time per call: `reps` calls captured in one HIP graph, replayed (the host launch
+    cost of a ctypes call would otherwise dominate these few-microsecond kernels)."""
+    fn()
     torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(replays):
+        g.replay()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps * 1e3
+    return a.elapsed_time(b) / (reps * replays) * 1e3
 
 
 def main():
