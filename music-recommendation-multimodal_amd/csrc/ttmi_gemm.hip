@@ -495,22 +495,27 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
   }
 }
 
-template <int NT, int KC, int EPI>
-__global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg, LnBwdArgs ln) {
+template <int NT, int KC, int EPI, int CS>
+__global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_per_wg, LnBwdArgs ln) {
   constexpr int K = KC * 32, N = NT * 16, WP = 2 * K + 16;
   constexpr bool LNB = EPI == PE_LNBWD, LNF = EPI == PE_RESLN;
   static_assert(NT % 8 == 0, "column groups of 128");
   static_assert(!(LNB || LNF) || NT == 8, "LayerNorm epilogues need N = 128");
+  // CS = 2: 16 waves, a pair per row tile, each wave one half of the column groups (twice the
+  // waves per SIMD to hide latency; the LayerNorm epilogues need whole rows: CS = 1)
+  static_assert(CS == 1 || ((NT / 8) % CS == 0 && !(LNB || LNF)), "column split");
+  constexpr int NTH = 512 * CS, CGW = NT / 8 / CS;
   constexpr int SROWS = LNB ? 8 : 1;                            // LNB: one row per wave
   __shared__ __attribute__((aligned(16))) char smem[N * WP + N * 4 + ((LNB || LNF) ? 2 * SROWS * N * 4 : 0)];
   float* sbias = reinterpret_cast<float*>(smem + N * WP);     // bias, or the LN weight
   float* sdw = sbias + N;                                       // LNB: per-wave dw / db sums
   float* sdb = sdw + SROWS * N;                                 // LNF: LN weight / bias
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rwave = wave / CS, cg0 = (wave % CS) * CGW;      // row-tile slot, first column group
   const int li = lane & 15, lg = lane >> 4;
   const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
   const int64_t tile_end = std::min<int64_t>((g.M + 15) / 16, tile_beg + tiles_per_wg);
-  const int64_t tile0 = tile_beg + wave;
+  const int64_t tile0 = tile_beg + rwave;
   uint4 a0[4];                       // this wave's first A fragments, in flight under the W load
   {                                  // (rows clamped into range: unconditional loads)
     const int64_t m = std::min<int64_t>(tile0 * 16 + li, g.M - 1);
@@ -528,8 +533,8 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
     const i32x4_t rw = make_rsrc(g.B, wbytes);
     const uint32_t base = lds_addr(smem);
 #pragma unroll
-    for (int t = 0; t < (INSTR + 7) / 8; ++t) {
-      const int ii = wave + 8 * t;
+    for (int t = 0; t < (INSTR + 8 * CS - 1) / (8 * CS); ++t) {
+      const int ii = wave + 8 * CS * t;
       if (ii >= INSTR) break;                   // wave-uniform
       const int q = ii * 64 + lane, n = q / CPRP, c = q % CPRP;
       const uint32_t voff = c == K / 8 ? wbytes : (uint32_t)(((int64_t)n * g.ldb + 8 * c) * 2);
@@ -538,21 +543,21 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   } else {   // W -> LDS, coalesced 16-byte chunks, 8 loads in flight per thread before the LDS
       // writes (a load -> wait -> write loop pays one memory round trip per chunk: 16 round
       // trips for a 128 KB W image, which used to be most of the kernel's time)
-    constexpr int CPR = K / 8, TOT = N * CPR, PER = (TOT + 511) / 512, BATCH = PER <= 16 ? PER : 8;
+    constexpr int CPR = K / 8, TOT = N * CPR, PER = (TOT + NTH - 1) / NTH, BATCH = PER <= 16 ? PER : 8;
 #pragma unroll
     for (int j0 = 0; j0 < PER; j0 += BATCH) {
       uint4 wv[BATCH];
 #pragma unroll
       for (int j = 0; j < BATCH; ++j) {
         if (j0 + j < PER) {            // compile-time; the chunk index is clamped, not branched
-          const int i = min(tid + 512 * (j0 + j), TOT - 1);    // (a branch here spilled wv)
+          const int i = min(tid + NTH * (j0 + j), TOT - 1);    // (a branch here spilled wv)
           const int n = i / CPR, c = i % CPR;
           wv[j] = *reinterpret_cast<const uint4*>(g.B + ((int64_t)n * g.ldb + 8 * c) * 2);
         }
       }
 #pragma unroll
       for (int j = 0; j < BATCH; ++j) {
-        const int i = tid + 512 * (j0 + j);
+        const int i = tid + NTH * (j0 + j);
         if (j0 + j < PER && i < TOT) {
           const int n = i / CPR, c = i % CPR;
           *reinterpret_cast<uint4*>(smem + n * WP + c * 16) = wv[j];
@@ -562,16 +567,16 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   }
   {
     if constexpr (LNB) {
-      for (int i = tid; i < N; i += 512) sbias[i] = ln.w[i];
-      for (int i = tid; i < SROWS * N; i += 512) { sdw[i] = 0.f; sdb[i] = 0.f; }
+      for (int i = tid; i < N; i += NTH) sbias[i] = ln.w[i];
+      for (int i = tid; i < SROWS * N; i += NTH) { sdw[i] = 0.f; sdb[i] = 0.f; }
     } else if constexpr (LNF) {
-      for (int i = tid; i < N; i += 512) {
+      for (int i = tid; i < N; i += NTH) {
         sbias[i] = g.bias ? g.bias[i] : 0.f;
         sdw[i] = ln.w[i];
         sdb[i] = ln.lnb[i];
       }
     } else {
-      for (int i = tid; i < N; i += 512) sbias[i] = g.bias ? g.bias[i] : 0.f;
+      for (int i = tid; i < N; i += NTH) sbias[i] = g.bias ? g.bias[i] : 0.f;
     }
   }
   const DropKeys dk = resolve_drop(g.drop);
@@ -587,7 +592,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   uint4 a[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) a[c] = a0[c];
-  for (int64_t tile = tile_beg + wave; tile < tile_end; tile += 8) {
+  for (int64_t tile = tile_beg + rwave; tile < tile_end; tile += 8) {
     const int64_t m = tile * 16 + li;
     const bool mok = m < g.M;
     const char* ap = g.A + (std::min<int64_t>(m, g.M - 1) * g.lda + lg * (K / 4)) * 2;
@@ -596,7 +601,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
     // column groups of 128 (8 MFMA tiles) and k groups of 4 chunks keep the accumulator,
     // A and W fragment state bounded (A re-reads per column group hit L1/L2)
 #pragma unroll 1
-    for (int cg = 0; cg < NT / 8; ++cg) {
+    for (int cg = cg0; cg < cg0 + CGW; ++cg) {
       f32x4_t acc[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -606,7 +611,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
 #pragma unroll 1
       for (int cq = 0; cq < KC / 4; ++cq) {
         uint4 an[4];
-        const char* src = cq + 1 < KC / 4 ? ap + 64 * (cq + 1) : (cg + 1 < NT / 8 ? ap : ap_next);
+        const char* src = cq + 1 < KC / 4 ? ap + 64 * (cq + 1) : (cg + 1 < cg0 + CGW ? ap : ap_next);
 #pragma unroll
         for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const uint4*>(src + 16 * c);
 #pragma unroll
@@ -714,7 +719,7 @@ __global__ __launch_bounds__(512) void panel_kernel(GemmArgs g, int tiles_per_wg
   }
   if constexpr (LNB) {
     __syncthreads();
-    for (int i = tid; i < N; i += 512) {
+    for (int i = tid; i < N; i += NTH) {
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int w = 0; w < SROWS; ++w) { a += sdw[w * N + i]; b += sdb[w * N + i]; }
@@ -1851,6 +1856,7 @@ bool panel_applies(const ttmi_gemm_desc* d) {
 
 template <int NT, int KC, int EPI>
 void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBwdArgs{}) {
+  constexpr bool split = EPI != PE_LNBWD && EPI != PE_RESLN && NT == 32;   // N = 512 (N = 256 spilled)
   // contiguous row ranges, about one workgroup per CU; fewer than 8 tiles per workgroup
   // leaves waves idle but puts a workgroup on more CUs (M = 25,600 -> 1,600 tiles -> 229
   // workgroups of 7 instead of 200 of 8 on 256 CUs)
@@ -1863,7 +1869,15 @@ void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBw
   }();
   GemmArgs b = a;
   b.wdma = wdma && a.ldb * 2 * a.N < ((int64_t)1 << 31);
-  hipLaunchKernelGGL((panel_kernel<NT, KC, EPI>), dim3((unsigned)grid), dim3(512), 0, s, b, (int)tpw, ln);
+  static const int cs = [] {              // TTMI_PANEL_CS=1: no column split (A/B runs only)
+    const char* e = getenv("TTMI_PANEL_CS");
+    return e ? atoi(e) : 2;
+  }();
+  if (split && cs == 2)
+    hipLaunchKernelGGL((panel_kernel<NT, KC, EPI, split ? 2 : 1>), dim3((unsigned)grid), dim3(split ? 1024 : 512), 0, s, b,
+                       (int)tpw, ln);
+  else
+    hipLaunchKernelGGL((panel_kernel<NT, KC, EPI, 1>), dim3((unsigned)grid), dim3(512), 0, s, b, (int)tpw, ln);
 }
 
 bool launch_panel(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
