@@ -826,7 +826,17 @@ TTMI_DEV void wgrad_body(const WgradArgs& g, const int bid) {
   const int wm = wave >> 1, wn = wave & 1;
   const int T = g.tiles_m * g.tiles_n;
   int tile, split;
-  if (g.xcd_remap) {          // splits % 8 == 0: one XCD per (split mod 8)
+  if (g.xcd_remap == 2) {     // split-major (split, tile) pairs dealt to the 8 XCDs in
+    // contiguous runs: the tiles of one split (which re-read the same operand rows) run side
+    // by side on one XCD and share its L2.  The entry's first block sits at a multiple of 8
+    // and its grid is 8 * ceil(P / 8) blocks; the surplus slots exit.
+    const int x = bid & 7, j = bid >> 3;
+    const int P = T * g.splits;
+    const int lo = (int)((int64_t)P * x / 8), hi = (int)((int64_t)P * (x + 1) / 8);
+    if (lo + j >= hi) return;
+    split = (lo + j) / T;
+    tile = (lo + j) % T;
+  } else if (g.xcd_remap) {   // splits % 8 == 0: one XCD per (split mod 8)
     const int x = bid & 7, j = bid >> 3;
     tile = j % T;
     split = (j / T) * 8 + x;
@@ -1149,6 +1159,15 @@ WgradGroupCfg wgrad_group_cfg() {
     return c;
   }();
   return cfg;
+}
+
+// TTMI_WGRAD_CHUNK=0 restores the tile-major block order of the grouped launch (A/B runs).
+bool wgrad_group_chunked() {
+  static const bool on = [] {
+    const char* e = getenv("TTMI_WGRAD_CHUNK");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
 }
 
 WgradPlan wgrad_group_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
@@ -2276,12 +2295,18 @@ extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int 
     TTMI_REQUIRE(need == 0 || (d->workspace && d->workspace_bytes >= need && al16(d->workspace)),
                  "ttmi_wgrad_batch: descriptor %d needs a workspace of %lld bytes", i,
                  (long long)need);
-    const int64_t nwg = (int64_t)p.tiles_m * p.tiles_n * p.S;
-    if (grp.n == WG_GROUP || (int64_t)grp.wg_begin[grp.n] + nwg > 2147483647LL) {
+    // tiles re-reading a split's rows grouped on one XCD (xcd_remap 2): the entry starts at a
+    // multiple of 8 blocks and its (split, tile) pairs are padded to a multiple of 8
+    const int64_t T = (int64_t)p.tiles_m * p.tiles_n;
+    const bool chunk = p.S > 1 && T > 1 && wgrad_group_chunked();
+    const int64_t nwg = chunk ? (T * p.S + 7) / 8 * 8 : T * p.S;
+    if (grp.n == WG_GROUP || (int64_t)grp.wg_begin[grp.n] + nwg + 8 > 2147483647LL) {
       rc = flush();
       if (rc) return rc;
     }
+    if (chunk) grp.wg_begin[grp.n] = (grp.wg_begin[grp.n] + 7) / 8 * 8;
     grp.e[grp.n] = wgrad_args(d, p);
+    if (chunk) grp.e[grp.n].xcd_remap = 2;
     grp.wg_begin[grp.n + 1] = grp.wg_begin[grp.n] + (int)nwg;
     ++grp.n;
   }
