@@ -1833,6 +1833,12 @@ int launch_big(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
     case BE_GELU_GRAD: hipLaunchKernelGGL(gemm_big_kernel<BE_GELU_GRAD>, grid, blk, 0, s, ba); break;
     case BE_BIAS | BE_GELU | BE_PRE:
       hipLaunchKernelGGL((gemm_big_kernel<BE_BIAS | BE_GELU | BE_PRE>), grid, blk, 0, s, ba); break;
+    // D = 256 SASRec FFN (linear1 + ReLU + dropout; its gated input grad): compiled epilogues
+    // keep the operand prefetch of big_epi_load (the run-time BE_ANY form took 72 vs ~30 µs)
+    case BE_BIAS | BE_RELU | BE_DROP:
+      hipLaunchKernelGGL((gemm_big_kernel<BE_BIAS | BE_RELU | BE_DROP>), grid, blk, 0, s, ba); break;
+    case BE_BIAS | BE_RELU: hipLaunchKernelGGL((gemm_big_kernel<BE_BIAS | BE_RELU>), grid, blk, 0, s, ba); break;
+    case BE_RELU_GATE: hipLaunchKernelGGL(gemm_big_kernel<BE_RELU_GATE>, grid, blk, 0, s, ba); break;
     default: hipLaunchKernelGGL(gemm_big_kernel<BE_ANY>, grid, blk, 0, s, ba); break;
   }
   return ttmi_check_launch("ttmi_gemm");

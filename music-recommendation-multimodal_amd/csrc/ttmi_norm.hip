@@ -106,34 +106,58 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
   for (int i = 0; i < NV; ++i) aw[i] = ab[i] = 0.f;
   const DropKeys dk16 = resolve_drop(dp16);
-  for (int64_t row = wid; row < M; row += nw) {
-    const float mu = mean[row], rs = rstd[row];
-    float g[NV], xh[NV];
-    float s1 = 0.f, s2 = 0.f;
+  // U rows per wave per pass (rows row0 + u·nw), every load of all U rows issued before any
+  // arithmetic: with the column sums the grid is capped (1,024 blocks), so a wave walks
+  // M / 4,096 rows and a row-at-a-time loop paid one dependent memory round trip per row.
+  // Rows are accumulated in the same order as one at a time (deterministic, unchanged sums).
+  constexpr int U = 4;
+  for (int64_t row0 = wid; row0 < M; row0 += U * nw) {
+    int64_t row[U];
+    bool live[U];
+    float mu[U], rs[U], d[U][NV], xv[U][NV], rv[U][NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
-      g[i] = 0.f; xh[i] = 0.f;
-      if (c < D) {
-        float d = dy[row * lddy + c];
-        if (gate) d = ld_dyn(gate, row * ldg + c, gate_f32) > 0.f ? d * gate_scale : 0.f;
-        xh[i] = (x[row * ldx + c] - mu) * rs;
-        aw[i] += d * xh[i];
-        ab[i] += d;
-        g[i] = d * w[c];
-        s1 += g[i];
-        s2 += g[i] * xh[i];
+    for (int u = 0; u < U; ++u) {          // clamped rows and columns: unconditional loads
+      live[u] = row0 + (int64_t)u * nw < M;
+      row[u] = live[u] ? row0 + (int64_t)u * nw : M - 1;
+      mu[u] = mean[row[u]];
+      rs[u] = rstd[row[u]];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = min(lane + 64 * i, D - 1);
+        d[u][i] = dy[row[u] * lddy + c];
+        if (gate) d[u][i] = ld_dyn(gate, row[u] * ldg + c, gate_f32) > 0.f ? d[u][i] * gate_scale : 0.f;
+        xv[u][i] = x[row[u] * ldx + c];
+        rv[u][i] = res ? res[row[u] * lddx + c] : 0.f;
       }
     }
-    const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < D) {
-        const float o = rs * (g[i] - c1 - xh[i] * c2);
-        const float v = (res ? res[row * lddx + c] : 0.f) + o;
-        dx[row * lddx + c] = v;
-        if (dx16) dx16[row * ld16 + c] = f2bf(drop_apply(dk16, (uint32_t)(row * D + c), v));
+    for (int u = 0; u < U; ++u) {
+      if (!live[u]) continue;                // wave-uniform
+      float g[NV], xh[NV];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = lane + 64 * i;
+        g[i] = 0.f; xh[i] = 0.f;
+        if (c < D) {
+          xh[i] = (xv[u][i] - mu[u]) * rs[u];
+          aw[i] += d[u][i] * xh[i];
+          ab[i] += d[u][i];
+          g[i] = d[u][i] * w[c];
+          s1 += g[i];
+          s2 += g[i] * xh[i];
+        }
+      }
+      const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = lane + 64 * i;
+        if (c < D) {
+          const float o = rs[u] * (g[i] - c1 - xh[i] * c2);
+          const float v = rv[u][i] + o;
+          dx[row[u] * lddx + c] = v;
+          if (dx16) dx16[row[u] * ld16 + c] = f2bf(drop_apply(dk16, (uint32_t)(row[u] * D + c), v));
+        }
       }
     }
   }
@@ -661,8 +685,11 @@ __global__ __launch_bounds__(512) void bnr_bwd_kernel(int B, int C, const float*
 // rows-per-thread class of the register kernels for batch B (0: use the looped kernels)
 int bnr_rpt(int B) { return B <= 4 * BNR_RG ? 4 : B <= 8 * BNR_RG ? 8 : B <= 16 * BNR_RG ? 16 : 0; }
 
-int rows_grid(int64_t rows) {   // 4 rows (waves) per 256-thread block, grid-stride beyond
-  return (int)std::min<int64_t>(std::max<int64_t>((rows + 3) / 4, 1), 2048);
+// 4 rows (waves) per 256-thread block, one row per wave up to 2^20 blocks (grid-stride beyond):
+// a row is a dependent load -> two wave reductions -> store chain, so rows in flight set the
+// time (the round-2 cap of 2,048 blocks made each wave walk ~3 rows serially at M = 25,600)
+int rows_grid(int64_t rows) {
+  return (int)std::min<int64_t>(std::max<int64_t>((rows + 3) / 4, 1), (int64_t)1 << 20);
 }
 
 }  // namespace
@@ -765,7 +792,13 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
   TTMI_REQUIRE(!ln2 || (w1 && b1 && mean1 && rstd1), "ttmi_seq_embed_fwd: norm1 needs w1, b1, mean1, rstd1");
   if (B == 0) return TTMI_OK;
   const DropParams dp = make_drop(drop_p, drop_seed);
-  const dim3 grid(rows_grid((int64_t)B * L));
+  // one row per wave (rows_grid): a row is a dependent chain ids -> E[id] -> two wave
+  // reductions -> stores.  TTMI_SEQ_GRID=cap caps the grid (A/B runs only; 2048 = round 2)
+  static const int64_t cap = [] {
+    const char* e = getenv("TTMI_SEQ_GRID");
+    return e ? (int64_t)atoll(e) : (int64_t)1 << 20;
+  }();
+  const dim3 grid((unsigned)std::min<int64_t>(rows_grid((int64_t)B * L), cap));
   TTMI_NV_DISPATCH(D, {
     if (ln2)
       hipLaunchKernelGGL((seq_embed_fwd_kernel<NV, true>), grid, dim3(256), 0, s, B, L, D, ids, E, V, P,
