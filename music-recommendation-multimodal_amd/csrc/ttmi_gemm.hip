@@ -988,8 +988,11 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(WgradGroup grp) {
   (void)grp;
   KWgradGroup kg = (KWgradGroup)__builtin_amdgcn_kernarg_segment_ptr();
   const int bid = blockIdx.x;
-  int k = 0;
-  while (k + 1 < kg->n && bid >= kg->wg_begin[k + 1]) ++k;
+  int k = 0;                 // the last entry with wg_begin[k] <= bid (binary search)
+  for (int lo = 0, hi = kg->n - 1; lo <= hi;) {
+    const int mid = (lo + hi) >> 1;
+    if (kg->wg_begin[mid] <= bid) { k = mid; lo = mid + 1; } else { hi = mid - 1; }
+  }
   const auto& e = kg->e[k];
   WgradArgs g;
   g.M = e.M; g.N = e.N; g.R = e.R;
@@ -1340,8 +1343,13 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   // units: launching the largest segment's block count for every segment dispatched tens of
   // thousands of empty blocks)
   const KFoldArgs ka = (KFoldArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  // the last k with blk_begin[k] <= blockIdx.x, by binary search (5 dependent scalar loads
+  // for 32 segments instead of a walk of up to 31)
   int k = 0;
-  while (k + 1 < ka->n && (int)blockIdx.x >= ka->blk_begin[k + 1]) ++k;
+  for (int lo = 0, hi = ka->n - 1; lo <= hi;) {
+    const int mid = (lo + hi) >> 1;
+    if (ka->blk_begin[mid] <= (int)blockIdx.x) { k = mid; lo = mid + 1; } else { hi = mid - 1; }
+  }
   const int bx = (int)blockIdx.x - ka->blk_begin[k], nbx = ka->blk_begin[k + 1] - ka->blk_begin[k];
   const auto& sgk = ka->seg[k];
   FoldSeg sg;
