@@ -283,6 +283,16 @@ int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float* i_hat, con
                        const float* logits, const float* lse, const int64_t* user_idx,
                        float inv_tau, const float* dloss, float* du, float* di, uint16_t* du16,
                        void* ws, hipStream_t stream);
+/* ttmi_infonce_bwd16 in ONE launch (ABI 18): the last of each 16-row block's key-split
+ * workgroups (arrival count in `counters`, ttmi_infonce_bwd_counter_bytes(B) bytes, zero on
+ * entry and left zero) sums the split partials in split order and runs the normalise backward
+ * (bit-identical to the two-launch form).  counters NULL, or shapes the fused kernels do not
+ * take: ttmi_infonce_bwd16. */
+int ttmi_infonce_bwd_fused(int B, int D, const float* u_hat, const float* i_hat, const float* norms,
+                           const float* logits, const float* lse, const int64_t* user_idx,
+                           float inv_tau, const float* dloss, float* du, float* di, uint16_t* du16,
+                           void* ws, int32_t* counters, hipStream_t stream);
+int64_t ttmi_infonce_bwd_counter_bytes(int B);
 
 /* ------------------------------------------------------------------------------------
  * Global in-batch negatives (BASELINE cfg 5; the reference InfoNCE two_tower.py:98-140
@@ -598,6 +608,21 @@ int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                     const int64_t* key_valid, const int32_t* rows, const float* lse,
                     const void* dctx, float drop_p, const uint64_t* drop_seed, void* dqkv,
                     hipStream_t stream);
+/* BatchNorm1d backward arguments of ttmi_batchnorm_bwd as a descriptor (ABI 18). */
+typedef struct ttmi_bn_bwd_desc {
+  int dtype, B, C;
+  const float* dy; const float* z; const float* w; const float* mean; const float* rstd;
+  const void* y; float gate_scale; int gated;
+  float* dz; float* dw; float* db; void* dz16;
+} ttmi_bn_bwd_desc;
+/* ttmi_mha_q1_bwd with ttmi_batchnorm_bwd(bn) on the same grid (ABI 18; bn may be NULL): the
+ * item head's BatchNorm1d backward (item_tower.py:125) does not depend on the user tower's
+ * attention, so its column blocks run on the one-query launch's grid (L <= 64, bn->B <= 1024;
+ * otherwise two launches).  Results equal the two separate calls. */
+int ttmi_mha_q1_bnr_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                        const int64_t* key_valid, const int32_t* rows, const float* lse,
+                        const void* dctx, float drop_p, const uint64_t* drop_seed, void* dqkv,
+                        const ttmi_bn_bwd_desc* bn, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * mDeBERTa-v3 text encoder (cfg 4; reference src/models/item_tower.py:41-83 = transformers
@@ -776,6 +801,18 @@ int ttmi_item_head_bwd_c(const ttmi_item_head_bwd_desc* d, hipStream_t stream);
 int64_t ttmi_item_head_bwd_ws_floats(int B);
 int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const ttmi_item_head_bwd_desc* it,
                             hipStream_t stream);
+/* ABI 18: the item head's stage A on the one-query forward's grid, stage C on the user head's.
+ *  - ttmi_mha_q1_gather_item_fwd: ttmi_mha_q1_gather_fwd plus item stage A of `it` (with its
+ *    fused BatchNorm statistics), dispatched first on the same grid (NULL: attention only).
+ *  - ttmi_user_item_head_fwd_c: ttmi_user_head_fwd plus item stage C of `it` (BatchNorm +
+ *    ReLU + dropout + Linear 4 + LayerNorm [+ l2norm]); needs the fused statistics of stage A
+ *    (it->bn_part / bn_cnt, B <= 512).  Together: the item head costs no launch of its own. */
+int ttmi_mha_q1_gather_item_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                                const int64_t* key_valid, const float* x, int32_t* rows, float* x_rows,
+                                float drop_p, const uint64_t* drop_seed, void* ctx, float* lse,
+                                const ttmi_item_head_desc* it, hipStream_t stream);
+int ttmi_user_item_head_fwd_c(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
+                              hipStream_t stream);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
 int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
 /* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);

@@ -11,7 +11,7 @@
 // Every value the backward reads is written out as the unfused ops did (x1, a2, m2, r2, h,
 // comb, rows, z, az, mz, rz) and the dropout masks are the same hash at the same indices
 // (drop_rows[m]·N + n).
-#include "ttmi_common.h"
+#include "ttmi_q1.h"
 
 namespace {
 
@@ -72,6 +72,7 @@ struct HeadArgs {
   // co-launched item head stage A (ttmi_user_item_head_fwd): workgroups >= nbu run
   // item_a_body on row block (l % it_nblk), column quarter (l / it_nblk)
   ItemArgs it; int nbu, it_nblk;
+  int it_stage;                // 0: item stage A (it_nblk x 8 workgroups), 2: item stage C (it_nblk)
 };
 
 struct HeadLds {
@@ -305,6 +306,105 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   if (tid == 0) __hip_atomic_store(a.bncnt + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+struct ItemLdsC {
+  char sY[HR * PI];
+  float red[4][HR];
+};
+
+// Item head stage C on row block bx (item_head_c_kernel, or the workgroups of
+// ttmi_user_item_head_fwd_c past the user head's).
+TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = bx * HR;
+  const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
+  if (a.bncnt != nullptr) {      // fused BatchNorm: y1 = drop(relu(BN(z))) staged from z rows
+    float4 zv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+      zv[k] = *reinterpret_cast<const float4*>(a.z + (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4);
+    }
+    const DropKeys dk = resolve_drop(a.bd);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+      const float4 mu = *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
+      const float4 rs = *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
+      const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
+      const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
+      float x[4] = {fmaxf((zv[k].x - mu.x) * rs.x * ww.x + bb.x, 0.f), fmaxf((zv[k].y - mu.y) * rs.y * ww.y + bb.y, 0.f),
+                    fmaxf((zv[k].z - mu.z) * rs.z * ww.z + bb.z, 0.f), fmaxf((zv[k].w - mu.w) * rs.w * ww.w + bb.w, 0.f)};
+      drop_apply_vec<4>(dk, (uint32_t)((int64_t)(r0 + r) * IN1 + 4 * c4), x);
+      st4_bf(L.sY + r * PI + c4 * 8, x);
+      if (r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.y1w + (int64_t)(r0 + r) * IN1 + 4 * c4), x);
+    }
+  } else {                                           // y1 rows: 16 x 64 chunks of 16 bytes
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = tid + 256 * k, r = idx >> 6, ch = idx & 63;
+      *reinterpret_cast<uint4*>(L.sY + r * PI + ch * 16) =
+          *reinterpret_cast<const uint4*>(a.y1 + (int64_t)min(r0 + r, a.B - 1) * IN1 + ch * 8);
+    }
+  }
+  WFrags<2, IN1> wf;
+  wf.load(a.w4, IN1, n0, lane, IN1);
+  float b4[2][4], lw[2][4], lb[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float4 b = *reinterpret_cast<const float4*>(a.b4 + n);
+    const float4 x = *reinterpret_cast<const float4*>(a.lnw + n);
+    const float4 y = *reinterpret_cast<const float4*>(a.lnb + n);
+    b4[t][0] = b.x; b4[t][1] = b.y; b4[t][2] = b.z; b4[t][3] = b.w;
+    lw[t][0] = x.x; lw[t][1] = x.y; lw[t][2] = x.z; lw[t][3] = x.w;
+    lb[t][0] = y.x; lb[t][1] = y.y; lb[t][2] = y.z; lb[t][3] = y.w;
+  }
+  __syncthreads();
+  f32x4_t v[2];
+  head_gemm<2, IN1, PI>(L.sY, wf, v, lane);
+  const int m = r0 + li;
+  const bool mrow = m < a.B;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[t][e] += b4[t][e];
+    if (mrow) *reinterpret_cast<float4*>(a.y2 + (int64_t)m * HD + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
+  }
+  // LayerNorm over the 128 columns (the 4 waves' 32 each), two-pass like ttmi_layernorm_fwd
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[t][e];
+  const float mu = row_sum(s, L, w, lane) * (1.f / HD);
+  float qv = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[t][e] - mu;
+      qv += d * d;
+    }
+  const float rs = 1.f / sqrtf(row_sum(qv, L, w, lane) * (1.f / HD) + a.ln_eps);
+  float oo[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    float* o = oo[t];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[t][e] - mu) * rs * lw[t][e] + lb[t][e];
+    if (mrow) *reinterpret_cast<float4*>(a.out + (int64_t)m * HD + n) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  if (mrow && lane < 16 && w == 0) { a.m5[m] = mu; a.r5[m] = rs; }
+  row_l2norm(oo, a.ohat, a.onrm, m, mrow, n0, L, w, lane);
+}
+
+__global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
+  __shared__ __attribute__((aligned(16))) ItemLdsC L;
+  item_c_body(a, blockIdx.x, L);
+}
+
 #ifdef HEAD_STAMP
 #define STAMP(i) do { if (threadIdx.x == 0) stamp[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
@@ -324,9 +424,11 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
   __shared__ __attribute__((aligned(16))) HeadLds L;
   __shared__ __attribute__((aligned(16))) HeadParams Q;
   static_assert(sizeof(HeadLds) >= sizeof(ItemLdsA), "item stage A reuses the head's LDS");
-  if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head stage A
+  static_assert(sizeof(HeadLds) >= sizeof(ItemLdsC), "item stage C reuses the head's LDS");
+  if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head stage A or C
     const int l = (int)blockIdx.x - a.nbu;
-    item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+    if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+    else item_c_body(a.it, l, *reinterpret_cast<ItemLdsC*>(&L));
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
@@ -871,97 +973,22 @@ __global__ __launch_bounds__(256) void item_head_a_kernel(ItemArgs a) {
   item_a_body(a, blockIdx.x, blockIdx.y, L);
 }
 
-struct ItemLdsC {
-  char sY[HR * PI];
-  float red[4][HR];
-};
-
-__global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
-  __shared__ __attribute__((aligned(16))) ItemLdsC L;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
-  const int r0 = blockIdx.x * HR;
-  const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
-  if (a.bncnt != nullptr) {      // fused BatchNorm: y1 = drop(relu(BN(z))) staged from z rows
-    float4 zv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-      zv[k] = *reinterpret_cast<const float4*>(a.z + (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4);
-    }
-    const DropKeys dk = resolve_drop(a.bd);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-      const float4 mu = *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
-      const float4 rs = *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
-      const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
-      const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
-      float x[4] = {fmaxf((zv[k].x - mu.x) * rs.x * ww.x + bb.x, 0.f), fmaxf((zv[k].y - mu.y) * rs.y * ww.y + bb.y, 0.f),
-                    fmaxf((zv[k].z - mu.z) * rs.z * ww.z + bb.z, 0.f), fmaxf((zv[k].w - mu.w) * rs.w * ww.w + bb.w, 0.f)};
-      drop_apply_vec<4>(dk, (uint32_t)((int64_t)(r0 + r) * IN1 + 4 * c4), x);
-      st4_bf(L.sY + r * PI + c4 * 8, x);
-      if (r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.y1w + (int64_t)(r0 + r) * IN1 + 4 * c4), x);
-    }
-  } else {                                           // y1 rows: 16 x 64 chunks of 16 bytes
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int idx = tid + 256 * k, r = idx >> 6, ch = idx & 63;
-      *reinterpret_cast<uint4*>(L.sY + r * PI + ch * 16) =
-          *reinterpret_cast<const uint4*>(a.y1 + (int64_t)min(r0 + r, a.B - 1) * IN1 + ch * 8);
-    }
+// The pruned layer's one-query attention (with the last-valid gather) and item stage A on one
+// grid (ttmi_mha_q1_gather_item_fwd): workgroups [0, nit) run item_a_body (they take longest,
+// so they are dispatched first), the rest one (sequence, head) per wave (ttmi_q1.h).
+template <typename T>
+__global__ __launch_bounds__(256) void q1_item_fwd_kernel(Q1Args q, ItemArgs it, int it_nblk, int nit) {
+  __shared__ __attribute__((aligned(16))) union U {
+    ItemLdsA ia;
+    Q1Lds q[4];
+  } S;
+  if ((int)blockIdx.x < nit) {
+    item_a_body(it, (int)blockIdx.x % it_nblk, (int)blockIdx.x / it_nblk, S.ia);
+    return;
   }
-  WFrags<2, IN1> wf;
-  wf.load(a.w4, IN1, n0, lane, IN1);
-  float b4[2][4], lw[2][4], lb[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int n = n0 + 16 * t + 4 * g;
-    const float4 b = *reinterpret_cast<const float4*>(a.b4 + n);
-    const float4 x = *reinterpret_cast<const float4*>(a.lnw + n);
-    const float4 y = *reinterpret_cast<const float4*>(a.lnb + n);
-    b4[t][0] = b.x; b4[t][1] = b.y; b4[t][2] = b.z; b4[t][3] = b.w;
-    lw[t][0] = x.x; lw[t][1] = x.y; lw[t][2] = x.z; lw[t][3] = x.w;
-    lb[t][0] = y.x; lb[t][1] = y.y; lb[t][2] = y.z; lb[t][3] = y.w;
-  }
-  __syncthreads();
-  f32x4_t v[2];
-  head_gemm<2, IN1, PI>(L.sY, wf, v, lane);
-  const int m = r0 + li;
-  const bool mrow = m < a.B;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int n = n0 + 16 * t + 4 * g;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[t][e] += b4[t][e];
-    if (mrow) *reinterpret_cast<float4*>(a.y2 + (int64_t)m * HD + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
-  }
-  // LayerNorm over the 128 columns (the 4 waves' 32 each), two-pass like ttmi_layernorm_fwd
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s += v[t][e];
-  const float mu = row_sum(s, L, w, lane) * (1.f / HD);
-  float qv = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float d = v[t][e] - mu;
-      qv += d * d;
-    }
-  const float rs = 1.f / sqrtf(row_sum(qv, L, w, lane) * (1.f / HD) + a.ln_eps);
-  float oo[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int n = n0 + 16 * t + 4 * g;
-    float* o = oo[t];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (v[t][e] - mu) * rs * lw[t][e] + lb[t][e];
-    if (mrow) *reinterpret_cast<float4*>(a.out + (int64_t)m * HD + n) = make_float4(o[0], o[1], o[2], o[3]);
-  }
-  if (mrow && lane < 16 && w == 0) { a.m5[m] = mu; a.r5[m] = rs; }
-  row_l2norm(oo, a.ohat, a.onrm, m, mrow, n0, L, w, lane);
+  const int w = threadIdx.x >> 6, bh = ((int)blockIdx.x - nit) * 4 + w;
+  if (bh >= q.B * q.H) return;
+  q1_fwd_wave<T, true>(q, bh, S.q[w]);
 }
 
 }  // namespace
@@ -1052,8 +1079,9 @@ extern "C" int ttmi_item_head_bwd_c(const ttmi_item_head_bwd_desc* d, hipStream_
   return ttmi_check_launch("ttmi_item_head_bwd_c");
 }
 
-extern "C" int ttmi_user_item_head_fwd(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
-                                       hipStream_t s) {
+namespace {
+int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it, int stage,
+                            hipStream_t s) {
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_fwd: null descriptor");
   TTMI_REQUIRE(d->B > 0 && d->D == HD, "ttmi_user_head_fwd: needs D == %d", HD);
   TTMI_REQUIRE(d->F > 0 && d->F <= FMAX && d->F % 256 == 0, "ttmi_user_head_fwd: needs F %% 256 == 0, F <= %d", FMAX);
@@ -1083,18 +1111,64 @@ extern "C" int ttmi_user_item_head_fwd(const ttmi_user_head_desc* d, const ttmi_
   TTMI_REQUIRE(!d->u_hat || d->u_norm, "ttmi_user_head_fwd: u_hat needs u_norm");
   a.nbu = (d->B + HR - 1) / HR;
   a.it_nblk = 1;
+  a.it_stage = stage;
   int extra = 0;
-  if (it) {                                          // item stage A on the idle CUs
+  if (it) {                                          // item stage A or C on the idle CUs
     const int rc = item_fwd_check(it);
     if (rc != TTMI_OK) return rc;
     a.it = item_args(it);
+    TTMI_REQUIRE(stage == 0 || a.it.bncnt != nullptr,
+                 "ttmi_user_item_head_fwd_c: stage C here needs the BatchNorm statistics of stage A "
+                 "(bn_part / bn_cnt, B <= %d)", BN_MAXBLK * HR);
     a.it_nblk = (it->B + HR - 1) / HR;
-    extra = a.it_nblk * (IN1 / 64);
+    extra = stage == 0 ? a.it_nblk * (IN1 / 64) : a.it_nblk;
   }
   const dim3 grid((unsigned)(a.nbu + extra));
   if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_kernel<512>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(user_head_fwd_kernel<256>, grid, dim3(256), 0, s, a);
   return ttmi_check_launch("ttmi_user_head_fwd");
+}
+}  // namespace
+
+extern "C" int ttmi_user_item_head_fwd(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
+                                       hipStream_t s) {
+  return user_item_head_fwd_impl(d, it, 0, s);
+}
+
+extern "C" int ttmi_user_item_head_fwd_c(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
+                                         hipStream_t s) {
+  TTMI_REQUIRE(it != nullptr, "ttmi_user_item_head_fwd_c: null item descriptor");
+  return user_item_head_fwd_impl(d, it, 2, s);
+}
+
+extern "C" int ttmi_mha_q1_gather_item_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                                           const int64_t* key_valid, const float* x, int32_t* rows,
+                                           float* x_rows, float drop_p, const uint64_t* drop_seed,
+                                           void* ctx, float* lse, const ttmi_item_head_desc* it,
+                                           hipStream_t s) {
+  if (it == nullptr || L > 64 || B == 0) {          // separate launches
+    if (it) {
+      const int rc = ttmi_item_head_fwd_stages(it, 1, s);
+      if (rc) return rc;
+    }
+    return ttmi_mha_q1_gather_fwd(dtype, B, L, H, Dh, qkv, key_valid, x, rows, x_rows, drop_p, drop_seed, ctx,
+                                  lse, s);
+  }
+  int rc = q1_validate("ttmi_mha_q1_gather_item_fwd", dtype, B, L, H, Dh, qkv, drop_p, drop_seed);
+  if (rc) return rc;
+  TTMI_REQUIRE(qkv && key_valid && x && rows && x_rows && ctx && lse, "ttmi_mha_q1_gather_item_fwd: null argument");
+  rc = item_fwd_check(it);
+  if (rc) return rc;
+  Q1Args q{};
+  q.B = B; q.L = L; q.H = H; q.Dh = Dh; q.scale = 1.f / sqrtf((float)Dh);
+  q.qkv = qkv; q.kvalid = key_valid; q.rows = rows; q.x = x; q.x_rows = x_rows;
+  q.dp = make_drop(drop_p, drop_seed); q.ctx = ctx; q.lse = lse;
+  const ItemArgs ia = item_args(it);
+  const int it_nblk = (it->B + HR - 1) / HR, nit = it_nblk * (IN1 / 64);
+  const dim3 grid((unsigned)(nit + (B * H + 3) / 4));
+  if (dtype == TTMI_BF16) hipLaunchKernelGGL(q1_item_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, q, ia, it_nblk, nit);
+  else hipLaunchKernelGGL(q1_item_fwd_kernel<float>, grid, dim3(256), 0, s, q, ia, it_nblk, nit);
+  return ttmi_check_launch("ttmi_mha_q1_gather_item_fwd");
 }
 
 extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {

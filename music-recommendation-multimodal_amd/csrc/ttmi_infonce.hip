@@ -495,13 +495,18 @@ TTMI_DEV void load4(const float* __restrict__ p, int k, int n, float (&v)[4]) {
   }
 }
 
-template <int DC, bool VEC>
+// The finish's arguments when it runs inside the backward launch (ttmi_infonce_bwd_fused).
+struct NceFinish {
+  const float* norms; float inv_tau; float* du; float* di; bf16_t* du16; int* cnt;
+};
+
+template <int DC, bool VEC, bool FIN>
 __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __restrict__ uh,
                                                       const float* __restrict__ ih,
                                                       const float* __restrict__ S,
                                                       const float* __restrict__ lse,
                                                       const float* __restrict__ dloss,
-                                                      float* __restrict__ part) {
+                                                      float* __restrict__ part, NceFinish fin) {
   constexpr int D = 16 * DC, TPW = DC / 4;
   static_assert(DC % 4 == 0, "D % 64 == 0");
   constexpr int VP = D + 4, GP = NKB + 4;          // LDS pitches (floats)
@@ -588,12 +593,90 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
   }
   // lane holds D[d = dtile*16 + 4lg + r][row = r0 + li]
   const int row = r0 + li;
-  if (row < B) {
-    float* pr = part + ((int64_t)split * 2 * B + (int64_t)dir * B + row) * D;
+  if constexpr (!FIN) {
+    if (row < B) {
+      float* pr = part + ((int64_t)split * 2 * B + (int64_t)dir * B + row) * D;
 #pragma unroll
-    for (int q = 0; q < TPW; ++q)
-      *reinterpret_cast<float4*>(pr + (wave + 4 * q) * 16 + 4 * lg) =
-          make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+      for (int q = 0; q < TPW; ++q)
+        *reinterpret_cast<float4*>(pr + (wave + 4 * q) * 16 + 4 * lg) =
+            make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+    }
+    return;
+  } else {
+    // ---- the finish in the same launch: the last of a row block's NSPLIT workgroups sums the
+    // NSPLIT partial rows in split order (the separate finish kernel's order: bit-identical)
+    // and runs the normalise backward.  Hand-off (MI355X_MICROARCH.md, valid forms, row 1):
+    // every partial byte is stored write-through (sc1, 16 B per lane), every storing wave
+    // drains vmcnt before the workgroup barrier, one lane's agent-scope add is the arrival, the
+    // last arriver (told by the returned count) reads the partials with sc1 loads only.
+    if (row < B) {
+      const uint32_t base = (uint32_t)(((int64_t)split * 2 * B + (int64_t)dir * B + row) * D * 4);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) {
+        const i32x4_t v = {(int)__float_as_uint(acc[q][0]), (int)__float_as_uint(acc[q][1]),
+                           (int)__float_as_uint(acc[q][2]), (int)__float_as_uint(acc[q][3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, base + ((wave + 4 * q) * 16 + 4 * lg) * 4, 0, 16);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int s_last;
+    __syncthreads();
+    if (tid == 0)
+      s_last = __hip_atomic_fetch_add(fin.cnt + qb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NSPLIT - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (tid == 0) __hip_atomic_store(fin.cnt + qb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    constexpr int CPL = (D + 63) / 64;               // columns per lane (c = lane + 64q)
+    constexpr int RPW = NQ / 4;                      // rows per wave: r0 + wave + 4k
+    const float* Y = dir ? ih : uh;
+    float* dX = dir ? fin.di : fin.du;
+    float pv[RPW][NSPLIT][CPL];                      // every partial load in flight first
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      const int64_t prow = (int64_t)dir * B + min(r0 + wave + 4 * k, B - 1);
+#pragma unroll
+      for (int sp = 0; sp < NSPLIT; ++sp)
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+          const int c = min(lane + 64 * q, D - 1);
+          pv[k][sp][q] = __hip_atomic_load(part + ((int64_t)sp * 2 * B + prow) * D + c, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      const int rr = r0 + wave + 4 * k;
+      if (rr >= B) break;
+      const int64_t prow = (int64_t)dir * B + rr;
+      const float nrm = fin.norms[prow];
+      float v[CPL], y[CPL];
+      float sdot = 0.f;
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        const int c = lane + 64 * q;
+        float t = 0.f;
+        y[q] = 0.f;
+        if (c < D) {
+#pragma unroll
+          for (int sp = 0; sp < NSPLIT; ++sp) t += pv[k][sp][q];
+          t *= fin.inv_tau;
+          y[q] = Y[(int64_t)rr * D + c];
+          sdot += y[q] * t;
+        }
+        v[q] = t;
+      }
+      sdot = wave_sum(sdot);
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        const int c = lane + 64 * q;
+        if (c < D) {
+          const float g = nrm > NORM_EPS ? (v[q] - y[q] * sdot) / nrm : v[q] / NORM_EPS;
+          dX[(int64_t)rr * D + c] = g;
+          if (dir == 0 && fin.du16) fin.du16[(int64_t)rr * D + c] = f2bf(g);
+        }
+      }
+    }
   }
 }
 
@@ -778,7 +861,7 @@ extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float*
                                            ((int64_t)3 * NSPLIT * 2 * B * 4 + 255) / 256 * 256);
     const int nb = (B + NQ - 1) / NQ;
     const dim3 grid(2 * nb * NSPLIT);
-#define TTMI_NCE_BWD(DC, V) hipLaunchKernelGGL((nce_bwd_kernel<DC, V>), grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part)
+#define TTMI_NCE_BWD(DC, V) hipLaunchKernelGGL((nce_bwd_kernel<DC, V, false>), grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part, NceFinish{})
 #define TTMI_NCE_BWD2(DC) do { if (B % 4 == 0) TTMI_NCE_BWD(DC, true); else TTMI_NCE_BWD(DC, false); } while (0)
     switch (D / 16) {
       case 4: TTMI_NCE_BWD2(4); break;
@@ -812,6 +895,41 @@ extern "C" int ttmi_infonce_bwd16(int B, int D, const float* u_hat, const float*
   rc = ttmi_check_launch("ttmi_infonce_bwd/l2norm_bwd");
   if (rc || !du16) return rc;
   return ttmi_cast_f32_bf16((int64_t)B * D, du, du16, s);
+}
+
+extern "C" int64_t ttmi_infonce_bwd_counter_bytes(int B) {
+  return B > 0 ? (int64_t)(2 * ((B + NQ - 1) / NQ)) * 4 : 0;
+}
+
+extern "C" int ttmi_infonce_bwd_fused(int B, int D, const float* u_hat, const float* i_hat,
+                                      const float* norms, const float* logits, const float* lse,
+                                      const int64_t* user_idx, float inv_tau, const float* dloss,
+                                      float* du, float* di, uint16_t* du16, void* ws, int32_t* counters,
+                                      hipStream_t s) {
+  if (counters == nullptr || !fused_ok(B, D))
+    return ttmi_infonce_bwd16(B, D, u_hat, i_hat, norms, logits, lse, user_idx, inv_tau, dloss, du, di, du16,
+                              ws, s);
+  TTMI_REQUIRE(B > 0 && u_hat && i_hat && norms && logits && lse && du && di && ws,
+               "ttmi_infonce_bwd_fused: null argument");
+  TTMI_REQUIRE(((uintptr_t)counters & 3) == 0, "ttmi_infonce_bwd_fused: counters need 4-byte alignment");
+  TTMI_REQUIRE((int64_t)NSPLIT * 2 * B * D * 4 < 0x7FFFFFFF, "ttmi_infonce_bwd_fused: batch too large");
+  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                         ((int64_t)3 * NSPLIT * 2 * B * 4 + 255) / 256 * 256);
+  TTMI_REQUIRE(((uintptr_t)part & 15) == 0, "ttmi_infonce_bwd_fused: workspace needs 16-byte alignment");
+  const int nb = (B + NQ - 1) / NQ;
+  const dim3 grid(2 * nb * NSPLIT);
+  const NceFinish fin{norms, inv_tau, du, di, (bf16_t*)du16, counters};
+#define TTMI_NCE_BWDF(DC, V) hipLaunchKernelGGL((nce_bwd_kernel<DC, V, true>), grid, dim3(256), 0, s, B, u_hat, i_hat, logits, lse, dloss, part, fin)
+#define TTMI_NCE_BWDF2(DC) do { if (B % 4 == 0) TTMI_NCE_BWDF(DC, true); else TTMI_NCE_BWDF(DC, false); } while (0)
+  switch (D / 16) {
+    case 4: TTMI_NCE_BWDF2(4); break;
+    case 8: TTMI_NCE_BWDF2(8); break;
+    case 12: TTMI_NCE_BWDF2(12); break;
+    default: TTMI_NCE_BWDF2(16); break;
+  }
+#undef TTMI_NCE_BWDF2
+#undef TTMI_NCE_BWDF
+  return ttmi_check_launch("ttmi_infonce_bwd_fused");
 }
 
 // ------------------------------------------------------------ building blocks (cfg 5)

@@ -219,8 +219,14 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             ctx = torch.empty(B, D, device=dev, dtype=dt)
             lse = torch.empty(B * H, **f32)
             # the last-valid rows, their residual rows and the one-query attention: one launch
+            # (with the item head's stage A on the same grid when its BatchNorm statistics are
+            # merged in-launch: stage C then rides in the user head launch, ABI 18)
+            co_a = co_item is not None and co_item.bn_fused and L <= 64
             ops.mha_q1_gather_fwd(qkv, key_valid, x, rows, res_in, B, L, H, ctx, lse,
-                                  _drop(cfg, seeds, site_attn(i)))
+                                  _drop(cfg, seeds, site_attn(i)),
+                                  co_item=co_item.desc if co_a else None)
+            if co_a:
+                co_item.a_done = True
             if ops.user_head_fusable(W, P, pre, D, dt):      # the rest of the tower: one launch
                 F_ = W[pre + "linear1.weight"].shape[0]
                 Wc = D + P["gender_embedding.weight"].shape[1] + P["country_embedding.weight"].shape[1]
@@ -235,9 +241,12 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                                   (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_ffn(i)),
                                    _drop(cfg, seeds, site_drop2(i))), o,
                                   co_item=co_item.desc if co_item is not None else None,
-                                  normed=normed)
+                                  normed=normed, co_stage="C" if co_a else "A")
                 if co_item is not None:
-                    co_item.a_done = True
+                    if co_a:
+                        co_item.c_done = True
+                    else:
+                        co_item.a_done = True
                 st.normed = normed is not None
                 st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, o["x1"], o["a2"], o["m2"],
                                             o["r2"], o["h"], rows))
@@ -346,8 +355,9 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         dx = None
     else:
         dx = _head_bwd_unfused(P, W, st, du, grads, cfg, du16, gathered)
+    bn_co = None       # the item BatchNorm backward, on the pruned layer's one-query grid
     if co_item is not None:
-        item_fusion_bwd_end(co_item)
+        bn_co = item_fusion_bwd_end(co_item, defer_bn=gathered and L <= 64)
     # ---- encoder layers, reversed (user_tower.py:37-45)
     p = cfg.p_drop
     dy2_next = None        # layer i's dy2, emitted by layer i+1's fused LN1 backward
@@ -366,7 +376,10 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         if drows is not None:
             ops.mha_q1_bwd(s.qkv, st.key_valid, drows, s.lse, dctx, B, L, H, dqkv,
-                           _drop(cfg, seeds, site_attn(i)))
+                           _drop(cfg, seeds, site_attn(i)), bn=bn_co.desc if bn_co else None)
+            if bn_co is not None:
+                bn_co.finish()
+                bn_co = None
         else:
             ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
                         _drop(cfg, seeds, site_attn(i)))
@@ -395,6 +408,10 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
                 ops.layernorm_bwd(da1, s.x, s.m1, s.r1, P[pre + "norm1.weight"], dxn,
                                   grads[pre + "norm1.weight"], grads[pre + "norm1.bias"], res=dx1)
         dx = dxn
+        if bn_co is not None:         # no one-query launch carried it
+            ops.bn_bwd_run(bn_co.desc)
+            bn_co.finish()
+            bn_co = None
         if on_layer_done is not None:
             on_layer_done(i)
     # ---- input block (user_tower.py:83-93)
@@ -548,6 +565,8 @@ class ItemHeadPending:
     modal: Tensor
     seeds: Optional[Tensor]
     a_done: bool = False
+    c_done: bool = False
+    bn_fused: bool = False      # BatchNorm statistics merged in stage A (B <= 512)
 
 
 def item_fusion_fwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Tensor, cfg: TowerCfg,
@@ -572,12 +591,14 @@ def item_fusion_fwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], modal: Ten
         o["out_hat"], o["out_norm"] = normed
     m = modal.contiguous()
     d = ops.item_head_desc(m, W, P, buffers or {}, _drop(cfg, seeds, SITE_ITEM, p_drop), cfg.eps, o)
-    return ItemHeadPending(d, o, m, seeds)
+    return ItemHeadPending(d, o, m, seeds, bn_fused=bool(d.bn_part))
 
 
 def item_fusion_fwd_end(pend: ItemHeadPending):
     """The pending forward's remaining stages; returns (out, ItemSaved) as item_fusion_fwd."""
-    ops.item_head_fwd_stages(pend.desc, 6 if pend.a_done else 7)
+    stages = (0 if pend.a_done else 1) | (0 if pend.c_done else 6)
+    if stages:
+        ops.item_head_fwd_stages(pend.desc, stages)
     o = pend.o
     return o["out"], ItemSaved(o["m16"], o["z"], o["bn_mean"], o["bn_rstd"], o["y1"], o["y2"],
                                o["m5"], o["r5"], pend.seeds)
@@ -614,9 +635,21 @@ def item_fusion_bwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSa
     return ItemBwdPending(d, (dc, w4t), dy2, dy1, ws, (P, W, st, grads, cfg, p_drop, dmodal))
 
 
-def item_fusion_bwd_end(pend: ItemBwdPending) -> None:
+@dataclass
+class ItemBnPending:
+    """The item head's BatchNorm1d backward held back to ride on another launch's grid
+    (ttmi_mha_q1_bnr_bwd, ABI 18): ``desc`` goes to ops.mha_q1_bwd(bn=...), then ``finish()``
+    records what depends on it (fusion_layer.0's weight gradient, dmodal)."""
+    desc: object
+    keep: tuple
+    finish: Callable[[], None]
+
+
+def item_fusion_bwd_end(pend: ItemBwdPending, defer_bn: bool = False) -> Optional[ItemBnPending]:
     """The rest of item_fusion_bwd: the row-local launch if the user head did not carry it,
-    the LayerNorm parameter sums, the weight gradients and the BatchNorm backward."""
+    the LayerNorm parameter sums, the weight gradients and the BatchNorm backward.  With
+    ``defer_bn`` the BatchNorm backward (when its bf16 register path applies) is returned as an
+    ItemBnPending for the caller to co-launch; otherwise None."""
     P, W, st, grads, cfg, p_drop, dmodal = pend.args
     if not pend.done:
         ops.item_head_bwd_c(pend.desc)
@@ -624,7 +657,29 @@ def item_fusion_bwd_end(pend: ItemBwdPending) -> None:
     D = pend.dy2.shape[1]
     ops.ln_sum_folds(pend.ws, (grads["fusion_layer.5.weight"], grads["fusion_layer.5.bias"]), 2, D)
     ops.linear_dw(pend.dy2, st.y1, grads["fusion_layer.4.weight"], grads["fusion_layer.4.bias"])
+    if defer_bn and cfg.dtype == torch.bfloat16 and pend.dy1.shape[0] <= 512:
+        return _item_bn_pending(P, W, st, pend.dy1, grads, cfg, p_drop, dmodal)
     _item_bwd_tail(P, W, st, pend.dy1, grads, cfg, p_drop, dmodal)
+    return None
+
+
+def _item_bn_pending(P, W, st: ItemSaved, dy1: Tensor, grads, cfg: TowerCfg, p_drop: float,
+                     dmodal: Optional[Tensor]) -> ItemBnPending:
+    """_item_bwd_tail split at its BatchNorm backward (bf16 register path, B <= 512)."""
+    dev = dy1.device
+    B, H1 = dy1.shape
+    pd = p_drop if st.seeds is not None else 0.0
+    dz = torch.empty(B, H1, device=dev, dtype=torch.float32)
+    dz_c = torch.empty(B, H1, device=dev, dtype=cfg.dtype)
+    d = ops.bn_bwd_desc(dy1, st.z, P["fusion_layer.1.weight"], st.bn_mean, st.bn_rstd, st.y1, dz,
+                        grads["fusion_layer.1.weight"], grads["fusion_layer.1.bias"],
+                        gate_scale=_scale(pd), gated=True, dz16=dz_c)
+
+    def finish() -> None:
+        ops.linear_dw(dz_c, st.modal, grads["fusion_layer.0.weight"], grads["fusion_layer.0.bias"])
+        if dmodal is not None:
+            ops.linear_dx(dz_c, W["fusion_layer.0.weight"], dmodal)
+    return ItemBnPending(d, (dy1, dz, dz_c), finish)
 
 
 def item_fusion_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSaved, dout: Tensor,

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -97,6 +97,14 @@ class ItemHeadDesc(ctypes.Structure):
                 ("modal16", c_p), ("z", c_p), ("bn_mean", c_p), ("bn_rstd", c_p), ("y1", c_p), ("y2", c_p),
                 ("out", c_p), ("m5", c_p), ("r5", c_p), ("ws", c_p),
                 ("out_hat", c_p), ("out_norm", c_p), ("bn_part", c_p), ("bn_cnt", c_p)]
+
+
+class BnBwdDesc(ctypes.Structure):
+    """ttmi_bn_bwd_desc (include/ttmi.h, ABI 18)."""
+    _fields_ = [("dtype", c_i), ("B", c_i), ("C", c_i),
+                ("dy", c_p), ("z", c_p), ("w", c_p), ("mean", c_p), ("rstd", c_p),
+                ("y", c_p), ("gate_scale", c_f), ("gated", c_i),
+                ("dz", c_p), ("dw", c_p), ("db", c_p), ("dz16", c_p)]
 
 
 class ItemHeadBwdDesc(ctypes.Structure):
@@ -218,6 +226,9 @@ SIGNATURES = {
     "ttmi_infonce_counter_bytes": (ctypes.c_int64, [c_i]),
     "ttmi_infonce_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_infonce_bwd16": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_infonce_bwd_fused": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p,
+                                     c_p, c_p]),
+    "ttmi_infonce_bwd_counter_bytes": (ctypes.c_int64, [c_i]),
     "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),
     "ttmi_adamw_fx": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
                             c_p]),
@@ -244,6 +255,7 @@ SIGNATURES = {
     "ttmi_item_head_fwd": (c_i, [c_p, c_p]),
     "ttmi_item_head_fwd_stages": (c_i, [c_p, c_i, c_p]),
     "ttmi_user_item_head_fwd": (c_i, [c_p, c_p, c_p]),
+    "ttmi_user_item_head_fwd_c": (c_i, [c_p, c_p, c_p]),
     "ttmi_item_head_bwd_c": (c_i, [c_p, c_p]),
     "ttmi_item_head_bn_part_floats": (ctypes.c_int64, [c_i]),
     "ttmi_item_head_bn_counter_bytes": (ctypes.c_int64, [c_i]),
@@ -298,6 +310,10 @@ SIGNATURES = {
     "ttmi_mha_q1_gather_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p,
                                      c_p, c_p]),
     "ttmi_mha_q1_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "ttmi_mha_q1_bnr_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p,
+                                  c_p]),
+    "ttmi_mha_q1_gather_item_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p,
+                                          c_p, c_p, c_p, c_p]),
     "ttmi_colsum": (c_i, [c_i, c_i64, c_i, c_p, c_i64, c_p, c_p]),
 }
 

@@ -13,8 +13,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from . import lib as _L
-from .lib import (BF16, F32, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc, UserHeadBwdDesc,
-                  UserHeadDesc, ItemHeadBwdDesc, ItemHeadDesc, WgradDesc, call)
+from .lib import (BF16, F32, BnBwdDesc, ConvDesc, DisAttnDesc, FoldDesc, GemmDesc, LnBwdDesc,
+                  UserHeadBwdDesc, UserHeadDesc, ItemHeadBwdDesc, ItemHeadDesc, WgradDesc, call)
 
 Tensor = torch.Tensor
 # Dropout spec: (p, seed) where seed is a 1-element int64 DEVICE tensor holding the 64-bit
@@ -851,11 +851,17 @@ def infonce_fwd_pre(user_idx: Optional[Tensor], inv_tau: float, u_hat: Tensor, i
 
 def infonce_bwd(u_hat: Tensor, i_hat: Tensor, norms: Tensor, logits: Tensor, lse: Tensor,
                 user_idx: Optional[Tensor], inv_tau: float, dloss: Optional[Tensor], du: Tensor,
-                di: Tensor, ws: Tensor, du16: Optional[Tensor] = None):
-    """du16 (bf16 [B, D], optional): a bf16 copy of du from the same launch."""
+                di: Tensor, ws: Tensor, du16: Optional[Tensor] = None, fused_finish: bool = True):
+    """du16 (bf16 [B, D], optional): a bf16 copy of du from the same launch.  fused_finish:
+    the normalise backward runs inside the logit-gradient launch (ttmi_infonce_bwd_fused)."""
     B, D = u_hat.shape
     if du16 is not None and (du16.dtype != torch.bfloat16 or du16.shape != du.shape):
         raise ValueError("infonce_bwd: du16 must be bf16 shaped like du")
+    if fused_finish:      # one launch: the split partials are summed by the last arriver (ABI 18)
+        cnt = _zero_ws("ttmi_infonce_bwd_counter_bytes", (B,), u_hat.device)
+        call("ttmi_infonce_bwd_fused", B, D, _p(u_hat), _p(i_hat), _p(norms), _p(logits), _p(lse),
+             _p(user_idx), inv_tau, _p(dloss), _p(du), _p(di), _p(du16), _p(ws), _p(cnt), _s())
+        return
     call("ttmi_infonce_bwd16", B, D, _p(u_hat), _p(i_hat), _p(norms), _p(logits), _p(lse),
          _p(user_idx), inv_tau, _p(dloss), _p(du), _p(di), _p(du16), _p(ws), _s())
 
@@ -999,24 +1005,63 @@ def mha_q1_fwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, B: int, L: int, H: 
     return ctx
 
 
+def _q1_batch_check(who: str, B: int, L: int, H: int, drop: Drop) -> None:
+    """The one-query kernels index dropout masks in 32 bits: with dropout on, B·H·L² < 2^32."""
+    if float(drop[0]) > 0 and B * H * L * L >= 1 << 32:
+        raise ValueError(f"{who}: with attention dropout on, batch {B} x {H} heads x L={L} exceeds the "
+                         f"32-bit mask index (B*H*L*L < 2^32); split the batch")
+
+
 def mha_q1_gather_fwd(qkv: Tensor, key_valid: Tensor, x: Tensor, rows: Tensor, x_rows: Tensor,
-                      B: int, L: int, H: int, ctx: Tensor, lse: Tensor, drop: Drop = NO_DROP) -> Tensor:
+                      B: int, L: int, H: int, ctx: Tensor, lse: Tensor, drop: Drop = NO_DROP,
+                      co_item: Optional[ItemHeadDesc] = None) -> Tensor:
     """last_rows_gather + mha_q1_fwd in one launch: rows[b] = the last valid row of sequence b
-    (right padding), x_rows[b] = x[rows[b]], ctx[b] = its one-query attention."""
+    (right padding), x_rows[b] = x[rows[b]], ctx[b] = its one-query attention.  ``co_item``
+    (item_head_desc): the item head's stage A runs on the same grid (ABI 18)."""
     _dev(qkv, key_valid, x, rows, x_rows, ctx, lse)
     D = qkv.shape[1] // 3
     if x.dtype != torch.float32 or x.shape[1] != D or x_rows.shape != (B, D) or rows.dtype != torch.int32:
         raise TypeError("mha_q1_gather_fwd: x / x_rows fp32 [*, D], rows int32 [B]")
-    call("ttmi_mha_q1_gather_fwd", code(qkv.dtype), B, L, H, D // H, _p(qkv), _p(key_valid), _p(x),
-         _p(rows), _p(x_rows), float(drop[0]), _p(drop[1]), _p(ctx), _p(lse), _s())
+    _q1_batch_check("mha_q1_gather_fwd", B, L, H, drop)
+    args = (code(qkv.dtype), B, L, H, D // H, _p(qkv), _p(key_valid), _p(x), _p(rows), _p(x_rows),
+            float(drop[0]), _p(drop[1]), _p(ctx), _p(lse))
+    if co_item is None:
+        call("ttmi_mha_q1_gather_fwd", *args, _s())
+    else:
+        call("ttmi_mha_q1_gather_item_fwd", *args, ctypes.byref(co_item), _s())
     return ctx
 
 
+def bn_bwd_desc(dy: Tensor, z: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, y: Tensor,
+                dz: Tensor, dw: Tensor, db: Tensor, *, gate_scale: float = 1.0, gated: bool = True,
+                dz16: Optional[Tensor] = None) -> BnBwdDesc:
+    """ttmi_bn_bwd_desc of a batchnorm_bwd call (the caller keeps the tensors alive)."""
+    _dev(dy, z, w, mean, rstd, y, dz, dw, db, dz16)
+    if dz16 is not None and dz16.dtype != torch.bfloat16:
+        raise ValueError("bn_bwd_desc: dz16 must be bf16")
+    d = BnBwdDesc()
+    d.dtype, (d.B, d.C) = code(y.dtype), z.shape
+    d.dy, d.z, d.w, d.mean, d.rstd, d.y = _p(dy), _p(z), _p(w), _p(mean), _p(rstd), _p(y)
+    d.gate_scale, d.gated = gate_scale, int(gated)
+    d.dz, d.dw, d.db, d.dz16 = _p(dz), _p(dw), _p(db), _p(dz16)
+    return d
+
+
+def bn_bwd_run(d: BnBwdDesc) -> None:
+    """ttmi_batchnorm_bwd from a bn_bwd_desc (its own launch)."""
+    call("ttmi_batchnorm_bwd", d.dtype, d.B, d.C, d.dy, d.z, d.w, d.mean, d.rstd, d.y, d.gate_scale,
+         d.gated, d.dz, d.dw, d.db, d.dz16, _s())
+
+
 def mha_q1_bwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, lse: Tensor, dctx: Tensor, B: int,
-               L: int, H: int, dqkv: Tensor, drop: Drop = NO_DROP):
+               L: int, H: int, dqkv: Tensor, drop: Drop = NO_DROP, bn: Optional[BnBwdDesc] = None):
+    """One-query attention backward; ``bn`` (bn_bwd_desc): the item head's BatchNorm1d backward
+    runs on the same grid (ttmi_mha_q1_bnr_bwd, ABI 18)."""
     Dh = qkv.shape[1] // (3 * H)
-    call("ttmi_mha_q1_bwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(rows),
-         _p(lse), _p(dctx), float(drop[0]), _p(drop[1]), _p(dqkv), _s())
+    _q1_batch_check("mha_q1_bwd", B, L, H, drop)
+    call("ttmi_mha_q1_bnr_bwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(rows),
+         _p(lse), _p(dctx), float(drop[0]), _p(drop[1]), _p(dqkv),
+         ctypes.byref(bn) if bn is not None else None, _s())
     return dqkv
 
 
@@ -1117,7 +1162,7 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
                   P: Dict[str, Tensor], pre: str, gender: Tensor, country: Tensor, eps: float,
                   drops: Tuple[Drop, Drop, Drop], out: Dict[str, Tensor],
                   co_item: Optional[ItemHeadDesc] = None,
-                  normed: Optional[Tuple[Tensor, Tensor]] = None) -> None:
+                  normed: Optional[Tuple[Tensor, Tensor]] = None, co_stage: str = "A") -> None:
     """The user tower head in one launch (ttmi_user_head_fwd): the pruned last layer's
     out-proj + residual + norm2 + FFN on the gathered rows, the demographic concat and the
     fusion MLP.  ``pre`` is the last layer's parameter prefix; ``out`` holds x1, a2, m2, r2, h,
@@ -1146,8 +1191,10 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
         d.u_hat, d.u_norm = _p(normed[0]), _p(normed[1])
     if co_item is None:
         call("ttmi_user_head_fwd", ctypes.byref(d), _s())
-    else:      # item head stage A on the CUs the 16-row user blocks leave idle (ABI 15)
+    elif co_stage == "A":      # item head stage A on the CUs the 16-row user blocks leave idle
         call("ttmi_user_item_head_fwd", ctypes.byref(d), ctypes.byref(co_item), _s())
+    else:                      # stage C (stage A ran beside the one-query attention, ABI 18)
+        call("ttmi_user_item_head_fwd_c", ctypes.byref(d), ctypes.byref(co_item), _s())
 
 
 def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: Dict[str, Tensor],
