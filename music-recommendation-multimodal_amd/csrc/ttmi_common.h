@@ -245,6 +245,35 @@ TTMI_DEV uint32_t lds_addr(const void* p) {
 }
 
 
+// ---------------------------------------------------------------- phase stamps (diagnostic builds)
+// Built with -DTTMI_STAMP (tools/stamp_build.sh; never the shipped library): lane 0 of each
+// wave records s_memrealtime (100 MHz) at named phases of an instrumented kernel into
+// ttmi_stamps[block][wave][phase]; ttmi_dbg_stamps() copies them out.
+constexpr int TTMI_STAMP_BLOCKS = 512, TTMI_STAMP_WAVES = 16, TTMI_STAMP_PHASES = 8;
+#ifdef TTMI_STAMP
+// one array per translation unit (no relocatable device code); TTMI_STAMP_DUMP(tu) defines
+// that unit's host copy-out, extern "C" ttmi_dbg_stamps_<tu>(uint64_t* host, int64_t n)
+static __device__ uint64_t ttmi_stamps[TTMI_STAMP_BLOCKS * TTMI_STAMP_WAVES * TTMI_STAMP_PHASES];
+#define TTMI_STAMP_DUMP(tu)                                                                    \
+  extern "C" int ttmi_dbg_stamps_##tu(uint64_t* host, int64_t n) {                             \
+    const int64_t tot = (int64_t)TTMI_STAMP_BLOCKS * TTMI_STAMP_WAVES * TTMI_STAMP_PHASES;      \
+    if (!host || n < tot) return TTMI_ERR_ARG;                                                 \
+    if (hipDeviceSynchronize() != hipSuccess) return TTMI_ERR_LAUNCH;                           \
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ttmi_stamps), tot * 8) != hipSuccess) return TTMI_ERR_LAUNCH; \
+    static uint64_t zero[TTMI_STAMP_BLOCKS * TTMI_STAMP_WAVES * TTMI_STAMP_PHASES];            \
+    return hipMemcpyToSymbol(HIP_SYMBOL(ttmi_stamps), zero, tot * 8) == hipSuccess ? TTMI_OK : TTMI_ERR_LAUNCH; \
+  }
+#define TTMI_TSTAMP(ph)                                                                        \
+  do {                                                                                         \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < TTMI_STAMP_BLOCKS)                             \
+      ttmi_stamps[((int)blockIdx.x * TTMI_STAMP_WAVES + (int)(threadIdx.x >> 6)) * TTMI_STAMP_PHASES + (ph)] = \
+          __builtin_amdgcn_s_memrealtime();                                                   \
+  } while (0)
+#else
+#define TTMI_TSTAMP(ph) do {} while (0)
+#define TTMI_STAMP_DUMP(tu)
+#endif
+
 // ---------------------------------------------------------------- host-side error plumbing
 void ttmi_set_error(const char* fmt, ...);
 #define TTMI_REQUIRE(cond, ...)                      \

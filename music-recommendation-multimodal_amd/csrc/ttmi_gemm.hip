@@ -510,19 +510,29 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
   float* sbias = reinterpret_cast<float*>(smem + N * WP);     // bias, or the LN weight
   float* sdw = sbias + N;                                       // LNB: per-wave dw / db sums
   float* sdb = sdw + SROWS * N;                                 // LNF: LN weight / bias
+  TTMI_TSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rwave = wave / CS, cg0 = (wave % CS) * CGW;      // row-tile slot, first column group
   const int li = lane & 15, lg = lane >> 4;
   const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
   const int64_t tile_end = std::min<int64_t>((g.M + 15) / 16, tile_beg + tiles_per_wg);
   const int64_t tile0 = tile_beg + rwave;
-  uint4 a0[4];                       // this wave's first A fragments, in flight under the W load
-  {                                  // (rows clamped into range: unconditional loads)
-    const int64_t m = std::min<int64_t>(tile0 * 16 + li, g.M - 1);
+  // A fragments.  K <= 256 (AFULL): the wave's whole first tile of A (16 rows x K: KC 16-byte
+  // fragments per lane) is loaded BEFORE the W staging and stays in registers across the column
+  // groups (QKV 11.7 -> 10.7 us, FFN1 15.6 -> ~14.5 us in the cfg-2 step).  K >= 384: one k group
+  // (4 fragments) in flight ahead of the MFMAs; loading the whole A row up front there measured
+  // slower (FFN1 dgrad + LN 21.0 -> 22.4 us): the extra 16 KB per wave competes with the W image
+  // for the CU's ingest and the MFMA phase stays LDS / issue bound (tools/stamp_phases.py).
+  constexpr bool AFULL = KC <= 8;
+  constexpr int AR = AFULL ? KC : 4;
+  uint4 af[AR];
+  auto load_af = [&](int64_t tile) {   // rows clamped into range: unconditional loads
+    const int64_t m = std::min<int64_t>(tile * 16 + li, g.M - 1);
     const char* ap = g.A + (m * g.lda + lg * (K / 4)) * 2;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) a0[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
-  }
+    for (int c = 0; c < AR; ++c) af[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
+  };
+  load_af(tile0);
   if (g.wdma) {
     // W -> LDS by LDS-DMA, every chunk in flight at once (no VGPR round trip): the image is
     // a run of 16-byte chunks, K/8 + 1 per row (the last one is the row pad, filled with the
@@ -581,25 +591,22 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
   }
   const DropKeys dk = resolve_drop(g.drop);
   const DropKeys dk2 = resolve_drop(ln.drop);
+  TTMI_TSTAMP(1);
   if (g.wdma) wait_vm<0>();          // this wave's W DMAs landed (the barrier covers the rest)
   __syncthreads();
+  TTMI_TSTAMP(2);
+  bool first_tile = true;
 
   // W fragment base for this lane (column-paired: tile 2p slot 4q+r <-> column 32p+8q+r)
   const int wrow = 8 * (li >> 2) + (li & 3);
-  // A fragments run one k group ahead, across column groups and across tiles: group cq+1's
-  // loads (or the next column group's / next tile's first group) are in flight under group
-  // cq's MFMAs and the epilogue, so no tile starts with an exposed memory latency
-  uint4 a[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) a[c] = a0[c];
   for (int64_t tile = tile_beg + rwave; tile < tile_end; tile += 8) {
     const int64_t m = tile * 16 + li;
     const bool mok = m < g.M;
     const char* ap = g.A + (std::min<int64_t>(m, g.M - 1) * g.lda + lg * (K / 4)) * 2;
     // the next tile's rows (clamped: past the last tile the prefetch is a harmless re-load)
     const char* ap_next = g.A + (std::min<int64_t>(m + 128, g.M - 1) * g.lda + lg * (K / 4)) * 2;
-    // column groups of 128 (8 MFMA tiles) and k groups of 4 chunks keep the accumulator,
-    // A and W fragment state bounded (A re-reads per column group hit L1/L2)
+    if (AFULL && !first_tile) load_af(tile);   // (one tile per wave at M = 25,600)
+    // column groups of 128 (8 MFMA tiles) keep the accumulator and W fragment state bounded
 #pragma unroll 1
     for (int cg = cg0; cg < cg0 + CGW; ++cg) {
       f32x4_t acc[8];
@@ -608,23 +615,43 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
       const char* wb = smem + (cg * 128 + wrow) * WP + lg * (K / 2);
       LnBwdRow pre;
       if constexpr (LNB) panel_ln_bwd_load(ln, m, g.M, lg, pre);
-#pragma unroll 1
-      for (int cq = 0; cq < KC / 4; ++cq) {
-        uint4 an[4];
-        const char* src = cq + 1 < KC / 4 ? ap + 64 * (cq + 1) : (cg + 1 < cg0 + CGW ? ap : ap_next);
+      if constexpr (AFULL) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const uint4*>(src + 16 * c);
+        for (int cq = 0; cq < KC / 4; ++cq) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+          for (int c = 0; c < 4; ++c) {
 #pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const uint4 wf = lds16(wb + (32 * (t >> 1) + 4 * (t & 1)) * WP + 64 * cq + 16 * c);
-            Mma<bf16_t>::run(acc[t], wf, a[c]);
+            for (int t = 0; t < 8; ++t) {
+              const uint4 wf = lds16(wb + (32 * (t >> 1) + 4 * (t & 1)) * WP + 64 * cq + 16 * c);
+              Mma<bf16_t>::run(acc[t], wf, af[4 * cq + c]);
+            }
+            // bound the scheduler's window to one 16-byte k chunk: hoisting every W fragment
+            // read of the unrolled loop ahead of the MFMAs spilled
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
+      } else {
+        // k groups of 4 fragments, the next group's (or the next column group's / next tile's
+        // first group's) loads in flight under this group's MFMAs
+#pragma unroll 1
+        for (int cq = 0; cq < KC / 4; ++cq) {
+          uint4 an[4];
+          const char* src = cq + 1 < KC / 4 ? ap + 64 * (cq + 1) : (cg + 1 < cg0 + CGW ? ap : ap_next);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) a[c] = an[c];
+          for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const uint4*>(src + 16 * c);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const uint4 wf = lds16(wb + (32 * (t >> 1) + 4 * (t & 1)) * WP + 64 * cq + 16 * c);
+              Mma<bf16_t>::run(acc[t], wf, af[c]);
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) af[c] = an[c];
+        }
       }
+      if (first_tile && cg == cg0) TTMI_TSTAMP(3);
       if constexpr (LNB) {
         panel_ln_bwd_epilogue(g, ln, acc, m, mok, li, lg, sbias, sdw + wave * N, sdb + wave * N, dk2, pre);
         continue;
@@ -716,7 +743,10 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
         }
       }
     }
+    if (first_tile) TTMI_TSTAMP(4);
+    first_tile = false;
   }
+  TTMI_TSTAMP(5);
   if constexpr (LNB) {
     __syncthreads();
     for (int i = tid; i < N; i += NTH) {
@@ -733,6 +763,7 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
       }
     }
   }
+  TTMI_TSTAMP(6);
 }
 
 // ------------------------------------------------------------ weight-gradient GEMM (bf16)
@@ -2328,3 +2359,5 @@ extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int 
   if (rc) return rc;
   return wgrad_fold_impl(n, descs, nf, folds, stream, true);
 }
+
+TTMI_STAMP_DUMP(gemm)

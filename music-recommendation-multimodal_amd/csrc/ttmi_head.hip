@@ -405,11 +405,8 @@ __global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
   item_c_body(a, blockIdx.x, L);
 }
 
-#ifdef HEAD_STAMP
-#define STAMP(i) do { if (threadIdx.x == 0) stamp[i] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define STAMP(i) do {} while (0)
-#endif
+// phase stamps of the diagnostic build (ttmi_common.h TTMI_TSTAMP; tools/stamp_build.sh)
+#define STAMP(i) TTMI_TSTAMP(i)
 
 // Each stage's weight fragments are loaded one stage ahead.  (Loading every stage's weights
 // at the start, with the whole register file, measured slower: the ~360 KB of weights a
@@ -417,9 +414,6 @@ __global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
 // and vmcnt retires in order, so the first stage then waited for all of them.)
 template <int F>
 __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
-#ifdef HEAD_STAMP
-  uint64_t stamp[8];
-#endif
   STAMP(0);
   __shared__ __attribute__((aligned(16))) HeadLds L;
   __shared__ __attribute__((aligned(16))) HeadParams Q;
@@ -604,12 +598,7 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
       *reinterpret_cast<float4*>(a.u + (int64_t)m * HD + n) = make_float4(uo[t][0], uo[t][1], uo[t][2], uo[t][3]);
   }
   row_l2norm(uo, a.uhat, a.unrm, m, mrow, n0, L, w, lane);
-#ifdef HEAD_STAMP
-  __syncthreads();
   STAMP(6);
-  if (threadIdx.x == 0 && blockIdx.x < 4)
-    for (int i = 1; i < 7; ++i) a.rz[blockIdx.x * 8 + i] = (float)(stamp[i] - stamp[0]);
-#endif
 }
 
 // ------------------------------------------------------------------------------ backward
@@ -750,9 +739,6 @@ __global__ __launch_bounds__(256) void item_head_bwd_c_kernel(ItemBwdArgs a) {
 
 template <int F>
 __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
-#ifdef HEAD_STAMP
-  uint64_t stamp[8];
-#endif
   STAMP(0);
   __shared__ __attribute__((aligned(16))) HeadBwdLds L;
   if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head backward (rows)
@@ -951,12 +937,7 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
       fx_add(isg ? a.dG + (int64_t)key[r] * a.dg + k : a.dC + (int64_t)key[r] * a.dc + k, sum, TTMI_FX_GRAD);
     }
   }
-#ifdef HEAD_STAMP
-  __syncthreads();
   STAMP(7);
-  if (threadIdx.x == 0 && blockIdx.x < 4)
-    for (int i = 1; i < 8; ++i) a.dx1[blockIdx.x * 8 + i] = (float)(stamp[i] - stamp[0]);
-#endif
 }
 
 // ------------------------------------------------------------------------------ item head
@@ -1216,3 +1197,5 @@ extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const t
 extern "C" int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t s) {
   return ttmi_user_item_head_bwd(d, nullptr, s);
 }
+
+TTMI_STAMP_DUMP(head)

@@ -286,8 +286,13 @@ class TrainStep:
     def __init__(self, model: TwoTowerModel, lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.01, use_graph: bool = True,
                  seed: int = 0, group=None, broadcast_buffers: bool = True,
-                 overlap_grad_sync: bool = True):
+                 overlap_grad_sync: bool = True, grad_sink: bool = True):
         self.model = model
+        # grad_sink (one process only): the [V, D] item-embedding gradient stays in its int64
+        # fixed-point accumulator and AdamW reads it there (a 31 MB conversion pass saved), so
+        # its slot of flat.grad reads ZERO between backward and update.  Anything that must see
+        # complete gradients there (clipping, norms, hooks) needs grad_sink=False.
+        self.grad_sink = grad_sink
         model.train()
         dev = next(model.parameters()).device
         self.device = dev
@@ -547,7 +552,7 @@ class TrainStep:
         # one process: the item-embedding gradient goes from its fixed-point accumulator
         # straight into AdamW (no fold pass over the [V, D] table); with DDP it is folded
         # into the flat gradient for the all-reduce
-        self._fwd_bwd(b, cut, fx_sink=self.world == 1)
+        self._fwd_bwd(b, cut, fx_sink=self.world == 1 and self.grad_sink)
         if self.broadcast_buffers:             # rank 0 contributes its buffers, others zeros
             ops.batch_copy([self.flat.grad_extra], [self.fbufs.data if self.is_root else self.bzero])
         if self.world > 1:

@@ -222,3 +222,27 @@ def test_infonce_bwd_fused_finish_equals_two_launch(gpu_pkg, B, D):
             for a, b in zip(o, outs[0]):
                 assert torch.equal(a, b)
         assert rel(outs[0][0], outs[0][0]) == 0.0
+
+
+def test_trainstep_grad_sink_off_is_bit_identical(gpu_pkg):
+    """TrainStep(grad_sink=False) folds the item-embedding gradient into flat.grad (complete
+    gradients between backward and update, for clipping / norms / hooks) and must update the
+    parameters bit-identically to the default sink (AdamW converting the fixed-point
+    accumulator itself)."""
+    from oracle import two_tower_ref as ref
+    B, L, V, D = 64, 20, 301, 128
+    outs = []
+    for sink in (True, False):
+        torch.manual_seed(3)
+        m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128,
+                                  num_genders=3, num_countries=16, max_seq_len=L, user_embedding_dim=D,
+                                  item_embedding_dim=D, user_dropout=0.1,
+                                  compute_dtype=torch.bfloat16).to(DEV)
+        step = gpu_pkg.TrainStep(m, lr=1e-3, grad_sink=sink, seed=5)
+        for s in range(2):
+            b = ref.synthetic_batch(B, L, V, 3, 16, generator=torch.Generator().manual_seed(70 + s))
+            step.step({k: v.to(DEV) for k, v in b.items()})
+        torch.cuda.synchronize()
+        outs.append({k: v.detach().clone() for k, v in m.named_parameters()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k

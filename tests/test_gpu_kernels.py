@@ -348,7 +348,8 @@ def masks(B, L, g):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (3, 1, 4, 16),
-                                      (4, 65, 2, 32), (3, 200, 4, 32), (2, 130, 2, 64), (2, 512, 1, 8)])
+                                      (4, 65, 2, 32), (3, 200, 4, 32), (2, 130, 2, 64), (2, 512, 1, 8),
+                                      (3, 128, 4, 32), (3, 512, 4, 32)])
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
     ops = gpu_pkg.ops
@@ -377,7 +378,7 @@ def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (5, 150, 4, 32),
-                                      (3, 300, 2, 64)])
+                                      (3, 300, 2, 64), (4, 65, 4, 32), (4, 128, 4, 32), (3, 512, 4, 32)])
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_mha_single_query_matches_full_row(gpu_pkg, dtype, B, L, H, Dh, p):
     """ttmi_mha_q1_* (pruned last layer) == the full attention restricted to each
@@ -529,6 +530,43 @@ def test_seq_embed_fwd_bwd(gpu_pkg, p, deferred):
     assert rel(dP, Pt.grad) < 5e-5
     assert rel(dw, wt.grad) < 5e-5
     assert rel(db, bt.grad) < 5e-5
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-3, 1e-6])
+def test_seq_embed_bwd_fixed_point_range(gpu_pkg, scale):
+    """The embedding-row scatter adds in int64 fixed point (2^-36 per unit, TTMI_FX_GRAD_SHIFT;
+    order-independent, so the sum is bit-reproducible).  Each adder is rounded once, so the
+    error bound is absolute: |dE - dE_fp64| <= count(row) * 2^-37 + fp32 rounding, whatever the
+    gradient's magnitude.  With the upstream gradient scaled down to 1e-6 (element gradients
+    ~1e-8) that is still ~1e-3 relative; the test states the bound per element and checks it
+    against a float64 reference (small-gradient regime)."""
+    ops = gpu_pkg.ops
+    B, L, D, V = 64, 50, 128, 97
+    g = torch.Generator().manual_seed(31)
+    ids = torch.randint(0, V, (B, L), generator=g)
+    E = torch.randn(V, D, generator=g)
+    P = torch.randn(L, D, generator=g)
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    Et = E.double().clone().requires_grad_(True)
+    x_ref = TF.layer_norm(TF.embedding(ids, Et, padding_idx=0) + P.double()[None], (D,), w.double(),
+                          b.double(), 1e-5)
+    dx = torch.randn(B * L, D, generator=g) * scale
+    x_ref.reshape(B * L, D).backward(dx.double())
+    x = torch.empty(B * L, D, device=DEV)
+    mean, rstd = torch.empty(B * L, device=DEV), torch.empty(B * L, device=DEV)
+    Ed = E.to(DEV)
+    ops.seq_embed_fwd(ids.to(DEV), Ed, P.to(DEV), w.to(DEV), b.to(DEV), x, mean, rstd)
+    dE = torch.zeros(V, D, device=DEV)
+    dP, dw, db = torch.zeros(L, D, device=DEV), torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ops.seq_embed_bwd(ids.to(DEV), Ed, P.to(DEV), w.to(DEV), mean, rstd, dx.to(DEV), dE, dP, dw, db,
+                      padding_idx=0)
+    cnt = torch.bincount(ids.reshape(-1), minlength=V).double()[:, None]
+    ref = Et.grad
+    err = (dE.cpu().double() - ref).abs()
+    bound = cnt * 2.0 ** -37 * 1.01 + 2e-6 * ref.abs().max() + 1e-7 * ref.abs()
+    assert bool((err <= bound).all()), (scale, (err - bound).max().item())
+    assert dE[0].abs().max().item() == 0.0
 
 
 # ------------------------------------------------------------------------------ batchnorm
