@@ -9,8 +9,20 @@ support does not cover every collective; the arithmetic and the rank order are t
 * ``reduce_scatter_sum(out, inp)`` — out = Σ_ranks inp[rank·n : (rank+1)·n] (owner's slice).
 * ``all_reduce_sum(t, async_op)`` — in place; returns the work handle when ``async_op``.
 * ``broadcast(t, src)`` — in place.
+
+A staged ``all_reduce_sum(..., async_op=True)`` does not block the caller: an event recorded on
+the current stream orders a device→pinned-host copy on a side stream; one worker thread per
+process waits for that copy and runs the gloo reduction; ``wait()`` joins it and queues the
+host→device copy on the caller's current stream.  The worker is FIFO, so ranks that issue
+their buckets in the same order reduce them in the same order; every other helper (and a
+synchronous all-reduce) first drains the pending staged work, so no collective overtakes one
+already issued.  This is what makes the overlap of the gradient all-reduce with the rest of the
+backward real under gloo (TrainStep's layer-1 cut, train.py GradSync).
 """
 from __future__ import annotations
+
+import concurrent.futures
+import threading
 
 import torch
 import torch.distributed as dist
@@ -32,13 +44,103 @@ def _staged(t: Tensor, group) -> bool:
 
 
 class _HostWork:
-    """Completed-work stand-in for staged (synchronous) collectives."""
+    """Completed-work stand-in (world size 1)."""
 
     def wait(self) -> bool:
         return True
 
 
+class _Stager:
+    """The asynchronous gloo staging of device tensors (module docstring).  Pinned host
+    buffers are cached per (device pointer, bytes): a bucket's buffer is reused every step."""
+
+    def __init__(self):
+        self.pool = None
+        self.lock = threading.Lock()
+        self.pending = []
+        self.host = {}
+        self.side = {}
+
+    def _executor(self):
+        if self.pool is None:
+            self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=1,
+                                                              thread_name_prefix="ttmi-gloo")
+        return self.pool
+
+    def _buffer(self, t: Tensor) -> Tensor:
+        key = (t.data_ptr(), t.numel(), t.dtype)
+        h = self.host.get(key)
+        if h is None:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=t.is_cuda and torch.cuda.is_available())
+            self.host[key] = h
+        return h.view(t.shape)
+
+    def all_reduce(self, t: Tensor, group) -> "_StagedWork":
+        h = self._buffer(t)
+        ev = None
+        if t.is_cuda:
+            ready = torch.cuda.Event()
+            ready.record()                                   # the gradient slice is final here
+            side = self.side.get(t.device)
+            if side is None:
+                side = self.side[t.device] = torch.cuda.Stream(device=t.device)
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                h.copy_(t, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+        else:
+            h.copy_(t)
+
+        def run():
+            if ev is not None:
+                ev.synchronize()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        w = _StagedWork(self, t, h, self._executor().submit(run))
+        with self.lock:
+            self.pending.append(w)
+        return w
+
+    def drain(self) -> None:
+        with self.lock:
+            works, self.pending = self.pending, []
+        for w in works:
+            w.wait()
+
+
+class _StagedWork:
+    def __init__(self, stager: _Stager, t: Tensor, h: Tensor, fut):
+        self.stager, self.t, self.h, self.fut = stager, t, h, fut
+        self.done = False
+
+    def is_completed(self) -> bool:
+        return self.done or self.fut.done()
+
+    def wait(self) -> bool:
+        if self.done:
+            return True
+        self.fut.result()                                    # re-raises a failed reduction
+        # ordered on the caller's stream ahead of every later consumer; the pinned buffer is
+        # only rewritten by a later start, whose copy waits for an event recorded after this
+        self.t.copy_(self.h, non_blocking=self.t.is_cuda)
+        self.done = True
+        with self.stager.lock:
+            if self in self.stager.pending:
+                self.stager.pending.remove(self)
+        return True
+
+
+_STAGER = _Stager()
+
+
+def drain() -> None:
+    """Complete every pending staged all-reduce (in issue order)."""
+    if _STAGER.pending:
+        _STAGER.drain()
+
+
 def all_gather_into(out: Tensor, inp: Tensor, group=None) -> None:
+    drain()
     if world_size(group) == 1:
         out.copy_(inp)
         return
@@ -51,6 +153,7 @@ def all_gather_into(out: Tensor, inp: Tensor, group=None) -> None:
 
 
 def reduce_scatter_sum(out: Tensor, inp: Tensor, group=None) -> None:
+    drain()
     if world_size(group) == 1:
         out.copy_(inp)
         return
@@ -65,15 +168,22 @@ def reduce_scatter_sum(out: Tensor, inp: Tensor, group=None) -> None:
 def all_reduce_sum(t: Tensor, group=None, async_op: bool = False):
     if world_size(group) == 1:
         return _HostWork() if async_op else None
-    if _staged(t, group):
-        h = t.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-        t.copy_(h)
-        return _HostWork() if async_op else None
+    if _staged(t, group) or (_FORCE_STAGE and async_op):
+        w = _STAGER.all_reduce(t, group)
+        if async_op:
+            return w
+        drain()
+        return None
+    drain()
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
 
 
+# tests: stage host tensors too, so the asynchronous path runs on a CPU-only gloo world
+_FORCE_STAGE = False
+
+
 def broadcast(t: Tensor, src: int = 0, group=None) -> None:
+    drain()
     if world_size(group) == 1:
         return
     if _staged(t, group):
@@ -92,4 +202,4 @@ def group_src(src: int, group=None) -> int:
 
 
 __all__ = ["world_size", "rank", "all_gather_into", "reduce_scatter_sum", "all_reduce_sum",
-           "broadcast", "group_src"]
+           "broadcast", "group_src", "drain"]

@@ -15,7 +15,10 @@ stages device tensors through the host under gloo — the arithmetic is the same
 * The bf16 product step at D = 128 (every fused head on its fused path: co-launched user /
   item heads, ``infonce_fwd_pre`` with the loss accumulator, the fused item BatchNorm, the
   overlap hook that flushes the deferred weight gradients at the layer-1 cut) with dropout
-  on, local and global negatives: run with ``overlap_grad_sync`` on and off, the flat
+  on, local and global negatives.  With the overlap on, the head buckets reduce on comm's
+  gloo worker thread (pinned-host staging on a side stream) while the second graph segment
+  runs — the concurrency is real, not a synchronous copy.  Run with ``overlap_grad_sync`` on
+  and off, the flat
   parameters, AdamW moments and BatchNorm buffers are bit-identical (the step is
   deterministic, so any flush-placement or bucket-split error shows as a bit difference),
   identical on both ranks, and the losses stay within the bf16 emulation's distance of the
