@@ -499,7 +499,9 @@ int ttmi_batch_copy(int n, void* const* dst, const void* const* src, const int64
  *   next = bf16(dropout(dx)) with keep over (drop_rows ? drop_rows[m] : m)*ld_drop + n,
  * replacing linear_dx + ttmi_layernorm_bwd + ttmi_dropout_bwd (reference
  * src/models/user_tower.py:37-45 TransformerEncoderLayer(norm_first=True) backward).
- * res / next / drop_rows / ln_dw / ln_db may be NULL.  K % 128 == 0, K <= 512. */
+ * res / next / drop_rows / ln_dw / ln_db may be NULL.  N = 128: K % 128 == 0, K <= 512.
+ * ABI 19: N = 256 (the reference's default width) with K in {256, 512, 768, 1024} (W streamed
+ * through LDS; dh and wt each under 4 GB, ln_w 16-byte aligned). */
 typedef struct ttmi_linear_ln_bwd_desc {
   int64_t M, N, K;
   const void* dh; int64_t ld_dh;        /* bf16 [M, K] */
@@ -513,17 +515,19 @@ typedef struct ttmi_linear_ln_bwd_desc {
   float drop_p; const uint64_t* drop_seed; int64_t ld_drop; const int32_t* drop_rows;
   float* ln_dw; float* ln_db;           /* [N], accumulated */
   float* sum_ws;   /* ABI 10; NULL: ln_dw / ln_db take float atomics.  Else [G][2][N] fp32 with
-                      G = ttmi_linear_ln_bwd_sum_blocks(M): each workgroup's dw row and db row,
+                      G = ttmi_linear_ln_bwd_sum_blocks_n(M, N): each workgroup's dw / db rows,
                       plain stores; ln_dw / ln_db are then left to a fold (ttmi_wgrad_fold with
                       {part = sum_ws (+ N for db), S = G, s_stride = 2N, M = 1}): deterministic. */
   const int32_t* res_rows; int64_t res_L;  /* ABI 13; non-NULL: res is [M / res_L, N] and its row
                       b is added only to row res_rows[b] (b = m / res_L), other rows get none —
                       the pruned last layer's gathered residual (replaces ttmi_scatter_add_rows) */
 } ttmi_linear_ln_bwd_desc;
-int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M);
+int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M);           /* N = 128 */
+int64_t ttmi_linear_ln_bwd_sum_blocks_n(int64_t M, int64_t N);   /* ABI 19: any supported N */
 int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream);
-/* Fused residual sub-block end + the next LayerNorm (N = 128, K % 128 == 0, K <= 512):
- *   out = residual + dropout(x · wᵀ + bias)   (fp32 [M, 128]; dropout keep index m*ld_drop + n)
+/* Fused residual sub-block end + the next LayerNorm (N = 128 with K % 128 == 0, K <= 512; ABI 19:
+ * N = 256 with K in {256, 512, 768, 1024}, x and w each under 4 GB, bias / LN params 16-byte aligned):
+ *   out = residual + dropout(x · wᵀ + bias)   (fp32 [M, N]; dropout keep index m*ld_drop + n)
  *   y = bf16(LN(out) * ln_w + ln_b), mean / rstd = the row statistics
  * i.e. TransformerEncoderLayer(norm_first=True)'s `x = x + dropout(out_proj(...))` followed by
  * norm2(x) (or `x = x + dropout(linear2(...))` followed by the next layer's norm1(x)), the
@@ -813,6 +817,14 @@ int ttmi_mha_q1_gather_item_fwd(int dtype, int B, int L, int H, int Dh, const vo
                                 const ttmi_item_head_desc* it, hipStream_t stream);
 int ttmi_user_item_head_fwd_c(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
                               hipStream_t stream);
+/* ttmi_user_head_fwd plus BOTH item stages in one launch (ABI 18): stage A's workgroups, then
+ * stage C's, which wait inside the launch (a bounded poll of an arrival count in it->bn_cnt)
+ * until A's column-quarter mergers have published the BatchNorm statistics (handed over by
+ * write-through stores and loads).  Needs the fused statistics (B <= 512).  bn_cnt must hold
+ * ttmi_item_head_bn_counter_bytes(B) zero bytes; every call leaves them zero except the last
+ * word, which a C workgroup sets to 1 if its poll timed out (then its outputs are invalid). */
+int ttmi_user_item_head_fwd_ac(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
+                               hipStream_t stream);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
 int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStream_t stream);
 /* TextEncoder mean-pool (item_tower.py:73-80): out[b] = Σ_s m·x[b,s] / max(Σ_s m, 1e-9);

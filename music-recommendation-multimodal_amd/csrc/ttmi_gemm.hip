@@ -47,6 +47,8 @@ struct GemmArgs {
   float* rowsum_a;   // rowsum_a[m] += Σ_k A(m,k)  (bias grad of a weight-gradient GEMM)
   bf16_t* pre_out;   // act 2: the pre-activation (after bias) is also stored here (row stride ldc)
   int wdma;          // panel kernel: stage W by LDS-DMA (set by launch_panel_t)
+  int wrot;          // panel kernel: rotate the W DMA order per workgroup (TTMI_PANEL_WROT)
+  int nslice, rgroups;   // panel kernel: N split into nslice column panels over rgroups row groups
 };
 
 // Sum of the 8 bf16 / 4 f32 operand values a lane holds in one fragment.
@@ -514,7 +516,22 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rwave = wave / CS, cg0 = (wave % CS) * CGW;      // row-tile slot, first column group
   const int li = lane & 15, lg = lane >> 4;
-  const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
+  // column slices (g.nslice > 1: the output is nslice panels of N columns, one per workgroup;
+  // the slices of one row group sit on one XCD, consecutive, so its A rows are read from HBM
+  // once and from that XCD's L2 after)
+  int rg = blockIdx.x, dn0 = 0;
+  if (!(LNB || LNF) && g.nslice > 1) {
+    const int k = blockIdx.x / 8, sl = k % g.nslice;
+    rg = (k / g.nslice) * 8 + blockIdx.x % 8;
+    if (rg >= g.rgroups) return;                                  // grid padding (uniform)
+    dn0 = sl * N;
+    g.B += (int64_t)dn0 * g.ldb * 2;
+    g.C = static_cast<char*>(g.C) + (int64_t)dn0 * (g.c_f32 ? 4 : 2);
+    if (g.bias) g.bias += dn0;
+    if (g.gate) g.gate = static_cast<const char*>(g.gate) + (int64_t)dn0 * (g.gate_f32 ? 4 : 2);
+    if (g.residual) g.residual += dn0;
+  }
+  const int64_t tile_beg = (int64_t)rg * tiles_per_wg;
   const int64_t tile_end = std::min<int64_t>((g.M + 15) / 16, tile_beg + tiles_per_wg);
   const int64_t tile0 = tile_beg + rwave;
   // A fragments.  K <= 256 (AFULL): the wave's whole first tile of A (16 rows x K: KC 16-byte
@@ -542,10 +559,14 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
     const uint32_t wbytes = (uint32_t)(((int64_t)(N - 1) * g.ldb + K) * 2);
     const i32x4_t rw = make_rsrc(g.B, wbytes);
     const uint32_t base = lds_addr(smem);
+    // every workgroup fetches the same image: start each at its own point of it (a rotation
+    // of the instruction order) so the CUs of an XCD do not queue on the same L2 channel
+    const int rot = g.wrot ? (int)((blockIdx.x * 5u + blockIdx.x / 8u) % INSTR) : 0;
 #pragma unroll
     for (int t = 0; t < (INSTR + 8 * CS - 1) / (8 * CS); ++t) {
-      const int ii = wave + 8 * CS * t;
-      if (ii >= INSTR) break;                   // wave-uniform
+      const int i0 = wave + 8 * CS * t;
+      if (i0 >= INSTR) break;                   // wave-uniform
+      const int ii = i0 + rot < INSTR ? i0 + rot : i0 + rot - INSTR;
       const int q = ii * 64 + lane, n = q / CPRP, c = q % CPRP;
       const uint32_t voff = c == K / 8 ? wbytes : (uint32_t)(((int64_t)n * g.ldb + 8 * c) * 2);
       dma16(rw, voff, base + ii * 1024);
@@ -671,7 +692,7 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + n), v);
+        drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + dn0 + n), v);
         if constexpr (EPI == PE_GATE_BF16) {
           const uint4 q = *reinterpret_cast<const uint4*>((const bf16_t*)g.gate + m * g.ld_gate + n);
           const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
@@ -764,6 +785,293 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
     }
   }
   TTMI_TSTAMP(6);
+}
+
+// ------------------------------------- N = 256 LayerNorm-epilogue panels, W and A streamed
+// The D = 256 encoder (the reference's default width, user_tower.py:9) ends its residual
+// sub-blocks with GEMMs of N = 256 columns and K up to 1,024 (FFN2 forward; the QKV and FFN1
+// input grads), whose W image (up to 512 KB) does not fit in LDS.  Here:
+//  * 8 waves, one 16-row tile each (one tile group per workgroup: tiles_per_wg <= 8);
+//  * W and A stream through 3-slot LDS rings of 64-wide k chunks by LDS-DMA (W 256 rows x
+//    128 B, A 8 waves x 16 rows x 128 B per chunk), two chunks in flight under the MFMAs and
+//    one barrier per chunk.  Everything in the loop is DMA: no compiler-visible global load,
+//    so hipcc inserts no vmcnt(0) that would drain the ring (the counts are explicit);
+//  * both images are unpadded with the 16-byte pieces of row r XOR-swizzled by
+//    swz(r) = ((r >> 1) ^ r) & 7 (on the DMA source: the destination is lane-linear), which
+//    puts the 16 rows each ds_read_b128 lane group reads into distinct bank windows for the
+//    A tile and for every W column tile of the column-paired layout;
+//  * k order: lane group g of chunk ch holds k = 64 ch + 16 g + 8 c .. +7 (c < 2) of both
+//    operands; output layout and epilogues as the N = 128 panel over two column groups, the
+//    LayerNorm statistics over 256 columns (residual + LayerNorm forward, PE_RESLN; the
+//    LayerNorm backward, PE_LNBWD, its per-wave dw / db rows in a drained W slot).
+TTMI_DEV int swz8(int r) { return ((r >> 1) ^ r) & 7; }
+
+template <int KCH, int EPI>
+__global__ __launch_bounds__(512) void panel256_kernel(GemmArgs g, int tiles_per_wg, LnBwdArgs ln) {
+  constexpr int N = 256, KW = 64, K = KW * KCH;
+  constexpr int WSLOT = N * KW * 2, ASLOT = 8 * 16 * KW * 2;      // 32 KB, 16 KB
+  constexpr int WI = WSLOT / 1024 / 8, AI = 2;                     // DMA instructions per wave
+  constexpr bool LNB = EPI == PE_LNBWD;
+  static_assert(EPI == PE_LNBWD || EPI == PE_RESLN, "LayerNorm epilogues only");
+  static_assert(KCH >= 2, "K >= 128");
+  __shared__ __attribute__((aligned(16))) char smem[3 * WSLOT + 3 * ASLOT + 3 * N * 4];
+  float* sw = reinterpret_cast<float*>(smem + 3 * WSLOT + 3 * ASLOT);   // bias (RESLN) / LN w (LNBWD)
+  float* slw = sw + N;                                                // RESLN: LN weight, bias
+  float* slb = slw + N;
+  TTMI_TSTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int64_t tiles = (g.M + 15) / 16;
+  const int64_t tile_beg = (int64_t)blockIdx.x * tiles_per_wg;
+  const int64_t tile_end = std::min<int64_t>(tiles, tile_beg + tiles_per_wg);
+  const int64_t tile = tile_beg + wave;
+  const int64_t m = tile * 16 + li;
+  const bool mok = tile < tile_end && m < g.M;
+  const int64_t mc = std::min<int64_t>(m, g.M - 1);
+  // ---- DMA sources
+  const i32x4_t rw = make_rsrc(g.B, (uint32_t)(((int64_t)(N - 1) * g.ldb + K) * 2));
+  const i32x4_t ra = make_rsrc(g.A, (uint32_t)(g.M * g.lda * 2));
+  const uint32_t wbase = lds_addr(smem), abase = wbase + 3 * WSLOT + wave * (ASLOT / 8);
+  // every workgroup streams the same W: each starts at its own point of the chunk
+  const int rot = g.wrot ? (int)((blockIdx.x * 5u + blockIdx.x / 8u) % (WI * 8)) : 0;
+  uint32_t woff[WI], aoff[AI];        // chunk-0 source offsets; chunk ch adds 128 ch bytes
+#pragma unroll
+  for (int u = 0; u < WI; ++u) {
+    int ii = wave + 8 * u + rot;
+    ii = ii < WI * 8 ? ii : ii - WI * 8;
+    const int n = ii * 8 + (lane >> 3), q = (lane & 7) ^ swz8(n);
+    woff[u] = (uint32_t)(((int64_t)n * g.ldb + 8 * q) * 2);
+  }
+#pragma unroll
+  for (int u = 0; u < AI; ++u) {      // the wave's 16 rows (clamped) of A
+    const int r = u * 8 + (lane >> 3), q = (lane & 7) ^ swz8(r);
+    const int64_t row = std::min<int64_t>(tile * 16 + r, g.M - 1);
+    aoff[u] = (uint32_t)((row * g.lda + 8 * q) * 2);
+  }
+  auto stage = [&](int ch, int slot) {
+#pragma unroll
+    for (int u = 0; u < WI; ++u) {
+      int ii = wave + 8 * u + rot;
+      ii = ii < WI * 8 ? ii : ii - WI * 8;
+      dma16(rw, woff[u] + ch * KW * 2, wbase + slot * WSLOT + ii * 1024);
+    }
+#pragma unroll
+    for (int u = 0; u < AI; ++u) dma16(ra, aoff[u] + ch * KW * 2, abase + slot * ASLOT + u * 1024);
+  };
+  // the per-column parameters (1 KB each) by DMA too, ahead of chunk 0 (a compiler-visible
+  // load here would make hipcc drain every DMA before its LDS store); a null bias reads zeros
+  if (wave < (LNB ? 1 : 3)) {
+    const float* src = LNB ? ln.w : wave == 0 ? g.bias : wave == 1 ? ln.w : ln.lnb;
+    dma16(make_rsrc(src, src ? N * 4 : 0), lane * 16, lds_addr(sw + wave * N));
+  }
+  stage(0, 0);
+  stage(1, 1);
+  TTMI_TSTAMP(1);
+  // W fragment: column tile t of group cg at row n = 128 cg + 32 (t >> 1) + 4 (t & 1) + wrow;
+  // swz8(n) depends on n & 15 only, i.e. on t & 1 and the lane
+  const int wrow = 8 * (li >> 2) + (li & 3);
+  const int key[2] = {swz8(wrow), swz8(wrow + 4)};
+  const int akey = swz8(li);
+  f32x4_t acc[2][8];
+#pragma unroll
+  for (int cg = 0; cg < 2; ++cg)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[cg][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < KCH; ++ch) {
+    // this wave's chunk-ch pieces landed (ch + 1's in flight) and its LDS reads returned, then
+    // the barrier: everyone's chunk ch landed, everyone is done with ch - 1 (one asm statement,
+    // not __syncthreads, whose release fence would drain vmcnt to 0)
+    if (ch + 1 < KCH) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(WI + AI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (ch + 2 < KCH) stage(ch + 2, (ch + 2) % 3);
+    const char* ws = smem + (ch % 3) * WSLOT;
+    const char* as = smem + 3 * WSLOT + (ch % 3) * ASLOT + wave * (ASLOT / 8) + li * (KW * 2);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int q = 2 * lg + c;
+      const uint4 a = lds16(as + ((q ^ akey) << 4));
+#pragma unroll
+      for (int cg = 0; cg < 2; ++cg) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int n = 128 * cg + 32 * (t >> 1) + 4 * (t & 1) + wrow;
+          const uint4 wf = lds16(ws + n * (KW * 2) + ((q ^ key[t & 1]) << 4));
+          Mma<bf16_t>::run(acc[cg][t], wf, a);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  TTMI_TSTAMP(2);
+  // ---- epilogues: lane (li, lg) holds row li, columns 128 cg + 32 p + 8 lg + e
+  const DropKeys dk = resolve_drop(g.drop);
+  const DropKeys dk2 = resolve_drop(ln.drop);
+  if constexpr (!LNB) {
+    float vr[64];
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int n = 128 * cg + 32 * p + 8 * lg;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = g.alpha * acc[cg][2 * p][e] + sw[n + e];
+          v[4 + e] = g.alpha * acc[cg][2 * p + 1][e] + sw[n + 4 + e];
+        }
+        drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + n), v);
+        const float* rp = g.residual + mc * g.ld_res + n;
+        const float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
+        v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+        v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+        if (mok) {
+          float* cp = reinterpret_cast<float*>(g.C) + m * g.ldc + n;
+          *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vr[32 * cg + 8 * p + e] = v[e];
+      }
+    }
+    float s1 = 0.f;                    // two-pass mean / variance over the 256 columns (ln_fwd)
+#pragma unroll
+    for (int e = 0; e < 64; ++e) s1 += vr[e];
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    const float mu = s1 * (1.f / 256.f);
+    float s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) s2 += (vr[e] - mu) * (vr[e] - mu);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const float rs = 1.f / sqrtf(s2 * (1.f / 256.f) + ln.eps);
+    if (mok) {
+#pragma unroll
+      for (int cg = 0; cg < 2; ++cg) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int n = 128 * cg + 32 * p + 8 * lg;
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (vr[32 * cg + 8 * p + e] - mu) * rs * slw[n + e] + slb[n + e];
+          uint4 qv;
+          qv.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+          qv.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+          qv.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+          qv.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+          *reinterpret_cast<uint4*>(ln.y + m * ln.ldy + n) = qv;
+        }
+      }
+      if (lg == 0) {
+        ln.mean_out[m] = mu;
+        ln.rstd_out[m] = rs;
+      }
+    }
+  } else {
+    const float mu = mok ? ln.mean[mc] : 0.f, rs = mok ? ln.rstd[mc] : 0.f;
+    int64_t rr = mc;
+    bool rhit = ln.res != nullptr;
+    if (ln.res && ln.res_rows) {
+      rr = mc / ln.res_L;
+      rhit = (int64_t)ln.res_rows[rr] == mc;
+    }
+    float dy[64], xh[64];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int n = 128 * cg + 32 * p + 8 * lg;
+        const float4 x0 = *reinterpret_cast<const float4*>(ln.x + mc * ln.ldx + n);
+        const float4 x1 = *reinterpret_cast<const float4*>(ln.x + mc * ln.ldx + n + 4);
+        const float xr[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = mok ? g.alpha * (e < 4 ? acc[cg][2 * p][e] : acc[cg][2 * p + 1][e - 4]) : 0.f;
+          const float h = mok ? (xr[e] - mu) * rs : 0.f;
+          const float gg = d * sw[n + e];
+          dy[32 * cg + 8 * p + e] = d;
+          xh[32 * cg + 8 * p + e] = h;
+          s1 += gg;
+          s2 += gg * h;
+        }
+      }
+    }
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const float c1 = s1 * (1.f / 256.f), c2 = s2 * (1.f / 256.f);
+    const int64_t drow = ln.drop_rows ? (int64_t)ln.drop_rows[mc] : m;
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int n = 128 * cg + 32 * p + 8 * lg;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          o[e] = rs * (dy[32 * cg + 8 * p + e] * sw[n + e] - c1 - xh[32 * cg + 8 * p + e] * c2);
+        if (ln.res) {
+          const float4 r0 = *reinterpret_cast<const float4*>(ln.res + rr * ln.ld_res + n);
+          const float4 r1 = *reinterpret_cast<const float4*>(ln.res + rr * ln.ld_res + n + 4);
+          if (rhit) {
+            o[0] += r0.x; o[1] += r0.y; o[2] += r0.z; o[3] += r0.w;
+            o[4] += r1.x; o[5] += r1.y; o[6] += r1.z; o[7] += r1.w;
+          }
+        }
+        if (mok) {
+          float* dp = ln.dx + m * ln.lddx + n;
+          *reinterpret_cast<float4*>(dp) = make_float4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<float4*>(dp + 4) = make_float4(o[4], o[5], o[6], o[7]);
+          if (ln.next) {
+            drop_apply_vec<8>(dk2, (uint32_t)(drow * ln.ld_drop + n), o);
+            uint4 qv;
+            qv.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+            qv.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+            qv.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+            qv.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+            *reinterpret_cast<uint4*>(ln.next + m * ln.ld_next + n) = qv;
+          }
+        }
+      }
+    }
+    // dw / db: the tile's 16 rows summed per column (one DPP row), stored into this wave's
+    // own row of a drained W slot (the last iteration's barrier retired every read of it),
+    // then the waves' rows summed in wave order: deterministic, no atomics
+    float* srow = reinterpret_cast<float*>(smem + ((KCH + 1) % 3) * WSLOT) + wave * 2 * N;
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = 32 * cg + 8 * p + e;
+          const float a = row16_sum(dy[i] * xh[i]);
+          const float b = row16_sum(dy[i]);
+          if (li == 0) {
+            srow[128 * cg + 32 * p + 8 * lg + e] = a;
+            srow[N + 128 * cg + 32 * p + 8 * lg + e] = b;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const float* rows = reinterpret_cast<const float*>(smem + ((KCH + 1) % 3) * WSLOT);
+    for (int i = tid; i < 2 * N; i += 512) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) a += rows[w * 2 * N + i];
+      if (ln.sum_ws) {          // folded later in workgroup order (ttmi_fold)
+        ln.sum_ws[(int64_t)blockIdx.x * 2 * N + i] = a;
+      } else {
+        float* dst = i < N ? ln.dw : ln.db;
+        if (dst) atomicAdd(dst + (i < N ? i : i - N), a);
+      }
+    }
+  }
+  TTMI_TSTAMP(3);
 }
 
 // ------------------------------------------------------------ weight-gradient GEMM (bf16)
@@ -1925,14 +2233,24 @@ void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBw
   // leaves waves idle but puts a workgroup on more CUs (M = 25,600 -> 1,600 tiles -> 229
   // workgroups of 7 instead of 200 of 8 on 256 CUs)
   const int64_t tiles = (a.M + 15) / 16;
-  const int64_t tpw = std::max<int64_t>(1, (tiles + num_cus() - 1) / num_cus());
-  const int64_t grid = (tiles + tpw - 1) / tpw;
+  const int S = std::max(1, a.nslice);
+  const int64_t tpw = std::max<int64_t>(1, (tiles * S + num_cus() - 1) / num_cus());
+  const int64_t rgroups = (tiles + tpw - 1) / tpw;
+  // column slices: row groups padded to whole XCD rounds (panel_kernel's block decode)
+  const int64_t grid = S > 1 ? (rgroups + 7) / 8 * 8 * S : rgroups;
   static const int wdma = [] {            // TTMI_PANEL_WDMA=0: VGPR staging (A/B runs only)
     const char* e = getenv("TTMI_PANEL_WDMA");
     return e ? atoi(e) : 1;
   }();
+  static const int wrot = [] {            // TTMI_PANEL_WROT=0: one DMA order for all (A/B runs)
+    const char* e = getenv("TTMI_PANEL_WROT");
+    return e ? atoi(e) : 1;
+  }();
   GemmArgs b = a;
   b.wdma = wdma && a.ldb * 2 * a.N < ((int64_t)1 << 31);
+  b.wrot = wrot;
+  b.nslice = S;
+  b.rgroups = (int)rgroups;
   static const int cs = [] {              // TTMI_PANEL_CS=1: no column split (A/B runs only)
     const char* e = getenv("TTMI_PANEL_CS");
     return e ? atoi(e) : 2;
@@ -1944,12 +2262,38 @@ void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBw
     hipLaunchKernelGGL((panel_kernel<NT, KC, EPI, 1>), dim3((unsigned)grid), dim3(512), 0, s, b, (int)tpw, ln);
 }
 
+// Column-sliced row panels (N a multiple of 256 past what one W image in LDS holds, K = 256:
+// the D = 256 encoder's QKV / FFN1 forward and FFN2 input grad): nslice panels of 256 columns.
+int panel_slices(const ttmi_gemm_desc* d) {
+  if (getenv("TTMI_NO_PANEL") || getenv("TTMI_NO_PANEL_SLICE")) return 0;
+  if (d->dtype != TTMI_BF16 || !d->a_kmajor || !d->b_kmajor || d->c_mode != 0) return 0;
+  if (d->colsum || d->split_k > 1 || d->drop_rows || d->M < 2048 || d->act >= 2) return 0;
+  if (d->K != 256 || d->N % 256 || d->N < 512 || d->N > 4096) return 0;
+  const int E = panel_epi(d);
+  if (E != PE_NONE && E != PE_GATE_BF16) return 0;
+  if (d->ldc % 8 || !al16(d->C) || !al16(d->A) || !al16(d->B) || d->lda % 8 || d->ldb % 8) return 0;
+  if (d->bias && !al16(d->bias)) return 0;
+  const int64_t lim = (int64_t)INT_MAX;
+  if (d->M * d->lda * 2 >= lim || d->N * d->ldb * 2 >= lim) return 0;
+  if (d->gate && (d->ld_gate % 8 || !al16(d->gate) || d->M * d->ld_gate * 4 >= lim)) return 0;
+  return (int)(d->N / 256);
+}
+
+bool launch_panel_sliced(const ttmi_gemm_desc* d, const GemmArgs& a0, int S, hipStream_t s) {
+  GemmArgs a = a0;
+  a.N = 256;
+  a.nslice = S;
+  if (panel_epi(d) == PE_GATE_BF16) launch_panel_t<16, 8, PE_GATE_BF16>(a, s);
+  else launch_panel_t<16, 8, PE_NONE>(a, s);
+  return true;
+}
+
 bool launch_panel(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
   const int NT = (int)(a.N / 16), KC = (int)(a.K / 32), E = panel_epi(d);
 #define TTMI_PANEL(nt, kc, e) if (NT == nt && KC == kc && E == e) { launch_panel_t<nt, kc, e>(a, s); return true; }
   TTMI_PANEL(8, 4, PE_NONE) TTMI_PANEL(8, 4, PE_RES) TTMI_PANEL(8, 4, PE_GATE_BF16)      // N=128
   TTMI_PANEL(8, 12, PE_NONE) TTMI_PANEL(8, 16, PE_NONE) TTMI_PANEL(8, 16, PE_RES)
-  TTMI_PANEL(16, 4, PE_NONE) TTMI_PANEL(16, 8, PE_NONE)                                  // N=256
+  TTMI_PANEL(16, 4, PE_NONE) TTMI_PANEL(16, 8, PE_NONE) TTMI_PANEL(16, 8, PE_GATE_BF16)  // N=256
   TTMI_PANEL(24, 4, PE_NONE)                                                             // N=384
   TTMI_PANEL(32, 4, PE_NONE) TTMI_PANEL(32, 4, PE_GATE_BF16) TTMI_PANEL(32, 4, PE_GATE_F32)  // N=512
 #undef TTMI_PANEL
@@ -1957,6 +2301,31 @@ bool launch_panel(const ttmi_gemm_desc* d, const GemmArgs& a, hipStream_t s) {
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// panel256_kernel's grid: one tile group (<= 8 tiles) per workgroup, about one per CU
+int64_t panel256_tpw(int64_t M) {
+  const int64_t tiles = (M + 15) / 16;
+  return std::min<int64_t>(8, std::max<int64_t>(1, (tiles + num_cus() - 1) / num_cus()));
+}
+
+template <int EPI>
+int launch_panel256(const GemmArgs& a, const LnBwdArgs& ln, hipStream_t s) {
+  const int64_t tiles = (a.M + 15) / 16, tpw = panel256_tpw(a.M);
+  const dim3 grid((unsigned)((tiles + tpw - 1) / tpw));
+  static const int wrot = [] {
+    const char* e = getenv("TTMI_PANEL_WROT");
+    return e ? atoi(e) : 1;
+  }();
+  GemmArgs b = a;
+  b.wrot = wrot;
+  switch (a.K) {
+    case 256: hipLaunchKernelGGL((panel256_kernel<4, EPI>), grid, dim3(512), 0, s, b, (int)tpw, ln); break;
+    case 512: hipLaunchKernelGGL((panel256_kernel<8, EPI>), grid, dim3(512), 0, s, b, (int)tpw, ln); break;
+    case 768: hipLaunchKernelGGL((panel256_kernel<12, EPI>), grid, dim3(512), 0, s, b, (int)tpw, ln); break;
+    default: hipLaunchKernelGGL((panel256_kernel<16, EPI>), grid, dim3(512), 0, s, b, (int)tpw, ln); break;
+  }
+  return TTMI_OK;
+}
 
 }  // namespace
 
@@ -2028,7 +2397,7 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
   split = (int)std::max<int64_t>(1, (d->K + kspl - 1) / kspl);
   TTMI_REQUIRE(split <= 65535, "ttmi_gemm: too many splits");
 
-  GemmArgs a;
+  GemmArgs a{};
   a.M = d->M; a.N = d->N; a.K = d->K;
   a.A = static_cast<const char*>(d->A); a.lda = d->lda;
   a.B = static_cast<const char*>(d->B); a.ldb = d->ldb;
@@ -2050,6 +2419,10 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
           (!d->gate || (d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 16 == 0));
 
   if (panel_applies(d) && launch_panel(d, a, stream)) return ttmi_check_launch("ttmi_gemm");
+  if (const int S = panel_slices(d)) {
+    launch_panel_sliced(d, a, S, stream);
+    return ttmi_check_launch("ttmi_gemm");
+  }
   if (big_applies(d)) return launch_big(d, a, stream);
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)split);
   if (d->dtype == TTMI_BF16) launch_typed<bf16_t>(a, d->a_kmajor, d->b_kmajor, bm, bn, grid, stream);
@@ -2059,31 +2432,44 @@ extern "C" int ttmi_gemm(const ttmi_gemm_desc* d, hipStream_t stream) {
 
 extern "C" int ttmi_linear_res_ln(const ttmi_linear_res_ln_desc* d, hipStream_t stream) {
   TTMI_REQUIRE(d != nullptr, "ttmi_linear_res_ln: null descriptor");
-  TTMI_REQUIRE(d->M >= 0 && d->N == 128, "ttmi_linear_res_ln: N must be 128 (got %lld)", (long long)d->N);
-  TTMI_REQUIRE(d->K > 0 && d->K % 128 == 0 && d->K <= 512, "ttmi_linear_res_ln: K must be 128, 256, 384 or 512");
+  TTMI_REQUIRE(d->M >= 0 && (d->N == 128 || d->N == 256), "ttmi_linear_res_ln: N must be 128 or 256 (got %lld)",
+               (long long)d->N);
+  TTMI_REQUIRE(d->N == 256 || (d->K > 0 && d->K % 128 == 0 && d->K <= 512),
+               "ttmi_linear_res_ln: N = 128 needs K in {128, 256, 384, 512}");
+  TTMI_REQUIRE(d->N == 128 || (d->K >= 256 && d->K % 256 == 0 && d->K <= 1024),
+               "ttmi_linear_res_ln: N = 256 needs K in {256, 512, 768, 1024}");
   if (d->M == 0) return TTMI_OK;
+  const int64_t NN = d->N;
   TTMI_REQUIRE(d->x && d->w && d->residual && d->out && d->ln_w && d->ln_b && d->y && d->mean && d->rstd,
                "ttmi_linear_res_ln: null argument");
   TTMI_REQUIRE(al16(d->x) && al16(d->w) && d->ldx % 8 == 0 && d->ldw % 8 == 0 && d->ldx >= d->K &&
                d->ldw >= d->K, "ttmi_linear_res_ln: x/w need 16-byte rows");
-  TTMI_REQUIRE(al16(d->residual) && d->ld_res % 4 == 0 && d->ld_res >= 128 && al16(d->out) &&
-               d->ld_out % 4 == 0 && d->ld_out >= 128, "ttmi_linear_res_ln: residual/out need 16-byte rows");
-  TTMI_REQUIRE(al16(d->y) && d->ldy % 8 == 0 && d->ldy >= 128, "ttmi_linear_res_ln: y needs 16-byte rows");
+  TTMI_REQUIRE(al16(d->residual) && d->ld_res % 4 == 0 && d->ld_res >= NN && al16(d->out) &&
+               d->ld_out % 4 == 0 && d->ld_out >= NN, "ttmi_linear_res_ln: residual/out need 16-byte rows");
+  TTMI_REQUIRE(al16(d->y) && d->ldy % 8 == 0 && d->ldy >= NN, "ttmi_linear_res_ln: y needs 16-byte rows");
+  TTMI_REQUIRE(NN == 128 || (d->M * d->ldx * 2 < ((int64_t)1 << 32) && (NN * d->ldw) * 2 < ((int64_t)1 << 32)),
+               "ttmi_linear_res_ln: N = 256 needs x and w under 4 GB (32-bit DMA offsets)");
+  TTMI_REQUIRE(NN == 128 || ((!d->bias || al16(d->bias)) && al16(d->ln_w) && al16(d->ln_b)),
+               "ttmi_linear_res_ln: N = 256 needs 16-byte aligned bias / LayerNorm parameters");
   TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f && (d->drop_p == 0.f || d->drop_seed),
                "ttmi_linear_res_ln: bad dropout");
   GemmArgs a{};
-  a.M = d->M; a.N = 128; a.K = d->K;
+  a.M = d->M; a.N = NN; a.K = d->K;
   a.A = static_cast<const char*>(d->x); a.lda = d->ldx;
   a.B = static_cast<const char*>(d->w); a.ldb = d->ldw;
   a.C = d->out; a.ldc = d->ld_out; a.c_f32 = 1;
   a.alpha = 1.f;
   a.bias = d->bias;
-  a.drop = make_drop(d->drop_p, d->drop_seed); a.ld_drop = d->ld_drop ? d->ld_drop : 128;
+  a.drop = make_drop(d->drop_p, d->drop_seed); a.ld_drop = d->ld_drop ? d->ld_drop : NN;
   a.residual = d->residual; a.ld_res = d->ld_res;
   LnBwdArgs ln{};
   ln.w = d->ln_w; ln.lnb = d->ln_b; ln.eps = d->eps;
   ln.y = static_cast<bf16_t*>(d->y); ln.ldy = d->ldy;
   ln.mean_out = d->mean; ln.rstd_out = d->rstd;
+  if (NN == 256) {
+    launch_panel256<PE_RESLN>(a, ln, stream);
+    return ttmi_check_launch("ttmi_linear_res_ln");
+  }
   switch (d->K) {
     case 128: launch_panel_t<8, 4, PE_RESLN>(a, stream, ln); break;
     case 256: launch_panel_t<8, 8, PE_RESLN>(a, stream, ln); break;
@@ -2095,24 +2481,32 @@ extern "C" int ttmi_linear_res_ln(const ttmi_linear_res_ln_desc* d, hipStream_t 
 
 extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t stream) {
   TTMI_REQUIRE(d != nullptr, "ttmi_linear_ln_bwd: null descriptor");
-  TTMI_REQUIRE(d->M >= 0 && d->N == 128, "ttmi_linear_ln_bwd: N must be 128 (got %lld)", (long long)d->N);
-  TTMI_REQUIRE(d->K > 0 && d->K % 128 == 0 && d->K <= 512, "ttmi_linear_ln_bwd: K must be 128, 256, 384 or 512");
+  TTMI_REQUIRE(d->M >= 0 && (d->N == 128 || d->N == 256), "ttmi_linear_ln_bwd: N must be 128 or 256 (got %lld)",
+               (long long)d->N);
+  TTMI_REQUIRE(d->N == 256 || (d->K > 0 && d->K % 128 == 0 && d->K <= 512),
+               "ttmi_linear_ln_bwd: N = 128 needs K in {128, 256, 384, 512}");
+  TTMI_REQUIRE(d->N == 128 || (d->K >= 256 && d->K % 256 == 0 && d->K <= 1024),
+               "ttmi_linear_ln_bwd: N = 256 needs K in {256, 512, 768, 1024}");
   if (d->M == 0) return TTMI_OK;
+  const int64_t NN = d->N;
   TTMI_REQUIRE(d->dh && d->wt && d->x && d->mean && d->rstd && d->ln_w && d->dx,
                "ttmi_linear_ln_bwd: null argument");
   TTMI_REQUIRE(al16(d->dh) && al16(d->wt) && d->ld_dh % 8 == 0 && d->ld_wt % 8 == 0 &&
                d->ld_dh >= d->K && d->ld_wt >= d->K, "ttmi_linear_ln_bwd: dh/wt need 16-byte rows");
-  TTMI_REQUIRE(al16(d->x) && d->ldx % 4 == 0 && d->ldx >= 128 && al16(d->dx) && d->lddx % 4 == 0 &&
-               d->lddx >= 128, "ttmi_linear_ln_bwd: x/dx need 16-byte rows");
-  TTMI_REQUIRE(!d->res || (al16(d->res) && d->ld_res % 4 == 0 && d->ld_res >= 128),
+  TTMI_REQUIRE(al16(d->x) && d->ldx % 4 == 0 && d->ldx >= NN && al16(d->dx) && d->lddx % 4 == 0 &&
+               d->lddx >= NN, "ttmi_linear_ln_bwd: x/dx need 16-byte rows");
+  TTMI_REQUIRE(!d->res || (al16(d->res) && d->ld_res % 4 == 0 && d->ld_res >= NN),
                "ttmi_linear_ln_bwd: res needs 16-byte rows");
+  TTMI_REQUIRE(NN == 128 || (d->M * d->ld_dh * 2 < ((int64_t)1 << 32) && (NN * d->ld_wt) * 2 < ((int64_t)1 << 32)
+                             && al16(d->ln_w)),
+               "ttmi_linear_ln_bwd: N = 256 needs dh and wt under 4 GB and an aligned LayerNorm weight");
   TTMI_REQUIRE(!d->res_rows || (d->res && d->res_L > 0), "ttmi_linear_ln_bwd: res_rows needs res and res_L > 0");
-  TTMI_REQUIRE(!d->next || (al16(d->next) && d->ld_next % 8 == 0 && d->ld_next >= 128),
+  TTMI_REQUIRE(!d->next || (al16(d->next) && d->ld_next % 8 == 0 && d->ld_next >= NN),
                "ttmi_linear_ln_bwd: next needs 16-byte rows");
   TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f && (d->drop_p == 0.f || d->drop_seed),
                "ttmi_linear_ln_bwd: bad dropout");
   GemmArgs a{};
-  a.M = d->M; a.N = 128; a.K = d->K;
+  a.M = d->M; a.N = NN; a.K = d->K;
   a.A = static_cast<const char*>(d->dh); a.lda = d->ld_dh;
   a.B = static_cast<const char*>(d->wt); a.ldb = d->ld_wt;
   a.alpha = 1.f;
@@ -2123,10 +2517,14 @@ extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t 
   ln.res_rows = d->res_rows; ln.res_L = d->res_L;
   ln.dx = d->dx; ln.lddx = d->lddx;
   ln.next = static_cast<bf16_t*>(d->next); ln.ld_next = d->ld_next;
-  ln.drop = make_drop(d->drop_p, d->drop_seed); ln.ld_drop = d->ld_drop ? d->ld_drop : 128;
+  ln.drop = make_drop(d->drop_p, d->drop_seed); ln.ld_drop = d->ld_drop ? d->ld_drop : NN;
   ln.drop_rows = d->drop_rows;
   ln.dw = d->ln_dw; ln.db = d->ln_db;
   ln.sum_ws = d->sum_ws;
+  if (NN == 256) {
+    launch_panel256<PE_LNBWD>(a, ln, stream);
+    return ttmi_check_launch("ttmi_linear_ln_bwd");
+  }
   switch (d->K) {
     case 128: launch_panel_t<8, 4, PE_LNBWD>(a, stream, ln); break;
     case 256: launch_panel_t<8, 8, PE_LNBWD>(a, stream, ln); break;
@@ -2238,6 +2636,13 @@ extern "C" int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M) {
   const int64_t tiles = (M + 15) / 16;
   const int64_t tpw = std::max<int64_t>(1, (tiles + num_cus() - 1) / num_cus());
   return (tiles + tpw - 1) / tpw;     // launch_panel_t's grid
+}
+
+extern "C" int64_t ttmi_linear_ln_bwd_sum_blocks_n(int64_t M, int64_t N) {
+  if (N != 256) return ttmi_linear_ln_bwd_sum_blocks(M);
+  if (M <= 0) return 0;
+  const int64_t tiles = (M + 15) / 16, tpw = panel256_tpw(M);
+  return (tiles + tpw - 1) / tpw;     // launch_panel256's grid
 }
 
 namespace {

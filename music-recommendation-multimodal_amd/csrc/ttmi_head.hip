@@ -40,6 +40,10 @@ struct ItemArgs {
   float* rmean; float* rvar; int64_t* nbt; float* bmean; float* brstd; bf16_t* y1w;
   DropParams bd;
   float* bnpart; int* bncnt;
+  // ABI 18, ttmi_user_item_head_fwd_ac: stages A and C in ONE launch (beside the user head).
+  // Stage A stores z, bmean, brstd write-through (sc1) and its quarter mergers count on
+  // bncnt[IN1/64]; the C workgroups poll that count, then read them with sc1 loads.
+  int fin;
 };
 
 struct ItemLdsA {
@@ -72,7 +76,8 @@ struct HeadArgs {
   // co-launched item head stage A (ttmi_user_item_head_fwd): workgroups >= nbu run
   // item_a_body on row block (l % it_nblk), column quarter (l / it_nblk)
   ItemArgs it; int nbu, it_nblk;
-  int it_stage;                // 0: item stage A (it_nblk x 8 workgroups), 2: item stage C (it_nblk)
+  int it_stage;                // 0: item stage A (it_nblk x 8 workgroups), 2: item stage C (it_nblk),
+                               // 3: both, A's then C's (C waits for A's statistics in-launch)
 };
 
 struct HeadLds {
@@ -218,6 +223,20 @@ TTMI_DEV void st_agent(float* p, float v) {
 TTMI_DEV float ld_agent(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-byte write-through (sc1) store / load for data handed to another workgroup inside a launch
+// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms row 1).
+TTMI_DEV void st16_wt(float* p, float4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
+  const i32x4_t q = {(int)__float_as_uint(v.x), (int)__float_as_uint(v.y), (int)__float_as_uint(v.z),
+                     (int)__float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(q, r, 0, 0, 16);
+}
+TTMI_DEV float4 ld16_wt(const float* p) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 16, 0x00020000);
+  const i32x4_t q = __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 16);
+  return make_float4(__int_as_float(q.x), __int_as_float(q.y), __int_as_float(q.z), __int_as_float(q.w));
+}
+constexpr int BN_DONE = IN1 / 64, BN_CDONE = IN1 / 64 + 1;   // bncnt slots past the quarters'
 
 // Item head stage A on row block bx, column quarter q (item_head_a_kernel, or the workgroups
 // of ttmi_user_item_head_fwd past the user head's).
@@ -241,9 +260,11 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   f32x4_t v[1];
   head_gemm<1, IK, PI>(L.sA, wf, v, lane);
   const int m = r0 + li;
-  if (m < a.B)
-    *reinterpret_cast<float4*>(a.z + (int64_t)m * IN1 + n0 + 4 * g) =
-        make_float4(v[0][0] + bias.x, v[0][1] + bias.y, v[0][2] + bias.z, v[0][3] + bias.w);
+  if (m < a.B) {
+    const float4 zo = make_float4(v[0][0] + bias.x, v[0][1] + bias.y, v[0][2] + bias.z, v[0][3] + bias.w);
+    if (a.fin) st16_wt(a.z + (int64_t)m * IN1 + n0 + 4 * g, zo);     // read by this launch's C
+    else *reinterpret_cast<float4*>(a.z + (int64_t)m * IN1 + n0 + 4 * g) = zo;
+  }
   if (a.bncnt == nullptr) return;
   // ---- fused BatchNorm statistics: this block's (mean, M2) of its 4 x 16 columns over its
   // valid rows (the 16 lanes of a lane group share the columns), exchanged through agent-scope
@@ -298,12 +319,21 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
     }
   }
   const float var = M2 / (float)a.B;
-  a.bmean[c] = mean;
-  a.brstd[c] = 1.f / sqrtf(var + a.bn_eps);
+  if (a.fin) {                                       // read by this launch's C workgroups
+    st_agent(a.bmean + c, mean);
+    st_agent(a.brstd + c, 1.f / sqrtf(var + a.bn_eps));
+  } else {
+    a.bmean[c] = mean;
+    a.brstd[c] = 1.f / sqrtf(var + a.bn_eps);
+  }
   if (a.rmean) a.rmean[c] = (1.f - a.bn_mom) * a.rmean[c] + a.bn_mom * mean;
   if (a.rvar) a.rvar[c] = (1.f - a.bn_mom) * a.rvar[c] + a.bn_mom * var * ((float)a.B / (float)(a.B - 1));
   if (q == 0 && tid == 0 && a.nbt) a.nbt[0] += 1;
   if (tid == 0) __hip_atomic_store(a.bncnt + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.fin) {      // this (single) storing wave drained, then one lane signals the quarter done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) __hip_atomic_fetch_add(a.bncnt + BN_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 struct ItemLdsC {
@@ -317,19 +347,42 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = bx * HR;
   const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
+  if (a.fin) {
+    // stage A runs in this launch: wait until the IN1/64 column-quarter mergers have published
+    // the batch statistics (one lane polls the count, sc1 loads with s_sleep; bounded: on a
+    // timeout the error word bncnt[BN_CDONE + 1] is set instead of hanging the GPU)
+    if (tid == 0) {
+      int spins = 0;
+      while (__hip_atomic_load(a.bncnt + BN_DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < IN1 / 64) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 22)) {
+          __hip_atomic_store(a.bncnt + BN_CDONE + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      // the last C workgroup past the poll resets both counts for the next launch
+      const int nb = (a.B + HR - 1) / HR;
+      if (__hip_atomic_fetch_add(a.bncnt + BN_CDONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) {
+        __hip_atomic_store(a.bncnt + BN_DONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.bncnt + BN_CDONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+  }
   if (a.bncnt != nullptr) {      // fused BatchNorm: y1 = drop(relu(BN(z))) staged from z rows
     float4 zv[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-      zv[k] = *reinterpret_cast<const float4*>(a.z + (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4);
+      const float* zp = a.z + (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4;
+      zv[k] = a.fin ? ld16_wt(zp) : *reinterpret_cast<const float4*>(zp);
     }
     const DropKeys dk = resolve_drop(a.bd);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-      const float4 mu = *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
-      const float4 rs = *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
+      const float4 mu = a.fin ? ld16_wt(a.bmean + 4 * c4) : *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
+      const float4 rs = a.fin ? ld16_wt(a.brstd + 4 * c4) : *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
       const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
       const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
       float x[4] = {fmaxf((zv[k].x - mu.x) * rs.x * ww.x + bb.x, 0.f), fmaxf((zv[k].y - mu.y) * rs.y * ww.y + bb.y, 0.f),
@@ -421,8 +474,12 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
   static_assert(sizeof(HeadLds) >= sizeof(ItemLdsC), "item stage C reuses the head's LDS");
   if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head stage A or C
     const int l = (int)blockIdx.x - a.nbu;
-    if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
-    else item_c_body(a.it, l, *reinterpret_cast<ItemLdsC*>(&L));
+    const int na = a.it_stage == 3 ? a.it_nblk * (IN1 / 64) : 0;     // stage 3: A then C blocks
+    if (a.it_stage == 0 || l < na) {
+      item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+    } else {
+      item_c_body(a.it, l - na, *reinterpret_cast<ItemLdsC*>(&L));
+    }
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
@@ -1048,7 +1105,9 @@ extern "C" int ttmi_item_head_fwd(const ttmi_item_head_desc* d, hipStream_t s) {
 }
 
 extern "C" int64_t ttmi_item_head_bn_part_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 2 * IN1; }
-extern "C" int64_t ttmi_item_head_bn_counter_bytes(int B) { (void)B; return (IN1 / 64) * 4; }
+// the column quarters' arrival counts, then (ABI 18) stage A's done count, stage C's count and an
+// error word (a C workgroup's poll timed out)
+extern "C" int64_t ttmi_item_head_bn_counter_bytes(int B) { (void)B; return (IN1 / 64 + 3) * 4; }
 
 extern "C" int64_t ttmi_item_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 2 * HD; }
 
@@ -1102,7 +1161,8 @@ int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_d
                  "ttmi_user_item_head_fwd_c: stage C here needs the BatchNorm statistics of stage A "
                  "(bn_part / bn_cnt, B <= %d)", BN_MAXBLK * HR);
     a.it_nblk = (it->B + HR - 1) / HR;
-    extra = stage == 0 ? a.it_nblk * (IN1 / 64) : a.it_nblk;
+    a.it.fin = stage == 3;
+    extra = stage == 0 ? a.it_nblk * (IN1 / 64) : stage == 2 ? a.it_nblk : a.it_nblk * (IN1 / 64 + 1);
   }
   const dim3 grid((unsigned)(a.nbu + extra));
   if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_kernel<512>, grid, dim3(256), 0, s, a);
@@ -1120,6 +1180,12 @@ extern "C" int ttmi_user_item_head_fwd_c(const ttmi_user_head_desc* d, const ttm
                                          hipStream_t s) {
   TTMI_REQUIRE(it != nullptr, "ttmi_user_item_head_fwd_c: null item descriptor");
   return user_item_head_fwd_impl(d, it, 2, s);
+}
+
+extern "C" int ttmi_user_item_head_fwd_ac(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
+                                          hipStream_t s) {
+  TTMI_REQUIRE(it != nullptr, "ttmi_user_item_head_fwd_ac: null item descriptor");
+  return user_item_head_fwd_impl(d, it, 3, s);
 }
 
 extern "C" int ttmi_mha_q1_gather_item_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,

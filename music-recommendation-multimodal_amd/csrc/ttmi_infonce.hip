@@ -302,6 +302,7 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
   constexpr int D = 16 * DC, QP = D * 4 + 16;
   __shared__ __attribute__((aligned(16))) char sq[NQ * QP];
   __shared__ float sm[4][NQ], ss[4][NQ], st[4][NQ];
+  TTMI_TSTAMP(0);
   const int nb = (B + NQ - 1) / NQ;
   const int split = blockIdx.x % NSPLIT;
   const int qb = blockIdx.x / NSPLIT;
@@ -318,6 +319,7 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
     *reinterpret_cast<float4*>(sq + r * QP + c4 * 16) = v;
   }
   __syncthreads();
+  TTMI_TSTAMP(1);
   const int i = i0 + li;
   const bool iok = i < B;
   const int64_t ui = (uid && iok) ? uid[i] : 0;
@@ -358,6 +360,7 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
       }
     }
   }
+  TTMI_TSTAMP(2);
   // merge the 4 lane groups holding row li, then the 4 waves
 #pragma unroll
   for (int off = 16; off <= 32; off <<= 1) {
@@ -394,9 +397,11 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
   const int nqb = 2 * nb;
   __builtin_amdgcn_s_waitcnt(0);                     // every counter at zero: stores retired
   __syncthreads();
+  TTMI_TSTAMP(3);
   if (tid == 0)
     s_last = __hip_atomic_fetch_add(cnt + qb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NSPLIT - 1;
   __syncthreads();
+  TTMI_TSTAMP(4);
   if (!s_last) return;
   if (tid < 64) {
     float c = 0.f;
@@ -425,10 +430,12 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  TTMI_TSTAMP(5);
   if (tid == 0)
     s_last = __hip_atomic_fetch_add(cnt + nqb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nqb - 1;
   __syncthreads();
   if (!s_last) return;
+  TTMI_TSTAMP(6);
   if (tid < 64) {
     float c = 0.f;
     for (int q = tid; q < nqb; q += 64) c += ld_agent(qsum + q);
@@ -512,6 +519,7 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
   constexpr int VP = D + 4, GP = NKB + 4;          // LDS pitches (floats)
   __shared__ __attribute__((aligned(16))) float sV[NKB * VP];
   __shared__ __attribute__((aligned(16))) float sG[NQ * GP];
+  TTMI_TSTAMP(0);
   const int nb = (B + NQ - 1) / NQ;
   const int split = blockIdx.x % NSPLIT;
   const int qb = blockIdx.x / NSPLIT;
@@ -591,6 +599,7 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
       }
     }
   }
+  TTMI_TSTAMP(1);
   // lane holds D[d = dtile*16 + 4lg + r][row = r0 + li]
   const int row = r0 + li;
   if constexpr (!FIN) {
@@ -622,9 +631,11 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __shared__ int s_last;
     __syncthreads();
+    TTMI_TSTAMP(2);
     if (tid == 0)
       s_last = __hip_atomic_fetch_add(fin.cnt + qb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NSPLIT - 1;
     __syncthreads();
+    TTMI_TSTAMP(3);
     if (!s_last) return;
     if (tid == 0) __hip_atomic_store(fin.cnt + qb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     constexpr int CPL = (D + 63) / 64;               // columns per lane (c = lane + 64q)
@@ -677,6 +688,7 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
         }
       }
     }
+    TTMI_TSTAMP(4);
   }
 }
 
@@ -996,3 +1008,5 @@ extern "C" int ttmi_sum_scaled(int n, const float* x, float scale, float* out, h
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, n, x, scale, out);
   return ttmi_check_launch("ttmi_sum_scaled");
 }
+
+TTMI_STAMP_DUMP(infonce)

@@ -310,6 +310,84 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
   }
 }
 
+// Forward, 16-byte lanes (D = 128 or 256): a row is LPR = D / 4 lanes holding 4 consecutive
+// columns each (2 rows per wave at D = 128), and a wave keeps U row groups in flight with every
+// load issued before any arithmetic (the one-row-per-wave kernel above ran a dependent
+// ids -> E[id] -> reduce -> store chain per row with 4-byte loads: ~1.8 TB/s at cfg 2).
+template <int LPR>
+TTMI_DEV float lane_group_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int D, bool LN2, int U>
+__global__ __launch_bounds__(256) void seq_embed_fwd_vec_kernel(
+    int B, int L, const int64_t* __restrict__ ids, const float* __restrict__ E, int64_t V,
+    const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ b,
+    float eps, DropParams dp, float* __restrict__ x, float* __restrict__ mean,
+    float* __restrict__ rstd, const float* __restrict__ w1, const float* __restrict__ b1,
+    float eps1, bf16_t* __restrict__ y1, float* __restrict__ mean1, float* __restrict__ rstd1) {
+  constexpr int LPR = D / 4, RPW = 64 / LPR;          // lanes per row, rows per wave instruction
+  const int lane = threadIdx.x & 63, j = lane % LPR, sub = lane / LPR;
+  const int64_t M = (int64_t)B * L;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  constexpr float invD = 1.f / (float)D;
+  const DropKeys dk = resolve_drop(dp);
+  const float4 wv = reinterpret_cast<const float4*>(w)[j], bv = reinterpret_cast<const float4*>(b)[j];
+  float4 w1v = make_float4(0.f, 0.f, 0.f, 0.f), b1v = w1v;
+  if constexpr (LN2) { w1v = reinterpret_cast<const float4*>(w1)[j]; b1v = reinterpret_cast<const float4*>(b1)[j]; }
+  for (int64_t g0 = wid * (U * RPW); g0 < M; g0 += nw * (U * RPW)) {
+    int64_t row[U], id[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      row[u] = g0 + u * RPW + sub;
+      id[u] = ids[min(row[u], M - 1)];              // clamped: unconditional loads
+    }
+    float4 e[U], pv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = id[u] >= 0 && id[u] < V;
+      const int l = (int)(min(row[u], M - 1) % L);
+      e[u] = reinterpret_cast<const float4*>(E + (ok ? id[u] : 0) * D)[j];
+      if (!ok) e[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      pv[u] = reinterpret_cast<const float4*>(P + (int64_t)l * D)[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float v[4] = {e[u].x + pv[u].x, e[u].y + pv[u].y, e[u].z + pv[u].z, e[u].w + pv[u].w};
+      const float mu = lane_group_sum<LPR>(v[0] + v[1] + v[2] + v[3]) * invD;
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q += (v[k] - mu) * (v[k] - mu);
+      const float rs = 1.f / sqrtf(lane_group_sum<LPR>(q) * invD + eps);
+      const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, ba[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = (v[k] - mu) * rs * wa[k] + ba[k];
+      drop_apply_vec<4>(dk, (uint32_t)(row[u] * D + 4 * j), v);
+      if (row[u] >= M) continue;
+      reinterpret_cast<float4*>(x + row[u] * D)[j] = make_float4(v[0], v[1], v[2], v[3]);
+      if (j == 0) { mean[row[u]] = mu; rstd[row[u]] = rs; }
+      if constexpr (LN2) {
+        const float mu1 = lane_group_sum<LPR>(v[0] + v[1] + v[2] + v[3]) * invD;
+        float q1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q1 += (v[k] - mu1) * (v[k] - mu1);
+        const float rs1 = 1.f / sqrtf(lane_group_sum<LPR>(q1) * invD + eps1);
+        const float wa1[4] = {w1v.x, w1v.y, w1v.z, w1v.w}, ba1[4] = {b1v.x, b1v.y, b1v.z, b1v.w};
+        ushort4 o;
+        o.x = f2bf((v[0] - mu1) * rs1 * wa1[0] + ba1[0]);
+        o.y = f2bf((v[1] - mu1) * rs1 * wa1[1] + ba1[1]);
+        o.z = f2bf((v[2] - mu1) * rs1 * wa1[2] + ba1[2]);
+        o.w = f2bf((v[3] - mu1) * rs1 * wa1[3] + ba1[3]);
+        reinterpret_cast<ushort4*>(y1 + row[u] * D)[j] = o;
+        if (j == 0) { mean1[row[u]] = mu1; rstd1[row[u]] = rs1; }
+      }
+    }
+  }
+}
+
 // Backward: block (l, b-chunk) of SEB_W waves; each wave walks b = chunk*bpc + wave,
 // + SEB_W, ... so the position gradient dP[l] accumulates in registers (one add per column
 // per block).  The chunk is sized so a wave makes ONE pass of U rows: the kernel is a
@@ -798,7 +876,27 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
     const char* e = getenv("TTMI_SEQ_GRID");
     return e ? (int64_t)atoll(e) : (int64_t)1 << 20;
   }();
-  const dim3 grid((unsigned)std::min<int64_t>(rows_grid((int64_t)B * L), cap));
+  const int64_t M = (int64_t)B * L;
+  static const int vec = [] {                        // TTMI_SEQ_VEC=0: the row-per-wave kernel (A/B)
+    const char* e = getenv("TTMI_SEQ_VEC");
+    return e ? atoi(e) : 1;
+  }();
+  const bool al = (((uintptr_t)E | (uintptr_t)P | (uintptr_t)w | (uintptr_t)b | (uintptr_t)x |
+                    (uintptr_t)(ln2 ? w1 : w) | (uintptr_t)(ln2 ? b1 : b)) & 15) == 0 &&
+                  (!ln2 || ((uintptr_t)y1 & 7) == 0);
+  if (vec && al && (D == 128 || D == 256)) {
+    constexpr int U = 2;
+    const int rpw = D == 128 ? 2 : 1;
+    const int64_t waves = (M + U * rpw - 1) / (U * rpw);
+    const dim3 g((unsigned)std::min<int64_t>((waves + 3) / 4, cap));
+#define TTMI_SEQV(DD, LN) hipLaunchKernelGGL((seq_embed_fwd_vec_kernel<DD, LN, U>), g, dim3(256), 0, s, B, L, ids, E, V, P, \
+                                             w, b, eps, dp, x, mean, rstd, w1, b1, eps1, (bf16_t*)y1, mean1, rstd1)
+    if (D == 128) { if (ln2) TTMI_SEQV(128, true); else TTMI_SEQV(128, false); }
+    else { if (ln2) TTMI_SEQV(256, true); else TTMI_SEQV(256, false); }
+#undef TTMI_SEQV
+    return ttmi_check_launch("ttmi_seq_embed_fwd");
+  }
+  const dim3 grid((unsigned)std::min<int64_t>(rows_grid(M), cap));
   TTMI_NV_DISPATCH(D, {
     if (ln2)
       hipLaunchKernelGGL((seq_embed_fwd_kernel<NV, true>), grid, dim3(256), 0, s, B, L, D, ids, E, V, P,

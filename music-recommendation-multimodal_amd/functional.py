@@ -146,13 +146,21 @@ def _dx(dy: Tensor, W: Dict[str, Tensor], name: str, out: Tensor, gate: Optional
     return ops.linear_dx(dy, W[name], out, gate=gate, gate_scale=gate_scale)
 
 
+def _ln_k_ok(D: int, K: int) -> bool:
+    """K a fused LayerNorm-epilogue GEMM takes at LayerNorm width D (ttmi_linear_ln_bwd /
+    ttmi_linear_res_ln): D = 128 with W resident in LDS, D = 256 with W streamed (ABI 19)."""
+    if D == 128:
+        return K % 128 == 0 and 0 < K <= 512
+    return D == 256 and K % 256 == 0 and 0 < K <= 1024
+
+
 def _ln_fusable(W: Dict[str, Tensor], pre: str, D: int) -> bool:
     """The layer's input-grad GEMMs can carry the LayerNorm backward in their epilogue:
-    bf16 with the transposed weight mirrors present and the LayerNorm width 128."""
+    bf16 with the transposed weight mirrors present and the LayerNorm width 128 or 256."""
     wt1 = W.get(transposed_name(pre + "linear1.weight"))
     wti = W.get(transposed_name(pre + "self_attn.in_proj_weight"))
-    return (D == 128 and wt1 is not None and wti is not None and wt1.shape[1] % 128 == 0
-            and wt1.shape[1] <= 512 and wti.shape[1] % 128 == 0 and wti.shape[1] <= 512)
+    return (wt1 is not None and wti is not None and _ln_k_ok(D, wt1.shape[1])
+            and _ln_k_ok(D, wti.shape[1]))
 
 
 def _lp(i: int) -> str:
@@ -161,10 +169,10 @@ def _lp(i: int) -> str:
 
 def _resln_ok(W: Dict[str, Tensor], name: str, D: int) -> bool:
     """The Linear `name` can end its residual sub-block with the following LayerNorm fused
-    (ttmi_linear_res_ln): bf16 weight [128, K], K % 128 == 0, K <= 512."""
+    (ttmi_linear_res_ln): bf16 weight [D, K], D = 128 (K % 128 == 0, K <= 512) or D = 256
+    (K in {256, 512, 768, 1024})."""
     w = W[name]
-    return (D == 128 and w.dtype == torch.bfloat16 and w.shape[0] == 128
-            and w.shape[1] % 128 == 0 and w.shape[1] <= 512)
+    return w.dtype == torch.bfloat16 and w.shape[0] == D and _ln_k_ok(D, w.shape[1])
 
 
 def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gender: Tensor,
@@ -221,13 +229,18 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             # the last-valid rows, their residual rows and the one-query attention: one launch
             # (with the item head's stage A on the same grid when its BatchNorm statistics are
             # merged in-launch: stage C then rides in the user head launch, ABI 18)
-            co_a = co_item is not None and co_item.bn_fused and L <= 64
+            # (the item head's two stages ride in the fused user head launch, stage C waiting
+            # in-launch for stage A's BatchNorm statistics, ABI 18; without the fused head, stage
+            # A rides on this grid instead)
+            head_fused = ops.user_head_fusable(W, P, pre, D, dt)
+            co_ac = co_item is not None and co_item.bn_fused and head_fused
+            co_a = co_item is not None and co_item.bn_fused and L <= 64 and not head_fused
             ops.mha_q1_gather_fwd(qkv, key_valid, x, rows, res_in, B, L, H, ctx, lse,
                                   _drop(cfg, seeds, site_attn(i)),
                                   co_item=co_item.desc if co_a else None)
             if co_a:
                 co_item.a_done = True
-            if ops.user_head_fusable(W, P, pre, D, dt):      # the rest of the tower: one launch
+            if head_fused:      # the rest of the tower: one launch
                 F_ = W[pre + "linear1.weight"].shape[0]
                 Wc = D + P["gender_embedding.weight"].shape[1] + P["country_embedding.weight"].shape[1]
                 o = dict(x1=torch.empty(B, D, **f32), a2=torch.empty(B, D, device=dev, dtype=dt),
@@ -241,12 +254,10 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                                   (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_ffn(i)),
                                    _drop(cfg, seeds, site_drop2(i))), o,
                                   co_item=co_item.desc if co_item is not None else None,
-                                  normed=normed, co_stage="C" if co_a else "A")
+                                  normed=normed, co_stage="AC" if co_ac else "A")
                 if co_item is not None:
-                    if co_a:
-                        co_item.c_done = True
-                    else:
-                        co_item.a_done = True
+                    co_item.a_done = True
+                    co_item.c_done = co_ac
                 st.normed = normed is not None
                 st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, o["x1"], o["a2"], o["m2"],
                                             o["r2"], o["h"], rows))

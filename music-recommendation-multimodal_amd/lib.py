@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -196,6 +196,7 @@ SIGNATURES = {
     "ttmi_wgrad_fold": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
                               ctypes.POINTER(FoldDesc), c_p]),
     "ttmi_linear_ln_bwd_sum_blocks": (c_i64, [c_i64]),
+    "ttmi_linear_ln_bwd_sum_blocks_n": (c_i64, [c_i64, c_i64]),
     "ttmi_wgrad_batch": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
                                ctypes.POINTER(FoldDesc), c_p]),
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
@@ -256,6 +257,7 @@ SIGNATURES = {
     "ttmi_item_head_fwd_stages": (c_i, [c_p, c_i, c_p]),
     "ttmi_user_item_head_fwd": (c_i, [c_p, c_p, c_p]),
     "ttmi_user_item_head_fwd_c": (c_i, [c_p, c_p, c_p]),
+    "ttmi_user_item_head_fwd_ac": (c_i, [c_p, c_p, c_p]),
     "ttmi_item_head_bwd_c": (c_i, [c_p, c_p]),
     "ttmi_item_head_bn_part_floats": (ctypes.c_int64, [c_i]),
     "ttmi_item_head_bn_counter_bytes": (ctypes.c_int64, [c_i]),

@@ -223,7 +223,7 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
         # per-workgroup sums, folded in workgroup order (with the step's weight gradients
         # inside deferred_wgrad, else right after the launch): bit-reproducible
         _L.load()
-        G = int(_L._lib.ttmi_linear_ln_bwd_sum_blocks(M))
+        G = int(_L._lib.ttmi_linear_ln_bwd_sum_blocks_n(M, N))
         ws = torch.empty(G * 2 * N, device=dx.device, dtype=torch.float32)
         d.sum_ws = _p(ws)
         for j, g in enumerate((ln_dw, ln_db)):
@@ -241,7 +241,8 @@ def linear_res_ln(x: Tensor, w: Tensor, bias: Optional[Tensor], residual: Tensor
                   ln_w: Tensor, ln_b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor, *,
                   eps: float = 1e-5, drop: Drop = NO_DROP) -> Tensor:
     """out = residual + dropout(x·wᵀ + bias) (fp32), y = bf16(LN(out)·ln_w + ln_b), mean/rstd:
-    a residual sub-block's end and the following LayerNorm in one kernel (N = 128)."""
+    a residual sub-block's end and the following LayerNorm in one kernel (N = 128, or N = 256
+    with K in {256, 512, 768, 1024}: the streamed-W panel, ABI 19)."""
     _dev(x, w, residual, out, y)
     M, K = x.shape
     N = w.shape[0]
@@ -1193,8 +1194,10 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
         call("ttmi_user_head_fwd", ctypes.byref(d), _s())
     elif co_stage == "A":      # item head stage A on the CUs the 16-row user blocks leave idle
         call("ttmi_user_item_head_fwd", ctypes.byref(d), ctypes.byref(co_item), _s())
-    else:                      # stage C (stage A ran beside the one-query attention, ABI 18)
+    elif co_stage == "C":      # stage C (stage A ran beside the one-query attention, ABI 18)
         call("ttmi_user_item_head_fwd_c", ctypes.byref(d), ctypes.byref(co_item), _s())
+    else:                      # "AC": both item stages, C waiting for A's statistics in-launch
+        call("ttmi_user_item_head_fwd_ac", ctypes.byref(d), ctypes.byref(co_item), _s())
 
 
 def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: Dict[str, Tensor],

@@ -91,10 +91,13 @@ def test_q1_gather_item_fwd_equals_separate(gpu_pkg, B, p):
             assert torch.equal(b1[k], b0[k]), k
 
 
-@pytest.mark.parametrize("B,p", [(512, 0.1), (37, 0.0)])
+@pytest.mark.parametrize("B,p", [(512, 0.1), (37, 0.0), (2, 0.1)])
 def test_user_head_item_c_equals_separate(gpu_pkg, B, p):
-    """ttmi_user_item_head_fwd_c (user head + item stage C on one grid) == the user head alone
-    + item_head_fwd_stages(C), bit for bit, including InfoNCE's l2norm outputs."""
+    """ttmi_user_item_head_fwd_c (user head + item stage C on one grid) and
+    ttmi_user_item_head_fwd_ac (user head + item stages A and C on one grid, C waiting for A's
+    BatchNorm statistics inside the launch) == the user head alone + item_head_fwd_stages(A, C),
+    bit for bit, including InfoNCE's l2norm outputs and the running statistics, on repeated
+    calls (the in-launch counts are left zero)."""
     ops = gpu_pkg.ops
     D, F = 128, 512
     g = torch.Generator().manual_seed(B + 9)
@@ -132,29 +135,36 @@ def test_user_head_item_c_equals_separate(gpu_pkg, B, p):
                     az=torch.full((B, D), 7, dtype=torch.bfloat16, **f), mz=torch.full((B,), 7., **f),
                     rz=torch.full((B,), 7., **f), u=torch.full((B, D), 7., **f))
 
-    def run(co):
+    def run(mode):
         uo, io = uouts(), _item_outs(B)
         nrm = torch.full((2 * B,), 7., device=DEV)
         uh, ih = torch.full((B, D), 7., device=DEV), torch.full((B, D), 7., device=DEV)
         io["out_hat"], io["out_norm"] = ih, nrm[B:]
-        d = ops.item_head_desc(modal, Wi, Pi, _bufs(), drop_i, 1e-5, io)
-        ops.item_head_fwd_stages(d, 1)                        # stage A (+ the BatchNorm merge)
-        if co:
-            ops.user_head_fwd(ctx, res, drows, Wu, Pu, pre, gender, country, 1e-5, drops, uo,
-                              co_item=d, normed=(uh, nrm[:B]), co_stage="C")
-        else:
+        bufs = _bufs()
+        d = ops.item_head_desc(modal, Wi, Pi, bufs, drop_i, 1e-5, io)
+        if mode != "AC":
+            ops.item_head_fwd_stages(d, 1)                    # stage A (+ the BatchNorm merge)
+        if mode == "sep":
             ops.user_head_fwd(ctx, res, drows, Wu, Pu, pre, gender, country, 1e-5, drops, uo,
                               normed=(uh, nrm[:B]))
             ops.item_head_fwd_stages(d, 6)
-        torch.cuda.synchronize()
-        return uo, io, uh, ih, nrm
-    a, b = run(False), run(True)
-    for x, y in zip(a, b):
-        if isinstance(x, dict):
-            for k in x:
-                assert torch.equal(x[k], y[k]), k
         else:
-            assert torch.equal(x, y)
+            ops.user_head_fwd(ctx, res, drows, Wu, Pu, pre, gender, country, 1e-5, drops, uo,
+                              co_item=d, normed=(uh, nrm[:B]), co_stage=mode)
+        torch.cuda.synchronize()
+        if mode == "AC":      # every in-launch count left zero, no C workgroup's poll timed out
+            cnt = ops._zero_ws("ttmi_item_head_bn_counter_bytes", (0,), modal.device)
+            assert int(cnt.view(torch.int32).abs().sum()) == 0
+        return uo, io, uh, ih, nrm, bufs
+    ref = run("sep")
+    for mode in ("C", "AC", "AC", "AC"):
+        got = run(mode)
+        for x, y in zip(ref, got):
+            if isinstance(x, dict):
+                for k in x:
+                    assert torch.equal(x[k], y[k]), (mode, k)
+            else:
+                assert torch.equal(x, y), mode
 
 
 @pytest.mark.parametrize("B,p,dt", [(512, 0.1, torch.bfloat16), (37, 0.0, torch.bfloat16),

@@ -83,12 +83,14 @@ def test_gemm_epilogue(gpu_pkg, dtype):
 
 
 @pytest.mark.parametrize("M,N,K", [(3000, 384, 128), (4100, 512, 128), (2100, 128, 512),
-                                   (2048, 128, 384), (2500, 256, 256), (2048, 128, 128)])
+                                   (2048, 128, 384), (2500, 256, 256), (2048, 128, 128),
+                                   (3000, 768, 256), (25600, 1024, 256), (2100, 512, 256)])
 @pytest.mark.parametrize("epi", ["res", "gate_bf16", "gate_f32", "none"])
 def test_gemm_row_panel(gpu_pkg, M, N, K, epi):
     """Skinny-K row-panel kernel (persistent, W-stationary): each epilogue family, fp32 and
     bf16 out, rows not a multiple of the tile; shapes without a panel instantiation take the
-    generic kernel and must agree just the same."""
+    generic kernel and must agree just the same.  N = 512 / 768 / 1,024 at K = 256 (the D = 256
+    encoder): column-sliced panels, 256 columns per workgroup (ABI 19)."""
     ops = gpu_pkg.ops
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16)
@@ -482,12 +484,12 @@ def test_gather_scatter_rows(gpu_pkg):
 
 # ------------------------------------------------------------------------------ embedding
 @pytest.mark.parametrize("p,deferred", [(0.0, False), (0.1, False), (0.1, True)])
-def test_seq_embed_fwd_bwd(gpu_pkg, p, deferred):
+@pytest.mark.parametrize("B,L,D,V", [(37, 50, 128, 301), (64, 20, 128, 997), (9, 20, 256, 50)])
+def test_seq_embed_fwd_bwd(gpu_pkg, p, deferred, B, L, D, V):
     """seq_embed_fwd/bwd vs torch autograd.  deferred (ABI 15): inside deferred_wgrad the LN
     partials are folded by the weight-gradient fold (accumulate bit 2 leaves the workspace
     zero), so two deferred calls in a row must each give the same gradients."""
     ops = gpu_pkg.ops
-    B, L, D, V = 37, 50, 128, 301
     g = torch.Generator().manual_seed(9)
     ids = torch.randint(0, V, (B, L), generator=g)
     E = torch.randn(V, D, generator=g)
@@ -506,6 +508,9 @@ def test_seq_embed_fwd_bwd(gpu_pkg, p, deferred):
     sd = seed_dev(seed)
     ops.seq_embed_fwd(ids.to(DEV), Ed, Pd, wd, bd, x, mean, rstd, drop=(p, sd))
     assert rel(x, x_ref.reshape(B * L, D)) < 2e-5
+    xe = TF.embedding(ids, E) + P[None]
+    assert rel(mean, xe.mean(-1).reshape(-1)) < 1e-5
+    assert rel(rstd, 1.0 / torch.sqrt(xe.var(-1, unbiased=False) + 1e-5).reshape(-1)) < 1e-5
     dx = torch.randn(B * L, D, generator=g)
     x_ref.reshape(B * L, D).backward(dx)
     dE = torch.zeros(V, D, device=DEV)
@@ -696,14 +701,16 @@ def test_transpose_batch(gpu_pkg):
         assert torch.equal(d.cpu(), s_.t().cpu())
 
 
-@pytest.mark.parametrize("M,K", [(3000, 384), (2048, 512), (100, 128), (512, 256)])
+@pytest.mark.parametrize("D,M,K", [(128, 3000, 384), (128, 2048, 512), (128, 100, 128), (128, 512, 256),
+                                   (256, 3000, 768), (256, 2048, 1024), (256, 100, 256),
+                                   (256, 512, 512), (256, 25600, 1024)])
 @pytest.mark.parametrize("with_res,with_next", [(True, True), (False, False), (True, False)])
-def test_linear_ln_bwd(gpu_pkg, M, K, with_res, with_next):
+def test_linear_ln_bwd(gpu_pkg, D, M, K, with_res, with_next):
     """Fused Linear input grad + LayerNorm backward (+ dropout backward) vs torch autograd
-    on the same bf16 operands (fp32 math): dx, LN dw/db, and the bf16 dropout output."""
+    on the same bf16 operands (fp32 math): dx, LN dw/db, and the bf16 dropout output.
+    D = 256: the streamed-W panel (panel256_kernel, ABI 19)."""
     ops = gpu_pkg.ops
-    D = 128
-    g = torch.Generator().manual_seed(M + K)
+    g = torch.Generator().manual_seed(M + K + D)
     dh = torch.randn(M, K, generator=g).to(torch.bfloat16)
     wt = (torch.randn(D, K, generator=g) / math.sqrt(K)).to(torch.bfloat16)
     x = torch.randn(M, D, generator=g) * 2 + 0.5
@@ -754,14 +761,16 @@ def test_linear_ln_bwd(gpu_pkg, M, K, with_res, with_next):
         assert torch.equal(outs[0][2], dx)
 
 
-@pytest.mark.parametrize("M,K", [(300, 128), (4096, 512), (25600, 128)])
+@pytest.mark.parametrize("D,M,K", [(128, 300, 128), (128, 4096, 512), (128, 25600, 128),
+                                   (256, 300, 256), (256, 4096, 1024), (256, 25600, 256),
+                                   (256, 25600, 1024), (256, 1000, 768)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_linear_res_ln(gpu_pkg, M, K, p):
+def test_linear_res_ln(gpu_pkg, D, M, K, p):
     """Fused out = res + dropout(x·wᵀ + b) and y = LN(out) (ttmi_linear_res_ln) vs fp32 torch
-    on the same bf16 operands: out to fp32 accumulation error, y to bf16 rounding, row stats."""
+    on the same bf16 operands: out to fp32 accumulation error, y to bf16 rounding, row stats.
+    D = 256: the streamed-W panel (ABI 19)."""
     ops = gpu_pkg.ops
-    D = 128
-    g = torch.Generator().manual_seed(M + K + int(p * 10))
+    g = torch.Generator().manual_seed(M + K + D + int(p * 10))
     x = torch.randn(M, K, generator=g).to(torch.bfloat16)
     w = (torch.randn(D, K, generator=g) / math.sqrt(K)).to(torch.bfloat16)
     b = torch.randn(D, generator=g)

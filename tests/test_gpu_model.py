@@ -277,11 +277,19 @@ def test_dropout_on_matches_oracle_hash(gpu_pkg, L):
                                      running=running)
     lo.backward()
     mine = dict(m.named_parameters())
+    # A single ReLU whose input sits within ~1e-7 of zero flips with the summation order: the
+    # fp32 oracle itself, with its item embedding perturbed by 2e-7 relative, moves to 7.4e-4
+    # (item embedding rows) and 3.3e-3 (linear1 rows) of its unperturbed gradients at L = 20
+    # (one token's row, one hidden unit's row).  So all rows but at most 2 are held to 1e-4 and
+    # those 2 to 1e-2 (a mask or indexing error moves many rows, or one by O(1)).
     for k in ("user_tower.item_embedding.weight",
               "user_tower.transformer_encoder.layers.0.linear1.weight",
               "user_tower.transformer_encoder.layers.1.self_attn.in_proj_weight",
               "item_tower.fusion_layer.4.weight"):
-        assert rel(mine[k].grad, params[k].grad) < 1e-4, k
+        a, b = mine[k].grad.detach().double().cpu(), params[k].grad.double()
+        rows = (a - b).abs().reshape(a.shape[0], -1).amax(1) / b.abs().max()
+        top = rows.sort(descending=True).values
+        assert top[2:].max().item() < 1e-4 and top[0].item() < 1e-2, (k, top[:4].tolist())
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
@@ -416,7 +424,11 @@ def test_cfg2_bf16_trainstep_vs_oracle_full_size(gpu_pkg, D, p):
         check_bf16_grad(k, grads1[k], g_ref[k], g_emu[k])
         d_gpu, d_ref, d_emu = got[k] - p0[k].double(), p_ref[k] - p0[k].double(), p_emu[k] - p0[k].double()
         c_gpu, c_emu = cosine(d_gpu, d_ref), cosine(d_emu, d_ref)
-        assert c_gpu >= c_emu - 0.05, (k, c_gpu, c_emu)
+        # AdamW's first steps are near sign(g): a tiny parameter's update direction moves with
+        # rounding alone (gender embedding, 48 values: the emulation's own cosine spreads
+        # 0.923-0.950 under 2e-7 perturbations, tools/diag_update_spread.py)
+        margin = 0.05 if d_ref.numel() >= 1024 else 0.10
+        assert c_gpu >= c_emu - margin, (k, c_gpu, c_emu)
         n_gpu, n_emu = d_gpu.norm() / d_ref.norm(), d_emu.norm() / d_ref.norm()
         assert abs(n_gpu - 1) <= 2 * abs(n_emu - 1) + 0.05, (k, float(n_gpu), float(n_emu))
 

@@ -19,7 +19,7 @@ pkg.lib.load(os.environ["TTMI_LIB"])
 ops = pkg.ops
 NB, NW, NP = 512, 16, 8
 lib = pkg.lib._lib
-for tu in ("gemm", "head"):
+for tu in ("gemm", "head", "infonce"):
     getattr(lib, "ttmi_dbg_stamps_" + tu).argtypes = [ctypes.c_void_p, ctypes.c_int64]
 buf = (ctypes.c_uint64 * (NB * NW * NP))()
 
@@ -110,6 +110,21 @@ def main():
              mz=f32(B), rz=f32(B), u=f32(B, D))
     stamps(lambda: ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, o),
            "user head fwd (B=512)", tu="head")
+    # InfoNCE at B = 512 (phases: fwd 0 start, 1 Q staged, 2 logit tiles done, 3 partials
+    # retired, 4 arrival counted, 5 block combine done, 6 final combine; bwd 0 start,
+    # 1 G.V MFMAs done, 2 partials retired, 3 arrival counted, 4 finish done)
+    F_ = pkg.functional
+    u, it = f32(B, D), f32(B, D)
+    uid = torch.randint(0, 840, (B,), generator=g).to(dev)
+    _, _, _, _, st = F_.infonce_fwd(u, it, uid)
+    loss = torch.empty((), device=dev)
+    stamps(lambda: ops.infonce_fwd_pre(uid, st.inv_tau, st.u_hat, st.i_hat, st.norms, st.logits, st.lse,
+                                       loss, st.ws),
+           "infonce fwd (B=512)", tu="infonce")
+    du, di = torch.empty(B, D, device=dev), torch.empty(B, D, device=dev)
+    du16 = torch.empty(B, D, device=dev, dtype=torch.bfloat16)
+    stamps(lambda: ops.infonce_bwd(st.u_hat, st.i_hat, st.norms, st.logits, st.lse, uid, st.inv_tau, None,
+                                   du, di, st.ws, du16), "infonce bwd fused (B=512)", nph=5, tu="infonce")
 
 
 if __name__ == "__main__":
