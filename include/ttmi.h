@@ -130,6 +130,23 @@ int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int nf,
  * when this runs (the caller keeps them alive and unmodified).  ABI 10. */
 int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int nf,
                      const ttmi_fold_desc* folds, hipStream_t stream);
+/* ABI 19: the fold of ttmi_wgrad_batch left to the optimizer.  ttmi_wgrad_batch_plan runs the
+ * grouped GEMMs and records their partials' segments (and the generic folds') in `plan` instead
+ * of folding them (plan->n = 0 when they do not fit: then it folds them itself);
+ * ttmi_adamw_folded is ttmi_adamw_fx that sums each planned segment in the fold's order and
+ * applies AdamW to it in the same launch (one process: nothing reads the folded gradient in
+ * between).  The partials' workspaces must stay alive and unmodified until it has run; a plan
+ * whose segments do not tile the flat buffer in float4 units folds first, then updates. */
+typedef struct ttmi_fold_plan {
+  int32_t n, reserved;
+  uint64_t seg[32 * 16];           /* opaque */
+} ttmi_fold_plan;
+int ttmi_wgrad_batch_plan(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                          const ttmi_fold_desc* folds, ttmi_fold_plan* plan, hipStream_t stream);
+int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
+                      const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
+                      int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
+                      hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0) — TransformerEncoderLayer

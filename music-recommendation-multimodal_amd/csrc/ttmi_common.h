@@ -163,6 +163,32 @@ TTMI_DEV void fx_add(int64_t* p, float v, int shift) {
 TTMI_DEV double fx_to_d(int64_t q, int shift) { return __builtin_ldexp((double)q, -shift); }
 TTMI_DEV float fx_to_f(int64_t q, int shift) { return (float)fx_to_d(q, shift); }
 
+// ---------------------------------------------------------------- AdamW (torch.optim.AdamW)
+// Non-amsgrad, maximize=False.  The scalar terms in double, as torch computes them on the host
+// (then used as f32 scalars); shared by adamw_kernel and the fold-fused AdamW (ttmi_gemm.hip) so
+// both run the same arithmetic.  hyper = {lr, beta1, beta2, eps, weight_decay}, step = t.
+struct AdamScalars { float step_size, bc2_sqrt, decay, b1c, b2, b2c, eps; };
+TTMI_DEV AdamScalars adam_scalars(const double* hyper, const int32_t* step) {
+  const double lr = hyper[0], b1d = hyper[1], b2d = hyper[2], wd = hyper[4];
+  const double tt = (double)step[0];
+  AdamScalars a;
+  a.step_size = (float)(lr / (1.0 - pow(b1d, tt)));
+  a.bc2_sqrt = (float)sqrt(1.0 - pow(b2d, tt));
+  a.decay = (float)(1.0 - lr * wd);
+  a.b1c = (float)(1.0 - b1d);
+  a.b2 = (float)b2d;
+  a.b2c = (float)(1.0 - b2d);
+  a.eps = (float)hyper[3];
+  return a;
+}
+TTMI_DEV void adam_upd(const AdamScalars& a, float& P, float G, float& Mv, float& Vv) {
+  P *= a.decay;
+  Mv += a.b1c * (G - Mv);                         // exp_avg.lerp_(grad, 1-beta1)
+  Vv = Vv * a.b2 + a.b2c * (G * G);               // exp_avg_sq.mul_(b2).addcmul_(g,g,1-b2)
+  const float denom = sqrtf(Vv) / a.bc2_sqrt + a.eps;
+  P -= a.step_size * (Mv / denom);
+}
+
 // ---------------------------------------------------------------- XCD-aware block order
 // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  This bijection of
 // [0, n) gives each XCD a contiguous run of logical ids, so neighbouring logical blocks that

@@ -26,6 +26,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <vector>
 
 namespace {
 
@@ -1634,8 +1636,12 @@ TTMI_DEV void fold_store(const FoldSeg& sg, int64_t u, int64_t nq, float4 v) {
 // slabs (a LayerNorm's per-workgroup column sums, S ~ 229, 32-64 units), where 4 partitions
 // meant ~57 dependent loads per thread in 4 serial batches.
 constexpr int FOLD_WIDE_S = 32;
-template <int P>
-TTMI_DEV void fold_parts(const FoldSeg& sg, int bx, int nbx, bool consume, int64_t nel, int64_t nq) {
+// The fold of one segment's units over this block's share [bx, nbx), handing each finished
+// unit to store4(u, float4 sum) (a 4-column weight unit) or store1(m, sum) (a bias row):
+// wgrad_fold_kernel stores them into the gradient, adamw_fold_kernel updates the parameters.
+template <int P, class S4, class S1>
+TTMI_DEV void fold_parts(const FoldSeg& sg, int bx, int nbx, bool consume, int64_t nel, int64_t nq,
+                         S4& store4, S1& store1) {
   constexpr int U = 256 / P;
   __shared__ float4 red[256];
   const int ul = threadIdx.x % U, q = threadIdx.x / U;
@@ -1665,15 +1671,54 @@ TTMI_DEV void fold_parts(const FoldSeg& sg, int bx, int nbx, bool consume, int64
         const float4 w = red[k * U + ul];
         v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
       }
-      if (u < nel) {
-        fold_store(sg, u, nq, v);
-      } else {
-        const int64_t m = u - nel;
-        sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v.x : v.x;
-      }
+      if (u < nel) store4(u, v);
+      else store1(u - nel, v.x);
     }
     __syncthreads();
   }
+}
+
+template <class S4, class S1>
+TTMI_DEV void fold_segment(const FoldSeg& sg, int bx, int nbx, S4& store4, S1& store1) {
+  const int64_t nq = sg.N / 4, nel = sg.M * nq;
+  const bool consume = (sg.acc & 2) != 0;
+  if (sg.S <= 2) {            // few partials (a fixed-point accumulator): one unit per thread
+    for (int64_t u = (int64_t)bx * 256 + threadIdx.x; u < sg.units; u += (int64_t)nbx * 256) {
+      if (u < nel) {
+        const int64_t m = u / nq, n = (u % nq) * 4;
+        store4(u, fold_unit(sg, m * sg.N + n, 0, sg.S, consume));
+      } else {                // a weight gradient's bias: the split row sums
+        const int64_t m = u - nel;
+        float v = 0.f;
+        for (int s = 0; s < sg.S; ++s) v += sg.part_rs[(int64_t)s * sg.M + m];
+        store1(m, v);
+      }
+    }
+    return;
+  }
+  if (sg.S > FOLD_WIDE_S) fold_parts<16>(sg, bx, nbx, consume, nel, nq, store4, store1);
+  else fold_parts<4>(sg, bx, nbx, consume, nel, nq, store4, store1);
+}
+
+// The last k < n with begin[k] <= b, by binary search over a kernel-argument array (dependent
+// scalar loads: 5 for 32 entries instead of a walk)
+template <class KA>
+TTMI_DEV int find_job(KA begin, int n, int b) {
+  int k = 0;
+  for (int lo = 0, hi = n - 1; lo <= hi;) {
+    const int mid = (lo + hi) >> 1;
+    if (begin[mid] <= b) { k = mid; lo = mid + 1; } else { hi = mid - 1; }
+  }
+  return k;
+}
+
+TTMI_DEV FoldSeg load_seg(const __attribute__((address_space(4))) FoldSeg& sgk) {
+  FoldSeg sg;
+  sg.part = sgk.part; sg.part_rs = sgk.part_rs; sg.C = sgk.C; sg.rs = sgk.rs;
+  sg.M = sgk.M; sg.N = sgk.N; sg.ldc = sgk.ldc; sg.units = sgk.units; sg.base = 0;
+  sg.s_stride = sgk.s_stride;
+  sg.S = sgk.S; sg.acc = sgk.acc; sg.fx = sgk.fx;
+  return sg;
 }
 
 __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
@@ -1682,38 +1727,122 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
   // units: launching the largest segment's block count for every segment dispatched tens of
   // thousands of empty blocks)
   const KFoldArgs ka = (KFoldArgs)__builtin_amdgcn_kernarg_segment_ptr();
-  // the last k with blk_begin[k] <= blockIdx.x, by binary search (5 dependent scalar loads
-  // for 32 segments instead of a walk of up to 31)
-  int k = 0;
-  for (int lo = 0, hi = ka->n - 1; lo <= hi;) {
-    const int mid = (lo + hi) >> 1;
-    if (ka->blk_begin[mid] <= (int)blockIdx.x) { k = mid; lo = mid + 1; } else { hi = mid - 1; }
-  }
+  const int k = find_job(ka->blk_begin, ka->n, (int)blockIdx.x);
   const int bx = (int)blockIdx.x - ka->blk_begin[k], nbx = ka->blk_begin[k + 1] - ka->blk_begin[k];
-  const auto& sgk = ka->seg[k];
-  FoldSeg sg;
-  sg.part = sgk.part; sg.part_rs = sgk.part_rs; sg.C = sgk.C; sg.rs = sgk.rs;
-  sg.M = sgk.M; sg.N = sgk.N; sg.ldc = sgk.ldc; sg.units = sgk.units; sg.base = 0;
-  sg.s_stride = sgk.s_stride;
-  sg.S = sgk.S; sg.acc = sgk.acc; sg.fx = sgk.fx;
-  const int64_t nq = sg.N / 4, nel = sg.M * nq;
-  const bool consume = (sg.acc & 2) != 0;
-  if (sg.S <= 2) {            // few partials (a fixed-point accumulator): one unit per thread
-    for (int64_t u = (int64_t)bx * 256 + threadIdx.x; u < sg.units; u += (int64_t)nbx * 256) {
-      if (u < nel) {
-        const int64_t m = u / nq, n = (u % nq) * 4;
-        fold_store(sg, u, nq, fold_unit(sg, m * sg.N + n, 0, sg.S, consume));
-      } else {                // a weight gradient's bias: the split row sums
-        const int64_t m = u - nel;
-        float v = 0.f;
-        for (int s = 0; s < sg.S; ++s) v += sg.part_rs[(int64_t)s * sg.M + m];
-        sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v : v;
+  const FoldSeg sg = load_seg(ka->seg[k]);
+  const int64_t nq = sg.N / 4;
+  auto store4 = [&](int64_t u, float4 v) { fold_store(sg, u, nq, v); };
+  auto store1 = [&](int64_t m, float v) { sg.rs[m] = (sg.acc & 1) ? sg.rs[m] + v : v; };
+  fold_segment(sg, bx, nbx, store4, store1);
+}
+
+// ----------------------------------------------------- AdamW with the gradient fold fused
+// One process (no gradient all-reduce between the fold and the update): the fold's segments
+// (weight-gradient split partials, LayerNorm per-workgroup sums, fixed-point accumulators) are
+// summed in the fold's order and applied by AdamW right there, instead of stored into the flat
+// gradient by wgrad_fold_kernel and read back by adamw_kernel: one launch and one round trip of
+// those gradients less per step.  The grid is jobs: plain AdamW over the flat ranges no segment
+// covers (float4 units, 512 per block, the fixed-point range read from fx as adamw_kernel does),
+// then one job per segment.
+constexpr int AF_SEGS = FOLD_SEGS, AF_PLAIN = 40;
+struct AdamFoldArgs {
+  float* p; float* g; float* m; float* v; bf16_t* pb;
+  const double* hyper; const int32_t* step;
+  int64_t* fx; int64_t fx_lo, fx_hi; int fx_shift, zero_grad;
+  int nplain, nseg;
+  int blk_begin[AF_PLAIN + AF_SEGS + 1];
+  int plo[AF_PLAIN], phi[AF_PLAIN];             // float4 units
+  FoldSeg seg[AF_SEGS];
+};
+typedef const __attribute__((address_space(4))) AdamFoldArgs* KAdamFoldArgs;
+
+__global__ __launch_bounds__(256) void adamw_fold_kernel(AdamFoldArgs a) {
+  (void)a;
+  const KAdamFoldArgs ka = (KAdamFoldArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  const int nj = ka->nplain + ka->nseg;
+  const int k = find_job(ka->blk_begin, nj, (int)blockIdx.x);
+  const int bx = (int)blockIdx.x - ka->blk_begin[k], nbx = ka->blk_begin[k + 1] - ka->blk_begin[k];
+  float* __restrict__ p = ka->p;
+  float* __restrict__ g = ka->g;
+  float* __restrict__ mo = ka->m;
+  float* __restrict__ vo = ka->v;
+  bf16_t* __restrict__ pb = ka->pb;
+  const int zero_grad = ka->zero_grad;
+  const AdamScalars as = adam_scalars(ka->hyper, ka->step);
+  auto upd4 = [&](int64_t q, float4 gg) {
+    float4 pp = reinterpret_cast<const float4*>(p)[q];
+    float4 mm = reinterpret_cast<const float4*>(mo)[q];
+    float4 vv = reinterpret_cast<const float4*>(vo)[q];
+    adam_upd(as, pp.x, gg.x, mm.x, vv.x);
+    adam_upd(as, pp.y, gg.y, mm.y, vv.y);
+    adam_upd(as, pp.z, gg.z, mm.z, vv.z);
+    adam_upd(as, pp.w, gg.w, mm.w, vv.w);
+    reinterpret_cast<float4*>(p)[q] = pp;
+    reinterpret_cast<float4*>(mo)[q] = mm;
+    reinterpret_cast<float4*>(vo)[q] = vv;
+    if (pb) {
+      ushort4 o;
+      o.x = f2bf(pp.x); o.y = f2bf(pp.y); o.z = f2bf(pp.z); o.w = f2bf(pp.w);
+      reinterpret_cast<ushort4*>(pb)[q] = o;
+    }
+  };
+  if (k < ka->nplain) {
+    const int64_t lo = ka->plo[k], hi = ka->phi[k];
+    int64_t* fx = ka->fx;
+    const int64_t fx_lo = ka->fx_lo, fx_hi = ka->fx_hi;
+    const int fx_shift = ka->fx_shift;
+    constexpr int U = 2;
+    float4 gg[U];
+    int64_t q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      q[u] = lo + (int64_t)bx * (256 * U) + u * 256 + threadIdx.x;
+      const int64_t qc = min(q[u], hi - 1);
+      if (fx != nullptr && qc >= fx_lo && qc < fx_hi) {
+        const longlong2 x0 = reinterpret_cast<const longlong2*>(fx)[2 * (qc - fx_lo)];
+        const longlong2 x1 = reinterpret_cast<const longlong2*>(fx)[2 * (qc - fx_lo) + 1];
+        gg[u] = make_float4(fx_to_f(x0.x, fx_shift), fx_to_f(x0.y, fx_shift), fx_to_f(x1.x, fx_shift),
+                            fx_to_f(x1.y, fx_shift));
+      } else {
+        gg[u] = reinterpret_cast<const float4*>(g)[qc];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (q[u] >= hi) break;
+      upd4(q[u], gg[u]);
+      if (fx != nullptr && q[u] >= fx_lo && q[u] < fx_hi) {
+        reinterpret_cast<longlong2*>(fx)[2 * (q[u] - fx_lo)] = make_longlong2(0, 0);
+        reinterpret_cast<longlong2*>(fx)[2 * (q[u] - fx_lo) + 1] = make_longlong2(0, 0);
+      } else if (zero_grad) {
+        reinterpret_cast<float4*>(g)[q[u]] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
     return;
   }
-  if (sg.S > FOLD_WIDE_S) fold_parts<16>(sg, bx, nbx, consume, nel, nq);
-  else fold_parts<4>(sg, bx, nbx, consume, nel, nq);
+  const FoldSeg sg = load_seg(ka->seg[k - ka->nplain]);
+  const int64_t nq = sg.N / 4;
+  auto store4 = [&](int64_t u, float4 v) {       // fold_store's sum, then the update
+    const int64_t mr = u / nq, n = (u % nq) * 4;
+    float* cp = sg.C + mr * sg.ldc + n;
+    if (sg.acc & 1) {
+      const float4 c = *reinterpret_cast<const float4*>(cp);
+      v.x = c.x + v.x; v.y = c.y + v.y; v.z = c.z + v.z; v.w = c.w + v.w;
+    }
+    upd4((cp - g) / 4, v);
+    if (zero_grad) *reinterpret_cast<float4*>(cp) = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store1 = [&](int64_t mr, float v) {
+    float* rp = sg.rs + mr;
+    if (sg.acc & 1) v = *rp + v;
+    const int64_t e = rp - g;
+    float P = p[e], Mv = mo[e], Vv = vo[e];
+    adam_upd(as, P, v, Mv, Vv);
+    p[e] = P; mo[e] = Mv; vo[e] = Vv;
+    if (pb) pb[e] = f2bf(P);
+    if (zero_grad) *rp = 0.f;
+  };
+  fold_segment(sg, bx, nbx, store4, store1);
 }
 
 // ------------------------------------------- large token GEMM: 256x256x64 tiles, 8 waves
@@ -2647,7 +2776,7 @@ extern "C" int64_t ttmi_linear_ln_bwd_sum_blocks_n(int64_t M, int64_t N) {
 
 namespace {
 int wgrad_fold_impl(int n, const ttmi_wgrad_desc* const* descs, int nf, const ttmi_fold_desc* folds,
-                    hipStream_t stream, bool grouped) {
+                    hipStream_t stream, bool grouped, std::vector<FoldSeg>* collect = nullptr) {
   TTMI_REQUIRE(n >= 0 && (n == 0 || descs) && nf >= 0 && (nf == 0 || folds),
                "ttmi_wgrad_fold: bad arguments");
   FoldArgs f;
@@ -2670,6 +2799,7 @@ int wgrad_fold_impl(int n, const ttmi_wgrad_desc* const* descs, int nf, const tt
     sg.M = d->M; sg.N = d->N; sg.ldc = d->ldc; sg.units = d->M * (d->N / 4);
     sg.base = f.total; sg.s_stride = d->s_stride;
     sg.S = (int)d->S; sg.acc = d->accumulate; sg.fx = d->fx_shift;
+    if (collect) { collect->push_back(sg); continue; }
     f.seg[f.n++] = sg;
     f.total += sg.units;
   }
@@ -2690,6 +2820,7 @@ int wgrad_fold_impl(int n, const ttmi_wgrad_desc* const* descs, int nf, const tt
     }
     FoldSeg sg = fold_seg(d, p);
     sg.base = f.total;
+    if (collect) { collect->push_back(sg); continue; }
     f.seg[f.n++] = sg;
     f.total += sg.units;
   }
@@ -2702,8 +2833,9 @@ extern "C" int ttmi_wgrad_fold(int n, const ttmi_wgrad_desc* const* descs, int n
   return wgrad_fold_impl(n, descs, nf, folds, stream, false);
 }
 
-extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int nf,
-                                const ttmi_fold_desc* folds, hipStream_t stream) {
+namespace {
+int wgrad_batch_impl(int n, const ttmi_wgrad_desc* const* descs, int nf, const ttmi_fold_desc* folds,
+                     hipStream_t stream, std::vector<FoldSeg>* collect) {
   TTMI_REQUIRE(n >= 0 && (n == 0 || descs) && nf >= 0 && (nf == 0 || folds),
                "ttmi_wgrad_batch: bad arguments");
   WgradGroup grp;
@@ -2762,7 +2894,125 @@ extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int 
   }
   int rc = flush();
   if (rc) return rc;
-  return wgrad_fold_impl(n, descs, nf, folds, stream, true);
+  return wgrad_fold_impl(n, descs, nf, folds, stream, true, collect);
+}
+
+// The segments of a plan, launched as ordinary folds (the fused update's fallback).
+int launch_fold_segs(const FoldSeg* segs, int n, hipStream_t s) {
+  FoldArgs f;
+  f.n = 0;
+  f.total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (f.n == FOLD_SEGS) {
+      int rc = launch_fold(f, s);
+      if (rc) return rc;
+      f.n = 0;
+      f.total = 0;
+    }
+    f.seg[f.n] = segs[i];
+    f.seg[f.n].base = f.total;
+    f.total += segs[i].units;
+    ++f.n;
+  }
+  return launch_fold(f, s);
+}
+
+int fold_blocks(const FoldSeg& sg) {        // launch_fold's per-segment block count
+  const int per = sg.S <= 2 ? 256 : sg.S > FOLD_WIDE_S ? 16 : 64;
+  return (int)std::max<int64_t>(1, std::min<int64_t>((sg.units + per - 1) / per, 1024));
+}
+}  // namespace
+
+extern "C" int ttmi_wgrad_batch(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                                const ttmi_fold_desc* folds, hipStream_t stream) {
+  return wgrad_batch_impl(n, descs, nf, folds, stream, nullptr);
+}
+
+static_assert(sizeof(FoldSeg) * AF_SEGS <= sizeof(((ttmi_fold_plan*)nullptr)->seg), "fold plan storage");
+
+extern "C" int ttmi_wgrad_batch_plan(int n, const ttmi_wgrad_desc* const* descs, int nf,
+                                     const ttmi_fold_desc* folds, ttmi_fold_plan* plan, hipStream_t stream) {
+  TTMI_REQUIRE(plan != nullptr, "ttmi_wgrad_batch_plan: null plan");
+  plan->n = 0;
+  std::vector<FoldSeg> segs;
+  int rc = wgrad_batch_impl(n, descs, nf, folds, stream, &segs);
+  if (rc) return rc;
+  if ((int)segs.size() > AF_SEGS || getenv("TTMI_NO_FOLD_PLAN"))   // too many: fold them now
+    return launch_fold_segs(segs.data(), (int)segs.size(), stream);
+  memcpy(plan->seg, segs.data(), segs.size() * sizeof(FoldSeg));
+  plan->n = (int32_t)segs.size();
+  return TTMI_OK;
+}
+
+extern "C" int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
+                                 const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
+                                 int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
+                                 hipStream_t s) {
+  if (!plan || plan->n <= 0)
+    return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, s);
+  TTMI_REQUIRE(plan->n <= AF_SEGS, "ttmi_adamw_folded: bad plan");
+  const FoldSeg* segs = reinterpret_cast<const FoldSeg*>(plan->seg);
+  // the flat ranges the segments update (float4 units), which the plain jobs then skip
+  std::vector<std::pair<int64_t, int64_t>> cov;
+  bool ok = n % 4 == 0 && n / 4 < INT_MAX && ((uintptr_t)g & 15) == 0;
+  for (int i = 0; ok && i < plan->n; ++i) {
+    const FoldSeg& sg = segs[i];
+    const int64_t c0 = sg.C - g, clen = sg.M == 1 ? sg.N : (sg.ldc == sg.N ? sg.M * sg.N : -1);
+    ok = clen > 0 && c0 >= 0 && c0 % 4 == 0 && clen % 4 == 0 && c0 + clen <= n;
+    if (ok) cov.push_back({c0 / 4, (c0 + clen) / 4});
+    const bool has_rs = sg.units > sg.M * (sg.N / 4);
+    if (ok && has_rs) {
+      const int64_t r0 = sg.rs - g;
+      ok = sg.rs && r0 >= 0 && r0 % 4 == 0 && sg.M % 4 == 0 && r0 + sg.M <= n;
+      if (ok) cov.push_back({r0 / 4, (r0 + sg.M) / 4});
+    }
+  }
+  if (ok && fx) cov.push_back({fx_off / 4, (fx_off + fx_len) / 4});   // must not overlap: checked below
+  std::sort(cov.begin(), cov.end());
+  for (size_t i = 1; ok && i < cov.size(); ++i) ok = cov[i].first >= cov[i - 1].second;
+  AdamFoldArgs a;
+  a.nplain = 0;
+  if (ok) {                   // the complement of the segments' ranges (the fx range stays plain)
+    int64_t at = 0;
+    const int64_t fxl = fx ? fx_off / 4 : -1, fxh = fx ? (fx_off + fx_len) / 4 : -1;
+    for (const auto& r : cov) {
+      if (r.first == fxl && r.second == fxh) continue;
+      if (r.first > at) {
+        if (a.nplain == AF_PLAIN) { ok = false; break; }
+        a.plo[a.nplain] = (int)at;
+        a.phi[a.nplain++] = (int)r.first;
+      }
+      at = r.second;
+    }
+    if (ok && at < n / 4) {
+      if (a.nplain == AF_PLAIN) ok = false;
+      else { a.plo[a.nplain] = (int)at; a.phi[a.nplain++] = (int)(n / 4); }
+    }
+  }
+  if (!ok) {                  // layout the fused form cannot take: fold, then the plain update
+    int rc = launch_fold_segs(segs, plan->n, s);
+    if (rc) return rc;
+    return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, s);
+  }
+  TTMI_REQUIRE(((uintptr_t)p & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0 &&
+               ((uintptr_t)p_bf16 & 7) == 0, "ttmi_adamw_folded: buffers must be 16-B aligned (bf16 mirror 8-B)");
+  a.p = p; a.g = g; a.m = m; a.v = v; a.pb = (bf16_t*)p_bf16;
+  a.hyper = hyper; a.step = step; a.zero_grad = zero_grad;
+  a.fx = fx; a.fx_lo = fx ? fx_off / 4 : 0; a.fx_hi = fx ? (fx_off + fx_len) / 4 : 0; a.fx_shift = fx_shift;
+  a.nseg = plan->n;
+  int nb = 0;
+  for (int j = 0; j < a.nplain; ++j) {
+    a.blk_begin[j] = nb;
+    nb += (int)((a.phi[j] - a.plo[j] + 511) / 512);
+  }
+  for (int i = 0; i < a.nseg; ++i) {
+    a.seg[i] = segs[i];
+    a.blk_begin[a.nplain + i] = nb;
+    nb += fold_blocks(segs[i]);
+  }
+  a.blk_begin[a.nplain + a.nseg] = nb;
+  hipLaunchKernelGGL(adamw_fold_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
+  return ttmi_check_launch("ttmi_adamw_folded");
 }
 
 TTMI_STAMP_DUMP(gemm)

@@ -224,16 +224,20 @@ TTMI_DEV float ld_agent(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // 16-byte write-through (sc1) store / load for data handed to another workgroup inside a launch
-// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms row 1).
-TTMI_DEV void st16_wt(float* p, float4 v) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
+// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms row 1).  The buffer resource is
+// built from a workgroup-uniform base (it lives in SGPRs) and each lane passes its byte offset:
+// a per-lane base makes hipcc wrap every access in a readfirstlane loop over the 64 lanes, which
+// cost this launch ~70 us (a 64-way serialised load per access).
+TTMI_DEV void st16_wt(float* base, uint32_t off, float4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
   const i32x4_t q = {(int)__float_as_uint(v.x), (int)__float_as_uint(v.y), (int)__float_as_uint(v.z),
                      (int)__float_as_uint(v.w)};
-  __builtin_amdgcn_raw_buffer_store_b128(q, r, 0, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(q, r, off, 0, 16);
 }
-TTMI_DEV float4 ld16_wt(const float* p) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 16, 0x00020000);
-  const i32x4_t q = __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 16);
+TTMI_DEV float4 ld16_wt(const float* base, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7FFFFFFF, 0x00020000);
+  const i32x4_t q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
   return make_float4(__int_as_float(q.x), __int_as_float(q.y), __int_as_float(q.z), __int_as_float(q.w));
 }
 constexpr int BN_DONE = IN1 / 64, BN_CDONE = IN1 / 64 + 1;   // bncnt slots past the quarters'
@@ -241,6 +245,7 @@ constexpr int BN_DONE = IN1 / 64, BN_CDONE = IN1 / 64 + 1;   // bncnt slots past
 // Item head stage A on row block bx, column quarter q (item_head_a_kernel, or the workgroups
 // of ttmi_user_item_head_fwd past the user head's).
 TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
+  TTMI_TSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = bx * HR;
   const int n0 = 64 * q + 16 * w;                    // this wave's 16 of the 512 columns
@@ -262,9 +267,10 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   const int m = r0 + li;
   if (m < a.B) {
     const float4 zo = make_float4(v[0][0] + bias.x, v[0][1] + bias.y, v[0][2] + bias.z, v[0][3] + bias.w);
-    if (a.fin) st16_wt(a.z + (int64_t)m * IN1 + n0 + 4 * g, zo);     // read by this launch's C
+    if (a.fin) st16_wt(a.z, (uint32_t)(((int64_t)m * IN1 + n0 + 4 * g) * 4), zo);   // read by this launch's C
     else *reinterpret_cast<float4*>(a.z + (int64_t)m * IN1 + n0 + 4 * g) = zo;
   }
+  TTMI_TSTAMP(1);
   if (a.bncnt == nullptr) return;
   // ---- fused BatchNorm statistics: this block's (mean, M2) of its 4 x 16 columns over its
   // valid rows (the 16 lanes of a lane group share the columns), exchanged through agent-scope
@@ -334,6 +340,7 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid == 0) __hip_atomic_fetch_add(a.bncnt + BN_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  TTMI_TSTAMP(2);
 }
 
 struct ItemLdsC {
@@ -347,6 +354,7 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = bx * HR;
   const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
+  TTMI_TSTAMP(0);
   if (a.fin) {
     // stage A runs in this launch: wait until the IN1/64 column-quarter mergers have published
     // the batch statistics (one lane polls the count, sc1 loads with s_sleep; bounded: on a
@@ -369,20 +377,21 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
     }
     __syncthreads();
   }
+  TTMI_TSTAMP(3);
   if (a.bncnt != nullptr) {      // fused BatchNorm: y1 = drop(relu(BN(z))) staged from z rows
     float4 zv[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-      const float* zp = a.z + (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4;
-      zv[k] = a.fin ? ld16_wt(zp) : *reinterpret_cast<const float4*>(zp);
+      const int64_t zo = (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4;
+      zv[k] = a.fin ? ld16_wt(a.z, (uint32_t)(zo * 4)) : *reinterpret_cast<const float4*>(a.z + zo);
     }
     const DropKeys dk = resolve_drop(a.bd);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-      const float4 mu = a.fin ? ld16_wt(a.bmean + 4 * c4) : *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
-      const float4 rs = a.fin ? ld16_wt(a.brstd + 4 * c4) : *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
+      const float4 mu = a.fin ? ld16_wt(a.bmean, 16u * c4) : *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
+      const float4 rs = a.fin ? ld16_wt(a.brstd, 16u * c4) : *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
       const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
       const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
       float x[4] = {fmaxf((zv[k].x - mu.x) * rs.x * ww.x + bb.x, 0.f), fmaxf((zv[k].y - mu.y) * rs.y * ww.y + bb.y, 0.f),
@@ -451,6 +460,7 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
   }
   if (mrow && lane < 16 && w == 0) { a.m5[m] = mu; a.r5[m] = rs; }
   row_l2norm(oo, a.ohat, a.onrm, m, mrow, n0, L, w, lane);
+  TTMI_TSTAMP(4);
 }
 
 __global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {

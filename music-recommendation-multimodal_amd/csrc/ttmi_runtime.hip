@@ -80,21 +80,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
       vv[u] = reinterpret_cast<const float4*>(v)[q];
     }
   }
-  // scalar terms in double, as torch computes them on the host (then used as f32 scalars)
-  const double lr = hyper[0], b1d = hyper[1], b2d = hyper[2], wd = hyper[4];
-  const double tt = (double)step[0];
-  const float step_size = (float)(lr / (1.0 - pow(b1d, tt)));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow(b2d, tt));
-  const float decay = (float)(1.0 - lr * wd);
-  const float b1c = (float)(1.0 - b1d), b2 = (float)b2d, b2c = (float)(1.0 - b2d);
-  const float eps = (float)hyper[3];
-  auto upd = [&](float& P, float G, float& Mv, float& Vv) {
-    P *= decay;
-    Mv += b1c * (G - Mv);                         // exp_avg.lerp_(grad, 1-beta1)
-    Vv = Vv * b2 + b2c * (G * G);                 // exp_avg_sq.mul_(b2).addcmul_(g,g,1-b2)
-    const float denom = sqrtf(Vv) / bc2_sqrt + eps;
-    P -= step_size * (Mv / denom);
-  };
+  const AdamScalars as = adam_scalars(hyper, step);
+  auto upd = [&](float& P, float G, float& Mv, float& Vv) { adam_upd(as, P, G, Mv, Vv); };
 #pragma unroll
   for (int u = 0; u < ADAM_U; ++u) {
     const int64_t q = t0 + u * T;

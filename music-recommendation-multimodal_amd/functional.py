@@ -12,6 +12,8 @@ mirror, or ``P`` itself in fp32 mode).
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -163,6 +165,12 @@ def _ln_fusable(W: Dict[str, Tensor], pre: str, D: int) -> bool:
             and _ln_k_ok(D, wti.shape[1]))
 
 
+# The item head's stages A and C both inside the fused user head launch (C polling A's
+# BatchNorm statistics in-launch, ttmi_user_item_head_fwd_ac) measured 104 us against 18 + 17 us
+# for A beside the one-query attention and C beside the user head: off until that wait is fixed
+_HEAD_AC = os.environ.get("TTMI_HEAD_AC", "0") == "1"
+
+
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
@@ -233,8 +241,8 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             # in-launch for stage A's BatchNorm statistics, ABI 18; without the fused head, stage
             # A rides on this grid instead)
             head_fused = ops.user_head_fusable(W, P, pre, D, dt)
-            co_ac = co_item is not None and co_item.bn_fused and head_fused
-            co_a = co_item is not None and co_item.bn_fused and L <= 64 and not head_fused
+            co_ac = co_item is not None and co_item.bn_fused and head_fused and _HEAD_AC
+            co_a = co_item is not None and co_item.bn_fused and L <= 64 and not co_ac
             ops.mha_q1_gather_fwd(qkv, key_valid, x, rows, res_in, B, L, H, ctx, lse,
                                   _drop(cfg, seeds, site_attn(i)),
                                   co_item=co_item.desc if co_a else None)
@@ -254,10 +262,11 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                                   (_drop(cfg, seeds, site_drop1(i)), _drop(cfg, seeds, site_ffn(i)),
                                    _drop(cfg, seeds, site_drop2(i))), o,
                                   co_item=co_item.desc if co_item is not None else None,
-                                  normed=normed, co_stage="AC" if co_ac else "A")
+                                  normed=normed,
+                                  co_stage="AC" if co_ac else ("C" if co_a else "A"))
                 if co_item is not None:
+                    co_item.c_done = co_ac or co_a
                     co_item.a_done = True
-                    co_item.c_done = co_ac
                 st.normed = normed is not None
                 st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, o["x1"], o["a2"], o["m2"],
                                             o["r2"], o["h"], rows))

@@ -171,6 +171,11 @@ class FoldDesc(ctypes.Structure):
                 ("C", c_p), ("ldc", c_i64), ("accumulate", c_i), ("fx_shift", c_i)]
 
 
+class FoldPlan(ctypes.Structure):
+    """ttmi_fold_plan (include/ttmi.h, ABI 19): opaque fold segments for ttmi_adamw_folded."""
+    _fields_ = [("n", ctypes.c_int32), ("reserved", ctypes.c_int32), ("seg", c_u64 * (32 * 16))]
+
+
 class ResLnDesc(ctypes.Structure):
     """ttmi_linear_res_ln_desc (include/ttmi.h)."""
     _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
@@ -199,6 +204,10 @@ SIGNATURES = {
     "ttmi_linear_ln_bwd_sum_blocks_n": (c_i64, [c_i64, c_i64]),
     "ttmi_wgrad_batch": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
                                ctypes.POINTER(FoldDesc), c_p]),
+    "ttmi_wgrad_batch_plan": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
+                                    ctypes.POINTER(FoldDesc), ctypes.POINTER(FoldPlan), c_p]),
+    "ttmi_adamw_folded": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
+                                ctypes.POINTER(FoldPlan), c_p]),
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
                                  c_i64, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),

@@ -113,10 +113,16 @@ class WgradPending:
     runs every recorded GEMM as one grouped launch and folds all partials in a fixed order
     (ttmi_wgrad_batch: two launches per flush)."""
 
-    def __init__(self):
+    def __init__(self, defer_fold: bool = False):
         self.items = []
         self.folds = []
         self.slots: Dict[str, int] = {}
+        # defer_fold (ABI 19, one process): the flush runs the grouped GEMMs only and leaves
+        # the partials to the optimizer (``plan`` for adamw(fold_plan=...); ``keep`` holds the
+        # partials' workspaces and operands until that update has been issued)
+        self.defer_fold = defer_fold
+        self.plan = None
+        self.keep: list = []
 
     def slot(self, key: str) -> int:
         """Index of the next persistent zero workspace for ``key`` within this block: calls
@@ -132,7 +138,13 @@ class WgradPending:
         arr = (ctypes.POINTER(WgradDesc) * max(len(self.items), 1))(
             *[ctypes.pointer(d) for d, *_ in self.items])
         farr = (FoldDesc * max(len(self.folds), 1))(*[f for f, *_ in self.folds])
-        call("ttmi_wgrad_batch", len(self.items), arr, len(self.folds), farr, _s())
+        if self.defer_fold and self.plan is None:
+            self.plan = _L.FoldPlan()
+            call("ttmi_wgrad_batch_plan", len(self.items), arr, len(self.folds), farr,
+                 ctypes.byref(self.plan), _s())
+            self.keep = self.items + self.folds
+        else:
+            call("ttmi_wgrad_batch", len(self.items), arr, len(self.folds), farr, _s())
         self.items = []
         self.folds = []
         self.slots = {}
@@ -142,11 +154,12 @@ _PENDING: List[WgradPending] = []
 
 
 @contextlib.contextmanager
-def deferred_wgrad():
+def deferred_wgrad(defer_fold: bool = False):
     """Inside the block, bf16 ``linear_dw`` calls (and the fused LN-backward's weight sums)
     are deferred to the yielded WgradPending (flushed, at the latest, on exit): a backward's
-    weight gradients become one grouped GEMM launch plus one fold launch."""
-    pend = WgradPending()
+    weight gradients become one grouped GEMM launch plus one fold launch.  ``defer_fold``:
+    the last flush leaves the fold to ``adamw(fold_plan=pend.plan)`` (one process only)."""
+    pend = WgradPending(defer_fold)
     _PENDING.append(pend)
     try:
         yield pend
@@ -880,11 +893,21 @@ def bump_param_epoch() -> None:
 
 def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
           step: Tensor, zero_grad: bool = False,
-          fx: Optional[Tuple[Tensor, Tensor]] = None):
+          fx: Optional[Tuple[Tensor, Tensor]] = None, fold_plan=None):
     """Fused AdamW over flat buffers.  ``fx`` = (acc, grad_view): the gradient of the slot
     ``grad_view`` (a view into ``g``) is still in the int64 fixed-point accumulator ``acc``
-    (fx_grad_sink): read from there and ``acc`` cleared (ttmi_adamw_fx)."""
+    (fx_grad_sink): read from there and ``acc`` cleared (ttmi_adamw_fx).  ``fold_plan``
+    (WgradPending(defer_fold=True).plan): the step's weight-gradient partials are folded and
+    applied in the same launch (ttmi_adamw_folded)."""
     bump_param_epoch()
+    if fold_plan is not None:
+        acc, off, cnt = None, 0, 0
+        if fx is not None:
+            acc, view = fx
+            off, cnt = (view.data_ptr() - g.data_ptr()) // g.element_size(), view.numel()
+        call("ttmi_adamw_folded", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper),
+             _p(step), int(zero_grad), _p(acc), off, cnt, FX_GRAD_SHIFT, ctypes.byref(fold_plan), _s())
+        return
     if fx is None:
         call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
              int(zero_grad), _s())

@@ -293,6 +293,10 @@ class TrainStep:
         # its slot of flat.grad reads ZERO between backward and update.  Anything that must see
         # complete gradients there (clipping, norms, hooks) needs grad_sink=False.
         self.grad_sink = grad_sink
+        # one process: the weight-gradient fold runs inside the AdamW launch (ABI 19), so the
+        # folded slots of flat.grad are never written either (same caveat as grad_sink)
+        self.fold_in_update = grad_sink and os.environ.get("TTMI_FOLD_IN_UPDATE", "1") != "0"
+        self._fold = None
         model.train()
         dev = next(model.parameters()).device
         self.device = dev
@@ -305,6 +309,7 @@ class TrainStep:
         self.world = self.sync.world
         self.global_negatives = bool(getattr(model, "global_negatives", False))
         self.overlap = overlap_grad_sync and self.world > 1 and self.ucfg.n_layers >= 2
+        self.fold_in_update = self.fold_in_update and self.world == 1
         self.fbufs = FlatBuffers(model)
         self.broadcast_buffers = broadcast_buffers and self.world > 1 and \
             self.fbufs.data is not None
@@ -428,10 +433,12 @@ class TrainStep:
             it, ist = F.item_fusion_fwd(self.Pi, self.Wi, modal, self.icfg, seeds,
                                         self.bufs, self.p_item)
         self._fx = None
-        with ops.deferred_wgrad() as pend, \
+        # one process: the step's weight-gradient partials are folded inside the AdamW launch
+        with ops.deferred_wgrad(defer_fold=self.fold_in_update) as pend, \
                 (ops.fx_grad_sink() if fx_sink else contextlib.nullcontext([])) as sink:
             # one fold launch for the step's weight grads
             self._bwd(b, u, it, modal, ust, ist, rst if self.raw_items else None, cut, pend)
+        self._fold = (pend.plan, pend.keep) if pend.plan is not None else None
         if sink:
             acc, view = sink[0]
             if view.data_ptr() >= self.flat.grad.data_ptr() and \
@@ -545,8 +552,9 @@ class TrainStep:
     def _update(self) -> None:
         f = self.flat
         ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
-                  zero_grad=True, fx=self._fx)
+                  zero_grad=True, fx=self._fx, fold_plan=self._fold[0] if self._fold else None)
         self._fx = None
+        self._fold = None
 
     def _body(self, b: Dict[str, Tensor], cut: Callable = _no_cut) -> None:
         # one process: the item-embedding gradient goes from its fixed-point accumulator

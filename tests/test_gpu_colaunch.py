@@ -256,3 +256,35 @@ def test_trainstep_grad_sink_off_is_bit_identical(gpu_pkg):
         outs.append({k: v.detach().clone() for k, v in m.named_parameters()})
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("D", [128, 256])
+def test_trainstep_fold_in_update_is_bit_identical(gpu_pkg, D, monkeypatch):
+    """One process folds the step's weight-gradient partials inside the AdamW launch
+    (ttmi_wgrad_batch_plan + ttmi_adamw_folded, ABI 19): the same sums in the same order, the
+    same AdamW arithmetic, so the parameters and both moments are bit-identical to the fold
+    launch + AdamW launch path (TTMI_FOLD_IN_UPDATE=0), in graph replays and eagerly."""
+    from oracle import two_tower_ref as ref
+    B, L, V = 64, 20, 301
+    outs = []
+    for fold, graph in ((True, True), (False, True), (True, False)):
+        monkeypatch.setenv("TTMI_FOLD_IN_UPDATE", "1" if fold else "0")
+        torch.manual_seed(3)
+        m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128,
+                                  num_genders=3, num_countries=16, max_seq_len=L, user_embedding_dim=D,
+                                  item_embedding_dim=D, user_dropout=0.1,
+                                  compute_dtype=torch.bfloat16).to(DEV)
+        step = gpu_pkg.TrainStep(m, lr=1e-3, seed=5, use_graph=graph)
+        assert step.fold_in_update == fold
+        for s in range(3):
+            b = ref.synthetic_batch(B, L, V, 3, 16, generator=torch.Generator().manual_seed(70 + s))
+            step.step({k: v.to(DEV) for k, v in b.items()})
+        torch.cuda.synchronize()
+        st = {k: v.detach().clone() for k, v in m.named_parameters()}
+        st.update({"m/" + k: v.clone() for k, v in step.flat.views(step.flat.exp_avg).items()})
+        st.update({"v/" + k: v.clone() for k, v in step.flat.views(step.flat.exp_avg_sq).items()})
+        assert step.flat.grad.abs().max().item() == 0.0          # zero_grad covered every slot
+        outs.append(st)
+    for o in outs[1:]:
+        bad = [k for k in outs[0] if not torch.equal(outs[0][k], o[k])]
+        assert not bad, bad[:8]

@@ -10,7 +10,7 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_c
 rc=$?
 tail -5 gpurun_out/${tag}_tests.log
 [ $rc -eq 0 ] || exit $rc
-bash tools/ab.sh 1 TTMI_PANEL_WROT=0 TTMI_PANEL_WROT=1 || exit 1
+bash tools/ab.sh 1 TTMI_PANEL_WROT=0 TTMI_FOLD_IN_UPDATE=0 TTMI_SEQ_VEC=0 - || exit 1
 bash tools/ab.sh 1 - -- --dim 256 || exit 1
 bash tools/prof_step.sh ${tag} && cat gpurun_out/prof_${tag}_step.txt | head -30 || exit 1
 bash tools/prof_step.sh ${tag}_d256 --dim 256 && cat gpurun_out/prof_${tag}_d256_step.txt | head -40 || exit 1

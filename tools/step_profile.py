@@ -7,7 +7,7 @@ import csv
 import sys
 
 path = sys.argv[1]
-marker = sys.argv[2] if len(sys.argv) > 2 else "adamw_kernel"
+marker = sys.argv[2] if len(sys.argv) > 2 else "adamw"
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
