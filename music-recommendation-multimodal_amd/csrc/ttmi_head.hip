@@ -252,12 +252,20 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   WFrags<1, IK> wf;
   wf.load(a.w0, IK, n0, lane, IK);
   const float4 bias = *reinterpret_cast<const float4*>(a.b0 + n0 + 4 * g);
+  // 16 rows x 128 float4 of modal -> bf16: every load issued before the first store (the m16
+  // copy's global store may alias modal for all hipcc knows, so a load after it waited for the
+  // loads before it: eight serial round trips)
+  float4 mv[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {                      // 16 rows x 128 float4 of modal -> bf16
+  for (int k = 0; k < 8; ++k) {
     const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
     const int rr = min(r0 + r, a.B - 1);
-    const float4 v = *reinterpret_cast<const float4*>(a.modal + (int64_t)rr * IK + 4 * c4);
-    const float x[4] = {v.x, v.y, v.z, v.w};
+    mv[k] = *reinterpret_cast<const float4*>(a.modal + (int64_t)rr * IK + 4 * c4);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+    const float x[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
     st4_bf(L.sA + r * PI + c4 * 8, x);
     if (q == 0 && r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.m16 + (int64_t)(r0 + r) * IK + 4 * c4), x);
   }
@@ -350,12 +358,13 @@ struct ItemLdsC {
 
 // Item head stage C on row block bx (item_head_c_kernel, or the workgroups of
 // ttmi_user_item_head_fwd_c past the user head's).
+template <bool FIN>
 TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = bx * HR;
   const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
   TTMI_TSTAMP(0);
-  if (a.fin) {
+  if constexpr (FIN) {
     // stage A runs in this launch: wait until the IN1/64 column-quarter mergers have published
     // the batch statistics (one lane polls the count, sc1 loads with s_sleep; bounded: on a
     // timeout the error word bncnt[BN_CDONE + 1] is set instead of hanging the GPU)
@@ -378,22 +387,31 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
     __syncthreads();
   }
   TTMI_TSTAMP(3);
+  // the weight fragments first: their loads then overlap the staging below, instead of
+  // waiting behind its y1 stores
+  WFrags<2, IN1> wf;
+  wf.load(a.w4, IN1, n0, lane, IN1);
   if (a.bncnt != nullptr) {      // fused BatchNorm: y1 = drop(relu(BN(z))) staged from z rows
     float4 zv[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
       const int64_t zo = (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4;
-      zv[k] = a.fin ? ld16_wt(a.z, (uint32_t)(zo * 4)) : *reinterpret_cast<const float4*>(a.z + zo);
+      if constexpr (FIN) zv[k] = ld16_wt(a.z, (uint32_t)(zo * 4));
+      else zv[k] = *reinterpret_cast<const float4*>(a.z + zo);
     }
     const DropKeys dk = resolve_drop(a.bd);
+    // a thread's column quad is the same for all 8 rows it stages (idx & 127 = tid & 127): its
+    // BatchNorm parameters are loaded once, with the z rows, before any store (a load after
+    // the y1 store would wait for it: hipcc cannot tell the buffers apart)
+    const int c4 = tid & 127;
+    const float4 mu = FIN ? ld16_wt(a.bmean, 16u * c4) : *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
+    const float4 rs = FIN ? ld16_wt(a.brstd, 16u * c4) : *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
+    const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
+    const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
-      const float4 mu = a.fin ? ld16_wt(a.bmean, 16u * c4) : *reinterpret_cast<const float4*>(a.bmean + 4 * c4);
-      const float4 rs = a.fin ? ld16_wt(a.brstd, 16u * c4) : *reinterpret_cast<const float4*>(a.brstd + 4 * c4);
-      const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
-      const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
+      const int idx = tid + 256 * k, r = idx >> 7;
       float x[4] = {fmaxf((zv[k].x - mu.x) * rs.x * ww.x + bb.x, 0.f), fmaxf((zv[k].y - mu.y) * rs.y * ww.y + bb.y, 0.f),
                     fmaxf((zv[k].z - mu.z) * rs.z * ww.z + bb.z, 0.f), fmaxf((zv[k].w - mu.w) * rs.w * ww.w + bb.w, 0.f)};
       drop_apply_vec<4>(dk, (uint32_t)((int64_t)(r0 + r) * IN1 + 4 * c4), x);
@@ -408,8 +426,6 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
           *reinterpret_cast<const uint4*>(a.y1 + (int64_t)min(r0 + r, a.B - 1) * IN1 + ch * 8);
     }
   }
-  WFrags<2, IN1> wf;
-  wf.load(a.w4, IN1, n0, lane, IN1);
   float b4[2][4], lw[2][4], lb[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -465,7 +481,7 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
 
 __global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
   __shared__ __attribute__((aligned(16))) ItemLdsC L;
-  item_c_body(a, blockIdx.x, L);
+  item_c_body<false>(a, blockIdx.x, L);
 }
 
 // phase stamps of the diagnostic build (ttmi_common.h TTMI_TSTAMP; tools/stamp_build.sh)
@@ -482,18 +498,29 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
   __shared__ __attribute__((aligned(16))) HeadParams Q;
   static_assert(sizeof(HeadLds) >= sizeof(ItemLdsA), "item stage A reuses the head's LDS");
   static_assert(sizeof(HeadLds) >= sizeof(ItemLdsC), "item stage C reuses the head's LDS");
-  if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head stage A or C
-    const int l = (int)blockIdx.x - a.nbu;
-    const int na = a.it_stage == 3 ? a.it_nblk * (IN1 / 64) : 0;     // stage 3: A then C blocks
-    if (a.it_stage == 0 || l < na) {
-      item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
-    } else {
-      item_c_body(a.it, l - na, *reinterpret_cast<ItemLdsC*>(&L));
+  // block order: stages 0 / 2, the user head's row blocks first, then the item blocks; stage 3,
+  // the item stage-A blocks first (one per CU as the grid is dispatched: the slowest of them
+  // sets when stage C can start), then the user head's, then stage C's
+  int ub = (int)blockIdx.x;
+  if (a.it_stage == 3) {
+    const int na = a.it_nblk * (IN1 / 64);
+    if (ub < na) {
+      item_a_body(a.it, ub % a.it_nblk, ub / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+      return;
     }
+    ub -= na;
+    if (ub >= a.nbu) {
+      item_c_body<true>(a.it, ub - a.nbu, *reinterpret_cast<ItemLdsC*>(&L));
+      return;
+    }
+  } else if (ub >= a.nbu) {                          // co-launched item head stage A or C
+    const int l = ub - a.nbu;
+    if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+    else item_c_body<false>(a.it, l, *reinterpret_cast<ItemLdsC*>(&L));
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
-  const int r0 = blockIdx.x * HR, m = r0 + li;
+  const int r0 = ub * HR, m = r0 + li;
   const bool mrow = m < a.B;
   const int W = HD + a.dg + a.dc;
   const int n0 = w * 32;                             // this wave's 32 of the 128 columns

@@ -103,6 +103,6 @@ if os.environ.get("TTMI_LIB", "").endswith("libttmi_stamp.so"):     # phase stam
             v = rel[rows, k][a[rows, k] > 0]
             if v.size:
                 print(f"{name:6s} p{k}: min {v.min():7.2f} med {np.median(v):7.2f} max {v.max():7.2f} (n={v.size})")
-    show("user", slice(0, nu), range(7))
-    show("A", slice(nu, nu + na), range(3))
+    show("A", slice(0, na), range(3))
+    show("user", slice(na, na + nu), range(7))
     show("C", slice(nu + na, nu + na + 32), (0, 3, 4))
