@@ -315,7 +315,12 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   __syncthreads();
   if (!L.s_last || tid >= 64) return;
   const int c = 64 * q + tid;
-  float pm[BN_MAXBLK], p2[BN_MAXBLK];                // every load in flight first
+  // every load in flight first, the running statistics' read-modify-writes included (three
+  // dependent round trips at the end of the merge otherwise)
+  const float rm0 = a.rmean ? a.rmean[c] : 0.f, rv0 = a.rvar ? a.rvar[c] : 0.f;
+  const bool nbt_lane = q == 0 && tid == 0 && a.nbt;
+  const int64_t nbt0 = nbt_lane ? a.nbt[0] : 0;
+  float pm[BN_MAXBLK], p2[BN_MAXBLK];
 #pragma unroll
   for (int b = 0; b < BN_MAXBLK; ++b) {
     const int bb = min(b, nblk - 1);
@@ -340,9 +345,9 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
     a.bmean[c] = mean;
     a.brstd[c] = 1.f / sqrtf(var + a.bn_eps);
   }
-  if (a.rmean) a.rmean[c] = (1.f - a.bn_mom) * a.rmean[c] + a.bn_mom * mean;
-  if (a.rvar) a.rvar[c] = (1.f - a.bn_mom) * a.rvar[c] + a.bn_mom * var * ((float)a.B / (float)(a.B - 1));
-  if (q == 0 && tid == 0 && a.nbt) a.nbt[0] += 1;
+  if (a.rmean) a.rmean[c] = (1.f - a.bn_mom) * rm0 + a.bn_mom * mean;
+  if (a.rvar) a.rvar[c] = (1.f - a.bn_mom) * rv0 + a.bn_mom * var * ((float)a.B / (float)(a.B - 1));
+  if (nbt_lane) a.nbt[0] = nbt0 + 1;
   if (tid == 0) __hip_atomic_store(a.bncnt + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.fin) {      // this (single) storing wave drained, then one lane signals the quarter done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -326,17 +326,31 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
   float m = -INFINITY, sum = 0.f, tgt = 0.f;
   const int nkt = (B + 15) / 16;
   const int kt0 = (int)((int64_t)nkt * split / NSPLIT), kt1 = (int)((int64_t)nkt * (split + 1) / NSPLIT);
-  for (int t = kt0 + wave; t < kt1; t += 4) {
-    f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int jrow = 16 * t + li;
-    const float* kp = Kp + (int64_t)min(jrow, B - 1) * D + 4 * lg;   // clamped; masked below
-    uint4 a[DC];
+  // the key tile's fragments and user ids are loaded one tile ahead (each tile was a K load
+  // round trip, then a dependent uid round trip: 4 serial round trips per wave at B = 512)
+  uint4 a[DC];
+  int64_t uk[4];
+  auto load_tile = [&](int t) {
+    const float* kp = Kp + (int64_t)min(16 * t + li, B - 1) * D + 4 * lg;   // clamped; masked below
 #pragma unroll
     for (int c = 0; c < DC; ++c) a[c] = *reinterpret_cast<const uint4*>(kp + 16 * c);
 #pragma unroll
+    for (int r = 0; r < 4; ++r) uk[r] = uid ? uid[min(16 * t + 4 * lg + r, B - 1)] : 0;
+  };
+  if (kt0 + wave < kt1) load_tile(kt0 + wave);
+  for (int t = kt0 + wave; t < kt1; t += 4) {
+    f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    uint4 ac[DC];
+    int64_t ukc[4];
+#pragma unroll
+    for (int c = 0; c < DC; ++c) ac[c] = a[c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ukc[r] = uk[r];
+    if (t + 4 < kt1) load_tile(t + 4);
+#pragma unroll
     for (int c = 0; c < DC; ++c) {
       const uint4 b = lds16(sq + li * QP + (16 * c + 4 * lg) * 4);
-      Mma<float>::run(acc, a[c], b);
+      Mma<float>::run(acc, ac[c], b);
     }
     // this lane: query row li, keys 16t + 4lg + r
     float o[4];
@@ -345,7 +359,7 @@ __global__ __launch_bounds__(256) void nce_fwd_kernel(int B, const float* __rest
       const int j = 16 * t + 4 * lg + r;
       float v = acc[r] * inv_tau;
       if (j >= B) v = -INFINITY;
-      else if (uid && j != i && uid[j] == ui) v = MASK_FILL;
+      else if (uid && j != i && ukc[r] == ui) v = MASK_FILL;
       if (j == i) tgt = v;
       o[r] = v;
       online_add(m, sum, v);
@@ -535,44 +549,62 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
   for (int q = 0; q < TPW; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int kbeg = (int)((int64_t)B * split / NSPLIT) / 4 * 4;
   const int kend = split == NSPLIT - 1 ? B : (int)((int64_t)B * (split + 1) / NSPLIT) / 4 * 4;
-  for (int k0 = kbeg; k0 < kend; k0 += NKB) {
-    // ---- stage V[k0 .. k0+64) (rows past kend zero) and G[16][64]
-    constexpr int VQ = NKB * D / 4 / 256;          // float4 per thread
-    float4 v[VQ];
+  // the next key block's V rows, S values and lse terms are loaded while this block's G and
+  // MFMAs run (each block was a load round trip before its LDS staging: 2 per workgroup at
+  // B = 512, serial)
+  constexpr int VQ = NKB * D / 4 / 256;            // float4 per thread
+  float4 v[VQ];
+  float sv[4], l4[4], l1;
+  auto load_blk = [&](int k0) {
 #pragma unroll
     for (int j = 0; j < VQ; ++j) {
       const int idx = tid + 256 * j, kr = idx / (D / 4), c4 = idx % (D / 4);
       v[j] = *reinterpret_cast<const float4*>(V + (int64_t)min(k0 + kr, B - 1) * D + 4 * c4);
     }
+    if (dir == 0) {      // thread -> row tid/16, keys 4·(tid%16) .. +3 (one float4 of S's row)
+      const int row = r0 + (tid >> 4), k = k0 + (tid & 15) * 4;
+      load4<VEC>(S + (int64_t)min(row, B - 1) * B, k, B, sv);
+      load4<VEC>(lse_k, k, B, l4);
+      l1 = lse_q[min(row, B - 1)];
+    } else {             // thread -> key tid/4, rows 4·(tid%4) .. +3 (one float4 of S's row k)
+      const int k = k0 + (tid >> 2), row = r0 + (tid & 3) * 4;
+      load4<VEC>(S + (int64_t)min(k, B - 1) * B, row, B, sv);
+      load4<VEC>(lse_q, row, B, l4);
+      l1 = lse_k[min(k, B - 1)];
+    }
+  };
+  if (kbeg < kend) load_blk(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += NKB) {
+    // ---- stage V[k0 .. k0+64) (rows past kend zero) and G[16][64]
+    float4 vc[VQ];
+    float svv[4], lv[4];
+#pragma unroll
+    for (int j = 0; j < VQ; ++j) vc[j] = v[j];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { svv[e] = sv[e]; lv[e] = l4[e]; }
+    const float lc = l1;
+    if (k0 + NKB < kend) load_blk(k0 + NKB);
     float g[4];
     int gr[4], gk[4];
-    if (dir == 0) {      // thread -> row tid/16, keys 4·(tid%16) .. +3 (one float4 of S's row)
+    if (dir == 0) {
       const int r = tid >> 4, kq = (tid & 15) * 4;
       const int row = r0 + r, k = k0 + kq;
-      float svv[4], lkv[4];
-      load4<VEC>(S + (int64_t)min(row, B - 1) * B, k, B, svv);
-      load4<VEC>(lse_k, k, B, lkv);
-      const float lq = lse_q[min(row, B - 1)];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         gr[e] = r;
         gk[e] = kq + e;
         const bool ok = row < B && k + e < kend;
-        g[e] = ok ? coef * (__expf(svv[e] - lq) + __expf(svv[e] - lkv[e]) - (k + e == row ? 2.f : 0.f)) : 0.f;
+        g[e] = ok ? coef * (__expf(svv[e] - lc) + __expf(svv[e] - lv[e]) - (k + e == row ? 2.f : 0.f)) : 0.f;
       }
-    } else {             // thread -> key tid/4, rows 4·(tid%4) .. +3 (one float4 of S's row k)
+    } else {
       const int kk = tid >> 2, rq = (tid & 3) * 4;
       const int k = k0 + kk, row = r0 + rq;
-      float svv[4], lqv[4];
-      load4<VEC>(S + (int64_t)min(k, B - 1) * B, row, B, svv);
-      load4<VEC>(lse_q, row, B, lqv);
-      const float lk = lse_k[min(k, B - 1)];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         gr[e] = rq + e;
         gk[e] = kk;
         const bool ok = row + e < B && k < kend;
-        g[e] = ok ? coef * (__expf(svv[e] - lqv[e]) + __expf(svv[e] - lk) - (k == row + e ? 2.f : 0.f)) : 0.f;
+        g[e] = ok ? coef * (__expf(svv[e] - lv[e]) + __expf(svv[e] - lc) - (k == row + e ? 2.f : 0.f)) : 0.f;
       }
     }
     __syncthreads();                               // previous block's MFMAs done with LDS
@@ -580,7 +612,7 @@ __global__ __launch_bounds__(256) void nce_bwd_kernel(int B, const float* __rest
     for (int j = 0; j < VQ; ++j) {
       const int idx = tid + 256 * j, kr = idx / (D / 4), c4 = idx % (D / 4);
       *reinterpret_cast<float4*>(sV + kr * VP + 4 * c4) =
-          k0 + kr < kend ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+          k0 + kr < kend ? vc[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) sG[gr[e] * GP + gk[e]] = g[e];

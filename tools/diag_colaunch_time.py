@@ -88,21 +88,27 @@ if os.environ.get("TTMI_LIB", "").endswith("libttmi_stamp.so"):     # phase stam
     lib.ttmi_dbg_stamps_head.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     NB, NW, NP = 512, 16, 8
     buf = (ctypes.c_uint64 * (NB * NW * NP))()
-    run("AC")
-    torch.cuda.synchronize()
-    lib.ttmi_dbg_stamps_head(buf, NB * NW * NP)
-    run("AC")
-    assert lib.ttmi_dbg_stamps_head(buf, NB * NW * NP) == 0
-    a = np.array(buf, dtype=np.float64).reshape(NB, NW, NP)[:, 0, :]
-    t0 = a[:320, 0][a[:320, 0] > 0].min()
-    rel = (a - t0) / 100.0
-    nu, na = 32, 256
+    for mode in ("AC", "C"):
+        run(mode)
+        torch.cuda.synchronize()
+        lib.ttmi_dbg_stamps_head(buf, NB * NW * NP)
+        run(mode)
+        assert lib.ttmi_dbg_stamps_head(buf, NB * NW * NP) == 0
+        a = np.array(buf, dtype=np.float64).reshape(NB, NW, NP)[:, 0, :]
+        nu, na = 32, (256 if mode == "AC" else 0)
+        tot = nu + na + 32
+        t0 = a[:tot, 0][a[:tot, 0] > 0].min()
+        rel = (a - t0) / 100.0
 
-    def show(name, rows, phases):
-        for k in phases:
-            v = rel[rows, k][a[rows, k] > 0]
-            if v.size:
-                print(f"{name:6s} p{k}: min {v.min():7.2f} med {np.median(v):7.2f} max {v.max():7.2f} (n={v.size})")
-    show("A", slice(0, na), range(3))
-    show("user", slice(na, na + nu), range(7))
-    show("C", slice(nu + na, nu + na + 32), (0, 3, 4))
+        def show(name, rows, phases):
+            for k in phases:
+                v = rel[rows, k][a[rows, k] > 0]
+                if v.size:
+                    print(f"{mode:3s} {name:6s} p{k}: min {v.min():7.2f} med {np.median(v):7.2f} max {v.max():7.2f} (n={v.size})")
+        if mode == "AC":
+            show("A", slice(0, na), range(3))
+            show("user", slice(na, na + nu), range(7))
+            show("C", slice(na + nu, tot), (0, 3, 4))
+        else:
+            show("user", slice(0, nu), range(7))
+            show("C", slice(nu, tot), (0, 3, 4))
