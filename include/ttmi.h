@@ -288,6 +288,13 @@ int ttmi_infonce_fwd_pre(int B, int D, const int64_t* user_idx, float inv_tau, c
                          const float* i_hat, const float* norms, float* logits, float* lse,
                          float* loss, void* ws, int32_t* counters, float* loss_acc,
                          hipStream_t stream);
+/* ABI 19: ttmi_infonce_fwd with the lse / loss combine inside the logits launch (persistent
+ * zero `counters` of ttmi_infonce_counter_bytes(B)) and loss_acc (may be NULL) += loss: two
+ * launches.  D % 64 == 0, D <= 256. */
+int ttmi_infonce_fwd_acc(int B, int D, const float* u, const float* it, const int64_t* user_idx,
+                         float inv_tau, float* u_hat, float* i_hat, float* norms, float* logits,
+                         float* lse, float* loss, void* ws, int32_t* counters, float* loss_acc,
+                         hipStream_t stream);
 int64_t ttmi_infonce_counter_bytes(int B);
 /* Backward given dloss (device scalar; NULL means 1): writes du, di [B,D]. */
 int ttmi_infonce_bwd(int B, int D, const float* u_hat, const float* i_hat, const float* norms,

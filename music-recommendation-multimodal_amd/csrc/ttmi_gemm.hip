@@ -1523,7 +1523,10 @@ WgradPlan wgrad_group_plan(int64_t R, int64_t M, int64_t N, int64_t ldmax) {
   p.tiles_n = (int)((N + c.tile - 1) / c.tile);
   const int T = p.tiles_m * p.tiles_n;
   const int64_t stages = std::max<int64_t>(1, (R + 63) / 64);
-  int S = c.splits > 0 ? c.splits : std::max(1, 256 / T);
+  // at most ~64 workgroups per GEMM (every split one CU-resident 128 KB ring): the D = 256
+  // encoder's four long weight gradients have 12-16 tiles each, and 12 splits of them made
+  // 576 workgroups = 2.25 rounds on 256 CUs (117 us); the D = 128 shapes (<= 4 tiles) keep 12
+  int S = c.splits > 0 ? std::min(c.splits, std::max(1, 64 / T)) : std::max(1, 256 / T);
   S = (int)std::max<int64_t>(1, std::min<int64_t>(S, stages / 6));
   int64_t sps = (stages + S - 1) / S;
   while (sps > 1 && sps * 64 * ldmax * 2 >= (int64_t)1 << 31) sps = (sps + 1) / 2;
@@ -2363,7 +2366,11 @@ void launch_panel_t(const GemmArgs& a, hipStream_t s, const LnBwdArgs& ln = LnBw
   // workgroups of 7 instead of 200 of 8 on 256 CUs)
   const int64_t tiles = (a.M + 15) / 16;
   const int S = std::max(1, a.nslice);
-  const int64_t tpw = std::max<int64_t>(1, (tiles * S + num_cus() - 1) / num_cus());
+  // column slices: one workgroup per CU (a 135 KB W image each) in ONE round: the row groups,
+  // padded to whole XCD rounds, times the slices must not exceed the CUs (264 workgroups on
+  // 256 CUs ran the D = 256 QKV panel in two rounds: 38 us)
+  const int64_t rg_max = S > 1 ? std::max<int64_t>(8, (int64_t)(num_cus() / S) / 8 * 8) : (int64_t)num_cus();
+  const int64_t tpw = std::max<int64_t>(1, (tiles + rg_max - 1) / rg_max);
   const int64_t rgroups = (tiles + tpw - 1) / tpw;
   // column slices: row groups padded to whole XCD rounds (panel_kernel's block decode)
   const int64_t grid = S > 1 ? (rgroups + 7) / 8 * 8 * S : rgroups;

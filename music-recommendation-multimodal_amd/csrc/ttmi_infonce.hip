@@ -864,6 +864,19 @@ extern "C" int ttmi_infonce_fwd(int B, int D, const float* u, const float* it,
                           ws, true, nullptr, nullptr, s);
 }
 
+// ttmi_infonce_fwd with the combine inside the logits launch and the loss accumulator (ABI 19):
+// the normalise launch + one launch, for callers whose rows are not normalised by their producers
+// (the unfused heads, D = 256).
+extern "C" int ttmi_infonce_fwd_acc(int B, int D, const float* u, const float* it,
+                                    const int64_t* user_idx, float inv_tau, float* u_hat, float* i_hat,
+                                    float* norms, float* logits, float* lse, float* loss, void* ws,
+                                    int32_t* counters, float* loss_acc, hipStream_t s) {
+  TTMI_REQUIRE(counters && ((uintptr_t)counters & 3) == 0 && fused_ok(B, D),
+               "ttmi_infonce_fwd_acc: needs 4-byte aligned counters and D %% 64 == 0, D <= 256");
+  return infonce_fwd_impl(B, D, u, it, user_idx, inv_tau, u_hat, i_hat, norms, logits, lse, loss,
+                          ws, true, counters, loss_acc, s);
+}
+
 extern "C" int64_t ttmi_infonce_counter_bytes(int B) {
   return B > 0 ? (int64_t)(2 * ((B + NQ - 1) / NQ) + 1) * 4 : 0;
 }

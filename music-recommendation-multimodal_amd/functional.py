@@ -784,6 +784,10 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], temperature: 
     if normed is not None:
         ops.infonce_fwd_pre(user_idx, inv_tau, u_hat, i_hat, norms, logits, lse, loss, ws,
                             loss_acc=loss_acc)
+    elif loss_acc is not None and D % 64 == 0 and D <= 256 and loss_acc.dtype == torch.float32:
+        # normalise launch + logits launch with the combine and the accumulator (ABI 19)
+        ops.infonce_fwd_acc(u.contiguous(), it.contiguous(), user_idx, inv_tau, u_hat, i_hat, norms,
+                            logits, lse, loss, ws, loss_acc)
     else:
         ops.infonce_fwd(u.contiguous(), it.contiguous(), user_idx, inv_tau, u_hat, i_hat, norms,
                         logits, lse, loss, ws)

@@ -231,6 +231,8 @@ SIGNATURES = {
                                  c_p, c_p]),
     "ttmi_infonce_workspace": (c_i64, [c_i, c_i]),
     "ttmi_infonce_fwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "ttmi_infonce_fwd_acc": (c_i, [c_i, c_i, c_p, c_p, c_p, ctypes.c_float, c_p, c_p, c_p, c_p, c_p, c_p,
+                                   c_p, c_p, c_p, c_p]),
     "ttmi_infonce_fwd_pre": (c_i, [c_i, c_i, c_p, ctypes.c_float, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                    c_p]),
     "ttmi_infonce_counter_bytes": (ctypes.c_int64, [c_i]),

@@ -849,6 +849,17 @@ def infonce_fwd(u: Tensor, it: Tensor, user_idx: Optional[Tensor], inv_tau: floa
          _p(norms), _p(logits), _p(lse), _p(loss), _p(ws), _s())
 
 
+def infonce_fwd_acc(u: Tensor, it: Tensor, user_idx: Optional[Tensor], inv_tau: float, u_hat: Tensor,
+                    i_hat: Tensor, norms: Tensor, logits: Tensor, lse: Tensor, loss: Tensor, ws: Tensor,
+                    loss_acc: Optional[Tensor]):
+    """infonce_fwd with the combine inside the logits launch and ``loss_acc`` += loss
+    (ttmi_infonce_fwd_acc: two launches; D % 64 == 0, D <= 256)."""
+    B, D = u.shape
+    cnt = _zero_ws("ttmi_infonce_counter_bytes", (B,), u.device)
+    call("ttmi_infonce_fwd_acc", B, D, _p(u), _p(it), _p(user_idx), inv_tau, _p(u_hat), _p(i_hat),
+         _p(norms), _p(logits), _p(lse), _p(loss), _p(ws), _p(cnt), _p(loss_acc), _s())
+
+
 def infonce_fwd_pre(user_idx: Optional[Tensor], inv_tau: float, u_hat: Tensor, i_hat: Tensor,
                     norms: Tensor, logits: Tensor, lse: Tensor, loss: Tensor, ws: Tensor,
                     fused_combine: bool = True, loss_acc: Optional[Tensor] = None):

@@ -288,3 +288,34 @@ def test_trainstep_fold_in_update_is_bit_identical(gpu_pkg, D, monkeypatch):
     for o in outs[1:]:
         bad = [k for k in outs[0] if not torch.equal(outs[0][k], o[k])]
         assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("B,D", [(512, 256), (37, 128), (64, 64)])
+def test_infonce_fwd_acc_equals_unfused(gpu_pkg, B, D):
+    """ttmi_infonce_fwd_acc (normalise launch + logits launch with the in-launch combine and the
+    loss accumulator, ABI 19) == ttmi_infonce_fwd: logits, lse, normalised rows bit for bit; the
+    loss to float reassociation; loss_acc += loss; repeated calls (counters left zero)."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(B + D)
+    u = torch.randn(B, D, generator=g).to(DEV)
+    it = torch.randn(B, D, generator=g).to(DEV)
+    uid = torch.randint(0, max(B // 3, 1), (B,), generator=g).to(DEV)
+    f32 = dict(device=DEV, dtype=torch.float32)
+
+    def outs():
+        return (torch.empty(B, D, **f32), torch.empty(B, D, **f32), torch.empty(2 * B, **f32),
+                torch.empty(B, B, **f32), torch.empty(2 * B, **f32), torch.empty((), **f32),
+                torch.empty(ops.infonce_workspace(B, D), device=DEV, dtype=torch.uint8))
+    ref = outs()
+    ops.infonce_fwd(u, it, uid, 1 / 0.07, *ref)
+    acc = torch.full((1,), 0.25, **f32)
+    for k in range(2):
+        got = outs()
+        ops.infonce_fwd_acc(u, it, uid, 1 / 0.07, *got, acc)
+        torch.cuda.synchronize()
+        for a, b in zip(got[:5], ref[:5]):
+            assert torch.equal(a, b)
+        assert abs(float(got[5]) - float(ref[5])) <= 1e-6 * abs(float(ref[5]))
+    assert abs(float(acc) - (0.25 + 2 * float(ref[5]))) <= 1e-5 * abs(float(acc))
+    cnt = ops._zero_ws("ttmi_infonce_counter_bytes", (B,), u.device)
+    assert int(cnt.view(torch.int32).abs().sum()) == 0
