@@ -640,14 +640,17 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
 
 
 int check_mha(const char* fn, int dtype, int B, int L, int H, int Dh, const void* qkv,
-              const int64_t* kv) {
+              const int64_t* kv, float drop_p) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "%s: bad dtype", fn);
   TTMI_REQUIRE(B >= 0 && L > 0 && L <= TTMI_ATTN_LMAX && H > 0, "%s: need 0 < L <= %d (got L=%d)", fn,
                TTMI_ATTN_LMAX, L);
   TTMI_REQUIRE(Dh > 0 && Dh <= 64 && Dh % 8 == 0, "%s: need Dh %% 8 == 0 and Dh <= 64 (got %d)", fn, Dh);
   TTMI_REQUIRE(qkv && kv, "%s: null argument", fn);
   TTMI_REQUIRE(((uintptr_t)qkv & 15) == 0, "%s: qkv must be 16-byte aligned", fn);
-  TTMI_REQUIRE((int64_t)B * H * L * L < (1LL << 32), "%s: dropout index space exceeds 2^32", fn);
+  // the attention-dropout mask index (b·H + h)·L² + i·L + j is 32-bit: bounded only when
+  // dropout is on (eval and inference encoding of any batch size pass)
+  TTMI_REQUIRE(drop_p == 0.f || (int64_t)B * H * L * L < (1LL << 32),
+               "%s: with dropout on, B*H*L*L must stay below 2^32 (32-bit mask index); split the batch", fn);
   return TTMI_OK;
 }
 
@@ -656,7 +659,7 @@ int check_mha(const char* fn, int dtype, int B, int L, int H, int Dh, const void
 extern "C" int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                             const int64_t* key_valid, float drop_p, const uint64_t* drop_seed, void* ctx,
                             float* lse, hipStream_t s) {
-  int rc = check_mha("ttmi_mha_fwd", dtype, B, L, H, Dh, qkv, key_valid);
+  int rc = check_mha("ttmi_mha_fwd", dtype, B, L, H, Dh, qkv, key_valid, drop_p);
   if (rc) return rc;
   TTMI_REQUIRE(ctx && lse, "ttmi_mha_fwd: null output");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_mha_fwd: drop_p out of [0,1)");
@@ -685,7 +688,7 @@ extern "C" int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* 
 extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                             const int64_t* key_valid, const float* lse, const void* dctx,
                             float drop_p, const uint64_t* drop_seed, void* dqkv, hipStream_t s) {
-  int rc = check_mha("ttmi_mha_bwd", dtype, B, L, H, Dh, qkv, key_valid);
+  int rc = check_mha("ttmi_mha_bwd", dtype, B, L, H, Dh, qkv, key_valid, drop_p);
   if (rc) return rc;
   TTMI_REQUIRE(lse && dctx && dqkv, "ttmi_mha_bwd: null argument");
   TTMI_REQUIRE(((uintptr_t)dctx & 15) == 0, "ttmi_mha_bwd: dctx must be 16-byte aligned");

@@ -678,6 +678,7 @@ def seq_embed_bwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, mean: Tensor, rs
 def mha_fwd(qkv: Tensor, key_valid: Tensor, B: int, L: int, H: int, ctx: Tensor, lse: Tensor,
             drop: Drop = NO_DROP):
     Dh = qkv.shape[1] // (3 * H)
+    _q1_batch_check("mha_fwd", B, L, H, drop)
     call("ttmi_mha_fwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), float(drop[0]),
          _p(drop[1]), _p(ctx), _p(lse), _s())
     return ctx
@@ -686,6 +687,7 @@ def mha_fwd(qkv: Tensor, key_valid: Tensor, B: int, L: int, H: int, ctx: Tensor,
 def mha_bwd(qkv: Tensor, key_valid: Tensor, lse: Tensor, dctx: Tensor, B: int, L: int, H: int,
             dqkv: Tensor, drop: Drop = NO_DROP):
     Dh = qkv.shape[1] // (3 * H)
+    _q1_batch_check("mha_bwd", B, L, H, drop)
     call("ttmi_mha_bwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(lse), _p(dctx),
          float(drop[0]), _p(drop[1]), _p(dqkv), _s())
     return dqkv
@@ -1041,7 +1043,8 @@ def mha_q1_fwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, B: int, L: int, H: 
 
 
 def _q1_batch_check(who: str, B: int, L: int, H: int, drop: Drop) -> None:
-    """The one-query kernels index dropout masks in 32 bits: with dropout on, B·H·L² < 2^32."""
+    """The attention kernels (full and one-query) index dropout masks in 32 bits: with dropout
+    on, B·H·L² < 2^32 (without dropout any batch size runs: eval and inference encoding)."""
     if float(drop[0]) > 0 and B * H * L * L >= 1 << 32:
         raise ValueError(f"{who}: with attention dropout on, batch {B} x {H} heads x L={L} exceeds the "
                          f"32-bit mask index (B*H*L*L < 2^32); split the batch")
