@@ -380,6 +380,33 @@ TTMI_DEV void stage_heads(char* const (&dst)[NOP], const bf16_t* const (&src)[NO
     }
 }
 
+// stage_heads in two halves (per-operand row strides): every operand's loads are issued, the
+// caller issues its other loads, then the LDS images are written — one memory round trip for
+// the whole prologue instead of one per operand group and per dependent small load
+template <int DH, int NOP>
+struct HeadStage {
+  static constexpr int PER = 64 * Img2<DH>::CPR / 256;
+  uint4 v[NOP][PER];
+  TTMI_DEV void load(const bf16_t* const (&src)[NOP], const int64_t (&ld)[NOP], int L, int tid) {
+#pragma unroll
+    for (int o = 0; o < NOP; ++o)
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const int idx = tid + 256 * c, r = idx / Img2<DH>::CPR, ch = idx % Img2<DH>::CPR;
+        v[o][c] = *reinterpret_cast<const uint4*>(src[o] + (int64_t)min(r, L - 1) * ld[o] + ch * 8);
+      }
+  }
+  TTMI_DEV void store(char* const (&dst)[NOP], int L, int tid) const {
+#pragma unroll
+    for (int o = 0; o < NOP; ++o)
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const int idx = tid + 256 * c, r = idx / Img2<DH>::CPR, ch = idx % Img2<DH>::CPR;
+        *reinterpret_cast<uint4*>(dst[o] + r * Img2<DH>::P + ch * 16) = r < L ? v[o][c] : make_uint4(0u, 0u, 0u, 0u);
+      }
+  }
+};
+
 template <int DH>
 __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
                                                       const int64_t* __restrict__ kvalid, DropParams dp,
@@ -396,16 +423,20 @@ __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_
   const int D = H * DH;
   const int64_t ld = 3LL * D;
   const bf16_t* base = qkv + (int64_t)b * L * ld + (int64_t)h * DH;
+  // key validity as one 64-bit ballot of wave 0 (one 8-byte load per lane, not 16); its load
+  // and the head slices' are all in flight before the first LDS write
+  const int64_t kvl = kvalid[(int64_t)b * L + min(lane, L - 1)];
   {
-    char* const dst[3] = {sQ, sK, sV};
+    HeadStage<DH, 3> st;
     const bf16_t* const src[3] = {base, base + D, base + 2 * D};
-    stage_heads<DH, 3>(dst, src, ld, L, threadIdx.x);
+    const int64_t lds3[3] = {ld, ld, ld};
+    st.load(src, lds3, L, threadIdx.x);
+    char* const dst[3] = {sQ, sK, sV};
+    st.store(dst, L, threadIdx.x);
   }
-  // key validity of the 4 keys 16t + 4lg + e this lane holds, per key tile t
-  // key validity as one 64-bit ballot of wave 0 (one 8-byte load per lane, not 16)
   __shared__ uint64_t s_kv;
   if (wave == 0) {
-    const uint64_t bal = __ballot(lane < L && kvalid[(int64_t)b * L + min(lane, L - 1)] != 0);
+    const uint64_t bal = __ballot(lane < L && kvl != 0);
     if (lane == 0) s_kv = bal;
   }
   __syncthreads();
@@ -507,21 +538,22 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
   const int D = H * DH;
   const int64_t ld = 3LL * D;
   const bf16_t* base = qkv + (int64_t)b * L * ld + (int64_t)h * DH;
+  // every global load of the prologue in flight at once (the head slices, the key validity,
+  // this lane's query row's log-sum-exp), then the LDS images: one memory round trip
+  const int64_t kvl = kvalid[(int64_t)b * L + min(lane, L - 1)];
+  const int qrow = 16 * wave + li;
+  const float lr0 = lse[(int64_t)bh * L + min(qrow, L - 1)];
   {
-    char* const dst[4] = {sQ, sK, sV, sdO};
+    HeadStage<DH, 4> st;
     const bf16_t* const src[4] = {base, base + D, base + 2 * D, dctx + (int64_t)b * L * D + (int64_t)h * DH};
-    // dctx rows have stride D, qkv rows 3D: stage in two calls
-    char* const d3[3] = {dst[0], dst[1], dst[2]};
-    const bf16_t* const s3[3] = {src[0], src[1], src[2]};
-    stage_heads<DH, 3>(d3, s3, ld, L, threadIdx.x);
-    char* const d1[1] = {dst[3]};
-    const bf16_t* const s1[1] = {src[3]};
-    stage_heads<DH, 1>(d1, s1, D, L, threadIdx.x);
+    const int64_t lds4[4] = {ld, ld, ld, (int64_t)D};
+    st.load(src, lds4, L, threadIdx.x);
+    char* const dst[4] = {sQ, sK, sV, sdO};
+    st.store(dst, L, threadIdx.x);
   }
-  // key validity as one 64-bit ballot of wave 0 (one 8-byte load per lane, not 16)
   __shared__ uint64_t s_kv;
   if (wave == 0) {
-    const uint64_t bal = __ballot(lane < L && kvalid[(int64_t)b * L + min(lane, L - 1)] != 0);
+    const uint64_t bal = __ballot(lane < L && kvl != 0);
     if (lane == 0) s_kv = bal;
   }
   __syncthreads();
@@ -544,7 +576,7 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
       qf[c] = a_fk<G::P>(sQ, 16 * i, c, lane);
       of[c] = a_fk<G::P>(sdO, 16 * i, c, lane);
     }
-    const float lr = q < L ? lse[(int64_t)bh * L + q] : INFINITY;
+    const float lr = q < L ? lr0 : INFINITY;      // (q = qrow: wave w owns query tile w)
     f32x4_t s[4], dpv[4];
     uint32_t keep[4];                              // dropout keep bits, one hash pass
     float dsum = 0.f;

@@ -638,6 +638,25 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
       const char* wb = smem + (cg * 128 + wrow) * WP + lg * (K / 2);
       LnBwdRow pre;
       if constexpr (LNB) panel_ln_bwd_load(ln, m, g.M, lg, pre);
+      // the epilogue's other row operands (the residual rows, the ReLU / dropout gate) are
+      // loaded before the MFMAs too: read in the epilogue they were one more memory round trip
+      // after the last MFMA of every tile (rows clamped: unconditional loads)
+      constexpr bool RPRE = EPI == PE_RES || LNF, GPRE = EPI == PE_GATE_BF16;
+      float4 rpre[RPRE ? 8 : 1];
+      uint4 gpre[GPRE ? 4 : 1];
+      {
+        const int64_t mcl = std::min<int64_t>(m, g.M - 1);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int n = cg * 128 + 32 * p + 8 * lg;
+          if constexpr (RPRE) {
+            const float* rp = g.residual + mcl * g.ld_res + n;
+            rpre[2 * p] = *reinterpret_cast<const float4*>(rp);
+            rpre[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 4);
+          }
+          if constexpr (GPRE) gpre[p] = *reinterpret_cast<const uint4*>((const bf16_t*)g.gate + mcl * g.ld_gate + n);
+        }
+      }
       if constexpr (AFULL) {
 #pragma unroll
         for (int cq = 0; cq < KC / 4; ++cq) {
@@ -696,7 +715,7 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
         }
         drop_apply_vec<8>(dk, (uint32_t)(m * g.ld_drop + dn0 + n), v);
         if constexpr (EPI == PE_GATE_BF16) {
-          const uint4 q = *reinterpret_cast<const uint4*>((const bf16_t*)g.gate + m * g.ld_gate + n);
+          const uint4 q = gpre[p];
           const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -712,8 +731,7 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
           for (int e = 0; e < 8; ++e) v[e] = gv[e] > 0.f ? v[e] * g.gate_scale : 0.f;
         }
         if constexpr (EPI == PE_RES || LNF) {
-          const float* rp = g.residual + m * g.ld_res + n;
-          const float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
+          const float4 r0 = rpre[2 * p], r1 = rpre[2 * p + 1];
           v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
           v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
         }
