@@ -277,7 +277,9 @@ TTMI_DEV void online_merge(float& m, float& s, float m2, float s2) {
   if (m2 == -INFINITY) return;
   if (m == -INFINITY) { m = m2; s = s2; return; }
   const float M = fmaxf(m, m2);
-  s = s * expf(m - M) + s2 * expf(m2 - M);
+  // explicit fma: the contraction is otherwise the backend's per-context choice, and the
+  // in-launch combine must match nce_combine_kernel bit for bit
+  s = fmaf(s, expf(m - M), s2 * expf(m2 - M));
   m = M;
 }
 
