@@ -575,10 +575,27 @@ class TrainStep:
         return tuple((k, tuple(batch[k].shape), batch[k].dtype)
                      for k in TrainStep.INPUT_KEYS if k in batch)
 
+    def _check_ids(self, batch: Dict[str, Tensor]) -> None:
+        """The embedding lookups index their tables unchecked on the device, so the first batch
+        of every new shape (one host sync per shape, not per step) is range-checked here; an
+        id outside its table raises IndexError as the reference's nn.Embedding does
+        (user_tower.py:153-156)."""
+        ut = self.model.user_tower
+        for key, emb in (("history_ids", ut.item_embedding), ("user_gender", ut.gender_embedding),
+                         ("user_country", ut.country_embedding)):
+            t = batch.get(key)
+            if t is None or t.numel() == 0:
+                continue
+            lo, hi = int(t.min()), int(t.max())
+            if lo < 0 or hi >= emb.num_embeddings:
+                raise IndexError(f"TrainStep: {key} holds ids in [{lo}, {hi}], outside its table "
+                                 f"of {emb.num_embeddings} rows (index out of range in self)")
+
     def _stage(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         sig = self._signature(batch)
         e = self._entries.get(sig)
         if e is None:
+            self._check_ids(batch)
             e = _Entry({k: torch.empty(batch[k].shape, dtype=batch[k].dtype, device=self.device)
                         for k in self.INPUT_KEYS if k in batch})
             self._entries[sig] = e

@@ -273,7 +273,8 @@ def test_catalogue_indexer_follows_rehomed_parameters(gpu_pkg):
     before = ix.index(loader).clone()
     from oracle import two_tower_ref as ref
     step = gpu_pkg.TrainStep(m, lr=1e-2, use_graph=False)
-    b = ref.synthetic_batch(8, 12, V, generator=torch.Generator().manual_seed(9))
+    # the model's demographic tables have the reference's default single row each
+    b = ref.synthetic_batch(8, 12, V, 1, 1, generator=torch.Generator().manual_seed(9))
     for _ in range(3):
         step.step({k: v.to(DEV) for k, v in b.items()})
     torch.cuda.synchronize()
