@@ -295,8 +295,18 @@ static __device__ uint64_t ttmi_stamps[TTMI_STAMP_BLOCKS * TTMI_STAMP_WAVES * TT
       ttmi_stamps[((int)blockIdx.x * TTMI_STAMP_WAVES + (int)(threadIdx.x >> 6)) * TTMI_STAMP_PHASES + (ph)] = \
           __builtin_amdgcn_s_memrealtime();                                                   \
   } while (0)
+// an arbitrary per-wave value in the phase slot (e.g. cycles accumulated inside a loop)
+#define TTMI_TSTAMP_VAL(ph, v)                                                                 \
+  do {                                                                                         \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < TTMI_STAMP_BLOCKS)                             \
+      ttmi_stamps[((int)blockIdx.x * TTMI_STAMP_WAVES + (int)(threadIdx.x >> 6)) * TTMI_STAMP_PHASES + (ph)] = \
+          (uint64_t)(v);                                                                       \
+  } while (0)
+#define TTMI_TNOW() __builtin_amdgcn_s_memrealtime()
 #else
 #define TTMI_TSTAMP(ph) do {} while (0)
+#define TTMI_TSTAMP_VAL(ph, v) do {} while (0)
+#define TTMI_TNOW() 0ull
 #define TTMI_STAMP_DUMP(tu)
 #endif
 

@@ -1181,6 +1181,7 @@ TTMI_DEV void wgrad_body(const WgradArgs& g, const int bid) {
   constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
   __shared__ __attribute__((aligned(1024))) char ring[NS * STAGE];
 
+  TTMI_TSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int T = g.tiles_m * g.tiles_n;
@@ -1232,16 +1233,22 @@ TTMI_DEV void wgrad_body(const WgradArgs& g, const int bid) {
       IB::issue(rb, g.ldb, (int)n0, s * 64, ring_lds + s * STAGE + IA::BYTES, wave, lane);
     }
   }
+  TTMI_TSTAMP(1);
+  uint64_t waited = 0, issued = 0;   // (diagnostic build) realtime ticks in the ring waits / DMA issue
   for (int t = 0; t < nst; ++t) {
     // stage t landed for every wave; every wave is done reading slot (t-1) % NS
+    const uint64_t w0 = TTMI_TNOW();
     if (t + NS - 2 < nst) wait_vm_barrier<(NS - 2) * P>();
     else wait_vm_barrier<0>();
+    waited += TTMI_TNOW() - w0;
     const int tn_ = t + NS - 1;
+    const uint64_t i0 = TTMI_TNOW();
     if (tn_ < nst) {
       const uint32_t dst = ring_lds + (tn_ % NS) * STAGE;
       IA::issue(ra, g.lda, (int)m0, tn_ * 64, dst, wave, lane);
       IB::issue(rb, g.ldb, (int)n0, tn_ * 64, dst + IA::BYTES, wave, lane);
     }
+    issued += TTMI_TNOW() - i0;
     const char* sA = ring + (t % NS) * STAGE;
     const char* sB = sA + IA::BYTES;
 #pragma unroll
@@ -1262,6 +1269,12 @@ TTMI_DEV void wgrad_body(const WgradArgs& g, const int bid) {
     }
   }
 
+  TTMI_TSTAMP(2);
+  TTMI_TSTAMP_VAL(3, waited);
+  TTMI_TSTAMP_VAL(4, nst);
+  TTMI_TSTAMP_VAL(5, issued);
+  (void)waited;
+  (void)issued;
   const int li = lane & 15, lg = lane >> 4;
   if (do_asum) {
 #pragma unroll
