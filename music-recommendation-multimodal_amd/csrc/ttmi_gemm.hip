@@ -1519,14 +1519,16 @@ WgradPlan wgrad_plan64(int64_t R, int64_t M, int64_t N, int64_t ldmax, bool allo
 // operand row slice once for twice the outputs of a 64 x 64 one, halving what the CUs ingest
 // (the family is bound by per-CU ingest from L2 / Infinity Cache), at one workgroup per CU
 // (128 KB ring).  TTMI_WGRAD_GROUP="T:S" (T = 64 or 128, S = splits per long-GEMM tile, 0 =
-// the 64-tile default sizing) selects it.  Default 128:12, the measured best (cfg-2 step on
-// MI355X, tools/wgrad_group_sweep.sh: per GEMM 64:0 4.73 µs, 128:8 5.11, 128:12 4.28,
-// 128:16 5.02, 128:24 4.83, 128:32 5.01).
+// the 64-tile default sizing) selects it.  Default 128:14: the cfg-2 step's group is 14
+// long-GEMM tiles x S splits + ~33 short-GEMM workgroups, and a workgroup holds a CU (128 KB
+// ring), so the launch takes one round only while that sum stays <= 256 CUs: per GEMM
+// 128:12 4.05 us, 128:14 3.80, 128:15 5.04 (a second round), 128:16 4.95 (tools/ab.sh, three
+// pairs each; round 2: 64:0 4.73, 128:8 5.11, 128:24 4.83, 128:32 5.01).
 struct WgradGroupCfg { int tile, splits; };
 
 WgradGroupCfg wgrad_group_cfg() {
   static const WgradGroupCfg cfg = [] {
-    WgradGroupCfg c{128, 12};
+    WgradGroupCfg c{128, 14};
     if (const char* e = getenv("TTMI_WGRAD_GROUP")) {
       int t = 0, sp = 0;
       if (sscanf(e, "%d:%d", &t, &sp) >= 1 && (t == 64 || t == 128)) c = WgradGroupCfg{t, std::max(sp, 0)};
