@@ -2901,10 +2901,23 @@ int wgrad_batch_impl(int n, const ttmi_wgrad_desc* const* descs, int nf, const t
     grp.wg_begin[0] = 0;
     return ttmi_check_launch("ttmi_wgrad_batch");
   };
+  // entries in decreasing rows per split (longest workgroups first): when a group needs more
+  // than one round of workgroups (D = 256), the long ones must not be the ones left for the
+  // second round.  The order changes no result: each GEMM's splits and sums are its own.
+  std::vector<int> order(n);
+  std::vector<int64_t> len(n, 0);
   for (int i = 0; i < n; ++i) {
     const ttmi_wgrad_desc* d = descs[i];
     int rc = wgrad_check(d);
     if (rc) return rc;
+    order[i] = i;
+    if (d->R > 0) len[i] = wgrad_group_plan(d->R, d->M, d->N, std::max(d->ld_dy, d->ld_x)).sps;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return len[x] > len[y]; });
+  for (int oi = 0; oi < n; ++oi) {
+    const int i = order[oi];
+    const ttmi_wgrad_desc* d = descs[i];
+    int rc;
     if (d->R == 0) {                                   // dW (+)= 0: no reduction to group
       ttmi_wgrad_desc z = *d;
       z.defer = 1;
