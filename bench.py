@@ -183,6 +183,86 @@ def probe_dominant(step, batch, device, iters: int = 20):
             "mfma_tflops": round(fl / sec / 1e12, 1)}
 
 
+def probe_panels(step, batch, device, iters: int = 20, min_rows: int = 4096):
+    """Roofline of the second kernel family, the row-panel GEMMs over the encoder's B·L rows
+    (panel_kernel / panel256_kernel: QKV, out-proj + residual + LayerNorm, FFN, and their input
+    gradients with the LayerNorm backward fused).  As probe_dominant: one eager forward +
+    backward records the step's calls of ops.gemm (input-grad / forward GEMMs, weight gradients
+    excluded), ops.linear_res_ln and ops.linear_ln_bwd over >= min_rows rows; the mix is
+    captured into a HIP graph and replayed between HIP events on the launch stream.
+    Algorithmic bytes per launch: every tensor operand once (activations, weights, residual,
+    gate, outputs, LayerNorm statistics), i.e. the bytes the launch cannot avoid moving."""
+    ops = pkg.ops
+    calls = []
+    names = ("gemm", "linear_res_ln", "linear_ln_bwd")
+    orig = {n: getattr(ops, n) for n in names}
+
+    def wrap(n):
+        def rec(*a, **kw):
+            rows = a[3] if n == "gemm" else a[0].shape[0]
+            if rows >= min_rows and not (n == "gemm" and _wgrad_call(kw)):
+                calls.append((n, a, dict(kw)))
+            return orig[n](*a, **kw)
+        return rec
+
+    for n in names:
+        setattr(ops, n, wrap(n))
+    try:
+        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
+    finally:
+        for n in names:
+            setattr(ops, n, orig[n])
+    torch.cuda.synchronize(device)
+    if not calls:
+        return None
+
+    def mix():
+        for n, a, kw in calls:
+            orig[n](*a, **kw)
+
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with ops.deferred_wgrad():                # LayerNorm-backward partials: folded at exit
+        with torch.cuda.stream(side):
+            mix()                                          # warm
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                mix()
+    torch.cuda.current_stream(device).wait_stream(side)
+    torch.cuda.synchronize(device)
+    st = torch.cuda.current_stream(device)
+    g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        g.replay()
+    e1.record(st)
+    torch.cuda.synchronize(device)
+    n = len(calls)
+    sec = e0.elapsed_time(e1) / 1e3 / (iters * n)
+    by = fl = 0.0
+    for name, a, kw in calls:
+        seen = set()
+        for t in list(a) + list(kw.values()):
+            if isinstance(t, torch.Tensor) and (t.data_ptr(), t.numel()) not in seen:
+                seen.add((t.data_ptr(), t.numel()))
+                by += t.numel() * t.element_size()
+        if name == "gemm":
+            fl += 2.0 * a[3] * a[4] * a[5]
+        else:
+            fl += 2.0 * a[0].shape[0] * a[1].numel()
+    by, fl = by / n, fl / n
+    gbs = by / sec / 1e9
+    return {"kernel": "row-panel GEMMs over the encoder rows (forward QKV / out-proj+res+LN / "
+                      "FFN, input grads with the fused LayerNorm backward), graph-replayed; "
+                      "per-launch figures",
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+            "avg_us": round(sec * 1e6, 2), "launches_per_step": n,
+            "bytes_per_launch": round(by), "flops_per_launch": round(fl),
+            "mfma_tflops": round(fl / sec / 1e12, 1)}
+
+
 def probe_conv(step, batch, device, iters: int = 3):
     """cfg 3 roofline of the dominant kernel, the implicit-GEMM conv (conv_tile_kernel: FWD,
     DGRAD and WGRAD launches of both ResNet-18s).  As probe_dominant: one eager forward +
@@ -678,7 +758,7 @@ def main():
         el = float(t)
     mean_loss = float(step.loss_sum) / max(args.steps, 1)
 
-    roof = None
+    roof = roof_panel = None
     if rank == 0:
         if cfg4:
             roof = probe_text_gemm(step, batches[0], device)
@@ -686,6 +766,10 @@ def main():
             roof = probe_conv(step, batches[0], device)
         else:
             roof = probe_dominant(step, batches[0], device)
+            try:
+                roof_panel = probe_panels(step, batches[0], device)
+            except Exception as exc:           # a probe must never sink the bench line
+                print(f"probe_panels: {exc!r}", file=sys.stderr)
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu:
         if cfg4:
@@ -730,6 +814,7 @@ def main():
                        "vocab": V, "d_model": D, "parallelism": f"dp{world}",
                        "graph": not args.no_graph},
             "roofline": roof,
+            "roofline_panel": roof_panel,
             "step_mfma": {"achieved": round(step_tf, 3), "peak": PEAK_BF16_TFLOPS,
                           "unit": "TFLOP/s", "frac": round(step_tf / PEAK_BF16_TFLOPS, 5),
                           "flops_per_step_per_gpu": flops,
