@@ -25,6 +25,8 @@ import glob
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,7 +35,8 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-pkg = importlib.import_module("music-recommendation-multimodal_amd")
+PKG = "music-recommendation-multimodal_amd"
+pkg = None          # imported in main(), after the --gpus N launcher has spawned its ranks
 
 V, L, D, H = 10136, 50, 128, 4
 N_GENDERS, N_COUNTRIES, N_USERS = 3, 64, 840
@@ -111,6 +114,22 @@ def step_flops(B: int, pruned: bool = True) -> float:
     return 3.0 * (full + last + user_head + item_head + loss)
 
 
+def record_step(step, batch) -> None:
+    """One eager forward + backward of ``step`` for a probe to record its launch mix: no
+    collectives, and the fold that TrainStep leaves to AdamW (fold_in_update) switched off, so
+    every deferred partial is folded and its persistent workspace re-zeroed here; the flat
+    gradient is cleared afterwards.  (The step counter and BatchNorm running statistics advance
+    as in a step: the probes run after the timed region.)"""
+    keep = step.fold_in_update
+    step.fold_in_update = False
+    try:
+        step._fwd_bwd(step._stage(batch), lambda fn: None)
+    finally:
+        step.fold_in_update = keep
+    step._fold = step._fx = None
+    step.flat.grad.zero_()
+
+
 def _wgrad_call(kw) -> bool:
     return kw.get("accumulate") and not kw["a_kmajor"] and not kw["b_kmajor"]
 
@@ -136,7 +155,7 @@ def probe_dominant(step, batch, device, iters: int = 20):
 
     ops.linear_dw = rec
     try:
-        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
+        record_step(step, batch)
     finally:
         ops.linear_dw = orig
     torch.cuda.synchronize(device)
@@ -208,7 +227,7 @@ def probe_panels(step, batch, device, iters: int = 20, min_rows: int = 4096):
     for n in names:
         setattr(ops, n, wrap(n))
     try:
-        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
+        record_step(step, batch)
     finally:
         for n in names:
             setattr(ops, n, orig[n])
@@ -279,7 +298,7 @@ def probe_conv(step, batch, device, iters: int = 3):
 
     ops.conv2d = rec
     try:
-        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
+        record_step(step, batch)
     finally:
         ops.conv2d = orig
     torch.cuda.synchronize(device)
@@ -326,7 +345,7 @@ def probe_text_gemm(step, batch, device, iters: int = 3):
 
     ops.gemm = rec
     try:
-        step._fwd_bwd(step._stage(batch), lambda fn: None)   # record only: no collectives
+        record_step(step, batch)
     finally:
         ops.gemm = orig
     torch.cuda.synchronize(device)
@@ -674,6 +693,61 @@ def main_prep(args, world, rank, device):
         dist.destroy_process_group()
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv=None, poll_s: float = 0.2, script=None) -> int:
+    """`bench.py --gpus N` without a launcher: one fresh child process per rank (the reference's
+    `torchrun --nproc_per_node`, src/jobs/train.sh:48), env RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT.  This parent makes no GPU call and imports nothing that
+    does (the package is imported in main() after this returns); it forwards rank 0's stdout
+    (the JSON line) and, if any rank fails, stops the others (their exact PIDs) and returns
+    that rank's exit code."""
+    argv = sys.argv[1:] if argv is None else argv
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
+    rc = 0
+    out = []
+    try:
+        import threading
+        reader = threading.Thread(target=lambda: out.extend(procs[0].stdout), daemon=True)
+        reader.start()
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:
+                        q.terminate()
+            time.sleep(poll_s)
+        reader.join(timeout=10)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for line in out:
+        sys.stdout.write(line)
+    sys.stdout.flush()
+    if rc == 0:
+        rows = [json.loads(l) for l in out if l.startswith("{")]
+        if not rows or rows[-1].get("n_gpus") != n:
+            print(f"bench.py: expected one JSON line with n_gpus={n} from rank 0", file=sys.stderr)
+            return 1
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -695,10 +769,17 @@ def main():
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
-    global D
+    global D, pkg
     D = args.dim
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: n_gpus must equal "
+                         f"the ranks that run (launch with --nproc-per-node {args.gpus}, or drop "
+                         f"WORLD_SIZE and let --gpus spawn the ranks)")
+    pkg = importlib.import_module(PKG)
     rank = int(os.environ.get("RANK", "0"))
     # one rank per GPU; ranks beyond the visible GPU count share them (a multi-rank rehearsal
     # on a 1-GPU box, with TTMI_DIST_BACKEND=gloo since RCCL wants distinct devices)

@@ -40,6 +40,21 @@ const char* ttmi_last_error(void);
 /* ABI version (bumped on any signature change). */
 int ttmi_abi_version(void);
 
+/* Embedding-id range flags (ABI 20).  The reference's nn.Embedding lookups raise IndexError for
+ * an id outside the table (user_tower.py:26,30-31 item / gender / country embeddings,
+ * two_tower.py:82-87 callers; the DeBERTa word embedding behind item_tower.py:47; the catalogue
+ * index assignment evaluate_metrics.py:102, inference.py:204).  The device entry points that
+ * index such a table take `int32_t* id_err` (may be NULL): an id outside [0, rows) never reads
+ * or writes outside the table (it is clamped, or its row reads as zero / is skipped, as each
+ * call states), and id_err[TTMI_IDERR_<key>] is set to 1 by a plain store (racing writers store
+ * the same value).  The flags are never cleared by the library: the host reads them (a
+ * host-mapped buffer needs no device sync) and raises IndexError naming the key. */
+enum { TTMI_IDERR_HISTORY = 0, TTMI_IDERR_GENDER = 1, TTMI_IDERR_COUNTRY = 2,
+       TTMI_IDERR_TEXT = 3, TTMI_IDERR_CATALOGUE = 4,
+       TTMI_IDERR_HEAD_POLL = 7,  /* not an id: ttmi_user_item_head_fwd_ac's stage-C poll timed out
+                                     (its item outputs are invalid); set through the user head's id_err */
+       TTMI_IDERR_WORDS = 8 };
+
 /* ------------------------------------------------------------------------------------
  * GEMM with fused epilogue — every nn.Linear on the path, forward and backward:
  *   user_tower.py:37-45 (MHA in_proj/out_proj, linear1/linear2 of TransformerEncoderLayer),
@@ -184,12 +199,13 @@ int ttmi_layernorm_bwd(int64_t M, int D, const float* dy, int64_t lddy, const fl
  * Optional (y1 != NULL): the first encoder layer's norm1 on the same rows,
  *   y1 = bf16(LN(x) * w1 + b1), mean1 / rstd1 its row statistics (user_tower.py:111-116,
  *   TransformerEncoderLayer(norm_first=True) layer 0), fused while the row is in registers.
+ * An id outside [0, V) reads a zero embedding row and sets id_err[TTMI_IDERR_HISTORY] (ABI 20).
  * ---------------------------------------------------------------------------------- */
 int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const float* E, int64_t V,
                        const float* P, const float* w, const float* b, float eps,
                        float drop_p, const uint64_t* drop_seed, float* x, float* mean, float* rstd,
                        const float* w1, const float* b1, float eps1, void* y1, float* mean1,
-                       float* rstd1, hipStream_t stream);
+                       float* rstd1, int32_t* id_err, hipStream_t stream);
 /* Backward: dE[ids] += g (rows with ids == padding_idx skipped, nn.Embedding(padding_idx=0)
  * user_tower.py:27; ids outside [0, V) contribute nothing), dP[l] += Σ_b g, dw/db += LN affine
  * grads.  All accumulate (fp32).  ABI 16: the cross-row sums go to int64 fixed-point
@@ -231,18 +247,22 @@ int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
  *   len_b = Σ_l (len_src[b,l] != 0) - 1 clamped >= 0; rows[b] = b*L + len_b
  *   (len_src == NULL: x is already gathered, rows[b] = b*L with L == 1);
  *   comb[b] = [x[rows[b]], G[gender[b]], C[country[b]]]   ([B, D+dg+dc], dtype)
+ * G has n_genders rows, C n_countries (ABI 20): an id outside its table reads the clamped row
+ * and sets id_err[TTMI_IDERR_GENDER / _COUNTRY].
  * ---------------------------------------------------------------------------------- */
 int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
                          const int64_t* len_src, const int64_t* gender, const float* G, int dg,
                          const int64_t* country, const float* C, int dc, void* comb,
-                         int32_t* rows, hipStream_t stream);
+                         int32_t* rows, int n_genders, int n_countries, int32_t* id_err,
+                         hipStream_t stream);
 /* Backward: dx[rows[b]] += dcomb[b,:D] (accumulate != 0; = when 0; rows distinct);
  * dG[gender[b]] += ...; dC[country[b]] += ... into int64 fixed-point accumulators (ABI 16,
  * scale 2^36 = TTMI_FX_GRAD_SHIFT, zero on entry; the caller folds them with a
- * ttmi_fold_desc of fx_shift 36; may be NULL). */
+ * ttmi_fold_desc of fx_shift 36; may be NULL).  Ids are clamped as in the forward. */
 int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
                          const int64_t* gender, int dg, const int64_t* country, int dc,
-                         float* dx, int64_t* dG, int64_t* dC, int accumulate, hipStream_t stream);
+                         float* dx, int64_t* dG, int64_t* dC, int accumulate, int n_genders,
+                         int n_countries, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * BatchNorm1d + ReLU + dropout (item_tower.py:122-126 fusion head, item_tower.py:89-93
@@ -658,11 +678,12 @@ int ttmi_mha_q1_bnr_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
  * ---------------------------------------------------------------------------------- */
 /* DebertaV2Embeddings.forward: y = dropout(LN(table[ids]) · mask) per token row (H % 64 == 0);
  * y32 (fp32 [M,H], may be NULL) and y16 (bf16, row stride ld16). table is the bf16 copy of
- * word_embeddings.weight; mask may be NULL. */
+ * word_embeddings.weight ([V, H]); mask may be NULL.  ABI 20: an id outside [0, V) reads the
+ * clamped row and sets id_err[TTMI_IDERR_TEXT]. */
 int ttmi_deb_embed_fwd(int64_t M, int H, const int64_t* ids, const uint16_t* table,
                        const float* ln_w, const float* ln_b, float eps, const int64_t* mask,
                        float drop_p, const uint64_t* drop_seed, float* y32, uint16_t* y16,
-                       int64_t ld16, hipStream_t stream);
+                       int64_t ld16, int64_t V, int32_t* id_err, hipStream_t stream);
 /* Post-LayerNorm (DebertaV2SelfOutput / DebertaV2Output LayerNorm(h + residual)): y = LN(z),
  * z fp32 [M,H]; y32 (fp32, may be NULL) and y16 (bf16, stride ld16, may be NULL); mean/rstd.
  * yq / yv (bf16 [M,H], may be NULL; H % 256 == 0): bf16(dropout(y)) with the next layer's
@@ -769,6 +790,8 @@ typedef struct ttmi_user_head_desc {
   float* x1; void* a2; float* m2; float* r2; void* h; void* comb; int32_t* rows;
   float* z; void* az; float* mz; float* rz; float* u;
   float* u_hat; float* u_norm;       /* ABI 15, optional (NULL): F.normalize(u) and ||u|| */
+  int n_genders, n_countries;        /* ABI 20: rows of G / C; an id outside its table reads the */
+  int32_t* id_err;                   /* clamped row and sets id_err[TTMI_IDERR_GENDER / _COUNTRY] */
 } ttmi_user_head_desc;
 int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t stream);
 /* Its backward, one launch (ABI 12), from du (bf16 [B, D]) and the forward's saved values:
@@ -797,6 +820,7 @@ typedef struct ttmi_user_head_bwd_desc {
   float d2_p; const uint64_t* d2_seed;
   int64_t* dG; int64_t* dC;
   void* dz16; void* dy2; void* dz1; float* dx1; void* dy1; void* dctx; float* ws;
+  int n_genders, n_countries;        /* ABI 20: ids clamped into the tables as in the forward */
 } ttmi_user_head_bwd_desc;
 int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t stream);
 int64_t ttmi_user_head_bwd_ws_floats(int B);
@@ -846,7 +870,8 @@ int ttmi_user_item_head_fwd_c(const ttmi_user_head_desc* d, const ttmi_item_head
  * until A's column-quarter mergers have published the BatchNorm statistics (handed over by
  * write-through stores and loads).  Needs the fused statistics (B <= 512).  bn_cnt must hold
  * ttmi_item_head_bn_counter_bytes(B) zero bytes; every call leaves them zero except the last
- * word, which a C workgroup sets to 1 if its poll timed out (then its outputs are invalid). */
+ * word, which a C workgroup sets to 1 if its poll timed out (then its outputs are invalid; ABI
+ * 20: d->id_err[TTMI_IDERR_HEAD_POLL] is set too, so the host can raise). */
 int ttmi_user_item_head_fwd_ac(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it,
                                hipStream_t stream);
 /* y = GELU(x) (erf form), bf16, n % 8 == 0 (DebertaV2Intermediate). */
@@ -912,9 +937,10 @@ int ttmi_topk_rows(int R, int V, int K, const float* scores, int64_t ld, int ski
 /* Catalogue index rows (evaluate_metrics.py:58-104 compute_all_item_embeddings,
  * inference.py:175-201 index_catalog): for each of n item-tower outputs x [n][ldx] (fp32),
  * e = x / max(|x|, 1e-12) (get_item_embedding), NaN -> 0, e / max(|e|, 1e-8), written to row
- * ids[r] of the dense [V][D] index (ids outside [0, V) skipped; other rows untouched).  ABI 10. */
+ * ids[r] of the dense [V][D] index (ids outside [0, V) skipped and flagged in
+ * id_err[TTMI_IDERR_CATALOGUE], ABI 20; other rows untouched).  ABI 10. */
 int ttmi_catalogue_rows(int n, int D, const float* x, int64_t ldx, const int64_t* ids, int64_t V,
-                        float* dense, hipStream_t stream);
+                        float* dense, int32_t* id_err, hipStream_t stream);
 /* scores[r, ids[r, j]] = -inf for j < Lh and 0 <= id < V (serving: exclude the user's history,
  * reference src/inference.py:294-303). */
 int ttmi_mask_items(int R, int V, float* scores, int64_t ld, const int64_t* ids, int Lh,

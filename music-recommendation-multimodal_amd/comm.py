@@ -22,6 +22,8 @@ backward real under gloo (TrainStep's layer-1 cut, train.py GradSync).
 from __future__ import annotations
 
 import concurrent.futures
+import os
+import queue
 import threading
 
 import torch
@@ -63,8 +65,7 @@ class _Stager:
 
     def _executor(self):
         if self.pool is None:
-            self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=1,
-                                                              thread_name_prefix="ttmi-gloo")
+            self.pool = _FifoWorker()
         return self.pool
 
     def _buffer(self, t: Tensor) -> Tensor:
@@ -108,6 +109,34 @@ class _Stager:
             w.wait()
 
 
+class _FifoWorker:
+    """One daemon thread running submitted reductions in order (a ThreadPoolExecutor's worker is
+    joined at interpreter exit, so a reduction stuck on a dead peer would block the exit)."""
+
+    def __init__(self):
+        self.q = queue.Queue()
+        threading.Thread(target=self._loop, name="ttmi-gloo", daemon=True).start()
+
+    def _loop(self) -> None:
+        while True:
+            fut, fn = self.q.get()
+            if not fut.set_running_or_notify_cancel():
+                continue
+            try:
+                fut.set_result(fn())
+            except BaseException as exc:                     # handed to the waiter
+                fut.set_exception(exc)
+
+    def submit(self, fn) -> concurrent.futures.Future:
+        fut = concurrent.futures.Future()
+        self.q.put((fut, fn))
+        return fut
+
+
+# seconds a staged reduction may take before wait() gives up (a peer that never joins)
+STAGED_TIMEOUT_S = float(os.environ.get("TTMI_GLOO_TIMEOUT", "600"))
+
+
 class _StagedWork:
     def __init__(self, stager: _Stager, t: Tensor, h: Tensor, fut):
         self.stager, self.t, self.h, self.fut = stager, t, h, fut
@@ -119,14 +148,16 @@ class _StagedWork:
     def wait(self) -> bool:
         if self.done:
             return True
-        self.fut.result()                                    # re-raises a failed reduction
+        try:       # re-raises a failed reduction once; it leaves `pending` either way
+            self.fut.result(timeout=STAGED_TIMEOUT_S)
+        finally:
+            with self.stager.lock:
+                if self in self.stager.pending:
+                    self.stager.pending.remove(self)
         # ordered on the caller's stream ahead of every later consumer; the pinned buffer is
         # only rewritten by a later start, whose copy waits for an event recorded after this
         self.t.copy_(self.h, non_blocking=self.t.is_cuda)
         self.done = True
-        with self.stager.lock:
-            if self in self.stager.pending:
-                self.stager.pending.remove(self)
         return True
 
 

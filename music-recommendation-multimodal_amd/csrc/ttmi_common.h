@@ -310,6 +310,16 @@ static __device__ uint64_t ttmi_stamps[TTMI_STAMP_BLOCKS * TTMI_STAMP_WAVES * TT
 #define TTMI_STAMP_DUMP(tu)
 #endif
 
+// ---------------------------------------------------------------- embedding-id range (ABI 20)
+// nn.Embedding raises on an id outside its table; the device lookups clamp it into [0, n)
+// (no out-of-bounds access) and raise flag k of the caller's id_err array (include/ttmi.h
+// TTMI_IDERR_*) with a plain store: every writer stores the same 1, so no atomic is needed.
+TTMI_DEV int64_t clamp_id(int64_t id, int64_t n, int32_t* id_err, int k) {
+  const bool bad = (uint64_t)id >= (uint64_t)n;
+  if (bad && id_err) id_err[k] = 1;
+  return bad ? (id < 0 ? 0 : n - 1) : id;
+}
+
 // ---------------------------------------------------------------- host-side error plumbing
 void ttmi_set_error(const char* fmt, ...);
 #define TTMI_REQUIRE(cond, ...)                      \

@@ -18,14 +18,15 @@ __global__ __launch_bounds__(256) void deb_embed_kernel(int64_t M, int H, const 
                                                         const float* __restrict__ lb, float eps,
                                                         const int64_t* __restrict__ mask,
                                                         DropParams drop, float* __restrict__ y32,
-                                                        bf16_t* __restrict__ y16, int64_t ld16) {
+                                                        bf16_t* __restrict__ y16, int64_t ld16,
+                                                        int64_t V, int32_t* __restrict__ id_err) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const DropKeys dk = resolve_drop(drop);
   const int per = H / 64;                                  // <= 16 values per lane
   float v[16];
-  const bf16_t* src = table + ids[row] * (int64_t)H;
+  const bf16_t* src = table + clamp_id(ids[row], V, id_err, TTMI_IDERR_TEXT) * (int64_t)H;
   float s = 0.f;
   for (int e = 0; e < per; ++e) { v[e] = bf2f(src[e * 64 + lane]); s += v[e]; }
   for (int off = 32; off; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -411,13 +412,15 @@ extern "C" int ttmi_deb_gelu(int64_t n, const uint16_t* x, uint16_t* y, hipStrea
 extern "C" int ttmi_deb_embed_fwd(int64_t M, int H, const int64_t* ids, const uint16_t* table,
                                   const float* ln_w, const float* ln_b, float eps,
                                   const int64_t* mask, float drop_p, const uint64_t* drop_seed,
-                                  float* y32, uint16_t* y16, int64_t ld16, hipStream_t s) {
-  TTMI_REQUIRE(M > 0 && H % 64 == 0 && H <= 1024 && ld16 >= H, "ttmi_deb_embed_fwd: need H %% 64 == 0, H <= 1024");
+                                  float* y32, uint16_t* y16, int64_t ld16, int64_t V, int32_t* id_err,
+                                  hipStream_t s) {
+  TTMI_REQUIRE(M > 0 && H % 64 == 0 && H <= 1024 && ld16 >= H && V > 0,
+               "ttmi_deb_embed_fwd: need H %% 64 == 0, H <= 1024, V > 0");
   TTMI_REQUIRE(ids && table && ln_w && ln_b && y16, "ttmi_deb_embed_fwd: null argument");
   TTMI_REQUIRE(drop_p == 0.f || drop_seed, "ttmi_deb_embed_fwd: dropout needs a seed");
   hipLaunchKernelGGL(deb_embed_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, M, H, ids,
                      (const bf16_t*)table, ln_w, ln_b, eps, mask, make_drop(drop_p, drop_seed), y32,
-                     (bf16_t*)y16, ld16);
+                     (bf16_t*)y16, ld16, V, id_err);
   return ttmi_check_launch("ttmi_deb_embed_fwd");
 }
 

@@ -44,6 +44,7 @@ struct ItemArgs {
   // Stage A stores z, bmean, brstd write-through (sc1) and its quarter mergers count on
   // bncnt[IN1/64]; the C workgroups poll that count, then read them with sc1 loads.
   int fin;
+  int32_t* err;                // the user head's id_err flags: [TTMI_IDERR_HEAD_POLL] on a poll timeout
 };
 
 struct ItemLdsA {
@@ -78,6 +79,7 @@ struct HeadArgs {
   ItemArgs it; int nbu, it_nblk;
   int it_stage;                // 0: item stage A (it_nblk x 8 workgroups), 2: item stage C (it_nblk),
                                // 3: both, A's then C's (C waits for A's statistics in-launch)
+  int ng, nc; int32_t* id_err; // table rows of G / C; ids outside are clamped and flagged (ABI 20)
 };
 
 struct HeadLds {
@@ -379,6 +381,7 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > (1 << 22)) {
           __hip_atomic_store(a.bncnt + BN_CDONE + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (a.err) a.err[TTMI_IDERR_HEAD_POLL] = 1;      // the host raises (ops.check_id_errors)
           break;
         }
       }
@@ -556,7 +559,8 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
   {   // demographics: a thread owns 4 of a row's 64 trailing columns (one index load, then
       // both tables read at clamped addresses and the value selected: no conditional load)
     const int r = tid >> 4, k0 = HD + 4 * (tid & 15), rr = min(r0 + r, a.B - 1);
-    const int64_t gi = a.gender[rr], ci = a.country[rr];
+    const int64_t gi = clamp_id(a.gender[rr], a.ng, a.id_err, TTMI_IDERR_GENDER);
+    const int64_t ci = clamp_id(a.country[rr], a.nc, a.id_err, TTMI_IDERR_COUNTRY);
     float v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -723,6 +727,7 @@ struct HeadBwdArgs {
   int64_t* dG; int64_t* dC;          // TTMI_FX_GRAD fixed-point accumulators
   bf16_t* dz16; bf16_t* dy2; bf16_t* dz1; float* dx1; bf16_t* dy1; bf16_t* dctx; float* ws;
   ItemBwdArgs it; int nbu;     // co-launched item head backward: workgroups >= nbu
+  int ng, nc;                  // table rows of G / C (ids clamped as in the forward)
 };
 
 struct HeadBwdLds {
@@ -863,8 +868,8 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
   const DropKeys dk1{(uint32_t)s1, (uint32_t)(s1 >> 32), a.d1.thresh, a.d1.scale, a.d1.on};
   const DropKeys dk2{(uint32_t)s2, (uint32_t)(s2 >> 32), a.d2.thresh, a.d2.scale, a.d2.on};
   if (tid < HR) {
-    L.sGi[tid] = (int)a.gender[min(r0 + tid, a.B - 1)];
-    L.sCi[tid] = (int)a.country[min(r0 + tid, a.B - 1)];
+    L.sGi[tid] = (int)clamp_id(a.gender[min(r0 + tid, a.B - 1)], a.ng, nullptr, 0);
+    L.sCi[tid] = (int)clamp_id(a.country[min(r0 + tid, a.B - 1)], a.nc, nullptr, 0);
   }
   // every per-row operand of the chain now, before any weight prefetch: vmcnt retires in
   // order, so a late small load would also wait for the weights issued before it
@@ -1168,6 +1173,7 @@ int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_d
   TTMI_REQUIRE(d->B > 0 && d->D == HD, "ttmi_user_head_fwd: needs D == %d", HD);
   TTMI_REQUIRE(d->F > 0 && d->F <= FMAX && d->F % 256 == 0, "ttmi_user_head_fwd: needs F %% 256 == 0, F <= %d", FMAX);
   TTMI_REQUIRE(d->dg == 16 && d->dc == 32, "ttmi_user_head_fwd: demographic widths must be 16 and 32");
+  TTMI_REQUIRE(d->n_genders > 0 && d->n_countries > 0, "ttmi_user_head_fwd: n_genders / n_countries must be > 0");
   TTMI_REQUIRE(d->ctx && d->res && d->drop_rows && d->wo && d->bo && d->n2w && d->n2b && d->w1 && d->b1 && d->w2 &&
                d->b2 && d->gender && d->G && d->country && d->C && d->wf0 && d->bf0 && d->lnw &&
                d->lnb && d->wf3 && d->bf3 && d->x1 && d->a2 && d->m2 && d->r2 && d->h && d->comb &&
@@ -1180,6 +1186,7 @@ int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_d
   a.wo = (const bf16_t*)d->wo; a.bo = d->bo; a.n2w = d->n2w; a.n2b = d->n2b;
   a.w1 = (const bf16_t*)d->w1; a.b1 = d->b1; a.w2 = (const bf16_t*)d->w2; a.b2 = d->b2;
   a.gender = d->gender; a.G = d->G; a.country = d->country; a.C = d->C;
+  a.ng = d->n_genders; a.nc = d->n_countries; a.id_err = d->id_err;
   a.wf0 = (const bf16_t*)d->wf0; a.bf0 = d->bf0; a.lnw = d->lnw; a.lnb = d->lnb;
   a.wf3 = (const bf16_t*)d->wf3; a.bf3 = d->bf3;
   const uint64_t* any = reinterpret_cast<const uint64_t*>(d->bo);   // read, never used when off
@@ -1204,6 +1211,7 @@ int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_d
                  "(bn_part / bn_cnt, B <= %d)", BN_MAXBLK * HR);
     a.it_nblk = (it->B + HR - 1) / HR;
     a.it.fin = stage == 3;
+    a.it.err = d->id_err;
     extra = stage == 0 ? a.it_nblk * (IN1 / 64) : stage == 2 ? a.it_nblk : a.it_nblk * (IN1 / 64 + 1);
   }
   const dim3 grid((unsigned)(a.nbu + extra));
@@ -1271,6 +1279,7 @@ extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const t
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_bwd: null descriptor");
   TTMI_REQUIRE(d->B > 0 && d->D == HD && (d->F == 256 || d->F == 512) && d->dg == 16 && d->dc == 32,
                "ttmi_user_head_bwd: needs D == %d, F in {256, 512}, dg == 16, dc == 32", HD);
+  TTMI_REQUIRE(d->n_genders > 0 && d->n_countries > 0, "ttmi_user_head_bwd: n_genders / n_countries must be > 0");
   TTMI_REQUIRE(d->du && d->az && d->z && d->mz && d->rz && d->h && d->x1 && d->m2 && d->r2 &&
                d->drop_rows && d->gender && d->country && d->wf3t && d->wf0t && d->w2t && d->w1t &&
                d->wot && d->lnw && d->n2w && d->dG && d->dC && d->dz16 && d->dy2 && d->dz1 &&
@@ -1280,6 +1289,7 @@ extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const t
   a.du = (const bf16_t*)d->du; a.az = (const bf16_t*)d->az; a.z = d->z; a.mz = d->mz; a.rz = d->rz;
   a.h = (const bf16_t*)d->h; a.x1 = d->x1; a.m2 = d->m2; a.r2 = d->r2;
   a.drows = d->drop_rows; a.gender = d->gender; a.country = d->country;
+  a.ng = d->n_genders; a.nc = d->n_countries;
   a.wf3t = (const bf16_t*)d->wf3t; a.wf0t = (const bf16_t*)d->wf0t; a.w2t = (const bf16_t*)d->w2t;
   a.w1t = (const bf16_t*)d->w1t; a.wot = (const bf16_t*)d->wot; a.lnw = d->lnw; a.n2w = d->n2w;
   const uint64_t* any = reinterpret_cast<const uint64_t*>(d->lnw);   // read, never used when off

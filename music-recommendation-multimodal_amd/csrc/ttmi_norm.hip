@@ -249,7 +249,8 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
     const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ b,
     float eps, DropParams dp, float* __restrict__ x, float* __restrict__ mean,
     float* __restrict__ rstd, const float* __restrict__ w1, const float* __restrict__ b1,
-    float eps1, bf16_t* __restrict__ y1, float* __restrict__ mean1, float* __restrict__ rstd1) {
+    float eps1, bf16_t* __restrict__ y1, float* __restrict__ mean1, float* __restrict__ rstd1,
+    int32_t* __restrict__ id_err) {
   const int lane = threadIdx.x & 63;
   const int64_t M = (int64_t)B * L;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -259,7 +260,8 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
   for (int64_t row = wid; row < M; row += nw) {
     const int l = (int)(row % L);
     const int64_t id = ids[row];
-    const bool ok = id >= 0 && id < V;
+    const bool ok = id >= 0 && id < V;      // an id outside the table reads a zero row and flags
+    if (!ok && id_err) id_err[TTMI_IDERR_HISTORY] = 1;
     float v[NV];
     float s = 0.f;
 #pragma unroll
@@ -327,7 +329,8 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_vec_kernel(
     const float* __restrict__ P, const float* __restrict__ w, const float* __restrict__ b,
     float eps, DropParams dp, float* __restrict__ x, float* __restrict__ mean,
     float* __restrict__ rstd, const float* __restrict__ w1, const float* __restrict__ b1,
-    float eps1, bf16_t* __restrict__ y1, float* __restrict__ mean1, float* __restrict__ rstd1) {
+    float eps1, bf16_t* __restrict__ y1, float* __restrict__ mean1, float* __restrict__ rstd1,
+    int32_t* __restrict__ id_err) {
   constexpr int LPR = D / 4, RPW = 64 / LPR;          // lanes per row, rows per wave instruction
   const int lane = threadIdx.x & 63, j = lane % LPR, sub = lane / LPR;
   const int64_t M = (int64_t)B * L;
@@ -348,7 +351,8 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_vec_kernel(
     float4 e[U], pv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool ok = id[u] >= 0 && id[u] < V;
+      const bool ok = id[u] >= 0 && id[u] < V;   // outside the table: a zero row, flagged
+      if (!ok && id_err) id_err[TTMI_IDERR_HISTORY] = 1;
       const int l = (int)(min(row[u], M - 1) % L);
       e[u] = reinterpret_cast<const float4*>(E + (ok ? id[u] : 0) * D)[j];
       if (!ok) e[u] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -488,7 +492,8 @@ __global__ void user_concat_fwd_kernel(int B, int L, int D, const float* __restr
                                        const float* __restrict__ G, int dg,
                                        const int64_t* __restrict__ country,
                                        const float* __restrict__ C, int dc, T* __restrict__ comb,
-                                       int32_t* __restrict__ rows) {
+                                       int32_t* __restrict__ rows, int ng, int nc,
+                                       int32_t* __restrict__ id_err) {
   const int lane = threadIdx.x & 63;
   const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (b >= B) return;
@@ -498,7 +503,8 @@ __global__ void user_concat_fwd_kernel(int B, int L, int D, const float* __restr
   const int len = len_src ? (int)(wave_sum(cnt) + 0.5f) : 1;
   const int64_t row = (int64_t)b * L + max(len - 1, 0);
   const int W = D + dg + dc;
-  const int64_t g = gender[b], c = country[b];
+  const int64_t g = clamp_id(gender[b], ng, id_err, TTMI_IDERR_GENDER);
+  const int64_t c = clamp_id(country[b], nc, id_err, TTMI_IDERR_COUNTRY);
   for (int k = lane; k < W; k += 64) {
     float v;
     if (k < D) v = x[row * D + k];
@@ -514,13 +520,13 @@ __global__ void user_concat_bwd_kernel(int B, int D, const float* __restrict__ d
                                        const int64_t* __restrict__ gender, int dg,
                                        const int64_t* __restrict__ country, int dc,
                                        float* __restrict__ dx, int64_t* __restrict__ dG,
-                                       int64_t* __restrict__ dC, int accumulate) {
+                                       int64_t* __restrict__ dC, int accumulate, int ng, int nc) {
   const int lane = threadIdx.x & 63;
   const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (b >= B) return;
   const int W = D + dg + dc;
   const int64_t row = rows[b];
-  const int64_t g = gender[b], c = country[b];
+  const int64_t g = clamp_id(gender[b], ng, nullptr, 0), c = clamp_id(country[b], nc, nullptr, 0);
   for (int k = lane; k < W; k += 64) {
     const float v = dcomb[(int64_t)b * W + k];
     if (k < D) {
@@ -862,7 +868,7 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
                                   const float* P, const float* w, const float* b, float eps,
                                   float drop_p, const uint64_t* drop_seed, float* x, float* mean,
                                   float* rstd, const float* w1, const float* b1, float eps1, void* y1,
-                                  float* mean1, float* rstd1, hipStream_t s) {
+                                  float* mean1, float* rstd1, int32_t* id_err, hipStream_t s) {
   TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && D <= 64 * MAXV, "ttmi_seq_embed_fwd: bad sizes");
   TTMI_REQUIRE(ids && E && P && w && b && x && mean && rstd, "ttmi_seq_embed_fwd: null argument");
   TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "ttmi_seq_embed_fwd: drop_p out of [0,1)");
@@ -890,7 +896,7 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
     const int64_t waves = (M + U * rpw - 1) / (U * rpw);
     const dim3 g((unsigned)std::min<int64_t>((waves + 3) / 4, cap));
 #define TTMI_SEQV(DD, LN) hipLaunchKernelGGL((seq_embed_fwd_vec_kernel<DD, LN, U>), g, dim3(256), 0, s, B, L, ids, E, V, P, \
-                                             w, b, eps, dp, x, mean, rstd, w1, b1, eps1, (bf16_t*)y1, mean1, rstd1)
+                                             w, b, eps, dp, x, mean, rstd, w1, b1, eps1, (bf16_t*)y1, mean1, rstd1, id_err)
     if (D == 128) { if (ln2) TTMI_SEQV(128, true); else TTMI_SEQV(128, false); }
     else { if (ln2) TTMI_SEQV(256, true); else TTMI_SEQV(256, false); }
 #undef TTMI_SEQV
@@ -900,10 +906,10 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
   TTMI_NV_DISPATCH(D, {
     if (ln2)
       hipLaunchKernelGGL((seq_embed_fwd_kernel<NV, true>), grid, dim3(256), 0, s, B, L, D, ids, E, V, P,
-                         w, b, eps, dp, x, mean, rstd, w1, b1, eps1, (bf16_t*)y1, mean1, rstd1);
+                         w, b, eps, dp, x, mean, rstd, w1, b1, eps1, (bf16_t*)y1, mean1, rstd1, id_err);
     else
       hipLaunchKernelGGL((seq_embed_fwd_kernel<NV, false>), grid, dim3(256), 0, s, B, L, D, ids, E, V, P,
-                         w, b, eps, dp, x, mean, rstd, nullptr, nullptr, 0.f, nullptr, nullptr, nullptr);
+                         w, b, eps, dp, x, mean, rstd, nullptr, nullptr, 0.f, nullptr, nullptr, nullptr, id_err);
   });
   return ttmi_check_launch("ttmi_seq_embed_fwd");
 }
@@ -961,9 +967,11 @@ extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, int64_t V, const int64_t*
 extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float* x,
                                     const int64_t* len_src, const int64_t* gender, const float* G,
                                     int dg, const int64_t* country, const float* C, int dc,
-                                    void* comb, int32_t* rows, hipStream_t s) {
+                                    void* comb, int32_t* rows, int n_genders, int n_countries,
+                                    int32_t* id_err, hipStream_t s) {
   TTMI_REQUIRE(dtype == TTMI_F32 || dtype == TTMI_BF16, "ttmi_user_concat_fwd: bad dtype");
-  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && dg >= 0 && dc >= 0, "ttmi_user_concat_fwd: bad sizes");
+  TTMI_REQUIRE(B >= 0 && L > 0 && D > 0 && dg >= 0 && dc >= 0 && n_genders > 0 && n_countries > 0,
+               "ttmi_user_concat_fwd: bad sizes");
   TTMI_REQUIRE(x && gender && country && comb && rows && (dg == 0 || G) && (dc == 0 || C),
                "ttmi_user_concat_fwd: null argument");
   TTMI_REQUIRE(len_src || L == 1, "ttmi_user_concat_fwd: len_src == NULL needs L == 1");
@@ -971,21 +979,23 @@ extern "C" int ttmi_user_concat_fwd(int dtype, int B, int L, int D, const float*
   dim3 grid((B + 3) / 4);
   if (dtype == TTMI_BF16)
     hipLaunchKernelGGL(user_concat_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, L, D, x, len_src,
-                       gender, G, dg, country, C, dc, (bf16_t*)comb, rows);
+                       gender, G, dg, country, C, dc, (bf16_t*)comb, rows, n_genders, n_countries, id_err);
   else
     hipLaunchKernelGGL(user_concat_fwd_kernel<float>, grid, dim3(256), 0, s, B, L, D, x, len_src,
-                       gender, G, dg, country, C, dc, (float*)comb, rows);
+                       gender, G, dg, country, C, dc, (float*)comb, rows, n_genders, n_countries, id_err);
   return ttmi_check_launch("ttmi_user_concat_fwd");
 }
 
 extern "C" int ttmi_user_concat_bwd(int B, int D, const float* dcomb, const int32_t* rows,
                                     const int64_t* gender, int dg, const int64_t* country, int dc,
-                                    float* dx, int64_t* dG, int64_t* dC, int accumulate, hipStream_t s) {
-  TTMI_REQUIRE(B >= 0 && D > 0 && dg >= 0 && dc >= 0, "ttmi_user_concat_bwd: bad sizes");
+                                    float* dx, int64_t* dG, int64_t* dC, int accumulate,
+                                    int n_genders, int n_countries, hipStream_t s) {
+  TTMI_REQUIRE(B >= 0 && D > 0 && dg >= 0 && dc >= 0 && n_genders > 0 && n_countries > 0,
+               "ttmi_user_concat_bwd: bad sizes");
   TTMI_REQUIRE(dcomb && rows && gender && country && dx, "ttmi_user_concat_bwd: null argument");
   if (B == 0) return TTMI_OK;
   hipLaunchKernelGGL(user_concat_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, B, D, dcomb, rows,
-                     gender, dg, country, dc, dx, dG, dC, accumulate);
+                     gender, dg, country, dc, dx, dG, dC, accumulate, n_genders, n_countries);
   return ttmi_check_launch("ttmi_user_concat_bwd");
 }
 

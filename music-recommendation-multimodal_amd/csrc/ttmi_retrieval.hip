@@ -231,12 +231,16 @@ __global__ __launch_bounds__(256) void mask_items_kernel(int R, int V, float* __
 // max(|e|, 1e-8) (:82); dense[ids[r]] = e.  One wave per row.
 __global__ __launch_bounds__(256) void catalogue_rows_kernel(int n, int D, const float* __restrict__ x,
                                                              int64_t ldx, const int64_t* __restrict__ ids,
-                                                             int64_t V, float* __restrict__ dense) {
+                                                             int64_t V, float* __restrict__ dense,
+                                                             int32_t* __restrict__ id_err) {
   const int lane = threadIdx.x & 63;
   const int r = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (r >= n) return;
   const int64_t id = ids[r];
-  if (id < 0 || id >= V) return;
+  if (id < 0 || id >= V) {                 // skipped; the host raises IndexError (ABI 20)
+    if (id_err) id_err[TTMI_IDERR_CATALOGUE] = 1;
+    return;
+  }
   const float* xr = x + (int64_t)r * ldx;
   float s = 0.f;
   for (int c = lane; c < D; c += 64) s += xr[c] * xr[c];
@@ -257,12 +261,12 @@ __global__ __launch_bounds__(256) void catalogue_rows_kernel(int n, int D, const
 }
 
 extern "C" int ttmi_catalogue_rows(int n, int D, const float* x, int64_t ldx, const int64_t* ids,
-                                   int64_t V, float* dense, hipStream_t s) {
+                                   int64_t V, float* dense, int32_t* id_err, hipStream_t s) {
   TTMI_REQUIRE(n >= 0 && D > 0 && ldx >= D && V > 0, "ttmi_catalogue_rows: bad sizes");
   if (n == 0) return TTMI_OK;
   TTMI_REQUIRE(x && ids && dense, "ttmi_catalogue_rows: null argument");
   hipLaunchKernelGGL(catalogue_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, s, n, D, x, ldx, ids,
-                     V, dense);
+                     V, dense, id_err);
   return ttmi_check_launch("ttmi_catalogue_rows");
 }
 

@@ -148,21 +148,23 @@ def _dx(dy: Tensor, W: Dict[str, Tensor], name: str, out: Tensor, gate: Optional
     return ops.linear_dx(dy, W[name], out, gate=gate, gate_scale=gate_scale)
 
 
-def _ln_k_ok(D: int, K: int) -> bool:
+def _ln_k_ok(D: int, K: int, M: int = 0) -> bool:
     """K a fused LayerNorm-epilogue GEMM takes at LayerNorm width D (ttmi_linear_ln_bwd /
-    ttmi_linear_res_ln): D = 128 with W resident in LDS, D = 256 with W streamed (ABI 19)."""
+    ttmi_linear_res_ln): D = 128 with W resident in LDS, D = 256 with W streamed (ABI 19), whose
+    DMA offsets are 32-bit: its [M, K] bf16 operand must stay under 4 GB (else the unfused
+    path runs)."""
     if D == 128:
         return K % 128 == 0 and 0 < K <= 512
-    return D == 256 and K % 256 == 0 and 0 < K <= 1024
+    return D == 256 and K % 256 == 0 and 0 < K <= 1024 and M * K * 2 < (1 << 32)
 
 
-def _ln_fusable(W: Dict[str, Tensor], pre: str, D: int) -> bool:
+def _ln_fusable(W: Dict[str, Tensor], pre: str, D: int, M: int) -> bool:
     """The layer's input-grad GEMMs can carry the LayerNorm backward in their epilogue:
     bf16 with the transposed weight mirrors present and the LayerNorm width 128 or 256."""
     wt1 = W.get(transposed_name(pre + "linear1.weight"))
     wti = W.get(transposed_name(pre + "self_attn.in_proj_weight"))
-    return (wt1 is not None and wti is not None and _ln_k_ok(D, wt1.shape[1])
-            and _ln_k_ok(D, wti.shape[1]))
+    return (wt1 is not None and wti is not None and _ln_k_ok(D, wt1.shape[1], M)
+            and _ln_k_ok(D, wti.shape[1], M))
 
 
 # The item head's stages A and C both inside the fused user head launch (C polling A's
@@ -175,12 +177,12 @@ def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
 
-def _resln_ok(W: Dict[str, Tensor], name: str, D: int) -> bool:
+def _resln_ok(W: Dict[str, Tensor], name: str, D: int, M: int) -> bool:
     """The Linear `name` can end its residual sub-block with the following LayerNorm fused
     (ttmi_linear_res_ln): bf16 weight [D, K], D = 128 (K % 128 == 0, K <= 512) or D = 256
-    (K in {256, 512, 768, 1024})."""
+    (K in {256, 512, 768, 1024}) over M rows."""
     w = W[name]
-    return w.dtype == torch.bfloat16 and w.shape[0] == D and _ln_k_ok(D, w.shape[1])
+    return w.dtype == torch.bfloat16 and w.shape[0] == D and _ln_k_ok(D, w.shape[1], M)
 
 
 def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gender: Tensor,
@@ -281,7 +283,7 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
         x1 = torch.empty(R, D, **f32)
         a2, m2, r2 = ln_out(R)
         name = pre + "self_attn.out_proj.weight"
-        if not pruned and _resln_ok(W, name, D):       # out_proj + residual + norm2, one kernel
+        if not pruned and _resln_ok(W, name, D, R):    # out_proj + residual + norm2, one kernel
             ops.linear_res_ln(ctx, W[name], P[pre + "self_attn.out_proj.bias"], res_in, x1,
                               P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2,
                               eps=cfg.eps, drop=_drop(cfg, seeds, site_drop1(i)))
@@ -294,7 +296,7 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                    drop=_drop(cfg, seeds, site_ffn(i)), drop_rows=drows)
         x2 = torch.empty(R, D, **f32)
         name = pre + "linear2.weight"
-        if not pruned and i + 1 < cfg.n_layers and _resln_ok(W, name, D):
+        if not pruned and i + 1 < cfg.n_layers and _resln_ok(W, name, D, R):
             # linear2 + residual + the next layer's norm1, one kernel
             nxt = ln_out(M)
             nx = _lp(i + 1)
@@ -387,7 +389,7 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         R = s.x1.shape[0]                 # B for the pruned layer, M otherwise
         drows = s.rows
         F_ = W[pre + "linear1.weight"].shape[0]
-        fuse = _ln_fusable(W, pre, D)
+        fuse = _ln_fusable(W, pre, D, R)
         if head is not None and i == cfg.n_layers - 1:
             dctx, dx1 = head["dctx"], head["dx1"]
         else:
@@ -475,7 +477,7 @@ def _head_bwd_unfused(P, W, st, du, grads, cfg, du16, gathered):
     C = P["country_embedding.weight"]
     ops.user_concat_bwd(dcomb, st.rows, st.gender, G.shape[1], st.country, C.shape[1], dx,
                         grads["gender_embedding.weight"], grads["country_embedding.weight"],
-                        accumulate=not gathered)
+                        accumulate=not gathered, n_tables=(G.shape[0], C.shape[0]))
     return dx
 
 

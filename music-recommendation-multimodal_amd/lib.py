@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -129,7 +129,8 @@ class UserHeadDesc(ctypes.Structure):
                 ("d2_p", ctypes.c_float), ("d2_seed", c_p),
                 ("x1", c_p), ("a2", c_p), ("m2", c_p), ("r2", c_p), ("h", c_p), ("comb", c_p),
                 ("rows", c_p), ("z", c_p), ("az", c_p), ("mz", c_p), ("rz", c_p), ("u", c_p),
-                ("u_hat", c_p), ("u_norm", c_p)]
+                ("u_hat", c_p), ("u_norm", c_p),
+                ("n_genders", c_i), ("n_countries", c_i), ("id_err", c_p)]
 
 
 class UserHeadBwdDesc(ctypes.Structure):
@@ -145,7 +146,8 @@ class UserHeadBwdDesc(ctypes.Structure):
                 ("d2_p", ctypes.c_float), ("d2_seed", c_p),
                 ("dG", c_p), ("dC", c_p),
                 ("dz16", c_p), ("dy2", c_p), ("dz1", c_p), ("dx1", c_p), ("dy1", c_p),
-                ("dctx", c_p), ("ws", c_p)]
+                ("dctx", c_p), ("ws", c_p),
+                ("n_genders", c_i), ("n_countries", c_i)]
 
 
 class LnBwdDesc(ctypes.Structure):
@@ -195,7 +197,7 @@ SIGNATURES = {
     "ttmi_last_error": (ctypes.c_char_p, []),
     "ttmi_abi_version": (c_i, []),
     "ttmi_gemm": (c_i, [ctypes.POINTER(GemmDesc), c_p]),
-    "ttmi_catalogue_rows": (c_i, [c_i, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p]),
+    "ttmi_catalogue_rows": (c_i, [c_i, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p]),
     "ttmi_wgrad_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64, c_i64]),
     "ttmi_wgrad": (c_i, [ctypes.POINTER(WgradDesc), c_p]),
     "ttmi_wgrad_fold": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
@@ -215,7 +217,7 @@ SIGNATURES = {
     "ttmi_layernorm_bwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i, c_i64,
                                  c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f, c_p, c_i, c_p]),
     "ttmi_seq_embed_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_i64, c_p, c_p, c_p, c_f, c_f, c_p, c_p,
-                                 c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
+                                 c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_seq_embed_bwd_workspace": (c_i64, [c_i64, c_i, c_i]),
     "ttmi_seq_embed_bwd_folds": (c_i, [c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_seq_embed_bwd": (c_i, [c_i, c_i, c_i, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p,
@@ -223,8 +225,9 @@ SIGNATURES = {
     "ttmi_mha_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_user_concat_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_p,
-                                   c_p, c_p]),
-    "ttmi_user_concat_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p, c_i, c_p]),
+                                   c_p, c_i, c_i, c_p, c_p]),
+    "ttmi_user_concat_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p, c_i, c_i,
+                                   c_i, c_p]),
     "ttmi_batchnorm_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_i, c_i,
                                  c_f, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_batchnorm_bwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_i, c_p, c_p, c_p,
@@ -250,7 +253,7 @@ SIGNATURES = {
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
     "ttmi_linear_res_ln": (c_i, [c_p, c_p]),
     "ttmi_deb_embed_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, ctypes.c_float, c_p,
-                                 ctypes.c_float, c_p, c_p, c_p, c_i64, c_p]),
+                                 ctypes.c_float, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p]),
     "ttmi_deb_ln_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p,
                                c_f, c_p, c_p, c_p]),
     "ttmi_deb_gelu": (c_i, [c_i64, c_p, c_p, c_p]),

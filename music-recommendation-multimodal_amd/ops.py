@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -44,6 +45,92 @@ def _dev(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
             raise ValueError("libttmi ops need GPU tensors")
+
+
+# ----------------------------------------------------------------------------- id range flags
+# The reference's nn.Embedding lookups raise IndexError for an id outside the table
+# (user_tower.py:26,30-31; the DeBERTa word embedding; the catalogue assignment
+# evaluate_metrics.py:102).  The device lookups never index outside a table (include/ttmi.h
+# TTMI_IDERR_*): they clamp / skip and set a flag.  The flags live in host-mapped memory
+# (hipHostMalloc, mapped + coherent), so reading them needs no device sync and costs the step
+# nothing: check_id_errors() raises once the flagging launch has run (the next step / forward,
+# or any point after a sync).
+ID_ERR_KEYS = ("history_ids", "user_gender", "user_country", "target_input_ids", "target_id")
+_IDERR_HEAD_POLL = 7        # TTMI_IDERR_HEAD_POLL: not an id, the co-launched head's poll timed out
+_N_IDERR = 8
+
+
+class _IdFlags:
+    """int32[8] flags of one device: host-mapped (``host`` reads them, ``dptr`` is what the
+    kernels get), or, if the runtime refuses the mapping, a device tensor read on sync only."""
+
+    def __init__(self, device: torch.device):
+        self.host = None
+        self.dev = None
+        self.dptr = None
+        try:
+            hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD)   # torch's runtime
+            ptr, dptr = ctypes.c_void_p(), ctypes.c_void_p()
+            flags = 0x1 | 0x2 | 0x40000000      # hipHostMallocPortable | Mapped | Coherent
+            with torch.cuda.device(device):
+                if hip.hipHostMalloc(ctypes.byref(ptr), ctypes.c_size_t(4 * _N_IDERR),
+                                     ctypes.c_uint(flags)) == 0 and \
+                        hip.hipHostGetDevicePointer(ctypes.byref(dptr), ptr, ctypes.c_uint(0)) == 0:
+                    self.host = (ctypes.c_int32 * _N_IDERR).from_address(ptr.value)
+                    for i in range(_N_IDERR):
+                        self.host[i] = 0
+                    self.dptr = dptr.value
+        except OSError:
+            pass
+        if self.host is None:
+            self.dev = torch.zeros(_N_IDERR, dtype=torch.int32, device=device)
+            self.dptr = self.dev.data_ptr()
+
+    def take(self, sync: bool) -> List[int]:
+        """Indices of the raised flags (cleared)."""
+        if self.host is not None:
+            vals = list(self.host)
+            for i, v in enumerate(vals):
+                if v:
+                    self.host[i] = 0
+        elif sync:
+            vals = self.dev.tolist()
+            if any(vals):
+                self.dev.zero_()
+        else:
+            return []
+        return [i for i, v in enumerate(vals) if v]
+
+
+_IDF: Dict[int, _IdFlags] = {}
+
+
+def id_err_ptr(t: Tensor) -> int:
+    """Device pointer of the id range flags of ``t``'s device (allocated on first use)."""
+    idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    f = _IDF.get(idx)
+    if f is None:
+        f = _IDF[idx] = _IdFlags(torch.device("cuda", idx))
+    return f.dptr
+
+
+def check_id_errors(sync: bool = False) -> None:
+    """Raise IndexError (as nn.Embedding does) if a device lookup has met an id outside its
+    table since the last check; the flags are cleared.  sync=True first waits for the device,
+    so every launch issued so far is covered; otherwise only launches that have finished."""
+    if not _IDF:
+        return
+    if sync:
+        torch.cuda.synchronize()
+    for f in _IDF.values():
+        bad = f.take(sync)
+        if _IDERR_HEAD_POLL in bad:
+            raise RuntimeError("ttmi_user_item_head_fwd_ac: the item head's stage-C poll timed out "
+                               "(TTMI_HEAD_AC=1); that step's item embeddings are invalid")
+        if bad:
+            keys = ", ".join(ID_ERR_KEYS[i] if i < len(ID_ERR_KEYS) else f"flag {i}" for i in bad)
+            raise IndexError(f"index out of range in self: {keys} held an id outside its embedding "
+                             f"table (the device lookup was clamped)")
 
 
 # ----------------------------------------------------------------------------- GEMM
@@ -584,7 +671,7 @@ def seq_embed_fwd(ids: Tensor, E: Tensor, P: Tensor, w: Tensor, b: Tensor, x: Te
         raise ValueError("seq_embed_fwd: norm1 output must be bf16")
     call("ttmi_seq_embed_fwd", B, L, D, _p(ids), _p(E), V, _p(P), _p(w), _p(b), eps,
          float(drop[0]), _p(drop[1]), _p(x), _p(mean), _p(rstd), _p(w1), _p(b1), float(eps1),
-         _p(y1), _p(m1), _p(r1), _s())
+         _p(y1), _p(m1), _p(r1), id_err_ptr(ids), _s())
     return x
 
 
@@ -698,21 +785,23 @@ def user_concat_fwd(x: Tensor, len_src: Optional[Tensor], gender: Tensor, G: Ten
                     country: Tensor, C: Tensor, comb: Tensor, rows: Tensor, B: int, L: int):
     D = x.shape[1]
     call("ttmi_user_concat_fwd", code(comb.dtype), B, L, D, _p(x), _p(len_src), _p(gender), _p(G),
-         G.shape[1], _p(country), _p(C), C.shape[1], _p(comb), _p(rows), _s())
+         G.shape[1], _p(country), _p(C), C.shape[1], _p(comb), _p(rows), G.shape[0], C.shape[0],
+         id_err_ptr(gender), _s())
     return comb
 
 
 def user_concat_bwd(dcomb: Tensor, rows: Tensor, gender: Tensor, dg: int, country: Tensor,
                     dc: int, dx: Tensor, dG: Optional[Tensor], dC: Optional[Tensor],
-                    accumulate: bool = True):
+                    accumulate: bool = True, n_tables: Tuple[int, int] = (1, 1)):
     """Concat backward: dx rows (one writer each) and the demographic embedding gradients,
-    whose rows users share, through int64 fixed-point accumulators folded into dG / dC."""
+    whose rows users share, through int64 fixed-point accumulators folded into dG / dC.
+    n_tables = (rows of G, rows of C): the ids are clamped into them as in the forward."""
     B = dcomb.shape[0]
     D = dcomb.shape[1] - dg - dc
     aG = _fx_zero("concat.dG", dG.numel(), dG.device) if dG is not None else None
     aC = _fx_zero("concat.dC", dC.numel(), dC.device) if dC is not None else None
     call("ttmi_user_concat_bwd", B, D, _p(dcomb), _p(rows), _p(gender), dg, _p(country), dc,
-         _p(dx), _p(aG), _p(aC), int(accumulate), _s())
+         _p(dx), _p(aG), _p(aC), int(accumulate), int(n_tables[0]), int(n_tables[1]), _s())
     fx_folds([(aG, dG), (aC, dC)])
 
 
@@ -1119,7 +1208,8 @@ def deb_embed_fwd(ids: Tensor, table: Tensor, w: Tensor, b: Tensor, eps: float,
     if y16.shape[0] < M or y16.stride(0) < H or (y32 is not None and y32.numel() < M * H):
         raise ValueError("deb_embed_fwd: output too small")
     call("ttmi_deb_embed_fwd", M, H, _p(ids), _p(table), _p(w), _p(b), eps, _p(mask),
-         float(drop[0]), _p(drop[1]), _p(y32), _p(y16), y16.stride(0), _s())
+         float(drop[0]), _p(drop[1]), _p(y32), _p(y16), y16.stride(0), table.shape[0],
+         id_err_ptr(ids), _s())
     return y16
 
 
@@ -1218,6 +1308,9 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
     d.w2, d.b2 = _p(W[pre + "linear2.weight"]), _p(P[pre + "linear2.bias"])
     d.gender, d.G = _p(gender), _p(P["gender_embedding.weight"])
     d.country, d.C = _p(country), _p(P["country_embedding.weight"])
+    d.n_genders = P["gender_embedding.weight"].shape[0]
+    d.n_countries = P["country_embedding.weight"].shape[0]
+    d.id_err = id_err_ptr(gender)
     d.wf0, d.bf0 = _p(W["fusion_layer.0.weight"]), _p(P["fusion_layer.0.bias"])
     d.lnw, d.lnb = _p(P["fusion_layer.1.weight"]), _p(P["fusion_layer.1.bias"])
     d.wf3, d.bf3 = _p(W["fusion_layer.3.weight"]), _p(P["fusion_layer.3.bias"])
@@ -1265,6 +1358,8 @@ def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: 
     for k in ("az", "z", "mz", "rz", "h", "x1", "m2", "r2"):
         setattr(d, k, _p(saved[k]))
     d.drop_rows, d.gender, d.country = _p(drop_rows), _p(gender), _p(country)
+    d.n_genders = P["gender_embedding.weight"].shape[0]
+    d.n_countries = P["country_embedding.weight"].shape[0]
     T = ".T"
     d.wf3t, d.wf0t = _p(W["fusion_layer.3.weight" + T]), _p(W["fusion_layer.0.weight" + T])
     d.w2t, d.w1t = _p(W[pre + "linear2.weight" + T]), _p(W[pre + "linear1.weight" + T])
@@ -1401,7 +1496,8 @@ def catalogue_rows(x: Tensor, ids: Tensor, dense: Tensor) -> Tensor:
     n, D = x.shape
     if dense.shape[1] != D or ids.shape[0] != n:
         raise ValueError("catalogue_rows: shape mismatch")
-    call("ttmi_catalogue_rows", n, D, _p(x), x.stride(0), _p(ids), dense.shape[0], _p(dense), _s())
+    call("ttmi_catalogue_rows", n, D, _p(x), x.stride(0), _p(ids), dense.shape[0], _p(dense),
+         id_err_ptr(ids), _s())
     return dense
 
 

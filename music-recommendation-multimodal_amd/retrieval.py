@@ -103,6 +103,7 @@ class GlobalEvaluator:
         return target_ranks(u, self.items, b["target_id"], self.max_k)
 
     def ranks(self, batch: Dict[str, Tensor]) -> Tensor:
+        ops.check_id_errors()          # ids outside a table in an earlier (finished) batch
         dev = self.items.device
         b = {k: batch[k].to(dev, non_blocking=True) for k in self.KEYS if batch.get(k) is not None}
         self.model.eval()
@@ -177,6 +178,7 @@ class CatalogueIndexer:
 
     def add(self, batch: Dict[str, Tensor]) -> None:
         """Index one batch of items."""
+        ops.check_id_errors()          # target_id / token ids outside their tables, earlier batches
         dev = self.device
         b = {k: batch[k].to(dev, non_blocking=True) for k in self.KEYS if batch.get(k) is not None}
         b["target_id"] = b["target_id"].long()
@@ -217,6 +219,7 @@ class CatalogueIndexer:
         self.dense.zero_()
         for batch in loader:
             self.add(batch)
+        ops.check_id_errors(sync=True)     # dense[target_id] = emb raises for a bad id (:102)
         return self.dense
 
 
@@ -240,6 +243,7 @@ def calculate_metrics_global(model, val_loader: Iterable, item_embeddings: Tenso
             ranks = ev.ranks(batch)
             for name, v in metrics_from_ranks(ranks, k_list).items():
                 per[name].append(v.cpu())
+    ops.check_id_errors(sync=True)
     return {name: torch.cat(v).mean().item() for name, v in per.items()}
 
 

@@ -552,6 +552,7 @@ class TextEncoder(nn.Module):
 
     def forward(self, input_ids: Tensor, attention_mask: Tensor,
                 seeds: Optional[Tensor] = None) -> Tensor:
+        ops.check_id_errors()          # token ids outside the word table met by earlier launches
         names, params = zip(*self.trainable())
         if self.training and seeds is None:
             seeds = torch.randint(-(2 ** 62), 2 ** 62, (N_TEXT_SITES,), device=input_ids.device,

@@ -67,6 +67,7 @@ def train_one_epoch(model, dataloader, optimizer, device, epoch, is_main_process
         loss.backward()
         optimizer.step()
         loss_val = loss.item()
+        ops.check_id_errors()     # synced by .item(): an id outside its table raises this step
         total_loss += loss_val
         if is_main_process and (i + 1) % log_interval == 0:
             logger.info(f"Epoch {epoch} [{i + 1}/{num_batches}] | Loss: {loss_val:.4f}")
@@ -575,27 +576,17 @@ class TrainStep:
         return tuple((k, tuple(batch[k].shape), batch[k].dtype)
                      for k in TrainStep.INPUT_KEYS if k in batch)
 
-    def _check_ids(self, batch: Dict[str, Tensor]) -> None:
-        """The embedding lookups index their tables unchecked on the device, so the first batch
-        of every new shape (one host sync per shape, not per step) is range-checked here; an
-        id outside its table raises IndexError as the reference's nn.Embedding does
-        (user_tower.py:153-156)."""
-        ut = self.model.user_tower
-        for key, emb in (("history_ids", ut.item_embedding), ("user_gender", ut.gender_embedding),
-                         ("user_country", ut.country_embedding)):
-            t = batch.get(key)
-            if t is None or t.numel() == 0:
-                continue
-            lo, hi = int(t.min()), int(t.max())
-            if lo < 0 or hi >= emb.num_embeddings:
-                raise IndexError(f"TrainStep: {key} holds ids in [{lo}, {hi}], outside its table "
-                                 f"of {emb.num_embeddings} rows (index out of range in self)")
+    def check(self) -> None:
+        """Wait for the queued steps and raise IndexError if any of them met an embedding id
+        outside its table (the reference's nn.Embedding raises, user_tower.py:26,30-31).  The
+        device lookups clamp such an id and set a host-mapped flag, so ``step()`` also raises at
+        its start for any earlier step that has finished, with no sync of its own."""
+        ops.check_id_errors(sync=True)
 
     def _stage(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         sig = self._signature(batch)
         e = self._entries.get(sig)
         if e is None:
-            self._check_ids(batch)
             e = _Entry({k: torch.empty(batch[k].shape, dtype=batch[k].dtype, device=self.device)
                         for k in self.INPUT_KEYS if k in batch})
             self._entries[sig] = e
@@ -633,6 +624,7 @@ class TrainStep:
         e.seg, e.loss, e.logits = seg, self.loss, self.logits
 
     def step(self, batch: Dict[str, Tensor]) -> Tensor:
+        ops.check_id_errors()                  # bad ids of earlier (finished) steps: IndexError
         ops.bump_param_epoch()                 # the replay below rewrites the parameters
         b = self._stage(batch)
         e = self._cur

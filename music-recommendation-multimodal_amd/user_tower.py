@@ -188,6 +188,9 @@ class SequentialUserEncoder(nn.Module):
 
     def forward(self, history_ids: Tensor, user_gender: Tensor, user_country: Tensor,
                 history_mask: Optional[Tensor] = None, seeds: Optional[Tensor] = None) -> Tensor:
+        # an id outside an embedding table met by an earlier (finished) launch raises here, as
+        # nn.Embedding raises (user_tower.py:26,30-31); the device lookups clamp and flag it
+        ops.check_id_errors()
         cfg = self.cfg()
         if cfg.p_drop > 0 and seeds is None:
             seeds = new_dropout_seeds(history_ids.device)

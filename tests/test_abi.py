@@ -95,3 +95,27 @@ def test_attention_dropout_index_bound_only_with_dropout():
         with pytest.raises(ValueError, match="2\\^32"):
             fn((0.1, seed))
     ops._q1_batch_check("mha_q1", B, L, H, ops.NO_DROP)        # no dropout: accepted
+
+
+def test_id_error_flags_raise_and_clear(pkg):
+    """ops.check_id_errors reads the device lookups' range flags (include/ttmi.h TTMI_IDERR_*,
+    host-mapped on a GPU) and raises IndexError naming the key, as nn.Embedding does
+    (reference user_tower.py:26,30-31), then clears them; the co-launched head's poll-timeout
+    flag raises RuntimeError.  A stand-in host array replaces the hipHostMalloc'd one here."""
+    ops = pkg.ops
+    f = ops._IdFlags.__new__(ops._IdFlags)
+    f.host, f.dev, f.dptr = (ctypes.c_int32 * 8)(), None, 0
+    ops._IDF[-1] = f
+    try:
+        ops.check_id_errors()
+        f.host[2] = 1
+        f.host[0] = 1
+        with pytest.raises(IndexError, match="history_ids, user_country"):
+            ops.check_id_errors()
+        assert list(f.host) == [0] * 8
+        ops.check_id_errors()
+        f.host[7] = 1
+        with pytest.raises(RuntimeError, match="poll timed out"):
+            ops.check_id_errors()
+    finally:
+        del ops._IDF[-1]
