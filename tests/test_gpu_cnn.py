@@ -97,9 +97,9 @@ class _GradRound(torch.autograd.Function):
 # "bf16 storage, fp32 accumulation" implementation; they differ only in the order the K
 # products are summed, which moves individual bf16 roundings of the stored activations and
 # gradients, and the train-mode BatchNorm backward amplifies that (tools/diag_resnet_margin.py
-# measures the spread).  The GPU's conv tiles use yet another order (LDS-DMA k-steps of 64
-# channels x taps, 16x16x32 MFMA partial sums), so the GPU is judged against the worst of them.
-EMU_ORDERS = ("torch", "f64", "half", "evenodd", "quarter", "quarters")
+# measures the spread).  "kernel" is the conv kernels' own order (_KConv below): the GPU is
+# judged against it; the others show how far equally valid orders spread.
+EMU_ORDERS = ("kernel", "torch", "f64", "half", "evenodd", "quarter", "quarters")
 
 
 def _conv_order(x, w, stride, pad, order):
@@ -121,14 +121,143 @@ def _conv_order(x, w, stride, pad, order):
             TF.conv2d(x[:, :h], w[:, :h], stride=stride, padding=pad))
 
 
+# ---- the conv kernels' own accumulation order (ttmi_conv.hip), order "kernel" -------------
+# MFMA chunks of 32 products (v_mfma_f32_16x16x32_bf16) are modelled as one exact dot product
+# rounded into the fp32 accumulator (acc = fl32(acc + Σ32)); the chunks are added in the
+# kernels' k order:
+#   FWD    k = (tap, channel), 64-wide k-steps of 2 chunks (conv_dma_kernel; the space-to-depth
+#          stem: k = (4x4 tap (a, b), s2d channel (ph·2 + pw)·Cin + ci padded to Cp), i.e. the
+#          7x7 tap (2a + ph − 1, 2b + pw − 1));
+#   DGRAD  each input pixel sums its stride-lattice taps in (kh, kw) order, 32 output channels a
+#          chunk (one tap per 64-channel k-step);
+#   WGRAD  the output pixels (n, ho, wo) are split in k_split ranges (conv_plan: per = max(min(8,
+#          ksteps), ceil(ksteps / ceil(1024 / tiles))) 64-pixel k-steps), each range summed 32
+#          pixels a chunk, the splits then summed in order in chunks of 16 (wgrad_reduce_kernel).
+_KCHUNK = 32
+
+
+def _stem_cols(Cin):
+    """Column of the 7x7 unfold (ci·49 + kh·7 + kw) for each k of the s2d stem's K, -1 = zero."""
+    cp = 8 if Cin == 1 else 16
+    cols = []
+    for a in range(4):
+        for b in range(4):
+            for sc in range(cp):
+                q, ci = divmod(sc, Cin)
+                kh, kw = 2 * a + (q >> 1) - 1, 2 * b + (q & 1) - 1
+                ok = sc < 4 * Cin and 0 <= kh < 7 and 0 <= kw < 7
+                cols.append(ci * 49 + kh * 7 + kw if ok else -1)
+    return torch.tensor(cols)
+
+
+def _kernel_cols(x, KH, KW, stride, pad, stem):
+    """im2col in the FWD kernel's k order: [N, K, L] float64 (zero columns where the kernel's
+    K has padding)."""
+    N, C = x.shape[:2]
+    u = TF.unfold(x.double(), (KH, KW), padding=pad, stride=stride)       # [N, C·T, L], c-major
+    T = KH * KW
+    if stem:
+        idx = _stem_cols(C)
+        u = torch.cat([u, torch.zeros_like(u[:, :1])], 1)
+        return u[:, torch.where(idx < 0, torch.full_like(idx, C * T), idx)]
+    return u.view(N, C, T, -1).transpose(1, 2).reshape(N, T * C, -1)
+
+
+def _kernel_w(w, stem):
+    Co, C, KH, KW = w.shape
+    if stem:
+        idx = _stem_cols(C)
+        wf = torch.cat([w.double().reshape(Co, -1), torch.zeros(Co, 1, dtype=torch.float64)], 1)
+        return wf[:, torch.where(idx < 0, torch.full_like(idx, C * KH * KW), idx)]
+    return w.double().permute(0, 2, 3, 1).reshape(Co, KH * KW * C)
+
+
+class _KConv(torch.autograd.Function):
+    """conv2d (no bias) with the FWD / DGRAD / WGRAD accumulation orders of ttmi_conv.hip."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, stem):
+        N, C, H, W = x.shape
+        Co, _, KH, KW = w.shape
+        Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+        cols = _kernel_cols(x, KH, KW, stride, pad, stem)                  # [N, K, L]
+        wk = _kernel_w(w, stem)                                              # [Co, K]
+        acc = torch.zeros(N, Co, Ho * Wo)
+        for k0 in range(0, wk.shape[1], _KCHUNK):
+            acc += torch.einsum("ok,nkl->nol", wk[:, k0:k0 + _KCHUNK], cols[:, k0:k0 + _KCHUNK]).float()
+        ctx.save_for_backward(x, w)
+        ctx.geo = (stride, pad, stem)
+        return acc.view(N, Co, Ho, Wo)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        stride, pad, stem = ctx.geo
+        N, C, H, W = x.shape
+        Co, _, KH, KW = w.shape
+        Ho, Wo = gy.shape[2:]
+        gd = gy.double()
+        dx = None
+        if ctx.needs_input_grad[0] and not stem:     # DGRAD (the stem's input grad is never needed)
+            s = stride
+            buf = torch.zeros(N, C, H + 2 * pad + s * KH, W + 2 * pad + s * KW)
+            for kh in range(KH):
+                for kw in range(KW):
+                    sl = buf[:, :, kh:kh + s * Ho:s, kw:kw + s * Wo:s]
+                    for c0 in range(0, Co, _KCHUNK):
+                        sl += torch.einsum("nohw,oc->nchw", gd[:, c0:c0 + _KCHUNK],
+                                           w[c0:c0 + _KCHUNK, :, kh, kw].double()).float()
+            dx = buf[:, :, pad:pad + H, pad:pad + W].contiguous()
+        # WGRAD: pixels m = (n, ho, wo); splits as conv_plan; 32-pixel chunks; split order
+        cols = _kernel_cols(x, KH, KW, stride, pad, stem)                   # [N, K, L]
+        K = cols.shape[1]
+        cm = cols.permute(0, 2, 1).reshape(N * Ho * Wo, K)                  # [M, K]
+        dm = gd.permute(0, 2, 3, 1).reshape(N * Ho * Wo, Co)                 # [M, Co]
+        M = cm.shape[0]
+        bm = 128 if Co % 128 == 0 else 64
+        tiles = -(-Co // bm) * -(-K // 128)
+        ksteps = -(-M // 64)
+        want = max(1, -(-1024 // tiles))
+        per = max(min(8, ksteps), -(-ksteps // want))
+        ksplit = per * 64
+        parts = []
+        for s0 in range(0, M, ksplit):
+            acc = torch.zeros(Co, K)
+            for p0 in range(s0, min(M, s0 + ksplit), _KCHUNK):
+                acc += (dm[p0:p0 + _KCHUNK].t() @ cm[p0:p0 + _KCHUNK]).float()
+            parts.append(acc)
+        if len(parts) > 16:                       # chunk totals in place, then the chunk slabs
+            parts = [_seq_sum(parts[i:i + 16]) for i in range(0, len(parts), 16)]
+        dwk = _seq_sum(parts)
+        if stem:
+            idx = _stem_cols(C)
+            dw = torch.zeros(Co, C * KH * KW)
+            dw[:, idx[idx >= 0]] = dwk[:, idx >= 0]
+            dw = dw.view(Co, C, KH, KW)
+        else:
+            dw = dwk.view(Co, KH, KW, C).permute(0, 3, 1, 2).contiguous()
+        return dx, dw, None, None, None
+
+
+def _seq_sum(ts):
+    s = torch.zeros_like(ts[0])
+    for t in ts:
+        s += t
+    return s
+
+
 _ORDER = ["torch"]
 
 
-def _emu_conv_bn(p, x, wname, bn, stride, pad, residual=None, relu=True):
+def _emu_conv_bn(p, x, wname, bn, stride, pad, residual=None, relu=True, stem=False):
     """conv (bf16 operands, fp32 accumulate in the order _ORDER[0]) -> BN as the kernels
     compute it (_BnKernel) -> residual -> ReLU -> bf16."""
     w = p[wname]
-    y32 = _conv_order(x, w.detach().to(torch.bfloat16).float() + (w - w.detach()), stride, pad, _ORDER[0])
+    wq = w.detach().to(torch.bfloat16).float() + (w - w.detach())
+    if _ORDER[0] == "kernel":
+        y32 = _KConv.apply(x, wq, stride, pad, stem)
+    else:
+        y32 = _conv_order(x, wq, stride, pad, _ORDER[0])
     out = _BnKernel.apply(y32, p[bn + ".weight"], p[bn + ".bias"])
     if residual is not None:
         out = out + residual
@@ -148,7 +277,7 @@ def resnet18_bf16_emulation(p, x, prefix="", update_running=False, order="torch"
 def _resnet18_bf16_emulation(p, x, prefix=""):
     if prefix:
         p = {k[len(prefix):]: v for k, v in p.items() if k.startswith(prefix)}
-    y = _emu_conv_bn(p, rb(x), "conv1.weight", "bn1", 2, 3)
+    y = _emu_conv_bn(p, rb(x), "conv1.weight", "bn1", 2, 3, stem=x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
     y = rb(TF.max_pool2d(y, 3, 2, 1))
     for lname, cin, cout, s in rref.LAYERS:
         for bi in range(2):
@@ -183,11 +312,14 @@ def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W, N):
     0.98 at layer4 and 1.0 at fc — the train-mode BN backward over 20 layers amplifies bf16
     storage noise.  Which bf16 roundings happen depends on the fp32 accumulation order of the
     convolutions, and at N = 4 that alone moves a BatchNorm parameter's cosine by up to 0.024
-    (1x128x256) / 0.036 (3x224²) between the EMU_ORDERS (tools/diag_resnet_margin.py).  So per
-    parameter the GPU gradient must be as close to fp32 as the WORST of those equally valid
-    accumulation orders, within 0.03 (every parameter, every size), with a norm deviation
-    within 2x the largest of theirs + 10 %; the output must agree to 5e-2 (fp32) / 2e-2
-    (emulation, torch order)."""
+    (1x128x256) / 0.036 (3x224²) between the EMU_ORDERS (tools/diag_resnet_margin.py).  The
+    conv kernels' own order (_KConv: their k-step / MFMA-chunk / split-K sums) is one of them,
+    and it does not narrow the band: at 3x224² its BatchNorm-parameter cosines fall anywhere
+    inside the other orders' range (the MFMA's internal summation order, which no emulation
+    here knows, already moves individual bf16 roundings).  So per parameter the GPU gradient
+    must be as close to fp32 as the worst of those orders within 0.03 in cosine, with a norm
+    ratio within 0.05 of the farthest (every parameter, every size); the output must agree to
+    5e-2 (fp32) / 2e-2 (the kernel-order emulation)."""
     cnn = gpu_pkg.cnn
     torch.manual_seed(in_ch)
     net = cnn.ResNet18(in_ch, 128).to(DEV)
@@ -224,7 +356,8 @@ def test_resnet18_vs_oracle(gpu_pkg, in_ch, H, W, N):
         ne = [Pe[name].grad.norm().item() / gr.norm().item() for _, Pe in emus]
         print("GRAD", name, f"gpu~fp32 {cr:.4f} emu~fp32 min {min(ce):.4f} max {max(ce):.4f} "
               f"norm gpu {nr:.4f} emu {min(ne):.4f}..{max(ne):.4f}")
-        if not (cr > min(ce) - 0.03 and abs(nr - 1) < 2 * max(abs(v - 1) for v in ne) + 0.1):
+        print("GRAD", name, f"kernel-order emu~fp32 {ce[0]:.4f} norm {ne[0]:.4f}")
+        if not (cr > min(ce) - 0.03 and abs(nr - 1) < max(abs(v - 1) for v in ne) + 0.05):
             bad.append((name, cr, min(ce), nr, ne))
     assert not bad, bad
     sd = net.state_dict()
@@ -348,9 +481,10 @@ def _cfg3(pkg, B=8, L=12, V=211, T=32, mel=(64, 96), cover=(64, 64), seed=0, p=0
 @pytest.mark.parametrize("B,mel,cover", [(8, (64, 96), (64, 64)), (4, (128, 256), (224, 224))])
 def test_cfg3_two_tower_vs_oracle(gpu_pkg, B, mel, cover):
     """cfg 3 (raw mels / covers / tabular, zero text slot): loss and logits vs the fp32
-    oracle, item-tower gradients by direction and norm against the same emulation yardstick
-    (cosine within 0.05 of the emulation's; every reduction is fixed-order or int64 fixed point,
-    so the GPU value is the same on every run).  bf16 storage through two ResNet-18s moves the
+    oracle, item-tower gradients by direction and norm against the same emulation yardstick in
+    three accumulation orders, the conv kernels' own among them (cosine within 0.03 of the
+    worst, norm ratio within 0.05 of the farthest; every reduction is fixed-order or int64 fixed
+    point, so the GPU value is the same on every run).  bf16 storage through two ResNet-18s moves the
     item embedding ~2 %, which τ = 0.07 amplifies in the logits; the loss bound is 2x the
     deviation of the bf16-emulating oracle (same rounding points as the kernels) + 2e-2: the
     summation order alone moves the full-size loss by that much (tools/diag_cfg3_loss.py: the
@@ -363,14 +497,18 @@ def test_cfg3_two_tower_vs_oracle(gpu_pkg, B, mel, cover):
     lref, logits_ref, _, _ = ref.two_tower_loss(params, batch, running=None)
     lref.backward()
     orig = rref.resnet18_forward
-    rref.resnet18_forward = resnet18_bf16_emulation       # bf16-storage yardstick
-    try:
-        pe = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
-        le, logits_emu = ref.two_tower_loss(pe, batch, running=None)[:2]
-        le.backward()
-        lemu = float(le)
-    finally:
-        rref.resnet18_forward = orig
+    emus = []
+    for order in ("kernel", "torch", "f64"):     # bf16-storage yardsticks (see test_resnet18_vs_oracle)
+        rref.resnet18_forward = lambda p, x, prefix="", update_running=False, o=order: \
+            resnet18_bf16_emulation(p, x, prefix, order=o)
+        try:
+            pe = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
+            le, le_logits = ref.two_tower_loss(pe, batch, running=None)[:2]
+            le.backward()
+            emus.append((pe, float(le), le_logits))
+        finally:
+            rref.resnet18_forward = orig
+    pe, lemu, logits_emu = emus[0]
     bd = {k: v.to(DEV) for k, v in batch.items()}
     loss, logits, _, _ = m(bd)
     loss.backward()
@@ -391,13 +529,17 @@ def test_cfg3_two_tower_vs_oracle(gpu_pkg, B, mel, cover):
                 1.0, params[k].grad.abs().max().item()), k
     names = [k for k in mine if k.startswith("item_tower.") and not k.endswith(zero)]
     assert any("audio_encoder" in k for k in names) and any("visual_encoder" in k for k in names)
-    for k in names:       # as close to fp32 as the bf16-storage emulation gets (see above)
-        g, gr, ge = mine[k].grad, params[k].grad, pe[k].grad
-        cos, cos_e = _cos(g, gr), _cos(ge, gr)
+    bad = []
+    for k in names:       # as close to fp32 as the bf16 emulations get (see above)
+        g, gr = mine[k].grad, params[k].grad
+        cos = _cos(g, gr)
         nr = g.norm().item() / gr.norm().item()
-        ne = ge.norm().item() / gr.norm().item()
-        assert cos > cos_e - 0.05, (k, cos, cos_e)
-        assert abs(nr - 1) < 2 * abs(ne - 1) + 0.15, (k, nr, ne)
+        cos_e = min(_cos(e[0][k].grad, gr) for e in emus)
+        ne = max(abs(e[0][k].grad.norm().item() / gr.norm().item() - 1) for e in emus)
+        print("GRAD", k, f"gpu~fp32 {cos:.4f} emu~fp32 min {cos_e:.4f} norm gpu {nr:.4f} emu dev {ne:.4f}")
+        if not (cos > cos_e - 0.03 and abs(nr - 1) < ne + 0.05):
+            bad.append((k, cos, cos_e, nr, ne))
+    assert not bad, bad
 
 
 def test_cfg3_train_step_graph_equals_eager_bitexact_and_learns(gpu_pkg):
