@@ -241,6 +241,17 @@ int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
 int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                  const int64_t* key_valid, const float* lse, const void* dctx, float drop_p,
                  const uint64_t* drop_seed, void* dqkv, hipStream_t stream);
+/* The encoder layer's input projection and attention in one launch (ABI 21; reference
+ * user_tower.py:111-116, nn.MultiheadAttention in_proj then SDPA): qkv = a·w_inᵀ + b_in
+ * (a [B*L, 128] bf16 normed rows, w_in [384, 128] bf16, b_in [384] fp32), written to qkv as
+ * ttmi_linear's panel kernel would (bit-identical to ttmi_linear from M = 2048 rows, where
+ * that kernel serves it), then ctx / lse exactly as ttmi_mha_fwd on that qkv.  Served shapes: ttmi_qkv_attn_supported() (bf16, H*Dh = 128, Dh = 32,
+ * L <= 64); anything else is TTMI_ERR_ARG. */
+int ttmi_qkv_attn_supported(int dtype, int L, int H, int Dh);
+int ttmi_qkv_attn_fwd(int dtype, int B, int L, int H, int Dh, const void* a, const void* w_in,
+                      const float* b_in, const int64_t* key_valid, float drop_p,
+                      const uint64_t* drop_seed, void* qkv, void* ctx, float* lse,
+                      hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Last-valid gather + demographics concat (user_tower.py:118-139):

@@ -407,6 +407,96 @@ struct HeadStage {
   }
 };
 
+// One wave's share of one (sequence, head): query tile i (rows 16i..16i+15) against the
+// causal keys of the [64][DH] Q, K, V images at sQ / sK / sV (row pitch P bytes; rows >= L
+// finite — they are masked keys / unstored queries).  kvm: the sequence's key-validity bits.
+// ctx points at the sequence's first row of this head (row stride D), lse at the head's
+// first query.  Shared by mha2_fwd_kernel and the fused projection + attention kernel.
+template <int DH, int P>
+TTMI_DEV void attn_tile_fwd(const char* sQ, const char* sK, const char* sV, uint64_t kvm, int i,
+                            int L, int lane, const DropKeys& dk, uint32_t pbase, float scale,
+                            bf16_t* ctx, int D, float* lse) {
+  if (16 * i >= L) return;
+  // The per-score work is VALU-issue bound (the softmax, the mask and the dropout hash over 16
+  // scores a lane): key tiles above the diagonal (t > i, wave-uniform) are skipped outright, the
+  // mask is one bit test per score, the scale rides in the exp2 argument and the dropout scale
+  // in the row's 1/sum.
+  const int li = lane & 15, lg = lane >> 4;
+  const int q = 16 * i + li;
+  // keys this query may attend: valid, causal (k <= q), and none for padded query rows
+  const uint64_t causal = q >= 63 ? ~0ull : ((2ull << q) - 1ull);
+  const uint64_t allow = q < L ? (kvm & causal) : 0ull;
+  constexpr int NC = DH / 32;                      // 32-wide k chunks of the head dim
+  uint4 qf[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) qf[c] = a_fk<P>(sQ, 16 * i, c, lane);
+  f32x4_t s[4];
+  float m = -INFINITY;                             // row max of the raw scores
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (t > i) continue;                           // wave-uniform
+#pragma unroll
+    for (int c = 0; c < NC; ++c) Mma<bf16_t>::run(s[t], a_fk<P>(sK, 16 * t, c, lane), qf[c]);
+    const uint32_t nib = (uint32_t)(allow >> (16 * t + 4 * lg));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s[t][e] = (nib >> e) & 1u ? s[t][e] : -INFINITY;
+      m = fmaxf(m, s[t][e]);
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  const float sl2 = scale * 1.4426950408889634f;   // exp(scale (s - m)) = exp2(sl2 (s - m))
+  const float mo = m == -INFINITY ? 0.f : m;       // fully masked row: every exp2(-inf) = 0
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t > i) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float p = __builtin_amdgcn_exp2f((s[t][e] - mo) * sl2);   // v_exp_f32 (no range fix-up)
+      s[t][e] = p;
+      sum += p;
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = sum > 0.f ? (dk.on ? dk.scale : 1.f) / sum : 0.f;
+  if (dk.on) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t > i) continue;
+      // (the pair hash when L is even; identical to drop_keep per index)
+      bool kp[4];
+      drop_keep4(dk, pbase + (uint32_t)(q * L + 16 * t + 4 * lg), kp);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[t][e] = kp[e] ? s[t][e] * inv : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[t][e] *= inv;
+  }
+  f32x4_t o[DH / 16];
+#pragma unroll
+  for (int u = 0; u < DH / 16; ++u) o[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {                  // 32-key chunks
+    if (32 * c > 16 * i + 15) break;
+    const uint4 pf = a_freg(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+    for (int u = 0; u < DH / 16; ++u) Mma<bf16_t>::run(o[u], a_ft<P>(sV, 16 * u, c, lane), pf);
+  }
+  if (q < L) {
+    bf16_t* dst = ctx + (int64_t)q * D + 4 * lg;
+#pragma unroll
+    for (int u = 0; u < DH / 16; ++u) a_st4(dst + 16 * u, o[u]);
+    if (lg == 0) lse[q] = m == -INFINITY ? INFINITY : m * scale + __logf(sum);
+  }
+}
+
 template <int DH>
 __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
                                                       const int64_t* __restrict__ kvalid, DropParams dp,
@@ -417,7 +507,7 @@ __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_
   char* sQ = smem;
   char* sK = sQ + G::BYTES;
   char* sV = sK + G::BYTES;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // the H heads of one sequence read the same QKV rows: keep them on one XCD
   const int bh = xcd_contiguous(blockIdx.x, gridDim.x), b = bh / H, h = bh % H;
   const int D = H * DH;
@@ -440,82 +530,10 @@ __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_
     if (lane == 0) s_kv = bal;
   }
   __syncthreads();
-  const uint64_t kvm = s_kv;
-  bool kv[4][4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) kv[t][e] = (kvm >> (16 * t + 4 * lg + e)) & 1ull;
   const DropKeys dk = resolve_drop(dp);
-  const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
-  constexpr int NC = DH / 32;                      // 32-wide k chunks of the head dim
-#pragma unroll
-  for (int i = wave; i < 4; i += 4) {      // wave w owns query tile w
-    if (16 * i >= L) break;
-    const int q = 16 * i + li;
-    uint4 qf[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) qf[c] = a_fk<G::P>(sQ, 16 * i, c, lane);
-    f32x4_t s[4];
-    float m = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      if (t <= i) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) Mma<bf16_t>::run(s[t], a_fk<G::P>(sK, 16 * t, c, lane), qf[c]);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = 16 * t + 4 * lg + e;
-        const bool ok = t <= i && kv[t][e] && k <= q && q < L;
-        s[t][e] = ok ? s[t][e] * scale : -INFINITY;
-        m = fmaxf(m, s[t][e]);
-      }
-    }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float p = m == -INFINITY ? 0.f : __expf(s[t][e] - m);
-        s[t][e] = p;
-        sum += p;
-      }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = sum > 0.f ? 1.f / sum : 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      // masked scores are 0 already, so the mask applies without a range check (the pair
-      // hash when L is even; identical to drop_keep per index)
-      bool kp[4] = {true, true, true, true};
-      if (dk.on) drop_keep4(dk, pbase + (uint32_t)(q * L + 16 * t + 4 * lg), kp);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float p = s[t][e] * inv;
-        s[t][e] = kp[e] ? (dk.on ? p * dk.scale : p) : 0.f;
-      }
-    }
-    f32x4_t o[DH / 16];
-#pragma unroll
-    for (int u = 0; u < DH / 16; ++u) o[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {                  // 32-key chunks
-      if (32 * c > 16 * i + 15) break;
-      const uint4 pf = a_freg(s[2 * c], s[2 * c + 1]);
-#pragma unroll
-      for (int u = 0; u < DH / 16; ++u) Mma<bf16_t>::run(o[u], a_ft<G::P>(sV, 16 * u, c, lane), pf);
-    }
-    if (q < L) {
-      bf16_t* dst = ctx + ((int64_t)b * L + q) * D + (int64_t)h * DH + 4 * lg;
-#pragma unroll
-      for (int u = 0; u < DH / 16; ++u) a_st4(dst + 16 * u, o[u]);
-      if (lg == 0) lse[(int64_t)bh * L + q] = m == -INFINITY ? INFINITY : m + __logf(sum);
-    }
-  }
+  // wave w owns query tile w
+  attn_tile_fwd<DH, G::P>(sQ, sK, sV, s_kv, wave, L, lane, dk, (uint32_t)((int64_t)bh * L * L), scale,
+                          ctx + (int64_t)b * L * D + (int64_t)h * DH, D, lse + (int64_t)bh * L);
 }
 
 template <int DH>
@@ -558,12 +576,8 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
   }
   __syncthreads();
   const uint64_t kvm = s_kv;
-  bool kv[4][4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) kv[t][e] = (kvm >> (16 * t + 4 * lg + e)) & 1ull;
   const DropKeys dk = resolve_drop(dp);
+  const float dsc = dk.on ? dk.scale : 1.f;
   const uint32_t pbase = (uint32_t)((int64_t)bh * L * L);
   constexpr int NC = DH / 32;
   bf16_t* gq = dqkv + (int64_t)b * L * ld + (int64_t)h * DH;
@@ -576,33 +590,35 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
       qf[c] = a_fk<G::P>(sQ, 16 * i, c, lane);
       of[c] = a_fk<G::P>(sdO, 16 * i, c, lane);
     }
-    const float lr = q < L ? lr0 : INFINITY;      // (q = qrow: wave w owns query tile w)
+    // the recomputed P is VALU-issue bound like the forward's softmax (attn_tile_fwd): key
+    // tiles above the diagonal are skipped, the mask is a bit test, exp(s·scale - lse) one exp2
+    const uint64_t causal = q >= 63 ? ~0ull : ((2ull << q) - 1ull);
+    const uint64_t allow = q < L ? (kvm & causal) : 0ull;
+    const float sl2 = scale * 1.4426950408889634f, lr2 = lr0 * 1.4426950408889634f;
     f32x4_t s[4], dpv[4];
     uint32_t keep[4];                              // dropout keep bits, one hash pass
     float dsum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       s[t] = dpv[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      if (t <= i) {
+      keep[t] = 0xFu;
+      if (t > i) continue;                         // wave-uniform
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          Mma<bf16_t>::run(s[t], a_fk<G::P>(sK, 16 * t, c, lane), qf[c]);
-          Mma<bf16_t>::run(dpv[t], a_fk<G::P>(sV, 16 * t, c, lane), of[c]);
-        }
+      for (int c = 0; c < NC; ++c) {
+        Mma<bf16_t>::run(s[t], a_fk<G::P>(sK, 16 * t, c, lane), qf[c]);
+        Mma<bf16_t>::run(dpv[t], a_fk<G::P>(sV, 16 * t, c, lane), of[c]);
       }
-      bool kp[4] = {true, true, true, true};
-      if (dk.on) drop_keep4(dk, pbase + (uint32_t)(q * L + 16 * t + 4 * lg), kp);
-      keep[t] = (kp[0] ? 1u : 0u) | (kp[1] ? 2u : 0u) | (kp[2] ? 4u : 0u) | (kp[3] ? 8u : 0u);
+      if (dk.on) {
+        bool kp[4];
+        drop_keep4(dk, pbase + (uint32_t)(q * L + 16 * t + 4 * lg), kp);
+        keep[t] = (kp[0] ? 1u : 0u) | (kp[1] ? 2u : 0u) | (kp[2] ? 4u : 0u) | (kp[3] ? 8u : 0u);
+      }
+      const uint32_t nib = (uint32_t)(allow >> (16 * t + 4 * lg));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = 16 * t + 4 * lg + e;
-        const bool ok = t <= i && kv[t][e] && k <= q && q < L;
-        const float p = ok ? __expf(s[t][e] * scale - lr) : 0.f;
-        float dP = 0.f;
-        if (ok) {
-          dP = dpv[t][e];
-          if (dk.on) dP = kp[e] ? dP * dk.scale : 0.f;
-        }
+        const bool ok = (nib >> e) & 1u;
+        const float p = ok ? __builtin_amdgcn_exp2f(fmaf(s[t][e], sl2, -lr2)) : 0.f;
+        const float dP = ok && ((keep[t] >> e) & 1u) ? dpv[t][e] * dsc : 0.f;
         s[t][e] = p;
         dpv[t][e] = dP;
         dsum += p * dP;
@@ -614,11 +630,15 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       f32x4_t pd;
+      if (t > i) {                                 // zeros: the dK / dV pass reads these rows
+        ds[t] = pd = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float p = s[t][e];
-        ds[t][e] = p * (dpv[t][e] - dsum) * scale;
-        pd[e] = dk.on ? (((keep[t] >> e) & 1u) ? p * dk.scale : 0.f) : p;
+        for (int e = 0; e < 4; ++e) {
+          const float p = s[t][e];
+          ds[t][e] = p * (dpv[t][e] - dsum) * scale;
+          pd[e] = ((keep[t] >> e) & 1u) ? p * dsc : 0.f;
+        }
       }
       a_st4(sdS + q * G::SP + (16 * t + 4 * lg) * 2, ds[t]);
       a_st4(sPd + q * G::SP + (16 * t + 4 * lg) * 2, pd);
@@ -670,6 +690,196 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
   }
 }
 
+// ---------------------------------------------------------------- in_proj + attention (forward)
+// nn.MultiheadAttention's input projection and its SDPA core in one launch (reference
+// user_tower.py:111-116) for d_model 128, 4 heads of 32.  A workgroup owns whole sequences
+// (2 at L = 50: 100 rows, 7 row tiles of 16), so the attention reads Q, K, V straight from the
+// LDS images of the projection it has just computed — the separate attention launch, its
+// dispatch ramp and its qkv re-read are gone.  qkv still goes to HBM (the backward reads it),
+// copied out of the images with coalesced stores under the attention.
+//
+// Every operand arrives by LDS-DMA, all of it issued up front (the A rows, the bias, the three
+// 128-column groups of W_in: one memory round trip), so no compiler-counted load sits in the
+// vmcnt queue ahead of a manual wait.  LDS: W0 | W1 | W2 | A (later the Q image) | bias.  The
+// K image overlays W0 once group 0 is consumed, V overlays W1.  The projection's MFMA order,
+// bias add and bf16 rounding are the panel kernel's (ttmi_gemm.hip), the attention is
+// attn_tile_fwd: bit-identical to ttmi_linear (from M = 2048 rows, where the panel serves it)
+// + ttmi_mha_fwd.
+constexpr int QA_D = 128;                         // d_model (= in_proj K)
+constexpr int QA_P = 2 * QA_D + 16;               // row pitch (bytes) of every image (W, A, Q, K, V)
+constexpr int QA_CPR = QA_D / 8 + 1;              // 16-byte chunks per image row (incl. the pad)
+constexpr int QA_WBUF = 128 * QA_P;               // one W column group's image
+constexpr int QA_ROWS = 114;                      // Q / K / V image rows (the last key tile of the
+                                                  // last sequence reads up to row (spw-1)L + 63)
+constexpr int QA_IMG = QA_ROWS * QA_P;
+constexpr int QA_AI = (112 * QA_CPR + 63) / 64;   // A DMA wave-instructions (7 row tiles)
+constexpr int QA_BI = 2;                          // bias DMA wave-instructions (384 fp32)
+constexpr int QA_WI = 128 * QA_CPR / 64;          // one W group's DMA wave-instructions
+constexpr int QA_I0 = QA_AI + QA_BI + QA_WI;      // the first wait's instructions (A, bias, W0)
+constexpr int QA_NW = 16;                         // waves per workgroup
+constexpr int QA_MAXSEQ = 8;
+static_assert(QA_AI * 1024 <= QA_IMG, "A staging fits the Q image");
+static_assert((128 * QA_CPR) % 64 == 0, "whole W DMA instructions");
+
+struct QaArgs {
+  const bf16_t* a;          // [B*L, 128] normed input
+  const bf16_t* w;          // [384, 128] in_proj weight
+  const float* bias;        // [384]
+  const int64_t* kvalid;    // [B, L]
+  bf16_t* qkv;              // [B*L, 384]
+  bf16_t* ctx;              // [B*L, 128]
+  float* lse;               // [B*4*L]
+  DropParams dp;
+  float scale;
+  int B, L, spw;
+};
+
+// s_waitcnt vmcnt(N) for a wave-dependent N in {lo, hi}
+template <int HI, int LO>
+TTMI_DEV void qa_wait(bool hi) {
+  if (hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HI) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LO) : "memory");
+}
+
+__global__ __launch_bounds__(1024) void qkv_attn_fwd_kernel(QaArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * QA_WBUF + QA_IMG + QA_BI * 1024];
+  __shared__ uint64_t s_kv[QA_MAXSEQ];
+  char* const sq = smem + 3 * QA_WBUF;            // A staging, then the Q image
+  const float* const sbias = reinterpret_cast<const float*>(sq + QA_IMG);
+  TTMI_TSTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
+  const int L = g.L, b0 = blockIdx.x * g.spw, nseq = min(g.spw, g.B - b0), R = nseq * L;
+  const int64_t r0 = (int64_t)b0 * L;
+  const int ntiles = (R + 15) >> 4;               // <= 7 (host: spw * L <= 112)
+  const int64_t kvl = wave < nseq ? g.kvalid[r0 + (int64_t)wave * L + min(lane, L - 1)] : 0;
+  // ---- every DMA up front; wave w issues wave-instructions w, w + 16, ... of each batch
+  {
+    // (the row pad chunks read at each buffer's end: out of range, zeros)
+    const uint32_t abytes = (uint32_t)R * QA_D * 2, wbytes = 3 * QA_D * QA_D * 2;
+    const i32x4_t ra = make_rsrc(g.a + r0 * QA_D, abytes);          // rows >= R: zeros
+    const i32x4_t rb = make_rsrc(g.bias, 3 * QA_D * 4);
+    const i32x4_t rw = make_rsrc(g.w, wbytes);
+    const uint32_t lw = lds_addr(smem), la = lds_addr(sq), lb = lds_addr(sq + QA_IMG);
+#pragma unroll
+    for (int t = 0; t < (QA_I0 + QA_NW - 1) / QA_NW; ++t) {
+      const int ii = wave + QA_NW * t;            // wave-uniform branches
+      if (ii >= QA_I0) break;
+      if (ii < QA_AI) {
+        const int q = ii * 64 + lane, r = q / QA_CPR, c = q % QA_CPR;
+        dma16(ra, c == QA_CPR - 1 ? abytes : (uint32_t)((r * QA_D + 8 * c) * 2), la + ii * 1024);
+      } else if (ii < QA_AI + QA_BI) {
+        const int j = ii - QA_AI;
+        dma16(rb, (uint32_t)((j * 64 + lane) * 16), lb + j * 1024);
+      } else {
+        const int j = ii - QA_AI - QA_BI, q = j * 64 + lane, n = q / QA_CPR, c = q % QA_CPR;
+        dma16(rw, c == QA_CPR - 1 ? wbytes : (uint32_t)((n * QA_D + 8 * c) * 2), lw + j * 1024);
+      }
+    }
+#pragma unroll
+    for (int cg = 1; cg < 3; ++cg)
+#pragma unroll
+      for (int t = 0; t < (QA_WI + QA_NW - 1) / QA_NW; ++t) {
+        const int j = wave + QA_NW * t;
+        if (j >= QA_WI) break;
+        const int q = j * 64 + lane, n = q / QA_CPR, c = q % QA_CPR;
+        dma16(rw, c == QA_CPR - 1 ? wbytes : (uint32_t)(((cg * 128 + n) * QA_D + 8 * c) * 2),
+              lw + cg * QA_WBUF + j * 1024);
+      }
+  }
+  // per-wave DMA counts of the W1 and W2 batches: the waits below leave exactly those in flight
+  constexpr int C_HI = (QA_WI + QA_NW - 1) / QA_NW;             // waves below QA_WI % 16
+  static_assert(QA_WI % QA_NW != 0 && C_HI - 1 == QA_WI / QA_NW, "two per-wave counts");
+  const bool hi = wave < QA_WI % QA_NW;
+  // the Q image's rows past the A staging are read as masked keys: zero
+  for (int i = QA_AI * 64 + tid; i < QA_ROWS * QA_CPR; i += 64 * QA_NW)
+    *reinterpret_cast<uint4*>(sq + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
+  // ---- projection: 16 waves, wave w computes row tile w & 7, column half w >> 3 (4 of the 8
+  // column tiles of each group)
+  const int rt = wave & 7, half = wave >> 3;
+  const int wrow = 8 * (li >> 2) + (li & 3);      // column-paired W rows (panel layout)
+  const int row = 16 * rt + li;
+  const bool mine = rt < ntiles;
+  uint4 af[4];
+#pragma unroll 1
+  for (int cg = 0; cg < 3; ++cg) {
+    if (cg == 0) qa_wait<2 * C_HI, 2 * (C_HI - 1)>(hi);
+    else if (cg == 1) qa_wait<C_HI, C_HI - 1>(hi);
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                              // every wave's DMAs of this batch landed
+    if (cg == 0) {
+      TTMI_TSTAMP(1);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) af[c] = lds16(sq + row * QA_P + lg * 64 + 16 * c);
+    } else {
+      // group cg - 1's W image is consumed: it becomes the K (cg 1) / V (cg 2) image, whose
+      // rows past the last tile must read as zeros
+      char* img = smem + (cg - 1) * QA_WBUF;
+      for (int i = 16 * ntiles * QA_CPR + tid; i < QA_ROWS * QA_CPR; i += 64 * QA_NW)
+        *reinterpret_cast<uint4*>(img + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    f32x4_t acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (mine) {
+      const char* wb = smem + cg * QA_WBUF + (64 * half + wrow) * QA_P + lg * (QA_D / 2);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          Mma<bf16_t>::run(acc[t], lds16(wb + (32 * (t >> 1) + 4 * (t & 1)) * QA_P + 16 * c), af[c]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (cg == 0) __syncthreads();                 // every wave's A rows read: Q overwrites them
+    if (mine) {
+      char* lrow = (cg == 0 ? sq : smem + (cg - 1) * QA_WBUF) + row * QA_P;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int nl = 64 * half + 32 * p + 8 * lg;   // column within the group
+        const float* bp = sbias + cg * 128 + nl;
+        const float4 b_lo = *reinterpret_cast<const float4*>(bp);
+        const float4 b_hi = *reinterpret_cast<const float4*>(bp + 4);
+        const float v[8] = {acc[2 * p][0] + b_lo.x, acc[2 * p][1] + b_lo.y, acc[2 * p][2] + b_lo.z,
+                            acc[2 * p][3] + b_lo.w, acc[2 * p + 1][0] + b_hi.x, acc[2 * p + 1][1] + b_hi.y,
+                            acc[2 * p + 1][2] + b_hi.z, acc[2 * p + 1][3] + b_hi.w};
+        *reinterpret_cast<uint4*>(lrow + 2 * nl) =
+            make_uint4(a_pk2(v[0], v[1]), a_pk2(v[2], v[3]), a_pk2(v[4], v[5]), a_pk2(v[6], v[7]));
+      }
+    }
+  }
+  if (wave < nseq) {
+    const uint64_t bal = __ballot(lane < L && kvl != 0);
+    if (lane == 0) s_kv[wave] = bal;
+  }
+  __syncthreads();
+  TTMI_TSTAMP(2);
+  // ---- qkv to HBM from the images (coalesced 16-byte stores, in flight under the attention)
+  for (int i = tid; i < R * 48; i += 64 * QA_NW) {
+    const int r = i / 48, c = i % 48, m = c >> 4;  // m: Q (A region), K (W0), V (W1)
+    const char* src = (m == 0 ? sq : smem + (m - 1) * QA_WBUF) + r * QA_P + 16 * (c & 15);
+    *reinterpret_cast<uint4*>(g.qkv + (r0 + r) * (3 * QA_D) + 8 * c) = lds16(src);
+  }
+  // ---- attention: round s handles sequence s, wave w its head w >> 2, query tile w & 3
+  const DropKeys dk = resolve_drop(g.dp);
+  for (int s = 0; s < nseq; ++s) {
+    const int h = wave >> 2;
+    const int64_t bh = (int64_t)(b0 + s) * 4 + h;
+    const int off = s * L * QA_P + h * 64;
+    attn_tile_fwd<32, QA_P>(sq + off, smem + off, smem + QA_WBUF + off, s_kv[s], wave & 3, L, lane, dk,
+                            (uint32_t)(bh * L * L), g.scale, g.ctx + (r0 + (int64_t)s * L) * QA_D + h * 32,
+                            QA_D, g.lse + bh * L);
+  }
+  TTMI_TSTAMP(3);
+}
+
+// sequences per workgroup for the fused kernel: the most whose rows fit the 7 row tiles and
+// whose last key tile stays inside the image; 0 = shape not served
+int qa_spw(int L) {
+  if (L <= 0 || L > 64) return 0;
+  for (int s = QA_MAXSEQ; s >= 1; --s)
+    if (s * L <= 112 && (s - 1) * L + 64 <= QA_ROWS) return s;
+  return 0;
+}
 
 int check_mha(const char* fn, int dtype, int B, int L, int H, int Dh, const void* qkv,
               const int64_t* kv, float drop_p) {
@@ -717,6 +927,30 @@ extern "C" int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* 
   return ttmi_check_launch("ttmi_mha_fwd");
 }
 
+extern "C" int ttmi_qkv_attn_supported(int dtype, int L, int H, int Dh) {
+  return dtype == TTMI_BF16 && H * Dh == QA_D && Dh == 32 && qa_spw(L) > 0;
+}
+
+extern "C" int ttmi_qkv_attn_fwd(int dtype, int B, int L, int H, int Dh, const void* a, const void* w_in,
+                                 const float* b_in, const int64_t* key_valid, float drop_p,
+                                 const uint64_t* drop_seed, void* qkv, void* ctx, float* lse, hipStream_t s) {
+  static const char* fn = "ttmi_qkv_attn_fwd";
+  int rc = check_mha(fn, dtype, B, L, H, Dh, qkv, key_valid, drop_p);
+  if (rc) return rc;
+  TTMI_REQUIRE(ttmi_qkv_attn_supported(dtype, L, H, Dh),
+               "%s: serves bf16, H*Dh = 128 with Dh = 32, L <= 64 (got L=%d H=%d Dh=%d); use ttmi_linear + "
+               "ttmi_mha_fwd", fn, L, H, Dh);
+  TTMI_REQUIRE(a && w_in && b_in && ctx && lse, "%s: null argument", fn);
+  TTMI_REQUIRE((((uintptr_t)a | (uintptr_t)w_in | (uintptr_t)b_in | (uintptr_t)ctx) & 15) == 0,
+               "%s: a, w_in, b_in, ctx must be 16-byte aligned", fn);
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "%s: drop_p out of [0,1)", fn);
+  if (B == 0) return TTMI_OK;
+  QaArgs g{(const bf16_t*)a, (const bf16_t*)w_in, b_in, key_valid, (bf16_t*)qkv, (bf16_t*)ctx, lse,
+           make_drop(drop_p, drop_seed), 1.f / sqrtf((float)Dh), B, L, qa_spw(L)};
+  hipLaunchKernelGGL(qkv_attn_fwd_kernel, dim3((B + g.spw - 1) / g.spw), dim3(1024), 0, s, g);
+  return ttmi_check_launch(fn);
+}
+
 extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                             const int64_t* key_valid, const float* lse, const void* dctx,
                             float drop_p, const uint64_t* drop_seed, void* dqkv, hipStream_t s) {
@@ -747,3 +981,4 @@ extern "C" int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* 
   return ttmi_check_launch("ttmi_mha_bwd");
 }
 
+TTMI_STAMP_DUMP(attn)

@@ -26,7 +26,7 @@ int ttmi_check_launch(const char* what) {
 
 extern "C" const char* ttmi_last_error(void) { return g_err; }
 
-extern "C" int ttmi_abi_version(void) { return 20; }
+extern "C" int ttmi_abi_version(void) { return 21; }
 
 namespace {
 

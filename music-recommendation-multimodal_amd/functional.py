@@ -173,6 +173,18 @@ def _ln_fusable(W: Dict[str, Tensor], pre: str, D: int, M: int) -> bool:
 _HEAD_AC = os.environ.get("TTMI_HEAD_AC", "0") == "1"
 
 
+# the fused in_proj + attention launch (ttmi_qkv_attn_fwd); TTMI_NO_QA=1 restores the
+# ttmi_linear + ttmi_mha_fwd pair (A/B measurements)
+_QA = os.environ.get("TTMI_NO_QA", "0") != "1"
+
+
+def _qa_ok(w_in: Tensor, a1: Tensor, L: int, H: int) -> bool:
+    D = a1.shape[1]
+    return (_QA and a1.dtype == torch.bfloat16 and w_in.dtype == torch.bfloat16
+            and tuple(w_in.shape) == (3 * D, D) and w_in.is_contiguous() and a1.is_contiguous()
+            and ops.qkv_attn_supported(a1.dtype, L, H, D // H))
+
+
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
@@ -229,7 +241,10 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             a1, m1, r1 = ln_out(M)
             ops.layernorm_fwd(x, P[pre + "norm1.weight"], P[pre + "norm1.bias"], a1, m1, r1, eps=cfg.eps)
         qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
-        ops.linear(a1, W[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"], qkv)
+        w_in, b_in = W[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"]
+        fused_qa = not pruned and _qa_ok(w_in, a1, L, H)
+        if not fused_qa:
+            ops.linear(a1, w_in, b_in, qkv)
         F_ = W[pre + "linear1.weight"].shape[0]
         if pruned:
             rows = torch.empty(B, device=dev, dtype=torch.int32)
@@ -279,7 +294,11 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             rows, R, res_in, drows = None, M, x, None
             ctx = torch.empty(M, D, device=dev, dtype=dt)
             lse = torch.empty(B * H * L, **f32)
-            ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
+            if fused_qa:     # in_proj + attention, one launch (bit-identical to the pair at M >= 2048)
+                ops.qkv_attn_fwd(a1, w_in, b_in, key_valid, B, L, H, qkv, ctx, lse,
+                                 _drop(cfg, seeds, site_attn(i)))
+            else:
+                ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
         x1 = torch.empty(R, D, **f32)
         a2, m2, r2 = ln_out(R)
         name = pre + "self_attn.out_proj.weight"

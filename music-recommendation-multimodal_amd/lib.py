@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -224,6 +224,9 @@ SIGNATURES = {
                                  c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_p]),
     "ttmi_mha_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "ttmi_qkv_attn_supported": (c_i, [c_i, c_i, c_i, c_i]),
+    "ttmi_qkv_attn_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p,
+                                c_p]),
     "ttmi_user_concat_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_i, c_p,
                                    c_p, c_i, c_i, c_p, c_p]),
     "ttmi_user_concat_bwd": (c_i, [c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p, c_i, c_i,

@@ -771,6 +771,32 @@ def mha_fwd(qkv: Tensor, key_valid: Tensor, B: int, L: int, H: int, ctx: Tensor,
     return ctx
 
 
+_QA_OK: Dict[Tuple[int, int, int, int], bool] = {}
+
+
+def qkv_attn_supported(dtype: torch.dtype, L: int, H: int, Dh: int) -> bool:
+    """Whether ttmi_qkv_attn_fwd serves this shape (bf16, H·Dh = 128, Dh = 32, L <= 64)."""
+    if dtype not in _DT:
+        return False
+    key = (code(dtype), L, H, Dh)
+    if key not in _QA_OK:
+        _QA_OK[key] = bool(_L.load().ttmi_qkv_attn_supported(*key))
+    return _QA_OK[key]
+
+
+def qkv_attn_fwd(a: Tensor, w: Tensor, b: Tensor, key_valid: Tensor, B: int, L: int, H: int,
+                 qkv: Tensor, ctx: Tensor, lse: Tensor, drop: Drop = NO_DROP) -> Tensor:
+    """in_proj + attention in one launch: qkv = a·wᵀ + b (kept for the backward), then
+    ctx / lse as mha_fwd — bit-identical to linear() (from M = 2048 rows, its panel kernel)
+    + mha_fwd()."""
+    _dev(a, w, b, key_valid, qkv, ctx, lse)
+    Dh = w.shape[0] // (3 * H)
+    _q1_batch_check("qkv_attn_fwd", B, L, H, drop)
+    call("ttmi_qkv_attn_fwd", code(a.dtype), B, L, H, Dh, _p(a), _p(w), _p(b), _p(key_valid),
+         float(drop[0]), _p(drop[1]), _p(qkv), _p(ctx), _p(lse), _s())
+    return ctx
+
+
 def mha_bwd(qkv: Tensor, key_valid: Tensor, lse: Tensor, dctx: Tensor, B: int, L: int, H: int,
             dqkv: Tensor, drop: Drop = NO_DROP):
     Dh = qkv.shape[1] // (3 * H)

@@ -1,0 +1,75 @@
+"""The fused in_proj + attention forward (ttmi_qkv_attn_fwd, reference user_tower.py:111-116)
+against the two launches it replaces — ttmi_linear then ttmi_mha_fwd, themselves parity-tested
+against the oracle in test_gpu_kernels.py.  The fused kernel shares the panel GEMM's MFMA order
+(ttmi_linear's kernel from M = 2048 rows) and the attention tile code, so qkv (there), ctx and
+lse must be bit-identical, on ragged batches (a last
+workgroup with fewer sequences), every sequences-per-workgroup packing, empty / left-padded /
+full key masks, with and without dropout."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _seed(val):
+    v = val - (1 << 64) if val >= (1 << 63) else val
+    return torch.tensor([v], dtype=torch.int64, device=DEV)
+
+
+def _masks(B, L, g):
+    lengths = torch.randint(1, L + 1, (B,), generator=g)
+    lengths[0] = L
+    lengths[1 % B] = 0
+    m = (torch.arange(L)[None] < lengths[:, None]).long()
+    if B > 2:
+        m[2] = m[2].flip(0)            # left-padded row
+    return m
+
+
+@pytest.mark.parametrize("B,L,p", [(512, 50, 0.1), (7, 50, 0.0), (3, 50, 0.1), (33, 64, 0.1),
+                                   (21, 20, 0.1), (5, 1, 0.0), (64, 37, 0.2), (9, 56, 0.0)])
+def test_qkv_attn_matches_linear_then_mha(gpu_pkg, B, L, p):
+    ops = gpu_pkg.ops
+    H, D = 4, 128
+    assert ops.qkv_attn_supported(torch.bfloat16, L, H, D // H)
+    g = torch.Generator().manual_seed(1000 * L + B)
+    a = torch.randn(B * L, D, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(3 * D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    kv = _masks(B, L, g).to(DEV)
+    drop = (p, _seed(0x0DDBA11CAFEF00D5 + L)) if p > 0 else (0.0, None)
+    qkv1 = torch.full((B * L, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ctx1 = torch.full((B * L, D), float("nan"), device=DEV, dtype=torch.bfloat16)
+    lse1 = torch.full((B * H * L,), float("nan"), device=DEV)
+    ops.qkv_attn_fwd(a, w, b, kv, B, L, H, qkv1, ctx1, lse1, drop)
+    # the projection: within bf16 rounding of the fp32 product; at M >= 2048, where ttmi_linear
+    # runs the panel kernel, bit-identical to it (same MFMA order, bias add, rounding)
+    ref = a.float() @ w.float().t() + b
+    err = (qkv1.float() - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -8 + 1e-5).all()), f"projection off by {err.max().item()}"
+    if B * L >= 2048:
+        qkv0 = torch.empty_like(qkv1)
+        ops.linear(a, w, b, qkv0)
+        assert torch.equal(qkv1.view(torch.int16), qkv0.view(torch.int16)), "projection differs"
+    # the attention on that projection: bit-identical to ttmi_mha_fwd
+    ctx0 = torch.empty_like(ctx1)
+    lse0 = torch.empty_like(lse1)
+    ops.mha_fwd(qkv1, kv, B, L, H, ctx0, lse0, drop)
+    torch.cuda.synchronize()
+    assert torch.equal(lse1, lse0), "lse differs"
+    assert torch.equal(ctx1.view(torch.int16), ctx0.view(torch.int16)), "context differs"
+
+
+def test_qkv_attn_refuses_unserved_shapes(gpu_pkg):
+    ops = gpu_pkg.ops
+    assert not ops.qkv_attn_supported(torch.bfloat16, 50, 4, 64)      # d_model 256
+    assert not ops.qkv_attn_supported(torch.bfloat16, 65, 4, 32)      # L > 64
+    assert not ops.qkv_attn_supported(torch.float32, 50, 4, 32)
+    a = torch.zeros(4 * 65, 128, device=DEV, dtype=torch.bfloat16)
+    w = torch.zeros(384, 128, device=DEV, dtype=torch.bfloat16)
+    b = torch.zeros(384, device=DEV)
+    kv = torch.ones(4, 65, device=DEV, dtype=torch.int64)
+    qkv = torch.empty(4 * 65, 384, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(Exception, match="ttmi_qkv_attn_fwd"):
+        ops.qkv_attn_fwd(a, w, b, kv, 4, 65, 4, qkv, torch.empty_like(a), torch.empty(4 * 4 * 65, device=DEV))

@@ -3,6 +3,7 @@ the fused user head, from the diagnostic build (tools/stamp_build.sh).  GPU diag
     TTMI_LIB=music-recommendation-multimodal_amd/lib/diag/libttmi_stamp.so python tools/stamp_phases.py
 Phases (panel_kernel): 0 start, 1 W DMA issued, 2 W in LDS (after the barrier), 3 first
 tile's first column group MFMAs done, 4 first tile done, 5 all tiles done, 6 end.
+Phases (qkv_attn_fwd): 0 start, 1 W group 0 in LDS, 2 projection done, 3 attention done.
 Phases (user_head_fwd): 0 start, 1 prologue, 2 out-proj + LN2, 3 FFN1, 4 FFN2, 5 fusion0 + LN,
 6 end."""
 import ctypes
@@ -19,7 +20,7 @@ pkg.lib.load(os.environ["TTMI_LIB"])
 ops = pkg.ops
 NB, NW, NP = 512, 16, 8
 lib = pkg.lib._lib
-for tu in ("gemm", "head", "infonce"):
+for tu in ("gemm", "head", "infonce", "attn"):
     getattr(lib, "ttmi_dbg_stamps_" + tu).argtypes = [ctypes.c_void_p, ctypes.c_int64]
 buf = (ctypes.c_uint64 * (NB * NW * NP))()
 
@@ -59,6 +60,13 @@ def main():
     w_in, b_in = bf(3 * D, D), f32(3 * D, sc=0.1)
     qkv = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
     stamps(lambda: ops.linear(a1, w_in, b_in, qkv), "qkv fwd 384x128")
+    # the fused in_proj + attention (phases: 0 start, 1 W group 0 in LDS, 2 projection done,
+    # 3 attention done)
+    kvm = (torch.arange(50)[None] < torch.randint(1, 51, (512, 1), generator=g)).long().to(dev)
+    ctxq = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    lseq = torch.empty(512 * 4 * 50, device=dev)
+    stamps(lambda: ops.qkv_attn_fwd(a1, w_in, b_in, kvm, 512, 50, 4, qkv, ctxq, lseq, drop),
+           "qkv + attention fwd", nph=4, tu="attn")
     wo, bo = bf(D, D), f32(D, sc=0.1)
     x, x1 = f32(M, D), torch.empty(M, D, device=dev)
     lnw, lnb = 1 + f32(D, sc=0.1), f32(D, sc=0.1)
