@@ -803,8 +803,14 @@ typedef struct ttmi_user_head_desc {
   float* u_hat; float* u_norm;       /* ABI 15, optional (NULL): F.normalize(u) and ||u|| */
   int n_genders, n_countries;        /* ABI 20: rows of G / C; an id outside its table reads the */
   int32_t* id_err;                   /* clamped row and sets id_err[TTMI_IDERR_GENDER / _COUNTRY] */
+  void* ffn_ws;                      /* ABI 21, optional: ttmi_user_head_ffn_ws_bytes(B, F) bytes, */
+                                     /* zero before first use (every launch leaves it reusable): */
+                                     /* the FFN runs split over its hidden units, F / 128 */
+                                     /* workgroups per 16-row block, whose last arriver sums the */
+                                     /* partials in split order and runs the fusion MLP */
 } ttmi_user_head_desc;
 int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t stream);
+int64_t ttmi_user_head_ffn_ws_bytes(int B, int F);
 /* Its backward, one launch (ABI 12), from du (bf16 [B, D]) and the forward's saved values:
  *   daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0]); dcomb = dz·Wf0 (dG[gender] / dC[country] +=);
  *   dy2 = drop2ᵀ(dcomb[:, :D]); dz1 = (dy2·W2) ⊙ [h > 0]·ffn_scale;

@@ -859,13 +859,15 @@ __global__ __launch_bounds__(1024) void qkv_attn_fwd_kernel(QaArgs g) {
     const char* src = (m == 0 ? sq : smem + (m - 1) * QA_WBUF) + r * QA_P + 16 * (c & 15);
     *reinterpret_cast<uint4*>(g.qkv + (r0 + r) * (3 * QA_D) + 8 * c) = lds16(src);
   }
-  // ---- attention: round s handles sequence s, wave w its head w >> 2, query tile w & 3
+  // ---- attention: round s handles sequence s, wave w its head w >> 2 and query tile w & 3 on
+  // even rounds, 3 - (w & 3) on odd ones (tile i costs i + 1 key tiles: pairing i with 3 - i
+  // evens the waves' work, the workgroup ends with its slowest wave)
   const DropKeys dk = resolve_drop(g.dp);
   for (int s = 0; s < nseq; ++s) {
-    const int h = wave >> 2;
+    const int h = wave >> 2, qt = (s & 1) ? 3 - (wave & 3) : (wave & 3);
     const int64_t bh = (int64_t)(b0 + s) * 4 + h;
     const int off = s * L * QA_P + h * 64;
-    attn_tile_fwd<32, QA_P>(sq + off, smem + off, smem + QA_WBUF + off, s_kv[s], wave & 3, L, lane, dk,
+    attn_tile_fwd<32, QA_P>(sq + off, smem + off, smem + QA_WBUF + off, s_kv[s], qt, L, lane, dk,
                             (uint32_t)(bh * L * L), g.scale, g.ctx + (r0 + (int64_t)s * L) * QA_D + h * 32,
                             QA_D, g.lse + bh * L);
   }

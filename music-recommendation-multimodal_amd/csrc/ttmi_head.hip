@@ -13,6 +13,8 @@
 // (drop_rows[m]·N + n).
 #include "ttmi_q1.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int HR = 16;                 // rows per workgroup (one MFMA row tile)
@@ -80,6 +82,7 @@ struct HeadArgs {
   int it_stage;                // 0: item stage A (it_nblk x 8 workgroups), 2: item stage C (it_nblk),
                                // 3: both, A's then C's (C waits for A's statistics in-launch)
   int ng, nc; int32_t* id_err; // table rows of G / C; ids outside are clamped and flagged (ABI 20)
+  float* ffn_part; int* ffn_cnt;   // ABI 21: the FFN split's exchange slots and arrival counts
 };
 
 struct HeadLds {
@@ -704,6 +707,238 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
   STAMP(6);
 }
 
+// ---- the FFN split over its hidden units (ABI 21, ttmi_user_head_desc::ffn_ws)
+// The kernel above runs 32 row blocks: 7 of 8 CUs idle, and each workgroup streams all 368 KB
+// of the head's weights through its one CU (~36 GB/s a CU: that stream is the kernel's time).
+// Here row block rb runs on NS = F / 128 workgroups j.  Each computes out-proj + LN2 for the
+// block's rows (the 32 KB out-proj weights, redundantly), the hidden units [128 j, 128 j + 128)
+// of FFN1 and their partial FFN2 product (32 + 32 KB), and hands the fp32 partial [16 x 128]
+// over through write-through stores and an agent-scope arrival count (the item head's handoff
+// pattern above).  The last of the NS to arrive sums the partials in split order — the same
+// bits whichever arrives last — then runs the residual, the concat and the fusion MLP (80 KB).
+// Weight bytes through a CU: 96 KB (176 KB for the last arriver) instead of 368.
+template <int F>
+__global__ __launch_bounds__(256) void user_head_fwd_split_kernel(HeadArgs a) {
+  constexpr int NS = F / 128;
+  STAMP(0);
+  __shared__ __attribute__((aligned(16))) HeadLds L;
+  __shared__ __attribute__((aligned(16))) HeadParams Q;
+  __shared__ int s_last;
+  const int nsplit = a.nbu * NS;
+  int ub = (int)blockIdx.x;
+  if (a.it_stage == 3) {
+    const int na = a.it_nblk * (IN1 / 64);
+    if (ub < na) {
+      item_a_body(a.it, ub % a.it_nblk, ub / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+      return;
+    }
+    ub -= na;
+    if (ub >= nsplit) {
+      item_c_body<true>(a.it, ub - nsplit, *reinterpret_cast<ItemLdsC*>(&L));
+      return;
+    }
+  } else if (ub >= nsplit) {                         // co-launched item head stage A or C
+    const int l = ub - nsplit;
+    if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+    else item_c_body<false>(a.it, l, *reinterpret_cast<ItemLdsC*>(&L));
+    return;
+  }
+  const int rb = ub / NS, j = ub % NS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = rb * HR, m = r0 + li;
+  const bool mrow = m < a.B;
+  const bool lead = j == 0;                          // writes what every split computes alike
+  const int W = HD + a.dg + a.dc;
+  const int n0 = w * 32;                             // this wave's 32 of the 128 columns
+  const int nh = 128 * j + 32 * w;                   // ... and its 32 of the split's hidden units
+  WFrags<2, HD> wo;
+  wo.load(a.wo, HD, n0, lane, HD);
+  {                                                  // ctx: 16 rows x 16 chunks of 16 bytes
+    const int r = tid >> 4, ch = tid & 15;
+    *reinterpret_cast<uint4*>(L.sA + r * PD + ch * 16) =
+        *reinterpret_cast<const uint4*>(a.ctx + (int64_t)min(r0 + r, a.B - 1) * HD + ch * 8);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {                     // residual: 16 rows x 32 float4
+      const int idx = tid + 256 * q;
+      *reinterpret_cast<float4*>(&L.sX1[idx >> 5][(idx & 31) * 4]) =
+          *reinterpret_cast<const float4*>(a.res + (int64_t)min(r0 + (idx >> 5), a.B - 1) * HD + (idx & 31) * 4);
+    }
+  }
+  {
+    const float4 p0 = vec_ld<HD>(a.bo, tid), p1 = vec_ld<HD>(a.n2w, tid), p2 = vec_ld<HD>(a.n2b, tid);
+    const float4 p3 = vec_ld<F>(a.b1, tid), p4 = vec_ld<HD>(a.b2, tid), p5 = vec_ld<HD>(a.bf0, tid);
+    const float4 p6 = vec_ld<HD>(a.lnw, tid), p7 = vec_ld<HD>(a.lnb, tid), p8 = vec_ld<HD>(a.bf3, tid);
+    vec_st<HD>(Q.bo, p0, tid); vec_st<HD>(Q.n2w, p1, tid); vec_st<HD>(Q.n2b, p2, tid);
+    vec_st<F>(Q.b1, p3, tid); vec_st<HD>(Q.b2, p4, tid); vec_st<HD>(Q.bf0, p5, tid);
+    vec_st<HD>(Q.lnw, p6, tid); vec_st<HD>(Q.lnb, p7, tid); vec_st<HD>(Q.bf3, p8, tid);
+  }
+  {   // demographics (as user_head_fwd_kernel); the lead writes comb's trailing columns
+    const int r = tid >> 4, k0 = HD + 4 * (tid & 15), rr = min(r0 + r, a.B - 1);
+    const int64_t gi = clamp_id(a.gender[rr], a.ng, a.id_err, TTMI_IDERR_GENDER);
+    const int64_t ci = clamp_id(a.country[rr], a.nc, a.id_err, TTMI_IDERR_COUNTRY);
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kk = k0 + e;
+      float gv = a.G[gi * a.dg + min(kk - HD, a.dg - 1)];
+      float cv = a.C[ci * a.dc + min(max(kk - HD - a.dg, 0), a.dc - 1)];
+      asm volatile("" : "+v"(gv), "+v"(cv));
+      v[e] = kk < HD + a.dg ? gv : (kk < W ? cv : 0.f);
+    }
+    st4_bf(L.sC + r * PW + k0 * 2, v);
+    if (lead && k0 < W && r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.comb + (int64_t)(r0 + r) * W + k0), v);
+  }
+  if (lead && tid < HR && r0 + tid < a.B) a.rows[r0 + tid] = r0 + tid;
+  const int drow = a.drows[min(m, a.B - 1)];
+  const uint64_t s1 = *a.d1.seed, sf = *a.dff.seed, s2 = *a.d2.seed;
+  const DropKeys dk1{(uint32_t)s1, (uint32_t)(s1 >> 32), a.d1.thresh, a.d1.scale, a.d1.on};
+  const DropKeys dkf{(uint32_t)sf, (uint32_t)(sf >> 32), a.dff.thresh, a.dff.scale, a.dff.on};
+  const DropKeys dk2{(uint32_t)s2, (uint32_t)(s2 >> 32), a.d2.thresh, a.d2.scale, a.d2.on};
+  __syncthreads();
+  STAMP(1);
+  // ---- x1 = res + drop1(ctx·Woᵀ + bo); a2 = LN2(x1)   (every split; the lead stores them)
+  f32x4_t v[2];
+  head_gemm<2, HD, PD>(L.sA, wo, v, lane);
+  WFrags<2, HD> w1s;
+  w1s.load(a.w1, HD, nh, lane, HD);
+  {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = v[t][e] + Q.bo[n + e];
+      drop_apply_vec<4>(dk1, (uint32_t)(drow * HD + n), x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] += L.sX1[li][n + e];
+        v[t][e] = x[e];
+      }
+      if (lead && mrow) *reinterpret_cast<float4*>(a.x1 + (int64_t)m * HD + n) = make_float4(x[0], x[1], x[2], x[3]);
+    }
+    __syncthreads();                                 // every wave is done reading ctx and res
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) L.sX1[li][n0 + 16 * t + 4 * g + e] = v[t][e];
+    float mu, rs;
+    row_ln(v, Q.n2w, Q.n2b, a.eps, false, n0, L, w, lane, mu, rs);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+      st4_bf(L.sA + li * PD + n * 2, x);
+      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.a2 + (int64_t)m * HD + n), x);
+    }
+    if (lead && mrow && lane < 16 && w == 0) { a.m2[m] = mu; a.r2[m] = rs; }
+  }
+  __syncthreads();
+  STAMP(2);
+  // ---- h[:, 128j ..) = dropf(relu(a2·W1ᵀ + b1)): the wave's 32 hidden units
+  WFrags<2, 128> w2s;                                // W2[:, 128j .. 128j + 128): k window
+  {
+    f32x4_t hv[2];
+    head_gemm<2, HD, PD>(L.sA, w1s, hv, lane);
+    w2s.load(a.w2 + 128 * j, F, n0, lane, 128);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = nh + 16 * t + 4 * g;
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = fmaxf(hv[t][e] + Q.b1[n + e], 0.f);
+      drop_apply_vec<4>(dkf, (uint32_t)(drow * F + n), x);
+      st4_bf(L.sH + li * PF + (n - 128 * j) * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.h + (int64_t)m * F + n), x);
+    }
+  }
+  __syncthreads();
+  STAMP(3);
+  // ---- this split's FFN2 partial -> exchange slot (rb, j); the last arriver goes on
+  head_gemm<2, 128, PF>(L.sH, w2s, v, lane);
+  STAMP(4);
+  // fusion_layer.0's fragments before the handoff (every split: their L2 round trip then
+  // overlaps the exchange's instead of following it)
+  WFrags<2, WPAD> wf0;
+  wf0.load(a.wf0, W, n0, lane, W);
+  float* const part = a.ffn_part + (int64_t)rb * NS * HR * HD;      // [NS][HR][HD]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    st16_wt(part, (uint32_t)(((j * HR + li) * HD + n0 + 16 * t + 4 * g) * 4),
+            make_float4(v[t][0], v[t][1], v[t][2], v[t][3]));
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(a.ffn_cnt + rb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) __hip_atomic_store(a.ffn_cnt + rb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  STAMP(5);
+  {
+    // x2 = x1 + drop2(Σ_j partial_j + b2), summed in split order -> comb[:, :128]
+    float4 pp[NS][2];
+#pragma unroll
+    for (int jj = 0; jj < NS; ++jj)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        pp[jj][t] = ld16_wt(part, (uint32_t)(((jj * HR + li) * HD + n0 + 16 * t + 4 * g) * 4));
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      float x[4] = {pp[0][t].x, pp[0][t].y, pp[0][t].z, pp[0][t].w};
+#pragma unroll
+      for (int jj = 1; jj < NS; ++jj) {
+        x[0] += pp[jj][t].x; x[1] += pp[jj][t].y; x[2] += pp[jj][t].z; x[3] += pp[jj][t].w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] += Q.b2[n + e];
+      drop_apply_vec<4>(dk2, (uint32_t)(drow * HD + n), x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] += L.sX1[li][n + e];
+      st4_bf(L.sC + li * PW + n * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.comb + (int64_t)m * W + n), x);
+    }
+  }
+  __syncthreads();
+  STAMP(6);
+  // ---- z = comb·Wf0ᵀ + bf0; az = relu(LN(z))
+  head_gemm<2, WPAD, PW>(L.sC, wf0, v, lane);
+  WFrags<2, HD> wf3;
+  wf3.load(a.wf3, HD, n0, lane, HD);
+  {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[t][e] += Q.bf0[n + e];
+      if (mrow) *reinterpret_cast<float4*>(a.z + (int64_t)m * HD + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
+    }
+    float mu, rs;
+    row_ln(v, Q.lnw, Q.lnb, a.eps, true, n0, L, w, lane, mu, rs);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+      st4_bf(L.sA + li * PD + n * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.az + (int64_t)m * HD + n), x);
+    }
+    if (mrow && lane < 16 && w == 0) { a.mz[m] = mu; a.rz[m] = rs; }
+  }
+  __syncthreads();
+  // ---- u = az·Wf3ᵀ + bf3
+  head_gemm<2, HD, PD>(L.sA, wf3, v, lane);
+  float uo[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) uo[t][e] = v[t][e] + Q.bf3[n + e];
+    if (mrow)
+      *reinterpret_cast<float4*>(a.u + (int64_t)m * HD + n) = make_float4(uo[t][0], uo[t][1], uo[t][2], uo[t][3]);
+  }
+  row_l2norm(uo, a.uhat, a.unrm, m, mrow, n0, L, w, lane);
+  STAMP(7);
+}
+
 // ------------------------------------------------------------------------------ backward
 // The head's backward, one launch (the unfused sequence: linear_dx of fusion_layer.3, the
 // ReLU-gated LayerNorm backward, linear_dx of fusion_layer.0, the concat backward, the
@@ -1167,6 +1402,10 @@ extern "C" int ttmi_item_head_bwd_c(const ttmi_item_head_bwd_desc* d, hipStream_
 }
 
 namespace {
+// the FFN split's workspace: arrival counts (one int per row block, 256-byte padded), then the
+// exchange slots [nbu][F / 128][HR][HD] fp32
+int64_t ffn_cnt_bytes(int B) { return ((int64_t)((B + HR - 1) / HR) * 4 + 255) / 256 * 256; }
+
 int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it, int stage,
                             hipStream_t s) {
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_fwd: null descriptor");
@@ -1213,6 +1452,15 @@ int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_d
     a.it.fin = stage == 3;
     a.it.err = d->id_err;
     extra = stage == 0 ? a.it_nblk * (IN1 / 64) : stage == 2 ? a.it_nblk : a.it_nblk * (IN1 / 64 + 1);
+  }
+  if (d->ffn_ws && !getenv("TTMI_HEAD_NOSPLIT")) {   // the FFN split over its hidden units
+    TTMI_REQUIRE(((uintptr_t)d->ffn_ws & 255) == 0, "ttmi_user_head_fwd: ffn_ws must be 256-byte aligned");
+    a.ffn_cnt = static_cast<int*>(d->ffn_ws);
+    a.ffn_part = reinterpret_cast<float*>(static_cast<char*>(d->ffn_ws) + ffn_cnt_bytes(d->B));
+    const dim3 grid((unsigned)(a.nbu * (d->F / 128) + extra));
+    if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_split_kernel<512>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(user_head_fwd_split_kernel<256>, grid, dim3(256), 0, s, a);
+    return ttmi_check_launch("ttmi_user_head_fwd");
   }
   const dim3 grid((unsigned)(a.nbu + extra));
   if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_kernel<512>, grid, dim3(256), 0, s, a);
@@ -1266,6 +1514,11 @@ extern "C" int ttmi_mha_q1_gather_item_fwd(int dtype, int B, int L, int H, int D
   if (dtype == TTMI_BF16) hipLaunchKernelGGL(q1_item_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, q, ia, it_nblk, nit);
   else hipLaunchKernelGGL(q1_item_fwd_kernel<float>, grid, dim3(256), 0, s, q, ia, it_nblk, nit);
   return ttmi_check_launch("ttmi_mha_q1_gather_item_fwd");
+}
+
+extern "C" int64_t ttmi_user_head_ffn_ws_bytes(int B, int F) {
+  if (B <= 0 || F <= 0 || F % 128) return 0;
+  return ffn_cnt_bytes(B) + (int64_t)((B + HR - 1) / HR) * (F / 128) * HR * HD * 4;
 }
 
 extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {

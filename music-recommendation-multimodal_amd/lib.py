@@ -130,7 +130,7 @@ class UserHeadDesc(ctypes.Structure):
                 ("x1", c_p), ("a2", c_p), ("m2", c_p), ("r2", c_p), ("h", c_p), ("comb", c_p),
                 ("rows", c_p), ("z", c_p), ("az", c_p), ("mz", c_p), ("rz", c_p), ("u", c_p),
                 ("u_hat", c_p), ("u_norm", c_p),
-                ("n_genders", c_i), ("n_countries", c_i), ("id_err", c_p)]
+                ("n_genders", c_i), ("n_countries", c_i), ("id_err", c_p), ("ffn_ws", c_p)]
 
 
 class UserHeadBwdDesc(ctypes.Structure):
@@ -278,6 +278,7 @@ SIGNATURES = {
     "ttmi_item_head_bwd_c": (c_i, [c_p, c_p]),
     "ttmi_item_head_bn_part_floats": (ctypes.c_int64, [c_i]),
     "ttmi_item_head_bn_counter_bytes": (ctypes.c_int64, [c_i]),
+    "ttmi_user_head_ffn_ws_bytes": (ctypes.c_int64, [c_i, c_i]),
     "ttmi_item_head_bwd_ws_floats": (ctypes.c_int64, [c_i]),
     "ttmi_user_item_head_bwd": (c_i, [c_p, c_p, c_p]),
     "ttmi_deb_pool_fwd": (c_i, [c_i, c_i, c_i, c_p, c_p, c_p, c_p]),

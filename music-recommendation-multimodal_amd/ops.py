@@ -1346,6 +1346,9 @@ def user_head_fwd(ctx: Tensor, res: Tensor, drop_rows: Optional[Tensor], W: Dict
         setattr(d, k, _p(out[k]))
     if normed is not None:     # (u_hat [B, D], norms [B]): InfoNCE's l2norm of u, same launch
         d.u_hat, d.u_norm = _p(normed[0]), _p(normed[1])
+    # the FFN split over its hidden units (ABI 21): arrival counts (reset by each launch) and
+    # exchange slots (overwritten before they are read), one buffer per (device, B, F)
+    d.ffn_ws = _p(_zero_ws("ttmi_user_head_ffn_ws_bytes", (B, d.F), ctx.device))
     if co_item is None:
         call("ttmi_user_head_fwd", ctypes.byref(d), _s())
     elif co_stage == "A":      # item head stage A on the CUs the 16-row user blocks leave idle

@@ -4,8 +4,8 @@ the fused user head, from the diagnostic build (tools/stamp_build.sh).  GPU diag
 Phases (panel_kernel): 0 start, 1 W DMA issued, 2 W in LDS (after the barrier), 3 first
 tile's first column group MFMAs done, 4 first tile done, 5 all tiles done, 6 end.
 Phases (qkv_attn_fwd): 0 start, 1 W group 0 in LDS, 2 projection done, 3 attention done.
-Phases (user_head_fwd): 0 start, 1 prologue, 2 out-proj + LN2, 3 FFN1, 4 FFN2, 5 fusion0 + LN,
-6 end."""
+Phases (user_head_fwd, the FFN-split kernel): 0 start, 1 prologue, 2 out-proj + LN2, 3 FFN1
+slice, 4 FFN2 partial, 5 handoff done (the last arriver), 6 x2, 7 end."""
 import ctypes
 import importlib
 import os
@@ -30,6 +30,8 @@ def stamps(fn, name, nph=7, tu="gemm"):
     fn()
     torch.cuda.synchronize()
     dump(buf, NB * NW * NP)                         # clear
+    if os.environ.get("STAMP_BUSY"):   # keep every XCD busy up to the measured launch
+        torch.cuda._sleep(int(os.environ["STAMP_BUSY"]))
     fn()
     assert dump(buf, NB * NW * NP) == 0
     a = np.array(buf, dtype=np.float64).reshape(NB, NW, NP)[:, :, :nph]
@@ -41,6 +43,15 @@ def stamps(fn, name, nph=7, tu="gemm"):
         v = rel[:, :, k][live & (a[:, :, k] > 0)]
         cols.append(f"{np.median(v):6.2f}/{v.max():6.2f}" if v.size else "   -   ")
     print(f"{name:34s} " + "  ".join(cols), flush=True)
+    if os.environ.get("STAMP_XCD"):    # start-time spread by XCD (block id % 8)
+        blk = np.arange(NB)
+        for x in range(8):
+            sel = (blk % 8 == x)[:, None] & live
+            v = rel[:, :, 0][sel]
+            e = rel[:, :, nph - 1][sel & (a[:, :, nph - 1] > 0)]
+            if v.size:
+                print(f"    xcd {x}: start min {v.min():5.2f} med {np.median(v):5.2f} max {v.max():5.2f}  "
+                      f"end med {np.median(e) if e.size else 0:6.2f} max {e.max() if e.size else 0:6.2f}  n={v.size}")
 
 
 def main():
@@ -117,7 +128,7 @@ def main():
              rows=torch.empty(B, dtype=torch.int32, device=dev), z=f32(B, D), az=bf(B, D),
              mz=f32(B), rz=f32(B), u=f32(B, D))
     stamps(lambda: ops.user_head_fwd(ctx, res, drows, W, P, pre, gender, country, 1e-5, drops, o),
-           "user head fwd (B=512)", tu="head")
+           "user head fwd (B=512)", nph=8, tu="head")
     # InfoNCE at B = 512 (phases: fwd 0 start, 1 Q staged, 2 logit tiles done, 3 partials
     # retired, 4 arrival counted, 5 block combine done, 6 final combine; bwd 0 start,
     # 1 G.V MFMAs done, 2 partials retired, 3 arrival counted, 4 finish done)
