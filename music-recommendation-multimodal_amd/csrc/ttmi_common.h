@@ -204,6 +204,11 @@ TTMI_DEV float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// The same sum through the device library's DPP reduction (row shifts within 16 lanes, a row
+// mirror, two lane reads): a few cycles a step instead of an LDS-permute round trip.  A
+// different (fixed) order than wave_sum: use it where no other kernel must match bit for bit.
+extern "C" __device__ float __ockl_wfred_add_f32(float);
+TTMI_DEV float wave_sum_dpp(float v) { return __ockl_wfred_add_f32(v); }
 TTMI_DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

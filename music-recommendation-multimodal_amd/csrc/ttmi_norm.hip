@@ -394,14 +394,14 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_vec_kernel(
 
 // Backward: block (l, b-chunk) of SEB_W waves; each wave walks b = chunk*bpc + wave,
 // + SEB_W, ... so the position gradient dP[l] accumulates in registers (one add per column
-// per block).  The chunk is sized so a wave makes ONE pass of U rows: the kernel is a
-// dependent-gather latency chain (ids -> E[id]), so waves, not rows per wave, hide it.
+// per block).  A wave makes SEB_R passes of U rows whose loads are all in flight at once (the
+// dependent gather ids -> E[id]: two memory round trips per wave), so the grid is one round.
 // Every cross-block sum goes to int64 fixed-point accumulators (ABI 16): the item-embedding
 // rows accE[V][D] (one add per token and column) and accL[3][L][D] (dP, and the LayerNorm
 // weight / bias partials per position), converted into the fp32 gradients by the fold
 // (ttmi_seq_embed_bwd_folds): the gradient is bit-identical run to run (the fp32 atomics it
 // replaces summed in arrival order).
-constexpr int SEB_W = 8;
+constexpr int SEB_W = 4, SEB_R = 4;
 template <int NV>
 __global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
     int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E,
@@ -409,6 +409,7 @@ __global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
     const float* __restrict__ rstd, DropParams dp, const float* __restrict__ dx,
     int64_t* __restrict__ accE, int64_t* __restrict__ accL, int64_t padding_idx, int64_t V, int bpc) {
   __shared__ float red[SEB_W * 64 * NV];
+  TTMI_TSTAMP(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l = blockIdx.x;
   const int b0 = blockIdx.y * bpc;
@@ -418,35 +419,71 @@ __global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
   float ap[NV], aw[NV], ab[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) ap[i] = aw[i] = ab[i] = 0.f;
-  // two rows per wave per iteration, every load of both issued before any arithmetic (the
-  // loop is latency-bound: ids -> E[id] is a dependent gather)
-  constexpr int U = 2;
-  for (int bq = b0 + wave; bq < b1; bq += SEB_W * U) {
-    int64_t row[U], id[U];
-    bool ok[U], live[U];
-    float mu[U], rs[U], d[U][NV], e[U][NV];
+  // two rows per wave per pass, SEB_R passes
+  constexpr int U = 2, STEP = SEB_W * U;
+  struct Rows { int64_t row[U], id[U]; float mu[U], rs[U], d[U][NV], e[U][NV]; };
+  auto load_ids = [&](int bq, int64_t (&row)[U], int64_t (&id)[U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      live[u] = bq + SEB_W * u < b1;
+    for (int u = 0; u < U; ++u) {       // rows past the chunk clamped: harmless re-loads
       row[u] = (int64_t)min(bq + SEB_W * u, b1 - 1) * L + l;
       id[u] = ids[row[u]];
     }
+  };
+  // the padding row E[padding_idx], read once: about half the tokens are padding, and every
+  // wave gathering that one 512-byte row queued on the same L2 channel of its XCD
+  const bool pad_ok = padding_idx >= 0 && padding_idx < V;
+  float epad[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) epad[i] = pad_ok ? E[padding_idx * D + min(lane + 64 * i, D - 1)] : 0.f;
+  // r.e: the row's embedding value (E[id], the padding row, or 0 for an id outside [0, V))
+  auto load_rows = [&](const int64_t (&row)[U], const int64_t (&id)[U], Rows& r) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      ok[u] = id[u] >= 0 && id[u] < V;
-      const int64_t er = ok[u] ? id[u] : 0;
-      mu[u] = mean[row[u]];
-      rs[u] = rstd[row[u]];
+      r.row[u] = row[u];
+      r.id[u] = id[u];
+      const bool ok = id[u] >= 0 && id[u] < V;
+      r.mu[u] = mean[row[u]];
+      r.rs[u] = rstd[row[u]];
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int c = min(lane + 64 * i, D - 1);
-        d[u][i] = dx[row[u] * D + c];
-        e[u][i] = E[er * D + c];
+        r.d[u][i] = dx[row[u] * D + c];
+        r.e[u][i] = id[u] == padding_idx ? epad[i] : 0.f;
+      }
+      if (ok && id[u] != padding_idx) {          // wave-uniform (one row per wave)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) r.e[u][i] = E[id[u] * D + min(lane + 64 * i, D - 1)];
       }
     }
+  };
+  float pl[NV], wl[NV];                  // this block's position row and LayerNorm weight
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = min(lane + 64 * i, D - 1);
+    pl[i] = P[(int64_t)l * D + c];
+    wl[i] = w[c];
+  }
+  // all SEB_R passes' ids, then all their rows, in flight at once: two memory round trips per
+  // wave (under the kernel's load a round trip is ~3 us: a one-pass-ahead pipeline still paid
+  // about one per pass)
+  Rows rr[SEB_R];
+  {
+    int64_t row0[SEB_R][U], id0[SEB_R][U];
+#pragma unroll
+    for (int k = 0; k < SEB_R; ++k) load_ids(b0 + wave + k * STEP, row0[k], id0[k]);
+#pragma unroll
+    for (int k = 0; k < SEB_R; ++k) load_rows(row0[k], id0[k], rr[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < SEB_R; ++k) {
+    TTMI_TSTAMP(1 + k);                          // (diagnostic build: pass k starts)
+    const int bq = b0 + wave + k * STEP;
+    const Rows& cur = rr[k];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (!live[u]) continue;
+      if (bq + SEB_W * u >= b1) continue;
+      const int64_t row = cur.row[u], id = cur.id[u];
+      const bool ok = id >= 0 && id < V;
       float g[NV], xh[NV];
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -454,34 +491,40 @@ __global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
         const int c = lane + 64 * i;
         g[i] = 0.f; xh[i] = 0.f;
         if (c < D) {
-          float dd = d[u][i];
-          if (dk.on) dd = drop_keep(dk, (uint32_t)(row[u] * D + c)) ? dd * dk.scale : 0.f;
-          const float ev = (ok[u] ? e[u][i] : 0.f) + P[(int64_t)l * D + c];
-          xh[i] = (ev - mu[u]) * rs[u];
+          float dd = cur.d[u][i];
+          if (dk.on) dd = drop_keep(dk, (uint32_t)(row * D + c)) ? dd * dk.scale : 0.f;
+          const float ev = cur.e[u][i] + pl[i];
+          xh[i] = (ev - cur.mu[u]) * cur.rs[u];
           aw[i] += dd * xh[i];
           ab[i] += dd;
-          g[i] = dd * w[c];
+          g[i] = dd * wl[i];
           s1 += g[i];
           s2 += g[i] * xh[i];
         }
       }
-      const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
-      const bool emb = ok[u] && id[u] != padding_idx;
+      const float c1 = wave_sum_dpp(s1) * invD, c2 = wave_sum_dpp(s2) * invD;
+      const bool emb = ok && id != padding_idx;
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int c = lane + 64 * i;
         if (c < D) {
-          const float o = rs[u] * (g[i] - c1 - xh[i] * c2);
+          const float o = cur.rs[u] * (g[i] - c1 - xh[i] * c2);
           ap[i] += o;
-          if (emb) fx_add(accE + id[u] * D + c, o, TTMI_FX_GRAD);
+#ifndef TTMI_DIAG_NOATOM
+          if (emb) fx_add(accE + id * D + c, o, TTMI_FX_GRAD);
+#else
+          if (emb && o == 12345.f) accE[id * D + c] = 1;   // diagnostic build: no scatter
+#endif
         }
       }
     }
   }
+  TTMI_TSTAMP(1 + SEB_R);
   const int64_t LD = (int64_t)L * D;
   block_col_fx<NV, SEB_W>(ap, D, accL + (int64_t)l * D, red);
   block_col_fx<NV, SEB_W>(aw, D, accL + LD + (int64_t)l * D, red);
   block_col_fx<NV, SEB_W>(ab, D, accL + 2 * LD + (int64_t)l * D, red);
+  TTMI_TSTAMP(2 + SEB_R);
 }
 
 // ------------------------------------------------------------ last-valid gather + concat
@@ -948,7 +991,9 @@ extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, int64_t V, const int64_t*
                "ttmi_seq_embed_bwd: null argument");
   TTMI_REQUIRE(((uintptr_t)ws & 15) == 0, "ttmi_seq_embed_bwd: ws must be 16-byte aligned");
   if (B > 0) {
-    const int bpc = 2 * SEB_W;                   // one pass of two rows per wave
+    // SEB_R passes of two rows per wave (400 blocks at B = 512, L = 50: one round on the
+    // chip; one pass per wave, 1,600 blocks, measured 20.5 us in the step, this 17)
+    const int bpc = 2 * SEB_R * SEB_W;
     dim3 grid(L, (B + bpc - 1) / bpc);
     int64_t* accE = static_cast<int64_t*>(ws);
     TTMI_NV_DISPATCH(D, hipLaunchKernelGGL((seq_embed_bwd_kernel<NV>), grid, dim3(64 * SEB_W), 0, s, B, L, D, ids,
@@ -1067,3 +1112,5 @@ extern "C" int ttmi_batchnorm_bwd(int dtype, int B, int C, const float* dy, cons
                        (const float*)y, gate_scale, gated, dz, dw, db);
   return ttmi_check_launch("ttmi_batchnorm_bwd");
 }
+
+TTMI_STAMP_DUMP(norm)
