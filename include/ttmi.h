@@ -838,6 +838,8 @@ typedef struct ttmi_user_head_bwd_desc {
   int64_t* dG; int64_t* dC;
   void* dz16; void* dy2; void* dz1; float* dx1; void* dy1; void* dctx; float* ws;
   int n_genders, n_countries;        /* ABI 20: ids clamped into the tables as in the forward */
+  void* ffn_ws;                      /* ABI 21, optional: as ttmi_user_head_desc::ffn_ws (the */
+                                     /* same size; the backward's FFN split over hidden units) */
 } ttmi_user_head_bwd_desc;
 int ttmi_user_head_bwd(const ttmi_user_head_bwd_desc* d, hipStream_t stream);
 int64_t ttmi_user_head_bwd_ws_floats(int B);

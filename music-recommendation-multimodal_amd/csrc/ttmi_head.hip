@@ -963,6 +963,7 @@ struct HeadBwdArgs {
   bf16_t* dz16; bf16_t* dy2; bf16_t* dz1; float* dx1; bf16_t* dy1; bf16_t* dctx; float* ws;
   ItemBwdArgs it; int nbu;     // co-launched item head backward: workgroups >= nbu
   int ng, nc;                  // table rows of G / C (ids clamped as in the forward)
+  float* ffn_part; int* ffn_cnt;   // ABI 21: the FFN split's exchange slots and arrival counts
 };
 
 struct HeadBwdLds {
@@ -991,7 +992,8 @@ TTMI_DEV float bwd_row_sum(float s, HeadBwdLds& L, int w, int lane) {
 // The weight / bias gradient terms are summed over the block's 16 rows through LDS and
 // written to ws (wsw / wsb rows).
 TTMI_DEV void ln_bwd16(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, float rs, const float (&wv)[2][4],
-                       int n0, bool mrow, HeadBwdLds& L, int w, int lane, float* wsw, float* wsb) {
+                       int n0, bool mrow, HeadBwdLds& L, int w, int lane, float* wsw, float* wsb,
+                       bool sums = true) {
   const int g = lane >> 4, li = lane & 15;
   float xh[2][4], gg[2][4];
   float s1 = 0.f, s2 = 0.f;
@@ -1011,7 +1013,7 @@ TTMI_DEV void ln_bwd16(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, floa
   }
   const float c1 = bwd_row_sum(s1, L, w, lane) * (1.f / HD);   // (its barriers publish sW, sB)
   const float c2 = bwd_row_sum(s2, L, w, lane) * (1.f / HD);
-  if (threadIdx.x < HD) {                            // one column per thread, rows in order
+  if (sums && threadIdx.x < HD) {                    // one column per thread, rows in order
     const int c = threadIdx.x;
     float cw = 0.f, cb = 0.f;
 #pragma unroll
@@ -1273,6 +1275,241 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
       float sum = 0.f;
 #pragma unroll
       for (int j = r; j < HR; ++j) sum += (j < nr && key[j] == key[r]) ? val[j] : 0.f;
+      fx_add(isg ? a.dG + (int64_t)key[r] * a.dg + k : a.dC + (int64_t)key[r] * a.dc + k, sum, TTMI_FX_GRAD);
+    }
+  }
+  STAMP(7);
+}
+
+// ---- the FFN split over its hidden units (ABI 21, ttmi_user_head_bwd_desc::ffn_ws), as the
+// forward's: row block rb on NS = F / 128 workgroups j.  Each runs the fusion MLP's backward
+// (daz, the ReLU-gated LayerNorm backward, dcomb, dy2: 76 KB of weights, redundantly; the lead
+// split stores what they all compute alike), the hidden units [128 j, 128 j + 128) of
+// dz1 = (dy2·W2) ⊙ gate and their partial dz1·W1 (32 + 32 KB), handed over like the forward's
+// partial; the last to arrive sums the partials in split order, then runs LN2's backward, the
+// residual, drop1, dctx = dy1·Wo and the dG / dC adds.
+template <int F>
+__global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a) {
+  constexpr int NS = F / 128;
+  STAMP(0);
+  __shared__ __attribute__((aligned(16))) HeadBwdLds L;
+  __shared__ int s_last;
+  const int nsplit = a.nbu * NS;
+  if ((int)blockIdx.x >= nsplit) {                  // co-launched item head backward (rows)
+    item_c_bwd_body(a.it, (int)blockIdx.x - nsplit, L);
+    return;
+  }
+  const int rb = (int)blockIdx.x / NS, j = (int)blockIdx.x % NS;
+  const bool lead = j == 0;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
+  const int r0 = rb * HR, m = r0 + li, mc = min(m, a.B - 1);
+  const bool mrow = m < a.B;
+  const int W = HD + a.dg + a.dc;
+  const int n0 = w * 32;
+  const int nh = 128 * j + 32 * w;                   // this wave's 32 of the split's hidden units
+  float* wsb = a.ws + (int64_t)rb * 4 * HD;          // the row block's four sum rows
+  WFrags<2, HD> wf3;
+  wf3.load(a.wf3t, HD, n0, lane, HD);
+  {                                                  // du rows -> LDS
+    const int r = tid >> 4, ch = tid & 15;
+    *reinterpret_cast<uint4*>(L.sA + r * PD + ch * 16) =
+        *reinterpret_cast<const uint4*>(a.du + (int64_t)min(r0 + r, a.B - 1) * HD + ch * 8);
+  }
+  const int drow = a.drows[mc];
+  const float mzr = a.mz[mc], rzr = a.rz[mc], m2r = a.m2[mc], r2r = a.r2[mc];
+  const uint64_t s1 = *a.d1.seed, s2 = *a.d2.seed;
+  const DropKeys dk1{(uint32_t)s1, (uint32_t)(s1 >> 32), a.d1.thresh, a.d1.scale, a.d1.on};
+  const DropKeys dk2{(uint32_t)s2, (uint32_t)(s2 >> 32), a.d2.thresh, a.d2.scale, a.d2.on};
+  if (tid < HR) {
+    L.sGi[tid] = (int)clamp_id(a.gender[min(r0 + tid, a.B - 1)], a.ng, nullptr, 0);
+    L.sCi[tid] = (int)clamp_id(a.country[min(r0 + tid, a.B - 1)], a.nc, nullptr, 0);
+  }
+  uint2 azq[2];
+  float zs[2][4], x1s[2][4], lnw[2][4], n2w[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float4 lw = *reinterpret_cast<const float4*>(a.lnw + n);
+    const float4 nw = *reinterpret_cast<const float4*>(a.n2w + n);
+    lnw[t][0] = lw.x; lnw[t][1] = lw.y; lnw[t][2] = lw.z; lnw[t][3] = lw.w;
+    n2w[t][0] = nw.x; n2w[t][1] = nw.y; n2w[t][2] = nw.z; n2w[t][3] = nw.w;
+    azq[t] = *reinterpret_cast<const uint2*>(a.az + (int64_t)mc * HD + n);
+    const float4 zv = *reinterpret_cast<const float4*>(a.z + (int64_t)mc * HD + n);
+    const float4 xv = *reinterpret_cast<const float4*>(a.x1 + (int64_t)mc * HD + n);
+    zs[t][0] = zv.x; zs[t][1] = zv.y; zs[t][2] = zv.z; zs[t][3] = zv.w;
+    x1s[t][0] = xv.x; x1s[t][1] = xv.y; x1s[t][2] = xv.z; x1s[t][3] = xv.w;
+  }
+  uint2 hq[2];                                       // the wave's 32 gate columns, 4 per lane
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+    hq[q] = *reinterpret_cast<const uint2*>(a.h + (int64_t)mc * F + nh + 16 * q + 4 * g);
+  __syncthreads();
+  STAMP(1);
+  // ---- daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0])
+  f32x4_t v[2];
+  head_gemm<2, HD, PD>(L.sA, wf3, v, lane);
+  WFrags<3, HD> wf0;                                 // dcomb's 11 column tiles: w, w+4, w+8
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) {
+    const int tj = min(w + 4 * jj, W / 16 - 1);
+#pragma unroll
+    for (int c = 0; c < HD / 32; ++c) wf0.f[c][jj] = wfrag(a.wf0t, HD, 16 * tj + li, c, lane, HD);
+  }
+  {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {                    // ReLU gate of the forward's az
+      const uint2 q = azq[t];
+      const float gz[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[t][e] = gz[e] > 0.f ? v[t][e] : 0.f;
+    }
+    __syncthreads();                                 // every wave is done reading du
+    ln_bwd16(v, zs, mzr, rzr, lnw, n0, mrow, L, w, lane, wsb, wsb + HD, lead);   // (the lead's sums)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + 16 * t + 4 * g;
+      const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+      st4_bf(L.sA + li * PD + n * 2, x);
+      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.dz16 + (int64_t)m * HD + n), x);
+    }
+  }
+  __syncthreads();
+  STAMP(2);
+  // ---- dcomb = dz·Wf0: columns < D -> dx2 (LDS), the demographic ones -> sDem
+  WFrags<2, HD> w2s;                                 // W2ᵀ rows of the wave's hidden units
+  {
+    f32x4_t dc[3];
+    head_gemm<3, HD, PD>(L.sA, wf0, dc, lane);
+    w2s.load(a.w2t, HD, nh, lane, HD);
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      const int tj = w + 4 * jj;
+      if (tj >= W / 16) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 16 * tj + 4 * g + e;
+        const float val = dc[jj][e];
+        if (k < HD) L.sX[li][k] = mrow ? val : 0.f;
+        else L.sDem[li][k - HD] = val;
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(3);
+  // ---- dy2 = drop2ᵀ(dx2) -> LDS (A of the next product); the lead stores it
+  {
+    const int n = n0 + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = L.sX[li][n + 16 * t + e];
+      drop_apply_vec<4>(dk2, (uint32_t)(drow * HD + n + 16 * t), x);
+      st4_bf(L.sA + li * PD + (n + 16 * t) * 2, x);
+      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.dy2 + (int64_t)m * HD + n + 16 * t), x);
+    }
+  }
+  __syncthreads();
+  STAMP(4);
+  // ---- dz1[:, 128j ..) = (dy2·W2) ⊙ [h > 0]·sf
+  WFrags<2, 128> w1s;                                // W1ᵀ[:, 128j .. 128j + 128): k window
+  {
+    f32x4_t hv[2];
+    head_gemm<2, HD, PD>(L.sA, w2s, hv, lane);
+    w1s.load(a.w1t + 128 * j, F, n0, lane, 128);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = nh + 16 * t + 4 * g;
+      const uint2 q = hq[t];
+      const float hg[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u)};
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = hg[e] > 0.f ? hv[t][e] * a.sf : 0.f;
+      st4_bf(L.sH + li * PF + (n - 128 * j) * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.dz1 + (int64_t)m * F + n), x);
+    }
+  }
+  __syncthreads();
+  STAMP(5);
+  // ---- this split's partial dz1·W1 -> exchange slot (rb, j); the last arriver goes on
+  head_gemm<2, 128, PF>(L.sH, w1s, v, lane);
+  WFrags<2, HD> wo;                                  // (before the handoff, as the forward's wf0)
+  wo.load(a.wot, HD, n0, lane, HD);
+  float* const part = a.ffn_part + (int64_t)rb * NS * HR * HD;      // [NS][HR][HD]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    st16_wt(part, (uint32_t)(((j * HR + li) * HD + n0 + 16 * t + 4 * g) * 4),
+            make_float4(v[t][0], v[t][1], v[t][2], v[t][3]));
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(a.ffn_cnt + rb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) __hip_atomic_store(a.ffn_cnt + rb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  STAMP(6);
+  // ---- dx1 = LN2ᵀ(Σ_j partial_j) + dx2; dy1 = drop1ᵀ(dx1)
+  {
+    float4 pp[NS][2];
+#pragma unroll
+    for (int jj = 0; jj < NS; ++jj)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        pp[jj][t] = ld16_wt(part, (uint32_t)(((jj * HR + li) * HD + n0 + 16 * t + 4 * g) * 4));
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      v[t] = f32x4_t{pp[0][t].x, pp[0][t].y, pp[0][t].z, pp[0][t].w};
+#pragma unroll
+      for (int jj = 1; jj < NS; ++jj) {
+        v[t][0] += pp[jj][t].x; v[t][1] += pp[jj][t].y; v[t][2] += pp[jj][t].z; v[t][3] += pp[jj][t].w;
+      }
+    }
+  }
+  ln_bwd16(v, x1s, m2r, r2r, n2w, n0, mrow, L, w, lane, wsb + 2 * HD, wsb + 3 * HD);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    float x[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = v[t][e] + L.sX[li][n + e];
+    if (mrow) *reinterpret_cast<float4*>(a.dx1 + (int64_t)m * HD + n) = make_float4(x[0], x[1], x[2], x[3]);
+    drop_apply_vec<4>(dk1, (uint32_t)(drow * HD + n), x);
+    st4_bf(L.sA + li * PD + n * 2, x);               // every wave is past its dy2 reads
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dy1 + (int64_t)m * HD + n), x);
+  }
+  __syncthreads();
+  // ---- dctx = dy1·Wo
+  head_gemm<2, HD, PD>(L.sA, wo, v, lane);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+    const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dctx + (int64_t)m * HD + n), x);
+  }
+  // ---- dG / dC (as user_head_bwd_kernel)
+  if (lane < 48) {
+    const bool isg = lane < 16;
+    const int k = isg ? lane : lane - 16;
+    const int nr = min(HR, a.B - r0);
+    int key[HR];
+    float val[HR];
+#pragma unroll
+    for (int jj = 0; jj < HR; ++jj) {
+      key[jj] = isg ? L.sGi[jj] : L.sCi[jj];
+      val[jj] = L.sDem[jj][lane];
+    }
+#pragma unroll
+    for (int r = 0; r < HR; ++r) {
+      if ((r & 3) != w || r >= nr) continue;
+      bool first = true;
+#pragma unroll
+      for (int jj = 0; jj < r; ++jj) first &= key[jj] != key[r];
+      if (!first) continue;
+      float sum = 0.f;
+#pragma unroll
+      for (int jj = r; jj < HR; ++jj) sum += (jj < nr && key[jj] == key[r]) ? val[jj] : 0.f;
       fx_add(isg ? a.dG + (int64_t)key[r] * a.dg + k : a.dC + (int64_t)key[r] * a.dc + k, sum, TTMI_FX_GRAD);
     }
   }
@@ -1558,6 +1795,15 @@ extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const t
     if (rc != TTMI_OK) return rc;
     a.it = item_bwd_args(it);
     extra = (it->B + HR - 1) / HR;
+  }
+  if (d->ffn_ws && !getenv("TTMI_HEAD_NOSPLIT")) {   // the FFN split over its hidden units
+    TTMI_REQUIRE(((uintptr_t)d->ffn_ws & 255) == 0, "ttmi_user_head_bwd: ffn_ws must be 256-byte aligned");
+    a.ffn_cnt = static_cast<int*>(d->ffn_ws);
+    a.ffn_part = reinterpret_cast<float*>(static_cast<char*>(d->ffn_ws) + ffn_cnt_bytes(d->B));
+    const dim3 grid((unsigned)(a.nbu * (d->F / 128) + extra));
+    if (d->F == 512) hipLaunchKernelGGL(user_head_bwd_split_kernel<512>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(user_head_bwd_split_kernel<256>, grid, dim3(256), 0, s, a);
+    return ttmi_check_launch("ttmi_user_head_bwd");
   }
   const dim3 grid((unsigned)(a.nbu + extra));
   if (d->F == 512) hipLaunchKernelGGL(user_head_bwd_kernel<512>, grid, dim3(256), 0, s, a);

@@ -147,7 +147,7 @@ class UserHeadBwdDesc(ctypes.Structure):
                 ("dG", c_p), ("dC", c_p),
                 ("dz16", c_p), ("dy2", c_p), ("dz1", c_p), ("dx1", c_p), ("dy1", c_p),
                 ("dctx", c_p), ("ws", c_p),
-                ("n_genders", c_i), ("n_countries", c_i)]
+                ("n_genders", c_i), ("n_countries", c_i), ("ffn_ws", c_p)]
 
 
 class LnBwdDesc(ctypes.Structure):

@@ -1402,6 +1402,7 @@ def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: 
     for k in ("dz16", "dy2", "dz1", "dx1", "dy1", "dctx"):
         setattr(d, k, _p(o[k]))
     d.ws = _p(ws)
+    d.ffn_ws = _p(_zero_ws("ttmi_user_head_ffn_ws_bytes", (B, F), dev))   # (the forward's buffer)
     if co_item is None:
         call("ttmi_user_head_bwd", ctypes.byref(d), _s())
     else:      # the item head's row-local backward on the idle CUs (ABI 15)
