@@ -809,7 +809,10 @@ typedef struct ttmi_user_head_desc {
                                      /* workgroups per 16-row block, whose last arriver sums the */
                                      /* partials in split order and runs the fusion MLP */
 } ttmi_user_head_desc;
+/* ABI 21: D = 256 with F = 1024 (the reference's default width) is served by the FFN-split
+ * kernel only: ffn_ws is required there and no item head stage may ride in the launch. */
 int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t stream);
+/* Bytes of ffn_ws for B rows and FFN width F (sized for D = 256). */
 int64_t ttmi_user_head_ffn_ws_bytes(int B, int F);
 /* Its backward, one launch (ABI 12), from du (bf16 [B, D]) and the forward's saved values:
  *   daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0]); dcomb = dz·Wf0 (dG[gender] / dC[country] +=);
@@ -818,7 +821,9 @@ int64_t ttmi_user_head_ffn_ws_bytes(int B, int F);
  * The *t weights are the transposed k-major mirrors ([in, out]).  Outputs dz16, dy2, dz1, dy1
  * (bf16: the weight-gradient GEMMs' dY operands), dx1 (fp32), dctx (bf16).  ws
  * [ttmi_user_head_bwd_ws_floats(B)] receives per-16-row-block column sums of the four
- * LayerNorm parameter gradients (dlnw, dlnb, dn2w, dn2b, [nblk][4][D]) to be folded.
+ * LayerNorm parameter gradients (dlnw, dlnb, dn2w, dn2b, [nblk][4][D], nblk = ceil(B / 16);
+ * the size function covers D = 256) to be folded.  ABI 21: D = 256 with F = 1024 runs on
+ * the FFN-split kernel (ffn_ws required, no item head co-launch), as the forward.
  * ABI 16: dG / dC are int64 fixed-point accumulators ([n_genders][dg], [n_countries][dc],
  * scale 2^36, TTMI_FX_GRAD_SHIFT; zero on entry): adds in any order give the same bits.  The
  * caller converts them into the fp32 gradients with a ttmi_fold_desc (fx_shift = 36, S = 1,

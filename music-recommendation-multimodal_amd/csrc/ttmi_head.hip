@@ -711,81 +711,173 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
 // The kernel above runs 32 row blocks: 7 of 8 CUs idle, and each workgroup streams all 368 KB
 // of the head's weights through its one CU (~36 GB/s a CU: that stream is the kernel's time).
 // Here row block rb runs on NS = F / 128 workgroups j.  Each computes out-proj + LN2 for the
-// block's rows (the 32 KB out-proj weights, redundantly), the hidden units [128 j, 128 j + 128)
-// of FFN1 and their partial FFN2 product (32 + 32 KB), and hands the fp32 partial [16 x 128]
-// over through write-through stores and an agent-scope arrival count (the item head's handoff
-// pattern above).  The last of the NS to arrive sums the partials in split order — the same
-// bits whichever arrives last — then runs the residual, the concat and the fusion MLP (80 KB).
-// Weight bytes through a CU: 96 KB (176 KB for the last arriver) instead of 368.
-template <int F>
-__global__ __launch_bounds__(256) void user_head_fwd_split_kernel(HeadArgs a) {
-  constexpr int NS = F / 128;
+// block's rows (the out-proj weights, redundantly), the hidden units [128 j, 128 j + 128) of
+// FFN1 and their partial FFN2 product, and hands the fp32 partial [16 x D] over through
+// write-through stores and an agent-scope arrival count (the item head's handoff pattern
+// above).  The last of the NS to arrive sums the partials in split order — the same bits
+// whichever arrives last — then runs the residual, the concat and the fusion MLP.  Weight bytes
+// through a CU at D = 128: 96 KB (176 KB for the last arriver) instead of 368.
+// D = 128 (4 waves) or 256 (8 waves, F = 1024: the reference's default width, ABI 21); each
+// wave owns 32 of the D columns of every D-wide stage.
+template <int D_>
+struct SplitGeo {
+  static constexpr int NW = D_ / 32;                 // waves
+  static constexpr int PD = (D_ + 8) * 2;            // LDS pitches (bytes)
+  static constexpr int PH = (128 + 8) * 2;           // the split's 128 hidden units
+  static constexpr int WPAD = (D_ + 48 + 31) / 32 * 32;
+  static constexpr int PW = (WPAD + 8) * 2;
+  static constexpr int TH = 128 / 16 / NW;           // hidden 16-column tiles per wave
+};
+template <int D_, int F>
+struct SplitLds {
+  using G = SplitGeo<D_>;
+  char sA[HR * G::PD];      // ctx, then a2, then az
+  char sH[HR * G::PH];      // the split's h columns
+  char sC[HR * G::PW];      // comb (zero-padded to WPAD)
+  float sX1[HR][D_ + 4];    // x1 (fp32 residual of the FFN)
+  float red[G::NW][HR];     // LayerNorm cross-wave partials
+  float bo[D_], n2w[D_], n2b[D_], b1[F], b2[D_], bf0[D_], lnw[D_], lnb[D_], bf3[D_];
+};
+// Row sum over the D columns held by the 4 lanes of row li in each of NW waves (in wave order).
+template <int NW>
+TTMI_DEV float split_row_sum(float s, float (*red)[HR], int w, int lane) {
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  if (lane < 16) red[w][lane] = s;
+  __syncthreads();
+  const int li = lane & 15;
+  float tot = red[0][li];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) tot += red[k][li];
+  __syncthreads();
+  return tot;
+}
+template <int D_>
+TTMI_DEV void split_row_ln(f32x4_t (&v)[2], const float* w_, const float* b_, float eps, bool relu, int n0,
+                           float (*red)[HR], int w, int lane, float& mu, float& rs) {
+  constexpr int NW = SplitGeo<D_>::NW;
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[t][e];
+  mu = split_row_sum<NW>(s, red, w, lane) * (1.f / D_);
+  float q = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[t][e] - mu;
+      q += d * d;
+    }
+  rs = 1.f / sqrtf(split_row_sum<NW>(q, red, w, lane) * (1.f / D_) + eps);
+  const int g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + 16 * t + 4 * g + e;
+      float o = (v[t][e] - mu) * rs * w_[n] + b_[n];
+      v[t][e] = relu ? fmaxf(o, 0.f) : o;
+    }
+}
+template <int D_>
+TTMI_DEV void split_row_l2norm(const float (&x)[2][4], float* xhat, float* nrm, int m, bool mrow, int n0,
+                               float (*red)[HR], int w, int lane) {
+  if (xhat == nullptr) return;                       // uniform: a kernel argument
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += x[t][e] * x[t][e];
+  const float nr = sqrtf(split_row_sum<SplitGeo<D_>::NW>(s, red, w, lane));
+  const float inv = 1.f / fmaxf(nr, 1e-12f);
+  const int g = lane >> 4;
+  if (mrow) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      *reinterpret_cast<float4*>(xhat + (int64_t)m * D_ + n0 + 16 * t + 4 * g) =
+          make_float4(x[t][0] * inv, x[t][1] * inv, x[t][2] * inv, x[t][3] * inv);
+    if (lane < 16 && w == 0) nrm[m] = nr;
+  }
+}
+
+template <int D_, int F>
+__global__ __launch_bounds__(D_ * 2) void user_head_fwd_split_kernel(HeadArgs a) {
+  using G = SplitGeo<D_>;
+  constexpr int NS = F / 128, NW = G::NW, NT = NW * 64, TH = G::TH;
   STAMP(0);
-  __shared__ __attribute__((aligned(16))) HeadLds L;
-  __shared__ __attribute__((aligned(16))) HeadParams Q;
+  __shared__ __attribute__((aligned(16))) union {
+    SplitLds<D_, F> s;
+    ItemLdsA ia;
+    ItemLdsC ic;
+  } U;
+  SplitLds<D_, F>& L = U.s;
   __shared__ int s_last;
   const int nsplit = a.nbu * NS;
   int ub = (int)blockIdx.x;
-  if (a.it_stage == 3) {
-    const int na = a.it_nblk * (IN1 / 64);
-    if (ub < na) {
-      item_a_body(a.it, ub % a.it_nblk, ub / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
+  if constexpr (D_ == HD) {                          // co-launched item head stages (D = 128)
+    if (a.it_stage == 3) {
+      const int na = a.it_nblk * (IN1 / 64);
+      if (ub < na) {
+        item_a_body(a.it, ub % a.it_nblk, ub / a.it_nblk, U.ia);
+        return;
+      }
+      ub -= na;
+      if (ub >= nsplit) {
+        item_c_body<true>(a.it, ub - nsplit, U.ic);
+        return;
+      }
+    } else if (ub >= nsplit) {
+      const int l = ub - nsplit;
+      if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, U.ia);
+      else item_c_body<false>(a.it, l, U.ic);
       return;
     }
-    ub -= na;
-    if (ub >= nsplit) {
-      item_c_body<true>(a.it, ub - nsplit, *reinterpret_cast<ItemLdsC*>(&L));
-      return;
-    }
-  } else if (ub >= nsplit) {                         // co-launched item head stage A or C
-    const int l = ub - nsplit;
-    if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, *reinterpret_cast<ItemLdsA*>(&L));
-    else item_c_body<false>(a.it, l, *reinterpret_cast<ItemLdsC*>(&L));
-    return;
   }
   const int rb = ub / NS, j = ub % NS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = rb * HR, m = r0 + li;
   const bool mrow = m < a.B;
   const bool lead = j == 0;                          // writes what every split computes alike
-  const int W = HD + a.dg + a.dc;
-  const int n0 = w * 32;                             // this wave's 32 of the 128 columns
-  const int nh = 128 * j + 32 * w;                   // ... and its 32 of the split's hidden units
-  WFrags<2, HD> wo;
-  wo.load(a.wo, HD, n0, lane, HD);
-  {                                                  // ctx: 16 rows x 16 chunks of 16 bytes
-    const int r = tid >> 4, ch = tid & 15;
-    *reinterpret_cast<uint4*>(L.sA + r * PD + ch * 16) =
-        *reinterpret_cast<const uint4*>(a.ctx + (int64_t)min(r0 + r, a.B - 1) * HD + ch * 8);
+  const int W = D_ + a.dg + a.dc;
+  const int n0 = w * 32;                             // this wave's 32 of the D columns
+  const int nh = 128 * j + 16 * TH * w;              // ... and its hidden units of the split
+  WFrags<2, D_> wo;
+  wo.load(a.wo, D_, n0, lane, D_);
+  {                                                  // ctx: 16 rows x D/8 chunks of 16 bytes
+    const int r = tid / (D_ / 8), ch = tid % (D_ / 8);
+    *reinterpret_cast<uint4*>(L.sA + r * G::PD + ch * 16) =
+        *reinterpret_cast<const uint4*>(a.ctx + (int64_t)min(r0 + r, a.B - 1) * D_ + ch * 8);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {                     // residual: 16 rows x 32 float4
-      const int idx = tid + 256 * q;
-      *reinterpret_cast<float4*>(&L.sX1[idx >> 5][(idx & 31) * 4]) =
-          *reinterpret_cast<const float4*>(a.res + (int64_t)min(r0 + (idx >> 5), a.B - 1) * HD + (idx & 31) * 4);
+    for (int q = 0; q < 2; ++q) {                     // residual: 16 rows x D/4 float4
+      const int idx = tid + NT * q, rr = idx / (D_ / 4), c4 = idx % (D_ / 4);
+      *reinterpret_cast<float4*>(&L.sX1[rr][c4 * 4]) =
+          *reinterpret_cast<const float4*>(a.res + (int64_t)min(r0 + rr, a.B - 1) * D_ + c4 * 4);
     }
   }
   {
-    const float4 p0 = vec_ld<HD>(a.bo, tid), p1 = vec_ld<HD>(a.n2w, tid), p2 = vec_ld<HD>(a.n2b, tid);
-    const float4 p3 = vec_ld<F>(a.b1, tid), p4 = vec_ld<HD>(a.b2, tid), p5 = vec_ld<HD>(a.bf0, tid);
-    const float4 p6 = vec_ld<HD>(a.lnw, tid), p7 = vec_ld<HD>(a.lnb, tid), p8 = vec_ld<HD>(a.bf3, tid);
-    vec_st<HD>(Q.bo, p0, tid); vec_st<HD>(Q.n2w, p1, tid); vec_st<HD>(Q.n2b, p2, tid);
-    vec_st<F>(Q.b1, p3, tid); vec_st<HD>(Q.b2, p4, tid); vec_st<HD>(Q.bf0, p5, tid);
-    vec_st<HD>(Q.lnw, p6, tid); vec_st<HD>(Q.lnb, p7, tid); vec_st<HD>(Q.bf3, p8, tid);
+    const float4 p0 = vec_ld<D_>(a.bo, tid), p1 = vec_ld<D_>(a.n2w, tid), p2 = vec_ld<D_>(a.n2b, tid);
+    const float4 p3 = vec_ld<F>(a.b1, tid), p4 = vec_ld<D_>(a.b2, tid), p5 = vec_ld<D_>(a.bf0, tid);
+    const float4 p6 = vec_ld<D_>(a.lnw, tid), p7 = vec_ld<D_>(a.lnb, tid), p8 = vec_ld<D_>(a.bf3, tid);
+    vec_st<D_>(L.bo, p0, tid); vec_st<D_>(L.n2w, p1, tid); vec_st<D_>(L.n2b, p2, tid);
+    vec_st<F>(L.b1, p3, tid); vec_st<D_>(L.b2, p4, tid); vec_st<D_>(L.bf0, p5, tid);
+    vec_st<D_>(L.lnw, p6, tid); vec_st<D_>(L.lnb, p7, tid); vec_st<D_>(L.bf3, p8, tid);
   }
-  {   // demographics (as user_head_fwd_kernel); the lead writes comb's trailing columns
-    const int r = tid >> 4, k0 = HD + 4 * (tid & 15), rr = min(r0 + r, a.B - 1);
+  if (tid < 256) {   // demographics (as user_head_fwd_kernel); the lead writes comb's trailing columns
+    const int r = tid >> 4, k0 = D_ + 4 * (tid & 15), rr = min(r0 + r, a.B - 1);
     const int64_t gi = clamp_id(a.gender[rr], a.ng, a.id_err, TTMI_IDERR_GENDER);
     const int64_t ci = clamp_id(a.country[rr], a.nc, a.id_err, TTMI_IDERR_COUNTRY);
     float v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int kk = k0 + e;
-      float gv = a.G[gi * a.dg + min(kk - HD, a.dg - 1)];
-      float cv = a.C[ci * a.dc + min(max(kk - HD - a.dg, 0), a.dc - 1)];
+      float gv = a.G[gi * a.dg + min(kk - D_, a.dg - 1)];
+      float cv = a.C[ci * a.dc + min(max(kk - D_ - a.dg, 0), a.dc - 1)];
       asm volatile("" : "+v"(gv), "+v"(cv));
-      v[e] = kk < HD + a.dg ? gv : (kk < W ? cv : 0.f);
+      v[e] = kk < D_ + a.dg ? gv : (kk < W ? cv : 0.f);
     }
-    st4_bf(L.sC + r * PW + k0 * 2, v);
+    st4_bf(L.sC + r * G::PW + k0 * 2, v);
     if (lead && k0 < W && r0 + r < a.B) st4_bf(reinterpret_cast<char*>(a.comb + (int64_t)(r0 + r) * W + k0), v);
   }
   if (lead && tid < HR && r0 + tid < a.B) a.rows[r0 + tid] = r0 + tid;
@@ -798,23 +890,23 @@ __global__ __launch_bounds__(256) void user_head_fwd_split_kernel(HeadArgs a) {
   STAMP(1);
   // ---- x1 = res + drop1(ctx·Woᵀ + bo); a2 = LN2(x1)   (every split; the lead stores them)
   f32x4_t v[2];
-  head_gemm<2, HD, PD>(L.sA, wo, v, lane);
-  WFrags<2, HD> w1s;
-  w1s.load(a.w1, HD, nh, lane, HD);
+  head_gemm<2, D_, G::PD>(L.sA, wo, v, lane);
+  WFrags<TH, D_> w1s;
+  w1s.load(a.w1, D_, nh, lane, D_);
   {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + 16 * t + 4 * g;
       float x[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = v[t][e] + Q.bo[n + e];
-      drop_apply_vec<4>(dk1, (uint32_t)(drow * HD + n), x);
+      for (int e = 0; e < 4; ++e) x[e] = v[t][e] + L.bo[n + e];
+      drop_apply_vec<4>(dk1, (uint32_t)(drow * D_ + n), x);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         x[e] += L.sX1[li][n + e];
         v[t][e] = x[e];
       }
-      if (lead && mrow) *reinterpret_cast<float4*>(a.x1 + (int64_t)m * HD + n) = make_float4(x[0], x[1], x[2], x[3]);
+      if (lead && mrow) *reinterpret_cast<float4*>(a.x1 + (int64_t)m * D_ + n) = make_float4(x[0], x[1], x[2], x[3]);
     }
     __syncthreads();                                 // every wave is done reading ctx and res
 #pragma unroll
@@ -822,48 +914,48 @@ __global__ __launch_bounds__(256) void user_head_fwd_split_kernel(HeadArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) L.sX1[li][n0 + 16 * t + 4 * g + e] = v[t][e];
     float mu, rs;
-    row_ln(v, Q.n2w, Q.n2b, a.eps, false, n0, L, w, lane, mu, rs);
+    split_row_ln<D_>(v, L.n2w, L.n2b, a.eps, false, n0, L.red, w, lane, mu, rs);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + 16 * t + 4 * g;
       const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
-      st4_bf(L.sA + li * PD + n * 2, x);
-      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.a2 + (int64_t)m * HD + n), x);
+      st4_bf(L.sA + li * G::PD + n * 2, x);
+      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.a2 + (int64_t)m * D_ + n), x);
     }
     if (lead && mrow && lane < 16 && w == 0) { a.m2[m] = mu; a.r2[m] = rs; }
   }
   __syncthreads();
   STAMP(2);
-  // ---- h[:, 128j ..) = dropf(relu(a2·W1ᵀ + b1)): the wave's 32 hidden units
+  // ---- h[:, 128j ..) = dropf(relu(a2·W1ᵀ + b1)): the wave's hidden units
   WFrags<2, 128> w2s;                                // W2[:, 128j .. 128j + 128): k window
   {
-    f32x4_t hv[2];
-    head_gemm<2, HD, PD>(L.sA, w1s, hv, lane);
+    f32x4_t hv[TH];
+    head_gemm<TH, D_, G::PD>(L.sA, w1s, hv, lane);
     w2s.load(a.w2 + 128 * j, F, n0, lane, 128);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < TH; ++t) {
       const int n = nh + 16 * t + 4 * g;
       float x[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = fmaxf(hv[t][e] + Q.b1[n + e], 0.f);
+      for (int e = 0; e < 4; ++e) x[e] = fmaxf(hv[t][e] + L.b1[n + e], 0.f);
       drop_apply_vec<4>(dkf, (uint32_t)(drow * F + n), x);
-      st4_bf(L.sH + li * PF + (n - 128 * j) * 2, x);
+      st4_bf(L.sH + li * G::PH + (n - 128 * j) * 2, x);
       if (mrow) st4_bf(reinterpret_cast<char*>(a.h + (int64_t)m * F + n), x);
     }
   }
   __syncthreads();
   STAMP(3);
   // ---- this split's FFN2 partial -> exchange slot (rb, j); the last arriver goes on
-  head_gemm<2, 128, PF>(L.sH, w2s, v, lane);
+  head_gemm<2, 128, G::PH>(L.sH, w2s, v, lane);
   STAMP(4);
   // fusion_layer.0's fragments before the handoff (every split: their L2 round trip then
   // overlaps the exchange's instead of following it)
-  WFrags<2, WPAD> wf0;
+  WFrags<2, G::WPAD> wf0;
   wf0.load(a.wf0, W, n0, lane, W);
-  float* const part = a.ffn_part + (int64_t)rb * NS * HR * HD;      // [NS][HR][HD]
+  float* const part = a.ffn_part + (int64_t)rb * NS * HR * D_;      // [NS][HR][D]
 #pragma unroll
   for (int t = 0; t < 2; ++t)
-    st16_wt(part, (uint32_t)(((j * HR + li) * HD + n0 + 16 * t + 4 * g) * 4),
+    st16_wt(part, (uint32_t)(((j * HR + li) * D_ + n0 + 16 * t + 4 * g) * 4),
             make_float4(v[t][0], v[t][1], v[t][2], v[t][3]));
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -874,13 +966,13 @@ __global__ __launch_bounds__(256) void user_head_fwd_split_kernel(HeadArgs a) {
   if (tid == 0) __hip_atomic_store(a.ffn_cnt + rb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   STAMP(5);
   {
-    // x2 = x1 + drop2(Σ_j partial_j + b2), summed in split order -> comb[:, :128]
+    // x2 = x1 + drop2(Σ_j partial_j + b2), summed in split order -> comb[:, :D]
     float4 pp[NS][2];
 #pragma unroll
     for (int jj = 0; jj < NS; ++jj)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        pp[jj][t] = ld16_wt(part, (uint32_t)(((jj * HR + li) * HD + n0 + 16 * t + 4 * g) * 4));
+        pp[jj][t] = ld16_wt(part, (uint32_t)(((jj * HR + li) * D_ + n0 + 16 * t + 4 * g) * 4));
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + 16 * t + 4 * g;
@@ -890,52 +982,52 @@ __global__ __launch_bounds__(256) void user_head_fwd_split_kernel(HeadArgs a) {
         x[0] += pp[jj][t].x; x[1] += pp[jj][t].y; x[2] += pp[jj][t].z; x[3] += pp[jj][t].w;
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] += Q.b2[n + e];
-      drop_apply_vec<4>(dk2, (uint32_t)(drow * HD + n), x);
+      for (int e = 0; e < 4; ++e) x[e] += L.b2[n + e];
+      drop_apply_vec<4>(dk2, (uint32_t)(drow * D_ + n), x);
 #pragma unroll
       for (int e = 0; e < 4; ++e) x[e] += L.sX1[li][n + e];
-      st4_bf(L.sC + li * PW + n * 2, x);
+      st4_bf(L.sC + li * G::PW + n * 2, x);
       if (mrow) st4_bf(reinterpret_cast<char*>(a.comb + (int64_t)m * W + n), x);
     }
   }
   __syncthreads();
   STAMP(6);
   // ---- z = comb·Wf0ᵀ + bf0; az = relu(LN(z))
-  head_gemm<2, WPAD, PW>(L.sC, wf0, v, lane);
-  WFrags<2, HD> wf3;
-  wf3.load(a.wf3, HD, n0, lane, HD);
+  head_gemm<2, G::WPAD, G::PW>(L.sC, wf0, v, lane);
+  WFrags<2, D_> wf3;
+  wf3.load(a.wf3, D_, n0, lane, D_);
   {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + 16 * t + 4 * g;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[t][e] += Q.bf0[n + e];
-      if (mrow) *reinterpret_cast<float4*>(a.z + (int64_t)m * HD + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
+      for (int e = 0; e < 4; ++e) v[t][e] += L.bf0[n + e];
+      if (mrow) *reinterpret_cast<float4*>(a.z + (int64_t)m * D_ + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
     }
     float mu, rs;
-    row_ln(v, Q.lnw, Q.lnb, a.eps, true, n0, L, w, lane, mu, rs);
+    split_row_ln<D_>(v, L.lnw, L.lnb, a.eps, true, n0, L.red, w, lane, mu, rs);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + 16 * t + 4 * g;
       const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
-      st4_bf(L.sA + li * PD + n * 2, x);
-      if (mrow) st4_bf(reinterpret_cast<char*>(a.az + (int64_t)m * HD + n), x);
+      st4_bf(L.sA + li * G::PD + n * 2, x);
+      if (mrow) st4_bf(reinterpret_cast<char*>(a.az + (int64_t)m * D_ + n), x);
     }
     if (mrow && lane < 16 && w == 0) { a.mz[m] = mu; a.rz[m] = rs; }
   }
   __syncthreads();
   // ---- u = az·Wf3ᵀ + bf3
-  head_gemm<2, HD, PD>(L.sA, wf3, v, lane);
+  head_gemm<2, D_, G::PD>(L.sA, wf3, v, lane);
   float uo[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n = n0 + 16 * t + 4 * g;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) uo[t][e] = v[t][e] + Q.bf3[n + e];
+    for (int e = 0; e < 4; ++e) uo[t][e] = v[t][e] + L.bf3[n + e];
     if (mrow)
-      *reinterpret_cast<float4*>(a.u + (int64_t)m * HD + n) = make_float4(uo[t][0], uo[t][1], uo[t][2], uo[t][3]);
+      *reinterpret_cast<float4*>(a.u + (int64_t)m * D_ + n) = make_float4(uo[t][0], uo[t][1], uo[t][2], uo[t][3]);
   }
-  row_l2norm(uo, a.uhat, a.unrm, m, mrow, n0, L, w, lane);
+  split_row_l2norm<D_>(uo, a.uhat, a.unrm, m, mrow, n0, L.red, w, lane);
   STAMP(7);
 }
 
@@ -1283,37 +1375,95 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
 
 // ---- the FFN split over its hidden units (ABI 21, ttmi_user_head_bwd_desc::ffn_ws), as the
 // forward's: row block rb on NS = F / 128 workgroups j.  Each runs the fusion MLP's backward
-// (daz, the ReLU-gated LayerNorm backward, dcomb, dy2: 76 KB of weights, redundantly; the lead
-// split stores what they all compute alike), the hidden units [128 j, 128 j + 128) of
-// dz1 = (dy2·W2) ⊙ gate and their partial dz1·W1 (32 + 32 KB), handed over like the forward's
-// partial; the last to arrive sums the partials in split order, then runs LN2's backward, the
-// residual, drop1, dctx = dy1·Wo and the dG / dC adds.
-template <int F>
-__global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a) {
-  constexpr int NS = F / 128;
+// (daz, the ReLU-gated LayerNorm backward, dcomb, dy2: 76 KB of weights at D = 128, redundantly;
+// the lead split stores what they all compute alike), the hidden units [128 j, 128 j + 128) of
+// dz1 = (dy2·W2) ⊙ gate and their partial dz1·W1, handed over like the forward's partial; the
+// last to arrive sums the partials in split order, then runs LN2's backward, the residual,
+// drop1, dctx = dy1·Wo and the dG / dC adds.  D = 128 (4 waves) or 256 (8 waves, F = 1024).
+template <int D_>
+struct SplitBwdLds {
+  static constexpr int NW = D_ / 32;
+  char sA[HR * SplitGeo<D_>::PD];   // du, then dz, then dy2, then dy1
+  char sH[HR * SplitGeo<D_>::PH];   // the split's dz1 columns
+  float sX[HR][D_ + 4];             // dx2 (fp32 residual of dx1)
+  float sW[HR][D_ + 4];             // LayerNorm weight-gradient terms dy·x̂ (column sums)
+  float sB[HR][D_ + 4];             // ... and dy
+  float sDem[HR][48];               // dcomb's demographic columns (dG, dC rows)
+  int sGi[HR], sCi[HR];
+  float red[NW][HR];
+};
+// ln_bwd16 over D_ columns and NW waves (same arithmetic and order at D = 128).
+template <int D_>
+TTMI_DEV void split_ln_bwd(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, float rs, const float (&wv)[2][4],
+                           int n0, bool mrow, SplitBwdLds<D_>& L, int w, int lane, float* wsw, float* wsb,
+                           bool sums) {
+  constexpr int NW = D_ / 32;
+  const int g = lane >> 4, li = lane & 15;
+  float xh[2][4], gg[2][4];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = mrow ? dy[t][e] : 0.f;
+      xh[t][e] = (xs[t][e] - mu) * rs;
+      L.sW[li][n + e] = d * xh[t][e];
+      L.sB[li][n + e] = d;
+      gg[t][e] = d * wv[t][e];
+      s1 += gg[t][e];
+      s2 += gg[t][e] * xh[t][e];
+    }
+  }
+  const float c1 = split_row_sum<NW>(s1, L.red, w, lane) * (1.f / D_);   // (its barriers publish sW, sB)
+  const float c2 = split_row_sum<NW>(s2, L.red, w, lane) * (1.f / D_);
+  if (sums && threadIdx.x < D_) {                    // one column per thread, rows in order
+    const int c = threadIdx.x;
+    float cw = 0.f, cb = 0.f;
+#pragma unroll
+    for (int r = 0; r < HR; ++r) { cw += L.sW[r][c]; cb += L.sB[r][c]; }
+    wsw[c] = cw;
+    wsb[c] = cb;
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dy[t][e] = rs * (gg[t][e] - c1 - xh[t][e] * c2);
+}
+
+template <int D_, int F>
+__global__ __launch_bounds__(D_ * 2) void user_head_bwd_split_kernel(HeadBwdArgs a) {
+  using G = SplitGeo<D_>;
+  constexpr int NS = F / 128, NW = G::NW, TH = G::TH;
   STAMP(0);
-  __shared__ __attribute__((aligned(16))) HeadBwdLds L;
+  __shared__ __attribute__((aligned(16))) union {
+    SplitBwdLds<D_> s;
+    HeadBwdLds ic;
+  } U;
+  SplitBwdLds<D_>& L = U.s;
   __shared__ int s_last;
   const int nsplit = a.nbu * NS;
-  if ((int)blockIdx.x >= nsplit) {                  // co-launched item head backward (rows)
-    item_c_bwd_body(a.it, (int)blockIdx.x - nsplit, L);
-    return;
+  if constexpr (D_ == HD) {
+    if ((int)blockIdx.x >= nsplit) {                // co-launched item head backward (rows)
+      item_c_bwd_body(a.it, (int)blockIdx.x - nsplit, U.ic);
+      return;
+    }
   }
   const int rb = (int)blockIdx.x / NS, j = (int)blockIdx.x % NS;
   const bool lead = j == 0;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = rb * HR, m = r0 + li, mc = min(m, a.B - 1);
   const bool mrow = m < a.B;
-  const int W = HD + a.dg + a.dc;
+  const int W = D_ + a.dg + a.dc;
   const int n0 = w * 32;
-  const int nh = 128 * j + 32 * w;                   // this wave's 32 of the split's hidden units
-  float* wsb = a.ws + (int64_t)rb * 4 * HD;          // the row block's four sum rows
-  WFrags<2, HD> wf3;
-  wf3.load(a.wf3t, HD, n0, lane, HD);
+  const int nh = 128 * j + 16 * TH * w;              // this wave's hidden units of the split
+  float* wsb = a.ws + (int64_t)rb * 4 * D_;          // the row block's four sum rows
+  WFrags<2, D_> wf3;
+  wf3.load(a.wf3t, D_, n0, lane, D_);
   {                                                  // du rows -> LDS
-    const int r = tid >> 4, ch = tid & 15;
-    *reinterpret_cast<uint4*>(L.sA + r * PD + ch * 16) =
-        *reinterpret_cast<const uint4*>(a.du + (int64_t)min(r0 + r, a.B - 1) * HD + ch * 8);
+    const int r = tid / (D_ / 8), ch = tid % (D_ / 8);
+    *reinterpret_cast<uint4*>(L.sA + r * G::PD + ch * 16) =
+        *reinterpret_cast<const uint4*>(a.du + (int64_t)min(r0 + r, a.B - 1) * D_ + ch * 8);
   }
   const int drow = a.drows[mc];
   const float mzr = a.mz[mc], rzr = a.rz[mc], m2r = a.m2[mc], r2r = a.r2[mc];
@@ -1333,27 +1483,27 @@ __global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a)
     const float4 nw = *reinterpret_cast<const float4*>(a.n2w + n);
     lnw[t][0] = lw.x; lnw[t][1] = lw.y; lnw[t][2] = lw.z; lnw[t][3] = lw.w;
     n2w[t][0] = nw.x; n2w[t][1] = nw.y; n2w[t][2] = nw.z; n2w[t][3] = nw.w;
-    azq[t] = *reinterpret_cast<const uint2*>(a.az + (int64_t)mc * HD + n);
-    const float4 zv = *reinterpret_cast<const float4*>(a.z + (int64_t)mc * HD + n);
-    const float4 xv = *reinterpret_cast<const float4*>(a.x1 + (int64_t)mc * HD + n);
+    azq[t] = *reinterpret_cast<const uint2*>(a.az + (int64_t)mc * D_ + n);
+    const float4 zv = *reinterpret_cast<const float4*>(a.z + (int64_t)mc * D_ + n);
+    const float4 xv = *reinterpret_cast<const float4*>(a.x1 + (int64_t)mc * D_ + n);
     zs[t][0] = zv.x; zs[t][1] = zv.y; zs[t][2] = zv.z; zs[t][3] = zv.w;
     x1s[t][0] = xv.x; x1s[t][1] = xv.y; x1s[t][2] = xv.z; x1s[t][3] = xv.w;
   }
-  uint2 hq[2];                                       // the wave's 32 gate columns, 4 per lane
+  uint2 hq[TH];                                      // the wave's gate columns, 4 per lane
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < TH; ++q)
     hq[q] = *reinterpret_cast<const uint2*>(a.h + (int64_t)mc * F + nh + 16 * q + 4 * g);
   __syncthreads();
   STAMP(1);
   // ---- daz = du·Wf3; dz = LNᵀ(daz ⊙ [az > 0])
   f32x4_t v[2];
-  head_gemm<2, HD, PD>(L.sA, wf3, v, lane);
-  WFrags<3, HD> wf0;                                 // dcomb's 11 column tiles: w, w+4, w+8
+  head_gemm<2, D_, G::PD>(L.sA, wf3, v, lane);
+  WFrags<3, D_> wf0;                                 // dcomb's W / 16 column tiles: w, w+NW, w+2NW
 #pragma unroll
   for (int jj = 0; jj < 3; ++jj) {
-    const int tj = min(w + 4 * jj, W / 16 - 1);
+    const int tj = min(w + NW * jj, W / 16 - 1);
 #pragma unroll
-    for (int c = 0; c < HD / 32; ++c) wf0.f[c][jj] = wfrag(a.wf0t, HD, 16 * tj + li, c, lane, HD);
+    for (int c = 0; c < D_ / 32; ++c) wf0.f[c][jj] = wfrag(a.wf0t, D_, 16 * tj + li, c, lane, D_);
   }
   {
 #pragma unroll
@@ -1365,33 +1515,33 @@ __global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a)
       for (int e = 0; e < 4; ++e) v[t][e] = gz[e] > 0.f ? v[t][e] : 0.f;
     }
     __syncthreads();                                 // every wave is done reading du
-    ln_bwd16(v, zs, mzr, rzr, lnw, n0, mrow, L, w, lane, wsb, wsb + HD, lead);   // (the lead's sums)
+    split_ln_bwd<D_>(v, zs, mzr, rzr, lnw, n0, mrow, L, w, lane, wsb, wsb + D_, lead);   // (the lead's sums)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + 16 * t + 4 * g;
       const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
-      st4_bf(L.sA + li * PD + n * 2, x);
-      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.dz16 + (int64_t)m * HD + n), x);
+      st4_bf(L.sA + li * G::PD + n * 2, x);
+      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.dz16 + (int64_t)m * D_ + n), x);
     }
   }
   __syncthreads();
   STAMP(2);
   // ---- dcomb = dz·Wf0: columns < D -> dx2 (LDS), the demographic ones -> sDem
-  WFrags<2, HD> w2s;                                 // W2ᵀ rows of the wave's hidden units
+  WFrags<TH, D_> w2s;                                // W2ᵀ rows of the wave's hidden units
   {
     f32x4_t dc[3];
-    head_gemm<3, HD, PD>(L.sA, wf0, dc, lane);
-    w2s.load(a.w2t, HD, nh, lane, HD);
+    head_gemm<3, D_, G::PD>(L.sA, wf0, dc, lane);
+    w2s.load(a.w2t, D_, nh, lane, D_);
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) {
-      const int tj = w + 4 * jj;
+      const int tj = w + NW * jj;
       if (tj >= W / 16) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = 16 * tj + 4 * g + e;
         const float val = dc[jj][e];
-        if (k < HD) L.sX[li][k] = mrow ? val : 0.f;
-        else L.sDem[li][k - HD] = val;
+        if (k < D_) L.sX[li][k] = mrow ? val : 0.f;
+        else L.sDem[li][k - D_] = val;
       }
     }
   }
@@ -1405,9 +1555,9 @@ __global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a)
       float x[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) x[e] = L.sX[li][n + 16 * t + e];
-      drop_apply_vec<4>(dk2, (uint32_t)(drow * HD + n + 16 * t), x);
-      st4_bf(L.sA + li * PD + (n + 16 * t) * 2, x);
-      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.dy2 + (int64_t)m * HD + n + 16 * t), x);
+      drop_apply_vec<4>(dk2, (uint32_t)(drow * D_ + n + 16 * t), x);
+      st4_bf(L.sA + li * G::PD + (n + 16 * t) * 2, x);
+      if (lead && mrow) st4_bf(reinterpret_cast<char*>(a.dy2 + (int64_t)m * D_ + n + 16 * t), x);
     }
   }
   __syncthreads();
@@ -1415,11 +1565,11 @@ __global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a)
   // ---- dz1[:, 128j ..) = (dy2·W2) ⊙ [h > 0]·sf
   WFrags<2, 128> w1s;                                // W1ᵀ[:, 128j .. 128j + 128): k window
   {
-    f32x4_t hv[2];
-    head_gemm<2, HD, PD>(L.sA, w2s, hv, lane);
+    f32x4_t hv[TH];
+    head_gemm<TH, D_, G::PD>(L.sA, w2s, hv, lane);
     w1s.load(a.w1t + 128 * j, F, n0, lane, 128);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < TH; ++t) {
       const int n = nh + 16 * t + 4 * g;
       const uint2 q = hq[t];
       const float hg[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
@@ -1427,20 +1577,20 @@ __global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a)
       float x[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) x[e] = hg[e] > 0.f ? hv[t][e] * a.sf : 0.f;
-      st4_bf(L.sH + li * PF + (n - 128 * j) * 2, x);
+      st4_bf(L.sH + li * G::PH + (n - 128 * j) * 2, x);
       if (mrow) st4_bf(reinterpret_cast<char*>(a.dz1 + (int64_t)m * F + n), x);
     }
   }
   __syncthreads();
   STAMP(5);
   // ---- this split's partial dz1·W1 -> exchange slot (rb, j); the last arriver goes on
-  head_gemm<2, 128, PF>(L.sH, w1s, v, lane);
-  WFrags<2, HD> wo;                                  // (before the handoff, as the forward's wf0)
-  wo.load(a.wot, HD, n0, lane, HD);
-  float* const part = a.ffn_part + (int64_t)rb * NS * HR * HD;      // [NS][HR][HD]
+  head_gemm<2, 128, G::PH>(L.sH, w1s, v, lane);
+  WFrags<2, D_> wo;                                  // (before the handoff, as the forward's wf0)
+  wo.load(a.wot, D_, n0, lane, D_);
+  float* const part = a.ffn_part + (int64_t)rb * NS * HR * D_;      // [NS][HR][D]
 #pragma unroll
   for (int t = 0; t < 2; ++t)
-    st16_wt(part, (uint32_t)(((j * HR + li) * HD + n0 + 16 * t + 4 * g) * 4),
+    st16_wt(part, (uint32_t)(((j * HR + li) * D_ + n0 + 16 * t + 4 * g) * 4),
             make_float4(v[t][0], v[t][1], v[t][2], v[t][3]));
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -1457,7 +1607,7 @@ __global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a)
     for (int jj = 0; jj < NS; ++jj)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        pp[jj][t] = ld16_wt(part, (uint32_t)(((jj * HR + li) * HD + n0 + 16 * t + 4 * g) * 4));
+        pp[jj][t] = ld16_wt(part, (uint32_t)(((jj * HR + li) * D_ + n0 + 16 * t + 4 * g) * 4));
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       v[t] = f32x4_t{pp[0][t].x, pp[0][t].y, pp[0][t].z, pp[0][t].w};
@@ -1467,29 +1617,29 @@ __global__ __launch_bounds__(256) void user_head_bwd_split_kernel(HeadBwdArgs a)
       }
     }
   }
-  ln_bwd16(v, x1s, m2r, r2r, n2w, n0, mrow, L, w, lane, wsb + 2 * HD, wsb + 3 * HD);
+  split_ln_bwd<D_>(v, x1s, m2r, r2r, n2w, n0, mrow, L, w, lane, wsb + 2 * D_, wsb + 3 * D_, true);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n = n0 + 16 * t + 4 * g;
     float x[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) x[e] = v[t][e] + L.sX[li][n + e];
-    if (mrow) *reinterpret_cast<float4*>(a.dx1 + (int64_t)m * HD + n) = make_float4(x[0], x[1], x[2], x[3]);
-    drop_apply_vec<4>(dk1, (uint32_t)(drow * HD + n), x);
-    st4_bf(L.sA + li * PD + n * 2, x);               // every wave is past its dy2 reads
-    if (mrow) st4_bf(reinterpret_cast<char*>(a.dy1 + (int64_t)m * HD + n), x);
+    if (mrow) *reinterpret_cast<float4*>(a.dx1 + (int64_t)m * D_ + n) = make_float4(x[0], x[1], x[2], x[3]);
+    drop_apply_vec<4>(dk1, (uint32_t)(drow * D_ + n), x);
+    st4_bf(L.sA + li * G::PD + n * 2, x);            // every wave is past its dy2 reads
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dy1 + (int64_t)m * D_ + n), x);
   }
   __syncthreads();
   // ---- dctx = dy1·Wo
-  head_gemm<2, HD, PD>(L.sA, wo, v, lane);
+  head_gemm<2, D_, G::PD>(L.sA, wo, v, lane);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n = n0 + 16 * t + 4 * g;
     const float x[4] = {v[t][0], v[t][1], v[t][2], v[t][3]};
-    if (mrow) st4_bf(reinterpret_cast<char*>(a.dctx + (int64_t)m * HD + n), x);
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dctx + (int64_t)m * D_ + n), x);
   }
-  // ---- dG / dC (as user_head_bwd_kernel)
-  if (lane < 48) {
+  // ---- dG / dC (as user_head_bwd_kernel; lanes < 48 of waves 0-3 issue the rows)
+  if (lane < 48 && w < 4) {
     const bool isg = lane < 16;
     const int k = isg ? lane : lane - 16;
     const int nr = min(HR, a.B - r0);
@@ -1646,8 +1796,15 @@ int64_t ffn_cnt_bytes(int B) { return ((int64_t)((B + HR - 1) / HR) * 4 + 255) /
 int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_desc* it, int stage,
                             hipStream_t s) {
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_fwd: null descriptor");
-  TTMI_REQUIRE(d->B > 0 && d->D == HD, "ttmi_user_head_fwd: needs D == %d", HD);
-  TTMI_REQUIRE(d->F > 0 && d->F <= FMAX && d->F % 256 == 0, "ttmi_user_head_fwd: needs F %% 256 == 0, F <= %d", FMAX);
+  // D = 128 with F in {256, 512}; D = 256 with F = 1024 on the split kernel only (the
+  // reference's default width), without item head co-launches
+  const bool d256 = d->D == 2 * HD && d->F == 4 * 2 * HD;
+  TTMI_REQUIRE(d->B > 0 && (d->D == HD || d256), "ttmi_user_head_fwd: needs D == %d, or D == %d with F == %d",
+               HD, 2 * HD, 8 * HD);
+  TTMI_REQUIRE(d256 || (d->F > 0 && d->F <= FMAX && d->F % 256 == 0),
+               "ttmi_user_head_fwd: needs F %% 256 == 0, F <= %d", FMAX);
+  TTMI_REQUIRE(!d256 || (d->ffn_ws && !it && !getenv("TTMI_HEAD_NOSPLIT")),
+               "ttmi_user_head_fwd: D == 256 runs the FFN split only (ffn_ws, no item co-launch)");
   TTMI_REQUIRE(d->dg == 16 && d->dc == 32, "ttmi_user_head_fwd: demographic widths must be 16 and 32");
   TTMI_REQUIRE(d->n_genders > 0 && d->n_countries > 0, "ttmi_user_head_fwd: n_genders / n_countries must be > 0");
   TTMI_REQUIRE(d->ctx && d->res && d->drop_rows && d->wo && d->bo && d->n2w && d->n2b && d->w1 && d->b1 && d->w2 &&
@@ -1695,8 +1852,9 @@ int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_d
     a.ffn_cnt = static_cast<int*>(d->ffn_ws);
     a.ffn_part = reinterpret_cast<float*>(static_cast<char*>(d->ffn_ws) + ffn_cnt_bytes(d->B));
     const dim3 grid((unsigned)(a.nbu * (d->F / 128) + extra));
-    if (d->F == 512) hipLaunchKernelGGL(user_head_fwd_split_kernel<512>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(user_head_fwd_split_kernel<256>, grid, dim3(256), 0, s, a);
+    if (d->D == 256) hipLaunchKernelGGL((user_head_fwd_split_kernel<256, 1024>), grid, dim3(512), 0, s, a);
+    else if (d->F == 512) hipLaunchKernelGGL((user_head_fwd_split_kernel<128, 512>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((user_head_fwd_split_kernel<128, 256>), grid, dim3(256), 0, s, a);
     return ttmi_check_launch("ttmi_user_head_fwd");
   }
   const dim3 grid((unsigned)(a.nbu + extra));
@@ -1755,20 +1913,25 @@ extern "C" int ttmi_mha_q1_gather_item_fwd(int dtype, int B, int L, int H, int D
 
 extern "C" int64_t ttmi_user_head_ffn_ws_bytes(int B, int F) {
   if (B <= 0 || F <= 0 || F % 128) return 0;
-  return ffn_cnt_bytes(B) + (int64_t)((B + HR - 1) / HR) * (F / 128) * HR * HD * 4;
+  return ffn_cnt_bytes(B) + (int64_t)((B + HR - 1) / HR) * (F / 128) * HR * 2 * HD * 4;   // D <= 256
 }
 
 extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
   return ttmi_user_item_head_fwd(d, nullptr, s);
 }
 
-extern "C" int64_t ttmi_user_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 4 * HD; }
+// (sized for D = 256: the D = 128 layout uses its first half)
+extern "C" int64_t ttmi_user_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 4 * 2 * HD; }
 
 extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const ttmi_item_head_bwd_desc* it,
                                        hipStream_t s) {
   TTMI_REQUIRE(d != nullptr, "ttmi_user_head_bwd: null descriptor");
-  TTMI_REQUIRE(d->B > 0 && d->D == HD && (d->F == 256 || d->F == 512) && d->dg == 16 && d->dc == 32,
-               "ttmi_user_head_bwd: needs D == %d, F in {256, 512}, dg == 16, dc == 32", HD);
+  const bool d256 = d->D == 2 * HD && d->F == 8 * HD;
+  TTMI_REQUIRE(d->B > 0 && ((d->D == HD && (d->F == 256 || d->F == 512)) || d256) && d->dg == 16 && d->dc == 32,
+               "ttmi_user_head_bwd: needs D == %d with F in {256, 512} (or D == %d with F == %d), dg == 16, dc == 32",
+               HD, 2 * HD, 8 * HD);
+  TTMI_REQUIRE(!d256 || (d->ffn_ws && !it && !getenv("TTMI_HEAD_NOSPLIT")),
+               "ttmi_user_head_bwd: D == 256 runs the FFN split only (ffn_ws, no item co-launch)");
   TTMI_REQUIRE(d->n_genders > 0 && d->n_countries > 0, "ttmi_user_head_bwd: n_genders / n_countries must be > 0");
   TTMI_REQUIRE(d->du && d->az && d->z && d->mz && d->rz && d->h && d->x1 && d->m2 && d->r2 &&
                d->drop_rows && d->gender && d->country && d->wf3t && d->wf0t && d->w2t && d->w1t &&
@@ -1801,8 +1964,9 @@ extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const t
     a.ffn_cnt = static_cast<int*>(d->ffn_ws);
     a.ffn_part = reinterpret_cast<float*>(static_cast<char*>(d->ffn_ws) + ffn_cnt_bytes(d->B));
     const dim3 grid((unsigned)(a.nbu * (d->F / 128) + extra));
-    if (d->F == 512) hipLaunchKernelGGL(user_head_bwd_split_kernel<512>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(user_head_bwd_split_kernel<256>, grid, dim3(256), 0, s, a);
+    if (d256) hipLaunchKernelGGL((user_head_bwd_split_kernel<256, 1024>), grid, dim3(512), 0, s, a);
+    else if (d->F == 512) hipLaunchKernelGGL((user_head_bwd_split_kernel<128, 512>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((user_head_bwd_split_kernel<128, 256>), grid, dim3(256), 0, s, a);
     return ttmi_check_launch("ttmi_user_head_bwd");
   }
   const dim3 grid((unsigned)(a.nbu + extra));

@@ -1376,9 +1376,8 @@ def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: 
     o = dict(dz16=torch.empty(B, D, device=dev, dtype=bf), dy2=torch.empty(B, D, device=dev, dtype=bf),
              dz1=torch.empty(B, F, device=dev, dtype=bf), dx1=torch.empty(B, D, device=dev),
              dy1=torch.empty(B, D, device=dev, dtype=bf), dctx=torch.empty(B, D, device=dev, dtype=bf))
-    _L.load()
-    nws = int(_L._lib.ttmi_user_head_bwd_ws_floats(B))
-    ws = torch.empty(nws, device=dev)
+    nblk = (B + 15) // 16
+    ws = torch.empty(nblk * 4 * D, device=dev)      # [nblk][4][D] column sums
     d = UserHeadBwdDesc()
     d.B, d.D, d.F = B, D, F
     d.dg, d.dc = P["gender_embedding.weight"].shape[1], P["country_embedding.weight"].shape[1]
@@ -1407,7 +1406,7 @@ def user_head_bwd(du16: Tensor, saved: Dict[str, Tensor], drop_rows: Tensor, W: 
         call("ttmi_user_head_bwd", ctypes.byref(d), _s())
     else:      # the item head's row-local backward on the idle CUs (ABI 15)
         call("ttmi_user_item_head_bwd", ctypes.byref(d), ctypes.byref(co_item), _s())
-    ln_sum_folds(ws, ln_grads, 4, D)
+    ln_sum_folds(ws, ln_grads, 4, D, S=nblk)
     fx_folds([(aG, dG), (aC, dC)])
     return o
 
@@ -1421,9 +1420,12 @@ def user_head_bwd_fusable(W: Dict[str, Tensor], pre: str) -> bool:
 
 def user_head_fusable(W: Dict[str, Tensor], P: Dict[str, Tensor], pre: str, D: int,
                       dtype) -> bool:
-    """Shapes ttmi_user_head_fwd takes (include/ttmi.h)."""
+    """Shapes ttmi_user_head_fwd takes (include/ttmi.h): D = 128 with F in {256, 512}, or the
+    reference's default width D = 256 with F = 1024 (the FFN-split kernels only, ABI 21)."""
     F = W[pre + "linear1.weight"].shape[0]
-    return (dtype == torch.bfloat16 and D == 128 and F % 256 == 0 and F <= 512 and
+    shape_ok = (D == 128 and F % 256 == 0 and F <= 512) or \
+        (D == 256 and F == 1024 and not os.environ.get("TTMI_HEAD_NOSPLIT"))
+    return (dtype == torch.bfloat16 and shape_ok and
             P["gender_embedding.weight"].shape[1] == 16 and
             P["country_embedding.weight"].shape[1] == 32 and
             all(W[n].dtype == torch.bfloat16 for n in (

@@ -328,14 +328,15 @@ def assert_bit_equal(a, b):
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_cfg2_graph_equals_eager_bitexact(gpu_pkg, p):
+@pytest.mark.parametrize("D,p", [(128, 0.0), (128, 0.1), (256, 0.1)])
+def test_cfg2_graph_equals_eager_bitexact(gpu_pkg, D, p):
     """The benchmarked step (cfg 2: B 512, L 50, D 128, V 10,136, bf16) is deterministic: the
     HIP-graph replay and the eager schedule give bit-identical losses, parameters, BatchNorm
     buffers and AdamW moments for 3 steps (every cross-workgroup sum is fixed-order or int64
-    fixed point: the embedding scatter, the LN / BN column sums, the split weight gradients)."""
-    m1, batch = _cfg2(gpu_pkg, torch.bfloat16, p=p, seed=7)
-    m2, _ = _cfg2(gpu_pkg, torch.bfloat16, p=p, seed=7)
+    fixed point: the embedding scatter, the LN / BN column sums, the split weight gradients).
+    D = 256 (the reference's default width) runs the FFN-split user head at its own width."""
+    m1, batch = _cfg2(gpu_pkg, torch.bfloat16, D=D, p=p, seed=7)
+    m2, _ = _cfg2(gpu_pkg, torch.bfloat16, D=D, p=p, seed=7)
     bd = {k: v.to(DEV) for k, v in batch.items()}
     s1 = gpu_pkg.TrainStep(m1, lr=1e-3, use_graph=True, seed=11)
     s2 = gpu_pkg.TrainStep(m2, lr=1e-3, use_graph=False, seed=11)
