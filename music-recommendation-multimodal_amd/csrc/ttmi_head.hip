@@ -31,6 +31,7 @@ constexpr int PI = (IK + 8) * 2;       // LDS pitch of a bf16 row of 512
 
 struct ItemArgs {
   int B;
+  int D;                       // output width (fusion_layer.4 rows): 128 or 256 (ABI 21)
   const float* modal; const bf16_t* w0; const float* b0;
   const bf16_t* y1; const bf16_t* w4; const float* b4; const float* lnw; const float* lnb; float ln_eps;
   bf16_t* m16; float* z; float* y2; float* out; float* m5; float* r5;
@@ -58,6 +59,7 @@ struct ItemLdsA {
 // fusion_layer.5 and the input gradient of fusion_layer.4 on 16 rows per workgroup.
 struct ItemBwdArgs {
   int B;
+  int D;
   const float* dout; const float* y2; const float* m5; const float* r5; const float* lnw;
   const bf16_t* w4t;
   bf16_t* dy2; float* dy1; float* ws;
@@ -361,18 +363,96 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   TTMI_TSTAMP(2);
 }
 
-struct ItemLdsC {
-  char sY[HR * PI];
-  float red[4][HR];
+// ---- per-width geometry and row reductions of the D-templated head kernels (D = 128 / 256)
+template <int D_>
+struct SplitGeo {
+  static constexpr int NW = D_ / 32;                 // waves
+  static constexpr int PD = (D_ + 8) * 2;            // LDS pitches (bytes)
+  static constexpr int PH = (128 + 8) * 2;           // the split's 128 hidden units
+  static constexpr int WPAD = (D_ + 48 + 31) / 32 * 32;
+  static constexpr int PW = (WPAD + 8) * 2;
+  static constexpr int TH = 128 / 16 / NW;           // hidden 16-column tiles per wave
 };
+// Row sum over the D columns held by the 4 lanes of row li in each of NW waves (in wave order).
+template <int NW>
+TTMI_DEV float split_row_sum(float s, float (*red)[HR], int w, int lane) {
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  if (lane < 16) red[w][lane] = s;
+  __syncthreads();
+  const int li = lane & 15;
+  float tot = red[0][li];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) tot += red[k][li];
+  __syncthreads();
+  return tot;
+}
+template <int D_>
+TTMI_DEV void split_row_ln(f32x4_t (&v)[2], const float* w_, const float* b_, float eps, bool relu, int n0,
+                           float (*red)[HR], int w, int lane, float& mu, float& rs) {
+  constexpr int NW = SplitGeo<D_>::NW;
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[t][e];
+  mu = split_row_sum<NW>(s, red, w, lane) * (1.f / D_);
+  float q = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[t][e] - mu;
+      q += d * d;
+    }
+  rs = 1.f / sqrtf(split_row_sum<NW>(q, red, w, lane) * (1.f / D_) + eps);
+  const int g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + 16 * t + 4 * g + e;
+      float o = (v[t][e] - mu) * rs * w_[n] + b_[n];
+      v[t][e] = relu ? fmaxf(o, 0.f) : o;
+    }
+}
+template <int D_>
+TTMI_DEV void split_row_l2norm(const float (&x)[2][4], float* xhat, float* nrm, int m, bool mrow, int n0,
+                               float (*red)[HR], int w, int lane) {
+  if (xhat == nullptr) return;                       // uniform: a kernel argument
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += x[t][e] * x[t][e];
+  const float nr = sqrtf(split_row_sum<SplitGeo<D_>::NW>(s, red, w, lane));
+  const float inv = 1.f / fmaxf(nr, 1e-12f);
+  const int g = lane >> 4;
+  if (mrow) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      *reinterpret_cast<float4*>(xhat + (int64_t)m * D_ + n0 + 16 * t + 4 * g) =
+          make_float4(x[t][0] * inv, x[t][1] * inv, x[t][2] * inv, x[t][3] * inv);
+    if (lane < 16 && w == 0) nrm[m] = nr;
+  }
+}
+
+template <int D_>
+struct ItemLdsCT {
+  char sY[HR * PI];
+  float red[D_ / 32][HR];
+};
+using ItemLdsC = ItemLdsCT<HD>;
 
 // Item head stage C on row block bx (item_head_c_kernel, or the workgroups of
 // ttmi_user_item_head_fwd_c past the user head's).
-template <bool FIN>
-TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
+// D_ = 128 (4 waves) or 256 (8 waves): a wave owns 32 of the D_ output columns.
+template <bool FIN, int D_ = HD>
+TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsCT<D_>& L) {
+  constexpr int NW = D_ / 32, NT = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = bx * HR;
-  const int n0 = 32 * w;                             // this wave's 32 of the 128 output columns
+  const int n0 = 32 * w;                             // this wave's 32 of the D_ output columns
   TTMI_TSTAMP(0);
   if constexpr (FIN) {
     // stage A runs in this launch: wait until the IN1/64 column-quarter mergers have published
@@ -403,10 +483,11 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
   WFrags<2, IN1> wf;
   wf.load(a.w4, IN1, n0, lane, IN1);
   if (a.bncnt != nullptr) {      // fused BatchNorm: y1 = drop(relu(BN(z))) staged from z rows
-    float4 zv[8];
+    constexpr int ZK = HR * IN1 / 4 / NT;            // float4 of z per thread
+    float4 zv[ZK];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = tid + 256 * k, r = idx >> 7, c4 = idx & 127;
+    for (int k = 0; k < ZK; ++k) {
+      const int idx = tid + NT * k, r = idx >> 7, c4 = idx & 127;
       const int64_t zo = (int64_t)min(r0 + r, a.B - 1) * IN1 + 4 * c4;
       if constexpr (FIN) zv[k] = ld16_wt(a.z, (uint32_t)(zo * 4));
       else zv[k] = *reinterpret_cast<const float4*>(a.z + zo);
@@ -421,8 +502,8 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
     const float4 ww = *reinterpret_cast<const float4*>(a.bnw + 4 * c4);
     const float4 bb = *reinterpret_cast<const float4*>(a.bnb + 4 * c4);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = tid + 256 * k, r = idx >> 7;
+    for (int k = 0; k < ZK; ++k) {
+      const int idx = tid + NT * k, r = idx >> 7;
       float x[4] = {fmaxf((zv[k].x - mu.x) * rs.x * ww.x + bb.x, 0.f), fmaxf((zv[k].y - mu.y) * rs.y * ww.y + bb.y, 0.f),
                     fmaxf((zv[k].z - mu.z) * rs.z * ww.z + bb.z, 0.f), fmaxf((zv[k].w - mu.w) * rs.w * ww.w + bb.w, 0.f)};
       drop_apply_vec<4>(dk, (uint32_t)((int64_t)(r0 + r) * IN1 + 4 * c4), x);
@@ -431,8 +512,8 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
     }
   } else {                                           // y1 rows: 16 x 64 chunks of 16 bytes
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int idx = tid + 256 * k, r = idx >> 6, ch = idx & 63;
+    for (int k = 0; k < HR * IN1 / 8 / NT; ++k) {
+      const int idx = tid + NT * k, r = idx >> 6, ch = idx & 63;
       *reinterpret_cast<uint4*>(L.sY + r * PI + ch * 16) =
           *reinterpret_cast<const uint4*>(a.y1 + (int64_t)min(r0 + r, a.B - 1) * IN1 + ch * 8);
     }
@@ -458,15 +539,15 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
     const int n = n0 + 16 * t + 4 * g;
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[t][e] += b4[t][e];
-    if (mrow) *reinterpret_cast<float4*>(a.y2 + (int64_t)m * HD + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
+    if (mrow) *reinterpret_cast<float4*>(a.y2 + (int64_t)m * D_ + n) = make_float4(v[t][0], v[t][1], v[t][2], v[t][3]);
   }
-  // LayerNorm over the 128 columns (the 4 waves' 32 each), two-pass like ttmi_layernorm_fwd
+  // LayerNorm over the D_ columns (the waves' 32 each), two-pass like ttmi_layernorm_fwd
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int e = 0; e < 4; ++e) s += v[t][e];
-  const float mu = row_sum(s, L, w, lane) * (1.f / HD);
+  const float mu = split_row_sum<NW>(s, L.red, w, lane) * (1.f / D_);
   float qv = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -475,7 +556,7 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
       const float d = v[t][e] - mu;
       qv += d * d;
     }
-  const float rs = 1.f / sqrtf(row_sum(qv, L, w, lane) * (1.f / HD) + a.ln_eps);
+  const float rs = 1.f / sqrtf(split_row_sum<NW>(qv, L.red, w, lane) * (1.f / D_) + a.ln_eps);
   float oo[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -483,16 +564,17 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsC& L) {
     float* o = oo[t];
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[t][e] - mu) * rs * lw[t][e] + lb[t][e];
-    if (mrow) *reinterpret_cast<float4*>(a.out + (int64_t)m * HD + n) = make_float4(o[0], o[1], o[2], o[3]);
+    if (mrow) *reinterpret_cast<float4*>(a.out + (int64_t)m * D_ + n) = make_float4(o[0], o[1], o[2], o[3]);
   }
   if (mrow && lane < 16 && w == 0) { a.m5[m] = mu; a.r5[m] = rs; }
-  row_l2norm(oo, a.ohat, a.onrm, m, mrow, n0, L, w, lane);
+  split_row_l2norm<D_>(oo, a.ohat, a.onrm, m, mrow, n0, L.red, w, lane);
   TTMI_TSTAMP(4);
 }
 
-__global__ __launch_bounds__(256) void item_head_c_kernel(ItemArgs a) {
-  __shared__ __attribute__((aligned(16))) ItemLdsC L;
-  item_c_body<false>(a, blockIdx.x, L);
+template <int D_>
+__global__ __launch_bounds__(D_ * 2) void item_head_c_kernel(ItemArgs a) {
+  __shared__ __attribute__((aligned(16))) ItemLdsCT<D_> L;
+  item_c_body<false, D_>(a, blockIdx.x, L);
 }
 
 // phase stamps of the diagnostic build (ttmi_common.h TTMI_TSTAMP; tools/stamp_build.sh)
@@ -719,15 +801,6 @@ __global__ __launch_bounds__(256) void user_head_fwd_kernel(HeadArgs a) {
 // through a CU at D = 128: 96 KB (176 KB for the last arriver) instead of 368.
 // D = 128 (4 waves) or 256 (8 waves, F = 1024: the reference's default width, ABI 21); each
 // wave owns 32 of the D columns of every D-wide stage.
-template <int D_>
-struct SplitGeo {
-  static constexpr int NW = D_ / 32;                 // waves
-  static constexpr int PD = (D_ + 8) * 2;            // LDS pitches (bytes)
-  static constexpr int PH = (128 + 8) * 2;           // the split's 128 hidden units
-  static constexpr int WPAD = (D_ + 48 + 31) / 32 * 32;
-  static constexpr int PW = (WPAD + 8) * 2;
-  static constexpr int TH = 128 / 16 / NW;           // hidden 16-column tiles per wave
-};
 template <int D_, int F>
 struct SplitLds {
   using G = SplitGeo<D_>;
@@ -738,70 +811,6 @@ struct SplitLds {
   float red[G::NW][HR];     // LayerNorm cross-wave partials
   float bo[D_], n2w[D_], n2b[D_], b1[F], b2[D_], bf0[D_], lnw[D_], lnb[D_], bf3[D_];
 };
-// Row sum over the D columns held by the 4 lanes of row li in each of NW waves (in wave order).
-template <int NW>
-TTMI_DEV float split_row_sum(float s, float (*red)[HR], int w, int lane) {
-  s += __shfl_xor(s, 16, 64);
-  s += __shfl_xor(s, 32, 64);
-  if (lane < 16) red[w][lane] = s;
-  __syncthreads();
-  const int li = lane & 15;
-  float tot = red[0][li];
-#pragma unroll
-  for (int k = 1; k < NW; ++k) tot += red[k][li];
-  __syncthreads();
-  return tot;
-}
-template <int D_>
-TTMI_DEV void split_row_ln(f32x4_t (&v)[2], const float* w_, const float* b_, float eps, bool relu, int n0,
-                           float (*red)[HR], int w, int lane, float& mu, float& rs) {
-  constexpr int NW = SplitGeo<D_>::NW;
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s += v[t][e];
-  mu = split_row_sum<NW>(s, red, w, lane) * (1.f / D_);
-  float q = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float d = v[t][e] - mu;
-      q += d * d;
-    }
-  rs = 1.f / sqrtf(split_row_sum<NW>(q, red, w, lane) * (1.f / D_) + eps);
-  const int g = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int n = n0 + 16 * t + 4 * g + e;
-      float o = (v[t][e] - mu) * rs * w_[n] + b_[n];
-      v[t][e] = relu ? fmaxf(o, 0.f) : o;
-    }
-}
-template <int D_>
-TTMI_DEV void split_row_l2norm(const float (&x)[2][4], float* xhat, float* nrm, int m, bool mrow, int n0,
-                               float (*red)[HR], int w, int lane) {
-  if (xhat == nullptr) return;                       // uniform: a kernel argument
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s += x[t][e] * x[t][e];
-  const float nr = sqrtf(split_row_sum<SplitGeo<D_>::NW>(s, red, w, lane));
-  const float inv = 1.f / fmaxf(nr, 1e-12f);
-  const int g = lane >> 4;
-  if (mrow) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-      *reinterpret_cast<float4*>(xhat + (int64_t)m * D_ + n0 + 16 * t + 4 * g) =
-          make_float4(x[t][0] * inv, x[t][1] * inv, x[t][2] * inv, x[t][3] * inv);
-    if (lane < 16 && w == 0) nrm[m] = nr;
-  }
-}
-
 template <int D_, int F>
 __global__ __launch_bounds__(D_ * 2) void user_head_fwd_split_kernel(HeadArgs a) {
   using G = SplitGeo<D_>;
@@ -810,30 +819,28 @@ __global__ __launch_bounds__(D_ * 2) void user_head_fwd_split_kernel(HeadArgs a)
   __shared__ __attribute__((aligned(16))) union {
     SplitLds<D_, F> s;
     ItemLdsA ia;
-    ItemLdsC ic;
+    ItemLdsCT<D_> ic;
   } U;
   SplitLds<D_, F>& L = U.s;
   __shared__ int s_last;
   const int nsplit = a.nbu * NS;
   int ub = (int)blockIdx.x;
-  if constexpr (D_ == HD) {                          // co-launched item head stages (D = 128)
-    if (a.it_stage == 3) {
-      const int na = a.it_nblk * (IN1 / 64);
-      if (ub < na) {
-        item_a_body(a.it, ub % a.it_nblk, ub / a.it_nblk, U.ia);
-        return;
-      }
-      ub -= na;
-      if (ub >= nsplit) {
-        item_c_body<true>(a.it, ub - nsplit, U.ic);
-        return;
-      }
-    } else if (ub >= nsplit) {
-      const int l = ub - nsplit;
-      if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, U.ia);
-      else item_c_body<false>(a.it, l, U.ic);
+  if (a.it_stage == 3) {                             // co-launched item head stages
+    const int na = a.it_nblk * (IN1 / 64);
+    if (ub < na) {
+      item_a_body(a.it, ub % a.it_nblk, ub / a.it_nblk, U.ia);
       return;
     }
+    ub -= na;
+    if (ub >= nsplit) {
+      item_c_body<true, D_>(a.it, ub - nsplit, U.ic);
+      return;
+    }
+  } else if (ub >= nsplit) {
+    const int l = ub - nsplit;
+    if (a.it_stage == 0) item_a_body(a.it, l % a.it_nblk, l / a.it_nblk, U.ia);
+    else item_c_body<false, D_>(a.it, l, U.ic);
+    return;
   }
   const int rb = ub / NS, j = ub % NS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
@@ -1119,63 +1126,122 @@ TTMI_DEV void ln_bwd16(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, floa
     for (int e = 0; e < 4; ++e) dy[t][e] = rs * (gg[t][e] - c1 - xh[t][e] * c2);
 }
 
+template <int D_>
+struct SplitBwdLds {
+  static constexpr int NW = D_ / 32;
+  char sA[HR * SplitGeo<D_>::PD];   // du, then dz, then dy2, then dy1
+  char sH[HR * SplitGeo<D_>::PH];   // the split's dz1 columns
+  float sX[HR][D_ + 4];             // dx2 (fp32 residual of dx1)
+  float sW[HR][D_ + 4];             // LayerNorm weight-gradient terms dy·x̂ (column sums)
+  float sB[HR][D_ + 4];             // ... and dy
+  float sDem[HR][48];               // dcomb's demographic columns (dG, dC rows)
+  int sGi[HR], sCi[HR];
+  float red[NW][HR];
+};
+// ln_bwd16 over D_ columns and NW waves (same arithmetic and order at D = 128).
+template <int D_>
+TTMI_DEV void split_ln_bwd(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, float rs, const float (&wv)[2][4],
+                           int n0, bool mrow, SplitBwdLds<D_>& L, int w, int lane, float* wsw, float* wsb,
+                           bool sums) {
+  constexpr int NW = D_ / 32;
+  const int g = lane >> 4, li = lane & 15;
+  float xh[2][4], gg[2][4];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = n0 + 16 * t + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = mrow ? dy[t][e] : 0.f;
+      xh[t][e] = (xs[t][e] - mu) * rs;
+      L.sW[li][n + e] = d * xh[t][e];
+      L.sB[li][n + e] = d;
+      gg[t][e] = d * wv[t][e];
+      s1 += gg[t][e];
+      s2 += gg[t][e] * xh[t][e];
+    }
+  }
+  const float c1 = split_row_sum<NW>(s1, L.red, w, lane) * (1.f / D_);   // (its barriers publish sW, sB)
+  const float c2 = split_row_sum<NW>(s2, L.red, w, lane) * (1.f / D_);
+  if (sums && threadIdx.x < D_) {                    // one column per thread, rows in order
+    const int c = threadIdx.x;
+    float cw = 0.f, cb = 0.f;
+#pragma unroll
+    for (int r = 0; r < HR; ++r) { cw += L.sW[r][c]; cb += L.sB[r][c]; }
+    wsw[c] = cw;
+    wsb[c] = cb;
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dy[t][e] = rs * (gg[t][e] - c1 - xh[t][e] * c2);
+}
+
 // Item head backward, row-local part (ABI 15; reference item_tower.py:122-129 under autograd),
 // on 16 rows: dy2 = backward of LayerNorm fusion_layer.5 (stored mean / rstd), written bf16
 // (the fusion_layer.4 weight-gradient operand) and kept in LDS; dy1 = dy2·W4 (fp32, the
 // BatchNorm backward's input) from W4ᵀ fragments.  The LN weight / bias gradient terms leave
 // as this block's column sums (ws rows 2·bx, 2·bx + 1), folded later in block order.
-TTMI_DEV void item_c_bwd_body(const ItemBwdArgs& a, int bx, HeadBwdLds& L) {
+template <int D_ = HD>
+TTMI_DEV void item_c_bwd_body(const ItemBwdArgs& a, int bx, SplitBwdLds<D_>& L) {
+  constexpr int NW = D_ / 32, TD = IN1 / NW / 16;    // dy1: a wave's IN1 / NW columns, TD tiles
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
   const int r0 = bx * HR, m = r0 + li, mc = min(m, a.B - 1);
   const bool mrow = m < a.B;
-  const int n0 = 32 * w;                             // LN: this wave's 32 of the 128 columns
-  const int nn0 = 128 * w;                           // dy1: this wave's 128 of the 512 columns
+  const int n0 = 32 * w;                             // LN: this wave's 32 of the D_ columns
+  const int nn0 = (IN1 / NW) * w;                    // dy1: this wave's columns of the 512
   float xs[2][4], wv[2][4];
   f32x4_t dy[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n = n0 + 16 * t + 4 * g;
-    const float4 d = *reinterpret_cast<const float4*>(a.dout + (int64_t)mc * HD + n);
-    const float4 x = *reinterpret_cast<const float4*>(a.y2 + (int64_t)mc * HD + n);
+    const float4 d = *reinterpret_cast<const float4*>(a.dout + (int64_t)mc * D_ + n);
+    const float4 x = *reinterpret_cast<const float4*>(a.y2 + (int64_t)mc * D_ + n);
     const float4 v = *reinterpret_cast<const float4*>(a.lnw + n);
     dy[t] = f32x4_t{d.x, d.y, d.z, d.w};
     xs[t][0] = x.x; xs[t][1] = x.y; xs[t][2] = x.z; xs[t][3] = x.w;
     wv[t][0] = v.x; wv[t][1] = v.y; wv[t][2] = v.z; wv[t][3] = v.w;
   }
   const float mu = a.m5[mc], rs = a.r5[mc];
-  WFrags<8, HD> wf;                                  // W4ᵀ [512, 128]: the wave's 8 column tiles
-  wf.load(a.w4t, HD, nn0, lane, HD);
-  float* wsr = a.ws + (int64_t)bx * 2 * HD;
-  ln_bwd16(dy, xs, mu, rs, wv, n0, mrow, L, w, lane, wsr, wsr + HD);
+  WFrags<TD, D_> wf;                                 // W4ᵀ [512, D_]: the wave's column tiles
+  wf.load(a.w4t, D_, nn0, lane, D_);
+  float* wsr = a.ws + (int64_t)bx * 2 * D_;
+  split_ln_bwd<D_>(dy, xs, mu, rs, wv, n0, mrow, L, w, lane, wsr, wsr + D_, true);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int n = n0 + 16 * t + 4 * g;
     const float o[4] = {dy[t][0], dy[t][1], dy[t][2], dy[t][3]};
-    st4_bf(L.sA + li * PD + n * 2, o);
-    if (mrow) st4_bf(reinterpret_cast<char*>(a.dy2 + (int64_t)m * HD + n), o);
+    st4_bf(L.sA + li * SplitGeo<D_>::PD + n * 2, o);
+    if (mrow) st4_bf(reinterpret_cast<char*>(a.dy2 + (int64_t)m * D_ + n), o);
   }
   __syncthreads();
-  f32x4_t acc[8];
-  head_gemm<8, HD, PD>(L.sA, wf, acc, lane);
+  f32x4_t acc[TD];
+  head_gemm<TD, D_, SplitGeo<D_>::PD>(L.sA, wf, acc, lane);
   if (mrow) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < TD; ++t)
       *reinterpret_cast<float4*>(a.dy1 + (int64_t)m * IN1 + nn0 + 16 * t + 4 * g) =
           make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
   }
 }
 
-__global__ __launch_bounds__(256) void item_head_bwd_c_kernel(ItemBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) HeadBwdLds L;
-  item_c_bwd_body(a, blockIdx.x, L);
+template <int D_>
+__global__ __launch_bounds__(D_ * 2) void item_head_bwd_c_kernel(ItemBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) SplitBwdLds<D_> L;
+  item_c_bwd_body<D_>(a, blockIdx.x, L);
 }
+
 
 template <int F>
 __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
   STAMP(0);
-  __shared__ __attribute__((aligned(16))) HeadBwdLds L;
+  __shared__ __attribute__((aligned(16))) union {
+    HeadBwdLds h;
+    SplitBwdLds<HD> ic;
+  } U;
+  HeadBwdLds& L = U.h;
   if ((int)blockIdx.x >= a.nbu) {                   // co-launched item head backward (rows)
-    item_c_bwd_body(a.it, (int)blockIdx.x - a.nbu, L);
+    item_c_bwd_body<HD>(a.it, (int)blockIdx.x - a.nbu, U.ic);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, g = lane >> 4;
@@ -1380,74 +1446,17 @@ __global__ __launch_bounds__(256) void user_head_bwd_kernel(HeadBwdArgs a) {
 // dz1 = (dy2·W2) ⊙ gate and their partial dz1·W1, handed over like the forward's partial; the
 // last to arrive sums the partials in split order, then runs LN2's backward, the residual,
 // drop1, dctx = dy1·Wo and the dG / dC adds.  D = 128 (4 waves) or 256 (8 waves, F = 1024).
-template <int D_>
-struct SplitBwdLds {
-  static constexpr int NW = D_ / 32;
-  char sA[HR * SplitGeo<D_>::PD];   // du, then dz, then dy2, then dy1
-  char sH[HR * SplitGeo<D_>::PH];   // the split's dz1 columns
-  float sX[HR][D_ + 4];             // dx2 (fp32 residual of dx1)
-  float sW[HR][D_ + 4];             // LayerNorm weight-gradient terms dy·x̂ (column sums)
-  float sB[HR][D_ + 4];             // ... and dy
-  float sDem[HR][48];               // dcomb's demographic columns (dG, dC rows)
-  int sGi[HR], sCi[HR];
-  float red[NW][HR];
-};
-// ln_bwd16 over D_ columns and NW waves (same arithmetic and order at D = 128).
-template <int D_>
-TTMI_DEV void split_ln_bwd(f32x4_t (&dy)[2], const float (&xs)[2][4], float mu, float rs, const float (&wv)[2][4],
-                           int n0, bool mrow, SplitBwdLds<D_>& L, int w, int lane, float* wsw, float* wsb,
-                           bool sums) {
-  constexpr int NW = D_ / 32;
-  const int g = lane >> 4, li = lane & 15;
-  float xh[2][4], gg[2][4];
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int n = n0 + 16 * t + 4 * g;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float d = mrow ? dy[t][e] : 0.f;
-      xh[t][e] = (xs[t][e] - mu) * rs;
-      L.sW[li][n + e] = d * xh[t][e];
-      L.sB[li][n + e] = d;
-      gg[t][e] = d * wv[t][e];
-      s1 += gg[t][e];
-      s2 += gg[t][e] * xh[t][e];
-    }
-  }
-  const float c1 = split_row_sum<NW>(s1, L.red, w, lane) * (1.f / D_);   // (its barriers publish sW, sB)
-  const float c2 = split_row_sum<NW>(s2, L.red, w, lane) * (1.f / D_);
-  if (sums && threadIdx.x < D_) {                    // one column per thread, rows in order
-    const int c = threadIdx.x;
-    float cw = 0.f, cb = 0.f;
-#pragma unroll
-    for (int r = 0; r < HR; ++r) { cw += L.sW[r][c]; cb += L.sB[r][c]; }
-    wsw[c] = cw;
-    wsb[c] = cb;
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) dy[t][e] = rs * (gg[t][e] - c1 - xh[t][e] * c2);
-}
-
 template <int D_, int F>
 __global__ __launch_bounds__(D_ * 2) void user_head_bwd_split_kernel(HeadBwdArgs a) {
   using G = SplitGeo<D_>;
   constexpr int NS = F / 128, NW = G::NW, TH = G::TH;
   STAMP(0);
-  __shared__ __attribute__((aligned(16))) union {
-    SplitBwdLds<D_> s;
-    HeadBwdLds ic;
-  } U;
-  SplitBwdLds<D_>& L = U.s;
+  __shared__ __attribute__((aligned(16))) SplitBwdLds<D_> L;
   __shared__ int s_last;
   const int nsplit = a.nbu * NS;
-  if constexpr (D_ == HD) {
-    if ((int)blockIdx.x >= nsplit) {                // co-launched item head backward (rows)
-      item_c_bwd_body(a.it, (int)blockIdx.x - nsplit, U.ic);
-      return;
-    }
+  if ((int)blockIdx.x >= nsplit) {                  // co-launched item head backward (rows)
+    item_c_bwd_body<D_>(a.it, (int)blockIdx.x - nsplit, L);
+    return;
   }
   const int rb = (int)blockIdx.x / NS, j = (int)blockIdx.x % NS;
   const bool lead = j == 0;
@@ -1703,8 +1712,9 @@ __global__ __launch_bounds__(256) void q1_item_fwd_kernel(Q1Args q, ItemArgs it,
 namespace {
 int item_fwd_check(const ttmi_item_head_desc* d) {
   TTMI_REQUIRE(d != nullptr, "ttmi_item_head_fwd: null descriptor");
-  TTMI_REQUIRE(d->B > 1 && d->K == IK && d->N1 == IN1 && d->D == HD,
-               "ttmi_item_head_fwd: needs B > 1 (training BatchNorm), K == N1 == %d, D == %d", IK, HD);
+  TTMI_REQUIRE(d->B > 1 && d->K == IK && d->N1 == IN1 && (d->D == HD || d->D == 2 * HD),
+               "ttmi_item_head_fwd: needs B > 1 (training BatchNorm), K == N1 == %d, D in {%d, %d}", IK, HD,
+               2 * HD);
   TTMI_REQUIRE(d->modal && d->w0 && d->b0 && d->bn_w && d->bn_b && d->w4 && d->b4 && d->ln_w && d->ln_b &&
                d->modal16 && d->z && d->bn_mean && d->bn_rstd && d->y1 && d->y2 && d->out && d->m5 &&
                d->r5 && (!d->out_hat || d->out_norm), "ttmi_item_head_fwd: null argument");
@@ -1713,6 +1723,7 @@ int item_fwd_check(const ttmi_item_head_desc* d) {
 ItemArgs item_args(const ttmi_item_head_desc* d) {
   ItemArgs a{};
   a.B = d->B;
+  a.D = d->D;
   a.modal = d->modal; a.w0 = (const bf16_t*)d->w0; a.b0 = d->b0;
   a.y1 = (const bf16_t*)d->y1; a.w4 = (const bf16_t*)d->w4; a.b4 = d->b4;
   a.lnw = d->ln_w; a.lnb = d->ln_b; a.ln_eps = d->ln_eps;
@@ -1729,7 +1740,8 @@ ItemArgs item_args(const ttmi_item_head_desc* d) {
 }
 int item_bwd_check(const ttmi_item_head_bwd_desc* d) {
   TTMI_REQUIRE(d != nullptr, "ttmi_item_head_bwd_c: null descriptor");
-  TTMI_REQUIRE(d->B > 0 && d->D == HD && d->N1 == IN1, "ttmi_item_head_bwd_c: needs D == %d, N1 == %d", HD, IN1);
+  TTMI_REQUIRE(d->B > 0 && (d->D == HD || d->D == 2 * HD) && d->N1 == IN1,
+               "ttmi_item_head_bwd_c: needs D in {%d, %d}, N1 == %d", HD, 2 * HD, IN1);
   TTMI_REQUIRE(d->dout && d->y2 && d->m5 && d->r5 && d->ln_w && d->w4t && d->dy2 && d->dy1 && d->ws,
                "ttmi_item_head_bwd_c: null argument");
   TTMI_REQUIRE(((uintptr_t)d->dout & 15) == 0 && ((uintptr_t)d->y2 & 15) == 0 && ((uintptr_t)d->dy1 & 15) == 0 &&
@@ -1739,7 +1751,7 @@ int item_bwd_check(const ttmi_item_head_bwd_desc* d) {
 }
 ItemBwdArgs item_bwd_args(const ttmi_item_head_bwd_desc* d) {
   ItemBwdArgs a{};
-  a.B = d->B; a.dout = d->dout; a.y2 = d->y2; a.m5 = d->m5; a.r5 = d->r5; a.lnw = d->ln_w;
+  a.B = d->B; a.D = d->D; a.dout = d->dout; a.y2 = d->y2; a.m5 = d->m5; a.r5 = d->r5; a.lnw = d->ln_w;
   a.w4t = (const bf16_t*)d->w4t; a.dy2 = (bf16_t*)d->dy2; a.dy1 = d->dy1; a.ws = d->ws;
   return a;
 }
@@ -1763,7 +1775,8 @@ extern "C" int ttmi_item_head_fwd_stages(const ttmi_item_head_desc* d, int stage
     if (rc != TTMI_OK) return rc;
   }
   if (stages & 4) {
-    hipLaunchKernelGGL(item_head_c_kernel, dim3(nblk), dim3(256), 0, s, a);
+    if (d->D == 2 * HD) hipLaunchKernelGGL(item_head_c_kernel<2 * HD>, dim3(nblk), dim3(4 * HD), 0, s, a);
+    else hipLaunchKernelGGL(item_head_c_kernel<HD>, dim3(nblk), dim3(2 * HD), 0, s, a);
     return ttmi_check_launch("ttmi_item_head_fwd");
   }
   return TTMI_OK;
@@ -1778,13 +1791,18 @@ extern "C" int64_t ttmi_item_head_bn_part_floats(int B) { return (int64_t)((B + 
 // error word (a C workgroup's poll timed out)
 extern "C" int64_t ttmi_item_head_bn_counter_bytes(int B) { (void)B; return (IN1 / 64 + 3) * 4; }
 
-extern "C" int64_t ttmi_item_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 2 * HD; }
+// [nblk][2][D] column sums, sized for D = 256 (ABI 21)
+extern "C" int64_t ttmi_item_head_bwd_ws_floats(int B) { return (int64_t)((B + HR - 1) / HR) * 2 * 2 * HD; }
 
 extern "C" int ttmi_item_head_bwd_c(const ttmi_item_head_bwd_desc* d, hipStream_t s) {
   const int rc = item_bwd_check(d);
   if (rc != TTMI_OK) return rc;
-  hipLaunchKernelGGL(item_head_bwd_c_kernel, dim3((unsigned)((d->B + HR - 1) / HR)), dim3(256), 0, s,
-                     item_bwd_args(d));
+  if (d->D == 2 * HD)
+    hipLaunchKernelGGL(item_head_bwd_c_kernel<2 * HD>, dim3((unsigned)((d->B + HR - 1) / HR)), dim3(4 * HD), 0, s,
+                       item_bwd_args(d));
+  else
+    hipLaunchKernelGGL(item_head_bwd_c_kernel<HD>, dim3((unsigned)((d->B + HR - 1) / HR)), dim3(2 * HD), 0, s,
+                       item_bwd_args(d));
   return ttmi_check_launch("ttmi_item_head_bwd_c");
 }
 
@@ -1803,8 +1821,9 @@ int user_item_head_fwd_impl(const ttmi_user_head_desc* d, const ttmi_item_head_d
                HD, 2 * HD, 8 * HD);
   TTMI_REQUIRE(d256 || (d->F > 0 && d->F <= FMAX && d->F % 256 == 0),
                "ttmi_user_head_fwd: needs F %% 256 == 0, F <= %d", FMAX);
-  TTMI_REQUIRE(!d256 || (d->ffn_ws && !it && !getenv("TTMI_HEAD_NOSPLIT")),
-               "ttmi_user_head_fwd: D == 256 runs the FFN split only (ffn_ws, no item co-launch)");
+  TTMI_REQUIRE(!d256 || (d->ffn_ws && !getenv("TTMI_HEAD_NOSPLIT")),
+               "ttmi_user_head_fwd: D == 256 runs the FFN split only (ffn_ws)");
+  TTMI_REQUIRE(!it || it->D == d->D, "ttmi_user_item_head_fwd: the item head's width must be the user head's");
   TTMI_REQUIRE(d->dg == 16 && d->dc == 32, "ttmi_user_head_fwd: demographic widths must be 16 and 32");
   TTMI_REQUIRE(d->n_genders > 0 && d->n_countries > 0, "ttmi_user_head_fwd: n_genders / n_countries must be > 0");
   TTMI_REQUIRE(d->ctx && d->res && d->drop_rows && d->wo && d->bo && d->n2w && d->n2b && d->w1 && d->b1 && d->w2 &&
@@ -1930,8 +1949,9 @@ extern "C" int ttmi_user_item_head_bwd(const ttmi_user_head_bwd_desc* d, const t
   TTMI_REQUIRE(d->B > 0 && ((d->D == HD && (d->F == 256 || d->F == 512)) || d256) && d->dg == 16 && d->dc == 32,
                "ttmi_user_head_bwd: needs D == %d with F in {256, 512} (or D == %d with F == %d), dg == 16, dc == 32",
                HD, 2 * HD, 8 * HD);
-  TTMI_REQUIRE(!d256 || (d->ffn_ws && !it && !getenv("TTMI_HEAD_NOSPLIT")),
-               "ttmi_user_head_bwd: D == 256 runs the FFN split only (ffn_ws, no item co-launch)");
+  TTMI_REQUIRE(!d256 || (d->ffn_ws && !getenv("TTMI_HEAD_NOSPLIT")),
+               "ttmi_user_head_bwd: D == 256 runs the FFN split only (ffn_ws)");
+  TTMI_REQUIRE(!it || it->D == d->D, "ttmi_user_item_head_bwd: the item head's width must be the user head's");
   TTMI_REQUIRE(d->n_genders > 0 && d->n_countries > 0, "ttmi_user_head_bwd: n_genders / n_countries must be > 0");
   TTMI_REQUIRE(d->du && d->az && d->z && d->mz && d->rz && d->h && d->x1 && d->m2 && d->r2 &&
                d->drop_rows && d->gender && d->country && d->wf3t && d->wf0t && d->w2t && d->w1t &&

@@ -664,13 +664,13 @@ def item_fusion_bwd_begin(P: Dict[str, Tensor], W: Dict[str, Tensor], st: ItemSa
     in the user head backward launch), or None when the shapes or the W4ᵀ mirror are missing."""
     w4t = W.get(transposed_name("fusion_layer.4.weight"))
     B, D = dout.shape
-    if cfg.dtype != torch.bfloat16 or w4t is None or D != 128 or tuple(w4t.shape) != (512, 128) \
+    if cfg.dtype != torch.bfloat16 or w4t is None or D not in (128, 256) or tuple(w4t.shape) != (512, D) \
             or st.y2.dtype != torch.float32:
         return None
     dev = dout.device
     dy2 = torch.empty(B, D, device=dev, dtype=cfg.dtype)
     dy1 = torch.empty(B, w4t.shape[0], device=dev, dtype=torch.float32)
-    ws = ops.item_head_bwd_ws(B, dev)
+    ws = ops.item_head_bwd_ws(B, dev, D)
     dc = dout.contiguous()
     d = ops.item_head_bwd_desc(dc, st.y2, st.m5, st.r5, P["fusion_layer.5.weight"], w4t, dy2, dy1, ws)
     return ItemBwdPending(d, (dc, w4t), dy2, dy1, ws, (P, W, st, grads, cfg, p_drop, dmodal))

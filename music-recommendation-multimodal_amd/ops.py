@@ -908,9 +908,9 @@ def item_head_bwd_desc(dout: Tensor, y2: Tensor, m5: Tensor, r5: Tensor, ln_w: T
     return d
 
 
-def item_head_bwd_ws(B: int, device) -> Tensor:
-    _L.load()
-    return torch.empty(int(_L._lib.ttmi_item_head_bwd_ws_floats(B)), device=device)
+def item_head_bwd_ws(B: int, device, D: int = 128) -> Tensor:
+    """[nblk][2][D] LayerNorm column sums of ttmi_item_head_bwd_c (nblk = ceil(B / 16))."""
+    return torch.empty((B + 15) // 16 * 2 * D, device=device)
 
 
 def item_head_bwd_c(d: ItemHeadBwdDesc) -> None:
@@ -933,11 +933,13 @@ def ln_sum_folds(ws: Tensor, grads: Sequence[Tensor], rows: int, D: int, S: Opti
 
 
 def item_head_fusable(W: Dict[str, Tensor], modal: Tensor, dtype) -> bool:
-    """Shapes ttmi_item_head_fwd takes (include/ttmi.h): bf16, 512 -> 512 -> BN -> 128."""
+    """Shapes ttmi_item_head_fwd takes (include/ttmi.h): bf16, 512 -> 512 -> BN -> D, D = 128
+    or (ABI 21) the reference's default 256."""
     w0, w4 = W["fusion_layer.0.weight"], W["fusion_layer.4.weight"]
     return (dtype == torch.bfloat16 and modal.dim() == 2 and modal.shape[0] > 1 and
             modal.shape[1] == 512 and modal.dtype == torch.float32 and tuple(w0.shape) == (512, 512) and
-            tuple(w4.shape) == (128, 512) and w0.dtype == torch.bfloat16 and w4.dtype == torch.bfloat16)
+            tuple(w4.shape) in ((128, 512), (256, 512)) and w0.dtype == torch.bfloat16 and
+            w4.dtype == torch.bfloat16)
 
 
 def batchnorm_bwd(dy: Tensor, z: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, y: Tensor,
