@@ -661,6 +661,19 @@ int ttmi_mha_q1_gather_fwd(int dtype, int B, int L, int H, int Dh, const void* q
                            const int64_t* key_valid, const float* x, int32_t* rows, float* x_rows,
                            float drop_p, const uint64_t* drop_seed, void* ctx, float* lse,
                            hipStream_t stream);
+/* ttmi_mha_q1_gather_fwd whose query rows are projected in the launch (ABI 21; the pruned last
+ * encoder layer, user_tower.py:111-116 evaluated only where :131-136 reads it): for each
+ * gathered row r, q = a_in[r]·wq[h·Dh ..]ᵀ + bq (a_in [B·L, 128] bf16 normed rows, wq the first
+ * 128 rows of in_proj_weight, bq its first 128 biases, fp32 sums rounded to bf16), written into
+ * qkv[r, 0:128]; qkv's K / V columns come from the caller (a 256-column projection), its other
+ * Q entries are never read.  bf16, H·Dh = 128 with Dh = 32, L <= 64; `it` (nullable): the item
+ * head's stage A on the same grid, as ttmi_mha_q1_gather_item_fwd. */
+struct ttmi_item_head_desc;
+int ttmi_mha_q1_proj_gather_fwd(int B, int L, int H, int Dh, void* qkv, const int64_t* key_valid,
+                                const void* a_in, const void* wq, const float* bq, const float* x,
+                                int32_t* rows, float* x_rows, float drop_p, const uint64_t* drop_seed,
+                                void* ctx, float* lse, const struct ttmi_item_head_desc* it,
+                                hipStream_t stream);
 /* Backward: writes the full dqkv [B*L, 3HDh] (dQ only on the query rows, zero elsewhere;
  * dK, dV on every row). */
 int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,

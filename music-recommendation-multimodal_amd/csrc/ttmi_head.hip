@@ -1935,6 +1935,33 @@ extern "C" int64_t ttmi_user_head_ffn_ws_bytes(int B, int F) {
   return ffn_cnt_bytes(B) + (int64_t)((B + HR - 1) / HR) * (F / 128) * HR * 2 * HD * 4;   // D <= 256
 }
 
+extern "C" int ttmi_mha_q1_proj_gather_fwd(int B, int L, int H, int Dh, void* qkv, const int64_t* key_valid,
+                                           const void* a_in, const void* wq, const float* bq, const float* x,
+                                           int32_t* rows, float* x_rows, float drop_p, const uint64_t* drop_seed,
+                                           void* ctx, float* lse, const ttmi_item_head_desc* it, hipStream_t s) {
+  static const char* fn = "ttmi_mha_q1_proj_gather_fwd";
+  int rc = q1_validate(fn, TTMI_BF16, B, L, H, Dh, qkv, drop_p, drop_seed);
+  if (rc) return rc;
+  TTMI_REQUIRE(H * Dh == HD && Dh == 32 && L <= 64, "%s: serves bf16, H*Dh = %d with Dh = 32, L <= 64", fn, HD);
+  TTMI_REQUIRE(qkv && key_valid && a_in && wq && bq && x && rows && x_rows && ctx && lse, "%s: null argument", fn);
+  TTMI_REQUIRE((((uintptr_t)a_in | (uintptr_t)wq) & 15) == 0, "%s: a_in and wq must be 16-byte aligned", fn);
+  if (B == 0) return TTMI_OK;
+  if (it) {
+    rc = item_fwd_check(it);
+    if (rc) return rc;
+  }
+  Q1Args q{};
+  q.B = B; q.L = L; q.H = H; q.Dh = Dh; q.scale = 1.f / sqrtf((float)Dh);
+  q.qkv = qkv; q.kvalid = key_valid; q.rows = rows; q.x = x; q.x_rows = x_rows;
+  q.dp = make_drop(drop_p, drop_seed); q.ctx = ctx; q.lse = lse;
+  q.qa = (const bf16_t*)a_in; q.wq = (const bf16_t*)wq; q.bq = bq;
+  const ItemArgs ia = it ? item_args(it) : ItemArgs{};
+  const int it_nblk = it ? (it->B + HR - 1) / HR : 1, nit = it ? it_nblk * (IN1 / 64) : 0;
+  const dim3 grid((unsigned)(nit + (B * H + 3) / 4));
+  hipLaunchKernelGGL(q1_item_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, q, ia, it_nblk, nit);
+  return ttmi_check_launch(fn);
+}
+
 extern "C" int ttmi_user_head_fwd(const ttmi_user_head_desc* d, hipStream_t s) {
   return ttmi_user_item_head_fwd(d, nullptr, s);
 }

@@ -29,6 +29,10 @@ struct Q1Args {
   DropParams dp;
   void* ctx; float* lse;                             // fwd outputs / bwd: lse input
   const void* dctx; void* dqkv;                      // bwd
+  // ABI 21, fwd (bf16, H·Dh = 128, Dh = 32): the query row's projection is computed here,
+  // q = a_in[row]·wq[h·Dh ..]ᵀ + bq (wq: in_proj's first D rows), and written into qkv's Q
+  // columns of that row only (the pruned layer projects K / V alone for the other rows)
+  const bf16_t* qa; const bf16_t* wq; const float* bq;
 };
 
 // Per-wave LDS of the one-query bodies (2.5 KB).
@@ -113,7 +117,36 @@ TTMI_DEV void q1_fwd_wave(const Q1Args& a, int bh, Q1Lds& S) {
   }
   const int p = (int)(r - (int64_t)b * L);
   const T* seq = qkv + (int64_t)b * L * ld + (int64_t)h * Dh;
-  if (j < Dh) S.sq[j] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + j);
+  bool proj = false;
+  if constexpr (sizeof(T) == 2) proj = a.qa != nullptr;
+  if (proj) {
+    // two lanes per output d (64 of the 128 k each), fp32 sums, rounded to bf16 as the
+    // projection GEMM's output would be
+    const int d = j >> 1, hf = j & 1;
+    const uint4* wr = reinterpret_cast<const uint4*>(a.wq + (int64_t)(h * Dh + d) * D + hf * 64);
+    const uint4* ar = reinterpret_cast<const uint4*>(a.qa + r * D + hf * 64);
+    uint4 wv[8], av[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { wv[c] = wr[c]; av[c] = ar[c]; }
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint32_t wx[4] = {wv[c].x, wv[c].y, wv[c].z, wv[c].w}, ax[4] = {av[c].x, av[c].y, av[c].z, av[c].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc = fmaf(__uint_as_float(ax[e] << 16), __uint_as_float(wx[e] << 16), acc);
+        acc = fmaf(__uint_as_float(ax[e] & 0xFFFF0000u), __uint_as_float(wx[e] & 0xFFFF0000u), acc);
+      }
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    const bf16_t qb = f2bf(acc + a.bq[h * Dh + d]);
+    if (hf == 0) {
+      S.sq[d] = __uint_as_float((uint32_t)qb << 16);
+      reinterpret_cast<bf16_t*>(const_cast<void*>(a.qkv))[r * ld + (int64_t)h * Dh + d] = qb;
+    }
+  } else if (j < Dh) {
+    S.sq[j] = ldf<T>(qkv, r * ld + (int64_t)h * Dh + j);
+  }
   wave_lds_sync();
   const bool ok = j < L && j <= p && a.kvalid[(int64_t)b * L + j] != 0;
   const float s = ok ? q1_dot_row<T>(S.sq, seq + (int64_t)j * ld + D, Dh) * a.scale : -INFINITY;

@@ -185,6 +185,18 @@ def _qa_ok(w_in: Tensor, a1: Tensor, L: int, H: int) -> bool:
             and ops.qkv_attn_supported(a1.dtype, L, H, D // H))
 
 
+# the pruned layer's query projected inside the one-query attention (ttmi_mha_q1_proj_gather_fwd);
+# TTMI_NO_Q1PROJ=1 restores the full 384-column projection (A/B measurements)
+_Q1PROJ = os.environ.get("TTMI_NO_Q1PROJ", "0") != "1"
+
+
+def _q1_proj_ok(w_in: Tensor, a1: Tensor, L: int, H: int) -> bool:
+    D = a1.shape[1]
+    return (_Q1PROJ and a1.dtype == torch.bfloat16 and w_in.dtype == torch.bfloat16 and D == 128
+            and H * 32 == D and L <= 64 and tuple(w_in.shape) == (3 * D, D) and w_in.is_contiguous()
+            and a1.is_contiguous())
+
+
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
@@ -243,7 +255,13 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
         qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         w_in, b_in = W[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"]
         fused_qa = not pruned and _qa_ok(w_in, a1, L, H)
-        if not fused_qa:
+        # the pruned layer reads Q at the gathered rows only: K / V over every row (a 256-column
+        # projection), Q inside the one-query attention launch (ABI 21)
+        proj_q1 = pruned and _q1_proj_ok(w_in, a1, L, H)
+        if proj_q1:
+            ops.gemm(a1, w_in[D:], qkv[:, D:], M, 2 * D, D, lda=D, a_kmajor=True, ldb=D, b_kmajor=True,
+                     ldc=3 * D, bias=b_in[D:])
+        elif not fused_qa:
             ops.linear(a1, w_in, b_in, qkv)
         F_ = W[pre + "linear1.weight"].shape[0]
         if pruned:
@@ -260,9 +278,14 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             head_fused = ops.user_head_fusable(W, P, pre, D, dt)
             co_ac = co_item is not None and co_item.bn_fused and head_fused and _HEAD_AC
             co_a = co_item is not None and co_item.bn_fused and L <= 64 and not co_ac
-            ops.mha_q1_gather_fwd(qkv, key_valid, x, rows, res_in, B, L, H, ctx, lse,
-                                  _drop(cfg, seeds, site_attn(i)),
-                                  co_item=co_item.desc if co_a else None)
+            if proj_q1:
+                ops.mha_q1_proj_gather_fwd(qkv, key_valid, a1, w_in[:D], b_in[:D], x, rows, res_in, B, L,
+                                           H, ctx, lse, _drop(cfg, seeds, site_attn(i)),
+                                           co_item=co_item.desc if co_a else None)
+            else:
+                ops.mha_q1_gather_fwd(qkv, key_valid, x, rows, res_in, B, L, H, ctx, lse,
+                                      _drop(cfg, seeds, site_attn(i)),
+                                      co_item=co_item.desc if co_a else None)
             if co_a:
                 co_item.a_done = True
             if head_fused:      # the rest of the tower: one launch

@@ -1187,6 +1187,22 @@ def mha_q1_gather_fwd(qkv: Tensor, key_valid: Tensor, x: Tensor, rows: Tensor, x
     return ctx
 
 
+def mha_q1_proj_gather_fwd(qkv: Tensor, key_valid: Tensor, a_in: Tensor, wq: Tensor, bq: Tensor,
+                           x: Tensor, rows: Tensor, x_rows: Tensor, B: int, L: int, H: int, ctx: Tensor,
+                           lse: Tensor, drop: Drop = NO_DROP,
+                           co_item: Optional[ItemHeadDesc] = None) -> Tensor:
+    """mha_q1_gather_fwd whose query rows are projected in the launch (ABI 21): q =
+    a_in[row]·wqᵀ + bq for the gathered rows only, written into qkv's Q columns there; the
+    caller has filled qkv's K / V columns (the pruned layer's 256-column projection)."""
+    _dev(qkv, key_valid, a_in, wq, bq, x, rows, x_rows, ctx, lse)
+    D = qkv.shape[1] // 3
+    _q1_batch_check("mha_q1_proj_gather_fwd", B, L, H, drop)
+    call("ttmi_mha_q1_proj_gather_fwd", B, L, H, D // H, _p(qkv), _p(key_valid), _p(a_in), _p(wq),
+         _p(bq), _p(x), _p(rows), _p(x_rows), float(drop[0]), _p(drop[1]), _p(ctx), _p(lse),
+         ctypes.byref(co_item) if co_item is not None else None, _s())
+    return ctx
+
+
 def bn_bwd_desc(dy: Tensor, z: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, y: Tensor,
                 dz: Tensor, dw: Tensor, db: Tensor, *, gate_scale: float = 1.0, gated: bool = True,
                 dz16: Optional[Tensor] = None) -> BnBwdDesc:

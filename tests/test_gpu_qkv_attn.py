@@ -73,3 +73,49 @@ def test_qkv_attn_refuses_unserved_shapes(gpu_pkg):
     qkv = torch.empty(4 * 65, 384, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(Exception, match="ttmi_qkv_attn_fwd"):
         ops.qkv_attn_fwd(a, w, b, kv, 4, 65, 4, qkv, torch.empty_like(a), torch.empty(4 * 4 * 65, device=DEV))
+
+
+@pytest.mark.parametrize("B,L,p", [(512, 50, 0.1), (9, 20, 0.0), (4, 64, 0.1)])
+def test_q1_proj_gather_matches_full_projection(gpu_pkg, B, L, p):
+    """The pruned layer's one-query attention with its query rows projected in the launch
+    (ttmi_mha_q1_proj_gather_fwd, K / V from a 256-column projection) against the full
+    384-column projection + ttmi_mha_q1_gather_fwd: the gathered rows and residual rows equal,
+    the query row within bf16 rounding of the fp32 product, ctx / lse to fp32-accumulation noise."""
+    ops = gpu_pkg.ops
+    H, D = 4, 128
+    g = torch.Generator().manual_seed(77 * L + B)
+    a = torch.randn(B * L, D, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(3 * D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    x = torch.randn(B * L, D, generator=g).to(DEV)
+    kv = _masks(B, L, g).to(DEV)
+    kv[1 % B] = 0
+    kv[1 % B, 0] = 1                                    # (the gather needs one valid key)
+    drop = (p, _seed(0x5EED0F00D + L)) if p > 0 else (0.0, None)
+    outs = []
+    for proj in (False, True):
+        qkv = torch.zeros(B * L, 3 * D, device=DEV, dtype=torch.bfloat16)
+        rows = torch.empty(B, device=DEV, dtype=torch.int32)
+        xr = torch.empty(B, D, device=DEV)
+        ctx = torch.empty(B, D, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B * H, device=DEV)
+        if proj:
+            ops.gemm(a, w[D:], qkv[:, D:], B * L, 2 * D, D, lda=D, a_kmajor=True, ldb=D, b_kmajor=True,
+                     ldc=3 * D, bias=b[D:])
+            ops.mha_q1_proj_gather_fwd(qkv, kv, a, w[:D], b[:D], x, rows, xr, B, L, H, ctx, lse, drop)
+        else:
+            ops.linear(a, w, b, qkv)
+            ops.mha_q1_gather_fwd(qkv, kv, x, rows, xr, B, L, H, ctx, lse, drop)
+        torch.cuda.synchronize()
+        outs.append((qkv, rows, xr, ctx, lse))
+    (q0, r0, x0, c0, l0), (q1, r1, x1, c1, l1) = outs
+    assert torch.equal(r0, r1) and torch.equal(x0, x1)
+    rl = r1.long()
+    ref = a.float()[rl] @ w.float()[:D].t() + b[:D]
+    err = (q1[rl, :D].float() - ref).abs()
+    assert bool((err <= ref.abs() * 2 ** -8 + 1e-5).all()), float(err.max())
+    assert torch.equal(q1[:, D:], q0[:, D:]) if B * L >= 2048 else True
+    assert float((c1.float() - c0.float()).abs().max()) <= 0.02 * float(c0.float().abs().max()) + 1e-3
+    fin = torch.isfinite(l0)
+    assert torch.equal(fin, torch.isfinite(l1))
+    assert float((l1[fin] - l0[fin]).abs().max()) <= 1e-2
