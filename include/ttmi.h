@@ -241,6 +241,14 @@ int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
 int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                  const int64_t* key_valid, const float* lse, const void* dctx, float drop_p,
                  const uint64_t* drop_seed, void* dqkv, hipStream_t stream);
+/* ttmi_mha_bwd with dctx computed in the launch from the out-projection's output gradient
+ * (ABI 21): dctx = dy·W_o (dy [B*L, 128] bf16; wot = W_oᵀ, the transposed k-major mirror,
+ * [128, 128] bf16), rounded to bf16 with ttmi_linear's fragment and MFMA order, so dqkv is
+ * bit-identical to ttmi_linear(dy, wot) + ttmi_mha_bwd where the row-panel kernel serves that
+ * linear (M >= 2048).  bf16, H*Dh = 128 with Dh = 32, L <= 64. */
+int ttmi_mha_bwd_dy(int B, int L, int H, int Dh, const void* qkv, const int64_t* key_valid,
+                    const float* lse, const void* dy, const void* wot, float drop_p,
+                    const uint64_t* drop_seed, void* dqkv, hipStream_t stream);
 /* The encoder layer's input projection and attention in one launch (ABI 21; reference
  * user_tower.py:111-116, nn.MultiheadAttention in_proj then SDPA): qkv = a·w_inᵀ + b_in
  * (a [B*L, 128] bf16 normed rows, w_in [384, 128] bf16, b_in [384] fp32), written to qkv as

@@ -536,12 +536,20 @@ __global__ __launch_bounds__(256) void mha2_fwd_kernel(int L, int H, const bf16_
                           ctx + (int64_t)b * L * D + (int64_t)h * DH, D, lse + (int64_t)bh * L);
 }
 
-template <int DH>
+// DY: dO is not read from dctx but computed here from the out-projection's output gradient,
+// dO = dy·W_o (the head's 32 columns; dy [B·L, 128] bf16, wot = W_oᵀ's k-major mirror), with
+// the row-panel kernel's fragment order, MFMA order and bf16 rounding: the separate input-grad
+// launch and its dctx round trip are gone, the values are the ones it would have written
+// (DH = 32, D = 128 only; ABI 21, ttmi_mha_bwd_dy).
+template <int DH, bool DY = false>
 __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_t* __restrict__ qkv,
                                                       const int64_t* __restrict__ kvalid,
                                                       const float* __restrict__ lse,
                                                       const bf16_t* __restrict__ dctx, DropParams dp,
-                                                      bf16_t* __restrict__ dqkv, float scale) {
+                                                      bf16_t* __restrict__ dqkv, float scale,
+                                                      const bf16_t* __restrict__ dy = nullptr,
+                                                      const bf16_t* __restrict__ wot = nullptr) {
+  static_assert(!DY || DH == 32, "dO from dy: d_model 128, 4 heads of 32");
   using G = Img2<DH>;
   __shared__ __attribute__((aligned(16))) char smem[4 * G::BYTES + 2 * 64 * G::SP];
   char* sQ = smem;
@@ -561,13 +569,47 @@ __global__ __launch_bounds__(256) void mha2_bwd_kernel(int L, int H, const bf16_
   const int64_t kvl = kvalid[(int64_t)b * L + min(lane, L - 1)];
   const int qrow = 16 * wave + li;
   const float lr0 = lse[(int64_t)bh * L + min(qrow, L - 1)];
-  {
+  uint4 daf[DY ? 4 : 1], dwf[DY ? 2 : 1][DY ? 4 : 1];
+  if constexpr (DY) {
+    // this wave's 16 rows of dy (k = 32 lg + 8 c) and the head's 32 rows of W_oᵀ, column-paired
+    // as the panel pairs them (tile t rows 4 t + 8 (li >> 2) + (li & 3) of the head's 32)
+    const char* ap = reinterpret_cast<const char*>(dy + ((int64_t)b * L + min(qrow, L - 1)) * 128 + lg * 32);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) daf[c] = *reinterpret_cast<const uint4*>(ap + 16 * c);
+    const int wrow = 8 * (li >> 2) + (li & 3);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const char* wp = reinterpret_cast<const char*>(wot + (int64_t)(32 * h + 4 * t + wrow) * 128 + lg * 32);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dwf[t][c] = *reinterpret_cast<const uint4*>(wp + 16 * c);
+    }
+    HeadStage<DH, 3> st;
+    const bf16_t* const src[3] = {base, base + D, base + 2 * D};
+    const int64_t lds3[3] = {ld, ld, ld};
+    st.load(src, lds3, L, threadIdx.x);
+    char* const dst[3] = {sQ, sK, sV};
+    st.store(dst, L, threadIdx.x);
+  } else {
     HeadStage<DH, 4> st;
     const bf16_t* const src[4] = {base, base + D, base + 2 * D, dctx + (int64_t)b * L * D + (int64_t)h * DH};
     const int64_t lds4[4] = {ld, ld, ld, (int64_t)D};
     st.load(src, lds4, L, threadIdx.x);
     char* const dst[4] = {sQ, sK, sV, sdO};
     st.store(dst, L, threadIdx.x);
+  }
+  if constexpr (DY) {   // dO rows of this wave's tile (rows >= L zero, as the staging writes them)
+    f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) Mma<bf16_t>::run(acc[t], dwf[t][c], daf[c]);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = acc[0][e] + 0.f; v[4 + e] = acc[1][e] + 0.f; }
+    const bool live = qrow < L;
+    *reinterpret_cast<uint4*>(sdO + qrow * G::P + lg * 16) =
+        live ? make_uint4(a_pk2(v[0], v[1]), a_pk2(v[2], v[3]), a_pk2(v[4], v[5]), a_pk2(v[6], v[7]))
+             : make_uint4(0u, 0u, 0u, 0u);
   }
   __shared__ uint64_t s_kv;
   if (wave == 0) {
@@ -950,6 +992,24 @@ extern "C" int ttmi_qkv_attn_fwd(int dtype, int B, int L, int H, int Dh, const v
   QaArgs g{(const bf16_t*)a, (const bf16_t*)w_in, b_in, key_valid, (bf16_t*)qkv, (bf16_t*)ctx, lse,
            make_drop(drop_p, drop_seed), 1.f / sqrtf((float)Dh), B, L, qa_spw(L)};
   hipLaunchKernelGGL(qkv_attn_fwd_kernel, dim3((B + g.spw - 1) / g.spw), dim3(1024), 0, s, g);
+  return ttmi_check_launch(fn);
+}
+
+extern "C" int ttmi_mha_bwd_dy(int B, int L, int H, int Dh, const void* qkv, const int64_t* key_valid,
+                               const float* lse, const void* dy, const void* wot, float drop_p,
+                               const uint64_t* drop_seed, void* dqkv, hipStream_t s) {
+  static const char* fn = "ttmi_mha_bwd_dy";
+  int rc = check_mha(fn, TTMI_BF16, B, L, H, Dh, qkv, key_valid, drop_p);
+  if (rc) return rc;
+  TTMI_REQUIRE(Dh == 32 && H * Dh == 128 && L <= LP, "%s: serves bf16, H*Dh = 128 with Dh = 32, L <= 64", fn);
+  TTMI_REQUIRE(lse && dy && wot && dqkv, "%s: null argument", fn);
+  TTMI_REQUIRE((((uintptr_t)dy | (uintptr_t)wot) & 15) == 0 && ((uintptr_t)dqkv & 7) == 0,
+               "%s: dy / wot must be 16-byte, dqkv 8-byte aligned", fn);
+  TTMI_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "%s: drop_p out of [0,1)", fn);
+  if (B == 0) return TTMI_OK;
+  hipLaunchKernelGGL((mha2_bwd_kernel<32, true>), dim3(B * H), dim3(256), 0, s, L, H, (const bf16_t*)qkv,
+                     key_valid, lse, nullptr, make_drop(drop_p, drop_seed), (bf16_t*)dqkv, 1.f / sqrtf(32.f),
+                     (const bf16_t*)dy, (const bf16_t*)wot);
   return ttmi_check_launch(fn);
 }
 

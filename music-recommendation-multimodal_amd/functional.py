@@ -197,6 +197,11 @@ def _q1_proj_ok(w_in: Tensor, a1: Tensor, L: int, H: int) -> bool:
             and a1.is_contiguous())
 
 
+# the attention backward computes dctx from dy1 itself (ttmi_mha_bwd_dy); TTMI_NO_DYATT=1
+# restores the out-projection input-grad launch (A/B measurements)
+_DYATT = os.environ.get("TTMI_NO_DYATT", "0") != "1"
+
+
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
@@ -432,11 +437,15 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         drows = s.rows
         F_ = W[pre + "linear1.weight"].shape[0]
         fuse = _ln_fusable(W, pre, D, R)
+        # the attention backward computes dctx = dy1·W_o itself (ttmi_mha_bwd_dy, ABI 21)
+        wot = W.get(transposed_name(pre + "self_attn.out_proj.weight"))
+        dy_attn = (_DYATT and drows is None and dt == torch.bfloat16 and D == 128 and H == 4 and L <= 64
+                   and wot is not None and not (head is not None and i == cfg.n_layers - 1))
         if head is not None and i == cfg.n_layers - 1:
             dctx, dx1 = head["dctx"], head["dx1"]
         else:
             dx1, dctx, dy2_next = _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre,
-                                                  R, drows, F_, fuse, D, dt, p)
+                                                  R, drows, F_, fuse, D, dt, p, want_dctx=not dy_attn)
         dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         if drows is not None:
             ops.mha_q1_bwd(s.qkv, st.key_valid, drows, s.lse, dctx, B, L, H, dqkv,
@@ -444,6 +453,9 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
             if bn_co is not None:
                 bn_co.finish()
                 bn_co = None
+        elif dy_attn:      # (dctx holds dy1 here)
+            ops.mha_bwd_dy(s.qkv, st.key_valid, s.lse, dctx, wot, B, L, H, dqkv,
+                           _drop(cfg, seeds, site_attn(i)))
         else:
             ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
                         _drop(cfg, seeds, site_attn(i)))
@@ -523,10 +535,12 @@ def _head_bwd_unfused(P, W, st, du, grads, cfg, du16, gathered):
     return dx
 
 
-def _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre, R, drows, F_, fuse, D, dt, p):
+def _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre, R, drows, F_, fuse, D, dt, p,
+                    want_dctx=True):
     """One encoder layer's backward from its output grad dx down to dctx (FFN, LN2, residual,
     out_proj input grad).  Returns dx1 (the grad of the attention residual), dctx and the
-    pending dy2 (None)."""
+    pending dy2 (None).  ``want_dctx`` False: dctx is left to the attention backward
+    (ttmi_mha_bwd_dy) and dy1, the out-projection's output grad, is returned in its place."""
     dev = dx.device
     f32 = dict(device=dev, dtype=torch.float32)
     if dy2_next is not None:
@@ -553,6 +567,8 @@ def _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre, R, drows, 
         ops.dropout_bwd(dx1, dy1, None, _drop(cfg, seeds, site_drop1(i)), drop_rows=drows)
     ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"],
                   grads[pre + "self_attn.out_proj.bias"])
+    if not want_dctx:
+        return dx1, dy1, None
     dctx = torch.empty(R, D, device=dev, dtype=dt)
     _dx(dy1, W, pre + "self_attn.out_proj.weight", dctx)
     return dx1, dctx, None

@@ -225,6 +225,7 @@ SIGNATURES = {
     "ttmi_mha_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_qkv_attn_supported": (c_i, [c_i, c_i, c_i, c_i]),
+    "ttmi_mha_bwd_dy": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_mha_q1_proj_gather_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p,
                                           c_p, c_p, c_p, c_p]),
     "ttmi_qkv_attn_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p,

@@ -806,6 +806,18 @@ def mha_bwd(qkv: Tensor, key_valid: Tensor, lse: Tensor, dctx: Tensor, B: int, L
     return dqkv
 
 
+def mha_bwd_dy(qkv: Tensor, key_valid: Tensor, lse: Tensor, dy: Tensor, wot: Tensor, B: int, L: int,
+               H: int, dqkv: Tensor, drop: Drop = NO_DROP) -> Tensor:
+    """mha_bwd with dctx = dy·W_o computed in the launch (ABI 21; wot = the W_oᵀ mirror):
+    bit-identical to linear(dy, wot) + mha_bwd where the row panel serves that linear."""
+    _dev(qkv, key_valid, lse, dy, wot, dqkv)
+    Dh = qkv.shape[1] // (3 * H)
+    _q1_batch_check("mha_bwd_dy", B, L, H, drop)
+    call("ttmi_mha_bwd_dy", B, L, H, Dh, _p(qkv), _p(key_valid), _p(lse), _p(dy), _p(wot), float(drop[0]),
+         _p(drop[1]), _p(dqkv), _s())
+    return dqkv
+
+
 # ----------------------------------------------------------------------------- user head
 def user_concat_fwd(x: Tensor, len_src: Optional[Tensor], gender: Tensor, G: Tensor,
                     country: Tensor, C: Tensor, comb: Tensor, rows: Tensor, B: int, L: int):

@@ -119,3 +119,33 @@ def test_q1_proj_gather_matches_full_projection(gpu_pkg, B, L, p):
     fin = torch.isfinite(l0)
     assert torch.equal(fin, torch.isfinite(l1))
     assert float((l1[fin] - l0[fin]).abs().max()) <= 1e-2
+
+
+@pytest.mark.parametrize("B,L,p", [(512, 50, 0.1), (7, 50, 0.0), (33, 64, 0.1), (21, 20, 0.1)])
+def test_mha_bwd_dy_matches_linear_then_mha_bwd(gpu_pkg, B, L, p):
+    """ttmi_mha_bwd_dy (dctx = dy·W_o computed in the attention backward) against
+    ttmi_linear(dy, W_oᵀ) + ttmi_mha_bwd: bit-identical where the row panel serves the linear
+    (M >= 2048), else within bf16 rounding of dctx's accumulation order."""
+    ops = gpu_pkg.ops
+    H, D = 4, 128
+    g = torch.Generator().manual_seed(31 * L + B)
+    qkv = (torch.randn(B * L, 3 * D, generator=g) * 1.5).to(torch.bfloat16).to(DEV)
+    dy = torch.randn(B * L, D, generator=g).to(torch.bfloat16).to(DEV)
+    wot = (torch.randn(D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    kv = _masks(B, L, g).to(DEV)
+    drop = (p, _seed(0xD0D0 + L)) if p > 0 else (0.0, None)
+    ctx = torch.empty(B * L, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * L, device=DEV)
+    ops.mha_fwd(qkv, kv, B, L, H, ctx, lse, drop)
+    dctx = torch.empty(B * L, D, device=DEV, dtype=torch.bfloat16)
+    ops.linear(dy, wot, None, dctx)
+    d0 = torch.empty(B * L, 3 * D, device=DEV, dtype=torch.bfloat16)
+    ops.mha_bwd(qkv, kv, lse, dctx, B, L, H, d0, drop)
+    d1 = torch.full_like(d0, float("nan"))
+    ops.mha_bwd_dy(qkv, kv, lse, dy, wot, B, L, H, d1, drop)
+    torch.cuda.synchronize()
+    if B * L >= 2048:
+        assert torch.equal(d1.view(torch.int16), d0.view(torch.int16))
+    else:
+        err = (d1.float() - d0.float()).abs().max()
+        assert float(err) <= 0.02 * float(d0.float().abs().max()) + 1e-3, float(err)
