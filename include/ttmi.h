@@ -241,6 +241,23 @@ int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
 int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                  const int64_t* key_valid, const float* lse, const void* dctx, float drop_p,
                  const uint64_t* drop_seed, void* dqkv, hipStream_t stream);
+/* The encoder layer's whole attention sub-block forward in one launch (ABI 21; reference
+ * user_tower.py:37-45, norm_first): ttmi_qkv_attn_fwd's qkv / ctx / lse, then
+ *   x1 = res + drop1(ctx·woᵀ + bo)   (fp32 [B*L, 128]; drop1 index m·128 + n)
+ *   a2 = norm2(x1) (bf16), m2 / r2 its row mean / rstd
+ * as ttmi_linear_res_ln computes them (the row statistics summed in another order).  bf16,
+ * H*Dh = 128 with Dh = 32, 38 <= L <= 64 (two sequences per workgroup). */
+typedef struct ttmi_attn_block_desc {
+  int B, L, H, Dh;
+  const void* a; const void* w_in; const float* b_in; const int64_t* key_valid;
+  float drop_p; const uint64_t* drop_seed;         /* the attention probabilities */
+  void* qkv; void* ctx; float* lse;
+  const void* wo; const float* bo; const float* res; const float* n2w; const float* n2b;
+  float eps;
+  float drop1_p; const uint64_t* drop1_seed;       /* the out-projection's output */
+  float* x1; void* a2; float* m2; float* r2;
+} ttmi_attn_block_desc;
+int ttmi_attn_block_fwd(const ttmi_attn_block_desc* d, hipStream_t stream);
 /* ttmi_mha_bwd with dctx computed in the launch from the out-projection's output gradient
  * (ABI 21): dctx = dy·W_o (dy [B*L, 128] bf16; wot = W_oᵀ, the transposed k-major mirror,
  * [128, 128] bf16), rounded to bf16 with ttmi_linear's fragment and MFMA order, so dqkv is

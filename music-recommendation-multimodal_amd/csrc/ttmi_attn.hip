@@ -415,7 +415,7 @@ struct HeadStage {
 template <int DH, int P>
 TTMI_DEV void attn_tile_fwd(const char* sQ, const char* sK, const char* sV, uint64_t kvm, int i,
                             int L, int lane, const DropKeys& dk, uint32_t pbase, float scale,
-                            bf16_t* ctx, int D, float* lse) {
+                            bf16_t* ctx, int D, float* lse, f32x4_t* o_out = nullptr) {
   if (16 * i >= L) return;
   // The per-score work is VALU-issue bound (the softmax, the mask and the dropout hash over 16
   // scores a lane): key tiles above the diagonal (t > i, wave-uniform) are skipped outright, the
@@ -488,6 +488,10 @@ TTMI_DEV void attn_tile_fwd(const char* sQ, const char* sK, const char* sV, uint
     const uint4 pf = a_freg(s[2 * c], s[2 * c + 1]);
 #pragma unroll
     for (int u = 0; u < DH / 16; ++u) Mma<bf16_t>::run(o[u], a_ft<P>(sV, 16 * u, c, lane), pf);
+  }
+  if (o_out != nullptr) {
+#pragma unroll
+    for (int u = 0; u < DH / 16; ++u) o_out[u] = o[u];
   }
   if (q < L) {
     bf16_t* dst = ctx + (int64_t)q * D + 4 * lg;
@@ -774,6 +778,10 @@ struct QaArgs {
   DropParams dp;
   float scale;
   int B, L, spw;
+  // OP (ABI 21, ttmi_attn_block_fwd): the out-projection, residual, dropout 1 and norm2 too
+  const bf16_t* wo; const float* bo; const float* res; const float* n2w; const float* n2b;
+  float eps; DropParams dp1;
+  float* x1; bf16_t* a2; float* m2; float* r2;
 };
 
 // s_waitcnt vmcnt(N) for a wave-dependent N in {lo, hi}
@@ -783,11 +791,23 @@ TTMI_DEV void qa_wait(bool hi) {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LO) : "memory");
 }
 
+// OP: the attention's out-projection, residual (+ dropout 1) and norm2 in the same launch
+// (user_tower.py:37-45, norm_first: x1 = x + drop1(ctx·W_oᵀ + b_o), a2 = norm2(x1)).  W_o is
+// DMA'd into the consumed W2 image under the attention, the context rows stay in registers
+// until the attention's last read of the Q / K / V images, then become an LDS image over K's.
+// Each wave computes one row tile's half (64 columns); norm2's row statistics meet across the
+// two halves through LDS.  Two rounds of (sequence, head) pairs at most (spw <= 2).
+constexpr int QA_PI = 3;                          // OP: b_o, norm2 weight / bias, 1 KB slot each
+template <bool OP>
 __global__ __launch_bounds__(1024) void qkv_attn_fwd_kernel(QaArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * QA_WBUF + QA_IMG + QA_BI * 1024];
+  __shared__ __attribute__((aligned(16))) char smem[3 * QA_WBUF + QA_IMG + QA_BI * 1024 + (OP ? QA_PI * 1024 : 0)];
   __shared__ uint64_t s_kv[QA_MAXSEQ];
+  __shared__ float s_red[OP ? 2 : 1][8][2][16];  // OP: norm2's per-half row sums (mean, variance)
   char* const sq = smem + 3 * QA_WBUF;            // A staging, then the Q image
   const float* const sbias = reinterpret_cast<const float*>(sq + QA_IMG);
+  const float* const sbo = sbias + QA_BI * 256;   // OP: b_o, n2w, n2b at 1 KB strides
+  const float* const sn2w = sbo + 256;
+  const float* const sn2b = sbo + 512;
   TTMI_TSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
   const int L = g.L, b0 = blockIdx.x * g.spw, nseq = min(g.spw, g.B - b0), R = nseq * L;
@@ -802,6 +822,13 @@ __global__ __launch_bounds__(1024) void qkv_attn_fwd_kernel(QaArgs g) {
     const i32x4_t rb = make_rsrc(g.bias, 3 * QA_D * 4);
     const i32x4_t rw = make_rsrc(g.w, wbytes);
     const uint32_t lw = lds_addr(smem), la = lds_addr(sq), lb = lds_addr(sq + QA_IMG);
+    if constexpr (OP) {      // (batch 0: older than the W1 / W2 batches the waits below count)
+      if (wave >= QA_NW - QA_PI) {
+        const int k = wave - (QA_NW - QA_PI);
+        const float* src = k == 0 ? g.bo : (k == 1 ? g.n2w : g.n2b);
+        dma16(make_rsrc(src, QA_D * 4), (uint32_t)(lane * 16), lb + (QA_BI + k) * 1024);
+      }
+    }
 #pragma unroll
     for (int t = 0; t < (QA_I0 + QA_NW - 1) / QA_NW; ++t) {
       const int ii = wave + QA_NW * t;            // wave-uniform branches
@@ -895,6 +922,29 @@ __global__ __launch_bounds__(1024) void qkv_attn_fwd_kernel(QaArgs g) {
   }
   __syncthreads();
   TTMI_TSTAMP(2);
+  // the dropout seeds and (OP) the residual values are loaded BEFORE W_o's DMAs: a compiler-
+  // counted wait for them then never includes the DMAs behind it (vmcnt retires in order)
+  const DropKeys dk = resolve_drop(g.dp);
+  const DropKeys dk1 = OP ? resolve_drop(g.dp1) : dk;
+  float4 rpre[OP ? 4 : 1];
+  if constexpr (OP) {
+    const float* rp = g.res + (r0 + min(row, R - 1)) * QA_D + 64 * half + 8 * lg;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      rpre[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
+      rpre[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
+    }
+    // W_o into the consumed W2 image (lands under the attention)
+    const i32x4_t ro = make_rsrc(g.wo, QA_D * QA_D * 2);
+    const uint32_t lo = lds_addr(smem + 2 * QA_WBUF);
+#pragma unroll
+    for (int t = 0; t < (QA_WI + QA_NW - 1) / QA_NW; ++t) {
+      const int j = wave + QA_NW * t;
+      if (j >= QA_WI) break;
+      const int q = j * 64 + lane, n = q / QA_CPR, c = q % QA_CPR;
+      dma16(ro, c == QA_CPR - 1 ? (uint32_t)(QA_D * QA_D * 2) : (uint32_t)((n * QA_D + 8 * c) * 2), lo + j * 1024);
+    }
+  }
   // ---- qkv to HBM from the images (coalesced 16-byte stores, in flight under the attention)
   for (int i = tid; i < R * 48; i += 64 * QA_NW) {
     const int r = i / 48, c = i % 48, m = c >> 4;  // m: Q (A region), K (W0), V (W1)
@@ -904,17 +954,114 @@ __global__ __launch_bounds__(1024) void qkv_attn_fwd_kernel(QaArgs g) {
   // ---- attention: round s handles sequence s, wave w its head w >> 2 and query tile w & 3 on
   // even rounds, 3 - (w & 3) on odd ones (tile i costs i + 1 key tiles: pairing i with 3 - i
   // evens the waves' work, the workgroup ends with its slowest wave)
-  const DropKeys dk = resolve_drop(g.dp);
+  f32x4_t oc[OP ? 2 : 1][2];
+  if constexpr (OP) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) oc[s][0] = oc[s][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
   for (int s = 0; s < nseq; ++s) {
     const int h = wave >> 2, qt = (s & 1) ? 3 - (wave & 3) : (wave & 3);
     const int64_t bh = (int64_t)(b0 + s) * 4 + h;
     const int off = s * L * QA_P + h * 64;
     attn_tile_fwd<32, QA_P>(sq + off, smem + off, smem + QA_WBUF + off, s_kv[s], qt, L, lane, dk,
                             (uint32_t)(bh * L * L), g.scale, g.ctx + (r0 + (int64_t)s * L) * QA_D + h * 32,
-                            QA_D, g.lse + bh * L);
+                            QA_D, g.lse + bh * L, OP ? oc[s & 1] : nullptr);
   }
   TTMI_TSTAMP(3);
+  if constexpr (OP) {
+    __syncthreads();                              // every wave is past its Q / K / V reads
+    char* const sctx = smem;                      // the context image over K's
+    {
+      const int h = wave >> 2;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s >= nseq) break;
+        const int qt = (s & 1) ? 3 - (wave & 3) : (wave & 3), q = 16 * qt + li;
+        if (q < L) {
+          char* dst = sctx + (s * L + q) * QA_P + (h * 32 + 4 * lg) * 2;
+          a_st4(dst, oc[s][0]);
+          a_st4(dst + 32, oc[s][1]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W_o landed (this wave's DMAs)
+    __syncthreads();
+    // ---- x1 = res + drop1(ctx·W_oᵀ + b_o) for this wave's row tile, 64 columns
+    f32x4_t acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (mine) {
+      uint4 cf[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) cf[c] = lds16(sctx + row * QA_P + lg * 64 + 16 * c);
+      const char* wb = smem + 2 * QA_WBUF + (64 * half + wrow) * QA_P + lg * (QA_D / 2);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          Mma<bf16_t>::run(acc[t], lds16(wb + (32 * (t >> 1) + 4 * (t & 1)) * QA_P + 16 * c), cf[c]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    const int64_t m = r0 + row;
+    const bool mok = mine && row < R;
+    float vr[16];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = 64 * half + 32 * p + 8 * lg;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * p][e] + sbo[n + e];
+        v[4 + e] = acc[2 * p + 1][e] + sbo[n + 4 + e];
+      }
+      drop_apply_vec<8>(dk1, (uint32_t)(m * QA_D + n), v);
+      const float4 q0 = rpre[2 * p], q1 = rpre[2 * p + 1];
+      v[0] += q0.x; v[1] += q0.y; v[2] += q0.z; v[3] += q0.w;
+      v[4] += q1.x; v[5] += q1.y; v[6] += q1.z; v[7] += q1.w;
+      if (mok) {
+        float* xp = g.x1 + m * QA_D + n;
+        *reinterpret_cast<float4*>(xp) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(xp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vr[8 * p + e] = v[e];
+    }
+    // ---- a2 = norm2(x1): the row's 128 columns over two waves (mean, then variance)
+    float s1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s1 += vr[e];
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    if (lg == 0) s_red[0][rt][half][li] = s1;
+    __syncthreads();
+    const float mu = (s_red[0][rt][0][li] + s_red[0][rt][1][li]) * (1.f / QA_D);
+    float s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s2 += (vr[e] - mu) * (vr[e] - mu);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (lg == 0) s_red[1][rt][half][li] = s2;
+    __syncthreads();
+    const float rs = 1.f / sqrtf((s_red[1][rt][0][li] + s_red[1][rt][1][li]) * (1.f / QA_D) + g.eps);
+    if (mok) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int n = 64 * half + 32 * p + 8 * lg;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (vr[8 * p + e] - mu) * rs * sn2w[n + e] + sn2b[n + e];
+        *reinterpret_cast<uint4*>(g.a2 + m * QA_D + n) =
+            make_uint4(a_pk2(o[0], o[1]), a_pk2(o[2], o[3]), a_pk2(o[4], o[5]), a_pk2(o[6], o[7]));
+      }
+      if (half == 0 && lg == 0) {
+        g.m2[m] = mu;
+        g.r2[m] = rs;
+      }
+    }
+  }
 }
+
 
 // sequences per workgroup for the fused kernel: the most whose rows fit the 7 row tiles and
 // whose last key tile stays inside the image; 0 = shape not served
@@ -991,7 +1138,35 @@ extern "C" int ttmi_qkv_attn_fwd(int dtype, int B, int L, int H, int Dh, const v
   if (B == 0) return TTMI_OK;
   QaArgs g{(const bf16_t*)a, (const bf16_t*)w_in, b_in, key_valid, (bf16_t*)qkv, (bf16_t*)ctx, lse,
            make_drop(drop_p, drop_seed), 1.f / sqrtf((float)Dh), B, L, qa_spw(L)};
-  hipLaunchKernelGGL(qkv_attn_fwd_kernel, dim3((B + g.spw - 1) / g.spw), dim3(1024), 0, s, g);
+  hipLaunchKernelGGL(qkv_attn_fwd_kernel<false>, dim3((B + g.spw - 1) / g.spw), dim3(1024), 0, s, g);
+  return ttmi_check_launch(fn);
+}
+
+extern "C" int ttmi_attn_block_fwd(const ttmi_attn_block_desc* d, hipStream_t s) {
+  static const char* fn = "ttmi_attn_block_fwd";
+  TTMI_REQUIRE(d != nullptr, "%s: null descriptor", fn);
+  int rc = check_mha(fn, TTMI_BF16, d->B, d->L, d->H, d->Dh, d->qkv, d->key_valid, d->drop_p);
+  if (rc) return rc;
+  const int spw = qa_spw(d->L);
+  TTMI_REQUIRE(d->H * d->Dh == QA_D && d->Dh == 32 && spw > 0 && spw <= 2,
+               "%s: serves bf16, H*Dh = 128 with Dh = 32 and 38 <= L <= 64 (got L=%d)", fn, d->L);
+  TTMI_REQUIRE(d->a && d->w_in && d->b_in && d->ctx && d->lse && d->wo && d->bo && d->res && d->n2w && d->n2b &&
+                   d->x1 && d->a2 && d->m2 && d->r2, "%s: null argument", fn);
+  TTMI_REQUIRE((((uintptr_t)d->a | (uintptr_t)d->w_in | (uintptr_t)d->b_in | (uintptr_t)d->ctx | (uintptr_t)d->wo |
+                 (uintptr_t)d->bo | (uintptr_t)d->res | (uintptr_t)d->n2w | (uintptr_t)d->n2b | (uintptr_t)d->x1 |
+                 (uintptr_t)d->a2) & 15) == 0, "%s: operands must be 16-byte aligned", fn);
+  TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f && d->drop1_p >= 0.f && d->drop1_p < 1.f,
+               "%s: dropout out of [0,1)", fn);
+  if (d->B == 0) return TTMI_OK;
+  QaArgs g{};
+  g.a = (const bf16_t*)d->a; g.w = (const bf16_t*)d->w_in; g.bias = d->b_in; g.kvalid = d->key_valid;
+  g.qkv = (bf16_t*)d->qkv; g.ctx = (bf16_t*)d->ctx; g.lse = d->lse;
+  g.dp = make_drop(d->drop_p, d->drop_seed); g.scale = 1.f / sqrtf((float)d->Dh);
+  g.B = d->B; g.L = d->L; g.spw = spw;
+  g.wo = (const bf16_t*)d->wo; g.bo = d->bo; g.res = d->res; g.n2w = d->n2w; g.n2b = d->n2b; g.eps = d->eps;
+  g.dp1 = make_drop(d->drop1_p, d->drop1_seed);
+  g.x1 = d->x1; g.a2 = (bf16_t*)d->a2; g.m2 = d->m2; g.r2 = d->r2;
+  hipLaunchKernelGGL(qkv_attn_fwd_kernel<true>, dim3((d->B + spw - 1) / spw), dim3(1024), 0, s, g);
   return ttmi_check_launch(fn);
 }
 

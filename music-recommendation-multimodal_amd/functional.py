@@ -185,6 +185,10 @@ def _qa_ok(w_in: Tensor, a1: Tensor, L: int, H: int) -> bool:
             and ops.qkv_attn_supported(a1.dtype, L, H, D // H))
 
 
+# the attention sub-block in one launch (ttmi_attn_block_fwd); TTMI_NO_BLOCK=1 runs the
+# out-projection + residual + norm2 as its own launch (A/B measurements)
+_BLOCK = os.environ.get("TTMI_NO_BLOCK", "0") != "1"
+
 # the pruned layer's query projected inside the one-query attention (ttmi_mha_q1_proj_gather_fwd);
 # TTMI_NO_Q1PROJ=1 restores the full 384-column projection (A/B measurements)
 _Q1PROJ = os.environ.get("TTMI_NO_Q1PROJ", "0") != "1"
@@ -322,15 +326,25 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             rows, R, res_in, drows = None, M, x, None
             ctx = torch.empty(M, D, device=dev, dtype=dt)
             lse = torch.empty(B * H * L, **f32)
-            if fused_qa:     # in_proj + attention, one launch (bit-identical to the pair at M >= 2048)
+        x1 = torch.empty(R, D, **f32)
+        a2, m2, r2 = ln_out(R)
+        name = pre + "self_attn.out_proj.weight"
+        block = (not pruned and fused_qa and _BLOCK and 38 <= L <= 64 and W[name].dtype == torch.bfloat16
+                 and tuple(W[name].shape) == (D, D))
+        if not pruned:
+            if block:        # in_proj + attention + out_proj + residual + norm2, one launch
+                ops.attn_block_fwd(a1, w_in, b_in, key_valid, B, L, H, qkv, ctx, lse,
+                                   _drop(cfg, seeds, site_attn(i)), W[name], P[pre + "self_attn.out_proj.bias"],
+                                   res_in, P[pre + "norm2.weight"], P[pre + "norm2.bias"], cfg.eps,
+                                   _drop(cfg, seeds, site_drop1(i)), x1, a2, m2, r2)
+            elif fused_qa:   # in_proj + attention, one launch (bit-identical to the pair at M >= 2048)
                 ops.qkv_attn_fwd(a1, w_in, b_in, key_valid, B, L, H, qkv, ctx, lse,
                                  _drop(cfg, seeds, site_attn(i)))
             else:
                 ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
-        x1 = torch.empty(R, D, **f32)
-        a2, m2, r2 = ln_out(R)
-        name = pre + "self_attn.out_proj.weight"
-        if not pruned and _resln_ok(W, name, D, R):    # out_proj + residual + norm2, one kernel
+        if block:
+            pass
+        elif not pruned and _resln_ok(W, name, D, R):    # out_proj + residual + norm2, one kernel
             ops.linear_res_ln(ctx, W[name], P[pre + "self_attn.out_proj.bias"], res_in, x1,
                               P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2,
                               eps=cfg.eps, drop=_drop(cfg, seeds, site_drop1(i)))

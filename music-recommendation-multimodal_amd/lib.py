@@ -133,6 +133,18 @@ class UserHeadDesc(ctypes.Structure):
                 ("n_genders", c_i), ("n_countries", c_i), ("id_err", c_p), ("ffn_ws", c_p)]
 
 
+class AttnBlockDesc(ctypes.Structure):
+    """ttmi_attn_block_desc (include/ttmi.h, ABI 21)."""
+    _fields_ = [("B", c_i), ("L", c_i), ("H", c_i), ("Dh", c_i),
+                ("a", c_p), ("w_in", c_p), ("b_in", c_p), ("key_valid", c_p),
+                ("drop_p", ctypes.c_float), ("drop_seed", c_p),
+                ("qkv", c_p), ("ctx", c_p), ("lse", c_p),
+                ("wo", c_p), ("bo", c_p), ("res", c_p), ("n2w", c_p), ("n2b", c_p),
+                ("eps", ctypes.c_float),
+                ("drop1_p", ctypes.c_float), ("drop1_seed", c_p),
+                ("x1", c_p), ("a2", c_p), ("m2", c_p), ("r2", c_p)]
+
+
 class UserHeadBwdDesc(ctypes.Structure):
     """ttmi_user_head_bwd_desc (include/ttmi.h)."""
     _fields_ = [("B", c_i), ("D", c_i), ("F", c_i), ("dg", c_i), ("dc", c_i),
@@ -226,6 +238,7 @@ SIGNATURES = {
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_qkv_attn_supported": (c_i, [c_i, c_i, c_i, c_i]),
     "ttmi_mha_bwd_dy": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "ttmi_attn_block_fwd": (c_i, [c_p, c_p]),
     "ttmi_mha_q1_proj_gather_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p,
                                           c_p, c_p, c_p, c_p]),
     "ttmi_qkv_attn_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p,

@@ -806,6 +806,25 @@ def mha_bwd(qkv: Tensor, key_valid: Tensor, lse: Tensor, dctx: Tensor, B: int, L
     return dqkv
 
 
+def attn_block_fwd(a: Tensor, w_in: Tensor, b_in: Tensor, key_valid: Tensor, B: int, L: int, H: int,
+                   qkv: Tensor, ctx: Tensor, lse: Tensor, drop: Drop, wo: Tensor, bo: Tensor,
+                   res: Tensor, n2w: Tensor, n2b: Tensor, eps: float, drop1: Drop, x1: Tensor,
+                   a2: Tensor, m2: Tensor, r2: Tensor) -> None:
+    """The attention sub-block forward in one launch (ttmi_attn_block_fwd, ABI 21): in_proj,
+    attention, out_proj + residual + dropout 1, norm2."""
+    _dev(a, w_in, b_in, key_valid, qkv, ctx, lse, wo, bo, res, n2w, n2b, x1, a2, m2, r2)
+    _q1_batch_check("attn_block_fwd", B, L, H, drop)
+    d = _L.AttnBlockDesc()
+    d.B, d.L, d.H, d.Dh = B, L, H, a.shape[1] // H
+    d.a, d.w_in, d.b_in, d.key_valid = _p(a), _p(w_in), _p(b_in), _p(key_valid)
+    d.drop_p, d.drop_seed = float(drop[0]), _p(drop[1])
+    d.qkv, d.ctx, d.lse = _p(qkv), _p(ctx), _p(lse)
+    d.wo, d.bo, d.res, d.n2w, d.n2b, d.eps = _p(wo), _p(bo), _p(res), _p(n2w), _p(n2b), float(eps)
+    d.drop1_p, d.drop1_seed = float(drop1[0]), _p(drop1[1])
+    d.x1, d.a2, d.m2, d.r2 = _p(x1), _p(a2), _p(m2), _p(r2)
+    call("ttmi_attn_block_fwd", ctypes.byref(d), _s())
+
+
 def mha_bwd_dy(qkv: Tensor, key_valid: Tensor, lse: Tensor, dy: Tensor, wot: Tensor, B: int, L: int,
                H: int, dqkv: Tensor, drop: Drop = NO_DROP) -> Tensor:
     """mha_bwd with dctx = dy·W_o computed in the launch (ABI 21; wot = the W_oᵀ mirror):

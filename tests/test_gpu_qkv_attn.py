@@ -149,3 +149,49 @@ def test_mha_bwd_dy_matches_linear_then_mha_bwd(gpu_pkg, B, L, p):
     else:
         err = (d1.float() - d0.float()).abs().max()
         assert float(err) <= 0.02 * float(d0.float().abs().max()) + 1e-3, float(err)
+
+
+@pytest.mark.parametrize("B,L,p", [(512, 50, 0.1), (7, 50, 0.0), (33, 64, 0.1), (5, 38, 0.1)])
+def test_attn_block_matches_qkv_attn_then_res_ln(gpu_pkg, B, L, p):
+    """ttmi_attn_block_fwd (in_proj + attention + out_proj + residual + dropout 1 + norm2 in one
+    launch) against ttmi_qkv_attn_fwd + ttmi_linear_res_ln: qkv / ctx / lse / x1 bit-identical
+    (the same MFMA orders, bias adds and dropout indices; the out-projection as the row panel
+    computes it from M = 2048 rows), norm2's outputs to its summation order (1e-5)."""
+    ops = gpu_pkg.ops
+    H, D = 4, 128
+    g = torch.Generator().manual_seed(5 * L + B)
+    a = torch.randn(B * L, D, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(3 * D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    wo = (torch.randn(D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    bo = (torch.randn(D, generator=g) * 0.1).to(DEV)
+    res = torch.randn(B * L, D, generator=g).to(DEV)
+    n2w, n2b = (1 + 0.1 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    kv = _masks(B, L, g).to(DEV)
+    drop = (p, _seed(0xB10C + L)) if p > 0 else (0.0, None)
+    drop1 = (p, _seed(0xB10D + L)) if p > 0 else (0.0, None)
+    M = B * L
+    bf = dict(device=DEV, dtype=torch.bfloat16)
+    outs = []
+    for fused in (False, True):
+        qkv, ctx = torch.empty(M, 3 * D, **bf), torch.empty(M, D, **bf)
+        lse = torch.empty(B * H * L, device=DEV)
+        x1, a2 = torch.empty(M, D, device=DEV), torch.empty(M, D, **bf)
+        m2, r2 = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+        if fused:
+            ops.attn_block_fwd(a, w, b, kv, B, L, H, qkv, ctx, lse, drop, wo, bo, res, n2w, n2b, 1e-5, drop1,
+                               x1, a2, m2, r2)
+        else:
+            ops.qkv_attn_fwd(a, w, b, kv, B, L, H, qkv, ctx, lse, drop)
+            ops.linear_res_ln(ctx, wo, bo, res, x1, n2w, n2b, a2, m2, r2, eps=1e-5, drop=drop1)
+        torch.cuda.synchronize()
+        outs.append((qkv, ctx, lse, x1, a2, m2, r2))
+    (q0, c0, l0, x0, a0, mu0, r0), (q1, c1, l1, x1_, a1, mu1, r1) = outs
+    assert torch.equal(q1.view(torch.int16), q0.view(torch.int16))
+    assert torch.equal(c1.view(torch.int16), c0.view(torch.int16)) and torch.equal(l1, l0)
+    if M >= 2048:
+        assert torch.equal(x1_, x0)
+    else:
+        assert float((x1_ - x0).abs().max()) <= 1e-2 * float(x0.abs().max())
+    assert float((mu1 - mu0).abs().max()) <= 1e-4 and float(((r1 - r0) / r0).abs().max()) <= 1e-4
+    assert float((a1.float() - a0.float()).abs().max()) <= 0.02 * float(a0.float().abs().max())
