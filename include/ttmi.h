@@ -258,6 +258,28 @@ typedef struct ttmi_attn_block_desc {
   float* x1; void* a2; float* m2; float* r2;
 } ttmi_attn_block_desc;
 int ttmi_attn_block_fwd(const ttmi_attn_block_desc* d, hipStream_t stream);
+/* The encoder layer's feed-forward sub-block forward and the next layer's norm1 in one launch
+ * (ABI 21; reference user_tower.py:37-45, norm_first, then :111-116 for layer i + 1):
+ *   h  = drop_f(relu(a·w1ᵀ + b1))     bf16 [M, F] (drop_f index m·F + n; the FFN1 row panel's bits)
+ *   x2 = res + drop2(h·w2ᵀ + b2)       fp32 [M, D] (drop2 index m·D + n)
+ *   y  = bf16(LN(x2)·lnw + lnb), mean / rstd its row statistics
+ * as ttmi_linear(act = ReLU) + ttmi_linear_res_ln compute them, h never read back (x2 summed in
+ * hidden-unit order: equal to fp32 rounding).  bf16, D = 128, F in {256, 512}, M·F·2 < 2 GB;
+ * ttmi_ffn_block_supported(dtype, D, F) says whether a shape is served. */
+typedef struct ttmi_ffn_block_desc {
+  int M, D, F;
+  const void* a;                                   /* [M, D] bf16: norm2's output */
+  const void* w1; const float* b1;                 /* [F, D] bf16, [F] */
+  const void* w2; const float* b2;                 /* [D, F] bf16, [D] */
+  const float* res;                                /* [M, D] fp32: the sub-block's input x1 */
+  float dropf_p; const uint64_t* dropf_seed;
+  float drop2_p; const uint64_t* drop2_seed;
+  void* h; float* x2;
+  const float* lnw; const float* lnb; float eps;
+  void* y; float* mean; float* rstd;
+} ttmi_ffn_block_desc;
+int ttmi_ffn_block_supported(int dtype, int D, int F);
+int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t stream);
 /* ttmi_mha_bwd with dctx computed in the launch from the out-projection's output gradient
  * (ABI 21): dctx = dy·W_o (dy [B*L, 128] bf16; wot = W_oᵀ, the transposed k-major mirror,
  * [128, 128] bf16), rounded to bf16 with ttmi_linear's fragment and MFMA order, so dqkv is

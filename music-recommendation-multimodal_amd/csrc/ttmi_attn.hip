@@ -339,7 +339,7 @@ TTMI_DEV uint4 a_ft(const char* s, int row0, int c, int lane) {
   const uint2 lo = a_tr8(p), hi = a_tr8(p + 16 * P);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
-TTMI_DEV uint32_t a_pk2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+TTMI_DEV uint32_t a_pk2(float a, float b) { return pk_bf2(a, b); }
 TTMI_DEV uint4 a_freg(const f32x4_t& lo, const f32x4_t& hi) {
   return make_uint4(a_pk2(lo[0], lo[1]), a_pk2(lo[2], lo[3]), a_pk2(hi[0], hi[1]), a_pk2(hi[2], hi[3]));
 }

@@ -26,6 +26,14 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
 TTMI_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 TTMI_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// Two floats to a bf16 pair (a in the low half): the same RNE rounding as f2bf, one
+// v_cvt_pk_bf16_f32 (two scalar conversions pack through a shift and an or).
+typedef __bf16 ttmi_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float ttmi_f32x2_t __attribute__((ext_vector_type(2)));
+TTMI_DEV uint32_t pk_bf2(float a, float b) {
+  const ttmi_f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, ttmi_bf16x2_t));
+}
 
 template <typename T> struct Elem;
 template <> struct Elem<float> {
@@ -372,10 +380,10 @@ TTMI_DEV void unpack8(const uint4& q, float* v) {
 }
 TTMI_DEV uint4 pack8(const float* v) {
   uint4 q;
-  q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-  q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  q.x = pk_bf2(v[0], v[1]);
+  q.y = pk_bf2(v[2], v[3]);
+  q.z = pk_bf2(v[4], v[5]);
+  q.w = pk_bf2(v[6], v[7]);
   return q;
 }
 

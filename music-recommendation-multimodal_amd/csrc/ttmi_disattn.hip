@@ -76,7 +76,7 @@ TTMI_DEV uint4 ft(const char* s, int row0, int c, int lane) {
   const uint2 lo = lds_tr8(p), hi = lds_tr8(p + 16 * P);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
-TTMI_DEV uint32_t pk2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+TTMI_DEV uint32_t pk2(float a, float b) { return pk_bf2(a, b); }
 // ... and from score-layout registers (tile t holds columns 16t + 4·lg + e of row lane & 15).
 TTMI_DEV uint4 freg(const f32x4_t& lo, const f32x4_t& hi) {
   return make_uint4(pk2(lo[0], lo[1]), pk2(lo[2], lo[3]), pk2(hi[0], hi[1]), pk2(hi[2], hi[3]));

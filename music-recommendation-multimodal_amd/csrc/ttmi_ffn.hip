@@ -1,0 +1,310 @@
+// ttmi_ffn.hip — the encoder layer's feed-forward sub-block forward in one launch (ABI 21).
+//
+// Reference: nn.TransformerEncoderLayer(norm_first=True)'s _ff_block and its residual, then the
+// next layer's norm1 (user_tower.py:37-45, 111-116):
+//   h  = drop_f(relu(a2·W1ᵀ + b1))         bf16 [M, F]   (kept: the backward's gate and dW2 operand)
+//   x2 = x1 + drop2(h·W2ᵀ + b2)             fp32 [M, 128]
+//   y  = bf16(LN(x2)·w + b), mean / rstd    (the next layer's norm1)
+// The unfused pair (the FFN1 row panel, then ttmi_linear_res_ln) writes h and reads it back
+// (26 MB each way at cfg 2) and stages each weight image in its own launch.  Here h never
+// leaves the wave between the two GEMMs: FFN1's MFMA output fragment — lane (li, g) holds row li,
+// hidden units 32p + 8g .. +7 — is, bf16-packed, exactly the B-operand fragment of FFN2's k-step
+// over hidden units [32p, 32p + 32), so it feeds straight back (and is stored once for the
+// backward).  The weights stream through LDS in groups of 128 hidden units (the group's W1 rows
+// and W2 columns, two 128 x 128 bf16 images, 68 KB), double-buffered by LDS-DMA under the
+// previous group's MFMAs.  One 16-row tile per wave, NWV waves per workgroup.
+//
+// Bits: h is the FFN1 row panel's (same fragments, MFMA order, epilogue).  FFN2 sums its k-steps
+// in hidden-unit order (the row panel sums lane-group-strided k): x2 / y / mean / rstd agree
+// with ttmi_linear_res_ln to fp32 rounding, not bit for bit.
+#include "ttmi_common.h"
+
+namespace {
+
+constexpr int FB_D = 128;                    // the LayerNorm width (d_model)
+constexpr int FB_P = 2 * FB_D + 16;          // image row pitch (bytes): a lane group's 16 rows
+                                             // fall in distinct bank slots
+constexpr int FB_IMG = 128 * FB_P;           // one 128 x 128 bf16 image (34,816 B)
+constexpr int FB_BUF = 2 * FB_IMG;           // a group's W1 rows + W2 columns
+constexpr int FB_CPR = FB_D / 8 + 1;         // 16-byte chunks per image row (the last: pad zeros)
+constexpr int FB_INS = 128 * FB_CPR / 64;    // DMA wave-instructions per image (34)
+static_assert((128 * FB_CPR) % 64 == 0, "whole DMA instructions");
+
+struct FfnArgs {
+  const bf16_t* a; const bf16_t* w1; const float* b1; const bf16_t* w2; const float* b2;
+  const float* res; bf16_t* h; float* x2;
+  const float* lnw; const float* lnb; float eps; bf16_t* y; float* mean; float* rstd;
+  DropParams df, d2;
+  int M;
+};
+
+template <int NWV, int NG>
+__global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
+  constexpr int F = NG * 128;
+  // Every operand reaches LDS by LDS-DMA — the rows' A tile too, staged in buffer 1's W2 image
+  // — so no compiler-counted load sits among the DMAs: a compiler wait (vmcnt(0) before a
+  // register's first use) there would also wait for every DMA behind it.  Each wave issues the
+  // same number of wave-instructions per image (PW; the surplus re-issues an instruction another
+  // wave also issues: identical bytes), so one vmcnt immediate serves every wave.
+  static_assert(NWV == 8, "the vmcnt immediates below count 8 waves");
+  constexpr int PW = (FB_INS + NWV - 1) / NWV;           // 5 per 34-instruction image
+  constexpr int NPI = F / 256 + 5;                       // b1 (1 KB each), b2, LN w / b, 2 seeds
+  static_assert(NPI <= NWV, "one parameter instruction per wave");
+  constexpr int PB = F * 4;                              // parameter slots: b1 | b2 | lnw | lnb | seeds
+  __shared__ __attribute__((aligned(16))) char smem[2 * FB_BUF + PB + 5 * 1024];
+  char* const spar = smem + 2 * FB_BUF;
+  TTMI_TSTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int64_t r0 = (int64_t)blockIdx.x * (16 * NWV);
+  const int64_t m = r0 + 16 * wave + li;
+  const bool mok = m < g.M;
+  const int64_t mc = mok ? m : (int64_t)g.M - 1;
+  const uint32_t wbytes = (uint32_t)F * FB_D * 2;        // W1 and W2 alike
+  const uint32_t abytes = (uint32_t)min<int64_t>(16 * NWV, g.M - r0) * FB_D * 2;
+  const i32x4_t r1 = make_rsrc(g.w1, wbytes), r2 = make_rsrc(g.w2, wbytes);
+  const i32x4_t ra = make_rsrc(g.a + r0 * FB_D, abytes);  // rows past M: zeros
+  // per-lane offsets of this wave's PW slots of a 128-row image (row n, chunk c; the pad chunk
+  // reads at the range end: zeros); a W group adds a uniform shift (computed once: the row /
+  // chunk split was ~15 VALU a DMA)
+  uint32_t oA[PW], oW1[PW], oW2[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    int ii = wv + NWV * j;
+    if (ii >= FB_INS) ii -= FB_INS;
+    const int q = ii * 64 + lane, n = q / FB_CPR, c = q % FB_CPR;
+    const bool pad = c == FB_CPR - 1;
+    oA[j] = pad ? (uint32_t)(16 * NWV * FB_D * 2) : (uint32_t)((n * FB_D + 8 * c) * 2);
+    oW1[j] = pad ? wbytes : (uint32_t)((n * FB_D + 8 * c) * 2);
+    oW2[j] = pad ? wbytes : (uint32_t)((n * F + 8 * c) * 2);
+  }
+  auto slot = [&](int j) { int ii = wv + NWV * j; return ii >= FB_INS ? ii - FB_INS : ii; };
+  auto issue_a = [&]() {                                 // the A tile -> buffer 1's W2 image
+    const uint32_t base = lds_addr(smem + FB_BUF + FB_IMG);
+#pragma unroll
+    for (int j = 0; j < PW; ++j) dma16(ra, oA[j], base + slot(j) * 1024);
+  };
+  auto issue_w1 = [&](int grp) {                         // W1 rows [128 grp, +128)
+    const uint32_t base = lds_addr(smem + (grp & 1) * FB_BUF);
+#pragma unroll
+    for (int j = 0; j < PW; ++j) dma16(r1, oW1[j] + (uint32_t)(grp * 128 * FB_D * 2), base + slot(j) * 1024);
+  };
+  auto issue_w2 = [&](int grp) {                         // W2 columns [128 grp, +128)
+    const uint32_t base = lds_addr(smem + (grp & 1) * FB_BUF + FB_IMG);
+#pragma unroll
+    for (int j = 0; j < PW; ++j) dma16(r2, oW2[j] + (uint32_t)(grp * 128 * 2), base + slot(j) * 1024);
+  };
+  {                                                      // parameters and dropout seeds
+    const int k = wv < NPI ? wv : wv - NPI;              // (NPI <= 8 < 2 NPI)
+    const uint32_t dst = lds_addr(spar) + (uint32_t)(k * 1024);
+    const uint32_t off = (uint32_t)(lane * 16);
+    if (k < F / 256) dma16(make_rsrc(g.b1, PB), off + (uint32_t)(k * 1024), dst);
+    else if (k == F / 256) dma16(make_rsrc(g.b2, FB_D * 4), off, dst);
+    else if (k == F / 256 + 1) dma16(make_rsrc(g.lnw, FB_D * 4), off, dst);
+    else if (k == F / 256 + 2) dma16(make_rsrc(g.lnb, FB_D * 4), off, dst);
+    else if (k == F / 256 + 3) dma16(make_rsrc(g.df.seed, g.df.on ? 8 : 0), off, dst);
+    else dma16(make_rsrc(g.d2.seed, g.d2.on ? 8 : 0), off, dst);
+  }
+  issue_a();
+  issue_w1(0);
+  issue_w2(0);
+  if (NG > 1) issue_w1(1);
+  // in flight behind the parameters, the A tile and W1 group 0: W2 group 0 and W1 group 1
+  if (NG > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+  __syncthreads();
+  TTMI_TSTAMP(1);
+  const float* sb1 = reinterpret_cast<const float*>(spar);
+  const float* sb2 = reinterpret_cast<const float*>(spar + PB);
+  const float* slw = reinterpret_cast<const float*>(spar + PB + 1024);
+  const float* slb = reinterpret_cast<const float*>(spar + PB + 2048);
+  DropKeys dkf, dk2;
+  {
+    const uint64_t sf = *reinterpret_cast<const uint64_t*>(spar + PB + 3072);
+    const uint64_t s2 = *reinterpret_cast<const uint64_t*>(spar + PB + 4096);
+    dkf = DropKeys{(uint32_t)sf, (uint32_t)(sf >> 32), g.df.thresh, g.df.scale, g.df.on};
+    dk2 = DropKeys{(uint32_t)s2, (uint32_t)(s2 >> 32), g.d2.thresh, g.d2.scale, g.d2.on};
+  }
+  // the row's FFN1 operand: lane group lg holds k = 32 lg + 8c (the row panel's permutation)
+  uint4 af[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) af[c] = lds16(smem + FB_BUF + FB_IMG + (16 * wave + li) * FB_P + 64 * lg + 16 * c);
+  const int wrow = 8 * (li >> 2) + (li & 3);             // column-paired rows (the panel layout)
+  // h stores go through a buffer resource: rows past M are dropped by its range, so every wave
+  // issues exactly 4 stores a group and the vmcnt immediates below stay exact
+  const __amdgpu_buffer_rsrc_t rh =
+      __builtin_amdgcn_make_buffer_rsrc(g.h, 0, (int)((int64_t)g.M * F * 2), 0x00020000);
+  f32x4_t acc2[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc2[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float4 rpre[8];
+  uint64_t twait = 0;                                    // (diagnostic builds) ticks at the group seams
+#pragma unroll
+  for (int grp = 0; grp < NG; ++grp) {
+    const char* w1b = smem + (grp & 1) * FB_BUF + wrow * FB_P + 64 * lg;
+    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 16 * lg;
+    if (grp == NG - 1) {                                 // x1's row (after the last DMA: exact waits)
+      const float* rp = g.res + mc * FB_D + 8 * lg;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        rpre[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
+        rpre[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
+      }
+    }
+    // ---- FFN1: 16 rows x the group's 128 hidden units
+    f32x4_t acc1[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc1[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        Mma<bf16_t>::run(acc1[t], lds16(w1b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * c), af[c]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- h = drop_f(relu(. + b1)) -> bf16 fragments (stored for the backward)
+    uint4 hq[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = 128 * grp + 32 * p + 8 * lg;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = fmaxf(acc1[2 * p][e] + sb1[n + e], 0.f);
+        v[4 + e] = fmaxf(acc1[2 * p + 1][e] + sb1[n + 4 + e], 0.f);
+      }
+      drop_apply_vec<8>(dkf, (uint32_t)(m * F + n), v);
+      hq[p] = pack8(v);
+      const i32x4_t q = {(int)hq[p].x, (int)hq[p].y, (int)hq[p].z, (int)hq[p].w};
+      __builtin_amdgcn_raw_buffer_store_b128(q, rh, (uint32_t)((m * F + n) * 2), 0, 0);
+    }
+    if (grp == 0) {
+      // W2 group 0 landed (behind it: W1 group 1, this group's 4 h stores); every wave has read
+      // its A fragments, so W2 group 1 may overwrite the A tile
+      if (NG > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW + 4) : "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      __syncthreads();
+      if (NG > 1) issue_w2(1);
+    }
+    // ---- FFN2's k-steps over these hidden units
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 64 * p), hq[p]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (grp + 1 < NG) {
+      const uint64_t tw0 = TTMI_TNOW();
+      __syncthreads();                                   // every wave is done with this buffer
+      // group grp + 1 landed; younger: group grp + 2's DMAs and (grp >= 1) this group's h stores
+      // (group 0's precede W2 group 1)
+      if (grp + 2 < NG) {
+        issue_w1(grp + 2);
+        issue_w2(grp + 2);
+        if (grp == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW + 4) : "memory");
+      } else {
+        if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      __syncthreads();                                   // group grp + 1's image landed
+      twait += TTMI_TNOW() - tw0;
+    }
+    TTMI_TSTAMP(2 + (grp < 4 ? grp : 3));
+  }
+  // ---- x2 = x1 + drop2(. + b2); y = LN(x2) (the row's 128 columns in lanes li, li+16, li+32, li+48)
+  float vr[32];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int n = 32 * p + 8 * lg;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = acc2[2 * p][e] + sb2[n + e];
+      v[4 + e] = acc2[2 * p + 1][e] + sb2[n + 4 + e];
+    }
+    drop_apply_vec<8>(dk2, (uint32_t)(m * FB_D + n), v);
+    const float4 r0 = rpre[2 * p], r1v = rpre[2 * p + 1];
+    v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+    v[4] += r1v.x; v[5] += r1v.y; v[6] += r1v.z; v[7] += r1v.w;
+    if (mok) {
+      float* cp = g.x2 + m * FB_D + n;
+      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vr[8 * p + e] = v[e];
+  }
+  float s1 = 0.f;                                        // two-pass mean / variance (as ln_fwd)
+#pragma unroll
+  for (int e = 0; e < 32; ++e) s1 += vr[e];
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  const float mu = s1 * (1.f / FB_D);
+  float s2 = 0.f;
+#pragma unroll
+  for (int e = 0; e < 32; ++e) s2 += (vr[e] - mu) * (vr[e] - mu);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  const float rs = 1.f / sqrtf(s2 * (1.f / FB_D) + g.eps);
+  if (mok) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = 32 * p + 8 * lg;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (vr[8 * p + e] - mu) * rs * slw[n + e] + slb[n + e];
+      *reinterpret_cast<uint4*>(g.y + m * FB_D + n) = pack8(o);
+    }
+    if (lg == 0) {
+      g.mean[m] = mu;
+      g.rstd[m] = rs;
+    }
+  }
+  TTMI_TSTAMP(6);
+  TTMI_TSTAMP_VAL(7, twait);
+  (void)twait;
+}
+
+template <int NG>
+void launch_ffn(const FfnArgs& a, hipStream_t s) {
+  const dim3 grid((unsigned)((a.M + 127) / 128));       // 8 waves, one 16-row tile each
+  hipLaunchKernelGGL((ffn_block_kernel<8, NG>), grid, dim3(512), 0, s, a);
+}
+
+}  // namespace
+
+TTMI_STAMP_DUMP(ffn)
+
+extern "C" int ttmi_ffn_block_supported(int dtype, int D, int F) {
+  return dtype == TTMI_BF16 && D == FB_D && (F == 256 || F == 512);
+}
+
+extern "C" int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t s) {
+  static const char* fn = "ttmi_ffn_block_fwd";
+  TTMI_REQUIRE(d != nullptr, "%s: null descriptor", fn);
+  TTMI_REQUIRE(ttmi_ffn_block_supported(TTMI_BF16, d->D, d->F),
+               "%s: serves D = 128 with F in {256, 512} (got D=%d F=%d); use ttmi_linear + "
+               "ttmi_linear_res_ln", fn, d->D, d->F);
+  TTMI_REQUIRE(d->M >= 0, "%s: M < 0", fn);
+  TTMI_REQUIRE((int64_t)d->M * d->F * 2 + 16 * d->F * 2 * 8 < ((int64_t)1 << 31),
+               "%s: [M, F] bf16 must stay under 2 GB (32-bit buffer offsets; got M=%d)", fn, d->M);
+  TTMI_REQUIRE(d->a && d->w1 && d->b1 && d->w2 && d->b2 && d->res && d->h && d->x2 && d->lnw && d->lnb && d->y &&
+                   d->mean && d->rstd, "%s: null argument", fn);
+  TTMI_REQUIRE((((uintptr_t)d->a | (uintptr_t)d->w1 | (uintptr_t)d->w2 | (uintptr_t)d->res | (uintptr_t)d->h |
+                 (uintptr_t)d->x2 | (uintptr_t)d->y) & 15) == 0, "%s: row operands must be 16-byte aligned", fn);
+  TTMI_REQUIRE(d->dropf_p >= 0.f && d->dropf_p < 1.f && d->drop2_p >= 0.f && d->drop2_p < 1.f,
+               "%s: dropout out of [0,1)", fn);
+  if (d->M == 0) return TTMI_OK;
+  FfnArgs a{};
+  a.a = (const bf16_t*)d->a; a.w1 = (const bf16_t*)d->w1; a.b1 = d->b1; a.w2 = (const bf16_t*)d->w2; a.b2 = d->b2;
+  a.res = d->res; a.h = (bf16_t*)d->h; a.x2 = d->x2;
+  a.lnw = d->lnw; a.lnb = d->lnb; a.eps = d->eps; a.y = (bf16_t*)d->y; a.mean = d->mean; a.rstd = d->rstd;
+  a.df = make_drop(d->dropf_p, d->dropf_seed);
+  a.d2 = make_drop(d->drop2_p, d->drop2_seed);
+  a.M = d->M;
+  if (d->F == 512) launch_ffn<4>(a, s);
+  else launch_ffn<2>(a, s);
+  return ttmi_check_launch(fn);
+}

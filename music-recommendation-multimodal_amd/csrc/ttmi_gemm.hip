@@ -474,10 +474,10 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
       if (ln.next) {
         drop_apply_vec<8>(dk2, (uint32_t)(drow * ln.ld_drop + n), o);
         uint4 q;
-        q.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-        q.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-        q.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-        q.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+        q.x = pk_bf2(o[0], o[1]);
+        q.y = pk_bf2(o[2], o[3]);
+        q.z = pk_bf2(o[4], o[5]);
+        q.w = pk_bf2(o[6], o[7]);
         *reinterpret_cast<uint4*>(ln.next + m * ln.ld_next + n) = q;
       }
     }
@@ -741,10 +741,10 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
           *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
         } else {
           uint4 q;
-          q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-          q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          q.x = pk_bf2(v[0], v[1]);
+          q.y = pk_bf2(v[2], v[3]);
+          q.z = pk_bf2(v[4], v[5]);
+          q.w = pk_bf2(v[6], v[7]);
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.C) + m * g.ldc + n) = q;
         }
         if constexpr (LNF) {
@@ -772,10 +772,10 @@ __global__ __launch_bounds__(512 * CS) void panel_kernel(GemmArgs g, int tiles_p
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = (vr[8 * p + e] - mu) * rs * sdw[n + e] + sdb[n + e];
           uint4 q;
-          q.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-          q.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-          q.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-          q.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+          q.x = pk_bf2(o[0], o[1]);
+          q.y = pk_bf2(o[2], o[3]);
+          q.z = pk_bf2(o[4], o[5]);
+          q.w = pk_bf2(o[6], o[7]);
           *reinterpret_cast<uint4*>(ln.y + m * ln.ldy + n) = q;
         }
         if (lg == 0) {
@@ -976,10 +976,10 @@ __global__ __launch_bounds__(512) void panel256_kernel(GemmArgs g, int tiles_per
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = (vr[32 * cg + 8 * p + e] - mu) * rs * slw[n + e] + slb[n + e];
           uint4 qv;
-          qv.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-          qv.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-          qv.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-          qv.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+          qv.x = pk_bf2(o[0], o[1]);
+          qv.y = pk_bf2(o[2], o[3]);
+          qv.z = pk_bf2(o[4], o[5]);
+          qv.w = pk_bf2(o[6], o[7]);
           *reinterpret_cast<uint4*>(ln.y + m * ln.ldy + n) = qv;
         }
       }
@@ -1048,10 +1048,10 @@ __global__ __launch_bounds__(512) void panel256_kernel(GemmArgs g, int tiles_per
           if (ln.next) {
             drop_apply_vec<8>(dk2, (uint32_t)(drow * ln.ld_drop + n), o);
             uint4 qv;
-            qv.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-            qv.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-            qv.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-            qv.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+            qv.x = pk_bf2(o[0], o[1]);
+            qv.y = pk_bf2(o[2], o[3]);
+            qv.z = pk_bf2(o[4], o[5]);
+            qv.w = pk_bf2(o[6], o[7]);
             *reinterpret_cast<uint4*>(ln.next + m * ln.ld_next + n) = qv;
           }
         }

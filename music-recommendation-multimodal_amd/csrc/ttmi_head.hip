@@ -137,8 +137,8 @@ TTMI_DEV void head_gemm(const char* sA, const WFrags<NT, K>& wf, f32x4_t (&acc)[
 }
 
 TTMI_DEV void st4_bf(char* p, const float* v) {
-  *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                                            (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  *reinterpret_cast<uint2*>(p) = make_uint2(pk_bf2(v[0], v[1]),
+                                            pk_bf2(v[2], v[3]));
 }
 
 // Row sum over the 128 columns held as v[t][e] by the 4 lanes of row li in each of 4 waves.

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void cover_prep_kernel(CoverArgs a) {
   }
   if (a.out_nhwc8) {
     uint4 q;
-    q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    q.x = pk_bf2(v[0], v[1]);
     q.y = (uint32_t)f2bf(v[2]);
     q.z = 0u;
     q.w = 0u;

@@ -206,6 +206,11 @@ def _q1_proj_ok(w_in: Tensor, a1: Tensor, L: int, H: int) -> bool:
 _DYATT = os.environ.get("TTMI_NO_DYATT", "0") != "1"
 
 
+# the feed-forward sub-block in one launch (ttmi_ffn_block_fwd); TTMI_NO_FFN=1 runs the FFN1
+# row panel + ttmi_linear_res_ln pair (A/B measurements)
+_FFN = os.environ.get("TTMI_NO_FFN", "0") != "1"
+
+
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
 
@@ -353,10 +358,23 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
                        drop=_drop(cfg, seeds, site_drop1(i)), residual=res_in, drop_rows=drows)
             ops.layernorm_fwd(x1, P[pre + "norm2.weight"], P[pre + "norm2.bias"], a2, m2, r2, eps=cfg.eps)
         h = torch.empty(R, F_, device=dev, dtype=dt)
-        ops.linear(a2, W[pre + "linear1.weight"], P[pre + "linear1.bias"], h, act=1,
-                   drop=_drop(cfg, seeds, site_ffn(i)), drop_rows=drows)
         x2 = torch.empty(R, D, **f32)
         name = pre + "linear2.weight"
+        w1 = W[pre + "linear1.weight"]
+        if (not pruned and i + 1 < cfg.n_layers and _FFN and w1.dtype == torch.bfloat16
+                and W[name].dtype == torch.bfloat16 and R * F_ * 2 < (1 << 30)
+                and ops.ffn_block_supported(dt, D, F_)):
+            # FFN1 + ReLU / dropout + FFN2 + residual + the next layer's norm1, one launch
+            nxt = ln_out(M)
+            nx = _lp(i + 1)
+            ops.ffn_block_fwd(a2, w1, P[pre + "linear1.bias"], W[name], P[pre + "linear2.bias"], x1,
+                              _drop(cfg, seeds, site_ffn(i)), _drop(cfg, seeds, site_drop2(i)), h, x2,
+                              P[nx + "norm1.weight"], P[nx + "norm1.bias"], cfg.eps, *nxt)
+            st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, x1, a2, m2, r2, h, rows))
+            x = x2
+            continue
+        ops.linear(a2, w1, P[pre + "linear1.bias"], h, act=1,
+                   drop=_drop(cfg, seeds, site_ffn(i)), drop_rows=drows)
         if not pruned and i + 1 < cfg.n_layers and _resln_ok(W, name, D, R):
             # linear2 + residual + the next layer's norm1, one kernel
             nxt = ln_out(M)

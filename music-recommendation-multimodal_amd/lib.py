@@ -145,6 +145,16 @@ class AttnBlockDesc(ctypes.Structure):
                 ("x1", c_p), ("a2", c_p), ("m2", c_p), ("r2", c_p)]
 
 
+class FfnBlockDesc(ctypes.Structure):
+    """ttmi_ffn_block_desc (include/ttmi.h, ABI 21)."""
+    _fields_ = [("M", c_i), ("D", c_i), ("F", c_i),
+                ("a", c_p), ("w1", c_p), ("b1", c_p), ("w2", c_p), ("b2", c_p), ("res", c_p),
+                ("dropf_p", ctypes.c_float), ("dropf_seed", c_p),
+                ("drop2_p", ctypes.c_float), ("drop2_seed", c_p),
+                ("h", c_p), ("x2", c_p), ("lnw", c_p), ("lnb", c_p), ("eps", ctypes.c_float),
+                ("y", c_p), ("mean", c_p), ("rstd", c_p)]
+
+
 class UserHeadBwdDesc(ctypes.Structure):
     """ttmi_user_head_bwd_desc (include/ttmi.h)."""
     _fields_ = [("B", c_i), ("D", c_i), ("F", c_i), ("dg", c_i), ("dc", c_i),
@@ -239,6 +249,8 @@ SIGNATURES = {
     "ttmi_qkv_attn_supported": (c_i, [c_i, c_i, c_i, c_i]),
     "ttmi_mha_bwd_dy": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_attn_block_fwd": (c_i, [c_p, c_p]),
+    "ttmi_ffn_block_supported": (c_i, [c_i, c_i, c_i]),
+    "ttmi_ffn_block_fwd": (c_i, [c_p, c_p]),
     "ttmi_mha_q1_proj_gather_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p,
                                           c_p, c_p, c_p, c_p]),
     "ttmi_qkv_attn_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p,

@@ -825,6 +825,43 @@ def attn_block_fwd(a: Tensor, w_in: Tensor, b_in: Tensor, key_valid: Tensor, B: 
     call("ttmi_attn_block_fwd", ctypes.byref(d), _s())
 
 
+_FFN_OK: dict = {}
+
+
+def ffn_block_supported(dtype: torch.dtype, D: int, F: int) -> bool:
+    """Whether ttmi_ffn_block_fwd serves this (dtype, D, F)."""
+    if dtype not in (torch.bfloat16,):
+        return False
+    key = (code(dtype), D, F)
+    if key not in _FFN_OK:
+        _FFN_OK[key] = bool(_L.load().ttmi_ffn_block_supported(*key))
+    return _FFN_OK[key]
+
+
+def ffn_block_fwd(a: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, res: Tensor,
+                  drop_f: Drop, drop2: Drop, h: Tensor, x2: Tensor, lnw: Tensor, lnb: Tensor,
+                  eps: float, y: Tensor, mean: Tensor, rstd: Tensor) -> Tensor:
+    """The feed-forward sub-block and the next layer's norm1 in one launch (ttmi_ffn_block_fwd,
+    ABI 21): h = drop_f(relu(a·w1ᵀ + b1)), x2 = res + drop2(h·w2ᵀ + b2), y = LN(x2) — as
+    linear(act=1) + linear_res_ln, with h never read back."""
+    _dev(a, w1, b1, w2, b2, res, h, x2, lnw, lnb, y, mean, rstd)
+    M, D = a.shape
+    F = w1.shape[0]
+    for t, shp in ((a, (M, D)), (w1, (F, D)), (w2, (D, F)), (res, (M, D)), (h, (M, F)), (x2, (M, D)),
+                   (y, (M, D))):
+        if tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"ffn_block_fwd: operand of shape {tuple(t.shape)} (contiguous {shp} expected)")
+    d = _L.FfnBlockDesc()
+    d.M, d.D, d.F = M, D, F
+    d.a, d.w1, d.b1, d.w2, d.b2, d.res = _p(a), _p(w1), _p(b1), _p(w2), _p(b2), _p(res)
+    d.dropf_p, d.dropf_seed = float(drop_f[0]), _p(drop_f[1])
+    d.drop2_p, d.drop2_seed = float(drop2[0]), _p(drop2[1])
+    d.h, d.x2, d.lnw, d.lnb, d.eps = _p(h), _p(x2), _p(lnw), _p(lnb), float(eps)
+    d.y, d.mean, d.rstd = _p(y), _p(mean), _p(rstd)
+    call("ttmi_ffn_block_fwd", ctypes.byref(d), _s())
+    return x2
+
+
 def mha_bwd_dy(qkv: Tensor, key_valid: Tensor, lse: Tensor, dy: Tensor, wot: Tensor, B: int, L: int,
                H: int, dqkv: Tensor, drop: Drop = NO_DROP) -> Tensor:
     """mha_bwd with dctx = dy·W_o computed in the launch (ABI 21; wot = the W_oᵀ mirror):

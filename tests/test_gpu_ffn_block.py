@@ -1,0 +1,97 @@
+"""The fused feed-forward sub-block forward (ttmi_ffn_block_fwd, reference user_tower.py:37-45 and
+the next layer's norm1, :111-116) against the two launches it replaces — ttmi_linear(act=ReLU)
+then ttmi_linear_res_ln, themselves parity-tested against the oracle in test_gpu_kernels.py — and
+against a torch fp32 restatement.  h shares the FFN1 row panel's fragments and MFMA order (the
+kernel ttmi_linear runs from M = 2048 rows): bit-identical there.  FFN2 sums its k-steps in
+hidden-unit order, so x2 / y / mean / rstd agree to fp32 rounding (tolerances below)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _seed(val):
+    v = val - (1 << 64) if val >= (1 << 63) else val
+    return torch.tensor([v], dtype=torch.int64, device=DEV)
+
+
+def _operands(M, F, g, D=128):
+    a = torch.randn(M, D, generator=g).to(torch.bfloat16)
+    w1 = (torch.randn(F, D, generator=g) / D ** 0.5).to(torch.bfloat16)
+    b1 = torch.randn(F, generator=g) * 0.1
+    w2 = (torch.randn(D, F, generator=g) / F ** 0.5).to(torch.bfloat16)
+    b2 = torch.randn(D, generator=g) * 0.1
+    res = torch.randn(M, D, generator=g)
+    lnw = 1 + 0.1 * torch.randn(D, generator=g)
+    lnb = 0.1 * torch.randn(D, generator=g)
+    return [t.to(DEV) for t in (a, w1, b1, w2, b2, res, lnw, lnb)]
+
+
+def _run(ops, fused, M, F, ops_in, drop_f, drop2, D=128):
+    a, w1, b1, w2, b2, res, lnw, lnb = ops_in
+    h = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    x2 = torch.empty(M, D, device=DEV)
+    y = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    mu, rs = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    if fused:
+        ops.ffn_block_fwd(a, w1, b1, w2, b2, res, drop_f, drop2, h, x2, lnw, lnb, 1e-5, y, mu, rs)
+    else:
+        ops.linear(a, w1, b1, h, act=1, drop=drop_f)
+        ops.linear_res_ln(h, w2, b2, res, x2, lnw, lnb, y, mu, rs, eps=1e-5, drop=drop2)
+    torch.cuda.synchronize()
+    return h, x2, y, mu, rs
+
+
+@pytest.mark.parametrize("M,F,p", [(25600, 512, 0.1), (2053, 512, 0.0), (2048, 256, 0.1), (7, 512, 0.1),
+                                   (113, 256, 0.0), (1, 512, 0.0)])
+def test_ffn_block_matches_linear_then_res_ln(gpu_pkg, M, F, p):
+    ops = gpu_pkg.ops
+    assert ops.ffn_block_supported(torch.bfloat16, 128, F)
+    g = torch.Generator().manual_seed(17 * M + F)
+    ops_in = _operands(M, F, g)
+    drop_f = (p, _seed(0xFF1 + M)) if p > 0 else (0.0, None)
+    drop2 = (p, _seed(0xFF2 + M)) if p > 0 else (0.0, None)
+    h0, x0, y0, mu0, rs0 = _run(ops, False, M, F, ops_in, drop_f, drop2)
+    h1, x1, y1, mu1, rs1 = _run(ops, True, M, F, ops_in, drop_f, drop2)
+    if M >= 2048:
+        assert torch.equal(h1.view(torch.int16), h0.view(torch.int16))
+    else:       # ttmi_linear's small-M GEMM: another MFMA order
+        assert float((h1.float() - h0.float()).abs().max()) <= 0.02 * float(h0.float().abs().max())
+    # x2 from the fused kernel's own h, restated in fp32 (the FFN2 sum order aside: exact)
+    a, w1, b1, w2, b2, res, lnw, lnb = ops_in
+    keep2 = (x0 - res) != 0 if p > 0 else None
+    ref = h1.float() @ w2.float().t() + b2
+    if p > 0:
+        ref = torch.where(keep2 | (ref == 0), ref / (1 - p), torch.zeros_like(ref))
+    ref = ref + res
+    tol = 2e-5 * float(ref.abs().max())
+    assert float((x1 - ref).abs().max()) <= max(tol, 1e-5) * 4
+    if M >= 2048:
+        assert float((x1 - x0).abs().max()) <= max(tol, 1e-5) * 4
+    assert float((mu1 - mu0).abs().max()) <= 1e-4 and float(((rs1 - rs0) / rs0).abs().max()) <= 1e-3
+    assert float((y1.float() - y0.float()).abs().max()) <= 0.05
+
+
+def test_ffn_block_no_dropout_vs_torch(gpu_pkg):
+    """p = 0 against a torch fp32 restatement of the whole sub-block (h to bf16 rounding)."""
+    ops = gpu_pkg.ops
+    M, F = 4096, 512
+    g = torch.Generator().manual_seed(3)
+    ops_in = _operands(M, F, g)
+    a, w1, b1, w2, b2, res, lnw, lnb = ops_in
+    h, x2, y, mu, rs = _run(ops, True, M, F, ops_in, (0.0, None), (0.0, None))
+    h_ref = torch.relu(a.float() @ w1.float().t() + b1)
+    assert float((h.float() - h_ref).abs().max()) <= 2 ** -7 * float(h_ref.abs().max())
+    x_ref = res + h_ref @ w2.float().t() + b2
+    assert float((x2 - x_ref).abs().max()) <= 0.02
+    y_ref = torch.nn.functional.layer_norm(x2, (128,), lnw, lnb, 1e-5)
+    assert float((y.float() - y_ref).abs().max()) <= 0.03
+    assert float((mu - x2.mean(1)).abs().max()) <= 1e-5
+
+
+def test_ffn_block_refuses_unserved(gpu_pkg):
+    ops = gpu_pkg.ops
+    assert not ops.ffn_block_supported(torch.bfloat16, 256, 1024)
+    assert not ops.ffn_block_supported(torch.bfloat16, 128, 384)
+    assert not ops.ffn_block_supported(torch.float32, 128, 512)

@@ -59,7 +59,7 @@ profile() {
 pmc() {
   local tag=$1 cfg=$2 c
   for c in FETCH_SIZE WRITE_SIZE; do
-    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/pmc_${tag}_$c -o run \
+    (cd /tmp && timeout -s KILL 60 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/pmc_${tag}_$c -o run \
       -- python3 $R/bench.py --config $cfg --steps 5 --warmup 2 --skip-cpu) > gpurun_out/pmc_${tag}_$c.log 2>&1 \
       || { tail -20 gpurun_out/pmc_${tag}_$c.log; return 1; }
   done
@@ -113,10 +113,26 @@ dis_counters() {
   local i=0 P
   for P in "$P1" "$P2"; do
     i=$((i+1))
-    (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/dis_pmc$i -o run \
+    (cd /tmp && timeout -s KILL 60 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/dis_pmc$i -o run \
       -- python3 $R/tools/attn_bench.py) > gpurun_out/dis_pmc$i.log 2>&1 || { tail -20 gpurun_out/dis_pmc$i.log; return 1; }
   done
   python3 tools/pmc_kernels.py dis_ $(ls gpurun_out/dis_pmc*/*/run_counter_collection.csv gpurun_out/dis_pmc*/run_counter_collection.csv 2>/dev/null)
+}
+
+# kcounters SCRIPT FILTER: two SQ counter passes over SCRIPT's launches, per-kernel means of the
+# kernels whose name contains FILTER
+kcounters() {
+  local script=$1 flt=$2 i=0 P
+  local P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES"
+  local P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_WAVES GRBM_GUI_ACTIVE"
+  timeout -k 10 120 python3 -u $script > gpurun_out/kc_time.log 2>&1 || { tail -20 gpurun_out/kc_time.log; return 1; }
+  cat gpurun_out/kc_time.log
+  for P in "$P1" "$P2"; do
+    i=$((i+1))
+    (cd /tmp && timeout -s KILL 60 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/kc_pmc$i -o run \
+      -- python3 $R/$script) > gpurun_out/kc_pmc$i.log 2>&1 || { tail -20 gpurun_out/kc_pmc$i.log; return 1; }
+  done
+  python3 tools/pmc_kernels.py $flt $(ls gpurun_out/kc_pmc*/*/run_counter_collection.csv gpurun_out/kc_pmc*/run_counter_collection.csv 2>/dev/null)
 }
 
 final() {
@@ -152,6 +168,7 @@ case $cmd in
   serial) serial "$@" ;;
   profile) profile "$@" ;;
   pmc) pmc "$@" ;;
+  kcounters) kcounters "$@" ;;
   bench-all) bench_all "$@" ;;
   ab) ab "$@" ;;
   dis-counters) dis_counters "$@" ;;

@@ -4,6 +4,7 @@ the fused user head, from the diagnostic build (tools/stamp_build.sh).  GPU diag
 Phases (panel_kernel): 0 start, 1 W DMA issued, 2 W in LDS (after the barrier), 3 first
 tile's first column group MFMAs done, 4 first tile done, 5 all tiles done, 6 end.
 Phases (qkv_attn_fwd): 0 start, 1 W group 0 in LDS, 2 projection done, 3 attention done.
+Phases (ffn_block_fwd): 0 start, 1 group 0 in LDS, 2-5 hidden groups 0-3 done, 6 end.
 Phases (user_head_fwd, the FFN-split kernel): 0 start, 1 prologue, 2 out-proj + LN2, 3 FFN1
 slice, 4 FFN2 partial, 5 handoff done (the last arriver), 6 x2, 7 end."""
 import ctypes
@@ -20,7 +21,7 @@ pkg.lib.load(os.environ["TTMI_LIB"])
 ops = pkg.ops
 NB, NW, NP = 512, 16, 8
 lib = pkg.lib._lib
-for tu in ("gemm", "head", "infonce", "attn"):
+for tu in ("gemm", "head", "infonce", "attn", "ffn"):
     getattr(lib, "ttmi_dbg_stamps_" + tu).argtypes = [ctypes.c_void_p, ctypes.c_int64]
 buf = (ctypes.c_uint64 * (NB * NW * NP))()
 
@@ -78,6 +79,23 @@ def main():
     lseq = torch.empty(512 * 4 * 50, device=dev)
     stamps(lambda: ops.qkv_attn_fwd(a1, w_in, b_in, kvm, 512, 50, 4, qkv, ctxq, lseq, drop),
            "qkv + attention fwd", nph=4, tu="attn")
+    # the fused feed-forward sub-block (phases: 0 start, 1 group 0 in LDS, 2-5 groups 0-3 done
+    # (after the next group's wait), 6 end)
+    w1f, b1f, w2f, b2f = bf(512, D), f32(512, sc=0.1), bf(D, 512), f32(D, sc=0.1)
+    x1f, hf, x2f = f32(M, D), torch.empty(M, 512, device=dev, dtype=torch.bfloat16), torch.empty(M, D, device=dev)
+    yf, muf, rsf = torch.empty(M, D, device=dev, dtype=torch.bfloat16), torch.empty(M, device=dev), torch.empty(M, device=dev)
+    lnwf, lnbf = f32(D), f32(D)
+    stamps(lambda: ops.ffn_block_fwd(a1, w1f, b1f, w2f, b2f, x1f, drop, drop, hf, x2f, lnwf, lnbf, 1e-5, yf, muf, rsf),
+           "ffn block fwd", nph=7, tu="ffn")
+    w = np.array(buf, dtype=np.float64).reshape(NB, NW, NP)[:, :8, 7]
+    w = w[w > 0] / 100.0
+    if w.size:
+        print(f"    group-seam wait per wave (us): median {np.median(w):.2f}  max {w.max():.2f}")
+    nod = (0.0, None)
+    stamps(lambda: ops.ffn_block_fwd(a1, w1f, b1f, w2f, b2f, x1f, nod, nod, hf, x2f, lnwf, lnbf, 1e-5, yf, muf, rsf),
+           "ffn block fwd, no dropout", nph=7, tu="ffn")
+    if os.environ.get("STAMP_FFN_ONLY"):
+        return
     wo, bo = bf(D, D), f32(D, sc=0.1)
     x, x1 = f32(M, D), torch.empty(M, D, device=dev)
     lnw, lnb = 1 + f32(D, sc=0.1), f32(D, sc=0.1)
