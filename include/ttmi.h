@@ -280,6 +280,29 @@ typedef struct ttmi_ffn_block_desc {
 } ttmi_ffn_block_desc;
 int ttmi_ffn_block_supported(int dtype, int D, int F);
 int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t stream);
+/* Its input-grad half (ABI 21): on the transposed weight mirrors w2t = linear2.weightᵀ [F, D],
+ * w1t = linear1.weightᵀ [D, F] (bf16, k-major),
+ *   dz1 = (dy2·w2ᵀᵀ) ⊙ [h > 0]·gate_scale   bf16 [M, F] (ttmi_linear with gate = h: its bits)
+ *   dY  = dz1·w1 (not stored); norm2's backward as ttmi_linear_ln_bwd: dx1 = LN2ᵀ(dY) + res
+ *   (fp32), dy1 = bf16(drop1ᵀ(dx1)) (index m·D + n), and per workgroup Σ_rows dY·x̂ (norm2.weight)
+ *   and Σ_rows dY (norm2.bias) -> sum_ws[blk][2][D], blk < ttmi_ffn_block_bwd_sum_blocks(M):
+ *   the caller folds them in workgroup order (ttmi_fold_desc: S = blocks, s_stride = 2·D).
+ * dY sums in hidden-unit order: dx1 / dy1 / the sums agree with the row panels to fp32 rounding.
+ * Shapes as ttmi_ffn_block_fwd. */
+typedef struct ttmi_ffn_block_bwd_desc {
+  int M, D, F;
+  const void* dy2;                                 /* [M, D] bf16: FFN output grad (drop2ᵀ applied) */
+  const void* w2t; const void* w1t;
+  const void* h; float gate_scale;                 /* [M, F] bf16: the forward's h; 1 / (1 - p_ffn) */
+  void* dz1;                                       /* [M, F] bf16 out */
+  const float* x1; const float* m2; const float* r2; const float* n2w;   /* norm2's input, stats, weight */
+  const float* res;                                /* [M, D] fp32: added to dx1 */
+  float* dx1; void* dy1;
+  float drop1_p; const uint64_t* drop1_seed;
+  float* sum_ws;
+} ttmi_ffn_block_bwd_desc;
+int ttmi_ffn_block_bwd_sum_blocks(int M);
+int ttmi_ffn_block_bwd(const ttmi_ffn_block_bwd_desc* d, hipStream_t stream);
 /* ttmi_mha_bwd with dctx computed in the launch from the out-projection's output gradient
  * (ABI 21): dctx = dy·W_o (dy [B*L, 128] bf16; wot = W_oᵀ, the transposed k-major mirror,
  * [128, 128] bf16), rounded to bf16 with ttmi_linear's fragment and MFMA order, so dqkv is

@@ -267,6 +267,252 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   (void)twait;
 }
 
+// ------------------------------------------------------------------------------ backward
+// The sub-block's input-grad half (ABI 21, ttmi_ffn_block_bwd): the same two back-to-back GEMMs
+// on the transposed weight mirrors — W2ᵀ [F, D] has the forward W1's layout, W1ᵀ [D, F] the
+// forward W2's — with the row panels' epilogues:
+//   dz1 = (dy2·W2) ⊙ [h > 0]·sf                  bf16 [M, F] (stored: dW1's operand; the gated
+//                                                 row panel's bits)
+//   dY  = dz1·W1 (never stored), then norm2's backward (ttmi_linear_ln_bwd's epilogue):
+//   dx1 = rstd·(dY·w − mean(dY·w) − x̂·mean(dY·w·x̂)) + res,  dy1 = bf16(drop1ᵀ(dx1)),
+//   Σ_rows dY·x̂ and Σ_rows dY per workgroup -> sum_ws[blk][2][D] (folded in workgroup order).
+// dY sums its k-steps in hidden-unit order: dx1 / dy1 / the sums agree with the row panels to
+// fp32 rounding.  The gate rows are compiler-counted loads, so the group seams wait with a full
+// vmcnt(0) the compiler sees: each gate load is issued right after one seam and read after the
+// next (a wait for it inside a group would also wait for the DMAs behind it).
+struct FfnBwdArgs {
+  const bf16_t* dy; const bf16_t* w2t; const bf16_t* w1t; const bf16_t* h; float sf;
+  bf16_t* dz1;
+  const float* x1; const float* m2; const float* r2; const float* lnw; const float* res;
+  float* dx1; bf16_t* dy1; DropParams d1; float* sum_ws;
+  int M;
+};
+
+template <int CTRL>
+TTMI_DEV float fb_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+TTMI_DEV float fb_row16_sum(float v) {     // the 16 lanes of a DPP row, every lane gets the sum
+  v += fb_dpp<0xB1>(v);                    // quad_perm [1,0,3,2]
+  v += fb_dpp<0x4E>(v);                    // quad_perm [2,3,0,1]
+  v += fb_dpp<0x141>(v);                   // row_half_mirror
+  v += fb_dpp<0x140>(v);                   // row_mirror
+  return v;
+}
+
+template <int NG>
+__global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
+  constexpr int NWV = 8, F = NG * 128;
+  constexpr int PW = (FB_INS + NWV - 1) / NWV;
+  __shared__ __attribute__((aligned(16))) char smem[2 * FB_BUF + 2 * 1024];   // + LN weight | seed
+  __shared__ float sdw[NWV][FB_D], sdb[NWV][FB_D];
+  char* const spar = smem + 2 * FB_BUF;
+  TTMI_TSTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int64_t r0 = (int64_t)blockIdx.x * (16 * NWV);
+  const int64_t m = r0 + 16 * wave + li;
+  const bool mok = m < g.M;
+  const int64_t mc = mok ? m : (int64_t)g.M - 1;
+  const uint32_t wbytes = (uint32_t)F * FB_D * 2;
+  const uint32_t abytes = (uint32_t)min<int64_t>(16 * NWV, g.M - r0) * FB_D * 2;
+  const i32x4_t r1 = make_rsrc(g.w2t, wbytes), r2 = make_rsrc(g.w1t, wbytes);
+  const i32x4_t ra = make_rsrc(g.dy + r0 * FB_D, abytes);
+  uint32_t oA[PW], oW1[PW], oW2[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    int ii = wv + NWV * j;
+    if (ii >= FB_INS) ii -= FB_INS;
+    const int q = ii * 64 + lane, n = q / FB_CPR, c = q % FB_CPR;
+    const bool pad = c == FB_CPR - 1;
+    oA[j] = pad ? (uint32_t)(16 * NWV * FB_D * 2) : (uint32_t)((n * FB_D + 8 * c) * 2);
+    oW1[j] = pad ? wbytes : (uint32_t)((n * FB_D + 8 * c) * 2);
+    oW2[j] = pad ? wbytes : (uint32_t)((n * F + 8 * c) * 2);
+  }
+  auto slot = [&](int j) { int ii = wv + NWV * j; return ii >= FB_INS ? ii - FB_INS : ii; };
+  auto issue_group = [&](int grp) {      // W2ᵀ rows [128 grp, +128), W1ᵀ columns [128 grp, +128)
+    const uint32_t b1 = lds_addr(smem + (grp & 1) * FB_BUF), b2 = b1 + FB_IMG;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) dma16(r1, oW1[j] + (uint32_t)(grp * 128 * FB_D * 2), b1 + slot(j) * 1024);
+#pragma unroll
+    for (int j = 0; j < PW; ++j) dma16(r2, oW2[j] + (uint32_t)(grp * 128 * 2), b2 + slot(j) * 1024);
+  };
+  auto load_gate = [&](int grp, uint4 (&q)[4]) {          // h[m, 128 grp + 32p + 8lg ..]
+    const uint4* hp = reinterpret_cast<const uint4*>(g.h + mc * F + 128 * grp + 8 * lg);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) q[p] = hp[4 * p];
+  };
+  {
+    const uint32_t dst = lds_addr(spar) + (uint32_t)(wv * 1024), off = (uint32_t)(lane * 16);
+    if (wv == 0) dma16(make_rsrc(g.lnw, FB_D * 4), off, dst);
+    else if (wv == 1) dma16(make_rsrc(g.d1.seed, g.d1.on ? 8 : 0), off, dst);
+  }
+  {                                                      // the dy2 tile -> buffer 1's W2ᵀ image
+    const uint32_t base = lds_addr(smem + FB_BUF + FB_IMG);
+#pragma unroll
+    for (int j = 0; j < PW; ++j) dma16(ra, oA[j], base + slot(j) * 1024);
+  }
+  issue_group(0);
+  uint4 hg[4], hn[4];
+  load_gate(0, hg);
+  for (int i = tid; i < NWV * FB_D; i += 64 * NWV) { (&sdw[0][0])[i] = 0.f; (&sdb[0][0])[i] = 0.f; }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  uint4 af[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) af[c] = lds16(smem + FB_BUF + FB_IMG + (16 * wave + li) * FB_P + 64 * lg + 16 * c);
+  const float* slw = reinterpret_cast<const float*>(spar);
+  DropKeys dk1;
+  {
+    const uint64_t s1 = *reinterpret_cast<const uint64_t*>(spar + 1024);
+    dk1 = DropKeys{(uint32_t)s1, (uint32_t)(s1 >> 32), g.d1.thresh, g.d1.scale, g.d1.on};
+  }
+  __syncthreads();                                       // every wave has its dy2 fragments
+  TTMI_TSTAMP(1);
+  float4 rx[8], rr[8];
+  float mu = 0.f, rs = 0.f;
+  auto load_rows = [&]() {                               // the LayerNorm backward's row operands
+    const float* xp = g.x1 + mc * FB_D + 8 * lg;
+    const float* rp = g.res + mc * FB_D + 8 * lg;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      rx[2 * p] = *reinterpret_cast<const float4*>(xp + 32 * p);
+      rx[2 * p + 1] = *reinterpret_cast<const float4*>(xp + 32 * p + 4);
+      rr[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
+      rr[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
+    }
+    mu = g.m2[mc];
+    rs = g.r2[mc];
+  };
+  if (NG > 1) {
+    issue_group(1);
+    load_gate(1, hn);
+  }
+  if (NG == 1) load_rows();
+  const int wrow = 8 * (li >> 2) + (li & 3);
+  f32x4_t acc2[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc2[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int grp = 0; grp < NG; ++grp) {
+    const char* w1b = smem + (grp & 1) * FB_BUF + wrow * FB_P + 64 * lg;
+    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 16 * lg;
+    f32x4_t acc1[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc1[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        Mma<bf16_t>::run(acc1[t], lds16(w1b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * c), af[c]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- dz1 = gate(acc): the row panel's PE_GATE_BF16 epilogue (+ 0 as its absent bias)
+    uint4 hq[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = 128 * grp + 32 * p + 8 * lg;
+      const uint32_t qw[4] = {hg[p].x, hg[p].y, hg[p].z, hg[p].w};
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = 1.f * (e < 2 ? acc1[2 * p][2 * e] : acc1[2 * p + 1][2 * e - 4]) + 0.f;
+        v[2 * e + 1] = 1.f * (e < 2 ? acc1[2 * p][2 * e + 1] : acc1[2 * p + 1][2 * e - 3]) + 0.f;
+        v[2 * e] = __uint_as_float(qw[e] << 16) > 0.f ? v[2 * e] * g.sf : 0.f;
+        v[2 * e + 1] = __uint_as_float(qw[e] & 0xFFFF0000u) > 0.f ? v[2 * e + 1] * g.sf : 0.f;
+      }
+      hq[p] = pack8(v);
+      if (mok) *reinterpret_cast<uint4*>(g.dz1 + m * F + n) = hq[p];
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 64 * p), hq[p]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (grp + 1 < NG) {
+      __syncthreads();                                   // every wave is done with this buffer
+      __builtin_amdgcn_s_waitcnt(0);                     // group grp + 1's images and gate rows
+#pragma unroll
+      for (int p = 0; p < 4; ++p) hg[p] = hn[p];
+      if (grp + 2 < NG) {
+        issue_group(grp + 2);
+        load_gate(grp + 2, hn);
+      } else {
+        load_rows();
+      }
+      __syncthreads();                                   // every wave's part of the images landed
+    }
+    TTMI_TSTAMP(2 + (grp < 4 ? grp : 3));
+  }
+  // ---- norm2's backward of the finished rows (ttmi_linear_ln_bwd's PE_LNBWD epilogue)
+  float dy[32], xh[32];
+  float s1 = 0.f, s2 = 0.f;
+  if (!mok) { mu = 0.f; rs = 0.f; }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int n = 32 * p + 8 * lg;
+    const float4 x0 = rx[2 * p], x1v = rx[2 * p + 1];
+    const float xr[8] = {x0.x, x0.y, x0.z, x0.w, x1v.x, x1v.y, x1v.z, x1v.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = mok ? (e < 4 ? acc2[2 * p][e] : acc2[2 * p + 1][e - 4]) : 0.f;
+      const float hx = ((mok ? xr[e] : 0.f) - mu) * rs;
+      const float gg = d * slw[n + e];
+      dy[8 * p + e] = d;
+      xh[8 * p + e] = hx;
+      s1 += gg;
+      s2 += gg * hx;
+    }
+  }
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  const float c1 = s1 * (1.f / FB_D), c2 = s2 * (1.f / FB_D);
+  if (mok) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = 32 * p + 8 * lg;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rs * (dy[8 * p + e] * slw[n + e] - c1 - xh[8 * p + e] * c2);
+      const float4 q0 = rr[2 * p], q1 = rr[2 * p + 1];
+      o[0] += q0.x; o[1] += q0.y; o[2] += q0.z; o[3] += q0.w;
+      o[4] += q1.x; o[5] += q1.y; o[6] += q1.z; o[7] += q1.w;
+      float* dp = g.dx1 + m * FB_D + n;
+      *reinterpret_cast<float4*>(dp) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(dp + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      drop_apply_vec<8>(dk1, (uint32_t)(m * FB_D + n), o);
+      *reinterpret_cast<uint4*>(g.dy1 + m * FB_D + n) = pack8(o);
+    }
+  }
+  // LayerNorm weight / bias grads: the tile's 16 rows (one DPP row) -> this wave's LDS row
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float a = fb_row16_sum(dy[8 * p + e] * xh[8 * p + e]);
+      const float b = fb_row16_sum(dy[8 * p + e]);
+      if (li == 0) {
+        sdw[wave][32 * p + 8 * lg + e] = a;
+        sdb[wave][32 * p + 8 * lg + e] = b;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < FB_D) {                                      // the waves' rows in wave order
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) { a += sdw[w][tid]; b += sdb[w][tid]; }
+    float* o = g.sum_ws + (int64_t)blockIdx.x * 2 * FB_D;
+    o[tid] = a;
+    o[FB_D + tid] = b;
+  }
+  TTMI_TSTAMP(6);
+}
+
 template <int NG>
 void launch_ffn(const FfnArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)((a.M + 127) / 128));       // 8 waves, one 16-row tile each
@@ -306,5 +552,35 @@ extern "C" int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t s) {
   a.M = d->M;
   if (d->F == 512) launch_ffn<4>(a, s);
   else launch_ffn<2>(a, s);
+  return ttmi_check_launch(fn);
+}
+
+extern "C" int ttmi_ffn_block_bwd_sum_blocks(int M) { return M > 0 ? (M + 127) / 128 : 0; }
+
+extern "C" int ttmi_ffn_block_bwd(const ttmi_ffn_block_bwd_desc* d, hipStream_t s) {
+  static const char* fn = "ttmi_ffn_block_bwd";
+  TTMI_REQUIRE(d != nullptr, "%s: null descriptor", fn);
+  TTMI_REQUIRE(ttmi_ffn_block_supported(TTMI_BF16, d->D, d->F),
+               "%s: serves D = 128 with F in {256, 512} (got D=%d F=%d); use ttmi_linear + "
+               "ttmi_linear_ln_bwd", fn, d->D, d->F);
+  TTMI_REQUIRE(d->M >= 0, "%s: M < 0", fn);
+  TTMI_REQUIRE((int64_t)d->M * d->F * 2 + 16 * d->F * 2 * 8 < ((int64_t)1 << 31),
+               "%s: [M, F] bf16 must stay under 2 GB (got M=%d)", fn, d->M);
+  TTMI_REQUIRE(d->dy2 && d->w2t && d->w1t && d->h && d->dz1 && d->x1 && d->m2 && d->r2 && d->n2w && d->res &&
+                   d->dx1 && d->dy1 && d->sum_ws, "%s: null argument", fn);
+  TTMI_REQUIRE((((uintptr_t)d->dy2 | (uintptr_t)d->w2t | (uintptr_t)d->w1t | (uintptr_t)d->h | (uintptr_t)d->dz1 |
+                 (uintptr_t)d->x1 | (uintptr_t)d->res | (uintptr_t)d->dx1 | (uintptr_t)d->dy1) & 15) == 0,
+               "%s: row operands must be 16-byte aligned", fn);
+  TTMI_REQUIRE(d->drop1_p >= 0.f && d->drop1_p < 1.f, "%s: dropout out of [0,1)", fn);
+  if (d->M == 0) return TTMI_OK;
+  FfnBwdArgs a{};
+  a.dy = (const bf16_t*)d->dy2; a.w2t = (const bf16_t*)d->w2t; a.w1t = (const bf16_t*)d->w1t;
+  a.h = (const bf16_t*)d->h; a.sf = d->gate_scale; a.dz1 = (bf16_t*)d->dz1;
+  a.x1 = d->x1; a.m2 = d->m2; a.r2 = d->r2; a.lnw = d->n2w; a.res = d->res;
+  a.dx1 = d->dx1; a.dy1 = (bf16_t*)d->dy1; a.d1 = make_drop(d->drop1_p, d->drop1_seed); a.sum_ws = d->sum_ws;
+  a.M = d->M;
+  const dim3 grid((unsigned)((d->M + 127) / 128));
+  if (d->F == 512) hipLaunchKernelGGL(ffn_block_bwd_kernel<4>, grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(ffn_block_bwd_kernel<2>, grid, dim3(512), 0, s, a);
   return ttmi_check_launch(fn);
 }

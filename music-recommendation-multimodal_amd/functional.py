@@ -582,6 +582,25 @@ def _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre, R, drows, 
         ops.dropout_bwd(dx, dy2, None, _drop(cfg, seeds, site_drop2(i)), drop_rows=drows)
     ops.linear_dw(dy2, s.h, grads[pre + "linear2.weight"], grads[pre + "linear2.bias"])
     dz1 = torch.empty(R, F_, device=dev, dtype=dt)
+    w2t = W.get(transposed_name(pre + "linear2.weight"))
+    w1t = W.get(transposed_name(pre + "linear1.weight"))
+    if (fuse and drows is None and _FFN and dt == torch.bfloat16 and w2t is not None and w1t is not None
+            and w2t.dtype == torch.bfloat16 and w1t.dtype == torch.bfloat16 and R * F_ * 2 < (1 << 30)
+            and ops.ffn_block_supported(dt, D, F_)):
+        # FFN2 input grad + ReLU / dropout gate + FFN1 input grad + norm2 backward, one launch
+        dx1 = torch.empty(R, D, **f32)
+        dy1 = torch.empty(R, D, device=dev, dtype=dt)
+        ops.ffn_block_bwd(dy2, w2t, w1t, s.h, _scale(p), dz1, s.x1, s.m2, s.r2, P[pre + "norm2.weight"], dx,
+                          dx1, dy1, _drop(cfg, seeds, site_drop1(i)), grads[pre + "norm2.weight"],
+                          grads[pre + "norm2.bias"])
+        ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"], grads[pre + "linear1.bias"])
+        ops.linear_dw(dy1, s.ctx, grads[pre + "self_attn.out_proj.weight"],
+                      grads[pre + "self_attn.out_proj.bias"])
+        if not want_dctx:
+            return dx1, dy1, None
+        dctx = torch.empty(R, D, device=dev, dtype=dt)
+        _dx(dy1, W, pre + "self_attn.out_proj.weight", dctx)
+        return dx1, dctx, None
     _dx(dy2, W, pre + "linear2.weight", dz1, gate=s.h, gate_scale=_scale(p))
     ops.linear_dw(dz1, s.a2, grads[pre + "linear1.weight"], grads[pre + "linear1.bias"])
     dx1 = torch.empty(R, D, **f32)

@@ -155,6 +155,15 @@ class FfnBlockDesc(ctypes.Structure):
                 ("y", c_p), ("mean", c_p), ("rstd", c_p)]
 
 
+class FfnBlockBwdDesc(ctypes.Structure):
+    """ttmi_ffn_block_bwd_desc (include/ttmi.h, ABI 21)."""
+    _fields_ = [("M", c_i), ("D", c_i), ("F", c_i),
+                ("dy2", c_p), ("w2t", c_p), ("w1t", c_p), ("h", c_p), ("gate_scale", ctypes.c_float),
+                ("dz1", c_p), ("x1", c_p), ("m2", c_p), ("r2", c_p), ("n2w", c_p), ("res", c_p),
+                ("dx1", c_p), ("dy1", c_p), ("drop1_p", ctypes.c_float), ("drop1_seed", c_p),
+                ("sum_ws", c_p)]
+
+
 class UserHeadBwdDesc(ctypes.Structure):
     """ttmi_user_head_bwd_desc (include/ttmi.h)."""
     _fields_ = [("B", c_i), ("D", c_i), ("F", c_i), ("dg", c_i), ("dc", c_i),
@@ -251,6 +260,8 @@ SIGNATURES = {
     "ttmi_attn_block_fwd": (c_i, [c_p, c_p]),
     "ttmi_ffn_block_supported": (c_i, [c_i, c_i, c_i]),
     "ttmi_ffn_block_fwd": (c_i, [c_p, c_p]),
+    "ttmi_ffn_block_bwd_sum_blocks": (c_i, [c_i]),
+    "ttmi_ffn_block_bwd": (c_i, [c_p, c_p]),
     "ttmi_mha_q1_proj_gather_fwd": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p,
                                           c_p, c_p, c_p, c_p]),
     "ttmi_qkv_attn_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p,

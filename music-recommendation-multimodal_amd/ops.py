@@ -862,6 +862,42 @@ def ffn_block_fwd(a: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, res
     return x2
 
 
+def ffn_block_bwd(dy2: Tensor, w2t: Tensor, w1t: Tensor, h: Tensor, gate_scale: float, dz1: Tensor,
+                  x1: Tensor, m2: Tensor, r2: Tensor, n2w: Tensor, res: Tensor, dx1: Tensor, dy1: Tensor,
+                  drop1: Drop, n2w_grad: Optional[Tensor], n2b_grad: Optional[Tensor]) -> Tensor:
+    """The feed-forward sub-block's input-grad half in one launch (ttmi_ffn_block_bwd, ABI 21):
+    dz1 = (dy2·W2) ⊙ [h > 0]·gate_scale (linear(dy2, w2t, gate=h)'s bits), then
+    linear_ln_bwd(dz1, w1t, ...)'s dx1 / dy1 / norm2 grads (sums folded in workgroup order, with
+    the step's weight gradients inside deferred_wgrad)."""
+    _dev(dy2, w2t, w1t, h, dz1, x1, m2, r2, n2w, res, dx1, dy1)
+    M, D = dy2.shape
+    F = w2t.shape[0]
+    for t, shp in ((dy2, (M, D)), (w2t, (F, D)), (w1t, (D, F)), (h, (M, F)), (dz1, (M, F)), (x1, (M, D)),
+                   (res, (M, D)), (dx1, (M, D)), (dy1, (M, D))):
+        if tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"ffn_block_bwd: operand of shape {tuple(t.shape)} (contiguous {shp} expected)")
+    _L.load()
+    G = int(_L._lib.ttmi_ffn_block_bwd_sum_blocks(M))
+    ws = torch.empty(max(G, 1) * 2 * D, device=dy2.device, dtype=torch.float32)
+    d = _L.FfnBlockBwdDesc()
+    d.M, d.D, d.F = M, D, F
+    d.dy2, d.w2t, d.w1t, d.h, d.gate_scale = _p(dy2), _p(w2t), _p(w1t), _p(h), float(gate_scale)
+    d.dz1, d.x1, d.m2, d.r2, d.n2w, d.res = _p(dz1), _p(x1), _p(m2), _p(r2), _p(n2w), _p(res)
+    d.dx1, d.dy1 = _p(dx1), _p(dy1)
+    d.drop1_p, d.drop1_seed = float(drop1[0]), _p(drop1[1])
+    d.sum_ws = _p(ws)
+    folds = []
+    for j, gr in enumerate((n2w_grad, n2b_grad)):
+        if gr is not None and G > 0:
+            f = FoldDesc()
+            f.part, f.S, f.s_stride, f.M, f.N = ws.data_ptr() + 4 * D * j, G, 2 * D, 1, D
+            f.C, f.ldc, f.accumulate, f.fx_shift = _p(gr), D, 1, 0
+            folds.append((f, ws, gr))
+    call("ttmi_ffn_block_bwd", ctypes.byref(d), _s())
+    _run_folds(folds)
+    return dx1
+
+
 def mha_bwd_dy(qkv: Tensor, key_valid: Tensor, lse: Tensor, dy: Tensor, wot: Tensor, B: int, L: int,
                H: int, dqkv: Tensor, drop: Drop = NO_DROP) -> Tensor:
     """mha_bwd with dctx = dy·W_o computed in the launch (ABI 21; wot = the W_oᵀ mirror):

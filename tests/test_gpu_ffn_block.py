@@ -95,3 +95,55 @@ def test_ffn_block_refuses_unserved(gpu_pkg):
     assert not ops.ffn_block_supported(torch.bfloat16, 256, 1024)
     assert not ops.ffn_block_supported(torch.bfloat16, 128, 384)
     assert not ops.ffn_block_supported(torch.float32, 128, 512)
+
+
+@pytest.mark.parametrize("M,F,p", [(25600, 512, 0.1), (2053, 512, 0.0), (2048, 256, 0.1), (7, 512, 0.1),
+                                   (129, 256, 0.0)])
+def test_ffn_block_bwd_matches_gated_linear_then_ln_bwd(gpu_pkg, M, F, p):
+    """ttmi_ffn_block_bwd against ttmi_linear(gate = h) + ttmi_linear_ln_bwd (both row panels from
+    M = 2048): dz1 bit-identical there; dx1 / dy1 / norm2's weight and bias grads to the fp32
+    rounding of FFN1's input-grad sum order (it sums hidden-unit order)."""
+    ops = gpu_pkg.ops
+    D = 128
+    g = torch.Generator().manual_seed(31 * M + F)
+    dy2 = (torch.randn(M, D, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    w2t = (torch.randn(F, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    w1t = (torch.randn(D, F, generator=g) / F ** 0.5).to(torch.bfloat16).to(DEV)
+    hv = torch.randn(M, F, generator=g)
+    hv[hv < 0.3] = 0.0                                  # the ReLU / dropout zeros
+    h = hv.to(torch.bfloat16).to(DEV)
+    x1 = torch.randn(M, D, generator=g).to(DEV)
+    m2, r2 = x1.mean(1), torch.rsqrt(x1.var(1, unbiased=False) + 1e-5)
+    n2w = (1 + 0.1 * torch.randn(D, generator=g)).to(DEV)
+    res = torch.randn(M, D, generator=g).to(DEV)
+    sf = 1.0 / (1.0 - p) if p > 0 else 1.0
+    drop1 = (p, _seed(0xD1 + M)) if p > 0 else (0.0, None)
+    outs = []
+    for fused in (False, True):
+        dz1 = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+        dx1 = torch.empty(M, D, device=DEV)
+        dy1 = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+        gw, gb = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+        if fused:
+            ops.ffn_block_bwd(dy2, w2t, w1t, h, sf, dz1, x1, m2, r2, n2w, res, dx1, dy1, drop1, gw, gb)
+        else:
+            ops.linear(dy2, w2t, None, dz1, gate=h, gate_scale=sf)
+            ops.linear_ln_bwd(dz1, w1t, x1, m2, r2, n2w, dx1, gw, gb, res=res, next_=dy1, drop=drop1)
+        torch.cuda.synchronize()
+        outs.append((dz1, dx1, dy1, gw, gb))
+    (z0, x0, y0, w0, b0), (z1, x1_, y1, w1_, b1_) = outs
+    if M >= 2048 and F == 512:      # the N = 512 row panel (ttmi_linear serves N = 256 otherwise)
+        assert torch.equal(z1.view(torch.int16), z0.view(torch.int16))
+    else:
+        assert float((z1.float() - z0.float()).abs().max()) <= 0.02 * float(z0.float().abs().max())
+    # dx1 against a torch fp32 restatement from the fused kernel's own dz1
+    dY = z1.float() @ w1t.float().t()
+    xh = (x1 - m2[:, None]) * r2[:, None]
+    gg = dY * n2w
+    ref = r2[:, None] * (gg - gg.mean(1, keepdim=True) - xh * (gg * xh).mean(1, keepdim=True)) + res
+    assert float((x1_ - ref).abs().max()) <= 2e-4 * float(ref.abs().max())
+    assert float((x1_ - x0).abs().max()) <= 5e-3 * float(x0.abs().max())
+    assert float((y1.float() - y0.float()).abs().max()) <= 0.02 * float(y0.float().abs().max()) + 1e-3
+    assert torch.allclose(w1_, (dY * xh).sum(0), rtol=1e-3, atol=1e-3 * float(w1_.abs().max()))
+    assert torch.allclose(b1_, dY.sum(0), rtol=1e-3, atol=1e-3 * float(b1_.abs().max()))
+    assert torch.allclose(w1_, w0, rtol=1e-2, atol=1e-2 * float(w0.abs().max()))
