@@ -234,7 +234,7 @@ int ttmi_seq_embed_bwd(int B, int L, int D, int64_t V, const int64_t* ids, const
  * in one LDS image (MFMA), 64 < L <= TTMI_ATTN_LMAX (ABI 17) the tiled long-sequence kernels
  * (online softmax over 64-key blocks).  The one-query ttmi_mha_q1_* calls take the same range.
  * ---------------------------------------------------------------------------------- */
-#define TTMI_ATTN_LMAX 512
+#define TTMI_ATTN_LMAX 2048
 int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                  const int64_t* key_valid, float drop_p, const uint64_t* drop_seed, void* ctx,
                  float* lse, hipStream_t stream);

@@ -413,7 +413,7 @@ def conv_out_hw(H: int, W: int, k: int, stride: int, pad: int):
 
 
 CONV_STAT_REPS = 16    # TTMI_CONV_STAT_REPS: BatchNorm column stats are [16][C] int64 replica rows
-ATTN_LMAX = 512        # TTMI_ATTN_LMAX: longest sequence the attention kernels take
+ATTN_LMAX = 2048       # TTMI_ATTN_LMAX: longest sequence the attention kernels take
 
 
 def conv2d(mode: int, N: int, H: int, W: int, C: int, Cin: int, Co: int, k: int, stride: int,

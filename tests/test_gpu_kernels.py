@@ -351,7 +351,7 @@ def masks(B, L, g):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (3, 1, 4, 16),
                                       (4, 65, 2, 32), (3, 200, 4, 32), (2, 130, 2, 64), (2, 512, 1, 8),
-                                      (3, 128, 4, 32), (3, 512, 4, 32)])
+                                      (3, 128, 4, 32), (3, 512, 4, 32), (2, 1000, 2, 32), (2, 2048, 1, 16)])
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
     ops = gpu_pkg.ops
@@ -380,7 +380,8 @@ def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (5, 150, 4, 32),
-                                      (3, 300, 2, 64), (4, 65, 4, 32), (4, 128, 4, 32), (3, 512, 4, 32)])
+                                      (3, 300, 2, 64), (4, 65, 4, 32), (4, 128, 4, 32), (3, 512, 4, 32),
+                                      (2, 1000, 2, 32), (2, 2048, 1, 16)])
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_mha_single_query_matches_full_row(gpu_pkg, dtype, B, L, H, Dh, p):
     """ttmi_mha_q1_* (pruned last layer) == the full attention restricted to each

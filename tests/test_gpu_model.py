@@ -255,6 +255,18 @@ def test_cfg2_loss_parity_full_size(gpu_pkg, dtype, tol):
     assert rel(logits, logits_ref) < (3e-2 if dtype == torch.bfloat16 else 1e-4)
 
 
+def test_long_history_matches_oracle(gpu_pkg):
+    """max_seq_len past 512 (ABI 21 raised TTMI_ATTN_LMAX to 2048; the reference takes any
+    length, user_tower.py:5-13): L = 1100 with dropout on through the tiled long-sequence and
+    one-query kernels, loss against the oracle's restatement."""
+    F = gpu_pkg.functional
+    m, batch = _cfg2(gpu_pkg, torch.float32, B=8, L=1100, V=997, p=0.1, seed=5)
+    seeds = F.site_seeds(0x10A6, 1)
+    lref, _ = _oracle_loss(m, batch, drop=ref.HashDropout(seeds), p=0.1)
+    loss, _, _, _ = m({k: v.to(DEV) for k, v in batch.items()}, seeds=F.seed_table(seeds, DEV))
+    assert abs(float(loss) - lref) < 1e-4
+
+
 @pytest.mark.parametrize("L", [20, 150])
 def test_dropout_on_matches_oracle_hash(gpu_pkg, L):
     """Dropout ON (p=0.1 at every site) — kernels' masks vs the oracle's restatement.  L = 150
