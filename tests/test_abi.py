@@ -38,8 +38,8 @@ def test_abi_version_and_error_path(pkg):
     lib = pkg.lib.load()
     assert lib.ttmi_abi_version() == pkg.lib.ABI_VERSION
     # invalid shapes are rejected before launch, with a message
-    with pytest.raises(pkg.lib.TTMIError, match="L <= 512"):
-        pkg.lib.call("ttmi_mha_fwd", 1, 2, 513, 4, 32, ctypes.c_void_p(16), ctypes.c_void_p(16),
+    with pytest.raises(pkg.lib.TTMIError, match="L <= 2048"):
+        pkg.lib.call("ttmi_mha_fwd", 1, 2, 2049, 4, 32, ctypes.c_void_p(16), ctypes.c_void_p(16),
                      0.0, None, ctypes.c_void_p(16), ctypes.c_void_p(16), None)
     with pytest.raises(pkg.lib.TTMIError, match="more than 1 value"):
         pkg.lib.call("ttmi_batchnorm_fwd", 1, 1, 8, ctypes.c_void_p(16), ctypes.c_void_p(16),
