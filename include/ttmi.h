@@ -646,6 +646,9 @@ typedef struct ttmi_linear_ln_bwd_desc {
   const int32_t* res_rows; int64_t res_L;  /* ABI 13; non-NULL: res is [M / res_L, N] and its row
                       b is added only to row res_rows[b] (b = m / res_L), other rows get none —
                       the pruned last layer's gathered residual (replaces ttmi_scatter_add_rows) */
+  const float* dy_add; int64_t ld_add;     /* ABI 21 (N = 128, needs res_rows): [M / res_L, N] fp32
+                      added to the GEMM output dY of row res_rows[b] BEFORE the LayerNorm backward
+                      — the pruned layer's query-row term dq·W_q (its dqkv keeps K / V columns only) */
 } ttmi_linear_ln_bwd_desc;
 int64_t ttmi_linear_ln_bwd_sum_blocks(int64_t M);           /* N = 128 */
 int64_t ttmi_linear_ln_bwd_sum_blocks_n(int64_t M, int64_t N);   /* ABI 19: any supported N */
@@ -744,6 +747,24 @@ int ttmi_mha_q1_proj_gather_fwd(int B, int L, int H, int Dh, void* qkv, const in
                                 int32_t* rows, float* x_rows, float drop_p, const uint64_t* drop_seed,
                                 void* ctx, float* lse, const struct ttmi_item_head_desc* it,
                                 hipStream_t stream);
+/* The pruned layer's one-query backward for the K / V-only in_proj input grad (ABI 21; bf16,
+ * H = 4, Dh = 32, L <= 64): dqkv's K / V columns as ttmi_mha_q1_bwd writes them, its Q columns
+ * left untouched, and
+ *   dq_rows[b] = bf16(dQ of row rows[b])   a_rows[b] = a_in[rows[b]]      (bf16 [B, 128])
+ *   dyq[b]     = dq_rows[b]·W_q (fp32 [B, 128]; wqt = in_projᵀ [128, 3·128], row-major, ld_wqt)
+ * so that the LN1-backward panel takes K = 256 (dy_add = dyq) and in_proj's Q-row weight
+ * gradient is a B-row GEMM (dq_rows, a_rows).  bn: ttmi_mha_q1_bnr_bwd's co-launched BatchNorm1d
+ * backward (may be NULL). */
+typedef struct ttmi_q1_kv_bwd_desc {
+  int B, L, H, Dh;
+  const void* qkv; const int64_t* key_valid; const int32_t* rows; const float* lse; const void* dctx;
+  float drop_p; const uint64_t* drop_seed;
+  void* dqkv;
+  const void* wqt; int64_t ld_wqt; const void* a_in;
+  void* dq_rows; void* a_rows; float* dyq;
+  const struct ttmi_bn_bwd_desc* bn;
+} ttmi_q1_kv_bwd_desc;
+int ttmi_mha_q1_kv_bwd(const ttmi_q1_kv_bwd_desc* d, hipStream_t stream);
 /* Backward: writes the full dqkv [B*L, 3HDh] (dQ only on the query rows, zero elsewhere;
  * dK, dV on every row). */
 int ttmi_mha_q1_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,

@@ -361,6 +361,7 @@ struct LnBwdArgs {
   const float* mean; const float* rstd; const float* w;
   const float* res; int64_t ld_res;
   const int32_t* res_rows; int64_t res_L;   // res row b feeds row res_rows[b] (b = m / res_L) only
+  const float* dy_add; int64_t ld_add;      // row b added to dY of row res_rows[b] (before the LN)
   float* dx; int64_t lddx;
   bf16_t* next; int64_t ld_next;
   DropParams drop; int64_t ld_drop; const int32_t* drop_rows;
@@ -389,6 +390,7 @@ TTMI_DEV float row16_sum(float v) {
 struct LnBwdRow {
   float4 x[8];
   float4 r[8];
+  float4 a[8];              // dy_add's row (zero unless this is the gathered row)
   float mu, rs;
 };
 
@@ -418,6 +420,18 @@ TTMI_DEV void panel_ln_bwd_load(const LnBwdArgs& ln, int64_t m, int64_t M, int l
 #pragma unroll
     for (int q = 0; q < 8; ++q) o.r[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  if (ln.dy_add) {          // (the launcher requires res_rows with it)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = 32 * p + 8 * lg;
+      o.a[2 * p] = *reinterpret_cast<const float4*>(ln.dy_add + rr * ln.ld_add + n);
+      o.a[2 * p + 1] = *reinterpret_cast<const float4*>(ln.dy_add + rr * ln.ld_add + n + 4);
+    }
+    if (!rhit) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o.a[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
 }
 
 // LayerNorm-backward epilogue of one 16-row tile (N = 128): lane (li, lg) holds row li,
@@ -438,9 +452,16 @@ TTMI_DEV void panel_ln_bwd_epilogue(const GemmArgs& g, const LnBwdArgs& ln, cons
       xr[0] = x0.x; xr[1] = x0.y; xr[2] = x0.z; xr[3] = x0.w;
       xr[4] = x1.x; xr[5] = x1.y; xr[6] = x1.z; xr[7] = x1.w;
     }
+    float ad[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ln.dy_add) {
+      const float4 a0 = pre.a[2 * p], a1 = pre.a[2 * p + 1];
+      ad[0] = a0.x; ad[1] = a0.y; ad[2] = a0.z; ad[3] = a0.w;
+      ad[4] = a1.x; ad[5] = a1.y; ad[6] = a1.z; ad[7] = a1.w;
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float d = mok ? g.alpha * (e < 4 ? acc[2 * p][e] : acc[2 * p + 1][e - 4]) : 0.f;
+      float d = mok ? g.alpha * (e < 4 ? acc[2 * p][e] : acc[2 * p + 1][e - 4]) : 0.f;
+      if (ln.dy_add && mok) d += ad[e];
       const float h = (xr[e] - mu) * rs;
       const float gg = d * sw[n + e];
       dy[8 * p + e] = d;
@@ -2670,6 +2691,8 @@ extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t 
                              && al16(d->ln_w)),
                "ttmi_linear_ln_bwd: N = 256 needs dh and wt under 4 GB and an aligned LayerNorm weight");
   TTMI_REQUIRE(!d->res_rows || (d->res && d->res_L > 0), "ttmi_linear_ln_bwd: res_rows needs res and res_L > 0");
+  TTMI_REQUIRE(!d->dy_add || (d->res_rows && NN == 128 && al16(d->dy_add) && d->ld_add % 4 == 0 && d->ld_add >= NN),
+               "ttmi_linear_ln_bwd: dy_add needs res_rows, N = 128 and 16-byte rows");
   TTMI_REQUIRE(!d->next || (al16(d->next) && d->ld_next % 8 == 0 && d->ld_next >= NN),
                "ttmi_linear_ln_bwd: next needs 16-byte rows");
   TTMI_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f && (d->drop_p == 0.f || d->drop_seed),
@@ -2684,6 +2707,7 @@ extern "C" int ttmi_linear_ln_bwd(const ttmi_linear_ln_bwd_desc* d, hipStream_t 
   ln.x = d->x; ln.ldx = d->ldx; ln.mean = d->mean; ln.rstd = d->rstd; ln.w = d->ln_w;
   ln.res = d->res; ln.ld_res = d->ld_res;
   ln.res_rows = d->res_rows; ln.res_L = d->res_L;
+  ln.dy_add = d->dy_add; ln.ld_add = d->ld_add;
   ln.dx = d->dx; ln.lddx = d->lddx;
   ln.next = static_cast<bf16_t*>(d->next); ln.ld_next = d->ld_next;
   ln.drop = make_drop(d->drop_p, d->drop_seed); ln.ld_drop = d->ld_drop ? d->ld_drop : NN;

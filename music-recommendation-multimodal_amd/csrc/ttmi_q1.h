@@ -164,9 +164,11 @@ TTMI_DEV void q1_fwd_wave(const Q1Args& a, int bh, Q1Lds& S) {
 }
 
 // Backward of one (b, h): writes the (b, h) slices of dqkv for all L rows (dQ zero except the
-// query row, dK_j = dS_j q, dV_j = Pd_j dO) and dQ_p = Σ_j dS_j k_j.
-template <typename T>
-TTMI_DEV void q1_bwd_wave(const Q1Args& a, int bh, Q1Lds& S) {
+// query row, dK_j = dS_j q, dV_j = Pd_j dO) and dQ_p = Σ_j dS_j k_j.  KV (ABI 21,
+// ttmi_mha_q1_kv_bwd): dqkv's Q columns are left alone and dQ_p goes to sdq[h·Dh + t] (the
+// workgroup's query-row gradient, for the caller's dq·W_q) instead.
+template <typename T, bool KV = false>
+TTMI_DEV void q1_bwd_wave(const Q1Args& a, int bh, Q1Lds& S, float* sdq = nullptr) {
   constexpr int E = 16 / sizeof(T);
   const int t = threadIdx.x & 63;
   const int b = bh / a.H, h = bh % a.H, L = a.L, Dh = a.Dh;
@@ -208,7 +210,7 @@ TTMI_DEV void q1_bwd_wave(const Q1Args& a, int bh, Q1Lds& S) {
     }
     for (int jj = grp; jj < L; jj += ngrp) {
       T* row = dseq + (int64_t)jj * ld + cv * E;
-      if (jj != p) q1_st16<T>(row, z);
+      if (!KV && jj != p) q1_st16<T>(row, z);
       const float c1 = S.s1[jj], c2 = S.s2[jj];
 #pragma unroll
       for (int i = 0; i < E; ++i) v[i] = c1 * qv[i];
@@ -219,7 +221,11 @@ TTMI_DEV void q1_bwd_wave(const Q1Args& a, int bh, Q1Lds& S) {
     }
   }
   const float acc = q1_rows_combine<T>(S.s1, seq + D, ld, min(p, L - 1) + 1, Dh, S.red, t);
-  if (t < Dh) stf<T>(dseq + (int64_t)p * ld, t, acc);
+  if constexpr (KV) {
+    if (t < Dh) sdq[h * Dh + t] = acc;
+  } else {
+    if (t < Dh) stf<T>(dseq + (int64_t)p * ld, t, acc);
+  }
 }
 
 // ------------------------------------------------------------ BatchNorm1d backward body

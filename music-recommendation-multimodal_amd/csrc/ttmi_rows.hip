@@ -98,6 +98,69 @@ __global__ __launch_bounds__(256) void mha_q1_bnr_bwd_kernel(Q1Args a, BnrBwdArg
   q1_bwd_wave<T>(a, bh, S.q[w]);
 }
 
+// ttmi_mha_q1_kv_bwd (ABI 21; cfg 2: bf16, H = 4, Dh = 32, so workgroup x is sequence x): the
+// one-query backward leaving dqkv's Q columns alone, then, from the four heads' dQ_p in LDS,
+//   dq_rows[b] = bf16(dQ_p)   (the gathered rows' in_proj Q-row gradient operand)
+//   a_rows[b]  = a_in[rows[b]]
+//   dyq[b][d]  = Σ_j bf16(dQ_p)[j]·W_q[j][d]   (fp32; W_q = in_proj rows [0, D), read through the
+//                transposed mirror wqt = in_projᵀ [D, 3D]: row d is contiguous over j)
+// which the LN1-backward panel adds to that row's dY (ttmi_linear_ln_bwd dy_add).
+struct Q1Kv {
+  const bf16_t* wqt; int64_t ld_wqt;
+  const bf16_t* a_in; bf16_t* dq_rows; bf16_t* a_rows; float* dyq;
+};
+TTMI_DEV void q1_kv_tail(const Q1Args& a, const Q1Kv& k, int b, const float* sdq) {
+  constexpr int D = 128;
+  const int tid = threadIdx.x;
+  __syncthreads();                                   // the four heads' dQ_p are in sdq
+  const int64_t r = a.rows[b];
+  if (tid < D / 8) {                                 // 16-byte chunks: dq_rows, a_rows
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = sdq[8 * tid + e];
+    *reinterpret_cast<uint4*>(k.dq_rows + (int64_t)b * D + 8 * tid) = pack8(v);
+    *reinterpret_cast<uint4*>(k.a_rows + (int64_t)b * D + 8 * tid) =
+        *reinterpret_cast<const uint4*>(k.a_in + r * D + 8 * tid);
+  }
+  // dyq: thread (d, half) dots the bf16-rounded dq with 64 of W_q's column d (row d of wqt)
+  const int d = tid >> 1, hf = tid & 1;
+  const uint4* wr = reinterpret_cast<const uint4*>(k.wqt + (int64_t)d * k.ld_wqt + 64 * hf);
+  uint4 wv[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) wv[c] = wr[c];
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const uint32_t wx[4] = {wv[c].x, wv[c].y, wv[c].z, wv[c].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 64 * hf + 8 * c + 2 * e;
+      const float q0 = bf2f(f2bf(sdq[j])), q1 = bf2f(f2bf(sdq[j + 1]));
+      acc = fmaf(q0, __uint_as_float(wx[e] << 16), acc);
+      acc = fmaf(q1, __uint_as_float(wx[e] & 0xFFFF0000u), acc);
+    }
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  if (hf == 0) k.dyq[(int64_t)b * D + d] = acc;
+}
+
+template <typename TB, int RPT, bool BN>
+__global__ __launch_bounds__(256) void mha_q1_kv_bwd_kernel(Q1Args a, Q1Kv k, BnrBwdArgs bn, int nbn) {
+  __shared__ union U {
+    Q1Lds q[4];
+    BnrLds<CO_BN_COLS, CO_BN_RG> b;
+  } S;
+  __shared__ float sdq[128];
+  if (BN && (int)blockIdx.x < nbn) {
+    bnr_bwd_body<TB, CO_BN_COLS, CO_BN_RG, RPT>(bn, blockIdx.x, S.b);
+    return;
+  }
+  const int x = (int)blockIdx.x - (BN ? nbn : 0);
+  const int w = threadIdx.x >> 6;
+  q1_bwd_wave<bf16_t, true>(a, x * 4 + w, S.q[w], sdq);
+  q1_kv_tail(a, k, x, sdq);
+}
+
 Q1Args q1_args(int B, int L, int H, int Dh, const void* qkv, const int64_t* kv, int32_t* rows,
                const float* x, float* x_rows, DropParams dp, void* ctx, float* lse, const void* dctx,
                void* dqkv) {
@@ -254,4 +317,49 @@ extern "C" int ttmi_mha_q1_bnr_bwd(int dtype, int B, int L, int H, int Dh, const
 #undef TTMI_Q1BN_R
 #undef TTMI_Q1BN
   return ttmi_check_launch("ttmi_mha_q1_bnr_bwd");
+}
+
+extern "C" int ttmi_mha_q1_kv_bwd(const ttmi_q1_kv_bwd_desc* d, hipStream_t s) {
+  static const char* fn = "ttmi_mha_q1_kv_bwd";
+  TTMI_REQUIRE(d != nullptr, "%s: null descriptor", fn);
+  int rc = q1_validate(fn, TTMI_BF16, d->B, d->L, d->H, d->Dh, d->qkv, d->drop_p, d->drop_seed);
+  if (rc) return rc;
+  TTMI_REQUIRE(d->H == 4 && d->Dh == 32 && d->L <= 64, "%s: serves bf16, H = 4, Dh = 32, L <= 64", fn);
+  TTMI_REQUIRE(d->qkv && d->key_valid && d->rows && d->lse && d->dctx && d->dqkv && d->wqt && d->a_in &&
+                   d->dq_rows && d->a_rows && d->dyq, "%s: null argument", fn);
+  TTMI_REQUIRE((((uintptr_t)d->dqkv | (uintptr_t)d->wqt | (uintptr_t)d->a_in | (uintptr_t)d->dq_rows |
+                 (uintptr_t)d->a_rows) & 15) == 0 && d->ld_wqt % 8 == 0 && d->ld_wqt >= 128,
+               "%s: operands must be 16-byte aligned", fn);
+  const ttmi_bn_bwd_desc* bn = d->bn;
+  const int rpt = bn ? (bn->B <= 4 * CO_BN_RG ? 4 : bn->B <= 8 * CO_BN_RG ? 8 : bn->B <= 16 * CO_BN_RG ? 16 : 0) : 0;
+  const bool co = bn && rpt && d->B > 0;
+  if (bn && !co) {
+    rc = ttmi_batchnorm_bwd(bn->dtype, bn->B, bn->C, bn->dy, bn->z, bn->w, bn->mean, bn->rstd, bn->y,
+                            bn->gate_scale, bn->gated, bn->dz, bn->dw, bn->db, bn->dz16, s);
+    if (rc) return rc;
+  }
+  if (d->B == 0) return TTMI_OK;
+  const Q1Args a = q1_args(d->B, d->L, d->H, d->Dh, d->qkv, d->key_valid, const_cast<int32_t*>(d->rows), nullptr,
+                           nullptr, make_drop(d->drop_p, d->drop_seed), nullptr, const_cast<float*>(d->lse),
+                           d->dctx, d->dqkv);
+  Q1Kv k{(const bf16_t*)d->wqt, d->ld_wqt, (const bf16_t*)d->a_in, (bf16_t*)d->dq_rows, (bf16_t*)d->a_rows, d->dyq};
+  if (!co) {
+    hipLaunchKernelGGL((mha_q1_kv_bwd_kernel<float, 4, false>), dim3(d->B), dim3(256), 0, s, a, k, BnrBwdArgs{}, 0);
+    return ttmi_check_launch(fn);
+  }
+  TTMI_REQUIRE(bn->dtype == TTMI_F32 || bn->dtype == TTMI_BF16, "%s: bad BatchNorm dtype", fn);
+  TTMI_REQUIRE(bn->B > 1 && bn->C > 0 && bn->dy && bn->z && bn->w && bn->mean && bn->rstd && bn->dz &&
+                   (!bn->gated || bn->y), "%s: bad BatchNorm descriptor", fn);
+  BnrBwdArgs b{};
+  b.B = bn->B; b.C = bn->C; b.dy = bn->dy; b.z = bn->z; b.w = bn->w; b.mean = bn->mean; b.rstd = bn->rstd;
+  b.y = bn->y; b.gate_scale = bn->gate_scale; b.gated = bn->gated; b.dz = bn->dz; b.dw = bn->dw; b.db = bn->db;
+  b.dz16 = (bf16_t*)bn->dz16;
+  const int nbn = (bn->C + CO_BN_COLS - 1) / CO_BN_COLS;
+  const dim3 grid((unsigned)d->B + (unsigned)nbn);
+#define TTMI_Q1KV(TB, R) hipLaunchKernelGGL((mha_q1_kv_bwd_kernel<TB, R, true>), grid, dim3(256), 0, s, a, k, b, nbn)
+#define TTMI_Q1KV_R(TB) do { if (rpt == 4) TTMI_Q1KV(TB, 4); else if (rpt == 8) TTMI_Q1KV(TB, 8); else TTMI_Q1KV(TB, 16); } while (0)
+  if (bn->dtype == TTMI_BF16) TTMI_Q1KV_R(bf16_t); else TTMI_Q1KV_R(float);
+#undef TTMI_Q1KV_R
+#undef TTMI_Q1KV
+  return ttmi_check_launch(fn);
 }

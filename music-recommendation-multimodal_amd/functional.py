@@ -206,6 +206,10 @@ def _q1_proj_ok(w_in: Tensor, a1: Tensor, L: int, H: int) -> bool:
 _DYATT = os.environ.get("TTMI_NO_DYATT", "0") != "1"
 
 
+# the pruned layer's K / V-only in_proj input grad (ttmi_mha_q1_kv_bwd + dy_add); TTMI_NO_KVB=1
+# restores the full-dqkv form (A/B measurements)
+_KVB = os.environ.get("TTMI_NO_KVB", "0") != "1"
+
 # the feed-forward sub-block in one launch (ttmi_ffn_block_fwd); TTMI_NO_FFN=1 runs the FFN1
 # row panel + ttmi_linear_res_ln pair (A/B measurements)
 _FFN = os.environ.get("TTMI_NO_FFN", "0") != "1"
@@ -479,7 +483,23 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
             dx1, dctx, dy2_next = _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre,
                                                   R, drows, F_, fuse, D, dt, p, want_dctx=not dy_attn)
         dqkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
-        if drows is not None:
+        wti = W.get(transposed_name(pre + "self_attn.in_proj_weight"))
+        # the pruned layer's dQ lives on its B gathered rows only: its in_proj input grad runs
+        # on the K / V columns (K = 256) with dq·W_q added to those rows' dY in the LN1 backward,
+        # and the Q rows' weight gradient is a B-row GEMM (ABI 21)
+        kv_only = (drows is not None and fuse and _KVB and dt == torch.bfloat16 and D == 128 and H == 4
+                   and L <= 64 and wti is not None and wti.dtype == torch.bfloat16)
+        if kv_only:
+            dq_g = torch.empty(B, D, device=dev, dtype=dt)
+            a_g = torch.empty(B, D, device=dev, dtype=dt)
+            dyq = torch.empty(B, D, **f32)
+            ops.mha_q1_kv_bwd(s.qkv, st.key_valid, drows, s.lse, dctx, B, L, H, dqkv,
+                              _drop(cfg, seeds, site_attn(i)), wti, s.a1, dq_g, a_g, dyq,
+                              bn=bn_co.desc if bn_co else None)
+            if bn_co is not None:
+                bn_co.finish()
+                bn_co = None
+        elif drows is not None:
             ops.mha_q1_bwd(s.qkv, st.key_valid, drows, s.lse, dctx, B, L, H, dqkv,
                            _drop(cfg, seeds, site_attn(i)), bn=bn_co.desc if bn_co else None)
             if bn_co is not None:
@@ -491,19 +511,24 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         else:
             ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
                         _drop(cfg, seeds, site_attn(i)))
-        ops.linear_dw(dqkv, s.a1, grads[pre + "self_attn.in_proj_weight"],
-                      grads[pre + "self_attn.in_proj_bias"])
+        gw_in, gb_in = grads[pre + "self_attn.in_proj_weight"], grads[pre + "self_attn.in_proj_bias"]
+        if kv_only:
+            ops.linear_dw(dqkv[:, D:], s.a1, gw_in[D:], gb_in[D:])
+            ops.linear_dw(dq_g, a_g, gw_in[:D], gb_in[:D])
+        else:
+            ops.linear_dw(dqkv, s.a1, gw_in, gb_in)
         dxn = torch.empty(M, D, **f32)
         if fuse:     # in_proj input grad + LN1 backward (+ the layer below's dropout2 backward);
             # the pruned layer's residual grad dx1 [B, D] lands on its gathered rows in-kernel
             emit = i > 0
             nxt = torch.empty(M, D, device=dev, dtype=dt) if emit else None
-            ops.linear_ln_bwd(dqkv, W[transposed_name(pre + "self_attn.in_proj_weight")], s.x,
+            ops.linear_ln_bwd(dqkv[:, D:] if kv_only else dqkv, wti[:, D:] if kv_only else wti, s.x,
                               s.m1, s.r1, P[pre + "norm1.weight"], dxn,
                               grads[pre + "norm1.weight"], grads[pre + "norm1.bias"],
                               res=dx1, res_rows=drows, res_L=L if drows is not None else 0,
                               next_=nxt,
-                              drop=_drop(cfg, seeds, site_drop2(i - 1)) if emit else ops.NO_DROP)
+                              drop=_drop(cfg, seeds, site_drop2(i - 1)) if emit else ops.NO_DROP,
+                              dy_add=dyq if kv_only else None)
             dy2_next = nxt
         else:
             da1 = torch.empty(M, D, **f32)

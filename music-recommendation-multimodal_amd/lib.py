@@ -145,6 +145,15 @@ class AttnBlockDesc(ctypes.Structure):
                 ("x1", c_p), ("a2", c_p), ("m2", c_p), ("r2", c_p)]
 
 
+class Q1KvBwdDesc(ctypes.Structure):
+    """ttmi_q1_kv_bwd_desc (include/ttmi.h, ABI 21)."""
+    _fields_ = [("B", c_i), ("L", c_i), ("H", c_i), ("Dh", c_i),
+                ("qkv", c_p), ("key_valid", c_p), ("rows", c_p), ("lse", c_p), ("dctx", c_p),
+                ("drop_p", ctypes.c_float), ("drop_seed", c_p),
+                ("dqkv", c_p), ("wqt", c_p), ("ld_wqt", ctypes.c_int64), ("a_in", c_p),
+                ("dq_rows", c_p), ("a_rows", c_p), ("dyq", c_p), ("bn", c_p)]
+
+
 class FfnBlockDesc(ctypes.Structure):
     """ttmi_ffn_block_desc (include/ttmi.h, ABI 21)."""
     _fields_ = [("M", c_i), ("D", c_i), ("F", c_i),
@@ -195,7 +204,8 @@ class LnBwdDesc(ctypes.Structure):
                 ("ld_drop", ctypes.c_int64), ("drop_rows", ctypes.c_void_p),
                 ("ln_dw", ctypes.c_void_p), ("ln_db", ctypes.c_void_p),
                 ("sum_ws", ctypes.c_void_p),
-                ("res_rows", ctypes.c_void_p), ("res_L", ctypes.c_int64)]
+                ("res_rows", ctypes.c_void_p), ("res_L", ctypes.c_int64),
+                ("dy_add", ctypes.c_void_p), ("ld_add", ctypes.c_int64)]
 
 
 class FoldDesc(ctypes.Structure):
@@ -369,6 +379,7 @@ SIGNATURES = {
     "ttmi_mha_q1_gather_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p,
                                      c_p, c_p]),
     "ttmi_mha_q1_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "ttmi_mha_q1_kv_bwd": (c_i, [c_p, c_p]),
     "ttmi_mha_q1_bnr_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p,
                                   c_p]),
     "ttmi_mha_q1_gather_item_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p,

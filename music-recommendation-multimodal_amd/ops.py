@@ -296,10 +296,15 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
                   dx: Tensor, ln_dw: Optional[Tensor], ln_db: Optional[Tensor], *,
                   res: Optional[Tensor] = None, next_: Optional[Tensor] = None,
                   drop: Drop = NO_DROP, drop_rows: Optional[Tensor] = None,
-                  res_rows: Optional[Tensor] = None, res_L: int = 0) -> Tensor:
+                  res_rows: Optional[Tensor] = None, res_L: int = 0,
+                  dy_add: Optional[Tensor] = None) -> Tensor:
     """dx = LN'(dh · wtᵀ) + res; ln_dw/ln_db += LN param grads; next_ = bf16(dropout(dx))
     (one kernel: the Linear input grad, LayerNorm backward and dropout backward).  res_rows:
-    res is [M / res_L, N] and its row b is added only to row res_rows[b] (b = m / res_L)."""
+    res is [M / res_L, N] and its row b is added only to row res_rows[b] (b = m / res_L);
+    dy_add (fp32 [M / res_L, N], with res_rows): its row b joins dh·wtᵀ of row res_rows[b]
+    before the LayerNorm backward (ABI 21)."""
+    if dy_add is not None and (res_rows is None or tuple(dy_add.shape) != (res_rows.shape[0], wt.shape[0])):
+        raise ValueError("linear_ln_bwd: dy_add needs res_rows and shape [M / res_L, N]")
     if res_rows is not None and (res is None or res_L <= 0 or res.shape[0] * res_L != dh.shape[0]):
         raise ValueError("linear_ln_bwd: res_rows needs res [M / res_L, N]")
     _dev(dh, wt, x, dx)
@@ -317,6 +322,7 @@ def linear_ln_bwd(dh: Tensor, wt: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
     d.drop_p, d.drop_seed, d.ld_drop = float(drop[0]), _p(drop[1]), N
     d.drop_rows = _p(drop_rows)
     d.res_rows, d.res_L = _p(res_rows), int(res_L)
+    d.dy_add, d.ld_add = _p(dy_add), (dy_add.stride(0) if dy_add is not None else 0)
     d.ln_dw, d.ln_db = _p(ln_dw), _p(ln_db)
     folds = []
     if ln_dw is not None or ln_db is not None:
@@ -1338,6 +1344,24 @@ def mha_q1_bwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, lse: Tensor, dctx: 
          _p(lse), _p(dctx), float(drop[0]), _p(drop[1]), _p(dqkv),
          ctypes.byref(bn) if bn is not None else None, _s())
     return dqkv
+
+
+def mha_q1_kv_bwd(qkv: Tensor, key_valid: Tensor, rows: Tensor, lse: Tensor, dctx: Tensor, B: int, L: int,
+                  H: int, dqkv: Tensor, drop: Drop, wqt: Tensor, a_in: Tensor, dq_rows: Tensor, a_rows: Tensor,
+                  dyq: Tensor, bn: Optional[BnBwdDesc] = None) -> None:
+    """The pruned layer's one-query backward for a K / V-only in_proj input grad
+    (ttmi_mha_q1_kv_bwd, ABI 21): dqkv's K / V columns (its Q columns untouched), the gathered
+    rows' dq (bf16) and a_in rows, and dyq = dq·W_q (fp32, wqt = the in_proj transposed mirror)."""
+    _dev(qkv, key_valid, rows, lse, dctx, dqkv, wqt, a_in, dq_rows, a_rows, dyq)
+    _q1_batch_check("mha_q1_kv_bwd", B, L, H, drop)
+    d = _L.Q1KvBwdDesc()
+    d.B, d.L, d.H, d.Dh = B, L, H, qkv.shape[1] // (3 * H)
+    d.qkv, d.key_valid, d.rows, d.lse, d.dctx = _p(qkv), _p(key_valid), _p(rows), _p(lse), _p(dctx)
+    d.drop_p, d.drop_seed = float(drop[0]), _p(drop[1])
+    d.dqkv, d.wqt, d.ld_wqt, d.a_in = _p(dqkv), _p(wqt), wqt.stride(0), _p(a_in)
+    d.dq_rows, d.a_rows, d.dyq = _p(dq_rows), _p(a_rows), _p(dyq)
+    d.bn = ctypes.cast(ctypes.pointer(bn), ctypes.c_void_p) if bn is not None else None
+    call("ttmi_mha_q1_kv_bwd", ctypes.byref(d), _s())
 
 
 def colsum(x: Tensor, out: Tensor) -> Tensor:

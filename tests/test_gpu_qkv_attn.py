@@ -195,3 +195,58 @@ def test_attn_block_matches_qkv_attn_then_res_ln(gpu_pkg, B, L, p):
         assert float((x1_ - x0).abs().max()) <= 1e-2 * float(x0.abs().max())
     assert float((mu1 - mu0).abs().max()) <= 1e-4 and float(((r1 - r0) / r0).abs().max()) <= 1e-4
     assert float((a1.float() - a0.float()).abs().max()) <= 0.02 * float(a0.float().abs().max())
+
+
+@pytest.mark.parametrize("B,L,p", [(512, 50, 0.1), (7, 50, 0.0), (33, 64, 0.1), (5, 1, 0.0)])
+def test_q1_kv_bwd_and_dy_add_match_full_dqkv(gpu_pkg, B, L, p):
+    """ttmi_mha_q1_kv_bwd + ttmi_linear_ln_bwd(K = 256, dy_add) against ttmi_mha_q1_bwd +
+    ttmi_linear_ln_bwd(K = 384) for the pruned layer: dqkv's K / V columns and the gathered dq
+    bit-identical, a_rows = a_in[rows], dyq = dq·W_q in fp32, and the LN1 backward (dx, the
+    emitted bf16 rows, norm1's grads) equal to the K = 384 form to fp32 rounding."""
+    ops = gpu_pkg.ops
+    H, D = 4, 128
+    M = B * L
+    g = torch.Generator().manual_seed(91 * L + B)
+    qkv = (torch.randn(M, 3 * D, generator=g) * 0.7).to(torch.bfloat16).to(DEV)
+    kv = _masks(B, L, g).to(DEV)
+    rows = torch.empty(B, dtype=torch.int32, device=DEV)
+    ops.last_rows(kv, rows)
+    lse, ctx = torch.empty(B * H, device=DEV), torch.empty(B, D, device=DEV, dtype=torch.bfloat16)
+    drop = (p, _seed(0x91 + L)) if p > 0 else (0.0, None)
+    ops.mha_q1_fwd(qkv, kv, rows, B, L, H, ctx, lse, drop)
+    dctx = torch.randn(B, D, generator=g).to(torch.bfloat16).to(DEV)
+    w_in = (torch.randn(3 * D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    wti = w_in.t().contiguous()
+    a_in = torch.randn(M, D, generator=g).to(torch.bfloat16).to(DEV)
+    dq0 = torch.empty(M, 3 * D, device=DEV, dtype=torch.bfloat16)
+    ops.mha_q1_bwd(qkv, kv, rows, lse, dctx, B, L, H, dq0, drop)
+    dq1 = torch.zeros(M, 3 * D, device=DEV, dtype=torch.bfloat16)
+    dqg, ag = torch.empty(B, D, device=DEV, dtype=torch.bfloat16), torch.empty(B, D, device=DEV, dtype=torch.bfloat16)
+    dyq = torch.empty(B, D, device=DEV)
+    ops.mha_q1_kv_bwd(qkv, kv, rows, lse, dctx, B, L, H, dq1, drop, wti, a_in, dqg, ag, dyq)
+    torch.cuda.synchronize()
+    r = rows.long()
+    assert torch.equal(dq1[:, D:].view(torch.int16), dq0[:, D:].view(torch.int16))
+    assert torch.equal(dqg.view(torch.int16), dq0[r, :D].view(torch.int16))
+    assert torch.equal(ag.view(torch.int16), a_in[r].view(torch.int16))
+    ref = dqg.float() @ w_in[:D].float()
+    assert float((dyq - ref).abs().max()) <= 1e-5 * max(float(ref.abs().max()), 1.0)
+    # the LN1 backward both ways
+    x = torch.randn(M, D, generator=g).to(DEV)
+    mu, rs = x.mean(1), torch.rsqrt(x.var(1, unbiased=False) + 1e-5)
+    n1w = (1 + 0.1 * torch.randn(D, generator=g)).to(DEV)
+    res = torch.randn(B, D, generator=g).to(DEV)
+    outs = []
+    for kvo in (False, True):
+        dx = torch.empty(M, D, device=DEV)
+        nxt = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+        gw, gb = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+        ops.linear_ln_bwd(dq1[:, D:] if kvo else dq0, wti[:, D:] if kvo else wti, x, mu, rs, n1w, dx, gw, gb,
+                          res=res, res_rows=rows, res_L=L, next_=nxt, dy_add=dyq if kvo else None)
+        torch.cuda.synchronize()
+        outs.append((dx, nxt, gw, gb))
+    (x0, n0, w0, b0), (x1, n1, w1, b1) = outs
+    assert float((x1 - x0).abs().max()) <= 1e-4 * float(x0.abs().max())
+    assert float((n1.float() - n0.float()).abs().max()) <= 0.01 * float(n0.float().abs().max())
+    assert torch.allclose(w1, w0, rtol=1e-3, atol=1e-4 * float(w0.abs().max()))
+    assert torch.allclose(b1, b0, rtol=1e-3, atol=1e-4 * float(b0.abs().max()))
