@@ -38,7 +38,7 @@ struct FfnArgs {
   int M;
 };
 
-template <int NWV, int NG>
+template <int NWV, int NG, bool PIPE, bool DF>
 __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   constexpr int F = NG * 128;
   // Every operand reaches LDS by LDS-DMA — the rows' A tile too, staged in buffer 1's W2 image
@@ -122,7 +122,8 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   {
     const uint64_t sf = *reinterpret_cast<const uint64_t*>(spar + PB + 3072);
     const uint64_t s2 = *reinterpret_cast<const uint64_t*>(spar + PB + 4096);
-    dkf = DropKeys{(uint32_t)sf, (uint32_t)(sf >> 32), g.df.thresh, g.df.scale, g.df.on};
+    dkf = DropKeys{(uint32_t)sf, (uint32_t)(sf >> 32), g.df.thresh, g.df.scale, DF};   // (DF: no branch
+                                                                              // splits the group's block)
     dk2 = DropKeys{(uint32_t)s2, (uint32_t)(s2 >> 32), g.d2.thresh, g.d2.scale, g.d2.on};
   }
   // the row's FFN1 operand: lane group lg holds k = 32 lg + 8c (the row panel's permutation)
@@ -139,45 +140,125 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   for (int t = 0; t < 8; ++t) acc2[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float4 rpre[8];
   uint64_t twait = 0;                                    // (diagnostic builds) ticks at the group seams
+  auto load_res = [&]() {                                // x1's row (after the last DMA: exact waits)
+    const float* rp = g.res + mc * FB_D + 8 * lg;
 #pragma unroll
-  for (int grp = 0; grp < NG; ++grp) {
-    const char* w1b = smem + (grp & 1) * FB_BUF + wrow * FB_P + 64 * lg;
-    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 16 * lg;
-    if (grp == NG - 1) {                                 // x1's row (after the last DMA: exact waits)
-      const float* rp = g.res + mc * FB_D + 8 * lg;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        rpre[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
-        rpre[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
-      }
+    for (int p = 0; p < 4; ++p) {
+      rpre[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
+      rpre[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
     }
-    // ---- FFN1: 16 rows x the group's 128 hidden units
-    f32x4_t acc1[8];
+  };
+  auto ffn1 = [&](int grp, f32x4_t (&acc)[8], bool barriers) {   // 16 rows x 128 hidden units
+    const char* w1b = smem + (grp & 1) * FB_BUF + wrow * FB_P + 64 * lg;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc1[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 8; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
 #pragma unroll
       for (int t = 0; t < 8; ++t)
-        Mma<bf16_t>::run(acc1[t], lds16(w1b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * c), af[c]);
-      __builtin_amdgcn_sched_barrier(0);
+        Mma<bf16_t>::run(acc[t], lds16(w1b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * c), af[c]);
+      if (barriers) __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- h = drop_f(relu(. + b1)) -> bf16 fragments (stored for the backward)
-    uint4 hq[4];
+  };
+  auto epi1 = [&](int grp, const f32x4_t (&acc)[8], uint4 (&hq)[4]) {   // h = drop_f(relu(. + b1))
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int n = 128 * grp + 32 * p + 8 * lg;
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = fmaxf(acc1[2 * p][e] + sb1[n + e], 0.f);
-        v[4 + e] = fmaxf(acc1[2 * p + 1][e] + sb1[n + 4 + e], 0.f);
+        v[e] = fmaxf(acc[2 * p][e] + sb1[n + e], 0.f);
+        v[4 + e] = fmaxf(acc[2 * p + 1][e] + sb1[n + 4 + e], 0.f);
       }
       drop_apply_vec<8>(dkf, (uint32_t)(m * F + n), v);
       hq[p] = pack8(v);
       const i32x4_t q = {(int)hq[p].x, (int)hq[p].y, (int)hq[p].z, (int)hq[p].w};
       __builtin_amdgcn_raw_buffer_store_b128(q, rh, (uint32_t)((m * F + n) * 2), 0, 0);
     }
+  };
+  auto ffn2 = [&](int grp, const uint4 (&hq)[4]) {       // FFN2's k-steps over the group's units
+    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 16 * lg;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 64 * p), hq[p]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if constexpr (PIPE) {
+    // Software pipeline: group k's epilogue (VALU: bias, ReLU, the dropout hash) runs beside group
+    // k + 1's FFN1 MFMAs, then group k's FFN2.  W1 and W2 images keep their slots (group & 1) but
+    // are re-filled on their own schedule: W1 group k + 2 as soon as FFN1 k is done (start of
+    // iteration k), W2 group k + 1 as soon as FFN2 k - 1 is (start of iteration k).  Each
+    // iteration starts with one wait — the images it reads landed; younger: the previous
+    // iteration's 4 h stores (iteration 0: W2 group 1) — and one barrier.
+    if (NG > 1) {
+      __syncthreads();                                   // every wave has its A fragments
+      issue_w2(1);                                       // (over the A tile)
+    }
+    f32x4_t acc1[8];
+    ffn1(0, acc1, true);
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const uint64_t tw0 = TTMI_TNOW();
+      if (k == 0) {
+        if (NG > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      __syncthreads();
+      twait += TTMI_TNOW() - tw0;
+      if (k >= 1 && k + 1 < NG) issue_w2(k + 1);
+      if (k + 2 < NG) issue_w1(k + 2);
+      if (k == NG - 1) load_res();
+      f32x4_t acc1n[8];
+      uint4 hq[4];
+      if (k + 1 < NG) {
+        // group k + 1's FFN1 k-step p (8 MFMAs) beside group k's epilogue columns 32p..32p+31, in
+        // fenced quarters so the MFMAs issue among the hash VALU rather than in one run
+        const char* w1b = smem + ((k + 1) & 1) * FB_BUF + wrow * FB_P + 64 * lg;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc1n[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int n = 128 * k + 32 * p + 8 * lg;
+          float v[8];
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+            for (int t = 4 * hf; t < 4 * hf + 4; ++t)
+              Mma<bf16_t>::run(acc1n[t], lds16(w1b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * p), af[p]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[4 * hf + e] = fmaxf(acc1[2 * p + hf][e] + sb1[n + 4 * hf + e], 0.f);
+            drop_apply_vec<4>(dkf, (uint32_t)(m * F + n + 4 * hf), v + 4 * hf);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          hq[p] = pack8(v);
+          const i32x4_t q = {(int)hq[p].x, (int)hq[p].y, (int)hq[p].z, (int)hq[p].w};
+          __builtin_amdgcn_raw_buffer_store_b128(q, rh, (uint32_t)((m * F + n) * 2), 0, 0);
+        }
+      } else {
+        epi1(k, acc1, hq);
+      }
+      ffn2(k, hq);
+      if (k + 1 < NG) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc1[t] = acc1n[t];
+      }
+      TTMI_TSTAMP(2 + (k < 4 ? k : 3));
+    }
+  } else {
+#pragma unroll
+  for (int grp = 0; grp < NG; ++grp) {
+    if (grp == NG - 1) load_res();
+    // ---- FFN1: 16 rows x the group's 128 hidden units
+    f32x4_t acc1[8];
+    ffn1(grp, acc1, true);
+    // ---- h = drop_f(relu(. + b1)) -> bf16 fragments (stored for the backward)
+    uint4 hq[4];
+    epi1(grp, acc1, hq);
     if (grp == 0) {
       // W2 group 0 landed (behind it: W1 group 1, this group's 4 h stores); every wave has read
       // its A fragments, so W2 group 1 may overwrite the A tile
@@ -186,14 +267,7 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
       __syncthreads();
       if (NG > 1) issue_w2(1);
     }
-    // ---- FFN2's k-steps over these hidden units
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 64 * p), hq[p]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    ffn2(grp, hq);
     if (grp + 1 < NG) {
       const uint64_t tw0 = TTMI_TNOW();
       __syncthreads();                                   // every wave is done with this buffer
@@ -212,6 +286,7 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
       twait += TTMI_TNOW() - tw0;
     }
     TTMI_TSTAMP(2 + (grp < 4 ? grp : 3));
+  }
   }
   // ---- x2 = x1 + drop2(. + b2); y = LN(x2) (the row's 128 columns in lanes li, li+16, li+32, li+48)
   float vr[32];
@@ -516,7 +591,11 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
 template <int NG>
 void launch_ffn(const FfnArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)((a.M + 127) / 128));       // 8 waves, one 16-row tile each
-  hipLaunchKernelGGL((ffn_block_kernel<8, NG>), grid, dim3(512), 0, s, a);
+  static const bool pipe = !getenv("TTMI_FFN_NOPIPE");  // (A/B: the unpipelined group loop)
+  if (pipe && a.df.on) hipLaunchKernelGGL((ffn_block_kernel<8, NG, true, true>), grid, dim3(512), 0, s, a);
+  else if (pipe) hipLaunchKernelGGL((ffn_block_kernel<8, NG, true, false>), grid, dim3(512), 0, s, a);
+  else if (a.df.on) hipLaunchKernelGGL((ffn_block_kernel<8, NG, false, true>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((ffn_block_kernel<8, NG, false, false>), grid, dim3(512), 0, s, a);
 }
 
 }  // namespace
