@@ -352,9 +352,9 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
 //   dx1 = rstd·(dY·w − mean(dY·w) − x̂·mean(dY·w·x̂)) + res,  dy1 = bf16(drop1ᵀ(dx1)),
 //   Σ_rows dY·x̂ and Σ_rows dY per workgroup -> sum_ws[blk][2][D] (folded in workgroup order).
 // dY sums its k-steps in hidden-unit order: dx1 / dy1 / the sums agree with the row panels to
-// fp32 rounding.  The gate rows are compiler-counted loads, so the group seams wait with a full
-// vmcnt(0) the compiler sees: each gate load is issued right after one seam and read after the
-// next (a wait for it inside a group would also wait for the DMAs behind it).
+// fp32 rounding.  The gate rows are compiler-counted loads: each is issued right after one seam
+// (behind the next images' DMAs) and read after the next seam, whose wait the compiler sees
+// (a builtin s_waitcnt: vmcnt(4), the group's dz1 buffer stores left in flight).
 struct FfnBwdArgs {
   const bf16_t* dy; const bf16_t* w2t; const bf16_t* w1t; const bf16_t* h; float sf;
   bf16_t* dz1;
@@ -465,6 +465,9 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
   }
   if (NG == 1) load_rows();
   const int wrow = 8 * (li >> 2) + (li & 3);
+  // dz1 stores through a buffer resource (rows past M dropped by its range): exactly 4 a group
+  const __amdgpu_buffer_rsrc_t rdz =
+      __builtin_amdgcn_make_buffer_rsrc(g.dz1, 0, (int)((int64_t)g.M * F * 2), 0x00020000);
   f32x4_t acc2[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc2[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -497,7 +500,8 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
         v[2 * e + 1] = __uint_as_float(qw[e] & 0xFFFF0000u) > 0.f ? v[2 * e + 1] * g.sf : 0.f;
       }
       hq[p] = pack8(v);
-      if (mok) *reinterpret_cast<uint4*>(g.dz1 + m * F + n) = hq[p];
+      const i32x4_t q = {(int)hq[p].x, (int)hq[p].y, (int)hq[p].z, (int)hq[p].w};
+      __builtin_amdgcn_raw_buffer_store_b128(q, rdz, (uint32_t)((m * F + n) * 2), 0, 0);
     }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -508,7 +512,9 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
     }
     if (grp + 1 < NG) {
       __syncthreads();                                   // every wave is done with this buffer
-      __builtin_amdgcn_s_waitcnt(0);                     // group grp + 1's images and gate rows
+      // group grp + 1's images and gate rows; younger: this group's 4 dz1 stores (vmcnt 4,
+      // expcnt / lgkmcnt not waited), which stay in flight across the seam
+      __builtin_amdgcn_s_waitcnt(0x0F74);
 #pragma unroll
       for (int p = 0; p < 4; ++p) hg[p] = hn[p];
       if (grp + 2 < NG) {
