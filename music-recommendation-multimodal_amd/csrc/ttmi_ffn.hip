@@ -363,18 +363,6 @@ struct FfnBwdArgs {
   int M;
 };
 
-template <int CTRL>
-TTMI_DEV float fb_dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-TTMI_DEV float fb_row16_sum(float v) {     // the 16 lanes of a DPP row, every lane gets the sum
-  v += fb_dpp<0xB1>(v);                    // quad_perm [1,0,3,2]
-  v += fb_dpp<0x4E>(v);                    // quad_perm [2,3,0,1]
-  v += fb_dpp<0x141>(v);                   // row_half_mirror
-  v += fb_dpp<0x140>(v);                   // row_mirror
-  return v;
-}
-
 template <int NG>
 __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
   constexpr int NWV = 8, F = NG * 128;
@@ -569,16 +557,41 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
       *reinterpret_cast<uint4*>(g.dy1 + m * FB_D + n) = pack8(o);
     }
   }
-  // LayerNorm weight / bias grads: the tile's 16 rows (one DPP row) -> this wave's LDS row
+  TTMI_TSTAMP(7);
+  // LayerNorm weight / bias grads: the tile's 16 rows summed per column in row order through a
+  // wave-private LDS slice (16 rows x 132 floats) of the W buffer no wave reads any more (the
+  // last group used the other one): 8 ds_write_b128 + 8 ds_read_b128 a lane per quantity, where
+  // DPP row sums cost 4 dependent steps per column value.  Lanes 0-31 sum rows 0-7 and lanes
+  // 32-63 rows 8-15 of column group lane & 31; the halves meet in that order.
+  {
+    constexpr int RS = 132;                              // row stride (floats): 16 B bank shift
+    float* red = reinterpret_cast<float*>(smem + (NG & 1) * FB_BUF) + wave * 16 * RS;
+    const int cg = lane & 31, rh = lane >> 5;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+    for (int qd = 0; qd < 2; ++qd) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float a = fb_row16_sum(dy[8 * p + e] * xh[8 * p + e]);
-      const float b = fb_row16_sum(dy[8 * p + e]);
-      if (li == 0) {
-        sdw[wave][32 * p + 8 * lg + e] = a;
-        sdb[wave][32 * p + 8 * lg + e] = b;
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int b = 8 * p + 4 * hf;
+          const float4 v = qd == 0 ? make_float4(dy[b] * xh[b], dy[b + 1] * xh[b + 1], dy[b + 2] * xh[b + 2],
+                                                 dy[b + 3] * xh[b + 3])
+                                   : make_float4(dy[b], dy[b + 1], dy[b + 2], dy[b + 3]);
+          *reinterpret_cast<float4*>(red + li * RS + 32 * p + 8 * lg + 4 * hf) = v;
+        }
+      }
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float4 w = *reinterpret_cast<const float4*>(red + (8 * rh + r) * RS + 4 * cg);
+        acc.x += w.x; acc.y += w.y; acc.z += w.z; acc.w += w.w;
+      }
+      float4 hi;
+      hi.x = __shfl_down(acc.x, 32, 64); hi.y = __shfl_down(acc.y, 32, 64);
+      hi.z = __shfl_down(acc.z, 32, 64); hi.w = __shfl_down(acc.w, 32, 64);
+      if (rh == 0) {
+        acc.x += hi.x; acc.y += hi.y; acc.z += hi.z; acc.w += hi.w;
+        *reinterpret_cast<float4*>((qd == 0 ? &sdw[wave][0] : &sdb[wave][0]) + 4 * cg) = acc;
       }
     }
   }

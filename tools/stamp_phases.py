@@ -94,13 +94,14 @@ def main():
     nod = (0.0, None)
     stamps(lambda: ops.ffn_block_fwd(a1, w1f, b1f, w2f, b2f, x1f, nod, nod, hf, x2f, lnwf, lnbf, 1e-5, yf, muf, rsf),
            "ffn block fwd, no dropout", nph=7, tu="ffn")
-    # its backward (phases: 0 start, 1 prologue done, 2-5 hidden groups 0-3 done, 6 end)
+    # its backward (phases: 0 start, 1 prologue done, 2-5 hidden groups 0-3 done, 6 end, 7 the
+    # LayerNorm backward's row stores issued)
     dy2f, w2tf, w1tf = bf(M, D, sc=0.1), bf(512, D), bf(D, 512)
     dz1f, dx1f, dy1f = torch.empty(M, 512, device=dev, dtype=torch.bfloat16), torch.empty(M, D, device=dev), \
         torch.empty(M, D, device=dev, dtype=torch.bfloat16)
     gwf, gbf = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
     stamps(lambda: ops.ffn_block_bwd(dy2f, w2tf, w1tf, hf, 1 / 0.9, dz1f, x1f, muf, rsf, lnwf, x2f, dx1f, dy1f,
-                                     drop, gwf, gbf), "ffn block bwd", nph=7, tu="ffn")
+                                     drop, gwf, gbf), "ffn block bwd (p7: row stores issued)", nph=8, tu="ffn")
     if os.environ.get("STAMP_FFN_ONLY"):
         return
     wo, bo = bf(D, D), f32(D, sc=0.1)
