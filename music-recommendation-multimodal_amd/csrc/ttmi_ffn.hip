@@ -434,24 +434,31 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
   TTMI_TSTAMP(1);
   float4 rx[8], rr[8];
   float mu = 0.f, rs = 0.f;
-  auto load_rows = [&]() {                               // the LayerNorm backward's row operands
+  // the LayerNorm backward's row operands: x1 (+ its statistics) and the residual grad, issued at
+  // two different seams so no one seam queues 1 KB of loads a row behind its DMAs
+  auto load_x1 = [&]() {
     const float* xp = g.x1 + mc * FB_D + 8 * lg;
-    const float* rp = g.res + mc * FB_D + 8 * lg;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       rx[2 * p] = *reinterpret_cast<const float4*>(xp + 32 * p);
       rx[2 * p + 1] = *reinterpret_cast<const float4*>(xp + 32 * p + 4);
-      rr[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
-      rr[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
     }
     mu = g.m2[mc];
     rs = g.r2[mc];
+  };
+  auto load_res = [&]() {
+    const float* rp = g.res + mc * FB_D + 8 * lg;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      rr[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
+      rr[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
+    }
   };
   if (NG > 1) {
     issue_group(1);
     load_gate(1, hn);
   }
-  if (NG == 1) load_rows();
+  if (NG == 1) { load_x1(); load_res(); }
   const int wrow = 8 * (li >> 2) + (li & 3);
   // dz1 stores through a buffer resource (rows past M dropped by its range): exactly 4 a group
   const __amdgpu_buffer_rsrc_t rdz =
@@ -508,9 +515,9 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
       if (grp + 2 < NG) {
         issue_group(grp + 2);
         load_gate(grp + 2, hn);
-      } else {
-        load_rows();
       }
+      if (grp == (NG > 2 ? NG - 3 : 0)) load_x1();
+      if (grp == NG - 2) load_res();
       __syncthreads();                                   // every wave's part of the images landed
     }
     TTMI_TSTAMP(2 + (grp < 4 ? grp : 3));
