@@ -405,6 +405,8 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) q[p] = hp[4 * p];
   };
+  uint4 hg[4], hn[4];
+  load_gate(0, hg);                                      // (from HBM: issued ahead of the DMAs)
   {
     const uint32_t dst = lds_addr(spar) + (uint32_t)(wv * 1024), off = (uint32_t)(lane * 16);
     if (wv == 0) dma16(make_rsrc(g.lnw, FB_D * 4), off, dst);
@@ -416,8 +418,6 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
     for (int j = 0; j < PW; ++j) dma16(ra, oA[j], base + slot(j) * 1024);
   }
   issue_group(0);
-  uint4 hg[4], hn[4];
-  load_gate(0, hg);
   for (int i = tid; i < NWV * FB_D; i += 64 * NWV) { (&sdw[0][0])[i] = 0.f; (&sdb[0][0])[i] = 0.f; }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
