@@ -158,6 +158,9 @@ typedef struct ttmi_fold_plan {
 } ttmi_fold_plan;
 int ttmi_wgrad_batch_plan(int n, const ttmi_wgrad_desc* const* descs, int nf,
                           const ttmi_fold_desc* folds, ttmi_fold_plan* plan, hipStream_t stream);
+/* Append src's segments to dst (one update for GEMMs planned early on a side stream and folds
+ * planned later); when dst has no room left, src's segments are folded on `stream` instead. */
+int ttmi_fold_plan_merge(ttmi_fold_plan* dst, const ttmi_fold_plan* src, hipStream_t stream);
 int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                       const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
                       int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,

@@ -3021,6 +3021,16 @@ extern "C" int ttmi_wgrad_batch_plan(int n, const ttmi_wgrad_desc* const* descs,
   return TTMI_OK;
 }
 
+extern "C" int ttmi_fold_plan_merge(ttmi_fold_plan* dst, const ttmi_fold_plan* src, hipStream_t stream) {
+  TTMI_REQUIRE(dst && src && dst->n >= 0 && dst->n <= AF_SEGS && src->n >= 0 && src->n <= AF_SEGS,
+               "ttmi_fold_plan_merge: bad plan");
+  const FoldSeg* b = reinterpret_cast<const FoldSeg*>(src->seg);
+  if (dst->n + src->n > AF_SEGS) return launch_fold_segs(b, src->n, stream);   // no room: fold now
+  memcpy(reinterpret_cast<FoldSeg*>(dst->seg) + dst->n, b, (size_t)src->n * sizeof(FoldSeg));
+  dst->n += src->n;
+  return TTMI_OK;
+}
+
 extern "C" int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                                  const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
                                  int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,

@@ -548,6 +548,9 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         if on_layer_done is not None:
             on_layer_done(i)
     # ---- input block (user_tower.py:83-93)
+    # every weight gradient is recorded: the grouped GEMMs run on a side stream beside the
+    # input block's backward (its 4-wave, 2 KB-LDS workgroups fit beside theirs on a CU)
+    ops.wgrad_launch_early()
     ops.seq_embed_bwd(st.ids, P["item_embedding.weight"], P["position_embedding.weight"],
                       P["layer_norm.weight"], st.m0, st.r0, dx, grads["item_embedding.weight"],
                       grads["position_embedding.weight"], grads["layer_norm.weight"],

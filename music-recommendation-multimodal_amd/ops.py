@@ -210,6 +210,7 @@ class WgradPending:
         self.defer_fold = defer_fold
         self.plan = None
         self.keep: list = []
+        self.side = None          # launch_early's stream, joined by flush()
 
     def slot(self, key: str) -> int:
         """Index of the next persistent zero workspace for ``key`` within this block: calls
@@ -219,7 +220,40 @@ class WgradPending:
         self.slots[key] = k + 1
         return k
 
+    def launch_early(self, side: "torch.cuda.Stream") -> bool:
+        """defer_fold only: run the GEMMs recorded so far now, as one grouped launch on ``side``
+        (after the current stream's work), so they overlap what the current stream does next;
+        their fold segments join the folds' at flush(), which also joins ``side``.  Nothing may
+        be recorded after this call but LayerNorm sums / fixed-point folds."""
+        if not self.defer_fold or self.plan is not None or not self.items:
+            return False
+        arr = (ctypes.POINTER(WgradDesc) * len(self.items))(*[ctypes.pointer(d) for d, *_ in self.items])
+        side.wait_stream(torch.cuda.current_stream(side.device))
+        self.plan = _L.FoldPlan()
+        with torch.cuda.stream(side):
+            call("ttmi_wgrad_batch_plan", len(self.items), arr, 0, (FoldDesc * 1)(),
+                 ctypes.byref(self.plan), _s())
+        self.keep = self.items
+        self.items = []
+        self.side = side
+        return True
+
     def flush(self) -> None:
+        if self.side is not None:         # launch_early ran: plan the folds, join the GEMMs
+            if self.items:
+                raise RuntimeError("WgradPending: weight gradients recorded after launch_early")
+            if self.folds:
+                farr = (FoldDesc * len(self.folds))(*[f for f, *_ in self.folds])
+                p2 = _L.FoldPlan()
+                call("ttmi_wgrad_batch_plan", 0, (ctypes.POINTER(WgradDesc) * 1)(), len(self.folds), farr,
+                     ctypes.byref(p2), _s())
+                call("ttmi_fold_plan_merge", ctypes.byref(self.plan), ctypes.byref(p2), _s())
+                self.keep = self.keep + self.folds
+            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+            self.side = None
+            self.folds = []
+            self.slots = {}
+            return
         if not self.items and not self.folds:
             return
         arr = (ctypes.POINTER(WgradDesc) * max(len(self.items), 1))(
@@ -253,6 +287,27 @@ def deferred_wgrad(defer_fold: bool = False):
     finally:
         _PENDING.pop()
         pend.flush()
+
+
+_WG_SIDE: Dict[str, "torch.cuda.Stream"] = {}
+_WG_EARLY = os.environ.get("TTMI_WGRAD_EARLY", "1") != "0"
+
+
+def wgrad_launch_early() -> bool:
+    """Inside ``deferred_wgrad(defer_fold=True)``: launch the weight-gradient GEMMs recorded so
+    far on a side stream (created per device on first use, i.e. in an eager step before any
+    graph capture) so they overlap the rest of the backward (``TTMI_WGRAD_EARLY=0``: at the
+    block's exit, as before).  Results are unchanged: same GEMMs, same fold order."""
+    if not (_WG_EARLY and _PENDING):
+        return False
+    pend = _PENDING[-1]
+    if not pend.defer_fold or not pend.items:
+        return False
+    dev = pend.items[0][2].device
+    key = str(dev)
+    if key not in _WG_SIDE:
+        _WG_SIDE[key] = torch.cuda.Stream(dev)
+    return pend.launch_early(_WG_SIDE[key])
 
 
 def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
