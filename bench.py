@@ -29,6 +29,7 @@ import socket
 import subprocess
 import sys
 import time
+from typing import Optional
 
 import torch
 import torch.distributed as dist
@@ -190,7 +191,10 @@ def probe_dominant(step, batch, device, iters: int = 20):
     gbs = by / sec / 1e9
     # PMC bytes of the family's two launches per step (tools/traffic.py), shared out over the
     # step's weight-gradient GEMMs like avg_us
-    tg, tfold = read_traffic("wgrad_group_kernel"), read_traffic("wgrad_fold_kernel")
+    # (the fold counts only when measured in the same file: since the fold moved into the
+    # AdamW launch no step runs wgrad_fold_kernel, and an older round's figure must not join)
+    src = traffic_file("wgrad_group_kernel")
+    tg, tfold = read_traffic("wgrad_group_kernel"), read_traffic("wgrad_fold_kernel", src)
     traffic = round((tg + (tfold or 0)) / n) if tg is not None else None
     return {"kernel": "ttmi_wgrad_batch: the step's 12 weight-gradient GEMMs as one "
                       "wgrad_group_kernel launch + 1 wgrad_fold_kernel (deterministic split "
@@ -401,18 +405,29 @@ def cpu_baseline_cfg4(B: int, budget_s: float = 20.0):
                       f"rate ({c3['value']} pairs/s: {c3['sample']}); fp32 torch-CPU oracle"}
 
 
-def read_traffic(name: str):
-    """Per-launch HBM bytes of `name` from the committed rocprofv3 PMC summary
-    (profiles/*traffic*.json, written by tools/traffic.py), or None."""
+def _traffic_lookup(name: str, only: Optional[str] = None):
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+        if only is not None and path != only:
+            continue
         try:                                   # newest round's file that measured `name`
             with open(path) as f:
                 v = json.load(f).get(name, {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             continue
         if v is not None:
-            return v
-    return None
+            return path, v
+    return None, None
+
+
+def traffic_file(name: str) -> Optional[str]:
+    """The committed PMC summary read_traffic(name) takes its figure from."""
+    return _traffic_lookup(name)[0]
+
+
+def read_traffic(name: str, only: Optional[str] = None):
+    """Per-launch HBM bytes of `name` from the committed rocprofv3 PMC summary
+    (profiles/*traffic*.json, written by tools/traffic.py; `only`: that file alone), or None."""
+    return _traffic_lookup(name, only)[1]
 
 
 def _cpu_host() -> dict:
