@@ -158,6 +158,13 @@ typedef struct ttmi_fold_plan {
 } ttmi_fold_plan;
 int ttmi_wgrad_batch_plan(int n, const ttmi_wgrad_desc* const* descs, int nf,
                           const ttmi_fold_desc* folds, ttmi_fold_plan* plan, hipStream_t stream);
+/* ttmi_adamw_folded leaving [skip_off, skip_off + skip_len) (float4-aligned; fx must be NULL)
+ * untouched: a range already updated by its own ttmi_adamw_fx launch (the item-embedding rows,
+ * updated beside the weight-gradient GEMMs while they run on a side stream). */
+int ttmi_adamw_folded_skip(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
+                           const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
+                           int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
+                           int64_t skip_off, int64_t skip_len, hipStream_t stream);
 /* Append src's segments to dst (one update for GEMMs planned early on a side stream and folds
  * planned later); when dst has no room left, src's segments are folded on `stream` instead. */
 int ttmi_fold_plan_merge(ttmi_fold_plan* dst, const ttmi_fold_plan* src, hipStream_t stream);

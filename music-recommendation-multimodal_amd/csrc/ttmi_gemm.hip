@@ -3035,6 +3035,25 @@ extern "C" int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float*
                                  const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
                                  int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
                                  hipStream_t s) {
+  return ttmi_adamw_folded_skip(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift,
+                                plan, 0, 0, s);
+}
+
+extern "C" int ttmi_adamw_folded_skip(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
+                                      const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
+                                      int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
+                                      int64_t skip_off, int64_t skip_len, hipStream_t s) {
+  TTMI_REQUIRE(skip_len == 0 || (!fx && skip_off >= 0 && skip_len > 0 && skip_off % 4 == 0 && skip_len % 4 == 0 &&
+                                 skip_off + skip_len <= n),
+               "ttmi_adamw_folded_skip: the skipped range must be float4-aligned, inside [0, n), without fx");
+  if (skip_len > 0 && (!plan || plan->n <= 0 || n % 4 != 0)) {   // the plain update around it
+    int rc = plan && plan->n > 0 ? launch_fold_segs(reinterpret_cast<const FoldSeg*>(plan->seg), plan->n, s) : 0;
+    if (rc) return rc;
+    const int64_t e = skip_off + skip_len;
+    rc = ttmi_adamw(skip_off, p, g, m, v, p_bf16, hyper, step, zero_grad, s);
+    if (rc) return rc;
+    return ttmi_adamw(n - e, p + e, g + e, m + e, v + e, p_bf16 ? p_bf16 + e : nullptr, hyper, step, zero_grad, s);
+  }
   if (!plan || plan->n <= 0)
     return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, s);
   TTMI_REQUIRE(plan->n <= AF_SEGS, "ttmi_adamw_folded: bad plan");
@@ -3055,6 +3074,7 @@ extern "C" int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float*
     }
   }
   if (ok && fx) cov.push_back({fx_off / 4, (fx_off + fx_len) / 4});   // must not overlap: checked below
+  if (ok && skip_len > 0) cov.push_back({skip_off / 4, (skip_off + skip_len) / 4});   // updated already
   std::sort(cov.begin(), cov.end());
   for (size_t i = 1; ok && i < cov.size(); ++i) ok = cov[i].first >= cov[i - 1].second;
   AdamFoldArgs a;
@@ -3079,6 +3099,13 @@ extern "C" int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float*
   if (!ok) {                  // layout the fused form cannot take: fold, then the plain update
     int rc = launch_fold_segs(segs, plan->n, s);
     if (rc) return rc;
+    if (skip_len > 0) {
+      const int64_t e = skip_off + skip_len;
+      rc = ttmi_adamw(skip_off, p, g, m, v, p_bf16, hyper, step, zero_grad, s);
+      if (rc) return rc;
+      return ttmi_adamw(n - e, p + e, g + e, m + e, v + e, p_bf16 ? p_bf16 + e : nullptr, hyper, step,
+                        zero_grad, s);
+    }
     return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, s);
   }
   TTMI_REQUIRE(((uintptr_t)p & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0 &&

@@ -249,6 +249,8 @@ SIGNATURES = {
                                ctypes.POINTER(FoldDesc), c_p]),
     "ttmi_wgrad_batch_plan": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
                                     ctypes.POINTER(FoldDesc), ctypes.POINTER(FoldPlan), c_p]),
+    "ttmi_adamw_folded_skip": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
+                                     ctypes.POINTER(FoldPlan), c_i64, c_i64, c_p]),
     "ttmi_fold_plan_merge": (c_i, [ctypes.POINTER(FoldPlan), ctypes.POINTER(FoldPlan), c_p]),
     "ttmi_adamw_folded": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
                                 ctypes.POINTER(FoldPlan), c_p]),

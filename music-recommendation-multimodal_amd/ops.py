@@ -211,6 +211,7 @@ class WgradPending:
         self.plan = None
         self.keep: list = []
         self.side = None          # launch_early's stream, joined by flush()
+        self.hold_join = False    # flush() leaves the join to the caller (join())
 
     def slot(self, key: str) -> int:
         """Index of the next persistent zero workspace for ``key`` within this block: calls
@@ -238,6 +239,12 @@ class WgradPending:
         self.side = side
         return True
 
+    def join(self) -> None:
+        """The current stream waits for launch_early's GEMMs (no-op when none ran)."""
+        if self.side is not None:
+            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+            self.side = None
+
     def flush(self) -> None:
         if self.side is not None:         # launch_early ran: plan the folds, join the GEMMs
             if self.items:
@@ -249,8 +256,8 @@ class WgradPending:
                      ctypes.byref(p2), _s())
                 call("ttmi_fold_plan_merge", ctypes.byref(self.plan), ctypes.byref(p2), _s())
                 self.keep = self.keep + self.folds
-            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
-            self.side = None
+            if not self.hold_join:
+                self.join()
             self.folds = []
             self.slots = {}
             return
@@ -1186,15 +1193,39 @@ def bump_param_epoch() -> None:
     PARAM_EPOCH[0] += 1
 
 
+def adamw_fx_range(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
+                   step: Tensor, fx: Tuple[Tensor, Tensor], zero_grad: bool = False) -> Tuple[int, int]:
+    """AdamW over the flat slot ``fx[1]`` alone, its gradient read from (and cleared in) the
+    fixed-point accumulator ``fx[0]`` (ttmi_adamw_fx on the slot's sub-range); returns the slot's
+    (offset, length) for adamw(skip=...)."""
+    acc, view = fx
+    off, cnt = (view.data_ptr() - g.data_ptr()) // g.element_size(), view.numel()
+    if off % 4 or cnt % 4 or off < 0 or off + cnt > g.numel():
+        raise ValueError("adamw_fx_range: the slot must be float4-aligned inside the flat buffer")
+    e = 4 * off
+    call("ttmi_adamw_fx", cnt, p.data_ptr() + e, g.data_ptr() + e, m.data_ptr() + e, v.data_ptr() + e,
+         (p_bf16.data_ptr() + 2 * off) if p_bf16 is not None else None, _p(hyper), _p(step),
+         int(zero_grad), _p(acc), 0, cnt, FX_GRAD_SHIFT, _s())
+    return off, cnt
+
+
 def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
           step: Tensor, zero_grad: bool = False,
-          fx: Optional[Tuple[Tensor, Tensor]] = None, fold_plan=None):
+          fx: Optional[Tuple[Tensor, Tensor]] = None, fold_plan=None,
+          skip: Optional[Tuple[int, int]] = None):
     """Fused AdamW over flat buffers.  ``fx`` = (acc, grad_view): the gradient of the slot
     ``grad_view`` (a view into ``g``) is still in the int64 fixed-point accumulator ``acc``
     (fx_grad_sink): read from there and ``acc`` cleared (ttmi_adamw_fx).  ``fold_plan``
     (WgradPending(defer_fold=True).plan): the step's weight-gradient partials are folded and
     applied in the same launch (ttmi_adamw_folded)."""
     bump_param_epoch()
+    if skip is not None:                   # (offset, length) updated by adamw_fx_range
+        if fx is not None:
+            raise ValueError("adamw: skip and fx are exclusive")
+        call("ttmi_adamw_folded_skip", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper),
+             _p(step), int(zero_grad), None, 0, 0, FX_GRAD_SHIFT,
+             ctypes.byref(fold_plan) if fold_plan is not None else None, int(skip[0]), int(skip[1]), _s())
+        return
     if fold_plan is not None:
         acc, off, cnt = None, 0, 0
         if fx is not None:

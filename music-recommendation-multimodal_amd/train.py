@@ -34,6 +34,8 @@ from .item_tower import ITEM_GEMMS
 
 Tensor = torch.Tensor
 logger = logging.getLogger(__name__)
+# the item-embedding rows' AdamW beside the side-stream weight-gradient GEMMs (TrainStep._update)
+_ADAM_SPLIT = os.environ.get("TTMI_ADAM_SPLIT", "0") == "1"
 
 
 # ------------------------------------------------------------------ reference-shaped API
@@ -298,6 +300,7 @@ class TrainStep:
         # folded slots of flat.grad are never written either (same caveat as grad_sink)
         self.fold_in_update = grad_sink and os.environ.get("TTMI_FOLD_IN_UPDATE", "1") != "0"
         self._fold = None
+        self._pend = None
         model.train()
         dev = next(model.parameters()).device
         self.device = dev
@@ -437,9 +440,12 @@ class TrainStep:
         # one process: the step's weight-gradient partials are folded inside the AdamW launch
         with ops.deferred_wgrad(defer_fold=self.fold_in_update) as pend, \
                 (ops.fx_grad_sink() if fx_sink else contextlib.nullcontext([])) as sink:
-            # one fold launch for the step's weight grads
+            # one fold launch for the step's weight grads; with the GEMMs on the side stream
+            # (ops.wgrad_launch_early) the update joins them (_update)
+            pend.hold_join = True
             self._bwd(b, u, it, modal, ust, ist, rst if self.raw_items else None, cut, pend)
         self._fold = (pend.plan, pend.keep) if pend.plan is not None else None
+        self._pend = pend
         if sink:
             acc, view = sink[0]
             if view.data_ptr() >= self.flat.grad.data_ptr() and \
@@ -552,8 +558,22 @@ class TrainStep:
 
     def _update(self) -> None:
         f = self.flat
-        ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
-                  zero_grad=True, fx=self._fx, fold_plan=self._fold[0] if self._fold else None)
+        pend, self._pend = self._pend, None
+        plan = self._fold[0] if self._fold else None
+        if pend is not None and pend.side is not None and self._fx is not None and _ADAM_SPLIT:
+            # the item-embedding rows' update (their gradient complete in the fixed-point
+            # accumulator) runs while the weight-gradient GEMMs finish on the side stream; the
+            # rest of the flat buffer after the join
+            skip = ops.adamw_fx_range(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper,
+                                      self.step_t, self._fx, zero_grad=True)
+            pend.join()
+            ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
+                      zero_grad=True, fold_plan=plan, skip=skip)
+        else:
+            if pend is not None:
+                pend.join()
+            ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
+                      zero_grad=True, fx=self._fx, fold_plan=plan)
         self._fx = None
         self._fold = None
 

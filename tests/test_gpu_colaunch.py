@@ -263,12 +263,19 @@ def test_trainstep_fold_in_update_is_bit_identical(gpu_pkg, D, monkeypatch):
     """One process folds the step's weight-gradient partials inside the AdamW launch
     (ttmi_wgrad_batch_plan + ttmi_adamw_folded, ABI 19): the same sums in the same order, the
     same AdamW arithmetic, so the parameters and both moments are bit-identical to the fold
-    launch + AdamW launch path (TTMI_FOLD_IN_UPDATE=0), in graph replays and eagerly."""
+    launch + AdamW launch path (TTMI_FOLD_IN_UPDATE=0), in graph replays and eagerly; and with
+    the weight-gradient GEMMs on the main stream and one AdamW launch (no side-stream overlap,
+    no item-embedding update of its own: TTMI_WGRAD_EARLY=0, TTMI_ADAM_SPLIT=0)."""
+    import importlib
     from oracle import two_tower_ref as ref
+    train_mod = importlib.import_module(gpu_pkg.__name__ + ".train")
     B, L, V = 64, 20, 301
     outs = []
-    for fold, graph in ((True, True), (False, True), (True, False)):
+    for fold, graph, overlap in ((True, True, True), (False, True, True), (True, False, True),
+                                 (True, True, False)):
         monkeypatch.setenv("TTMI_FOLD_IN_UPDATE", "1" if fold else "0")
+        monkeypatch.setattr(gpu_pkg.ops, "_WG_EARLY", overlap)
+        monkeypatch.setattr(train_mod, "_ADAM_SPLIT", overlap)
         torch.manual_seed(3)
         m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=V, tabular_input_dim=128,
                                   num_genders=3, num_countries=16, max_seq_len=L, user_embedding_dim=D,
