@@ -140,14 +140,15 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   for (int t = 0; t < 8; ++t) acc2[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float4 rpre[8];
   uint64_t twait = 0;                                    // (diagnostic builds) ticks at the group seams
-  auto load_res = [&]() {                                // x1's row (after the last DMA: exact waits)
+  auto load_res_half = [&](int h) {                      // x1's row, column quarters 2h, 2h + 1
     const float* rp = g.res + mc * FB_D + 8 * lg;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 2 * h; p < 2 * h + 2; ++p) {
       rpre[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
       rpre[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
     }
   };
+  auto load_res = [&]() { load_res_half(0); load_res_half(1); };
   auto ffn1 = [&](int grp, f32x4_t (&acc)[8], bool barriers) {   // 16 rows x 128 hidden units
     const char* w1b = smem + (grp & 1) * FB_BUF + wrow * FB_P + 64 * lg;
 #pragma unroll
@@ -212,7 +213,13 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
       twait += TTMI_TNOW() - tw0;
       if (k >= 1 && k + 1 < NG) issue_w2(k + 1);
       if (k + 2 < NG) issue_w1(k + 2);
-      if (k == NG - 1) load_res();
+      // x1's row for the epilogue, half an iteration early (after that iteration's DMAs: the
+      // next seam's vmcnt(4) covers it), half in the last
+      if (NG > 1 && k == NG - 2) load_res_half(0);
+      if (k == NG - 1) {
+        if (NG > 1) load_res_half(1);
+        else load_res();
+      }
       f32x4_t acc1n[8];
       uint4 hq[4];
       if (k + 1 < NG) {
