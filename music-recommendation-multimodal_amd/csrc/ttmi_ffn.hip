@@ -443,20 +443,22 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
   float mu = 0.f, rs = 0.f;
   // the LayerNorm backward's row operands: x1 (+ its statistics) and the residual grad, issued at
   // two different seams so no one seam queues 1 KB of loads a row behind its DMAs
-  auto load_x1 = [&]() {
+  auto load_x1 = [&](int h) {                            // column quarters 2h, 2h + 1
     const float* xp = g.x1 + mc * FB_D + 8 * lg;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 2 * h; p < 2 * h + 2; ++p) {
       rx[2 * p] = *reinterpret_cast<const float4*>(xp + 32 * p);
       rx[2 * p + 1] = *reinterpret_cast<const float4*>(xp + 32 * p + 4);
     }
-    mu = g.m2[mc];
-    rs = g.r2[mc];
+    if (h == 0) {
+      mu = g.m2[mc];
+      rs = g.r2[mc];
+    }
   };
-  auto load_res = [&]() {
+  auto load_res = [&](int h) {
     const float* rp = g.res + mc * FB_D + 8 * lg;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 2 * h; p < 2 * h + 2; ++p) {
       rr[2 * p] = *reinterpret_cast<const float4*>(rp + 32 * p);
       rr[2 * p + 1] = *reinterpret_cast<const float4*>(rp + 32 * p + 4);
     }
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
     issue_group(1);
     load_gate(1, hn);
   }
-  if (NG == 1) { load_x1(); load_res(); }
+  if (NG == 1) { load_x1(0); load_x1(1); load_res(0); load_res(1); }
   const int wrow = 8 * (li >> 2) + (li & 3);
   // dz1 stores through a buffer resource (rows past M dropped by its range): exactly 4 a group
   const __amdgpu_buffer_rsrc_t rdz =
@@ -523,8 +525,10 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
         issue_group(grp + 2);
         load_gate(grp + 2, hn);
       }
-      if (grp == (NG > 2 ? NG - 3 : 0)) load_x1();
-      if (grp == NG - 2) load_res();
+      // 256 B a row at each of the last three seams (at NG = 2 all at the one seam)
+      if (grp == (NG > 3 ? NG - 4 : 0)) load_x1(0);
+      if (grp == (NG > 2 ? NG - 3 : 0)) { load_x1(1); load_res(0); }
+      if (grp == NG - 2) load_res(1);
       __syncthreads();                                   // every wave's part of the images landed
     }
     TTMI_TSTAMP(2 + (grp < 4 ? grp : 3));
