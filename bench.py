@@ -137,12 +137,13 @@ def _wgrad_call(kw) -> bool:
 
 def probe_dominant(step, batch, device, iters: int = 20):
     """Roofline of the dominant kernel family, the deterministic weight-gradient GEMMs: the
-    step's 12 nn.Linear weight gradients (five over 25,600 rows, seven over 512), computed as
-    one grouped launch (wgrad_group_kernel) plus one wgrad_fold_kernel that sums the split
-    partials (ttmi_wgrad_batch).  One eager forward+backward records the exact call mix of a
-    step; the mix (inside one deferred_wgrad block, as in the step) is captured into a HIP
-    graph and replayed `iters` times between HIP events on the launch stream, so avg_us =
-    device time of the two launches / 12 GEMMs.
+    step's 13 nn.Linear weight gradients (five over 25,600 rows, eight over 512), computed as
+    one grouped launch (wgrad_group_kernel) whose split partials the step folds inside its
+    AdamW launch (ttmi_wgrad_batch_plan + ttmi_adamw_folded).  One eager forward+backward
+    records the exact call mix of a step; the mix, inside one deferred_wgrad(defer_fold=True)
+    block as in the step, so the replay is the group launch alone, is captured into a HIP graph
+    and replayed `iters` times between HIP events on the launch stream: avg_us = device time of
+    the launch / GEMMs.
     Algorithmic bytes per launch: both bf16 operands once (R x (M + N) x 2) plus the fp32
     gradient tile (M x N x 4)."""
     ops = pkg.ops
@@ -162,7 +163,7 @@ def probe_dominant(step, batch, device, iters: int = 20):
     torch.cuda.synchronize(device)
 
     def mix():
-        with ops.deferred_wgrad():
+        with ops.deferred_wgrad(defer_fold=True):      # GEMMs only: the fold is AdamW's
             for dy, x, gw, gb in calls:
                 orig(dy, x, gw, gb)
 
@@ -189,16 +190,13 @@ def probe_dominant(step, batch, device, iters: int = 20):
     by = sum(R * (M + N) * 2 + M * N * 4 for R, M, N in shapes) / n
     fl = sum(2.0 * M * N * R for R, M, N in shapes) / n
     gbs = by / sec / 1e9
-    # PMC bytes of the family's two launches per step (tools/traffic.py), shared out over the
-    # step's weight-gradient GEMMs like avg_us
-    # (the fold counts only when measured in the same file: since the fold moved into the
-    # AdamW launch no step runs wgrad_fold_kernel, and an older round's figure must not join)
-    src = traffic_file("wgrad_group_kernel")
-    tg, tfold = read_traffic("wgrad_group_kernel"), read_traffic("wgrad_fold_kernel", src)
-    traffic = round((tg + (tfold or 0)) / n) if tg is not None else None
-    return {"kernel": "ttmi_wgrad_batch: the step's 12 weight-gradient GEMMs as one "
-                      "wgrad_group_kernel launch + 1 wgrad_fold_kernel (deterministic split "
-                      "partials), graph-replayed; per-GEMM figures",
+    # PMC bytes of the family's launch per step (tools/traffic.py), shared out over the step's
+    # weight-gradient GEMMs like avg_us
+    tg = read_traffic("wgrad_group_kernel")
+    traffic = round(tg / n) if tg is not None else None
+    return {"kernel": f"ttmi_wgrad_batch_plan: the step's {len(calls)} weight-gradient GEMMs as "
+                      "one wgrad_group_kernel launch (deterministic split partials, folded inside "
+                      "the step's AdamW launch), graph-replayed; per-GEMM figures",
             "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
             "avg_us": round(sec * 1e6, 2), "launches_per_step": len(calls),
@@ -704,7 +702,7 @@ def main_prep(args, world, rank, device):
                        "samples_per_clip": N, "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -781,6 +779,13 @@ def main():
                     help="d_model of both towers (128 = BASELINE cfg 2; 256 = the reference's "
                          "own default, src/train.py:289-297)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--ddp-schedule", action="store_true",
+                    help="run the data-parallel schedule even at --gpus 1: a world-1 process group "
+                         "(TTMI_DIST_BACKEND, default nccl = RCCL) whose collectives all run "
+                         "(comm.force_dp): the per-rank cost of DDP without the wire")
+    ap.add_argument("--no-capture-collectives", action="store_true",
+                    help="data-parallel schedule: collectives between graph segments (host cuts) "
+                         "instead of inside the step's graph")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
@@ -799,9 +804,16 @@ def main():
     # one rank per GPU; ranks beyond the visible GPU count share them (a multi-rank rehearsal
     # on a 1-GPU box, with TTMI_DIST_BACKEND=gloo since RCCL wants distinct devices)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    if world > 1 or args.ddp_schedule:
         torch.cuda.set_device(local)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group(os.environ.get("TTMI_DIST_BACKEND", "nccl"))
+        if args.ddp_schedule:
+            pkg.comm.force_dp(True)
     device = torch.device("cuda", local)
     if args.config == "eval":
         return main_eval(args, world, rank, device)
@@ -822,7 +834,8 @@ def main():
     if world > 1:   # identical replicas, as DDP broadcasts from rank 0
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, 0)
-    step = pkg.TrainStep(model, lr=1e-4, use_graph=not args.no_graph, seed=rank + 1)
+    step = pkg.TrainStep(model, lr=1e-4, use_graph=not args.no_graph, seed=rank + 1,
+                         capture_collectives=False if args.no_capture_collectives else None)
     batches = synthetic_batches(2 if cfg3 else 4, B, seed=rank, device=device)
     if cfg3:
         batches = add_raw_items(batches, rank, device)
@@ -848,6 +861,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     el = time.perf_counter() - t0
+    step.check()                  # an id outside its table in any timed step raises here
     if world > 1:
         t = torch.tensor([el], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -908,7 +922,12 @@ def main():
             "config": {"workload": workload,
                        "global_batch": world * B, "per_gpu_batch": B, "seq_len": L,
                        "vocab": V, "d_model": D, "parallelism": f"dp{world}",
-                       "graph": not args.no_graph},
+                       "graph": not args.no_graph,
+                       "schedule": ("ddp" if step.dp else "single-process") +
+                                   (f" ({dist.get_backend()}, collectives "
+                                    f"{'captured in the step graph' if step.capture_collectives else 'between graph segments'}, "
+                                    f"{step._cur.seg.n_graphs if step._cur.seg else 0} graph(s) per step)"
+                                    if step.dp else "")},
             "roofline": roof,
             "roofline_panel": roof_panel,
             "step_mfma": {"achieved": round(step_tf, 3), "peak": PEAK_BF16_TFLOPS,

@@ -40,15 +40,19 @@ const char* ttmi_last_error(void);
 /* ABI version (bumped on any signature change). */
 int ttmi_abi_version(void);
 
-/* Embedding-id range flags (ABI 20).  The reference's nn.Embedding lookups raise IndexError for
- * an id outside the table (user_tower.py:26,30-31 item / gender / country embeddings,
- * two_tower.py:82-87 callers; the DeBERTa word embedding behind item_tower.py:47; the catalogue
- * index assignment evaluate_metrics.py:102, inference.py:204).  The device entry points that
- * index such a table take `int32_t* id_err` (may be NULL): an id outside [0, rows) never reads
- * or writes outside the table (it is clamped, or its row reads as zero / is skipped, as each
- * call states), and id_err[TTMI_IDERR_<key>] is set to 1 by a plain store (racing writers store
- * the same value).  The flags are never cleared by the library: the host reads them (a
- * host-mapped buffer needs no device sync) and raises IndexError naming the key. */
+/* Embedding-id range flags (ABI 20; block layout ABI 22).  The reference's nn.Embedding lookups
+ * raise IndexError for an id outside the table (user_tower.py:26,30-31 item / gender / country
+ * embeddings, two_tower.py:82-87 callers; the DeBERTa word embedding behind item_tower.py:47; the
+ * catalogue index assignment evaluate_metrics.py:102, inference.py:204).  The device entry
+ * points that index such a table take `int32_t* id_err` (may be NULL): an id outside [0, rows)
+ * never reads or writes outside the table (it is clamped, or its row reads as zero / is skipped,
+ * as each call states), and flag TTMI_IDERR_<key> is set to 1 by plain stores (racing writers
+ * store the same value).  id_err points to a 16-B aligned block in DEVICE memory: int32
+ * flags[8], then at byte 32 an `int32_t*` to a host-mapped int32[8] (may be NULL); both arrays
+ * get the flag (the device one as 0x3F800000, the bit pattern of 1.0f, so that a data-parallel
+ * step can SUM-all-reduce the flags of every rank as floats; the host one as 1).  The library never clears either: the host polls the host-mapped copy (no
+ * device sync) and raises IndexError naming the key; the device copy is what ttmi_adamw*'s
+ * `skip_if` reads (the train step clears it when it stages a batch). */
 enum { TTMI_IDERR_HISTORY = 0, TTMI_IDERR_GENDER = 1, TTMI_IDERR_COUNTRY = 2,
        TTMI_IDERR_TEXT = 3, TTMI_IDERR_CATALOGUE = 4,
        TTMI_IDERR_HEAD_POLL = 7,  /* not an id: ttmi_user_item_head_fwd_ac's stage-C poll timed out
@@ -164,14 +168,19 @@ int ttmi_wgrad_batch_plan(int n, const ttmi_wgrad_desc* const* descs, int nf,
 int ttmi_adamw_folded_skip(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                            const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
                            int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
-                           int64_t skip_off, int64_t skip_len, hipStream_t stream);
+                           int64_t skip_off, int64_t skip_len, const int32_t* skip_if,
+                           hipStream_t stream);
 /* Append src's segments to dst (one update for GEMMs planned early on a side stream and folds
  * planned later); when dst has no room left, src's segments are folded on `stream` instead. */
 int ttmi_fold_plan_merge(ttmi_fold_plan* dst, const ttmi_fold_plan* src, hipStream_t stream);
+/* ABI 22: the plan's folds as ordinary fold launches (ttmi_wgrad_batch's second half): the
+ * data-parallel step plans its GEMMs early (side stream) like the one-process step, but must
+ * complete the gradient before the all-reduce, so it folds the plan itself. */
+int ttmi_fold_plan_run(const ttmi_fold_plan* plan, hipStream_t stream);
 int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                       const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
                       int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
-                      hipStream_t stream);
+                      const int32_t* skip_if, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0) — TransformerEncoderLayer
@@ -603,8 +612,14 @@ int ttmi_avgpool_bwd(int N, int HW, int C, const void* dy, int dy_dtype, const u
  * reading it (optimizer.zero_grad folded into the update).  p_bf16 (optional)
  * receives the bf16 mirror used as GEMM operand by the next step.
  * ---------------------------------------------------------------------------------- */
+/* skip_if (ABI 22, may be NULL): the device half of an id_err block.  When any of its 8 flags is
+ * set, p, m, v and p_bf16 are left untouched (the step whose lookups met an id outside a table
+ * updates nothing, as the reference's nn.Embedding raises before optimizer.step()); g and the
+ * fixed-point accumulators are still cleared.  Same parameter in ttmi_adamw_fx /
+ * ttmi_adamw_folded / ttmi_adamw_folded_skip. */
 int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
-               const double* hyper, const int32_t* step, int zero_grad, hipStream_t stream);
+               const double* hyper, const int32_t* step, int zero_grad, const int32_t* skip_if,
+               hipStream_t stream);
 /* ttmi_adamw where the gradient of elements [fx_off, fx_off + fx_len) is read from an int64
  * fixed-point accumulator fx (value = fx[i - fx_off]·2^-fx_shift; ttmi_seq_embed_bwd's
  * item-embedding rows, ABI 16) instead of g, and fx (not g) is cleared there: the train step
@@ -612,7 +627,8 @@ int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf
  * aligned; fx = NULL is ttmi_adamw. */
 int ttmi_adamw_fx(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                   const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
-                  int64_t fx_off, int64_t fx_len, int fx_shift, hipStream_t stream);
+                  int64_t fx_off, int64_t fx_len, int fx_shift, const int32_t* skip_if,
+                  hipStream_t stream);
 int ttmi_step_inc(int32_t* step, hipStream_t stream);
 
 /* ------------------------------------------------------------------------------------

@@ -10,6 +10,16 @@ support does not cover every collective; the arithmetic and the rank order are t
 * ``all_reduce_sum(t, async_op)`` — in place; returns the work handle when ``async_op``.
 * ``broadcast(t, src)`` — in place.
 
+``force_dp()`` (env ``TTMI_FORCE_DP=1``) makes a world-size-1 process group run the
+data-parallel schedule: every helper then calls the real collective instead of returning early,
+so RCCL itself executes (and can be timed and graph-captured) on a one-GPU box.  At world size 1
+every collective is the identity, so the forced schedule must reproduce the single-process
+step bit for bit (tests/test_gpu_rccl.py).
+
+``capturable(group)``: the backend's collectives can be recorded inside a HIP graph (RCCL can;
+gloo's host-side collectives cannot), so TrainStep captures the whole data-parallel step as one
+graph with the all-reduces as graph nodes on RCCL's stream instead of cutting it into segments.
+
 A staged ``all_reduce_sum(..., async_op=True)`` does not block the caller: an event recorded on
 the current stream orders a device→pinned-host copy on a side stream; one worker thread per
 process waits for that copy and runs the gloo reduction; ``wait()`` joins it and queues the
@@ -40,6 +50,31 @@ def rank(group=None) -> int:
     return dist.get_rank(group) if dist.is_initialized() else 0
 
 
+_FORCE_DP = os.environ.get("TTMI_FORCE_DP", "0") == "1"
+
+
+def force_dp(on: bool = True) -> None:
+    """Run the data-parallel schedule (and its collectives) even at world size 1."""
+    global _FORCE_DP
+    _FORCE_DP = bool(on)
+
+
+def dp_active(group=None) -> bool:
+    """True when the step must run its collectives: a process group of world size > 1, or any
+    initialised group under ``force_dp``."""
+    if not dist.is_initialized():
+        return False
+    return dist.get_world_size(group) > 1 or _FORCE_DP
+
+
+def capturable(group=None) -> bool:
+    """The group's collectives can be recorded in a HIP graph: RCCL (``nccl``) only;
+    ``TTMI_CAPTURE_COLLECTIVES=0`` keeps the segmented schedule (host cuts)."""
+    if not dist.is_initialized() or os.environ.get("TTMI_CAPTURE_COLLECTIVES", "1") == "0":
+        return False
+    return dist.get_backend(group) == "nccl"
+
+
 def _staged(t: Tensor, group) -> bool:
     """True when the collective must run on a host copy of ``t`` (gloo + device tensor)."""
     return t.is_cuda and dist.get_backend(group) == "gloo"
@@ -62,6 +97,9 @@ class _Stager:
         self.pending = []
         self.host = {}
         self.side = {}
+        # set when a staged reduction timed out: its worker thread may still be stuck in it
+        # (and may later write the pinned buffer), so neither is used again
+        self.broken = None
 
     def _executor(self):
         if self.pool is None:
@@ -77,6 +115,7 @@ class _Stager:
         return h.view(t.shape)
 
     def all_reduce(self, t: Tensor, group) -> "_StagedWork":
+        self.check()
         h = self._buffer(t)
         ev = None
         if t.is_cuda:
@@ -101,6 +140,11 @@ class _Stager:
         with self.lock:
             self.pending.append(w)
         return w
+
+    def check(self) -> None:
+        if self.broken is not None:
+            raise RuntimeError(f"comm: a staged gloo all-reduce timed out earlier ({self.broken}); "
+                               "the staging worker is unusable for the rest of this process")
 
     def drain(self) -> None:
         with self.lock:
@@ -148,8 +192,12 @@ class _StagedWork:
     def wait(self) -> bool:
         if self.done:
             return True
+        self.stager.check()
         try:       # re-raises a failed reduction once; it leaves `pending` either way
             self.fut.result(timeout=STAGED_TIMEOUT_S)
+        except concurrent.futures.TimeoutError:
+            self.stager.broken = f"no result after {STAGED_TIMEOUT_S:.0f} s"
+            raise
         finally:
             with self.stager.lock:
                 if self in self.stager.pending:
@@ -172,7 +220,7 @@ def drain() -> None:
 
 def all_gather_into(out: Tensor, inp: Tensor, group=None) -> None:
     drain()
-    if world_size(group) == 1:
+    if not dp_active(group):
         out.copy_(inp)
         return
     if _staged(inp, group):
@@ -185,7 +233,7 @@ def all_gather_into(out: Tensor, inp: Tensor, group=None) -> None:
 
 def reduce_scatter_sum(out: Tensor, inp: Tensor, group=None) -> None:
     drain()
-    if world_size(group) == 1:
+    if not dp_active(group):
         out.copy_(inp)
         return
     if _staged(inp, group):
@@ -197,7 +245,7 @@ def reduce_scatter_sum(out: Tensor, inp: Tensor, group=None) -> None:
 
 
 def all_reduce_sum(t: Tensor, group=None, async_op: bool = False):
-    if world_size(group) == 1:
+    if not dp_active(group):
         return _HostWork() if async_op else None
     if _staged(t, group) or (_FORCE_STAGE and async_op):
         w = _STAGER.all_reduce(t, group)
@@ -215,7 +263,7 @@ _FORCE_STAGE = False
 
 def broadcast(t: Tensor, src: int = 0, group=None) -> None:
     drain()
-    if world_size(group) == 1:
+    if not dp_active(group):
         return
     if _staged(t, group):
         h = t.cpu()
@@ -233,4 +281,4 @@ def group_src(src: int, group=None) -> int:
 
 
 __all__ = ["world_size", "rank", "all_gather_into", "reduce_scatter_sum", "all_reduce_sum",
-           "broadcast", "group_src", "drain"]
+           "broadcast", "group_src", "drain", "force_dp", "dp_active", "capturable"]

@@ -189,12 +189,16 @@ TTMI_DEV AdamScalars adam_scalars(const double* hyper, const int32_t* step) {
   a.eps = (float)hyper[3];
   return a;
 }
+// Contraction off, fma spelled out: hipcc may contract a*b + c differently in two kernels, and
+// adamw_kernel / adamw_fold_kernel (one-process fold-in-update vs the data-parallel plain
+// update) must produce the same bits from the same gradient.
 TTMI_DEV void adam_upd(const AdamScalars& a, float& P, float G, float& Mv, float& Vv) {
-  P *= a.decay;
-  Mv += a.b1c * (G - Mv);                         // exp_avg.lerp_(grad, 1-beta1)
-  Vv = Vv * a.b2 + a.b2c * (G * G);               // exp_avg_sq.mul_(b2).addcmul_(g,g,1-b2)
+#pragma clang fp contract(off)
+  P = P * a.decay;
+  Mv = fmaf(a.b1c, G - Mv, Mv);                   // exp_avg.lerp_(grad, 1-beta1)
+  Vv = fmaf(Vv, a.b2, a.b2c * (G * G));           // exp_avg_sq.mul_(b2).addcmul_(g,g,1-b2)
   const float denom = sqrtf(Vv) / a.bc2_sqrt + a.eps;
-  P -= a.step_size * (Mv / denom);
+  P = fmaf(-a.step_size, Mv / denom, P);
 }
 
 // ---------------------------------------------------------------- XCD-aware block order
@@ -323,14 +327,32 @@ static __device__ uint64_t ttmi_stamps[TTMI_STAMP_BLOCKS * TTMI_STAMP_WAVES * TT
 #define TTMI_STAMP_DUMP(tu)
 #endif
 
-// ---------------------------------------------------------------- embedding-id range (ABI 20)
+// ---------------------------------------------------------------- embedding-id range (ABI 22)
 // nn.Embedding raises on an id outside its table; the device lookups clamp it into [0, n)
-// (no out-of-bounds access) and raise flag k of the caller's id_err array (include/ttmi.h
-// TTMI_IDERR_*) with a plain store: every writer stores the same 1, so no atomic is needed.
+// (no out-of-bounds access) and raise flag k of the caller's id_err block (include/ttmi.h
+// TTMI_IDERR_*) with plain vector stores: every writer stores the same value, so no atomic is
+// needed.  The block is int32 flags[8] in device memory (what AdamW's skip_if reads) followed, at
+// byte 32, by an optional pointer to the host-mapped int32[8] the host polls; both get the flag.
+// The device flag is stored as the bit pattern of 1.0f (TTMI_IDERR_RAISED): a data-parallel step
+// can then sum every rank's flags in its fp32 gradient all-reduce and skip on all ranks at once.
+#define TTMI_IDERR_RAISED 0x3F800000
+TTMI_DEV void raise_id_err(int32_t* id_err, int k) {
+  if (!id_err) return;
+  id_err[k] = TTMI_IDERR_RAISED;
+  int32_t* host = *reinterpret_cast<int32_t* const*>(id_err + 8);
+  if (host) host[k] = 1;
+}
 TTMI_DEV int64_t clamp_id(int64_t id, int64_t n, int32_t* id_err, int k) {
   const bool bad = (uint64_t)id >= (uint64_t)n;
-  if (bad && id_err) id_err[k] = 1;
+  if (bad) raise_id_err(id_err, k);
   return bad ? (id < 0 ? 0 : n - 1) : id;
+}
+// AdamW's bad-step skip (ABI 22): any raised flag of the block's device half.
+TTMI_DEV bool id_err_raised(const int32_t* skip_if) {
+  if (!skip_if) return false;
+  const int4 a = reinterpret_cast<const int4*>(skip_if)[0];
+  const int4 b = reinterpret_cast<const int4*>(skip_if)[1];
+  return ((a.x | a.y | a.z | a.w) | (b.x | b.y | b.z | b.w)) != 0;
 }
 
 // ---------------------------------------------------------------- host-side error plumbing

@@ -1806,6 +1806,7 @@ struct AdamFoldArgs {
   float* p; float* g; float* m; float* v; bf16_t* pb;
   const double* hyper; const int32_t* step;
   int64_t* fx; int64_t fx_lo, fx_hi; int fx_shift, zero_grad;
+  const int32_t* skip_if;                       // ABI 22: bad-id step, no update
   int nplain, nseg;
   int blk_begin[AF_PLAIN + AF_SEGS + 1];
   int plo[AF_PLAIN], phi[AF_PLAIN];             // float4 units
@@ -1826,6 +1827,7 @@ __global__ __launch_bounds__(256) void adamw_fold_kernel(AdamFoldArgs a) {
   bf16_t* __restrict__ pb = ka->pb;
   const int zero_grad = ka->zero_grad;
   const AdamScalars as = adam_scalars(ka->hyper, ka->step);
+  const bool keep = !id_err_raised(ka->skip_if);
   auto upd4 = [&](int64_t q, float4 gg) {
     float4 pp = reinterpret_cast<const float4*>(p)[q];
     float4 mm = reinterpret_cast<const float4*>(mo)[q];
@@ -1834,6 +1836,7 @@ __global__ __launch_bounds__(256) void adamw_fold_kernel(AdamFoldArgs a) {
     adam_upd(as, pp.y, gg.y, mm.y, vv.y);
     adam_upd(as, pp.z, gg.z, mm.z, vv.z);
     adam_upd(as, pp.w, gg.w, mm.w, vv.w);
+    if (!keep) return;
     reinterpret_cast<float4*>(p)[q] = pp;
     reinterpret_cast<float4*>(mo)[q] = mm;
     reinterpret_cast<float4*>(vo)[q] = vv;
@@ -1895,8 +1898,10 @@ __global__ __launch_bounds__(256) void adamw_fold_kernel(AdamFoldArgs a) {
     const int64_t e = rp - g;
     float P = p[e], Mv = mo[e], Vv = vo[e];
     adam_upd(as, P, v, Mv, Vv);
-    p[e] = P; mo[e] = Mv; vo[e] = Vv;
-    if (pb) pb[e] = f2bf(P);
+    if (keep) {
+      p[e] = P; mo[e] = Mv; vo[e] = Vv;
+      if (pb) pb[e] = f2bf(P);
+    }
     if (zero_grad) *rp = 0.f;
   };
   fold_segment(sg, bx, nbx, store4, store1);
@@ -3021,6 +3026,12 @@ extern "C" int ttmi_wgrad_batch_plan(int n, const ttmi_wgrad_desc* const* descs,
   return TTMI_OK;
 }
 
+extern "C" int ttmi_fold_plan_run(const ttmi_fold_plan* plan, hipStream_t stream) {
+  TTMI_REQUIRE(plan && plan->n >= 0 && plan->n <= AF_SEGS, "ttmi_fold_plan_run: bad plan");
+  if (plan->n == 0) return TTMI_OK;
+  return launch_fold_segs(reinterpret_cast<const FoldSeg*>(plan->seg), plan->n, stream);
+}
+
 extern "C" int ttmi_fold_plan_merge(ttmi_fold_plan* dst, const ttmi_fold_plan* src, hipStream_t stream) {
   TTMI_REQUIRE(dst && src && dst->n >= 0 && dst->n <= AF_SEGS && src->n >= 0 && src->n <= AF_SEGS,
                "ttmi_fold_plan_merge: bad plan");
@@ -3034,15 +3045,16 @@ extern "C" int ttmi_fold_plan_merge(ttmi_fold_plan* dst, const ttmi_fold_plan* s
 extern "C" int ttmi_adamw_folded(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                                  const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
                                  int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
-                                 hipStream_t s) {
+                                 const int32_t* skip_if, hipStream_t s) {
   return ttmi_adamw_folded_skip(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift,
-                                plan, 0, 0, s);
+                                plan, 0, 0, skip_if, s);
 }
 
 extern "C" int ttmi_adamw_folded_skip(int64_t n, float* p, float* g, float* m, float* v, uint16_t* p_bf16,
                                       const double* hyper, const int32_t* step, int zero_grad, int64_t* fx,
                                       int64_t fx_off, int64_t fx_len, int fx_shift, const ttmi_fold_plan* plan,
-                                      int64_t skip_off, int64_t skip_len, hipStream_t s) {
+                                      int64_t skip_off, int64_t skip_len, const int32_t* skip_if,
+                                      hipStream_t s) {
   TTMI_REQUIRE(skip_len == 0 || (!fx && skip_off >= 0 && skip_len > 0 && skip_off % 4 == 0 && skip_len % 4 == 0 &&
                                  skip_off + skip_len <= n),
                "ttmi_adamw_folded_skip: the skipped range must be float4-aligned, inside [0, n), without fx");
@@ -3050,12 +3062,13 @@ extern "C" int ttmi_adamw_folded_skip(int64_t n, float* p, float* g, float* m, f
     int rc = plan && plan->n > 0 ? launch_fold_segs(reinterpret_cast<const FoldSeg*>(plan->seg), plan->n, s) : 0;
     if (rc) return rc;
     const int64_t e = skip_off + skip_len;
-    rc = ttmi_adamw(skip_off, p, g, m, v, p_bf16, hyper, step, zero_grad, s);
+    rc = ttmi_adamw(skip_off, p, g, m, v, p_bf16, hyper, step, zero_grad, skip_if, s);
     if (rc) return rc;
-    return ttmi_adamw(n - e, p + e, g + e, m + e, v + e, p_bf16 ? p_bf16 + e : nullptr, hyper, step, zero_grad, s);
+    return ttmi_adamw(n - e, p + e, g + e, m + e, v + e, p_bf16 ? p_bf16 + e : nullptr, hyper, step, zero_grad,
+                      skip_if, s);
   }
   if (!plan || plan->n <= 0)
-    return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, s);
+    return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, skip_if, s);
   TTMI_REQUIRE(plan->n <= AF_SEGS, "ttmi_adamw_folded: bad plan");
   const FoldSeg* segs = reinterpret_cast<const FoldSeg*>(plan->seg);
   // the flat ranges the segments update (float4 units), which the plain jobs then skip
@@ -3101,17 +3114,17 @@ extern "C" int ttmi_adamw_folded_skip(int64_t n, float* p, float* g, float* m, f
     if (rc) return rc;
     if (skip_len > 0) {
       const int64_t e = skip_off + skip_len;
-      rc = ttmi_adamw(skip_off, p, g, m, v, p_bf16, hyper, step, zero_grad, s);
+      rc = ttmi_adamw(skip_off, p, g, m, v, p_bf16, hyper, step, zero_grad, skip_if, s);
       if (rc) return rc;
       return ttmi_adamw(n - e, p + e, g + e, m + e, v + e, p_bf16 ? p_bf16 + e : nullptr, hyper, step,
-                        zero_grad, s);
+                        zero_grad, skip_if, s);
     }
-    return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, s);
+    return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, fx, fx_off, fx_len, fx_shift, skip_if, s);
   }
   TTMI_REQUIRE(((uintptr_t)p & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0 &&
                ((uintptr_t)p_bf16 & 7) == 0, "ttmi_adamw_folded: buffers must be 16-B aligned (bf16 mirror 8-B)");
   a.p = p; a.g = g; a.m = m; a.v = v; a.pb = (bf16_t*)p_bf16;
-  a.hyper = hyper; a.step = step; a.zero_grad = zero_grad;
+  a.hyper = hyper; a.step = step; a.zero_grad = zero_grad; a.skip_if = skip_if;
   a.fx = fx; a.fx_lo = fx ? fx_off / 4 : 0; a.fx_hi = fx ? (fx_off + fx_len) / 4 : 0; a.fx_shift = fx_shift;
   a.nseg = plan->n;
   int nb = 0;

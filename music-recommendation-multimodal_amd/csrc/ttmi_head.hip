@@ -464,7 +464,7 @@ TTMI_DEV void item_c_body(const ItemArgs& a, int bx, ItemLdsCT<D_>& L) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > (1 << 22)) {
           __hip_atomic_store(a.bncnt + BN_CDONE + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (a.err) a.err[TTMI_IDERR_HEAD_POLL] = 1;      // the host raises (ops.check_id_errors)
+          raise_id_err(a.err, TTMI_IDERR_HEAD_POLL);      // the host raises (ops.check_id_errors)
           break;
         }
       }

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_kernel(
     const int l = (int)(row % L);
     const int64_t id = ids[row];
     const bool ok = id >= 0 && id < V;      // an id outside the table reads a zero row and flags
-    if (!ok && id_err) id_err[TTMI_IDERR_HISTORY] = 1;
+    if (!ok) raise_id_err(id_err, TTMI_IDERR_HISTORY);
     float v[NV];
     float s = 0.f;
 #pragma unroll
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_vec_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool ok = id[u] >= 0 && id[u] < V;   // outside the table: a zero row, flagged
-      if (!ok && id_err) id_err[TTMI_IDERR_HISTORY] = 1;
+      if (!ok) raise_id_err(id_err, TTMI_IDERR_HISTORY);
       const int l = (int)(min(row[u], M - 1) % L);
       e[u] = reinterpret_cast<const float4*>(E + (ok ? id[u] : 0) * D)[j];
       if (!ok) e[u] = make_float4(0.f, 0.f, 0.f, 0.f);

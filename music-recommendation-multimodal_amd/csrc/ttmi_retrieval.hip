@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void catalogue_rows_kernel(int n, int D, const
   if (r >= n) return;
   const int64_t id = ids[r];
   if (id < 0 || id >= V) {                 // skipped; the host raises IndexError (ABI 20)
-    if (id_err) id_err[TTMI_IDERR_CATALOGUE] = 1;
+    raise_id_err(id_err, TTMI_IDERR_CATALOGUE);
     return;
   }
   const float* xr = x + (int64_t)r * ldx;

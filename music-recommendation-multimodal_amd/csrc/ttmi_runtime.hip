@@ -26,7 +26,7 @@ int ttmi_check_launch(const char* what) {
 
 extern "C" const char* ttmi_last_error(void) { return g_err; }
 
-extern "C" int ttmi_abi_version(void) { return 21; }
+extern "C" int ttmi_abi_version(void) { return 22; }
 
 namespace {
 
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
                                                     bf16_t* __restrict__ pb, const double* __restrict__ hyper,
                                                     const int32_t* __restrict__ step, int zero_grad,
                                                     int64_t* __restrict__ fx, int64_t fx_lo, int64_t fx_hi,
-                                                    int fx_shift) {
+                                                    int fx_shift, const int32_t* __restrict__ skip_if) {
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n4 = n / 4;
@@ -81,6 +81,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
     }
   }
   const AdamScalars as = adam_scalars(hyper, step);
+  // a step whose lookups met an id outside a table leaves p, m, v untouched (skip_if, ABI 22);
+  // its gradient is still cleared
+  const bool keep = !id_err_raised(skip_if);
   auto upd = [&](float& P, float G, float& Mv, float& Vv) { adam_upd(as, P, G, Mv, Vv); };
 #pragma unroll
   for (int u = 0; u < ADAM_U; ++u) {
@@ -90,16 +93,18 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
     upd(pp[u].y, gg[u].y, mm[u].y, vv[u].y);
     upd(pp[u].z, gg[u].z, mm[u].z, vv[u].z);
     upd(pp[u].w, gg[u].w, mm[u].w, vv[u].w);
-    reinterpret_cast<float4*>(p)[q] = pp[u];
-    reinterpret_cast<float4*>(m)[q] = mm[u];
-    reinterpret_cast<float4*>(v)[q] = vv[u];
+    if (keep) {
+      reinterpret_cast<float4*>(p)[q] = pp[u];
+      reinterpret_cast<float4*>(m)[q] = mm[u];
+      reinterpret_cast<float4*>(v)[q] = vv[u];
+    }
     if (fx != nullptr && q >= fx_lo && q < fx_hi) {
       reinterpret_cast<longlong2*>(fx)[2 * (q - fx_lo)] = make_longlong2(0, 0);
       reinterpret_cast<longlong2*>(fx)[2 * (q - fx_lo) + 1] = make_longlong2(0, 0);
     } else if (zero_grad) {
       reinterpret_cast<float4*>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (pb) {
+    if (pb && keep) {
       ushort4 o;
       o.x = f2bf(pp[u].x); o.y = f2bf(pp[u].y); o.z = f2bf(pp[u].z); o.w = f2bf(pp[u].w);
       reinterpret_cast<ushort4*>(pb)[q] = o;
@@ -109,9 +114,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
     for (int64_t j = 4 * n4; j < n; ++j) {
       float pj = p[j], mj = m[j], vj = v[j];
       upd(pj, g[j], mj, vj);
-      p[j] = pj; m[j] = mj; v[j] = vj;
+      if (keep) {
+        p[j] = pj; m[j] = mj; v[j] = vj;
+        if (pb) pb[j] = f2bf(pj);
+      }
       if (zero_grad) g[j] = 0.f;
-      if (pb) pb[j] = f2bf(pj);
     }
   }
 }
@@ -336,7 +343,7 @@ extern "C" int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hi
 extern "C" int ttmi_adamw_fx(int64_t n, float* p, float* g, float* m, float* v,
                              uint16_t* p_bf16, const double* hyper, const int32_t* step,
                              int zero_grad, int64_t* fx, int64_t fx_off, int64_t fx_len,
-                             int fx_shift, hipStream_t s) {
+                             int fx_shift, const int32_t* skip_if, hipStream_t s) {
   TTMI_REQUIRE(n >= 0 && p && g && m && v && hyper && step, "ttmi_adamw: null argument");
   TTMI_REQUIRE(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 &&
                ((uintptr_t)v & 15) == 0 && ((uintptr_t)p_bf16 & 7) == 0,
@@ -350,14 +357,14 @@ extern "C" int ttmi_adamw_fx(int64_t n, float* p, float* g, float* m, float* v,
   const int blocks = (int)std::max<int64_t>((groups + 256 * ADAM_U - 1) / (256 * ADAM_U), 1);
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, n, p, g, m, v, (bf16_t*)p_bf16,
                      hyper, step, zero_grad, fx, fx ? fx_off / 4 : 0, fx ? (fx_off + fx_len) / 4 : 0,
-                     fx_shift);
+                     fx_shift, skip_if);
   return ttmi_check_launch("ttmi_adamw");
 }
 
 extern "C" int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v,
                           uint16_t* p_bf16, const double* hyper, const int32_t* step,
-                          int zero_grad, hipStream_t s) {
-  return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, nullptr, 0, 0, 0, s);
+                          int zero_grad, const int32_t* skip_if, hipStream_t s) {
+  return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, nullptr, 0, 0, 0, skip_if, s);
 }
 
 extern "C" int ttmi_batch_copy(int n, void* const* dst, const void* const* src,

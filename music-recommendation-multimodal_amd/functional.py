@@ -975,6 +975,7 @@ class GlobalLossSaved:
     dI: Optional[Tensor] = None
     rs_u: Optional[Tensor] = None     # this rank's share of the key grads (reduce-scattered)
     rs_i: Optional[Tensor] = None
+    dp: bool = False                  # the collectives run (world > 1, or comm.force_dp)
 
 
 def _world_rank(group, local: bool):
@@ -989,6 +990,7 @@ def infonce_global_prep(u: Tensor, it: Tensor, user_idx: Optional[Tensor], tempe
     """Phase 1 of the cfg-5 loss: L2-normalise this rank's rows and size the gathered buffers
     (no collective; TrainStep captures it in the forward graph)."""
     world, rank = _world_rank(group, local)
+    dp = not local and comm.dp_active(group)
     B, D = u.shape
     dev = u.device
     f32 = dict(device=dev, dtype=torch.float32)
@@ -1000,18 +1002,18 @@ def infonce_global_prep(u: Tensor, it: Tensor, user_idx: Optional[Tensor], tempe
     if user_idx is not None:
         uid = user_idx if user_idx.dtype == torch.int64 else user_idx.to(torch.int64)
         uid = uid.contiguous()
-    if world > 1:
+    if dp:
         U, I = torch.empty(world * B, D, **f32), torch.empty(world * B, D, **f32)
         UID = torch.empty(world * B, device=dev, dtype=torch.int64) if uid is not None else None
     else:
         U, I, UID = u_hat, i_hat, uid
     return GlobalLossSaved(u_hat, i_hat, nu, ni, U, I, uid, UID, rank * B, world,
-                           1.0 / temperature)
+                           1.0 / temperature, dp=dp)
 
 
 def infonce_global_gather(st: GlobalLossSaved, group=None) -> None:
     """Phase 2 (collective): all-gather û, î and user_idx over the group (RCCL)."""
-    if st.world == 1:
+    if not st.dp:
         return
     comm.all_gather_into(st.U, st.u_hat, group)
     comm.all_gather_into(st.I, st.i_hat, group)
@@ -1045,7 +1047,7 @@ def infonce_global_loss_bwd(st: GlobalLossSaved, dloss: Optional[Tensor]) -> Non
                   dloss, scale, st.duh, st.dI)
     ops.rowce_bwd(st.i_hat, st.U, st.s_i2u, st.lse_i2u, st.uid, st.UID, st.row0, st.inv_tau,
                   dloss, scale, st.dih, st.dU)
-    if st.world > 1:
+    if st.dp:
         st.rs_u, st.rs_i = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
     else:
         st.rs_u, st.rs_i = st.dU, st.dI
@@ -1053,7 +1055,7 @@ def infonce_global_loss_bwd(st: GlobalLossSaved, dloss: Optional[Tensor]) -> Non
 
 def infonce_global_scatter(st: GlobalLossSaved, group=None) -> None:
     """Phase 5 (collective): reduce-scatter (SUM) of the key grads back to their owners."""
-    if st.world == 1:
+    if not st.dp:
         return
     comm.reduce_scatter_sum(st.rs_u, st.dU, group)
     comm.reduce_scatter_sum(st.rs_i, st.dI, group)

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libttmi.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 c_i, c_i64, c_u64, c_f, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                ctypes.c_void_p)
@@ -250,10 +250,11 @@ SIGNATURES = {
     "ttmi_wgrad_batch_plan": (c_i, [c_i, ctypes.POINTER(ctypes.POINTER(WgradDesc)), c_i,
                                     ctypes.POINTER(FoldDesc), ctypes.POINTER(FoldPlan), c_p]),
     "ttmi_adamw_folded_skip": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
-                                     ctypes.POINTER(FoldPlan), c_i64, c_i64, c_p]),
+                                     ctypes.POINTER(FoldPlan), c_i64, c_i64, c_p, c_p]),
     "ttmi_fold_plan_merge": (c_i, [ctypes.POINTER(FoldPlan), ctypes.POINTER(FoldPlan), c_p]),
+    "ttmi_fold_plan_run": (c_i, [ctypes.POINTER(FoldPlan), c_p]),
     "ttmi_adamw_folded": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
-                                ctypes.POINTER(FoldPlan), c_p]),
+                                ctypes.POINTER(FoldPlan), c_p, c_p]),
     "ttmi_layernorm_fwd": (c_i, [c_i64, c_i, c_p, c_i64, c_p, c_p, c_f, c_i, c_f, c_p, c_p, c_i,
                                  c_i64, c_p, c_p, c_p]),
     "ttmi_layernorm_bwd_workspace": (c_i64, [c_i]),
@@ -299,9 +300,9 @@ SIGNATURES = {
     "ttmi_infonce_bwd_fused": (c_i, [c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p,
                                      c_p, c_p]),
     "ttmi_infonce_bwd_counter_bytes": (ctypes.c_int64, [c_i]),
-    "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p]),
+    "ttmi_adamw": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_p]),
     "ttmi_adamw_fx": (c_i, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_p, c_i64, c_i64, c_i,
-                            c_p]),
+                            c_p, c_p]),
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch_seeds": (c_i, [c_i, c_p, c_p, c_p, c_p, c_u64, c_p, c_p, c_i, c_i, c_p]),

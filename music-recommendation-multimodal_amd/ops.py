@@ -9,6 +9,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
+import warnings
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -51,25 +52,54 @@ def _dev(*ts):
 # The reference's nn.Embedding lookups raise IndexError for an id outside the table
 # (user_tower.py:26,30-31; the DeBERTa word embedding; the catalogue assignment
 # evaluate_metrics.py:102).  The device lookups never index outside a table (include/ttmi.h
-# TTMI_IDERR_*): they clamp / skip and set a flag.  The flags live in host-mapped memory
-# (hipHostMalloc, mapped + coherent), so reading them needs no device sync and costs the step
-# nothing: check_id_errors() raises once the flagging launch has run (the next step / forward,
-# or any point after a sync).
+# TTMI_IDERR_*): they clamp / skip and set a flag in two places (ABI 22): a device int32[8] that
+# the fused AdamW reads (``skip_if``: a step that met a bad id updates no parameter, as the
+# reference raises before optimizer.step()) and that TrainStep clears when it stages a batch; and
+# a host-mapped int32[8] (hipHostMalloc, mapped + coherent), so reading them needs no device
+# sync and costs the step nothing: check_id_errors() raises once the flagging launch has run
+# (the next step / forward, or any point after a sync).
 ID_ERR_KEYS = ("history_ids", "user_gender", "user_country", "target_input_ids", "target_id")
 _IDERR_HEAD_POLL = 7        # TTMI_IDERR_HEAD_POLL: not an id, the co-launched head's poll timed out
 _N_IDERR = 8
 
 
+def _hip_runtime():
+    """The HIP runtime torch has loaded (found in this process's mappings, whatever its soname
+    version), opened without loading a second copy; None if there is none."""
+    paths = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                i = line.find("/")
+                if i >= 0 and "libamdhip64.so" in line[i:]:
+                    paths.append(line[i:].strip())
+    except OSError:
+        pass
+    for name in dict.fromkeys(paths + ["libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"]):
+        try:
+            return ctypes.CDLL(name, mode=os.RTLD_NOLOAD)
+        except OSError:
+            continue
+    return None
+
+
+_WARNED_NO_HOST_MAP = [False]
+
+
 class _IdFlags:
-    """int32[8] flags of one device: host-mapped (``host`` reads them, ``dptr`` is what the
-    kernels get), or, if the runtime refuses the mapping, a device tensor read on sync only."""
+    """The id_err block of one device (include/ttmi.h, ABI 22): ``dev`` int32[16] on the device —
+    flags [0, 8) and, at byte 32, the device address of the host-mapped int32[8] ``host`` — and
+    ``dptr`` (what the kernels get).  If the runtime refuses the host mapping, the pointer slot
+    stays NULL and the device flags are read on sync only (warned once).  The 32-byte pinned
+    block lives as long as the process (one per device; never freed)."""
 
     def __init__(self, device: torch.device):
         self.host = None
-        self.dev = None
-        self.dptr = None
-        try:
-            hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD)   # torch's runtime
+        self.dev = torch.zeros(16, dtype=torch.int32, device=device)
+        self.zeros = torch.zeros(_N_IDERR, dtype=torch.int32, device=device)
+        self.dptr = self.dev.data_ptr()
+        hip = _hip_runtime()
+        if hip is not None:
             ptr, dptr = ctypes.c_void_p(), ctypes.c_void_p()
             flags = 0x1 | 0x2 | 0x40000000      # hipHostMallocPortable | Mapped | Coherent
             with torch.cuda.device(device):
@@ -79,24 +109,25 @@ class _IdFlags:
                     self.host = (ctypes.c_int32 * _N_IDERR).from_address(ptr.value)
                     for i in range(_N_IDERR):
                         self.host[i] = 0
-                    self.dptr = dptr.value
-        except OSError:
-            pass
-        if self.host is None:
-            self.dev = torch.zeros(_N_IDERR, dtype=torch.int32, device=device)
-            self.dptr = self.dev.data_ptr()
+                    self.dev.view(torch.int64)[4] = dptr.value
+        if self.host is None and not _WARNED_NO_HOST_MAP[0]:
+            _WARNED_NO_HOST_MAP[0] = True
+            warnings.warn("libttmi: no host-mapped id-range flags (HIP runtime not found or the "
+                          "mapping was refused); out-of-table ids are reported only by "
+                          "check_id_errors(sync=True) / TrainStep.check()", RuntimeWarning)
 
     def take(self, sync: bool) -> List[int]:
-        """Indices of the raised flags (cleared)."""
+        """Indices of the raised flags (cleared).  A flag raised again between the read and the
+        clear is lost, which only drops a duplicate report: the caller raises for the first."""
         if self.host is not None:
             vals = list(self.host)
             for i, v in enumerate(vals):
                 if v:
                     self.host[i] = 0
         elif sync:
-            vals = self.dev.tolist()
+            vals = self.dev[:_N_IDERR].tolist()
             if any(vals):
-                self.dev.zero_()
+                self.dev[:_N_IDERR].zero_()
         else:
             return []
         return [i for i, v in enumerate(vals) if v]
@@ -105,13 +136,35 @@ class _IdFlags:
 _IDF: Dict[int, _IdFlags] = {}
 
 
-def id_err_ptr(t: Tensor) -> int:
-    """Device pointer of the id range flags of ``t``'s device (allocated on first use)."""
+def _id_flags(t: Tensor) -> _IdFlags:
     idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
     f = _IDF.get(idx)
     if f is None:
+        if torch.cuda.is_current_stream_capturing():
+            # the block's zero fill and pointer write would be recorded, not run
+            raise RuntimeError("libttmi: the id-range flag block is first needed inside a graph "
+                               "capture; run the captured ops once eagerly first (a warm-up)")
         f = _IDF[idx] = _IdFlags(torch.device("cuda", idx))
-    return f.dptr
+    return f
+
+
+def id_err_ptr(t: Tensor) -> int:
+    """Device pointer of the id_err block of ``t``'s device (allocated on first use); also
+    AdamW's ``skip_if``."""
+    return _id_flags(t).dptr
+
+
+def id_err_flags(t: Tensor) -> Tensor:
+    """The device half of the id_err block of ``t``'s device: int32[8], a raised flag holds the
+    bit pattern of 1.0f (include/ttmi.h)."""
+    return _id_flags(t).dev[:_N_IDERR]
+
+
+def id_err_step_reset(t: Tensor):
+    """(dst, src) for batch_copy: zeroes the device flags of ``t``'s device (the per-step half
+    that AdamW's skip_if reads; TrainStep does this in its staging launch)."""
+    f = _id_flags(t)
+    return f.dev[:_N_IDERR], f.zeros
 
 
 def check_id_errors(sync: bool = False) -> None:
@@ -211,6 +264,7 @@ class WgradPending:
         self.plan = None
         self.keep: list = []
         self.side = None          # launch_early's stream, joined by flush()
+        self.side_flushed = None  # flush_on's stream, joined by join()
         self.hold_join = False    # flush() leaves the join to the caller (join())
 
     def slot(self, key: str) -> int:
@@ -234,16 +288,39 @@ class WgradPending:
         with torch.cuda.stream(side):
             call("ttmi_wgrad_batch_plan", len(self.items), arr, 0, (FoldDesc * 1)(),
                  ctypes.byref(self.plan), _s())
-        self.keep = self.items
+        self.keep = self.keep + self.items
         self.items = []
         self.side = side
         return True
 
     def join(self) -> None:
-        """The current stream waits for launch_early's GEMMs (no-op when none ran)."""
-        if self.side is not None:
-            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
-            self.side = None
+        """The current stream waits for launch_early's GEMMs and flush_on's work (no-op when
+        neither ran)."""
+        for st in (self.side, self.side_flushed):
+            if st is not None:
+                torch.cuda.current_stream(st.device).wait_stream(st)
+        self.side = None
+        self.side_flushed = None
+
+    def flush_on(self, side: "torch.cuda.Stream") -> None:
+        """Complete every weight gradient and fold recorded so far on ``side`` (after the current
+        stream's work): the data-parallel step's first bucket, whose all-reduce then follows on
+        ``side`` while the current stream goes on with the rest of the backward.  Operands are
+        kept alive until join()."""
+        if self.side is not None or self.plan is not None:
+            raise RuntimeError("WgradPending.flush_on: after launch_early")
+        side.wait_stream(torch.cuda.current_stream(side.device))
+        with torch.cuda.stream(side):
+            if self.items or self.folds:
+                arr = (ctypes.POINTER(WgradDesc) * max(len(self.items), 1))(
+                    *[ctypes.pointer(d) for d, *_ in self.items])
+                farr = (FoldDesc * max(len(self.folds), 1))(*[f for f, *_ in self.folds])
+                call("ttmi_wgrad_batch", len(self.items), arr, len(self.folds), farr, _s())
+        self.keep = self.keep + self.items + self.folds
+        self.items = []
+        self.folds = []
+        self.slots = {}
+        self.side_flushed = side
 
     def flush(self) -> None:
         if self.side is not None:         # launch_early ran: plan the folds, join the GEMMs
@@ -270,7 +347,7 @@ class WgradPending:
             self.plan = _L.FoldPlan()
             call("ttmi_wgrad_batch_plan", len(self.items), arr, len(self.folds), farr,
                  ctypes.byref(self.plan), _s())
-            self.keep = self.items + self.folds
+            self.keep = self.keep + self.items + self.folds
         else:
             call("ttmi_wgrad_batch", len(self.items), arr, len(self.folds), farr, _s())
         self.items = []
@@ -300,6 +377,21 @@ _WG_SIDE: Dict[str, "torch.cuda.Stream"] = {}
 _WG_EARLY = os.environ.get("TTMI_WGRAD_EARLY", "1") != "0"
 
 
+def wgrad_side_stream(dev) -> "torch.cuda.Stream":
+    """The per-device side stream of the weight-gradient GEMMs (created on first use, i.e. in an
+    eager step before any graph capture)."""
+    key = str(dev)
+    if key not in _WG_SIDE:
+        _WG_SIDE[key] = torch.cuda.Stream(dev)
+    return _WG_SIDE[key]
+
+
+def fold_plan_run(plan) -> None:
+    """Fold a WgradPending plan's segments now (ttmi_fold_plan_run): the data-parallel step
+    completes its gradient before the all-reduce instead of folding inside AdamW."""
+    call("ttmi_fold_plan_run", ctypes.byref(plan), _s())
+
+
 def wgrad_launch_early() -> bool:
     """Inside ``deferred_wgrad(defer_fold=True)``: launch the weight-gradient GEMMs recorded so
     far on a side stream (created per device on first use, i.e. in an eager step before any
@@ -310,11 +402,7 @@ def wgrad_launch_early() -> bool:
     pend = _PENDING[-1]
     if not pend.defer_fold or not pend.items:
         return False
-    dev = pend.items[0][2].device
-    key = str(dev)
-    if key not in _WG_SIDE:
-        _WG_SIDE[key] = torch.cuda.Stream(dev)
-    return pend.launch_early(_WG_SIDE[key])
+    return pend.launch_early(wgrad_side_stream(pend.items[0][2].device))
 
 
 def linear_dw(dy: Tensor, x: Tensor, gw: Tensor, gb: Optional[Tensor] = None,
@@ -1194,7 +1282,8 @@ def bump_param_epoch() -> None:
 
 
 def adamw_fx_range(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
-                   step: Tensor, fx: Tuple[Tensor, Tensor], zero_grad: bool = False) -> Tuple[int, int]:
+                   step: Tensor, fx: Tuple[Tensor, Tensor], zero_grad: bool = False,
+                   skip_if: Optional[int] = None) -> Tuple[int, int]:
     """AdamW over the flat slot ``fx[1]`` alone, its gradient read from (and cleared in) the
     fixed-point accumulator ``fx[0]`` (ttmi_adamw_fx on the slot's sub-range); returns the slot's
     (offset, length) for adamw(skip=...)."""
@@ -1205,26 +1294,28 @@ def adamw_fx_range(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[
     e = 4 * off
     call("ttmi_adamw_fx", cnt, p.data_ptr() + e, g.data_ptr() + e, m.data_ptr() + e, v.data_ptr() + e,
          (p_bf16.data_ptr() + 2 * off) if p_bf16 is not None else None, _p(hyper), _p(step),
-         int(zero_grad), _p(acc), 0, cnt, FX_GRAD_SHIFT, _s())
+         int(zero_grad), _p(acc), 0, cnt, FX_GRAD_SHIFT, skip_if, _s())
     return off, cnt
 
 
 def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], hyper: Tensor,
           step: Tensor, zero_grad: bool = False,
           fx: Optional[Tuple[Tensor, Tensor]] = None, fold_plan=None,
-          skip: Optional[Tuple[int, int]] = None):
+          skip: Optional[Tuple[int, int]] = None, skip_if: Optional[int] = None):
     """Fused AdamW over flat buffers.  ``fx`` = (acc, grad_view): the gradient of the slot
     ``grad_view`` (a view into ``g``) is still in the int64 fixed-point accumulator ``acc``
     (fx_grad_sink): read from there and ``acc`` cleared (ttmi_adamw_fx).  ``fold_plan``
     (WgradPending(defer_fold=True).plan): the step's weight-gradient partials are folded and
-    applied in the same launch (ttmi_adamw_folded)."""
+    applied in the same launch (ttmi_adamw_folded).  ``skip_if`` (id_err_ptr): the update is
+    skipped on the device when a lookup of this step met an id outside its table."""
     bump_param_epoch()
     if skip is not None:                   # (offset, length) updated by adamw_fx_range
         if fx is not None:
             raise ValueError("adamw: skip and fx are exclusive")
         call("ttmi_adamw_folded_skip", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper),
              _p(step), int(zero_grad), None, 0, 0, FX_GRAD_SHIFT,
-             ctypes.byref(fold_plan) if fold_plan is not None else None, int(skip[0]), int(skip[1]), _s())
+             ctypes.byref(fold_plan) if fold_plan is not None else None, int(skip[0]), int(skip[1]),
+             skip_if, _s())
         return
     if fold_plan is not None:
         acc, off, cnt = None, 0, 0
@@ -1232,16 +1323,17 @@ def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], 
             acc, view = fx
             off, cnt = (view.data_ptr() - g.data_ptr()) // g.element_size(), view.numel()
         call("ttmi_adamw_folded", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper),
-             _p(step), int(zero_grad), _p(acc), off, cnt, FX_GRAD_SHIFT, ctypes.byref(fold_plan), _s())
+             _p(step), int(zero_grad), _p(acc), off, cnt, FX_GRAD_SHIFT, ctypes.byref(fold_plan), skip_if,
+             _s())
         return
     if fx is None:
         call("ttmi_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
-             int(zero_grad), _s())
+             int(zero_grad), skip_if, _s())
         return
     acc, view = fx
     off = (view.data_ptr() - g.data_ptr()) // g.element_size()
     call("ttmi_adamw_fx", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(hyper), _p(step),
-         int(zero_grad), _p(acc), off, view.numel(), FX_GRAD_SHIFT, _s())
+         int(zero_grad), _p(acc), off, view.numel(), FX_GRAD_SHIFT, skip_if, _s())
 
 
 _FX_SINK: List[list] = []

@@ -66,10 +66,12 @@ def train_one_epoch(model, dataloader, optimizer, device, epoch, is_main_process
                 batch[k] = v.to(device)
         optimizer.zero_grad(set_to_none=True)
         loss, _, _, _ = model(batch)
+        # nn.Embedding raises inside the forward, before any update: wait for the forward's
+        # lookups, and raise for an id outside its table before backward / optimizer.step()
+        ops.check_id_errors(sync=True)
         loss.backward()
         optimizer.step()
         loss_val = loss.item()
-        ops.check_id_errors()     # synced by .item(): an id outside its table raises this step
         total_loss += loss_val
         if is_main_process and (i + 1) % log_interval == 0:
             logger.info(f"Epoch {epoch} [{i + 1}/{num_batches}] | Loss: {loss_val:.4f}")
@@ -171,6 +173,8 @@ class GradSync:
     def __init__(self, group=None, bucket_bytes: int = 32 << 20):
         self.group = group
         self.world = comm.world_size(group)
+        # the collectives run: world > 1, or comm.force_dp at world 1 (the RCCL rehearsal)
+        self.active = comm.dp_active(group)
         self.bucket = max(1, bucket_bytes // 4)
 
     @property
@@ -178,7 +182,7 @@ class GradSync:
         return 1.0 / self.world
 
     def start(self, flat_grad: Tensor) -> List:
-        if self.world == 1:
+        if not self.active:
             return []
         n = flat_grad.numel()
         return [comm.all_reduce_sum(flat_grad[s:s + self.bucket], self.group, async_op=True)
@@ -192,12 +196,15 @@ class GradSync:
 class _Segments:
     """A step recorded as HIP-graph segments separated by host actions (the collectives, which
     run between graph replays on the same stream).  With no cut the step is one graph.  In
-    eager mode ``cut`` runs its action at once, so one code path serves both."""
+    eager mode ``cut`` runs its action at once, so one code path serves both.  ``inline``
+    (collectives that can be captured, comm.capturable): ``cut`` records its action into the
+    open graph, so the whole step stays one graph."""
 
-    def __init__(self, device, capture: bool, pool=None):
+    def __init__(self, device, capture: bool, pool=None, inline: bool = False):
         self.device = device
         self.capture = capture
         self.pool = pool
+        self.inline = inline
         self.items: List = []           # ("graph", CUDAGraph) | ("host", fn)
         self.cur = None
         self.stream = None
@@ -220,7 +227,7 @@ class _Segments:
         self.cur = None
 
     def cut(self, fn: Callable[[], None]) -> None:
-        if not self.capture:
+        if not self.capture or self.inline:
             fn()
             return
         self._close()
@@ -289,7 +296,8 @@ class TrainStep:
     def __init__(self, model: TwoTowerModel, lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.01, use_graph: bool = True,
                  seed: int = 0, group=None, broadcast_buffers: bool = True,
-                 overlap_grad_sync: bool = True, grad_sink: bool = True):
+                 overlap_grad_sync: bool = True, grad_sink: bool = True,
+                 capture_collectives: Optional[bool] = None):
         self.model = model
         # grad_sink (one process only): the [V, D] item-embedding gradient stays in its int64
         # fixed-point accumulator and AdamW reads it there (a 31 MB conversion pass saved), so
@@ -301,6 +309,7 @@ class TrainStep:
         self.fold_in_update = grad_sink and os.environ.get("TTMI_FOLD_IN_UPDATE", "1") != "0"
         self._fold = None
         self._pend = None
+        self._keep = None
         model.train()
         dev = next(model.parameters()).device
         self.device = dev
@@ -311,16 +320,34 @@ class TrainStep:
         self.group = group if group is not None else getattr(model, "process_group", None)
         self.sync = GradSync(self.group)
         self.world = self.sync.world
+        # the data-parallel schedule: world > 1, or comm.force_dp at world 1 (RCCL rehearsal)
+        self.dp = self.sync.active
+        # the collectives recorded inside the step's HIP graph (RCCL) instead of host cuts
+        self.capture_collectives = self.dp and (comm.capturable(self.group)
+                                                if capture_collectives is None else capture_collectives)
         self.global_negatives = bool(getattr(model, "global_negatives", False))
-        self.overlap = overlap_grad_sync and self.world > 1 and self.ucfg.n_layers >= 2
-        self.fold_in_update = self.fold_in_update and self.world == 1
+        self.overlap = overlap_grad_sync and self.dp and self.ucfg.n_layers >= 2
+        self.fold_in_update = self.fold_in_update and not self.dp
+        # the weight-gradient GEMMs planned (their partials folded later): inside AdamW in one
+        # process; data-parallel, by a fold launch before the tail all-reduce — either way the
+        # GEMMs can run early on the side stream beside the input block's backward
+        self.plan_wgrad = self.fold_in_update or (
+            self.dp and os.environ.get("TTMI_DP_PLAN_WGRAD", "1") != "0")
+        self._split_cuts = False               # capturing with host cuts (segmented schedule)
+        self._extra_filled = False
         self.fbufs = FlatBuffers(model)
-        self.broadcast_buffers = broadcast_buffers and self.world > 1 and \
+        self.broadcast_buffers = broadcast_buffers and self.dp and \
             self.fbufs.data is not None
+        # fp32 slots after the gradients that ride the all-reduce: rank 0's BatchNorm buffers
+        # (broadcast_buffers) and, data-parallel, every rank's 8 id-range flags (1.0f when
+        # raised): summed, they make every rank skip the update of a step in which any rank met
+        # an id outside a table, so the replicas never diverge
+        self.n_bufx = self.fbufs.numel if self.broadcast_buffers else 0
+        self.flag_off = (self.n_bufx + 3) // 4 * 4 if self.dp else None
         self.flat = FlatParams(model, self.dtype, tail=self.LATE if self.overlap else (),
-                               grad_extra=self.fbufs.numel if self.broadcast_buffers else 0)
+                               grad_extra=self.flag_off + 8 if self.dp else self.n_bufx)
         ops.bump_param_epoch()                 # parameters now live in (and move with) the flat buffer
-        if self.world > 1:                     # DDP's constructor: rank 0's parameters and buffers
+        if self.dp:                            # DDP's constructor: rank 0's parameters and buffers
             src = comm.group_src(0, self.group)
             comm.broadcast(self.flat.data, src, self.group)
             if self.fbufs.data is not None:
@@ -329,8 +356,9 @@ class TrainStep:
             # broadcast_buffers without a collective of its own: rank 0's buffers after step
             # k's forward are exactly what DDP broadcasts at the start of step k + 1, so they
             # ride step k's gradient all-reduce (rank 0 adds them, the others add zeros) into
-            # `bstage`, which the next step's first kernel copies over every rank's buffers
-            self.bstage = self.fbufs.data.clone()
+            # the gradient's extra slots, which the next step's staging launch copies over every
+            # rank's buffers (AdamW and the backward never write those slots)
+            self.flat.grad_extra[:self.n_bufx].copy_(self.fbufs.data)
             self.bzero = torch.zeros_like(self.fbufs.data)
             self.is_root = comm.rank(self.group) == 0
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay],
@@ -410,8 +438,6 @@ class TrainStep:
             seeds = self.seeds
         else:
             ops.step_inc(self.step_t)
-        if self.broadcast_buffers:             # rank 0's buffers from the last all-reduce
-            ops.batch_copy([self.fbufs.data], [self.bstage])
         # cfg 2: the item head's first stage rides in the user head launch (idle CUs)
         # and both heads also write InfoNCE's l2norm of their rows (no normalise launch)
         normed = None
@@ -438,7 +464,7 @@ class TrainStep:
                                         self.bufs, self.p_item)
         self._fx = None
         # one process: the step's weight-gradient partials are folded inside the AdamW launch
-        with ops.deferred_wgrad(defer_fold=self.fold_in_update) as pend, \
+        with ops.deferred_wgrad(defer_fold=self.plan_wgrad) as pend, \
                 (ops.fx_grad_sink() if fx_sink else contextlib.nullcontext([])) as sink:
             # one fold launch for the step's weight grads; with the GEMMs on the side stream
             # (ops.wgrad_launch_early) the update joins them (_update)
@@ -461,13 +487,13 @@ class TrainStep:
         if self.global_negatives:         # cfg 5: negatives from every rank's batch
             gst = F.infonce_global_prep(u, it, b.get("user_idx"), self.model.temperature,
                                         self.group)
-            if gst.world > 1:
+            if gst.dp:
                 cut(lambda: F.infonce_global_gather(gst, self.group))
             loss = F.infonce_global_loss(gst)
             self.loss_sum.add_(loss.view(1))
             logits = gst.s_u2i
             F.infonce_global_loss_bwd(gst, self.dloss)
-            if gst.world > 1:
+            if gst.dp:
                 cut(lambda: F.infonce_global_scatter(gst, self.group))
             F.infonce_global_norm_bwd(gst, du, di)
         else:
@@ -488,9 +514,21 @@ class TrainStep:
         hook = None
         if self.overlap:
             def hook(i: int) -> None:
-                if i == 1:       # every gradient before the tail slots is final
-                    pend.flush()
+                if i != 1:       # every gradient before the tail slots is final
+                    return
+                if self._split_cuts:           # host cuts: complete them here, reduce at the cut
+                    pend.flush_on(torch.cuda.current_stream(self.device))
+                    self._fill_extra()
                     cut(self._sync_head)
+                    return
+                # their GEMMs + folds and the head bucket's all-reduce run on the side stream
+                # (RCCL's own stream after it) while this stream differentiates layer 0 and
+                # the input block; the update joins them
+                side = ops.wgrad_side_stream(self.device)
+                pend.flush_on(side)
+                with torch.cuda.stream(side):
+                    self._fill_extra()         # BN buffers + id flags: final since the forward
+                    self._sync_head()
         F.user_tower_bwd(self.Pu, self.Wu, ust, du, self.Gu, self.ucfg, du16, on_layer_done=hook,
                          co_item=ib)
         self.loss, self.logits = loss, logits
@@ -507,6 +545,21 @@ class TrainStep:
             dsts.append(self.Wi[t4])
             srcs.append(self.Wi["fusion_layer.4.weight"])
         ops.transpose_batch(dsts, srcs, seeds)
+
+    def _fill_extra(self) -> None:
+        """The all-reduced slots after the gradients: rank 0's BatchNorm buffers (the others add
+        zeros) and this rank's id-range flags; one copy launch."""
+        gx = self.flat.grad_extra
+        dsts, srcs = [], []
+        if self.broadcast_buffers:
+            dsts.append(gx[:self.n_bufx])
+            srcs.append(self.fbufs.data if self.is_root else self.bzero)
+        if self.dp:
+            dsts.append(gx[self.flag_off:self.flag_off + 8])
+            srcs.append(ops.id_err_flags(self.flat.data))
+        if dsts:
+            ops.batch_copy(dsts, srcs)
+        self._extra_filled = True
 
     def _sync_head(self) -> None:
         self._pending = self.sync.start(self.flat.grad[:self.flat.tail_offset])
@@ -560,20 +613,22 @@ class TrainStep:
         f = self.flat
         pend, self._pend = self._pend, None
         plan = self._fold[0] if self._fold else None
+        # a step whose lookups met an id outside a table (on any rank) updates nothing
+        skip_if = f.grad_extra[self.flag_off:].data_ptr() if self.dp else ops.id_err_ptr(f.data)
         if pend is not None and pend.side is not None and self._fx is not None and _ADAM_SPLIT:
             # the item-embedding rows' update (their gradient complete in the fixed-point
             # accumulator) runs while the weight-gradient GEMMs finish on the side stream; the
             # rest of the flat buffer after the join
             skip = ops.adamw_fx_range(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper,
-                                      self.step_t, self._fx, zero_grad=True)
+                                      self.step_t, self._fx, zero_grad=True, skip_if=skip_if)
             pend.join()
             ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
-                      zero_grad=True, fold_plan=plan, skip=skip)
+                      zero_grad=True, fold_plan=plan, skip=skip, skip_if=skip_if)
         else:
             if pend is not None:
                 pend.join()
             ops.adamw(f.data, f.grad, f.exp_avg, f.exp_avg_sq, f.mirror, self.hyper, self.step_t,
-                      zero_grad=True, fx=self._fx, fold_plan=plan)
+                      zero_grad=True, fx=self._fx, fold_plan=plan, skip_if=skip_if)
         self._fx = None
         self._fold = None
 
@@ -581,14 +636,22 @@ class TrainStep:
         # one process: the item-embedding gradient goes from its fixed-point accumulator
         # straight into AdamW (no fold pass over the [V, D] table); with DDP it is folded
         # into the flat gradient for the all-reduce
-        self._fwd_bwd(b, cut, fx_sink=self.world == 1 and self.grad_sink)
-        if self.broadcast_buffers:             # rank 0 contributes its buffers, others zeros
-            ops.batch_copy([self.flat.grad_extra], [self.fbufs.data if self.is_root else self.bzero])
-        if self.world > 1:
+        self._extra_filled = False
+        self._fwd_bwd(b, cut, fx_sink=not self.dp and self.grad_sink)
+        if self.dp:
+            # complete the gradient before the tail all-reduce: join the side stream (the head
+            # bucket's GEMMs, folds and all-reduce launch; the early weight-gradient GEMMs) and
+            # fold the planned partials here instead of inside AdamW
+            self._pend.join()
+            if self._fold is not None:
+                ops.fold_plan_run(self._fold[0])
+                self._keep = self._fold[1]
+                self._fold = None
+            if not self._extra_filled:
+                self._fill_extra()
             cut(self._sync_tail)
         self._update()
-        if self.broadcast_buffers:
-            ops.batch_copy([self.bstage], [self.flat.grad_extra])
+        self._keep = None
 
     # ---------------------------------------------------------------- capture
     @staticmethod
@@ -599,8 +662,11 @@ class TrainStep:
     def check(self) -> None:
         """Wait for the queued steps and raise IndexError if any of them met an embedding id
         outside its table (the reference's nn.Embedding raises, user_tower.py:26,30-31).  The
-        device lookups clamp such an id and set a host-mapped flag, so ``step()`` also raises at
-        its start for any earlier step that has finished, with no sync of its own."""
+        device lookups clamp such an id and set a flag; that step's AdamW then updates nothing
+        (parameters, moments and the bf16 mirror keep their values; its BatchNorm running
+        statistics and ``loss_sum`` do include it, and Adam's step count advances), and
+        ``step()`` raises at its start for any earlier step that has finished, with no sync of
+        its own.  Call ``check()`` at the end of a loop so the last steps are covered too."""
         ops.check_id_errors(sync=True)
 
     def _stage(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
@@ -613,18 +679,27 @@ class TrainStep:
         self._cur = e
         keys = list(e.static)
         srcs = [batch[k] for k in keys]
+        # the same launch clears the device id-range flags (this step's AdamW skips only for this
+        # step's bad ids) and, data-parallel, copies rank 0's BatchNorm buffers from the last
+        # all-reduce over this rank's (DDP broadcast_buffers)
+        fl_dst, fl_src = ops.id_err_step_reset(self.flat.data)
+        xd, xs = [fl_dst], [fl_src]
+        if self.broadcast_buffers:
+            xd.append(self.fbufs.data)
+            xs.append(self.flat.grad_extra[:self.n_bufx])
         if all(t.is_cuda and t.is_contiguous() and t.dtype == e.static[k].dtype
                for k, t in zip(keys, srcs)):
-            ops.batch_copy([e.static[k] for k in keys], srcs)   # one launch
+            ops.batch_copy([e.static[k] for k in keys] + xd, srcs + xs)   # one launch
         else:
             for k, t in zip(keys, srcs):
                 e.static[k].copy_(t, non_blocking=True)
+            ops.batch_copy(xd, xs)
         return e.static
 
     def _state(self):
         return [self.flat.data, self.flat.exp_avg, self.flat.exp_avg_sq, self.step_t, self.loss_sum,
                 *self.bufs.values()] + ([self.flat.mirror] if self.flat.mirror is not None else []) + \
-            ([self.bstage] if self.broadcast_buffers else [])
+            ([self.flat.grad_extra] if self.dp else [])
 
     def _capture(self, e: _Entry) -> None:
         b = e.static
@@ -637,10 +712,15 @@ class TrainStep:
         for t, s in zip(self._state(), snap):   # undo the warm-up's state changes
             t.copy_(s)
         torch.cuda.synchronize(self.device)
-        seg = _Segments(self.device, capture=True, pool=torch.cuda.graph_pool_handle())
-        seg.begin()
-        self._body(b, seg.cut)
-        seg.end()
+        seg = _Segments(self.device, capture=True, pool=torch.cuda.graph_pool_handle(),
+                        inline=self.capture_collectives)
+        self._split_cuts = self.dp and not seg.inline
+        try:
+            seg.begin()
+            self._body(b, seg.cut)
+            seg.end()
+        finally:
+            self._split_cuts = False
         e.seg, e.loss, e.logits = seg, self.loss, self.logits
 
     def step(self, batch: Dict[str, Tensor]) -> Tensor:

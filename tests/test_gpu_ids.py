@@ -1,8 +1,11 @@
 """Embedding ids outside their tables (reference nn.Embedding raises IndexError,
 src/models/user_tower.py:26,30-31) on every batch and every path, without a GPU fault and without
-a host sync per step: the device lookups clamp the id and set a host-mapped flag
-(include/ttmi.h TTMI_IDERR_*); TrainStep.step() / the module forward raise at their start for an
-earlier finished launch, TrainStep.check() and train_one_epoch (after loss.item()) right away."""
+a host sync per step: the device lookups clamp the id and set a device + host-mapped flag
+(include/ttmi.h TTMI_IDERR_*, ABI 22); TrainStep.step() / the module forward raise at their
+start for an earlier finished launch, TrainStep.check() and train_one_epoch (right after the
+forward) right away.  As the reference raises before optimizer.step(), a bad step updates no
+parameter: TrainStep's AdamW reads the device flags and skips (parameters, moments and the bf16
+mirror bit-identical afterwards), train_one_epoch raises before backward."""
 import ctypes
 
 import pytest
@@ -87,9 +90,58 @@ def test_module_forward_bad_id(gpu_pkg, key, bad, dtype):
 def test_train_one_epoch_raises_at_the_bad_batch(gpu_pkg):
     m = _model(gpu_pkg)
     opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
-    loader = [_batch(1), _batch(2, "user_country", 64), _batch(3)]
+    gpu_pkg.train.train_one_epoch(m, [_batch(1)], opt, DEV, epoch=0)
+    before = {k: v.detach().clone() for k, v in m.named_parameters()}
+    loader = [_batch(2, "user_country", 64), _batch(3)]
     with pytest.raises(IndexError, match="user_country"):
         gpu_pkg.train.train_one_epoch(m, loader, opt, DEV, epoch=0)
+    for k, v in m.named_parameters():       # raised before backward / optimizer.step()
+        assert torch.equal(v.detach(), before[k]), k
+
+
+def _flat_state(step):
+    f = step.flat
+    return [t.detach().clone() for t in (f.data, f.exp_avg, f.exp_avg_sq) +
+            ((f.mirror,) if f.mirror is not None else ())]
+
+
+@pytest.mark.parametrize("key,bad", BAD[:3] + [("history_ids", -7)])
+@pytest.mark.parametrize("use_graph", [True, False])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_trainstep_bad_batch_updates_nothing(gpu_pkg, key, bad, use_graph, dtype):
+    """AdamW's skip_if: the step that met the bad id leaves parameters, moments and the bf16
+    mirror bit-identical (also the fixed-point item-embedding gradient and the folded weight
+    gradients are consumed, so the next good step is exactly a normal step)."""
+    m = _model(gpu_pkg, dtype)
+    step = gpu_pkg.TrainStep(m, use_graph=use_graph)
+    step.step(_batch(1))
+    step.check()
+    before = _flat_state(step)
+    step.step(_batch(2, key, bad))
+    torch.cuda.synchronize()
+    for a, b in zip(_flat_state(step), before):
+        assert torch.equal(a, b)
+    assert not step.flat.grad.any()          # the gradient was still cleared
+    with pytest.raises(IndexError, match=key):
+        step.check()
+    step.step(_batch(3))                     # a good step updates again
+    step.check()
+    assert not torch.equal(step.flat.data, before[0])
+    # ... exactly as a run that never saw the bad batch (Adam's step count aside, which the
+    # skipped step advanced): compare against a twin stepped on batches 1 and 3 only, with its
+    # step counter advanced once
+    twin_m = _model(gpu_pkg, dtype)
+    twin = gpu_pkg.TrainStep(twin_m, use_graph=use_graph)
+    twin.step(_batch(1))
+    torch.cuda.synchronize()
+    twin.step_t.add_(1)
+    twin.step(_batch(3))
+    twin.check()
+    # dropout seeds are drawn from (seed, step count): the same masks in both runs.  (The fp32
+    # path's split-K weight gradients add with float atomics, so only bf16 is bit-reproducible.)
+    if dtype == torch.bfloat16:
+        for a, b in zip(_flat_state(step), _flat_state(twin)):
+            assert torch.equal(a, b)
 
 
 def test_catalogue_indexer_bad_target_id(gpu_pkg):
@@ -111,3 +163,5 @@ def test_flags_are_host_mapped(gpu_pkg):
     f = ops._IDF[torch.device(DEV).index]
     assert f.host is not None and f.dptr is not None
     assert isinstance(f.host, ctypes.Array)
+    # the device block's pointer slot (byte 32) holds the host array's device address
+    assert int(f.dev.view(torch.int64)[4]) != 0

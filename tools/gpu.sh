@@ -12,6 +12,9 @@
 #   tools/gpu.sh bench-all TAG [cfgs]    bench lines of 2, 2d256, 3, 4, 5, eval, prep
 #   tools/gpu.sh ab PAIRS A B [...] [-- bench args]   alternate env settings ("N=V[,N=V]" or
 #                                        "-"), 200-step cfg-2 benches
+#   tools/gpu.sh ddp TAG [bench args]   RCCL world-1 tests, then cfg-2 bench lines: single-process,
+#                                        forced DDP schedule with captured RCCL collectives, and
+#                                        with host cuts (-> gpurun_out/ddp_TAG_*.json)
 #   tools/gpu.sh dis-counters            disentangled-attention timing + SQ counters (cfg 4)
 #   tools/gpu.sh final TAG               closing measurements: suite, default bench under
 #                                        rocprofv3, the other configs, cfg-2/3/4 step profiles,
@@ -105,6 +108,27 @@ ab() {
   done
 }
 
+ddp() {
+  local tag=$1; shift
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_rccl.py -v --timeout 300 --timeout-method thread \
+    > gpurun_out/ddp_${tag}_tests.log 2>&1
+  local rc=$?
+  tail -8 gpurun_out/ddp_${tag}_tests.log
+  [ $rc -eq 0 ] || [ $rc -eq 1 ] || return $rc
+  local v args
+  for v in single captured segmented; do
+    case $v in
+      single) args="" ;;
+      captured) args="--ddp-schedule" ;;
+      segmented) args="--ddp-schedule --no-capture-collectives" ;;
+    esac
+    timeout -k 10 300 python bench.py --skip-cpu --steps 200 --warmup 20 $args "$@" > gpurun_out/ddp_${tag}_$v.json \
+      2> gpurun_out/ddp_${tag}_$v.err || { tail -20 gpurun_out/ddp_${tag}_$v.err; return 1; }
+    python3 -c "import json;d=json.loads(open('gpurun_out/ddp_${tag}_$v.json').read().strip().splitlines()[-1]);print('$v', d['value'], d['ms_per_step'], d['config'].get('schedule'))"
+  done
+  return $rc
+}
+
 dis_counters() {
   timeout -k 10 120 python3 -u tools/attn_bench.py > gpurun_out/dis_time.log 2>&1 || { tail -20 gpurun_out/dis_time.log; return 1; }
   cat gpurun_out/dis_time.log
@@ -172,6 +196,7 @@ case $cmd in
   bench-all) bench_all "$@" ;;
   ab) ab "$@" ;;
   dis-counters) dis_counters "$@" ;;
+  ddp) ddp "$@" ;;
   final) final "$@" ;;
   *) sed -n 2,22p "$0"; exit 2 ;;
 esac
