@@ -783,6 +783,9 @@ def main():
                     help="run the data-parallel schedule even at --gpus 1: a world-1 process group "
                          "(TTMI_DIST_BACKEND, default nccl = RCCL) whose collectives all run "
                          "(comm.force_dp): the per-rank cost of DDP without the wire")
+    ap.add_argument("--overlap-grad-sync", action="store_true",
+                    help="data-parallel schedule: two gradient buckets, the first all-reduced "
+                         "while layer 0 and the input block are differentiated")
     ap.add_argument("--no-capture-collectives", action="store_true",
                     help="data-parallel schedule: collectives between graph segments (host cuts) "
                          "instead of inside the step's graph")
@@ -835,7 +838,8 @@ def main():
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, 0)
     step = pkg.TrainStep(model, lr=1e-4, use_graph=not args.no_graph, seed=rank + 1,
-                         capture_collectives=False if args.no_capture_collectives else None)
+                         capture_collectives=False if args.no_capture_collectives else None,
+                         overlap_grad_sync=True if args.overlap_grad_sync else None)
     batches = synthetic_batches(2 if cfg3 else 4, B, seed=rank, device=device)
     if cfg3:
         batches = add_raw_items(batches, rank, device)
@@ -924,7 +928,8 @@ def main():
                        "vocab": V, "d_model": D, "parallelism": f"dp{world}",
                        "graph": not args.no_graph,
                        "schedule": ("ddp" if step.dp else "single-process") +
-                                   (f" ({dist.get_backend()}, collectives "
+                                   (f" ({dist.get_backend()}, "
+                                    f"{'two buckets' if step.overlap else 'one all-reduce'}, collectives "
                                     f"{'captured in the step graph' if step.capture_collectives else 'between graph segments'}, "
                                     f"{step._cur.seg.n_graphs if step._cur.seg else 0} graph(s) per step)"
                                     if step.dp else "")},

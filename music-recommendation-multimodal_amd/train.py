@@ -219,7 +219,11 @@ class _Segments:
 
     def _open(self) -> None:
         self.cur = torch.cuda.CUDAGraph()
-        self.cur.capture_begin(pool=self.pool)
+        # collectives in the graph: thread-local capture, so that the process group's watchdog
+        # thread may still query the events of earlier (uncaptured) collectives meanwhile (a
+        # global-mode capture makes that query fail and the watchdog abort the process)
+        self.cur.capture_begin(pool=self.pool,
+                               capture_error_mode="thread_local" if self.inline else "global")
 
     def _close(self) -> None:
         self.cur.capture_end()
@@ -296,7 +300,7 @@ class TrainStep:
     def __init__(self, model: TwoTowerModel, lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.01, use_graph: bool = True,
                  seed: int = 0, group=None, broadcast_buffers: bool = True,
-                 overlap_grad_sync: bool = True, grad_sink: bool = True,
+                 overlap_grad_sync: Optional[bool] = None, grad_sink: bool = True,
                  capture_collectives: Optional[bool] = None):
         self.model = model
         # grad_sink (one process only): the [V, D] item-embedding gradient stays in its int64
@@ -326,6 +330,13 @@ class TrainStep:
         self.capture_collectives = self.dp and (comm.capturable(self.group)
                                                 if capture_collectives is None else capture_collectives)
         self.global_negatives = bool(getattr(model, "global_negatives", False))
+        # two-bucket overlap (the head bucket all-reduced while layer 0 and the input block are
+        # differentiated) is opt-in: measured at world size 1 on RCCL it costs the rank ~38 us
+        # of compute (its GEMMs split from the tail's, cross-stream graph joins), about what it
+        # hides of an 8-GPU ring all-reduce of its 2.8 MB; the default computes
+        # every weight gradient in the one-process schedule and all-reduces once
+        if overlap_grad_sync is None:
+            overlap_grad_sync = os.environ.get("TTMI_DP_OVERLAP", "0") == "1"
         self.overlap = overlap_grad_sync and self.dp and self.ucfg.n_layers >= 2
         self.fold_in_update = self.fold_in_update and not self.dp
         # the weight-gradient GEMMs planned (their partials folded later): inside AdamW in one

@@ -182,7 +182,7 @@ def _trainstep_worker(rank, global_negatives, use_graph, out):
                           global_negatives=global_negatives).cuda()
     m.item_tower.fusion_layer[3].p = 0.0
     p0 = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
-    step = pkg.TrainStep(m, lr=LR, use_graph=use_graph, seed=rank + 1)
+    step = pkg.TrainStep(m, lr=LR, use_graph=use_graph, seed=rank + 1, overlap_grad_sync=True)
     assert step.world == WORLD and step.overlap and step.broadcast_buffers
     assert step.flat.tail_offset < step.flat.numel
     losses = []

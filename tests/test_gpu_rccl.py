@@ -12,9 +12,9 @@ At world size 1 every collective is the identity, so:
   reduce-scatter) overwrite a NaN-filled output, which proves the RCCL kernel ran;
 * the same collectives recorded inside a HIP graph replay correctly (the captured schedule);
 * ``TrainStep`` on the forced schedule — RCCL with the collectives captured into the step's
-  graph, RCCL with host cuts between graph segments, and gloo (host-staged, segmented) — gives
-  parameters, AdamW moments, BN buffers and losses bit-identical to the single-process step,
-  for local and global (cfg 5) negatives.
+  graph (one all-reduce, and the two-bucket overlap), RCCL with host cuts between graph
+  segments, and gloo (host-staged, segmented) — gives parameters, AdamW moments, BN buffers and
+  losses bit-identical to the single-process step, for local and global (cfg 5) negatives.
 
 Each case runs in one fresh spawned process (nothing else has touched the GPU there), which
 initialises the process group itself on 127.0.0.1.
@@ -107,7 +107,8 @@ def _collectives_worker():
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture, as TrainStep's: the watchdog may query earlier works meanwhile
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             x.mul_(2.0)
             ws = pkg.GradSync(bucket_bytes=4 * 16_384).start(x)
             for w in ws:
@@ -170,23 +171,27 @@ def _trainstep_worker(global_negatives):
     try:
         runs["single"] = _train(pkg, global_negatives)          # one process, fused schedule
         comm.force_dp(True)
-        runs["rccl_captured"] = _train(pkg, global_negatives)
-        runs["rccl_segmented"] = _train(pkg, global_negatives, capture_collectives=False)
+        runs["rccl_captured"] = _train(pkg, global_negatives)   # default: one all-reduce
+        runs["rccl_captured_overlap"] = _train(pkg, global_negatives, overlap_grad_sync=True)
+        runs["rccl_segmented"] = _train(pkg, global_negatives, capture_collectives=False,
+                                        overlap_grad_sync=True)
     finally:
         comm.force_dp(False)
         dist.destroy_process_group()
     _init("gloo")
     try:
         comm.force_dp(True)
-        runs["gloo"] = _train(pkg, global_negatives)
+        runs["gloo"] = _train(pkg, global_negatives, overlap_grad_sync=True)
     finally:
         comm.force_dp(False)
         dist.destroy_process_group()
     info = {k: v[3] for k, v in runs.items()}
     # (dp, captured collectives, overlap, fold_in_update, broadcast_buffers, graphs per step)
     assert info["single"][:5] == (False, False, False, True, False) and info["single"][5] == 1, info
-    assert info["rccl_captured"][:5] == (True, True, True, False, True), info
+    assert info["rccl_captured"][:5] == (True, True, False, False, True), info
     assert info["rccl_captured"][5] == 1, info                 # one graph: collectives inside
+    assert info["rccl_captured_overlap"][:5] == (True, True, True, False, True), info
+    assert info["rccl_captured_overlap"][5] == 1, info
     assert info["rccl_segmented"][:3] == (True, False, True) and info["rccl_segmented"][5] > 1, info
     assert info["gloo"][:3] == (True, False, True) and info["gloo"][5] > 1, info
     base_st, base_l, base_sum, _ = runs["single"]

@@ -116,11 +116,12 @@ ddp() {
   tail -8 gpurun_out/ddp_${tag}_tests.log
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || return $rc
   local v args
-  for v in single captured segmented; do
+  for v in single captured overlap segmented; do
     case $v in
       single) args="" ;;
       captured) args="--ddp-schedule" ;;
-      segmented) args="--ddp-schedule --no-capture-collectives" ;;
+      overlap) args="--ddp-schedule --overlap-grad-sync" ;;
+      segmented) args="--ddp-schedule --overlap-grad-sync --no-capture-collectives" ;;
     esac
     timeout -k 10 300 python bench.py --skip-cpu --steps 200 --warmup 20 $args "$@" > gpurun_out/ddp_${tag}_$v.json \
       2> gpurun_out/ddp_${tag}_$v.err || { tail -20 gpurun_out/ddp_${tag}_$v.err; return 1; }
