@@ -715,6 +715,16 @@ int ttmi_transpose_bf16_batch_seeds(int n, void* const* dst, const void* const* 
                                     const int64_t* rows, const int64_t* cols, uint64_t seed_base,
                                     int32_t* step, uint64_t* seeds, int n_seeds, int inc_step,
                                     hipStream_t stream);
+/* ABI 22: the train step's whole prologue in one dispatch — ttmi_batch_copy of the n_copy
+ * tensors (the batch staged into the captured graph's static inputs, the id-range flags
+ * cleared, the data-parallel BatchNorm buffers restored), ttmi_transpose_bf16_batch_seeds'
+ * transposes, and its seed workgroup (n_seeds seeds; n_seeds = 0 with inc_step: only the step
+ * count advances, ttmi_step_inc).  Issued on the stream ahead of the graph replay (the copy
+ * sources change every step), it replaces one launch per step; same semantics as the three. */
+int ttmi_step_prologue(int n_copy, void* const* cdst, const void* const* csrc,
+                       const int64_t* nbytes, int n_tr, void* const* tdst, const void* const* tsrc,
+                       const int64_t* rows, const int64_t* cols, uint64_t seed_base, int32_t* step,
+                       uint64_t* seeds, int n_seeds, int inc_step, hipStream_t stream);
 /* dst = bf16(src) (parameter mirror for bf16 GEMM operands). */
 int ttmi_cast_f32_bf16(int64_t n, const float* src, uint16_t* dst, hipStream_t stream);
 /* Residual-branch dropout backward (TransformerEncoderLayer dropout1/dropout2):

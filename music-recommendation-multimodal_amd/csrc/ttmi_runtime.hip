@@ -306,14 +306,13 @@ struct CopyList {
   int n;
 };
 
-// blockIdx.y = tensor; 16-byte vectors when both ends are aligned, bytes otherwise.
-__global__ void batch_copy_kernel(CopyList cl) {
-  const int t = blockIdx.y;
+// Tensor t, block bx of gx: 16-byte vectors when both ends are aligned, bytes otherwise.
+TTMI_DEV void copy_body(const CopyList& cl, int t, int bx, int gx) {
   char* dst = cl.dst[t];
   const char* src = cl.src[t];
   const int64_t nb = cl.bytes[t];
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)bx * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gx * blockDim.x;
   if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
     const int64_t nv = nb / 16;
     for (int64_t i = tid; i < nv; i += stride)
@@ -323,6 +322,8 @@ __global__ void batch_copy_kernel(CopyList cl) {
     for (int64_t i = tid; i < nb; i += stride) dst[i] = src[i];
   }
 }
+// blockIdx.y = tensor.
+__global__ void batch_copy_kernel(CopyList cl) { copy_body(cl, blockIdx.y, blockIdx.x, gridDim.x); }
 
 int grid_for(int64_t n, int per_thread) {
   int64_t b = (n + 256 * per_thread - 1) / (256 * per_thread);
@@ -367,25 +368,6 @@ extern "C" int ttmi_adamw(int64_t n, float* p, float* g, float* m, float* v,
   return ttmi_adamw_fx(n, p, g, m, v, p_bf16, hyper, step, zero_grad, nullptr, 0, 0, 0, skip_if, s);
 }
 
-extern "C" int ttmi_batch_copy(int n, void* const* dst, const void* const* src,
-                               const int64_t* nbytes, hipStream_t s) {
-  TTMI_REQUIRE(n >= 0 && n <= MAX_COPIES, "ttmi_batch_copy: at most %d tensors", MAX_COPIES);
-  if (n == 0) return TTMI_OK;
-  TTMI_REQUIRE(dst && src && nbytes, "ttmi_batch_copy: null argument");
-  CopyList cl;
-  int64_t mx = 0;
-  for (int i = 0; i < n; ++i) {
-    TTMI_REQUIRE(nbytes[i] >= 0 && (nbytes[i] == 0 || (dst[i] && src[i])), "ttmi_batch_copy: bad entry %d", i);
-    cl.dst[i] = static_cast<char*>(dst[i]);
-    cl.src[i] = static_cast<const char*>(src[i]);
-    cl.bytes[i] = nbytes[i];
-    mx = std::max(mx, nbytes[i]);
-  }
-  cl.n = n;
-  const int gx = (int)std::min<int64_t>(std::max<int64_t>((mx / 16 + 255) / 256, 1), 256);
-  hipLaunchKernelGGL(batch_copy_kernel, dim3(gx, n), dim3(256), 0, s, cl);
-  return ttmi_check_launch("ttmi_batch_copy");
-}
 
 // ------------------------------------------------------------ batched bf16 transpose
 // dst_i[c][r] = src_i[r][c] for up to MAX_COPIES row-major matrices in one launch (the
@@ -409,9 +391,9 @@ struct SeedJob {
   int n, inc;
 };
 
-__global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl, SeedJob sj) {
+TTMI_DEV void transpose_body(const TransposeList& tl, const SeedJob& sj, int bid) {
   __shared__ uint16_t t[64][65];
-  if ((int)blockIdx.x == tl.tile0[tl.n]) {         // the seed workgroup (launched when sj.n > 0)
+  if (bid == tl.tile0[tl.n]) {                     // the seed workgroup (sj.n > 0 or sj.inc)
     const int s = threadIdx.x;
     const int32_t st = sj.step[0] + (sj.inc ? 1 : 0);
     if (s < sj.n) sj.seeds[s] = splitmix64(splitmix64(sj.base) ^ ((uint64_t)(int64_t)st * 64ull + (uint64_t)s));
@@ -420,8 +402,8 @@ __global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl, 
     return;
   }
   int i = 0;
-  while (i + 1 < tl.n && (int)blockIdx.x >= tl.tile0[i + 1]) ++i;
-  const int local = blockIdx.x - tl.tile0[i];
+  while (i + 1 < tl.n && bid >= tl.tile0[i + 1]) ++i;
+  const int local = bid - tl.tile0[i];
   const int R = tl.rows[i], C = tl.cols[i];
   const int tcol = (C + 63) / 64;
   const int r0 = (local / tcol) * 64, c0 = (local % tcol) * 64;
@@ -440,18 +422,26 @@ __global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl, 
   for (int c = ty; c < 64; c += 4)
     if (c0 + c < C && r0 + tx < R) dst[(int64_t)(c0 + c) * R + r0 + tx] = t[tx][c];
 }
+__global__ __launch_bounds__(256) void transpose_batch_kernel(TransposeList tl, SeedJob sj) {
+  transpose_body(tl, sj, (int)blockIdx.x);
+}
+// The train step's prologue in one launch (ABI 22): the batch staging copies (blocks
+// [0, cgx·cl.n)), then the transposed weight mirrors, then the seed / step-count workgroup.
+__global__ __launch_bounds__(256) void step_prologue_kernel(CopyList cl, int cgx, TransposeList tl, SeedJob sj) {
+  const int nc = cgx * cl.n;
+  const int b = (int)blockIdx.x;
+  if (b < nc) {
+    copy_body(cl, b / cgx, b % cgx, cgx);
+    return;
+  }
+  transpose_body(tl, sj, b - nc);
+}
 
-extern "C" int ttmi_transpose_bf16_batch_seeds(int n, void* const* dst, const void* const* src,
-                                               const int64_t* rows, const int64_t* cols,
-                                               uint64_t seed_base, int32_t* step, uint64_t* seeds,
-                                               int n_seeds, int inc_step, hipStream_t s) {
+namespace {
+int transpose_list(int n, void* const* dst, const void* const* src, const int64_t* rows,
+                   const int64_t* cols, TransposeList& tl) {
   TTMI_REQUIRE(n >= 0 && n <= MAX_COPIES, "ttmi_transpose_bf16_batch: at most %d matrices", MAX_COPIES);
-  TTMI_REQUIRE(n_seeds >= 0 && n_seeds <= 256 && (n_seeds == 0 || (step && seeds)),
-               "ttmi_transpose_bf16_batch_seeds: bad seed arguments");
-  SeedJob sj{seed_base, step, seeds, n_seeds, inc_step};
-  if (n == 0 && n_seeds == 0) return TTMI_OK;
   TTMI_REQUIRE(n == 0 || (dst && src && rows && cols), "ttmi_transpose_bf16_batch: null argument");
-  TransposeList tl;
   tl.n = n;
   tl.tile0[0] = 0;
   for (int i = 0; i < n; ++i) {
@@ -466,10 +456,74 @@ extern "C" int ttmi_transpose_bf16_batch_seeds(int n, void* const* dst, const vo
     TTMI_REQUIRE(tl.tile0[i] + tiles < (1 << 30), "ttmi_transpose_bf16_batch: too large");
     tl.tile0[i + 1] = tl.tile0[i] + (int)tiles;
   }
+  return TTMI_OK;
+}
+int copy_list(int n, void* const* dst, const void* const* src, const int64_t* nbytes, CopyList& cl,
+              int& gx) {
+  TTMI_REQUIRE(n >= 0 && n <= MAX_COPIES, "ttmi_batch_copy: at most %d tensors", MAX_COPIES);
+  TTMI_REQUIRE(n == 0 || (dst && src && nbytes), "ttmi_batch_copy: null argument");
+  int64_t mx = 0;
+  for (int i = 0; i < n; ++i) {
+    TTMI_REQUIRE(nbytes[i] >= 0 && (nbytes[i] == 0 || (dst[i] && src[i])), "ttmi_batch_copy: bad entry %d", i);
+    cl.dst[i] = static_cast<char*>(dst[i]);
+    cl.src[i] = static_cast<const char*>(src[i]);
+    cl.bytes[i] = nbytes[i];
+    mx = std::max(mx, nbytes[i]);
+  }
+  cl.n = n;
+  gx = (int)std::min<int64_t>(std::max<int64_t>((mx / 16 + 255) / 256, 1), 256);
+  return TTMI_OK;
+}
+}  // namespace
+
+extern "C" int ttmi_transpose_bf16_batch_seeds(int n, void* const* dst, const void* const* src,
+                                               const int64_t* rows, const int64_t* cols,
+                                               uint64_t seed_base, int32_t* step, uint64_t* seeds,
+                                               int n_seeds, int inc_step, hipStream_t s) {
+  TTMI_REQUIRE(n_seeds >= 0 && n_seeds <= 256 && (n_seeds == 0 || (step && seeds)),
+               "ttmi_transpose_bf16_batch_seeds: bad seed arguments");
+  SeedJob sj{seed_base, step, seeds, n_seeds, inc_step};
+  if (n == 0 && n_seeds == 0) return TTMI_OK;
+  TransposeList tl;
+  int rc = transpose_list(n, dst, src, rows, cols, tl);
+  if (rc) return rc;
   const int blocks = tl.tile0[n] + (n_seeds > 0 ? 1 : 0);
   if (blocks == 0) return TTMI_OK;
   hipLaunchKernelGGL(transpose_batch_kernel, dim3(blocks), dim3(256), 0, s, tl, sj);
   return ttmi_check_launch("ttmi_transpose_bf16_batch");
+}
+
+extern "C" int ttmi_step_prologue(int n_copy, void* const* cdst, const void* const* csrc,
+                                  const int64_t* nbytes, int n_tr, void* const* tdst,
+                                  const void* const* tsrc, const int64_t* rows, const int64_t* cols,
+                                  uint64_t seed_base, int32_t* step, uint64_t* seeds, int n_seeds,
+                                  int inc_step, hipStream_t s) {
+  TTMI_REQUIRE(n_seeds >= 0 && n_seeds <= 256 && (n_seeds == 0 || seeds) && ((n_seeds == 0 && !inc_step) || step),
+               "ttmi_step_prologue: bad seed arguments");
+  CopyList cl;
+  int cgx = 1;
+  int rc = copy_list(n_copy, cdst, csrc, nbytes, cl, cgx);
+  if (rc) return rc;
+  TransposeList tl;
+  rc = transpose_list(n_tr, tdst, tsrc, rows, cols, tl);
+  if (rc) return rc;
+  SeedJob sj{seed_base, step, seeds, n_seeds, inc_step};
+  const int64_t blocks = (int64_t)cgx * n_copy + tl.tile0[n_tr] + ((n_seeds > 0 || inc_step) ? 1 : 0);
+  TTMI_REQUIRE(blocks < (1 << 30), "ttmi_step_prologue: too large");
+  if (blocks == 0) return TTMI_OK;
+  hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cl, cgx, tl, sj);
+  return ttmi_check_launch("ttmi_step_prologue");
+}
+
+extern "C" int ttmi_batch_copy(int n, void* const* dst, const void* const* src,
+                               const int64_t* nbytes, hipStream_t s) {
+  if (n == 0) return TTMI_OK;
+  CopyList cl;
+  int gx = 1;
+  const int rc = copy_list(n, dst, src, nbytes, cl, gx);
+  if (rc) return rc;
+  hipLaunchKernelGGL(batch_copy_kernel, dim3(gx, n), dim3(256), 0, s, cl);
+  return ttmi_check_launch("ttmi_batch_copy");
 }
 
 extern "C" int ttmi_transpose_bf16_batch(int n, void* const* dst, const void* const* src,

@@ -306,6 +306,8 @@ SIGNATURES = {
     "ttmi_batch_copy": (c_i, [c_i, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch": (c_i, [c_i, c_p, c_p, c_p, c_p, c_p]),
     "ttmi_transpose_bf16_batch_seeds": (c_i, [c_i, c_p, c_p, c_p, c_p, c_u64, c_p, c_p, c_i, c_i, c_p]),
+    "ttmi_step_prologue": (c_i, [c_i, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_u64, c_p, c_p, c_i,
+                                 c_i, c_p]),
     "ttmi_linear_ln_bwd": (c_i, [c_p, c_p]),
     "ttmi_linear_res_ln": (c_i, [c_p, c_p]),
     "ttmi_deb_embed_fwd": (c_i, [c_i64, c_i, c_p, c_p, c_p, c_p, ctypes.c_float, c_p,

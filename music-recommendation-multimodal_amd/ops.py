@@ -1390,6 +1390,35 @@ def transpose_batch(dsts, srcs, seeds=None):
          sd.numel(), int(inc), _s())
 
 
+def step_prologue(copy_dsts, copy_srcs, tr_dsts, tr_srcs, step: Tensor, seeds=None) -> None:
+    """One launch (ttmi_step_prologue): batch_copy(copy_dsts, copy_srcs), the transposes
+    tr_dsts[i] = tr_srcs[i].t() (bf16), and ``seeds=(base, seeds_tensor)``: the step's dropout
+    seeds with the step count advanced (dropout_seeds(..., inc_step=True)); seeds=None: the step
+    count alone advances (step_inc)."""
+    nc, nt = len(copy_dsts), len(tr_dsts)
+    for d, s_ in zip(copy_dsts, copy_srcs):
+        if d.numel() * d.element_size() != s_.numel() * s_.element_size():
+            raise ValueError("step_prologue: copy size mismatch")
+    for d, s_ in zip(tr_dsts, tr_srcs):
+        if s_.dim() != 2 or d.shape != (s_.shape[1], s_.shape[0]) or not s_.is_contiguous() \
+                or not d.is_contiguous() or s_.dtype != torch.bfloat16 or d.dtype != torch.bfloat16:
+            raise ValueError("step_prologue: transposes need contiguous bf16 [R,C] -> [C,R]")
+    if step.dtype != torch.int32:
+        raise ValueError("step_prologue: the step count is int32")
+    CD = (ctypes.c_void_p * max(nc, 1))(*[t.data_ptr() for t in copy_dsts])
+    CS = (ctypes.c_void_p * max(nc, 1))(*[t.data_ptr() for t in copy_srcs])
+    NB = (ctypes.c_int64 * max(nc, 1))(*[t.numel() * t.element_size() for t in copy_dsts])
+    TD = (ctypes.c_void_p * max(nt, 1))(*[t.data_ptr() for t in tr_dsts])
+    TS = (ctypes.c_void_p * max(nt, 1))(*[t.data_ptr() for t in tr_srcs])
+    R = (ctypes.c_int64 * max(nt, 1))(*[t.shape[0] for t in tr_srcs])
+    C = (ctypes.c_int64 * max(nt, 1))(*[t.shape[1] for t in tr_srcs])
+    base, sd = seeds if seeds is not None else (0, None)
+    if sd is not None and (sd.dtype != torch.int64 or not (0 < sd.numel() <= 256)):
+        raise ValueError("step_prologue: 1..256 int64 seeds")
+    call("ttmi_step_prologue", nc, CD, CS, NB, nt, TD, TS, R, C, base & (2**64 - 1), _p(step), _p(sd),
+         sd.numel() if sd is not None else 0, 1, _s())
+
+
 def step_inc(step: Tensor):
     call("ttmi_step_inc", _p(step), _s())
 

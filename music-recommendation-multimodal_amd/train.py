@@ -418,6 +418,8 @@ class TrainStep:
                 pre = "text_encoder."
                 self.text = (it.text_encoder, sub(self.Pi, pre), sub(self.Gi, pre))
                 self.text_seeds = torch.zeros(T.N_TEXT_SITES, dtype=torch.int64, device=dev)
+        # dropout anywhere in the step: the prologue draws the seeds
+        self._draw = self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0)
         self.sync_mirror()
         self.use_graph = use_graph
         self._entries: Dict[tuple, _Entry] = {}
@@ -437,18 +439,10 @@ class TrainStep:
         """Forward + backward into the flat gradient.  ``cut(fn)`` marks a point where a
         collective ``fn`` runs between graph segments (see _Segments).  ``fx_sink``: leave the
         item-embedding gradient in its fixed-point accumulator for the update (self._fx)."""
-        # the gradient buffer is zero here: it starts zeroed and the fused AdamW clears it
-        seeds = None
-        draw = self.ucfg.p_drop > 0 or self.p_item > 0 or (self.raw_items and self.p_tab > 0)
-        if self.flat.mirror is not None:
-            # Wᵀ mirrors of the just-updated bf16 weights, and the step's seeds: one launch
-            self._refresh_mirrors((self.base_seed, self.step_t, self.seeds, True) if draw else None)
-        if draw:
-            if self.flat.mirror is None:
-                ops.dropout_seeds(self.base_seed, self.step_t, self.seeds, inc_step=True)
-            seeds = self.seeds
-        else:
-            ops.step_inc(self.step_t)
+        # the gradient buffer is zero here: it starts zeroed and the fused AdamW clears it.  The
+        # step's prologue — Wᵀ mirrors of the just-updated bf16 weights, the dropout seeds, the
+        # step count — ran in the staging launch (_stage), ahead of the graph
+        seeds = self.seeds if self._draw else None
         # cfg 2: the item head's first stage rides in the user head launch (idle CUs)
         # and both heads also write InfoNCE's l2norm of their rows (no normalise launch)
         normed = None
@@ -544,9 +538,11 @@ class TrainStep:
                          co_item=ib)
         self.loss, self.logits = loss, logits
 
-    def _refresh_mirrors(self, seeds) -> None:
-        """Every Wᵀ mirror of the just-updated bf16 weights (user tower encoder + fusion MLP,
-        item W4) and the step's dropout seeds: one launch."""
+    def _mirror_transposes(self):
+        """(dsts, srcs) of every Wᵀ mirror of the bf16 weights (user tower encoder + fusion MLP,
+        item W4), refreshed by each step's prologue after the previous step's AdamW."""
+        if self.flat.mirror is None:
+            return [], []
         T = F.transposed_name
         names = [n for n in encoder_weight_names(_gemm_names(list(self.Pu))) if T(n) in self.Wu]
         dsts = [self.Wu[T(n)] for n in names]
@@ -555,7 +551,7 @@ class TrainStep:
         if t4 in self.Wi:
             dsts.append(self.Wi[t4])
             srcs.append(self.Wi["fusion_layer.4.weight"])
-        ops.transpose_batch(dsts, srcs, seeds)
+        return dsts, srcs
 
     def _fill_extra(self) -> None:
         """The all-reduced slots after the gradients: rank 0's BatchNorm buffers (the others add
@@ -690,9 +686,11 @@ class TrainStep:
         self._cur = e
         keys = list(e.static)
         srcs = [batch[k] for k in keys]
-        # the same launch clears the device id-range flags (this step's AdamW skips only for this
-        # step's bad ids) and, data-parallel, copies rank 0's BatchNorm buffers from the last
-        # all-reduce over this rank's (DDP broadcast_buffers)
+        # the step's prologue in one launch (ttmi_step_prologue), ahead of the graph: the batch
+        # into the static inputs, the device id-range flags cleared (this step's AdamW skips
+        # only for this step's bad ids), data-parallel: rank 0's BatchNorm buffers from the last
+        # all-reduce over this rank's (DDP broadcast_buffers); the Wᵀ mirrors of the updated
+        # bf16 weights; the dropout seeds and the step count
         fl_dst, fl_src = ops.id_err_step_reset(self.flat.data)
         xd, xs = [fl_dst], [fl_src]
         if self.broadcast_buffers:
@@ -700,11 +698,13 @@ class TrainStep:
             xs.append(self.flat.grad_extra[:self.n_bufx])
         if all(t.is_cuda and t.is_contiguous() and t.dtype == e.static[k].dtype
                for k, t in zip(keys, srcs)):
-            ops.batch_copy([e.static[k] for k in keys] + xd, srcs + xs)   # one launch
+            xd, xs = [e.static[k] for k in keys] + xd, srcs + xs
         else:
             for k, t in zip(keys, srcs):
                 e.static[k].copy_(t, non_blocking=True)
-            ops.batch_copy(xd, xs)
+        td, ts = self._mirror_transposes()
+        ops.step_prologue(xd, xs, td, ts, self.step_t,
+                          (self.base_seed, self.seeds) if self._draw else None)
         return e.static
 
     def _state(self):

@@ -247,3 +247,51 @@ def _bad_id_worker():
 
 def test_dp_schedule_bad_id_skips_update_on_every_rank():
     _run(_bad_id_worker)
+
+
+# ------------------------------------------------------------------ cfg 3 on the DP schedule
+def _train3(pkg, **kw):
+    from oracle import resnet_ref as rref
+    torch.manual_seed(7)
+    m = pkg.TwoTowerModel(with_text=False, vocab_size=211, tabular_input_dim=32, num_genders=3,
+                          num_countries=8, max_seq_len=12, user_embedding_dim=128,
+                          item_embedding_dim=128, user_dropout=0.1,
+                          precomputed_modalities=False).cuda()
+    m.item_tower.fusion_layer[3].p = 0.1
+    m.item_tower.tabular_encoder.mlp[3].p = 0.1
+    g = torch.Generator().manual_seed(8)
+    batch = ref.synthetic_batch(8, 12, 211, num_countries=8, generator=g)
+    del batch["target_modal"]
+    batch.update(rref.synthetic_items(8, 32, (64, 96), (64, 64), generator=g))
+    b = {k: v.cuda() for k, v in batch.items()}
+    step = pkg.TrainStep(m, lr=1e-3, seed=11, **kw)
+    losses = [float(step.step(b)) for _ in range(2)]
+    step.check()
+    torch.cuda.synchronize()
+    st = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    st["__m"], st["__v"] = step.flat.exp_avg.cpu().clone(), step.flat.exp_avg_sq.cpu().clone()
+    return st, losses, step.dp
+
+
+def _cfg3_worker():
+    pkg = importlib.import_module(PKG_NAME)
+    comm = pkg.comm
+    _init("nccl")
+    try:
+        sa, la, dpa = _train3(pkg)
+        comm.force_dp(True)
+        sb, lb, dpb = _train3(pkg)
+    finally:
+        comm.force_dp(False)
+        dist.destroy_process_group()
+    assert not dpa and dpb
+    assert la == lb, (la, lb)
+    bad = [k for k in sa if not torch.equal(sa[k], sb[k])]
+    assert not bad, bad[:8]
+
+
+def test_cfg3_forced_dp_schedule_rccl_bitexact():
+    """BASELINE configs[2] (ResNet-18 audio / visual + tabular item tower, BatchNorm2d in train
+    mode, dropout on) on the RCCL data-parallel schedule: bit-identical to the one-process step
+    (parameters, BN running buffers, AdamW moments, losses)."""
+    _run(_cfg3_worker)
