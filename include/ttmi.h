@@ -296,6 +296,11 @@ typedef struct ttmi_ffn_block_desc {
   void* h; float* x2;
   const float* lnw; const float* lnb; float eps;
   void* y; float* mean; float* rstd;
+  /* ABI 22 (kv may be NULL): the next layer's K / V input projection of y in the same launch,
+   * kv[m·ld_kv + n] = bf16(y[m]·wkv[n]ᵀ + bkv[n]) for n < 2·D (wkv [2D, D] bf16 = in_proj_weight
+   * rows D..3D): the pruned last layer's full-length K / V (its Q is projected for the gathered
+   * rows only), with the row panel's fragments and MFMA order (ttmi_gemm's bits). */
+  const void* wkv; const float* bkv; void* kv; int64_t ld_kv;
 } ttmi_ffn_block_desc;
 int ttmi_ffn_block_supported(int dtype, int D, int F);
 int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t stream);

@@ -36,9 +36,11 @@ struct FfnArgs {
   const float* lnw; const float* lnb; float eps; bf16_t* y; float* mean; float* rstd;
   DropParams df, d2;
   int M;
+  // KV (ABI 22): the next layer's K / V input projection of y, kv[m, n] = y·wkvᵀ + bkv (n < 256)
+  const bf16_t* wkv; const float* bkv; bf16_t* kv; int64_t ldkv;
 };
 
-template <int NWV, int NG, bool PIPE, bool DF>
+template <int NWV, int NG, bool PIPE, bool DF, bool KV = false>
 __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   constexpr int F = NG * 128;
   // Every operand reaches LDS by LDS-DMA — the rows' A tile too, staged in buffer 1's W2 image
@@ -48,10 +50,10 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   // wave also issues: identical bytes), so one vmcnt immediate serves every wave.
   static_assert(NWV == 8, "the vmcnt immediates below count 8 waves");
   constexpr int PW = (FB_INS + NWV - 1) / NWV;           // 5 per 34-instruction image
-  constexpr int NPI = F / 256 + 5;                       // b1 (1 KB each), b2, LN w / b, 2 seeds
+  constexpr int NPI = F / 256 + 5 + (KV ? 1 : 0);        // b1 (1 KB each), b2, LN w / b, 2 seeds, bkv
   static_assert(NPI <= NWV, "one parameter instruction per wave");
-  constexpr int PB = F * 4;                              // parameter slots: b1 | b2 | lnw | lnb | seeds
-  __shared__ __attribute__((aligned(16))) char smem[2 * FB_BUF + PB + 5 * 1024];
+  constexpr int PB = F * 4;                              // parameter slots: b1 | b2 | lnw | lnb | seeds | bkv
+  __shared__ __attribute__((aligned(16))) char smem[2 * FB_BUF + PB + (KV ? 6 : 5) * 1024];
   char* const spar = smem + 2 * FB_BUF;
   TTMI_TSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
@@ -103,8 +105,21 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
     else if (k == F / 256 + 1) dma16(make_rsrc(g.lnw, FB_D * 4), off, dst);
     else if (k == F / 256 + 2) dma16(make_rsrc(g.lnb, FB_D * 4), off, dst);
     else if (k == F / 256 + 3) dma16(make_rsrc(g.df.seed, g.df.on ? 8 : 0), off, dst);
-    else dma16(make_rsrc(g.d2.seed, g.d2.on ? 8 : 0), off, dst);
+    else if (!KV || k == F / 256 + 4) dma16(make_rsrc(g.d2.seed, g.d2.on ? 8 : 0), off, dst);
+    else dma16(make_rsrc(g.bkv, 2 * FB_D * 4), off, dst);   // 256 floats: one 1 KB slot
   }
+  // KV: W_kv [256, 128] (two images) into the buffer the last group does not use, issued at the
+  // last group's start (that buffer is free then); the row tiles' y into the other one at the end
+  constexpr int KVBUF = ((NG - 1) & 1) ^ 1, ABUF = (NG - 1) & 1;
+  auto issue_kv = [&]() {
+    const i32x4_t rkv = make_rsrc(g.wkv, 2 * FB_D * FB_D * 2);   // pad chunks past it: zeros
+    const uint32_t base = lds_addr(smem + KVBUF * FB_BUF);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int j = 0; j < PW; ++j)
+        dma16(rkv, oW1[j] + (uint32_t)(hf * 128 * FB_D * 2), base + hf * FB_IMG + slot(j) * 1024);
+  };
   issue_a();
   issue_w1(0);
   issue_w2(0);
@@ -219,6 +234,7 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
       if (k == NG - 1) {
         if (NG > 1) load_res_half(1);
         else load_res();
+        if constexpr (KV) issue_kv();
       }
       f32x4_t acc1n[8];
       uint4 hq[4];
@@ -259,7 +275,10 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   } else {
 #pragma unroll
   for (int grp = 0; grp < NG; ++grp) {
-    if (grp == NG - 1) load_res();
+    if (grp == NG - 1) {
+      load_res();
+      if constexpr (KV) issue_kv();
+    }
     // ---- FFN1: 16 rows x the group's 128 hidden units
     f32x4_t acc1[8];
     ffn1(grp, acc1, true);
@@ -310,7 +329,7 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
     const float4 r0 = rpre[2 * p], r1v = rpre[2 * p + 1];
     v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
     v[4] += r1v.x; v[5] += r1v.y; v[6] += r1v.z; v[7] += r1v.w;
-    if (mok) {
+    if (!KV && mok) {                                    // (KV: stored after the projection)
       float* cp = g.x2 + m * FB_D + n;
       *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -330,7 +349,72 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   s2 += __shfl_xor(s2, 16, 64);
   s2 += __shfl_xor(s2, 32, 64);
   const float rs = 1.f / sqrtf(s2 * (1.f / FB_D) + g.eps);
-  if (mok) {
+  if constexpr (KV) {
+    // ---- the next layer's K / V projection of the tile's y rows, with the row panel's fragments
+    // and MFMA order (ttmi_gemm's bits): y -> a row image in the last group's buffer, A
+    // fragments k = 32 lg + 8 c, W_kv images in the other buffer (column-paired rows)
+    uint4 yq[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = 32 * p + 8 * lg;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (vr[8 * p + e] - mu) * rs * slw[n + e] + slb[n + e];
+      yq[p] = pack8(o);
+    }
+    // W_kv landed (the 4 youngest: the last group's h stores); every wave is past its last
+    // FFN2 read of the buffer the row image overwrites
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __syncthreads();
+    char* const arow = smem + ABUF * FB_BUF + (16 * wave + li) * FB_P;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) *reinterpret_cast<uint4*>(arow + 2 * (32 * p + 8 * lg)) = yq[p];
+    uint4 ak[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ak[c] = lds16(arow + 64 * lg + 16 * c);
+    f32x4_t kacc[2][8];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const char* wb = smem + KVBUF * FB_BUF + hf * FB_IMG + wrow * FB_P + 64 * lg;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) kacc[hf][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          Mma<bf16_t>::run(kacc[hf][t], lds16(wb + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * c), ak[c]);
+      }
+    }
+    const float* sbkv = reinterpret_cast<const float*>(spar + PB + 5 * 1024);
+    if (mok) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int n = 128 * hf + 32 * p + 8 * lg;
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = kacc[hf][2 * p][e] + sbkv[n + e];
+            v[4 + e] = kacc[hf][2 * p + 1][e] + sbkv[n + 4 + e];
+          }
+          *reinterpret_cast<uint4*>(g.kv + m * g.ldkv + n) = pack8(v);
+        }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int n = 32 * p + 8 * lg;
+        float* cp = g.x2 + m * FB_D + n;
+        *reinterpret_cast<float4*>(cp) = make_float4(vr[8 * p], vr[8 * p + 1], vr[8 * p + 2], vr[8 * p + 3]);
+        *reinterpret_cast<float4*>(cp + 4) =
+            make_float4(vr[8 * p + 4], vr[8 * p + 5], vr[8 * p + 6], vr[8 * p + 7]);
+        *reinterpret_cast<uint4*>(g.y + m * FB_D + n) = yq[p];
+      }
+      if (lg == 0) {
+        g.mean[m] = mu;
+        g.rstd[m] = rs;
+      }
+    }
+  } else if (mok) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int n = 32 * p + 8 * lg;
@@ -625,14 +709,19 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
   TTMI_TSTAMP(6);
 }
 
-template <int NG>
-void launch_ffn(const FfnArgs& a, hipStream_t s) {
+template <int NG, bool KV>
+void launch_ffn_kv(const FfnArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)((a.M + 127) / 128));       // 8 waves, one 16-row tile each
   static const bool pipe = !getenv("TTMI_FFN_NOPIPE");  // (A/B: the unpipelined group loop)
-  if (pipe && a.df.on) hipLaunchKernelGGL((ffn_block_kernel<8, NG, true, true>), grid, dim3(512), 0, s, a);
-  else if (pipe) hipLaunchKernelGGL((ffn_block_kernel<8, NG, true, false>), grid, dim3(512), 0, s, a);
-  else if (a.df.on) hipLaunchKernelGGL((ffn_block_kernel<8, NG, false, true>), grid, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL((ffn_block_kernel<8, NG, false, false>), grid, dim3(512), 0, s, a);
+  if (pipe && a.df.on) hipLaunchKernelGGL((ffn_block_kernel<8, NG, true, true, KV>), grid, dim3(512), 0, s, a);
+  else if (pipe) hipLaunchKernelGGL((ffn_block_kernel<8, NG, true, false, KV>), grid, dim3(512), 0, s, a);
+  else if (a.df.on) hipLaunchKernelGGL((ffn_block_kernel<8, NG, false, true, KV>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((ffn_block_kernel<8, NG, false, false, KV>), grid, dim3(512), 0, s, a);
+}
+template <int NG>
+void launch_ffn(const FfnArgs& a, hipStream_t s) {
+  if (a.kv) launch_ffn_kv<NG, true>(a, s);
+  else launch_ffn_kv<NG, false>(a, s);
 }
 
 }  // namespace
@@ -666,6 +755,13 @@ extern "C" int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t s) {
   a.df = make_drop(d->dropf_p, d->dropf_seed);
   a.d2 = make_drop(d->drop2_p, d->drop2_seed);
   a.M = d->M;
+  if (d->kv) {
+    TTMI_REQUIRE(d->wkv && d->bkv && d->ld_kv >= 2 * FB_D && d->ld_kv % 8 == 0 &&
+                     (((uintptr_t)d->kv | (uintptr_t)d->wkv | (uintptr_t)d->bkv) & 15) == 0,
+                 "%s: kv needs wkv [256, 128] bf16, bkv [256], 16-byte alignment and ld_kv >= 256, %% 8 == 0", fn);
+    TTMI_REQUIRE((int64_t)d->M * d->ld_kv < ((int64_t)1 << 31), "%s: kv rows past 2^31 elements", fn);
+    a.wkv = (const bf16_t*)d->wkv; a.bkv = d->bkv; a.kv = (bf16_t*)d->kv; a.ldkv = d->ld_kv;
+  }
   if (d->F == 512) launch_ffn<4>(a, s);
   else launch_ffn<2>(a, s);
   return ttmi_check_launch(fn);

@@ -214,6 +214,10 @@ _KVB = os.environ.get("TTMI_NO_KVB", "0") != "1"
 # row panel + ttmi_linear_res_ln pair (A/B measurements)
 _FFN = os.environ.get("TTMI_NO_FFN", "0") != "1"
 
+# the pruned layer's K / V projection inside the previous layer's FFN block (ABI 22);
+# TTMI_NO_FFN_KV=1 runs it as its own row-panel launch (A/B measurements)
+_FFN_KV = os.environ.get("TTMI_NO_FFN_KV", "0") != "1"
+
 
 def _lp(i: int) -> str:
     return f"transformer_encoder.layers.{i}."
@@ -251,8 +255,10 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
         return (torch.empty(R, D, device=dev, dtype=dt), torch.empty(R, **f32),
                 torch.empty(R, **f32))
 
-    # nxt: the next layer's norm1 output (a1, m1, r1) when a fused kernel already produced it
+    # nxt: the next layer's norm1 output (a1, m1, r1) when a fused kernel already produced it;
+    # nxt_qkv: the next (pruned) layer's qkv buffer whose K / V columns it also produced
     nxt = None
+    nxt_qkv = None
     norm1 = None
     if cfg.n_layers > 0 and dt == torch.bfloat16:
         nxt = ln_out(M)
@@ -270,17 +276,21 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
         else:
             a1, m1, r1 = ln_out(M)
             ops.layernorm_fwd(x, P[pre + "norm1.weight"], P[pre + "norm1.bias"], a1, m1, r1, eps=cfg.eps)
-        qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
         w_in, b_in = W[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"]
         fused_qa = not pruned and _qa_ok(w_in, a1, L, H)
         # the pruned layer reads Q at the gathered rows only: K / V over every row (a 256-column
-        # projection), Q inside the one-query attention launch (ABI 21)
+        # projection: inside the previous layer's FFN block launch when that ran, ABI 22), Q
+        # inside the one-query attention launch (ABI 21)
         proj_q1 = pruned and _q1_proj_ok(w_in, a1, L, H)
-        if proj_q1:
-            ops.gemm(a1, w_in[D:], qkv[:, D:], M, 2 * D, D, lda=D, a_kmajor=True, ldb=D, b_kmajor=True,
-                     ldc=3 * D, bias=b_in[D:])
-        elif not fused_qa:
-            ops.linear(a1, w_in, b_in, qkv)
+        if nxt_qkv is not None:
+            qkv, nxt_qkv = nxt_qkv, None
+        else:
+            qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
+            if proj_q1:
+                ops.gemm(a1, w_in[D:], qkv[:, D:], M, 2 * D, D, lda=D, a_kmajor=True, ldb=D, b_kmajor=True,
+                         ldc=3 * D, bias=b_in[D:])
+            elif not fused_qa:
+                ops.linear(a1, w_in, b_in, qkv)
         F_ = W[pre + "linear1.weight"].shape[0]
         if pruned:
             rows = torch.empty(B, device=dev, dtype=torch.int32)
@@ -368,12 +378,19 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
         if (not pruned and i + 1 < cfg.n_layers and _FFN and w1.dtype == torch.bfloat16
                 and W[name].dtype == torch.bfloat16 and R * F_ * 2 < (1 << 30)
                 and ops.ffn_block_supported(dt, D, F_)):
-            # FFN1 + ReLU / dropout + FFN2 + residual + the next layer's norm1, one launch
+            # FFN1 + ReLU / dropout + FFN2 + residual + the next layer's norm1, one launch; when the
+            # next layer is the pruned one, its K / V projection too
             nxt = ln_out(M)
             nx = _lp(i + 1)
+            kv = None
+            w_nx = W[nx + "self_attn.in_proj_weight"]
+            if (_FFN_KV and cfg.prune_last and i + 1 == cfg.n_layers - 1
+                    and _q1_proj_ok(w_nx, nxt[0], L, H)):
+                nxt_qkv = torch.empty(M, 3 * D, device=dev, dtype=dt)
+                kv = (w_nx[D:], P[nx + "self_attn.in_proj_bias"][D:], nxt_qkv[:, D:])
             ops.ffn_block_fwd(a2, w1, P[pre + "linear1.bias"], W[name], P[pre + "linear2.bias"], x1,
                               _drop(cfg, seeds, site_ffn(i)), _drop(cfg, seeds, site_drop2(i)), h, x2,
-                              P[nx + "norm1.weight"], P[nx + "norm1.bias"], cfg.eps, *nxt)
+                              P[nx + "norm1.weight"], P[nx + "norm1.bias"], cfg.eps, *nxt, kv=kv)
             st.layers.append(LayerSaved(x, a1, m1, r1, qkv, ctx, lse, x1, a2, m2, r2, h, rows))
             x = x2
             continue

@@ -155,13 +155,14 @@ class Q1KvBwdDesc(ctypes.Structure):
 
 
 class FfnBlockDesc(ctypes.Structure):
-    """ttmi_ffn_block_desc (include/ttmi.h, ABI 21)."""
+    """ttmi_ffn_block_desc (include/ttmi.h, ABI 21; kv fields ABI 22)."""
     _fields_ = [("M", c_i), ("D", c_i), ("F", c_i),
                 ("a", c_p), ("w1", c_p), ("b1", c_p), ("w2", c_p), ("b2", c_p), ("res", c_p),
                 ("dropf_p", ctypes.c_float), ("dropf_seed", c_p),
                 ("drop2_p", ctypes.c_float), ("drop2_seed", c_p),
                 ("h", c_p), ("x2", c_p), ("lnw", c_p), ("lnb", c_p), ("eps", ctypes.c_float),
-                ("y", c_p), ("mean", c_p), ("rstd", c_p)]
+                ("y", c_p), ("mean", c_p), ("rstd", c_p),
+                ("wkv", c_p), ("bkv", c_p), ("kv", c_p), ("ld_kv", c_i64)]
 
 
 class FfnBlockBwdDesc(ctypes.Structure):

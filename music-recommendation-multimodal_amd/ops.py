@@ -996,10 +996,13 @@ def ffn_block_supported(dtype: torch.dtype, D: int, F: int) -> bool:
 
 def ffn_block_fwd(a: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, res: Tensor,
                   drop_f: Drop, drop2: Drop, h: Tensor, x2: Tensor, lnw: Tensor, lnb: Tensor,
-                  eps: float, y: Tensor, mean: Tensor, rstd: Tensor) -> Tensor:
+                  eps: float, y: Tensor, mean: Tensor, rstd: Tensor,
+                  kv: Optional[Tuple[Tensor, Tensor, Tensor]] = None) -> Tensor:
     """The feed-forward sub-block and the next layer's norm1 in one launch (ttmi_ffn_block_fwd,
     ABI 21): h = drop_f(relu(a·w1ᵀ + b1)), x2 = res + drop2(h·w2ᵀ + b2), y = LN(x2) — as
-    linear(act=1) + linear_res_ln, with h never read back."""
+    linear(act=1) + linear_res_ln, with h never read back.  ``kv = (wkv, bkv, out)`` (ABI 22):
+    also out = y·wkvᵀ + bkv (wkv [2D, D] bf16, out a [M, 2D] bf16 view with unit column stride,
+    e.g. qkv[:, D:]): the next layer's K / V projection, the row panel's bits."""
     _dev(a, w1, b1, w2, b2, res, h, x2, lnw, lnb, y, mean, rstd)
     M, D = a.shape
     F = w1.shape[0]
@@ -1014,6 +1017,14 @@ def ffn_block_fwd(a: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, res
     d.drop2_p, d.drop2_seed = float(drop2[0]), _p(drop2[1])
     d.h, d.x2, d.lnw, d.lnb, d.eps = _p(h), _p(x2), _p(lnw), _p(lnb), float(eps)
     d.y, d.mean, d.rstd = _p(y), _p(mean), _p(rstd)
+    if kv is not None:
+        wkv, bkv, out = kv
+        if (tuple(wkv.shape) != (2 * D, D) or not wkv.is_contiguous() or wkv.dtype != torch.bfloat16
+                or tuple(bkv.shape) != (2 * D,) or tuple(out.shape) != (M, 2 * D) or out.stride(1) != 1
+                or out.dtype != torch.bfloat16):
+            raise ValueError("ffn_block_fwd: kv needs wkv [2D, D] bf16, bkv [2D], out [M, 2D] bf16 rows")
+        _dev(wkv, bkv, out)
+        d.wkv, d.bkv, d.kv, d.ld_kv = _p(wkv), _p(bkv.contiguous()), _p(out), out.stride(0)
     call("ttmi_ffn_block_fwd", ctypes.byref(d), _s())
     return x2
 

@@ -147,3 +147,49 @@ def test_ffn_block_bwd_matches_gated_linear_then_ln_bwd(gpu_pkg, M, F, p):
     assert torch.allclose(w1_, (dY * xh).sum(0), rtol=1e-3, atol=1e-3 * float(w1_.abs().max()))
     assert torch.allclose(b1_, dY.sum(0), rtol=1e-3, atol=1e-3 * float(b1_.abs().max()))
     assert torch.allclose(w1_, w0, rtol=1e-2, atol=1e-2 * float(w0.abs().max()))
+
+
+@pytest.mark.parametrize("M,F,p,pipe", [(25600, 512, 0.1, True), (2053, 512, 0.0, True), (2048, 256, 0.1, True),
+                                        (113, 256, 0.1, True), (4100, 512, 0.1, False)])
+def test_ffn_block_kv_projection(gpu_pkg, monkeypatch, M, F, p, pipe):
+    """ABI 22: the next (pruned) layer's K / V projection inside the FFN block launch.  The
+    launch's other outputs match the launch without it (h bit for bit), and kv is the K / V row
+    panel's (ttmi_gemm of y against in_proj rows D..3D, + bias) bits from M = 2048 rows; below
+    that the small-M GEMM sums in another order (bf16 rounding).  (TTMI_FFN_NOPIPE, the
+    unpipelined group loop, is read once per process: A/B runs only.)"""
+    ops = gpu_pkg.ops
+    if not pipe:
+        pytest.skip("TTMI_FFN_NOPIPE is read once per process; the unpipelined loop runs in A/B runs")
+    D = 128
+    g = torch.Generator().manual_seed(29 * M + F)
+    ops_in = _operands(M, F, g)
+    wkv = (torch.randn(2 * D, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    bkv = (torch.randn(2 * D, generator=g) * 0.1).to(DEV)
+    drop_f = (p, _seed(0xAF1 + M)) if p > 0 else (0.0, None)
+    drop2 = (p, _seed(0xAF2 + M)) if p > 0 else (0.0, None)
+    h0, x0, y0, mu0, rs0 = _run(ops, True, M, F, ops_in, drop_f, drop2)
+    a, w1, b1, w2, b2, res, lnw, lnb = ops_in
+    h = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    x2 = torch.empty(M, D, device=DEV)
+    y = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    mu, rs = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    qkv = torch.full((M, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.ffn_block_fwd(a, w1, b1, w2, b2, res, drop_f, drop2, h, x2, lnw, lnb, 1e-5, y, mu, rs,
+                      kv=(wkv, bkv, qkv[:, D:]))
+    torch.cuda.synchronize()
+    # h is bit-identical; x2 / LN to fp32 rounding (another instantiation: hipcc contracts the
+    # epilogue's a·b + c differently), y to one bf16 step
+    assert torch.equal(h0.view(torch.int16), h.view(torch.int16))
+    assert float((x2 - x0).abs().max()) <= 1e-6 * float(x0.abs().max())
+    assert float((mu - mu0).abs().max()) <= 1e-6 and float(((rs - rs0) / rs0).abs().max()) <= 1e-5
+    assert float((y.float() - y0.float()).abs().max()) <= 0.02 * float(y0.float().abs().max())
+    assert torch.isnan(qkv[:, :D].float()).all()                  # Q columns untouched
+    # the K / V row panel on the launch's own y
+    ref = torch.empty(M, 2 * D, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(y, wkv, ref, M, 2 * D, D, lda=D, a_kmajor=True, ldb=D, b_kmajor=True, ldc=2 * D, bias=bkv)
+    torch.cuda.synchronize()
+    got = qkv[:, D:].contiguous()
+    if M >= 2048:
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    else:
+        assert float((got.float() - ref.float()).abs().max()) <= 0.02 * float(ref.float().abs().max())
