@@ -317,9 +317,11 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   const int nblk = (a.B + HR - 1) / HR;
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  TTMI_TSTAMP(3);
   if (tid == 0)
     L.s_last = __hip_atomic_fetch_add(a.bncnt + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
   __syncthreads();
+  TTMI_TSTAMP(4);
   if (!L.s_last || tid >= 64) return;
   const int c = 64 * q + tid;
   // every load in flight first, the running statistics' read-modify-writes included (three
@@ -327,24 +329,33 @@ TTMI_DEV void item_a_body(const ItemArgs& a, int bx, int q, ItemLdsA& L) {
   const float rm0 = a.rmean ? a.rmean[c] : 0.f, rv0 = a.rvar ? a.rvar[c] : 0.f;
   const bool nbt_lane = q == 0 && tid == 0 && a.nbt;
   const int64_t nbt0 = nbt_lane ? a.nbt[0] : 0;
-  float pm[BN_MAXBLK], p2[BN_MAXBLK];
+  float pm[BN_MAXBLK], p2[BN_MAXBLK], pn[BN_MAXBLK];
 #pragma unroll
   for (int b = 0; b < BN_MAXBLK; ++b) {
     const int bb = min(b, nblk - 1);
     pm[b] = ld_agent(a.bnpart + (int64_t)(2 * bb) * IN1 + c);
     p2[b] = ld_agent(a.bnpart + (int64_t)(2 * bb + 1) * IN1 + c);
+    pn[b] = b < nblk ? (float)min(HR, a.B - HR * b) : 0.f;
   }
-  float n = 0.f, mean = 0.f, M2 = 0.f;
+  TTMI_TSTAMP_VAL(5, TTMI_TNOW() + (uint64_t)(pm[0] == 1234.5f) + (uint64_t)(p2[BN_MAXBLK - 1] == 1234.5f));
+  // Chan's pairwise update in a fixed tree order (blocks b and b + w, w = 1, 2, 4, ...): five
+  // dependent levels instead of a 32-step chain (2.7 us of the launch, phase stamps); the
+  // order is fixed, so the statistics are the same bits on every run
 #pragma unroll
-  for (int b = 0; b < BN_MAXBLK; ++b) {
-    if (b < nblk) {
-      const float nb = (float)min(HR, a.B - HR * b), tot = n + nb, delta = pm[b] - mean;
-      mean += delta * (nb / tot);
-      M2 += p2[b] + delta * delta * (n * nb / tot);
-      n = tot;
+  for (int w = 1; w < BN_MAXBLK; w <<= 1)
+#pragma unroll
+    for (int b = 0; b + w < BN_MAXBLK; b += 2 * w) {
+      const float na = pn[b], nb = pn[b + w];
+      if (nb > 0.f) {
+        const float tot = na + nb, f = nb / tot, delta = pm[b + w] - pm[b];
+        pm[b] += delta * f;
+        p2[b] += p2[b + w] + delta * delta * (na * f);
+        pn[b] = tot;
+      }
     }
-  }
+  const float mean = pm[0], M2 = p2[0];
   const float var = M2 / (float)a.B;
+  TTMI_TSTAMP_VAL(6, TTMI_TNOW() + (uint64_t)(var == 1234.5f));
   if (a.fin) {                                       // read by this launch's C workgroups
     st_agent(a.bmean + c, mean);
     st_agent(a.brstd + c, 1.f / sqrtf(var + a.bn_eps));
