@@ -78,7 +78,9 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
     const bool pad = c == FB_CPR - 1;
     oA[j] = pad ? (uint32_t)(16 * NWV * FB_D * 2) : (uint32_t)((n * FB_D + 8 * c) * 2);
     oW1[j] = pad ? wbytes : (uint32_t)((n * FB_D + 8 * c) * 2);
-    oW2[j] = pad ? wbytes : (uint32_t)((n * F + 8 * c) * 2);
+    // (slot c holds unit chunk 4 (c & 3) + (c >> 2): FFN2's lane group lg reads its four k-step
+    // chunks 4p + lg side by side, so a ds_read_b128's lane groups hit distinct banks)
+    oW2[j] = pad ? wbytes : (uint32_t)((n * F + 8 * (4 * (c & 3) + (c >> 2))) * 2);
   }
   auto slot = [&](int j) { int ii = wv + NWV * j; return ii >= FB_INS ? ii - FB_INS : ii; };
   auto issue_a = [&]() {                                 // the A tile -> buffer 1's W2 image
@@ -193,12 +195,12 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
     }
   };
   auto ffn2 = [&](int grp, const uint4 (&hq)[4]) {       // FFN2's k-steps over the group's units
-    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 16 * lg;
+    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 64 * lg;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
 #pragma unroll
       for (int t = 0; t < 8; ++t)
-        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 64 * p), hq[p]);
+        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * p), hq[p]);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -433,6 +435,300 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
   (void)twait;
 }
 
+// ------------------------------------------------------------------------------ D = 256
+// The same sub-block at the reference's default width (ABI 22): d_model 256, F = 1024
+// (src/train.py:289-297; user_tower.py:37-45).  128 rows a workgroup, F2_RT 16-row tiles a wave
+// (F2_NW = 8 / F2_RT waves); the weights stream through LDS in 16 groups of 64 hidden units —
+// the group's W1 rows [64][256] and W2 columns [256][64], 70 KB — double-buffered by LDS-DMA
+// under the previous group's MFMAs; the row tile (A, [128][256]) is staged in buffer 1 before its
+// first W group lands.  Each W fragment read from LDS feeds F2_RT MFMAs (one per row tile).
+// Measured at 25,600 rows (tools/ffn_time.py): RT 1 (8 waves) 58.6 us, RT 2 (4 waves, one a SIMD,
+// half the LDS reads) 72 us — the lone wave exposes its own latencies — so RT 1 ships; the
+// unfused pair takes 64.7 us.  FFN1's output fragment (row li, units
+// 32p + 8lg .. +7 of the group) is FFN2's B operand as at D = 128, so h never leaves the wave
+// between the GEMMs (it is stored once, for the backward).  The A / W1 fragments read k =
+// 128 (c >> 2) + 32 lg + 8 (c & 3) (c < 8) and the W2 image holds its unit chunks permuted, so
+// every ds_read_b128's lane groups hit distinct LDS banks.  x2 / y agree with the unfused row
+// panels to fp32 rounding, h to bf16 rounding (another k order).
+#ifndef F2_RT
+#define F2_RT 1                                      // 16-row tiles a wave
+#endif
+#ifndef F2_PF
+#define F2_PF 2                                      // W fragment stages (k-steps read ahead + 1;
+#endif                                               // 2, 3, 4 within 2 %)
+constexpr int F2_D = 256, F2_F = 1024, F2_GU = 64, F2_NG = F2_F / F2_GU;
+constexpr int F2_PA = 2 * F2_D + 16;                 // A / W1 image pitch (33 chunks)
+constexpr int F2_PW2 = 2 * F2_GU + 16;               // W2 image pitch (9 chunks)
+constexpr int F2_CA = F2_PA / 16, F2_CW2 = F2_PW2 / 16;
+constexpr int F2_W1IMG = F2_GU * F2_PA;              // 33,792 B
+constexpr int F2_W2IMG = F2_D * F2_PW2;              // 36,864 B
+constexpr int F2_BUF = F2_W1IMG + F2_W2IMG;          // 70,656 B
+constexpr int F2_AIMG = 128 * F2_PA;                 // 67,584 B (in buffer 1)
+constexpr int F2_IA = 128 * F2_CA / 64;              // 66 DMA wave-instructions
+constexpr int F2_IW1 = F2_GU * F2_CA / 64;           // 33
+constexpr int F2_IW2 = F2_D * F2_CW2 / 64;           // 36
+constexpr int F2_NW = 8 / F2_RT;
+constexpr int F2_PAW = (F2_IA + F2_NW - 1) / F2_NW;  // per wave (RT 1: 9, 5, 5)
+constexpr int F2_P1W = (F2_IW1 + F2_NW - 1) / F2_NW;
+constexpr int F2_P2W = (F2_IW2 + F2_NW - 1) / F2_NW;
+constexpr int F2_PAR = 9;                            // 1 KB parameter slots: b1 x4 | b2 | lnw | lnb | 2 seeds
+constexpr int F2_PPW = (F2_PAR + F2_NW - 1) / F2_NW;
+static_assert(F2_AIMG <= F2_BUF, "the A tile fits buffer 1");
+static_assert(F2_IA * 64 == 128 * F2_CA && F2_IW1 * 64 == F2_GU * F2_CA && F2_IW2 * 64 == F2_D * F2_CW2,
+              "whole DMA instructions");
+static_assert(2 * F2_RT + F2_P1W + F2_P2W <= 63, "vmcnt immediate");
+
+template <bool DF>
+__global__ __launch_bounds__(F2_NW * 64) void ffn256_block_kernel(FfnArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * F2_BUF + F2_PAR * 1024];
+  char* const spar = smem + 2 * F2_BUF;
+  TTMI_TSTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int64_t r0 = (int64_t)blockIdx.x * 128;
+  int64_t m[F2_RT], mc[F2_RT];                           // row tile rt: rows 16 (RT wave + rt) + li
+  bool mok[F2_RT];
+#pragma unroll
+  for (int rt = 0; rt < F2_RT; ++rt) {
+    m[rt] = r0 + 16 * (F2_RT * wave + rt) + li;
+    mok[rt] = m[rt] < g.M;
+    mc[rt] = mok[rt] ? m[rt] : (int64_t)g.M - 1;
+  }
+  const uint32_t w1bytes = (uint32_t)F2_F * F2_D * 2, w2bytes = (uint32_t)F2_D * F2_F * 2;
+  const uint32_t abytes = (uint32_t)min<int64_t>(128, g.M - r0) * F2_D * 2;
+  const i32x4_t r1 = make_rsrc(g.w1, w1bytes), r2 = make_rsrc(g.w2, w2bytes);
+  const i32x4_t ra = make_rsrc(g.a + r0 * F2_D, abytes);           // rows past M: zeros
+  // slot j of a batch of NI wave-instructions: ii = wave + NW j (re-issued mod NI: every wave
+  // issues the same count, so one vmcnt immediate serves all)
+  auto slot = [&](int j, int ni) { int ii = wv + F2_NW * j; return ii >= ni ? ii - ni : ii; };
+  uint32_t oW1[F2_P1W], oW2[F2_P2W];
+#pragma unroll
+  for (int j = 0; j < F2_P1W; ++j) {
+    const int q = slot(j, F2_IW1) * 64 + lane, n = q / F2_CA, c = q % F2_CA;
+    oW1[j] = c == F2_CA - 1 ? w1bytes : (uint32_t)((n * F2_D + 8 * c) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < F2_P2W; ++j) {
+    const int q = slot(j, F2_IW2) * 64 + lane, n = q / F2_CW2, c = q % F2_CW2;
+    // slot c holds unit chunk 4 ((c >> 1) & 1) + 2 (c & 1) + (c >> 2) (conflict-free FFN2 reads)
+    oW2[j] = c == F2_CW2 - 1 ? w2bytes
+                             : (uint32_t)((n * F2_F + 8 * (4 * ((c >> 1) & 1) + 2 * (c & 1) + (c >> 2))) * 2);
+  }
+  auto issue_w = [&](int grp) {                          // W1 rows / W2 columns [64 grp, +64)
+    const uint32_t base = lds_addr(smem + (grp & 1) * F2_BUF);
+#pragma unroll
+    for (int j = 0; j < F2_P1W; ++j)
+      dma16(r1, oW1[j] + (uint32_t)(grp * F2_GU * F2_D * 2), base + slot(j, F2_IW1) * 1024);
+#pragma unroll
+    for (int j = 0; j < F2_P2W; ++j)
+      dma16(r2, oW2[j] + (uint32_t)(grp * F2_GU * 2), base + F2_W1IMG + slot(j, F2_IW2) * 1024);
+  };
+  {                                                      // parameters
+    const uint32_t off = (uint32_t)(lane * 16);
+#pragma unroll
+    for (int h = 0; h < F2_PPW; ++h) {
+      int k = wv + F2_NW * h;
+      if (k >= F2_PAR) k -= F2_PAR;
+      const uint32_t dst = lds_addr(spar) + (uint32_t)(k * 1024);
+      if (k < 4) dma16(make_rsrc(g.b1, F2_F * 4), off + (uint32_t)(k * 1024), dst);
+      else if (k == 4) dma16(make_rsrc(g.b2, F2_D * 4), off, dst);
+      else if (k == 5) dma16(make_rsrc(g.lnw, F2_D * 4), off, dst);
+      else if (k == 6) dma16(make_rsrc(g.lnb, F2_D * 4), off, dst);
+      else if (k == 7) dma16(make_rsrc(g.df.seed, g.df.on ? 8 : 0), off, dst);
+      else dma16(make_rsrc(g.d2.seed, g.d2.on ? 8 : 0), off, dst);
+    }
+  }
+  {
+    const uint32_t base = lds_addr(smem + F2_BUF);
+#pragma unroll
+    for (int j = 0; j < F2_PAW; ++j) {
+      const int ii = slot(j, F2_IA), q = ii * 64 + lane, n = q / F2_CA, c = q % F2_CA;
+      dma16(ra, c == F2_CA - 1 ? (uint32_t)(128 * F2_D * 2) : (uint32_t)((n * F2_D + 8 * c) * 2),
+            base + ii * 1024);
+    }
+  }
+  issue_w(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  TTMI_TSTAMP(1);
+  const float* sb1 = reinterpret_cast<const float*>(spar);
+  const float* sb2 = reinterpret_cast<const float*>(spar + 4096);
+  const float* slw = reinterpret_cast<const float*>(spar + 5120);
+  const float* slb = reinterpret_cast<const float*>(spar + 6144);
+  DropKeys dkf, dk2;
+  {
+    const uint64_t sf = *reinterpret_cast<const uint64_t*>(spar + 7168);
+    const uint64_t s2 = *reinterpret_cast<const uint64_t*>(spar + 8192);
+    dkf = DropKeys{(uint32_t)sf, (uint32_t)(sf >> 32), g.df.thresh, g.df.scale, DF};
+    dk2 = DropKeys{(uint32_t)s2, (uint32_t)(s2 >> 32), g.d2.thresh, g.d2.scale, g.d2.on};
+  }
+  // k-step c, lane group lg: k = 128 (c >> 2) + 32 lg + 8 (c & 3) (the D = 128 permutation per
+  // 128-k half: with the 33-chunk pitch a ds_read_b128's lane groups hit distinct banks)
+  auto koff = [&](int c) { return 256 * (c >> 2) + 64 * lg + 16 * (c & 3); };
+  uint4 af[F2_RT][8];
+#pragma unroll
+  for (int rt = 0; rt < F2_RT; ++rt)
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      af[rt][c] = lds16(smem + F2_BUF + (16 * (F2_RT * wave + rt) + li) * F2_PA + koff(c));
+  __syncthreads();                                       // every wave has its A fragments
+  issue_w(1);                                            // over the A tile
+  const int wrow = 8 * (li >> 2) + (li & 3);             // column-paired rows (the panel layout)
+  const __amdgpu_buffer_rsrc_t rh =
+      __builtin_amdgcn_make_buffer_rsrc(g.h, 0, (int)((int64_t)g.M * F2_F * 2), 0x00020000);
+  f32x4_t acc2[F2_RT][16];
+#pragma unroll
+  for (int rt = 0; rt < F2_RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc2[rt][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float4 rpre[F2_RT][16];
+  // One group.  The W fragments are read F2_PF - 1 k-steps ahead of their MFMAs into explicit
+  // register stages (a read, then its MFMA, back to back, exposes the LDS latency on every MFMA).
+  auto group = [&](int grp, bool last) {
+    const char* bufp = smem + (grp & 1) * F2_BUF;
+    if (last) {                                          // x1's rows for the epilogue (behind this
+#pragma unroll                                           // group's MFMAs)
+      for (int rt = 0; rt < F2_RT; ++rt) {
+        const float* rp = g.res + mc[rt] * F2_D + 8 * lg;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          rpre[rt][2 * q] = *reinterpret_cast<const float4*>(rp + 32 * q);
+          rpre[rt][2 * q + 1] = *reinterpret_cast<const float4*>(rp + 32 * q + 4);
+        }
+      }
+    }
+    const char* w1b = bufp + wrow * F2_PA;
+    const char* w2b = bufp + F2_W1IMG + wrow * F2_PW2 + 16 * (4 * (lg & 1) + (lg >> 1));
+    auto ld1 = [&](int c, uint4 (&f)[4]) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) f[t] = lds16(w1b + (32 * (t >> 1) + 4 * (t & 1)) * F2_PA + koff(c));
+    };
+    auto ld2 = [&](int j, uint4 (&f)[4]) {              // FFN2 chunk j: k-step p = j >> 2, tiles 4 (j & 3) + u
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = 4 * (j & 3) + u;
+        f[u] = lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * F2_PW2 + 32 * (j >> 2));
+      }
+    };
+    // ---- FFN1: the tiles' rows x the group's 64 hidden units
+    f32x4_t acc1[F2_RT][4];
+#pragma unroll
+    for (int rt = 0; rt < F2_RT; ++rt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc1[rt][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    uint4 wf[F2_PF][4];
+#pragma unroll
+    for (int c = 0; c < F2_PF - 1; ++c) ld1(c, wf[c]);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int c2 = c + F2_PF - 1;
+      if (c2 < 8) ld1(c2, wf[c2 % F2_PF]);
+      else ld2(c2 - 8, wf[c2 % F2_PF]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rt = 0; rt < F2_RT; ++rt) Mma<bf16_t>::run(acc1[rt][t], wf[c % F2_PF][t], af[rt][c]);
+    }
+    // ---- h = drop_f(relu(. + b1)), bf16: FFN2's operand and the stored activation
+    uint4 hq[F2_RT][2];
+#pragma unroll
+    for (int rt = 0; rt < F2_RT; ++rt)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int n = F2_GU * grp + 32 * p + 8 * lg;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = fmaxf(acc1[rt][2 * p][e] + sb1[n + e], 0.f);
+          v[4 + e] = fmaxf(acc1[rt][2 * p + 1][e] + sb1[n + 4 + e], 0.f);
+        }
+        if (DF) drop_apply_vec<8>(dkf, (uint32_t)(m[rt] * F2_F + n), v);
+        hq[rt][p] = pack8(v);
+        const i32x4_t q = {(int)hq[rt][p].x, (int)hq[rt][p].y, (int)hq[rt][p].z, (int)hq[rt][p].w};
+        __builtin_amdgcn_raw_buffer_store_b128(q, rh, (uint32_t)((m[rt] * F2_F + n) * 2), 0, 0);
+      }
+    // ---- FFN2's k-steps over the group's units, 8 chunks of 4 fragments
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int j2 = j + F2_PF - 1;
+      if (j2 < 8) ld2(j2, wf[(j2 + 8) % F2_PF]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int rt = 0; rt < F2_RT; ++rt)
+          Mma<bf16_t>::run(acc2[rt][4 * (j & 3) + u], wf[(j + 8) % F2_PF][u], hq[rt][j >> 2]);
+    }
+    if (!last) {
+      __syncthreads();                                   // every wave is done with this buffer
+      // group grp + 1 landed; younger: this group's 2 RT h stores and group grp + 2's DMAs
+      if (grp + 2 < F2_NG) {
+        issue_w(grp + 2);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * F2_RT + F2_P1W + F2_P2W) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * F2_RT) : "memory");
+      }
+      __syncthreads();                                   // group grp + 1's images landed
+    }
+  };
+#pragma unroll 1
+  for (int grp = 0; grp < F2_NG - 1; ++grp) group(grp, false);
+  group(F2_NG - 1, true);
+  TTMI_TSTAMP(2);
+  // ---- x2 = x1 + drop2(. + b2); y = LN(x2) (a row's 256 columns in lanes li, li+16, li+32, li+48)
+#pragma unroll
+  for (int rt = 0; rt < F2_RT; ++rt) {
+    float vr[64];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int n = 32 * q + 8 * lg;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc2[rt][2 * q][e] + sb2[n + e];
+        v[4 + e] = acc2[rt][2 * q + 1][e] + sb2[n + 4 + e];
+      }
+      drop_apply_vec<8>(dk2, (uint32_t)(m[rt] * F2_D + n), v);
+      const float4 a0 = rpre[rt][2 * q], a1 = rpre[rt][2 * q + 1];
+      v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w;
+      v[4] += a1.x; v[5] += a1.y; v[6] += a1.z; v[7] += a1.w;
+      if (mok[rt]) {
+        float* cp = g.x2 + m[rt] * F2_D + n;
+        *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vr[8 * q + e] = v[e];
+    }
+    float s1 = 0.f;                                      // two-pass mean / variance (as ln_fwd)
+#pragma unroll
+    for (int e = 0; e < 64; ++e) s1 += vr[e];
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    const float mu = s1 * (1.f / F2_D);
+    float s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) s2 += (vr[e] - mu) * (vr[e] - mu);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const float rs = 1.f / sqrtf(s2 * (1.f / F2_D) + g.eps);
+    if (mok[rt]) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int n = 32 * q + 8 * lg;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (vr[8 * q + e] - mu) * rs * slw[n + e] + slb[n + e];
+        *reinterpret_cast<uint4*>(g.y + m[rt] * F2_D + n) = pack8(o);
+      }
+      if (lg == 0) {
+        g.mean[m[rt]] = mu;
+        g.rstd[m[rt]] = rs;
+      }
+    }
+  }
+  TTMI_TSTAMP(3);
+}
+
 // ------------------------------------------------------------------------------ backward
 // The sub-block's input-grad half (ABI 21, ttmi_ffn_block_bwd): the same two back-to-back GEMMs
 // on the transposed weight mirrors — W2ᵀ [F, D] has the forward W1's layout, W1ᵀ [D, F] the
@@ -481,7 +777,9 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
     const bool pad = c == FB_CPR - 1;
     oA[j] = pad ? (uint32_t)(16 * NWV * FB_D * 2) : (uint32_t)((n * FB_D + 8 * c) * 2);
     oW1[j] = pad ? wbytes : (uint32_t)((n * FB_D + 8 * c) * 2);
-    oW2[j] = pad ? wbytes : (uint32_t)((n * F + 8 * c) * 2);
+    // (slot c holds unit chunk 4 (c & 3) + (c >> 2): FFN2's lane group lg reads its four k-step
+    // chunks 4p + lg side by side, so a ds_read_b128's lane groups hit distinct banks)
+    oW2[j] = pad ? wbytes : (uint32_t)((n * F + 8 * (4 * (c & 3) + (c >> 2))) * 2);
   }
   auto slot = [&](int j) { int ii = wv + NWV * j; return ii >= FB_INS ? ii - FB_INS : ii; };
   auto issue_group = [&](int grp) {      // W2ᵀ rows [128 grp, +128), W1ᵀ columns [128 grp, +128)
@@ -562,7 +860,7 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
 #pragma unroll
   for (int grp = 0; grp < NG; ++grp) {
     const char* w1b = smem + (grp & 1) * FB_BUF + wrow * FB_P + 64 * lg;
-    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 16 * lg;
+    const char* w2b = smem + (grp & 1) * FB_BUF + FB_IMG + wrow * FB_P + 64 * lg;
     f32x4_t acc1[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc1[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -595,7 +893,7 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
     for (int p = 0; p < 4; ++p) {
 #pragma unroll
       for (int t = 0; t < 8; ++t)
-        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 64 * p), hq[p]);
+        Mma<bf16_t>::run(acc2[t], lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * FB_P + 16 * p), hq[p]);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (grp + 1 < NG) {
@@ -729,6 +1027,10 @@ void launch_ffn(const FfnArgs& a, hipStream_t s) {
 TTMI_STAMP_DUMP(ffn)
 
 extern "C" int ttmi_ffn_block_supported(int dtype, int D, int F) {
+  return dtype == TTMI_BF16 && ((D == FB_D && (F == 256 || F == 512)) || (D == F2_D && F == F2_F));
+}
+
+extern "C" int ttmi_ffn_block_bwd_supported(int dtype, int D, int F) {
   return dtype == TTMI_BF16 && D == FB_D && (F == 256 || F == 512);
 }
 
@@ -736,9 +1038,10 @@ extern "C" int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t s) {
   static const char* fn = "ttmi_ffn_block_fwd";
   TTMI_REQUIRE(d != nullptr, "%s: null descriptor", fn);
   TTMI_REQUIRE(ttmi_ffn_block_supported(TTMI_BF16, d->D, d->F),
-               "%s: serves D = 128 with F in {256, 512} (got D=%d F=%d); use ttmi_linear + "
-               "ttmi_linear_res_ln", fn, d->D, d->F);
+               "%s: serves D = 128 with F in {256, 512}, D = 256 with F = 1024 (got D=%d F=%d); use "
+               "ttmi_linear + ttmi_linear_res_ln", fn, d->D, d->F);
   TTMI_REQUIRE(d->M >= 0, "%s: M < 0", fn);
+  TTMI_REQUIRE(!d->kv || d->D == FB_D, "%s: the fused K / V projection serves D = 128", fn);
   TTMI_REQUIRE((int64_t)d->M * d->F * 2 + 16 * d->F * 2 * 8 < ((int64_t)1 << 31),
                "%s: [M, F] bf16 must stay under 2 GB (32-bit buffer offsets; got M=%d)", fn, d->M);
   TTMI_REQUIRE(d->a && d->w1 && d->b1 && d->w2 && d->b2 && d->res && d->h && d->x2 && d->lnw && d->lnb && d->y &&
@@ -762,8 +1065,15 @@ extern "C" int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t s) {
     TTMI_REQUIRE((int64_t)d->M * d->ld_kv < ((int64_t)1 << 31), "%s: kv rows past 2^31 elements", fn);
     a.wkv = (const bf16_t*)d->wkv; a.bkv = d->bkv; a.kv = (bf16_t*)d->kv; a.ldkv = d->ld_kv;
   }
-  if (d->F == 512) launch_ffn<4>(a, s);
-  else launch_ffn<2>(a, s);
+  if (d->D == F2_D) {
+    const dim3 grid((unsigned)((d->M + 127) / 128));
+    if (a.df.on) hipLaunchKernelGGL(ffn256_block_kernel<true>, grid, dim3(F2_NW * 64), 0, s, a);
+    else hipLaunchKernelGGL(ffn256_block_kernel<false>, grid, dim3(F2_NW * 64), 0, s, a);
+  } else if (d->F == 512) {
+    launch_ffn<4>(a, s);
+  } else {
+    launch_ffn<2>(a, s);
+  }
   return ttmi_check_launch(fn);
 }
 
@@ -772,7 +1082,7 @@ extern "C" int ttmi_ffn_block_bwd_sum_blocks(int M) { return M > 0 ? (M + 127) /
 extern "C" int ttmi_ffn_block_bwd(const ttmi_ffn_block_bwd_desc* d, hipStream_t s) {
   static const char* fn = "ttmi_ffn_block_bwd";
   TTMI_REQUIRE(d != nullptr, "%s: null descriptor", fn);
-  TTMI_REQUIRE(ttmi_ffn_block_supported(TTMI_BF16, d->D, d->F),
+  TTMI_REQUIRE(ttmi_ffn_block_bwd_supported(TTMI_BF16, d->D, d->F),
                "%s: serves D = 128 with F in {256, 512} (got D=%d F=%d); use ttmi_linear + "
                "ttmi_linear_ln_bwd", fn, d->D, d->F);
   TTMI_REQUIRE(d->M >= 0, "%s: M < 0", fn);

@@ -274,6 +274,7 @@ SIGNATURES = {
     "ttmi_mha_bwd_dy": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_attn_block_fwd": (c_i, [c_p, c_p]),
     "ttmi_ffn_block_supported": (c_i, [c_i, c_i, c_i]),
+    "ttmi_ffn_block_bwd_supported": (c_i, [c_i, c_i, c_i]),
     "ttmi_ffn_block_fwd": (c_i, [c_p, c_p]),
     "ttmi_ffn_block_bwd_sum_blocks": (c_i, [c_i]),
     "ttmi_ffn_block_bwd": (c_i, [c_p, c_p]),

@@ -984,13 +984,15 @@ def attn_block_fwd(a: Tensor, w_in: Tensor, b_in: Tensor, key_valid: Tensor, B: 
 _FFN_OK: dict = {}
 
 
-def ffn_block_supported(dtype: torch.dtype, D: int, F: int) -> bool:
-    """Whether ttmi_ffn_block_fwd serves this (dtype, D, F)."""
+def ffn_block_supported(dtype: torch.dtype, D: int, F: int, bwd: bool = False) -> bool:
+    """Whether ttmi_ffn_block_fwd (``bwd``: ttmi_ffn_block_bwd) serves this (dtype, D, F).  The
+    forward serves D = 128 with F in {256, 512} and D = 256 with F = 1024; the backward D = 128."""
     if dtype not in (torch.bfloat16,):
         return False
-    key = (code(dtype), D, F)
+    key = (code(dtype), D, F, bwd)
     if key not in _FFN_OK:
-        _FFN_OK[key] = bool(_L.load().ttmi_ffn_block_supported(*key))
+        fn = _L.load().ttmi_ffn_block_bwd_supported if bwd else _L.load().ttmi_ffn_block_supported
+        _FFN_OK[key] = bool(fn(*key[:3]))
     return _FFN_OK[key]
 
 
@@ -1025,6 +1027,8 @@ def ffn_block_fwd(a: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, res
             raise ValueError("ffn_block_fwd: kv needs wkv [2D, D] bf16, bkv [2D], out [M, 2D] bf16 rows")
         _dev(wkv, bkv, out)
         d.wkv, d.bkv, d.kv, d.ld_kv = _p(wkv), _p(bkv.contiguous()), _p(out), out.stride(0)
+    if kv is not None and D != 128:
+        raise ValueError("ffn_block_fwd: the fused K / V projection serves D = 128")
     call("ttmi_ffn_block_fwd", ctypes.byref(d), _s())
     return x2
 

@@ -92,9 +92,47 @@ def test_ffn_block_no_dropout_vs_torch(gpu_pkg):
 
 def test_ffn_block_refuses_unserved(gpu_pkg):
     ops = gpu_pkg.ops
-    assert not ops.ffn_block_supported(torch.bfloat16, 256, 1024)
+    assert ops.ffn_block_supported(torch.bfloat16, 256, 1024)
+    assert not ops.ffn_block_supported(torch.bfloat16, 256, 1024, bwd=True)
+    assert ops.ffn_block_supported(torch.bfloat16, 128, 512, bwd=True)
+    assert not ops.ffn_block_supported(torch.bfloat16, 256, 512)
     assert not ops.ffn_block_supported(torch.bfloat16, 128, 384)
     assert not ops.ffn_block_supported(torch.float32, 128, 512)
+
+
+@pytest.mark.parametrize("M,p", [(25600, 0.1), (2053, 0.0), (2048, 0.1), (7, 0.1), (129, 0.0)])
+def test_ffn_block_d256(gpu_pkg, M, p):
+    """ABI 22: the D = 256, F = 1024 forward (the reference's default width) against
+    ttmi_linear(act=ReLU) + ttmi_linear_res_ln.  Its FFN1 fragments sum k in another order than
+    the row panel (panel256), so h agrees to bf16 rounding; x2 is checked exactly
+    against an fp32 restatement from the launch's own h, y / mean / rstd against the unfused
+    pair."""
+    ops = gpu_pkg.ops
+    D, F = 256, 1024
+    g = torch.Generator().manual_seed(41 * M + 3)
+    ops_in = _operands(M, F, g, D=D)
+    drop_f = (p, _seed(0xDF1 + M)) if p > 0 else (0.0, None)
+    drop2 = (p, _seed(0xDF2 + M)) if p > 0 else (0.0, None)
+    h0, x0, y0, mu0, rs0 = _run(ops, False, M, F, ops_in, drop_f, drop2, D=D)
+    h1, x1, y1, mu1, rs1 = _run(ops, True, M, F, ops_in, drop_f, drop2, D=D)
+    # identical dropout masks: zeros in the same places (a kept unit's pre-activation can round
+    # to zero in one sum order only: allow a handful)
+    z0, z1 = h0 == 0, h1 == 0
+    assert int((z0 ^ z1).sum()) <= max(4, M * F // 100000)
+    assert float((h1.float() - h0.float()).abs().max()) <= 2 ** -6 * float(h0.float().abs().max())
+    a, w1, b1, w2, b2, res, lnw, lnb = ops_in
+    ref = h1.float() @ w2.float().t() + b2
+    if p > 0:
+        keep2 = (x0 - res) != 0
+        ref = torch.where(keep2 | (ref == 0), ref / (1 - p), torch.zeros_like(ref))
+    ref = ref + res
+    tol = 2e-5 * float(ref.abs().max())
+    assert float((x1 - ref).abs().max()) <= max(tol, 1e-5) * 4
+    assert float((x1 - x0).abs().max()) <= 0.02
+    assert float((mu1 - mu0).abs().max()) <= 1e-3 and float(((rs1 - rs0) / rs0).abs().max()) <= 1e-2
+    yr = torch.nn.functional.layer_norm(x1, (D,), lnw, lnb, 1e-5)
+    assert float((y1.float() - yr).abs().max()) <= 0.03
+    assert float((mu1 - x1.mean(1)).abs().max()) <= 1e-5
 
 
 @pytest.mark.parametrize("M,F,p", [(25600, 512, 0.1), (2053, 512, 0.0), (2048, 256, 0.1), (7, 512, 0.1),
