@@ -306,7 +306,7 @@ int ttmi_ffn_block_supported(int dtype, int D, int F);
 /* ABI 22: the forward also serves D = 256 with F = 1024 (the reference's default width; its
  * A / W1 fragments read k = 128 (c >> 2) + 32 lg + 8 (c & 3), so h agrees with the FFN1 row panel to bf16 rounding
  * there); ttmi_ffn_block_bwd_supported(dtype, D, F) says which shapes the backward serves
- * (D = 128, F in {256, 512}). */
+ * (the same: D = 128 with F in {256, 512}, D = 256 with F = 1024). */
 int ttmi_ffn_block_bwd_supported(int dtype, int D, int F);
 int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t stream);
 /* Its input-grad half (ABI 21): on the transposed weight mirrors w2t = linear2.weightᵀ [F, D],

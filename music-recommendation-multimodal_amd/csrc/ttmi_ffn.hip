@@ -450,6 +450,9 @@ __global__ __launch_bounds__(NWV * 64) void ffn_block_kernel(FfnArgs g) {
 // 128 (c >> 2) + 32 lg + 8 (c & 3) (c < 8) and the W2 image holds its unit chunks permuted, so
 // every ds_read_b128's lane groups hit distinct LDS banks.  x2 / y agree with the unfused row
 // panels to fp32 rounding, h to bf16 rounding (another k order).
+#ifndef F2B_X1SEAM
+#define F2B_X1SEAM 1                                 // (backward: x1's row at the last seam; 0: in
+#endif                                               // the epilogue, 1.3 us slower)
 #ifndef F2_RT
 #define F2_RT 1                                      // 16-row tiles a wave
 #endif
@@ -1007,6 +1010,282 @@ __global__ __launch_bounds__(512) void ffn_block_bwd_kernel(FfnBwdArgs g) {
   TTMI_TSTAMP(6);
 }
 
+// ---------------------------------------------------------------- backward at D = 256
+// ffn_block_bwd_kernel's math at d_model 256, F = 1,024 (round 6), on ffn256_block_kernel's
+// geometry: W2ᵀ rows [64][256] and W1ᵀ columns [256][64] of a 64-unit group stream through the
+// forward's two 70 KB LDS buffers (same images, same conflict-free fragment orders), one 16-row
+// tile per wave, 8 waves, 128 rows a workgroup; the dy2 tile is staged in buffer 1.  x1's row is
+// loaded at the last seam, the residual grad's in the epilogue; norm2's weight / bias row sums go
+// through wave-private LDS slices of both (then free) buffers.  Measured at 25,600 rows
+// (tools/ffn_time.py): 76.1-76.6 us with its fold against 74.2-75.3 for the gated row panel +
+// ttmi_linear_ln_bwd pair — the h read and dz1 write (52 MB each) dominate either way and the
+// fused loop does not hide them — so the framework keeps the pair at D = 256 (functional.py);
+// the entry point serves the shape and is parity-tested.
+template <bool DROP1>
+__global__ __launch_bounds__(512) void ffn256_block_bwd_kernel(FfnBwdArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * F2_BUF + 2 * 1024];   // + LN weight | seed
+  __shared__ float sdw[8][F2_D], sdb[8][F2_D];
+  char* const spar = smem + 2 * F2_BUF;
+  TTMI_TSTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lg = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int64_t r0 = (int64_t)blockIdx.x * 128;
+  const int64_t m = r0 + 16 * wave + li;
+  const bool mok = m < g.M;
+  const int64_t mc = mok ? m : (int64_t)g.M - 1;
+  const uint32_t wbytes = (uint32_t)F2_F * F2_D * 2;     // W2ᵀ and W1ᵀ alike
+  const uint32_t abytes = (uint32_t)min<int64_t>(128, g.M - r0) * F2_D * 2;
+  const i32x4_t r1 = make_rsrc(g.w2t, wbytes), r2 = make_rsrc(g.w1t, wbytes);
+  const i32x4_t ra = make_rsrc(g.dy + r0 * F2_D, abytes);
+  auto slot = [&](int j, int ni) { int ii = wv + 8 * j; return ii >= ni ? ii - ni : ii; };
+  uint32_t oW1[F2_P1W], oW2[F2_P2W];
+#pragma unroll
+  for (int j = 0; j < F2_P1W; ++j) {
+    const int q = slot(j, F2_IW1) * 64 + lane, n = q / F2_CA, c = q % F2_CA;
+    oW1[j] = c == F2_CA - 1 ? wbytes : (uint32_t)((n * F2_D + 8 * c) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < F2_P2W; ++j) {
+    const int q = slot(j, F2_IW2) * 64 + lane, n = q / F2_CW2, c = q % F2_CW2;
+    oW2[j] = c == F2_CW2 - 1 ? wbytes
+                             : (uint32_t)((n * F2_F + 8 * (4 * ((c >> 1) & 1) + 2 * (c & 1) + (c >> 2))) * 2);
+  }
+  auto issue_group = [&](int grp) {                      // W2ᵀ rows / W1ᵀ columns [64 grp, +64)
+    const uint32_t base = lds_addr(smem + (grp & 1) * F2_BUF);
+#pragma unroll
+    for (int j = 0; j < F2_P1W; ++j)
+      dma16(r1, oW1[j] + (uint32_t)(grp * F2_GU * F2_D * 2), base + slot(j, F2_IW1) * 1024);
+#pragma unroll
+    for (int j = 0; j < F2_P2W; ++j)
+      dma16(r2, oW2[j] + (uint32_t)(grp * F2_GU * 2), base + F2_W1IMG + slot(j, F2_IW2) * 1024);
+  };
+  auto load_gate = [&](int grp, uint4 (&q)[2]) {         // h[m, 64 grp + 32p + 8lg ..]
+    const uint4* hp = reinterpret_cast<const uint4*>(g.h + mc * F2_F + F2_GU * grp + 8 * lg);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) q[p] = hp[4 * p];
+  };
+  uint4 hg[2], hn[2];
+  load_gate(0, hg);                                      // (from HBM: issued ahead of the DMAs)
+  {
+    const uint32_t dst = lds_addr(spar) + (uint32_t)(wv * 1024), off = (uint32_t)(lane * 16);
+    if (wv == 0) dma16(make_rsrc(g.lnw, F2_D * 4), off, dst);
+    else if (wv == 1) dma16(make_rsrc(g.d1.seed, g.d1.on ? 8 : 0), off, dst);
+  }
+  {                                                      // the dy2 tile -> buffer 1
+    const uint32_t base = lds_addr(smem + F2_BUF);
+#pragma unroll
+    for (int j = 0; j < F2_PAW; ++j) {
+      const int ii = slot(j, F2_IA), q = ii * 64 + lane, n = q / F2_CA, c = q % F2_CA;
+      dma16(ra, c == F2_CA - 1 ? (uint32_t)(128 * F2_D * 2) : (uint32_t)((n * F2_D + 8 * c) * 2),
+            base + ii * 1024);
+    }
+  }
+  issue_group(0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  auto koff = [&](int c) { return 256 * (c >> 2) + 64 * lg + 16 * (c & 3); };
+  uint4 af[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) af[c] = lds16(smem + F2_BUF + (16 * wave + li) * F2_PA + koff(c));
+  const float* slw = reinterpret_cast<const float*>(spar);
+  DropKeys dk1;
+  {
+    const uint64_t s1 = *reinterpret_cast<const uint64_t*>(spar + 1024);
+    dk1 = DropKeys{(uint32_t)s1, (uint32_t)(s1 >> 32), g.d1.thresh, g.d1.scale, DROP1};
+  }
+  __syncthreads();                                       // every wave has its dy2 fragments
+  issue_group(1);                                        // over the dy2 tile
+  load_gate(1, hn);
+  TTMI_TSTAMP(1);
+  const int wrow = 8 * (li >> 2) + (li & 3);
+  const __amdgpu_buffer_rsrc_t rdz =
+      __builtin_amdgcn_make_buffer_rsrc(g.dz1, 0, (int)((int64_t)g.M * F2_F * 2), 0x00020000);
+  f32x4_t acc2[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc2[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t xh[16];                                        // x1's row, then x̂ (epilogue)
+  auto group = [&](int grp, bool last) {
+    const char* bufp = smem + (grp & 1) * F2_BUF;
+    const char* w1b = bufp + wrow * F2_PA;
+    const char* w2b = bufp + F2_W1IMG + wrow * F2_PW2 + 16 * (4 * (lg & 1) + (lg >> 1));
+    auto ld1 = [&](int c, uint4 (&f)[4]) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) f[t] = lds16(w1b + (32 * (t >> 1) + 4 * (t & 1)) * F2_PA + koff(c));
+    };
+    auto ld2 = [&](int j, uint4 (&f)[4]) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = 4 * (j & 3) + u;
+        f[u] = lds16(w2b + (32 * (t >> 1) + 4 * (t & 1)) * F2_PW2 + 32 * (j >> 2));
+      }
+    };
+    // ---- dy2 · W2 over the group's 64 hidden units
+    f32x4_t acc1[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc1[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // (fragments read straight into their MFMAs: the forward's register stages, with the gate
+    // rows in flight beside them, spilled here)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      uint4 wf[4];
+      ld1(c, wf);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) Mma<bf16_t>::run(acc1[t], wf[t], af[c]);
+    }
+    // ---- dz1 = gate(acc): the row panel's PE_GATE_BF16 epilogue
+    uint4 hq[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = F2_GU * grp + 32 * p + 8 * lg;
+      const uint32_t qw[4] = {hg[p].x, hg[p].y, hg[p].z, hg[p].w};
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = 1.f * (e < 2 ? acc1[2 * p][2 * e] : acc1[2 * p + 1][2 * e - 4]) + 0.f;
+        v[2 * e + 1] = 1.f * (e < 2 ? acc1[2 * p][2 * e + 1] : acc1[2 * p + 1][2 * e - 3]) + 0.f;
+        v[2 * e] = __uint_as_float(qw[e] << 16) > 0.f ? v[2 * e] * g.sf : 0.f;
+        v[2 * e + 1] = __uint_as_float(qw[e] & 0xFFFF0000u) > 0.f ? v[2 * e + 1] * g.sf : 0.f;
+      }
+      hq[p] = pack8(v);
+      const i32x4_t q = {(int)hq[p].x, (int)hq[p].y, (int)hq[p].z, (int)hq[p].w};
+      __builtin_amdgcn_raw_buffer_store_b128(q, rdz, (uint32_t)((m * F2_F + n) * 2), 0, 0);
+    }
+    // ---- dY += dz1 · W1 over the group's units
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint4 wf[4];
+      ld2(j, wf);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Mma<bf16_t>::run(acc2[4 * (j & 3) + u], wf[u], hq[j >> 2]);
+    }
+    if (!last) {
+      __syncthreads();                                   // every wave is done with this buffer
+      // group grp + 1's images and gate rows; younger: this group's 2 dz1 stores
+      __builtin_amdgcn_s_waitcnt(0x0F72);                // vmcnt(2), expcnt / lgkmcnt not waited
+#pragma unroll
+      for (int p = 0; p < 2; ++p) hg[p] = hn[p];
+      if (grp + 2 < F2_NG) {
+        issue_group(grp + 2);
+        load_gate(grp + 2, hn);
+      }
+      if (F2B_X1SEAM && grp + 2 == F2_NG) {              // x1's row, behind the last group's MFMAs
+        const float* xp = g.x1 + mc * F2_D + 8 * lg;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float4 a0 = *reinterpret_cast<const float4*>(xp + 32 * q);
+          const float4 a1 = *reinterpret_cast<const float4*>(xp + 32 * q + 4);
+          xh[2 * q] = f32x4_t{a0.x, a0.y, a0.z, a0.w};
+          xh[2 * q + 1] = f32x4_t{a1.x, a1.y, a1.z, a1.w};
+        }
+      }
+      __syncthreads();                                   // every wave's part of the images landed
+    }
+  };
+#pragma unroll 1
+  for (int grp = 0; grp < F2_NG; ++grp) group(grp, grp + 1 == F2_NG);   // (a peeled last group,
+                                                                         // scheduled apart, spilled)
+  TTMI_TSTAMP(2);
+  // ---- norm2's backward of the finished rows (ttmi_linear_ln_bwd's PE_LNBWD epilogue).  x1's
+  // and the residual grad's rows are loaded here, not at the last seam: the last group's
+  // fragments, accumulators and stages leave no registers for them.  In place, to stay in
+  // registers: dY is acc2 (exactly 0 on rows past M: their dy2 rows arrive as zeros), x1's row
+  // becomes x̂ (0 on rows past M: mean and rstd 0 there).
+  __builtin_amdgcn_sched_barrier(0);
+  if (!F2B_X1SEAM) {
+    const float* xp = g.x1 + mc * F2_D + 8 * lg;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 a0 = *reinterpret_cast<const float4*>(xp + 32 * q);
+      const float4 a1 = *reinterpret_cast<const float4*>(xp + 32 * q + 4);
+      xh[2 * q] = f32x4_t{a0.x, a0.y, a0.z, a0.w};
+      xh[2 * q + 1] = f32x4_t{a1.x, a1.y, a1.z, a1.w};
+    }
+  }
+  const float mu = mok ? g.m2[mc] : 0.f, rs = mok ? g.r2[mc] : 0.f;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int n = 32 * (t >> 1) + 8 * lg + 4 * (t & 1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xh[t][e] = (xh[t][e] - mu) * rs;
+      const float gg = acc2[t][e] * slw[n + e];
+      s1 += gg;
+      s2 += gg * xh[t][e];
+    }
+  }
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  const float c1 = s1 * (1.f / F2_D), c2 = s2 * (1.f / F2_D);
+  __builtin_amdgcn_sched_barrier(0);
+  if (mok) {
+    const float* rp = g.res + m * F2_D + 8 * lg;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int n = 32 * q + 8 * lg;
+      const float4 q0 = *reinterpret_cast<const float4*>(rp + 32 * q);
+      const float4 q1 = *reinterpret_cast<const float4*>(rp + 32 * q + 4);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = rs * (acc2[2 * q][e] * slw[n + e] - c1 - xh[2 * q][e] * c2);
+        o[4 + e] = rs * (acc2[2 * q + 1][e] * slw[n + 4 + e] - c1 - xh[2 * q + 1][e] * c2);
+      }
+      o[0] += q0.x; o[1] += q0.y; o[2] += q0.z; o[3] += q0.w;
+      o[4] += q1.x; o[5] += q1.y; o[6] += q1.z; o[7] += q1.w;
+      float* dp = g.dx1 + m * F2_D + n;
+      *reinterpret_cast<float4*>(dp) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(dp + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      if (DROP1) drop_apply_vec<8>(dk1, (uint32_t)(m * F2_D + n), o);
+      *reinterpret_cast<uint4*>(g.dy1 + m * F2_D + n) = pack8(o);
+    }
+  }
+  TTMI_TSTAMP(3);
+  // LayerNorm weight / bias grads: the tile's 16 rows summed per column in row order through a
+  // wave-private LDS slice (16 rows x 260 floats) of the two W buffers, free once every wave is
+  // past its last group
+  __syncthreads();
+  {
+    constexpr int RS = F2_D + 4;
+    float* red = reinterpret_cast<float*>(smem) + wave * 16 * RS;
+    static_assert(8 * 16 * RS * 4 <= 2 * F2_BUF, "the slices fit the W buffers");
+#pragma unroll
+    for (int qd = 0; qd < 2; ++qd) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = acc2[2 * q + hf][e];
+            v[e] = qd == 0 ? d * xh[2 * q + hf][e] : d;
+          }
+          *reinterpret_cast<float4*>(red + li * RS + 32 * q + 8 * lg + 4 * hf) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);      // column group lane: columns 4 lane .. +3
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float4 w = *reinterpret_cast<const float4*>(red + r * RS + 4 * lane);
+        acc.x += w.x; acc.y += w.y; acc.z += w.z; acc.w += w.w;
+      }
+      *reinterpret_cast<float4*>((qd == 0 ? &sdw[wave][0] : &sdb[wave][0]) + 4 * lane) = acc;
+    }
+  }
+  __syncthreads();
+  if (tid < F2_D) {                                      // the waves' rows in wave order
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) { a += sdw[w][tid]; b += sdb[w][tid]; }
+    float* o = g.sum_ws + (int64_t)blockIdx.x * 2 * F2_D;
+    o[tid] = a;
+    o[F2_D + tid] = b;
+  }
+  TTMI_TSTAMP(4);
+}
+
 template <int NG, bool KV>
 void launch_ffn_kv(const FfnArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)((a.M + 127) / 128));       // 8 waves, one 16-row tile each
@@ -1031,7 +1310,7 @@ extern "C" int ttmi_ffn_block_supported(int dtype, int D, int F) {
 }
 
 extern "C" int ttmi_ffn_block_bwd_supported(int dtype, int D, int F) {
-  return dtype == TTMI_BF16 && D == FB_D && (F == 256 || F == 512);
+  return dtype == TTMI_BF16 && ((D == FB_D && (F == 256 || F == 512)) || (D == F2_D && F == F2_F));
 }
 
 extern "C" int ttmi_ffn_block_fwd(const ttmi_ffn_block_desc* d, hipStream_t s) {
@@ -1083,8 +1362,8 @@ extern "C" int ttmi_ffn_block_bwd(const ttmi_ffn_block_bwd_desc* d, hipStream_t 
   static const char* fn = "ttmi_ffn_block_bwd";
   TTMI_REQUIRE(d != nullptr, "%s: null descriptor", fn);
   TTMI_REQUIRE(ttmi_ffn_block_bwd_supported(TTMI_BF16, d->D, d->F),
-               "%s: serves D = 128 with F in {256, 512} (got D=%d F=%d); use ttmi_linear + "
-               "ttmi_linear_ln_bwd", fn, d->D, d->F);
+               "%s: serves D = 128 with F in {256, 512}, D = 256 with F = 1024 (got D=%d F=%d); use "
+               "ttmi_linear + ttmi_linear_ln_bwd", fn, d->D, d->F);
   TTMI_REQUIRE(d->M >= 0, "%s: M < 0", fn);
   TTMI_REQUIRE((int64_t)d->M * d->F * 2 + 16 * d->F * 2 * 8 < ((int64_t)1 << 31),
                "%s: [M, F] bf16 must stay under 2 GB (got M=%d)", fn, d->M);
@@ -1102,7 +1381,13 @@ extern "C" int ttmi_ffn_block_bwd(const ttmi_ffn_block_bwd_desc* d, hipStream_t 
   a.dx1 = d->dx1; a.dy1 = (bf16_t*)d->dy1; a.d1 = make_drop(d->drop1_p, d->drop1_seed); a.sum_ws = d->sum_ws;
   a.M = d->M;
   const dim3 grid((unsigned)((d->M + 127) / 128));
-  if (d->F == 512) hipLaunchKernelGGL(ffn_block_bwd_kernel<4>, grid, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(ffn_block_bwd_kernel<2>, grid, dim3(512), 0, s, a);
+  if (d->D == F2_D) {
+    if (a.d1.on) hipLaunchKernelGGL(ffn256_block_bwd_kernel<true>, grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(ffn256_block_bwd_kernel<false>, grid, dim3(512), 0, s, a);
+  } else if (d->F == 512) {
+    hipLaunchKernelGGL(ffn_block_bwd_kernel<4>, grid, dim3(512), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(ffn_block_bwd_kernel<2>, grid, dim3(512), 0, s, a);
+  }
   return ttmi_check_launch(fn);
 }

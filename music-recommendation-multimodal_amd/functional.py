@@ -631,7 +631,8 @@ def _layer_tail_bwd(P, W, s, dx, dy2_next, grads, cfg, seeds, i, pre, R, drows, 
     w1t = W.get(transposed_name(pre + "linear1.weight"))
     if (fuse and drows is None and _FFN and dt == torch.bfloat16 and w2t is not None and w1t is not None
             and w2t.dtype == torch.bfloat16 and w1t.dtype == torch.bfloat16 and R * F_ * 2 < (1 << 30)
-            and ops.ffn_block_supported(dt, D, F_, bwd=True)):
+            and D == 128 and ops.ffn_block_supported(dt, D, F_, bwd=True)):
+        # (D = 256: the fused backward is served but measured slower than the pair)
         # FFN2 input grad + ReLU / dropout gate + FFN1 input grad + norm2 backward, one launch
         dx1 = torch.empty(R, D, **f32)
         dy1 = torch.empty(R, D, device=dev, dtype=dt)

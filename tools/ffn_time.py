@@ -55,8 +55,11 @@ def main():
             gw, gb = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
             bwd = timeit(lambda: ops.ffn_block_bwd(dy2, w2t, w1t, h, 1 / 0.9, dz1, x1, mu, rs, lnw, x2, dx1, dy1,
                                                    drop, gw, gb))
-            print(f"D={D} F={F} M={M}: fused bwd {bwd:7.2f} us ({flop / bwd / 1e6:6.1f} TFLOP/s, with its folds)",
-                  flush=True)
+            b1 = timeit(lambda: ops.linear(dy2, w2t, None, dz1, gate=h, gate_scale=1 / 0.9))
+            b2 = timeit(lambda: ops.linear_ln_bwd(dz1, w1t, x1, mu, rs, lnw, dx1, gw, gb, res=x2, next_=dy1,
+                                                  drop=drop))
+            print(f"D={D} F={F} M={M}: fused bwd {bwd:7.2f} us ({flop / bwd / 1e6:6.1f} TFLOP/s, with its folds)   "
+                  f"unfused {b1:6.2f} + {b2:6.2f} = {b1 + b2:7.2f} us", flush=True)
 
 
 if __name__ == "__main__":
