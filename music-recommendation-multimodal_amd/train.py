@@ -244,6 +244,22 @@ class _Segments:
             self._ctx.__exit__(None, None, None)
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
 
+    def abort(self) -> None:
+        """Leave a capture that raised: end it (its graph is discarded) and the capture stream."""
+        if not self.capture:
+            return
+        if self.cur is not None:
+            try:
+                self.cur.capture_end()
+            except Exception:                 # an invalidated capture refuses to end cleanly
+                pass
+            self.cur = None
+        self.items = []
+        if getattr(self, "_ctx", None) is not None:
+            self._ctx.__exit__(None, None, None)
+            self._ctx = None
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
     def replay(self) -> None:
         for kind, x in self.items:
             if kind == "graph":
@@ -723,6 +739,25 @@ class TrainStep:
         for t, s in zip(self._state(), snap):   # undo the warm-up's state changes
             t.copy_(s)
         torch.cuda.synchronize(self.device)
+        try:
+            seg = self._record(b)
+        except Exception as exc:
+            if not self.capture_collectives:
+                raise
+            # Collectives recorded into the graph were refused at this world size (exercised on
+            # the GPU at world 1 only: RCCL needs a device per rank).  Fall back to the segmented
+            # schedule, collectives between graph replays, rather than fail the run.
+            logging.getLogger(__name__).warning(
+                "TrainStep: recording the collectives into the step graph failed (%s); "
+                "falling back to graph segments with the collectives between them", exc)
+            for t, s0 in zip(self._state(), snap):
+                t.copy_(s0)
+            torch.cuda.synchronize(self.device)
+            self.capture_collectives = False
+            seg = self._record(b)
+        e.seg, e.loss, e.logits = seg, self.loss, self.logits
+
+    def _record(self, b: Dict[str, Tensor]) -> _Segments:
         seg = _Segments(self.device, capture=True, pool=torch.cuda.graph_pool_handle(),
                         inline=self.capture_collectives)
         self._split_cuts = self.dp and not seg.inline
@@ -730,9 +765,12 @@ class TrainStep:
             seg.begin()
             self._body(b, seg.cut)
             seg.end()
+        except BaseException:
+            seg.abort()
+            raise
         finally:
             self._split_cuts = False
-        e.seg, e.loss, e.logits = seg, self.loss, self.logits
+        return seg
 
     def step(self, batch: Dict[str, Tensor]) -> Tensor:
         ops.check_id_errors()                  # bad ids of earlier (finished) steps: IndexError

@@ -208,6 +208,40 @@ def test_trainstep_forced_dp_schedule_rccl_bitexact(global_negatives):
     _run(_trainstep_worker, global_negatives)
 
 
+# ------------------------------------------------------------------ capture refused: segments
+def _fallback_worker():
+    """If recording the collectives into the step graph fails (untested at world > 1 here: RCCL
+    needs a device per rank), TrainStep falls back to graph segments with the collectives
+    between them instead of failing the run — same bits as the one-process step."""
+    pkg = importlib.import_module(PKG_NAME)
+    comm = pkg.comm
+    _init("nccl")
+    real = comm.all_reduce_sum
+    try:
+        base = _train(pkg, False)
+
+        def refusing(t, *a, **k):
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("collective refused under capture (test)")
+            return real(t, *a, **k)
+        comm.force_dp(True)
+        comm.all_reduce_sum = refusing
+        fb = _train(pkg, False)
+    finally:
+        comm.all_reduce_sum = real
+        comm.force_dp(False)
+        dist.destroy_process_group()
+    info = fb[3]
+    assert info[:2] == (True, False) and info[5] > 1, info     # DP, segments, several graphs
+    assert fb[1] == base[1] and fb[2] == base[2]
+    bad = [k for k in base[0] if not torch.equal(fb[0][k], base[0][k])]
+    assert not bad, bad[:8]
+
+
+def test_captured_collectives_fall_back_to_segments():
+    _run(_fallback_worker)
+
+
 # ------------------------------------------------------------------ a bad id on the DP schedule
 def _bad_id_worker():
     pkg = importlib.import_module(PKG_NAME)
