@@ -282,6 +282,7 @@ def _staged_timeout_worker(rank):
     old = comm.STAGED_TIMEOUT_S
     try:
         x = torch.ones(64)
+        dist.barrier()                            # both ranks imported: the 1.5 s lateness is relative
         if rank == 0:
             comm.STAGED_TIMEOUT_S = 0.3
             works = pkg.GradSync().start(x)
@@ -295,6 +296,8 @@ def _staged_timeout_worker(rank):
             time.sleep(1.5)                       # late: rank 0's wait gave up meanwhile
             dist.all_reduce(x)                    # completes rank 0's stuck reduction
         dist.barrier()
+        if rank == 0:                             # the stuck reduction's thread has returned from
+            works[0].fut.result(timeout=60)       # gloo before the group is torn down
     finally:
         comm.STAGED_TIMEOUT_S = old
         comm._FORCE_STAGE = False
