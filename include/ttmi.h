@@ -260,6 +260,19 @@ int ttmi_mha_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
 int ttmi_mha_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
                  const int64_t* key_valid, const float* lse, const void* dctx, float drop_p,
                  const uint64_t* drop_seed, void* dqkv, hipStream_t stream);
+/* The same attention for the shapes ttmi_mha_fwd / _bwd refuse (ABI 22, ttmi_attn_generic.hip):
+ * any L, head widths 0 < Dh <= 512 (not only multiples of 8 up to 64).  Same operands, masks,
+ * dropout indices and lse convention (natural log, +inf on a row with no allowed key); a wave
+ * per query row / key row, no tiling: the path that keeps a model the reference accepts
+ * trainable, not a fast one.  The backward also needs the forward's ctx rows (D_i = dO_i·O_i)
+ * and a float workspace of B·H·L (dsum_ws). */
+int ttmi_mha_generic_fwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                         const int64_t* key_valid, float drop_p, const uint64_t* drop_seed, void* ctx,
+                         float* lse, hipStream_t stream);
+int ttmi_mha_generic_bwd(int dtype, int B, int L, int H, int Dh, const void* qkv,
+                         const int64_t* key_valid, const float* lse, const void* ctx, const void* dctx,
+                         float drop_p, const uint64_t* drop_seed, float* dsum_ws, void* dqkv,
+                         hipStream_t stream);
 /* The encoder layer's whole attention sub-block forward in one launch (ABI 21; reference
  * user_tower.py:37-45, norm_first): ttmi_qkv_attn_fwd's qkv / ctx / lse, then
  *   x1 = res + drop1(ctx·woᵀ + bo)   (fp32 [B*L, 128]; drop1 index m·128 + n)

@@ -359,8 +359,10 @@ def user_tower_fwd(P: Dict[str, Tensor], W: Dict[str, Tensor], ids: Tensor, gend
             elif fused_qa:   # in_proj + attention, one launch (bit-identical to the pair at M >= 2048)
                 ops.qkv_attn_fwd(a1, w_in, b_in, key_valid, B, L, H, qkv, ctx, lse,
                                  _drop(cfg, seeds, site_attn(i)))
-            else:
+            elif ops.mha_tuned_supported(L, D // H):
                 ops.mha_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
+            else:            # head widths / lengths the tuned kernels refuse (the constructor unprunes)
+                ops.mha_generic_fwd(qkv, key_valid, B, L, H, ctx, lse, _drop(cfg, seeds, site_attn(i)))
         if block:
             pass
         elif not pruned and _resln_ok(W, name, D, R):    # out_proj + residual + norm2, one kernel
@@ -525,9 +527,12 @@ def user_tower_bwd(P: Dict[str, Tensor], W: Dict[str, Tensor], st: UserSaved, du
         elif dy_attn:      # (dctx holds dy1 here)
             ops.mha_bwd_dy(s.qkv, st.key_valid, s.lse, dctx, wot, B, L, H, dqkv,
                            _drop(cfg, seeds, site_attn(i)))
-        else:
+        elif ops.mha_tuned_supported(L, D // H):
             ops.mha_bwd(s.qkv, st.key_valid, s.lse, dctx, B, L, H, dqkv,
                         _drop(cfg, seeds, site_attn(i)))
+        else:
+            ops.mha_generic_bwd(s.qkv, st.key_valid, s.lse, s.ctx, dctx, B, L, H, dqkv,
+                                _drop(cfg, seeds, site_attn(i)))
         gw_in, gb_in = grads[pre + "self_attn.in_proj_weight"], grads[pre + "self_attn.in_proj_bias"]
         if kv_only:
             ops.linear_dw(dqkv[:, D:], s.a1, gw_in[D:], gb_in[D:])

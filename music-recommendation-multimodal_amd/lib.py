@@ -270,6 +270,8 @@ SIGNATURES = {
                                  c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_p]),
     "ttmi_mha_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_mha_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "ttmi_mha_generic_fwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
+    "ttmi_mha_generic_bwd": (c_i, [c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p]),
     "ttmi_qkv_attn_supported": (c_i, [c_i, c_i, c_i, c_i]),
     "ttmi_mha_bwd_dy": (c_i, [c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "ttmi_attn_block_fwd": (c_i, [c_p, c_p]),

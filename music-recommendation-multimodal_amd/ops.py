@@ -927,6 +927,35 @@ def mha_fwd(qkv: Tensor, key_valid: Tensor, B: int, L: int, H: int, ctx: Tensor,
     return ctx
 
 
+def mha_tuned_supported(L: int, Dh: int) -> bool:
+    """Whether ttmi_mha_fwd / _bwd (and the fused and one-query attention kernels) serve this
+    shape: L <= TTMI_ATTN_LMAX and Dh a multiple of 8 up to 64.  Other shapes run
+    mha_generic_fwd / _bwd."""
+    return 0 < L <= ATTN_LMAX and 0 < Dh <= 64 and Dh % 8 == 0
+
+
+def mha_generic_fwd(qkv: Tensor, key_valid: Tensor, B: int, L: int, H: int, ctx: Tensor, lse: Tensor,
+                    drop: Drop = NO_DROP) -> Tensor:
+    """ttmi_mha_generic_fwd: mha_fwd for any L and head widths up to 512 (ABI 22)."""
+    _dev(qkv, key_valid, ctx, lse)
+    Dh = qkv.shape[1] // (3 * H)
+    call("ttmi_mha_generic_fwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), float(drop[0]),
+         _p(drop[1]), _p(ctx), _p(lse), _s())
+    return ctx
+
+
+def mha_generic_bwd(qkv: Tensor, key_valid: Tensor, lse: Tensor, ctx: Tensor, dctx: Tensor, B: int, L: int,
+                    H: int, dqkv: Tensor, drop: Drop = NO_DROP) -> Tensor:
+    """ttmi_mha_generic_bwd: mha_bwd for the shapes mha_generic_fwd serves; needs the forward's
+    ctx rows."""
+    _dev(qkv, key_valid, lse, ctx, dctx, dqkv)
+    Dh = qkv.shape[1] // (3 * H)
+    ws = torch.empty(max(B * H * L, 1), device=qkv.device, dtype=torch.float32)
+    call("ttmi_mha_generic_bwd", code(qkv.dtype), B, L, H, Dh, _p(qkv), _p(key_valid), _p(lse), _p(ctx),
+         _p(dctx), float(drop[0]), _p(drop[1]), _p(ws), _p(dqkv), _s())
+    return dqkv
+
+
 _QA_OK: Dict[Tuple[int, int, int, int], bool] = {}
 
 

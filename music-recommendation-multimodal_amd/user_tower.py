@@ -135,15 +135,18 @@ class SequentialUserEncoder(nn.Module):
         super().__init__()
         if embedding_dim % num_heads:
             raise ValueError("embedding_dim must be divisible by num_heads")
-        # the attention kernels (ttmi_attn.hip) keep a whole sequence's K/V head slice in one
-        # workgroup's LDS up to 64 positions and tile longer ones over 64-key blocks
-        # (ttmi_attn_long.hip) up to TTMI_ATTN_LMAX: reject other shapes here, not mid-epoch
+        # the tuned attention kernels (ttmi_attn.hip) keep a whole sequence's K/V head slice in
+        # one workgroup's LDS up to 64 positions and tile longer ones over 64-key blocks
+        # (ttmi_attn_long.hip) up to TTMI_ATTN_LMAX, for head widths that are multiples of 8 up
+        # to 64.  Other shapes (the reference accepts any) run the generic attention kernels
+        # (ttmi_attn_generic.hip, ABI 22) on an unpruned last layer: correct, not fast.
         d_h = embedding_dim // num_heads
-        if not 0 < max_seq_len <= ATTN_LMAX:
-            raise ValueError(f"max_seq_len must be in [1, {ATTN_LMAX}] (got {max_seq_len})")
-        if d_h > 64 or d_h % 8:
-            raise ValueError(f"head width embedding_dim / num_heads must be a multiple of 8 "
-                             f"and <= 64 (got {d_h})")
+        if max_seq_len <= 0:
+            raise ValueError(f"max_seq_len must be positive (got {max_seq_len})")
+        if d_h > 512:
+            raise ValueError(f"head width embedding_dim / num_heads must be <= 512 (got {d_h})")
+        if not (max_seq_len <= ATTN_LMAX and d_h <= 64 and d_h % 8 == 0):
+            prune_last = False          # the one-query kernels serve the tuned shapes only
         self.embedding_dim = embedding_dim
         self.max_seq_len = max_seq_len
         self.num_heads = num_heads

@@ -379,6 +379,45 @@ def test_mha_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 1, 128), (5, 50, 2, 96), (3, 20, 1, 256), (4, 33, 3, 12),
+                                      (2, 70, 1, 500), (2, 2100, 1, 16), (3, 50, 4, 32)])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_mha_generic_fwd_bwd(gpu_pkg, dtype, B, L, H, Dh, p):
+    """ttmi_mha_generic_fwd / _bwd (ABI 22): the shapes the tuned kernels refuse — head widths
+    above 64 or not a multiple of 8, L past TTMI_ATTN_LMAX — against the torch restatement, with
+    the same masks (left-padded, empty and full rows) and dropout indices; (3, 50, 4, 32) is a
+    tuned shape, where it must agree with ttmi_mha_fwd / _bwd too."""
+    ops = gpu_pkg.ops
+    g = torch.Generator().manual_seed(7 * B * L + Dh)
+    D = H * Dh
+    qkv = (torch.randn(B * L, 3 * D, generator=g) * 1.5).to(dtype)
+    kv = masks(B, L, g)
+    seed = 0x0F1E2D3C4B5A6978
+    qt = qkv.float().clone().requires_grad_(True)
+    o_ref, lse_ref = attn_ref(qt, kv, B, L, H, p, seed)
+    ctx = torch.empty(B * L, D, device=DEV, dtype=dtype)
+    lse = torch.empty(B * H * L, device=DEV)
+    sd = seed_dev(seed)
+    qd, kd = qkv.to(DEV), kv.to(DEV)
+    ops.mha_generic_fwd(qd, kd, B, L, H, ctx, lse, (p, sd))
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert rel(ctx.float(), o_ref) < tol
+    fin = torch.isfinite(lse_ref)
+    assert torch.equal(torch.isfinite(lse.cpu()), fin)
+    assert rel(lse.cpu()[fin], lse_ref[fin]) < (2e-6 if dtype == torch.float32 else 1e-2)
+    dctx = torch.randn(B * L, D, generator=g).to(dtype)
+    o_ref.backward(dctx.float())
+    dqkv = torch.empty(B * L, 3 * D, device=DEV, dtype=dtype)
+    ops.mha_generic_bwd(qd, kd, lse, ctx, dctx.to(DEV), B, L, H, dqkv, (p, sd))
+    assert rel(dqkv.float(), qt.grad) < (5e-5 if dtype == torch.float32 else 3e-2)
+    if ops.mha_tuned_supported(L, Dh):
+        ctx2 = torch.empty_like(ctx)
+        lse2 = torch.empty_like(lse)
+        ops.mha_fwd(qd, kd, B, L, H, ctx2, lse2, (p, sd))
+        assert rel(ctx2.float(), ctx.float()) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,L,H,Dh", [(6, 8, 4, 8), (16, 50, 4, 32), (4, 64, 2, 64), (5, 150, 4, 32),
                                       (3, 300, 2, 64), (4, 65, 4, 32), (4, 128, 4, 32), (3, 512, 4, 32),
                                       (2, 1000, 2, 32), (2, 2048, 1, 16)])

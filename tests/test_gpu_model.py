@@ -267,6 +267,43 @@ def test_long_history_matches_oracle(gpu_pkg):
     assert abs(float(loss) - lref) < 1e-4
 
 
+@pytest.mark.parametrize("D,H,L", [(128, 1, 20), (128, 32, 20), (256, 2, 30)])
+def test_generic_head_widths_match_oracle(gpu_pkg, D, H, L):
+    """Head widths the tuned attention kernels refuse — d_h = 128 (D = 128 with 1 head, D = 256
+    with 2) and d_h = 4, not a multiple of 8 (D = 128 with 32 heads) — which the reference
+    accepts (user_tower.py:5-13): the model runs the generic attention on an unpruned last
+    layer.  Loss and gradients against the oracle with dropout on."""
+    F = gpu_pkg.functional
+    torch.manual_seed(11)
+    m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=997, tabular_input_dim=128,
+                              num_genders=3, num_countries=64, max_seq_len=L, user_embedding_dim=D,
+                              item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
+                              compute_dtype=torch.float32).to(DEV)
+    m.item_tower.fusion_layer[3].p = 0.1
+    assert not m.user_tower.prune_last
+    g = torch.Generator().manual_seed(12)
+    batch = ref.synthetic_batch(16, L, 997, generator=g)
+    seeds = F.site_seeds(0x6E4, 1)
+    params = {k: v.detach().cpu() for k, v in m.named_parameters()}
+    running = {"running_mean": torch.zeros(512), "running_var": torch.ones(512),
+               "num_batches_tracked": torch.zeros((), dtype=torch.long)}
+    lref, _, _, _ = ref.two_tower_loss(params, batch, num_heads=H, p_drop=0.1, drop=ref.HashDropout(seeds),
+                                       running=running)
+    loss, _, _, _ = m({k: v.to(DEV) for k, v in batch.items()}, seeds=F.seed_table(seeds, DEV))
+    assert abs(float(loss) - float(lref)) < 1e-4
+    loss.backward()
+    pr = {k: v.detach().cpu().requires_grad_(True) for k, v in m.named_parameters()}
+    lo, _, _, _ = ref.two_tower_loss(pr, batch, num_heads=H, p_drop=0.1, drop=ref.HashDropout(seeds),
+                                     running=running)
+    lo.backward()
+    mine = dict(m.named_parameters())
+    for k in ("user_tower.transformer_encoder.layers.0.self_attn.in_proj_weight",
+              "user_tower.transformer_encoder.layers.1.self_attn.in_proj_weight",
+              "user_tower.item_embedding.weight"):
+        a, b = mine[k].grad.detach().double().cpu(), pr[k].grad.double()
+        assert float((a - b).abs().max()) <= 1e-3 * float(b.abs().max()), k
+
+
 @pytest.mark.parametrize("L", [20, 150])
 def test_dropout_on_matches_oracle_hash(gpu_pkg, L):
     """Dropout ON (p=0.1 at every site) — kernels' masks vs the oracle's restatement.  L = 150
@@ -357,6 +394,33 @@ def test_cfg2_graph_equals_eager_bitexact(gpu_pkg, D, p):
         assert l1 == l2, (i, l1, l2)
     torch.cuda.synchronize()
     assert_bit_equal(_state_bits(m1, s1), _state_bits(m2, s2))
+
+
+@pytest.mark.parametrize("D,H", [(128, 1), (128, 32)])
+def test_generic_head_widths_trainstep_graph_equals_eager(gpu_pkg, D, H):
+    """TrainStep on head widths the tuned kernels refuse (generic attention, unpruned last layer,
+    bf16): graph and eager bit-identical over 3 steps, and the loss falls."""
+    def build():
+        torch.manual_seed(13)
+        m = gpu_pkg.TwoTowerModel(precomputed_modalities=True, vocab_size=997, tabular_input_dim=128,
+                                  num_genders=3, num_countries=64, max_seq_len=20, user_embedding_dim=D,
+                                  item_embedding_dim=D, user_num_heads=H, user_dropout=0.1,
+                                  compute_dtype=torch.bfloat16).to(DEV)
+        m.item_tower.fusion_layer[3].p = 0.1
+        return m
+    g = torch.Generator().manual_seed(14)
+    bd = {k: v.to(DEV) for k, v in ref.synthetic_batch(64, 20, 997, generator=g).items()}
+    m1, m2 = build(), build()
+    s1 = gpu_pkg.TrainStep(m1, lr=3e-3, use_graph=True, seed=5)
+    s2 = gpu_pkg.TrainStep(m2, lr=3e-3, use_graph=False, seed=5)
+    losses = []
+    for i in range(3):
+        l1, l2 = float(s1.step(bd)), float(s2.step(bd))
+        assert l1 == l2, (i, l1, l2)
+        losses.append(l1)
+    torch.cuda.synchronize()
+    assert_bit_equal(_state_bits(m1, s1), _state_bits(m2, s2))
+    assert losses[-1] < losses[0]
 
 
 def test_train_step_graph_learns(gpu_pkg):
