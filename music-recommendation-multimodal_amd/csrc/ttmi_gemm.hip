@@ -1693,6 +1693,14 @@ TTMI_DEV void fold_store(const FoldSeg& sg, int64_t u, int64_t nq, float4 v) {
 // slabs (a LayerNorm's per-workgroup column sums, S ~ 229, 32-64 units), where 4 partitions
 // meant ~57 dependent loads per thread in 4 serial batches.
 constexpr int FOLD_WIDE_S = 32;
+// Up to FOLD_NARROW_S partials (a weight gradient's ~14 splits) a thread owns whole units and
+// sums all their partials itself, in split order: the partitioned form left 3 of 4 threads idle
+// in the update and padded each thread's 3-4 loads to a batch of 8.
+#ifndef TTMI_FOLD_NARROW_S
+#define TTMI_FOLD_NARROW_S 16
+#endif
+constexpr int FOLD_NARROW_S = TTMI_FOLD_NARROW_S < 2 ? 2 : TTMI_FOLD_NARROW_S;
+static_assert(FOLD_NARROW_S < FOLD_WIDE_S, "fold regimes");
 // The fold of one segment's units over this block's share [bx, nbx), handing each finished
 // unit to store4(u, float4 sum) (a 4-column weight unit) or store1(m, sum) (a bias row):
 // wgrad_fold_kernel stores them into the gradient, adamw_fold_kernel updates the parameters.
@@ -1739,7 +1747,7 @@ template <class S4, class S1>
 TTMI_DEV void fold_segment(const FoldSeg& sg, int bx, int nbx, S4& store4, S1& store1) {
   const int64_t nq = sg.N / 4, nel = sg.M * nq;
   const bool consume = (sg.acc & 2) != 0;
-  if (sg.S <= 2) {            // few partials (a fixed-point accumulator): one unit per thread
+  if (sg.S <= FOLD_NARROW_S) {   // few partials (fixed-point accumulators, split slabs): one unit a thread
     for (int64_t u = (int64_t)bx * 256 + threadIdx.x; u < sg.units; u += (int64_t)nbx * 256) {
       if (u < nel) {
         const int64_t m = u / nq, n = (u % nq) * 4;
@@ -1747,7 +1755,14 @@ TTMI_DEV void fold_segment(const FoldSeg& sg, int bx, int nbx, S4& store4, S1& s
       } else {                // a weight gradient's bias: the split row sums
         const int64_t m = u - nel;
         float v = 0.f;
-        for (int s = 0; s < sg.S; ++s) v += sg.part_rs[(int64_t)s * sg.M + m];
+        for (int s0 = 0; s0 < sg.S; s0 += 8) {     // batches of 8 loads in flight, split order
+          float w[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) w[j] = sg.part_rs[(int64_t)min(s0 + j, sg.S - 1) * sg.M + m];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (s0 + j < sg.S) v += w[j];
+        }
         store1(m, v);
       }
     }
@@ -2782,7 +2797,7 @@ int launch_fold(FoldArgs& a, hipStream_t s) {
   if (a.n == 0 || a.total == 0) return TTMI_OK;
   a.blk_begin[0] = 0;
   for (int k = 0; k < a.n; ++k) {
-    const int per = a.seg[k].S <= 2 ? 256 : a.seg[k].S > FOLD_WIDE_S ? 16 : 64;   // units per block pass
+    const int per = a.seg[k].S <= FOLD_NARROW_S ? 256 : a.seg[k].S > FOLD_WIDE_S ? 16 : 64;   // units per block pass
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((a.seg[k].units + per - 1) / per, 1024));
     a.blk_begin[k + 1] = a.blk_begin[k] + (int)nb;
   }
@@ -3000,7 +3015,7 @@ int launch_fold_segs(const FoldSeg* segs, int n, hipStream_t s) {
 }
 
 int fold_blocks(const FoldSeg& sg) {        // launch_fold's per-segment block count
-  const int per = sg.S <= 2 ? 256 : sg.S > FOLD_WIDE_S ? 16 : 64;
+  const int per = sg.S <= FOLD_NARROW_S ? 256 : sg.S > FOLD_WIDE_S ? 16 : 64;
   return (int)std::max<int64_t>(1, std::min<int64_t>((sg.units + per - 1) / per, 1024));
 }
 }  // namespace
