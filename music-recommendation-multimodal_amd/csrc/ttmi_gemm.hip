@@ -1814,9 +1814,13 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(FoldArgs a) {
 // summed in the fold's order and applied by AdamW right there, instead of stored into the flat
 // gradient by wgrad_fold_kernel and read back by adamw_kernel: one launch and one round trip of
 // those gradients less per step.  The grid is jobs: plain AdamW over the flat ranges no segment
-// covers (float4 units, 512 per block, the fixed-point range read from fx as adamw_kernel does),
+// covers (float4 units, 256·AF_U per block, the fixed-point range read from fx as adamw_kernel does),
 // then one job per segment.
 constexpr int AF_SEGS = FOLD_SEGS, AF_PLAIN = 40;
+#ifndef TTMI_AF_U
+#define TTMI_AF_U 4
+#endif
+constexpr int AF_U = TTMI_AF_U;                 // float4 units a thread of a plain job updates
 struct AdamFoldArgs {
   float* p; float* g; float* m; float* v; bf16_t* pb;
   const double* hyper; const int32_t* step;
@@ -1866,7 +1870,7 @@ __global__ __launch_bounds__(256) void adamw_fold_kernel(AdamFoldArgs a) {
     int64_t* fx = ka->fx;
     const int64_t fx_lo = ka->fx_lo, fx_hi = ka->fx_hi;
     const int fx_shift = ka->fx_shift;
-    constexpr int U = 2;
+    constexpr int U = AF_U;
     float4 gg[U];
     int64_t q[U];
 #pragma unroll
@@ -3145,7 +3149,7 @@ extern "C" int ttmi_adamw_folded_skip(int64_t n, float* p, float* g, float* m, f
   int nb = 0;
   for (int j = 0; j < a.nplain; ++j) {
     a.blk_begin[j] = nb;
-    nb += (int)((a.phi[j] - a.plo[j] + 511) / 512);
+    nb += (int)((a.phi[j] - a.plo[j] + 256 * AF_U - 1) / (256 * AF_U));
   }
   for (int i = 0; i < a.nseg; ++i) {
     a.seg[i] = segs[i];
