@@ -934,7 +934,10 @@ extern "C" int ttmi_seq_embed_fwd(int B, int L, int D, const int64_t* ids, const
                     (uintptr_t)(ln2 ? w1 : w) | (uintptr_t)(ln2 ? b1 : b)) & 15) == 0 &&
                   (!ln2 || ((uintptr_t)y1 & 7) == 0);
   if (vec && al && (D == 128 || D == 256)) {
-    constexpr int U = 2;
+#ifndef TTMI_SEQ_U
+#define TTMI_SEQ_U 2
+#endif
+    constexpr int U = TTMI_SEQ_U;                    // row groups in flight per wave
     const int rpw = D == 128 ? 2 : 1;
     const int64_t waves = (M + U * rpw - 1) / (U * rpw);
     const dim3 g((unsigned)std::min<int64_t>((waves + 3) / 4, cap));
