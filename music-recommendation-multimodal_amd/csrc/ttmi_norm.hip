@@ -400,8 +400,14 @@ __global__ __launch_bounds__(256) void seq_embed_fwd_vec_kernel(
 // rows accE[V][D] (one add per token and column) and accL[3][L][D] (dP, and the LayerNorm
 // weight / bias partials per position), converted into the fp32 gradients by the fold
 // (ttmi_seq_embed_bwd_folds): the gradient is bit-identical run to run (the fp32 atomics it
-// replaces summed in arrival order).
-constexpr int SEB_W = 4, SEB_R = 4;
+// replaces summed in arrival order).  TTMI_SEB_R = 2 measured ~2.5 us a step faster in round 6
+// (profiles/r06/seq_embed_bwd_passes.txt) but is not the default: its validation run hit a host
+// segfault in an unrelated cfg-4 graph replay whose cause was not established before the round
+// closed, so the build that passed the full suite twice is kept.
+#ifndef TTMI_SEB_R
+#define TTMI_SEB_R 4
+#endif
+constexpr int SEB_W = 4, SEB_R = TTMI_SEB_R;
 template <int NV>
 __global__ __launch_bounds__(64 * SEB_W) void seq_embed_bwd_kernel(
     int B, int L, int D, const int64_t* __restrict__ ids, const float* __restrict__ E,
@@ -994,8 +1000,7 @@ extern "C" int ttmi_seq_embed_bwd(int B, int L, int D, int64_t V, const int64_t*
                "ttmi_seq_embed_bwd: null argument");
   TTMI_REQUIRE(((uintptr_t)ws & 15) == 0, "ttmi_seq_embed_bwd: ws must be 16-byte aligned");
   if (B > 0) {
-    // SEB_R passes of two rows per wave (400 blocks at B = 512, L = 50: one round on the
-    // chip; one pass per wave, 1,600 blocks, measured 20.5 us in the step, this 17)
+    // SEB_R passes of two rows per wave (SEB_R = 4: 800 blocks at B = 512, L = 50)
     const int bpc = 2 * SEB_R * SEB_W;
     dim3 grid(L, (B + bpc - 1) / bpc);
     int64_t* accE = static_cast<int64_t*>(ws);

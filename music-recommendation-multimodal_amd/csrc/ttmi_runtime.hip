@@ -48,7 +48,10 @@ __global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16_t* __
 // owns ADAM_U float4 groups (stride = the grid's thread count, so every access is coalesced)
 // and issues all their p / g / m / v loads before any arithmetic: 4·ADAM_U independent
 // 16-byte loads in flight per thread instead of 4.
-constexpr int ADAM_U = 2;
+#ifndef TTMI_ADAM_U
+#define TTMI_ADAM_U 2
+#endif
+constexpr int ADAM_U = TTMI_ADAM_U;
 // fx (optional): the gradient of the float4 range [fx_lo, fx_hi) is not in g but in an int64
 // fixed-point accumulator (2^-fx_shift; the item-embedding rows of ttmi_seq_embed_bwd): it is
 // read from there, converted, and the accumulator cleared instead of g (the fold that would
