@@ -75,6 +75,18 @@ def capturable(group=None) -> bool:
     return dist.get_backend(group) == "nccl"
 
 
+def quiesce_before_capture(seconds: float = 0.3) -> None:
+    """Call after a device synchronize, before a capture that records collectives.  torch's
+    process-group watchdog polls its finished collectives about every 100 ms before retiring
+    them.  The first collective recorded in a capture joins the group's stream to that capture.
+    A finished collective still listed from before then has its event queried on a capturing
+    stream: HIP refuses the query (hipErrorCapturedEvent) and the watchdog aborts the process.
+    This was seen once in the GPU suite with thread-local capture.  Waiting a few polls lets
+    the watchdog retire every earlier collective first."""
+    import time
+    time.sleep(seconds)
+
+
 def _staged(t: Tensor, group) -> bool:
     """True when the collective must run on a host copy of ``t`` (gloo + device tensor)."""
     return t.is_cuda and dist.get_backend(group) == "gloo"

@@ -739,6 +739,8 @@ class TrainStep:
         for t, s in zip(self._state(), snap):   # undo the warm-up's state changes
             t.copy_(s)
         torch.cuda.synchronize(self.device)
+        if self.capture_collectives:
+            comm.quiesce_before_capture()       # the watchdog retires the warm-up's collectives
         try:
             seg = self._record(b)
         except Exception as exc:

@@ -106,6 +106,7 @@ def _collectives_worker():
             comm.all_reduce_sum(x)                       # warm the communicator off-capture
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        comm.quiesce_before_capture()                    # as TrainStep does before its capture
         graph = torch.cuda.CUDAGraph()
         # thread-local capture, as TrainStep's: the watchdog may query earlier works meanwhile
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
